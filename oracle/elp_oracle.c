@@ -1,0 +1,762 @@
+/*
+ * elp_oracle.c -- CPU restatement of the dense revised-simplex hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see elp_oracle.h).  Compiled with
+ * -ffp-contract=off; every fused multiply-add below is an explicit fma()
+ * so that the HIP kernels (also -ffp-contract=off, explicit fma) produce
+ * the same bits.  Reduction orders follow DESIGN.md "Reduction order
+ * contract":
+ *   price  : 4 contiguous slot chunks, fma chain per chunk, then
+ *            ((0+p0)+p1)+p2)+p3                          (PRICE_SPLIT)
+ *   wave   : 64 lane-strided fma chains + butterfly 32,16,..,1 (wave_dot)
+ *   zchunk : chunks of 64 bump positions, fma chain, sequential sum
+ *   seq    : one fma chain in index order
+ *
+ * Algorithm (bounded primal revised simplex, minimisation form):
+ *   - rows a_i'x + s_i = b_i; slack bounds encode dir (R/class.R:271-274,
+ *     "==" -> "=" at :272): '<=' [0,inf), '>=' (-inf,0], '==' [0,0];
+ *   - the basis B is kept as unit columns (slacks / artificials) covering
+ *     m-k rows plus a k x k "bump" M = A[R,S] (R: uncovered rows,
+ *     S: basic structurals) whose inverse Minv is stored explicitly and
+ *     updated by rank-one / bordered formulas (cases A-E below);
+ *   - dual y is zero on slack-covered rows, so pricing sweeps only the
+ *     rows Y = {i : slack i nonbasic}, kept as a row-major copy AR;
+ *   - Dantzig pricing (largest |d_j|, lowest index on ties), Harris
+ *     two-pass ratio test (largest |alpha|, lowest variable id on ties),
+ *     bound flips, Bland fallback after a run of degenerate pivots,
+ *     Gauss-Jordan refactor of M every refactor_period pivots;
+ *   - phase 1 minimises the sum of artificials, phase 2 the real costs.
+ */
+#include "elp_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#define VS_BASIC 0
+#define VS_LOWER 1
+#define VS_UPPER 2
+#define VS_FREE 3
+
+#define PRICE_SPLIT 4
+#define ZCHUNK 64
+#define WAVE 64
+
+/* ------------------------------------------------------------------ */
+/* synthetic generator (bit-identical in HIP and numpy)                */
+/* ------------------------------------------------------------------ */
+static inline uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+static inline double gen_u01(uint64_t seed, uint64_t stream, uint64_t idx) {
+    uint64_t key = mix64(seed * 0x9E3779B97F4A7C15ULL + stream * 0xD1B54A32D192ED03ULL +
+                         0x632BE59BD9B4E019ULL);
+    uint64_t z = mix64(key + (idx + 1) * 0x9E3779B97F4A7C15ULL);
+    return (double)(z >> 11) * 0x1.0p-53;
+}
+
+void orc_generate_dense(uint64_t seed, int64_t m, int64_t n, int64_t col0, int64_t ncols,
+                        double* A, double* b, double* c) {
+    if (A)
+        for (int64_t jj = 0; jj < ncols; ++jj) {
+            const uint64_t j = (uint64_t)(col0 + jj);
+            for (int64_t i = 0; i < m; ++i)
+                A[(size_t)jj * (size_t)m + (size_t)i] =
+                    gen_u01(seed, 0, (uint64_t)i + j * (uint64_t)m);
+        }
+    if (c)
+        for (int64_t jj = 0; jj < ncols; ++jj) c[jj] = gen_u01(seed, 1, (uint64_t)(col0 + jj));
+    if (b) {
+        const double e = (double)n / 8.0, q = (double)n / 4.0;
+        for (int64_t i = 0; i < m; ++i) b[i] = e + gen_u01(seed, 2, (uint64_t)i) * q;
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* solver state                                                        */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    int64_t m, n, nv;
+    const double* A; /* column-major m x n */
+    double* b;
+    double *lb, *ub, *cost, *xval;
+    int8_t* vstat;
+    double* asgn;     /* m: sign of artificial column n+m+i            */
+    int64_t k;        /* bump dimension                                 */
+    int64_t *cover;   /* m: covering unit variable or -1               */
+    int64_t *rpos;    /* m: position in Rl or -1                       */
+    int64_t *Rl, *Sl; /* m each                                         */
+    int64_t* spos;    /* n: position in Sl or -1                       */
+    double *xr, *xs;  /* values: covered rows, bump positions           */
+    double* Minv;     /* m x m capacity, row-major, ld = ldm           */
+    int64_t ldm;
+    int64_t ny, ycap; /* Y slots                                        */
+    int64_t *Yl, *ypos;
+    double* AR; /* ycap x n row-major                                   */
+    /* work */
+    double *y, *t, *yR, *yy, *acol, *aR, *alS, *alU, *z, *v, *tmp, *part;
+    int8_t* used;
+    int64_t* perm;
+    double tol_inf;
+} orc_t;
+
+static double* dalloc(size_t n) { return (double*)calloc(n ? n : 1, sizeof(double)); }
+static int64_t* ialloc(size_t n) { return (int64_t*)calloc(n ? n : 1, sizeof(int64_t)); }
+
+static inline double Aat(const orc_t* s, int64_t i, int64_t j) {
+    return s->A[(size_t)j * (size_t)s->m + (size_t)i];
+}
+static inline double unit_sign(const orc_t* s, int64_t var) {
+    return var >= s->n + s->m ? s->asgn[var - s->n - s->m] : 1.0;
+}
+static inline double* MI(orc_t* s, int64_t r, int64_t c) {
+    return &s->Minv[(size_t)r * (size_t)s->ldm + (size_t)c];
+}
+
+/* wave order: 64 lane-strided fma chains, then butterfly tree */
+static double wave_dot(int64_t len, const double* a, const double* b) {
+    double lane[WAVE];
+    for (int l = 0; l < WAVE; ++l) {
+        double acc = 0.0;
+        for (int64_t i = l; i < len; i += WAVE) acc = fma(a[i], b[i], acc);
+        lane[l] = acc;
+    }
+    for (int off = WAVE / 2; off >= 1; off >>= 1)
+        for (int l = 0; l < off; ++l) lane[l] = lane[l] + lane[l + off];
+    return lane[0];
+}
+
+/* z_i = sum_p A[i, S_p] * w_p in ZCHUNK order */
+static double zchunk_row(const orc_t* s, int64_t i, const double* w) {
+    double tot = 0.0;
+    for (int64_t c0 = 0; c0 < s->k; c0 += ZCHUNK) {
+        double acc = 0.0;
+        const int64_t c1 = c0 + ZCHUNK < s->k ? c0 + ZCHUNK : s->k;
+        for (int64_t p = c0; p < c1; ++p) acc = fma(Aat(s, i, s->Sl[p]), w[p], acc);
+        tot = tot + acc;
+    }
+    return tot;
+}
+
+/* v_c = sum_q A[i, S_q] * Minv[q][c]  (seq order over q) */
+static void row_times_minv(orc_t* s, int64_t i, double* out) {
+    for (int64_t c = 0; c < s->k; ++c) {
+        double acc = 0.0;
+        for (int64_t q = 0; q < s->k; ++q) acc = fma(Aat(s, i, s->Sl[q]), *MI(s, q, c), acc);
+        out[c] = acc;
+    }
+}
+
+static int y_grow(orc_t* s) {
+    int64_t nc = s->ycap ? s->ycap * 2 : 16;
+    if (nc > s->m) nc = s->m;
+    double* p = (double*)realloc(s->AR, (size_t)nc * (size_t)s->n * sizeof(double) + 8);
+    if (!p) return -1;
+    s->AR = p;
+    s->ycap = nc;
+    return 0;
+}
+static int y_append(orc_t* s, int64_t i) {
+    if (s->ny == s->ycap && y_grow(s)) return -1;
+    const int64_t p = s->ny++;
+    s->Yl[p] = i;
+    s->ypos[i] = p;
+    double* row = s->AR + (size_t)p * (size_t)s->n;
+    for (int64_t j = 0; j < s->n; ++j) row[j] = Aat(s, i, j);
+    return 0;
+}
+static void y_remove(orc_t* s, int64_t i) {
+    const int64_t p = s->ypos[i], last = s->ny - 1;
+    if (p != last) {
+        s->Yl[p] = s->Yl[last];
+        s->ypos[s->Yl[p]] = p;
+        memcpy(s->AR + (size_t)p * (size_t)s->n, s->AR + (size_t)last * (size_t)s->n,
+               (size_t)s->n * sizeof(double));
+    }
+    s->ypos[i] = -1;
+    s->ny--;
+}
+
+/* ------------------------------------------------------------------ */
+/* refactor: Gauss-Jordan with partial pivoting, then recompute x_B    */
+/* ------------------------------------------------------------------ */
+static int refactor(orc_t* s) {
+    const int64_t k = s->k, m = s->m, n = s->n;
+    if (k > 0) {
+        double *W = s->tmp, *W2 = s->tmp + (size_t)k * (size_t)k;
+        for (int64_t a = 0; a < k; ++a)
+            for (int64_t c = 0; c < k; ++c) W[a * k + c] = Aat(s, s->Rl[a], s->Sl[c]);
+        memset(s->used, 0, (size_t)k);
+        for (int64_t c = 0; c < k; ++c) {
+            int64_t p = -1;
+            double best = -1.0;
+            for (int64_t r = 0; r < k; ++r)
+                if (!s->used[r] && fabs(W[r * k + c]) > best) {
+                    best = fabs(W[r * k + c]);
+                    p = r;
+                }
+            const double piv = W[p * k + c];
+            if (!(fabs(piv) > 1e-13)) return -1;
+            s->perm[c] = p;
+            for (int64_t r = 0; r < k; ++r) {
+                if (r == p) {
+                    for (int64_t j = 0; j < k; ++j)
+                        W2[r * k + j] = (j == c) ? 1.0 / piv : W[p * k + j] / piv;
+                } else {
+                    const double f = W[r * k + c];
+                    for (int64_t j = 0; j < k; ++j)
+                        W2[r * k + j] = (j == c) ? -(f / piv) : fma(-f, W[p * k + j] / piv, W[r * k + j]);
+                }
+            }
+            s->used[p] = 1;
+            double* sw = W;
+            W = W2;
+            W2 = sw;
+        }
+        for (int64_t a = 0; a < k; ++a)
+            for (int64_t c = 0; c < k; ++c) *MI(s, a, s->perm[c]) = W[s->perm[a] * k + c];
+    }
+    /* primal values: rhs_i = (b_i - sum_{j nonbasic struct, x_j != 0} a_ij x_j) - s_i */
+    for (int64_t i = 0; i < m; ++i) {
+        double acc = 0.0;
+        for (int64_t j = 0; j < n; ++j)
+            if (s->vstat[j] != VS_BASIC && s->xval[j] != 0.0) acc = fma(Aat(s, i, j), s->xval[j], acc);
+        double r = s->b[i] - acc;
+        if (s->vstat[n + i] != VS_BASIC) r = r - s->xval[n + i];
+        s->acol[i] = r;
+    }
+    for (int64_t p = 0; p < k; ++p) s->aR[p] = s->acol[s->Rl[p]];
+    for (int64_t p = 0; p < k; ++p) s->xs[p] = wave_dot(k, MI(s, p, 0), s->aR);
+    for (int64_t i = 0; i < m; ++i)
+        if (s->cover[i] >= 0) s->xr[i] = unit_sign(s, s->cover[i]) * (s->acol[i] - zchunk_row(s, i, s->xs));
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* one phase of the simplex                                           */
+/* ------------------------------------------------------------------ */
+enum { PH_OPTIMAL = 0, PH_UNBOUNDED = 3, PH_NUMFAIL = 5, PH_ITERCAP = 1, PH_P1DONE = 10 };
+
+static double art_sum(const orc_t* s) {
+    double acc = 0.0;
+    for (int64_t i = 0; i < s->m; ++i)
+        if (s->cover[i] >= s->n + s->m) acc = acc + s->xr[i];
+    return acc;
+}
+
+/* basic entry e: covered row e (< m) or bump position e - m */
+static inline int basic_entry(const orc_t* s, int64_t e, double sig, int64_t* var, double* g,
+                              double* x) {
+    if (e < s->m) {
+        if (s->cover[e] < 0) return 0;
+        *var = s->cover[e];
+        *g = sig * s->alU[e];
+        *x = s->xr[e];
+    } else {
+        const int64_t p = e - s->m;
+        *var = s->Sl[p];
+        *g = sig * s->alS[p];
+        *x = s->xs[p];
+    }
+    return 1;
+}
+
+static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter, int64_t max_iter,
+                     int64_t* trace, int64_t trace_cap, orc_stats* st, int64_t* unb_var,
+                     double* unb_sigma) {
+    const int64_t m = s->m, n = s->n;
+    int64_t since_refactor = 0, ndegen = 0;
+    int bland = 0;
+    for (;;) {
+        if (phase == 1 && art_sum(s) <= s->tol_inf) return PH_P1DONE;
+        if (*iter >= max_iter) return PH_ITERCAP;
+        if (since_refactor >= ctl->refactor_period) {
+            if (refactor(s)) return PH_NUMFAIL;
+            st->refactors++;
+            since_refactor = 0;
+        }
+        const int64_t k = s->k;
+        /* ---- BTRAN ---- */
+        for (int64_t i = 0; i < m; ++i) {
+            const int64_t u = s->cover[i];
+            s->y[i] = u >= 0 ? unit_sign(s, u) * s->cost[u] : 0.0;
+        }
+        for (int64_t p = 0; p < k; ++p) {
+            double acc = 0.0;
+            for (int64_t i = 0; i < m; ++i)
+                if (s->cover[i] >= 0 && s->y[i] != 0.0) acc = fma(Aat(s, i, s->Sl[p]), s->y[i], acc);
+            s->t[p] = s->cost[s->Sl[p]] - acc;
+        }
+        for (int64_t p = 0; p < k; ++p) {
+            double acc = 0.0;
+            for (int64_t q = 0; q < k; ++q) acc = fma(*MI(s, q, p), s->t[q], acc);
+            s->yR[p] = acc;
+        }
+        for (int64_t p = 0; p < k; ++p) s->y[s->Rl[p]] = s->yR[p];
+        /* ---- pricing over structurals (AR sweep) and slacks ---- */
+        const int64_t ny = s->ny;
+        for (int64_t p = 0; p < ny; ++p) s->yy[p] = s->y[s->Yl[p]];
+        const int64_t L = (ny + PRICE_SPLIT - 1) / PRICE_SPLIT;
+        for (int w = 0; w < PRICE_SPLIT; ++w) {
+            double* pw = s->part + (size_t)w * (size_t)n;
+            for (int64_t j = 0; j < n; ++j) pw[j] = 0.0;
+            const int64_t p0 = (int64_t)w * L, p1 = p0 + L < ny ? p0 + L : ny;
+            for (int64_t p = p0; p < p1; ++p) {
+                const double yp = s->yy[p];
+                const double* row = s->AR + (size_t)p * (size_t)n;
+                for (int64_t j = 0; j < n; ++j) pw[j] = fma(row[j], yp, pw[j]);
+            }
+        }
+        st->price_bytes += 8.0 * ((double)ny * (double)n + (double)n + (double)ny);
+        int64_t q = -1;
+        double qscore = 0.0, dq = 0.0;
+        const double dtol = ctl->tol_dual;
+        for (int64_t j = 0; j < n + m; ++j) {
+            const int8_t vs = s->vstat[j];
+            if (vs == VS_BASIC || s->lb[j] == s->ub[j]) continue;
+            double d;
+            if (j < n) {
+                double tot = 0.0;
+                for (int w = 0; w < PRICE_SPLIT; ++w) tot = tot + s->part[(size_t)w * (size_t)n + (size_t)j];
+                d = s->cost[j] - tot;
+            } else {
+                d = s->cost[j] - s->y[j - n];
+            }
+            double score = 0.0;
+            if ((vs == VS_LOWER || vs == VS_FREE) && d < -dtol) score = -d;
+            else if ((vs == VS_UPPER || vs == VS_FREE) && d > dtol) score = d;
+            else continue;
+            if (bland) {
+                q = j;
+                dq = d;
+                break;
+            }
+            if (score > qscore) {
+                qscore = score;
+                q = j;
+                dq = d;
+            }
+        }
+        if (q < 0) return PH_OPTIMAL;
+        const double sig = dq < 0.0 ? 1.0 : -1.0;
+        /* ---- FTRAN ---- */
+        for (int64_t i = 0; i < m; ++i) s->acol[i] = (q < n) ? Aat(s, i, q) : (i == q - n ? 1.0 : 0.0);
+        for (int64_t p = 0; p < k; ++p) s->aR[p] = s->acol[s->Rl[p]];
+        for (int64_t p = 0; p < k; ++p) s->alS[p] = wave_dot(k, MI(s, p, 0), s->aR);
+        for (int64_t i = 0; i < m; ++i) {
+            if (s->cover[i] < 0) continue;
+            s->z[i] = zchunk_row(s, i, s->alS);
+            s->alU[i] = unit_sign(s, s->cover[i]) * (s->acol[i] - s->z[i]);
+        }
+        /* ---- ratio test (Harris two-pass, or textbook under Bland) ----
+         * basic entries e < m are covered rows, e >= m bump positions. */
+        const double ptol = ctl->tol_primal, pivtol = ctl->tol_pivot, INF = HUGE_VAL;
+        double theta_max = INF;
+        for (int64_t e = 0; e < m + k; ++e) {
+            int64_t var;
+            double g, x;
+            if (!basic_entry(s, e, sig, &var, &g, &x)) continue;
+            const double l = s->lb[var], u = s->ub[var];
+            double r;
+            if (g > pivtol && l > -INF) r = bland ? (x - l) / g : (x - l + ptol) / g;
+            else if (g < -pivtol && u < INF) r = bland ? (u - x) / (-g) : (u - x + ptol) / (-g);
+            else continue;
+            if (r < theta_max) theta_max = r;
+        }
+        int64_t lv = -1, lrow = -1, lpos = -1;
+        double lg = 0.0, lratio = 0.0;
+        for (int64_t e = 0; e < m + k; ++e) {
+            int64_t var;
+            double g, x;
+            if (!basic_entry(s, e, sig, &var, &g, &x)) continue;
+            const double l = s->lb[var], u = s->ub[var];
+            double r;
+            if (g > pivtol && l > -INF) r = (x - l) / g;
+            else if (g < -pivtol && u < INF) r = (u - x) / (-g);
+            else continue;
+            if (!(r <= theta_max)) continue;
+            int take;
+            if (lv < 0) take = 1;
+            else if (bland) take = (r < lratio) || (r == lratio && var < lv);
+            else take = (fabs(g) > fabs(lg)) || (fabs(g) == fabs(lg) && var < lv);
+            if (take) {
+                lv = var;
+                lrow = e < m ? e : -1;
+                lpos = e < m ? -1 : e - m;
+                lg = g;
+                lratio = r;
+            }
+        }
+        double theta = lv >= 0 ? (lratio > 0.0 ? lratio : 0.0) : INF;
+        const double flip = (s->lb[q] > -INF && s->ub[q] < INF) ? s->ub[q] - s->lb[q] : INF;
+        (*iter)++;
+        if (phase == 1) st->phase1_iterations++;
+        if (flip < INF && flip <= theta) {
+            /* bound flip */
+            for (int64_t i = 0; i < m; ++i)
+                if (s->cover[i] >= 0) s->xr[i] = fma(-flip, sig * s->alU[i], s->xr[i]);
+            for (int64_t p = 0; p < k; ++p) s->xs[p] = fma(-flip, sig * s->alS[p], s->xs[p]);
+            if (s->vstat[q] == VS_LOWER) {
+                s->vstat[q] = VS_UPPER;
+                s->xval[q] = s->ub[q];
+            } else {
+                s->vstat[q] = VS_LOWER;
+                s->xval[q] = s->lb[q];
+            }
+            st->bound_flips++;
+            if (trace && *iter - 1 < trace_cap) {
+                trace[2 * (*iter - 1)] = q;
+                trace[2 * (*iter - 1) + 1] = -1;
+            }
+            ndegen = 0;
+            bland = 0;
+            continue;
+        }
+        if (theta == INF) {
+            *unb_var = q;
+            *unb_sigma = sig;
+            return PH_UNBOUNDED;
+        }
+        if (trace && *iter - 1 < trace_cap) {
+            trace[2 * (*iter - 1)] = q;
+            trace[2 * (*iter - 1) + 1] = lv;
+        }
+        if (theta == 0.0) {
+            st->degenerate++;
+            if (++ndegen >= ctl->degen_switch) bland = 1;
+        } else {
+            ndegen = 0;
+            bland = 0;
+        }
+        /* ---- primal update ---- */
+        for (int64_t i = 0; i < m; ++i)
+            if (s->cover[i] >= 0) s->xr[i] = fma(-theta, sig * s->alU[i], s->xr[i]);
+        for (int64_t p = 0; p < k; ++p) s->xs[p] = fma(-theta, sig * s->alS[p], s->xs[p]);
+        const double xq = s->xval[q] + sig * theta;
+        /* leaving variable goes to the bound it hit */
+        const int at_lower = lg > 0.0;
+        const int leave_art = lv >= n + m;
+        if (leave_art) {
+            s->lb[lv] = 0.0;
+            s->ub[lv] = 0.0;
+            s->vstat[lv] = VS_LOWER;
+            s->xval[lv] = 0.0;
+        } else {
+            s->vstat[lv] = at_lower ? VS_LOWER : VS_UPPER;
+            s->xval[lv] = at_lower ? s->lb[lv] : s->ub[lv];
+        }
+        s->vstat[q] = VS_BASIC;
+        /* ---- basis change ---- */
+        if (q < n) {
+            if (lpos >= 0) {
+                /* case A: structural replaces structural at bump position lpos */
+                const int64_t p = lpos;
+                const double piv = s->alS[p];
+                for (int64_t j = 0; j < k; ++j) s->v[j] = *MI(s, p, j) / piv;
+                for (int64_t i = 0; i < k; ++i) {
+                    if (i == p) continue;
+                    const double wi = s->alS[i];
+                    for (int64_t j = 0; j < k; ++j) *MI(s, i, j) = fma(-wi, s->v[j], *MI(s, i, j));
+                }
+                for (int64_t j = 0; j < k; ++j) *MI(s, p, j) = s->v[j];
+                s->spos[lv] = -1;
+                s->Sl[p] = q;
+                s->spos[q] = p;
+                s->xs[p] = xq;
+            } else {
+                /* case B: structural enters, unit var of row lrow leaves; bump grows */
+                const int64_t i = lrow;
+                const double delta = s->acol[i] - s->z[i];
+                row_times_minv(s, i, s->v);
+                for (int64_t c = 0; c < k; ++c) s->v[c] = s->v[c] / delta;
+                for (int64_t a = 0; a < k; ++a) {
+                    const double wa = s->alS[a];
+                    for (int64_t c = 0; c < k; ++c) *MI(s, a, c) = fma(wa, s->v[c], *MI(s, a, c));
+                }
+                for (int64_t a = 0; a < k; ++a) *MI(s, a, k) = -(s->alS[a] / delta);
+                for (int64_t c = 0; c < k; ++c) *MI(s, k, c) = -s->v[c];
+                *MI(s, k, k) = 1.0 / delta;
+                s->Rl[k] = i;
+                s->rpos[i] = k;
+                s->Sl[k] = q;
+                s->spos[q] = k;
+                s->xs[k] = xq;
+                s->cover[i] = -1;
+                s->k = k + 1;
+                if (!leave_art && y_append(s, i)) return PH_NUMFAIL;
+            }
+        } else {
+            const int64_t i0 = q - n;
+            const int64_t a = s->rpos[i0];
+            if (a < 0) {
+                /* case E: slack replaces the artificial covering the same row */
+                if (lrow != i0) return PH_NUMFAIL;
+                s->cover[i0] = q;
+                s->xr[i0] = xq;
+            } else if (lpos >= 0) {
+                /* case C: slack of row i0 (in R) enters, structural at lpos leaves */
+                const int64_t b = lpos, last = k - 1;
+                const double piv = *MI(s, b, a);
+                for (int64_t c = 0; c < k; ++c) s->v[c] = *MI(s, b, c) / piv;
+                for (int64_t r = 0; r < k; ++r) {
+                    if (r == b) continue;
+                    const double f = *MI(s, r, a);
+                    for (int64_t c = 0; c < k; ++c)
+                        if (c != a) *MI(s, r, c) = fma(-f, s->v[c], *MI(s, r, c));
+                }
+                if (b != last) {
+                    for (int64_t c = 0; c < k; ++c) *MI(s, b, c) = *MI(s, last, c);
+                    s->Sl[b] = s->Sl[last];
+                    s->spos[s->Sl[b]] = b;
+                    s->xs[b] = s->xs[last];
+                }
+                if (a != last) {
+                    for (int64_t r = 0; r < k; ++r) *MI(s, r, a) = *MI(s, r, last);
+                    s->Rl[a] = s->Rl[last];
+                    s->rpos[s->Rl[a]] = a;
+                }
+                s->spos[lv] = -1;
+                s->rpos[i0] = -1;
+                s->cover[i0] = q;
+                s->xr[i0] = xq;
+                s->k = k - 1;
+            } else {
+                /* case D: slack of row i0 (in R) enters, unit var of row i1 leaves */
+                const int64_t i1 = lrow;
+                row_times_minv(s, i1, s->v);
+                const double piv = s->v[a];
+                for (int64_t r = 0; r < k; ++r) s->t[r] = *MI(s, r, a) / piv;
+                for (int64_t r = 0; r < k; ++r) {
+                    const double f = s->t[r];
+                    for (int64_t c = 0; c < k; ++c)
+                        if (c != a) *MI(s, r, c) = fma(-f, s->v[c], *MI(s, r, c));
+                    *MI(s, r, a) = f;
+                }
+                s->Rl[a] = i1;
+                s->rpos[i1] = a;
+                s->rpos[i0] = -1;
+                s->cover[i1] = -1;
+                s->cover[i0] = q;
+                s->xr[i0] = xq;
+            }
+            y_remove(s, i0);
+            if (a >= 0 && lpos < 0 && !leave_art) {
+                if (y_append(s, lrow)) return PH_NUMFAIL;
+            }
+        }
+        since_refactor++;
+    }
+}
+
+void orc_default_control(orc_control* c) {
+    c->tol_primal = 1e-9;
+    c->tol_dual = 1e-9;
+    c->tol_pivot = 1e-9;
+    c->infinity = 1e30;
+    c->max_iter = 0;
+    c->refactor_period = 100;
+    c->degen_switch = 50;
+}
+
+static int cmp_i64(const void* a, const void* b) {
+    const int64_t x = *(const int64_t*)a, y = *(const int64_t*)b;
+    return (x > y) - (x < y);
+}
+
+int orc_solve_dense(int64_t m, int64_t n, const double* A, const int32_t* dir, const double* rhs,
+                    const double* obj, const double* lo, const double* up, int32_t maximize,
+                    const orc_control* ctl_in, double* objval, double* xout, double* yout,
+                    int64_t* basis, int64_t* trace, int64_t trace_cap, orc_stats* st_out) {
+    if (m < 0 || n <= 0 || (m > 0 && (!A || !dir || !rhs)) || !obj) return -1;
+    for (int64_t i = 0; i < m; ++i)
+        if (dir[i] < 1 || dir[i] > 3) return -2;
+    orc_control ctl;
+    if (ctl_in) ctl = *ctl_in;
+    else orc_default_control(&ctl);
+    if (ctl.refactor_period <= 0) ctl.refactor_period = 100;
+    if (ctl.degen_switch <= 0) ctl.degen_switch = 50;
+    const int64_t max_iter = ctl.max_iter > 0 ? ctl.max_iter : 100 * (m + n) + 10000;
+    const double INF = HUGE_VAL, BIG = ctl.infinity;
+
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    orc_stats st;
+    memset(&st, 0, sizeof st);
+
+    orc_t S;
+    memset(&S, 0, sizeof S);
+    orc_t* s = &S;
+    s->m = m;
+    s->n = n;
+    s->nv = n + 2 * m;
+    s->A = A;
+    const int64_t nv = s->nv, mm = m > 0 ? m : 1;
+    s->b = dalloc((size_t)mm);
+    s->lb = dalloc((size_t)nv);
+    s->ub = dalloc((size_t)nv);
+    s->cost = dalloc((size_t)nv);
+    s->xval = dalloc((size_t)nv);
+    s->vstat = (int8_t*)calloc((size_t)nv, 1);
+    s->asgn = dalloc((size_t)mm);
+    s->cover = ialloc((size_t)mm);
+    s->rpos = ialloc((size_t)mm);
+    s->Rl = ialloc((size_t)mm);
+    s->Sl = ialloc((size_t)mm);
+    s->spos = ialloc((size_t)n);
+    s->xr = dalloc((size_t)mm);
+    s->xs = dalloc((size_t)mm);
+    s->ldm = mm;
+    s->Minv = dalloc((size_t)mm * (size_t)mm);
+    s->Yl = ialloc((size_t)mm);
+    s->ypos = ialloc((size_t)mm);
+    s->y = dalloc((size_t)mm);
+    s->t = dalloc((size_t)mm);
+    s->yR = dalloc((size_t)mm);
+    s->yy = dalloc((size_t)mm);
+    s->acol = dalloc((size_t)mm);
+    s->aR = dalloc((size_t)mm);
+    s->alS = dalloc((size_t)mm);
+    s->alU = dalloc((size_t)mm);
+    s->z = dalloc((size_t)mm);
+    s->v = dalloc((size_t)mm);
+    s->tmp = dalloc(2 * (size_t)mm * (size_t)mm);
+    s->part = dalloc((size_t)PRICE_SPLIT * (size_t)n);
+    s->used = (int8_t*)calloc((size_t)mm, 1);
+    s->perm = ialloc((size_t)mm);
+
+    int status = 0;
+    int64_t unb_var = -1;
+    double unb_sigma = 0.0;
+    double bmax = 0.0;
+    /* bounds and costs (R/class.R:261-269); |v| >= infinity means infinite */
+    for (int64_t j = 0; j < n; ++j) {
+        double l = lo ? lo[j] : 0.0, u = up ? up[j] : INF;
+        if (l <= -BIG) l = -INF;
+        if (u >= BIG) u = INF;
+        s->lb[j] = l;
+        s->ub[j] = u;
+        s->cost[j] = 0.0;
+        s->spos[j] = -1;
+        if (l > u) status = 2; /* R/class.R:297-298 */
+        if (l > -INF) {
+            s->vstat[j] = VS_LOWER;
+            s->xval[j] = l;
+        } else if (u < INF) {
+            s->vstat[j] = VS_UPPER;
+            s->xval[j] = u;
+        } else {
+            s->vstat[j] = VS_FREE;
+            s->xval[j] = 0.0;
+        }
+    }
+    int64_t iter = 0;
+    if (status == 0) {
+        int any_art = 0;
+        for (int64_t i = 0; i < m; ++i) {
+            double bi = rhs[i];
+            if (bi <= -BIG) bi = -INF;
+            if (bi >= BIG) bi = INF;
+            s->b[i] = bi;
+            if (fabs(bi) < INF && fabs(bi) > bmax) bmax = fabs(bi);
+            const int64_t sv = n + i, av = n + m + i;
+            s->lb[sv] = dir[i] == 2 ? -INF : 0.0;
+            s->ub[sv] = dir[i] == 1 ? INF : 0.0;
+            s->lb[av] = 0.0;
+            s->ub[av] = 0.0;
+            s->vstat[av] = VS_LOWER;
+            s->rpos[i] = -1;
+            s->ypos[i] = -1;
+            double acc = 0.0;
+            for (int64_t j = 0; j < n; ++j)
+                if (s->xval[j] != 0.0) acc = fma(Aat(s, i, j), s->xval[j], acc);
+            const double r = s->b[i] - acc;
+            if (r >= s->lb[sv] && r <= s->ub[sv]) {
+                s->vstat[sv] = VS_BASIC;
+                s->cover[i] = sv;
+                s->xr[i] = r;
+            } else {
+                const double sl = r < s->lb[sv] ? s->lb[sv] : s->ub[sv];
+                s->vstat[sv] = (sl == s->lb[sv]) ? VS_LOWER : VS_UPPER;
+                s->xval[sv] = sl;
+                const double res = r - sl;
+                s->asgn[i] = res > 0.0 ? 1.0 : -1.0;
+                s->ub[av] = INF;
+                s->cost[av] = 1.0;
+                s->vstat[av] = VS_BASIC;
+                s->cover[i] = av;
+                s->xr[i] = fabs(res);
+                any_art = 1;
+                if (y_append(s, i)) status = -3;
+            }
+        }
+        s->tol_inf = 1e-9 * (1.0 + bmax);
+        if (any_art && status == 0) {
+            int ph = run_phase(s, 1, &ctl, &iter, max_iter, trace, trace_cap, &st, &unb_var, &unb_sigma);
+            if (ph == PH_NUMFAIL) status = 5;
+            else if (ph == PH_ITERCAP) status = 1;
+            else if (art_sum(s) > s->tol_inf) status = 2;
+        }
+        if (status == 0) {
+            for (int64_t i = 0; i < m; ++i) {
+                const int64_t av = n + m + i;
+                s->cost[av] = 0.0;
+                s->lb[av] = 0.0;
+                s->ub[av] = 0.0;
+            }
+            for (int64_t j = 0; j < n; ++j) s->cost[j] = maximize ? -obj[j] : obj[j];
+            if (any_art && refactor(s)) status = 5;
+        }
+        if (status == 0) {
+            int ph = run_phase(s, 2, &ctl, &iter, max_iter, trace, trace_cap, &st, &unb_var, &unb_sigma);
+            if (ph == PH_NUMFAIL) status = 5;
+            else if (ph == PH_ITERCAP) status = 1;
+            else if (ph == PH_UNBOUNDED) status = 3;
+            else status = 0;
+        }
+    }
+
+    /* ---- outputs (get.objective / get.variables, R/class.R:277-278) ---- */
+    if (xout)
+        for (int64_t j = 0; j < n; ++j) {
+            double v = s->vstat[j] == VS_BASIC ? s->xs[s->spos[j]] : s->xval[j];
+            if (status == 3 && j == unb_var) v = unb_sigma > 0 ? BIG : -BIG;
+            xout[j] = v;
+        }
+    if (objval) {
+        if (status == 3) *objval = maximize ? BIG : -BIG;
+        else {
+            double acc = 0.0;
+            for (int64_t j = 0; j < n; ++j) {
+                const double v = s->vstat[j] == VS_BASIC ? s->xs[s->spos[j]] : s->xval[j];
+                acc = fma(obj[j], v, acc);
+            }
+            *objval = acc;
+        }
+    }
+    if (yout)
+        for (int64_t i = 0; i < m; ++i) yout[i] = maximize ? -s->y[i] : s->y[i];
+    if (basis) {
+        int64_t c = 0;
+        for (int64_t i = 0; i < m; ++i)
+            if (s->cover[i] >= 0) basis[c++] = s->cover[i];
+        for (int64_t p = 0; p < s->k; ++p) basis[c++] = s->Sl[p];
+        qsort(basis, (size_t)c, sizeof(int64_t), cmp_i64);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    st.iterations = iter;
+    st.bump_dim = s->k;
+    st.y_rows = s->ny;
+    st.seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    if (st_out) *st_out = st;
+
+    free(s->b); free(s->lb); free(s->ub); free(s->cost); free(s->xval); free(s->vstat);
+    free(s->asgn); free(s->cover); free(s->rpos); free(s->Rl); free(s->Sl); free(s->spos);
+    free(s->xr); free(s->xs); free(s->Minv); free(s->Yl); free(s->ypos); free(s->AR);
+    free(s->y); free(s->t); free(s->yR); free(s->yy); free(s->acol); free(s->aR);
+    free(s->alS); free(s->alU); free(s->z); free(s->v); free(s->tmp); free(s->part);
+    free(s->used); free(s->perm);
+    return status;
+}

@@ -1,0 +1,80 @@
+/*
+ * elp_oracle.h -- CPU restatement of the dense revised-simplex hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library.  The product path
+ * (easylp_amd/, libeasylp_hip.so) never links or calls it.
+ *
+ * What it restates: the LP solve that EasyLP hands to lp_solve at
+ * /root/reference/R/class.R:260-278 (make.lp / set.objfn / lp.control /
+ * set.bounds / add.constraint / solve / get.objective / get.variables),
+ * including the status numbering of R/class.R:279-295, the lower>upper
+ * override of R/class.R:297-298 and lp_solve's 1e30 "infinity" that
+ * R/utils.R:172-176 maps back to +-Inf.  lp_solve 5.5 itself is a
+ * third-party dependency that is absent from /root/reference (lpSolveAPI,
+ * unversioned, DESCRIPTION:18-21); its numbers are pinned instead by the
+ * reference's own LP tests (tests/testthat/test-DOP.R:53,
+ * tests/testthat/test-unbounded.R:8-9), the README LP (README.md:14-38),
+ * vignette LPs, and HiGHS-generated fixtures (tests/golden/).
+ *
+ * The floating-point order of every reduction here is the one the HIP
+ * kernels use (see DESIGN.md "Reduction order contract"), so the GPU and
+ * this oracle walk the same pivot sequence on the same input.
+ */
+#ifndef ELP_ORACLE_H
+#define ELP_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_control {
+    double tol_primal;     /* Harris primal feasibility tolerance            */
+    double tol_dual;       /* reduced-cost optimality tolerance              */
+    double tol_pivot;      /* |alpha| below this never limits the step       */
+    double infinity;       /* |v| >= infinity is treated as infinite (1e30)  */
+    int64_t max_iter;      /* <=0: default 100*(m+n)+10000                   */
+    int32_t refactor_period;
+    int32_t degen_switch;  /* consecutive degenerate pivots before Bland     */
+} orc_control;
+
+typedef struct orc_stats {
+    int64_t iterations;
+    int64_t phase1_iterations;
+    int64_t bound_flips;
+    int64_t degenerate;
+    int64_t refactors;
+    int64_t bump_dim;      /* k at exit: basic structurals                   */
+    int64_t y_rows;        /* |Y| at exit: rows with a nonbasic slack         */
+    double seconds;
+    double price_bytes;    /* sum over iterations of 8*(|Y|*n + n + |Y|)      */
+} orc_stats;
+
+void orc_default_control(orc_control* c);
+
+/* Solve  min/max obj'x  s.t.  A x (dir) rhs,  lo <= x <= up.
+ * A: column-major m x n (lda = m).  dir: 1 '<=', 2 '>=', 3 '=='.
+ * Outputs (caller-allocated, may be NULL): x[n], y[m] duals, basis[m]
+ * (sorted basic variable ids: j<n structural, n+i slack, n+m+i artificial).
+ * trace (may be NULL): up to trace_cap entries of (entering, leaving) per
+ * iteration; leaving = -1 for a bound flip.
+ * Returns lp_solve status: 0 optimal, 1 sub-optimal (iteration cap),
+ * 2 infeasible, 3 unbounded, 5 numerical failure.  Negative = usage error. */
+int orc_solve_dense(int64_t m, int64_t n, const double* A, const int32_t* dir,
+                    const double* rhs, const double* obj, const double* lo,
+                    const double* up, int32_t maximize, const orc_control* ctl,
+                    double* objval, double* x, double* y, int64_t* basis,
+                    int64_t* trace, int64_t trace_cap, orc_stats* st);
+
+/* Counter-based synthetic dense LP:
+ * maximize c'x, A x <= b, x >= 0; A_ij, c_j ~ U[0,1), b_i = n/8 + U[0,1) n/4.
+ * Columns [col0, col0+ncols) of the m x n instance are written to A
+ * (column-major, lda = m).  c (ncols) and b (m) may be NULL. */
+void orc_generate_dense(uint64_t seed, int64_t m, int64_t n, int64_t col0,
+                        int64_t ncols, double* A, double* b, double* c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

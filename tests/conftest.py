@@ -1,0 +1,64 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (run on the GPU box)")
+    config.addinivalue_line("markers", "slow: larger CPU cases")
+
+
+def _dec(v):
+    if v == "inf":
+        return np.inf
+    if v == "-inf":
+        return -np.inf
+    return float(v)
+
+
+def load_known_answers():
+    with open(os.path.join(GOLDEN, "known_answers.json")) as f:
+        recs = json.load(f)
+    for r in recs:
+        r["A"] = np.array(r["A_rowmajor"], dtype=np.float64).reshape(r["m"], r["n"])
+        r["rhs"] = np.array([_dec(v) for v in r["rhs"]], dtype=np.float64)
+        r["lo"] = np.array([_dec(v) for v in r["lo"]], dtype=np.float64)
+        r["up"] = np.array([_dec(v) for v in r["up"]], dtype=np.float64)
+        r["obj"] = np.array(r["obj"], dtype=np.float64)
+        r["dir"] = np.array(r["dir"], dtype=np.int32)
+    return recs
+
+
+def load_dense_lps():
+    with open(os.path.join(GOLDEN, "dense_lps.json")) as f:
+        return json.load(f)
+
+
+def load_generator_vectors():
+    with open(os.path.join(GOLDEN, "generator_vectors.json")) as f:
+        return json.load(f)
+
+
+def feasible(A, dirs, rhs, x, lo, up, tol=2e-8):
+    """R/class.R:533-540 + R/utils.R:167-171 (compare_tol), plus bounds."""
+    lhs = A @ x if A.shape[0] else np.zeros(0)
+    ok = True
+    for i, d in enumerate(dirs):
+        t = tol * max(1.0, abs(rhs[i]))
+        if d == 1:
+            ok &= lhs[i] <= rhs[i] + t
+        elif d == 2:
+            ok &= lhs[i] >= rhs[i] - t
+        else:
+            ok &= abs(lhs[i] - rhs[i]) <= t
+    ok &= bool(np.all(x >= lo - tol * np.maximum(1, np.abs(lo[np.isfinite(lo)]).max(initial=1))))
+    ok &= bool(np.all(x <= up + tol * np.maximum(1, np.abs(up[np.isfinite(up)]).max(initial=1))))
+    return bool(ok)
