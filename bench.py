@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""bench.py -- simplex iterations/s on the dense random LP of BASELINE.json.
+
+Workload (BASELINE.json configs[2], the config its metric is quoted on):
+maximize c'x s.t. A x <= b, x >= 0, A dense 5000 x 50000 fp64 with
+A_ij, c_j ~ U[0,1), b_i = n/8 + U n/4, generated on the device
+by the counter-based generator (data: synthetic).  A "step" is one simplex
+iteration (BTRAN, pricing sweep + argmin, FTRAN, ratio test, basis update;
+periodic refactor included).  Inputs are resident in HBM before timing.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+Rank 0 prints one JSON line.  With N > 1 (torchrun) the columns of A are
+sharded across ranks (one process per GPU, RCCL min-loc + entering-column
+exchange per iteration) and all ranks run the same iterations: value is the
+iteration rate of the one LP (strong scaling).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "simplex iterations/sec + time-to-optimal, dense LP m=5k n=50k at 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--m", type=int, default=5000)
+    ap.add_argument("--n", type=int, default=50000)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-iters", type=int, default=300,
+                    help="iterations of the CPU oracle sample (after --warmup)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-optimal", action="store_true", help="skip the run to optimality")
+    ap.add_argument("--profile-price", type=int, default=1,
+                    help="HIP events around the pricing kernel (roofline)")
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """The CPU oracle (same algorithm, 1 thread) on a bounded sample of the same LP."""
+    import numpy as np
+    from oracle import generate_dense, solve_dense
+    A, b, c = generate_dense(args.seed, args.m, args.n)
+    t0 = time.time()
+    r = solve_dense(A, np.ones(args.m, np.int32), b, c, maximize=True,
+                    max_iter=args.warmup + args.cpu_iters, t_mark_iter=args.warmup)
+    wall = time.time() - t0
+    it = r.stats["iterations"] - args.warmup
+    secs = r.stats["seconds_at_mark"]
+    return {
+        "value": it / secs if secs > 0 else None,
+        "unit": "iterations/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"oracle/ (C, -O3, 1 thread) on the same LP, iterations "
+                   f"[{args.warmup}, {args.warmup + it}) timed; {wall:.1f}s wall incl. "
+                   f"iterations [0,{args.warmup})"),
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+    torch.cuda.set_device(local)
+
+    from easylp_amd import Problem
+    from easylp_amd._lib import ELP_PROFILE_PRICE, load
+
+    lib = load()
+    verbose = ELP_PROFILE_PRICE if args.profile_price else 0
+    p = Problem(args.m, args.n, device=local, verbose=verbose)
+    if world > 1:
+        import ctypes
+        uid = ctypes.create_string_buffer(128)
+        if rank == 0:
+            rc = lib.elp_comm_unique_id(uid)
+            if rc < 0:
+                raise SystemExit("multi-GPU communicator unavailable: " + lib.elp_last_error().decode())
+        obj = [uid.raw if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        p.comm_init(obj[0], world, rank)
+
+    p.load_generated(args.seed)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    # warmup (untimed)
+    st = p.iterate(args.warmup)
+    barrier()
+    s0 = p.stats()
+    t0 = time.perf_counter()
+    st = p.iterate(args.steps)
+    barrier()
+    t1 = time.perf_counter()
+    s1 = p.stats()
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    iters = s1["iterations"] - s0["iterations"]
+    value = iters / elapsed if elapsed > 0 else 0.0
+
+    price_s = s1["price_seconds"] - s0["price_seconds"]
+    price_b = s1["price_timed_bytes"] - s0["price_timed_bytes"]
+    price_n = s1["price_timed_launches"] - s0["price_timed_launches"]
+    achieved = price_b / price_s / 1e9 if price_s > 0 else None
+
+    # run on to optimality: time-to-optimal (device generation excluded)
+    tto = None
+    final = None
+    if not args.no_optimal:
+        st = p.solve()
+        barrier()
+        s2 = p.stats()
+        sol = p.solution(st)
+        tto = s2["seconds_loop"]
+        final = {"status": st, "iterations_to_optimal": s2["iterations"],
+                 "objective": sol.objval, "bump_dim": s2["bump_dim"], "y_rows": s2["y_rows"],
+                 "refactors": s2["refactors"]}
+        if world > 1:
+            tt = torch.tensor([tto], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            tto = float(tt.item())
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "iterations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / max(iters, 1),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (counter-based generator on device, seed %d)" % args.seed,
+            "config": {
+                "workload": "dense random LP m=%d n=%d (BASELINE configs[2])" % (args.m, args.n),
+                "m": args.m, "n": args.n, "seed": args.seed,
+                "parallelism": "column-shard x%d" % world if world > 1 else "single GPU",
+                "iterations_timed": iters,
+            },
+            "time_to_optimal_s": tto,
+            "final": final,
+            "roofline": {
+                "kernel": "k_price (pricing sweep + Dantzig argmin)",
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                "traffic": None,
+                "bytes_per_launch": price_b / price_n if price_n else None,
+                "avg_launch_us": 1e6 * price_s / price_n if price_n else None,
+                "launches_timed": price_n,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    p.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

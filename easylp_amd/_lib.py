@@ -1,0 +1,127 @@
+"""ctypes binding of include/easylp_hip.h (the C ABI of libeasylp_hip.so).
+
+The product path has no fallback: if the HIP library is missing or no GPU is
+visible, calls raise.  Nothing here imports or calls oracle/.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libeasylp_hip.so")
+
+ELP_LE, ELP_GE, ELP_EQ = 1, 2, 3
+ELP_OPTIMAL, ELP_SUBOPTIMAL, ELP_INFEASIBLE, ELP_UNBOUNDED = 0, 1, 2, 3
+ELP_NUMFAILURE, ELP_TIMEOUT = 5, 7
+ELP_PROFILE_PRICE = 2
+
+# every entry point the header declares (checked by tests/test_abi.py)
+EXPORTS = (
+    "elp_default_control", "elp_create", "elp_load_dense", "elp_load_dense_device",
+    "elp_load_generated", "elp_solve", "elp_iterate", "elp_get_solution", "elp_get_stats",
+    "elp_set_trace", "elp_get_trace", "elp_comm_unique_id", "elp_comm_init", "elp_destroy",
+    "elp_last_error", "elp_abi_version",
+)
+
+
+class ElpControl(ctypes.Structure):
+    _fields_ = [
+        ("tol_primal", ctypes.c_double),
+        ("tol_dual", ctypes.c_double),
+        ("tol_pivot", ctypes.c_double),
+        ("infinity", ctypes.c_double),
+        ("time_limit", ctypes.c_double),
+        ("max_iter", ctypes.c_int64),
+        ("refactor_period", ctypes.c_int32),
+        ("degen_switch", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("sync_every", ctypes.c_int32),
+        ("verbose", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 7),
+    ]
+
+
+class ElpStats(ctypes.Structure):
+    _fields_ = [
+        ("iterations", ctypes.c_int64),
+        ("phase1_iterations", ctypes.c_int64),
+        ("bound_flips", ctypes.c_int64),
+        ("degenerate", ctypes.c_int64),
+        ("refactors", ctypes.c_int64),
+        ("bump_dim", ctypes.c_int64),
+        ("y_rows", ctypes.c_int64),
+        ("host_polls", ctypes.c_int64),
+        ("seconds_total", ctypes.c_double),
+        ("seconds_loop", ctypes.c_double),
+        ("seconds_load", ctypes.c_double),
+        ("price_bytes", ctypes.c_double),
+        ("world_size", ctypes.c_int32),
+        ("rank", ctypes.c_int32),
+        ("col0", ctypes.c_int64),
+        ("ncols", ctypes.c_int64),
+        ("price_seconds", ctypes.c_double),
+        ("price_timed_bytes", ctypes.c_double),
+        ("price_timed_launches", ctypes.c_int64),
+    ]
+
+
+class ElpError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load the HIP library; raises (loudly) if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise ElpError(f"{path} not built: run `python -m easylp_amd.build` (no CPU fallback)")
+    lib = ctypes.CDLL(path)
+    P, vp = ctypes.POINTER, ctypes.c_void_p
+    i64, i32, dbl = ctypes.c_int64, ctypes.c_int32, ctypes.c_double
+    lib.elp_default_control.argtypes = [P(ElpControl)]
+    lib.elp_default_control.restype = None
+    lib.elp_create.argtypes = [P(vp), i64, i64, P(ElpControl)]
+    lib.elp_load_dense.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32]
+    lib.elp_load_dense_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32]
+    lib.elp_load_generated.argtypes = [vp, ctypes.c_uint64]
+    lib.elp_solve.argtypes = [vp, P(i32)]
+    lib.elp_iterate.argtypes = [vp, i64, P(i32)]
+    lib.elp_get_solution.argtypes = [vp, P(dbl), vp, vp, vp]
+    lib.elp_get_stats.argtypes = [vp, P(ElpStats)]
+    lib.elp_set_trace.argtypes = [vp, i64]
+    lib.elp_get_trace.argtypes = [vp, vp, i64, P(i64)]
+    lib.elp_comm_unique_id.argtypes = [vp]
+    lib.elp_comm_init.argtypes = [vp, vp, i32, i32]
+    lib.elp_destroy.argtypes = [vp]
+    lib.elp_destroy.restype = None
+    lib.elp_last_error.restype = ctypes.c_char_p
+    lib.elp_abi_version.restype = i32
+    for name in ("elp_create", "elp_load_dense", "elp_load_dense_device", "elp_load_generated",
+                 "elp_solve", "elp_iterate", "elp_get_solution", "elp_get_stats",
+                 "elp_set_trace", "elp_get_trace", "elp_comm_unique_id", "elp_comm_init"):
+        getattr(lib, name).restype = ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc < 0:
+        msg = _lib.elp_last_error().decode(errors="replace") if _lib else ""
+        raise ElpError(f"{what} failed ({rc}): {msg}")
+
+
+def default_control(**overrides) -> ElpControl:
+    lib = load()
+    c = ElpControl()
+    lib.elp_default_control(ctypes.byref(c))
+    for k, v in overrides.items():
+        if not hasattr(c, k):
+            raise KeyError(f"unknown control field {k!r}")
+        setattr(c, k, v)
+    return c

@@ -1,0 +1,688 @@
+// elp_api.hip -- host driver and C ABI (include/easylp_hip.h).
+//
+// The host never looks at the LP data during the solve: it enqueues
+// `sync_every` iterations (7-8 kernels each) on one HIP stream, then reads
+// the 300-byte device control block once to decide what happens next
+// (refactor, phase switch, stop).  This mirrors the loop of
+// oracle/elp_oracle.c run_phase() and the status mapping of
+// /root/reference/R/class.R:279-295.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/easylp_hip.h"
+#include "elp_comm.h"
+#include "elp_internal.h"
+
+using namespace elp;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                    \
+    do {                                                                                \
+        hipError_t _e = (expr);                                                         \
+        if (_e != hipSuccess)                                                           \
+            return fail(ELP_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));  \
+    } while (0)
+
+double now_s() {
+    using namespace std::chrono;
+    return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+struct elp_handle {
+    int64_t m = 0, n = 0;        // global problem size
+    int64_t col0 = 0, nloc = 0;  // this rank's column shard
+    elp_control ctl{};
+    int dev = 0;
+    hipStream_t st = nullptr;
+    Dev d{};
+    double* A_owned = nullptr;
+    size_t w_cap = 0;
+    bool loaded = false, done = false;
+    int maximize = 0;
+    int phase = 2;
+    bool any_art = false;
+    int32_t final_status = ELP_SUBOPTIMAL;
+    DevCtl* hctl = nullptr;  // pinned mirror
+    int k_sync = 0, ny_sync = 0, since_refactor_sync = 0;
+    std::vector<double> obj_h;  // global objective (for the objective value)
+    elp_stats stats{};
+    double t_solve_start = 0.0;
+    bool timing_started = false;
+    int64_t trace_cap = 0;
+    elp::Comm comm;  // multi-GPU (world 1 = no-op)
+    std::vector<hipEvent_t> ev;  // pricing-kernel timing pairs (profile mode)
+};
+
+extern "C" void elp_default_control(elp_control* c) {
+    std::memset(c, 0, sizeof(*c));
+    c->tol_primal = 1e-9;
+    c->tol_dual = 1e-9;
+    c->tol_pivot = 1e-9;
+    c->infinity = 1e30;
+    c->time_limit = 0.0;
+    c->max_iter = 0;
+    c->refactor_period = 100;
+    c->degen_switch = 50;
+    c->device = 0;
+    c->sync_every = 32;
+    c->verbose = 0;
+}
+
+extern "C" const char* elp_last_error(void) { return g_err.c_str(); }
+extern "C" int32_t elp_abi_version(void) { return ELP_ABI_VERSION; }
+
+static void free_dev(elp_handle* h) {
+    Dev& d = h->d;
+    void* ptrs[] = {h->A_owned, d.AR,  d.AS,    d.Minv,  d.W0,   d.W1,    d.b,     d.obj,
+                    d.lb,       d.ub,  d.cost,  d.xval,  d.asgn, d.xr,    d.xs,    d.y,
+                    d.t,        d.acol, d.aR,   d.alS,   d.alU,  d.zz,    d.zpart, d.vrow,
+                    d.vvec,     d.colA, d.rhs,  d.vstat, d.cover, d.rpos, d.Rl,    d.Sl,
+                    d.spos,     d.Yl,  d.ypos,  d.perm,  d.pivstep, d.nzlist, d.nzcount,
+                    d.cand,     d.ctl, d.trace};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    h->A_owned = nullptr;
+    d = Dev{};
+    if (h->hctl) (void)hipHostFree(h->hctl);
+    h->hctl = nullptr;
+}
+
+template <class T>
+static hipError_t dalloc(T** p, size_t count) {
+    return hipMalloc((void**)p, (count ? count : 1) * sizeof(T));
+}
+
+extern "C" int elp_create(elp_handle** out, int64_t m, int64_t n, const elp_control* ctl) {
+    if (!out) return fail(ELP_E_ARG, "elp_create: out is NULL");
+    *out = nullptr;
+    if (m < 0 || n < 1) return fail(ELP_E_ARG, "elp_create: need m >= 0 and n >= 1");
+    if (m > 0x3fffffff || n > 0x3fffffff) return fail(ELP_E_ARG, "elp_create: dimension too large");
+    elp_handle* h = new elp_handle();
+    if (ctl) h->ctl = *ctl;
+    else elp_default_control(&h->ctl);
+    if (h->ctl.refactor_period <= 0) h->ctl.refactor_period = 100;
+    if (h->ctl.degen_switch <= 0) h->ctl.degen_switch = 50;
+    if (h->ctl.sync_every <= 0) h->ctl.sync_every = 32;
+    if (!(h->ctl.infinity > 0)) h->ctl.infinity = 1e30;
+    h->m = m;
+    h->n = n;
+    h->col0 = 0;
+    h->nloc = n;
+    h->dev = h->ctl.device;
+    if (hipSetDevice(h->dev) != hipSuccess) {
+        delete h;
+        return fail(ELP_E_HIP, "elp_create: hipSetDevice failed");
+    }
+    if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return fail(ELP_E_HIP, "elp_create: stream creation failed");
+    }
+    *out = h;
+    return 0;
+}
+
+// Allocate every device buffer for the local shard (called by elp_load_*).
+static int alloc_all(elp_handle* h) {
+    Dev& d = h->d;
+    const int64_t m = h->m, n = h->nloc;
+    const int64_t mm = m > 0 ? m : 1;
+    d.m = (int32_t)m;
+    d.n = (int32_t)n;
+    d.nv = (int32_t)(n + 2 * m);
+    d.ldm = mm;
+    d.ldr = ((n + TILE_COLS - 1) / TILE_COLS) * TILE_COLS;
+    d.infinity = h->ctl.infinity;
+    const size_t nv = (size_t)(n + 2 * m);
+    hipError_t e = hipSuccess;
+    auto A = [&](hipError_t x) {
+        if (e == hipSuccess) e = x;
+    };
+    A(dalloc(&d.AR, (size_t)mm * (size_t)d.ldr));
+    A(dalloc(&d.AS, (size_t)mm * (size_t)mm));
+    A(dalloc(&d.Minv, (size_t)mm * (size_t)mm));
+    A(dalloc(&d.b, mm));
+    A(dalloc(&d.obj, n));
+    A(dalloc(&d.lb, nv));
+    A(dalloc(&d.ub, nv));
+    A(dalloc(&d.cost, nv));
+    A(dalloc(&d.xval, nv));
+    A(dalloc(&d.vstat, nv));
+    A(dalloc(&d.asgn, mm));
+    A(dalloc(&d.xr, mm));
+    A(dalloc(&d.xs, mm));
+    A(dalloc(&d.y, mm));
+    A(dalloc(&d.t, mm));
+    A(dalloc(&d.acol, mm));
+    A(dalloc(&d.aR, mm));
+    A(dalloc(&d.alS, mm));
+    A(dalloc(&d.alU, mm));
+    A(dalloc(&d.zz, mm));
+    A(dalloc(&d.zpart, (size_t)mm * (size_t)((mm + ZCHUNK - 1) / ZCHUNK)));
+    A(dalloc(&d.vrow, mm));
+    A(dalloc(&d.vvec, mm));
+    A(dalloc(&d.colA, mm));
+    A(dalloc(&d.rhs, mm));
+    A(dalloc(&d.cover, mm));
+    A(dalloc(&d.rpos, mm));
+    A(dalloc(&d.Rl, mm));
+    A(dalloc(&d.Sl, mm));
+    A(dalloc(&d.spos, n));
+    A(dalloc(&d.Yl, mm));
+    A(dalloc(&d.ypos, mm));
+    A(dalloc(&d.perm, mm));
+    A(dalloc(&d.pivstep, mm));
+    A(dalloc(&d.nzlist, n));
+    A(dalloc(&d.nzcount, 1));
+    A(dalloc(&d.cand, (size_t)((n + TILE_COLS - 1) / TILE_COLS) + 64));
+    A(dalloc(&d.ctl, 1));
+    A(dalloc(&d.trace, (size_t)(h->trace_cap > 0 ? 2 * h->trace_cap : 2)));
+    if (e != hipSuccess) {
+        free_dev(h);
+        return fail(ELP_E_NOMEM, std::string("device allocation failed: ") + hipGetErrorString(e));
+    }
+    A(hipHostMalloc((void**)&h->hctl, sizeof(DevCtl)));
+    // AR padding columns must read as zeros; Minv / AS / work start clean
+    A(hipMemsetAsync(d.AR, 0, (size_t)mm * (size_t)d.ldr * sizeof(double), h->st));
+    A(hipMemsetAsync(d.Minv, 0, (size_t)mm * (size_t)mm * sizeof(double), h->st));
+    A(hipMemsetAsync(d.zpart, 0, (size_t)mm * ((mm + ZCHUNK - 1) / ZCHUNK) * sizeof(double), h->st));
+    if (e != hipSuccess) {
+        free_dev(h);
+        return fail(ELP_E_HIP, std::string("device init failed: ") + hipGetErrorString(e));
+    }
+    return 0;
+}
+
+static int ensure_w(elp_handle* h, int k) {
+    const size_t need = (size_t)k * (size_t)k;
+    if (need <= h->w_cap && h->d.W0) return 0;
+    if (h->d.W0) (void)hipFree(h->d.W0);
+    if (h->d.W1) (void)hipFree(h->d.W1);
+    h->d.W0 = h->d.W1 = nullptr;
+    size_t cap = std::max<size_t>(need, 64 * 64);
+    cap = std::max(cap, h->w_cap * 2);
+    if (dalloc(&h->d.W0, cap) != hipSuccess || dalloc(&h->d.W1, cap) != hipSuccess)
+        return fail(ELP_E_NOMEM, "refactor workspace allocation failed");
+    h->w_cap = cap;
+    return 0;
+}
+
+// common tail of elp_load_*: bounds, rows, control block, phase decision
+static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, const double* obj,
+                       const double* lo, const double* up, int32_t maximize) {
+    const int64_t m = h->m, n = h->n, n0 = h->col0, nl = h->nloc;
+    Dev& d = h->d;
+    for (int64_t i = 0; i < m; ++i)
+        if (dir[i] < ELP_LE || dir[i] > ELP_EQ) return fail(ELP_E_ARG, "dir must be 1 (<=), 2 (>=) or 3 (==)");
+    h->maximize = maximize ? 1 : 0;
+    d.maximize = h->maximize;
+    h->obj_h.assign(obj, obj + n);
+    // host-side staging of the small vectors (local column shard)
+    std::vector<double> lo_h(nl), up_h(nl), slb(m), sub(m);
+    for (int64_t j = 0; j < nl; ++j) {
+        lo_h[j] = lo ? lo[n0 + j] : 0.0;
+        up_h[j] = up ? up[n0 + j] : HUGE_VAL;
+    }
+    for (int64_t i = 0; i < m; ++i) {
+        slb[i] = dir[i] == ELP_GE ? -HUGE_VAL : 0.0;
+        sub[i] = dir[i] == ELP_LE ? HUGE_VAL : 0.0;
+    }
+    double *dlo = nullptr, *dup = nullptr, *drhs = nullptr;
+    HIPCHK(dalloc(&dlo, nl));
+    HIPCHK(dalloc(&dup, nl));
+    HIPCHK(dalloc(&drhs, m));
+    HIPCHK(hipMemcpyAsync(dlo, lo_h.data(), nl * sizeof(double), hipMemcpyHostToDevice, h->st));
+    HIPCHK(hipMemcpyAsync(dup, up_h.data(), nl * sizeof(double), hipMemcpyHostToDevice, h->st));
+    if (m) {
+        HIPCHK(hipMemcpyAsync(drhs, rhs, m * sizeof(double), hipMemcpyHostToDevice, h->st));
+        HIPCHK(hipMemcpyAsync(d.lb + nl, slb.data(), m * sizeof(double), hipMemcpyHostToDevice, h->st));
+        HIPCHK(hipMemcpyAsync(d.ub + nl, sub.data(), m * sizeof(double), hipMemcpyHostToDevice, h->st));
+    }
+    HIPCHK(hipMemcpyAsync(d.obj, obj + n0, nl * sizeof(double), hipMemcpyHostToDevice, h->st));
+    DevCtl c{};
+    c.status = ST_RUN;
+    c.phase = 1;
+    c.iter_limit = h->ctl.max_iter > 0 ? h->ctl.max_iter : 100 * (m + n) + 10000;
+    c.iter_stop = INT64_MAX;
+    c.refactor_period = h->ctl.refactor_period;
+    c.degen_switch = h->ctl.degen_switch;
+    c.tol_primal = h->ctl.tol_primal;
+    c.tol_dual = h->ctl.tol_dual;
+    c.tol_pivot = h->ctl.tol_pivot;
+    c.trace_cap = h->trace_cap;
+    c.unb_var = -1;
+    *h->hctl = c;
+    HIPCHK(hipMemcpyAsync(d.ctl, h->hctl, sizeof(DevCtl), hipMemcpyHostToDevice, h->st));
+    HIPCHK(launch_init(d, dlo, dup, drhs, h->st));
+    HIPCHK(hipMemcpyAsync(h->hctl, d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    (void)hipFree(dlo);
+    (void)hipFree(dup);
+    (void)hipFree(drhs);
+    int infeasible = h->hctl->infeasible_bounds;
+    if (h->comm.world > 1) infeasible = h->comm.allreduce_max_int(infeasible, h->st);
+    h->k_sync = 0;
+    h->ny_sync = h->hctl->ny;
+    h->since_refactor_sync = 0;
+    h->any_art = h->hctl->ny > 0;
+    h->loaded = true;
+    h->done = false;
+    h->stats = elp_stats{};
+    h->stats.world_size = h->comm.world;
+    h->stats.rank = h->comm.rank;
+    h->stats.col0 = h->col0;
+    h->stats.ncols = h->nloc;
+    h->timing_started = false;
+    if (infeasible) {  // R/class.R:297-298: lower > upper -> "unfeasible"
+        h->done = true;
+        h->final_status = ELP_INFEASIBLE;
+        return 0;
+    }
+    if (h->any_art) {
+        h->phase = 1;
+    } else {
+        HIPCHK(launch_phase2(d, h->st));
+        h->phase = 2;
+        c = *h->hctl;
+        h->hctl->phase = 2;
+        HIPCHK(hipMemcpyAsync(&d.ctl->phase, &h->hctl->phase, sizeof(int32_t), hipMemcpyHostToDevice, h->st));
+        HIPCHK(hipStreamSynchronize(h->st));
+    }
+    return 0;
+}
+
+static int prep_load(elp_handle* h) {
+    if (!h) return fail(ELP_E_ARG, "NULL handle");
+    HIPCHK(hipSetDevice(h->dev));
+    if (h->loaded) free_dev(h);
+    h->loaded = false;
+    if (h->comm.world > 1) {
+        const int64_t P = h->comm.world, r = h->comm.rank;
+        h->col0 = r * h->n / P;
+        h->nloc = (r + 1) * h->n / P - h->col0;
+    }
+    return alloc_all(h);
+}
+
+extern "C" int elp_load_dense(elp_handle* h, const double* A, const int32_t* dir, const double* rhs,
+                              const double* obj, const double* lo, const double* up, int32_t maximize) {
+    const double t0 = now_s();
+    if (!h || !obj || (h->m > 0 && (!A || !dir || !rhs))) return fail(ELP_E_ARG, "elp_load_dense: NULL input");
+    int rc = prep_load(h);
+    if (rc) return rc;
+    const size_t cnt = (size_t)h->m * (size_t)h->nloc;
+    HIPCHK(dalloc(&h->A_owned, cnt));
+    if (cnt)
+        HIPCHK(hipMemcpyAsync(h->A_owned, A + (size_t)h->col0 * (size_t)h->m, cnt * sizeof(double),
+                              hipMemcpyHostToDevice, h->st));
+    h->d.A = h->A_owned;
+    rc = load_common(h, dir, rhs, obj, lo, up, maximize);
+    h->stats.seconds_load = now_s() - t0;
+    return rc;
+}
+
+extern "C" int elp_load_dense_device(elp_handle* h, const double* dA, const int32_t* dir,
+                                     const double* rhs, const double* obj, const double* lo,
+                                     const double* up, int32_t maximize) {
+    const double t0 = now_s();
+    if (!h || !obj || (h->m > 0 && (!dA || !dir || !rhs)))
+        return fail(ELP_E_ARG, "elp_load_dense_device: NULL input");
+    int rc = prep_load(h);
+    if (rc) return rc;
+    h->d.A = dA + (size_t)h->col0 * (size_t)h->m;
+    rc = load_common(h, dir, rhs, obj, lo, up, maximize);
+    h->stats.seconds_load = now_s() - t0;
+    return rc;
+}
+
+extern "C" int elp_load_generated(elp_handle* h, uint64_t seed) {
+    const double t0 = now_s();
+    int rc = prep_load(h);
+    if (rc) return rc;
+    const int64_t m = h->m, n = h->n;
+    HIPCHK(dalloc(&h->A_owned, (size_t)m * (size_t)h->nloc));
+    double *db = nullptr, *dc = nullptr;
+    HIPCHK(dalloc(&db, m));
+    HIPCHK(dalloc(&dc, n));
+    // generate this rank's shard of A plus the full b and c (c globally, for the objective)
+    {
+        Dev g = h->d;
+        g.n = (int32_t)h->nloc;
+        HIPCHK(launch_generate(g, seed, h->col0, n, h->A_owned, db, nullptr, h->st));
+        g.n = (int32_t)n;
+        HIPCHK(launch_generate(g, seed, 0, n, nullptr, db, dc, h->st));
+    }
+    std::vector<double> b(m), c(n), lo(n, 0.0), up(n, HUGE_VAL);
+    std::vector<int32_t> dir(m, ELP_LE);
+    if (m) HIPCHK(hipMemcpyAsync(b.data(), db, m * sizeof(double), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipMemcpyAsync(c.data(), dc, n * sizeof(double), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    (void)hipFree(db);
+    (void)hipFree(dc);
+    h->d.A = h->A_owned;
+    rc = load_common(h, dir.data(), b.data(), c.data(), lo.data(), up.data(), 1);
+    h->stats.seconds_load = now_s() - t0;
+    return rc;
+}
+
+static int push_ctl_fields(elp_handle* h) {
+    // host-owned fields are written as one block (the device is idle at a poll)
+    HIPCHK(hipMemcpyAsync(h->d.ctl, h->hctl, sizeof(DevCtl), hipMemcpyHostToDevice, h->st));
+    return 0;
+}
+
+static int do_refactor(elp_handle* h, int k) {
+    int rc = ensure_w(h, k);
+    if (rc) return rc;
+    HIPCHK(launch_refactor(h->d, k, h->st));
+    h->stats.refactors++;
+    return 0;
+}
+
+// the polling loop; budget = iterations allowed in this call
+static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
+    if (h->done) {
+        *lp_status = h->final_status;
+        return 0;
+    }
+    const double t_loop0 = now_s();
+    if (!h->timing_started) {
+        h->t_solve_start = t_loop0;
+        h->timing_started = true;
+    }
+    DevCtl* c = h->hctl;
+    // resume: refresh the mirror, set the stop budget
+    HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    c->iter_stop = budget >= INT64_MAX - c->iter ? INT64_MAX : c->iter + budget;
+    if (c->status == ST_STOP) c->status = ST_RUN;
+    c->phase = h->phase;
+    int rc = push_ctl_fields(h);
+    if (rc) return rc;
+    const int period = h->ctl.refactor_period;
+    const bool prof = (h->ctl.verbose & ELP_PROFILE_PRICE) != 0;
+    if (prof && (int)h->ev.size() < 2 * h->ctl.sync_every) {
+        for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+        h->ev.assign(2 * h->ctl.sync_every, nullptr);
+        for (auto& e : h->ev) HIPCHK(hipEventCreate(&e));
+    }
+    for (;;) {
+        // host-side loop-top work at a poll (no launch is wasted on it):
+        // budget exhausted -> return; refactor due (phase 2) -> do it now.
+        if (c->status == ST_RUN && c->iter >= c->iter_stop && c->iter < c->iter_limit) {
+            *lp_status = ELP_SUBOPTIMAL;
+            h->stats.seconds_loop += now_s() - t_loop0;
+            return 0;
+        }
+        if (c->status == ST_RUN && h->phase == 2 && c->since_refactor >= period &&
+            c->iter < c->iter_limit) {
+            rc = do_refactor(h, c->k);
+            if (rc) return rc;
+            HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+            HIPCHK(hipStreamSynchronize(h->st));
+            if (c->status == ST_NUMFAIL) {
+                h->done = true;
+                h->final_status = ELP_NUMFAILURE;
+                break;
+            }
+            c->since_refactor = 0;
+            rc = push_ctl_fields(h);
+            if (rc) return rc;
+        }
+        const int k0 = c->k, ny0 = c->ny;
+        int chunk = h->ctl.sync_every;
+        const int to_refactor = period - c->since_refactor;
+        if (to_refactor > 0 && to_refactor < chunk) chunk = to_refactor;
+        const int64_t left = c->iter_stop - c->iter;
+        if (left > 0 && left < chunk) chunk = (int)left;
+        if (chunk < 1) chunk = 1;
+        const double bytes0 = c->price_bytes;
+        for (int t = 0; t < chunk; ++t) {
+            const int kub = (int)std::min<int64_t>(h->m, (int64_t)k0 + t);
+            const int nyub = (int)std::min<int64_t>(h->m, (int64_t)ny0 + t);
+            hipEvent_t e0 = prof ? h->ev[2 * t] : nullptr, e1 = prof ? h->ev[2 * t + 1] : nullptr;
+            HIPCHK(launch_iteration(h->d, kub, nyub, h->phase, h->st, e0, e1));
+        }
+        HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+        HIPCHK(hipStreamSynchronize(h->st));
+        h->stats.host_polls++;
+        const int32_t s = c->status;
+        if (prof && s == ST_RUN) {  // every launch of the chunk did work
+            for (int t = 0; t < chunk; ++t) {
+                float ms = 0.f;
+                HIPCHK(hipEventElapsedTime(&ms, h->ev[2 * t], h->ev[2 * t + 1]));
+                h->stats.price_seconds += 1e-3 * ms;
+            }
+            h->stats.price_timed_launches += chunk;
+            h->stats.price_timed_bytes += c->price_bytes - bytes0;
+        }
+        if (s == ST_RUN) {
+            if (h->ctl.time_limit > 0 && now_s() - h->t_solve_start > h->ctl.time_limit) {
+                h->done = true;
+                h->final_status = ELP_TIMEOUT;
+                break;
+            }
+            continue;
+        }
+        if (s == ST_REFACTOR) {
+            rc = do_refactor(h, c->k);
+            if (rc) return rc;
+            HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+            HIPCHK(hipStreamSynchronize(h->st));
+            if (c->status == ST_NUMFAIL) {
+                h->done = true;
+                h->final_status = ELP_NUMFAILURE;
+                break;
+            }
+            c->since_refactor = 0;
+            c->status = ST_RUN;
+            rc = push_ctl_fields(h);
+            if (rc) return rc;
+            continue;
+        }
+        if (s == ST_STOP) {
+            *lp_status = ELP_SUBOPTIMAL;
+            h->stats.seconds_loop += now_s() - t_loop0;
+            return 0;
+        }
+        if ((s == ST_PHASE_OPT || s == ST_P1DONE) && h->phase == 1) {
+            if (s == ST_PHASE_OPT && c->art_sum > c->tol_inf) {
+                h->done = true;
+                h->final_status = ELP_INFEASIBLE;
+                break;
+            }
+            HIPCHK(launch_phase2(h->d, h->st));
+            h->phase = 2;
+            rc = do_refactor(h, c->k);
+            if (rc) return rc;
+            HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+            HIPCHK(hipStreamSynchronize(h->st));
+            if (c->status == ST_NUMFAIL) {
+                h->done = true;
+                h->final_status = ELP_NUMFAILURE;
+                break;
+            }
+            c->phase = 2;
+            c->since_refactor = 0;
+            c->ndegen = 0;
+            c->bland = 0;
+            c->status = ST_RUN;
+            rc = push_ctl_fields(h);
+            if (rc) return rc;
+            continue;
+        }
+        h->done = true;
+        if (s == ST_PHASE_OPT) h->final_status = ELP_OPTIMAL;
+        else if (s == ST_UNBOUNDED) h->final_status = ELP_UNBOUNDED;
+        else if (s == ST_ITERCAP) h->final_status = ELP_SUBOPTIMAL;
+        else h->final_status = ELP_NUMFAILURE;
+        break;
+    }
+    h->stats.seconds_loop += now_s() - t_loop0;
+    *lp_status = h->final_status;
+    return 0;
+}
+
+extern "C" int elp_solve(elp_handle* h, int32_t* lp_status) {
+    if (!h || !lp_status) return fail(ELP_E_ARG, "elp_solve: NULL argument");
+    if (!h->loaded) return fail(ELP_E_STATE, "elp_solve: no problem loaded");
+    HIPCHK(hipSetDevice(h->dev));
+    const double t0 = now_s();
+    const int rc = run_loop(h, INT64_MAX, lp_status);
+    h->stats.seconds_total += now_s() - t0;
+    return rc;
+}
+
+extern "C" int elp_iterate(elp_handle* h, int64_t iters, int32_t* lp_status) {
+    if (!h || !lp_status || iters < 0) return fail(ELP_E_ARG, "elp_iterate: bad argument");
+    if (!h->loaded) return fail(ELP_E_STATE, "elp_iterate: no problem loaded");
+    HIPCHK(hipSetDevice(h->dev));
+    const double t0 = now_s();
+    const int rc = run_loop(h, iters, lp_status);
+    h->stats.seconds_total += now_s() - t0;
+    return rc;
+}
+
+extern "C" int elp_get_solution(elp_handle* h, double* objval, double* x, double* y, int64_t* basis) {
+    if (!h || !h->loaded) return fail(ELP_E_STATE, "elp_get_solution: no problem loaded");
+    HIPCHK(hipSetDevice(h->dev));
+    const int64_t m = h->m, n = h->n, nl = h->nloc;
+    HIPCHK(hipMemcpyAsync(h->hctl, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+    // structural values of the local shard, gathered to every rank
+    std::vector<double> xs((size_t)n, 0.0);
+    double* dx = nullptr;
+    HIPCHK(dalloc(&dx, nl));
+    HIPCHK(launch_extract(h->d, dx, h->st));
+    HIPCHK(hipMemcpyAsync(xs.data() + h->col0, dx, nl * sizeof(double), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    (void)hipFree(dx);
+    if (h->comm.world > 1) {
+        int rc = h->comm.allgather_shards(xs.data(), h->n, h->st);
+        if (rc) return rc;
+    }
+    const DevCtl& c = *h->hctl;
+    const double BIG = h->ctl.infinity;
+    const bool unb = h->done && h->final_status == ELP_UNBOUNDED;
+    // the unbounded variable's global id (shard-local q -> global)
+    int64_t uvar = -1;
+    if (unb && c.unb_var >= 0 && c.unb_var < h->nloc) uvar = h->col0 + c.unb_var;
+    if (unb && uvar >= 0 && uvar < n) xs[uvar] = c.unb_sig > 0 ? BIG : -BIG;
+    if (x) std::memcpy(x, xs.data(), (size_t)n * sizeof(double));
+    if (objval) {
+        if (unb) {
+            *objval = h->maximize ? BIG : -BIG;
+        } else {
+            // get.objective: sum obj_j x_j (seq fma, the oracle's order)
+            double acc = 0.0;
+            for (int64_t j = 0; j < n; ++j) {
+                acc = std::fma(h->obj_h[j], xs[j], acc);
+            }
+            *objval = acc;
+        }
+    }
+    if (y && m) {
+        HIPCHK(hipMemcpyAsync(y, h->d.y, m * sizeof(double), hipMemcpyDeviceToHost, h->st));
+        HIPCHK(hipStreamSynchronize(h->st));
+        if (h->maximize)
+            for (int64_t i = 0; i < m; ++i) y[i] = -y[i];
+    }
+    if (basis && m) {
+        std::vector<int32_t> cover(m), Sl(std::max(c.k, 1));
+        HIPCHK(hipMemcpyAsync(cover.data(), h->d.cover, m * sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
+        if (c.k)
+            HIPCHK(hipMemcpyAsync(Sl.data(), h->d.Sl, c.k * sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
+        HIPCHK(hipStreamSynchronize(h->st));
+        std::vector<int64_t> bv;
+        bv.reserve(m);
+        // local var ids -> global ids: structural j -> col0 + j; slack n_loc + i -> n + i
+        auto glob = [&](int64_t v) -> int64_t {
+            if (v < nl) return h->col0 + v;
+            if (v < nl + m) return n + (v - nl);
+            return n + m + (v - nl - m);
+        };
+        for (int64_t i = 0; i < m; ++i)
+            if (cover[i] >= 0) bv.push_back(glob(cover[i]));
+        for (int p = 0; p < c.k; ++p) bv.push_back(glob(Sl[p]));
+        std::sort(bv.begin(), bv.end());
+        for (size_t t = 0; t < bv.size() && (int64_t)t < m; ++t) basis[t] = bv[t];
+    }
+    return 0;
+}
+
+extern "C" int elp_get_stats(elp_handle* h, elp_stats* st) {
+    if (!h || !st) return fail(ELP_E_ARG, "elp_get_stats: NULL argument");
+    if (h->loaded) {
+        HIPCHK(hipSetDevice(h->dev));
+        HIPCHK(hipMemcpyAsync(h->hctl, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+        HIPCHK(hipStreamSynchronize(h->st));
+        const DevCtl& c = *h->hctl;
+        h->stats.iterations = c.iter;
+        h->stats.phase1_iterations = c.phase1_iters;
+        h->stats.bound_flips = c.flips;
+        h->stats.degenerate = c.degenerate;
+        h->stats.bump_dim = c.k;
+        h->stats.y_rows = c.ny;
+        h->stats.price_bytes = c.price_bytes;
+    }
+    *st = h->stats;
+    return 0;
+}
+
+extern "C" int elp_set_trace(elp_handle* h, int64_t capacity) {
+    if (!h || capacity < 0) return fail(ELP_E_ARG, "elp_set_trace: bad argument");
+    if (h->loaded) return fail(ELP_E_STATE, "elp_set_trace: call before elp_load_*");
+    h->trace_cap = capacity;
+    return 0;
+}
+
+extern "C" int elp_get_trace(elp_handle* h, int64_t* pairs, int64_t capacity, int64_t* count) {
+    if (!h || !count) return fail(ELP_E_ARG, "elp_get_trace: NULL argument");
+    if (!h->loaded) return fail(ELP_E_STATE, "elp_get_trace: no problem loaded");
+    HIPCHK(hipSetDevice(h->dev));
+    HIPCHK(hipMemcpyAsync(h->hctl, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    const int64_t cnt = std::min<int64_t>(std::min<int64_t>(h->hctl->iter, h->trace_cap), capacity);
+    if (cnt > 0 && pairs) {
+        HIPCHK(hipMemcpyAsync(pairs, h->d.trace, 2 * cnt * sizeof(int64_t), hipMemcpyDeviceToHost, h->st));
+        HIPCHK(hipStreamSynchronize(h->st));
+    }
+    *count = cnt;
+    return 0;
+}
+
+extern "C" void elp_destroy(elp_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->dev);
+    if (h->st) (void)hipStreamSynchronize(h->st);
+    free_dev(h);
+    for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+    h->comm.destroy();
+    if (h->st) (void)hipStreamDestroy(h->st);
+    delete h;
+}
+
+extern "C" int elp_comm_unique_id(uint8_t id[128]) { return elp::Comm::unique_id(id); }
+
+extern "C" int elp_comm_init(elp_handle* h, const uint8_t id[128], int32_t world_size, int32_t rank) {
+    if (!h || !id || world_size < 1 || rank < 0 || rank >= world_size)
+        return fail(ELP_E_ARG, "elp_comm_init: bad argument");
+    if (h->loaded) return fail(ELP_E_STATE, "elp_comm_init: call before elp_load_*");
+    HIPCHK(hipSetDevice(h->dev));
+    return h->comm.init(id, world_size, rank);
+}

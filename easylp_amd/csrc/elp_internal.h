@@ -1,0 +1,100 @@
+// elp_internal.h -- device state shared by the gfx950 kernels and the host
+// driver of the dense revised simplex (see DESIGN.md for the data layout).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace elp {
+
+// variable status (same codes as oracle/elp_oracle.c)
+// VS_FIXED: nonbasic with lb == ub (never enters; pricing then needs no bounds)
+enum : int8_t { VS_BASIC = 0, VS_LOWER = 1, VS_UPPER = 2, VS_FREE = 3, VS_FIXED = 4 };
+
+// device loop status
+enum : int32_t {
+    ST_RUN = 0,
+    ST_PHASE_OPT = 1,  // no entering candidate: current phase optimal
+    ST_UNBOUNDED = 2,
+    ST_REFACTOR = 3,   // refactor period reached at loop top
+    ST_ITERCAP = 4,
+    ST_P1DONE = 5,     // phase-1 artificial sum within tolerance at loop top
+    ST_NUMFAIL = 6,
+    ST_STOP = 7,       // elp_iterate budget reached at loop top
+};
+
+// pivot cases (oracle/elp_oracle.c "case A".."case E")
+enum : int32_t { PC_NONE = 0, PC_A = 1, PC_B = 2, PC_C = 3, PC_D = 4, PC_E = 5 };
+enum : int32_t { ACT_NONE = 0, ACT_FLIP = 1, ACT_PIVOT = 2 };
+
+constexpr int PRICE_SPLIT = 4;  // slot chunks per pricing tile (one per wave)
+constexpr int ZCHUNK = 64;      // bump positions per FTRAN-z partial
+constexpr int TILE_COLS = 128;  // columns per pricing workgroup (2 per lane)
+
+struct Plan {
+    int32_t action, pcase, k_old, p;
+    int32_t a, b, last, row;      // row: B leaving-cover row / D leaving row i1
+    int32_t q, pad0;
+    int32_t y_rm_slot, y_rm_last; // -1: no removal
+    int32_t y_ap_slot, y_ap_row;  // -1: no append
+    double piv;                   // A: alS[p]; B: delta; C: Minv[b][a]
+    double xq;
+};
+
+struct DevCtl {
+    int32_t status, phase, k, ny;
+    int64_t iter, iter_limit, iter_stop;
+    int32_t since_refactor, refactor_period;
+    int32_t ndegen, bland, degen_switch, unb_var;
+    int64_t phase1_iters, flips, degenerate;
+    double tol_inf, unb_sig;
+    double tol_primal, tol_dual, tol_pivot, art_sum;
+    int32_t q, ntiles;
+    double dq, sig;
+    Plan plan;
+    int64_t trace_cap;
+    int32_t infeasible_bounds, pad1;
+    double price_bytes;    // algorithmic bytes of every pricing pass that ran
+    int64_t price_passes;
+};
+
+struct Cand {
+    double score, d;
+    int64_t j;  // -1: none
+};
+
+// Everything a kernel needs, passed by value (pointers into device memory).
+struct Dev {
+    int32_t m, n, nv, pad;
+    int64_t ldm;   // Minv leading dimension (= max(m,1))
+    int64_t ldr;   // AR leading dimension (n rounded up to TILE_COLS)
+    const double* A;  // column-major m x n
+    double* AR;       // Y rows, row-major (m x ldr capacity)
+    double* AS;       // basic structural columns, column-major (m x m capacity)
+    double* Minv;     // bump inverse, row-major ldm x ldm
+    double *W0, *W1;  // Gauss-Jordan work (k x k each)
+    double *b, *obj, *lb, *ub, *cost, *xval, *asgn;
+    double *xr, *xs, *y, *t, *acol, *aR, *alS, *alU, *zz, *zpart;
+    double *vrow, *vvec, *colA, *rhs;
+    int8_t* vstat;
+    int32_t *cover, *rpos, *Rl, *Sl, *spos, *Yl, *ypos, *perm, *pivstep, *nzlist, *nzcount;
+    Cand* cand;
+    DevCtl* ctl;
+    int64_t* trace;
+    int32_t maximize, pad2;
+    double infinity;
+};
+
+// ---------------------------------------------------------------- launches
+// Each returns hipGetLastError() of its launch.
+hipError_t launch_generate(const Dev& d, uint64_t seed, int64_t col0, int64_t n_global,
+                           double* A, double* b, double* c, hipStream_t st);
+hipError_t launch_init(const Dev& d, const double* lo, const double* up, const double* rhs,
+                       hipStream_t st);
+// ev0/ev1 (may be null): events recorded around the pricing kernel
+hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStream_t st,
+                            hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+hipError_t launch_refactor(const Dev& d, int k, hipStream_t st);
+hipError_t launch_phase2(const Dev& d, hipStream_t st);
+hipError_t launch_extract(const Dev& d, double* xout, hipStream_t st);
+
+}  // namespace elp

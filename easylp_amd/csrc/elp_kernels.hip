@@ -1,0 +1,1134 @@
+// elp_kernels.hip -- gfx950 kernels of the dense revised simplex.
+//
+// One simplex iteration is seven launches on one stream:
+//   k_btran       y_R = Minv^T c_S (+ loop-top checks)             O(k^2)
+//   k_price       d_j = c_j - AR[:,j]^T y_Y, fused Dantzig argmax    O(|Y| n)  <- HBM sweep
+//   k_select      entering column q (min-loc over tiles + slacks)   O(n/128 + m)
+//   k_ftran_bump  alpha_S = Minv a_R(q)   (one wave per row)         O(k^2)
+//   k_ftran_z     z = AS alpha_S, chunked partials                   O(m k)
+//   k_ratio       Harris two-pass ratio test, primal update, plan    O(m)
+//   k_rowminv     row of B^-1 for cases B/D                          O(k^2)
+//   k_update      Minv rank-one / bordered update + AS / AR copies    O(k^2 + n)
+// Every fp reduction follows the order of oracle/elp_oracle.c (explicit fma,
+// built with -ffp-contract=off), so the pivot sequence is the oracle's.
+// Kernels read the device control block and return early unless the loop is
+// running, so the host can enqueue several iterations between polls.
+#include "elp_internal.h"
+
+#include <math.h>
+
+namespace elp {
+
+#define DEV __device__ __forceinline__
+
+// ------------------------------------------------------------ generator
+DEV uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+DEV uint64_t gen_key(uint64_t seed, uint64_t stream) {
+    return mix64(seed * 0x9E3779B97F4A7C15ULL + stream * 0xD1B54A32D192ED03ULL +
+                 0x632BE59BD9B4E019ULL);
+}
+DEV double gen_u01k(uint64_t key, uint64_t idx) {
+    const uint64_t z = mix64(key + (idx + 1) * 0x9E3779B97F4A7C15ULL);
+    return (double)(z >> 11) * 0x1.0p-53;
+}
+
+__global__ void k_gen_A(uint64_t seed, int m, int64_t ncols, int64_t col0, double* __restrict__ A) {
+    const uint64_t key = gen_key(seed, 0);
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    for (int64_t jj = blockIdx.y; jj < ncols; jj += gridDim.y) {
+        const uint64_t j = (uint64_t)(col0 + jj);
+        A[(size_t)jj * (size_t)m + (size_t)i] = gen_u01k(key, (uint64_t)i + j * (uint64_t)m);
+    }
+}
+__global__ void k_gen_bc(uint64_t seed, int m, int64_t ncols, int64_t col0, int64_t n_global,
+                         double* __restrict__ b, double* __restrict__ c) {
+    const uint64_t kb = gen_key(seed, 2), kc = gen_key(seed, 1);
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const double e = (double)n_global / 8.0, qq = (double)n_global / 4.0;
+    if (t < m) b[t] = e + gen_u01k(kb, (uint64_t)t) * qq;
+    if (t < ncols) c[t] = gen_u01k(kc, (uint64_t)(col0 + t));
+}
+
+// ------------------------------------------------------------ helpers
+DEV double wave_tree(double v) {  // butterfly 32..1; lane 0 == oracle wave_dot tree
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off);
+    return v;
+}
+DEV double unit_sign(const Dev& d, int var, int row) {
+    return var >= d.n + d.m ? d.asgn[row] : 1.0;
+}
+DEV bool cand_better(const Cand& a, const Cand& b, int bland) {
+    if (a.j < 0) return false;
+    if (b.j < 0) return true;
+    if (bland) return a.j < b.j;
+    return a.score > b.score || (a.score == b.score && a.j < b.j);
+}
+DEV Cand shfl_cand(const Cand& c, int off) {
+    Cand o;
+    o.score = __shfl_xor(c.score, off);
+    o.d = __shfl_xor(c.d, off);
+    o.j = __shfl_xor((long long)c.j, off);
+    return o;
+}
+// block-wide argmax of candidates; result valid in every thread
+template <int NT>
+DEV Cand block_best(Cand c, int bland, Cand* lds) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        Cand o = shfl_cand(c, off);
+        if (cand_better(o, c, bland)) c = o;
+    }
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) lds[w] = c;
+    __syncthreads();
+    Cand r = lds[0];
+    for (int i = 1; i < NT / 64; ++i)
+        if (cand_better(lds[i], r, bland)) r = lds[i];
+    __syncthreads();
+    return r;
+}
+template <int NT>
+DEV double block_min(double v, double* lds) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fmin(v, __shfl_xor(v, off));
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) lds[w] = v;
+    __syncthreads();
+    double r = lds[0];
+    for (int i = 1; i < NT / 64; ++i) r = fmin(r, lds[i]);
+    __syncthreads();
+    return r;
+}
+template <int NT>
+DEV double block_max(double v, double* lds) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) lds[w] = v;
+    __syncthreads();
+    double r = lds[0];
+    for (int i = 1; i < NT / 64; ++i) r = fmax(r, lds[i]);
+    __syncthreads();
+    return r;
+}
+
+// wave-order phase-1 sum (oracle art_sum): executed by ONE wave
+DEV double wave_art_sum(const Dev& d) {
+    const int lane = threadIdx.x & 63;
+    double acc = 0.0;
+    for (int i = lane; i < d.m; i += 64)
+        if (d.cover[i] >= d.n + d.m) acc = acc + d.xr[i];
+    return wave_tree(acc);
+}
+
+// ============================================================== init
+__global__ void k_init_cols(Dev d, const double* __restrict__ lo, const double* __restrict__ up) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= d.n) return;
+    double l = lo ? lo[j] : 0.0, u = up ? up[j] : HUGE_VAL;
+    if (l <= -d.infinity) l = -HUGE_VAL;
+    if (u >= d.infinity) u = HUGE_VAL;
+    d.lb[j] = l;
+    d.ub[j] = u;
+    d.cost[j] = 0.0;
+    d.spos[j] = -1;
+    if (l > u) atomicOr(&d.ctl->infeasible_bounds, 1);
+    if (l == u) {
+        d.vstat[j] = VS_FIXED;
+        d.xval[j] = l;
+    } else if (l > -HUGE_VAL) {
+        d.vstat[j] = VS_LOWER;
+        d.xval[j] = l;
+    } else if (u < HUGE_VAL) {
+        d.vstat[j] = VS_UPPER;
+        d.xval[j] = u;
+    } else {
+        d.vstat[j] = VS_FREE;
+        d.xval[j] = 0.0;
+    }
+}
+
+// ordered compaction (single block): nzlist = { j < n : vstat != BASIC && xval != 0 }
+__global__ void __launch_bounds__(1024) k_nzlist(Dev d) {
+    __shared__ int wsum[16];
+    __shared__ int base;
+    if (threadIdx.x == 0) base = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int j0 = 0; j0 < d.n; j0 += 1024) {
+        const int j = j0 + threadIdx.x;
+        const bool f = j < d.n && d.vstat[j] != VS_BASIC && d.xval[j] != 0.0;
+        const unsigned long long bal = __ballot(f);
+        const int before = __popcll(bal & ((1ULL << lane) - 1ULL));
+        if (lane == 0) wsum[w] = __popcll(bal);
+        __syncthreads();
+        int off = base;
+        for (int i = 0; i < w; ++i) off += wsum[i];
+        if (f) d.nzlist[off + before] = j;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int t = 0;
+            for (int i = 0; i < 16; ++i) t += wsum[i];
+            base += t;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *d.nzcount = base;
+}
+
+// rhs_i = b_i - sum_{j in nzlist} a_ij x_j  (seq fma chain, ascending j)
+DEV double row_activity(const Dev& d, int i, int nz) {
+    double acc = 0.0;
+    for (int t = 0; t < nz; ++t) {
+        const int j = d.nzlist[t];
+        acc = fma(d.A[(size_t)j * (size_t)d.m + (size_t)i], d.xval[j], acc);
+    }
+    return acc;
+}
+
+__global__ void k_init_rows(Dev d, const double* __restrict__ rhs_in) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= d.m) return;
+    double bi = rhs_in[i];
+    if (bi <= -d.infinity) bi = -HUGE_VAL;
+    if (bi >= d.infinity) bi = HUGE_VAL;
+    d.b[i] = bi;
+    const int n = d.n, m = d.m, sv = n + i, av = n + m + i;
+    // d.lb/d.ub for slacks were written by the host (dir); artificials:
+    d.lb[av] = 0.0;
+    d.ub[av] = 0.0;
+    d.cost[sv] = 0.0;
+    d.cost[av] = 0.0;
+    d.vstat[av] = VS_FIXED;
+    d.xval[av] = 0.0;
+    d.rpos[i] = -1;
+    d.ypos[i] = -1;
+    d.asgn[i] = 1.0;
+    const double r = bi - row_activity(d, i, *d.nzcount);
+    const double sl = d.lb[sv], su = d.ub[sv];
+    if (r >= sl && r <= su) {
+        d.vstat[sv] = VS_BASIC;
+        d.cover[i] = sv;
+        d.xr[i] = r;
+        d.xval[sv] = 0.0;
+    } else {
+        const double s = r < sl ? sl : su;
+        d.vstat[sv] = (sl == su) ? VS_FIXED : (s == sl) ? VS_LOWER : VS_UPPER;
+        d.xval[sv] = s;
+        const double res = r - s;
+        d.asgn[i] = res > 0.0 ? 1.0 : -1.0;
+        d.ub[av] = HUGE_VAL;
+        d.cost[av] = 1.0;
+        d.vstat[av] = VS_BASIC;
+        d.cover[i] = av;
+        d.xr[i] = fabs(res);
+    }
+}
+
+// single block: Y = rows covered by an artificial, ascending; tol_inf from max|b|
+__global__ void __launch_bounds__(1024) k_init_Y(Dev d) {
+    __shared__ int wsum[16];
+    __shared__ int base;
+    __shared__ double red[16];
+    if (threadIdx.x == 0) base = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double bmax = 0.0;
+    for (int i0 = 0; i0 < d.m; i0 += 1024) {
+        const int i = i0 + threadIdx.x;
+        bool f = false;
+        if (i < d.m) {
+            f = d.cover[i] >= d.n + d.m;
+            const double bi = fabs(d.b[i]);
+            if (bi < HUGE_VAL && bi > bmax) bmax = bi;
+        }
+        const unsigned long long bal = __ballot(f);
+        const int before = __popcll(bal & ((1ULL << lane) - 1ULL));
+        if (lane == 0) wsum[w] = __popcll(bal);
+        __syncthreads();
+        int off = base;
+        for (int k = 0; k < w; ++k) off += wsum[k];
+        if (f) {
+            d.Yl[off + before] = i;
+            d.ypos[i] = off + before;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int t = 0;
+            for (int k = 0; k < 16; ++k) t += wsum[k];
+            base += t;
+        }
+        __syncthreads();
+    }
+    bmax = block_max<1024>(bmax, red);
+    if (threadIdx.x == 0) {
+        d.ctl->ny = base;
+        d.ctl->k = 0;
+        d.ctl->tol_inf = 1e-9 * (1.0 + bmax);
+    }
+}
+
+// AR[p][j] = A[Yl[p]][j] for p < ny (initial fill)
+__global__ void k_fill_AR(Dev d) {
+    const int ny = d.ctl->ny;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= d.n) return;
+    for (int p = blockIdx.y; p < ny; p += gridDim.y)
+        d.AR[(size_t)p * (size_t)d.ldr + j] = d.A[(size_t)j * (size_t)d.m + (size_t)d.Yl[p]];
+}
+
+// ============================================================== BTRAN
+// phase 1 only: t_q = c_{S_q} - sum_{covered i, y_i != 0} a_{i,S_q} y_i (ascending i)
+__global__ void k_btran_t(Dev d) {
+    if (d.ctl->status != ST_RUN) return;
+    const int k = d.ctl->k;
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= k) return;
+    double acc = 0.0;
+    const double* col = d.AS + (size_t)q * (size_t)d.m;
+    for (int i = 0; i < d.m; ++i) {
+        const int u = d.cover[i];
+        if (u < 0) continue;
+        const double yi = unit_sign(d, u, i) * d.cost[u];
+        if (yi != 0.0) acc = fma(col[i], yi, acc);
+    }
+    d.t[q] = d.cost[d.Sl[q]] - acc;
+}
+
+// loop-top checks (block 0) + y on covered rows + y_R = Minv^T t
+__global__ void __launch_bounds__(256) k_btran(Dev d, int phase) {
+    DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
+        // oracle run_phase loop top: phase-1 done, iteration cap, stop, refactor
+        double s = 0.0;
+        if (phase == 1) s = wave_art_sum(d);
+        if (threadIdx.x == 0) {
+            if (phase == 1) c->art_sum = s;
+            if (phase == 1 && s <= c->tol_inf) c->status = ST_P1DONE;
+            else if (c->iter >= c->iter_limit) c->status = ST_ITERCAP;
+            else if (c->iter >= c->iter_stop) c->status = ST_STOP;
+            else if (c->since_refactor >= c->refactor_period) c->status = ST_REFACTOR;
+        }
+    }
+    const int k = c->k;
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int gsz = gridDim.x * blockDim.x;
+    for (int i = gid; i < d.m; i += gsz) {
+        const int u = d.cover[i];
+        if (u >= 0) d.y[i] = unit_sign(d, u, i) * d.cost[u];
+    }
+    for (int p = gid; p < k; p += gsz) {
+        double acc = 0.0;
+        if (phase == 1) {
+            for (int q = 0; q < k; ++q) acc = fma(d.Minv[(size_t)q * d.ldm + p], d.t[q], acc);
+        } else {
+            for (int q = 0; q < k; ++q)
+                acc = fma(d.Minv[(size_t)q * d.ldm + p], d.cost[d.Sl[q]], acc);
+        }
+        d.y[d.Rl[p]] = acc;
+    }
+}
+
+// ============================================================== pricing
+// One workgroup = 4 waves = 128 columns x all Y slots.  Wave w sweeps slot
+// chunk w (PRICE_SPLIT contiguous chunks), lane l owns columns 2l, 2l+1 of the
+// tile (16-byte loads, 1 KiB per wave instruction, row-major AR so every load
+// is fully coalesced).  y_Y is staged in LDS.  The four chunk partials are
+// combined in LDS in chunk order, then the tile's Dantzig argmax is written.
+template <bool LDS_Y>
+__global__ void __launch_bounds__(256) k_price(Dev d) {
+    extern __shared__ __attribute__((aligned(16))) double yy[];
+    __shared__ double part[PRICE_SPLIT][TILE_COLS];
+    __shared__ Cand red[4];
+    const DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    const int ny = c->ny, bland = c->bland;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (LDS_Y) {
+        for (int p = threadIdx.x; p < ny; p += 256) yy[p] = d.y[d.Yl[p]];
+        __syncthreads();
+    }
+    const int L = (ny + PRICE_SPLIT - 1) / PRICE_SPLIT;
+    const int p0 = w * L;
+    const int p1 = min(ny, p0 + L);
+    const int64_t j0 = (int64_t)blockIdx.x * TILE_COLS + 2 * lane;
+    const double* col = d.AR + j0;
+    double acc0 = 0.0, acc1 = 0.0;
+    int p = p0;
+    for (; p + 8 <= p1; p += 8) {
+        double2 v[8];
+        double yv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            v[u] = *reinterpret_cast<const double2*>(col + (size_t)(p + u) * (size_t)d.ldr);
+            yv[u] = LDS_Y ? yy[p + u] : d.y[d.Yl[p + u]];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            acc0 = fma(v[u].x, yv[u], acc0);
+            acc1 = fma(v[u].y, yv[u], acc1);
+        }
+    }
+    for (; p < p1; ++p) {
+        const double2 v = *reinterpret_cast<const double2*>(col + (size_t)p * (size_t)d.ldr);
+        const double yv = LDS_Y ? yy[p] : d.y[d.Yl[p]];
+        acc0 = fma(v.x, yv, acc0);
+        acc1 = fma(v.y, yv, acc1);
+    }
+    part[w][2 * lane] = acc0;
+    part[w][2 * lane + 1] = acc1;
+    __syncthreads();
+    Cand best;
+    best.j = -1;
+    best.score = 0.0;
+    best.d = 0.0;
+    if (threadIdx.x < TILE_COLS) {
+        const int64_t j = (int64_t)blockIdx.x * TILE_COLS + threadIdx.x;
+        if (j < d.n) {
+            const int8_t vs = d.vstat[j];
+            if (vs != VS_BASIC && vs != VS_FIXED) {
+                double tot = 0.0;
+#pragma unroll
+                for (int ww = 0; ww < PRICE_SPLIT; ++ww) tot = tot + part[ww][threadIdx.x];
+                const double dj = d.cost[j] - tot;
+                const double dtol = c->tol_dual;
+                if ((vs == VS_LOWER || vs == VS_FREE) && dj < -dtol) {
+                    best.j = j;
+                    best.score = -dj;
+                    best.d = dj;
+                } else if ((vs == VS_UPPER || vs == VS_FREE) && dj > dtol) {
+                    best.j = j;
+                    best.score = dj;
+                    best.d = dj;
+                }
+            }
+        }
+    }
+    best = block_best<256>(best, bland, red);
+    if (threadIdx.x == 0) d.cand[blockIdx.x] = best;
+}
+
+// ============================================================== select
+// Min-loc over tile candidates and the slack candidates; entering column to
+// acol (dense m-vector) and a_R = acol[R].
+__global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles) {
+    __shared__ Cand red[16];
+    DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    const int bland = c->bland, ny = c->ny, k = c->k;
+    Cand best;
+    best.j = -1;
+    best.score = 0.0;
+    best.d = 0.0;
+    for (int t = threadIdx.x; t < ntiles; t += 1024) {
+        const Cand o = d.cand[t];
+        if (cand_better(o, best, bland)) best = o;
+    }
+    const double dtol = c->tol_dual;
+    for (int p = threadIdx.x; p < ny; p += 1024) {
+        const int i = d.Yl[p];
+        const int j = d.n + i;
+        const int8_t vs = d.vstat[j];
+        if (vs == VS_FIXED) continue;
+        const double dj = d.cost[j] - d.y[i];
+        Cand o;
+        o.j = -1;
+        if ((vs == VS_LOWER || vs == VS_FREE) && dj < -dtol) {
+            o.j = j;
+            o.score = -dj;
+            o.d = dj;
+        } else if ((vs == VS_UPPER || vs == VS_FREE) && dj > dtol) {
+            o.j = j;
+            o.score = dj;
+            o.d = dj;
+        }
+        if (cand_better(o, best, bland)) best = o;
+    }
+    best = block_best<1024>(best, bland, red);
+    if (best.j < 0) {
+        if (threadIdx.x == 0) c->status = ST_PHASE_OPT;
+        return;
+    }
+    const int q = (int)best.j;
+    if (threadIdx.x == 0) {
+        // algorithmic bytes of this pricing pass: AR sweep + c + status + y_Y + Yl
+        c->price_bytes += 8.0 * (double)ny * (double)d.n + 9.0 * (double)d.n + 12.0 * (double)ny;
+        c->price_passes++;
+        c->q = q;
+        c->dq = best.d;
+        c->sig = best.d < 0.0 ? 1.0 : -1.0;
+    }
+    if (q < d.n) {
+        const double* col = d.A + (size_t)q * (size_t)d.m;
+        for (int i = threadIdx.x; i < d.m; i += 1024) d.acol[i] = col[i];
+    } else {
+        for (int i = threadIdx.x; i < d.m; i += 1024) d.acol[i] = (i == q - d.n) ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < k; p += 1024) d.aR[p] = d.acol[d.Rl[p]];
+}
+
+// ============================================================== FTRAN
+// out[p] = wave_dot(Minv[p, 0:k], vin[0:k]) -- one wave per bump row
+__global__ void __launch_bounds__(256) k_ftran_bump(Dev d, const double* __restrict__ vin,
+                                                    double* __restrict__ out, int check_run) {
+    if (check_run && d.ctl->status != ST_RUN) return;
+    const int k = d.ctl->k;
+    const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (p >= k) return;
+    const double* row = d.Minv + (size_t)p * d.ldm;
+    double acc = 0.0;
+    for (int i = lane; i < k; i += 64) acc = fma(row[i], vin[i], acc);
+    acc = wave_tree(acc);
+    if (lane == 0) out[p] = acc;
+}
+
+// zpart[c][i] = sum_{p in chunk c} AS[i][p] * w[p]  (ZCHUNK positions per chunk)
+__global__ void __launch_bounds__(256) k_ftran_z(Dev d, const double* __restrict__ wv, int check_run) {
+    if (check_run && d.ctl->status != ST_RUN) return;
+    const int k = d.ctl->k;
+    const int ch = blockIdx.y;
+    const int c0 = ch * ZCHUNK;
+    if (c0 >= k) return;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= d.m) return;
+    const int c1 = min(k, c0 + ZCHUNK);
+    double acc = 0.0;
+    for (int p = c0; p < c1; ++p) acc = fma(d.AS[(size_t)p * (size_t)d.m + i], wv[p], acc);
+    d.zpart[(size_t)ch * (size_t)d.m + i] = acc;
+}
+
+// x_u = sign * (v_i - z_i) on covered rows after a refactor (z from k_ftran_z)
+__global__ void k_xr_from_z(Dev d) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= d.m) return;
+    const int u = d.cover[i];
+    if (u < 0) return;
+    const int k = d.ctl->k;
+    const int nch = (k + ZCHUNK - 1) / ZCHUNK;
+    double z = 0.0;
+    for (int ch = 0; ch < nch; ++ch) z = z + d.zpart[(size_t)ch * d.m + i];
+    d.xr[i] = unit_sign(d, u, i) * (d.rhs[i] - z);
+}
+
+// ============================================================== ratio test
+struct Leave {
+    double ag, r, g;
+    int var, e;
+};
+DEV bool leave_better(const Leave& a, const Leave& b, int bland) {
+    if (a.var < 0) return false;
+    if (b.var < 0) return true;
+    if (bland) return a.r < b.r || (a.r == b.r && a.var < b.var);
+    return a.ag > b.ag || (a.ag == b.ag && a.var < b.var);
+}
+DEV Leave shfl_leave(const Leave& x, int off) {
+    Leave o;
+    o.ag = __shfl_xor(x.ag, off);
+    o.r = __shfl_xor(x.r, off);
+    o.g = __shfl_xor(x.g, off);
+    o.var = __shfl_xor(x.var, off);
+    o.e = __shfl_xor(x.e, off);
+    return o;
+}
+
+DEV bool basic_entry(const Dev& d, int e, int m, double sig, int& var, double& g, double& x) {
+    if (e < m) {
+        const int u = d.cover[e];
+        if (u < 0) return false;
+        var = u;
+        g = sig * d.alU[e];
+        x = d.xr[e];
+    } else {
+        const int p = e - m;
+        var = d.Sl[p];
+        g = sig * d.alS[p];
+        x = d.xs[p];
+    }
+    return true;
+}
+
+__global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
+    __shared__ double dred[16];
+    __shared__ Leave lred[16];
+    __shared__ int s_action;
+    __shared__ Plan s_plan;
+    DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    const int m = d.m, n = d.n, k = c->k, q = c->q;
+    const double sig = c->sig;
+    const int bland = c->bland;
+    const int tid = threadIdx.x;
+    // ---- alpha on covered rows: combine the z chunks in order
+    const int nch = (k + ZCHUNK - 1) / ZCHUNK;
+    for (int i = tid; i < m; i += 1024) {
+        const int u = d.cover[i];
+        if (u < 0) continue;
+        double z = 0.0;
+        for (int ch = 0; ch < nch; ++ch) z = z + d.zpart[(size_t)ch * m + i];
+        d.zz[i] = z;
+        d.alU[i] = unit_sign(d, u, i) * (d.acol[i] - z);
+    }
+    __syncthreads();
+    // ---- Harris pass 1
+    const double ptol = c->tol_primal, pivtol = c->tol_pivot, INF = HUGE_VAL;
+    double tmax = INF;
+    for (int e = tid; e < m + k; e += 1024) {
+        int var;
+        double g, x;
+        if (!basic_entry(d, e, m, sig, var, g, x)) continue;
+        const double l = d.lb[var], u = d.ub[var];
+        double r;
+        if (g > pivtol && l > -INF) r = bland ? (x - l) / g : (x - l + ptol) / g;
+        else if (g < -pivtol && u < INF) r = bland ? (u - x) / (-g) : (u - x + ptol) / (-g);
+        else continue;
+        if (r < tmax) tmax = r;
+    }
+    const double theta_max = block_min<1024>(tmax, dred);
+    // ---- pass 2
+    Leave best;
+    best.var = -1;
+    best.ag = 0.0;
+    best.r = 0.0;
+    best.g = 0.0;
+    best.e = -1;
+    for (int e = tid; e < m + k; e += 1024) {
+        int var;
+        double g, x;
+        if (!basic_entry(d, e, m, sig, var, g, x)) continue;
+        const double l = d.lb[var], u = d.ub[var];
+        double r;
+        if (g > pivtol && l > -INF) r = (x - l) / g;
+        else if (g < -pivtol && u < INF) r = (u - x) / (-g);
+        else continue;
+        if (!(r <= theta_max)) continue;
+        Leave o;
+        o.var = var;
+        o.ag = fabs(g);
+        o.r = r;
+        o.g = g;
+        o.e = e;
+        if (leave_better(o, best, bland)) best = o;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        Leave o = shfl_leave(best, off);
+        if (leave_better(o, best, bland)) best = o;
+    }
+    if ((tid & 63) == 0) lred[tid >> 6] = best;
+    __syncthreads();
+    best = lred[0];
+    for (int i = 1; i < 16; ++i)
+        if (leave_better(lred[i], best, bland)) best = lred[i];
+    // ---- decision (uniform across the block)
+    const double theta = best.var >= 0 ? (best.r > 0.0 ? best.r : 0.0) : INF;
+    const double flip = (d.lb[q] > -INF && d.ub[q] < INF) ? d.ub[q] - d.lb[q] : INF;
+    int action;
+    double step;
+    if (flip < INF && flip <= theta) {
+        action = ACT_FLIP;
+        step = flip;
+    } else if (theta == INF) {
+        action = ACT_NONE;  // unbounded
+        step = 0.0;
+    } else {
+        action = ACT_PIVOT;
+        step = theta;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const int64_t it = c->iter;
+        c->iter = it + 1;
+        if (phase == 1) c->phase1_iters++;
+        if (action == ACT_NONE) {
+            c->status = ST_UNBOUNDED;
+            c->unb_var = q;
+            c->unb_sig = sig;
+        } else if (it < c->trace_cap) {
+            d.trace[2 * it] = q;
+            d.trace[2 * it + 1] = action == ACT_FLIP ? -1 : best.var;
+        }
+    }
+    if (action == ACT_NONE) {
+        if (tid == 0) c->plan.action = ACT_NONE;
+        return;
+    }
+    // ---- primal update x_B -= step * g
+    for (int i = tid; i < m; i += 1024)
+        if (d.cover[i] >= 0) d.xr[i] = fma(-step, sig * d.alU[i], d.xr[i]);
+    for (int p = tid; p < k; p += 1024) d.xs[p] = fma(-step, sig * d.alS[p], d.xs[p]);
+    __syncthreads();
+    if (action == ACT_FLIP) {
+        if (tid == 0) {
+            if (d.vstat[q] == VS_LOWER) {
+                d.vstat[q] = VS_UPPER;
+                d.xval[q] = d.ub[q];
+            } else {
+                d.vstat[q] = VS_LOWER;
+                d.xval[q] = d.lb[q];
+            }
+            c->flips++;
+            c->ndegen = 0;
+            c->bland = 0;
+            c->plan.action = ACT_FLIP;
+        }
+        return;
+    }
+    // ---- pivot: bookkeeping by thread 0, staging by all
+    if (tid == 0) {
+        if (theta == 0.0) {
+            c->degenerate++;
+            if (++c->ndegen >= c->degen_switch) c->bland = 1;
+        } else {
+            c->ndegen = 0;
+            c->bland = 0;
+        }
+        const int lv = best.var;
+        const int lrow = best.e < m ? best.e : -1;
+        const int lpos = best.e < m ? -1 : best.e - m;
+        const double xq = d.xval[q] + sig * theta;
+        const bool at_lower = best.g > 0.0;
+        const bool leave_art = lv >= n + m;
+        if (leave_art) {
+            d.lb[lv] = 0.0;
+            d.ub[lv] = 0.0;
+            d.vstat[lv] = VS_FIXED;
+            d.xval[lv] = 0.0;
+        } else {
+            const double lbv = d.lb[lv], ubv = d.ub[lv];
+            d.vstat[lv] = lbv == ubv ? VS_FIXED : at_lower ? VS_LOWER : VS_UPPER;
+            d.xval[lv] = at_lower ? lbv : ubv;
+        }
+        d.vstat[q] = VS_BASIC;
+        Plan P;
+        P.action = ACT_PIVOT;
+        P.k_old = k;
+        P.q = q;
+        P.xq = xq;
+        P.p = P.a = P.b = P.last = P.row = -1;
+        P.y_rm_slot = P.y_rm_last = P.y_ap_slot = P.y_ap_row = -1;
+        P.piv = 0.0;
+        int ny = c->ny;
+        int newk = k;
+        if (q < n) {
+            if (lpos >= 0) {  // case A
+                P.pcase = PC_A;
+                P.p = lpos;
+                P.piv = d.alS[lpos];
+                d.spos[lv] = -1;
+                d.Sl[lpos] = q;
+                d.spos[q] = lpos;
+                d.xs[lpos] = xq;
+            } else {  // case B
+                const int i = lrow;
+                P.pcase = PC_B;
+                P.row = i;
+                P.p = k;
+                P.piv = d.acol[i] - d.zz[i];
+                d.Rl[k] = i;
+                d.rpos[i] = k;
+                d.Sl[k] = q;
+                d.spos[q] = k;
+                d.xs[k] = xq;
+                d.cover[i] = -1;
+                newk = k + 1;
+                if (!leave_art) {
+                    P.y_ap_slot = ny;
+                    P.y_ap_row = i;
+                    d.Yl[ny] = i;
+                    d.ypos[i] = ny;
+                    ny++;
+                }
+            }
+        } else {
+            const int i0 = q - n;
+            const int a = d.rpos[i0];
+            if (a < 0) {  // case E
+                P.pcase = PC_E;
+                if (lrow != i0) c->status = ST_NUMFAIL;
+                d.cover[i0] = q;
+                d.xr[i0] = xq;
+            } else if (lpos >= 0) {  // case C
+                const int b = lpos, last = k - 1;
+                P.pcase = PC_C;
+                P.a = a;
+                P.b = b;
+                P.last = last;
+                P.piv = d.Minv[(size_t)b * d.ldm + a];
+                if (b != last) {
+                    d.Sl[b] = d.Sl[last];
+                    d.spos[d.Sl[b]] = b;
+                    d.xs[b] = d.xs[last];
+                }
+                if (a != last) {
+                    d.Rl[a] = d.Rl[last];
+                    d.rpos[d.Rl[a]] = a;
+                }
+                d.spos[lv] = -1;
+                d.rpos[i0] = -1;
+                d.cover[i0] = q;
+                d.xr[i0] = xq;
+                newk = k - 1;
+            } else {  // case D
+                const int i1 = lrow;
+                P.pcase = PC_D;
+                P.a = a;
+                P.row = i1;
+                d.Rl[a] = i1;
+                d.rpos[i1] = a;
+                d.rpos[i0] = -1;
+                d.cover[i1] = -1;
+                d.cover[i0] = q;
+                d.xr[i0] = xq;
+            }
+            // row i0 leaves Y (its slack is basic now) ...
+            const int s = d.ypos[i0], last = ny - 1;
+            P.y_rm_slot = s;
+            P.y_rm_last = last;
+            if (s != last) {
+                d.Yl[s] = d.Yl[last];
+                d.ypos[d.Yl[s]] = s;
+            }
+            d.ypos[i0] = -1;
+            ny--;
+            // ... and in case D the leaving slack's row joins it
+            if (P.pcase == PC_D && !leave_art) {
+                P.y_ap_slot = ny;
+                P.y_ap_row = lrow;
+                d.Yl[ny] = lrow;
+                d.ypos[lrow] = ny;
+                ny++;
+            }
+        }
+        c->k = newk;
+        c->ny = ny;
+        c->since_refactor++;
+        c->plan = P;
+        s_plan = P;
+        s_action = P.pcase;
+    }
+    __syncthreads();
+    const Plan P = s_plan;
+    const int pc = s_action;
+    if (pc == PC_A) {
+        for (int j = tid; j < k; j += 1024) d.vrow[j] = d.Minv[(size_t)P.p * d.ldm + j] / P.piv;
+    } else if (pc == PC_C) {
+        for (int j = tid; j < k; j += 1024) {
+            d.vrow[j] = d.Minv[(size_t)P.b * d.ldm + j] / P.piv;
+            d.colA[j] = d.Minv[(size_t)j * d.ldm + P.a];
+        }
+    } else if (pc == PC_D) {
+        for (int j = tid; j < k; j += 1024) d.colA[j] = d.Minv[(size_t)j * d.ldm + P.a];
+    }
+}
+
+// cases B / D: vvec[c] = sum_q AS[row][q] * Minv[q][c]  (seq), B: / delta
+__global__ void __launch_bounds__(256) k_rowminv(Dev d) {
+    const DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    const Plan P = c->plan;
+    if (P.action != ACT_PIVOT || (P.pcase != PC_B && P.pcase != PC_D)) return;
+    const int k = P.k_old;
+    const int col = blockIdx.x * blockDim.x + threadIdx.x;
+    if (col >= k) return;
+    double acc = 0.0;
+    for (int q = 0; q < k; ++q)
+        acc = fma(d.AS[(size_t)q * (size_t)d.m + P.row], d.Minv[(size_t)q * d.ldm + col], acc);
+    d.vvec[col] = P.pcase == PC_B ? acc / P.piv : acc;
+}
+
+// Minv update (blocks [0, nb_minv)) + AS / AR copies (the rest)
+__global__ void __launch_bounds__(256) k_update(Dev d, int nb_minv) {
+    const DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    const Plan P = c->plan;
+    if (P.action != ACT_PIVOT) return;
+    const int k = P.k_old;
+    const size_t ldm = (size_t)d.ldm;
+    if ((int)blockIdx.x < nb_minv) {
+        const int64_t e0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        const int64_t estride = (int64_t)nb_minv * blockDim.x;
+        if (P.pcase == PC_A) {
+            for (int64_t e = e0; e < (int64_t)k * k; e += estride) {
+                const int i = (int)(e / k), j = (int)(e % k);
+                double* M = d.Minv + (size_t)i * ldm + j;
+                *M = (i == P.p) ? d.vrow[j] : fma(-d.alS[i], d.vrow[j], *M);
+            }
+        } else if (P.pcase == PC_B) {
+            const int kk = k + 1;
+            const double delta = P.piv;
+            for (int64_t e = e0; e < (int64_t)kk * kk; e += estride) {
+                const int a = (int)(e / kk), cc = (int)(e % kk);
+                double* M = d.Minv + (size_t)a * ldm + cc;
+                if (a < k && cc < k) *M = fma(d.alS[a], d.vvec[cc], *M);
+                else if (a < k) *M = -(d.alS[a] / delta);
+                else if (cc < k) *M = -d.vvec[cc];
+                else *M = 1.0 / delta;
+            }
+        } else if (P.pcase == PC_C) {
+            const int kk = k - 1, last = P.last;
+            for (int64_t e = e0; e < (int64_t)kk * kk; e += estride) {
+                const int r = (int)(e / kk), cc = (int)(e % kk);
+                const int sr = (r == P.b) ? last : r;
+                const int sc = (cc == P.a) ? last : cc;
+                d.Minv[(size_t)r * ldm + cc] =
+                    fma(-d.colA[sr], d.vrow[sc], d.Minv[(size_t)sr * ldm + sc]);
+            }
+        } else if (P.pcase == PC_D) {
+            const double piv = d.vvec[P.a];
+            for (int64_t e = e0; e < (int64_t)k * k; e += estride) {
+                const int r = (int)(e / k), cc = (int)(e % k);
+                const double ca = d.colA[r] / piv;
+                double* M = d.Minv + (size_t)r * ldm + cc;
+                *M = (cc == P.a) ? ca : fma(-ca, d.vvec[cc], *M);
+            }
+        }
+        return;
+    }
+    // ---- copies: thread t covers row t of AS and column t of AR
+    const int64_t t0 = (int64_t)(blockIdx.x - nb_minv) * blockDim.x + threadIdx.x;
+    const int64_t tstride = (int64_t)(gridDim.x - nb_minv) * blockDim.x;
+    const size_t m = (size_t)d.m;
+    for (int64_t t = t0; t < d.m; t += tstride) {
+        if (P.pcase == PC_A || P.pcase == PC_B) {
+            const int pos = P.pcase == PC_A ? P.p : k;
+            d.AS[(size_t)pos * m + t] = d.A[(size_t)P.q * m + t];
+        } else if (P.pcase == PC_C && P.b != P.last) {
+            d.AS[(size_t)P.b * m + t] = d.AS[(size_t)P.last * m + t];
+        }
+    }
+    if (P.y_rm_slot >= 0 || P.y_ap_slot >= 0) {
+        for (int64_t j = t0; j < d.n; j += tstride) {
+            if (P.y_rm_slot >= 0 && P.y_rm_slot != P.y_rm_last)
+                d.AR[(size_t)P.y_rm_slot * d.ldr + j] = d.AR[(size_t)P.y_rm_last * d.ldr + j];
+            if (P.y_ap_slot >= 0)
+                d.AR[(size_t)P.y_ap_slot * d.ldr + j] = d.A[(size_t)j * m + P.y_ap_row];
+        }
+    }
+}
+
+// ============================================================== refactor
+__global__ void k_gj_init(Dev d, int k) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < (int64_t)k * k) {
+        const int a = (int)(e / k), cc = (int)(e % k);
+        d.W0[e] = d.AS[(size_t)cc * (size_t)d.m + d.Rl[a]];
+    }
+    if (e < k) d.pivstep[e] = 0x7fffffff;
+}
+
+// one Gauss-Jordan column step: every block finds the pivot redundantly
+__global__ void __launch_bounds__(256) k_gj_step(Dev d, int k, int col, const double* __restrict__ W,
+                                                double* __restrict__ W2) {
+    __shared__ double sv[4];
+    __shared__ int sr[4];
+    __shared__ int s_p;
+    __shared__ double s_piv;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    double bv = -1.0;
+    int br = 0x7fffffff;
+    for (int r = tid; r < k; r += 256) {
+        if (d.pivstep[r] < col) continue;  // used in an earlier step
+        const double v = fabs(W[(size_t)r * k + col]);
+        if (v > bv || (v == bv && r < br)) {
+            bv = v;
+            br = r;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const double ov = __shfl_xor(bv, off);
+        const int orr = __shfl_xor(br, off);
+        if (ov > bv || (ov == bv && orr < br)) {
+            bv = ov;
+            br = orr;
+        }
+    }
+    if (lane == 0) {
+        sv[w] = bv;
+        sr[w] = br;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double v = sv[0];
+        int r = sr[0];
+        for (int i = 1; i < 4; ++i)
+            if (sv[i] > v || (sv[i] == v && sr[i] < r)) {
+                v = sv[i];
+                r = sr[i];
+            }
+        s_p = r;
+        s_piv = W[(size_t)r * k + col];
+        if (blockIdx.x == 0) {
+            d.perm[col] = r;
+            d.pivstep[r] = col;
+            if (!(fabs(s_piv) > 1e-13)) d.ctl->status = ST_NUMFAIL;
+        }
+    }
+    __syncthreads();
+    const int p = s_p;
+    const double piv = s_piv;
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + tid;
+    if (e >= (int64_t)k * k) return;
+    const int r = (int)(e / k), j = (int)(e % k);
+    double v;
+    if (r == p) {
+        v = (j == col) ? 1.0 / piv : W[(size_t)p * k + j] / piv;
+    } else {
+        const double f = W[(size_t)r * k + col];
+        v = (j == col) ? -(f / piv) : fma(-f, W[(size_t)p * k + j] / piv, W[(size_t)r * k + j]);
+    }
+    W2[e] = v;
+}
+
+__global__ void k_gj_final(Dev d, int k, const double* __restrict__ W) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)k * k) return;
+    const int a = (int)(e / k), cc = (int)(e % k);
+    d.Minv[(size_t)a * d.ldm + d.perm[cc]] = W[(size_t)d.perm[a] * k + cc];
+}
+
+// rhs_i = (b_i - sum_{nz} a_ij x_j) - s_i  and a_R for the bump solve
+__global__ void k_refactor_rhs(Dev d) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= d.m) return;
+    double r = d.b[i] - row_activity(d, i, *d.nzcount);
+    if (d.vstat[d.n + i] != VS_BASIC) r = r - d.xval[d.n + i];
+    d.rhs[i] = r;
+    const int p = d.rpos[i];
+    if (p >= 0) d.aR[p] = r;
+}
+
+// ============================================================== phase 2 / extract
+__global__ void k_phase2(Dev d) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < d.m) {
+        const int av = d.n + d.m + t;
+        d.cost[av] = 0.0;
+        d.lb[av] = 0.0;
+        d.ub[av] = 0.0;
+    }
+    if (t < d.n) d.cost[t] = d.maximize ? -d.obj[t] : d.obj[t];
+}
+
+__global__ void k_extract(Dev d, double* __restrict__ xout) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= d.n) return;
+    xout[j] = d.vstat[j] == VS_BASIC ? d.xs[d.spos[j]] : d.xval[j];
+}
+
+// ============================================================== launchers
+static inline unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
+
+hipError_t launch_generate(const Dev& d, uint64_t seed, int64_t col0, int64_t n_global, double* A,
+                           double* b, double* c, hipStream_t st) {
+    const int m = d.m;
+    const int64_t ncols = d.n;
+    if (m > 0 && A) {
+        dim3 g(cdiv(m, 256), (unsigned)(ncols < 65535 ? ncols : 65535));
+        k_gen_A<<<g, 256, 0, st>>>(seed, m, ncols, col0, A);
+    }
+    const int64_t mx = m > ncols ? m : ncols;
+    k_gen_bc<<<cdiv(mx, 256), 256, 0, st>>>(seed, m, ncols, col0, n_global, b, c);
+    return hipGetLastError();
+}
+
+hipError_t launch_init(const Dev& d, const double* lo, const double* up, const double* rhs,
+                       hipStream_t st) {
+    k_init_cols<<<cdiv(d.n, 256), 256, 0, st>>>(d, lo, up);
+    k_nzlist<<<1, 1024, 0, st>>>(d);
+    if (d.m > 0) {
+        k_init_rows<<<cdiv(d.m, 256), 256, 0, st>>>(d, rhs);
+        k_init_Y<<<1, 1024, 0, st>>>(d);
+        dim3 g(cdiv(d.n, 256), (unsigned)(d.m < 4096 ? d.m : 4096));
+        k_fill_AR<<<g, 256, 0, st>>>(d);
+    } else {
+        k_init_Y<<<1, 1024, 0, st>>>(d);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStream_t st,
+                            hipEvent_t ev0, hipEvent_t ev1) {
+    const int m = d.m;
+    if (phase == 1 && k_ub > 0) k_btran_t<<<cdiv(k_ub, 256), 256, 0, st>>>(d);
+    {
+        const int64_t work = m > k_ub ? m : k_ub;
+        unsigned g = cdiv(work > 0 ? work : 1, 256);
+        if (g > 1024) g = 1024;
+        k_btran<<<g, 256, 0, st>>>(d, phase);
+    }
+    const unsigned ntiles = cdiv(d.n, TILE_COLS);
+    const size_t ylds = (size_t)ny_ub * sizeof(double);
+    if (ev0) (void)hipEventRecord(ev0, st);
+    if (ylds <= 48 * 1024) k_price<true><<<ntiles, 256, ylds, st>>>(d);
+    else k_price<false><<<ntiles, 256, 0, st>>>(d);
+    if (ev1) (void)hipEventRecord(ev1, st);
+    k_select<<<1, 1024, 0, st>>>(d, (int)ntiles);
+    if (k_ub > 0) {
+        k_ftran_bump<<<cdiv(k_ub, 4), 256, 0, st>>>(d, d.aR, d.alS, 1);
+        if (m > 0) {
+            dim3 g(cdiv(m, 256), cdiv(k_ub, ZCHUNK));
+            k_ftran_z<<<g, 256, 0, st>>>(d, d.alS, 1);
+        }
+    }
+    k_ratio<<<1, 1024, 0, st>>>(d, phase);
+    if (k_ub > 0) k_rowminv<<<cdiv(k_ub, 256), 256, 0, st>>>(d);
+    {
+        const int64_t kk = (int64_t)(k_ub + 1) * (k_ub + 1);
+        unsigned nb_minv = cdiv(kk, 256);
+        if (nb_minv > 2048) nb_minv = 2048;
+        const int64_t cw = m > d.n ? m : d.n;
+        unsigned nb_copy = cdiv(cw, 256);
+        if (nb_copy > 1024) nb_copy = 1024;
+        k_update<<<nb_minv + nb_copy, 256, 0, st>>>(d, (int)nb_minv);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_refactor(const Dev& d, int k, hipStream_t st) {
+    if (k > 0) {
+        const int64_t kk = (int64_t)k * k;
+        k_gj_init<<<cdiv(kk > k ? kk : k, 256), 256, 0, st>>>(d, k);
+        double *W = d.W0, *W2 = d.W1;
+        for (int c = 0; c < k; ++c) {
+            k_gj_step<<<cdiv(kk, 256), 256, 0, st>>>(d, k, c, W, W2);
+            double* s = W;
+            W = W2;
+            W2 = s;
+        }
+        k_gj_final<<<cdiv(kk, 256), 256, 0, st>>>(d, k, W);
+    }
+    k_nzlist<<<1, 1024, 0, st>>>(d);
+    if (d.m > 0) {
+        k_refactor_rhs<<<cdiv(d.m, 256), 256, 0, st>>>(d);
+        if (k > 0) {
+            k_ftran_bump<<<cdiv(k, 4), 256, 0, st>>>(d, d.aR, d.xs, 0);
+            dim3 g(cdiv(d.m, 256), cdiv(k, ZCHUNK));
+            k_ftran_z<<<g, 256, 0, st>>>(d, d.xs, 0);
+        }
+        k_xr_from_z<<<cdiv(d.m, 256), 256, 0, st>>>(d);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_phase2(const Dev& d, hipStream_t st) {
+    const int64_t mx = d.m > d.n ? d.m : d.n;
+    k_phase2<<<cdiv(mx, 256), 256, 0, st>>>(d);
+    return hipGetLastError();
+}
+
+hipError_t launch_extract(const Dev& d, double* xout, hipStream_t st) {
+    k_extract<<<cdiv(d.n, 256), 256, 0, st>>>(d, xout);
+    return hipGetLastError();
+}
+
+}  // namespace elp

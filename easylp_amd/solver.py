@@ -1,0 +1,182 @@
+"""Host-side mirror of EasyLP's solver hand-off, over the HIP C ABI.
+
+`solve_dense()` takes exactly the arrays easylp$solve() hands to lp_solve at
+/root/reference/R/class.R:260-274 (constraint$mat column-major, dir, rhs,
+objective_fun, per-column bounds, sense) and returns what R reads back at
+:276-298 (status code and string, objective, variables with 1e30 -> Inf).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import ElpStats, check, default_control, load
+
+# R/class.R:279-295
+STATUS_TEXT = {
+    0: "optimal",
+    1: "sub-optimal",
+    2: "unfeasible",
+    3: "unbounded",
+    4: "degenerate model",
+    5: "numerical failure encountered",
+    6: "process aborted",
+    7: "timeout",
+    9: "the model was solved by presolve",
+    10: "the branch and bound routine failed",
+    11: "the branch and bound was stopped because of a break-at-first or break-at-value",
+    12: "a feasible branch and bound solution was found",
+    13: "no feasible branch and bound solution was found",
+}
+
+DIR_CODES = {"<=": 1, "<": 1, ">=": 2, ">": 2, "==": 3, "=": 3}
+
+
+def status_text(code: int) -> str:
+    return STATUS_TEXT.get(int(code), "undocumented status")
+
+
+def large_to_infinity(x, threshold: float = 1e30):
+    """R/utils.R:172-176."""
+    x = np.array(x, dtype=np.float64, copy=True)
+    x[x >= threshold] = np.inf
+    x[x <= -threshold] = -np.inf
+    return x
+
+
+def dir_codes(dirs) -> np.ndarray:
+    if len(dirs) and isinstance(dirs[0], str):
+        bad = [d for d in dirs if d not in DIR_CODES]
+        if bad:
+            raise ValueError(f"unknown constraint direction {bad[0]!r}")
+        return np.array([DIR_CODES[d] for d in dirs], dtype=np.int32)
+    return np.ascontiguousarray(dirs, dtype=np.int32)
+
+
+@dataclass
+class Solution:
+    status: int
+    objval: float                 # raw objective (get.objective)
+    x: np.ndarray                 # get.variables
+    y: np.ndarray                 # duals, user sense
+    basis: np.ndarray             # sorted basic variable ids
+    stats: dict = field(default_factory=dict)
+    trace: np.ndarray | None = None
+
+    @property
+    def status_text(self) -> str:
+        return status_text(self.status)
+
+
+class Problem:
+    """One LP on the GPU (the object R keeps in self$pointer, R/class.R:300)."""
+
+    def __init__(self, m: int, n: int, **control):
+        self._lib = load()
+        self.m, self.n = int(m), int(n)
+        self._ctl = default_control(**control)
+        h = ctypes.c_void_p()
+        check(self._lib.elp_create(ctypes.byref(h), self.m, self.n, ctypes.byref(self._ctl)),
+              "elp_create")
+        self._h = h
+        self._trace_cap = 0
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.elp_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_trace(self, capacity: int) -> None:
+        check(self._lib.elp_set_trace(self._h, int(capacity)), "elp_set_trace")
+        self._trace_cap = int(capacity)
+
+    def comm_init(self, unique_id: bytes, world_size: int, rank: int) -> None:
+        buf = ctypes.create_string_buffer(bytes(unique_id), 128)
+        check(self._lib.elp_comm_init(self._h, buf, int(world_size), int(rank)), "elp_comm_init")
+
+    def load_dense(self, A, dirs, rhs, obj, lo=None, up=None, maximize=False) -> None:
+        m, n = self.m, self.n
+        A = np.asfortranarray(np.asarray(A, dtype=np.float64).reshape(m, n))
+        d = dir_codes(dirs)
+        rhs = np.ascontiguousarray(rhs, dtype=np.float64).reshape(m)
+        obj = np.ascontiguousarray(obj, dtype=np.float64).reshape(n)
+        lo = np.zeros(n) if lo is None else np.ascontiguousarray(lo, dtype=np.float64)
+        up = np.full(n, np.inf) if up is None else np.ascontiguousarray(up, dtype=np.float64)
+        self._keep = (A, d, rhs, obj, lo, up)
+        check(self._lib.elp_load_dense(
+            self._h, A.ctypes.data if m else None, d.ctypes.data if m else None,
+            rhs.ctypes.data if m else None, obj.ctypes.data, lo.ctypes.data, up.ctypes.data,
+            int(bool(maximize))), "elp_load_dense")
+
+    def load_dense_device(self, dA_ptr: int, dirs, rhs, obj, lo=None, up=None, maximize=False):
+        m, n = self.m, self.n
+        d = dir_codes(dirs)
+        rhs = np.ascontiguousarray(rhs, dtype=np.float64).reshape(m)
+        obj = np.ascontiguousarray(obj, dtype=np.float64).reshape(n)
+        lo = np.zeros(n) if lo is None else np.ascontiguousarray(lo, dtype=np.float64)
+        up = np.full(n, np.inf) if up is None else np.ascontiguousarray(up, dtype=np.float64)
+        self._keep = (d, rhs, obj, lo, up)
+        check(self._lib.elp_load_dense_device(
+            self._h, ctypes.c_void_p(int(dA_ptr)), d.ctypes.data, rhs.ctypes.data, obj.ctypes.data,
+            lo.ctypes.data, up.ctypes.data, int(bool(maximize))), "elp_load_dense_device")
+
+    def load_generated(self, seed: int) -> None:
+        check(self._lib.elp_load_generated(self._h, int(seed)), "elp_load_generated")
+
+    def solve(self) -> int:
+        st = ctypes.c_int32(-1)
+        check(self._lib.elp_solve(self._h, ctypes.byref(st)), "elp_solve")
+        return st.value
+
+    def iterate(self, iters: int) -> int:
+        st = ctypes.c_int32(-1)
+        check(self._lib.elp_iterate(self._h, int(iters), ctypes.byref(st)), "elp_iterate")
+        return st.value
+
+    def stats(self) -> dict:
+        s = ElpStats()
+        check(self._lib.elp_get_stats(self._h, ctypes.byref(s)), "elp_get_stats")
+        return {f: getattr(s, f) for f, _ in ElpStats._fields_}
+
+    def trace(self) -> np.ndarray:
+        cap = self._trace_cap
+        buf = np.zeros(2 * max(cap, 1), dtype=np.int64)
+        cnt = ctypes.c_int64(0)
+        check(self._lib.elp_get_trace(self._h, buf.ctypes.data, cap, ctypes.byref(cnt)),
+              "elp_get_trace")
+        return buf[: 2 * cnt.value].reshape(-1, 2)
+
+    def solution(self, status: int) -> Solution:
+        m, n = self.m, self.n
+        x = np.zeros(n)
+        y = np.zeros(max(m, 1))
+        basis = np.zeros(max(m, 1), dtype=np.int64)
+        obj = ctypes.c_double(0.0)
+        check(self._lib.elp_get_solution(self._h, ctypes.byref(obj), x.ctypes.data,
+                                         y.ctypes.data, basis.ctypes.data), "elp_get_solution")
+        tr = self.trace() if self._trace_cap else None
+        return Solution(status, obj.value, x, y[:m], basis[:m], self.stats(), tr)
+
+
+def solve_dense(A, dirs, rhs, obj, lo=None, up=None, maximize=False, trace=0, **control) -> Solution:
+    """One-shot solve of a dense LP on the GPU (the R/class.R:260-278 hand-off)."""
+    m = len(rhs)
+    n = len(obj)
+    with Problem(m, n, **control) as p:
+        if trace:
+            p.set_trace(trace)
+        p.load_dense(A, dirs, rhs, obj, lo, up, maximize)
+        st = p.solve()
+        return p.solution(st)

@@ -1,0 +1,160 @@
+/*
+ * easylp_hip.h -- C ABI of the MI355X dense revised-simplex solver.
+ *
+ * Drop-in seam: the body of easylp$solve() at /root/reference/R/class.R:260-278
+ * (and the sensitivity read-back at :624, :641) hands a dense LP to lp_solve
+ * through lpSolveAPI.  These entry points are what an R .Call() shim (see
+ * INTEGRATION.md) binds instead; each one cites the lpSolveAPI call(s) it
+ * replaces.  Plain C types only: pointers, sizes, int32/int64, double.
+ *
+ * Error convention: functions return 0 on success and a negative ELP_E_* code
+ * on usage / device error (elp_last_error() explains).  The LP outcome is
+ * reported separately in lp_solve's numbering so R/class.R:279-295 is unchanged:
+ * 0 optimal, 1 sub-optimal (iteration cap), 2 infeasible, 3 unbounded,
+ * 5 numerical failure, 7 timeout.  Infinite values are accepted as +-Inf or as
+ * |v| >= control.infinity (1e30, lp_solve's infinity) and are reported back as
+ * +-1e30, so R/utils.R:172-176 (large_to_infinity) still applies.
+ */
+#ifndef EASYLP_HIP_H
+#define EASYLP_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ELP_ABI_VERSION 1
+
+/* row directions, mirroring R/class.R:272 ("==" -> "=") and the "<"/">"
+ * spellings accepted by R/methods.R:215-219 */
+#define ELP_LE 1
+#define ELP_GE 2
+#define ELP_EQ 3
+
+/* lp_solve status numbering (R/class.R:279-295) */
+#define ELP_OPTIMAL 0
+#define ELP_SUBOPTIMAL 1
+#define ELP_INFEASIBLE 2
+#define ELP_UNBOUNDED 3
+#define ELP_NUMFAILURE 5
+#define ELP_TIMEOUT 7
+
+/* usage / device errors (negative return values) */
+#define ELP_E_ARG -1
+#define ELP_E_STATE -2
+#define ELP_E_NOMEM -3
+#define ELP_E_HIP -4
+#define ELP_E_COMM -5
+#define ELP_E_UNSUPPORTED -6
+
+typedef struct elp_handle elp_handle;
+
+typedef struct elp_control {
+    double tol_primal;       /* Harris primal feasibility tolerance    (1e-9)  */
+    double tol_dual;         /* optimality tolerance on |d_j|          (1e-9)  */
+    double tol_pivot;        /* |alpha| below this never limits a step (1e-9)  */
+    double infinity;         /* lp_solve infinity                      (1e30)  */
+    double time_limit;       /* seconds, <= 0: none   (lp.control timeout)     */
+    int64_t max_iter;        /* <= 0: 100*(m+n)+10000                          */
+    int32_t refactor_period; /* pivots between Gauss-Jordan refactors  (100)   */
+    int32_t degen_switch;    /* degenerate pivots before Bland's rule  (50)    */
+    int32_t device;          /* HIP device ordinal for this handle     (0)     */
+    int32_t sync_every;      /* iterations launched between host polls (32)    */
+    int32_t verbose;         /* 0 quiet                                         */
+    int32_t reserved[7];
+} elp_control;
+
+typedef struct elp_stats {
+    int64_t iterations;        /* simplex iterations, both phases             */
+    int64_t phase1_iterations;
+    int64_t bound_flips;
+    int64_t degenerate;
+    int64_t refactors;
+    int64_t bump_dim;          /* k: basic structural columns at exit          */
+    int64_t y_rows;            /* |Y|: rows with a nonbasic slack at exit      */
+    int64_t host_polls;
+    double seconds_total;      /* elp_solve wall time                          */
+    double seconds_loop;       /* simplex loop only (excludes load / H2D)      */
+    double seconds_load;       /* elp_load_* (H2D + device canonicalisation)  */
+    double price_bytes;        /* algorithmic bytes of the pricing sweeps      */
+    int32_t world_size;        /* ranks sharing the column partition           */
+    int32_t rank;
+    int64_t col0, ncols;       /* this rank's column shard                     */
+    /* pricing-kernel timing (control.verbose & ELP_PROFILE_PRICE): HIP events
+     * on the solver's stream around every pricing launch of iteration chunks
+     * that ran to completion */
+    double price_seconds;      /* sum of timed pricing-kernel durations        */
+    double price_timed_bytes;  /* algorithmic bytes of those launches          */
+    int64_t price_timed_launches;
+} elp_stats;
+
+#define ELP_PROFILE_PRICE 2   /* elp_control.verbose bit */
+
+/* Fill *c with defaults. */
+void elp_default_control(elp_control* c);
+
+/* make.lp(nrow = 0, ncol = n) + lp.control(...)      R/class.R:260, :262
+ * m rows, n structural columns (n >= 1, m >= 0).  ctl may be NULL. */
+int elp_create(elp_handle** h, int64_t m, int64_t n, const elp_control* ctl);
+
+/* set.objfn / lp.control(sense=) / set.bounds / add.constraint   R/class.R:261-274
+ * A: column-major m x n host array (lda = m, R's native matrix layout).
+ * dir[m] in {ELP_LE, ELP_GE, ELP_EQ}; rhs[m]; obj[n]; lo[n], up[n] (NULL:
+ * 0 and +inf).  maximize != 0 for sense "max".  Inputs are copied. */
+int elp_load_dense(elp_handle* h, const double* A, const int32_t* dir, const double* rhs,
+                   const double* obj, const double* lo, const double* up, int32_t maximize);
+
+/* Same, with A already in device memory on the handle's device (lda = m);
+ * the solver reads it in place and never writes it; the caller keeps it alive
+ * until elp_destroy. The small vectors are host arrays. */
+int elp_load_dense_device(elp_handle* h, const double* dA, const int32_t* dir, const double* rhs,
+                          const double* obj, const double* lo, const double* up,
+                          int32_t maximize);
+
+/* Synthetic dense LP of SURVEY.md 8d generated on the device (bench / tests):
+ * maximize c'x, A x <= b, x >= 0, A_ij, c_j ~ U[0,1), b_i = n/8 + U n/4,
+ * counter-based (seed, stream, global index) so every rank / the oracle
+ * regenerate the same numbers. */
+int elp_load_generated(elp_handle* h, uint64_t seed);
+
+/* solve(prob)                                          R/class.R:276 */
+int elp_solve(elp_handle* h, int32_t* lp_status);
+
+/* Run at most `iters` more simplex iterations (bench steps); *lp_status is
+ * ELP_SUBOPTIMAL while the solve is still in progress. */
+int elp_iterate(elp_handle* h, int64_t iters, int32_t* lp_status);
+
+/* get.objective / get.variables (+ duals and basis)    R/class.R:277-278
+ * Any output pointer may be NULL.  x[n], y[m] (duals in the user's sense),
+ * basis[m] sorted basic variable ids: j < n structural, n+i slack of row i,
+ * n+m+i artificial of row i. */
+int elp_get_solution(elp_handle* h, double* objval, double* x, double* y, int64_t* basis);
+
+int elp_get_stats(elp_handle* h, elp_stats* st);
+
+/* Pivot trace for parity tests: (entering, leaving) per iteration, leaving
+ * = -1 for a bound flip.  Enable before elp_solve with capacity > 0. */
+int elp_set_trace(elp_handle* h, int64_t capacity);
+int elp_get_trace(elp_handle* h, int64_t* pairs, int64_t capacity, int64_t* count);
+
+/* Multi-GPU column sharding: one process per GPU.  Rank 0
+ * calls elp_comm_unique_id, ships the 128-byte id to every rank (e.g. over
+ * torch.distributed), every rank calls elp_comm_init with it BEFORE
+ * elp_load_*.  Rank r then owns columns [r*n/P, (r+1)*n/P). */
+int elp_comm_unique_id(uint8_t id[128]);
+int elp_comm_init(elp_handle* h, const uint8_t id[128], int32_t world_size, int32_t rank);
+
+/* R finalizer for self$pointer (R/class.R:300; EasyLP's finalize at
+ * R/class.R:497-501 is empty, this one frees device memory). */
+void elp_destroy(elp_handle* h);
+
+/* Thread-local description of the last negative return. */
+const char* elp_last_error(void);
+
+int32_t elp_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

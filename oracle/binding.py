@@ -27,6 +27,7 @@ class OrcControl(ctypes.Structure):
         ("max_iter", ctypes.c_int64),
         ("refactor_period", ctypes.c_int32),
         ("degen_switch", ctypes.c_int32),
+        ("t_mark_iter", ctypes.c_int64),
     ]
 
 
@@ -41,6 +42,7 @@ class OrcStats(ctypes.Structure):
         ("y_rows", ctypes.c_int64),
         ("seconds", ctypes.c_double),
         ("price_bytes", ctypes.c_double),
+        ("seconds_at_mark", ctypes.c_double),
     ]
 
 

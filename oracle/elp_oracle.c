@@ -240,11 +240,18 @@ static int refactor(orc_t* s) {
 /* ------------------------------------------------------------------ */
 enum { PH_OPTIMAL = 0, PH_UNBOUNDED = 3, PH_NUMFAIL = 5, PH_ITERCAP = 1, PH_P1DONE = 10 };
 
+/* phase-1 infeasibility sum, in wave order (one 64-lane wave on the GPU) */
 static double art_sum(const orc_t* s) {
-    double acc = 0.0;
-    for (int64_t i = 0; i < s->m; ++i)
-        if (s->cover[i] >= s->n + s->m) acc = acc + s->xr[i];
-    return acc;
+    double lane[WAVE];
+    for (int l = 0; l < WAVE; ++l) {
+        double acc = 0.0;
+        for (int64_t i = l; i < s->m; i += WAVE)
+            if (s->cover[i] >= s->n + s->m) acc = acc + s->xr[i];
+        lane[l] = acc;
+    }
+    for (int off = WAVE / 2; off >= 1; off >>= 1)
+        for (int l = 0; l < off; ++l) lane[l] = lane[l] + lane[l + off];
+    return lane[0];
 }
 
 /* basic entry e: covered row e (< m) or bump position e - m */
@@ -271,6 +278,11 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
     int64_t since_refactor = 0, ndegen = 0;
     int bland = 0;
     for (;;) {
+        if (*iter == ctl->t_mark_iter && st->seconds_at_mark == 0.0) {
+            struct timespec tm;
+            clock_gettime(CLOCK_MONOTONIC, &tm);
+            st->seconds_at_mark = (double)tm.tv_sec + 1e-9 * (double)tm.tv_nsec;
+        }
         if (phase == 1 && art_sum(s) <= s->tol_inf) return PH_P1DONE;
         if (*iter >= max_iter) return PH_ITERCAP;
         if (since_refactor >= ctl->refactor_period) {
@@ -559,6 +571,7 @@ void orc_default_control(orc_control* c) {
     c->max_iter = 0;
     c->refactor_period = 100;
     c->degen_switch = 50;
+    c->t_mark_iter = -1;
 }
 
 static int cmp_i64(const void* a, const void* b) {
@@ -750,6 +763,8 @@ int orc_solve_dense(int64_t m, int64_t n, const double* A, const int32_t* dir, c
     st.bump_dim = s->k;
     st.y_rows = s->ny;
     st.seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    if (st.seconds_at_mark != 0.0) /* -> seconds from the mark to the end */
+        st.seconds_at_mark = ((double)t1.tv_sec + 1e-9 * (double)t1.tv_nsec) - st.seconds_at_mark;
     if (st_out) *st_out = st;
 
     free(s->b); free(s->lb); free(s->ub); free(s->cost); free(s->xval); free(s->vstat);

@@ -37,6 +37,8 @@ typedef struct orc_control {
     int64_t max_iter;      /* <=0: default 100*(m+n)+10000                   */
     int32_t refactor_period;
     int32_t degen_switch;  /* consecutive degenerate pivots before Bland     */
+    int64_t t_mark_iter;   /* record the wall time when this many iterations
+                              have run (stats.seconds_at_mark); <0: never     */
 } orc_control;
 
 typedef struct orc_stats {
@@ -49,6 +51,7 @@ typedef struct orc_stats {
     int64_t y_rows;        /* |Y| at exit: rows with a nonbasic slack         */
     double seconds;
     double price_bytes;    /* sum over iterations of 8*(|Y|*n + n + |Y|)      */
+    double seconds_at_mark;
 } orc_stats;
 
 void orc_default_control(orc_control* c);
