@@ -50,8 +50,8 @@ __global__ void k_gen_bc(uint64_t seed, int m, int64_t ncols, int64_t col0, int6
     const uint64_t kb = gen_key(seed, 2), kc = gen_key(seed, 1);
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const double e = (double)n_global / 8.0, qq = (double)n_global / 4.0;
-    if (t < m) b[t] = e + gen_u01k(kb, (uint64_t)t) * qq;
-    if (t < ncols) c[t] = gen_u01k(kc, (uint64_t)(col0 + t));
+    if (b && t < m) b[t] = e + gen_u01k(kb, (uint64_t)t) * qq;
+    if (c && t < ncols) c[t] = gen_u01k(kc, (uint64_t)(col0 + t));
 }
 
 // ------------------------------------------------------------ helpers
@@ -652,9 +652,10 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
             c->status = ST_UNBOUNDED;
             c->unb_var = q;
             c->unb_sig = sig;
-        } else if (it < c->trace_cap) {
+        }
+        if (it < c->trace_cap) {  // leaving: -1 bound flip, -2 unbounded ray
             d.trace[2 * it] = q;
-            d.trace[2 * it + 1] = action == ACT_FLIP ? -1 : best.var;
+            d.trace[2 * it + 1] = action == ACT_FLIP ? -1 : action == ACT_NONE ? -2 : best.var;
         }
     }
     if (action == ACT_NONE) {

@@ -134,7 +134,7 @@ int elp_get_solution(elp_handle* h, double* objval, double* x, double* y, int64_
 int elp_get_stats(elp_handle* h, elp_stats* st);
 
 /* Pivot trace for parity tests: (entering, leaving) per iteration, leaving
- * = -1 for a bound flip.  Enable before elp_solve with capacity > 0. */
+ * = -1 for a bound flip, -2 for the unbounded ray.  Enable before elp_solve with capacity > 0. */
 int elp_set_trace(elp_handle* h, int64_t capacity);
 int elp_get_trace(elp_handle* h, int64_t* pairs, int64_t capacity, int64_t* count);
 

@@ -428,6 +428,10 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
             continue;
         }
         if (theta == INF) {
+            if (trace && *iter - 1 < trace_cap) { /* unbounded ray: leaving -2 */
+                trace[2 * (*iter - 1)] = q;
+                trace[2 * (*iter - 1) + 1] = -2;
+            }
             *unb_var = q;
             *unb_sigma = sig;
             return PH_UNBOUNDED;

@@ -61,7 +61,7 @@ void orc_default_control(orc_control* c);
  * Outputs (caller-allocated, may be NULL): x[n], y[m] duals, basis[m]
  * (sorted basic variable ids: j<n structural, n+i slack, n+m+i artificial).
  * trace (may be NULL): up to trace_cap entries of (entering, leaving) per
- * iteration; leaving = -1 for a bound flip.
+ * iteration; leaving = -1 for a bound flip, -2 for the unbounded ray.
  * Returns lp_solve status: 0 optimal, 1 sub-optimal (iteration cap),
  * 2 infeasible, 3 unbounded, 5 numerical failure.  Negative = usage error. */
 int orc_solve_dense(int64_t m, int64_t n, const double* A, const int32_t* dir,
