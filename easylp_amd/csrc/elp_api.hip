@@ -95,7 +95,7 @@ static void free_dev(elp_handle* h) {
                     d.t,        d.acol, d.aR,   d.alS,   d.alU,  d.zz,    d.zpart, d.vrow,
                     d.vvec,     d.colA, d.rhs,  d.vstat, d.cover, d.rpos, d.Rl,    d.Sl,
                     d.spos,     d.Yl,  d.ypos,  d.perm,  d.pivstep, d.nzlist, d.nzcount,
-                    d.cand,     d.ctl, d.trace};
+                    d.cand,     d.ctl, d.trace, d.MinvT, d.cS, d.slo, d.shi, d.rlo, d.rhi};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     h->A_owned = nullptr;
@@ -157,6 +157,12 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.AR, (size_t)mm * (size_t)d.ldr));
     A(dalloc(&d.AS, (size_t)mm * (size_t)mm));
     A(dalloc(&d.Minv, (size_t)mm * (size_t)mm));
+    A(dalloc(&d.MinvT, (size_t)mm * (size_t)mm));
+    A(dalloc(&d.cS, mm));
+    A(dalloc(&d.slo, mm));
+    A(dalloc(&d.shi, mm));
+    A(dalloc(&d.rlo, mm));
+    A(dalloc(&d.rhi, mm));
     A(dalloc(&d.b, mm));
     A(dalloc(&d.obj, n));
     A(dalloc(&d.lb, nv));
@@ -201,6 +207,7 @@ static int alloc_all(elp_handle* h) {
     // AR padding columns must read as zeros; Minv / AS / work start clean
     A(hipMemsetAsync(d.AR, 0, (size_t)mm * (size_t)d.ldr * sizeof(double), h->st));
     A(hipMemsetAsync(d.Minv, 0, (size_t)mm * (size_t)mm * sizeof(double), h->st));
+    A(hipMemsetAsync(d.MinvT, 0, (size_t)mm * (size_t)mm * sizeof(double), h->st));
     A(hipMemsetAsync(d.zpart, 0, (size_t)mm * ((mm + ZCHUNK - 1) / ZCHUNK) * sizeof(double), h->st));
     if (e != hipSuccess) {
         free_dev(h);

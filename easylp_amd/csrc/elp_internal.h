@@ -71,10 +71,13 @@ struct Dev {
     double* AR;       // Y rows, row-major (m x ldr capacity)
     double* AS;       // basic structural columns, column-major (m x m capacity)
     double* Minv;     // bump inverse, row-major ldm x ldm
+    double* MinvT;    // its transpose (BTRAN and B^-1 rows read rows of it)
     double *W0, *W1;  // Gauss-Jordan work (k x k each)
     double *b, *obj, *lb, *ub, *cost, *xval, *asgn;
     double *xr, *xs, *y, *t, *acol, *aR, *alS, *alU, *zz, *zpart;
     double *vrow, *vvec, *colA, *rhs;
+    double *cS, *slo, *shi;  // per bump position: cost, bounds of S_p
+    double *rlo, *rhi;       // per covered row: bounds of the covering unit variable
     int8_t* vstat;
     int32_t *cover, *rpos, *Rl, *Sl, *spos, *Yl, *ypos, *perm, *pivstep, *nzlist, *nzcount;
     Cand* cand;

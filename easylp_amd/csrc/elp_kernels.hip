@@ -217,6 +217,8 @@ __global__ void k_init_rows(Dev d, const double* __restrict__ rhs_in) {
         d.cover[i] = sv;
         d.xr[i] = r;
         d.xval[sv] = 0.0;
+        d.rlo[i] = sl;
+        d.rhi[i] = su;
     } else {
         const double s = r < sl ? sl : su;
         d.vstat[sv] = (sl == su) ? VS_FIXED : (s == sl) ? VS_LOWER : VS_UPPER;
@@ -228,6 +230,8 @@ __global__ void k_init_rows(Dev d, const double* __restrict__ rhs_in) {
         d.vstat[av] = VS_BASIC;
         d.cover[i] = av;
         d.xr[i] = fabs(res);
+        d.rlo[i] = 0.0;
+        d.rhi[i] = HUGE_VAL;
     }
 }
 
@@ -284,25 +288,31 @@ __global__ void k_fill_AR(Dev d) {
 }
 
 // ============================================================== BTRAN
-// phase 1 only: t_q = c_{S_q} - sum_{covered i, y_i != 0} a_{i,S_q} y_i (ascending i)
-__global__ void k_btran_t(Dev d) {
+// phase 1: y on covered rows (sigma_u c_u), 0 on R rows
+__global__ void k_ycov(Dev d) {
+    if (d.ctl->status != ST_RUN) return;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= d.m) return;
+    const int u = d.cover[i];
+    d.y[i] = u >= 0 ? unit_sign(d, u, i) * d.cost[u] : 0.0;
+}
+// phase 1: t_p = c_{S_p} - wave_dot(AS[:,p], y_cov)   (one wave per p)
+__global__ void __launch_bounds__(256) k_btran_t(Dev d) {
     if (d.ctl->status != ST_RUN) return;
     const int k = d.ctl->k;
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= k) return;
+    const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (p >= k) return;
+    const double* col = d.AS + (size_t)p * (size_t)d.m;
     double acc = 0.0;
-    const double* col = d.AS + (size_t)q * (size_t)d.m;
-    for (int i = 0; i < d.m; ++i) {
-        const int u = d.cover[i];
-        if (u < 0) continue;
-        const double yi = unit_sign(d, u, i) * d.cost[u];
-        if (yi != 0.0) acc = fma(col[i], yi, acc);
-    }
-    d.t[q] = d.cost[d.Sl[q]] - acc;
+    for (int i = lane; i < d.m; i += 64) acc = fma(col[i], d.y[i], acc);
+    acc = wave_tree(acc);
+    if (lane == 0) d.t[p] = d.cS[p] - acc;
 }
 
-// loop-top checks (block 0) + y on covered rows + y_R = Minv^T t
-__global__ void __launch_bounds__(256) k_btran(Dev d, int phase) {
+// loop-top checks (block 0, wave 0) + y on covered rows (phase 2: sigma*0)
+// + y_R[p] = wave_dot(MinvT[p, 0:k], tv) scattered to y[R_p]  (one wave per p)
+__global__ void __launch_bounds__(256) k_btran(Dev d, int phase, const double* __restrict__ tv) {
     DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
     if (blockIdx.x == 0 && threadIdx.x < 64) {
@@ -318,21 +328,19 @@ __global__ void __launch_bounds__(256) k_btran(Dev d, int phase) {
         }
     }
     const int k = c->k;
-    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-    const int gsz = gridDim.x * blockDim.x;
-    for (int i = gid; i < d.m; i += gsz) {
-        const int u = d.cover[i];
-        if (u >= 0) d.y[i] = unit_sign(d, u, i) * d.cost[u];
+    if (phase == 2) {
+        const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+        const int gsz = gridDim.x * blockDim.x;
+        for (int i = gid; i < d.m; i += gsz)
+            if (d.cover[i] >= 0) d.y[i] = unit_sign(d, d.cover[i], i) * d.cost[d.cover[i]];
     }
-    for (int p = gid; p < k; p += gsz) {
+    const int lane = threadIdx.x & 63;
+    for (int p = blockIdx.x * 4 + (threadIdx.x >> 6); p < k; p += gridDim.x * 4) {
+        const double* row = d.MinvT + (size_t)p * d.ldm;
         double acc = 0.0;
-        if (phase == 1) {
-            for (int q = 0; q < k; ++q) acc = fma(d.Minv[(size_t)q * d.ldm + p], d.t[q], acc);
-        } else {
-            for (int q = 0; q < k; ++q)
-                acc = fma(d.Minv[(size_t)q * d.ldm + p], d.cost[d.Sl[q]], acc);
-        }
-        d.y[d.Rl[p]] = acc;
+        for (int q = lane; q < k; q += 64) acc = fma(row[q], tv[q], acc);
+        acc = wave_tree(acc);
+        if (lane == 0) d.y[d.Rl[p]] = acc;
     }
 }
 
@@ -362,16 +370,17 @@ __global__ void __launch_bounds__(256) k_price(Dev d) {
     const double* col = d.AR + j0;
     double acc0 = 0.0, acc1 = 0.0;
     int p = p0;
-    for (; p + 8 <= p1; p += 8) {
-        double2 v[8];
-        double yv[8];
+    constexpr int UNR = 16;  // rows in flight per wave: 16 KiB
+    for (; p + UNR <= p1; p += UNR) {
+        double2 v[UNR];
+        double yv[UNR];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < UNR; ++u)
             v[u] = *reinterpret_cast<const double2*>(col + (size_t)(p + u) * (size_t)d.ldr);
-            yv[u] = LDS_Y ? yy[p + u] : d.y[d.Yl[p + u]];
-        }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < UNR; ++u) yv[u] = LDS_Y ? yy[p + u] : d.y[d.Yl[p + u]];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
             acc0 = fma(v[u].x, yv[u], acc0);
             acc1 = fma(v[u].y, yv[u], acc1);
         }
@@ -501,9 +510,19 @@ __global__ void __launch_bounds__(256) k_ftran_z(Dev d, const double* __restrict
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= d.m) return;
     const int c1 = min(k, c0 + ZCHUNK);
+    const double* col = d.AS + (size_t)c0 * (size_t)d.m + i;
+    const size_t m = (size_t)d.m;
     double acc = 0.0;
-    for (int p = c0; p < c1; ++p) acc = fma(d.AS[(size_t)p * (size_t)d.m + i], wv[p], acc);
-    d.zpart[(size_t)ch * (size_t)d.m + i] = acc;
+    int p = c0;
+    for (; p + 16 <= c1; p += 16) {
+        double a[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) a[u] = col[(size_t)(p - c0 + u) * m];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc = fma(a[u], wv[p + u], acc);
+    }
+    for (; p < c1; ++p) acc = fma(col[(size_t)(p - c0) * m], wv[p], acc);
+    d.zpart[(size_t)ch * m + i] = acc;
 }
 
 // x_u = sign * (v_i - z_i) on covered rows after a refactor (z from k_ftran_z)
@@ -540,18 +559,24 @@ DEV Leave shfl_leave(const Leave& x, int off) {
     return o;
 }
 
-DEV bool basic_entry(const Dev& d, int e, int m, double sig, int& var, double& g, double& x) {
+// basic entry e: covered row e (< m) or bump position e - m; contiguous arrays only
+DEV bool basic_entry(const Dev& d, int e, int m, double sig, int& var, double& g, double& x,
+                     double& l, double& u) {
     if (e < m) {
-        const int u = d.cover[e];
-        if (u < 0) return false;
-        var = u;
+        const int cv = d.cover[e];
+        if (cv < 0) return false;
+        var = cv;
         g = sig * d.alU[e];
         x = d.xr[e];
+        l = d.rlo[e];
+        u = d.rhi[e];
     } else {
         const int p = e - m;
         var = d.Sl[p];
         g = sig * d.alS[p];
         x = d.xs[p];
+        l = d.slo[p];
+        u = d.shi[p];
     }
     return true;
 }
@@ -583,9 +608,8 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
     double tmax = INF;
     for (int e = tid; e < m + k; e += 1024) {
         int var;
-        double g, x;
-        if (!basic_entry(d, e, m, sig, var, g, x)) continue;
-        const double l = d.lb[var], u = d.ub[var];
+        double g, x, l, u;
+        if (!basic_entry(d, e, m, sig, var, g, x, l, u)) continue;
         double r;
         if (g > pivtol && l > -INF) r = bland ? (x - l) / g : (x - l + ptol) / g;
         else if (g < -pivtol && u < INF) r = bland ? (u - x) / (-g) : (u - x + ptol) / (-g);
@@ -602,9 +626,8 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
     best.e = -1;
     for (int e = tid; e < m + k; e += 1024) {
         int var;
-        double g, x;
-        if (!basic_entry(d, e, m, sig, var, g, x)) continue;
-        const double l = d.lb[var], u = d.ub[var];
+        double g, x, l, u;
+        if (!basic_entry(d, e, m, sig, var, g, x, l, u)) continue;
         double r;
         if (g > pivtol && l > -INF) r = (x - l) / g;
         else if (g < -pivtol && u < INF) r = (u - x) / (-g);
@@ -629,8 +652,9 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
     for (int i = 1; i < 16; ++i)
         if (leave_better(lred[i], best, bland)) best = lred[i];
     // ---- decision (uniform across the block)
+    const double lbq = d.lb[q], ubq = d.ub[q];
     const double theta = best.var >= 0 ? (best.r > 0.0 ? best.r : 0.0) : INF;
-    const double flip = (d.lb[q] > -INF && d.ub[q] < INF) ? d.ub[q] - d.lb[q] : INF;
+    const double flip = (lbq > -INF && ubq < INF) ? ubq - lbq : INF;
     int action;
     double step;
     if (flip < INF && flip <= theta) {
@@ -671,10 +695,10 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
         if (tid == 0) {
             if (d.vstat[q] == VS_LOWER) {
                 d.vstat[q] = VS_UPPER;
-                d.xval[q] = d.ub[q];
+                d.xval[q] = ubq;
             } else {
                 d.vstat[q] = VS_LOWER;
-                d.xval[q] = d.lb[q];
+                d.xval[q] = lbq;
             }
             c->flips++;
             c->ndegen = 0;
@@ -709,6 +733,7 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
             d.xval[lv] = at_lower ? lbv : ubv;
         }
         d.vstat[q] = VS_BASIC;
+        const double cq = d.cost[q];
         Plan P;
         P.action = ACT_PIVOT;
         P.k_old = k;
@@ -728,6 +753,9 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
                 d.Sl[lpos] = q;
                 d.spos[q] = lpos;
                 d.xs[lpos] = xq;
+                d.cS[lpos] = cq;
+                d.slo[lpos] = lbq;
+                d.shi[lpos] = ubq;
             } else {  // case B
                 const int i = lrow;
                 P.pcase = PC_B;
@@ -739,6 +767,9 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
                 d.Sl[k] = q;
                 d.spos[q] = k;
                 d.xs[k] = xq;
+                d.cS[k] = cq;
+                d.slo[k] = lbq;
+                d.shi[k] = ubq;
                 d.cover[i] = -1;
                 newk = k + 1;
                 if (!leave_art) {
@@ -755,8 +786,6 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
             if (a < 0) {  // case E
                 P.pcase = PC_E;
                 if (lrow != i0) c->status = ST_NUMFAIL;
-                d.cover[i0] = q;
-                d.xr[i0] = xq;
             } else if (lpos >= 0) {  // case C
                 const int b = lpos, last = k - 1;
                 P.pcase = PC_C;
@@ -768,6 +797,9 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
                     d.Sl[b] = d.Sl[last];
                     d.spos[d.Sl[b]] = b;
                     d.xs[b] = d.xs[last];
+                    d.cS[b] = d.cS[last];
+                    d.slo[b] = d.slo[last];
+                    d.shi[b] = d.shi[last];
                 }
                 if (a != last) {
                     d.Rl[a] = d.Rl[last];
@@ -775,8 +807,6 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
                 }
                 d.spos[lv] = -1;
                 d.rpos[i0] = -1;
-                d.cover[i0] = q;
-                d.xr[i0] = xq;
                 newk = k - 1;
             } else {  // case D
                 const int i1 = lrow;
@@ -787,9 +817,12 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
                 d.rpos[i1] = a;
                 d.rpos[i0] = -1;
                 d.cover[i1] = -1;
-                d.cover[i0] = q;
-                d.xr[i0] = xq;
             }
+            // the entering slack covers row i0
+            d.cover[i0] = q;
+            d.xr[i0] = xq;
+            d.rlo[i0] = lbq;
+            d.rhi[i0] = ubq;
             // row i0 leaves Y (its slack is basic now) ...
             const int s = d.ypos[i0], last = ny - 1;
             P.y_rm_slot = s;
@@ -824,29 +857,63 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
     } else if (pc == PC_C) {
         for (int j = tid; j < k; j += 1024) {
             d.vrow[j] = d.Minv[(size_t)P.b * d.ldm + j] / P.piv;
-            d.colA[j] = d.Minv[(size_t)j * d.ldm + P.a];
+            d.colA[j] = d.MinvT[(size_t)P.a * d.ldm + j];
         }
-    } else if (pc == PC_D) {
-        for (int j = tid; j < k; j += 1024) d.colA[j] = d.Minv[(size_t)j * d.ldm + P.a];
+    } else if (pc == PC_D || pc == PC_B) {
+        // gathered row A[row, S] = AS[row, 0:k] for the B^-1 row kernel
+        for (int j = tid; j < k; j += 1024) d.vrow[j] = d.AS[(size_t)j * (size_t)m + P.row];
+        if (pc == PC_D)
+            for (int j = tid; j < k; j += 1024) d.colA[j] = d.MinvT[(size_t)P.a * d.ldm + j];
     }
 }
 
-// cases B / D: vvec[c] = sum_q AS[row][q] * Minv[q][c]  (seq), B: / delta
+// cases B / D: vvec[c] = wave_dot(MinvT[c, 0:k], A[row, S]); B: / delta
 __global__ void __launch_bounds__(256) k_rowminv(Dev d) {
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
     const Plan P = c->plan;
     if (P.action != ACT_PIVOT || (P.pcase != PC_B && P.pcase != PC_D)) return;
     const int k = P.k_old;
-    const int col = blockIdx.x * blockDim.x + threadIdx.x;
+    const int col = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
     if (col >= k) return;
+    const double* row = d.MinvT + (size_t)col * d.ldm;
     double acc = 0.0;
-    for (int q = 0; q < k; ++q)
-        acc = fma(d.AS[(size_t)q * (size_t)d.m + P.row], d.Minv[(size_t)q * d.ldm + col], acc);
-    d.vvec[col] = P.pcase == PC_B ? acc / P.piv : acc;
+    for (int q = lane; q < k; q += 64) acc = fma(row[q], d.vrow[q], acc);
+    acc = wave_tree(acc);
+    if (lane == 0) d.vvec[col] = P.pcase == PC_B ? acc / P.piv : acc;
 }
 
-// Minv update (blocks [0, nb_minv)) + AS / AR copies (the rest)
+// new value of bump-inverse element (i, j); old(r, c) reads the pre-update matrix
+struct OldM {
+    const double* M;
+    size_t ld;
+    bool tr;
+    DEV double operator()(int r, int c) const { return tr ? M[(size_t)c * ld + r] : M[(size_t)r * ld + c]; }
+};
+DEV double minv_new(const Dev& d, const Plan& P, int i, int j, const OldM& old) {
+    const int k = P.k_old;
+    switch (P.pcase) {
+        case PC_A:
+            return (i == P.p) ? d.vrow[j] : fma(-d.alS[i], d.vrow[j], old(i, j));
+        case PC_B:
+            if (i < k && j < k) return fma(d.alS[i], d.vvec[j], old(i, j));
+            if (i < k) return -(d.alS[i] / P.piv);
+            if (j < k) return -d.vvec[j];
+            return 1.0 / P.piv;
+        case PC_C: {
+            const int sr = (i == P.b) ? P.last : i;
+            const int sc = (j == P.a) ? P.last : j;
+            return fma(-d.colA[sr], d.vrow[sc], old(sr, sc));
+        }
+        default: {  // PC_D
+            const double ca = d.colA[i] / d.vvec[P.a];
+            return (j == P.a) ? ca : fma(-ca, d.vvec[j], old(i, j));
+        }
+    }
+}
+
+// Minv and MinvT update (blocks [0, nb_minv)) + AS / AR copies (the rest)
 __global__ void __launch_bounds__(256) k_update(Dev d, int nb_minv) {
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
@@ -855,41 +922,20 @@ __global__ void __launch_bounds__(256) k_update(Dev d, int nb_minv) {
     const int k = P.k_old;
     const size_t ldm = (size_t)d.ldm;
     if ((int)blockIdx.x < nb_minv) {
+        if (P.pcase == PC_E) return;
+        const int kk = P.pcase == PC_B ? k + 1 : P.pcase == PC_C ? k - 1 : k;
+        const int64_t nel = (int64_t)kk * kk;
         const int64_t e0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
         const int64_t estride = (int64_t)nb_minv * blockDim.x;
-        if (P.pcase == PC_A) {
-            for (int64_t e = e0; e < (int64_t)k * k; e += estride) {
-                const int i = (int)(e / k), j = (int)(e % k);
-                double* M = d.Minv + (size_t)i * ldm + j;
-                *M = (i == P.p) ? d.vrow[j] : fma(-d.alS[i], d.vrow[j], *M);
-            }
-        } else if (P.pcase == PC_B) {
-            const int kk = k + 1;
-            const double delta = P.piv;
-            for (int64_t e = e0; e < (int64_t)kk * kk; e += estride) {
-                const int a = (int)(e / kk), cc = (int)(e % kk);
-                double* M = d.Minv + (size_t)a * ldm + cc;
-                if (a < k && cc < k) *M = fma(d.alS[a], d.vvec[cc], *M);
-                else if (a < k) *M = -(d.alS[a] / delta);
-                else if (cc < k) *M = -d.vvec[cc];
-                else *M = 1.0 / delta;
-            }
-        } else if (P.pcase == PC_C) {
-            const int kk = k - 1, last = P.last;
-            for (int64_t e = e0; e < (int64_t)kk * kk; e += estride) {
-                const int r = (int)(e / kk), cc = (int)(e % kk);
-                const int sr = (r == P.b) ? last : r;
-                const int sc = (cc == P.a) ? last : cc;
-                d.Minv[(size_t)r * ldm + cc] =
-                    fma(-d.colA[sr], d.vrow[sc], d.Minv[(size_t)sr * ldm + sc]);
-            }
-        } else if (P.pcase == PC_D) {
-            const double piv = d.vvec[P.a];
-            for (int64_t e = e0; e < (int64_t)k * k; e += estride) {
-                const int r = (int)(e / k), cc = (int)(e % k);
-                const double ca = d.colA[r] / piv;
-                double* M = d.Minv + (size_t)r * ldm + cc;
-                *M = (cc == P.a) ? ca : fma(-ca, d.vvec[cc], *M);
+        const OldM oM{d.Minv, ldm, false}, oT{d.MinvT, ldm, true};
+        for (int64_t e = e0; e < 2 * nel; e += estride) {
+            if (e < nel) {
+                const int i = (int)(e / kk), j = (int)(e % kk);
+                d.Minv[(size_t)i * ldm + j] = minv_new(d, P, i, j, oM);
+            } else {
+                const int64_t f = e - nel;  // MinvT element (j, i) = new Minv (i, j)
+                const int j = (int)(f / kk), i = (int)(f % kk);
+                d.MinvT[(size_t)j * ldm + i] = minv_new(d, P, i, j, oT);
             }
         }
         return;
@@ -994,7 +1040,9 @@ __global__ void k_gj_final(Dev d, int k, const double* __restrict__ W) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= (int64_t)k * k) return;
     const int a = (int)(e / k), cc = (int)(e % k);
-    d.Minv[(size_t)a * d.ldm + d.perm[cc]] = W[(size_t)d.perm[a] * k + cc];
+    const double v = W[(size_t)d.perm[a] * k + cc];
+    d.Minv[(size_t)a * d.ldm + d.perm[cc]] = v;
+    d.MinvT[(size_t)d.perm[cc] * d.ldm + a] = v;
 }
 
 // rhs_i = (b_i - sum_{nz} a_ij x_j) - s_i  and a_R for the bump solve
@@ -1016,8 +1064,17 @@ __global__ void k_phase2(Dev d) {
         d.cost[av] = 0.0;
         d.lb[av] = 0.0;
         d.ub[av] = 0.0;
+        if (d.cover[t] == av) {
+            d.rlo[t] = 0.0;
+            d.rhi[t] = 0.0;
+        }
     }
     if (t < d.n) d.cost[t] = d.maximize ? -d.obj[t] : d.obj[t];
+}
+// c_S after the phase-2 costs are in place
+__global__ void k_phase2_cS(Dev d) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < d.ctl->k) d.cS[p] = d.cost[d.Sl[p]];
 }
 
 __global__ void k_extract(Dev d, double* __restrict__ xout) {
@@ -1060,12 +1117,18 @@ hipError_t launch_init(const Dev& d, const double* lo, const double* up, const d
 hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStream_t st,
                             hipEvent_t ev0, hipEvent_t ev1) {
     const int m = d.m;
-    if (phase == 1 && k_ub > 0) k_btran_t<<<cdiv(k_ub, 256), 256, 0, st>>>(d);
+    const double* tv = d.cS;
+    if (phase == 1) {
+        if (m > 0) k_ycov<<<cdiv(m, 256), 256, 0, st>>>(d);
+        if (k_ub > 0) k_btran_t<<<cdiv(k_ub, 4), 256, 0, st>>>(d);
+        tv = d.t;
+    }
     {
-        const int64_t work = m > k_ub ? m : k_ub;
-        unsigned g = cdiv(work > 0 ? work : 1, 256);
+        unsigned g = cdiv(k_ub > 0 ? k_ub : 1, 4);
+        const unsigned gm = cdiv(m > 0 ? m : 1, 256);
+        if (phase == 2 && g < gm) g = gm;
         if (g > 1024) g = 1024;
-        k_btran<<<g, 256, 0, st>>>(d, phase);
+        k_btran<<<g, 256, 0, st>>>(d, phase, tv);
     }
     const unsigned ntiles = cdiv(d.n, TILE_COLS);
     const size_t ylds = (size_t)ny_ub * sizeof(double);
@@ -1082,9 +1145,9 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
         }
     }
     k_ratio<<<1, 1024, 0, st>>>(d, phase);
-    if (k_ub > 0) k_rowminv<<<cdiv(k_ub, 256), 256, 0, st>>>(d);
+    if (k_ub > 0) k_rowminv<<<cdiv(k_ub, 4), 256, 0, st>>>(d);
     {
-        const int64_t kk = (int64_t)(k_ub + 1) * (k_ub + 1);
+        const int64_t kk = 2 * (int64_t)(k_ub + 1) * (k_ub + 1);
         unsigned nb_minv = cdiv(kk, 256);
         if (nb_minv > 2048) nb_minv = 2048;
         const int64_t cw = m > d.n ? m : d.n;
@@ -1124,6 +1187,7 @@ hipError_t launch_refactor(const Dev& d, int k, hipStream_t st) {
 hipError_t launch_phase2(const Dev& d, hipStream_t st) {
     const int64_t mx = d.m > d.n ? d.m : d.n;
     k_phase2<<<cdiv(mx, 256), 256, 0, st>>>(d);
+    if (d.m > 0) k_phase2_cS<<<cdiv(d.m, 256), 256, 0, st>>>(d);
     return hipGetLastError();
 }
 

@@ -8,9 +8,10 @@
  * contract":
  *   price  : 4 contiguous slot chunks, fma chain per chunk, then
  *            ((0+p0)+p1)+p2)+p3                          (PRICE_SPLIT)
- *   wave   : 64 lane-strided fma chains + butterfly 32,16,..,1 (wave_dot)
+ *   wave   : 64 lane-strided fma chains + butterfly 32,16,..,1 (wave_dot):
+ *            FTRAN / BTRAN / B^-1 rows, phase-1 c_S correction, phase-1 sum
  *   zchunk : chunks of 64 bump positions, fma chain, sequential sum
- *   seq    : one fma chain in index order
+ *   seq    : one fma chain in index order (row activities)
  *
  * Algorithm (bounded primal revised simplex, minimisation form):
  *   - rows a_i'x + s_i = b_i; slack bounds encode dir (R/class.R:271-274,
@@ -141,12 +142,14 @@ static double zchunk_row(const orc_t* s, int64_t i, const double* w) {
     return tot;
 }
 
-/* v_c = sum_q A[i, S_q] * Minv[q][c]  (seq order over q) */
+/* v_c = sum_q A[i, S_q] * Minv[q][c]  (wave order over q: one wave per c,
+ * reading row c of Minv^T) */
 static void row_times_minv(orc_t* s, int64_t i, double* out) {
-    for (int64_t c = 0; c < s->k; ++c) {
-        double acc = 0.0;
-        for (int64_t q = 0; q < s->k; ++q) acc = fma(Aat(s, i, s->Sl[q]), *MI(s, q, c), acc);
-        out[c] = acc;
+    const int64_t k = s->k;
+    for (int64_t q = 0; q < k; ++q) s->aR[q] = Aat(s, i, s->Sl[q]);
+    for (int64_t c = 0; c < k; ++c) {
+        for (int64_t q = 0; q < k; ++q) s->tmp[q] = *MI(s, q, c);
+        out[c] = wave_dot(k, s->tmp, s->aR);
     }
 }
 
@@ -296,16 +299,18 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
             const int64_t u = s->cover[i];
             s->y[i] = u >= 0 ? unit_sign(s, u) * s->cost[u] : 0.0;
         }
-        for (int64_t p = 0; p < k; ++p) {
-            double acc = 0.0;
-            for (int64_t i = 0; i < m; ++i)
-                if (s->cover[i] >= 0 && s->y[i] != 0.0) acc = fma(Aat(s, i, s->Sl[p]), s->y[i], acc);
-            s->t[p] = s->cost[s->Sl[p]] - acc;
+        /* t_p = c_{S_p} - A[:,S_p]' y_cov   (phase 1 only: y_cov = 0 in phase 2),
+         * wave order over all m rows with y = 0 on uncovered rows */
+        if (phase == 1) {
+            for (int64_t p = 0; p < k; ++p)
+                s->t[p] = s->cost[s->Sl[p]] - wave_dot(m, &s->A[(size_t)s->Sl[p] * (size_t)m], s->y);
+        } else {
+            for (int64_t p = 0; p < k; ++p) s->t[p] = s->cost[s->Sl[p]];
         }
+        /* y_R = Minv' t: one wave per p over row p of Minv^T */
         for (int64_t p = 0; p < k; ++p) {
-            double acc = 0.0;
-            for (int64_t q = 0; q < k; ++q) acc = fma(*MI(s, q, p), s->t[q], acc);
-            s->yR[p] = acc;
+            for (int64_t q = 0; q < k; ++q) s->tmp[q] = *MI(s, q, p);
+            s->yR[p] = wave_dot(k, s->tmp, s->t);
         }
         for (int64_t p = 0; p < k; ++p) s->y[s->Rl[p]] = s->yR[p];
         /* ---- pricing over structurals (AR sweep) and slacks ---- */
