@@ -38,7 +38,8 @@ class ElpControl(ctypes.Structure):
         ("device", ctypes.c_int32),
         ("sync_every", ctypes.c_int32),
         ("verbose", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 7),
+        ("refactor_mode", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 6),
     ]
 
 

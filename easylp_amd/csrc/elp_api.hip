@@ -68,6 +68,7 @@ struct elp_handle {
     int64_t trace_cap = 0;
     elp::Comm comm;  // multi-GPU (world 1 = no-op)
     std::vector<hipEvent_t> ev;  // pricing-kernel timing pairs (profile mode)
+    int64_t stats_gj = 0;        // refactors that needed Gauss-Jordan
 };
 
 extern "C" void elp_default_control(elp_control* c) {
@@ -95,7 +96,7 @@ static void free_dev(elp_handle* h) {
                     d.t,        d.acol, d.aR,   d.alS,   d.alU,  d.zz,    d.zpart, d.vrow,
                     d.vvec,     d.colA, d.rhs,  d.vstat, d.cover, d.rpos, d.Rl,    d.Sl,
                     d.spos,     d.Yl,  d.ypos,  d.perm,  d.pivstep, d.nzlist, d.nzcount,
-                    d.cand,     d.ctl, d.trace, d.MinvT, d.cS, d.slo, d.shi, d.rlo, d.rhi};
+                    d.cand,     d.ctl, d.trace, d.MinvT, d.yy, d.cS, d.slo, d.shi, d.rlo, d.rhi};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     h->A_owned = nullptr;
@@ -174,6 +175,7 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.xr, mm));
     A(dalloc(&d.xs, mm));
     A(dalloc(&d.y, mm));
+    A(dalloc(&d.yy, mm));
     A(dalloc(&d.t, mm));
     A(dalloc(&d.acol, mm));
     A(dalloc(&d.aR, mm));
@@ -394,10 +396,30 @@ static int push_ctl_fields(elp_handle* h) {
     return 0;
 }
 
+// Refactor at a poll: one Newton-Schulz correction of Minv when the residual
+// of the maintained inverse is small, else a Gauss-Jordan rebuild; then the
+// primal values from b (oracle/elp_oracle.c refactor()).
 static int do_refactor(elp_handle* h, int k) {
-    int rc = ensure_w(h, k);
-    if (rc) return rc;
-    HIPCHK(launch_refactor(h->d, k, h->st));
+    if (k > 0) {
+        int rc = ensure_w(h, k);
+        if (rc) return rc;
+        HIPCHK(hipMemsetAsync(&h->d.ctl->ns_emax_bits, 0, sizeof(unsigned long long), h->st));
+        HIPCHK(launch_refactor_ns_resid(h->d, k, h->st));
+        unsigned long long bits = 0;
+        HIPCHK(hipMemcpyAsync(&h->hctl->ns_emax_bits, &h->d.ctl->ns_emax_bits, sizeof(bits),
+                              hipMemcpyDeviceToHost, h->st));
+        HIPCHK(hipStreamSynchronize(h->st));
+        bits = h->hctl->ns_emax_bits;
+        double emax;
+        std::memcpy(&emax, &bits, sizeof(emax));
+        if (emax <= NS_TOL && h->ctl.refactor_mode == 0) {
+            HIPCHK(launch_refactor_ns_update(h->d, k, h->st));
+        } else {
+            HIPCHK(launch_refactor_gj(h->d, k, h->st));
+            h->stats_gj++;
+        }
+    }
+    HIPCHK(launch_refactor_primal(h->d, k, h->st));
     h->stats.refactors++;
     return 0;
 }

@@ -26,7 +26,7 @@ enum : int32_t {
 enum : int32_t { PC_NONE = 0, PC_A = 1, PC_B = 2, PC_C = 3, PC_D = 4, PC_E = 5 };
 enum : int32_t { ACT_NONE = 0, ACT_FLIP = 1, ACT_PIVOT = 2 };
 
-constexpr int PRICE_SPLIT = 4;  // slot chunks per pricing tile (one per wave)
+constexpr int PRICE_SPLIT = 8;  // slot chunks per pricing tile (one per wave)
 constexpr int ZCHUNK = 64;      // bump positions per FTRAN-z partial
 constexpr int TILE_COLS = 128;  // columns per pricing workgroup (2 per lane)
 
@@ -55,6 +55,7 @@ struct DevCtl {
     int32_t infeasible_bounds, pad1;
     double price_bytes;    // algorithmic bytes of every pricing pass that ran
     int64_t price_passes;
+    unsigned long long ns_emax_bits;  // max|I - M Minv| of the last refactor (bits of a double >= 0)
 };
 
 struct Cand {
@@ -74,7 +75,7 @@ struct Dev {
     double* MinvT;    // its transpose (BTRAN and B^-1 rows read rows of it)
     double *W0, *W1;  // Gauss-Jordan work (k x k each)
     double *b, *obj, *lb, *ub, *cost, *xval, *asgn;
-    double *xr, *xs, *y, *t, *acol, *aR, *alS, *alU, *zz, *zpart;
+    double *xr, *xs, *y, *yy, *t, *acol, *aR, *alS, *alU, *zz, *zpart;  // yy: y on Y slots
     double *vrow, *vvec, *colA, *rhs;
     double *cS, *slo, *shi;  // per bump position: cost, bounds of S_p
     double *rlo, *rhi;       // per covered row: bounds of the covering unit variable
@@ -96,7 +97,12 @@ hipError_t launch_init(const Dev& d, const double* lo, const double* up, const d
 // ev0/ev1 (may be null): events recorded around the pricing kernel
 hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStream_t st,
                             hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
-hipError_t launch_refactor(const Dev& d, int k, hipStream_t st);
+// refactor = ns_resid; (host reads ns_emax) ns_update | gauss_jordan; primal
+constexpr double NS_TOL = 1e-6;
+hipError_t launch_refactor_ns_resid(const Dev& d, int k, hipStream_t st);
+hipError_t launch_refactor_ns_update(const Dev& d, int k, hipStream_t st);
+hipError_t launch_refactor_gj(const Dev& d, int k, hipStream_t st);
+hipError_t launch_refactor_primal(const Dev& d, int k, hipStream_t st);
 hipError_t launch_phase2(const Dev& d, hipStream_t st);
 hipError_t launch_extract(const Dev& d, double* xout, hipStream_t st);
 

@@ -294,7 +294,10 @@ __global__ void k_ycov(Dev d) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= d.m) return;
     const int u = d.cover[i];
-    d.y[i] = u >= 0 ? unit_sign(d, u, i) * d.cost[u] : 0.0;
+    const double yi = u >= 0 ? unit_sign(d, u, i) * d.cost[u] : 0.0;
+    d.y[i] = yi;
+    const int sl = d.ypos[i];
+    if (u >= 0 && sl >= 0) d.yy[sl] = yi;
 }
 // phase 1: t_p = c_{S_p} - wave_dot(AS[:,p], y_cov)   (one wave per p)
 __global__ void __launch_bounds__(256) k_btran_t(Dev d) {
@@ -331,8 +334,14 @@ __global__ void __launch_bounds__(256) k_btran(Dev d, int phase, const double* _
     if (phase == 2) {
         const int gid = blockIdx.x * blockDim.x + threadIdx.x;
         const int gsz = gridDim.x * blockDim.x;
-        for (int i = gid; i < d.m; i += gsz)
-            if (d.cover[i] >= 0) d.y[i] = unit_sign(d, d.cover[i], i) * d.cost[d.cover[i]];
+        for (int i = gid; i < d.m; i += gsz) {
+            const int u = d.cover[i];
+            if (u < 0) continue;
+            const double yi = unit_sign(d, u, i) * d.cost[u];
+            d.y[i] = yi;
+            const int sl = d.ypos[i];
+            if (sl >= 0) d.yy[sl] = yi;
+        }
     }
     const int lane = threadIdx.x & 63;
     for (int p = blockIdx.x * 4 + (threadIdx.x >> 6); p < k; p += gridDim.x * 4) {
@@ -340,54 +349,54 @@ __global__ void __launch_bounds__(256) k_btran(Dev d, int phase, const double* _
         double acc = 0.0;
         for (int q = lane; q < k; q += 64) acc = fma(row[q], tv[q], acc);
         acc = wave_tree(acc);
-        if (lane == 0) d.y[d.Rl[p]] = acc;
+        if (lane == 0) {
+            const int i = d.Rl[p];
+            d.y[i] = acc;
+            d.yy[d.ypos[i]] = acc;  // R rows always have a nonbasic slack
+        }
     }
 }
 
 // ============================================================== pricing
-// One workgroup = 4 waves = 128 columns x all Y slots.  Wave w sweeps slot
+// One workgroup = 8 waves = 128 columns x all Y slots.  Wave w sweeps slot
 // chunk w (PRICE_SPLIT contiguous chunks), lane l owns columns 2l, 2l+1 of the
 // tile (16-byte loads, 1 KiB per wave instruction, row-major AR so every load
-// is fully coalesced).  y_Y is staged in LDS.  The four chunk partials are
-// combined in LDS in chunk order, then the tile's Dantzig argmax is written.
-template <bool LDS_Y>
-__global__ void __launch_bounds__(256) k_price(Dev d) {
-    extern __shared__ __attribute__((aligned(16))) double yy[];
+// is fully coalesced), 16 rows in flight per wave; y_Y comes from the
+// contiguous yy[] written by BTRAN (wave-uniform scalar loads).  The chunk
+// partials are combined in LDS in chunk order, then the tile's argmin.
+constexpr int PRICE_THREADS = 64 * PRICE_SPLIT;
+__global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d) {
     __shared__ double part[PRICE_SPLIT][TILE_COLS];
-    __shared__ Cand red[4];
+    __shared__ Cand red[PRICE_SPLIT];
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
     const int ny = c->ny, bland = c->bland;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    if (LDS_Y) {
-        for (int p = threadIdx.x; p < ny; p += 256) yy[p] = d.y[d.Yl[p]];
-        __syncthreads();
-    }
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int L = (ny + PRICE_SPLIT - 1) / PRICE_SPLIT;
     const int p0 = w * L;
     const int p1 = min(ny, p0 + L);
     const int64_t j0 = (int64_t)blockIdx.x * TILE_COLS + 2 * lane;
     const double* col = d.AR + j0;
+    const double* __restrict__ yy = d.yy;
     double acc0 = 0.0, acc1 = 0.0;
     int p = p0;
     constexpr int UNR = 16;  // rows in flight per wave: 16 KiB
     for (; p + UNR <= p1; p += UNR) {
         double2 v[UNR];
-        double yv[UNR];
 #pragma unroll
         for (int u = 0; u < UNR; ++u)
             v[u] = *reinterpret_cast<const double2*>(col + (size_t)(p + u) * (size_t)d.ldr);
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) yv[u] = LDS_Y ? yy[p + u] : d.y[d.Yl[p + u]];
-#pragma unroll
         for (int u = 0; u < UNR; ++u) {
-            acc0 = fma(v[u].x, yv[u], acc0);
-            acc1 = fma(v[u].y, yv[u], acc1);
+            const double yv = yy[p + u];
+            acc0 = fma(v[u].x, yv, acc0);
+            acc1 = fma(v[u].y, yv, acc1);
         }
     }
     for (; p < p1; ++p) {
         const double2 v = *reinterpret_cast<const double2*>(col + (size_t)p * (size_t)d.ldr);
-        const double yv = LDS_Y ? yy[p] : d.y[d.Yl[p]];
+        const double yv = yy[p];
         acc0 = fma(v.x, yv, acc0);
         acc1 = fma(v.y, yv, acc1);
     }
@@ -420,7 +429,7 @@ __global__ void __launch_bounds__(256) k_price(Dev d) {
             }
         }
     }
-    best = block_best<256>(best, bland, red);
+    best = block_best<PRICE_THREADS>(best, bland, red);
     if (threadIdx.x == 0) d.cand[blockIdx.x] = best;
 }
 
@@ -446,7 +455,7 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles) {
         const int j = d.n + i;
         const int8_t vs = d.vstat[j];
         if (vs == VS_FIXED) continue;
-        const double dj = d.cost[j] - d.y[i];
+        const double dj = d.cost[j] - d.yy[p];
         Cand o;
         o.j = -1;
         if ((vs == VS_LOWER || vs == VS_FREE) && dj < -dtol) {
@@ -540,7 +549,7 @@ __global__ void k_xr_from_z(Dev d) {
 
 // ============================================================== ratio test
 struct Leave {
-    double ag, r, g;
+    double ag, r, g, l, u;
     int var, e;
 };
 DEV bool leave_better(const Leave& a, const Leave& b, int bland) {
@@ -554,65 +563,115 @@ DEV Leave shfl_leave(const Leave& x, int off) {
     o.ag = __shfl_xor(x.ag, off);
     o.r = __shfl_xor(x.r, off);
     o.g = __shfl_xor(x.g, off);
+    o.l = __shfl_xor(x.l, off);
+    o.u = __shfl_xor(x.u, off);
     o.var = __shfl_xor(x.var, off);
     o.e = __shfl_xor(x.e, off);
     return o;
 }
 
-// basic entry e: covered row e (< m) or bump position e - m; contiguous arrays only
-DEV bool basic_entry(const Dev& d, int e, int m, double sig, int& var, double& g, double& x,
-                     double& l, double& u) {
+// Scalars the pivot bookkeeping needs, fetched in parallel at kernel start.
+enum { SC_LBQ, SC_UBQ, SC_XVQ, SC_CQ, SC_SLL, SC_CSL, SC_SLOL, SC_SHIL, SC_N };
+enum { SI_VSQ, SI_RPOS0, SI_YPOS0, SI_YLAST, SI_SLLAST, SI_RLLAST, SI_N };
+
+DEV void load_entry(const Dev& d, int e, int m, int k, int nch, double sig, int& var, double& g,
+                    double& x, double& lo, double& hi) {
+    var = -1;
+    g = x = lo = hi = 0.0;
     if (e < m) {
-        const int cv = d.cover[e];
-        if (cv < 0) return false;
-        var = cv;
-        g = sig * d.alU[e];
-        x = d.xr[e];
-        l = d.rlo[e];
-        u = d.rhi[e];
-    } else {
+        const int u = d.cover[e];
+        if (u >= 0) {
+            double z = 0.0;
+            for (int ch = 0; ch < nch; ++ch) z = z + d.zpart[(size_t)ch * m + e];
+            const double alU = unit_sign(d, u, e) * (d.acol[e] - z);
+            var = u;
+            g = sig * alU;
+            x = d.xr[e];
+            lo = d.rlo[e];
+            hi = d.rhi[e];
+        }
+    } else if (e < m + k) {
         const int p = e - m;
         var = d.Sl[p];
         g = sig * d.alS[p];
         x = d.xs[p];
-        l = d.slo[p];
-        u = d.shi[p];
+        lo = d.slo[p];
+        hi = d.shi[p];
     }
-    return true;
 }
 
+// Harris two-pass ratio test + primal update + pivot plan (one workgroup).
+// Every thread owns NR basic entries e = tid + 1024 t (covered rows first,
+// then bump positions), kept in registers across both passes; NR = 0 is the
+// streaming variant for very large m (entries re-read from memory per pass).
+template <int NR>
 __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
     __shared__ double dred[16];
     __shared__ Leave lred[16];
+    __shared__ double sc[SC_N];
+    __shared__ int si[SI_N];
+    __shared__ double s_xs_last;
     __shared__ int s_action;
     __shared__ Plan s_plan;
     DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
-    const int m = d.m, n = d.n, k = c->k, q = c->q;
+    const int m = d.m, n = d.n, k = c->k, q = c->q, ny = c->ny;
     const double sig = c->sig;
     const int bland = c->bland;
     const int tid = threadIdx.x;
-    // ---- alpha on covered rows: combine the z chunks in order
-    const int nch = (k + ZCHUNK - 1) / ZCHUNK;
-    for (int i = tid; i < m; i += 1024) {
-        const int u = d.cover[i];
-        if (u < 0) continue;
-        double z = 0.0;
-        for (int ch = 0; ch < nch; ++ch) z = z + d.zpart[(size_t)ch * m + i];
-        d.zz[i] = z;
-        d.alU[i] = unit_sign(d, u, i) * (d.acol[i] - z);
+    const int last = k - 1;
+    // ---- parallel prefetch of bookkeeping scalars
+    if (tid < SC_N + SI_N) {
+        const int i0 = q - n;
+        switch (tid) {
+            case SC_LBQ: sc[SC_LBQ] = d.lb[q]; break;
+            case SC_UBQ: sc[SC_UBQ] = d.ub[q]; break;
+            case SC_XVQ: sc[SC_XVQ] = d.xval[q]; break;
+            case SC_CQ: sc[SC_CQ] = d.cost[q]; break;
+            case SC_SLL: sc[SC_SLL] = 0.0; break;
+            case SC_CSL: sc[SC_CSL] = last >= 0 ? d.cS[last] : 0.0; break;
+            case SC_SLOL: sc[SC_SLOL] = last >= 0 ? d.slo[last] : 0.0; break;
+            case SC_SHIL: sc[SC_SHIL] = last >= 0 ? d.shi[last] : 0.0; break;
+            case SC_N + SI_VSQ: si[SI_VSQ] = d.vstat[q]; break;
+            case SC_N + SI_RPOS0: si[SI_RPOS0] = i0 >= 0 ? d.rpos[i0] : -1; break;
+            case SC_N + SI_YPOS0: si[SI_YPOS0] = i0 >= 0 ? d.ypos[i0] : -1; break;
+            case SC_N + SI_YLAST: si[SI_YLAST] = ny > 0 ? d.Yl[ny - 1] : -1; break;
+            case SC_N + SI_SLLAST: si[SI_SLLAST] = last >= 0 ? d.Sl[last] : -1; break;
+            case SC_N + SI_RLLAST: si[SI_RLLAST] = last >= 0 ? d.Rl[last] : -1; break;
+        }
     }
-    __syncthreads();
+    // ---- load entries; alpha on covered rows from the z chunks (in order)
+    const int nch = (k + ZCHUNK - 1) / ZCHUNK;
+    constexpr int NREG = NR > 0 ? NR : 1;
+    double g[NREG], x[NREG], lo[NREG], hi[NREG];
+    int var[NREG];
+    const int npass = NR > 0 ? NR : (m + k + 1023) / 1024;
+    // entry t of this thread: registers (NR > 0) or memory (NR == 0)
+#define ELP_ENTRY(t)                                                                     \
+    const int e_ = tid + 1024 * (t);                                                     \
+    int v_;                                                                              \
+    double g_, x_, lo_, hi_;                                                             \
+    if (NR > 0) {                                                                        \
+        v_ = var[(t) % NREG]; g_ = g[(t) % NREG]; x_ = x[(t) % NREG];                    \
+        lo_ = lo[(t) % NREG]; hi_ = hi[(t) % NREG];                                      \
+    } else {                                                                             \
+        load_entry(d, e_, m, k, nch, sig, v_, g_, x_, lo_, hi_);                         \
+    }
+    if (NR > 0) {
+#pragma unroll
+        for (int t = 0; t < NREG; ++t)
+            load_entry(d, tid + 1024 * t, m, k, nch, sig, var[t], g[t], x[t], lo[t], hi[t]);
+    }
     // ---- Harris pass 1
     const double ptol = c->tol_primal, pivtol = c->tol_pivot, INF = HUGE_VAL;
     double tmax = INF;
-    for (int e = tid; e < m + k; e += 1024) {
-        int var;
-        double g, x, l, u;
-        if (!basic_entry(d, e, m, sig, var, g, x, l, u)) continue;
+#pragma unroll
+    for (int t = 0; t < npass; ++t) {
+        ELP_ENTRY(t)
+        if (v_ < 0) continue;
         double r;
-        if (g > pivtol && l > -INF) r = bland ? (x - l) / g : (x - l + ptol) / g;
-        else if (g < -pivtol && u < INF) r = bland ? (u - x) / (-g) : (u - x + ptol) / (-g);
+        if (g_ > pivtol && lo_ > -INF) r = bland ? (x_ - lo_) / g_ : (x_ - lo_ + ptol) / g_;
+        else if (g_ < -pivtol && hi_ < INF) r = bland ? (hi_ - x_) / (-g_) : (hi_ - x_ + ptol) / (-g_);
         else continue;
         if (r < tmax) tmax = r;
     }
@@ -620,25 +679,25 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
     // ---- pass 2
     Leave best;
     best.var = -1;
-    best.ag = 0.0;
-    best.r = 0.0;
-    best.g = 0.0;
+    best.ag = best.r = best.g = best.l = best.u = 0.0;
     best.e = -1;
-    for (int e = tid; e < m + k; e += 1024) {
-        int var;
-        double g, x, l, u;
-        if (!basic_entry(d, e, m, sig, var, g, x, l, u)) continue;
+#pragma unroll
+    for (int t = 0; t < npass; ++t) {
+        ELP_ENTRY(t)
+        if (v_ < 0) continue;
         double r;
-        if (g > pivtol && l > -INF) r = (x - l) / g;
-        else if (g < -pivtol && u < INF) r = (u - x) / (-g);
+        if (g_ > pivtol && lo_ > -INF) r = (x_ - lo_) / g_;
+        else if (g_ < -pivtol && hi_ < INF) r = (hi_ - x_) / (-g_);
         else continue;
         if (!(r <= theta_max)) continue;
         Leave o;
-        o.var = var;
-        o.ag = fabs(g);
+        o.var = v_;
+        o.ag = fabs(g_);
         o.r = r;
-        o.g = g;
-        o.e = e;
+        o.g = g_;
+        o.l = lo_;
+        o.u = hi_;
+        o.e = e_;
         if (leave_better(o, best, bland)) best = o;
     }
 #pragma unroll
@@ -647,12 +706,12 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
         if (leave_better(o, best, bland)) best = o;
     }
     if ((tid & 63) == 0) lred[tid >> 6] = best;
-    __syncthreads();
+    __syncthreads();  // also publishes the prefetched scalars
     best = lred[0];
     for (int i = 1; i < 16; ++i)
         if (leave_better(lred[i], best, bland)) best = lred[i];
     // ---- decision (uniform across the block)
-    const double lbq = d.lb[q], ubq = d.ub[q];
+    const double lbq = sc[SC_LBQ], ubq = sc[SC_UBQ];
     const double theta = best.var >= 0 ? (best.r > 0.0 ? best.r : 0.0) : INF;
     const double flip = (lbq > -INF && ubq < INF) ? ubq - lbq : INF;
     int action;
@@ -667,7 +726,6 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
         action = ACT_PIVOT;
         step = theta;
     }
-    __syncthreads();
     if (tid == 0) {
         const int64_t it = c->iter;
         c->iter = it + 1;
@@ -686,14 +744,23 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
         if (tid == 0) c->plan.action = ACT_NONE;
         return;
     }
-    // ---- primal update x_B -= step * g
-    for (int i = tid; i < m; i += 1024)
-        if (d.cover[i] >= 0) d.xr[i] = fma(-step, sig * d.alU[i], d.xr[i]);
-    for (int p = tid; p < k; p += 1024) d.xs[p] = fma(-step, sig * d.alS[p], d.xs[p]);
+    // ---- primal update x_B -= step * g (from registers)
+#pragma unroll
+    for (int t = 0; t < npass; ++t) {
+        ELP_ENTRY(t)
+        if (v_ < 0) continue;
+        const double xn = fma(-step, g_, x_);
+        if (e_ < m) d.xr[e_] = xn;
+        else {
+            d.xs[e_ - m] = xn;
+            if (e_ - m == last) s_xs_last = xn;
+        }
+    }
+#undef ELP_ENTRY
     __syncthreads();
     if (action == ACT_FLIP) {
         if (tid == 0) {
-            if (d.vstat[q] == VS_LOWER) {
+            if (si[SI_VSQ] == VS_LOWER) {
                 d.vstat[q] = VS_UPPER;
                 d.xval[q] = ubq;
             } else {
@@ -707,7 +774,7 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
         }
         return;
     }
-    // ---- pivot: bookkeeping by thread 0, staging by all
+    // ---- pivot: bookkeeping by thread 0 (stores only, plus Minv[b][a] in case C)
     if (tid == 0) {
         if (theta == 0.0) {
             c->degenerate++;
@@ -719,7 +786,7 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
         const int lv = best.var;
         const int lrow = best.e < m ? best.e : -1;
         const int lpos = best.e < m ? -1 : best.e - m;
-        const double xq = d.xval[q] + sig * theta;
+        const double xq = sc[SC_XVQ] + sig * theta;
         const bool at_lower = best.g > 0.0;
         const bool leave_art = lv >= n + m;
         if (leave_art) {
@@ -728,12 +795,11 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
             d.vstat[lv] = VS_FIXED;
             d.xval[lv] = 0.0;
         } else {
-            const double lbv = d.lb[lv], ubv = d.ub[lv];
-            d.vstat[lv] = lbv == ubv ? VS_FIXED : at_lower ? VS_LOWER : VS_UPPER;
-            d.xval[lv] = at_lower ? lbv : ubv;
+            d.vstat[lv] = best.l == best.u ? VS_FIXED : at_lower ? VS_LOWER : VS_UPPER;
+            d.xval[lv] = at_lower ? best.l : best.u;
         }
         d.vstat[q] = VS_BASIC;
-        const double cq = d.cost[q];
+        const double cq = sc[SC_CQ];
         Plan P;
         P.action = ACT_PIVOT;
         P.k_old = k;
@@ -742,13 +808,13 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
         P.p = P.a = P.b = P.last = P.row = -1;
         P.y_rm_slot = P.y_rm_last = P.y_ap_slot = P.y_ap_row = -1;
         P.piv = 0.0;
-        int ny = c->ny;
+        int nny = ny;
         int newk = k;
         if (q < n) {
             if (lpos >= 0) {  // case A
                 P.pcase = PC_A;
                 P.p = lpos;
-                P.piv = d.alS[lpos];
+                P.piv = best.g * sig;  // alS[lpos]
                 d.spos[lv] = -1;
                 d.Sl[lpos] = q;
                 d.spos[q] = lpos;
@@ -761,7 +827,8 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
                 P.pcase = PC_B;
                 P.row = i;
                 P.p = k;
-                P.piv = d.acol[i] - d.zz[i];
+                // delta = acol_i - z_i = sigma_u * alU_i = sigma_u * sig * g (exact)
+                P.piv = unit_sign(d, lv, i) * (sig * best.g);
                 d.Rl[k] = i;
                 d.rpos[i] = k;
                 d.Sl[k] = q;
@@ -773,39 +840,41 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
                 d.cover[i] = -1;
                 newk = k + 1;
                 if (!leave_art) {
-                    P.y_ap_slot = ny;
+                    P.y_ap_slot = nny;
                     P.y_ap_row = i;
-                    d.Yl[ny] = i;
-                    d.ypos[i] = ny;
-                    ny++;
+                    d.Yl[nny] = i;
+                    d.ypos[i] = nny;
+                    nny++;
                 }
             }
         } else {
             const int i0 = q - n;
-            const int a = d.rpos[i0];
+            const int a = si[SI_RPOS0];
             if (a < 0) {  // case E
                 P.pcase = PC_E;
                 if (lrow != i0) c->status = ST_NUMFAIL;
             } else if (lpos >= 0) {  // case C
-                const int b = lpos, last = k - 1;
+                const int b = lpos;
                 P.pcase = PC_C;
                 P.a = a;
                 P.b = b;
                 P.last = last;
                 P.piv = d.Minv[(size_t)b * d.ldm + a];
                 if (b != last) {
-                    d.Sl[b] = d.Sl[last];
-                    d.spos[d.Sl[b]] = b;
-                    d.xs[b] = d.xs[last];
-                    d.cS[b] = d.cS[last];
-                    d.slo[b] = d.slo[last];
-                    d.shi[b] = d.shi[last];
+                    const int sl = si[SI_SLLAST];
+                    d.Sl[b] = sl;
+                    d.spos[sl] = b;
+                    d.xs[b] = s_xs_last;
+                    d.cS[b] = sc[SC_CSL];
+                    d.slo[b] = sc[SC_SLOL];
+                    d.shi[b] = sc[SC_SHIL];
                 }
                 if (a != last) {
-                    d.Rl[a] = d.Rl[last];
-                    d.rpos[d.Rl[a]] = a;
+                    const int rl = si[SI_RLLAST];
+                    d.Rl[a] = rl;
+                    d.rpos[rl] = a;
                 }
-                d.spos[lv] = -1;
+                d.spos[lv] = -1;  // lv != S_last whenever b != last
                 d.rpos[i0] = -1;
                 newk = k - 1;
             } else {  // case D
@@ -824,26 +893,27 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
             d.rlo[i0] = lbq;
             d.rhi[i0] = ubq;
             // row i0 leaves Y (its slack is basic now) ...
-            const int s = d.ypos[i0], last = ny - 1;
-            P.y_rm_slot = s;
-            P.y_rm_last = last;
-            if (s != last) {
-                d.Yl[s] = d.Yl[last];
-                d.ypos[d.Yl[s]] = s;
+            const int sl = si[SI_YPOS0], ylast = nny - 1;
+            P.y_rm_slot = sl;
+            P.y_rm_last = ylast;
+            if (sl != ylast) {
+                const int moved = si[SI_YLAST];
+                d.Yl[sl] = moved;
+                d.ypos[moved] = sl;
             }
             d.ypos[i0] = -1;
-            ny--;
+            nny--;
             // ... and in case D the leaving slack's row joins it
             if (P.pcase == PC_D && !leave_art) {
-                P.y_ap_slot = ny;
+                P.y_ap_slot = nny;
                 P.y_ap_row = lrow;
-                d.Yl[ny] = lrow;
-                d.ypos[lrow] = ny;
-                ny++;
+                d.Yl[nny] = lrow;
+                d.ypos[lrow] = nny;
+                nny++;
             }
         }
         c->k = newk;
-        c->ny = ny;
+        c->ny = nny;
         c->since_refactor++;
         c->plan = P;
         s_plan = P;
@@ -1056,6 +1126,70 @@ __global__ void k_refactor_rhs(Dev d) {
     if (p >= 0) d.aR[p] = r;
 }
 
+// ------------------------------------------------------------ Newton-Schulz
+// E = I - M Minv with M[i][l] = AS[l][Rl[i]] (= A[R_i, S_l]); 32x32 output
+// tiles, every output an fma chain over l in order (oracle newton_schulz).
+__global__ void __launch_bounds__(1024) k_ns_resid(Dev d, int k) {
+    __shared__ double Mt[32][33];
+    __shared__ double Bt[32][33];
+    __shared__ double red[16];
+    const int tx = threadIdx.x, ty = threadIdx.y;
+    const int i = blockIdx.y * 32 + ty, j = blockIdx.x * 32 + tx;
+    double acc = 0.0;
+    for (int l0 = 0; l0 < k; l0 += 32) {
+        const int li = l0 + tx, lj = l0 + ty;
+        const int ri = blockIdx.y * 32 + ty;
+        Mt[ty][tx] = (ri < k && li < k) ? d.AS[(size_t)li * (size_t)d.m + d.Rl[ri]] : 0.0;
+        Bt[ty][tx] = (lj < k && j < k) ? d.Minv[(size_t)lj * d.ldm + j] : 0.0;
+        __syncthreads();
+        const int lend = min(32, k - l0);
+        for (int ll = 0; ll < lend; ++ll) acc = fma(Mt[ty][ll], Bt[ll][tx], acc);
+        __syncthreads();
+    }
+    double e = 0.0;
+    if (i < k && j < k) {
+        e = (i == j ? 1.0 : 0.0) - acc;
+        d.W0[(size_t)i * k + j] = e;
+    }
+    const double am = block_max<1024>(fabs(e), red);
+    if (tx == 0 && ty == 0) atomicMax(&d.ctl->ns_emax_bits, (unsigned long long)__double_as_longlong(am));
+}
+
+// W1 = Minv + Minv E  (chain over l starting from Minv[i][j])
+__global__ void __launch_bounds__(1024) k_ns_update(Dev d, int k) {
+    __shared__ double At[32][33];
+    __shared__ double Et[32][33];
+    const int tx = threadIdx.x, ty = threadIdx.y;
+    const int i = blockIdx.y * 32 + ty, j = blockIdx.x * 32 + tx;
+    double acc = (i < k && j < k) ? d.Minv[(size_t)i * d.ldm + j] : 0.0;
+    for (int l0 = 0; l0 < k; l0 += 32) {
+        const int li = l0 + tx, lj = l0 + ty;
+        At[ty][tx] = (i < k && li < k) ? d.Minv[(size_t)i * d.ldm + li] : 0.0;
+        Et[ty][tx] = (lj < k && j < k) ? d.W0[(size_t)lj * k + j] : 0.0;
+        __syncthreads();
+        const int lend = min(32, k - l0);
+        for (int ll = 0; ll < lend; ++ll) acc = fma(At[ty][ll], Et[ll][tx], acc);
+        __syncthreads();
+    }
+    if (i < k && j < k) d.W1[(size_t)i * k + j] = acc;
+}
+
+// Minv = W1, MinvT = W1^T (transposed through LDS, both stores coalesced)
+__global__ void __launch_bounds__(1024) k_ns_store(Dev d, int k) {
+    __shared__ double T[32][33];
+    const int tx = threadIdx.x, ty = threadIdx.y;
+    const int i = blockIdx.y * 32 + ty, j = blockIdx.x * 32 + tx;
+    double v = 0.0;
+    if (i < k && j < k) {
+        v = d.W1[(size_t)i * k + j];
+        d.Minv[(size_t)i * d.ldm + j] = v;
+    }
+    T[ty][tx] = v;
+    __syncthreads();
+    const int ti = blockIdx.y * 32 + tx, tj = blockIdx.x * 32 + ty;  // MinvT[tj][ti]
+    if (ti < k && tj < k) d.MinvT[(size_t)tj * d.ldm + ti] = T[tx][ty];
+}
+
 // ============================================================== phase 2 / extract
 __global__ void k_phase2(Dev d) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1131,10 +1265,9 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
         k_btran<<<g, 256, 0, st>>>(d, phase, tv);
     }
     const unsigned ntiles = cdiv(d.n, TILE_COLS);
-    const size_t ylds = (size_t)ny_ub * sizeof(double);
+    (void)ny_ub;
     if (ev0) (void)hipEventRecord(ev0, st);
-    if (ylds <= 48 * 1024) k_price<true><<<ntiles, 256, ylds, st>>>(d);
-    else k_price<false><<<ntiles, 256, 0, st>>>(d);
+    k_price<<<ntiles, PRICE_THREADS, 0, st>>>(d);
     if (ev1) (void)hipEventRecord(ev1, st);
     k_select<<<1, 1024, 0, st>>>(d, (int)ntiles);
     if (k_ub > 0) {
@@ -1144,7 +1277,14 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
             k_ftran_z<<<g, 256, 0, st>>>(d, d.alS, 1);
         }
     }
-    k_ratio<<<1, 1024, 0, st>>>(d, phase);
+    {
+        const int ent = m + k_ub;  // basic entries: covered rows + bump positions
+        if (ent <= 1024) k_ratio<1><<<1, 1024, 0, st>>>(d, phase);
+        else if (ent <= 2048) k_ratio<2><<<1, 1024, 0, st>>>(d, phase);
+        else if (ent <= 4096) k_ratio<4><<<1, 1024, 0, st>>>(d, phase);
+        else if (ent <= 8192) k_ratio<8><<<1, 1024, 0, st>>>(d, phase);
+        else k_ratio<0><<<1, 1024, 0, st>>>(d, phase);
+    }
     if (k_ub > 0) k_rowminv<<<cdiv(k_ub, 4), 256, 0, st>>>(d);
     {
         const int64_t kk = 2 * (int64_t)(k_ub + 1) * (k_ub + 1);
@@ -1158,19 +1298,37 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
     return hipGetLastError();
 }
 
-hipError_t launch_refactor(const Dev& d, int k, hipStream_t st) {
-    if (k > 0) {
-        const int64_t kk = (int64_t)k * k;
-        k_gj_init<<<cdiv(kk > k ? kk : k, 256), 256, 0, st>>>(d, k);
-        double *W = d.W0, *W2 = d.W1;
-        for (int c = 0; c < k; ++c) {
-            k_gj_step<<<cdiv(kk, 256), 256, 0, st>>>(d, k, c, W, W2);
-            double* s = W;
-            W = W2;
-            W2 = s;
-        }
-        k_gj_final<<<cdiv(kk, 256), 256, 0, st>>>(d, k, W);
+hipError_t launch_refactor_ns_resid(const Dev& d, int k, hipStream_t st) {
+    if (k <= 0) return hipSuccess;
+    dim3 g(cdiv(k, 32), cdiv(k, 32));
+    k_ns_resid<<<g, dim3(32, 32), 0, st>>>(d, k);
+    return hipGetLastError();
+}
+
+hipError_t launch_refactor_ns_update(const Dev& d, int k, hipStream_t st) {
+    if (k <= 0) return hipSuccess;
+    dim3 g(cdiv(k, 32), cdiv(k, 32));
+    k_ns_update<<<g, dim3(32, 32), 0, st>>>(d, k);
+    k_ns_store<<<g, dim3(32, 32), 0, st>>>(d, k);
+    return hipGetLastError();
+}
+
+hipError_t launch_refactor_gj(const Dev& d, int k, hipStream_t st) {
+    if (k <= 0) return hipSuccess;
+    const int64_t kk = (int64_t)k * k;
+    k_gj_init<<<cdiv(kk > k ? kk : k, 256), 256, 0, st>>>(d, k);
+    double *W = d.W0, *W2 = d.W1;
+    for (int c = 0; c < k; ++c) {
+        k_gj_step<<<cdiv(kk, 256), 256, 0, st>>>(d, k, c, W, W2);
+        double* sw = W;
+        W = W2;
+        W2 = sw;
     }
+    k_gj_final<<<cdiv(kk, 256), 256, 0, st>>>(d, k, W);
+    return hipGetLastError();
+}
+
+hipError_t launch_refactor_primal(const Dev& d, int k, hipStream_t st) {
     k_nzlist<<<1, 1024, 0, st>>>(d);
     if (d.m > 0) {
         k_refactor_rhs<<<cdiv(d.m, 256), 256, 0, st>>>(d);

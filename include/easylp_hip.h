@@ -61,8 +61,10 @@ typedef struct elp_control {
     int32_t degen_switch;    /* degenerate pivots before Bland's rule  (50)    */
     int32_t device;          /* HIP device ordinal for this handle     (0)     */
     int32_t sync_every;      /* iterations launched between host polls (32)    */
-    int32_t verbose;         /* 0 quiet                                         */
-    int32_t reserved[7];
+    int32_t verbose;         /* 0 quiet; ELP_PROFILE_PRICE: time pricing kernel */
+    int32_t refactor_mode;   /* 0: Newton-Schulz correction, Gauss-Jordan when
+                                max|I - M Minv| > 1e-6; 1: always Gauss-Jordan */
+    int32_t reserved[6];
 } elp_control;
 
 typedef struct elp_stats {

@@ -28,6 +28,8 @@ class OrcControl(ctypes.Structure):
         ("refactor_period", ctypes.c_int32),
         ("degen_switch", ctypes.c_int32),
         ("t_mark_iter", ctypes.c_int64),
+        ("refactor_mode", ctypes.c_int32),
+        ("pad", ctypes.c_int32),
     ]
 
 
@@ -43,6 +45,7 @@ class OrcStats(ctypes.Structure):
         ("seconds", ctypes.c_double),
         ("price_bytes", ctypes.c_double),
         ("seconds_at_mark", ctypes.c_double),
+        ("gj_refactors", ctypes.c_int64),
     ]
 
 

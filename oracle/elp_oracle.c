@@ -6,8 +6,8 @@
  * so that the HIP kernels (also -ffp-contract=off, explicit fma) produce
  * the same bits.  Reduction orders follow DESIGN.md "Reduction order
  * contract":
- *   price  : 4 contiguous slot chunks, fma chain per chunk, then
- *            ((0+p0)+p1)+p2)+p3                          (PRICE_SPLIT)
+ *   price  : 8 contiguous slot chunks, fma chain per chunk, then the
+ *            partials added in chunk order starting from 0.0 (PRICE_SPLIT)
  *   wave   : 64 lane-strided fma chains + butterfly 32,16,..,1 (wave_dot):
  *            FTRAN / BTRAN / B^-1 rows, phase-1 c_S correction, phase-1 sum
  *   zchunk : chunks of 64 bump positions, fma chain, sequential sum
@@ -40,7 +40,7 @@
 #define VS_UPPER 2
 #define VS_FREE 3
 
-#define PRICE_SPLIT 4
+#define PRICE_SPLIT 8
 #define ZCHUNK 64
 #define WAVE 64
 
@@ -102,6 +102,8 @@ typedef struct {
     int8_t* used;
     int64_t* perm;
     double tol_inf;
+    int64_t gj_count; /* refactors that needed a fresh Gauss-Jordan */
+    int refactor_mode;
 } orc_t;
 
 static double* dalloc(size_t n) { return (double*)calloc(n ? n : 1, sizeof(double)); }
@@ -184,43 +186,83 @@ static void y_remove(orc_t* s, int64_t i) {
 }
 
 /* ------------------------------------------------------------------ */
-/* refactor: Gauss-Jordan with partial pivoting, then recompute x_B    */
+/* refactor: one Newton-Schulz correction of the maintained inverse    */
+/* (E = I - M Minv; Minv += Minv E) when max|E| <= NS_TOL, otherwise a  */
+/* fresh Gauss-Jordan inversion with partial pivoting; then x_B from b. */
 /* ------------------------------------------------------------------ */
+#define NS_TOL 1e-6
+
+static int gauss_jordan(orc_t* s) {
+    const int64_t k = s->k;
+    double *W = s->tmp, *W2 = s->tmp + (size_t)k * (size_t)k;
+    for (int64_t a = 0; a < k; ++a)
+        for (int64_t c = 0; c < k; ++c) W[a * k + c] = Aat(s, s->Rl[a], s->Sl[c]);
+    memset(s->used, 0, (size_t)k);
+    for (int64_t c = 0; c < k; ++c) {
+        int64_t p = -1;
+        double best = -1.0;
+        for (int64_t r = 0; r < k; ++r)
+            if (!s->used[r] && fabs(W[r * k + c]) > best) {
+                best = fabs(W[r * k + c]);
+                p = r;
+            }
+        const double piv = W[p * k + c];
+        if (!(fabs(piv) > 1e-13)) return -1;
+        s->perm[c] = p;
+        for (int64_t r = 0; r < k; ++r) {
+            if (r == p) {
+                for (int64_t j = 0; j < k; ++j)
+                    W2[r * k + j] = (j == c) ? 1.0 / piv : W[p * k + j] / piv;
+            } else {
+                const double f = W[r * k + c];
+                for (int64_t j = 0; j < k; ++j)
+                    W2[r * k + j] = (j == c) ? -(f / piv) : fma(-f, W[p * k + j] / piv, W[r * k + j]);
+            }
+        }
+        s->used[p] = 1;
+        double* sw = W;
+        W = W2;
+        W2 = sw;
+    }
+    for (int64_t a = 0; a < k; ++a)
+        for (int64_t c = 0; c < k; ++c) *MI(s, a, s->perm[c]) = W[s->perm[a] * k + c];
+    return 0;
+}
+
+/* one Newton-Schulz step; returns 1 if applied, 0 if the residual is too large */
+static int newton_schulz(orc_t* s) {
+    const int64_t k = s->k;
+    double *E = s->tmp, *Mk = s->tmp + (size_t)k * (size_t)k;
+    for (int64_t a = 0; a < k; ++a)
+        for (int64_t c = 0; c < k; ++c) Mk[a * k + c] = Aat(s, s->Rl[a], s->Sl[c]);
+    double emax = 0.0;
+    for (int64_t i = 0; i < k; ++i)
+        for (int64_t j = 0; j < k; ++j) {
+            double acc = 0.0; /* (M Minv)_ij, seq order over l */
+            for (int64_t l = 0; l < k; ++l) acc = fma(Mk[i * k + l], *MI(s, l, j), acc);
+            const double e = (i == j ? 1.0 : 0.0) - acc;
+            E[i * k + j] = e;
+            if (fabs(e) > emax) emax = fabs(e);
+        }
+    if (!(emax <= NS_TOL)) return 0;
+    /* Minv_new[i][j] = Minv[i][j] + sum_l Minv[i][l] E[l][j]  (seq, from Minv[i][j]) */
+    double* Nw = Mk;
+    for (int64_t i = 0; i < k; ++i)
+        for (int64_t j = 0; j < k; ++j) {
+            double acc = *MI(s, i, j);
+            for (int64_t l = 0; l < k; ++l) acc = fma(*MI(s, i, l), E[l * k + j], acc);
+            Nw[i * k + j] = acc;
+        }
+    for (int64_t i = 0; i < k; ++i)
+        for (int64_t j = 0; j < k; ++j) *MI(s, i, j) = Nw[i * k + j];
+    return 1;
+}
+
 static int refactor(orc_t* s) {
     const int64_t k = s->k, m = s->m, n = s->n;
-    if (k > 0) {
-        double *W = s->tmp, *W2 = s->tmp + (size_t)k * (size_t)k;
-        for (int64_t a = 0; a < k; ++a)
-            for (int64_t c = 0; c < k; ++c) W[a * k + c] = Aat(s, s->Rl[a], s->Sl[c]);
-        memset(s->used, 0, (size_t)k);
-        for (int64_t c = 0; c < k; ++c) {
-            int64_t p = -1;
-            double best = -1.0;
-            for (int64_t r = 0; r < k; ++r)
-                if (!s->used[r] && fabs(W[r * k + c]) > best) {
-                    best = fabs(W[r * k + c]);
-                    p = r;
-                }
-            const double piv = W[p * k + c];
-            if (!(fabs(piv) > 1e-13)) return -1;
-            s->perm[c] = p;
-            for (int64_t r = 0; r < k; ++r) {
-                if (r == p) {
-                    for (int64_t j = 0; j < k; ++j)
-                        W2[r * k + j] = (j == c) ? 1.0 / piv : W[p * k + j] / piv;
-                } else {
-                    const double f = W[r * k + c];
-                    for (int64_t j = 0; j < k; ++j)
-                        W2[r * k + j] = (j == c) ? -(f / piv) : fma(-f, W[p * k + j] / piv, W[r * k + j]);
-                }
-            }
-            s->used[p] = 1;
-            double* sw = W;
-            W = W2;
-            W2 = sw;
-        }
-        for (int64_t a = 0; a < k; ++a)
-            for (int64_t c = 0; c < k; ++c) *MI(s, a, s->perm[c]) = W[s->perm[a] * k + c];
+    if (k > 0 && (s->refactor_mode != 0 || !newton_schulz(s))) {
+        s->gj_count++;
+        if (gauss_jordan(s)) return -1;
     }
     /* primal values: rhs_i = (b_i - sum_{j nonbasic struct, x_j != 0} a_ij x_j) - s_i */
     for (int64_t i = 0; i < m; ++i) {
@@ -581,6 +623,8 @@ void orc_default_control(orc_control* c) {
     c->refactor_period = 100;
     c->degen_switch = 50;
     c->t_mark_iter = -1;
+    c->refactor_mode = 0;
+    c->pad = 0;
 }
 
 static int cmp_i64(const void* a, const void* b) {
@@ -615,6 +659,7 @@ int orc_solve_dense(int64_t m, int64_t n, const double* A, const int32_t* dir, c
     s->n = n;
     s->nv = n + 2 * m;
     s->A = A;
+    s->refactor_mode = ctl.refactor_mode;
     const int64_t nv = s->nv, mm = m > 0 ? m : 1;
     s->b = dalloc((size_t)mm);
     s->lb = dalloc((size_t)nv);
@@ -769,6 +814,7 @@ int orc_solve_dense(int64_t m, int64_t n, const double* A, const int32_t* dir, c
     }
     clock_gettime(CLOCK_MONOTONIC, &t1);
     st.iterations = iter;
+    st.gj_refactors = s->gj_count;
     st.bump_dim = s->k;
     st.y_rows = s->ny;
     st.seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);

@@ -39,6 +39,8 @@ typedef struct orc_control {
     int32_t degen_switch;  /* consecutive degenerate pivots before Bland     */
     int64_t t_mark_iter;   /* record the wall time when this many iterations
                               have run (stats.seconds_at_mark); <0: never     */
+    int32_t refactor_mode; /* 0 Newton-Schulz (GJ fallback), 1 always GJ     */
+    int32_t pad;
 } orc_control;
 
 typedef struct orc_stats {
@@ -52,6 +54,7 @@ typedef struct orc_stats {
     double seconds;
     double price_bytes;    /* sum over iterations of 8*(|Y|*n + n + |Y|)      */
     double seconds_at_mark;
+    int64_t gj_refactors;  /* refactors that fell back to Gauss-Jordan      */
 } orc_stats;
 
 void orc_default_control(orc_control* c);

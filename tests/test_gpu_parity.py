@@ -105,15 +105,17 @@ def test_iterate_in_chunks_equals_solve(gpu):
     np.testing.assert_array_equal(g.trace, ref.trace)
 
 
-@pytest.mark.parametrize("period", [1, 5, 37])
-def test_refactor_period_parity(gpu, period):
+@pytest.mark.parametrize("period,mode", [(1, 0), (5, 0), (37, 0), (5, 1), (37, 1)])
+def test_refactor_period_parity(gpu, period, mode):
+    """Newton-Schulz refactor (mode 0) and forced Gauss-Jordan (mode 1)."""
     from oracle import generate_dense, solve_dense as orc
     m, n = 120, 500
     A, b, c = generate_dense(9, m, n)
     g = gpu.solve_dense(A, np.ones(m, np.int32), b, c, maximize=True, trace=100000,
-                        refactor_period=period)
+                        refactor_period=period, refactor_mode=mode)
     o = orc(A, np.ones(m, np.int32), b, c, maximize=True, trace_cap=100000,
-            refactor_period=period)
+            refactor_period=period, refactor_mode=mode)
+    assert o.stats["gj_refactors"] == (o.stats["refactors"] if mode else 0)
     _cmp(g, o)
     np.testing.assert_array_equal(g.trace, o.trace)
 

@@ -87,3 +87,37 @@ def test_trace_records_pivots():
     r = solve_dense(A, np.ones(50, np.int32), b, c, maximize=True, trace_cap=10000)
     assert r.trace.shape == (r.stats["iterations"], 2)
     assert np.all(r.trace[:, 0] >= 0)
+
+
+def test_gauss_jordan_refactor_mode_same_optimum():
+    A, b, c = generate_dense(4, 200, 800)
+    r0 = solve_dense(A, np.ones(200, np.int32), b, c, maximize=True, refactor_period=10)
+    r1 = solve_dense(A, np.ones(200, np.int32), b, c, maximize=True, refactor_period=10,
+                     refactor_mode=1)
+    assert r0.stats["gj_refactors"] == 0 and r1.stats["gj_refactors"] == r1.stats["refactors"] > 0
+    np.testing.assert_array_equal(r0.basis, r1.basis)
+    assert abs(r0.objval - r1.objval) <= 1e-11 * abs(r0.objval)
+
+
+def test_general_lps_vs_highs():
+    """Random general-form LPs (phase 1, free/boxed columns, <=/>=/== rows)
+    against SciPy-HiGHS (build container only)."""
+    pytest.importorskip("scipy")
+    from golden.make_golden import highs
+    rng = np.random.default_rng(7)
+    for trial in range(8):
+        m, n = 20 + 5 * trial, 40 + 9 * trial
+        A = rng.uniform(-1, 1, (m, n))
+        x0 = rng.uniform(0, 2, n)
+        dirs = rng.integers(1, 4, m).astype(np.int32)
+        rhs = A @ x0 + np.where(dirs == 1, 1.0, np.where(dirs == 2, -1.0, 0.0))
+        lo = np.where(rng.random(n) < 0.3, -3.0, 0.0)
+        up = np.where(rng.random(n) < 0.5, 5.0, np.inf)
+        obj = rng.uniform(-1, 1, n)
+        mx = bool(trial % 2)
+        r = solve_dense(A, dirs, rhs, obj, lo, up, mx)
+        h = highs(A, dirs, rhs, obj, lo, up, mx)
+        assert r.status == {0: 0, 2: 2, 3: 3}[h.status]
+        if r.status == 0:
+            hv = -h.fun if mx else h.fun
+            assert abs(r.objval - hv) <= 1e-8 * max(1, abs(hv))
