@@ -64,6 +64,7 @@ class ElpStats(ctypes.Structure):
         ("price_seconds", ctypes.c_double),
         ("price_timed_bytes", ctypes.c_double),
         ("price_timed_launches", ctypes.c_int64),
+        ("gj_refactors", ctypes.c_int64),
     ]
 
 

@@ -68,7 +68,6 @@ struct elp_handle {
     int64_t trace_cap = 0;
     elp::Comm comm;  // multi-GPU (world 1 = no-op)
     std::vector<hipEvent_t> ev;  // pricing-kernel timing pairs (profile mode)
-    int64_t stats_gj = 0;        // refactors that needed Gauss-Jordan
 };
 
 extern "C" void elp_default_control(elp_control* c) {
@@ -96,7 +95,7 @@ static void free_dev(elp_handle* h) {
                     d.t,        d.acol, d.aR,   d.alS,   d.alU,  d.zz,    d.zpart, d.vrow,
                     d.vvec,     d.colA, d.rhs,  d.vstat, d.cover, d.rpos, d.Rl,    d.Sl,
                     d.spos,     d.Yl,  d.ypos,  d.perm,  d.pivstep, d.nzlist, d.nzcount,
-                    d.cand,     d.ctl, d.trace, d.MinvT, d.yy, d.cS, d.slo, d.shi, d.rlo, d.rhi};
+                    d.cand,     d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.cS, d.slo, d.shi, d.rlo, d.rhi};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     h->A_owned = nullptr;
@@ -176,6 +175,7 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.xs, mm));
     A(dalloc(&d.y, mm));
     A(dalloc(&d.yy, mm));
+    A(dalloc(&d.blockmin, (size_t)(mm / 64 + mm / 256 + 4)));
     A(dalloc(&d.t, mm));
     A(dalloc(&d.acol, mm));
     A(dalloc(&d.aR, mm));
@@ -416,7 +416,7 @@ static int do_refactor(elp_handle* h, int k) {
             HIPCHK(launch_refactor_ns_update(h->d, k, h->st));
         } else {
             HIPCHK(launch_refactor_gj(h->d, k, h->st));
-            h->stats_gj++;
+            h->stats.gj_refactors++;
         }
     }
     HIPCHK(launch_refactor_primal(h->d, k, h->st));

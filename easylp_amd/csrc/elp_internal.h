@@ -78,6 +78,7 @@ struct Dev {
     double *xr, *xs, *y, *yy, *t, *acol, *aR, *alS, *alU, *zz, *zpart;  // yy: y on Y slots
     double *vrow, *vvec, *colA, *rhs;
     double *cS, *slo, *shi;  // per bump position: cost, bounds of S_p
+    double* blockmin;        // per-workgroup Harris pass-1 minima (k_ftran_zr)
     double *rlo, *rhi;       // per covered row: bounds of the covering unit variable
     int8_t* vstat;
     int32_t *cover, *rpos, *Rl, *Sl, *spos, *Yl, *ypos, *perm, *pivstep, *nzlist, *nzcount;

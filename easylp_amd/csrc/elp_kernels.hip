@@ -106,10 +106,11 @@ DEV double block_min(double v, double* lds) {
     return r;
 }
 template <int NT>
-DEV double block_max(double v, double* lds) {
+DEV double block_max(double v, double* lds, int ltid = -1) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off));
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (ltid < 0) ltid = threadIdx.x;
+    const int w = ltid >> 6, lane = ltid & 63;
     if (lane == 0) lds[w] = v;
     __syncthreads();
     double r = lds[0];
@@ -394,11 +395,20 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d) {
             acc1 = fma(v[u].y, yv, acc1);
         }
     }
-    for (; p < p1; ++p) {
-        const double2 v = *reinterpret_cast<const double2*>(col + (size_t)p * (size_t)d.ldr);
-        const double yv = yy[p];
-        acc0 = fma(v.x, yv, acc0);
-        acc1 = fma(v.y, yv, acc1);
+    if (p < p1) {  // remainder: same order, loads issued together
+        double2 v[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u)
+            v[u] = (p + u < p1) ? *reinterpret_cast<const double2*>(col + (size_t)(p + u) * (size_t)d.ldr)
+                                : make_double2(0.0, 0.0);
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            if (p + u < p1) {
+                const double yv = yy[p + u];
+                acc0 = fma(v[u].x, yv, acc0);
+                acc1 = fma(v[u].y, yv, acc1);
+            }
+        }
     }
     part[w][2 * lane] = acc0;
     part[w][2 * lane + 1] = acc1;
@@ -483,14 +493,15 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles) {
         c->dq = best.d;
         c->sig = best.d < 0.0 ? 1.0 : -1.0;
     }
+    // a_R = entering column on the bump rows (the full column is read in
+    // place by k_ftran_zr: A[:, q] for a structural, e_{q-n} for a slack)
     if (q < d.n) {
         const double* col = d.A + (size_t)q * (size_t)d.m;
-        for (int i = threadIdx.x; i < d.m; i += 1024) d.acol[i] = col[i];
+        for (int p = threadIdx.x; p < k; p += 1024) d.aR[p] = col[d.Rl[p]];
     } else {
-        for (int i = threadIdx.x; i < d.m; i += 1024) d.acol[i] = (i == q - d.n) ? 1.0 : 0.0;
+        const int i0 = q - d.n;
+        for (int p = threadIdx.x; p < k; p += 1024) d.aR[p] = d.Rl[p] == i0 ? 1.0 : 0.0;
     }
-    __syncthreads();
-    for (int p = threadIdx.x; p < k; p += 1024) d.aR[p] = d.acol[d.Rl[p]];
 }
 
 // ============================================================== FTRAN
@@ -547,6 +558,85 @@ __global__ void k_xr_from_z(Dev d) {
     d.xr[i] = unit_sign(d, u, i) * (d.rhs[i] - z);
 }
 
+// FTRAN on covered rows fused with Harris pass 1.
+// Row tiles: 64 rows x 4 waves; wave w forms the z partials of chunks
+// w, w+4, ... (ZCHUNK bump positions each, fma chain in position order) in
+// LDS; wave 0 adds them in chunk order (the oracle's zchunk order), forms
+// alpha_u = sigma_u (a_iq - z_i), stores it and reduces its Harris pass-1
+// ratio.  Bump tiles (after the row tiles) reduce pass 1 over alpha_S.
+// One minimum per workgroup goes to blockmin[].
+DEV double harris1(double g, double x, double l, double u, double ptol, double pivtol, int bland) {
+    if (g > pivtol && l > -HUGE_VAL) return bland ? (x - l) / g : (x - l + ptol) / g;
+    if (g < -pivtol && u < HUGE_VAL) return bland ? (u - x) / (-g) : (u - x + ptol) / (-g);
+    return HUGE_VAL;
+}
+
+__global__ void __launch_bounds__(256) k_ftran_zr(Dev d, int nrt) {
+    extern __shared__ __attribute__((aligned(16))) double zp[];  // [nch][64]
+    __shared__ double red[4];
+    const DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    const int m = d.m, n = d.n, k = c->k, q = c->q, bland = c->bland;
+    const double sig = c->sig, ptol = c->tol_primal, pivtol = c->tol_pivot;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    double tmin = HUGE_VAL;
+    if ((int)blockIdx.x < nrt) {
+        const int i = blockIdx.x * 64 + lane;
+        const int nch = (k + ZCHUNK - 1) / ZCHUNK;
+        const size_t mm = (size_t)m;
+        for (int ch = w; ch < nch; ch += 4) {
+            const int c0 = ch * ZCHUNK, c1 = min(k, c0 + ZCHUNK);
+            double acc = 0.0;
+            if (i < m) {
+                const double* col = d.AS + (size_t)c0 * mm + i;
+                int p = c0;
+                for (; p + 16 <= c1; p += 16) {
+                    double a[16];
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) a[u] = col[(size_t)(p - c0 + u) * mm];
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) acc = fma(a[u], d.alS[p + u], acc);
+                }
+                if (p < c1) {
+                    double a[16];
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) a[u] = (p + u < c1) ? col[(size_t)(p - c0 + u) * mm] : 0.0;
+#pragma unroll
+                    for (int u = 0; u < 16; ++u)
+                        if (p + u < c1) acc = fma(a[u], d.alS[p + u], acc);
+                }
+            }
+            zp[ch * 64 + lane] = acc;
+        }
+        __syncthreads();
+        if (w == 0) {
+            if (i < m) {
+                const int u = d.cover[i];
+                if (u >= 0) {
+                    double z = 0.0;
+                    for (int ch = 0; ch < nch; ++ch) z = z + zp[ch * 64 + lane];
+                    const double aiq = q < n ? d.A[(size_t)q * mm + i] : (i == q - n ? 1.0 : 0.0);
+                    const double alU = unit_sign(d, u, i) * (aiq - z);
+                    d.alU[i] = alU;
+                    tmin = harris1(sig * alU, d.xr[i], d.rlo[i], d.rhi[i], ptol, pivtol, bland);
+                }
+            }
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) tmin = fmin(tmin, __shfl_xor(tmin, off));
+            if (lane == 0) d.blockmin[blockIdx.x] = tmin;
+        }
+    } else {
+        const int p = (blockIdx.x - nrt) * 256 + threadIdx.x;
+        if (p < k) tmin = harris1(sig * d.alS[p], d.xs[p], d.slo[p], d.shi[p], ptol, pivtol, bland);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) tmin = fmin(tmin, __shfl_xor(tmin, off));
+        if (lane == 0) red[w] = tmin;
+        __syncthreads();
+        if (threadIdx.x == 0) d.blockmin[blockIdx.x] = fmin(fmin(red[0], red[1]), fmin(red[2], red[3]));
+    }
+}
+
 // ============================================================== ratio test
 struct Leave {
     double ag, r, g, l, u;
@@ -574,21 +664,19 @@ DEV Leave shfl_leave(const Leave& x, int off) {
 enum { SC_LBQ, SC_UBQ, SC_XVQ, SC_CQ, SC_SLL, SC_CSL, SC_SLOL, SC_SHIL, SC_N };
 enum { SI_VSQ, SI_RPOS0, SI_YPOS0, SI_YLAST, SI_SLLAST, SI_RLLAST, SI_N };
 
-DEV void load_entry(const Dev& d, int e, int m, int k, int nch, double sig, int& var, double& g,
-                    double& x, double& lo, double& hi) {
+DEV void load_entry(const Dev& d, int e, int m, int k, double sig, int& var, double& g, double& x,
+                    double& lo, double& hi) {
     var = -1;
     g = x = lo = hi = 0.0;
     if (e < m) {
         const int u = d.cover[e];
+        const double a = d.alU[e], xv = d.xr[e], l = d.rlo[e], h = d.rhi[e];
         if (u >= 0) {
-            double z = 0.0;
-            for (int ch = 0; ch < nch; ++ch) z = z + d.zpart[(size_t)ch * m + e];
-            const double alU = unit_sign(d, u, e) * (d.acol[e] - z);
             var = u;
-            g = sig * alU;
-            x = d.xr[e];
-            lo = d.rlo[e];
-            hi = d.rhi[e];
+            g = sig * a;
+            x = xv;
+            lo = l;
+            hi = h;
         }
     } else if (e < m + k) {
         const int p = e - m;
@@ -600,12 +688,12 @@ DEV void load_entry(const Dev& d, int e, int m, int k, int nch, double sig, int&
     }
 }
 
-// Harris two-pass ratio test + primal update + pivot plan (one workgroup).
-// Every thread owns NR basic entries e = tid + 1024 t (covered rows first,
-// then bump positions), kept in registers across both passes; NR = 0 is the
-// streaming variant for very large m (entries re-read from memory per pass).
+// Harris pass 2 + primal update + pivot plan (one workgroup); pass 1 came
+// from k_ftran_zr's per-workgroup minima.  Every thread owns NR basic entries
+// e = tid + 1024 t (covered rows first, then bump positions) in registers;
+// NR = 0 is the streaming variant for very large m.
 template <int NR>
-__global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
+__global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase, int nblk) {
     __shared__ double dred[16];
     __shared__ Leave lred[16];
     __shared__ double sc[SC_N];
@@ -640,8 +728,6 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
             case SC_N + SI_RLLAST: si[SI_RLLAST] = last >= 0 ? d.Rl[last] : -1; break;
         }
     }
-    // ---- load entries; alpha on covered rows from the z chunks (in order)
-    const int nch = (k + ZCHUNK - 1) / ZCHUNK;
     constexpr int NREG = NR > 0 ? NR : 1;
     double g[NREG], x[NREG], lo[NREG], hi[NREG];
     int var[NREG];
@@ -655,26 +741,17 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase) {
         v_ = var[(t) % NREG]; g_ = g[(t) % NREG]; x_ = x[(t) % NREG];                    \
         lo_ = lo[(t) % NREG]; hi_ = hi[(t) % NREG];                                      \
     } else {                                                                             \
-        load_entry(d, e_, m, k, nch, sig, v_, g_, x_, lo_, hi_);                         \
+        load_entry(d, e_, m, k, sig, v_, g_, x_, lo_, hi_);                              \
     }
     if (NR > 0) {
 #pragma unroll
         for (int t = 0; t < NREG; ++t)
-            load_entry(d, tid + 1024 * t, m, k, nch, sig, var[t], g[t], x[t], lo[t], hi[t]);
+            load_entry(d, tid + 1024 * t, m, k, sig, var[t], g[t], x[t], lo[t], hi[t]);
     }
-    // ---- Harris pass 1
-    const double ptol = c->tol_primal, pivtol = c->tol_pivot, INF = HUGE_VAL;
+    // ---- Harris pass 1 result: min over the workgroup minima
+    const double pivtol = c->tol_pivot, INF = HUGE_VAL;
     double tmax = INF;
-#pragma unroll
-    for (int t = 0; t < npass; ++t) {
-        ELP_ENTRY(t)
-        if (v_ < 0) continue;
-        double r;
-        if (g_ > pivtol && lo_ > -INF) r = bland ? (x_ - lo_) / g_ : (x_ - lo_ + ptol) / g_;
-        else if (g_ < -pivtol && hi_ < INF) r = bland ? (hi_ - x_) / (-g_) : (hi_ - x_ + ptol) / (-g_);
-        else continue;
-        if (r < tmax) tmax = r;
-    }
+    for (int b = tid; b < nblk; b += 1024) tmax = fmin(tmax, d.blockmin[b]);
     const double theta_max = block_min<1024>(tmax, dred);
     // ---- pass 2
     Leave best;
@@ -1151,7 +1228,7 @@ __global__ void __launch_bounds__(1024) k_ns_resid(Dev d, int k) {
         e = (i == j ? 1.0 : 0.0) - acc;
         d.W0[(size_t)i * k + j] = e;
     }
-    const double am = block_max<1024>(fabs(e), red);
+    const double am = block_max<1024>(fabs(e), red, ty * 32 + tx);
     if (tx == 0 && ty == 0) atomicMax(&d.ctl->ns_emax_bits, (unsigned long long)__double_as_longlong(am));
 }
 
@@ -1270,20 +1347,27 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
     k_price<<<ntiles, PRICE_THREADS, 0, st>>>(d);
     if (ev1) (void)hipEventRecord(ev1, st);
     k_select<<<1, 1024, 0, st>>>(d, (int)ntiles);
-    if (k_ub > 0) {
-        k_ftran_bump<<<cdiv(k_ub, 4), 256, 0, st>>>(d, d.aR, d.alS, 1);
-        if (m > 0) {
-            dim3 g(cdiv(m, 256), cdiv(k_ub, ZCHUNK));
-            k_ftran_z<<<g, 256, 0, st>>>(d, d.alS, 1);
+    if (k_ub > 0) k_ftran_bump<<<cdiv(k_ub, 4), 256, 0, st>>>(d, d.aR, d.alS, 1);
+    const int nrt = (int)cdiv(m > 0 ? m : 1, 64);
+    const int nbt = (int)cdiv(k_ub, 256);
+    {
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)k_ftran_zr,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr = true;
         }
+        const size_t lds = (size_t)cdiv(k_ub, ZCHUNK) * 64 * sizeof(double);
+        k_ftran_zr<<<nrt + nbt, 256, lds, st>>>(d, nrt);
     }
     {
         const int ent = m + k_ub;  // basic entries: covered rows + bump positions
-        if (ent <= 1024) k_ratio<1><<<1, 1024, 0, st>>>(d, phase);
-        else if (ent <= 2048) k_ratio<2><<<1, 1024, 0, st>>>(d, phase);
-        else if (ent <= 4096) k_ratio<4><<<1, 1024, 0, st>>>(d, phase);
-        else if (ent <= 8192) k_ratio<8><<<1, 1024, 0, st>>>(d, phase);
-        else k_ratio<0><<<1, 1024, 0, st>>>(d, phase);
+        const int nblk = nrt + nbt;
+        if (ent <= 1024) k_ratio<1><<<1, 1024, 0, st>>>(d, phase, nblk);
+        else if (ent <= 2048) k_ratio<2><<<1, 1024, 0, st>>>(d, phase, nblk);
+        else if (ent <= 4096) k_ratio<4><<<1, 1024, 0, st>>>(d, phase, nblk);
+        else if (ent <= 8192) k_ratio<8><<<1, 1024, 0, st>>>(d, phase, nblk);
+        else k_ratio<0><<<1, 1024, 0, st>>>(d, phase, nblk);
     }
     if (k_ub > 0) k_rowminv<<<cdiv(k_ub, 4), 256, 0, st>>>(d);
     {

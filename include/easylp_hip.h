@@ -89,6 +89,7 @@ typedef struct elp_stats {
     double price_seconds;      /* sum of timed pricing-kernel durations        */
     double price_timed_bytes;  /* algorithmic bytes of those launches          */
     int64_t price_timed_launches;
+    int64_t gj_refactors;      /* refactors that needed a Gauss-Jordan rebuild */
 } elp_stats;
 
 #define ELP_PROFILE_PRICE 2   /* elp_control.verbose bit */

@@ -42,7 +42,7 @@ def test_control_struct_size_matches_header():
     # 5 doubles + int64 + 5 int32 + 7 reserved int32 = 96 bytes
     from easylp_amd._lib import ElpControl, ElpStats
     assert ctypes.sizeof(ElpControl) == 96  # 5 doubles, int64, 6 int32 fields, 6 reserved
-    assert ctypes.sizeof(ElpStats) == 8 * 8 + 4 * 8 + 4 + 4 + 16 + 8 + 8 + 8
+    assert ctypes.sizeof(ElpStats) == 8 * 8 + 4 * 8 + 4 + 4 + 16 + 8 + 8 + 8 + 8
 
 
 def test_usage_errors_without_gpu():
