@@ -1351,13 +1351,18 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
     const int nrt = (int)cdiv(m > 0 ? m : 1, 64);
     const int nbt = (int)cdiv(k_ub, 256);
     {
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void*)k_ftran_zr,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            attr = true;
-        }
+        // z partials: 512 B per chunk of 64 bump positions (k <= 16384 in 128 KiB)
         const size_t lds = (size_t)cdiv(k_ub, ZCHUNK) * 64 * sizeof(double);
+        if (lds > 64 * 1024) {
+            static bool attr = false;
+            if (!attr) {
+                const hipError_t e = hipFuncSetAttribute(
+                    (const void*)k_ftran_zr, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+                if (e != hipSuccess) return e;
+                attr = true;
+            }
+            if (lds > 128 * 1024) return hipErrorInvalidValue;
+        }
         k_ftran_zr<<<nrt + nbt, 256, lds, st>>>(d, nrt);
     }
     {
