@@ -95,7 +95,7 @@ static void free_dev(elp_handle* h) {
                     d.t,        d.acol, d.aR,   d.alS,   d.alU,  d.zz,    d.zpart, d.vrow,
                     d.vvec,     d.colA, d.rhs,  d.vstat, d.cover, d.rpos, d.Rl,    d.Sl,
                     d.spos,     d.Yl,  d.ypos,  d.perm,  d.pivstep, d.nzlist, d.nzcount,
-                    d.cand,     d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.cS, d.slo, d.shi, d.rlo, d.rhi};
+                    d.cand,     d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand, d.cS, d.slo, d.shi, d.rlo, d.rhi};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     h->A_owned = nullptr;
@@ -176,6 +176,7 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.y, mm));
     A(dalloc(&d.yy, mm));
     A(dalloc(&d.blockmin, (size_t)(mm / 64 + mm / 256 + 4)));
+    A(dalloc(&d.rcand, (size_t)(2 * mm + 2)));
     A(dalloc(&d.t, mm));
     A(dalloc(&d.acol, mm));
     A(dalloc(&d.aR, mm));

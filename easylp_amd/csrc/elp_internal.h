@@ -33,7 +33,9 @@ constexpr int TILE_COLS = 128;  // columns per pricing workgroup (2 per lane)
 struct Plan {
     int32_t action, pcase, k_old, p;
     int32_t a, b, last, row;      // row: B leaving-cover row / D leaving row i1
-    int32_t q, pad0;
+    int32_t q, i0;                // i0: row of an entering slack (-1 otherwise)
+    int32_t lrow, lpos;           // leaving entry: covered row / bump position
+    double step, sig;             // x_B -= step * sig * alpha
     int32_t y_rm_slot, y_rm_last; // -1: no removal
     int32_t y_ap_slot, y_ap_row;  // -1: no append
     double piv;                   // A: alS[p]; B: delta; C: Minv[b][a]
@@ -56,6 +58,14 @@ struct DevCtl {
     double price_bytes;    // algorithmic bytes of every pricing pass that ran
     int64_t price_passes;
     unsigned long long ns_emax_bits;  // max|I - M Minv| of the last refactor (bits of a double >= 0)
+    int32_t ncand, pad2;              // Harris pass-2 candidate count (k_ftran_zr)
+};
+
+// Harris pass-2 candidate (a superset of the global candidates: exact ratio
+// <= its workgroup's pass-1 minimum)
+struct RCand {
+    double g, r, l, u;
+    int32_t var, e;
 };
 
 struct Cand {
@@ -79,6 +89,7 @@ struct Dev {
     double *vrow, *vvec, *colA, *rhs;
     double *cS, *slo, *shi;  // per bump position: cost, bounds of S_p
     double* blockmin;        // per-workgroup Harris pass-1 minima (k_ftran_zr)
+    RCand* rcand;            // pass-2 candidates (capacity 2m)
     double *rlo, *rhi;       // per covered row: bounds of the covering unit variable
     int8_t* vstat;
     int32_t *cover, *rpos, *Rl, *Sl, *spos, *Yl, *ypos, *perm, *pivstep, *nzlist, *nzcount;

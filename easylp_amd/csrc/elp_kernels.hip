@@ -382,7 +382,7 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d) {
     const double* __restrict__ yy = d.yy;
     double acc0 = 0.0, acc1 = 0.0;
     int p = p0;
-    constexpr int UNR = 16;  // rows in flight per wave: 16 KiB
+    constexpr int UNR = 32;  // rows in flight per wave: 32 KiB
     for (; p + UNR <= p1; p += UNR) {
         double2 v[UNR];
 #pragma unroll
@@ -486,6 +486,7 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles) {
     }
     const int q = (int)best.j;
     if (threadIdx.x == 0) {
+        c->ncand = 0;
         // algorithmic bytes of this pricing pass: AR sweep + c + status + y_Y + Yl
         c->price_bytes += 8.0 * (double)ny * (double)d.n + 9.0 * (double)d.n + 12.0 * (double)ny;
         c->price_passes++;
@@ -571,6 +572,30 @@ DEV double harris1(double g, double x, double l, double u, double ptol, double p
     return HUGE_VAL;
 }
 
+// exact (pass-2) ratio of an entry; +inf if it cannot limit the step
+DEV double harris2(double g, double x, double l, double u, double pivtol) {
+    if (g > pivtol && l > -HUGE_VAL) return (x - l) / g;
+    if (g < -pivtol && u < HUGE_VAL) return (u - x) / (-g);
+    return HUGE_VAL;
+}
+// keep entry e as a pass-2 candidate if its exact ratio <= the workgroup's
+// pass-1 minimum (the global minimum can only be smaller)
+DEV void emit_cand(const Dev& d, int var, int e, double g, double x, double l, double u, double bmin,
+                   double pivtol) {
+    if (var < 0) return;
+    const double r = harris2(g, x, l, u, pivtol);
+    if (!(r <= bmin)) return;
+    const int slot = atomicAdd(&d.ctl->ncand, 1);
+    RCand cd;
+    cd.g = g;
+    cd.r = r;
+    cd.l = l;
+    cd.u = u;
+    cd.var = var;
+    cd.e = e;
+    d.rcand[slot] = cd;
+}
+
 __global__ void __launch_bounds__(256) k_ftran_zr(Dev d, int nrt) {
     extern __shared__ __attribute__((aligned(16))) double zp[];  // [nch][64]
     __shared__ double red[4];
@@ -581,6 +606,8 @@ __global__ void __launch_bounds__(256) k_ftran_zr(Dev d, int nrt) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double tmin = HUGE_VAL;
+    double ge = 0.0, xe = 0.0, le = 0.0, he = 0.0;
+    int ve = -1;
     if ((int)blockIdx.x < nrt) {
         const int i = blockIdx.x * 64 + lane;
         const int nch = (k + ZCHUNK - 1) / ZCHUNK;
@@ -619,21 +646,38 @@ __global__ void __launch_bounds__(256) k_ftran_zr(Dev d, int nrt) {
                     const double aiq = q < n ? d.A[(size_t)q * mm + i] : (i == q - n ? 1.0 : 0.0);
                     const double alU = unit_sign(d, u, i) * (aiq - z);
                     d.alU[i] = alU;
-                    tmin = harris1(sig * alU, d.xr[i], d.rlo[i], d.rhi[i], ptol, pivtol, bland);
+                    ge = sig * alU;
+                    xe = d.xr[i];
+                    le = d.rlo[i];
+                    he = d.rhi[i];
+                    ve = u;
+                    tmin = harris1(ge, xe, le, he, ptol, pivtol, bland);
                 }
             }
+            double bmin = tmin;
 #pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) tmin = fmin(tmin, __shfl_xor(tmin, off));
-            if (lane == 0) d.blockmin[blockIdx.x] = tmin;
+            for (int off = 32; off >= 1; off >>= 1) bmin = fmin(bmin, __shfl_xor(bmin, off));
+            if (lane == 0) d.blockmin[blockIdx.x] = bmin;
+            emit_cand(d, ve, i, ge, xe, le, he, bmin, pivtol);
         }
     } else {
         const int p = (blockIdx.x - nrt) * 256 + threadIdx.x;
-        if (p < k) tmin = harris1(sig * d.alS[p], d.xs[p], d.slo[p], d.shi[p], ptol, pivtol, bland);
+        if (p < k) {
+            ge = sig * d.alS[p];
+            xe = d.xs[p];
+            le = d.slo[p];
+            he = d.shi[p];
+            ve = d.Sl[p];
+            tmin = harris1(ge, xe, le, he, ptol, pivtol, bland);
+        }
+        double bmin = tmin;
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) tmin = fmin(tmin, __shfl_xor(tmin, off));
-        if (lane == 0) red[w] = tmin;
+        for (int off = 32; off >= 1; off >>= 1) bmin = fmin(bmin, __shfl_xor(bmin, off));
+        if (lane == 0) red[w] = bmin;
         __syncthreads();
-        if (threadIdx.x == 0) d.blockmin[blockIdx.x] = fmin(fmin(red[0], red[1]), fmin(red[2], red[3]));
+        bmin = fmin(fmin(red[0], red[1]), fmin(red[2], red[3]));
+        if (threadIdx.x == 0) d.blockmin[blockIdx.x] = bmin;
+        emit_cand(d, ve, m + p, ge, xe, le, he, bmin, pivtol);
     }
 }
 
@@ -664,46 +708,19 @@ DEV Leave shfl_leave(const Leave& x, int off) {
 enum { SC_LBQ, SC_UBQ, SC_XVQ, SC_CQ, SC_SLL, SC_CSL, SC_SLOL, SC_SHIL, SC_N };
 enum { SI_VSQ, SI_RPOS0, SI_YPOS0, SI_YLAST, SI_SLLAST, SI_RLLAST, SI_N };
 
-DEV void load_entry(const Dev& d, int e, int m, int k, double sig, int& var, double& g, double& x,
-                    double& lo, double& hi) {
-    var = -1;
-    g = x = lo = hi = 0.0;
-    if (e < m) {
-        const int u = d.cover[e];
-        const double a = d.alU[e], xv = d.xr[e], l = d.rlo[e], h = d.rhi[e];
-        if (u >= 0) {
-            var = u;
-            g = sig * a;
-            x = xv;
-            lo = l;
-            hi = h;
-        }
-    } else if (e < m + k) {
-        const int p = e - m;
-        var = d.Sl[p];
-        g = sig * d.alS[p];
-        x = d.xs[p];
-        lo = d.slo[p];
-        hi = d.shi[p];
-    }
-}
-
-// Harris pass 2 + primal update + pivot plan (one workgroup); pass 1 came
-// from k_ftran_zr's per-workgroup minima.  Every thread owns NR basic entries
-// e = tid + 1024 t (covered rows first, then bump positions) in registers;
-// NR = 0 is the streaming variant for very large m.
-template <int NR>
-__global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase, int nblk) {
-    __shared__ double dred[16];
-    __shared__ Leave lred[16];
+// Harris pass 2 + decision + pivot plan (one workgroup).  Pass 1 came from
+// k_ftran_zr's per-workgroup minima, the candidates from its emitted list; the
+// primal update x_B -= step * alpha runs in k_update.
+__global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk) {
+    __shared__ double dred[4];
+    __shared__ Leave lred[4];
     __shared__ double sc[SC_N];
     __shared__ int si[SI_N];
-    __shared__ double s_xs_last;
     __shared__ int s_action;
     __shared__ Plan s_plan;
     DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
-    const int m = d.m, n = d.n, k = c->k, q = c->q, ny = c->ny;
+    const int m = d.m, n = d.n, k = c->k, q = c->q, ny = c->ny, ncand = c->ncand;
     const double sig = c->sig;
     const int bland = c->bland;
     const int tid = threadIdx.x;
@@ -728,53 +745,28 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase, int nblk) {
             case SC_N + SI_RLLAST: si[SI_RLLAST] = last >= 0 ? d.Rl[last] : -1; break;
         }
     }
-    constexpr int NREG = NR > 0 ? NR : 1;
-    double g[NREG], x[NREG], lo[NREG], hi[NREG];
-    int var[NREG];
-    const int npass = NR > 0 ? NR : (m + k + 1023) / 1024;
-    // entry t of this thread: registers (NR > 0) or memory (NR == 0)
-#define ELP_ENTRY(t)                                                                     \
-    const int e_ = tid + 1024 * (t);                                                     \
-    int v_;                                                                              \
-    double g_, x_, lo_, hi_;                                                             \
-    if (NR > 0) {                                                                        \
-        v_ = var[(t) % NREG]; g_ = g[(t) % NREG]; x_ = x[(t) % NREG];                    \
-        lo_ = lo[(t) % NREG]; hi_ = hi[(t) % NREG];                                      \
-    } else {                                                                             \
-        load_entry(d, e_, m, k, sig, v_, g_, x_, lo_, hi_);                              \
-    }
-    if (NR > 0) {
-#pragma unroll
-        for (int t = 0; t < NREG; ++t)
-            load_entry(d, tid + 1024 * t, m, k, sig, var[t], g[t], x[t], lo[t], hi[t]);
-    }
-    // ---- Harris pass 1 result: min over the workgroup minima
+    // ---- pass 1 result: min over the workgroup minima
     const double pivtol = c->tol_pivot, INF = HUGE_VAL;
+    (void)pivtol;
     double tmax = INF;
-    for (int b = tid; b < nblk; b += 1024) tmax = fmin(tmax, d.blockmin[b]);
-    const double theta_max = block_min<1024>(tmax, dred);
-    // ---- pass 2
+    for (int b = tid; b < nblk; b += 256) tmax = fmin(tmax, d.blockmin[b]);
+    const double theta_max = block_min<256>(tmax, dred);
+    // ---- pass 2 over the candidates
     Leave best;
     best.var = -1;
     best.ag = best.r = best.g = best.l = best.u = 0.0;
     best.e = -1;
-#pragma unroll
-    for (int t = 0; t < npass; ++t) {
-        ELP_ENTRY(t)
-        if (v_ < 0) continue;
-        double r;
-        if (g_ > pivtol && lo_ > -INF) r = (x_ - lo_) / g_;
-        else if (g_ < -pivtol && hi_ < INF) r = (hi_ - x_) / (-g_);
-        else continue;
-        if (!(r <= theta_max)) continue;
+    for (int t = tid; t < ncand; t += 256) {
+        const RCand cd = d.rcand[t];
+        if (!(cd.r <= theta_max)) continue;
         Leave o;
-        o.var = v_;
-        o.ag = fabs(g_);
-        o.r = r;
-        o.g = g_;
-        o.l = lo_;
-        o.u = hi_;
-        o.e = e_;
+        o.var = cd.var;
+        o.ag = fabs(cd.g);
+        o.r = cd.r;
+        o.g = cd.g;
+        o.l = cd.l;
+        o.u = cd.u;
+        o.e = cd.e;
         if (leave_better(o, best, bland)) best = o;
     }
 #pragma unroll
@@ -785,7 +777,7 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase, int nblk) {
     if ((tid & 63) == 0) lred[tid >> 6] = best;
     __syncthreads();  // also publishes the prefetched scalars
     best = lred[0];
-    for (int i = 1; i < 16; ++i)
+    for (int i = 1; i < 4; ++i)
         if (leave_better(lred[i], best, bland)) best = lred[i];
     // ---- decision (uniform across the block)
     const double lbq = sc[SC_LBQ], ubq = sc[SC_UBQ];
@@ -821,20 +813,6 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase, int nblk) {
         if (tid == 0) c->plan.action = ACT_NONE;
         return;
     }
-    // ---- primal update x_B -= step * g (from registers)
-#pragma unroll
-    for (int t = 0; t < npass; ++t) {
-        ELP_ENTRY(t)
-        if (v_ < 0) continue;
-        const double xn = fma(-step, g_, x_);
-        if (e_ < m) d.xr[e_] = xn;
-        else {
-            d.xs[e_ - m] = xn;
-            if (e_ - m == last) s_xs_last = xn;
-        }
-    }
-#undef ELP_ENTRY
-    __syncthreads();
     if (action == ACT_FLIP) {
         if (tid == 0) {
             if (si[SI_VSQ] == VS_LOWER) {
@@ -847,7 +825,18 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase, int nblk) {
             c->flips++;
             c->ndegen = 0;
             c->bland = 0;
-            c->plan.action = ACT_FLIP;
+            Plan P;
+            P.action = ACT_FLIP;
+            P.pcase = PC_NONE;
+            P.k_old = k;
+            P.q = q;
+            P.step = step;
+            P.sig = sig;
+            P.p = P.a = P.b = P.last = P.row = P.i0 = P.lrow = P.lpos = -1;
+            P.y_rm_slot = P.y_rm_last = P.y_ap_slot = P.y_ap_row = -1;
+            P.piv = 0.0;
+            P.xq = 0.0;
+            c->plan = P;
         }
         return;
     }
@@ -882,7 +871,11 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase, int nblk) {
         P.k_old = k;
         P.q = q;
         P.xq = xq;
-        P.p = P.a = P.b = P.last = P.row = -1;
+        P.p = P.a = P.b = P.last = P.row = P.i0 = -1;
+        P.lrow = lrow;
+        P.lpos = lpos;
+        P.step = step;
+        P.sig = sig;
         P.y_rm_slot = P.y_rm_last = P.y_ap_slot = P.y_ap_row = -1;
         P.piv = 0.0;
         int nny = ny;
@@ -895,7 +888,6 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase, int nblk) {
                 d.spos[lv] = -1;
                 d.Sl[lpos] = q;
                 d.spos[q] = lpos;
-                d.xs[lpos] = xq;
                 d.cS[lpos] = cq;
                 d.slo[lpos] = lbq;
                 d.shi[lpos] = ubq;
@@ -910,7 +902,6 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase, int nblk) {
                 d.rpos[i] = k;
                 d.Sl[k] = q;
                 d.spos[q] = k;
-                d.xs[k] = xq;
                 d.cS[k] = cq;
                 d.slo[k] = lbq;
                 d.shi[k] = ubq;
@@ -941,7 +932,6 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase, int nblk) {
                     const int sl = si[SI_SLLAST];
                     d.Sl[b] = sl;
                     d.spos[sl] = b;
-                    d.xs[b] = s_xs_last;
                     d.cS[b] = sc[SC_CSL];
                     d.slo[b] = sc[SC_SLOL];
                     d.shi[b] = sc[SC_SHIL];
@@ -965,8 +955,8 @@ __global__ void __launch_bounds__(1024) k_ratio(Dev d, int phase, int nblk) {
                 d.cover[i1] = -1;
             }
             // the entering slack covers row i0
+            P.i0 = i0;
             d.cover[i0] = q;
-            d.xr[i0] = xq;
             d.rlo[i0] = lbq;
             d.rhi[i0] = ubq;
             // row i0 leaves Y (its slack is basic now) ...
@@ -1060,16 +1050,17 @@ DEV double minv_new(const Dev& d, const Plan& P, int i, int j, const OldM& old) 
     }
 }
 
-// Minv and MinvT update (blocks [0, nb_minv)) + AS / AR copies (the rest)
+// Minv and MinvT update (blocks [0, nb_minv)) + primal update x_B -= step*alpha
+// and AS / AR copies (the rest).  Flips only update x_B.
 __global__ void __launch_bounds__(256) k_update(Dev d, int nb_minv) {
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
     const Plan P = c->plan;
-    if (P.action != ACT_PIVOT) return;
+    if (P.action == ACT_NONE) return;
     const int k = P.k_old;
     const size_t ldm = (size_t)d.ldm;
     if ((int)blockIdx.x < nb_minv) {
-        if (P.pcase == PC_E) return;
+        if (P.action != ACT_PIVOT || P.pcase == PC_E) return;
         const int kk = P.pcase == PC_B ? k + 1 : P.pcase == PC_C ? k - 1 : k;
         const int64_t nel = (int64_t)kk * kk;
         const int64_t e0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1087,10 +1078,27 @@ __global__ void __launch_bounds__(256) k_update(Dev d, int nb_minv) {
         }
         return;
     }
-    // ---- copies: thread t covers row t of AS and column t of AR
+    // ---- primal update (oracle order: x -= step * (sig * alpha), then the
+    //      entering value / compaction of the pivot case)
     const int64_t t0 = (int64_t)(blockIdx.x - nb_minv) * blockDim.x + threadIdx.x;
     const int64_t tstride = (int64_t)(gridDim.x - nb_minv) * blockDim.x;
     const size_t m = (size_t)d.m;
+    const double step = P.step, sg = P.sig;
+    for (int64_t t = t0; t < d.m; t += tstride) {
+        if (t == P.i0) d.xr[t] = P.xq;       // entering slack's row (C, D, E)
+        else if (t == P.lrow) continue;      // leaving unit var's row (B, D)
+        else if (d.cover[t] >= 0) d.xr[t] = fma(-step, sg * d.alU[t], d.xr[t]);
+    }
+    for (int64_t p = t0; p < k; p += tstride) {
+        if (P.pcase == PC_A && p == P.lpos) d.xs[p] = P.xq;
+        else if (P.pcase == PC_C && p == P.last) continue;  // removed position
+        else if (P.pcase == PC_C && p == P.b)
+            d.xs[p] = fma(-step, sg * d.alS[P.last], d.xs[P.last]);
+        else d.xs[p] = fma(-step, sg * d.alS[p], d.xs[p]);
+    }
+    if (P.action != ACT_PIVOT) return;
+    if (P.pcase == PC_B && t0 == 0) d.xs[k] = P.xq;
+    // ---- copies: thread t covers row t of AS and column t of AR
     for (int64_t t = t0; t < d.m; t += tstride) {
         if (P.pcase == PC_A || P.pcase == PC_B) {
             const int pos = P.pcase == PC_A ? P.p : k;
@@ -1365,15 +1373,7 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
         }
         k_ftran_zr<<<nrt + nbt, 256, lds, st>>>(d, nrt);
     }
-    {
-        const int ent = m + k_ub;  // basic entries: covered rows + bump positions
-        const int nblk = nrt + nbt;
-        if (ent <= 1024) k_ratio<1><<<1, 1024, 0, st>>>(d, phase, nblk);
-        else if (ent <= 2048) k_ratio<2><<<1, 1024, 0, st>>>(d, phase, nblk);
-        else if (ent <= 4096) k_ratio<4><<<1, 1024, 0, st>>>(d, phase, nblk);
-        else if (ent <= 8192) k_ratio<8><<<1, 1024, 0, st>>>(d, phase, nblk);
-        else k_ratio<0><<<1, 1024, 0, st>>>(d, phase, nblk);
-    }
+    k_ratio<<<1, 256, 0, st>>>(d, phase, nrt + nbt);
     if (k_ub > 0) k_rowminv<<<cdiv(k_ub, 4), 256, 0, st>>>(d);
     {
         const int64_t kk = 2 * (int64_t)(k_ub + 1) * (k_ub + 1);
