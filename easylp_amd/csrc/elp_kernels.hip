@@ -584,7 +584,7 @@ DEV void emit_cand(const Dev& d, int var, int e, double g, double x, double l, d
                    double pivtol) {
     if (var < 0) return;
     const double r = harris2(g, x, l, u, pivtol);
-    if (!(r <= bmin)) return;
+    if (!(r <= bmin) || r == HUGE_VAL) return;
     const int slot = atomicAdd(&d.ctl->ncand, 1);
     RCand cd;
     cd.g = g;

@@ -151,3 +151,24 @@ def test_mixed_general_lp_vs_oracle(gpu):
         o = orc(A, dirs, rhs, obj, lo, up, bool(trial % 2), trace_cap=100000)
         _cmp(g, o)
         np.testing.assert_array_equal(g.trace, o.trace)
+
+
+def _equality_lp(m, n, seed):
+    rng = np.random.default_rng(seed)
+    A = rng.uniform(-1, 1, (m, n))
+    x0 = rng.uniform(0, 4, n)
+    rhs = A @ x0
+    obj = rng.uniform(-1, 1, n)
+    return A, np.full(m, 3, np.int32), rhs, obj, np.zeros(n), np.full(n, 5.0)
+
+
+def test_large_bump_vs_oracle(gpu):
+    """All-equality LP: the bump grows past 256 (two bump tiles, |Y| >= 256
+    pricing chunks of 32+ rows) -- the regime of the 5000x50000 benchmark."""
+    from oracle import solve_dense as orc
+    A, dirs, rhs, obj, lo, up = _equality_lp(420, 700, 3)
+    g = gpu.solve_dense(A, dirs, rhs, obj, lo, up, False, trace=200000)
+    o = orc(A, dirs, rhs, obj, lo, up, False, trace_cap=200000)
+    assert o.stats["bump_dim"] > 256, o.stats
+    _cmp(g, o)
+    np.testing.assert_array_equal(g.trace, o.trace)
