@@ -990,17 +990,17 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk) {
     const Plan P = s_plan;
     const int pc = s_action;
     if (pc == PC_A) {
-        for (int j = tid; j < k; j += 1024) d.vrow[j] = d.Minv[(size_t)P.p * d.ldm + j] / P.piv;
+        for (int j = tid; j < k; j += 256) d.vrow[j] = d.Minv[(size_t)P.p * d.ldm + j] / P.piv;
     } else if (pc == PC_C) {
-        for (int j = tid; j < k; j += 1024) {
+        for (int j = tid; j < k; j += 256) {
             d.vrow[j] = d.Minv[(size_t)P.b * d.ldm + j] / P.piv;
             d.colA[j] = d.MinvT[(size_t)P.a * d.ldm + j];
         }
     } else if (pc == PC_D || pc == PC_B) {
         // gathered row A[row, S] = AS[row, 0:k] for the B^-1 row kernel
-        for (int j = tid; j < k; j += 1024) d.vrow[j] = d.AS[(size_t)j * (size_t)m + P.row];
+        for (int j = tid; j < k; j += 256) d.vrow[j] = d.AS[(size_t)j * (size_t)m + P.row];
         if (pc == PC_D)
-            for (int j = tid; j < k; j += 1024) d.colA[j] = d.MinvT[(size_t)P.a * d.ldm + j];
+            for (int j = tid; j < k; j += 256) d.colA[j] = d.MinvT[(size_t)P.a * d.ldm + j];
     }
 }
 
