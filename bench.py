@@ -125,6 +125,7 @@ def main():
     iters = s1["iterations"] - s0["iterations"]
     value = iters / elapsed if elapsed > 0 else 0.0
 
+    price_dev_bytes = (s1["price_bytes"] - s0["price_bytes"]) / max(iters, 1)
     price_s = s1["price_seconds"] - s0["price_seconds"]
     price_b = s1["price_timed_bytes"] - s0["price_timed_bytes"]
     price_n = s1["price_timed_launches"] - s0["price_timed_launches"]
@@ -181,7 +182,7 @@ def main():
                 "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "traffic": None,
-                "bytes_per_launch": price_b / price_n if price_n else None,
+                "bytes_per_launch": price_b / price_n if price_n else price_dev_bytes,
                 "avg_launch_us": 1e6 * price_s / price_n if price_n else None,
                 "launches_timed": price_n,
             },

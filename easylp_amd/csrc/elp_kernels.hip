@@ -382,7 +382,7 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d) {
     const double* __restrict__ yy = d.yy;
     double acc0 = 0.0, acc1 = 0.0;
     int p = p0;
-    constexpr int UNR = 32;  // rows in flight per wave: 32 KiB
+    constexpr int UNR = 16;  // rows in flight per wave: 16 KiB (32 measured slower)
     for (; p + UNR <= p1; p += UNR) {
         double2 v[UNR];
 #pragma unroll

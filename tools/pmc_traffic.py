@@ -1,0 +1,33 @@
+"""HBM traffic of the pricing kernel from a rocprofv3 --pmc FETCH_SIZE pass.
+
+FETCH_SIZE is in KiB and, on gfx950, reports half the bytes of a wide
+coalesced streaming read (MI355X_MICROARCH.md, HBM section): bytes =
+2 * 1024 * FETCH_SIZE.  The PMC pass runs `bench.py --steps K --warmup W`;
+the timed launches are dispatches W+1 .. W+K of k_price (launch 0-based W..W+K-1).
+Usage: python tools/pmc_traffic.py <counter_collection.csv> <bench.json> W K
+"""
+import csv
+import json
+import sys
+
+
+def main(csv_path, bench_json, warmup, steps):
+    rows = [r for r in csv.DictReader(open(csv_path))
+            if r["Counter_Name"] == "FETCH_SIZE" and "k_price" in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    win = rows[warmup:warmup + steps]
+    fetch = [2 * 1024 * float(r["Counter_Value"]) for r in win]
+    b = json.loads(open(bench_json).read().strip().splitlines()[-1])
+    alg = b["roofline"]["bytes_per_launch"]
+    out = {
+        "launches": len(win),
+        "traffic_bytes_per_launch": sum(fetch) / len(fetch),
+        "algorithmic_bytes_per_launch": alg,
+        "traffic_over_algorithmic": (sum(fetch) / len(fetch)) / alg if alg else None,
+        "correction": "bytes = 2 * 1024 * FETCH_SIZE (gfx950 wide-read halving, MI355X_MICROARCH.md)",
+    }
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]))
