@@ -91,15 +91,8 @@ def main():
     verbose = ELP_PROFILE_PRICE if args.profile_price else 0
     p = Problem(args.m, args.n, device=local, verbose=verbose)
     if world > 1:
-        import ctypes
-        uid = ctypes.create_string_buffer(128)
-        if rank == 0:
-            rc = lib.elp_comm_unique_id(uid)
-            if rc < 0:
-                raise SystemExit("multi-GPU communicator unavailable: " + lib.elp_last_error().decode())
-        obj = [uid.raw if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        p.comm_init(obj[0], world, rank)
+        from easylp_amd.dist import share_unique_id
+        p.comm_init(share_unique_id(lib, rank), world, rank)
 
     p.load_generated(args.seed)
 

@@ -20,9 +20,17 @@ ELP_PROFILE_PRICE = 2
 EXPORTS = (
     "elp_default_control", "elp_create", "elp_load_dense", "elp_load_dense_device",
     "elp_load_generated", "elp_solve", "elp_iterate", "elp_get_solution", "elp_get_stats",
-    "elp_set_trace", "elp_get_trace", "elp_comm_unique_id", "elp_comm_init", "elp_destroy",
-    "elp_last_error", "elp_abi_version",
+    "elp_set_trace", "elp_get_trace", "elp_comm_unique_id", "elp_comm_init", "elp_comm_init_host",
+    "elp_destroy", "elp_last_error", "elp_abi_version",
 )
+
+# host transports for elp_comm_init_host (include/easylp_hip.h)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                ctypes.c_void_p)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int32,
+                                ctypes.c_void_p)
+BCAST_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int32,
+                            ctypes.c_void_p)
 
 
 class ElpControl(ctypes.Structure):
@@ -100,13 +108,15 @@ def load(path: str | None = None):
     lib.elp_get_trace.argtypes = [vp, vp, i64, P(i64)]
     lib.elp_comm_unique_id.argtypes = [vp]
     lib.elp_comm_init.argtypes = [vp, vp, i32, i32]
+    lib.elp_comm_init_host.argtypes = [vp, i32, i32, ALLGATHER_FN, ALLREDUCE_FN, BCAST_FN, vp]
     lib.elp_destroy.argtypes = [vp]
     lib.elp_destroy.restype = None
     lib.elp_last_error.restype = ctypes.c_char_p
     lib.elp_abi_version.restype = i32
     for name in ("elp_create", "elp_load_dense", "elp_load_dense_device", "elp_load_generated",
                  "elp_solve", "elp_iterate", "elp_get_solution", "elp_get_stats",
-                 "elp_set_trace", "elp_get_trace", "elp_comm_unique_id", "elp_comm_init"):
+                 "elp_set_trace", "elp_get_trace", "elp_comm_unique_id", "elp_comm_init",
+                 "elp_comm_init_host"):
         getattr(lib, name).restype = ctypes.c_int
     _lib = lib
     return lib

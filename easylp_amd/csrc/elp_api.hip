@@ -68,6 +68,7 @@ struct elp_handle {
     int64_t trace_cap = 0;
     elp::Comm comm;  // multi-GPU (world 1 = no-op)
     std::vector<hipEvent_t> ev;  // pricing-kernel timing pairs (profile mode)
+    int32_t* d_flag = nullptr;   // one int for cross-rank decisions
 };
 
 extern "C" void elp_default_control(elp_control* c) {
@@ -94,11 +95,13 @@ static void free_dev(elp_handle* h) {
                     d.lb,       d.ub,  d.cost,  d.xval,  d.asgn, d.xr,    d.xs,    d.y,
                     d.t,        d.acol, d.aR,   d.alS,   d.alU,  d.zz,    d.zpart, d.vrow,
                     d.vvec,     d.colA, d.rhs,  d.vstat, d.cover, d.rpos, d.Rl,    d.Sl,
-                    d.spos,     d.Yl,  d.ypos,  d.perm,  d.pivstep, d.nzlist, d.nzcount,
-                    d.cand,     d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand, d.cS, d.slo, d.shi, d.rlo, d.rhi};
+                    d.Yl,  d.ypos,  d.perm,  d.pivstep, d.nzlist, d.nzcount,
+                    d.cand,     d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand,
+                    d.pkt, d.objg, d.ract, d.cand_xchg, h->d_flag, d.cS, d.slo, d.shi, d.rlo, d.rhi};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     h->A_owned = nullptr;
+    h->d_flag = nullptr;
     d = Dev{};
     if (h->hctl) (void)hipHostFree(h->hctl);
     h->hctl = nullptr;
@@ -145,6 +148,10 @@ static int alloc_all(elp_handle* h) {
     const int64_t mm = m > 0 ? m : 1;
     d.m = (int32_t)m;
     d.n = (int32_t)n;
+    d.N = (int32_t)h->n;
+    d.col0 = h->col0;
+    d.world = h->comm.world;
+    d.sharded = h->comm.kind != 0;
     d.nv = (int32_t)(n + 2 * m);
     d.ldm = mm;
     d.ldr = ((n + TILE_COLS - 1) / TILE_COLS) * TILE_COLS;
@@ -177,6 +184,11 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.yy, mm));
     A(dalloc(&d.blockmin, (size_t)(mm / 64 + mm / 256 + 4)));
     A(dalloc(&d.rcand, (size_t)(2 * mm + 2)));
+    A(dalloc(&d.pkt, (size_t)(mm + 4)));
+    A(dalloc(&d.objg, (size_t)h->n));
+    A(dalloc(&d.ract, mm));
+    A(dalloc(&d.cand_xchg, (size_t)h->comm.world));
+    A(dalloc(&h->d_flag, 1));
     A(dalloc(&d.t, mm));
     A(dalloc(&d.acol, mm));
     A(dalloc(&d.aR, mm));
@@ -192,7 +204,6 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.rpos, mm));
     A(dalloc(&d.Rl, mm));
     A(dalloc(&d.Sl, mm));
-    A(dalloc(&d.spos, n));
     A(dalloc(&d.Yl, mm));
     A(dalloc(&d.ypos, mm));
     A(dalloc(&d.perm, mm));
@@ -233,6 +244,38 @@ static int ensure_w(elp_handle* h, int k) {
     return 0;
 }
 
+// ract = sum_j a_ij x_j over nonzero nonbasic columns, in global column order:
+// shard r continues the fma chain of shards 0..r-1 (broadcast after each turn)
+static int row_chain(elp_handle* h) {
+    const size_t mb = (size_t)h->m * sizeof(double);
+    if (h->m == 0) return 0;
+    HIPCHK(hipMemsetAsync(h->d.ract, 0, mb, h->st));
+    if (h->comm.kind == 0) {
+        HIPCHK(launch_row_chain(h->d, h->st));
+        return 0;
+    }
+    for (int r = 0; r < h->comm.world; ++r) {
+        if (r == h->comm.rank) HIPCHK(launch_row_chain(h->d, h->st));
+        const int rc = h->comm.bcast_f64(h->d.ract, (size_t)h->m, r, h->st);
+        if (rc) return fail(rc, "row activity broadcast failed");
+    }
+    return 0;
+}
+
+// max over ranks of an int decided on the host
+static int any_rank(elp_handle* h, int v, int* out) {
+    *out = v;
+    if (h->comm.kind == 0) return 0;
+    HIPCHK(hipMemcpyAsync(h->d_flag, &v, sizeof(int32_t), hipMemcpyHostToDevice, h->st));
+    const int rc = h->comm.allreduce_max_i32(h->d_flag, 1, h->st);
+    if (rc) return fail(rc, "flag all-reduce failed");
+    int32_t r = 0;
+    HIPCHK(hipMemcpyAsync(&r, h->d_flag, sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    *out = r;
+    return 0;
+}
+
 // common tail of elp_load_*: bounds, rows, control block, phase decision
 static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, const double* obj,
                        const double* lo, const double* up, int32_t maximize) {
@@ -265,6 +308,7 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
         HIPCHK(hipMemcpyAsync(d.ub + nl, sub.data(), m * sizeof(double), hipMemcpyHostToDevice, h->st));
     }
     HIPCHK(hipMemcpyAsync(d.obj, obj + n0, nl * sizeof(double), hipMemcpyHostToDevice, h->st));
+    HIPCHK(hipMemcpyAsync(d.objg, obj, n * sizeof(double), hipMemcpyHostToDevice, h->st));
     DevCtl c{};
     c.status = ST_RUN;
     c.phase = 1;
@@ -279,14 +323,22 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
     c.unb_var = -1;
     *h->hctl = c;
     HIPCHK(hipMemcpyAsync(d.ctl, h->hctl, sizeof(DevCtl), hipMemcpyHostToDevice, h->st));
-    HIPCHK(launch_init(d, dlo, dup, drhs, h->st));
+    HIPCHK(launch_init_cols(d, dlo, dup, h->st));
+    {
+        const int rc = row_chain(h);
+        if (rc) return rc;
+    }
+    HIPCHK(launch_init_rows(d, drhs, h->st));
     HIPCHK(hipMemcpyAsync(h->hctl, d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
     HIPCHK(hipStreamSynchronize(h->st));
     (void)hipFree(dlo);
     (void)hipFree(dup);
     (void)hipFree(drhs);
-    int infeasible = h->hctl->infeasible_bounds;
-    if (h->comm.world > 1) infeasible = h->comm.allreduce_max_int(infeasible, h->st);
+    int infeasible = 0;
+    {
+        const int rc = any_rank(h, h->hctl->infeasible_bounds, &infeasible);
+        if (rc) return rc;
+    }
     h->k_sync = 0;
     h->ny_sync = h->hctl->ny;
     h->since_refactor_sync = 0;
@@ -420,6 +472,11 @@ static int do_refactor(elp_handle* h, int k) {
             h->stats.gj_refactors++;
         }
     }
+    HIPCHK(launch_nzlist(h->d, h->st));
+    {
+        const int rc = row_chain(h);
+        if (rc) return rc;
+    }
     HIPCHK(launch_refactor_primal(h->d, k, h->st));
     h->stats.refactors++;
     return 0;
@@ -487,7 +544,20 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             const int kub = (int)std::min<int64_t>(h->m, (int64_t)k0 + t);
             const int nyub = (int)std::min<int64_t>(h->m, (int64_t)ny0 + t);
             hipEvent_t e0 = prof ? h->ev[2 * t] : nullptr, e1 = prof ? h->ev[2 * t + 1] : nullptr;
-            HIPCHK(launch_iteration(h->d, kub, nyub, h->phase, h->st, e0, e1));
+            if (h->comm.kind == 0) {
+                HIPCHK(launch_iteration(h->d, kub, nyub, h->phase, h->st, e0, e1));
+            } else {
+                // sharded: local min-loc -> all-gather -> global min-loc + owner's
+                // column packet -> all-reduce (non-owners contribute zeros) -> tail
+                HIPCHK(launch_iteration_head(h->d, kub, nyub, h->phase, h->comm.rank, h->st, e0, e1));
+                rc = h->comm.allgather(h->d.cand_xchg + h->comm.rank, h->d.cand_xchg, sizeof(Cand), h->st);
+                if (rc) return fail(rc, "candidate all-gather failed");
+                HIPCHK(launch_select_global(h->d, h->st));
+                rc = h->comm.allreduce_sum_f64(h->d.pkt, (size_t)h->m + 4, h->st);
+                if (rc) return fail(rc, "entering-column all-reduce failed");
+                HIPCHK(launch_select_finish(h->d, h->st));
+                HIPCHK(launch_iteration_tail(h->d, kub, h->phase, h->st));
+            }
         }
         HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
         HIPCHK(hipStreamSynchronize(h->st));
@@ -503,10 +573,15 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             h->stats.price_timed_bytes += c->price_bytes - bytes0;
         }
         if (s == ST_RUN) {
-            if (h->ctl.time_limit > 0 && now_s() - h->t_solve_start > h->ctl.time_limit) {
-                h->done = true;
-                h->final_status = ELP_TIMEOUT;
-                break;
+            if (h->ctl.time_limit > 0) {
+                int over = 0;
+                rc = any_rank(h, now_s() - h->t_solve_start > h->ctl.time_limit, &over);
+                if (rc) return rc;
+                if (over) {
+                    h->done = true;
+                    h->final_status = ELP_TIMEOUT;
+                    break;
+                }
             }
             continue;
         }
@@ -594,24 +669,26 @@ extern "C" int elp_get_solution(elp_handle* h, double* objval, double* x, double
     HIPCHK(hipSetDevice(h->dev));
     const int64_t m = h->m, n = h->n, nl = h->nloc;
     HIPCHK(hipMemcpyAsync(h->hctl, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
-    // structural values of the local shard, gathered to every rank
+    // structural values: each shard writes its columns into a zeroed full-length
+    // vector, the all-reduce (sum with zeros: exact) gives every rank all of x
     std::vector<double> xs((size_t)n, 0.0);
     double* dx = nullptr;
-    HIPCHK(dalloc(&dx, nl));
-    HIPCHK(launch_extract(h->d, dx, h->st));
-    HIPCHK(hipMemcpyAsync(xs.data() + h->col0, dx, nl * sizeof(double), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(dalloc(&dx, n));
+    HIPCHK(hipMemsetAsync(dx, 0, (size_t)n * sizeof(double), h->st));
+    HIPCHK(launch_extract(h->d, dx + h->col0, h->st));
+    {
+        const int rc = h->comm.allreduce_sum_f64(dx, (size_t)n, h->st);
+        if (rc) return fail(rc, "solution all-reduce failed");
+    }
+    HIPCHK(hipMemcpyAsync(xs.data(), dx, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, h->st));
     HIPCHK(hipStreamSynchronize(h->st));
     (void)hipFree(dx);
-    if (h->comm.world > 1) {
-        int rc = h->comm.allgather_shards(xs.data(), h->n, h->st);
-        if (rc) return rc;
-    }
+    (void)nl;
     const DevCtl& c = *h->hctl;
     const double BIG = h->ctl.infinity;
     const bool unb = h->done && h->final_status == ELP_UNBOUNDED;
     // the unbounded variable's global id (shard-local q -> global)
-    int64_t uvar = -1;
-    if (unb && c.unb_var >= 0 && c.unb_var < h->nloc) uvar = h->col0 + c.unb_var;
+    const int64_t uvar = unb ? (int64_t)c.unb_var : -1;  // global id
     if (unb && uvar >= 0 && uvar < n) xs[uvar] = c.unb_sig > 0 ? BIG : -BIG;
     if (x) std::memcpy(x, xs.data(), (size_t)n * sizeof(double));
     if (objval) {
@@ -640,15 +717,10 @@ extern "C" int elp_get_solution(elp_handle* h, double* objval, double* x, double
         HIPCHK(hipStreamSynchronize(h->st));
         std::vector<int64_t> bv;
         bv.reserve(m);
-        // local var ids -> global ids: structural j -> col0 + j; slack n_loc + i -> n + i
-        auto glob = [&](int64_t v) -> int64_t {
-            if (v < nl) return h->col0 + v;
-            if (v < nl + m) return n + (v - nl);
-            return n + m + (v - nl - m);
-        };
+        // cover and Sl hold global ids
         for (int64_t i = 0; i < m; ++i)
-            if (cover[i] >= 0) bv.push_back(glob(cover[i]));
-        for (int p = 0; p < c.k; ++p) bv.push_back(glob(Sl[p]));
+            if (cover[i] >= 0) bv.push_back(cover[i]);
+        for (int p = 0; p < c.k; ++p) bv.push_back(Sl[p]);
         std::sort(bv.begin(), bv.end());
         for (size_t t = 0; t < bv.size() && (int64_t)t < m; ++t) basis[t] = bv[t];
     }
@@ -714,5 +786,16 @@ extern "C" int elp_comm_init(elp_handle* h, const uint8_t id[128], int32_t world
         return fail(ELP_E_ARG, "elp_comm_init: bad argument");
     if (h->loaded) return fail(ELP_E_STATE, "elp_comm_init: call before elp_load_*");
     HIPCHK(hipSetDevice(h->dev));
-    return h->comm.init(id, world_size, rank);
+    const int rc = h->comm.init_rccl(id, world_size, rank);
+    return rc ? fail(rc, "RCCL communicator init failed") : 0;
+}
+
+extern "C" int elp_comm_init_host(elp_handle* h, int32_t world_size, int32_t rank,
+                                  elp_host_allgather_fn ag, elp_host_allreduce_fn ar,
+                                  elp_host_bcast_fn bc, void* user) {
+    if (!h || world_size < 1 || rank < 0 || rank >= world_size)
+        return fail(ELP_E_ARG, "elp_comm_init_host: bad argument");
+    if (h->loaded) return fail(ELP_E_STATE, "elp_comm_init_host: call before elp_load_*");
+    const int rc = h->comm.init_host(world_size, rank, ag, ar, bc, user);
+    return rc ? fail(rc, "elp_comm_init_host: NULL transport") : 0;
 }

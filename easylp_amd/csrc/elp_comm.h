@@ -1,19 +1,41 @@
-// elp_comm.h -- column-shard communicator.
-// World size 1 is a no-op; the RCCL path is added in elp_comm.hip.
+// elp_comm.h -- communicator for the column-sharded solve.
+//
+// Three primitives, all on device buffers and ordered on the solver stream:
+// all-gather of fixed-size records, all-reduce (f64 sum / i32 max) and
+// broadcast.  Transports: RCCL (one process per GPU, over xGMI), or host
+// callbacks (the caller moves host copies, e.g. with torch.distributed gloo;
+// used to run several ranks on one GPU in tests).  World size 1 is a no-op.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
+
+#include <vector>
+
+#include "../../include/easylp_hip.h"
 
 namespace elp {
 
 struct Comm {
     int world = 1, rank = 0;
+    int kind = 0;          // 0 none, 1 rccl, 2 host callbacks
     void* nccl = nullptr;  // ncclComm_t
+    elp_host_allgather_fn h_allgather = nullptr;
+    elp_host_allreduce_fn h_allreduce = nullptr;
+    elp_host_bcast_fn h_bcast = nullptr;
+    void* h_user = nullptr;
+    std::vector<unsigned char> stage;  // host staging for the callback transport
+
     static int unique_id(uint8_t id[128]);
-    int init(const uint8_t id[128], int world_size, int rank_);
+    int init_rccl(const uint8_t id[128], int world_size, int rank_);
+    int init_host(int world_size, int rank_, elp_host_allgather_fn ag, elp_host_allreduce_fn ar,
+                  elp_host_bcast_fn bc, void* user);
     void destroy();
-    int allreduce_max_int(int v, hipStream_t st);
-    int allgather_shards(double* x, int64_t n, hipStream_t st);
+    // recv holds world * bytes; send is this rank's record
+    int allgather(const void* dsend, void* drecv, size_t bytes, hipStream_t st);
+    int allreduce_sum_f64(double* dbuf, size_t count, hipStream_t st);
+    int allreduce_max_i32(int32_t* dbuf, size_t count, hipStream_t st);
+    int bcast_f64(double* dbuf, size_t count, int root, hipStream_t st);
 };
 
 }  // namespace elp

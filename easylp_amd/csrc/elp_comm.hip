@@ -1,26 +1,114 @@
-// elp_comm.hip -- communicator stub for world size 1 (multi-GPU: see DESIGN.md).
+// elp_comm.hip -- RCCL and host-callback transports for the sharded solve.
 #include "elp_comm.h"
 
-#include <cstring>
+#include <rccl/rccl.h>
 
-#include "../../include/easylp_hip.h"
+#include <cstdlib>
+#include <cstring>
 
 namespace elp {
 
 int Comm::unique_id(uint8_t id[128]) {
-    std::memset(id, 0, 128);
-    return ELP_E_UNSUPPORTED;
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return ELP_E_COMM;
+    std::memcpy(id, &u, 128);
+    return 0;
 }
-int Comm::init(const uint8_t*, int world_size, int rank_) {
-    if (world_size == 1) {
-        world = 1;
-        rank = rank_;
+
+int Comm::init_rccl(const uint8_t id[128], int world_size, int rank_) {
+    world = world_size;
+    rank = rank_;
+    // one rank: plain single-GPU path, unless ELP_RCCL_SINGLE=1 asks for the
+    // sharded pipeline over a 1-rank RCCL communicator (tests on one GPU)
+    if (world == 1 && !std::getenv("ELP_RCCL_SINGLE")) {
+        kind = 0;
         return 0;
     }
-    return ELP_E_UNSUPPORTED;
+    ncclUniqueId u;
+    std::memcpy(&u, id, 128);
+    ncclComm_t c = nullptr;
+    if (ncclCommInitRank(&c, world, u, rank) != ncclSuccess) return ELP_E_COMM;
+    nccl = c;
+    kind = 1;
+    return 0;
 }
-void Comm::destroy() {}
-int Comm::allreduce_max_int(int v, hipStream_t) { return v; }
-int Comm::allgather_shards(double*, int64_t, hipStream_t) { return 0; }
+
+int Comm::init_host(int world_size, int rank_, elp_host_allgather_fn ag, elp_host_allreduce_fn ar,
+                    elp_host_bcast_fn bc, void* user) {
+    if (!ag || !ar || !bc) return ELP_E_ARG;
+    world = world_size;
+    rank = rank_;
+    kind = world > 1 ? 2 : 0;
+    h_allgather = ag;
+    h_allreduce = ar;
+    h_bcast = bc;
+    h_user = user;
+    return 0;
+}
+
+void Comm::destroy() {
+    if (kind == 1 && nccl) ncclCommDestroy((ncclComm_t)nccl);
+    nccl = nullptr;
+    kind = 0;
+    world = 1;
+}
+
+int Comm::allgather(const void* dsend, void* drecv, size_t bytes, hipStream_t st) {
+    if (kind == 0) {
+        if (dsend != drecv && hipMemcpyAsync(drecv, dsend, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
+            return ELP_E_HIP;
+        return 0;
+    }
+    if (kind == 1)
+        return ncclAllGather(dsend, drecv, bytes, ncclUint8, (ncclComm_t)nccl, st) == ncclSuccess ? 0 : ELP_E_COMM;
+    stage.resize(bytes * (world + 1));
+    unsigned char* snd = stage.data() + bytes * world;
+    if (hipMemcpyAsync(snd, dsend, bytes, hipMemcpyDeviceToHost, st) != hipSuccess) return ELP_E_HIP;
+    if (hipStreamSynchronize(st) != hipSuccess) return ELP_E_HIP;
+    if (h_allgather(snd, stage.data(), bytes, h_user) != 0) return ELP_E_COMM;
+    if (hipMemcpyAsync(drecv, stage.data(), bytes * world, hipMemcpyHostToDevice, st) != hipSuccess) return ELP_E_HIP;
+    return hipStreamSynchronize(st) == hipSuccess ? 0 : ELP_E_HIP;
+}
+
+static int host_allreduce(Comm& c, void* dbuf, size_t count, size_t esize, int dtype, hipStream_t st) {
+    const size_t bytes = count * esize;
+    c.stage.resize(bytes);
+    if (hipMemcpyAsync(c.stage.data(), dbuf, bytes, hipMemcpyDeviceToHost, st) != hipSuccess) return ELP_E_HIP;
+    if (hipStreamSynchronize(st) != hipSuccess) return ELP_E_HIP;
+    if (c.h_allreduce(c.stage.data(), count, dtype, c.h_user) != 0) return ELP_E_COMM;
+    if (hipMemcpyAsync(dbuf, c.stage.data(), bytes, hipMemcpyHostToDevice, st) != hipSuccess) return ELP_E_HIP;
+    return hipStreamSynchronize(st) == hipSuccess ? 0 : ELP_E_HIP;
+}
+
+int Comm::allreduce_sum_f64(double* dbuf, size_t count, hipStream_t st) {
+    if (kind == 0) return 0;
+    if (kind == 1)
+        return ncclAllReduce(dbuf, dbuf, count, ncclFloat64, ncclSum, (ncclComm_t)nccl, st) == ncclSuccess
+                   ? 0 : ELP_E_COMM;
+    return host_allreduce(*this, dbuf, count, sizeof(double), 0, st);
+}
+
+int Comm::allreduce_max_i32(int32_t* dbuf, size_t count, hipStream_t st) {
+    if (kind == 0) return 0;
+    if (kind == 1)
+        return ncclAllReduce(dbuf, dbuf, count, ncclInt32, ncclMax, (ncclComm_t)nccl, st) == ncclSuccess
+                   ? 0 : ELP_E_COMM;
+    return host_allreduce(*this, dbuf, count, sizeof(int32_t), 1, st);
+}
+
+int Comm::bcast_f64(double* dbuf, size_t count, int root, hipStream_t st) {
+    if (kind == 0) return 0;
+    if (kind == 1)
+        return ncclBroadcast(dbuf, dbuf, count, ncclFloat64, root, (ncclComm_t)nccl, st) == ncclSuccess
+                   ? 0 : ELP_E_COMM;
+    const size_t bytes = count * sizeof(double);
+    stage.resize(bytes);
+    if (hipMemcpyAsync(stage.data(), dbuf, bytes, hipMemcpyDeviceToHost, st) != hipSuccess) return ELP_E_HIP;
+    if (hipStreamSynchronize(st) != hipSuccess) return ELP_E_HIP;
+    if (h_bcast(stage.data(), bytes, root, h_user) != 0) return ELP_E_COMM;
+    if (hipMemcpyAsync(dbuf, stage.data(), bytes, hipMemcpyHostToDevice, st) != hipSuccess) return ELP_E_HIP;
+    return hipStreamSynchronize(st) == hipSuccess ? 0 : ELP_E_HIP;
+}
 
 }  // namespace elp

@@ -74,8 +74,16 @@ struct Cand {
 };
 
 // Everything a kernel needs, passed by value (pointers into device memory).
+// Variable ids: replicated state (cover, Sl, candidates, q, trace) holds GLOBAL
+// ids -- structural j < N, slack N + i, artificial N + m + i; per-variable
+// arrays (lb, ub, cost, xval, vstat) are indexed by the shard-LOCAL id --
+// structural j - col0 < n, slack n + i, artificial n + m + i (loc_of()).
+// With one GPU, col0 = 0 and n = N, so both coincide.
 struct Dev {
-    int32_t m, n, nv, pad;
+    int32_t m, n, nv, N;  // n: local columns; N: global columns
+    int64_t col0;         // first global column of this shard
+    int32_t world;        // ranks sharing the columns
+    int32_t sharded;      // 1: entering column comes from the exchanged packet
     int64_t ldm;   // Minv leading dimension (= max(m,1))
     int64_t ldr;   // AR leading dimension (n rounded up to TILE_COLS)
     const double* A;  // column-major m x n
@@ -89,6 +97,10 @@ struct Dev {
     double *vrow, *vvec, *colA, *rhs;
     double *cS, *slo, *shi;  // per bump position: cost, bounds of S_p
     double* blockmin;        // per-workgroup Harris pass-1 minima (k_ftran_zr)
+    double* pkt;             // entering column + (lb, ub, x, cost) exchanged across shards
+    double* objg;            // global objective (N), for c_S of foreign basic columns
+    double* ract;            // row activities sum_j a_ij x_j of nonzero nonbasic columns
+    Cand* cand_xchg;         // [world] local best candidates (all-gathered)
     RCand* rcand;            // pass-2 candidates (capacity 2m)
     double *rlo, *rhi;       // per covered row: bounds of the covering unit variable
     int8_t* vstat;
@@ -104,18 +116,31 @@ struct Dev {
 // Each returns hipGetLastError() of its launch.
 hipError_t launch_generate(const Dev& d, uint64_t seed, int64_t col0, int64_t n_global,
                            double* A, double* b, double* c, hipStream_t st);
-hipError_t launch_init(const Dev& d, const double* lo, const double* up, const double* rhs,
-                       hipStream_t st);
+// init in two parts: columns (+ nonzero list), then rows once ract is complete
+hipError_t launch_init_cols(const Dev& d, const double* lo, const double* up, hipStream_t st);
+hipError_t launch_init_rows(const Dev& d, const double* rhs, hipStream_t st);
 // ev0/ev1 (may be null): events recorded around the pricing kernel
 hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStream_t st,
                             hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+// sharded iteration: head (BTRAN, pricing, local min-loc into cand_xchg[rank]),
+// then the host all-gathers cand_xchg, select_global packs pkt, the host
+// all-reduces pkt, then tail (a_R, FTRAN, ratio test, update)
+hipError_t launch_iteration_head(const Dev& d, int k_ub, int ny_ub, int phase, int rank,
+                                 hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+hipError_t launch_select_global(const Dev& d, hipStream_t st);
+hipError_t launch_select_finish(const Dev& d, hipStream_t st);
+hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t st);
+// row activities: ract = chain(ract, local nonzero nonbasic columns)
+hipError_t launch_row_chain(const Dev& d, hipStream_t st);
 // refactor = ns_resid; (host reads ns_emax) ns_update | gauss_jordan; primal
 constexpr double NS_TOL = 1e-6;
 hipError_t launch_refactor_ns_resid(const Dev& d, int k, hipStream_t st);
 hipError_t launch_refactor_ns_update(const Dev& d, int k, hipStream_t st);
 hipError_t launch_refactor_gj(const Dev& d, int k, hipStream_t st);
-hipError_t launch_refactor_primal(const Dev& d, int k, hipStream_t st);
+hipError_t launch_refactor_primal(const Dev& d, int k, hipStream_t st);  // needs ract
+hipError_t launch_nzlist(const Dev& d, hipStream_t st);
 hipError_t launch_phase2(const Dev& d, hipStream_t st);
+// x of the local shard into xout[0:n) (basic values from the replicated S list)
 hipError_t launch_extract(const Dev& d, double* xout, hipStream_t st);
 
 }  // namespace elp

@@ -60,8 +60,16 @@ DEV double wave_tree(double v) {  // butterfly 32..1; lane 0 == oracle wave_dot 
     for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off);
     return v;
 }
-DEV double unit_sign(const Dev& d, int var, int row) {
-    return var >= d.n + d.m ? d.asgn[row] : 1.0;
+DEV double unit_sign(const Dev& d, int var, int row) {  // var: global id
+    return var >= d.N + d.m ? d.asgn[row] : 1.0;
+}
+// global var id -> shard-local per-variable index (-1: another shard's column)
+DEV int loc_of(const Dev& d, int g) {
+    if (g < d.N) {
+        const int64_t j = (int64_t)g - d.col0;
+        return (j >= 0 && j < d.n) ? (int)j : -1;
+    }
+    return d.n + (g - d.N);
 }
 DEV bool cand_better(const Cand& a, const Cand& b, int bland) {
     if (a.j < 0) return false;
@@ -124,7 +132,7 @@ DEV double wave_art_sum(const Dev& d) {
     const int lane = threadIdx.x & 63;
     double acc = 0.0;
     for (int i = lane; i < d.m; i += 64)
-        if (d.cover[i] >= d.n + d.m) acc = acc + d.xr[i];
+        if (d.cover[i] >= d.N + d.m) acc = acc + d.xr[i];
     return wave_tree(acc);
 }
 
@@ -138,7 +146,6 @@ __global__ void k_init_cols(Dev d, const double* __restrict__ lo, const double* 
     d.lb[j] = l;
     d.ub[j] = u;
     d.cost[j] = 0.0;
-    d.spos[j] = -1;
     if (l > u) atomicOr(&d.ctl->infeasible_bounds, 1);
     if (l == u) {
         d.vstat[j] = VS_FIXED;
@@ -183,14 +190,18 @@ __global__ void __launch_bounds__(1024) k_nzlist(Dev d) {
     if (threadIdx.x == 0) *d.nzcount = base;
 }
 
-// rhs_i = b_i - sum_{j in nzlist} a_ij x_j  (seq fma chain, ascending j)
-DEV double row_activity(const Dev& d, int i, int nz) {
-    double acc = 0.0;
+// ract_i = chain(ract_i, a_ij x_j over this shard's nonzero nonbasic columns,
+// ascending j): the oracle's seq order, continued shard after shard
+__global__ void k_row_chain(Dev d) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= d.m) return;
+    const int nz = *d.nzcount;
+    double acc = d.ract[i];
     for (int t = 0; t < nz; ++t) {
         const int j = d.nzlist[t];
         acc = fma(d.A[(size_t)j * (size_t)d.m + (size_t)i], d.xval[j], acc);
     }
-    return acc;
+    d.ract[i] = acc;
 }
 
 __global__ void k_init_rows(Dev d, const double* __restrict__ rhs_in) {
@@ -200,7 +211,8 @@ __global__ void k_init_rows(Dev d, const double* __restrict__ rhs_in) {
     if (bi <= -d.infinity) bi = -HUGE_VAL;
     if (bi >= d.infinity) bi = HUGE_VAL;
     d.b[i] = bi;
-    const int n = d.n, m = d.m, sv = n + i, av = n + m + i;
+    const int n = d.n, m = d.m, sv = n + i, av = n + m + i;  // local ids
+    const int svg = d.N + i, avg = d.N + m + i;                 // global ids
     // d.lb/d.ub for slacks were written by the host (dir); artificials:
     d.lb[av] = 0.0;
     d.ub[av] = 0.0;
@@ -211,11 +223,11 @@ __global__ void k_init_rows(Dev d, const double* __restrict__ rhs_in) {
     d.rpos[i] = -1;
     d.ypos[i] = -1;
     d.asgn[i] = 1.0;
-    const double r = bi - row_activity(d, i, *d.nzcount);
+    const double r = bi - d.ract[i];
     const double sl = d.lb[sv], su = d.ub[sv];
     if (r >= sl && r <= su) {
         d.vstat[sv] = VS_BASIC;
-        d.cover[i] = sv;
+        d.cover[i] = svg;
         d.xr[i] = r;
         d.xval[sv] = 0.0;
         d.rlo[i] = sl;
@@ -229,7 +241,7 @@ __global__ void k_init_rows(Dev d, const double* __restrict__ rhs_in) {
         d.ub[av] = HUGE_VAL;
         d.cost[av] = 1.0;
         d.vstat[av] = VS_BASIC;
-        d.cover[i] = av;
+        d.cover[i] = avg;
         d.xr[i] = fabs(res);
         d.rlo[i] = 0.0;
         d.rhi[i] = HUGE_VAL;
@@ -249,7 +261,7 @@ __global__ void __launch_bounds__(1024) k_init_Y(Dev d) {
         const int i = i0 + threadIdx.x;
         bool f = false;
         if (i < d.m) {
-            f = d.cover[i] >= d.n + d.m;
+            f = d.cover[i] >= d.N + d.m;
             const double bi = fabs(d.b[i]);
             if (bi < HUGE_VAL && bi > bmax) bmax = bi;
         }
@@ -295,7 +307,7 @@ __global__ void k_ycov(Dev d) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= d.m) return;
     const int u = d.cover[i];
-    const double yi = u >= 0 ? unit_sign(d, u, i) * d.cost[u] : 0.0;
+    const double yi = u >= 0 ? unit_sign(d, u, i) * d.cost[loc_of(d, u)] : 0.0;
     d.y[i] = yi;
     const int sl = d.ypos[i];
     if (u >= 0 && sl >= 0) d.yy[sl] = yi;
@@ -338,7 +350,7 @@ __global__ void __launch_bounds__(256) k_btran(Dev d, int phase, const double* _
         for (int i = gid; i < d.m; i += gsz) {
             const int u = d.cover[i];
             if (u < 0) continue;
-            const double yi = unit_sign(d, u, i) * d.cost[u];
+            const double yi = unit_sign(d, u, i) * d.cost[loc_of(d, u)];
             d.y[i] = yi;
             const int sl = d.ypos[i];
             if (sl >= 0) d.yy[sl] = yi;
@@ -428,11 +440,11 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d) {
                 const double dj = d.cost[j] - tot;
                 const double dtol = c->tol_dual;
                 if ((vs == VS_LOWER || vs == VS_FREE) && dj < -dtol) {
-                    best.j = j;
+                    best.j = d.col0 + j;
                     best.score = -dj;
                     best.d = dj;
                 } else if ((vs == VS_UPPER || vs == VS_FREE) && dj > dtol) {
-                    best.j = j;
+                    best.j = d.col0 + j;
                     best.score = dj;
                     best.d = dj;
                 }
@@ -444,13 +456,12 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d) {
 }
 
 // ============================================================== select
-// Min-loc over tile candidates and the slack candidates; entering column to
-// acol (dense m-vector) and a_R = acol[R].
-__global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles) {
-    __shared__ Cand red[16];
-    DevCtl* c = d.ctl;
-    if (c->status != ST_RUN) return;
-    const int bland = c->bland, ny = c->ny, k = c->k;
+// Min-loc over this shard's tile candidates and the (replicated) slack
+// candidates.  One GPU: decide q and form a_R.  Sharded: write the local best
+// to cand_xchg[rank] for the all-gather (k_select_global decides).
+DEV Cand local_best(const Dev& d, int ntiles, Cand* red) {
+    const DevCtl* c = d.ctl;
+    const int bland = c->bland, ny = c->ny;
     Cand best;
     best.j = -1;
     best.score = 0.0;
@@ -462,47 +473,110 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles) {
     const double dtol = c->tol_dual;
     for (int p = threadIdx.x; p < ny; p += 1024) {
         const int i = d.Yl[p];
-        const int j = d.n + i;
-        const int8_t vs = d.vstat[j];
+        const int jl = d.n + i;  // local slack id
+        const int8_t vs = d.vstat[jl];
         if (vs == VS_FIXED) continue;
-        const double dj = d.cost[j] - d.yy[p];
+        const double dj = d.cost[jl] - d.yy[p];
         Cand o;
         o.j = -1;
         if ((vs == VS_LOWER || vs == VS_FREE) && dj < -dtol) {
-            o.j = j;
+            o.j = d.N + i;
             o.score = -dj;
             o.d = dj;
         } else if ((vs == VS_UPPER || vs == VS_FREE) && dj > dtol) {
-            o.j = j;
+            o.j = d.N + i;
             o.score = dj;
             o.d = dj;
         }
         if (cand_better(o, best, bland)) best = o;
     }
-    best = block_best<1024>(best, bland, red);
+    return block_best<1024>(best, bland, red);
+}
+
+DEV void entering_chosen(const Dev& d, const Cand& best) {
+    DevCtl* c = d.ctl;
+    const int ny = c->ny;
+    c->ncand = 0;
+    // algorithmic bytes of this pricing pass: AR sweep + c + status + y_Y + Yl
+    c->price_bytes += 8.0 * (double)ny * (double)d.n + 9.0 * (double)d.n + 12.0 * (double)ny;
+    c->price_passes++;
+    c->q = (int)best.j;
+    c->dq = best.d;
+    c->sig = best.d < 0.0 ? 1.0 : -1.0;
+}
+
+// a_R = entering column on the bump rows
+DEV void gather_aR(const Dev& d, int q, const double* qcol) {
+    const int k = d.ctl->k;
+    if (q < d.N) {
+        for (int p = threadIdx.x; p < k; p += blockDim.x) d.aR[p] = qcol[d.Rl[p]];
+    } else {
+        const int i0 = q - d.N;
+        for (int p = threadIdx.x; p < k; p += blockDim.x) d.aR[p] = d.Rl[p] == i0 ? 1.0 : 0.0;
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles) {
+    __shared__ Cand red[16];
+    DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    const Cand best = local_best(d, ntiles, red);
     if (best.j < 0) {
         if (threadIdx.x == 0) c->status = ST_PHASE_OPT;
         return;
     }
     const int q = (int)best.j;
-    if (threadIdx.x == 0) {
-        c->ncand = 0;
-        // algorithmic bytes of this pricing pass: AR sweep + c + status + y_Y + Yl
-        c->price_bytes += 8.0 * (double)ny * (double)d.n + 9.0 * (double)d.n + 12.0 * (double)ny;
-        c->price_passes++;
-        c->q = q;
-        c->dq = best.d;
-        c->sig = best.d < 0.0 ? 1.0 : -1.0;
+    if (threadIdx.x == 0) entering_chosen(d, best);
+    // one GPU: the full column is read in place by k_ftran_zr / k_update
+    gather_aR(d, q, q < d.N ? d.A + (size_t)(q - d.col0) * (size_t)d.m : nullptr);
+}
+
+__global__ void __launch_bounds__(1024) k_select_local(Dev d, int ntiles, int rank) {
+    __shared__ Cand red[16];
+    const DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    const Cand best = local_best(d, ntiles, red);
+    if (threadIdx.x == 0) d.cand_xchg[rank] = best;
+}
+
+// after the all-gather: global min-loc (same total order on every rank); the
+// owner of a structural q packs its column + (lb, ub, x, cost), others zeros
+__global__ void __launch_bounds__(256) k_select_global(Dev d) {
+    DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    const int bland = c->bland;
+    Cand best = d.cand_xchg[0];
+    for (int r = 1; r < d.world; ++r)
+        if (cand_better(d.cand_xchg[r], best, bland)) best = d.cand_xchg[r];
+    const int m = d.m;
+    if (best.j < 0) {
+        for (int i = threadIdx.x; i < m + 4; i += 256) d.pkt[i] = 0.0;
+        if (threadIdx.x == 0) c->status = ST_PHASE_OPT;
+        return;
     }
-    // a_R = entering column on the bump rows (the full column is read in
-    // place by k_ftran_zr: A[:, q] for a structural, e_{q-n} for a slack)
-    if (q < d.n) {
-        const double* col = d.A + (size_t)q * (size_t)d.m;
-        for (int p = threadIdx.x; p < k; p += 1024) d.aR[p] = col[d.Rl[p]];
+    const int q = (int)best.j;
+    const int ql = loc_of(d, q);
+    const bool own = q < d.N && ql >= 0;
+    if (own) {
+        const double* col = d.A + (size_t)ql * (size_t)m;
+        for (int i = threadIdx.x; i < m; i += 256) d.pkt[i] = col[i];
+        if (threadIdx.x == 0) {
+            d.pkt[m] = d.lb[ql];
+            d.pkt[m + 1] = d.ub[ql];
+            d.pkt[m + 2] = d.xval[ql];
+            d.pkt[m + 3] = d.cost[ql];
+        }
     } else {
-        const int i0 = q - d.n;
-        for (int p = threadIdx.x; p < k; p += 1024) d.aR[p] = d.Rl[p] == i0 ? 1.0 : 0.0;
+        for (int i = threadIdx.x; i < m + 4; i += 256) d.pkt[i] = 0.0;
     }
+    if (threadIdx.x == 0) entering_chosen(d, best);
+}
+
+// after the all-reduce of pkt: a_R from the exchanged column
+__global__ void __launch_bounds__(1024) k_select_finish(Dev d) {
+    const DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    gather_aR(d, c->q, d.pkt);
 }
 
 // ============================================================== FTRAN
@@ -601,7 +675,7 @@ __global__ void __launch_bounds__(256) k_ftran_zr(Dev d, int nrt) {
     __shared__ double red[4];
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
-    const int m = d.m, n = d.n, k = c->k, q = c->q, bland = c->bland;
+    const int m = d.m, k = c->k, q = c->q, bland = c->bland;
     const double sig = c->sig, ptol = c->tol_primal, pivtol = c->tol_pivot;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -643,7 +717,9 @@ __global__ void __launch_bounds__(256) k_ftran_zr(Dev d, int nrt) {
                 if (u >= 0) {
                     double z = 0.0;
                     for (int ch = 0; ch < nch; ++ch) z = z + zp[ch * 64 + lane];
-                    const double aiq = q < n ? d.A[(size_t)q * mm + i] : (i == q - n ? 1.0 : 0.0);
+                    const double aiq = q >= d.N ? (i == q - d.N ? 1.0 : 0.0)
+                                       : d.sharded ? d.pkt[i]
+                                                     : d.A[(size_t)(q - d.col0) * mm + i];
                     const double alU = unit_sign(d, u, i) * (aiq - z);
                     d.alU[i] = alU;
                     ge = sig * alU;
@@ -720,24 +796,26 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk) {
     __shared__ Plan s_plan;
     DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
-    const int m = d.m, n = d.n, k = c->k, q = c->q, ny = c->ny, ncand = c->ncand;
+    const int m = d.m, k = c->k, q = c->q, ny = c->ny, ncand = c->ncand;
     const double sig = c->sig;
     const int bland = c->bland;
     const int tid = threadIdx.x;
     const int last = k - 1;
     // ---- parallel prefetch of bookkeeping scalars
+    const int ql = loc_of(d, q);  // -1: the entering column lives on another shard
     if (tid < SC_N + SI_N) {
-        const int i0 = q - n;
+        const int i0 = q - d.N;
+        const bool pk = ql < 0 || (d.sharded && q < d.N);  // from the exchanged packet
         switch (tid) {
-            case SC_LBQ: sc[SC_LBQ] = d.lb[q]; break;
-            case SC_UBQ: sc[SC_UBQ] = d.ub[q]; break;
-            case SC_XVQ: sc[SC_XVQ] = d.xval[q]; break;
-            case SC_CQ: sc[SC_CQ] = d.cost[q]; break;
+            case SC_LBQ: sc[SC_LBQ] = pk ? d.pkt[m] : d.lb[ql]; break;
+            case SC_UBQ: sc[SC_UBQ] = pk ? d.pkt[m + 1] : d.ub[ql]; break;
+            case SC_XVQ: sc[SC_XVQ] = pk ? d.pkt[m + 2] : d.xval[ql]; break;
+            case SC_CQ: sc[SC_CQ] = pk ? d.pkt[m + 3] : d.cost[ql]; break;
             case SC_SLL: sc[SC_SLL] = 0.0; break;
             case SC_CSL: sc[SC_CSL] = last >= 0 ? d.cS[last] : 0.0; break;
             case SC_SLOL: sc[SC_SLOL] = last >= 0 ? d.slo[last] : 0.0; break;
             case SC_SHIL: sc[SC_SHIL] = last >= 0 ? d.shi[last] : 0.0; break;
-            case SC_N + SI_VSQ: si[SI_VSQ] = d.vstat[q]; break;
+            case SC_N + SI_VSQ: si[SI_VSQ] = ql >= 0 ? d.vstat[ql] : VS_LOWER; break;
             case SC_N + SI_RPOS0: si[SI_RPOS0] = i0 >= 0 ? d.rpos[i0] : -1; break;
             case SC_N + SI_YPOS0: si[SI_YPOS0] = i0 >= 0 ? d.ypos[i0] : -1; break;
             case SC_N + SI_YLAST: si[SI_YLAST] = ny > 0 ? d.Yl[ny - 1] : -1; break;
@@ -815,12 +893,14 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk) {
     }
     if (action == ACT_FLIP) {
         if (tid == 0) {
-            if (si[SI_VSQ] == VS_LOWER) {
-                d.vstat[q] = VS_UPPER;
-                d.xval[q] = ubq;
-            } else {
-                d.vstat[q] = VS_LOWER;
-                d.xval[q] = lbq;
+            if (ql >= 0) {  // the shard that stores q's status
+                if (si[SI_VSQ] == VS_LOWER) {
+                    d.vstat[ql] = VS_UPPER;
+                    d.xval[ql] = ubq;
+                } else {
+                    d.vstat[ql] = VS_LOWER;
+                    d.xval[ql] = lbq;
+                }
             }
             c->flips++;
             c->ndegen = 0;
@@ -854,17 +934,18 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk) {
         const int lpos = best.e < m ? -1 : best.e - m;
         const double xq = sc[SC_XVQ] + sig * theta;
         const bool at_lower = best.g > 0.0;
-        const bool leave_art = lv >= n + m;
+        const bool leave_art = lv >= d.N + m;
+        const int lvl = loc_of(d, lv);
         if (leave_art) {
-            d.lb[lv] = 0.0;
-            d.ub[lv] = 0.0;
-            d.vstat[lv] = VS_FIXED;
-            d.xval[lv] = 0.0;
-        } else {
-            d.vstat[lv] = best.l == best.u ? VS_FIXED : at_lower ? VS_LOWER : VS_UPPER;
-            d.xval[lv] = at_lower ? best.l : best.u;
+            d.lb[lvl] = 0.0;
+            d.ub[lvl] = 0.0;
+            d.vstat[lvl] = VS_FIXED;
+            d.xval[lvl] = 0.0;
+        } else if (lvl >= 0) {  // a structural of another shard keeps no status here
+            d.vstat[lvl] = best.l == best.u ? VS_FIXED : at_lower ? VS_LOWER : VS_UPPER;
+            d.xval[lvl] = at_lower ? best.l : best.u;
         }
-        d.vstat[q] = VS_BASIC;
+        if (ql >= 0) d.vstat[ql] = VS_BASIC;
         const double cq = sc[SC_CQ];
         Plan P;
         P.action = ACT_PIVOT;
@@ -880,14 +961,12 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk) {
         P.piv = 0.0;
         int nny = ny;
         int newk = k;
-        if (q < n) {
+        if (q < d.N) {
             if (lpos >= 0) {  // case A
                 P.pcase = PC_A;
                 P.p = lpos;
                 P.piv = best.g * sig;  // alS[lpos]
-                d.spos[lv] = -1;
                 d.Sl[lpos] = q;
-                d.spos[q] = lpos;
                 d.cS[lpos] = cq;
                 d.slo[lpos] = lbq;
                 d.shi[lpos] = ubq;
@@ -901,7 +980,6 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk) {
                 d.Rl[k] = i;
                 d.rpos[i] = k;
                 d.Sl[k] = q;
-                d.spos[q] = k;
                 d.cS[k] = cq;
                 d.slo[k] = lbq;
                 d.shi[k] = ubq;
@@ -916,7 +994,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk) {
                 }
             }
         } else {
-            const int i0 = q - n;
+            const int i0 = q - d.N;
             const int a = si[SI_RPOS0];
             if (a < 0) {  // case E
                 P.pcase = PC_E;
@@ -929,9 +1007,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk) {
                 P.last = last;
                 P.piv = d.Minv[(size_t)b * d.ldm + a];
                 if (b != last) {
-                    const int sl = si[SI_SLLAST];
-                    d.Sl[b] = sl;
-                    d.spos[sl] = b;
+                    d.Sl[b] = si[SI_SLLAST];
                     d.cS[b] = sc[SC_CSL];
                     d.slo[b] = sc[SC_SLOL];
                     d.shi[b] = sc[SC_SHIL];
@@ -941,7 +1017,6 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk) {
                     d.Rl[a] = rl;
                     d.rpos[rl] = a;
                 }
-                d.spos[lv] = -1;  // lv != S_last whenever b != last
                 d.rpos[i0] = -1;
                 newk = k - 1;
             } else {  // case D
@@ -1102,7 +1177,8 @@ __global__ void __launch_bounds__(256) k_update(Dev d, int nb_minv) {
     for (int64_t t = t0; t < d.m; t += tstride) {
         if (P.pcase == PC_A || P.pcase == PC_B) {
             const int pos = P.pcase == PC_A ? P.p : k;
-            d.AS[(size_t)pos * m + t] = d.A[(size_t)P.q * m + t];
+            d.AS[(size_t)pos * m + t] =
+                d.sharded ? d.pkt[t] : d.A[(size_t)(P.q - d.col0) * m + t];
         } else if (P.pcase == PC_C && P.b != P.last) {
             d.AS[(size_t)P.b * m + t] = d.AS[(size_t)P.last * m + t];
         }
@@ -1204,7 +1280,7 @@ __global__ void k_gj_final(Dev d, int k, const double* __restrict__ W) {
 __global__ void k_refactor_rhs(Dev d) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= d.m) return;
-    double r = d.b[i] - row_activity(d, i, *d.nzcount);
+    double r = d.b[i] - d.ract[i];
     if (d.vstat[d.n + i] != VS_BASIC) r = r - d.xval[d.n + i];
     d.rhs[i] = r;
     const int p = d.rpos[i];
@@ -1283,7 +1359,7 @@ __global__ void k_phase2(Dev d) {
         d.cost[av] = 0.0;
         d.lb[av] = 0.0;
         d.ub[av] = 0.0;
-        if (d.cover[t] == av) {
+        if (d.cover[t] == d.N + d.m + t) {
             d.rlo[t] = 0.0;
             d.rhi[t] = 0.0;
         }
@@ -1293,13 +1369,22 @@ __global__ void k_phase2(Dev d) {
 // c_S after the phase-2 costs are in place
 __global__ void k_phase2_cS(Dev d) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p < d.ctl->k) d.cS[p] = d.cost[d.Sl[p]];
+    if (p < d.ctl->k) {
+        const double o = d.objg[d.Sl[p]];
+        d.cS[p] = d.maximize ? -o : o;
+    }
 }
 
 __global__ void k_extract(Dev d, double* __restrict__ xout) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= d.n) return;
-    xout[j] = d.vstat[j] == VS_BASIC ? d.xs[d.spos[j]] : d.xval[j];
+    xout[j] = d.xval[j];  // basic columns are overwritten by k_extract_basic
+}
+__global__ void k_extract_basic(Dev d, double* __restrict__ xout) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= d.ctl->k) return;
+    const int64_t j = (int64_t)d.Sl[p] - d.col0;
+    if (j >= 0 && j < d.n) xout[j] = d.xs[p];
 }
 
 // ============================================================== launchers
@@ -1318,10 +1403,23 @@ hipError_t launch_generate(const Dev& d, uint64_t seed, int64_t col0, int64_t n_
     return hipGetLastError();
 }
 
-hipError_t launch_init(const Dev& d, const double* lo, const double* up, const double* rhs,
-                       hipStream_t st) {
+hipError_t launch_init_cols(const Dev& d, const double* lo, const double* up, hipStream_t st) {
     k_init_cols<<<cdiv(d.n, 256), 256, 0, st>>>(d, lo, up);
     k_nzlist<<<1, 1024, 0, st>>>(d);
+    return hipGetLastError();
+}
+
+hipError_t launch_nzlist(const Dev& d, hipStream_t st) {
+    k_nzlist<<<1, 1024, 0, st>>>(d);
+    return hipGetLastError();
+}
+
+hipError_t launch_row_chain(const Dev& d, hipStream_t st) {
+    if (d.m > 0) k_row_chain<<<cdiv(d.m, 256), 256, 0, st>>>(d);
+    return hipGetLastError();
+}
+
+hipError_t launch_init_rows(const Dev& d, const double* rhs, hipStream_t st) {
     if (d.m > 0) {
         k_init_rows<<<cdiv(d.m, 256), 256, 0, st>>>(d, rhs);
         k_init_Y<<<1, 1024, 0, st>>>(d);
@@ -1333,8 +1431,8 @@ hipError_t launch_init(const Dev& d, const double* lo, const double* up, const d
     return hipGetLastError();
 }
 
-hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStream_t st,
-                            hipEvent_t ev0, hipEvent_t ev1) {
+static hipError_t launch_btran_price(const Dev& d, int k_ub, int phase, hipStream_t st,
+                                     hipEvent_t ev0, hipEvent_t ev1) {
     const int m = d.m;
     const double* tv = d.cS;
     if (phase == 1) {
@@ -1350,11 +1448,14 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
         k_btran<<<g, 256, 0, st>>>(d, phase, tv);
     }
     const unsigned ntiles = cdiv(d.n, TILE_COLS);
-    (void)ny_ub;
     if (ev0) (void)hipEventRecord(ev0, st);
     k_price<<<ntiles, PRICE_THREADS, 0, st>>>(d);
     if (ev1) (void)hipEventRecord(ev1, st);
-    k_select<<<1, 1024, 0, st>>>(d, (int)ntiles);
+    return hipGetLastError();
+}
+
+hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t st) {
+    const int m = d.m;
     if (k_ub > 0) k_ftran_bump<<<cdiv(k_ub, 4), 256, 0, st>>>(d, d.aR, d.alS, 1);
     const int nrt = (int)cdiv(m > 0 ? m : 1, 64);
     const int nbt = (int)cdiv(k_ub, 256);
@@ -1384,6 +1485,34 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
         if (nb_copy > 1024) nb_copy = 1024;
         k_update<<<nb_minv + nb_copy, 256, 0, st>>>(d, (int)nb_minv);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStream_t st,
+                            hipEvent_t ev0, hipEvent_t ev1) {
+    (void)ny_ub;
+    hipError_t e = launch_btran_price(d, k_ub, phase, st, ev0, ev1);
+    if (e != hipSuccess) return e;
+    k_select<<<1, 1024, 0, st>>>(d, (int)cdiv(d.n, TILE_COLS));
+    return launch_iteration_tail(d, k_ub, phase, st);
+}
+
+hipError_t launch_iteration_head(const Dev& d, int k_ub, int ny_ub, int phase, int rank,
+                                 hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+    (void)ny_ub;
+    hipError_t e = launch_btran_price(d, k_ub, phase, st, ev0, ev1);
+    if (e != hipSuccess) return e;
+    k_select_local<<<1, 1024, 0, st>>>(d, (int)cdiv(d.n, TILE_COLS), rank);
+    return hipGetLastError();
+}
+
+hipError_t launch_select_global(const Dev& d, hipStream_t st) {
+    k_select_global<<<1, 256, 0, st>>>(d);
+    return hipGetLastError();
+}
+
+hipError_t launch_select_finish(const Dev& d, hipStream_t st) {
+    k_select_finish<<<1, 1024, 0, st>>>(d);
     return hipGetLastError();
 }
 
@@ -1418,7 +1547,6 @@ hipError_t launch_refactor_gj(const Dev& d, int k, hipStream_t st) {
 }
 
 hipError_t launch_refactor_primal(const Dev& d, int k, hipStream_t st) {
-    k_nzlist<<<1, 1024, 0, st>>>(d);
     if (d.m > 0) {
         k_refactor_rhs<<<cdiv(d.m, 256), 256, 0, st>>>(d);
         if (k > 0) {
@@ -1440,6 +1568,7 @@ hipError_t launch_phase2(const Dev& d, hipStream_t st) {
 
 hipError_t launch_extract(const Dev& d, double* xout, hipStream_t st) {
     k_extract<<<cdiv(d.n, 256), 256, 0, st>>>(d, xout);
+    if (d.m > 0) k_extract_basic<<<cdiv(d.m, 256), 256, 0, st>>>(d, xout);
     return hipGetLastError();
 }
 

@@ -103,8 +103,16 @@ class Problem:
         self._trace_cap = int(capacity)
 
     def comm_init(self, unique_id: bytes, world_size: int, rank: int) -> None:
+        """RCCL transport: one process per GPU (see easylp_amd.dist.share_unique_id)."""
         buf = ctypes.create_string_buffer(bytes(unique_id), 128)
         check(self._lib.elp_comm_init(self._h, buf, int(world_size), int(rank)), "elp_comm_init")
+
+    def comm_init_host(self, transport) -> None:
+        """Host-callback transport (easylp_amd.dist.TorchDistTransport)."""
+        self._transport = transport  # keeps the ctypes thunks alive
+        check(self._lib.elp_comm_init_host(self._h, transport.world, transport.rank,
+                                           transport.c_allgather, transport.c_allreduce,
+                                           transport.c_bcast, None), "elp_comm_init_host")
 
     def load_dense(self, A, dirs, rhs, obj, lo=None, up=None, maximize=False) -> None:
         m, n = self.m, self.n

@@ -18,6 +18,7 @@
 #ifndef EASYLP_HIP_H
 #define EASYLP_HIP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -147,6 +148,16 @@ int elp_get_trace(elp_handle* h, int64_t* pairs, int64_t capacity, int64_t* coun
  * elp_load_*.  Rank r then owns columns [r*n/P, (r+1)*n/P). */
 int elp_comm_unique_id(uint8_t id[128]);
 int elp_comm_init(elp_handle* h, const uint8_t id[128], int32_t world_size, int32_t rank);
+
+/* Same sharded algorithm over caller-provided host transports instead of RCCL
+ * (every rank may then share one GPU; used by the multi-rank tests).  Buffers
+ * are host memory; return 0 on success.  allgather: recv holds world*bytes.
+ * allreduce dtype: 0 = float64 sum, 1 = int32 max. */
+typedef int (*elp_host_allgather_fn)(const void* send, void* recv, size_t bytes, void* user);
+typedef int (*elp_host_allreduce_fn)(void* buf, size_t count, int32_t dtype, void* user);
+typedef int (*elp_host_bcast_fn)(void* buf, size_t bytes, int32_t root, void* user);
+int elp_comm_init_host(elp_handle* h, int32_t world_size, int32_t rank, elp_host_allgather_fn ag,
+                       elp_host_allreduce_fn ar, elp_host_bcast_fn bc, void* user);
 
 /* R finalizer for self$pointer (R/class.R:300; EasyLP's finalize at
  * R/class.R:497-501 is empty, this one frees device memory). */
