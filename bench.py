@@ -69,6 +69,22 @@ def cpu_baseline(args):
     }
 
 
+def committed_traffic(args):
+    """HBM traffic per pricing launch from the committed rocprofv3 --pmc FETCH_SIZE
+    pass of this same command (tools/gpu_check.sh -> profiles/pmc_traffic.json);
+    only used when that pass measured the same LP and iteration window."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        t = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    same = (t.get("m"), t.get("n"), t.get("warmup"), t.get("steps")) == (
+        args.m, args.n, args.warmup, args.steps)
+    if not same:
+        return None, None
+    return t["traffic_bytes_per_launch"], "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE, x2 gfx950)"
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -141,6 +157,8 @@ def main():
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             tto = float(tt.item())
 
+    traffic, traffic_src = committed_traffic(args) if world == 1 else (None, None)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args)
@@ -174,7 +192,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "bytes_per_launch": price_b / price_n if price_n else price_dev_bytes,
                 "avg_launch_us": 1e6 * price_s / price_n if price_n else None,
                 "launches_timed": price_n,

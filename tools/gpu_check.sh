@@ -27,7 +27,7 @@ cat "$OUT/bench_$TAG.json"
 
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- python3 "$ROOT/bench.py" --steps "$STEPS" --no-cpu > "$OUT/prof_bench_$TAG.json" 2> "$OUT/prof_bench_$TAG.err" || { echo "rocprof failed rc=$?"; tail -20 "$OUT/prof_bench_$TAG.err"; exit 5; }
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_price --output-format csv -d "$OUT/pmc_$TAG" -o run -- python3 "$ROOT/bench.py" --steps 300 --warmup 100 --no-cpu --no-optimal --profile-price 0 > "$OUT/pmc_bench_$TAG.json" 2> "$OUT/pmc_bench_$TAG.err" || { echo "rocprof pmc failed rc=$?"; tail -20 "$OUT/pmc_bench_$TAG.err"; exit 6; }
-python3 "$ROOT/tools/pmc_traffic.py" "$OUT/pmc_$TAG/run_counter_collection.csv" "$OUT/pmc_bench_$TAG.json" 100 300 > "$OUT/pmc_traffic_$TAG.json" && cat "$OUT/pmc_traffic_$TAG.json"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_price --output-format csv -d "$OUT/pmc_$TAG" -o run -- python3 "$ROOT/bench.py" --steps "$STEPS" --warmup 100 --no-cpu --no-optimal --profile-price 0 > "$OUT/pmc_bench_$TAG.json" 2> "$OUT/pmc_bench_$TAG.err" || { echo "rocprof pmc failed rc=$?"; tail -20 "$OUT/pmc_bench_$TAG.err"; exit 6; }
+python3 "$ROOT/tools/pmc_traffic.py" "$OUT/pmc_$TAG/run_counter_collection.csv" "$OUT/pmc_bench_$TAG.json" 100 "$STEPS" > "$OUT/pmc_traffic_$TAG.json" && cat "$OUT/pmc_traffic_$TAG.json"
 find "$OUT/prof_$TAG" "$OUT/pmc_$TAG" -name "*.csv" | head -20
 echo done

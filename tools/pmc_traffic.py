@@ -20,6 +20,10 @@ def main(csv_path, bench_json, warmup, steps):
     b = json.loads(open(bench_json).read().strip().splitlines()[-1])
     alg = b["roofline"]["bytes_per_launch"]
     out = {
+        "warmup": warmup,
+        "steps": steps,
+        "m": b["config"]["m"],
+        "n": b["config"]["n"],
         "launches": len(win),
         "traffic_bytes_per_launch": sum(fetch) / len(fetch),
         "algorithmic_bytes_per_launch": alg,
