@@ -12,6 +12,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -69,6 +70,7 @@ struct elp_handle {
     elp::Comm comm;  // multi-GPU (world 1 = no-op)
     std::vector<hipEvent_t> ev;  // pricing-kernel timing pairs (profile mode)
     int32_t* d_flag = nullptr;   // one int for cross-rank decisions
+    int64_t ar_rows = 0;         // AR capacity in rows (grown at polls)
 };
 
 extern "C" void elp_default_control(elp_control* c) {
@@ -161,7 +163,11 @@ static int alloc_all(elp_handle* h) {
     auto A = [&](hipError_t x) {
         if (e == hipSuccess) e = x;
     };
-    A(dalloc(&d.AR, (size_t)mm * (size_t)d.ldr));
+    // AR holds only the |Y| live rows: start small, grow at polls (ensure_ar)
+    h->ar_rows = std::min<int64_t>(mm, 1024);
+    if (const char* e = std::getenv("ELP_AR_INIT_ROWS"))  // test hook: force growth
+        h->ar_rows = std::max<int64_t>(1, std::min<int64_t>(mm, std::atoll(e)));
+    A(dalloc(&d.AR, (size_t)h->ar_rows * (size_t)d.ldr));
     A(dalloc(&d.AS, (size_t)mm * (size_t)mm));
     A(dalloc(&d.Minv, (size_t)mm * (size_t)mm));
     A(dalloc(&d.MinvT, (size_t)mm * (size_t)mm));
@@ -218,8 +224,8 @@ static int alloc_all(elp_handle* h) {
         return fail(ELP_E_NOMEM, std::string("device allocation failed: ") + hipGetErrorString(e));
     }
     A(hipHostMalloc((void**)&h->hctl, sizeof(DevCtl)));
-    // AR padding columns must read as zeros; Minv / AS / work start clean
-    A(hipMemsetAsync(d.AR, 0, (size_t)mm * (size_t)d.ldr * sizeof(double), h->st));
+    // (AR padding columns [n, ldr) are read by the 128-column tiles but their
+    //  results are discarded, so AR needs no clearing); Minv / work start clean
     A(hipMemsetAsync(d.Minv, 0, (size_t)mm * (size_t)mm * sizeof(double), h->st));
     A(hipMemsetAsync(d.MinvT, 0, (size_t)mm * (size_t)mm * sizeof(double), h->st));
     A(hipMemsetAsync(d.zpart, 0, (size_t)mm * ((mm + ZCHUNK - 1) / ZCHUNK) * sizeof(double), h->st));
@@ -227,6 +233,23 @@ static int alloc_all(elp_handle* h) {
         free_dev(h);
         return fail(ELP_E_HIP, std::string("device init failed: ") + hipGetErrorString(e));
     }
+    return 0;
+}
+
+// Grow AR to hold at least `rows` Y rows (device idle: called at a poll).
+static int ensure_ar(elp_handle* h, int64_t rows) {
+    rows = std::min<int64_t>(rows, std::max<int64_t>(h->m, 1));
+    if (rows <= h->ar_rows) return 0;
+    const int64_t cap = std::min<int64_t>(std::max<int64_t>(h->m, 1), std::max(rows, 2 * h->ar_rows));
+    double* nr = nullptr;
+    if (hipMalloc((void**)&nr, (size_t)cap * (size_t)h->d.ldr * sizeof(double)) != hipSuccess)
+        return fail(ELP_E_NOMEM, "AR growth failed");
+    HIPCHK(hipMemcpyAsync(nr, h->d.AR, (size_t)h->ar_rows * (size_t)h->d.ldr * sizeof(double),
+                          hipMemcpyDeviceToDevice, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    (void)hipFree(h->d.AR);
+    h->d.AR = nr;
+    h->ar_rows = cap;
     return 0;
 }
 
@@ -331,6 +354,11 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
     HIPCHK(launch_init_rows(d, drhs, h->st));
     HIPCHK(hipMemcpyAsync(h->hctl, d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
     HIPCHK(hipStreamSynchronize(h->st));
+    {
+        const int rc = ensure_ar(h, (int64_t)h->hctl->ny + 64);
+        if (rc) return rc;
+    }
+    HIPCHK(launch_fill_AR(h->d, h->st));
     (void)hipFree(dlo);
     (void)hipFree(dup);
     (void)hipFree(drhs);
@@ -534,6 +562,8 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
         }
         const int k0 = c->k, ny0 = c->ny;
         int chunk = h->ctl.sync_every;
+        rc = ensure_ar(h, (int64_t)ny0 + chunk + 1);  // |Y| grows by <= 1 per iteration
+        if (rc) return rc;
         const int to_refactor = period - c->since_refactor;
         if (to_refactor > 0 && to_refactor < chunk) chunk = to_refactor;
         const int64_t left = c->iter_stop - c->iter;

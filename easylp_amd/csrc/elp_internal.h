@@ -87,7 +87,7 @@ struct Dev {
     int64_t ldm;   // Minv leading dimension (= max(m,1))
     int64_t ldr;   // AR leading dimension (n rounded up to TILE_COLS)
     const double* A;  // column-major m x n
-    double* AR;       // Y rows, row-major (m x ldr capacity)
+    double* AR;       // Y rows, row-major (capacity grown on demand, <= m rows)
     double* AS;       // basic structural columns, column-major (m x m capacity)
     double* Minv;     // bump inverse, row-major ldm x ldm
     double* MinvT;    // its transpose (BTRAN and B^-1 rows read rows of it)
@@ -119,6 +119,7 @@ hipError_t launch_generate(const Dev& d, uint64_t seed, int64_t col0, int64_t n_
 // init in two parts: columns (+ nonzero list), then rows once ract is complete
 hipError_t launch_init_cols(const Dev& d, const double* lo, const double* up, hipStream_t st);
 hipError_t launch_init_rows(const Dev& d, const double* rhs, hipStream_t st);
+hipError_t launch_fill_AR(const Dev& d, hipStream_t st);  // AR rows for the initial Y
 // ev0/ev1 (may be null): events recorded around the pricing kernel
 hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStream_t st,
                             hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);

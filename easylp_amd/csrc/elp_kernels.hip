@@ -1409,6 +1409,14 @@ hipError_t launch_init_cols(const Dev& d, const double* lo, const double* up, hi
     return hipGetLastError();
 }
 
+hipError_t launch_fill_AR(const Dev& d, hipStream_t st) {
+    if (d.m > 0) {
+        dim3 g(cdiv(d.n, 256), (unsigned)(d.m < 4096 ? d.m : 4096));
+        k_fill_AR<<<g, 256, 0, st>>>(d);
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_nzlist(const Dev& d, hipStream_t st) {
     k_nzlist<<<1, 1024, 0, st>>>(d);
     return hipGetLastError();
@@ -1423,8 +1431,6 @@ hipError_t launch_init_rows(const Dev& d, const double* rhs, hipStream_t st) {
     if (d.m > 0) {
         k_init_rows<<<cdiv(d.m, 256), 256, 0, st>>>(d, rhs);
         k_init_Y<<<1, 1024, 0, st>>>(d);
-        dim3 g(cdiv(d.n, 256), (unsigned)(d.m < 4096 ? d.m : 4096));
-        k_fill_AR<<<g, 256, 0, st>>>(d);
     } else {
         k_init_Y<<<1, 1024, 0, st>>>(d);
     }

@@ -172,3 +172,16 @@ def test_large_bump_vs_oracle(gpu):
     assert o.stats["bump_dim"] > 256, o.stats
     _cmp(g, o)
     np.testing.assert_array_equal(g.trace, o.trace)
+
+
+def test_ar_growth_during_solve(gpu, monkeypatch):
+    """The Y-row copy AR starts at 8 rows and is grown at polls while |Y| rises."""
+    from oracle import generate_dense, solve_dense as orc
+    monkeypatch.setenv("ELP_AR_INIT_ROWS", "8")
+    m, n = 300, 1200
+    A, b, c = generate_dense(21, m, n)
+    g = gpu.solve_dense(A, np.ones(m, np.int32), b, c, maximize=True, trace=100000, sync_every=5)
+    o = orc(A, np.ones(m, np.int32), b, c, maximize=True, trace_cap=100000)
+    assert o.stats["y_rows"] > 16
+    _cmp(g, o)
+    np.testing.assert_array_equal(g.trace, o.trace)
