@@ -201,7 +201,7 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.alS, mm));
     A(dalloc(&d.alU, mm));
     A(dalloc(&d.zz, mm));
-    A(dalloc(&d.zpart, (size_t)mm * (size_t)((mm + ZCHUNK - 1) / ZCHUNK)));
+    A(dalloc(&d.zpart, (size_t)(mm + 64) * (size_t)((mm + ZCHUNK - 1) / ZCHUNK)));
     A(dalloc(&d.vrow, mm));
     A(dalloc(&d.vvec, mm));
     A(dalloc(&d.colA, mm));
@@ -228,7 +228,7 @@ static int alloc_all(elp_handle* h) {
     //  results are discarded, so AR needs no clearing); Minv / work start clean
     A(hipMemsetAsync(d.Minv, 0, (size_t)mm * (size_t)mm * sizeof(double), h->st));
     A(hipMemsetAsync(d.MinvT, 0, (size_t)mm * (size_t)mm * sizeof(double), h->st));
-    A(hipMemsetAsync(d.zpart, 0, (size_t)mm * ((mm + ZCHUNK - 1) / ZCHUNK) * sizeof(double), h->st));
+
     if (e != hipSuccess) {
         free_dev(h);
         return fail(ELP_E_HIP, std::string("device init failed: ") + hipGetErrorString(e));

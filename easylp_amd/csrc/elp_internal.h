@@ -27,7 +27,7 @@ enum : int32_t { PC_NONE = 0, PC_A = 1, PC_B = 2, PC_C = 3, PC_D = 4, PC_E = 5 }
 enum : int32_t { ACT_NONE = 0, ACT_FLIP = 1, ACT_PIVOT = 2 };
 
 constexpr int PRICE_SPLIT = 8;  // slot chunks per pricing tile (one per wave)
-constexpr int ZCHUNK = 64;      // bump positions per FTRAN-z partial
+constexpr int ZCHUNK = 32;      // bump positions per FTRAN-z partial
 constexpr int TILE_COLS = 128;  // columns per pricing workgroup (2 per lane)
 
 struct Plan {
@@ -59,6 +59,8 @@ struct DevCtl {
     int64_t price_passes;
     unsigned long long ns_emax_bits;  // max|I - M Minv| of the last refactor (bits of a double >= 0)
     int32_t ncand, pad2;              // Harris pass-2 candidate count (k_ftran_zr)
+    int32_t snap_k, snap_bland;       // k, bland as k_ratio's workgroups must see them
+                                      // (workgroup 0 rewrites k / bland meanwhile)
 };
 
 // Harris pass-2 candidate (a superset of the global candidates: exact ratio
@@ -130,7 +132,8 @@ hipError_t launch_iteration_head(const Dev& d, int k_ub, int ny_ub, int phase, i
                                  hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_select_global(const Dev& d, hipStream_t st);
 hipError_t launch_select_finish(const Dev& d, hipStream_t st);
-hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t st);
+hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t st,
+                                 bool bump_ftran = true);
 // row activities: ract = chain(ract, local nonzero nonbasic columns)
 hipError_t launch_row_chain(const Dev& d, hipStream_t st);
 // refactor = ns_resid; (host reads ns_emax) ns_update | gauss_jordan; primal

@@ -1,14 +1,16 @@
 // elp_kernels.hip -- gfx950 kernels of the dense revised simplex.
 //
-// One simplex iteration is seven launches on one stream:
-//   k_btran       y_R = Minv^T c_S (+ loop-top checks)             O(k^2)
-//   k_price       d_j = c_j - AR[:,j]^T y_Y, fused Dantzig argmax    O(|Y| n)  <- HBM sweep
-//   k_select      entering column q (min-loc over tiles + slacks)   O(n/128 + m)
-//   k_ftran_bump  alpha_S = Minv a_R(q)   (one wave per row)         O(k^2)
-//   k_ftran_z     z = AS alpha_S, chunked partials                   O(m k)
-//   k_ratio       Harris two-pass ratio test, primal update, plan    O(m)
-//   k_rowminv     row of B^-1 for cases B/D                          O(k^2)
-//   k_update      Minv rank-one / bordered update + AS / AR copies    O(k^2 + n)
+// One simplex iteration is six launches on one stream:
+//   k_btran        loop-top checks; y_R = Minv^T c_S, one wave per row   O(k^2)
+//   k_price        d_j = c_j - AR[:,j]^T y_Y + Dantzig argmin per tile    O(|Y| n)  <- the HBM sweep
+//   k_select_ftran min-loc over tiles + slacks (every workgroup), then
+//                  alpha_S = Minv a_R(q), one wave per bump row           O(k^2)
+//   k_ftran_zr     alpha on covered rows (z = AS alpha_S, chunked) fused
+//                  with Harris pass 1 and pass-2 candidate emission       O(m k)
+//   k_ratio        Harris pass 2, pivot plan, row of B^-1 (cases B/D)     O(k^2)
+//   k_update       Minv/MinvT update, x_B update, AS / AR copies          O(k^2 + n)
+// Sharded runs split k_select_ftran into k_select_local / (all-gather) /
+// k_select_global / (all-reduce) / k_select_finish + k_ftran_bump.
 // Every fp reduction follows the order of oracle/elp_oracle.c (explicit fma,
 // built with -ffp-contract=off), so the pivot sequence is the oracle's.
 // Kernels read the device control block and return early unless the loop is
@@ -531,6 +533,69 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles) {
     gather_aR(d, q, q < d.N ? d.A + (size_t)(q - d.col0) * (size_t)d.m : nullptr);
 }
 
+// One GPU, fused select + FTRAN on the bump: every workgroup reduces the tile and
+// slack candidates itself (a total order: all agree), gathers a_R into LDS and
+// computes alpha_S for its 4 bump rows (one wave per row, wave order).
+// Workgroup 0 publishes q.  Saves a launch and the single-workgroup select.
+__global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles) {
+    extern __shared__ __attribute__((aligned(16))) double aRs[];  // [k]
+    __shared__ Cand red[4];
+    DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    const int bland = c->bland, ny = c->ny, k = c->k;
+    Cand best;
+    best.j = -1;
+    best.score = 0.0;
+    best.d = 0.0;
+    for (int t = threadIdx.x; t < ntiles; t += 256) {
+        const Cand o = d.cand[t];
+        if (cand_better(o, best, bland)) best = o;
+    }
+    const double dtol = c->tol_dual;
+    for (int p = threadIdx.x; p < ny; p += 256) {
+        const int i = d.Yl[p];
+        const int jl = d.n + i;
+        const int8_t vs = d.vstat[jl];
+        if (vs == VS_FIXED) continue;
+        const double dj = d.cost[jl] - d.yy[p];
+        Cand o;
+        o.j = -1;
+        if ((vs == VS_LOWER || vs == VS_FREE) && dj < -dtol) {
+            o.j = d.N + i;
+            o.score = -dj;
+            o.d = dj;
+        } else if ((vs == VS_UPPER || vs == VS_FREE) && dj > dtol) {
+            o.j = d.N + i;
+            o.score = dj;
+            o.d = dj;
+        }
+        if (cand_better(o, best, bland)) best = o;
+    }
+    best = block_best<256>(best, bland, red);
+    if (best.j < 0) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) c->status = ST_PHASE_OPT;
+        return;
+    }
+    const int q = (int)best.j;
+    if (blockIdx.x == 0 && threadIdx.x == 0) entering_chosen(d, best);
+    if (q < d.N) {
+        const double* col = d.A + (size_t)(q - d.col0) * (size_t)d.m;
+        for (int p = threadIdx.x; p < k; p += 256) aRs[p] = col[d.Rl[p]];
+    } else {
+        const int i0 = q - d.N;
+        for (int p = threadIdx.x; p < k; p += 256) aRs[p] = d.Rl[p] == i0 ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (p >= k) return;
+    const double* row = d.Minv + (size_t)p * d.ldm;
+    double acc = 0.0;
+    for (int i = lane; i < k; i += 64) acc = fma(row[i], aRs[i], acc);
+    acc = wave_tree(acc);
+    if (lane == 0) d.alS[p] = acc;
+}
+
 __global__ void __launch_bounds__(1024) k_select_local(Dev d, int ntiles, int rank) {
     __shared__ Cand red[16];
     const DevCtl* c = d.ctl;
@@ -670,23 +735,31 @@ DEV void emit_cand(const Dev& d, int var, int e, double g, double x, double l, d
     d.rcand[slot] = cd;
 }
 
-__global__ void __launch_bounds__(256) k_ftran_zr(Dev d, int nrt) {
-    extern __shared__ __attribute__((aligned(16))) double zp[];  // [nch][64]
-    __shared__ double red[4];
+constexpr int ZR_WAVES = 8;  // waves per row tile of k_ftran_zr
+template <bool LDSZ>
+__global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt) {
+    extern __shared__ __attribute__((aligned(16))) double zlds[];  // [nch][64]
+    __shared__ double red[ZR_WAVES];
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
     const int m = d.m, k = c->k, q = c->q, bland = c->bland;
     const double sig = c->sig, ptol = c->tol_primal, pivtol = c->tol_pivot;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        d.ctl->snap_k = k;
+        d.ctl->snap_bland = bland;
+    }
     double tmin = HUGE_VAL;
     double ge = 0.0, xe = 0.0, le = 0.0, he = 0.0;
     int ve = -1;
+    // z partials of this tile's 64 rows: LDS, or (huge bumps) a private slice of zpart
+    double* zp = LDSZ ? zlds : d.zpart + (size_t)blockIdx.x * 64 * (size_t)((k + ZCHUNK - 1) / ZCHUNK);
     if ((int)blockIdx.x < nrt) {
         const int i = blockIdx.x * 64 + lane;
         const int nch = (k + ZCHUNK - 1) / ZCHUNK;
         const size_t mm = (size_t)m;
-        for (int ch = w; ch < nch; ch += 4) {
+        for (int ch = w; ch < nch; ch += ZR_WAVES) {
             const int c0 = ch * ZCHUNK, c1 = min(k, c0 + ZCHUNK);
             double acc = 0.0;
             if (i < m) {
@@ -737,7 +810,7 @@ __global__ void __launch_bounds__(256) k_ftran_zr(Dev d, int nrt) {
             emit_cand(d, ve, i, ge, xe, le, he, bmin, pivtol);
         }
     } else {
-        const int p = (blockIdx.x - nrt) * 256 + threadIdx.x;
+        const int p = (blockIdx.x - nrt) * (64 * ZR_WAVES) + threadIdx.x;
         if (p < k) {
             ge = sig * d.alS[p];
             xe = d.xs[p];
@@ -751,7 +824,8 @@ __global__ void __launch_bounds__(256) k_ftran_zr(Dev d, int nrt) {
         for (int off = 32; off >= 1; off >>= 1) bmin = fmin(bmin, __shfl_xor(bmin, off));
         if (lane == 0) red[w] = bmin;
         __syncthreads();
-        bmin = fmin(fmin(red[0], red[1]), fmin(red[2], red[3]));
+        bmin = red[0];
+        for (int ww = 1; ww < ZR_WAVES; ++ww) bmin = fmin(bmin, red[ww]);
         if (threadIdx.x == 0) d.blockmin[blockIdx.x] = bmin;
         emit_cand(d, ve, m + p, ge, xe, le, he, bmin, pivtol);
     }
@@ -784,10 +858,15 @@ DEV Leave shfl_leave(const Leave& x, int off) {
 enum { SC_LBQ, SC_UBQ, SC_XVQ, SC_CQ, SC_SLL, SC_CSL, SC_SLOL, SC_SHIL, SC_N };
 enum { SI_VSQ, SI_RPOS0, SI_YPOS0, SI_YLAST, SI_SLLAST, SI_RLLAST, SI_N };
 
-// Harris pass 2 + decision + pivot plan (one workgroup).  Pass 1 came from
-// k_ftran_zr's per-workgroup minima, the candidates from its emitted list; the
-// primal update x_B -= step * alpha runs in k_update.
-__global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk) {
+// Harris pass 2 + decision + pivot plan, fused with the B^-1 row of cases B/D.
+// Pass 1 came from k_ftran_zr's per-workgroup minima, the candidates from its
+// emitted list.  EVERY workgroup repeats the decision (same inputs, total
+// orders: all agree); workgroup 0 alone does the bookkeeping; every workgroup
+// then forms vvec for its 4 columns when a unit variable leaves.  k and bland
+// come from the snapshot (workgroup 0 rewrites them).  The primal update
+// x_B -= step * alpha runs in k_update.
+__global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int lds_row) {
+    extern __shared__ __attribute__((aligned(16))) double asrow_lds[];  // [k]: A[lrow, S]
     __shared__ double dred[4];
     __shared__ Leave lred[4];
     __shared__ double sc[SC_N];
@@ -796,9 +875,10 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk) {
     __shared__ Plan s_plan;
     DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
-    const int m = d.m, k = c->k, q = c->q, ny = c->ny, ncand = c->ncand;
+    const int m = d.m, k = c->snap_k, q = c->q, ny = c->ny, ncand = c->ncand;
     const double sig = c->sig;
-    const int bland = c->bland;
+    const int bland = c->snap_bland;
+    const bool lead = blockIdx.x == 0;
     const int tid = threadIdx.x;
     const int last = k - 1;
     // ---- parallel prefetch of bookkeeping scalars
@@ -873,7 +953,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk) {
         action = ACT_PIVOT;
         step = theta;
     }
-    if (tid == 0) {
+    if (lead && tid == 0) {
         const int64_t it = c->iter;
         c->iter = it + 1;
         if (phase == 1) c->phase1_iters++;
@@ -888,11 +968,11 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk) {
         }
     }
     if (action == ACT_NONE) {
-        if (tid == 0) c->plan.action = ACT_NONE;
+        if (lead && tid == 0) c->plan.action = ACT_NONE;
         return;
     }
     if (action == ACT_FLIP) {
-        if (tid == 0) {
+        if (lead && tid == 0) {
             if (ql >= 0) {  // the shard that stores q's status
                 if (si[SI_VSQ] == VS_LOWER) {
                     d.vstat[ql] = VS_UPPER;
@@ -920,6 +1000,29 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk) {
         }
         return;
     }
+    // ---- B^-1 row for a leaving unit variable (cases B, D; E wastes it):
+    //      vvec[c] = wave_dot(MinvT[c, 0:k], A[lrow, S]), case B / delta
+    const int lrow_all = best.e < m ? best.e : -1;
+    if (lrow_all >= 0 && k > 0) {
+        // huge bumps: every workgroup writes the same values to d.vrow (benign)
+        double* asrow = lds_row ? asrow_lds : d.vrow;
+        for (int j = tid; j < k; j += 256) asrow[j] = d.AS[(size_t)j * (size_t)m + lrow_all];
+        __syncthreads();
+        const int col = blockIdx.x * 4 + (tid >> 6);
+        const int lane = tid & 63;
+        if (col < k) {
+            const double* row = d.MinvT + (size_t)col * d.ldm;
+            double acc = 0.0;
+            for (int j = lane; j < k; j += 64) acc = fma(row[j], asrow[j], acc);
+            acc = wave_tree(acc);
+            if (lane == 0) {
+                // case B delta = acol_i - z_i = sigma_u * sig * g (exact)
+                const double delta = unit_sign(d, best.var, lrow_all) * (sig * best.g);
+                d.vvec[col] = q < d.N ? acc / delta : acc;
+            }
+        }
+    }
+    if (!lead) return;
     // ---- pivot: bookkeeping by thread 0 (stores only, plus Minv[b][a] in case C)
     if (tid == 0) {
         if (theta == 0.0) {
@@ -1071,29 +1174,9 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk) {
             d.vrow[j] = d.Minv[(size_t)P.b * d.ldm + j] / P.piv;
             d.colA[j] = d.MinvT[(size_t)P.a * d.ldm + j];
         }
-    } else if (pc == PC_D || pc == PC_B) {
-        // gathered row A[row, S] = AS[row, 0:k] for the B^-1 row kernel
-        for (int j = tid; j < k; j += 256) d.vrow[j] = d.AS[(size_t)j * (size_t)m + P.row];
-        if (pc == PC_D)
-            for (int j = tid; j < k; j += 256) d.colA[j] = d.MinvT[(size_t)P.a * d.ldm + j];
+    } else if (pc == PC_D) {
+        for (int j = tid; j < k; j += 256) d.colA[j] = d.MinvT[(size_t)P.a * d.ldm + j];
     }
-}
-
-// cases B / D: vvec[c] = wave_dot(MinvT[c, 0:k], A[row, S]); B: / delta
-__global__ void __launch_bounds__(256) k_rowminv(Dev d) {
-    const DevCtl* c = d.ctl;
-    if (c->status != ST_RUN) return;
-    const Plan P = c->plan;
-    if (P.action != ACT_PIVOT || (P.pcase != PC_B && P.pcase != PC_D)) return;
-    const int k = P.k_old;
-    const int col = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (col >= k) return;
-    const double* row = d.MinvT + (size_t)col * d.ldm;
-    double acc = 0.0;
-    for (int q = lane; q < k; q += 64) acc = fma(row[q], d.vrow[q], acc);
-    acc = wave_tree(acc);
-    if (lane == 0) d.vvec[col] = P.pcase == PC_B ? acc / P.piv : acc;
 }
 
 // new value of bump-inverse element (i, j); old(r, c) reads the pre-update matrix
@@ -1460,28 +1543,24 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int phase, hipStrea
     return hipGetLastError();
 }
 
-hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t st) {
+hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t st, bool bump_ftran) {
     const int m = d.m;
-    if (k_ub > 0) k_ftran_bump<<<cdiv(k_ub, 4), 256, 0, st>>>(d, d.aR, d.alS, 1);
+    if (bump_ftran && k_ub > 0) k_ftran_bump<<<cdiv(k_ub, 4), 256, 0, st>>>(d, d.aR, d.alS, 1);
     const int nrt = (int)cdiv(m > 0 ? m : 1, 64);
-    const int nbt = (int)cdiv(k_ub, 256);
+    const int nbt = (int)cdiv(k_ub, 64 * ZR_WAVES);
     {
-        // z partials: 512 B per chunk of 64 bump positions (k <= 16384 in 128 KiB)
+        // z partials: 512 B per chunk of ZCHUNK bump positions in LDS (<= 64 KiB,
+        // k <= 4096); larger bumps use a private slice of zpart per row tile
         const size_t lds = (size_t)cdiv(k_ub, ZCHUNK) * 64 * sizeof(double);
-        if (lds > 64 * 1024) {
-            static bool attr = false;
-            if (!attr) {
-                const hipError_t e = hipFuncSetAttribute(
-                    (const void*)k_ftran_zr, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
-                if (e != hipSuccess) return e;
-                attr = true;
-            }
-            if (lds > 128 * 1024) return hipErrorInvalidValue;
-        }
-        k_ftran_zr<<<nrt + nbt, 256, lds, st>>>(d, nrt);
+        if (lds <= 64 * 1024) k_ftran_zr<true><<<nrt + nbt, 64 * ZR_WAVES, lds, st>>>(d, nrt);
+        else k_ftran_zr<false><<<nrt + nbt, 64 * ZR_WAVES, 0, st>>>(d, nrt);
     }
-    k_ratio<<<1, 256, 0, st>>>(d, phase, nrt + nbt);
-    if (k_ub > 0) k_rowminv<<<cdiv(k_ub, 4), 256, 0, st>>>(d);
+    // ratio test + (cases B/D) B^-1 row: one workgroup per 4 bump columns
+    {
+        const size_t lds = (size_t)k_ub * sizeof(double);
+        const int lds_row = lds <= 48 * 1024;
+        k_ratio<<<cdiv(k_ub > 0 ? k_ub : 1, 4), 256, lds_row ? lds : 0, st>>>(d, phase, nrt + nbt, lds_row);
+    }
     {
         const int64_t kk = 2 * (int64_t)(k_ub + 1) * (k_ub + 1);
         unsigned nb_minv = cdiv(kk, 256);
@@ -1499,8 +1578,14 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
     (void)ny_ub;
     hipError_t e = launch_btran_price(d, k_ub, phase, st, ev0, ev1);
     if (e != hipSuccess) return e;
-    k_select<<<1, 1024, 0, st>>>(d, (int)cdiv(d.n, TILE_COLS));
-    return launch_iteration_tail(d, k_ub, phase, st);
+    const int ntiles = (int)cdiv(d.n, TILE_COLS);
+    const size_t lds = (size_t)k_ub * sizeof(double);
+    if (lds <= 48 * 1024) {  // fused select + bump FTRAN
+        k_select_ftran<<<cdiv(k_ub > 0 ? k_ub : 1, 4), 256, lds, st>>>(d, ntiles);
+        return launch_iteration_tail(d, k_ub, phase, st, false);
+    }
+    k_select<<<1, 1024, 0, st>>>(d, ntiles);
+    return launch_iteration_tail(d, k_ub, phase, st, true);
 }
 
 hipError_t launch_iteration_head(const Dev& d, int k_ub, int ny_ub, int phase, int rank,

@@ -10,7 +10,7 @@
  *            partials added in chunk order starting from 0.0 (PRICE_SPLIT)
  *   wave   : 64 lane-strided fma chains + butterfly 32,16,..,1 (wave_dot):
  *            FTRAN / BTRAN / B^-1 rows, phase-1 c_S correction, phase-1 sum
- *   zchunk : chunks of 64 bump positions, fma chain, sequential sum
+ *   zchunk : chunks of 32 bump positions, fma chain, sequential sum
  *   seq    : one fma chain in index order (row activities)
  *
  * Algorithm (bounded primal revised simplex, minimisation form):
@@ -41,7 +41,7 @@
 #define VS_FREE 3
 
 #define PRICE_SPLIT 8
-#define ZCHUNK 64
+#define ZCHUNK 32
 #define WAVE 64
 
 /* ------------------------------------------------------------------ */
