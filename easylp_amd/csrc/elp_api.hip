@@ -167,6 +167,7 @@ static int alloc_all(elp_handle* h) {
     h->ar_rows = std::min<int64_t>(mm, 1024);
     if (const char* e = std::getenv("ELP_AR_INIT_ROWS"))  // test hook: force growth
         h->ar_rows = std::max<int64_t>(1, std::min<int64_t>(mm, std::atoll(e)));
+    d.arcap = h->ar_rows;
     A(dalloc(&d.AR, (size_t)h->ar_rows * (size_t)d.ldr));
     A(dalloc(&d.AS, (size_t)mm * (size_t)mm));
     A(dalloc(&d.Minv, (size_t)mm * (size_t)mm));
@@ -244,12 +245,17 @@ static int ensure_ar(elp_handle* h, int64_t rows) {
     double* nr = nullptr;
     if (hipMalloc((void**)&nr, (size_t)cap * (size_t)h->d.ldr * sizeof(double)) != hipSuccess)
         return fail(ELP_E_NOMEM, "AR growth failed");
-    HIPCHK(hipMemcpyAsync(nr, h->d.AR, (size_t)h->ar_rows * (size_t)h->d.ldr * sizeof(double),
-                          hipMemcpyDeviceToDevice, h->st));
-    HIPCHK(hipStreamSynchronize(h->st));
-    (void)hipFree(h->d.AR);
+    // tile-major layout: rows of each tile move to the new capacity
+    double* old = h->d.AR;
+    const int64_t old_cap = h->ar_rows;
     h->d.AR = nr;
+    h->d.arcap = cap;
     h->ar_rows = cap;
+    HIPCHK(hipMemcpyAsync(h->hctl, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    HIPCHK(launch_ar_relayout(h->d, old, old_cap, (int)std::min<int64_t>(old_cap, h->hctl->ny), h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    (void)hipFree(old);
     return 0;
 }
 

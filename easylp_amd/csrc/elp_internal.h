@@ -87,9 +87,11 @@ struct Dev {
     int32_t world;        // ranks sharing the columns
     int32_t sharded;      // 1: entering column comes from the exchanged packet
     int64_t ldm;   // Minv leading dimension (= max(m,1))
-    int64_t ldr;   // AR leading dimension (n rounded up to TILE_COLS)
+    int64_t ldr;   // n rounded up to TILE_COLS
+    int64_t arcap; // AR rows per column tile (capacity)
     const double* A;  // column-major m x n
-    double* AR;       // Y rows, row-major (capacity grown on demand, <= m rows)
+    double* AR;       // Y rows, tile-major: [ldr/128 tiles][arcap rows][128 cols]
+                      // (a pricing wave streams one contiguous run of rows)
     double* AS;       // basic structural columns, column-major (m x m capacity)
     double* Minv;     // bump inverse, row-major ldm x ldm
     double* MinvT;    // its transpose (BTRAN and B^-1 rows read rows of it)
@@ -122,6 +124,9 @@ hipError_t launch_generate(const Dev& d, uint64_t seed, int64_t col0, int64_t n_
 hipError_t launch_init_cols(const Dev& d, const double* lo, const double* up, hipStream_t st);
 hipError_t launch_init_rows(const Dev& d, const double* rhs, hipStream_t st);
 hipError_t launch_fill_AR(const Dev& d, hipStream_t st);  // AR rows for the initial Y
+// copy the first `rows` rows of every tile from an AR with capacity old_cap
+hipError_t launch_ar_relayout(const Dev& d, const double* old_ar, int64_t old_cap, int rows,
+                              hipStream_t st);
 // ev0/ev1 (may be null): events recorded around the pricing kernel
 hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStream_t st,
                             hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);

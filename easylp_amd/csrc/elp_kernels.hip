@@ -293,13 +293,30 @@ __global__ void __launch_bounds__(1024) k_init_Y(Dev d) {
     }
 }
 
+// element (row p, column j) of the tile-major AR
+DEV size_t ar_at(const Dev& d, int64_t p, int64_t j) {
+    return ((size_t)(j / TILE_COLS) * (size_t)d.arcap + (size_t)p) * TILE_COLS + (size_t)(j % TILE_COLS);
+}
+
 // AR[p][j] = A[Yl[p]][j] for p < ny (initial fill)
 __global__ void k_fill_AR(Dev d) {
     const int ny = d.ctl->ny;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= d.n) return;
     for (int p = blockIdx.y; p < ny; p += gridDim.y)
-        d.AR[(size_t)p * (size_t)d.ldr + j] = d.A[(size_t)j * (size_t)d.m + (size_t)d.Yl[p]];
+        d.AR[ar_at(d, p, j)] = d.A[(size_t)j * (size_t)d.m + (size_t)d.Yl[p]];
+}
+
+// grow AR: rows [0, rows) of every tile into the new capacity
+__global__ void k_ar_relayout(Dev d, const double* __restrict__ old_ar, int64_t old_cap, int rows) {
+    const int64_t ntiles = d.ldr / TILE_COLS;
+    const int64_t total = ntiles * (int64_t)rows * TILE_COLS;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = e / ((int64_t)rows * TILE_COLS);
+        const int64_t r = e % ((int64_t)rows * TILE_COLS);
+        d.AR[(size_t)t * (size_t)d.arcap * TILE_COLS + (size_t)r] = old_ar[(size_t)t * (size_t)old_cap * TILE_COLS + (size_t)r];
+    }
 }
 
 // ============================================================== BTRAN
@@ -391,8 +408,8 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d) {
     const int L = (ny + PRICE_SPLIT - 1) / PRICE_SPLIT;
     const int p0 = w * L;
     const int p1 = min(ny, p0 + L);
-    const int64_t j0 = (int64_t)blockIdx.x * TILE_COLS + 2 * lane;
-    const double* col = d.AR + j0;
+    // this tile's rows are contiguous: row p at col + p * TILE_COLS
+    const double* col = d.AR + (size_t)blockIdx.x * (size_t)d.arcap * TILE_COLS + 2 * lane;
     const double* __restrict__ yy = d.yy;
     double acc0 = 0.0, acc1 = 0.0;
     int p = p0;
@@ -401,7 +418,7 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d) {
         double2 v[UNR];
 #pragma unroll
         for (int u = 0; u < UNR; ++u)
-            v[u] = *reinterpret_cast<const double2*>(col + (size_t)(p + u) * (size_t)d.ldr);
+            v[u] = *reinterpret_cast<const double2*>(col + (size_t)(p + u) * TILE_COLS);
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
             const double yv = yy[p + u];
@@ -413,7 +430,7 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d) {
         double2 v[UNR];
 #pragma unroll
         for (int u = 0; u < UNR; ++u)
-            v[u] = (p + u < p1) ? *reinterpret_cast<const double2*>(col + (size_t)(p + u) * (size_t)d.ldr)
+            v[u] = (p + u < p1) ? *reinterpret_cast<const double2*>(col + (size_t)(p + u) * TILE_COLS)
                                 : make_double2(0.0, 0.0);
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
@@ -1269,9 +1286,8 @@ __global__ void __launch_bounds__(256) k_update(Dev d, int nb_minv) {
     if (P.y_rm_slot >= 0 || P.y_ap_slot >= 0) {
         for (int64_t j = t0; j < d.n; j += tstride) {
             if (P.y_rm_slot >= 0 && P.y_rm_slot != P.y_rm_last)
-                d.AR[(size_t)P.y_rm_slot * d.ldr + j] = d.AR[(size_t)P.y_rm_last * d.ldr + j];
-            if (P.y_ap_slot >= 0)
-                d.AR[(size_t)P.y_ap_slot * d.ldr + j] = d.A[(size_t)j * m + P.y_ap_row];
+                d.AR[ar_at(d, P.y_rm_slot, j)] = d.AR[ar_at(d, P.y_rm_last, j)];
+            if (P.y_ap_slot >= 0) d.AR[ar_at(d, P.y_ap_slot, j)] = d.A[(size_t)j * m + P.y_ap_row];
         }
     }
 }
@@ -1497,6 +1513,12 @@ hipError_t launch_fill_AR(const Dev& d, hipStream_t st) {
         dim3 g(cdiv(d.n, 256), (unsigned)(d.m < 4096 ? d.m : 4096));
         k_fill_AR<<<g, 256, 0, st>>>(d);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_ar_relayout(const Dev& d, const double* old_ar, int64_t old_cap, int rows,
+                              hipStream_t st) {
+    if (rows > 0) k_ar_relayout<<<2048, 256, 0, st>>>(d, old_ar, old_cap, rows);
     return hipGetLastError();
 }
 
