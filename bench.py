@@ -44,6 +44,10 @@ def parse():
     ap.add_argument("--no-optimal", action="store_true", help="skip the run to optimality")
     ap.add_argument("--profile-price", type=int, default=1,
                     help="HIP events around the pricing kernel (roofline)")
+    ap.add_argument("--c4", type=int, default=1,
+                    help="also time the 10000x500000 column-sharded config (SURVEY config 4)")
+    ap.add_argument("--c4-steps", type=int, default=300)
+    ap.add_argument("--c4-warmup", type=int, default=100)
     return ap.parse_args()
 
 
@@ -83,6 +87,40 @@ def committed_traffic(args):
     if not same:
         return None, None
     return t["traffic_bytes_per_launch"], "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE, x2 gfx950)"
+
+
+def c4_rate(args, lib, world, rank, local, barrier, dist):
+    """Iterations/s of the north-star scaling config: dense LP m=10000 n=500000,
+    columns sharded over the ranks.  Same step definition."""
+    import torch
+    from easylp_amd import Problem
+    m, n = 10000, 500000
+    p = Problem(m, n, device=local)
+    if world > 1:
+        from easylp_amd.dist import share_unique_id
+        p.comm_init(share_unique_id(lib, rank), world, rank)
+    t_load = time.perf_counter()
+    p.load_generated(args.seed)
+    barrier()
+    t_load = time.perf_counter() - t_load
+    p.iterate(args.c4_warmup)
+    barrier()
+    s0 = p.stats()
+    t0 = time.perf_counter()
+    p.iterate(args.c4_steps)
+    barrier()
+    el = time.perf_counter() - t0
+    s1 = p.stats()
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    it = s1["iterations"] - s0["iterations"]
+    p.close()
+    return {"workload": "dense random LP m=10000 n=500000 (SURVEY config 4), columns sharded x%d" % world,
+            "value": it / el if el > 0 else None, "unit": "iterations/s", "iterations_timed": it,
+            "warmup": args.c4_warmup, "ms_per_step": 1e3 * el / max(it, 1),
+            "bump_dim": s1["bump_dim"], "y_rows": s1["y_rows"], "load_s": t_load}
 
 
 def main():
@@ -159,6 +197,11 @@ def main():
 
     traffic, traffic_src = committed_traffic(args) if world == 1 else (None, None)
 
+    c4 = None
+    if args.c4:
+        p.close()  # free the 5000x50000 problem first
+        c4 = c4_rate(args, lib, world, rank, local, barrier, dist)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args)
@@ -199,6 +242,7 @@ def main():
                 "launches_timed": price_n,
             },
             "cpu_baseline": cpu,
+            "scaling_config": c4,
         }
         print(json.dumps(line), flush=True)
     p.close()
