@@ -14,7 +14,8 @@ LIB_PATH = os.path.join(HERE, "lib", "libeasylp_hip.so")
 ELP_LE, ELP_GE, ELP_EQ = 1, 2, 3
 ELP_OPTIMAL, ELP_SUBOPTIMAL, ELP_INFEASIBLE, ELP_UNBOUNDED = 0, 1, 2, 3
 ELP_NUMFAILURE, ELP_TIMEOUT = 5, 7
-ELP_PROFILE_PRICE = 2
+ELP_PROFILE_PRICE = 2   # device-clock pricing timer
+ELP_PROFILE_EVENTS = 4  # HIP-event pricing timer
 
 # every entry point the header declares (checked by tests/test_abi.py)
 EXPORTS = (

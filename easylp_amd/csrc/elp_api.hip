@@ -47,6 +47,7 @@ double now_s() {
 }  // namespace
 
 struct elp_handle {
+    double dbg_enqueue = 0.0, dbg_wait = 0.0;  // ELP_DEBUG_ENQUEUE
     int64_t m = 0, n = 0;        // global problem size
     int64_t col0 = 0, nloc = 0;  // this rank's column shard
     elp_control ctl{};
@@ -98,7 +99,7 @@ static void free_dev(elp_handle* h) {
                     d.t,        d.acol, d.aR,   d.alS,   d.alU,  d.zz,    d.zpart, d.vrow,
                     d.vvec,     d.colA, d.rhs,  d.vstat, d.cover, d.rpos, d.Rl,    d.Sl,
                     d.Yl,  d.ypos,  d.perm,  d.pivstep, d.nzlist, d.nzcount,
-                    d.cand,     d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand,
+                    d.cand,     d.pstamp, d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand,
                     d.pkt, d.objg, d.ract, d.cand_xchg, h->d_flag, d.cS, d.slo, d.shi, d.rlo, d.rhi};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -158,6 +159,7 @@ static int alloc_all(elp_handle* h) {
     d.ldm = mm;
     d.ldr = ((n + TILE_COLS - 1) / TILE_COLS) * TILE_COLS;
     d.infinity = h->ctl.infinity;
+    d.ptimer = (h->ctl.verbose & ELP_PROFILE_PRICE) ? 1 : 0;
     const size_t nv = (size_t)(n + 2 * m);
     hipError_t e = hipSuccess;
     auto A = [&](hipError_t x) {
@@ -218,6 +220,7 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.nzlist, n));
     A(dalloc(&d.nzcount, 1));
     A(dalloc(&d.cand, (size_t)((n + TILE_COLS - 1) / TILE_COLS) + 64));
+    A(dalloc(&d.pstamp, 2 * ((size_t)((n + TILE_COLS - 1) / TILE_COLS) + 64)));
     A(dalloc(&d.ctl, 1));
     A(dalloc(&d.trace, (size_t)(h->trace_cap > 0 ? 2 * h->trace_cap : 2)));
     if (e != hipSuccess) {
@@ -537,7 +540,7 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
     int rc = push_ctl_fields(h);
     if (rc) return rc;
     const int period = h->ctl.refactor_period;
-    const bool prof = (h->ctl.verbose & ELP_PROFILE_PRICE) != 0;
+    const bool prof = (h->ctl.verbose & ELP_PROFILE_EVENTS) != 0;
     if (prof && (int)h->ev.size() < 2 * h->ctl.sync_every) {
         for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
         h->ev.assign(2 * h->ctl.sync_every, nullptr);
@@ -576,6 +579,7 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
         if (left > 0 && left < chunk) chunk = (int)left;
         if (chunk < 1) chunk = 1;
         const double bytes0 = c->price_bytes;
+        const double t_enq0 = now_s();
         for (int t = 0; t < chunk; ++t) {
             const int kub = (int)std::min<int64_t>(h->m, (int64_t)k0 + t);
             const int nyub = (int)std::min<int64_t>(h->m, (int64_t)ny0 + t);
@@ -595,8 +599,11 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
                 HIPCHK(launch_iteration_tail(h->d, kub, h->phase, h->st));
             }
         }
+        const double t_enq1 = now_s();
         HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
         HIPCHK(hipStreamSynchronize(h->st));
+        h->dbg_enqueue += t_enq1 - t_enq0;
+        h->dbg_wait += now_s() - t_enq1;
         h->stats.host_polls++;
         const int32_t s = c->status;
         if (prof && s == ST_RUN) {  // every launch of the chunk did work
@@ -777,6 +784,11 @@ extern "C" int elp_get_stats(elp_handle* h, elp_stats* st) {
         h->stats.bump_dim = c.k;
         h->stats.y_rows = c.ny;
         h->stats.price_bytes = c.price_bytes;
+        if (h->d.ptimer) {
+            h->stats.price_seconds = 1e-8 * (double)c.price_ticks;
+            h->stats.price_timed_launches = c.price_timed;
+            h->stats.price_timed_bytes = c.price_tbytes;
+        }
     }
     *st = h->stats;
     return 0;
@@ -808,6 +820,9 @@ extern "C" void elp_destroy(elp_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->dev);
     if (h->st) (void)hipStreamSynchronize(h->st);
+    if (getenv("ELP_DEBUG_ENQUEUE"))
+        fprintf(stderr, "elp: host enqueue %.4f s, poll wait %.4f s, polls %lld\n", h->dbg_enqueue,
+                h->dbg_wait, (long long)h->stats.host_polls);
     free_dev(h);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     h->comm.destroy();

@@ -61,6 +61,11 @@ struct DevCtl {
     int32_t ncand, pad2;              // Harris pass-2 candidate count (k_ftran_zr)
     int32_t snap_k, snap_bland;       // k, bland as k_ratio's workgroups must see them
                                       // (workgroup 0 rewrites k / bland meanwhile)
+    // pricing-kernel timer (Dev::ptimer): s_memrealtime ticks (100 MHz) from the
+    // first workgroup's start to the last one's end, summed over timed passes
+    unsigned long long price_ticks;
+    int64_t price_timed;
+    double price_tbytes;
 };
 
 // Harris pass-2 candidate (a superset of the global candidates: exact ratio
@@ -110,6 +115,8 @@ struct Dev {
     int8_t* vstat;
     int32_t *cover, *rpos, *Rl, *Sl, *spos, *Yl, *ypos, *perm, *pivstep, *nzlist, *nzcount;
     Cand* cand;
+    unsigned long long* pstamp;  // [tile][2] start / end stamps of the last pricing pass
+    int32_t ptimer, pad3;        // 1: k_price stamps, the select kernels sum them
     DevCtl* ctl;
     int64_t* trace;
     int32_t maximize, pad2;

@@ -402,6 +402,7 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d) {
     __shared__ Cand red[PRICE_SPLIT];
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
+    if (d.ptimer && threadIdx.x == 0) d.pstamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     const int ny = c->ny, bland = c->bland;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -471,7 +472,43 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d) {
         }
     }
     best = block_best<PRICE_THREADS>(best, bland, red);
-    if (threadIdx.x == 0) d.cand[blockIdx.x] = best;
+    if (threadIdx.x == 0) {
+        d.cand[blockIdx.x] = best;
+        if (d.ptimer) d.pstamp[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
+// Pricing-pass timer: first start to last end over the tiles' stamps (one
+// workgroup of NT threads), added to the control block with the pass's bytes.
+template <int NT>
+DEV void price_timer_sum(const Dev& d, int ntiles, unsigned long long* red) {
+    __syncthreads();  // red may still be read by the preceding reduction
+    unsigned long long lo = ~0ull, hi = 0;
+    for (int t = threadIdx.x; t < ntiles; t += NT) {
+        lo = min(lo, d.pstamp[2 * t]);
+        hi = max(hi, d.pstamp[2 * t + 1]);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        lo = min(lo, (unsigned long long)__shfl_xor(lo, off));
+        hi = max(hi, (unsigned long long)__shfl_xor(hi, off));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[2 * (threadIdx.x >> 6)] = lo;
+        red[2 * (threadIdx.x >> 6) + 1] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < NT / 64; ++w) {
+            lo = min(lo, red[2 * w]);
+            hi = max(hi, red[2 * w + 1]);
+        }
+        DevCtl* c = d.ctl;
+        const int ny = c->ny;
+        c->price_ticks += hi - lo;
+        c->price_timed++;
+        c->price_tbytes += 8.0 * (double)ny * (double)d.n + 9.0 * (double)d.n + 12.0 * (double)ny;
+    }
 }
 
 // ============================================================== select
@@ -546,6 +583,7 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles) {
     }
     const int q = (int)best.j;
     if (threadIdx.x == 0) entering_chosen(d, best);
+    if (d.ptimer) price_timer_sum<1024>(d, ntiles, reinterpret_cast<unsigned long long*>(red));
     // one GPU: the full column is read in place by k_ftran_zr / k_update
     gather_aR(d, q, q < d.N ? d.A + (size_t)(q - d.col0) * (size_t)d.m : nullptr);
 }
@@ -595,6 +633,10 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles) {
     }
     const int q = (int)best.j;
     if (blockIdx.x == 0 && threadIdx.x == 0) entering_chosen(d, best);
+    if (d.ptimer && blockIdx.x == gridDim.x - 1) {  // the extra timer workgroup
+        price_timer_sum<256>(d, ntiles, reinterpret_cast<unsigned long long*>(aRs));
+        return;
+    }
     if (q < d.N) {
         const double* col = d.A + (size_t)(q - d.col0) * (size_t)d.m;
         for (int p = threadIdx.x; p < k; p += 256) aRs[p] = col[d.Rl[p]];
@@ -619,6 +661,7 @@ __global__ void __launch_bounds__(1024) k_select_local(Dev d, int ntiles, int ra
     if (c->status != ST_RUN) return;
     const Cand best = local_best(d, ntiles, red);
     if (threadIdx.x == 0) d.cand_xchg[rank] = best;
+    if (d.ptimer) price_timer_sum<1024>(d, ntiles, reinterpret_cast<unsigned long long*>(red));
 }
 
 // after the all-gather: global min-loc (same total order on every rank); the
@@ -1603,7 +1646,8 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
     const int ntiles = (int)cdiv(d.n, TILE_COLS);
     const size_t lds = (size_t)k_ub * sizeof(double);
     if (lds <= 48 * 1024) {  // fused select + bump FTRAN
-        k_select_ftran<<<cdiv(k_ub > 0 ? k_ub : 1, 4), 256, lds, st>>>(d, ntiles);
+        const size_t ldsz = lds > 64 ? lds : 64;  // the timer workgroup reduces in it
+        k_select_ftran<<<cdiv(k_ub > 0 ? k_ub : 1, 4) + (d.ptimer ? 1 : 0), 256, ldsz, st>>>(d, ntiles);
         return launch_iteration_tail(d, k_ub, phase, st, false);
     }
     k_select<<<1, 1024, 0, st>>>(d, ntiles);

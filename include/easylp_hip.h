@@ -84,16 +84,19 @@ typedef struct elp_stats {
     int32_t world_size;        /* ranks sharing the column partition           */
     int32_t rank;
     int64_t col0, ncols;       /* this rank's column shard                     */
-    /* pricing-kernel timing (control.verbose & ELP_PROFILE_PRICE): HIP events
-     * on the solver's stream around every pricing launch of iteration chunks
-     * that ran to completion */
+    /* pricing-kernel timing (control.verbose & ELP_PROFILE_PRICE): every
+     * workgroup of the pricing kernel stamps s_memrealtime (the GPU's 100 MHz
+     * constant clock) at start and end; first start -> last end is summed per
+     * pricing pass that chose an entering variable.  With ELP_PROFILE_EVENTS
+     * instead: HIP events around every pricing launch of completed chunks. */
     double price_seconds;      /* sum of timed pricing-kernel durations        */
     double price_timed_bytes;  /* algorithmic bytes of those launches          */
     int64_t price_timed_launches;
     int64_t gj_refactors;      /* refactors that needed a Gauss-Jordan rebuild */
 } elp_stats;
 
-#define ELP_PROFILE_PRICE 2   /* elp_control.verbose bit */
+#define ELP_PROFILE_PRICE 2   /* elp_control.verbose bit: device-clock pricing timer */
+#define ELP_PROFILE_EVENTS 4  /* elp_control.verbose bit: HIP-event pricing timer  */
 
 /* Fill *c with defaults. */
 void elp_default_control(elp_control* c);
