@@ -398,6 +398,7 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
     } else {
         HIPCHK(launch_phase2(d, h->st));
         h->phase = 2;
+        HIPCHK(launch_btran_exact(d, 0, h->st));  // slack basis: y = 0
         c = *h->hctl;
         h->hctl->phase = 2;
         HIPCHK(hipMemcpyAsync(&d.ctl->phase, &h->hctl->phase, sizeof(int32_t), hipMemcpyHostToDevice, h->st));
@@ -515,6 +516,7 @@ static int do_refactor(elp_handle* h, int k) {
         if (rc) return rc;
     }
     HIPCHK(launch_refactor_primal(h->d, k, h->st));
+    if (h->phase == 2) HIPCHK(launch_btran_exact(h->d, k, h->st));  // exact duals again
     h->stats.refactors++;
     return 0;
 }
@@ -670,6 +672,23 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             c->since_refactor = 0;
             c->ndegen = 0;
             c->bland = 0;
+            c->status = ST_RUN;
+            rc = push_ctl_fields(h);
+            if (rc) return rc;
+            continue;
+        }
+        if (s == ST_PHASE_OPT && h->phase == 2 && c->since_refactor > 0) {
+            // optimal under updated duals: refactor (exact y) and price again
+            rc = do_refactor(h, c->k);
+            if (rc) return rc;
+            HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+            HIPCHK(hipStreamSynchronize(h->st));
+            if (c->status == ST_NUMFAIL) {
+                h->done = true;
+                h->final_status = ELP_NUMFAILURE;
+                break;
+            }
+            c->since_refactor = 0;
             c->status = ST_RUN;
             rc = push_ctl_fields(h);
             if (rc) return rc;

@@ -61,6 +61,10 @@ struct DevCtl {
     int32_t ncand, pad2;              // Harris pass-2 candidate count (k_ftran_zr)
     int32_t snap_k, snap_bland;       // k, bland as k_ratio's workgroups must see them
                                       // (workgroup 0 rewrites k / bland meanwhile)
+    // likewise the bookkeeping entries k_ratio's dual update reads (k_ftran_zr's
+    // snapshot workgroup): |Y|, rpos / ypos of the entering slack's row, the
+    // last Y row and its bump position
+    int32_t snap_ny, snap_apos, snap_ypos0, snap_ylast, snap_rposyl, pad4;
     // pricing-kernel timer (Dev::ptimer): s_memrealtime ticks (100 MHz) from the
     // first workgroup's start to the last one's end, summed over timed passes
     unsigned long long price_ticks;
@@ -153,6 +157,7 @@ constexpr double NS_TOL = 1e-6;
 hipError_t launch_refactor_ns_resid(const Dev& d, int k, hipStream_t st);
 hipError_t launch_refactor_ns_update(const Dev& d, int k, hipStream_t st);
 hipError_t launch_refactor_gj(const Dev& d, int k, hipStream_t st);
+hipError_t launch_btran_exact(const Dev& d, int k, hipStream_t st);  // phase-2 duals
 hipError_t launch_refactor_primal(const Dev& d, int k, hipStream_t st);  // needs ract
 hipError_t launch_nzlist(const Dev& d, hipStream_t st);
 hipError_t launch_phase2(const Dev& d, hipStream_t st);

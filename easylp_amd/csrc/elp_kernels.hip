@@ -347,6 +347,8 @@ __global__ void __launch_bounds__(256) k_btran_t(Dev d) {
 
 // loop-top checks (block 0, wave 0) + y on covered rows (phase 2: sigma*0)
 // + y_R[p] = wave_dot(MinvT[p, 0:k], tv) scattered to y[R_p]  (one wave per p)
+DEV void btran_body(const Dev& d, int phase, const double* __restrict__ tv);
+
 __global__ void __launch_bounds__(256) k_btran(Dev d, int phase, const double* __restrict__ tv) {
     DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
@@ -362,7 +364,15 @@ __global__ void __launch_bounds__(256) k_btran(Dev d, int phase, const double* _
             else if (c->since_refactor >= c->refactor_period) c->status = ST_REFACTOR;
         }
     }
-    const int k = c->k;
+    btran_body(d, phase, tv);
+}
+
+// exact duals after a refactor / at the phase-2 start (phase 2 then keeps y by
+// the dual update in k_ratio): no status test, no loop-top checks
+__global__ void __launch_bounds__(256) k_btran_exact(Dev d) { btran_body(d, 2, d.cS); }
+
+DEV void btran_body(const Dev& d, int phase, const double* __restrict__ tv) {
+    const int k = d.ctl->k;
     if (phase == 2) {
         const int gid = blockIdx.x * blockDim.x + threadIdx.x;
         const int gsz = gridDim.x * blockDim.x;
@@ -810,6 +820,19 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt) {
         d.ctl->snap_k = k;
         d.ctl->snap_bland = bland;
     }
+    if (blockIdx.x == gridDim.x - 1) {  // the snapshot workgroup (see DevCtl)
+        if (threadIdx.x == 0) {
+            DevCtl* cw = d.ctl;
+            const int ny = cw->ny, i0 = q - d.N;
+            const int yl = ny > 0 ? d.Yl[ny - 1] : -1;
+            cw->snap_ny = ny;
+            cw->snap_apos = i0 >= 0 ? d.rpos[i0] : -1;
+            cw->snap_ypos0 = i0 >= 0 ? d.ypos[i0] : -1;
+            cw->snap_ylast = yl;
+            cw->snap_rposyl = yl >= 0 ? d.rpos[yl] : -1;
+        }
+        return;
+    }
     double tmin = HUGE_VAL;
     double ge = 0.0, xe = 0.0, le = 0.0, he = 0.0;
     int ve = -1;
@@ -916,7 +939,7 @@ DEV Leave shfl_leave(const Leave& x, int off) {
 
 // Scalars the pivot bookkeeping needs, fetched in parallel at kernel start.
 enum { SC_LBQ, SC_UBQ, SC_XVQ, SC_CQ, SC_SLL, SC_CSL, SC_SLOL, SC_SHIL, SC_N };
-enum { SI_VSQ, SI_RPOS0, SI_YPOS0, SI_YLAST, SI_SLLAST, SI_RLLAST, SI_N };
+enum { SI_VSQ, SI_RPOS0, SI_YPOS0, SI_YLAST, SI_SLLAST, SI_RLLAST, SI_RPOSYL, SI_N };
 
 // Harris pass 2 + decision + pivot plan, fused with the B^-1 row of cases B/D.
 // Pass 1 came from k_ftran_zr's per-workgroup minima, the candidates from its
@@ -933,9 +956,13 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     __shared__ int si[SI_N];
     __shared__ int s_action;
     __shared__ Plan s_plan;
+    __shared__ double s_wd;
     DevCtl* c = d.ctl;
-    if (c->status != ST_RUN) return;
-    const int m = d.m, k = c->snap_k, q = c->q, ny = c->ny, ncand = c->ncand;
+    if (c->status != ST_RUN) {  // no plan this iteration: k_update must not re-apply one
+        if (blockIdx.x == 0 && threadIdx.x == 0) c->plan.action = ACT_NONE;
+        return;
+    }
+    const int m = d.m, k = c->snap_k, q = c->q, ny = c->snap_ny, ncand = c->ncand;
     const double sig = c->sig;
     const int bland = c->snap_bland;
     const bool lead = blockIdx.x == 0;
@@ -944,7 +971,6 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     // ---- parallel prefetch of bookkeeping scalars
     const int ql = loc_of(d, q);  // -1: the entering column lives on another shard
     if (tid < SC_N + SI_N) {
-        const int i0 = q - d.N;
         const bool pk = ql < 0 || (d.sharded && q < d.N);  // from the exchanged packet
         switch (tid) {
             case SC_LBQ: sc[SC_LBQ] = pk ? d.pkt[m] : d.lb[ql]; break;
@@ -956,11 +982,12 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
             case SC_SLOL: sc[SC_SLOL] = last >= 0 ? d.slo[last] : 0.0; break;
             case SC_SHIL: sc[SC_SHIL] = last >= 0 ? d.shi[last] : 0.0; break;
             case SC_N + SI_VSQ: si[SI_VSQ] = ql >= 0 ? d.vstat[ql] : VS_LOWER; break;
-            case SC_N + SI_RPOS0: si[SI_RPOS0] = i0 >= 0 ? d.rpos[i0] : -1; break;
-            case SC_N + SI_YPOS0: si[SI_YPOS0] = i0 >= 0 ? d.ypos[i0] : -1; break;
-            case SC_N + SI_YLAST: si[SI_YLAST] = ny > 0 ? d.Yl[ny - 1] : -1; break;
+            case SC_N + SI_RPOS0: si[SI_RPOS0] = c->snap_apos; break;
+            case SC_N + SI_YPOS0: si[SI_YPOS0] = c->snap_ypos0; break;
+            case SC_N + SI_YLAST: si[SI_YLAST] = c->snap_ylast; break;
             case SC_N + SI_SLLAST: si[SI_SLLAST] = last >= 0 ? d.Sl[last] : -1; break;
             case SC_N + SI_RLLAST: si[SI_RLLAST] = last >= 0 ? d.Rl[last] : -1; break;
+            case SC_N + SI_RPOSYL: si[SI_RPOSYL] = c->snap_rposyl; break;
         }
     }
     // ---- pass 1 result: min over the workgroup minima
@@ -1063,24 +1090,61 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     // ---- B^-1 row for a leaving unit variable (cases B, D; E wastes it):
     //      vvec[c] = wave_dot(MinvT[c, 0:k], A[lrow, S]), case B / delta
     const int lrow_all = best.e < m ? best.e : -1;
+    const int col = blockIdx.x * 4 + (tid >> 6);
+    const int lane = tid & 63;
+    double vcol = 0.0;  // vvec[col] (cases B, D)
+    // pivot case as workgroup 0's bookkeeping will classify it
+    const int lposx = best.e >= m ? best.e - m : -1;
+    const int apos = si[SI_RPOS0];
+    const int pcx = q < d.N ? (lposx >= 0 ? PC_A : PC_B) : apos < 0 ? PC_E : lposx >= 0 ? PC_C : PC_D;
     if (lrow_all >= 0 && k > 0) {
         // huge bumps: every workgroup writes the same values to d.vrow (benign)
         double* asrow = lds_row ? asrow_lds : d.vrow;
         for (int j = tid; j < k; j += 256) asrow[j] = d.AS[(size_t)j * (size_t)m + lrow_all];
         __syncthreads();
-        const int col = blockIdx.x * 4 + (tid >> 6);
-        const int lane = tid & 63;
         if (col < k) {
             const double* row = d.MinvT + (size_t)col * d.ldm;
             double acc = 0.0;
             for (int j = lane; j < k; j += 64) acc = fma(row[j], asrow[j], acc);
             acc = wave_tree(acc);
-            if (lane == 0) {
-                // case B delta = acol_i - z_i = sigma_u * sig * g (exact)
-                const double delta = unit_sign(d, best.var, lrow_all) * (sig * best.g);
-                d.vvec[col] = q < d.N ? acc / delta : acc;
-            }
+            // case B delta = acol_i - z_i = sigma_u * sig * g (exact)
+            const double delta = unit_sign(d, best.var, lrow_all) * (sig * best.g);
+            vcol = q < d.N ? acc / delta : acc;
+            if (lane == 0) d.vvec[col] = vcol;
         }
+        if (phase == 2 && pcx == PC_D && tid < 64) {  // vvec[a], redundantly per workgroup
+            const double* row = d.MinvT + (size_t)apos * d.ldm;
+            double acc = 0.0;
+            for (int j = lane; j < k; j += 64) acc = fma(row[j], asrow[j], acc);
+            acc = wave_tree(acc);
+            if (tid == 0) s_wd = c->dq / acc;
+        }
+        __syncthreads();
+    }
+    // ---- phase 2 dual update y += theta_d rho_r on the bump rows, one wave per
+    //      position (oracle run_phase cases A-D); the rows that join or leave R
+    //      and the Y slot that moves are workgroup 0's (below)
+    const double dq = c->dq;
+    const double wD = (phase == 2 && pcx == PC_D) ? s_wd : 0.0;
+    if (phase == 2 && lane == 0 && col < k && pcx != PC_E &&
+        !((pcx == PC_C || pcx == PC_D) && col == apos)) {
+        const int row = d.Rl[col];
+        const double yo = d.y[row];
+        double yn;
+        if (pcx == PC_A) {
+            yn = fma(dq, d.Minv[(size_t)lposx * d.ldm + col] / (best.g * sig), yo);
+        } else if (pcx == PC_B) {
+            yn = fma(-dq, vcol, yo);
+        } else if (pcx == PC_C) {
+            const double piv = d.Minv[(size_t)lposx * d.ldm + apos];
+            yn = fma(dq, d.Minv[(size_t)lposx * d.ldm + col] / piv, yo);
+        } else {
+            yn = fma(wD, vcol, yo);
+        }
+        d.y[row] = yn;
+        // the last Y row moves into the slot of row i0 (cases C, D)
+        const int slot = (pcx == PC_C || pcx == PC_D) && row == si[SI_YLAST] ? si[SI_YPOS0] : d.ypos[row];
+        if (slot >= 0) d.yy[slot] = yn;
     }
     if (!lead) return;
     // ---- pivot: bookkeeping by thread 0 (stores only, plus Minv[b][a] in case C)
@@ -1217,6 +1281,26 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
                 nny++;
             }
         }
+        if (phase == 2) {  // dual update: rows joining / leaving R, the moved Y slot
+            if (P.pcase == PC_B) {
+                const double yn = dq / P.piv;
+                d.y[P.row] = yn;
+                d.yy[d.ypos[P.row]] = yn;
+            } else if (P.pcase == PC_C || P.pcase == PC_D) {
+                d.y[P.i0] = 0.0;
+                if (P.pcase == PC_D) {
+                    d.y[P.row] = -wD;
+                    d.yy[d.ypos[P.row]] = -wD;
+                }
+            }
+            if (P.pcase >= PC_C) {  // C, D, E removed row i0 from Y
+                const int sl = si[SI_YPOS0], moved = si[SI_YLAST];
+                // the owner wave of a bump row wrote its moved slot already
+                const bool owned = P.pcase != PC_E && si[SI_RPOSYL] >= 0;
+                const bool special = P.pcase == PC_D && moved == P.row;
+                if (sl != ny - 1 && !owned && !special) d.yy[sl] = d.y[moved];
+            }
+        }
         c->k = newk;
         c->ny = nny;
         c->since_refactor++;
@@ -1270,11 +1354,17 @@ DEV double minv_new(const Dev& d, const Plan& P, int i, int j, const OldM& old) 
 
 // Minv and MinvT update (blocks [0, nb_minv)) + primal update x_B -= step*alpha
 // and AS / AR copies (the rest).  Flips only update x_B.
-__global__ void __launch_bounds__(256) k_update(Dev d, int nb_minv) {
-    const DevCtl* c = d.ctl;
-    if (c->status != ST_RUN) return;
+__global__ void __launch_bounds__(256) k_update(Dev d, int nb_minv, int phase) {
+    DevCtl* c = d.ctl;
+    if (phase == 2 && blockIdx.x == 0 && threadIdx.x == 0 && c->status == ST_RUN) {
+        // oracle run_phase loop top for the next iteration (phase 1: k_btran's)
+        if (c->iter >= c->iter_limit) c->status = ST_ITERCAP;
+        else if (c->iter >= c->iter_stop) c->status = ST_STOP;
+        else if (c->since_refactor >= c->refactor_period) c->status = ST_REFACTOR;
+    }
+    // the plan k_ratio made this iteration (ACT_NONE when it did not run)
     const Plan P = c->plan;
-    if (P.action == ACT_NONE) return;
+    if (P.action == ACT_NONE || c->status == ST_NUMFAIL) return;
     const int k = P.k_old;
     const size_t ldm = (size_t)d.ldm;
     if ((int)blockIdx.x < nb_minv) {
@@ -1594,10 +1684,8 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int phase, hipStrea
         if (k_ub > 0) k_btran_t<<<cdiv(k_ub, 4), 256, 0, st>>>(d);
         tv = d.t;
     }
-    {
+    if (phase == 1) {  // phase 2 keeps y by the dual update (k_ratio)
         unsigned g = cdiv(k_ub > 0 ? k_ub : 1, 4);
-        const unsigned gm = cdiv(m > 0 ? m : 1, 256);
-        if (phase == 2 && g < gm) g = gm;
         if (g > 1024) g = 1024;
         k_btran<<<g, 256, 0, st>>>(d, phase, tv);
     }
@@ -1617,8 +1705,9 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
         // z partials: 512 B per chunk of ZCHUNK bump positions in LDS (<= 64 KiB,
         // k <= 4096); larger bumps use a private slice of zpart per row tile
         const size_t lds = (size_t)cdiv(k_ub, ZCHUNK) * 64 * sizeof(double);
-        if (lds <= 64 * 1024) k_ftran_zr<true><<<nrt + nbt, 64 * ZR_WAVES, lds, st>>>(d, nrt);
-        else k_ftran_zr<false><<<nrt + nbt, 64 * ZR_WAVES, 0, st>>>(d, nrt);
+        // + 1: the snapshot workgroup
+        if (lds <= 64 * 1024) k_ftran_zr<true><<<nrt + nbt + 1, 64 * ZR_WAVES, lds, st>>>(d, nrt);
+        else k_ftran_zr<false><<<nrt + nbt + 1, 64 * ZR_WAVES, 0, st>>>(d, nrt);
     }
     // ratio test + (cases B/D) B^-1 row: one workgroup per 4 bump columns
     {
@@ -1633,7 +1722,7 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
         const int64_t cw = m > d.n ? m : d.n;
         unsigned nb_copy = cdiv(cw, 256);
         if (nb_copy > 1024) nb_copy = 1024;
-        k_update<<<nb_minv + nb_copy, 256, 0, st>>>(d, (int)nb_minv);
+        k_update<<<nb_minv + nb_copy, 256, 0, st>>>(d, (int)nb_minv, phase);
     }
     return hipGetLastError();
 }
@@ -1700,6 +1789,15 @@ hipError_t launch_refactor_gj(const Dev& d, int k, hipStream_t st) {
         W2 = sw;
     }
     k_gj_final<<<cdiv(kk, 256), 256, 0, st>>>(d, k, W);
+    return hipGetLastError();
+}
+
+hipError_t launch_btran_exact(const Dev& d, int k, hipStream_t st) {
+    unsigned g = cdiv(k > 0 ? k : 1, 4);
+    const unsigned gm = cdiv(d.m > 0 ? d.m : 1, 256);
+    if (g < gm) g = gm;
+    if (g > 1024) g = 1024;
+    k_btran_exact<<<g, 256, 0, st>>>(d);
     return hipGetLastError();
 }
 

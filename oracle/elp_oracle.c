@@ -322,21 +322,32 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
     const int64_t m = s->m, n = s->n;
     int64_t since_refactor = 0, ndegen = 0;
     int bland = 0;
+    /* phase 2 keeps y by the dual update y += theta_d rho_r after each pivot
+     * (the cases below); BTRAN recomputes it only when y_valid == 0: at the
+     * phase start and after every refactor.  Optimality found with updated
+     * duals is re-checked after a refactor (recheck: no loop-top checks). */
+    int y_valid = 0, recheck = 0;
     for (;;) {
         if (*iter == ctl->t_mark_iter && st->seconds_at_mark == 0.0) {
             struct timespec tm;
             clock_gettime(CLOCK_MONOTONIC, &tm);
             st->seconds_at_mark = (double)tm.tv_sec + 1e-9 * (double)tm.tv_nsec;
         }
-        if (phase == 1 && art_sum(s) <= s->tol_inf) return PH_P1DONE;
-        if (*iter >= max_iter) return PH_ITERCAP;
-        if (since_refactor >= ctl->refactor_period) {
-            if (refactor(s)) return PH_NUMFAIL;
-            st->refactors++;
-            since_refactor = 0;
+        if (!recheck) {
+            if (phase == 1 && art_sum(s) <= s->tol_inf) return PH_P1DONE;
+            if (*iter >= max_iter) return PH_ITERCAP;
+            if (since_refactor >= ctl->refactor_period) {
+                if (refactor(s)) return PH_NUMFAIL;
+                st->refactors++;
+                since_refactor = 0;
+                y_valid = 0;
+            }
         }
+        recheck = 0;
         const int64_t k = s->k;
-        /* ---- BTRAN ---- */
+        /* ---- BTRAN (phase 1: every iteration) ---- */
+        if (phase == 1 || !y_valid) {
+        y_valid = 1;
         for (int64_t i = 0; i < m; ++i) {
             const int64_t u = s->cover[i];
             s->y[i] = u >= 0 ? unit_sign(s, u) * s->cost[u] : 0.0;
@@ -355,6 +366,7 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
             s->yR[p] = wave_dot(k, s->tmp, s->t);
         }
         for (int64_t p = 0; p < k; ++p) s->y[s->Rl[p]] = s->yR[p];
+        }
         /* ---- pricing over structurals (AR sweep) and slacks ---- */
         const int64_t ny = s->ny;
         for (int64_t p = 0; p < ny; ++p) s->yy[p] = s->y[s->Yl[p]];
@@ -399,7 +411,17 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
                 dq = d;
             }
         }
-        if (q < 0) return PH_OPTIMAL;
+        if (q < 0) {
+            if (phase == 2 && since_refactor > 0) {  /* updated duals: confirm */
+                if (refactor(s)) return PH_NUMFAIL;
+                st->refactors++;
+                since_refactor = 0;
+                y_valid = 0;
+                recheck = 1;
+                continue;
+            }
+            return PH_OPTIMAL;
+        }
         const double sig = dq < 0.0 ? 1.0 : -1.0;
         /* ---- FTRAN ---- */
         for (int64_t i = 0; i < m; ++i) s->acol[i] = (q < n) ? Aat(s, i, q) : (i == q - n ? 1.0 : 0.0);
@@ -519,6 +541,8 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
                 const int64_t p = lpos;
                 const double piv = s->alS[p];
                 for (int64_t j = 0; j < k; ++j) s->v[j] = *MI(s, p, j) / piv;
+                if (phase == 2) /* dual update: rho_r = Minv row p, theta_d = dq / piv */
+                    for (int64_t j = 0; j < k; ++j) s->y[s->Rl[j]] = fma(dq, s->v[j], s->y[s->Rl[j]]);
                 for (int64_t i = 0; i < k; ++i) {
                     if (i == p) continue;
                     const double wi = s->alS[i];
@@ -535,6 +559,10 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
                 const double delta = s->acol[i] - s->z[i];
                 row_times_minv(s, i, s->v);
                 for (int64_t c = 0; c < k; ++c) s->v[c] = s->v[c] / delta;
+                if (phase == 2) { /* dual update: row i joins R with y_i = dq / delta */
+                    for (int64_t c = 0; c < k; ++c) s->y[s->Rl[c]] = fma(-dq, s->v[c], s->y[s->Rl[c]]);
+                    s->y[i] = dq / delta;
+                }
                 for (int64_t a = 0; a < k; ++a) {
                     const double wa = s->alS[a];
                     for (int64_t c = 0; c < k; ++c) *MI(s, a, c) = fma(wa, s->v[c], *MI(s, a, c));
@@ -564,6 +592,11 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
                 const int64_t b = lpos, last = k - 1;
                 const double piv = *MI(s, b, a);
                 for (int64_t c = 0; c < k; ++c) s->v[c] = *MI(s, b, c) / piv;
+                if (phase == 2) { /* dual update; row i0 leaves R (y = 0) */
+                    for (int64_t c = 0; c < k; ++c)
+                        if (c != a) s->y[s->Rl[c]] = fma(dq, s->v[c], s->y[s->Rl[c]]);
+                    s->y[i0] = 0.0;
+                }
                 for (int64_t r = 0; r < k; ++r) {
                     if (r == b) continue;
                     const double f = *MI(s, r, a);
@@ -591,6 +624,13 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
                 const int64_t i1 = lrow;
                 row_times_minv(s, i1, s->v);
                 const double piv = s->v[a];
+                if (phase == 2) { /* dual update; row i1 takes position a */
+                    const double w = dq / piv;
+                    for (int64_t c = 0; c < k; ++c)
+                        if (c != a) s->y[s->Rl[c]] = fma(w, s->v[c], s->y[s->Rl[c]]);
+                    s->y[i0] = 0.0;
+                    s->y[i1] = -w;
+                }
                 for (int64_t r = 0; r < k; ++r) s->t[r] = *MI(s, r, a) / piv;
                 for (int64_t r = 0; r < k; ++r) {
                     const double f = s->t[r];

@@ -62,3 +62,16 @@ def feasible(A, dirs, rhs, x, lo, up, tol=2e-8):
     ok &= bool(np.all(x >= lo - tol * np.maximum(1, np.abs(lo[np.isfinite(lo)]).max(initial=1))))
     ok &= bool(np.all(x <= up + tol * np.maximum(1, np.abs(up[np.isfinite(up)]).max(initial=1))))
     return bool(ok)
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    """The HIP library on a GPU.  torch initialises the device first (its
+    availability probe must not follow the library's own HIP start-up)."""
+    import torch
+    assert torch.cuda.is_available(), "GPU test run without a GPU"
+    torch.cuda.init()
+    from easylp_amd import build
+    build.build()
+    import easylp_amd
+    return easylp_amd

@@ -19,8 +19,8 @@ M, N, SEED = 5000, 50000, 1
 
 
 @pytest.fixture(scope="module")
-def c3():
-    import easylp_amd
+def c3(gpu):
+    easylp_amd = gpu
     from oracle import generate_dense
     with easylp_amd.Problem(M, N) as p:
         p.set_trace(100000)

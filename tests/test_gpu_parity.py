@@ -14,16 +14,6 @@ KNOWN = load_known_answers()
 DENSE = load_dense_lps()
 
 
-@pytest.fixture(scope="module")
-def gpu():
-    import torch
-    assert torch.cuda.is_available(), "GPU test run without a GPU"
-    from easylp_amd import build
-    build.build()
-    import easylp_amd
-    return easylp_amd
-
-
 def _cmp(g, o, rel=1e-12):
     assert g.status == o.status
     if hasattr(o, "stats") and "gj_refactors" in o.stats:
