@@ -1,12 +1,12 @@
 """Per-iteration timeline from a rocprofv3 kernel-trace CSV: kernel durations
 and the idle gap before each kernel, over iterations [skip, skip+count) (an
-iteration starts at each k_btran launch)."""
+iteration starts at each k_price launch)."""
 import csv
 import sys
 from collections import defaultdict
 
 
-def main(path, skip=100, count=1000, first="k_btran"):
+def main(path, skip=100, count=1000, first="k_price"):
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
