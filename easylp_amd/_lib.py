@@ -48,7 +48,8 @@ class ElpControl(ctypes.Structure):
         ("sync_every", ctypes.c_int32),
         ("verbose", ctypes.c_int32),
         ("refactor_mode", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 6),
+        ("replicate", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 5),
     ]
 
 

@@ -72,6 +72,7 @@ struct elp_handle {
     std::vector<hipEvent_t> ev;  // pricing-kernel timing pairs (profile mode)
     int32_t* d_flag = nullptr;   // one int for cross-rank decisions
     int64_t ar_rows = 0;         // AR capacity in rows (grown at polls)
+    bool replicated = false;     // sharded, every rank holds all of A (Dev::Afull)
 };
 
 extern "C" void elp_default_control(elp_control* c) {
@@ -417,6 +418,11 @@ static int prep_load(elp_handle* h) {
         h->col0 = r * h->n / P;
         h->nloc = (r + 1) * h->n / P - h->col0;
     }
+    // replicate A on every rank when it fits (288 GB of HBM per MI355X): the
+    // entering column is then read locally and never exchanged
+    const double abytes = 8.0 * (double)h->m * (double)h->n;
+    h->replicated = h->comm.kind != 0 &&
+                    (h->ctl.replicate == 1 || (h->ctl.replicate == 0 && abytes <= 64.0 * (1ull << 30)));
     return alloc_all(h);
 }
 
@@ -426,12 +432,14 @@ extern "C" int elp_load_dense(elp_handle* h, const double* A, const int32_t* dir
     if (!h || !obj || (h->m > 0 && (!A || !dir || !rhs))) return fail(ELP_E_ARG, "elp_load_dense: NULL input");
     int rc = prep_load(h);
     if (rc) return rc;
-    const size_t cnt = (size_t)h->m * (size_t)h->nloc;
+    const int64_t c0 = h->replicated ? 0 : h->col0, nc = h->replicated ? h->n : h->nloc;
+    const size_t cnt = (size_t)h->m * (size_t)nc;
     HIPCHK(dalloc(&h->A_owned, cnt));
     if (cnt)
-        HIPCHK(hipMemcpyAsync(h->A_owned, A + (size_t)h->col0 * (size_t)h->m, cnt * sizeof(double),
+        HIPCHK(hipMemcpyAsync(h->A_owned, A + (size_t)c0 * (size_t)h->m, cnt * sizeof(double),
                               hipMemcpyHostToDevice, h->st));
-    h->d.A = h->A_owned;
+    h->d.A = h->A_owned + (size_t)(h->col0 - c0) * (size_t)h->m;
+    h->d.Afull = h->replicated ? h->A_owned : nullptr;
     rc = load_common(h, dir, rhs, obj, lo, up, maximize);
     h->stats.seconds_load = now_s() - t0;
     return rc;
@@ -446,6 +454,7 @@ extern "C" int elp_load_dense_device(elp_handle* h, const double* dA, const int3
     int rc = prep_load(h);
     if (rc) return rc;
     h->d.A = dA + (size_t)h->col0 * (size_t)h->m;
+    h->d.Afull = h->replicated ? dA : nullptr;
     rc = load_common(h, dir, rhs, obj, lo, up, maximize);
     h->stats.seconds_load = now_s() - t0;
     return rc;
@@ -456,15 +465,17 @@ extern "C" int elp_load_generated(elp_handle* h, uint64_t seed) {
     int rc = prep_load(h);
     if (rc) return rc;
     const int64_t m = h->m, n = h->n;
-    HIPCHK(dalloc(&h->A_owned, (size_t)m * (size_t)h->nloc));
+    const int64_t c0 = h->replicated ? 0 : h->col0, nc = h->replicated ? n : h->nloc;
+    HIPCHK(dalloc(&h->A_owned, (size_t)m * (size_t)nc));
     double *db = nullptr, *dc = nullptr;
     HIPCHK(dalloc(&db, m));
     HIPCHK(dalloc(&dc, n));
-    // generate this rank's shard of A plus the full b and c (c globally, for the objective)
+    // generate this rank's shard of A (all of it when replicated) plus the full
+    // b and c (c globally, for the objective)
     {
         Dev g = h->d;
-        g.n = (int32_t)h->nloc;
-        HIPCHK(launch_generate(g, seed, h->col0, n, h->A_owned, db, nullptr, h->st));
+        g.n = (int32_t)nc;
+        HIPCHK(launch_generate(g, seed, c0, n, h->A_owned, db, nullptr, h->st));
         g.n = (int32_t)n;
         HIPCHK(launch_generate(g, seed, 0, n, nullptr, db, dc, h->st));
     }
@@ -475,7 +486,8 @@ extern "C" int elp_load_generated(elp_handle* h, uint64_t seed) {
     HIPCHK(hipStreamSynchronize(h->st));
     (void)hipFree(db);
     (void)hipFree(dc);
-    h->d.A = h->A_owned;
+    h->d.A = h->A_owned + (size_t)(h->col0 - c0) * (size_t)m;
+    h->d.Afull = h->replicated ? h->A_owned : nullptr;
     rc = load_common(h, dir.data(), b.data(), c.data(), lo.data(), up.data(), 1);
     h->stats.seconds_load = now_s() - t0;
     return rc;
@@ -589,11 +601,24 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             if (h->comm.kind == 0) {
                 HIPCHK(launch_iteration(h->d, kub, nyub, h->phase, h->st, e0, e1));
             } else {
-                // sharded: local min-loc -> all-gather -> global min-loc + owner's
-                // column packet -> all-reduce (non-owners contribute zeros) -> tail
+                // sharded: local min-loc -> all-gather -> global min-loc.  Replicated
+                // A: a_R + bump FTRAN straight from the local copy -> tail.  Else the
+                // owner packs its column, all-reduce (non-owners contribute zeros).
                 HIPCHK(launch_iteration_head(h->d, kub, nyub, h->phase, h->comm.rank, h->st, e0, e1));
-                rc = h->comm.allgather(h->d.cand_xchg + h->comm.rank, h->d.cand_xchg, sizeof(Cand), h->st);
+                rc = h->comm.allgather(h->d.cand_xchg + h->comm.rank, h->d.cand_xchg, sizeof(CandX), h->st);
                 if (rc) return fail(rc, "candidate all-gather failed");
+                if (h->replicated) {
+                    hipError_t le = hipSuccess;
+                    if (launch_select_xftran(h->d, kub, h->st, &le)) {
+                        HIPCHK(le);
+                        HIPCHK(launch_iteration_tail(h->d, kub, h->phase, h->st, false));
+                        continue;
+                    }
+                    HIPCHK(launch_select_global(h->d, h->st));
+                    HIPCHK(launch_select_finish(h->d, h->st));
+                    HIPCHK(launch_iteration_tail(h->d, kub, h->phase, h->st));
+                    continue;
+                }
                 HIPCHK(launch_select_global(h->d, h->st));
                 rc = h->comm.allreduce_sum_f64(h->d.pkt, (size_t)h->m + 4, h->st);
                 if (rc) return fail(rc, "entering-column all-reduce failed");

@@ -84,6 +84,14 @@ struct Cand {
     int64_t j;  // -1: none
 };
 
+// a rank's best candidate as exchanged between shards: with every rank holding
+// all of A (Dev::Afull) the record also carries the column's (lb, ub, x, cost),
+// so the entering column never travels
+struct CandX {
+    Cand c;
+    double lb, ub, x, cost;
+};
+
 // Everything a kernel needs, passed by value (pointers into device memory).
 // Variable ids: replicated state (cover, Sl, candidates, q, trace) holds GLOBAL
 // ids -- structural j < N, slack N + i, artificial N + m + i; per-variable
@@ -94,11 +102,13 @@ struct Dev {
     int32_t m, n, nv, N;  // n: local columns; N: global columns
     int64_t col0;         // first global column of this shard
     int32_t world;        // ranks sharing the columns
-    int32_t sharded;      // 1: entering column comes from the exchanged packet
+    int32_t sharded;      // 1: column-sharded solve (world > 1 or a test transport)
     int64_t ldm;   // Minv leading dimension (= max(m,1))
     int64_t ldr;   // n rounded up to TILE_COLS
     int64_t arcap; // AR rows per column tile (capacity)
-    const double* A;  // column-major m x n
+    const double* A;  // column-major m x n (this shard's columns)
+    const double* Afull;  // sharded + replicated: all N columns (A = Afull + col0*m);
+                          // null: the entering column comes in the exchanged pkt
     double* AR;       // Y rows, tile-major: [ldr/128 tiles][arcap rows][128 cols]
                       // (a pricing wave streams one contiguous run of rows)
     double* AS;       // basic structural columns, column-major (m x m capacity)
@@ -113,7 +123,7 @@ struct Dev {
     double* pkt;             // entering column + (lb, ub, x, cost) exchanged across shards
     double* objg;            // global objective (N), for c_S of foreign basic columns
     double* ract;            // row activities sum_j a_ij x_j of nonzero nonbasic columns
-    Cand* cand_xchg;         // [world] local best candidates (all-gathered)
+    CandX* cand_xchg;        // [world] local best candidates (all-gathered)
     RCand* rcand;            // pass-2 candidates (capacity 2m)
     double *rlo, *rhi;       // per covered row: bounds of the covering unit variable
     int8_t* vstat;
@@ -147,6 +157,9 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
 hipError_t launch_iteration_head(const Dev& d, int k_ub, int ny_ub, int phase, int rank,
                                  hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_select_global(const Dev& d, hipStream_t st);
+// replicated A: global min-loc + a_R + bump FTRAN in one launch (false: the
+// bump is too large for it; use select_global + select_finish + tail(bump_ftran))
+bool launch_select_xftran(const Dev& d, int k_ub, hipStream_t st, hipError_t* err);
 hipError_t launch_select_finish(const Dev& d, hipStream_t st);
 hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t st,
                                  bool bump_ftran = true);

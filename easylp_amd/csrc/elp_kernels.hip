@@ -73,6 +73,13 @@ DEV int loc_of(const Dev& d, int g) {
     }
     return d.n + (g - d.N);
 }
+// the entering structural column q (global id): read in place on one GPU or
+// from the replicated A, else from the exchanged packet
+DEV const double* qcolumn(const Dev& d, int q) {
+    if (!d.sharded) return d.A + (size_t)(q - d.col0) * (size_t)d.m;
+    if (d.Afull) return d.Afull + (size_t)q * (size_t)d.m;
+    return d.pkt;
+}
 DEV bool cand_better(const Cand& a, const Cand& b, int bland) {
     if (a.j < 0) return false;
     if (b.j < 0) return true;
@@ -670,7 +677,19 @@ __global__ void __launch_bounds__(1024) k_select_local(Dev d, int ntiles, int ra
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
     const Cand best = local_best(d, ntiles, red);
-    if (threadIdx.x == 0) d.cand_xchg[rank] = best;
+    if (threadIdx.x == 0) {
+        CandX x;
+        x.c = best;
+        x.lb = x.ub = x.x = x.cost = 0.0;
+        const int ql = best.j >= 0 && best.j < d.N ? loc_of(d, (int)best.j) : -1;
+        if (ql >= 0) {
+            x.lb = d.lb[ql];
+            x.ub = d.ub[ql];
+            x.x = d.xval[ql];
+            x.cost = d.cost[ql];
+        }
+        d.cand_xchg[rank] = x;
+    }
     if (d.ptimer) price_timer_sum<1024>(d, ntiles, reinterpret_cast<unsigned long long*>(red));
 }
 
@@ -680,9 +699,9 @@ __global__ void __launch_bounds__(256) k_select_global(Dev d) {
     DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
     const int bland = c->bland;
-    Cand best = d.cand_xchg[0];
+    Cand best = d.cand_xchg[0].c;
     for (int r = 1; r < d.world; ++r)
-        if (cand_better(d.cand_xchg[r], best, bland)) best = d.cand_xchg[r];
+        if (cand_better(d.cand_xchg[r].c, best, bland)) best = d.cand_xchg[r].c;
     const int m = d.m;
     if (best.j < 0) {
         for (int i = threadIdx.x; i < m + 4; i += 256) d.pkt[i] = 0.0;
@@ -692,7 +711,17 @@ __global__ void __launch_bounds__(256) k_select_global(Dev d) {
     const int q = (int)best.j;
     const int ql = loc_of(d, q);
     const bool own = q < d.N && ql >= 0;
-    if (own) {
+    if (d.Afull) {  // replicated: the column is read in place, pkt carries the scalars
+        if (threadIdx.x == 0) {
+            int win = 0;
+            for (int r = 1; r < d.world; ++r)
+                if (cand_better(d.cand_xchg[r].c, d.cand_xchg[win].c, bland)) win = r;
+            d.pkt[m] = d.cand_xchg[win].lb;
+            d.pkt[m + 1] = d.cand_xchg[win].ub;
+            d.pkt[m + 2] = d.cand_xchg[win].x;
+            d.pkt[m + 3] = d.cand_xchg[win].cost;
+        }
+    } else if (own) {
         const double* col = d.A + (size_t)ql * (size_t)m;
         for (int i = threadIdx.x; i < m; i += 256) d.pkt[i] = col[i];
         if (threadIdx.x == 0) {
@@ -711,7 +740,51 @@ __global__ void __launch_bounds__(256) k_select_global(Dev d) {
 __global__ void __launch_bounds__(1024) k_select_finish(Dev d) {
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
-    gather_aR(d, c->q, d.pkt);
+    gather_aR(d, c->q, c->q < d.N ? qcolumn(d, c->q) : nullptr);
+}
+
+// Replicated A, after the all-gather of the ranks' records: every workgroup
+// takes the global min-loc (a total order: all agree), reads a_R from its own
+// copy of A and forms alpha_S for its 4 bump rows (k_select_ftran's shape).
+// Workgroup 0 publishes q and the column's (lb, ub, x, cost) in pkt[m..m+3].
+__global__ void __launch_bounds__(256) k_select_xftran(Dev d) {
+    extern __shared__ __attribute__((aligned(16))) double aRs[];  // [k]
+    DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    const int bland = c->bland, k = c->k, m = d.m;
+    int win = 0;
+    for (int r = 1; r < d.world; ++r)
+        if (cand_better(d.cand_xchg[r].c, d.cand_xchg[win].c, bland)) win = r;
+    const Cand best = d.cand_xchg[win].c;
+    if (best.j < 0) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) c->status = ST_PHASE_OPT;
+        return;
+    }
+    const int q = (int)best.j;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const CandX& x = d.cand_xchg[win];
+        d.pkt[m] = x.lb;
+        d.pkt[m + 1] = x.ub;
+        d.pkt[m + 2] = x.x;
+        d.pkt[m + 3] = x.cost;
+        entering_chosen(d, best);
+    }
+    if (q < d.N) {
+        const double* col = d.Afull + (size_t)q * (size_t)m;
+        for (int p = threadIdx.x; p < k; p += 256) aRs[p] = col[d.Rl[p]];
+    } else {
+        const int i0 = q - d.N;
+        for (int p = threadIdx.x; p < k; p += 256) aRs[p] = d.Rl[p] == i0 ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (p >= k) return;
+    const double* row = d.Minv + (size_t)p * d.ldm;
+    double acc = 0.0;
+    for (int i = lane; i < k; i += 64) acc = fma(row[i], aRs[i], acc);
+    acc = wave_tree(acc);
+    if (lane == 0) d.alS[p] = acc;
 }
 
 // ============================================================== FTRAN
@@ -873,9 +946,7 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt) {
                 if (u >= 0) {
                     double z = 0.0;
                     for (int ch = 0; ch < nch; ++ch) z = z + zp[ch * 64 + lane];
-                    const double aiq = q >= d.N ? (i == q - d.N ? 1.0 : 0.0)
-                                       : d.sharded ? d.pkt[i]
-                                                     : d.A[(size_t)(q - d.col0) * mm + i];
+                    const double aiq = q >= d.N ? (i == q - d.N ? 1.0 : 0.0) : qcolumn(d, q)[i];
                     const double alU = unit_sign(d, u, i) * (aiq - z);
                     d.alU[i] = alU;
                     ge = sig * alU;
@@ -1410,8 +1481,7 @@ __global__ void __launch_bounds__(256) k_update(Dev d, int nb_minv, int phase) {
     for (int64_t t = t0; t < d.m; t += tstride) {
         if (P.pcase == PC_A || P.pcase == PC_B) {
             const int pos = P.pcase == PC_A ? P.p : k;
-            d.AS[(size_t)pos * m + t] =
-                d.sharded ? d.pkt[t] : d.A[(size_t)(P.q - d.col0) * m + t];
+            d.AS[(size_t)pos * m + t] = qcolumn(d, P.q)[t];
         } else if (P.pcase == PC_C && P.b != P.last) {
             d.AS[(size_t)P.b * m + t] = d.AS[(size_t)P.last * m + t];
         }
@@ -1755,6 +1825,14 @@ hipError_t launch_iteration_head(const Dev& d, int k_ub, int ny_ub, int phase, i
 hipError_t launch_select_global(const Dev& d, hipStream_t st) {
     k_select_global<<<1, 256, 0, st>>>(d);
     return hipGetLastError();
+}
+
+bool launch_select_xftran(const Dev& d, int k_ub, hipStream_t st, hipError_t* err) {
+    const size_t lds = (size_t)k_ub * sizeof(double);
+    if (lds > 48 * 1024) return false;
+    k_select_xftran<<<cdiv(k_ub > 0 ? k_ub : 1, 4), 256, lds > 64 ? lds : 64, st>>>(d);
+    *err = hipGetLastError();
+    return true;
 }
 
 hipError_t launch_select_finish(const Dev& d, hipStream_t st) {

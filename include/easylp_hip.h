@@ -65,7 +65,13 @@ typedef struct elp_control {
     int32_t verbose;         /* 0 quiet; ELP_PROFILE_PRICE: time pricing kernel */
     int32_t refactor_mode;   /* 0: Newton-Schulz correction, Gauss-Jordan when
                                 max|I - M Minv| > 1e-6; 1: always Gauss-Jordan */
-    int32_t reserved[6];
+    int32_t replicate;       /* column-sharded solves (elp_comm_init*): 0 auto --
+                                every rank keeps all of A when m*n*8 <= 64 GiB, so
+                                the entering column is read locally and only the
+                                min-loc record is exchanged; 1 always; 2 never
+                                (each rank holds its shard, the entering column
+                                travels in an all-reduce) */
+    int32_t reserved[5];
 } elp_control;
 
 typedef struct elp_stats {

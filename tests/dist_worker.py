@@ -51,8 +51,9 @@ def transport_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def sharded_solve_worker(rank, world, port, q, cases):
-    """GPU: every rank solves the same LPs on one shared GPU with the host transport."""
+def sharded_solve_worker(rank, world, port, q, cases, replicate=0):
+    """GPU: every rank solves the same LPs on one shared GPU with the host transport.
+    replicate: elp_control.replicate (1 every rank holds all of A, 2 shards only)."""
     import numpy as np
     dist = _init(rank, world, port)
     import easylp_amd
@@ -62,13 +63,13 @@ def sharded_solve_worker(rank, world, port, q, cases):
     for case in cases:
         if case["kind"] == "generated":
             m, n = case["m"], case["n"]
-            p = easylp_amd.Problem(m, n)
+            p = easylp_amd.Problem(m, n, replicate=replicate)
             p.set_trace(200000)
             p.comm_init_host(t)
             p.load_generated(case["seed"])
         else:
             A, dirs, rhs, obj, lo, up, mx = case["lp"]
-            p = easylp_amd.Problem(A.shape[0], A.shape[1])
+            p = easylp_amd.Problem(A.shape[0], A.shape[1], replicate=replicate)
             p.set_trace(200000)
             p.comm_init_host(t)
             p.load_dense(A, dirs, rhs, obj, lo, up, mx)

@@ -1,5 +1,6 @@
 """Column-sharded solve on the GPU: 2 and 3 ranks (one process each, all on
-the one GPU of the test box, host transport over gloo) must reproduce the
+the one GPU of the test box, host transport over gloo), with A replicated on
+every rank or sharded, must reproduce the
 single-rank pivot trace, objective, x and basis bit for bit (the reduction
 order never spans shards; the min-loc order is total)."""
 import multiprocessing as mp
@@ -33,15 +34,17 @@ def _cases():
     ]
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_matches_oracle(world):
+@pytest.mark.parametrize("world,replicate", [(2, 1), (3, 1), (2, 2), (3, 2)])
+def test_sharded_matches_oracle(world, replicate):
+    """replicate 1: every rank holds all of A and only the min-loc record is
+    exchanged; 2: column shards only, the entering column is all-reduced."""
     from dist_worker import sharded_solve_worker
     from oracle import generate_dense, solve_dense as orc
     cases = _cases()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=sharded_solve_worker, args=(r, world, port, q, cases))
+    procs = [ctx.Process(target=sharded_solve_worker, args=(r, world, port, q, cases, replicate))
              for r in range(world)]
     for p in procs:
         p.start()
