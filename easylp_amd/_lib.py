@@ -20,7 +20,8 @@ ELP_PROFILE_EVENTS = 4  # HIP-event pricing timer
 # every entry point the header declares (checked by tests/test_abi.py)
 EXPORTS = (
     "elp_default_control", "elp_create", "elp_load_dense", "elp_load_dense_device",
-    "elp_load_generated", "elp_solve", "elp_iterate", "elp_get_solution", "elp_get_stats",
+    "elp_load_generated", "elp_load_csc", "elp_solve", "elp_iterate", "elp_get_solution",
+    "elp_get_stats",
     "elp_set_trace", "elp_get_trace", "elp_comm_unique_id", "elp_comm_init", "elp_comm_init_host",
     "elp_destroy", "elp_last_error", "elp_abi_version",
 )
@@ -102,6 +103,7 @@ def load(path: str | None = None):
     lib.elp_load_dense.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32]
     lib.elp_load_dense_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32]
     lib.elp_load_generated.argtypes = [vp, ctypes.c_uint64]
+    lib.elp_load_csc.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32]
     lib.elp_solve.argtypes = [vp, P(i32)]
     lib.elp_iterate.argtypes = [vp, i64, P(i32)]
     lib.elp_get_solution.argtypes = [vp, P(dbl), vp, vp, vp]
@@ -116,6 +118,7 @@ def load(path: str | None = None):
     lib.elp_last_error.restype = ctypes.c_char_p
     lib.elp_abi_version.restype = i32
     for name in ("elp_create", "elp_load_dense", "elp_load_dense_device", "elp_load_generated",
+                 "elp_load_csc",
                  "elp_solve", "elp_iterate", "elp_get_solution", "elp_get_stats",
                  "elp_set_trace", "elp_get_trace", "elp_comm_unique_id", "elp_comm_init",
                  "elp_comm_init_host"):

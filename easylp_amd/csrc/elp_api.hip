@@ -73,6 +73,7 @@ struct elp_handle {
     int32_t* d_flag = nullptr;   // one int for cross-rank decisions
     int64_t ar_rows = 0;         // AR capacity in rows (grown at polls)
     bool replicated = false;     // sharded, every rank holds all of A (Dev::Afull)
+    bool csc = false;            // A given in CSC (elp_load_csc)
 };
 
 extern "C" void elp_default_control(elp_control* c) {
@@ -101,7 +102,9 @@ static void free_dev(elp_handle* h) {
                     d.vvec,     d.colA, d.rhs,  d.vstat, d.cover, d.rpos, d.Rl,    d.Sl,
                     d.Yl,  d.ypos,  d.perm,  d.pivstep, d.nzlist, d.nzcount,
                     d.cand,     d.pstamp, d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand,
-                    d.pkt, d.objg, d.ract, d.cand_xchg, h->d_flag, d.cS, d.slo, d.shi, d.rlo, d.rhi};
+                    d.pkt, d.objg, d.ract, d.cand_xchg, h->d_flag, d.cS, d.slo, d.shi, d.rlo, d.rhi,
+                    (void*)d.cptr, (void*)d.rind, (void*)d.cval, (void*)d.rptr, (void*)d.cind,
+                    (void*)d.rval, d.qcol};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     h->A_owned = nullptr;
@@ -161,6 +164,8 @@ static int alloc_all(elp_handle* h) {
     d.ldr = ((n + TILE_COLS - 1) / TILE_COLS) * TILE_COLS;
     d.infinity = h->ctl.infinity;
     d.ptimer = (h->ctl.verbose & ELP_PROFILE_PRICE) ? 1 : 0;
+    d.csc = h->csc ? 1 : 0;
+    d.force_select = std::getenv("ELP_FORCE_SELECT") ? 1 : 0;  // test hook
     const size_t nv = (size_t)(n + 2 * m);
     hipError_t e = hipSuccess;
     auto A = [&](hipError_t x) {
@@ -170,6 +175,7 @@ static int alloc_all(elp_handle* h) {
     h->ar_rows = std::min<int64_t>(mm, 1024);
     if (const char* e = std::getenv("ELP_AR_INIT_ROWS"))  // test hook: force growth
         h->ar_rows = std::max<int64_t>(1, std::min<int64_t>(mm, std::atoll(e)));
+    if (h->csc) h->ar_rows = 1;  // CSC prices from the columns: no AR
     d.arcap = h->ar_rows;
     A(dalloc(&d.AR, (size_t)h->ar_rows * (size_t)d.ldr));
     A(dalloc(&d.AS, (size_t)mm * (size_t)mm));
@@ -222,6 +228,7 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.nzcount, 1));
     A(dalloc(&d.cand, (size_t)((n + TILE_COLS - 1) / TILE_COLS) + 64));
     A(dalloc(&d.pstamp, 2 * ((size_t)((n + TILE_COLS - 1) / TILE_COLS) + 64)));
+    if (h->csc) A(dalloc(&d.qcol, mm));
     A(dalloc(&d.ctl, 1));
     A(dalloc(&d.trace, (size_t)(h->trace_cap > 0 ? 2 * h->trace_cap : 2)));
     if (e != hipSuccess) {
@@ -233,6 +240,7 @@ static int alloc_all(elp_handle* h) {
     //  results are discarded, so AR needs no clearing); Minv / work start clean
     A(hipMemsetAsync(d.Minv, 0, (size_t)mm * (size_t)mm * sizeof(double), h->st));
     A(hipMemsetAsync(d.MinvT, 0, (size_t)mm * (size_t)mm * sizeof(double), h->st));
+    if (d.qcol) A(hipMemsetAsync(d.qcol, 0, (size_t)mm * sizeof(double), h->st));
 
     if (e != hipSuccess) {
         free_dev(h);
@@ -243,6 +251,7 @@ static int alloc_all(elp_handle* h) {
 
 // Grow AR to hold at least `rows` Y rows (device idle: called at a poll).
 static int ensure_ar(elp_handle* h, int64_t rows) {
+    if (h->csc) return 0;
     rows = std::min<int64_t>(rows, std::max<int64_t>(h->m, 1));
     if (rows <= h->ar_rows) return 0;
     const int64_t cap = std::min<int64_t>(std::max<int64_t>(h->m, 1), std::max(rows, 2 * h->ar_rows));
@@ -354,6 +363,7 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
     c.tol_pivot = h->ctl.tol_pivot;
     c.trace_cap = h->trace_cap;
     c.unb_var = -1;
+    c.qcol_var = -1;
     *h->hctl = c;
     HIPCHK(hipMemcpyAsync(d.ctl, h->hctl, sizeof(DevCtl), hipMemcpyHostToDevice, h->st));
     HIPCHK(launch_init_cols(d, dlo, dup, h->st));
@@ -408,11 +418,14 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
     return 0;
 }
 
-static int prep_load(elp_handle* h) {
+static int prep_load(elp_handle* h, bool csc = false) {
     if (!h) return fail(ELP_E_ARG, "NULL handle");
     HIPCHK(hipSetDevice(h->dev));
     if (h->loaded) free_dev(h);
     h->loaded = false;
+    h->csc = csc;
+    if (csc && h->comm.kind != 0)
+        return fail(ELP_E_UNSUPPORTED, "elp_load_csc: column-sharded CSC solves are not supported");
     if (h->comm.world > 1) {
         const int64_t P = h->comm.world, r = h->comm.rank;
         h->col0 = r * h->n / P;
@@ -456,6 +469,75 @@ extern "C" int elp_load_dense_device(elp_handle* h, const double* dA, const int3
     h->d.A = dA + (size_t)h->col0 * (size_t)h->m;
     h->d.Afull = h->replicated ? dA : nullptr;
     rc = load_common(h, dir, rhs, obj, lo, up, maximize);
+    h->stats.seconds_load = now_s() - t0;
+    return rc;
+}
+
+// CSC input: validate, build the CSR copy on the host (row activities), upload.
+extern "C" int elp_load_csc(elp_handle* h, const int64_t* colptr, const int32_t* rowind,
+                            const double* val, const int32_t* dir, const double* rhs,
+                            const double* obj, const double* lo, const double* up, int32_t maximize) {
+    const double t0 = now_s();
+    if (!h || !obj || !colptr || (h->m > 0 && (!dir || !rhs))) return fail(ELP_E_ARG, "elp_load_csc: NULL input");
+    const int64_t m = h->m, n = h->n;
+    const int64_t nnz = colptr[n];
+    if (colptr[0] != 0 || nnz < 0 || (nnz > 0 && (!rowind || !val)))
+        return fail(ELP_E_ARG, "elp_load_csc: colptr[0] must be 0 and colptr[n] = nnz >= 0");
+    if (nnz > INT32_MAX) return fail(ELP_E_ARG, "elp_load_csc: more than 2^31-1 nonzeros");
+    for (int64_t j = 0; j < n; ++j) {
+        if (colptr[j + 1] < colptr[j]) return fail(ELP_E_ARG, "elp_load_csc: colptr must be nondecreasing");
+        for (int64_t t = colptr[j]; t < colptr[j + 1]; ++t) {
+            if (rowind[t] < 0 || rowind[t] >= m) return fail(ELP_E_ARG, "elp_load_csc: row index out of range");
+            if (t > colptr[j] && rowind[t] <= rowind[t - 1])
+                return fail(ELP_E_ARG, "elp_load_csc: row indices must be strictly increasing within a column");
+            if (!std::isfinite(val[t])) return fail(ELP_E_ARG, "elp_load_csc: non-finite coefficient");
+        }
+    }
+    int rc = prep_load(h, true);
+    if (rc) return rc;
+    // CSR copy: a counting sort by row keeps the columns ascending within a row
+    std::vector<int64_t> rp((size_t)m + 1, 0);
+    for (int64_t t = 0; t < nnz; ++t) rp[(size_t)rowind[t] + 1]++;
+    for (int64_t i = 0; i < m; ++i) rp[(size_t)i + 1] += rp[(size_t)i];
+    std::vector<int32_t> ci((size_t)nnz);
+    std::vector<double> rv((size_t)nnz);
+    {
+        std::vector<int64_t> next(rp.begin(), rp.end() - 1);
+        for (int64_t j = 0; j < n; ++j)
+            for (int64_t t = colptr[j]; t < colptr[j + 1]; ++t) {
+                const int64_t at = next[(size_t)rowind[t]]++;
+                ci[(size_t)at] = (int32_t)j;
+                rv[(size_t)at] = val[t];
+            }
+    }
+    Dev& d = h->d;
+    d.nnz = nnz;
+    int64_t *dcp = nullptr, *drp = nullptr;
+    int32_t *dri = nullptr, *dci = nullptr;
+    double *dcv = nullptr, *drv = nullptr;
+    HIPCHK(dalloc(&dcp, (size_t)n + 1));
+    HIPCHK(dalloc(&dri, (size_t)nnz));
+    HIPCHK(dalloc(&dcv, (size_t)nnz));
+    HIPCHK(dalloc(&drp, (size_t)m + 1));
+    HIPCHK(dalloc(&dci, (size_t)nnz));
+    HIPCHK(dalloc(&drv, (size_t)nnz));
+    d.cptr = dcp;
+    d.rind = dri;
+    d.cval = dcv;
+    d.rptr = drp;
+    d.cind = dci;
+    d.rval = drv;
+    HIPCHK(hipMemcpyAsync(dcp, colptr, ((size_t)n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, h->st));
+    HIPCHK(hipMemcpyAsync(drp, rp.data(), ((size_t)m + 1) * sizeof(int64_t), hipMemcpyHostToDevice, h->st));
+    if (nnz) {
+        HIPCHK(hipMemcpyAsync(dri, rowind, (size_t)nnz * sizeof(int32_t), hipMemcpyHostToDevice, h->st));
+        HIPCHK(hipMemcpyAsync(dcv, val, (size_t)nnz * sizeof(double), hipMemcpyHostToDevice, h->st));
+        HIPCHK(hipMemcpyAsync(dci, ci.data(), (size_t)nnz * sizeof(int32_t), hipMemcpyHostToDevice, h->st));
+        HIPCHK(hipMemcpyAsync(drv, rv.data(), (size_t)nnz * sizeof(double), hipMemcpyHostToDevice, h->st));
+    }
+    d.A = nullptr;
+    rc = load_common(h, dir, rhs, obj, lo, up, maximize);
+    HIPCHK(hipStreamSynchronize(h->st));  // the host CSR staging goes out of scope
     h->stats.seconds_load = now_s() - t0;
     return rc;
 }

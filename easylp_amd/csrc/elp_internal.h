@@ -70,6 +70,7 @@ struct DevCtl {
     unsigned long long price_ticks;
     int64_t price_timed;
     double price_tbytes;
+    int32_t qcol_var, pad6;  // CSC: the variable whose column is scattered in Dev::qcol
 };
 
 // Harris pass-2 candidate (a superset of the global candidates: exact ratio
@@ -135,6 +136,18 @@ struct Dev {
     int64_t* trace;
     int32_t maximize, pad2;
     double infinity;
+    // CSC input (elp_load_csc, one GPU): A is null, columns live in cptr/rind/cval
+    // (rows ascending), a CSR copy serves the row activities, and the entering
+    // column is scattered into the dense qcol each iteration
+    int32_t csc, force_select;  // force_select: test hook (ELP_FORCE_SELECT), large-bump launch shape
+    int64_t nnz;
+    const int64_t* cptr;
+    const int32_t* rind;
+    const double* cval;
+    const int64_t* rptr;
+    const int32_t* cind;
+    const double* rval;
+    double* qcol;
 };
 
 // ---------------------------------------------------------------- launches

@@ -76,6 +76,7 @@ DEV int loc_of(const Dev& d, int g) {
 // the entering structural column q (global id): read in place on one GPU or
 // from the replicated A, else from the exchanged packet
 DEV const double* qcolumn(const Dev& d, int q) {
+    if (d.csc) return d.qcol;
     if (!d.sharded) return d.A + (size_t)(q - d.col0) * (size_t)d.m;
     if (d.Afull) return d.Afull + (size_t)q * (size_t)d.m;
     return d.pkt;
@@ -209,6 +210,21 @@ __global__ void k_row_chain(Dev d) {
     for (int t = 0; t < nz; ++t) {
         const int j = d.nzlist[t];
         acc = fma(d.A[(size_t)j * (size_t)d.m + (size_t)i], d.xval[j], acc);
+    }
+    d.ract[i] = acc;
+}
+
+// CSC input: the same chain over row i's CSR entries (ascending j), with the
+// nonzero-list filter (nonbasic, x_j != 0) applied per entry; zero entries of
+// the dense layout contribute fma(0, x, acc) = acc there, so both agree
+__global__ void k_row_chain_csr(Dev d) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= d.m) return;
+    double acc = d.ract[i];
+    for (int64_t t = d.rptr[i]; t < d.rptr[i + 1]; ++t) {
+        const int j = d.cind[t];
+        const double xj = d.xval[j];
+        if (d.vstat[j] != VS_BASIC && xj != 0.0) acc = fma(d.rval[t], xj, acc);
     }
     d.ract[i] = acc;
 }
@@ -495,6 +511,105 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d) {
     }
 }
 
+// algorithmic bytes of one pricing pass.  Dense: the AR sweep (8|Y|n), c and
+// status (9n), y_Y and Yl (12|Y|).  CSC: row index + value per nonzero (12 nnz),
+// column pointer, c, status (17n); the y gathers hit L2 (m doubles)
+DEV double price_pass_bytes(const Dev& d, int ny) {
+    if (d.csc) return 12.0 * (double)d.nnz + 17.0 * (double)d.n + 8.0 * (double)d.m;
+    return 8.0 * (double)ny * (double)d.n + 9.0 * (double)d.n + 12.0 * (double)ny;
+}
+
+// CSC pricing: one workgroup = one tile of TILE_COLS columns, one thread per
+// column.  The tile's nonzeros are contiguous in the CSC arrays: the workgroup
+// stages them in LDS with coalesced loads (value, and y gathered at the row
+// index), then each thread runs its column's fma chain from LDS in ascending
+// row order (oracle price_mode 1).  Tiles with more than CSC_STAGE nonzeros
+// read straight from global memory (same order).
+constexpr int CSC_STAGE = 2048;  // staged nonzeros per tile: 32 KiB of LDS
+__global__ void __launch_bounds__(TILE_COLS) k_price_csc(Dev d) {
+    __shared__ double sv[CSC_STAGE], sy[CSC_STAGE];
+    __shared__ Cand red[TILE_COLS / 64];
+    const DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    if (d.ptimer && threadIdx.x == 0) d.pstamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    const int bland = c->bland;
+    const int64_t j0 = (int64_t)blockIdx.x * TILE_COLS;
+    const int64_t j = j0 + threadIdx.x;
+    const int64_t jend = j0 + TILE_COLS < d.n ? j0 + TILE_COLS : d.n;
+    const int64_t s0 = d.cptr[j0], s1 = d.cptr[jend];
+    const bool staged = s1 - s0 <= CSC_STAGE;
+    if (staged) {
+        for (int64_t t = s0 + threadIdx.x; t < s1; t += TILE_COLS) {
+            sv[t - s0] = d.cval[t];
+            sy[t - s0] = d.y[d.rind[t]];
+        }
+        __syncthreads();
+    }
+    double acc = 0.0;
+    if (j < d.n) {
+        const int64_t a = d.cptr[j], b = d.cptr[j + 1];
+        if (staged) {
+            for (int64_t t = a - s0; t < b - s0; ++t) acc = fma(sv[t], sy[t], acc);
+        } else {
+            for (int64_t t = a; t < b; ++t) acc = fma(d.cval[t], d.y[d.rind[t]], acc);
+        }
+    }
+    Cand best;
+    best.j = -1;
+    best.score = 0.0;
+    best.d = 0.0;
+    if (j < d.n) {
+        const int8_t vs = d.vstat[j];
+        if (vs != VS_BASIC && vs != VS_FIXED) {
+            const double dj = d.cost[j] - acc;
+            const double dtol = c->tol_dual;
+            if ((vs == VS_LOWER || vs == VS_FREE) && dj < -dtol) {
+                best.j = d.col0 + j;
+                best.score = -dj;
+                best.d = dj;
+            } else if ((vs == VS_UPPER || vs == VS_FREE) && dj > dtol) {
+                best.j = d.col0 + j;
+                best.score = dj;
+                best.d = dj;
+            }
+        }
+    }
+    best = block_best<TILE_COLS>(best, bland, red);
+    if (threadIdx.x == 0) {
+        d.cand[blockIdx.x] = best;
+        if (d.ptimer) d.pstamp[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
+// CSC: a_R[p] = A[R_p, q] by scattering column q's nonzeros through rpos
+// (block-wide; aR zeroed first).  Structural q only.
+DEV void scatter_aR_csc(const Dev& d, int q, double* aR, int k) {
+    for (int p = threadIdx.x; p < k; p += blockDim.x) aR[p] = 0.0;
+    __syncthreads();
+    const int64_t jl = (int64_t)q - d.col0;
+    for (int64_t t = d.cptr[jl] + threadIdx.x; t < d.cptr[jl + 1]; t += blockDim.x) {
+        const int p = d.rpos[d.rind[t]];
+        if (p >= 0 && p < k) aR[p] = d.cval[t];
+    }
+}
+
+// CSC: replace the dense copy of the previous entering column in qcol by
+// column q (one workgroup; q < 0 or a slack: just clear)
+DEV void scatter_qcol_csc(const Dev& d, int q) {
+    DevCtl* c = d.ctl;
+    const int prev = c->qcol_var;
+    if (prev >= 0 && prev < d.N) {
+        const int64_t pl = (int64_t)prev - d.col0;
+        for (int64_t t = d.cptr[pl] + threadIdx.x; t < d.cptr[pl + 1]; t += blockDim.x) d.qcol[d.rind[t]] = 0.0;
+    }
+    __syncthreads();
+    if (q >= 0 && q < d.N) {
+        const int64_t jl = (int64_t)q - d.col0;
+        for (int64_t t = d.cptr[jl] + threadIdx.x; t < d.cptr[jl + 1]; t += blockDim.x) d.qcol[d.rind[t]] = d.cval[t];
+    }
+    if (threadIdx.x == 0) c->qcol_var = q;
+}
+
 // Pricing-pass timer: first start to last end over the tiles' stamps (one
 // workgroup of NT threads), added to the control block with the pass's bytes.
 template <int NT>
@@ -524,7 +639,7 @@ DEV void price_timer_sum(const Dev& d, int ntiles, unsigned long long* red) {
         const int ny = c->ny;
         c->price_ticks += hi - lo;
         c->price_timed++;
-        c->price_tbytes += 8.0 * (double)ny * (double)d.n + 9.0 * (double)d.n + 12.0 * (double)ny;
+        c->price_tbytes += price_pass_bytes(d, ny);
     }
 }
 
@@ -571,7 +686,7 @@ DEV void entering_chosen(const Dev& d, const Cand& best) {
     const int ny = c->ny;
     c->ncand = 0;
     // algorithmic bytes of this pricing pass: AR sweep + c + status + y_Y + Yl
-    c->price_bytes += 8.0 * (double)ny * (double)d.n + 9.0 * (double)d.n + 12.0 * (double)ny;
+    c->price_bytes += price_pass_bytes(d, ny);
     c->price_passes++;
     c->q = (int)best.j;
     c->dq = best.d;
@@ -601,6 +716,14 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles) {
     const int q = (int)best.j;
     if (threadIdx.x == 0) entering_chosen(d, best);
     if (d.ptimer) price_timer_sum<1024>(d, ntiles, reinterpret_cast<unsigned long long*>(red));
+    if (d.csc) {  // dense copy of the entering column + a_R through rpos
+        scatter_qcol_csc(d, q);
+        if (q < d.N) {
+            __syncthreads();
+            scatter_aR_csc(d, q, d.aR, d.ctl->k);
+            return;
+        }
+    }
     // one GPU: the full column is read in place by k_ftran_zr / k_update
     gather_aR(d, q, q < d.N ? d.A + (size_t)(q - d.col0) * (size_t)d.m : nullptr);
 }
@@ -654,7 +777,13 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles) {
         price_timer_sum<256>(d, ntiles, reinterpret_cast<unsigned long long*>(aRs));
         return;
     }
-    if (q < d.N) {
+    if (d.csc && blockIdx.x == gridDim.x - 1 - d.ptimer) {  // CSC: dense entering column
+        scatter_qcol_csc(d, q);
+        return;
+    }
+    if (q < d.N && d.csc) {
+        scatter_aR_csc(d, q, aRs, k);
+    } else if (q < d.N) {
         const double* col = d.A + (size_t)(q - d.col0) * (size_t)d.m;
         for (int p = threadIdx.x; p < k; p += 256) aRs[p] = col[d.Rl[p]];
     } else {
@@ -1486,7 +1615,7 @@ __global__ void __launch_bounds__(256) k_update(Dev d, int nb_minv, int phase) {
             d.AS[(size_t)P.b * m + t] = d.AS[(size_t)P.last * m + t];
         }
     }
-    if (P.y_rm_slot >= 0 || P.y_ap_slot >= 0) {
+    if (!d.csc && (P.y_rm_slot >= 0 || P.y_ap_slot >= 0)) {  // CSC prices from the columns
         for (int64_t j = t0; j < d.n; j += tstride) {
             if (P.y_rm_slot >= 0 && P.y_rm_slot != P.y_rm_last)
                 d.AR[ar_at(d, P.y_rm_slot, j)] = d.AR[ar_at(d, P.y_rm_last, j)];
@@ -1712,7 +1841,7 @@ hipError_t launch_init_cols(const Dev& d, const double* lo, const double* up, hi
 }
 
 hipError_t launch_fill_AR(const Dev& d, hipStream_t st) {
-    if (d.m > 0) {
+    if (d.m > 0 && !d.csc) {
         dim3 g(cdiv(d.n, 256), (unsigned)(d.m < 4096 ? d.m : 4096));
         k_fill_AR<<<g, 256, 0, st>>>(d);
     }
@@ -1731,7 +1860,8 @@ hipError_t launch_nzlist(const Dev& d, hipStream_t st) {
 }
 
 hipError_t launch_row_chain(const Dev& d, hipStream_t st) {
-    if (d.m > 0) k_row_chain<<<cdiv(d.m, 256), 256, 0, st>>>(d);
+    if (d.m > 0 && d.csc) k_row_chain_csr<<<cdiv(d.m, 256), 256, 0, st>>>(d);
+    else if (d.m > 0) k_row_chain<<<cdiv(d.m, 256), 256, 0, st>>>(d);
     return hipGetLastError();
 }
 
@@ -1761,7 +1891,8 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int phase, hipStrea
     }
     const unsigned ntiles = cdiv(d.n, TILE_COLS);
     if (ev0) (void)hipEventRecord(ev0, st);
-    k_price<<<ntiles, PRICE_THREADS, 0, st>>>(d);
+    if (d.csc) k_price_csc<<<ntiles, TILE_COLS, 0, st>>>(d);
+    else k_price<<<ntiles, PRICE_THREADS, 0, st>>>(d);
     if (ev1) (void)hipEventRecord(ev1, st);
     return hipGetLastError();
 }
@@ -1776,13 +1907,13 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
         // k <= 4096); larger bumps use a private slice of zpart per row tile
         const size_t lds = (size_t)cdiv(k_ub, ZCHUNK) * 64 * sizeof(double);
         // + 1: the snapshot workgroup
-        if (lds <= 64 * 1024) k_ftran_zr<true><<<nrt + nbt + 1, 64 * ZR_WAVES, lds, st>>>(d, nrt);
+        if (lds <= 64 * 1024 && !d.force_select) k_ftran_zr<true><<<nrt + nbt + 1, 64 * ZR_WAVES, lds, st>>>(d, nrt);
         else k_ftran_zr<false><<<nrt + nbt + 1, 64 * ZR_WAVES, 0, st>>>(d, nrt);
     }
     // ratio test + (cases B/D) B^-1 row: one workgroup per 4 bump columns
     {
         const size_t lds = (size_t)k_ub * sizeof(double);
-        const int lds_row = lds <= 48 * 1024;
+        const int lds_row = lds <= 48 * 1024 && !d.force_select;
         k_ratio<<<cdiv(k_ub > 0 ? k_ub : 1, 4), 256, lds_row ? lds : 0, st>>>(d, phase, nrt + nbt, lds_row);
     }
     {
@@ -1804,9 +1935,11 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
     if (e != hipSuccess) return e;
     const int ntiles = (int)cdiv(d.n, TILE_COLS);
     const size_t lds = (size_t)k_ub * sizeof(double);
-    if (lds <= 48 * 1024) {  // fused select + bump FTRAN
+    if (lds <= 48 * 1024 && !d.force_select) {  // fused select + bump FTRAN
         const size_t ldsz = lds > 64 ? lds : 64;  // the timer workgroup reduces in it
-        k_select_ftran<<<cdiv(k_ub > 0 ? k_ub : 1, 4) + (d.ptimer ? 1 : 0), 256, ldsz, st>>>(d, ntiles);
+        // + the timer workgroup, + the CSC column-scatter workgroup
+        const unsigned g = cdiv(k_ub > 0 ? k_ub : 1, 4) + (d.ptimer ? 1 : 0) + (d.csc ? 1 : 0);
+        k_select_ftran<<<g, 256, ldsz, st>>>(d, ntiles);
         return launch_iteration_tail(d, k_ub, phase, st, false);
     }
     k_select<<<1, 1024, 0, st>>>(d, ntiles);
@@ -1829,7 +1962,7 @@ hipError_t launch_select_global(const Dev& d, hipStream_t st) {
 
 bool launch_select_xftran(const Dev& d, int k_ub, hipStream_t st, hipError_t* err) {
     const size_t lds = (size_t)k_ub * sizeof(double);
-    if (lds > 48 * 1024) return false;
+    if (lds > 48 * 1024 || d.force_select) return false;
     k_select_xftran<<<cdiv(k_ub > 0 ? k_ub : 1, 4), 256, lds > 64 ? lds : 64, st>>>(d);
     *err = hipGetLastError();
     return true;

@@ -140,6 +140,24 @@ class Problem:
             self._h, ctypes.c_void_p(int(dA_ptr)), d.ctypes.data, rhs.ctypes.data, obj.ctypes.data,
             lo.ctypes.data, up.ctypes.data, int(bool(maximize))), "elp_load_dense_device")
 
+    def load_csc(self, colptr, rowind, val, dirs, rhs, obj, lo=None, up=None, maximize=False) -> None:
+        """Sparse A in compressed sparse columns (rows strictly increasing per column)."""
+        m, n = self.m, self.n
+        colptr = np.ascontiguousarray(colptr, dtype=np.int64).reshape(n + 1)
+        rowind = np.ascontiguousarray(rowind, dtype=np.int32).reshape(-1)
+        val = np.ascontiguousarray(val, dtype=np.float64).reshape(-1)
+        d = dir_codes(dirs)
+        rhs = np.ascontiguousarray(rhs, dtype=np.float64).reshape(m)
+        obj = np.ascontiguousarray(obj, dtype=np.float64).reshape(n)
+        lo = np.zeros(n) if lo is None else np.ascontiguousarray(lo, dtype=np.float64)
+        up = np.full(n, np.inf) if up is None else np.ascontiguousarray(up, dtype=np.float64)
+        self._keep = (colptr, rowind, val, d, rhs, obj, lo, up)
+        check(self._lib.elp_load_csc(
+            self._h, colptr.ctypes.data, rowind.ctypes.data if rowind.size else None,
+            val.ctypes.data if val.size else None, d.ctypes.data if m else None,
+            rhs.ctypes.data if m else None, obj.ctypes.data, lo.ctypes.data, up.ctypes.data,
+            int(bool(maximize))), "elp_load_csc")
+
     def load_generated(self, seed: int) -> None:
         check(self._lib.elp_load_generated(self._h, int(seed)), "elp_load_generated")
 
@@ -176,6 +194,28 @@ class Problem:
                                          y.ctypes.data, basis.ctypes.data), "elp_get_solution")
         tr = self.trace() if self._trace_cap else None
         return Solution(status, obj.value, x, y[:m], basis[:m], self.stats(), tr)
+
+
+def csc_arrays(A):
+    """(colptr, rowind, val) of a scipy.sparse matrix or dense array: canonical
+    CSC (duplicates summed, rows sorted), explicit zeros kept."""
+    import scipy.sparse as sp
+    M = sp.csc_matrix(A, dtype=np.float64)
+    M.sum_duplicates()
+    M.sort_indices()
+    return (M.indptr.astype(np.int64), M.indices.astype(np.int32), M.data.astype(np.float64),
+            M.shape)
+
+
+def solve_sparse(A, dirs, rhs, obj, lo=None, up=None, maximize=False, trace=0, **control) -> Solution:
+    """One-shot solve with A sparse (scipy.sparse or dense array) through the CSC path."""
+    colptr, rowind, val, (m, n) = csc_arrays(A)
+    with Problem(m, n, **control) as p:
+        if trace:
+            p.set_trace(trace)
+        p.load_csc(colptr, rowind, val, dirs, rhs, obj, lo, up, maximize)
+        st = p.solve()
+        return p.solution(st)
 
 
 def solve_dense(A, dirs, rhs, obj, lo=None, up=None, maximize=False, trace=0, **control) -> Solution:

@@ -125,6 +125,16 @@ int elp_load_dense_device(elp_handle* h, const double* dA, const int32_t* dir, c
                           const double* obj, const double* lo, const double* up,
                           int32_t maximize);
 
+/* Sparse A in compressed sparse columns (BASELINE config 5):
+ * colptr[n+1] (colptr[0] = 0, colptr[n] = nnz), rowind[nnz] strictly increasing
+ * within each column, val[nnz] finite.  Same problem semantics as
+ * elp_load_dense; pricing then sweeps the nonzeros (12 bytes each) instead of
+ * dense rows.  One GPU only (ELP_E_UNSUPPORTED after elp_comm_init*).  Inputs
+ * are copied. */
+int elp_load_csc(elp_handle* h, const int64_t* colptr, const int32_t* rowind, const double* val,
+                 const int32_t* dir, const double* rhs, const double* obj, const double* lo,
+                 const double* up, int32_t maximize);
+
 /* Synthetic dense LP of SURVEY.md 8d generated on the device (bench / tests):
  * maximize c'x, A x <= b, x >= 0, A_ij, c_j ~ U[0,1), b_i = n/8 + U n/4,
  * counter-based (seed, stream, global index) so every rank / the oracle

@@ -29,7 +29,7 @@ class OrcControl(ctypes.Structure):
         ("degen_switch", ctypes.c_int32),
         ("t_mark_iter", ctypes.c_int64),
         ("refactor_mode", ctypes.c_int32),
-        ("pad", ctypes.c_int32),
+        ("price_mode", ctypes.c_int32),
     ]
 
 

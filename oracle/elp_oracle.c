@@ -12,6 +12,9 @@
  *            FTRAN / BTRAN / B^-1 rows, phase-1 c_S correction, phase-1 sum
  *   zchunk : chunks of 32 bump positions, fma chain, sequential sum
  *   seq    : one fma chain in index order (row activities)
+ *   column : price_mode 1 (the CSC path, elp_load_csc): d_j = c_j - one fma
+ *            chain over column j's nonzero rows in ascending row order, with
+ *            the full dual vector y (zero on slack-covered rows)
  *
  * Algorithm (bounded primal revised simplex, minimisation form):
  *   - rows a_i'x + s_i = b_i; slack bounds encode dir (R/class.R:271-274,
@@ -102,6 +105,7 @@ typedef struct {
     int8_t* used;
     int64_t* perm;
     double tol_inf;
+    int64_t nnz;      /* nonzeros of A (price_mode 1 byte count)          */
     int64_t gj_count; /* refactors that needed a fresh Gauss-Jordan */
     int refactor_mode;
 } orc_t;
@@ -371,6 +375,20 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
         const int64_t ny = s->ny;
         for (int64_t p = 0; p < ny; ++p) s->yy[p] = s->y[s->Yl[p]];
         const int64_t L = (ny + PRICE_SPLIT - 1) / PRICE_SPLIT;
+        if (ctl->price_mode == 1) {
+            /* column chains (CSC): the sum lands in part[0], part[1..] stay 0
+             * and add exactly */
+            for (int w = 1; w < PRICE_SPLIT; ++w)
+                for (int64_t j = 0; j < n; ++j) s->part[(size_t)w * (size_t)n + (size_t)j] = 0.0;
+            for (int64_t j = 0; j < n; ++j) {
+                const double* col = &s->A[(size_t)j * (size_t)m];
+                double acc = 0.0;
+                for (int64_t i = 0; i < m; ++i)
+                    if (col[i] != 0.0) acc = fma(col[i], s->y[i], acc);
+                s->part[j] = acc;
+            }
+            st->price_bytes += 12.0 * (double)s->nnz + 17.0 * (double)n;
+        } else {
         for (int w = 0; w < PRICE_SPLIT; ++w) {
             double* pw = s->part + (size_t)w * (size_t)n;
             for (int64_t j = 0; j < n; ++j) pw[j] = 0.0;
@@ -382,6 +400,7 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
             }
         }
         st->price_bytes += 8.0 * ((double)ny * (double)n + (double)n + (double)ny);
+        }
         int64_t q = -1;
         double qscore = 0.0, dq = 0.0;
         const double dtol = ctl->tol_dual;
@@ -664,7 +683,7 @@ void orc_default_control(orc_control* c) {
     c->degen_switch = 50;
     c->t_mark_iter = -1;
     c->refactor_mode = 0;
-    c->pad = 0;
+    c->price_mode = 0;
 }
 
 static int cmp_i64(const void* a, const void* b) {
@@ -699,6 +718,8 @@ int orc_solve_dense(int64_t m, int64_t n, const double* A, const int32_t* dir, c
     s->n = n;
     s->nv = n + 2 * m;
     s->A = A;
+    s->nnz = 0;
+    for (size_t t = 0; t < (size_t)m * (size_t)n; ++t) s->nnz += A[t] != 0.0;
     s->refactor_mode = ctl.refactor_mode;
     const int64_t nv = s->nv, mm = m > 0 ? m : 1;
     s->b = dalloc((size_t)mm);

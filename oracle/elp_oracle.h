@@ -40,7 +40,9 @@ typedef struct orc_control {
     int64_t t_mark_iter;   /* record the wall time when this many iterations
                               have run (stats.seconds_at_mark); <0: never     */
     int32_t refactor_mode; /* 0 Newton-Schulz (GJ fallback), 1 always GJ     */
-    int32_t pad;
+    int32_t price_mode;    /* 0 dense: chunked AR sweep over the Y rows;
+                              1 CSC path: one fma chain per column over its
+                              nonzero rows in ascending order (elp_load_csc)  */
 } orc_control;
 
 typedef struct orc_stats {

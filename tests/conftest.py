@@ -75,3 +75,25 @@ def gpu():
     build.build()
     import easylp_amd
     return easylp_amd
+
+
+def load_sparse_lps():
+    """tests/golden/sparse_lps.json (make_sparse.py): CSC arrays + HiGHS optimum;
+    A_dense is the same matrix densified (for the oracle)."""
+    with open(os.path.join(GOLDEN, "sparse_lps.json")) as f:
+        recs = json.load(f)
+    for r in recs:
+        r["colptr"] = np.array(r["colptr"], dtype=np.int64)
+        r["rowind"] = np.array(r["rowind"], dtype=np.int32)
+        r["val"] = np.array(r["val"], dtype=np.float64)
+        A = np.zeros((r["m"], r["n"]))
+        for j in range(r["n"]):
+            s, e = r["colptr"][j], r["colptr"][j + 1]
+            A[r["rowind"][s:e], j] = r["val"][s:e]
+        r["A"] = A
+        r["rhs"] = np.array([_dec(v) for v in r["rhs"]], dtype=np.float64)
+        r["lo"] = np.array([_dec(v) for v in r["lo"]], dtype=np.float64)
+        r["up"] = np.array([_dec(v) for v in r["up"]], dtype=np.float64)
+        r["obj"] = np.array(r["obj"], dtype=np.float64)
+        r["dir"] = np.array(r["dir"], dtype=np.int32)
+    return recs

@@ -1,0 +1,110 @@
+"""GPU parity of the CSC path (elp_load_csc, BASELINE config 5): the HIP
+kernels against the oracle in its CSC pricing order (price_mode 1, DESIGN.md
+"Reduction-order contract") -- status, pivot trace and basis identical,
+objective and x bit-identical (asserted within 1e-12) -- and against the HiGHS
+optima of tests/golden/sparse_lps.json (1e-9)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import feasible, load_known_answers, load_sparse_lps
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+
+pytestmark = pytest.mark.gpu
+
+SPARSE = load_sparse_lps()
+KNOWN = load_known_answers()
+
+
+def _same(g, o):
+    assert g.status == o.status
+    np.testing.assert_array_equal(g.trace, o.trace)
+    if g.status in (0, 1):
+        np.testing.assert_array_equal(g.basis, o.basis)
+        assert abs(g.objval - o.objval) <= 1e-12 * max(1.0, abs(o.objval))
+        np.testing.assert_allclose(g.x, o.x, rtol=1e-12, atol=1e-12 * max(1.0, np.abs(o.x).max()))
+    if g.status == 3:
+        assert g.objval == o.objval
+        np.testing.assert_array_equal(g.x, o.x)
+
+
+def _gpu_csc(gpu, rec, **ctl):
+    return gpu.solve_sparse(rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"],
+                            rec["maximize"], trace=200000, **ctl)
+
+
+@pytest.mark.parametrize("rec", SPARSE, ids=[r["name"] for r in SPARSE])
+def test_sparse_fixtures_gpu(gpu, rec):
+    from oracle import solve_dense as orc
+    g = _gpu_csc(gpu, rec)
+    o = orc(rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], rec["maximize"],
+            trace_cap=200000, price_mode=1)
+    _same(g, o)
+    exp = rec["expected"]
+    assert g.status == exp["status"]
+    assert abs(g.objval - exp["objective"]) <= 1e-9 * max(1.0, abs(exp["objective"]))
+    assert feasible(rec["A"], rec["dir"], rec["rhs"], g.x, rec["lo"], rec["up"])
+
+
+@pytest.mark.parametrize("rec", KNOWN, ids=[r["name"] for r in KNOWN])
+def test_known_answers_csc(gpu, rec):
+    from oracle import solve_dense as orc
+    g = _gpu_csc(gpu, rec)
+    o = orc(rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], rec["maximize"],
+            trace_cap=200000, price_mode=1)
+    assert g.status == rec["expected"]["status"]
+    _same(g, o)
+
+
+def test_klee_minty_12(gpu):
+    """Degenerate-path case: 2^12 - 1 Dantzig pivots to the optimum 5^12."""
+    from make_sparse import klee_minty
+    from oracle import solve_dense as orc
+    A, dirs, rhs, obj, lo, up, mx = klee_minty(12)
+    g = gpu.solve_sparse(A, dirs, rhs, obj, lo, up, mx, trace=10000)
+    o = orc(A.toarray(), dirs, rhs, obj, lo, up, mx, trace_cap=10000, price_mode=1)
+    _same(g, o)
+    assert g.objval == 5.0 ** 12 and g.stats["iterations"] == 2 ** 12 - 1
+
+
+@pytest.mark.parametrize("kind", ["packing", "general"])
+def test_larger_sparse_vs_oracle(gpu, kind):
+    from make_sparse import sparse_general, sparse_packing
+    from oracle import solve_dense as orc
+    gen = sparse_packing if kind == "packing" else sparse_general
+    A, dirs, rhs, obj, lo, up, mx = gen(31, 600, 3000, 5)
+    g = gpu.solve_sparse(A, dirs, rhs, obj, lo, up, mx, trace=100000)
+    o = orc(A.toarray(), dirs, rhs, obj, lo, up, mx, trace_cap=100000, price_mode=1)
+    assert g.status == 0
+    _same(g, o)
+
+
+def test_large_bump_launch_shape(gpu, monkeypatch):
+    """ELP_FORCE_SELECT: the launch shapes used for bumps beyond the LDS budget
+    (single-workgroup select + bump FTRAN, global z partials, global B^-1 row
+    staging), on the dense and the CSC path."""
+    from oracle import solve_dense as orc
+    monkeypatch.setenv("ELP_FORCE_SELECT", "1")
+    rec = next(r for r in SPARSE if r["name"] == "general_s13_90x300")
+    g = _gpu_csc(gpu, rec)
+    o = orc(rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], rec["maximize"],
+            trace_cap=200000, price_mode=1)
+    _same(g, o)
+    gd = gpu.solve_dense(rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"],
+                         rec["maximize"], trace=200000)
+    od = orc(rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], rec["maximize"],
+             trace_cap=200000)
+    _same(gd, od)
+
+
+def test_csc_usage_errors(gpu):
+    from easylp_amd import Problem
+    from easylp_amd._lib import ElpError
+    with Problem(2, 2) as p:
+        with pytest.raises(ElpError, match="strictly increasing"):
+            p.load_csc([0, 2, 3], [1, 0, 1], [1.0, 2.0, 3.0], [1, 1], [1.0, 1.0], [1.0, 1.0])
+        with pytest.raises(ElpError, match="out of range"):
+            p.load_csc([0, 1, 2], [0, 5], [1.0, 2.0], [1, 1], [1.0, 1.0], [1.0, 1.0])
