@@ -108,3 +108,19 @@ def test_csc_usage_errors(gpu):
             p.load_csc([0, 2, 3], [1, 0, 1], [1.0, 2.0, 3.0], [1, 1], [1.0, 1.0], [1.0, 1.0])
         with pytest.raises(ElpError, match="out of range"):
             p.load_csc([0, 1, 2], [0, 5], [1.0, 2.0], [1, 1], [1.0, 1.0], [1.0, 1.0])
+
+
+def test_mps_file_through_csc(gpu, tmp_path):
+    """An MPS file (ranges, bounds, sense, objective constant) read by
+    easylp_amd.mps and solved on the GPU: same pivots as the oracle."""
+    from easylp_amd.mps import read_mps, solve_mps
+    from oracle import solve_dense as orc
+    from test_mps import TEXT
+    f = tmp_path / "t.mps"
+    f.write_text(TEXT)
+    p, g = solve_mps(str(f), trace=0)
+    o = orc(p.dense(), p.dirs, p.rhs, p.obj, p.lo, p.up, p.maximize, price_mode=1)
+    assert g.status == o.status == 0
+    assert g.objval == o.objval
+    np.testing.assert_array_equal(g.basis, o.basis)
+    assert read_mps(str(f)).objective_constant == 3.5
