@@ -118,7 +118,7 @@ def test_mps_file_through_csc(gpu, tmp_path):
     from test_mps import TEXT
     f = tmp_path / "t.mps"
     f.write_text(TEXT)
-    p, g = solve_mps(str(f), trace=0)
+    p, g = solve_mps(str(f))
     o = orc(p.dense(), p.dirs, p.rhs, p.obj, p.lo, p.up, p.maximize, price_mode=1)
     assert g.status == o.status == 0
     assert g.objval == o.objval
