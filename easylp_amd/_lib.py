@@ -21,7 +21,7 @@ ELP_PROFILE_EVENTS = 4  # HIP-event pricing timer
 EXPORTS = (
     "elp_default_control", "elp_create", "elp_load_dense", "elp_load_dense_device",
     "elp_load_generated", "elp_load_csc", "elp_solve", "elp_iterate", "elp_get_solution",
-    "elp_get_stats",
+    "elp_get_stats", "elp_sensitivity",
     "elp_set_trace", "elp_get_trace", "elp_comm_unique_id", "elp_comm_init", "elp_comm_init_host",
     "elp_destroy", "elp_last_error", "elp_abi_version",
 )
@@ -108,6 +108,7 @@ def load(path: str | None = None):
     lib.elp_iterate.argtypes = [vp, i64, P(i32)]
     lib.elp_get_solution.argtypes = [vp, P(dbl), vp, vp, vp]
     lib.elp_get_stats.argtypes = [vp, P(ElpStats)]
+    lib.elp_sensitivity.argtypes = [vp, vp, vp, vp, vp, vp]
     lib.elp_set_trace.argtypes = [vp, i64]
     lib.elp_get_trace.argtypes = [vp, vp, i64, P(i64)]
     lib.elp_comm_unique_id.argtypes = [vp]
@@ -118,7 +119,7 @@ def load(path: str | None = None):
     lib.elp_last_error.restype = ctypes.c_char_p
     lib.elp_abi_version.restype = i32
     for name in ("elp_create", "elp_load_dense", "elp_load_dense_device", "elp_load_generated",
-                 "elp_load_csc",
+                 "elp_load_csc", "elp_sensitivity",
                  "elp_solve", "elp_iterate", "elp_get_solution", "elp_get_stats",
                  "elp_set_trace", "elp_get_trace", "elp_comm_unique_id", "elp_comm_init",
                  "elp_comm_init_host"):

@@ -64,6 +64,8 @@ struct elp_handle {
     DevCtl* hctl = nullptr;  // pinned mirror
     int k_sync = 0, ny_sync = 0, since_refactor_sync = 0;
     std::vector<double> obj_h;  // global objective (for the objective value)
+    std::vector<int32_t> dir_h;  // row directions and rhs (sensitivity report)
+    std::vector<double> rhs_h;
     elp_stats stats{};
     double t_solve_start = 0.0;
     bool timing_started = false;
@@ -328,6 +330,8 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
     h->maximize = maximize ? 1 : 0;
     d.maximize = h->maximize;
     h->obj_h.assign(obj, obj + n);
+    h->dir_h.assign(dir, dir + m);
+    h->rhs_h.assign(rhs, rhs + m);
     // host-side staging of the small vectors (local column shard)
     std::vector<double> lo_h(nl), up_h(nl), slb(m), sub(m);
     for (int64_t j = 0; j < nl; ++j) {
@@ -892,6 +896,113 @@ extern "C" int elp_get_solution(elp_handle* h, double* objval, double* x, double
         for (int p = 0; p < c.k; ++p) bv.push_back(Sl[p]);
         std::sort(bv.begin(), bv.end());
         for (size_t t = 0; t < bv.size() && (int64_t)t < m; ++t) basis[t] = bv[t];
+    }
+    return 0;
+}
+
+// get.sensitivity.obj / get.sensitivity.rhs (R/class.R:613-646) from the final
+// basis: the reduced costs and the two MFMA contractions run on the device
+// (launch_sensitivity), the per-variable assembly here mirrors
+// oracle/elp_oracle.c sensitivity() line by line.
+extern "C" int elp_sensitivity(elp_handle* h, double* objfrom, double* objtill, double* duals,
+                               double* dualsfrom, double* dualstill) {
+    if (!h || !h->loaded) return fail(ELP_E_STATE, "elp_sensitivity: no problem loaded");
+    if (!h->done || h->final_status != ELP_OPTIMAL)
+        return fail(ELP_E_STATE, "elp_sensitivity: problem is not optimal");
+    if (h->comm.kind != 0) return fail(ELP_E_UNSUPPORTED, "elp_sensitivity: column-sharded solves");
+    HIPCHK(hipSetDevice(h->dev));
+    HIPCHK(hipMemcpyAsync(h->hctl, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    const Dev& d = h->d;
+    const int64_t m = h->m, n = h->n;
+    const int k = h->hctl->k;
+    const int64_t ntc = (n + 63) / 64, ntr = (m + 63) / 64;
+    const double INF = HUGE_VAL, BIG = h->ctl.infinity;
+    double *dred = nullptr, *TR = nullptr, *plo = nullptr, *phi = nullptr, *qlo = nullptr,
+           *qhi = nullptr, *out4 = nullptr;
+    auto release = [&]() {
+        for (double* p : {dred, TR, plo, phi, qlo, qhi, out4})
+            if (p) (void)hipFree(p);
+    };
+    if (dalloc(&dred, n) != hipSuccess || dalloc(&TR, (size_t)k * n) != hipSuccess ||
+        dalloc(&plo, (size_t)k * ntc) != hipSuccess || dalloc(&phi, (size_t)k * ntc) != hipSuccess ||
+        dalloc(&qlo, (size_t)k * ntr) != hipSuccess || dalloc(&qhi, (size_t)k * ntr) != hipSuccess ||
+        dalloc(&out4, (size_t)4 * k) != hipSuccess) {
+        release();
+        return fail(ELP_E_NOMEM, "elp_sensitivity: work allocation failed");
+    }
+    hipError_t e = launch_sensitivity(d, k, dred, TR, plo, phi, qlo, qhi, out4, h->st);
+    std::vector<double> dr(n), o4(4 * (size_t)k), cost(n), lb(n), ub(n), xr(m), y(m), b(m);
+    std::vector<int8_t> vs(n + m);
+    std::vector<int32_t> Sl(k), Rl(k), cover(m), rpos(m);
+    auto d2h = [&](void* dst, const void* src, size_t bytes) {
+        if (e == hipSuccess && bytes) e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->st);
+    };
+    d2h(dr.data(), dred, n * sizeof(double));
+    d2h(o4.data(), out4, 4 * (size_t)k * sizeof(double));
+    d2h(cost.data(), d.cost, n * sizeof(double));
+    d2h(lb.data(), d.lb, n * sizeof(double));
+    d2h(ub.data(), d.ub, n * sizeof(double));
+    d2h(vs.data(), d.vstat, (n + m) * sizeof(int8_t));
+    d2h(Sl.data(), d.Sl, k * sizeof(int32_t));
+    d2h(Rl.data(), d.Rl, k * sizeof(int32_t));
+    d2h(cover.data(), d.cover, m * sizeof(int32_t));
+    d2h(rpos.data(), d.rpos, m * sizeof(int32_t));
+    d2h(xr.data(), d.xr, m * sizeof(double));
+    d2h(y.data(), d.y, m * sizeof(double));
+    d2h(b.data(), d.b, m * sizeof(double));
+    if (e == hipSuccess) e = hipStreamSynchronize(h->st);
+    release();
+    if (e != hipSuccess) return fail(ELP_E_HIP, std::string("elp_sensitivity: ") + hipGetErrorString(e));
+    auto clip = [&](double v) { return v <= -INF ? -BIG : v >= INF ? BIG : v; };
+    const bool mx = h->maximize != 0;
+    const double sg = mx ? -1.0 : 1.0;
+    if (duals) {
+        for (int64_t i = 0; i < m; ++i) duals[i] = sg * y[i];
+        for (int64_t j = 0; j < n; ++j) duals[m + j] = sg * dr[j];
+    }
+    std::vector<int> spos(n, -1);
+    for (int p = 0; p < k; ++p) spos[Sl[p]] = p;
+    for (int64_t j = 0; j < n && (objfrom || objtill); ++j) {
+        double lo = -INF, hi = INF;
+        const double c = cost[j];
+        if (vs[j] == VS_BASIC) {
+            const int p = spos[j];
+            lo = c + o4[p];
+            hi = c + o4[k + p];
+        } else if (lb[j] == ub[j]) {
+        } else if (vs[j] == VS_LOWER) {
+            lo = c - dr[j];
+        } else if (vs[j] == VS_UPPER) {
+            hi = c - dr[j];
+        } else {
+            lo = hi = c;
+        }
+        if (objfrom) objfrom[j] = clip(mx ? -hi : lo);
+        if (objtill) objtill[j] = clip(mx ? -lo : hi);
+    }
+    for (int64_t i = 0; i < m && (dualsfrom || dualstill); ++i) {
+        double lo = -INF, hi = INF;
+        const double bi = b[i];
+        const int u = cover[i];
+        if (u == (int)(n + i)) {
+            const double act = bi - xr[i];
+            if (h->dir_h[i] == ELP_LE) lo = act;
+            else if (h->dir_h[i] == ELP_GE) hi = act;
+            else lo = hi = bi;
+        } else if (u >= (int)(n + m)) {
+            lo = hi = bi;
+        } else {
+            const int c = rpos[i];
+            lo = bi + o4[2 * (size_t)k + c];
+            hi = bi + o4[3 * (size_t)k + c];
+        }
+        if (dualsfrom) dualsfrom[i] = clip(lo);
+        if (dualstill) dualstill[i] = clip(hi);
+    }
+    for (int64_t j = 0; j < n; ++j) {
+        if (dualsfrom) dualsfrom[m + j] = -BIG;
+        if (dualstill) dualstill[m + j] = BIG;
     }
     return 0;
 }

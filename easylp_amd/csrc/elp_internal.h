@@ -187,6 +187,11 @@ hipError_t launch_btran_exact(const Dev& d, int k, hipStream_t st);  // phase-2 
 hipError_t launch_refactor_primal(const Dev& d, int k, hipStream_t st);  // needs ract
 hipError_t launch_nzlist(const Dev& d, hipStream_t st);
 hipError_t launch_phase2(const Dev& d, hipStream_t st);
+// sensitivity (final basis, k = bump dimension): dred[n] reduced costs; TR
+// (k x n), plo/phi (k x ceil(n/64)), qlo/qhi (k x ceil(m/64)) work; out4 =
+// [olo(k) ohi(k) rlo(k) rhi(k)]: intervals of delta c_{S_p} and delta b_{R_c}
+hipError_t launch_sensitivity(const Dev& d, int k, double* dred, double* TR, double* plo,
+                              double* phi, double* qlo, double* qhi, double* out4, hipStream_t st);
 // x of the local shard into xout[0:n) (basic values from the replicated S list)
 hipError_t launch_extract(const Dev& d, double* xout, hipStream_t st);
 

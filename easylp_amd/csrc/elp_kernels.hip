@@ -1818,6 +1818,215 @@ __global__ void k_extract_basic(Dev d, double* __restrict__ xout) {
     if (j >= 0 && j < d.n) xout[j] = d.xs[p];
 }
 
+// ============================================================== sensitivity
+// Sensitivity report of the final basis (R/class.R:613-646; conventions in
+// oracle/elp_oracle.c sensitivity()).  The two dense contractions -- alpha =
+// Minv * A[R,:] (objective ranging of the basic structurals) and
+// G = A[:,S] * Minv (columns of B^-1 for the binding rows, rhs ranging) -- run
+// on the fp64 matrix cores (v_mfma_f64_16x16x4f64) with the ratio tests fused
+// into the epilogue, so neither k x n nor m x k product is ever stored.
+
+// reduced costs of the structurals (0 for basic): dense = wave order over all
+// m rows (one wave per column), CSC = the column chain
+__global__ void __launch_bounds__(256) k_sens_redcost(Dev d, double* __restrict__ dred) {
+    const int lane = threadIdx.x & 63;
+    if (d.csc) {
+        const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+        if (j >= d.n) return;
+        double acc = 0.0;
+        for (int64_t t = d.cptr[j]; t < d.cptr[j + 1]; ++t) acc = fma(d.cval[t], d.y[d.rind[t]], acc);
+        dred[j] = d.vstat[j] == VS_BASIC ? 0.0 : d.cost[j] - acc;
+        return;
+    }
+    const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (j >= d.n) return;
+    const double* col = d.A + (size_t)j * (size_t)d.m;
+    double acc = 0.0;
+    for (int i = lane; i < d.m; i += 64) acc = fma(col[i], d.y[i], acc);
+    acc = wave_tree(acc);
+    if (lane == 0) dred[j] = d.vstat[j] == VS_BASIC ? 0.0 : d.cost[j] - acc;
+}
+
+// TR[c][j] = A[R_c, j]  (k x n row-major; TR zeroed beforehand for CSC)
+__global__ void k_sens_gather_rows(Dev d, double* __restrict__ TR, int k) {
+    const int c = blockIdx.y;
+    if (c >= k) return;
+    const int i = d.Rl[c];
+    if (d.csc) {
+        for (int64_t t = d.rptr[i] + threadIdx.x; t < d.rptr[i + 1]; t += blockDim.x)
+            TR[(size_t)c * (size_t)d.n + d.cind[t]] = d.rval[t];
+        return;
+    }
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d.n; j += (int64_t)gridDim.x * blockDim.x)
+        TR[(size_t)c * (size_t)d.n + (size_t)j] = d.A[(size_t)j * (size_t)d.m + (size_t)i];
+}
+
+// ratio-interval update: keep l <= x + t g <= u  ->  t in [lo, hi]
+DEV void primal_interval(double g, double x, double l, double u, double tol, double& lo, double& hi) {
+    if (g > tol) {
+        hi = fmin(hi, (u - x) / g);
+        lo = fmax(lo, (l - x) / g);
+    } else if (g < -tol) {
+        hi = fmin(hi, (l - x) / g);
+        lo = fmax(lo, (u - x) / g);
+    }
+}
+// reduced-cost interval: keep s (d - t a) >= 0 for nonbasic status vs
+DEV void dual_interval(double a, double dk, int8_t vs, double tol, double& lo, double& hi) {
+    if (vs == VS_BASIC || vs == VS_FIXED) return;
+    const double r = dk / a;
+    if (vs == VS_FREE) {
+        if (fabs(a) > tol) {
+            hi = fmin(hi, r);
+            lo = fmax(lo, r);
+        }
+        return;
+    }
+    const double sa = vs == VS_LOWER ? a : -a;
+    if (sa > tol) hi = fmin(hi, r);
+    if (sa < -tol) lo = fmax(lo, r);
+}
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+// C = X (M x K) * Y (K x N) on the fp64 MFMA, X(r, kk) = X[r*xrs + kk*xcs],
+// Y(kk, c) = Y[kk*yrs + c*ycs].  Workgroup = 4 waves = a 64 x 64 tile, wave w
+// owns rows 16w..16w+15 (four 16x16 accumulators).  Epilogue:
+//   MODE 0 (objective): rows = bump positions p, columns = structurals j;
+//          interval of t = delta c_{S_p} from dual_interval(alpha, d_j) reduced
+//          over the tile's columns -> plo/phi[p * gridDim.x + blockIdx.x]
+//   MODE 1 (rhs): rows = covered rows i, columns = R positions c;
+//          g = -sigma_u G(i, c), primal_interval on the covering unit variable,
+//          reduced over the tile's rows -> plo/phi[c * gridDim.y + blockIdx.y]
+template <int MODE>
+__global__ void __launch_bounds__(256) k_sens_mfma(Dev d, const double* __restrict__ X, int64_t xrs,
+                                                   int64_t xcs, const double* __restrict__ Y,
+                                                   int64_t yrs, int64_t ycs, int M, int N, int K,
+                                                   const double* __restrict__ dred, double* plo,
+                                                   double* phi) {
+    __shared__ double slo[4][64], shi[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r0 = (MODE == 0 ? blockIdx.y : blockIdx.y) * 64 + 16 * w;
+    const int c0 = blockIdx.x * 64;
+    const int ar = r0 + (lane & 15);
+    const int kq = lane >> 4;
+    dbl4 acc[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[b] = dbl4{0.0, 0.0, 0.0, 0.0};
+    for (int k0 = 0; k0 < K; k0 += 4) {
+        const int kk = k0 + kq;
+        const double a = (ar < M && kk < K) ? X[(size_t)ar * xrs + (size_t)kk * xcs] : 0.0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int cc = c0 + 16 * b + (lane & 15);
+            const double bv = (cc < N && kk < K) ? Y[(size_t)kk * yrs + (size_t)cc * ycs] : 0.0;
+            acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc[b], 0, 0, 0);
+        }
+    }
+    const double tol = d.ctl->tol_pivot, INF = HUGE_VAL;
+    // lane holds (row r0 + (lane>>4) + 4*reg, column c0 + 16b + (lane&15))
+    if (MODE == 0) {
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+            double lo = -INF, hi = INF;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int j = c0 + 16 * b + (lane & 15);
+                if (j < N) dual_interval(acc[b][reg], dred[j], d.vstat[j], tol, lo, hi);
+            }
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) {
+                lo = fmax(lo, __shfl_xor(lo, off));
+                hi = fmin(hi, __shfl_xor(hi, off));
+            }
+            const int p = r0 + (lane >> 4) + 4 * reg;
+            if ((lane & 15) == 0 && p < M) {
+                plo[(size_t)p * gridDim.x + blockIdx.x] = lo;
+                phi[(size_t)p * gridDim.x + blockIdx.x] = hi;
+            }
+        }
+    } else {
+        double lo[4], hi[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            lo[b] = -INF;
+            hi[b] = INF;
+        }
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+            const int i = r0 + (lane >> 4) + 4 * reg;
+            if (i >= M) continue;
+            const int u = d.cover[i];
+            if (u < 0) continue;
+            const double x = d.xr[i], l = d.rlo[i], h = d.rhi[i], sg = unit_sign(d, u, i);
+#pragma unroll
+            for (int b = 0; b < 4; ++b) primal_interval(-sg * acc[b][reg], x, l, h, tol, lo[b], hi[b]);
+        }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            lo[b] = fmax(lo[b], __shfl_xor(lo[b], 16));
+            lo[b] = fmax(lo[b], __shfl_xor(lo[b], 32));
+            hi[b] = fmin(hi[b], __shfl_xor(hi[b], 16));
+            hi[b] = fmin(hi[b], __shfl_xor(hi[b], 32));
+            if (lane < 16) {
+                slo[w][16 * b + lane] = lo[b];
+                shi[w][16 * b + lane] = hi[b];
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const int c = c0 + threadIdx.x;
+            double L = slo[0][threadIdx.x], H = shi[0][threadIdx.x];
+            for (int ww = 1; ww < 4; ++ww) {
+                L = fmax(L, slo[ww][threadIdx.x]);
+                H = fmin(H, shi[ww][threadIdx.x]);
+            }
+            if (c < N) {
+                plo[(size_t)c * gridDim.y + blockIdx.y] = L;
+                phi[(size_t)c * gridDim.y + blockIdx.y] = H;
+            }
+        }
+    }
+}
+
+// per bump position: reduce the column-tile partials, add the slack columns of
+// the R rows (alpha = Minv[p][c]) -> olo/ohi (delta of c_{S_p}); and per R
+// position c: reduce the row-tile partials, add the bump part (g = Minv[p][c]
+// on x_S) -> rlo/rhi (delta of b_{R_c})
+__global__ void k_sens_final(Dev d, int k, int ntc, int ntr, const double* __restrict__ plo,
+                             const double* __restrict__ phi, const double* __restrict__ qlo,
+                             const double* __restrict__ qhi, double* olo, double* ohi, double* rlo,
+                             double* rhi) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 2 * k) return;
+    const double tol = d.ctl->tol_pivot, INF = HUGE_VAL;
+    double lo = -INF, hi = INF;
+    if (t < k) {
+        const int p = t;
+        for (int b = 0; b < ntc; ++b) {
+            lo = fmax(lo, plo[(size_t)p * ntc + b]);
+            hi = fmin(hi, phi[(size_t)p * ntc + b]);
+        }
+        for (int c = 0; c < k; ++c) {
+            const int i = d.Rl[c];
+            const int sv = d.n + i;  // the slack of an R row is nonbasic
+            dual_interval(d.Minv[(size_t)p * d.ldm + c], -d.y[i], d.vstat[sv], tol, lo, hi);
+        }
+        olo[p] = lo;
+        ohi[p] = hi;
+    } else {
+        const int c = t - k;
+        for (int b = 0; b < ntr; ++b) {
+            lo = fmax(lo, qlo[(size_t)c * ntr + b]);
+            hi = fmin(hi, qhi[(size_t)c * ntr + b]);
+        }
+        for (int p = 0; p < k; ++p)
+            primal_interval(d.Minv[(size_t)p * d.ldm + c], d.xs[p], d.slo[p], d.shi[p], tol, lo, hi);
+        rlo[c] = lo;
+        rhi[c] = hi;
+    }
+}
+
 // ============================================================== launchers
 static inline unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
 
@@ -2035,6 +2244,28 @@ hipError_t launch_phase2(const Dev& d, hipStream_t st) {
 hipError_t launch_extract(const Dev& d, double* xout, hipStream_t st) {
     k_extract<<<cdiv(d.n, 256), 256, 0, st>>>(d, xout);
     if (d.m > 0) k_extract_basic<<<cdiv(d.m, 256), 256, 0, st>>>(d, xout);
+    return hipGetLastError();
+}
+
+hipError_t launch_sensitivity(const Dev& d, int k, double* dred, double* TR, double* plo,
+                              double* phi, double* qlo, double* qhi, double* out4, hipStream_t st) {
+    const int n = d.n, m = d.m;
+    if (d.csc) k_sens_redcost<<<cdiv(n, 256), 256, 0, st>>>(d, dred);
+    else k_sens_redcost<<<cdiv(n, 4), 256, 0, st>>>(d, dred);
+    if (k > 0) {
+        if (d.csc) (void)hipMemsetAsync(TR, 0, (size_t)k * (size_t)n * sizeof(double), st);
+        dim3 gg(d.csc ? 1 : cdiv(n, 256) < 64 ? cdiv(n, 256) : 64, (unsigned)k);
+        k_sens_gather_rows<<<gg, 256, 0, st>>>(d, TR, k);
+        const int ntc = (int)cdiv(n, 64), ntr = (int)cdiv(m, 64);
+        // alpha = Minv (k x k, row-major ldm) * TR (k x n, row-major)
+        k_sens_mfma<0><<<dim3(ntc, cdiv(k, 64)), 256, 0, st>>>(d, d.Minv, d.ldm, 1, TR, n, 1, k, n, k,
+                                                                dred, plo, phi);
+        // G = AS (m x k, column-major ld m) * Minv (k x k)
+        k_sens_mfma<1><<<dim3(cdiv(k, 64), ntr), 256, 0, st>>>(d, d.AS, 1, m, d.Minv, d.ldm, 1, m, k, k,
+                                                               dred, qlo, qhi);
+        k_sens_final<<<cdiv(2 * k, 256), 256, 0, st>>>(d, k, ntc, ntr, plo, phi, qlo, qhi, out4,
+                                                       out4 + k, out4 + 2 * k, out4 + 3 * k);
+    }
     return hipGetLastError();
 }
 

@@ -65,6 +65,7 @@ class Solution:
     basis: np.ndarray             # sorted basic variable ids
     stats: dict = field(default_factory=dict)
     trace: np.ndarray | None = None
+    sens: dict | None = None      # sensitivity report (Problem.sensitivity)
 
     @property
     def status_text(self) -> str:
@@ -184,6 +185,17 @@ class Problem:
               "elp_get_trace")
         return buf[: 2 * cnt.value].reshape(-1, 2)
 
+    def sensitivity(self) -> dict:
+        """get.sensitivity.obj + get.sensitivity.rhs of the final basis
+        (R/class.R:613-646): objfrom/objtill (n), duals/dualsfrom/dualstill (m+n),
+        infinite limits as +-1e30 (apply large_to_infinity as R/class.R does)."""
+        m, n = self.m, self.n
+        out = {k: np.zeros(n) for k in ("objfrom", "objtill")}
+        out.update({k: np.zeros(m + n) for k in ("duals", "dualsfrom", "dualstill")})
+        check(self._lib.elp_sensitivity(self._h, *(out[k].ctypes.data for k in (
+            "objfrom", "objtill", "duals", "dualsfrom", "dualstill"))), "elp_sensitivity")
+        return out
+
     def solution(self, status: int) -> Solution:
         m, n = self.m, self.n
         x = np.zeros(n)
@@ -207,7 +219,8 @@ def csc_arrays(A):
             M.shape)
 
 
-def solve_sparse(A, dirs, rhs, obj, lo=None, up=None, maximize=False, trace=0, **control) -> Solution:
+def solve_sparse(A, dirs, rhs, obj, lo=None, up=None, maximize=False, trace=0, sensitivity=False,
+                 **control) -> Solution:
     """One-shot solve with A sparse (scipy.sparse or dense array) through the CSC path."""
     colptr, rowind, val, (m, n) = csc_arrays(A)
     with Problem(m, n, **control) as p:
@@ -215,11 +228,16 @@ def solve_sparse(A, dirs, rhs, obj, lo=None, up=None, maximize=False, trace=0, *
             p.set_trace(trace)
         p.load_csc(colptr, rowind, val, dirs, rhs, obj, lo, up, maximize)
         st = p.solve()
-        return p.solution(st)
+        sol = p.solution(st)
+        if sensitivity and st == 0:
+            sol.sens = p.sensitivity()
+        return sol
 
 
-def solve_dense(A, dirs, rhs, obj, lo=None, up=None, maximize=False, trace=0, **control) -> Solution:
-    """One-shot solve of a dense LP on the GPU (the R/class.R:260-278 hand-off)."""
+def solve_dense(A, dirs, rhs, obj, lo=None, up=None, maximize=False, trace=0, sensitivity=False,
+                **control) -> Solution:
+    """One-shot solve of a dense LP on the GPU (the R/class.R:260-278 hand-off).
+    sensitivity=True adds Solution.sens (Problem.sensitivity()) when optimal."""
     m = len(rhs)
     n = len(obj)
     with Problem(m, n, **control) as p:
@@ -227,4 +245,7 @@ def solve_dense(A, dirs, rhs, obj, lo=None, up=None, maximize=False, trace=0, **
             p.set_trace(trace)
         p.load_dense(A, dirs, rhs, obj, lo, up, maximize)
         st = p.solve()
-        return p.solution(st)
+        sol = p.solution(st)
+        if sensitivity and st == 0:
+            sol.sens = p.sensitivity()
+        return sol

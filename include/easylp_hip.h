@@ -156,6 +156,17 @@ int elp_get_solution(elp_handle* h, double* objval, double* x, double* y, int64_
 
 int elp_get_stats(elp_handle* h, elp_stats* st);
 
+/* get.sensitivity.obj / get.sensitivity.rhs             R/class.R:613-646
+ * Sensitivity report of the final basis of an OPTIMAL solve (ELP_E_STATE
+ * otherwise, as R's stop("Problem is not optimal"); one GPU only).  Any output
+ * may be NULL.  objfrom[n] / objtill[n]: range of each objective coefficient
+ * over which the basis stays optimal; duals[m+n]: constraint duals then reduced
+ * costs (user sense); dualsfrom / dualstill[m+n]: range of each constraint's rhs
+ * over which the duals stay valid (variable entries -1e30 / 1e30).  Infinite
+ * limits are reported as +-1e30 (R/utils.R:172-176 maps them back). */
+int elp_sensitivity(elp_handle* h, double* objfrom, double* objtill, double* duals,
+                    double* dualsfrom, double* dualstill);
+
 /* Pivot trace for parity tests: (entering, leaving) per iteration, leaving
  * = -1 for a bound flip, -2 for the unbounded ray.  Enable before elp_solve with capacity > 0. */
 int elp_set_trace(elp_handle* h, int64_t capacity);

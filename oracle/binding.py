@@ -70,6 +70,8 @@ def load():
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
         ctypes.c_int64, P(OrcStats),
     ]
+    lib.orc_solve_dense_sens.restype = ctypes.c_int
+    lib.orc_solve_dense_sens.argtypes = lib.orc_solve_dense.argtypes + [ctypes.c_void_p]
     lib.orc_generate_dense.restype = None
     lib.orc_generate_dense.argtypes = [
         ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
@@ -88,13 +90,16 @@ class OracleResult:
     basis: np.ndarray
     trace: np.ndarray
     stats: dict
+    sens: dict | None = None
 
 
 def _ptr(a):
     return None if a is None else a.ctypes.data
 
 
-def solve_dense(A, dir, rhs, obj, lo=None, up=None, maximize=False, trace_cap=0, **ctl):
+def solve_dense(A, dir, rhs, obj, lo=None, up=None, maximize=False, trace_cap=0, sens=False, **ctl):
+    """sens=True: also the sensitivity report of the final basis (objfrom, objtill,
+    duals, dualsfrom, dualstill; R/class.R:613-646) when the LP is optimal."""
     lib = load()
     obj = np.ascontiguousarray(obj, dtype=np.float64)
     n = obj.shape[0]
@@ -114,17 +119,22 @@ def solve_dense(A, dir, rhs, obj, lo=None, up=None, maximize=False, trace_cap=0,
     trace = np.full(2 * max(trace_cap, 1), -2, dtype=np.int64)
     objval = ctypes.c_double(0.0)
     st = OrcStats()
-    status = lib.orc_solve_dense(
+    sbuf = np.full(5 * n + 3 * m, np.nan) if sens else None
+    status = lib.orc_solve_dense_sens(
         m, n, A.ctypes.data if m else None, _ptr(dir) if m else None, _ptr(rhs) if m else None,
         obj.ctypes.data, lo.ctypes.data, up.ctypes.data, int(bool(maximize)), ctypes.byref(c),
         ctypes.addressof(objval), x.ctypes.data, y.ctypes.data, basis.ctypes.data,
-        trace.ctypes.data if trace_cap else None, trace_cap, ctypes.byref(st))
+        trace.ctypes.data if trace_cap else None, trace_cap, ctypes.byref(st), _ptr(sbuf))
     if status < 0:
         raise ValueError(f"orc_solve_dense usage error {status}")
     stats = {f: getattr(st, f) for f, _ in OrcStats._fields_}
     it = min(stats["iterations"], trace_cap)
+    sd = None
+    if sens and status == 0:
+        sd = {"objfrom": sbuf[:n], "objtill": sbuf[n:2 * n], "duals": sbuf[2 * n:2 * n + m + n],
+              "dualsfrom": sbuf[3 * n + m:4 * n + 2 * m], "dualstill": sbuf[4 * n + 2 * m:]}
     return OracleResult(status, objval.value, x, y[:m], basis[:m],
-                        trace[: 2 * it].reshape(-1, 2), stats)
+                        trace[: 2 * it].reshape(-1, 2), stats, sd)
 
 
 def generate_dense(seed, m, n, col0=0, ncols=None, want_A=True):

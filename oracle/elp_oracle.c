@@ -673,6 +673,150 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
     }
 }
 
+/* ------------------------------------------------------------------ */
+/* sensitivity from the final (optimal) basis: what get.sensitivity.obj and
+ * get.sensitivity.rhs return to R/class.R:613-646.  Textbook ranging on the
+ * basis the solve ended with (lp_solve's own routine is absent from this image:
+ * parity with it is unpinned; DESIGN.md documents the conventions):
+ *   reduced cost d_j = c_j - a_j'y (dense: wave order over all m rows;
+ *   price_mode 1: the column chain), slack d = -y_i;
+ *   objective ranging: nonbasic at lower [c - d, inf), at upper (-inf, c - d],
+ *   free nonbasic [c, c], fixed (-inf, inf); basic S_p: c + [dlo, dhi] with
+ *   alpha_pk = rho_p' a_k, rho_p = row p of Minv on the R rows, and
+ *   dhi = min d_k/alpha_pk over s_k alpha_pk > tol, dlo = max over < -tol
+ *   (s_k = +1 at lower, -1 at upper, both for free);
+ *   rhs ranging: basic slack: [activity, inf) for <=, (-inf, activity] for >=,
+ *   [b, b] for ==; artificial-covered row [b, b]; row R_c: b + [lo, hi] from
+ *   the primal ratio test along g = B^-1 e_i (g_S = Minv[:,c],
+ *   g_u = -sigma_u A[i',S] Minv[:,c] on covered rows);
+ *   variable entries of dualsfrom / dualstill: -inf / inf.
+ * Output (user sense, +-infinity as +-BIG): objfrom[n] objtill[n]
+ * duals[m+n] dualsfrom[m+n] dualstill[m+n]. */
+static void sensitivity(orc_t* s, const orc_control* ctl, const int32_t* dir, int maximize,
+                        double BIG, double* out) {
+    const int64_t m = s->m, n = s->n, k = s->k;
+    const double INF = HUGE_VAL, tol = ctl->tol_pivot;
+    double *objfrom = out, *objtill = out + n, *duals = out + 2 * n;
+    double *dfrom = duals + (m + n), *dtill = dfrom + (m + n);
+    double* d = dalloc((size_t)(n + m));
+    for (int64_t j = 0; j < n; ++j) {
+        const double* col = &s->A[(size_t)j * (size_t)m];
+        double dot = 0.0;
+        if (ctl->price_mode == 1) {
+            for (int64_t i = 0; i < m; ++i)
+                if (col[i] != 0.0) dot = fma(col[i], s->y[i], dot);
+        } else {
+            dot = wave_dot(m, col, s->y);
+        }
+        d[j] = s->vstat[j] == VS_BASIC ? 0.0 : s->cost[j] - dot;
+    }
+    for (int64_t i = 0; i < m; ++i) d[n + i] = s->vstat[n + i] == VS_BASIC ? 0.0 : -s->y[i];
+    const double sg = maximize ? -1.0 : 1.0;
+    for (int64_t i = 0; i < m; ++i) duals[i] = sg * s->y[i];
+    for (int64_t j = 0; j < n; ++j) duals[m + j] = sg * d[j];
+    /* ---- objective ranging (internal min-form costs) */
+    for (int64_t j = 0; j < n; ++j) {
+        double lo = -INF, hi = INF;
+        const double c = s->cost[j];
+        if (s->vstat[j] == VS_BASIC) {
+            const int64_t p = s->spos[j];
+            double dlo = -INF, dhi = INF;
+            for (int64_t kk = 0; kk < n + m; ++kk) {
+                if (s->vstat[kk] == VS_BASIC || s->lb[kk] == s->ub[kk]) continue;
+                double a = 0.0;
+                if (kk < n) {
+                    for (int64_t cc = 0; cc < k; ++cc)
+                        a = fma(*MI(s, p, cc), Aat(s, s->Rl[cc], kk), a);
+                } else {
+                    const int64_t cc = s->rpos[kk - n];
+                    if (cc < 0) continue;
+                    a = *MI(s, p, cc);
+                }
+                const int8_t vs = s->vstat[kk];
+                const double r = d[kk] / a;
+                if (vs == VS_FREE) {
+                    if (fabs(a) > tol) {
+                        if (r < dhi) dhi = r;
+                        if (r > dlo) dlo = r;
+                    }
+                    continue;
+                }
+                const double sa = vs == VS_LOWER ? a : -a;
+                if (sa > tol && r < dhi) dhi = r;
+                if (sa < -tol && r > dlo) dlo = r;
+            }
+            lo = c + dlo;
+            hi = c + dhi;
+        } else if (s->lb[j] == s->ub[j]) {
+            lo = -INF;
+            hi = INF;
+        } else if (s->vstat[j] == VS_LOWER) {
+            lo = c - d[j];
+        } else if (s->vstat[j] == VS_UPPER) {
+            hi = c - d[j];
+        } else {
+            lo = hi = c;
+        }
+        /* user sense: max negated the costs */
+        const double ulo = maximize ? -hi : lo, uhi = maximize ? -lo : hi;
+        objfrom[j] = ulo <= -INF ? -BIG : ulo >= INF ? BIG : ulo;
+        objtill[j] = uhi <= -INF ? -BIG : uhi >= INF ? BIG : uhi;
+    }
+    /* ---- rhs ranging */
+    for (int64_t i = 0; i < m; ++i) {
+        double lo = -INF, hi = INF;
+        const double b = s->b[i];
+        const int64_t u = s->cover[i];
+        if (u == n + i) {  /* basic slack: a_i x = b - s */
+            const double act = b - s->xr[i];
+            if (dir[i] == 1) lo = act;
+            else if (dir[i] == 2) hi = act;
+            else lo = hi = b;
+        } else if (u >= n + m) {
+            lo = hi = b;
+        } else {
+            const int64_t c = s->rpos[i];
+            double glo = -INF, ghi = INF;
+            for (int64_t p = 0; p < k; ++p) {  /* basic structurals */
+                const double gv = *MI(s, p, c);
+                const int64_t v = s->Sl[p];
+                const double x = s->xs[p], l = s->lb[v], h = s->ub[v];
+                if (gv > tol) {
+                    if ((h - x) / gv < ghi) ghi = (h - x) / gv;
+                    if ((l - x) / gv > glo) glo = (l - x) / gv;
+                } else if (gv < -tol) {
+                    if ((l - x) / gv < ghi) ghi = (l - x) / gv;
+                    if ((h - x) / gv > glo) glo = (h - x) / gv;
+                }
+            }
+            for (int64_t i2 = 0; i2 < m; ++i2) {  /* covering unit variables */
+                const int64_t u2 = s->cover[i2];
+                if (u2 < 0) continue;
+                double z = 0.0;
+                for (int64_t p = 0; p < k; ++p) z = fma(Aat(s, i2, s->Sl[p]), *MI(s, p, c), z);
+                const double gv = -unit_sign(s, u2) * z;
+                const double x = s->xr[i2], l = s->lb[u2], h = s->ub[u2];
+                if (gv > tol) {
+                    if ((h - x) / gv < ghi) ghi = (h - x) / gv;
+                    if ((l - x) / gv > glo) glo = (l - x) / gv;
+                } else if (gv < -tol) {
+                    if ((l - x) / gv < ghi) ghi = (l - x) / gv;
+                    if ((h - x) / gv > glo) glo = (h - x) / gv;
+                }
+            }
+            lo = b + glo;
+            hi = b + ghi;
+        }
+        dfrom[i] = lo <= -INF ? -BIG : lo >= INF ? BIG : lo;
+        dtill[i] = hi <= -INF ? -BIG : hi >= INF ? BIG : hi;
+    }
+    for (int64_t j = 0; j < n; ++j) {
+        dfrom[m + j] = -BIG;
+        dtill[m + j] = BIG;
+    }
+    free(d);
+}
+
 void orc_default_control(orc_control* c) {
     c->tol_primal = 1e-9;
     c->tol_dual = 1e-9;
@@ -695,6 +839,15 @@ int orc_solve_dense(int64_t m, int64_t n, const double* A, const int32_t* dir, c
                     const double* obj, const double* lo, const double* up, int32_t maximize,
                     const orc_control* ctl_in, double* objval, double* xout, double* yout,
                     int64_t* basis, int64_t* trace, int64_t trace_cap, orc_stats* st_out) {
+    return orc_solve_dense_sens(m, n, A, dir, rhs, obj, lo, up, maximize, ctl_in, objval, xout,
+                                yout, basis, trace, trace_cap, st_out, NULL);
+}
+
+int orc_solve_dense_sens(int64_t m, int64_t n, const double* A, const int32_t* dir,
+                         const double* rhs, const double* obj, const double* lo,
+                         const double* up, int32_t maximize, const orc_control* ctl_in,
+                         double* objval, double* xout, double* yout, int64_t* basis,
+                         int64_t* trace, int64_t trace_cap, orc_stats* st_out, double* sens) {
     if (m < 0 || n <= 0 || (m > 0 && (!A || !dir || !rhs)) || !obj) return -1;
     for (int64_t i = 0; i < m; ++i)
         if (dir[i] < 1 || dir[i] > 3) return -2;
@@ -873,6 +1026,7 @@ int orc_solve_dense(int64_t m, int64_t n, const double* A, const int32_t* dir, c
         for (int64_t p = 0; p < s->k; ++p) basis[c++] = s->Sl[p];
         qsort(basis, (size_t)c, sizeof(int64_t), cmp_i64);
     }
+    if (sens && status == 0) sensitivity(s, &ctl, dir, maximize, BIG, sens);
     clock_gettime(CLOCK_MONOTONIC, &t1);
     st.iterations = iter;
     st.gj_refactors = s->gj_count;

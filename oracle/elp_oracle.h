@@ -75,6 +75,16 @@ int orc_solve_dense(int64_t m, int64_t n, const double* A, const int32_t* dir,
                     double* objval, double* x, double* y, int64_t* basis,
                     int64_t* trace, int64_t trace_cap, orc_stats* st);
 
+/* orc_solve_dense plus, when the LP is solved to optimality and sens != NULL,
+ * the sensitivity report of the final basis (R/class.R:613-646; conventions in
+ * elp_oracle.c sensitivity()): sens = objfrom[n] objtill[n] duals[m+n]
+ * dualsfrom[m+n] dualstill[m+n] (5n + 3m doubles, user sense, +-1e30 = inf). */
+int orc_solve_dense_sens(int64_t m, int64_t n, const double* A, const int32_t* dir,
+                         const double* rhs, const double* obj, const double* lo,
+                         const double* up, int32_t maximize, const orc_control* ctl,
+                         double* objval, double* x, double* y, int64_t* basis,
+                         int64_t* trace, int64_t trace_cap, orc_stats* st, double* sens);
+
 /* Counter-based synthetic dense LP:
  * maximize c'x, A x <= b, x >= 0; A_ij, c_j ~ U[0,1), b_i = n/8 + U[0,1) n/4.
  * Columns [col0, col0+ncols) of the m x n instance are written to A
