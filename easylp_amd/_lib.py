@@ -20,7 +20,7 @@ ELP_PROFILE_EVENTS = 4  # HIP-event pricing timer
 # every entry point the header declares (checked by tests/test_abi.py)
 EXPORTS = (
     "elp_default_control", "elp_create", "elp_load_dense", "elp_load_dense_device",
-    "elp_load_generated", "elp_load_csc", "elp_solve", "elp_iterate", "elp_get_solution",
+    "elp_load_generated", "elp_load_csc", "elp_set_int", "elp_solve", "elp_iterate", "elp_get_solution",
     "elp_get_stats", "elp_sensitivity",
     "elp_set_trace", "elp_get_trace", "elp_comm_unique_id", "elp_comm_init", "elp_comm_init_host",
     "elp_destroy", "elp_last_error", "elp_abi_version",
@@ -50,7 +50,8 @@ class ElpControl(ctypes.Structure):
         ("verbose", ctypes.c_int32),
         ("refactor_mode", ctypes.c_int32),
         ("replicate", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 5),
+        ("max_nodes", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 4),
     ]
 
 
@@ -76,6 +77,8 @@ class ElpStats(ctypes.Structure):
         ("price_timed_bytes", ctypes.c_double),
         ("price_timed_launches", ctypes.c_int64),
         ("gj_refactors", ctypes.c_int64),
+        ("mip_nodes", ctypes.c_int64),
+        ("mip_lp_iterations", ctypes.c_int64),
     ]
 
 
@@ -104,6 +107,7 @@ def load(path: str | None = None):
     lib.elp_load_dense_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32]
     lib.elp_load_generated.argtypes = [vp, ctypes.c_uint64]
     lib.elp_load_csc.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32]
+    lib.elp_set_int.argtypes = [vp, vp]
     lib.elp_solve.argtypes = [vp, P(i32)]
     lib.elp_iterate.argtypes = [vp, i64, P(i32)]
     lib.elp_get_solution.argtypes = [vp, P(dbl), vp, vp, vp]
@@ -119,7 +123,7 @@ def load(path: str | None = None):
     lib.elp_last_error.restype = ctypes.c_char_p
     lib.elp_abi_version.restype = i32
     for name in ("elp_create", "elp_load_dense", "elp_load_dense_device", "elp_load_generated",
-                 "elp_load_csc", "elp_sensitivity",
+                 "elp_load_csc", "elp_sensitivity", "elp_set_int",
                  "elp_solve", "elp_iterate", "elp_get_solution", "elp_get_stats",
                  "elp_set_trace", "elp_get_trace", "elp_comm_unique_id", "elp_comm_init",
                  "elp_comm_init_host"):

@@ -64,8 +64,13 @@ struct elp_handle {
     DevCtl* hctl = nullptr;  // pinned mirror
     int k_sync = 0, ny_sync = 0, since_refactor_sync = 0;
     std::vector<double> obj_h;  // global objective (for the objective value)
-    std::vector<int32_t> dir_h;  // row directions and rhs (sensitivity report)
+    std::vector<int32_t> dir_h;  // row directions and rhs (sensitivity report, MIP nodes)
     std::vector<double> rhs_h;
+    std::vector<double> lo_h, up_h;  // column bounds as loaded (MIP root)
+    std::vector<int32_t> is_int;     // integer columns (elp_set_int); empty: LP
+    bool in_bnb = false;             // node reloads keep is_int / root bounds
+    bool mip = false;                // the last elp_solve ran branch and bound
+    int64_t mip_nodes = 0, mip_iters = 0;
     elp_stats stats{};
     double t_solve_start = 0.0;
     bool timing_started = false;
@@ -332,6 +337,16 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
     h->obj_h.assign(obj, obj + n);
     h->dir_h.assign(dir, dir + m);
     h->rhs_h.assign(rhs, rhs + m);
+    if (!h->in_bnb) {  // a fresh problem: root bounds, no integer columns yet
+        h->lo_h.assign(n, 0.0);
+        h->up_h.assign(n, HUGE_VAL);
+        for (int64_t j = 0; j < n; ++j) {
+            if (lo) h->lo_h[j] = lo[j];
+            if (up) h->up_h[j] = up[j];
+        }
+        h->is_int.clear();
+        h->mip = false;
+    }
     // host-side staging of the small vectors (local column shard)
     std::vector<double> lo_h(nl), up_h(nl), slb(m), sub(m);
     for (int64_t j = 0; j < nl; ++j) {
@@ -370,6 +385,7 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
     c.qcol_var = -1;
     *h->hctl = c;
     HIPCHK(hipMemcpyAsync(d.ctl, h->hctl, sizeof(DevCtl), hipMemcpyHostToDevice, h->st));
+    if (d.qcol) HIPCHK(hipMemsetAsync(d.qcol, 0, (size_t)std::max<int64_t>(m, 1) * sizeof(double), h->st));
     HIPCHK(launch_init_cols(d, dlo, dup, h->st));
     {
         const int rc = row_chain(h);
@@ -817,12 +833,129 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
     return 0;
 }
 
+extern "C" int elp_set_int(elp_handle* h, const int32_t* is_int) {
+    if (!h || !h->loaded) return fail(ELP_E_STATE, "elp_set_int: no problem loaded");
+    h->is_int.clear();
+    if (is_int) {
+        bool any = false;
+        for (int64_t j = 0; j < h->n; ++j) any |= is_int[j] != 0;
+        if (any) h->is_int.assign(is_int, is_int + h->n);
+    }
+    return 0;
+}
+
+// reload the LP with column bounds lo / up (a branch-and-bound node): A, rows
+// and objective stay; the device state restarts from the slack basis
+static int reload_bounds(elp_handle* h, const std::vector<double>& lo, const std::vector<double>& up) {
+    const std::vector<int32_t> dir = h->dir_h;
+    const std::vector<double> rhs = h->rhs_h, obj = h->obj_h;
+    h->in_bnb = true;
+    const int rc = load_common(h, dir.data(), rhs.data(), obj.data(), lo.data(), up.data(), h->maximize);
+    h->in_bnb = false;
+    return rc;
+}
+
+// Depth-first branch and bound over LP relaxations; the rules are
+// oracle/elp_oracle.c orc_solve_mip's, so both explore the same tree.
+static int run_bnb(elp_handle* h, int32_t* out_status) {
+    const int64_t n = h->n;
+    const double INF = HUGE_VAL, BIG = h->ctl.infinity;
+    std::vector<double> l0 = h->lo_h, u0 = h->up_h;
+    for (int64_t j = 0; j < n; ++j) {
+        if (l0[j] <= -BIG) l0[j] = -INF;
+        if (u0[j] >= BIG) u0[j] = INF;
+        if (h->is_int[j]) {
+            if (l0[j] > -INF) l0[j] = std::ceil(l0[j] - 1e-9);
+            if (u0[j] < INF) u0[j] = std::floor(u0[j] + 1e-9);
+        }
+    }
+    struct Node { std::vector<double> lo, up; };
+    std::vector<Node> stack;
+    stack.push_back({l0, u0});
+    double best = INF;
+    Node best_node;
+    bool have = false, limit = false, unbounded = false;
+    int64_t nodes = 0, iters = 0;
+    std::vector<double> x((size_t)n);
+    while (!stack.empty()) {
+        Node nd = std::move(stack.back());
+        stack.pop_back();
+        if (h->ctl.max_nodes > 0 && nodes >= h->ctl.max_nodes) {
+            limit = true;
+            continue;
+        }
+        nodes++;
+        int rc = nodes == 1 && h->lo_h == nd.lo && h->up_h == nd.up ? 0 : reload_bounds(h, nd.lo, nd.up);
+        if (rc) return rc;
+        int32_t s = 0;
+        rc = run_loop(h, INT64_MAX, &s);
+        if (rc) return rc;
+        {
+            elp_stats st{};
+            rc = elp_get_stats(h, &st);
+            if (rc) return rc;
+            iters += st.iterations;
+        }
+        if (s == ELP_UNBOUNDED) {
+            unbounded = true;
+            break;
+        }
+        if (s != ELP_OPTIMAL) continue;
+        double z = 0.0;
+        rc = elp_get_solution(h, &z, x.data(), nullptr, nullptr);
+        if (rc) return rc;
+        const double zmin = h->maximize ? -z : z;
+        const double tol = std::fabs(best) < INF ? std::max(1e-11, 1e-9 * std::fabs(best)) : 0.0;
+        if (std::fabs(best) < INF && zmin >= best - tol) continue;
+        int64_t jb = -1;
+        for (int64_t j = 0; j < n; ++j)
+            if (h->is_int[j] && std::fabs(x[j] - std::nearbyint(x[j])) > 1e-7) {
+                jb = j;
+                break;
+            }
+        if (jb < 0) {
+            best = zmin;
+            best_node = nd;
+            have = true;
+            continue;
+        }
+        Node fl = nd;  // floor child pushed first: the ceiling child is explored first
+        fl.up[jb] = std::floor(x[jb]);
+        nd.lo[jb] = std::ceil(x[jb]);
+        stack.push_back(std::move(fl));
+        stack.push_back(std::move(nd));
+    }
+    int32_t status;
+    if (unbounded) status = ELP_UNBOUNDED;
+    else if (have) status = limit ? ELP_SUBOPTIMAL : ELP_OPTIMAL;
+    else status = limit ? ELP_SUBOPTIMAL : ELP_INFEASIBLE;
+    if (have && !unbounded) {  // leave the incumbent's LP on the handle for elp_get_solution
+        int rc = reload_bounds(h, best_node.lo, best_node.up);
+        if (rc) return rc;
+        int32_t s = 0;
+        rc = run_loop(h, INT64_MAX, &s);
+        if (rc) return rc;
+    }
+    h->final_status = status;
+    h->done = true;
+    h->mip = true;
+    h->mip_nodes = nodes;
+    h->mip_iters = iters;
+    *out_status = status;
+    return 0;
+}
+
 extern "C" int elp_solve(elp_handle* h, int32_t* lp_status) {
     if (!h || !lp_status) return fail(ELP_E_ARG, "elp_solve: NULL argument");
     if (!h->loaded) return fail(ELP_E_STATE, "elp_solve: no problem loaded");
     HIPCHK(hipSetDevice(h->dev));
     const double t0 = now_s();
-    const int rc = run_loop(h, INT64_MAX, lp_status);
+    int rc;
+    if (!h->is_int.empty() && !h->mip && !h->done) {
+        rc = run_bnb(h, lp_status);
+    } else {
+        rc = run_loop(h, INT64_MAX, lp_status);
+    }
     h->stats.seconds_total += now_s() - t0;
     return rc;
 }
@@ -910,6 +1043,8 @@ extern "C" int elp_sensitivity(elp_handle* h, double* objfrom, double* objtill, 
     if (!h->done || h->final_status != ELP_OPTIMAL)
         return fail(ELP_E_STATE, "elp_sensitivity: problem is not optimal");
     if (h->comm.kind != 0) return fail(ELP_E_UNSUPPORTED, "elp_sensitivity: column-sharded solves");
+    if (h->mip || !h->is_int.empty())  // R/class.R:617-618, :634-635
+        return fail(ELP_E_STATE, "Sensitivity unavailable for problems with integer/binary variables");
     HIPCHK(hipSetDevice(h->dev));
     HIPCHK(hipMemcpyAsync(h->hctl, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
     HIPCHK(hipStreamSynchronize(h->st));
@@ -1020,6 +1155,8 @@ extern "C" int elp_get_stats(elp_handle* h, elp_stats* st) {
         h->stats.degenerate = c.degenerate;
         h->stats.bump_dim = c.k;
         h->stats.y_rows = c.ny;
+        h->stats.mip_nodes = h->mip ? h->mip_nodes : 0;
+        h->stats.mip_lp_iterations = h->mip ? h->mip_iters : 0;
         h->stats.price_bytes = c.price_bytes;
         if (h->d.ptimer) {
             h->stats.price_seconds = 1e-8 * (double)c.price_ticks;

@@ -315,15 +315,16 @@ def write_mps(p: MpsProblem, path: str | None = None) -> str:
 
 
 def solve_mps(path: str, **control):
-    """Read an MPS file and solve it through the CSC path on the GPU.  Returns
+    """Read an MPS file and solve it through the CSC path on the GPU (a MIP when
+    it has integer columns).  Returns
     (problem, Solution); Solution.objval excludes the objective constant, as
     lp_solve's get.objective does for EasyLP's addend (R/class.R:593-597)."""
     from .solver import Problem
     p = read_mps(path)
-    if p.is_int.any():
-        raise NotImplementedError("integer columns: use easylp_amd.mip.solve_mip")
     m, n = p.shape
     with Problem(m, n, **control) as pr:
         pr.load_csc(p.colptr, p.rowind, p.val, p.dirs, p.rhs, p.obj, p.lo, p.up, p.maximize)
+        if p.is_int.any():  # integer markers / BV / LI / UI: branch and bound
+            pr.set_int(p.is_int)
         st = pr.solve()
         return p, pr.solution(st)

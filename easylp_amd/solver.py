@@ -159,6 +159,16 @@ class Problem:
             rhs.ctypes.data if m else None, obj.ctypes.data, lo.ctypes.data, up.ctypes.data,
             int(bool(maximize))), "elp_load_csc")
 
+    def set_int(self, is_int) -> None:
+        """set.type(..., "integer" | "binary") (R/class.R:265): integer columns;
+        elp_solve then runs branch and bound over GPU LP relaxations."""
+        if is_int is None:
+            check(self._lib.elp_set_int(self._h, None), "elp_set_int")
+            return
+        ii = np.ascontiguousarray(is_int, dtype=np.int32).reshape(self.n)
+        self._keep_int = ii
+        check(self._lib.elp_set_int(self._h, ii.ctypes.data), "elp_set_int")
+
     def load_generated(self, seed: int) -> None:
         check(self._lib.elp_load_generated(self._h, int(seed)), "elp_load_generated")
 
@@ -220,13 +230,15 @@ def csc_arrays(A):
 
 
 def solve_sparse(A, dirs, rhs, obj, lo=None, up=None, maximize=False, trace=0, sensitivity=False,
-                 **control) -> Solution:
+                 is_int=None, **control) -> Solution:
     """One-shot solve with A sparse (scipy.sparse or dense array) through the CSC path."""
     colptr, rowind, val, (m, n) = csc_arrays(A)
     with Problem(m, n, **control) as p:
         if trace:
             p.set_trace(trace)
         p.load_csc(colptr, rowind, val, dirs, rhs, obj, lo, up, maximize)
+        if is_int is not None:
+            p.set_int(is_int)
         st = p.solve()
         sol = p.solution(st)
         if sensitivity and st == 0:
@@ -235,15 +247,18 @@ def solve_sparse(A, dirs, rhs, obj, lo=None, up=None, maximize=False, trace=0, s
 
 
 def solve_dense(A, dirs, rhs, obj, lo=None, up=None, maximize=False, trace=0, sensitivity=False,
-                **control) -> Solution:
+                is_int=None, **control) -> Solution:
     """One-shot solve of a dense LP on the GPU (the R/class.R:260-278 hand-off).
-    sensitivity=True adds Solution.sens (Problem.sensitivity()) when optimal."""
+    sensitivity=True adds Solution.sens (Problem.sensitivity()) when optimal;
+    is_int (n flags) makes it a MIP solved by branch and bound."""
     m = len(rhs)
     n = len(obj)
     with Problem(m, n, **control) as p:
         if trace:
             p.set_trace(trace)
         p.load_dense(A, dirs, rhs, obj, lo, up, maximize)
+        if is_int is not None:
+            p.set_int(is_int)
         st = p.solve()
         sol = p.solution(st)
         if sensitivity and st == 0:

@@ -71,7 +71,8 @@ typedef struct elp_control {
                                 min-loc record is exchanged; 1 always; 2 never
                                 (each rank holds its shard, the entering column
                                 travels in an all-reduce) */
-    int32_t reserved[5];
+    int32_t max_nodes;       /* branch and bound: node limit, <= 0 unlimited   */
+    int32_t reserved[4];
 } elp_control;
 
 typedef struct elp_stats {
@@ -99,6 +100,8 @@ typedef struct elp_stats {
     double price_timed_bytes;  /* algorithmic bytes of those launches          */
     int64_t price_timed_launches;
     int64_t gj_refactors;      /* refactors that needed a Gauss-Jordan rebuild */
+    int64_t mip_nodes;         /* branch-and-bound nodes (LP relaxations) solved */
+    int64_t mip_lp_iterations; /* simplex iterations over all of them           */
 } elp_stats;
 
 #define ELP_PROFILE_PRICE 2   /* elp_control.verbose bit: device-clock pricing timer */
@@ -140,6 +143,14 @@ int elp_load_csc(elp_handle* h, const int64_t* colptr, const int32_t* rowind, co
  * counter-based (seed, stream, global index) so every rank / the oracle
  * regenerate the same numbers. */
 int elp_load_generated(elp_handle* h, uint64_t seed);
+
+/* set.type(prob, columns, "integer" | "binary")        R/class.R:265
+ * is_int[n] != 0 marks integer columns (binary = integer with bounds [0, 1]);
+ * NULL clears.  Call after elp_load_*, before elp_solve, which then runs a
+ * depth-first branch and bound over GPU LP relaxations (lowest-index
+ * fractional column, ceiling branch first, as lp_solve's defaults) and reports
+ * the incumbent through elp_get_solution. */
+int elp_set_int(elp_handle* h, const int32_t* is_int);
 
 /* solve(prob)                                          R/class.R:276 */
 int elp_solve(elp_handle* h, int32_t* lp_status);

@@ -72,6 +72,13 @@ def load():
     ]
     lib.orc_solve_dense_sens.restype = ctypes.c_int
     lib.orc_solve_dense_sens.argtypes = lib.orc_solve_dense.argtypes + [ctypes.c_void_p]
+    lib.orc_solve_mip.restype = ctypes.c_int
+    lib.orc_solve_mip.argtypes = [
+        ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+        P(OrcControl), ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, P(ctypes.c_int64),
+        P(ctypes.c_int64),
+    ]
     lib.orc_generate_dense.restype = None
     lib.orc_generate_dense.argtypes = [
         ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
@@ -145,3 +152,31 @@ def generate_dense(seed, m, n, col0=0, ncols=None, want_A=True):
     c = np.zeros(ncols)
     lib.orc_generate_dense(seed, m, n, col0, ncols, _ptr(A), b.ctypes.data, c.ctypes.data)
     return A, b, c
+
+
+def solve_mip(A, dir, rhs, obj, lo, up, maximize, is_int, max_nodes=0, **ctl):
+    """Branch and bound over the oracle's LP (rules: oracle/elp_oracle.c orc_solve_mip)."""
+    lib = load()
+    obj = np.ascontiguousarray(obj, dtype=np.float64)
+    n = obj.shape[0]
+    rhs = np.ascontiguousarray(rhs, dtype=np.float64).reshape(-1)
+    m = rhs.shape[0]
+    A = np.asfortranarray(np.asarray(A, dtype=np.float64).reshape(m, n))
+    dir = np.ascontiguousarray(dir, dtype=np.int32).reshape(-1)
+    lo = np.zeros(n) if lo is None else np.ascontiguousarray(lo, dtype=np.float64)
+    up = np.full(n, np.inf) if up is None else np.ascontiguousarray(up, dtype=np.float64)
+    ii = np.ascontiguousarray(is_int, dtype=np.int32)
+    c = OrcControl()
+    lib.orc_default_control(ctypes.byref(c))
+    for key, val in ctl.items():
+        setattr(c, key, val)
+    x = np.zeros(n)
+    objval = ctypes.c_double(0.0)
+    nodes, iters = ctypes.c_int64(0), ctypes.c_int64(0)
+    status = lib.orc_solve_mip(m, n, A.ctypes.data if m else None, _ptr(dir) if m else None,
+                               _ptr(rhs) if m else None, obj.ctypes.data, lo.ctypes.data,
+                               up.ctypes.data, int(bool(maximize)), ii.ctypes.data, ctypes.byref(c),
+                               int(max_nodes), ctypes.addressof(objval), x.ctypes.data,
+                               ctypes.byref(nodes), ctypes.byref(iters))
+    return OracleResult(status, objval.value, x, np.zeros(m), np.zeros(0, np.int64),
+                        np.zeros((0, 2), np.int64), {"nodes": nodes.value, "lp_iterations": iters.value})

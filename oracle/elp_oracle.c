@@ -1045,3 +1045,128 @@ int orc_solve_dense_sens(int64_t m, int64_t n, const double* A, const int32_t* d
     free(s->used); free(s->perm);
     return status;
 }
+
+/* ------------------------------------------------------------------ */
+/* MIP: depth-first branch and bound over LP relaxations (the integer /   */
+/* binary columns of R/class.R:123-128, set.type at :265).  Rules (shared  */
+/* with the HIP host driver, easylp_amd/csrc/elp_api.hip run_bnb):         */
+/*   integer bounds tightened to ceil(lo - 1e-9) / floor(up + 1e-9);       */
+/*   node LP solved cold; LP unbounded -> MIP status 3; infeasible or      */
+/*   numerical failure -> prune; bound test zmin >= best - max(1e-11,      */
+/*   1e-9 |best|) -> prune (zmin: objective in minimisation form);         */
+/*   branch on the lowest-index integer column with |x - round(x)| > 1e-7  */
+/*   (lp_solve's epsint); ceiling branch explored first (lp_solve's        */
+/*   default floor_first = CEILING); LIFO stack.                            */
+typedef struct { double* lo; double* up; } bnb_node;
+
+int orc_solve_mip(int64_t m, int64_t n, const double* A, const int32_t* dir, const double* rhs,
+                  const double* obj, const double* lo, const double* up, int32_t maximize,
+                  const int32_t* is_int, const orc_control* ctl, int64_t max_nodes,
+                  double* objval, double* xout, int64_t* nodes_out, int64_t* lp_iters_out) {
+    const double INF = HUGE_VAL;
+    const double BIG = ctl ? ctl->infinity : 1e30;
+    int64_t cap = 64, top = 0, nodes = 0, iters = 0;
+    bnb_node* stack = (bnb_node*)malloc((size_t)cap * sizeof(bnb_node));
+    double* l0 = dalloc((size_t)n);
+    double* u0 = dalloc((size_t)n);
+    for (int64_t j = 0; j < n; ++j) {
+        double l = lo ? lo[j] : 0.0, u = up ? up[j] : INF;
+        if (l <= -BIG) l = -INF;
+        if (u >= BIG) u = INF;
+        if (is_int[j]) {
+            if (l > -INF) l = ceil(l - 1e-9);
+            if (u < INF) u = floor(u + 1e-9);
+        }
+        l0[j] = l;
+        u0[j] = u;
+    }
+    stack[top].lo = l0;
+    stack[top].up = u0;
+    top++;
+    double best = INF;
+    double* xbest = dalloc((size_t)n);
+    double* x = dalloc((size_t)n);
+    int have = 0, status = -1;
+    orc_stats st;
+    while (top > 0) {
+        bnb_node nd = stack[--top];
+        if (max_nodes > 0 && nodes >= max_nodes) {
+            free(nd.lo);
+            free(nd.up);
+            status = 1;
+            continue;
+        }
+        nodes++;
+        double z = 0.0;
+        const int s = orc_solve_dense(m, n, A, dir, rhs, obj, nd.lo, nd.up, maximize, ctl, &z, x,
+                                      NULL, NULL, NULL, 0, &st);
+        iters += st.iterations;
+        int branched = 0;
+        if (s == 3) {
+            status = 3;
+            free(nd.lo);
+            free(nd.up);
+            while (top > 0) {
+                --top;
+                free(stack[top].lo);
+                free(stack[top].up);
+            }
+            break;
+        }
+        if (s == 0) {
+            const double zmin = maximize ? -z : z;
+            const double tol = fabs(best) < INF ? fmax(1e-11, 1e-9 * fabs(best)) : 0.0;
+            if (!(fabs(best) < INF && zmin >= best - tol)) {
+                int64_t jb = -1;
+                for (int64_t j = 0; j < n; ++j)
+                    if (is_int[j] && fabs(x[j] - nearbyint(x[j])) > 1e-7) {
+                        jb = j;
+                        break;
+                    }
+                if (jb < 0) {
+                    best = zmin;
+                    memcpy(xbest, x, (size_t)n * sizeof(double));
+                    have = 1;
+                } else {
+                    if (top + 2 > cap) {
+                        cap *= 2;
+                        stack = (bnb_node*)realloc(stack, (size_t)cap * sizeof(bnb_node));
+                    }
+                    /* floor child pushed first so the ceiling child is explored first */
+                    double* fl = dalloc((size_t)n);
+                    double* fu = dalloc((size_t)n);
+                    memcpy(fl, nd.lo, (size_t)n * sizeof(double));
+                    memcpy(fu, nd.up, (size_t)n * sizeof(double));
+                    fu[jb] = floor(x[jb]);
+                    stack[top].lo = fl;
+                    stack[top].up = fu;
+                    top++;
+                    nd.lo[jb] = ceil(x[jb]);
+                    stack[top].lo = nd.lo;
+                    stack[top].up = nd.up;
+                    top++;
+                    branched = 1;
+                }
+            }
+        }
+        if (!branched) {
+            free(nd.lo);
+            free(nd.up);
+        }
+    }
+    if (status != 3) status = have ? (status == 1 ? 1 : 0) : (status == 1 ? 1 : 2);
+    if (have && status != 3) {
+        if (xout) memcpy(xout, xbest, (size_t)n * sizeof(double));
+        if (objval) {
+            double acc = 0.0;
+            for (int64_t j = 0; j < n; ++j) acc = fma(obj[j], xbest[j], acc);
+            *objval = acc;
+        }
+    }
+    if (nodes_out) *nodes_out = nodes;
+    if (lp_iters_out) *lp_iters_out = iters;
+    free(xbest);
+    free(x);
+    free(stack);
+    return status;
+}

@@ -85,6 +85,15 @@ int orc_solve_dense_sens(int64_t m, int64_t n, const double* A, const int32_t* d
                          double* objval, double* x, double* y, int64_t* basis,
                          int64_t* trace, int64_t trace_cap, orc_stats* st, double* sens);
 
+/* Mixed-integer LP (is_int[n] != 0: integer column; binary = integer in
+ * [0, 1]) by depth-first branch and bound over orc_solve_dense relaxations
+ * (rules in elp_oracle.c).  max_nodes <= 0: unlimited.  Returns 0 optimal,
+ * 1 node limit (x = best found, if any), 2 infeasible, 3 unbounded. */
+int orc_solve_mip(int64_t m, int64_t n, const double* A, const int32_t* dir, const double* rhs,
+                  const double* obj, const double* lo, const double* up, int32_t maximize,
+                  const int32_t* is_int, const orc_control* ctl, int64_t max_nodes,
+                  double* objval, double* x, int64_t* nodes, int64_t* lp_iters);
+
 /* Counter-based synthetic dense LP:
  * maximize c'x, A x <= b, x >= 0; A_ij, c_j ~ U[0,1), b_i = n/8 + U[0,1) n/4.
  * Columns [col0, col0+ncols) of the m x n instance are written to A

@@ -97,3 +97,19 @@ def load_sparse_lps():
         r["obj"] = np.array(r["obj"], dtype=np.float64)
         r["dir"] = np.array(r["dir"], dtype=np.int32)
     return recs
+
+
+def load_mip_known_answers():
+    """tests/golden/mip_known_answers.json (make_mip.py): the reference's MIP tests."""
+    with open(os.path.join(GOLDEN, "mip_known_answers.json")) as f:
+        recs = json.load(f)
+    for r in recs:
+        A = np.zeros((r["m"], r["n"]))
+        ii, jj, vv = r["A_triplets"]
+        A[np.array(ii, dtype=int), np.array(jj, dtype=int)] = vv
+        r["A"] = A
+        for k in ("rhs", "obj", "lo", "up"):
+            r[k] = np.array(r[k], dtype=np.float64)
+        r["dir"] = np.array(r["dir"], dtype=np.int32)
+        r["is_int"] = np.array(r["is_int"], dtype=np.int32)
+    return recs

@@ -39,10 +39,10 @@ def test_abi_version_and_defaults():
 
 
 def test_control_struct_size_matches_header():
-    # 5 doubles + int64 + 7 int32 fields + 5 reserved int32 = 96 bytes
+    # 5 doubles + int64 + 8 int32 fields + 4 reserved int32 = 96 bytes
     from easylp_amd._lib import ElpControl, ElpStats
     assert ctypes.sizeof(ElpControl) == 96
-    assert ctypes.sizeof(ElpStats) == 8 * 8 + 4 * 8 + 4 + 4 + 16 + 8 + 8 + 8 + 8
+    assert ctypes.sizeof(ElpStats) == 8 * 8 + 4 * 8 + 4 + 4 + 16 + 8 + 8 + 8 + 8 + 16
 
 
 def test_usage_errors_without_gpu():
