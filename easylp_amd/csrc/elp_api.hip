@@ -81,6 +81,9 @@ struct elp_handle {
     int64_t ar_rows = 0;         // AR capacity in rows (grown at polls)
     bool replicated = false;     // sharded, every rank holds all of A (Dev::Afull)
     bool csc = false;            // A given in CSC (elp_load_csc)
+    // ELP_STAMPS debug: k_ratio phase stamps, summed over polled chunks
+    std::vector<double> stamp_sum;
+    int64_t stamp_n = 0;
 };
 
 extern "C" void elp_default_control(elp_control* c) {
@@ -111,7 +114,7 @@ static void free_dev(elp_handle* h) {
                     d.cand,     d.pstamp, d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand,
                     d.pkt, d.objg, d.ract, d.cand_xchg, h->d_flag, d.cS, d.slo, d.shi, d.rlo, d.rhi,
                     (void*)d.cptr, (void*)d.rind, (void*)d.cval, (void*)d.rptr, (void*)d.cind,
-                    (void*)d.rval, d.qcol};
+                    (void*)d.rval, d.qcol, d.dstamp};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     h->A_owned = nullptr;
@@ -205,7 +208,7 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.xs, mm));
     A(dalloc(&d.y, mm));
     A(dalloc(&d.yy, mm));
-    A(dalloc(&d.blockmin, (size_t)(mm / 64 + mm / 256 + 4)));
+    A(dalloc(&d.blockmin, (size_t)(mm / 32 + mm / 256 + 4)));  // k_ftran_zr row + bump tiles
     A(dalloc(&d.rcand, (size_t)(2 * mm + 2)));
     A(dalloc(&d.pkt, (size_t)(mm + 4)));
     A(dalloc(&d.objg, (size_t)h->n));
@@ -236,6 +239,7 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.cand, (size_t)((n + TILE_COLS - 1) / TILE_COLS) + 64));
     A(dalloc(&d.pstamp, 2 * ((size_t)((n + TILE_COLS - 1) / TILE_COLS) + 64)));
     if (h->csc) A(dalloc(&d.qcol, mm));
+    if (std::getenv("ELP_STAMPS")) A(dalloc(&d.dstamp, 16 * 64));
     A(dalloc(&d.ctl, 1));
     A(dalloc(&d.trace, (size_t)(h->trace_cap > 0 ? 2 * h->trace_cap : 2)));
     if (e != hipSuccess) {
@@ -248,6 +252,10 @@ static int alloc_all(elp_handle* h) {
     A(hipMemsetAsync(d.Minv, 0, (size_t)mm * (size_t)mm * sizeof(double), h->st));
     A(hipMemsetAsync(d.MinvT, 0, (size_t)mm * (size_t)mm * sizeof(double), h->st));
     if (d.qcol) A(hipMemsetAsync(d.qcol, 0, (size_t)mm * sizeof(double), h->st));
+    // index lists: entries past k / |Y| are read speculatively (and discarded):
+    // start them at -1 rather than whatever the allocator hands out
+    for (int32_t* lst : {d.Rl, d.Sl, d.Yl, d.rpos, d.ypos})
+        A(hipMemsetAsync(lst, 0xff, (size_t)mm * sizeof(int32_t), h->st));
 
     if (e != hipSuccess) {
         free_dev(h);
@@ -695,13 +703,19 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
         if (left > 0 && left < chunk) chunk = (int)left;
         if (chunk < 1) chunk = 1;
         const double bytes0 = c->price_bytes;
+        if (h->d.dstamp) {  // debug: min-start slot at +inf, maxima at 0
+            std::vector<unsigned long long> init(16 * 64, 0ull);
+            for (int t = 0; t < 64; ++t) init[t * 16 + 11] = ~0ull;
+            HIPCHK(hipMemcpyAsync(h->d.dstamp, init.data(), init.size() * 8, hipMemcpyHostToDevice, h->st));
+            HIPCHK(hipStreamSynchronize(h->st));
+        }
         const double t_enq0 = now_s();
         for (int t = 0; t < chunk; ++t) {
             const int kub = (int)std::min<int64_t>(h->m, (int64_t)k0 + t);
             const int nyub = (int)std::min<int64_t>(h->m, (int64_t)ny0 + t);
             hipEvent_t e0 = prof ? h->ev[2 * t] : nullptr, e1 = prof ? h->ev[2 * t + 1] : nullptr;
             if (h->comm.kind == 0) {
-                HIPCHK(launch_iteration(h->d, kub, nyub, h->phase, h->st, e0, e1));
+                HIPCHK(launch_iteration(h->d, kub, nyub, h->phase, h->st, e0, e1, t));
             } else {
                 // sharded: local min-loc -> all-gather -> global min-loc.  Replicated
                 // A: a_R + bump FTRAN straight from the local copy -> tail.  Else the
@@ -731,7 +745,26 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
         const double t_enq1 = now_s();
         HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
         HIPCHK(hipStreamSynchronize(h->st));
+        if (c->plan_seq != c->applied_seq) {
+            // phase 2 defers each iteration's update into the next pricing launch:
+            // apply the last one now (phase 1 applied its plans in place)
+            if (h->phase == 2) HIPCHK(launch_apply_pending(h->d, std::max(k0, c->k), h->st));
+            c->applied_seq = c->plan_seq;
+            rc = push_ctl_fields(h);
+            if (rc) return rc;
+        }
         h->dbg_enqueue += t_enq1 - t_enq0;
+        if (h->d.dstamp && c->status == ST_RUN && h->phase == 2) {
+            std::vector<unsigned long long> v(16 * 64);
+            HIPCHK(hipMemcpy(v.data(), h->d.dstamp, v.size() * 8, hipMemcpyDeviceToHost));
+            if (h->stamp_sum.empty()) h->stamp_sum.assign(16, 0.0);
+            for (int t = 0; t < chunk; ++t) {
+                const unsigned long long* r = &v[(size_t)t * 16];
+                for (int i = 0; i < 11; ++i)
+                    if (r[i]) h->stamp_sum[i] += 10.0 * (double)(long long)(r[i] - r[11]);  // ns (100 MHz)
+                h->stamp_n++;
+            }
+        }
         h->dbg_wait += now_s() - t_enq1;
         h->stats.host_polls++;
         const int32_t s = c->status;
@@ -1191,6 +1224,14 @@ extern "C" int elp_get_trace(elp_handle* h, int64_t* pairs, int64_t capacity, in
 }
 
 extern "C" void elp_destroy(elp_handle* h) {
+    if (h && h->stamp_n) {
+        std::fprintf(stderr, "k_ratio stamps (us after the first workgroup start, %lld iterations):",
+                     (long long)h->stamp_n);
+        const char* nm[11] = {"wg0", "ctl", "pass1", "decide", "binv", "dual", "book", "end", "last_start",
+                              "main_end", "ar_end"};
+        for (int i = 0; i < 11; ++i) std::fprintf(stderr, " %s=%.2f", nm[i], h->stamp_sum[i] / h->stamp_n / 1e3);
+        std::fprintf(stderr, "\n");
+    }
     if (!h) return;
     (void)hipSetDevice(h->dev);
     if (h->st) (void)hipStreamSynchronize(h->st);

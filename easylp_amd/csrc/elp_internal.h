@@ -71,6 +71,11 @@ struct DevCtl {
     int64_t price_timed;
     double price_tbytes;
     int32_t qcol_var, pad6;  // CSC: the variable whose column is scattered in Dev::qcol
+    // phase-2 deferred update: k_ratio bumps plan_seq with every plan it makes;
+    // the next pricing launch applies it (Minv / MinvT / x_B / AS) and the next
+    // select kernel marks it applied; the host applies a plan still pending at
+    // a poll (k_update) -- see DESIGN.md "Iteration pipeline"
+    int32_t plan_seq, applied_seq;
 };
 
 // Harris pass-2 candidate (a superset of the global candidates: exact ratio
@@ -148,6 +153,8 @@ struct Dev {
     const int32_t* cind;
     const double* rval;
     double* qcol;
+    // debug (ELP_STAMPS): s_memrealtime stamps of k_ratio, 16 per chunk slot
+    unsigned long long* dstamp;
 };
 
 // ---------------------------------------------------------------- launches
@@ -163,19 +170,21 @@ hipError_t launch_ar_relayout(const Dev& d, const double* old_ar, int64_t old_ca
                               hipStream_t st);
 // ev0/ev1 (may be null): events recorded around the pricing kernel
 hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStream_t st,
-                            hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+                            hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, int dslot = 0);
 // sharded iteration: head (BTRAN, pricing, local min-loc into cand_xchg[rank]),
 // then the host all-gathers cand_xchg, select_global packs pkt, the host
 // all-reduces pkt, then tail (a_R, FTRAN, ratio test, update)
 hipError_t launch_iteration_head(const Dev& d, int k_ub, int ny_ub, int phase, int rank,
                                  hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_select_global(const Dev& d, hipStream_t st);
+// phase 2, at a host poll: apply a plan the last iteration left pending
+hipError_t launch_apply_pending(const Dev& d, int k_ub, hipStream_t st);
 // replicated A: global min-loc + a_R + bump FTRAN in one launch (false: the
 // bump is too large for it; use select_global + select_finish + tail(bump_ftran))
 bool launch_select_xftran(const Dev& d, int k_ub, hipStream_t st, hipError_t* err);
 hipError_t launch_select_finish(const Dev& d, hipStream_t st);
 hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t st,
-                                 bool bump_ftran = true);
+                                 bool bump_ftran = true, int dslot = 0);
 // row activities: ract = chain(ract, local nonzero nonbasic columns)
 hipError_t launch_row_chain(const Dev& d, hipStream_t st);
 // refactor = ns_resid; (host reads ns_emax) ns_update | gauss_jordan; primal

@@ -81,6 +81,19 @@ DEV const double* qcolumn(const Dev& d, int q) {
     if (d.Afull) return d.Afull + (size_t)q * (size_t)d.m;
     return d.pkt;
 }
+// KEEP(x): an empty asm that reads x.  Placed on an early-exit path it keeps
+// the compiler from sinking a prefetch load below the exit test (which would
+// serialise the prefetch behind the control-block round trip); the wait for x
+// lands on the exit path only.
+#define KEEP(x) asm volatile("" ::"v"(x))
+// Unconditional load of p[min(idx, lim - 1)] (p[0] when lim <= 0): a prefetch
+// whose bound is only an upper bound stays straight-line code, so the compiler
+// counts it in vmcnt instead of branching around it and draining the queue.
+template <class T>
+DEV T ld_clamp(const T* p, int idx, int lim) {
+    const int i = idx < lim ? idx : (lim > 0 ? lim - 1 : 0);
+    return p[i];
+}
 DEV bool cand_better(const Cand& a, const Cand& b, int bland) {
     if (a.j < 0) return false;
     if (b.j < 0) return true;
@@ -422,6 +435,21 @@ DEV void btran_body(const Dev& d, int phase, const double* __restrict__ tv) {
     }
 }
 
+// deferred update (phase 2): defined with k_update below
+struct Plan;
+DEV void apply_plan(const Dev& d, const Plan& P, int blk, int nb, int nb_minv, bool do_ar);
+DEV bool plan_pending(const DevCtl* c) { return c->plan_seq != c->applied_seq && c->plan.action != ACT_NONE; }
+// the pricing launch's trailing `napply` workgroups apply the pending plan
+DEV bool apply_role(const Dev& d, int napply, int nb_minv) {
+    if ((int)blockIdx.x < (int)gridDim.x - napply) return false;
+    const DevCtl* c = d.ctl;
+    if (plan_pending(c) && c->status != ST_NUMFAIL) {
+        const Plan P = c->plan;
+        apply_plan(d, P, blockIdx.x - (gridDim.x - napply), napply, nb_minv, false);
+    }
+    return true;
+}
+
 // ============================================================== pricing
 // One workgroup = 8 waves = 128 columns x all Y slots.  Wave w sweeps slot
 // chunk w (PRICE_SPLIT contiguous chunks), lane l owns columns 2l, 2l+1 of the
@@ -430,9 +458,10 @@ DEV void btran_body(const Dev& d, int phase, const double* __restrict__ tv) {
 // contiguous yy[] written by BTRAN (wave-uniform scalar loads).  The chunk
 // partials are combined in LDS in chunk order, then the tile's argmin.
 constexpr int PRICE_THREADS = 64 * PRICE_SPLIT;
-__global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d) {
+__global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int napply, int nb_minv) {
     __shared__ double part[PRICE_SPLIT][TILE_COLS];
     __shared__ Cand red[PRICE_SPLIT];
+    if (apply_role(d, napply, nb_minv)) return;
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
     if (d.ptimer && threadIdx.x == 0) d.pstamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -526,9 +555,10 @@ DEV double price_pass_bytes(const Dev& d, int ny) {
 // row order (oracle price_mode 1).  Tiles with more than CSC_STAGE nonzeros
 // read straight from global memory (same order).
 constexpr int CSC_STAGE = 2048;  // staged nonzeros per tile: 32 KiB of LDS
-__global__ void __launch_bounds__(TILE_COLS) k_price_csc(Dev d) {
+__global__ void __launch_bounds__(TILE_COLS) k_price_csc(Dev d, int napply, int nb_minv) {
     __shared__ double sv[CSC_STAGE], sy[CSC_STAGE];
     __shared__ Cand red[TILE_COLS / 64];
+    if (apply_role(d, napply, nb_minv)) return;
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
     if (d.ptimer && threadIdx.x == 0) d.pstamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -707,6 +737,7 @@ DEV void gather_aR(const Dev& d, int q, const double* qcol) {
 __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles) {
     __shared__ Cand red[16];
     DevCtl* c = d.ctl;
+    if (threadIdx.x == 0) c->applied_seq = c->plan_seq;  // the pricing launch applied it
     if (c->status != ST_RUN) return;
     const Cand best = local_best(d, ntiles, red);
     if (best.j < 0) {
@@ -732,47 +763,113 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles) {
 // slack candidates itself (a total order: all agree), gathers a_R into LDS and
 // computes alpha_S for its 4 bump rows (one wave per row, wave order).
 // Workgroup 0 publishes q.  Saves a launch and the single-workgroup select.
-__global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles) {
+__global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_ub, int ny_ub) {
     extern __shared__ __attribute__((aligned(16))) double aRs[];  // [k]
     __shared__ Cand red[4];
     DevCtl* c = d.ctl;
-    if (c->status != ST_RUN) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) c->applied_seq = c->plan_seq;  // applied by k_price
+    // Everything that does not depend on the control block or on q goes out
+    // first (bounded by the host's k_ub / ny_ub, masked below): the tile
+    // candidates, the Y slots' duals and rows, this wave's row of Minv, the R
+    // list.  After the min-loc only the a_R gather is left.
+    constexpr int PFM = 8;  // Minv values per lane held in registers (k <= 512)
+    constexpr int PFR = 4;  // R-list entries per thread (k <= 1024)
+    constexpr int PFC = 4;  // tile candidates per thread (<= 1024 tiles)
+    constexpr int PFY = 4;  // Y slots per thread (|Y| <= 1024)
+    const int pr = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, tid = threadIdx.x;
+    const bool pfm = k_ub <= 64 * PFM, pfr = k_ub <= 256 * PFR;
+    const bool pfc = ntiles <= 256 * PFC, pfy = ny_ub <= 256 * PFY;
+    double mrow[PFM];
+    int rl[PFR];
+    Cand cc[PFC];
+    int yl[PFY];
+    double yv[PFY];
+    int8_t vs[PFY];
+    // (unconditional, no branch around them: a load inside a conditional block
+    //  is drained at the block's end; masks are applied where values are used)
+#pragma unroll
+    for (int t = 0; t < PFC; ++t) cc[t] = ld_clamp(d.cand, tid + 256 * t, ntiles);
+#pragma unroll
+    for (int t = 0; t < PFY; ++t) {
+        yl[t] = ld_clamp(d.Yl, tid + 256 * t, ny_ub);
+        yv[t] = ld_clamp(d.yy, tid + 256 * t, ny_ub);
+    }
+    {
+        const double* row = d.Minv + (size_t)(pr < k_ub ? pr : 0) * d.ldm;
+#pragma unroll
+        for (int t = 0; t < PFM; ++t) mrow[t] = ld_clamp(row, lane + 64 * t, k_ub);
+    }
+#pragma unroll
+    for (int t = 0; t < PFR; ++t) rl[t] = ld_clamp(d.Rl, tid + 256 * t, k_ub);
+    // the slacks' status (second round trip: indexed by the Y rows; slots past
+    // the real |Y| are stale, so the index is range-checked)
+#pragma unroll
+    for (int t = 0; t < PFY; ++t) vs[t] = d.vstat[d.n + ((yl[t] >= 0 && yl[t] < d.m) ? yl[t] : 0)];
+    if (c->status != ST_RUN) {
+#pragma unroll
+        for (int t = 0; t < PFC; ++t) KEEP(cc[t].score);
+#pragma unroll
+        for (int t = 0; t < PFY; ++t) {
+            KEEP(yv[t]);
+            KEEP((int)vs[t]);
+        }
+#pragma unroll
+        for (int t = 0; t < PFM; ++t) KEEP(mrow[t]);
+#pragma unroll
+        for (int t = 0; t < PFR; ++t) KEEP(rl[t]);
+        return;
+    }
     const int bland = c->bland, ny = c->ny, k = c->k;
+    const double dtol = c->tol_dual;
     Cand best;
     best.j = -1;
     best.score = 0.0;
     best.d = 0.0;
-    for (int t = threadIdx.x; t < ntiles; t += 256) {
-        const Cand o = d.cand[t];
-        if (cand_better(o, best, bland)) best = o;
+    if (pfc) {
+#pragma unroll
+        for (int t = 0; t < PFC; ++t)
+            if (tid + 256 * t < ntiles && cand_better(cc[t], best, bland)) best = cc[t];
+    } else {
+        for (int t = tid; t < ntiles; t += 256) {
+            const Cand o = d.cand[t];
+            if (cand_better(o, best, bland)) best = o;
+        }
     }
-    const double dtol = c->tol_dual;
-    for (int p = threadIdx.x; p < ny; p += 256) {
-        const int i = d.Yl[p];
-        const int jl = d.n + i;
-        const int8_t vs = d.vstat[jl];
-        if (vs == VS_FIXED) continue;
-        const double dj = d.cost[jl] - d.yy[p];
+    // slack candidates (a slack's cost is 0: d = -y)
+    auto slack = [&](int p, int i, double yp, int8_t v) {
+        if (v == VS_FIXED) return;
+        const double dj = 0.0 - yp;
         Cand o;
         o.j = -1;
-        if ((vs == VS_LOWER || vs == VS_FREE) && dj < -dtol) {
+        if ((v == VS_LOWER || v == VS_FREE) && dj < -dtol) {
             o.j = d.N + i;
             o.score = -dj;
             o.d = dj;
-        } else if ((vs == VS_UPPER || vs == VS_FREE) && dj > dtol) {
+        } else if ((v == VS_UPPER || v == VS_FREE) && dj > dtol) {
             o.j = d.N + i;
             o.score = dj;
             o.d = dj;
         }
         if (cand_better(o, best, bland)) best = o;
+    };
+    if (pfy) {
+#pragma unroll
+        for (int t = 0; t < PFY; ++t)
+            if (tid + 256 * t < ny) slack(tid + 256 * t, yl[t], yv[t], vs[t]);  // (< ny: valid)
+    } else {
+        for (int p = tid; p < ny; p += 256) {
+            const int i = d.Yl[p];
+            slack(p, i, d.yy[p], d.vstat[d.n + i]);
+        }
     }
     best = block_best<256>(best, bland, red);
     if (best.j < 0) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) c->status = ST_PHASE_OPT;
+        if (blockIdx.x == 0 && tid == 0) c->status = ST_PHASE_OPT;
         return;
     }
     const int q = (int)best.j;
-    if (blockIdx.x == 0 && threadIdx.x == 0) entering_chosen(d, best);
+    if (blockIdx.x == 0 && tid == 0) entering_chosen(d, best);
     if (d.ptimer && blockIdx.x == gridDim.x - 1) {  // the extra timer workgroup
         price_timer_sum<256>(d, ntiles, reinterpret_cast<unsigned long long*>(aRs));
         return;
@@ -785,25 +882,45 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles) {
         scatter_aR_csc(d, q, aRs, k);
     } else if (q < d.N) {
         const double* col = d.A + (size_t)(q - d.col0) * (size_t)d.m;
-        for (int p = threadIdx.x; p < k; p += 256) aRs[p] = col[d.Rl[p]];
+        if (pfr) {
+            double g[PFR];
+#pragma unroll
+            for (int t = 0; t < PFR; ++t) g[t] = col[tid + 256 * t < k ? rl[t] : 0];  // straight-line
+#pragma unroll
+            for (int t = 0; t < PFR; ++t)
+                if (tid + 256 * t < k) aRs[tid + 256 * t] = g[t];
+        } else {
+            for (int p = tid; p < k; p += 256) aRs[p] = col[d.Rl[p]];
+        }
     } else {
         const int i0 = q - d.N;
-        for (int p = threadIdx.x; p < k; p += 256) aRs[p] = d.Rl[p] == i0 ? 1.0 : 0.0;
+        if (pfr) {
+#pragma unroll
+            for (int t = 0; t < PFR; ++t)
+                if (tid + 256 * t < k) aRs[tid + 256 * t] = rl[t] == i0 ? 1.0 : 0.0;
+        } else {
+            for (int p = tid; p < k; p += 256) aRs[p] = d.Rl[p] == i0 ? 1.0 : 0.0;
+        }
     }
     __syncthreads();
-    const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (p >= k) return;
-    const double* row = d.Minv + (size_t)p * d.ldm;
+    if (pr >= k) return;
     double acc = 0.0;
-    for (int i = lane; i < k; i += 64) acc = fma(row[i], aRs[i], acc);
+    if (pfm) {
+#pragma unroll
+        for (int t = 0; t < PFM; ++t)
+            if (lane + 64 * t < k) acc = fma(mrow[t], aRs[lane + 64 * t], acc);
+    } else {
+        const double* row = d.Minv + (size_t)pr * d.ldm;
+        for (int i = lane; i < k; i += 64) acc = fma(row[i], aRs[i], acc);
+    }
     acc = wave_tree(acc);
-    if (lane == 0) d.alS[p] = acc;
+    if (lane == 0) d.alS[pr] = acc;
 }
 
 __global__ void __launch_bounds__(1024) k_select_local(Dev d, int ntiles, int rank) {
     __shared__ Cand red[16];
-    const DevCtl* c = d.ctl;
+    DevCtl* c = d.ctl;
+    if (threadIdx.x == 0) c->applied_seq = c->plan_seq;  // applied by k_price
     if (c->status != ST_RUN) return;
     const Cand best = local_best(d, ntiles, red);
     if (threadIdx.x == 0) {
@@ -1007,17 +1124,48 @@ DEV void emit_cand(const Dev& d, int var, int e, double g, double x, double l, d
     d.rcand[slot] = cd;
 }
 
-constexpr int ZR_WAVES = 8;  // waves per row tile of k_ftran_zr
+constexpr int ZR_WAVES = 8;   // waves per row tile of k_ftran_zr
+constexpr int ZR_ROWS = 32;   // rows per row tile: lane = row + 32 * half; each
+                              // half-wave runs whole ZCHUNK chains (its own chunk)
 template <bool LDSZ>
-__global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt) {
-    extern __shared__ __attribute__((aligned(16))) double zlds[];  // [nch][64]
+__global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int k_ub) {
+    extern __shared__ __attribute__((aligned(16))) double zlds[];  // [nch][ZR_ROWS]
     __shared__ double red[ZR_WAVES];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & (ZR_ROWS - 1), hh = lane >> 5;
+    const int i = blockIdx.x * ZR_ROWS + r;
+    const size_t mm = (size_t)d.m;
+    // The first chunk's AS and alpha_S loads go out before the control block
+    // arrives: they are in bounds for any k <= k_ub (host upper bound) and the
+    // positions past the real k are dropped below.
+    const int ch0 = 2 * w + hh;
+    double a0[ZCHUNK], s0[ZCHUNK];
+    const bool row_tile = (int)blockIdx.x < nrt;
+    if (row_tile && ch0 * ZCHUNK < k_ub && i < d.m) {
+        const double* col = d.AS + (size_t)(ch0 * ZCHUNK) * mm + i;
+#pragma unroll
+        for (int t = 0; t < ZCHUNK; ++t) {
+            const bool in = ch0 * ZCHUNK + t < k_ub;
+            a0[t] = in ? col[(size_t)t * mm] : 0.0;
+            s0[t] = in ? d.alS[ch0 * ZCHUNK + t] : 0.0;
+        }
+    }
+    // likewise wave 0's epilogue operands (independent of q and z)
+    double tmin = HUGE_VAL;
+    double ge = 0.0, xe = 0.0, le = 0.0, he = 0.0;
+    int ve = -1;
+    int u = -1;
+    if (row_tile && w == 0 && hh == 0 && i < d.m) {
+        u = d.cover[i];
+        xe = d.xr[i];
+        le = d.rlo[i];
+        he = d.rhi[i];
+    }
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
     const int m = d.m, k = c->k, q = c->q, bland = c->bland;
     const double sig = c->sig, ptol = c->tol_primal, pivtol = c->tol_pivot;
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         d.ctl->snap_k = k;
         d.ctl->snap_bland = bland;
@@ -1035,56 +1183,53 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt) {
         }
         return;
     }
-    double tmin = HUGE_VAL;
-    double ge = 0.0, xe = 0.0, le = 0.0, he = 0.0;
-    int ve = -1;
-    // z partials of this tile's 64 rows: LDS, or (huge bumps) a private slice of zpart
-    double* zp = LDSZ ? zlds : d.zpart + (size_t)blockIdx.x * 64 * (size_t)((k + ZCHUNK - 1) / ZCHUNK);
-    if ((int)blockIdx.x < nrt) {
-        const int i = blockIdx.x * 64 + lane;
-        const int nch = (k + ZCHUNK - 1) / ZCHUNK;
-        const size_t mm = (size_t)m;
-        for (int ch = w; ch < nch; ch += ZR_WAVES) {
+    const int nch = (k + ZCHUNK - 1) / ZCHUNK;
+    // z partials of this tile's rows: LDS, or (huge bumps) a private slice of zpart
+    double* zp = LDSZ ? zlds : d.zpart + (size_t)blockIdx.x * ZR_ROWS * (size_t)nch;
+    if (row_tile) {
+        double aiq = 0.0;
+        if (u >= 0) aiq = q >= d.N ? (i == q - d.N ? 1.0 : 0.0) : qcolumn(d, q)[i];
+        if (ch0 < nch) {  // the prefetched chunk: fma chain over its real positions
+            double acc = 0.0;
+            if (i < m) {
+                const int len = min(ZCHUNK, k - ch0 * ZCHUNK);
+#pragma unroll
+                for (int t = 0; t < ZCHUNK; ++t)
+                    if (t < len) acc = fma(a0[t], s0[t], acc);
+            }
+            zp[ch0 * ZR_ROWS + r] = acc;
+        }
+        for (int ch = ch0 + 2 * ZR_WAVES; ch < nch; ch += 2 * ZR_WAVES) {
             const int c0 = ch * ZCHUNK, c1 = min(k, c0 + ZCHUNK);
             double acc = 0.0;
             if (i < m) {
                 const double* col = d.AS + (size_t)c0 * mm + i;
-                int p = c0;
-                for (; p + 16 <= c1; p += 16) {
-                    double a[16];
+                double a[ZCHUNK];  // the whole chunk in flight
+                if (c1 - c0 == ZCHUNK) {
 #pragma unroll
-                    for (int u = 0; u < 16; ++u) a[u] = col[(size_t)(p - c0 + u) * mm];
+                    for (int t = 0; t < ZCHUNK; ++t) a[t] = col[(size_t)t * mm];
 #pragma unroll
-                    for (int u = 0; u < 16; ++u) acc = fma(a[u], d.alS[p + u], acc);
-                }
-                if (p < c1) {
-                    double a[16];
+                    for (int t = 0; t < ZCHUNK; ++t) acc = fma(a[t], d.alS[c0 + t], acc);
+                } else {
 #pragma unroll
-                    for (int u = 0; u < 16; ++u) a[u] = (p + u < c1) ? col[(size_t)(p - c0 + u) * mm] : 0.0;
+                    for (int t = 0; t < ZCHUNK; ++t) a[t] = (c0 + t < c1) ? col[(size_t)t * mm] : 0.0;
 #pragma unroll
-                    for (int u = 0; u < 16; ++u)
-                        if (p + u < c1) acc = fma(a[u], d.alS[p + u], acc);
+                    for (int t = 0; t < ZCHUNK; ++t)
+                        if (c0 + t < c1) acc = fma(a[t], d.alS[c0 + t], acc);
                 }
             }
-            zp[ch * 64 + lane] = acc;
+            zp[ch * ZR_ROWS + r] = acc;
         }
         __syncthreads();
         if (w == 0) {
-            if (i < m) {
-                const int u = d.cover[i];
-                if (u >= 0) {
-                    double z = 0.0;
-                    for (int ch = 0; ch < nch; ++ch) z = z + zp[ch * 64 + lane];
-                    const double aiq = q >= d.N ? (i == q - d.N ? 1.0 : 0.0) : qcolumn(d, q)[i];
-                    const double alU = unit_sign(d, u, i) * (aiq - z);
-                    d.alU[i] = alU;
-                    ge = sig * alU;
-                    xe = d.xr[i];
-                    le = d.rlo[i];
-                    he = d.rhi[i];
-                    ve = u;
-                    tmin = harris1(ge, xe, le, he, ptol, pivtol, bland);
-                }
+            if (hh == 0 && i < m && u >= 0) {
+                double z = 0.0;
+                for (int ch = 0; ch < nch; ++ch) z = z + zp[ch * ZR_ROWS + r];
+                const double alU = unit_sign(d, u, i) * (aiq - z);
+                d.alU[i] = alU;
+                ge = sig * alU;
+                ve = u;
+                tmin = harris1(ge, xe, le, he, ptol, pivtol, bland);
             }
             double bmin = tmin;
 #pragma unroll
@@ -1148,7 +1293,14 @@ enum { SI_VSQ, SI_RPOS0, SI_YPOS0, SI_YLAST, SI_SLLAST, SI_RLLAST, SI_RPOSYL, SI
 // then forms vvec for its 4 columns when a unit variable leaves.  k and bland
 // come from the snapshot (workgroup 0 rewrites them).  The primal update
 // x_B -= step * alpha runs in k_update.
-__global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int lds_row) {
+// Phase 2 (defer != 0): workgroups [nmain, gridDim.x) copy this pivot's AR rows
+// (the only update the next pricing sweep needs), workgroup 0 runs the loop-top
+// checks, and the rest of the update is deferred into the next pricing launch.
+// debug stamps (Dev::dstamp, ELP_STAMPS): s_memrealtime at the phases of workgroup 0
+#define RSTAMP(i) do { if (d.dstamp && blockIdx.x == 0 && threadIdx.x == 0) \
+    d.dstamp[dslot * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+__global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int lds_row, int defer,
+                                               int nmain, int k_ub, int dslot) {
     extern __shared__ __attribute__((aligned(16))) double asrow_lds[];  // [k]: A[lrow, S]
     __shared__ double dred[4];
     __shared__ Leave lred[4];
@@ -1157,53 +1309,146 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     __shared__ int s_action;
     __shared__ Plan s_plan;
     __shared__ double s_wd;
+    const int tid = threadIdx.x;
+    const int col = blockIdx.x * 4 + (tid >> 6);
+    const int lane = tid & 63;
+    if (d.dstamp && tid == 0) {
+        const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+        atomicMin(&d.dstamp[dslot * 16 + 11], t);
+        atomicMax(&d.dstamp[dslot * 16 + 8], t);
+    }
+    RSTAMP(0);
+    // ---- loads that depend on neither the control block nor the decision go
+    //      out first (bounded by the host's k_ub, masked by the real k below):
+    //      the pass-1 minima, this wave's row of MinvT (B^-1 row, cases B / D)
+    //      and its bump row R_col (dual update)
+    constexpr int PFB = 4, PFT = 8;
+    const bool main_wg = (int)blockIdx.x < nmain;
+    const bool pfb = nblk <= 256 * PFB, pft = k_ub <= 64 * PFT;
+    double bm[PFB], trow[PFT];
+    // (unconditional, no branch around them: a load inside a conditional block
+    //  is drained at the block's end; masks are applied where the values are used)
+#pragma unroll
+    for (int t = 0; t < PFB; ++t) bm[t] = ld_clamp(d.blockmin, tid + 256 * t, nblk);
+    {  // (AR-copy workgroups fetch row 0: harmless)
+        const double* row = d.MinvT + (size_t)(main_wg && col < k_ub ? col : 0) * d.ldm;
+#pragma unroll
+        for (int t = 0; t < PFT; ++t) trow[t] = ld_clamp(row, lane + 64 * t, k_ub);
+    }
+    // entries of Rl past the real k are stale: range-checked before use
+    const int rcol = ld_clamp(d.Rl, main_wg ? col : 0, k_ub);
     DevCtl* c = d.ctl;
     if (c->status != ST_RUN) {  // no plan this iteration: k_update must not re-apply one
         if (blockIdx.x == 0 && threadIdx.x == 0) c->plan.action = ACT_NONE;
+#pragma unroll
+        for (int t = 0; t < PFB; ++t) KEEP(bm[t]);
+#pragma unroll
+        for (int t = 0; t < PFT; ++t) KEEP(trow[t]);
+        KEEP(rcol);
         return;
     }
     const int m = d.m, k = c->snap_k, q = c->q, ny = c->snap_ny, ncand = c->ncand;
-    const double sig = c->sig;
+    const double sig = c->sig, dq = c->dq;
     const int bland = c->snap_bland;
     const bool lead = blockIdx.x == 0;
-    const int tid = threadIdx.x;
+    RSTAMP(1);
+    // workgroup 0 / thread 0 keeps the counters it updates in registers
+    // (read once here instead of one dependent round trip per update)
+    // (every lane loads them -- one line, broadcast -- so no branch drains them)
+    const int64_t cs_iter = c->iter, cs_limit = c->iter_limit, cs_stop = c->iter_stop;
+    const int64_t cs_tcap = c->trace_cap, cs_p1 = c->phase1_iters, cs_flips = c->flips;
+    const int64_t cs_degen = c->degenerate;
+    const int32_t cs_ndegen = c->ndegen, cs_dswitch = c->degen_switch, cs_since = c->since_refactor;
+    const int32_t cs_period = c->refactor_period, cs_seq = c->plan_seq;
+    // oracle run_phase loop top for the next phase-2 iteration, on the values
+    // thread 0 has just written (phase 1: k_btran's)
+    auto loop_top = [&](int32_t status, int64_t iter, int32_t since) {
+        if (status != ST_RUN) return;
+        if (iter >= cs_limit) c->status = ST_ITERCAP;
+        else if (iter >= cs_stop) c->status = ST_STOP;
+        else if (since >= cs_period) c->status = ST_REFACTOR;
+    };
     const int last = k - 1;
+    // dual-update operands of this wave's bump row (read unconditionally at a
+    // valid index; only used when col < k)
+    const int rsafe = (rcol >= 0 && rcol < m) ? rcol : 0;
+    const double yold = d.y[rsafe];
+    const int ypos_r = d.ypos[rsafe];  // its Y slot (workgroup 0 rewrites no bump row's slot)
     // ---- parallel prefetch of bookkeeping scalars
     const int ql = loc_of(d, q);  // -1: the entering column lives on another shard
-    if (tid < SC_N + SI_N) {
+    {
+        // thread t < SC_N loads double scalar t, thread SC_N + u int scalar u:
+        // addresses picked by selects, one unconditional load each
         const bool pk = ql < 0 || (d.sharded && q < d.N);  // from the exchanged packet
+        const int ls = last >= 0 ? last : 0;
+        const double zero = 0.0;
+        const double* dp = &zero;
         switch (tid) {
-            case SC_LBQ: sc[SC_LBQ] = pk ? d.pkt[m] : d.lb[ql]; break;
-            case SC_UBQ: sc[SC_UBQ] = pk ? d.pkt[m + 1] : d.ub[ql]; break;
-            case SC_XVQ: sc[SC_XVQ] = pk ? d.pkt[m + 2] : d.xval[ql]; break;
-            case SC_CQ: sc[SC_CQ] = pk ? d.pkt[m + 3] : d.cost[ql]; break;
-            case SC_SLL: sc[SC_SLL] = 0.0; break;
-            case SC_CSL: sc[SC_CSL] = last >= 0 ? d.cS[last] : 0.0; break;
-            case SC_SLOL: sc[SC_SLOL] = last >= 0 ? d.slo[last] : 0.0; break;
-            case SC_SHIL: sc[SC_SHIL] = last >= 0 ? d.shi[last] : 0.0; break;
-            case SC_N + SI_VSQ: si[SI_VSQ] = ql >= 0 ? d.vstat[ql] : VS_LOWER; break;
-            case SC_N + SI_RPOS0: si[SI_RPOS0] = c->snap_apos; break;
-            case SC_N + SI_YPOS0: si[SI_YPOS0] = c->snap_ypos0; break;
-            case SC_N + SI_YLAST: si[SI_YLAST] = c->snap_ylast; break;
-            case SC_N + SI_SLLAST: si[SI_SLLAST] = last >= 0 ? d.Sl[last] : -1; break;
-            case SC_N + SI_RLLAST: si[SI_RLLAST] = last >= 0 ? d.Rl[last] : -1; break;
-            case SC_N + SI_RPOSYL: si[SI_RPOSYL] = c->snap_rposyl; break;
+            case SC_LBQ: dp = pk ? d.pkt + m : d.lb + ql; break;
+            case SC_UBQ: dp = pk ? d.pkt + m + 1 : d.ub + ql; break;
+            case SC_XVQ: dp = pk ? d.pkt + m + 2 : d.xval + ql; break;
+            case SC_CQ: dp = pk ? d.pkt + m + 3 : d.cost + ql; break;
+            case SC_CSL: dp = d.cS + ls; break;
+            case SC_SLOL: dp = d.slo + ls; break;
+            case SC_SHIL: dp = d.shi + ls; break;
+            default: break;
+        }
+        const int32_t neg = -1;
+        const int32_t* ip = &neg;
+        switch (tid - SC_N) {
+            case SI_SLLAST: ip = d.Sl + ls; break;
+            case SI_RLLAST: ip = d.Rl + ls; break;
+            default: break;
+        }
+        const int8_t* vp = d.vstat + (ql >= 0 ? ql : 0);
+        const double dv = *dp;
+        const int32_t iv = *ip;
+        const int8_t vv = *vp;
+        if (tid < SC_N) sc[tid] = (tid == SC_SLL || (last < 0 && tid >= SC_CSL)) ? 0.0 : dv;
+        switch (tid - SC_N) {
+            case SI_VSQ: si[SI_VSQ] = ql >= 0 ? vv : VS_LOWER; break;
+            case SI_RPOS0: si[SI_RPOS0] = c->snap_apos; break;
+            case SI_YPOS0: si[SI_YPOS0] = c->snap_ypos0; break;
+            case SI_YLAST: si[SI_YLAST] = c->snap_ylast; break;
+            case SI_SLLAST: si[SI_SLLAST] = last >= 0 ? iv : -1; break;
+            case SI_RLLAST: si[SI_RLLAST] = last >= 0 ? iv : -1; break;
+            case SI_RPOSYL: si[SI_RPOSYL] = c->snap_rposyl; break;
+            default: break;
         }
     }
+    // the pass-2 candidates (emitted by k_ftran_zr) go out with the rest
+    constexpr int PFQ = 4;  // per thread, held in registers (<= 1024 candidates)
+    const bool pfq = ncand <= 256 * PFQ;
+    RCand rq[PFQ];
+#pragma unroll
+    for (int t = 0; t < PFQ; ++t) rq[t] = ld_clamp(d.rcand, tid + 256 * t, ncand);
+    // case D needs wave_dot(MinvT[apos, :], A[lrow, S]) in every workgroup: wave 0
+    // fetches that row now (apos comes with the control block)
+    const int apos_c = c->snap_apos;
+    double arow[PFT];
+    {
+        const double* row = d.MinvT + (size_t)(apos_c >= 0 ? apos_c : 0) * d.ldm;
+#pragma unroll
+        for (int t = 0; t < PFT; ++t) arow[t] = ld_clamp(row, lane + 64 * t, k);
+    }
     // ---- pass 1 result: min over the workgroup minima
-    const double pivtol = c->tol_pivot, INF = HUGE_VAL;
-    (void)pivtol;
+    const double INF = HUGE_VAL;
     double tmax = INF;
-    for (int b = tid; b < nblk; b += 256) tmax = fmin(tmax, d.blockmin[b]);
+    if (pfb) {
+#pragma unroll
+        for (int t = 0; t < PFB; ++t) tmax = fmin(tmax, tid + 256 * t < nblk ? bm[t] : INF);
+    } else {
+        for (int b = tid; b < nblk; b += 256) tmax = fmin(tmax, d.blockmin[b]);
+    }
     const double theta_max = block_min<256>(tmax, dred);
+    RSTAMP(2);
     // ---- pass 2 over the candidates
     Leave best;
     best.var = -1;
     best.ag = best.r = best.g = best.l = best.u = 0.0;
     best.e = -1;
-    for (int t = tid; t < ncand; t += 256) {
-        const RCand cd = d.rcand[t];
-        if (!(cd.r <= theta_max)) continue;
+    auto consider = [&](const RCand& cd) {
+        if (!(cd.r <= theta_max)) return;
         Leave o;
         o.var = cd.var;
         o.ag = fabs(cd.g);
@@ -1213,6 +1458,13 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         o.u = cd.u;
         o.e = cd.e;
         if (leave_better(o, best, bland)) best = o;
+    };
+    if (pfq) {
+#pragma unroll
+        for (int t = 0; t < PFQ; ++t)
+            if (tid + 256 * t < ncand) consider(rq[t]);
+    } else {
+        for (int t = tid; t < ncand; t += 256) consider(d.rcand[t]);
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
@@ -1224,6 +1476,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     best = lred[0];
     for (int i = 1; i < 4; ++i)
         if (leave_better(lred[i], best, bland)) best = lred[i];
+    RSTAMP(3);
     // ---- decision (uniform across the block)
     const double lbq = sc[SC_LBQ], ubq = sc[SC_UBQ];
     const double theta = best.var >= 0 ? (best.r > 0.0 ? best.r : 0.0) : INF;
@@ -1241,15 +1494,15 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         step = theta;
     }
     if (lead && tid == 0) {
-        const int64_t it = c->iter;
+        const int64_t it = cs_iter;
         c->iter = it + 1;
-        if (phase == 1) c->phase1_iters++;
+        if (phase == 1) c->phase1_iters = cs_p1 + 1;
         if (action == ACT_NONE) {
             c->status = ST_UNBOUNDED;
             c->unb_var = q;
             c->unb_sig = sig;
         }
-        if (it < c->trace_cap) {  // leaving: -1 bound flip, -2 unbounded ray
+        if (it < cs_tcap) {  // leaving: -1 bound flip, -2 unbounded ray
             d.trace[2 * it] = q;
             d.trace[2 * it + 1] = action == ACT_FLIP ? -1 : action == ACT_NONE ? -2 : best.var;
         }
@@ -1269,7 +1522,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
                     d.xval[ql] = lbq;
                 }
             }
-            c->flips++;
+            c->flips = cs_flips + 1;
             c->ndegen = 0;
             c->bland = 0;
             Plan P;
@@ -1284,28 +1537,88 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
             P.piv = 0.0;
             P.xq = 0.0;
             c->plan = P;
+            c->plan_seq = cs_seq + 1;
+            if (defer) loop_top(ST_RUN, cs_iter + 1, cs_since);
+        }
+        return;
+    }
+    if ((int)blockIdx.x >= nmain) {  // deferred flow: this pivot's AR row copies
+        if (d.csc) return;
+        const int lrow = best.e < m ? best.e : -1;
+        const bool leave_art = best.var >= d.N + m;
+        int rm_slot = -1, rm_last = -1, ap_slot = -1, ap_row = -1;
+        if (q < d.N) {
+            if (lrow >= 0 && !leave_art) {  // case B: the leaving unit var's row joins Y
+                ap_slot = ny;
+                ap_row = lrow;
+            }
+        } else {  // C, D, E: row i0 leaves Y; D: the leaving slack's row joins it
+            rm_slot = si[SI_YPOS0];
+            rm_last = ny - 1;
+            if (si[SI_RPOS0] >= 0 && lrow >= 0 && !leave_art) {
+                ap_slot = ny - 1;
+                ap_row = lrow;
+            }
+        }
+        if (rm_slot < 0 && ap_slot < 0) return;
+        const int64_t tstride = (int64_t)(gridDim.x - nmain) * blockDim.x;
+        for (int64_t j = (int64_t)(blockIdx.x - nmain) * blockDim.x + tid; j < d.n; j += tstride) {
+            if (rm_slot >= 0 && rm_slot != rm_last) d.AR[ar_at(d, rm_slot, j)] = d.AR[ar_at(d, rm_last, j)];
+            if (ap_slot >= 0) d.AR[ar_at(d, ap_slot, j)] = d.A[(size_t)j * (size_t)m + ap_row];
+        }
+        if (d.dstamp) {
+            __syncthreads();
+            if (tid == 0) atomicMax(&d.dstamp[dslot * 16 + 10], __builtin_amdgcn_s_memrealtime());
         }
         return;
     }
     // ---- B^-1 row for a leaving unit variable (cases B, D; E wastes it):
     //      vvec[c] = wave_dot(MinvT[c, 0:k], A[lrow, S]), case B / delta
     const int lrow_all = best.e < m ? best.e : -1;
-    const int col = blockIdx.x * 4 + (tid >> 6);
-    const int lane = tid & 63;
     double vcol = 0.0;  // vvec[col] (cases B, D)
     // pivot case as workgroup 0's bookkeeping will classify it
     const int lposx = best.e >= m ? best.e - m : -1;
     const int apos = si[SI_RPOS0];
     const int pcx = q < d.N ? (lposx >= 0 ? PC_A : PC_B) : apos < 0 ? PC_E : lposx >= 0 ? PC_C : PC_D;
+    // operands of the dual update that need the decision (cases A, C)
+    const bool upd = phase == 2 && lane == 0 && col < k && pcx != PC_E &&
+                     !((pcx == PC_C || pcx == PC_D) && col == apos);
+    const size_t lrowoff = (size_t)(lposx >= 0 ? lposx : 0) * d.ldm;
+    const double mpc = d.Minv[lrowoff + (col < k ? col : 0)];
+    const double mpiv = d.Minv[lrowoff + (apos >= 0 ? apos : 0)];
+    // workgroup 0: what its bookkeeping and the closing vrow / colA copies read
+    constexpr int PFV = 4;  // k <= 1024
+    const bool pfv = k <= 256 * PFV;
+    double vr[PFV], ca[PFV];
+    double t0_piv = 0.0, t0_ymoved = 0.0;
+    int t0_yposl = -1;
+    {  // (straight-line; workgroup 0 uses them, the others discard them)
+        const size_t rv = (size_t)(lposx >= 0 ? lposx : 0) * d.ldm, ra = (size_t)(apos >= 0 ? apos : 0) * d.ldm;
+#pragma unroll
+        for (int t = 0; t < PFV; ++t) {
+            vr[t] = ld_clamp(d.Minv + rv, tid + 256 * t, k);
+            ca[t] = ld_clamp(d.MinvT + ra, tid + 256 * t, k);
+        }
+        t0_piv = d.Minv[rv + (apos >= 0 ? apos : 0)];
+        t0_yposl = d.ypos[lrow_all >= 0 ? lrow_all : 0];
+        const int moved = si[SI_YLAST];
+        t0_ymoved = d.y[moved >= 0 ? moved : 0];
+    }
     if (lrow_all >= 0 && k > 0) {
         // huge bumps: every workgroup writes the same values to d.vrow (benign)
         double* asrow = lds_row ? asrow_lds : d.vrow;
         for (int j = tid; j < k; j += 256) asrow[j] = d.AS[(size_t)j * (size_t)m + lrow_all];
         __syncthreads();
         if (col < k) {
-            const double* row = d.MinvT + (size_t)col * d.ldm;
             double acc = 0.0;
-            for (int j = lane; j < k; j += 64) acc = fma(row[j], asrow[j], acc);
+            if (pft) {
+#pragma unroll
+                for (int t = 0; t < PFT; ++t)
+                    if (lane + 64 * t < k) acc = fma(trow[t], asrow[lane + 64 * t], acc);
+            } else {
+                const double* row = d.MinvT + (size_t)col * d.ldm;
+                for (int j = lane; j < k; j += 64) acc = fma(row[j], asrow[j], acc);
+            }
             acc = wave_tree(acc);
             // case B delta = acol_i - z_i = sigma_u * sig * g (exact)
             const double delta = unit_sign(d, best.var, lrow_all) * (sig * best.g);
@@ -1313,45 +1626,57 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
             if (lane == 0) d.vvec[col] = vcol;
         }
         if (phase == 2 && pcx == PC_D && tid < 64) {  // vvec[a], redundantly per workgroup
-            const double* row = d.MinvT + (size_t)apos * d.ldm;
             double acc = 0.0;
-            for (int j = lane; j < k; j += 64) acc = fma(row[j], asrow[j], acc);
+            if (pft) {
+#pragma unroll
+                for (int t = 0; t < PFT; ++t)
+                    if (lane + 64 * t < k) acc = fma(arow[t], asrow[lane + 64 * t], acc);
+            } else {
+                const double* row = d.MinvT + (size_t)apos * d.ldm;
+                for (int j = lane; j < k; j += 64) acc = fma(row[j], asrow[j], acc);
+            }
             acc = wave_tree(acc);
-            if (tid == 0) s_wd = c->dq / acc;
+            if (tid == 0) s_wd = dq / acc;
         }
         __syncthreads();
     }
+    RSTAMP(4);
     // ---- phase 2 dual update y += theta_d rho_r on the bump rows, one wave per
     //      position (oracle run_phase cases A-D); the rows that join or leave R
     //      and the Y slot that moves are workgroup 0's (below)
-    const double dq = c->dq;
     const double wD = (phase == 2 && pcx == PC_D) ? s_wd : 0.0;
-    if (phase == 2 && lane == 0 && col < k && pcx != PC_E &&
-        !((pcx == PC_C || pcx == PC_D) && col == apos)) {
-        const int row = d.Rl[col];
-        const double yo = d.y[row];
+    if (upd) {
+        const int row = rcol;
+        const double yo = yold;
         double yn;
         if (pcx == PC_A) {
-            yn = fma(dq, d.Minv[(size_t)lposx * d.ldm + col] / (best.g * sig), yo);
+            yn = fma(dq, mpc / (best.g * sig), yo);
         } else if (pcx == PC_B) {
             yn = fma(-dq, vcol, yo);
         } else if (pcx == PC_C) {
-            const double piv = d.Minv[(size_t)lposx * d.ldm + apos];
-            yn = fma(dq, d.Minv[(size_t)lposx * d.ldm + col] / piv, yo);
+            yn = fma(dq, mpc / mpiv, yo);
         } else {
             yn = fma(wD, vcol, yo);
         }
         d.y[row] = yn;
         // the last Y row moves into the slot of row i0 (cases C, D)
-        const int slot = (pcx == PC_C || pcx == PC_D) && row == si[SI_YLAST] ? si[SI_YPOS0] : d.ypos[row];
+        // (workgroup 0 rewrites ypos only for rows that are not bump rows, the
+        //  entering slack's row -- excluded above -- and the moved last row)
+        const int slot = (pcx == PC_C || pcx == PC_D) && row == si[SI_YLAST] ? si[SI_YPOS0] : ypos_r;
         if (slot >= 0) d.yy[slot] = yn;
+    }
+    RSTAMP(5);
+    if (d.dstamp) {
+        __syncthreads();
+        if (tid == 0) atomicMax(&d.dstamp[dslot * 16 + 9], __builtin_amdgcn_s_memrealtime());
     }
     if (!lead) return;
     // ---- pivot: bookkeeping by thread 0 (stores only, plus Minv[b][a] in case C)
     if (tid == 0) {
         if (theta == 0.0) {
-            c->degenerate++;
-            if (++c->ndegen >= c->degen_switch) c->bland = 1;
+            c->degenerate = cs_degen + 1;
+            c->ndegen = cs_ndegen + 1;
+            if (cs_ndegen + 1 >= cs_dswitch) c->bland = 1;
         } else {
             c->ndegen = 0;
             c->bland = 0;
@@ -1432,7 +1757,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
                 P.a = a;
                 P.b = b;
                 P.last = last;
-                P.piv = d.Minv[(size_t)b * d.ldm + a];
+                P.piv = t0_piv;  // Minv[b][a]
                 if (b != last) {
                     d.Sl[b] = si[SI_SLLAST];
                     d.cS[b] = sc[SC_CSL];
@@ -1482,15 +1807,21 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
             }
         }
         if (phase == 2) {  // dual update: rows joining / leaving R, the moved Y slot
+            // Y slot of the leaving unit var's row: the appended slot, or (an
+            // artificial left: no append) the slot it already had
+            int yslot = P.y_ap_slot >= 0 ? P.y_ap_slot : t0_yposl;
+            if (P.y_ap_slot < 0 && P.pcase >= PC_C && P.y_rm_slot != P.y_rm_last &&
+                P.lrow == si[SI_YLAST])
+                yslot = P.y_rm_slot;  // the leaving row was the last Y row: moved into i0's slot
             if (P.pcase == PC_B) {
                 const double yn = dq / P.piv;
                 d.y[P.row] = yn;
-                d.yy[d.ypos[P.row]] = yn;
+                d.yy[yslot] = yn;
             } else if (P.pcase == PC_C || P.pcase == PC_D) {
                 d.y[P.i0] = 0.0;
                 if (P.pcase == PC_D) {
                     d.y[P.row] = -wD;
-                    d.yy[d.ypos[P.row]] = -wD;
+                    d.yy[yslot] = -wD;
                 }
             }
             if (P.pcase >= PC_C) {  // C, D, E removed row i0 from Y
@@ -1498,20 +1829,31 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
                 // the owner wave of a bump row wrote its moved slot already
                 const bool owned = P.pcase != PC_E && si[SI_RPOSYL] >= 0;
                 const bool special = P.pcase == PC_D && moved == P.row;
-                if (sl != ny - 1 && !owned && !special) d.yy[sl] = d.y[moved];
+                if (sl != ny - 1 && !owned && !special) d.yy[sl] = t0_ymoved;
             }
         }
         c->k = newk;
         c->ny = nny;
-        c->since_refactor++;
+        c->since_refactor = cs_since + 1;
         c->plan = P;
+        c->plan_seq = cs_seq + 1;
+        if (defer) loop_top(P.pcase == PC_E && lrow != q - d.N ? ST_NUMFAIL : ST_RUN, cs_iter + 1, cs_since + 1);
         s_plan = P;
         s_action = P.pcase;
     }
+    RSTAMP(6);
     __syncthreads();
     const Plan P = s_plan;
     const int pc = s_action;
-    if (pc == PC_A) {
+    if (pfv) {  // rows prefetched after the decision (P.p = P.b = lpos, P.a = apos)
+#pragma unroll
+        for (int t = 0; t < PFV; ++t) {
+            const int j = tid + 256 * t;
+            if (j >= k) continue;
+            if (pc == PC_A || pc == PC_C) d.vrow[j] = vr[t] / P.piv;
+            if (pc == PC_C || pc == PC_D) d.colA[j] = ca[t];
+        }
+    } else if (pc == PC_A) {
         for (int j = tid; j < k; j += 256) d.vrow[j] = d.Minv[(size_t)P.p * d.ldm + j] / P.piv;
     } else if (pc == PC_C) {
         for (int j = tid; j < k; j += 256) {
@@ -1520,6 +1862,10 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         }
     } else if (pc == PC_D) {
         for (int j = tid; j < k; j += 256) d.colA[j] = d.MinvT[(size_t)P.a * d.ldm + j];
+    }
+    if (d.dstamp) {
+        __syncthreads();
+        RSTAMP(7);
     }
 }
 
@@ -1552,26 +1898,17 @@ DEV double minv_new(const Dev& d, const Plan& P, int i, int j, const OldM& old) 
     }
 }
 
-// Minv and MinvT update (blocks [0, nb_minv)) + primal update x_B -= step*alpha
-// and AS / AR copies (the rest).  Flips only update x_B.
-__global__ void __launch_bounds__(256) k_update(Dev d, int nb_minv, int phase) {
-    DevCtl* c = d.ctl;
-    if (phase == 2 && blockIdx.x == 0 && threadIdx.x == 0 && c->status == ST_RUN) {
-        // oracle run_phase loop top for the next iteration (phase 1: k_btran's)
-        if (c->iter >= c->iter_limit) c->status = ST_ITERCAP;
-        else if (c->iter >= c->iter_stop) c->status = ST_STOP;
-        else if (c->since_refactor >= c->refactor_period) c->status = ST_REFACTOR;
-    }
-    // the plan k_ratio made this iteration (ACT_NONE when it did not run)
-    const Plan P = c->plan;
-    if (P.action == ACT_NONE || c->status == ST_NUMFAIL) return;
+// The plan k_ratio made: Minv and MinvT update (blocks [0, nb_minv)) + primal
+// update x_B -= step*alpha and AS copies (blocks [nb_minv, nb)); with do_ar also
+// the AR row copies (phase 1, where nothing is deferred).  Flips only update x_B.
+DEV void apply_plan(const Dev& d, const Plan& P, int blk, int nb, int nb_minv, bool do_ar) {
     const int k = P.k_old;
     const size_t ldm = (size_t)d.ldm;
-    if ((int)blockIdx.x < nb_minv) {
+    if (blk < nb_minv) {
         if (P.action != ACT_PIVOT || P.pcase == PC_E) return;
         const int kk = P.pcase == PC_B ? k + 1 : P.pcase == PC_C ? k - 1 : k;
         const int64_t nel = (int64_t)kk * kk;
-        const int64_t e0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        const int64_t e0 = (int64_t)blk * blockDim.x + threadIdx.x;
         const int64_t estride = (int64_t)nb_minv * blockDim.x;
         const OldM oM{d.Minv, ldm, false}, oT{d.MinvT, ldm, true};
         for (int64_t e = e0; e < 2 * nel; e += estride) {
@@ -1588,8 +1925,8 @@ __global__ void __launch_bounds__(256) k_update(Dev d, int nb_minv, int phase) {
     }
     // ---- primal update (oracle order: x -= step * (sig * alpha), then the
     //      entering value / compaction of the pivot case)
-    const int64_t t0 = (int64_t)(blockIdx.x - nb_minv) * blockDim.x + threadIdx.x;
-    const int64_t tstride = (int64_t)(gridDim.x - nb_minv) * blockDim.x;
+    const int64_t t0 = (int64_t)(blk - nb_minv) * blockDim.x + threadIdx.x;
+    const int64_t tstride = (int64_t)(nb - nb_minv) * blockDim.x;
     const size_t m = (size_t)d.m;
     const double step = P.step, sg = P.sig;
     for (int64_t t = t0; t < d.m; t += tstride) {
@@ -1615,13 +1952,24 @@ __global__ void __launch_bounds__(256) k_update(Dev d, int nb_minv, int phase) {
             d.AS[(size_t)P.b * m + t] = d.AS[(size_t)P.last * m + t];
         }
     }
-    if (!d.csc && (P.y_rm_slot >= 0 || P.y_ap_slot >= 0)) {  // CSC prices from the columns
+    if (do_ar && !d.csc && (P.y_rm_slot >= 0 || P.y_ap_slot >= 0)) {  // CSC prices from the columns
         for (int64_t j = t0; j < d.n; j += tstride) {
             if (P.y_rm_slot >= 0 && P.y_rm_slot != P.y_rm_last)
                 d.AR[ar_at(d, P.y_rm_slot, j)] = d.AR[ar_at(d, P.y_rm_last, j)];
             if (P.y_ap_slot >= 0) d.AR[ar_at(d, P.y_ap_slot, j)] = d.A[(size_t)j * m + P.y_ap_row];
         }
     }
+}
+
+// Standalone update.  mode 0 (phase 1): the plan k_ratio just made, AR included.
+// mode 1 (phase 2, host poll): a deferred plan still pending; its AR rows were
+// copied by k_ratio already.
+__global__ void __launch_bounds__(256) k_update(Dev d, int nb_minv, int mode) {
+    const DevCtl* c = d.ctl;
+    if (mode == 1 && !plan_pending(c)) return;
+    const Plan P = c->plan;
+    if (P.action == ACT_NONE || c->status == ST_NUMFAIL) return;
+    apply_plan(d, P, blockIdx.x, gridDim.x, nb_minv, mode == 0);
 }
 
 // ============================================================== refactor
@@ -2084,6 +2432,18 @@ hipError_t launch_init_rows(const Dev& d, const double* rhs, hipStream_t st) {
     return hipGetLastError();
 }
 
+// workgroups of a plan application for bumps up to k_ub: nb_minv for Minv /
+// MinvT, the rest for x_B, AS (and AR rows: with_ar)
+static void update_grid(const Dev& d, int k_ub, bool with_ar, unsigned* nb_minv, unsigned* nb) {
+    const int64_t kk = 2 * (int64_t)(k_ub + 1) * (k_ub + 1);
+    *nb_minv = cdiv(kk, 256);
+    if (*nb_minv > 2048) *nb_minv = 2048;
+    const int64_t cw = with_ar ? (d.m > d.n ? d.m : d.n) : (d.m > k_ub + 1 ? d.m : k_ub + 1);
+    unsigned nb_copy = cdiv(cw, 256);
+    if (nb_copy > 1024) nb_copy = 1024;
+    *nb = *nb_minv + nb_copy;
+}
+
 static hipError_t launch_btran_price(const Dev& d, int k_ub, int phase, hipStream_t st,
                                      hipEvent_t ev0, hipEvent_t ev1) {
     const int m = d.m;
@@ -2099,47 +2459,64 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int phase, hipStrea
         k_btran<<<g, 256, 0, st>>>(d, phase, tv);
     }
     const unsigned ntiles = cdiv(d.n, TILE_COLS);
+    // phase 2: the previous iteration's plan is applied by trailing workgroups
+    // of the pricing launch (it touches nothing the sweep reads)
+    unsigned nb_minv = 0, napply = 0;
+    if (phase == 2) update_grid(d, k_ub, false, &nb_minv, &napply);
     if (ev0) (void)hipEventRecord(ev0, st);
-    if (d.csc) k_price_csc<<<ntiles, TILE_COLS, 0, st>>>(d);
-    else k_price<<<ntiles, PRICE_THREADS, 0, st>>>(d);
+    if (d.csc) k_price_csc<<<ntiles + napply, TILE_COLS, 0, st>>>(d, (int)napply, (int)nb_minv);
+    else k_price<<<ntiles + napply, PRICE_THREADS, 0, st>>>(d, (int)napply, (int)nb_minv);
     if (ev1) (void)hipEventRecord(ev1, st);
     return hipGetLastError();
 }
 
-hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t st, bool bump_ftran) {
+hipError_t launch_apply_pending(const Dev& d, int k_ub, hipStream_t st) {
+    unsigned nb_minv, nb;
+    update_grid(d, k_ub, false, &nb_minv, &nb);
+    k_update<<<nb, 256, 0, st>>>(d, (int)nb_minv, 1);
+    return hipGetLastError();
+}
+
+hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t st, bool bump_ftran,
+                                 int dslot) {
     const int m = d.m;
     if (bump_ftran && k_ub > 0) k_ftran_bump<<<cdiv(k_ub, 4), 256, 0, st>>>(d, d.aR, d.alS, 1);
-    const int nrt = (int)cdiv(m > 0 ? m : 1, 64);
+    const int nrt = (int)cdiv(m > 0 ? m : 1, ZR_ROWS);
     const int nbt = (int)cdiv(k_ub, 64 * ZR_WAVES);
     {
-        // z partials: 512 B per chunk of ZCHUNK bump positions in LDS (<= 64 KiB,
-        // k <= 4096); larger bumps use a private slice of zpart per row tile
-        const size_t lds = (size_t)cdiv(k_ub, ZCHUNK) * 64 * sizeof(double);
+        // z partials: 256 B per chunk of ZCHUNK bump positions in LDS (<= 64 KiB,
+        // k <= 8192); larger bumps use a private slice of zpart per row tile
+        const size_t lds = (size_t)cdiv(k_ub, ZCHUNK) * ZR_ROWS * sizeof(double);
         // + 1: the snapshot workgroup
-        if (lds <= 64 * 1024 && !d.force_select) k_ftran_zr<true><<<nrt + nbt + 1, 64 * ZR_WAVES, lds, st>>>(d, nrt);
-        else k_ftran_zr<false><<<nrt + nbt + 1, 64 * ZR_WAVES, 0, st>>>(d, nrt);
+        if (lds <= 64 * 1024 && !d.force_select)
+            k_ftran_zr<true><<<nrt + nbt + 1, 64 * ZR_WAVES, lds, st>>>(d, nrt, k_ub);
+        else k_ftran_zr<false><<<nrt + nbt + 1, 64 * ZR_WAVES, 0, st>>>(d, nrt, k_ub);
     }
-    // ratio test + (cases B/D) B^-1 row: one workgroup per 4 bump columns
+    // ratio test + (cases B/D) B^-1 row: one workgroup per 4 bump columns;
+    // phase 2 adds the AR-copy workgroups and defers the rest of the update
+    const int defer = phase == 2;
     {
         const size_t lds = (size_t)k_ub * sizeof(double);
         const int lds_row = lds <= 48 * 1024 && !d.force_select;
-        k_ratio<<<cdiv(k_ub > 0 ? k_ub : 1, 4), 256, lds_row ? lds : 0, st>>>(d, phase, nrt + nbt, lds_row);
+        const unsigned nmain = cdiv(k_ub > 0 ? k_ub : 1, 4);
+        unsigned nar = 0;
+        if (defer && !d.csc) {
+            nar = cdiv(d.n, 256);
+            if (nar > 512) nar = 512;
+        }
+        k_ratio<<<nmain + nar, 256, lds_row ? lds : 0, st>>>(d, phase, nrt + nbt, lds_row, defer, (int)nmain,
+                                                           k_ub, dslot);
     }
-    {
-        const int64_t kk = 2 * (int64_t)(k_ub + 1) * (k_ub + 1);
-        unsigned nb_minv = cdiv(kk, 256);
-        if (nb_minv > 2048) nb_minv = 2048;
-        const int64_t cw = m > d.n ? m : d.n;
-        unsigned nb_copy = cdiv(cw, 256);
-        if (nb_copy > 1024) nb_copy = 1024;
-        k_update<<<nb_minv + nb_copy, 256, 0, st>>>(d, (int)nb_minv, phase);
+    if (!defer) {
+        unsigned nb_minv, nb;
+        update_grid(d, k_ub, true, &nb_minv, &nb);
+        k_update<<<nb, 256, 0, st>>>(d, (int)nb_minv, 0);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStream_t st,
-                            hipEvent_t ev0, hipEvent_t ev1) {
-    (void)ny_ub;
+                            hipEvent_t ev0, hipEvent_t ev1, int dslot) {
     hipError_t e = launch_btran_price(d, k_ub, phase, st, ev0, ev1);
     if (e != hipSuccess) return e;
     const int ntiles = (int)cdiv(d.n, TILE_COLS);
@@ -2148,11 +2525,11 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
         const size_t ldsz = lds > 64 ? lds : 64;  // the timer workgroup reduces in it
         // + the timer workgroup, + the CSC column-scatter workgroup
         const unsigned g = cdiv(k_ub > 0 ? k_ub : 1, 4) + (d.ptimer ? 1 : 0) + (d.csc ? 1 : 0);
-        k_select_ftran<<<g, 256, ldsz, st>>>(d, ntiles);
-        return launch_iteration_tail(d, k_ub, phase, st, false);
+        k_select_ftran<<<g, 256, ldsz, st>>>(d, ntiles, k_ub, ny_ub);
+        return launch_iteration_tail(d, k_ub, phase, st, false, dslot);
     }
     k_select<<<1, 1024, 0, st>>>(d, ntiles);
-    return launch_iteration_tail(d, k_ub, phase, st, true);
+    return launch_iteration_tail(d, k_ub, phase, st, true, dslot);
 }
 
 hipError_t launch_iteration_head(const Dev& d, int k_ub, int ny_ub, int phase, int rank,

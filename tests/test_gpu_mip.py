@@ -32,12 +32,20 @@ def test_reference_mips_gpu(gpu, rec, path):
 
 
 def test_mip_refuses_sensitivity_and_infeasible(gpu):
+    """R/class.R:615-618: "not optimal" is checked first, then integer columns."""
     from easylp_amd import Problem
     from easylp_amd._lib import ElpError
     with Problem(1, 1) as p:
         p.load_dense(np.array([[2.0]]), [3], [1.0], [1.0], [0.0], [5.0])
         p.set_int([1])
         assert p.solve() == 2
+        with pytest.raises(ElpError, match="not optimal"):
+            p.sensitivity()
+    with Problem(1, 1) as p:
+        p.load_dense(np.array([[2.0]]), [1], [3.0], [1.0], [0.0], [5.0], maximize=True)
+        p.set_int([1])
+        assert p.solve() == 0
+        assert p.solution(0).x[0] == 1.0
         with pytest.raises(ElpError, match="integer/binary"):
             p.sensitivity()
 
