@@ -48,6 +48,12 @@ def parse():
                     help="also time the 10000x500000 column-sharded config (SURVEY config 4)")
     ap.add_argument("--c4-steps", type=int, default=300)
     ap.add_argument("--c4-warmup", type=int, default=100)
+    ap.add_argument("--sparse", type=int, default=1,
+                    help="also time the CSC path on a sparse LP (BASELINE config 5)")
+    ap.add_argument("--sparse-m", type=int, default=1000)
+    ap.add_argument("--sparse-n", type=int, default=10000)
+    ap.add_argument("--sparse-steps", type=int, default=1000)
+    ap.add_argument("--sparse-cpu-iters", type=int, default=200)
     return ap.parse_args()
 
 
@@ -121,6 +127,71 @@ def c4_rate(args, lib, world, rank, local, barrier, dist):
             "value": it / el if el > 0 else None, "unit": "iterations/s", "iterations_timed": it,
             "warmup": args.c4_warmup, "ms_per_step": 1e3 * el / max(it, 1),
             "bump_dim": s1["bump_dim"], "y_rows": s1["y_rows"], "load_s": t_load}
+
+
+def sparse_rate(args, local, with_cpu):
+    """BASELINE config 5 on the CSC path: a seeded sparse LP of Netlib-like shape
+    (easylp_amd.synth.sparse_packing, 5 nonzeros per column) plus the Klee-Minty
+    cube n=12 (4095 Dantzig pivots).  Same step definition; the CPU leg is the
+    oracle in its CSC order (price_mode 1) over a bounded window."""
+    import numpy as np
+    from easylp_amd import Problem
+    from easylp_amd.synth import dense_of, sparse_packing
+    m, n = args.sparse_m, args.sparse_n
+    cp, ri, v, b, c = sparse_packing(args.seed, m, n, 5)
+    dirs = np.ones(m, np.int32)
+    p = Problem(m, n, device=local)
+    p.load_csc(cp, ri, v, dirs, b, c, maximize=True)
+    p.iterate(args.warmup)
+    s0 = p.stats()
+    t0 = time.perf_counter()
+    p.iterate(args.sparse_steps)
+    el = time.perf_counter() - t0
+    s1 = p.stats()
+    st = p.solve()
+    s2 = p.stats()
+    sol = p.solution(st)
+    p.close()
+    it = s1["iterations"] - s0["iterations"]
+    out = {"workload": "sparse LP m=%d n=%d nnz=%d (CSC, BASELINE configs[4])" % (m, n, int(cp[-1])),
+           "value": it / el if el > 0 else None, "unit": "iterations/s", "iterations_timed": it,
+           "warmup": args.warmup, "ms_per_step": 1e3 * el / max(it, 1),
+           "time_to_optimal_s": s2["seconds_loop"], "status": st, "objective": sol.objval,
+           "iterations_to_optimal": s2["iterations"], "bump_dim": s2["bump_dim"]}
+    # Klee-Minty cube (degenerate-path case): time to optimal on the GPU
+    km = 12
+    rows, cols, vals = [], [], []
+    for i in range(km):
+        for j in range(i + 1):
+            rows.append(i)
+            cols.append(j)
+            vals.append(1.0 if i == j else 2.0 ** (i - j + 1))
+    import scipy.sparse as sp
+    K = sp.csc_matrix((vals, (rows, cols)), shape=(km, km))
+    kb = np.array([5.0 ** (i + 1) for i in range(km)])
+    kc = np.array([2.0 ** (km - 1 - j) for j in range(km)])
+    with Problem(km, km, device=local) as pk:
+        pk.load_csc(K.indptr, K.indices, K.data, np.ones(km, np.int32), kb, kc, maximize=True)
+        kst = pk.solve()
+        ks = pk.stats()
+        kobj = pk.solution(kst).objval
+    out["klee_minty"] = {"n": km, "iterations": ks["iterations"], "seconds": ks["seconds_loop"],
+                         "objective": kobj, "expected": 5.0 ** km}
+    if with_cpu:
+        from oracle import solve_dense
+        A = dense_of(cp, ri, v, m, n)
+        w = args.warmup
+        r = solve_dense(A, dirs, b, c, maximize=True, price_mode=1,
+                        max_iter=w + args.sparse_cpu_iters, t_mark_iter=w)
+        cit = r.stats["iterations"] - w
+        out["cpu_baseline"] = {"value": cit / r.stats["seconds_at_mark"], "unit": "iterations/s",
+                               "cores": 1, "kind": "port",
+                               "sample": "oracle/ (C, -O3, 1 thread, CSC order) iterations [%d, %d)" % (w, w + cit)}
+        t0 = time.perf_counter()
+        rk = solve_dense(K.toarray(), np.ones(km, np.int32), kb, kc, maximize=True, price_mode=1)
+        out["klee_minty"]["cpu_seconds"] = time.perf_counter() - t0
+        out["klee_minty"]["cpu_iterations"] = rk.stats["iterations"]
+    return out
 
 
 def main():
@@ -206,6 +277,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args)
 
+    sparse = None
+    if args.sparse and world == 1:
+        sparse = sparse_rate(args, local, rank == 0 and not args.no_cpu)
+
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -243,6 +318,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "scaling_config": c4,
+            "sparse_config": sparse,
         }
         print(json.dumps(line), flush=True)
     p.close()

@@ -106,6 +106,7 @@ typedef struct {
     int64_t* perm;
     double tol_inf;
     int64_t nnz;      /* nonzeros of A (price_mode 1 byte count)          */
+    int64_t *cp, *ri; /* price_mode 1: nonzero pattern of A by column      */
     int64_t gj_count; /* refactors that needed a fresh Gauss-Jordan */
     int refactor_mode;
 } orc_t;
@@ -383,8 +384,8 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
             for (int64_t j = 0; j < n; ++j) {
                 const double* col = &s->A[(size_t)j * (size_t)m];
                 double acc = 0.0;
-                for (int64_t i = 0; i < m; ++i)
-                    if (col[i] != 0.0) acc = fma(col[i], s->y[i], acc);
+                for (int64_t t = s->cp[j]; t < s->cp[j + 1]; ++t)  /* ascending rows */
+                    acc = fma(col[s->ri[t]], s->y[s->ri[t]], acc);
                 s->part[j] = acc;
             }
             st->price_bytes += 12.0 * (double)s->nnz + 17.0 * (double)n;
@@ -873,6 +874,13 @@ int orc_solve_dense_sens(int64_t m, int64_t n, const double* A, const int32_t* d
     s->A = A;
     s->nnz = 0;
     for (size_t t = 0; t < (size_t)m * (size_t)n; ++t) s->nnz += A[t] != 0.0;
+    s->cp = ialloc((size_t)n + 1);
+    s->ri = ialloc((size_t)s->nnz);
+    for (int64_t j = 0, t = 0; j < n; ++j) {
+        for (int64_t i = 0; i < m; ++i)
+            if (A[(size_t)j * (size_t)m + (size_t)i] != 0.0) s->ri[t++] = i;
+        s->cp[j + 1] = t;
+    }
     s->refactor_mode = ctl.refactor_mode;
     const int64_t nv = s->nv, mm = m > 0 ? m : 1;
     s->b = dalloc((size_t)mm);
@@ -1042,7 +1050,7 @@ int orc_solve_dense_sens(int64_t m, int64_t n, const double* A, const int32_t* d
     free(s->xr); free(s->xs); free(s->Minv); free(s->Yl); free(s->ypos); free(s->AR);
     free(s->y); free(s->t); free(s->yR); free(s->yy); free(s->acol); free(s->aR);
     free(s->alS); free(s->alU); free(s->z); free(s->v); free(s->tmp); free(s->part);
-    free(s->used); free(s->perm);
+    free(s->used); free(s->perm); free(s->cp); free(s->ri);
     return status;
 }
 
