@@ -48,6 +48,10 @@ def parse():
                     help="also time the 10000x500000 column-sharded config (SURVEY config 4)")
     ap.add_argument("--c4-steps", type=int, default=300)
     ap.add_argument("--c4-warmup", type=int, default=100)
+    ap.add_argument("--p2p", type=int, default=1,
+                    help="N>1: per-iteration min-loc through the xGMI mailbox (0: RCCL all-gather)")
+    ap.add_argument("--force-sharded", action="store_true",
+                    help="N=1: run the sharded pipeline on a 1-rank RCCL communicator (overhead probe)")
     ap.add_argument("--sparse", type=int, default=1,
                     help="also time the CSC path on a sparse LP (BASELINE config 5)")
     ap.add_argument("--sparse-m", type=int, default=1000)
@@ -102,9 +106,11 @@ def c4_rate(args, lib, world, rank, local, barrier, dist):
     from easylp_amd import Problem
     m, n = 10000, 500000
     p = Problem(m, n, device=local)
-    if world > 1:
+    if world > 1 or args.force_sharded:
         from easylp_amd.dist import share_unique_id
         p.comm_init(share_unique_id(lib, rank), world, rank)
+        if args.p2p:
+            p.comm_enable_p2p()
     t_load = time.perf_counter()
     p.load_generated(args.seed)
     barrier()
@@ -207,6 +213,11 @@ def main():
 
     if world > 1:
         dist.init_process_group("gloo", init_method="env://")
+    elif args.force_sharded:
+        os.environ["ELP_RCCL_SINGLE"] = "1"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("gloo", init_method="env://", rank=0, world_size=1)
     torch.cuda.set_device(local)
 
     from easylp_amd import Problem
@@ -215,9 +226,11 @@ def main():
     lib = load()
     verbose = ELP_PROFILE_PRICE if args.profile_price else 0
     p = Problem(args.m, args.n, device=local, verbose=verbose)
-    if world > 1:
+    if world > 1 or args.force_sharded:
         from easylp_amd.dist import share_unique_id
         p.comm_init(share_unique_id(lib, rank), world, rank)
+        if args.p2p:
+            p.comm_enable_p2p()
 
     p.load_generated(args.seed)
 
@@ -298,7 +311,8 @@ def main():
             "config": {
                 "workload": "dense random LP m=%d n=%d (BASELINE configs[2])" % (args.m, args.n),
                 "m": args.m, "n": args.n, "seed": args.seed,
-                "parallelism": "column-shard x%d" % world if world > 1 else "single GPU",
+                "parallelism": ("column-shard x%d, %s min-loc" % (world, "xGMI mailbox" if args.p2p else "RCCL all-gather")
+                                if world > 1 or args.force_sharded else "single GPU"),
                 "iterations_timed": iters,
             },
             "time_to_optimal_s": tto,

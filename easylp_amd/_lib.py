@@ -22,7 +22,7 @@ EXPORTS = (
     "elp_default_control", "elp_create", "elp_load_dense", "elp_load_dense_device",
     "elp_load_generated", "elp_load_csc", "elp_set_int", "elp_solve", "elp_iterate", "elp_get_solution",
     "elp_get_stats", "elp_sensitivity",
-    "elp_set_trace", "elp_get_trace", "elp_comm_unique_id", "elp_comm_init", "elp_comm_init_host",
+    "elp_set_trace", "elp_get_trace", "elp_comm_unique_id", "elp_comm_init", "elp_comm_init_host", "elp_comm_enable_p2p",
     "elp_destroy", "elp_last_error", "elp_abi_version",
 )
 
@@ -118,6 +118,7 @@ def load(path: str | None = None):
     lib.elp_comm_unique_id.argtypes = [vp]
     lib.elp_comm_init.argtypes = [vp, vp, i32, i32]
     lib.elp_comm_init_host.argtypes = [vp, i32, i32, ALLGATHER_FN, ALLREDUCE_FN, BCAST_FN, vp]
+    lib.elp_comm_enable_p2p.argtypes = [vp]
     lib.elp_destroy.argtypes = [vp]
     lib.elp_destroy.restype = None
     lib.elp_last_error.restype = ctypes.c_char_p
@@ -126,7 +127,7 @@ def load(path: str | None = None):
                  "elp_load_csc", "elp_sensitivity", "elp_set_int",
                  "elp_solve", "elp_iterate", "elp_get_solution", "elp_get_stats",
                  "elp_set_trace", "elp_get_trace", "elp_comm_unique_id", "elp_comm_init",
-                 "elp_comm_init_host"):
+                 "elp_comm_init_host", "elp_comm_enable_p2p"):
         getattr(lib, name).restype = ctypes.c_int
     _lib = lib
     return lib

@@ -81,6 +81,7 @@ struct elp_handle {
     int64_t ar_rows = 0;         // AR capacity in rows (grown at polls)
     bool replicated = false;     // sharded, every rank holds all of A (Dev::Afull)
     bool csc = false;            // A given in CSC (elp_load_csc)
+    int64_t mb_epoch = 0;        // loads so far (xGMI mailbox sequence epoch)
     // ELP_STAMPS debug: k_ratio phase stamps, summed over polled chunks
     std::vector<double> stamp_sum;
     int64_t stamp_n = 0;
@@ -175,6 +176,10 @@ static int alloc_all(elp_handle* h) {
     d.infinity = h->ctl.infinity;
     d.ptimer = (h->ctl.verbose & ELP_PROFILE_PRICE) ? 1 : 0;
     d.csc = h->csc ? 1 : 0;
+    d.p2p = h->comm.p2p;
+    d.rank = h->comm.rank;
+    d.mbox = (MboxRec*)h->comm.mbox;
+    d.mpeers = (MboxRec* const*)h->comm.dpeers;
     d.force_select = std::getenv("ELP_FORCE_SELECT") ? 1 : 0;  // test hook
     const size_t nv = (size_t)(n + 2 * m);
     hipError_t e = hipSuccess;
@@ -391,6 +396,7 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
     c.trace_cap = h->trace_cap;
     c.unb_var = -1;
     c.qcol_var = -1;
+    c.mb_epoch = ++h->mb_epoch;
     *h->hctl = c;
     HIPCHK(hipMemcpyAsync(d.ctl, h->hctl, sizeof(DevCtl), hipMemcpyHostToDevice, h->st));
     if (d.qcol) HIPCHK(hipMemsetAsync(d.qcol, 0, (size_t)std::max<int64_t>(m, 1) * sizeof(double), h->st));
@@ -464,6 +470,8 @@ static int prep_load(elp_handle* h, bool csc = false) {
     const double abytes = 8.0 * (double)h->m * (double)h->n;
     h->replicated = h->comm.kind != 0 &&
                     (h->ctl.replicate == 1 || (h->ctl.replicate == 0 && abytes <= 64.0 * (1ull << 30)));
+    if (h->comm.p2p && !h->replicated)
+        return fail(ELP_E_UNSUPPORTED, "xGMI mailbox exchange needs A replicated on every rank");
     return alloc_all(h);
 }
 
@@ -714,7 +722,7 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             const int kub = (int)std::min<int64_t>(h->m, (int64_t)k0 + t);
             const int nyub = (int)std::min<int64_t>(h->m, (int64_t)ny0 + t);
             hipEvent_t e0 = prof ? h->ev[2 * t] : nullptr, e1 = prof ? h->ev[2 * t + 1] : nullptr;
-            if (h->comm.kind == 0) {
+            if (h->comm.kind == 0 || h->comm.p2p) {  // (p2p: min-loc inside the select kernel)
                 HIPCHK(launch_iteration(h->d, kub, nyub, h->phase, h->st, e0, e1, t));
             } else {
                 // sharded: local min-loc -> all-gather -> global min-loc.  Replicated
@@ -768,6 +776,7 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
         h->dbg_wait += now_s() - t_enq1;
         h->stats.host_polls++;
         const int32_t s = c->status;
+        if (s == ST_COMMFAIL) return fail(ELP_E_COMM, "xGMI mailbox: a peer's record did not arrive within 2 s");
         if (prof && s == ST_RUN) {  // every launch of the chunk did work
             for (int t = 0; t < chunk; ++t) {
                 float ms = 0.f;
@@ -1254,6 +1263,16 @@ extern "C" int elp_comm_init(elp_handle* h, const uint8_t id[128], int32_t world
     HIPCHK(hipSetDevice(h->dev));
     const int rc = h->comm.init_rccl(id, world_size, rank);
     return rc ? fail(rc, "RCCL communicator init failed") : 0;
+}
+
+extern "C" int elp_comm_enable_p2p(elp_handle* h) {
+    if (!h) return fail(ELP_E_ARG, "elp_comm_enable_p2p: NULL handle");
+    if (h->loaded) return fail(ELP_E_STATE, "elp_comm_enable_p2p: call before elp_load_*");
+    if (h->comm.kind == 0) return 0;  // one rank: nothing to exchange
+    if (h->comm.world > 64) return fail(ELP_E_UNSUPPORTED, "elp_comm_enable_p2p: more than 64 ranks");
+    HIPCHK(hipSetDevice(h->dev));
+    const int rc = h->comm.enable_p2p(sizeof(MboxRec), h->st);
+    return rc ? fail(rc, "elp_comm_enable_p2p: mailbox allocation / IPC exchange failed") : 0;
 }
 
 extern "C" int elp_comm_init_host(elp_handle* h, int32_t world_size, int32_t rank,

@@ -25,6 +25,14 @@ struct Comm {
     elp_host_bcast_fn h_bcast = nullptr;
     void* h_user = nullptr;
     std::vector<unsigned char> stage;  // host staging for the callback transport
+    // xGMI mailbox (enable_p2p): every iteration each rank writes its min-loc
+    // record straight into every peer's mailbox (2 parities x world records,
+    // uncached device memory shared by IPC) -- no collective launch per iteration
+    void* mbox = nullptr;              // this rank's mailbox
+    void** dpeers = nullptr;           // device array: every rank's mailbox, mapped here
+    std::vector<void*> opened;         // IPC-opened peer mailboxes
+    int p2p = 0;
+    int enable_p2p(size_t rec_bytes, hipStream_t st);
 
     static int unique_id(uint8_t id[128]);
     int init_rccl(const uint8_t id[128], int world_size, int rank_);

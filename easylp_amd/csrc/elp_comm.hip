@@ -47,7 +47,51 @@ int Comm::init_host(int world_size, int rank_, elp_host_allgather_fn ag, elp_hos
     return 0;
 }
 
+int Comm::enable_p2p(size_t rec_bytes, hipStream_t st) {
+    if (kind == 0) return ELP_E_STATE;
+    if (p2p) return 0;
+    const size_t bytes = 2 * (size_t)world * rec_bytes;
+    // uncached: a peer's remote store and this rank's polling load meet in memory
+    if (hipExtMallocWithFlags(&mbox, bytes, hipDeviceMallocUncached) != hipSuccess) return ELP_E_NOMEM;
+    if (hipMemset(mbox, 0, bytes) != hipSuccess) return ELP_E_HIP;
+    hipIpcMemHandle_t mine;
+    if (hipIpcGetMemHandle(&mine, mbox) != hipSuccess) return ELP_E_HIP;
+    static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
+    unsigned char* dstage = nullptr;
+    if (hipMalloc((void**)&dstage, 64 * ((size_t)world + 1)) != hipSuccess) return ELP_E_NOMEM;
+    std::vector<unsigned char> all(64 * (size_t)world);
+    int rc = hipMemcpy(dstage + 64 * world, &mine, 64, hipMemcpyHostToDevice) == hipSuccess ? 0 : ELP_E_HIP;
+    if (!rc) rc = allgather(dstage + 64 * world, dstage, 64, st);
+    if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = ELP_E_HIP;
+    if (!rc && hipMemcpy(all.data(), dstage, all.size(), hipMemcpyDeviceToHost) != hipSuccess) rc = ELP_E_HIP;
+    (void)hipFree(dstage);
+    if (rc) return rc;
+    std::vector<void*> ptrs((size_t)world, nullptr);
+    for (int r = 0; r < world; ++r) {
+        if (r == rank) {
+            ptrs[r] = mbox;
+            continue;
+        }
+        hipIpcMemHandle_t hd;
+        std::memcpy(&hd, all.data() + 64 * (size_t)r, 64);
+        if (hipIpcOpenMemHandle(&ptrs[r], hd, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return ELP_E_COMM;
+        opened.push_back(ptrs[r]);
+    }
+    if (hipMalloc((void**)&dpeers, sizeof(void*) * (size_t)world) != hipSuccess) return ELP_E_NOMEM;
+    if (hipMemcpy(dpeers, ptrs.data(), sizeof(void*) * (size_t)world, hipMemcpyHostToDevice) != hipSuccess)
+        return ELP_E_HIP;
+    p2p = 1;
+    return 0;
+}
+
 void Comm::destroy() {
+    for (void* p : opened) (void)hipIpcCloseMemHandle(p);
+    opened.clear();
+    if (dpeers) (void)hipFree(dpeers);
+    if (mbox) (void)hipFree(mbox);
+    dpeers = nullptr;
+    mbox = nullptr;
+    p2p = 0;
     if (kind == 1 && nccl) ncclCommDestroy((ncclComm_t)nccl);
     nccl = nullptr;
     kind = 0;

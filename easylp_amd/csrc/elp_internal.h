@@ -20,6 +20,7 @@ enum : int32_t {
     ST_P1DONE = 5,     // phase-1 artificial sum within tolerance at loop top
     ST_NUMFAIL = 6,
     ST_STOP = 7,       // elp_iterate budget reached at loop top
+    ST_COMMFAIL = 8,   // xGMI mailbox: a peer's record did not arrive in time
 };
 
 // pivot cases (oracle/elp_oracle.c "case A".."case E")
@@ -76,6 +77,7 @@ struct DevCtl {
     // select kernel marks it applied; the host applies a plan still pending at
     // a poll (k_update) -- see DESIGN.md "Iteration pipeline"
     int32_t plan_seq, applied_seq;
+    int64_t mb_epoch;  // xGMI mailbox: loads so far (seq = epoch << 40 | iteration + 1)
 };
 
 // Harris pass-2 candidate (a superset of the global candidates: exact ratio
@@ -96,6 +98,12 @@ struct Cand {
 struct CandX {
     Cand c;
     double lb, ub, x, cost;
+};
+
+// one mailbox slot: a rank's record for iteration seq - 1 (seq written last)
+struct MboxRec {
+    CandX x;
+    int64_t seq;
 };
 
 // Everything a kernel needs, passed by value (pointers into device memory).
@@ -155,6 +163,11 @@ struct Dev {
     double* qcol;
     // debug (ELP_STAMPS): s_memrealtime stamps of k_ratio, 16 per chunk slot
     unsigned long long* dstamp;
+    // xGMI mailbox exchange (Comm::enable_p2p): the select kernel publishes this
+    // rank's best candidate into every peer's slot and waits for all of them
+    MboxRec* mbox;          // this rank's mailbox [2 parities][world]
+    MboxRec* const* mpeers; // every rank's mailbox as mapped in this process
+    int32_t p2p, rank;
 };
 
 // ---------------------------------------------------------------- launches

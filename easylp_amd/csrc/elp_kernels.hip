@@ -674,6 +674,83 @@ DEV void price_timer_sum(const Dev& d, int ntiles, unsigned long long* red) {
 }
 
 // ============================================================== select
+constexpr int MAX_P2P = 64;  // ranks a mailbox exchange supports
+
+// xGMI mailbox min-loc (Dev::p2p, column-sharded with A replicated): workgroup
+// 0 publishes this rank's best candidate -- with the column's (lb, ub, x, cost)
+// when it is one of this shard's structurals -- into slot [parity][rank] of
+// every rank's mailbox (fields, system-scope fence, then the sequence word);
+// every workgroup waits until all slots of this iteration carry its sequence
+// number and reduces them with the candidate total order, so all ranks agree.
+// Returns false (status ST_COMMFAIL) if a peer stays silent for 2 s.
+DEV bool p2p_exchange(const Dev& d, Cand& best, int bland, int64_t iter, int64_t epoch, CandX* s_rec,
+                      int* s_fail) {
+    const int P = d.world;
+    const int par = (int)(iter & 1);
+    const int64_t want = (epoch << 40) | (iter + 1);
+    if (threadIdx.x == 0) *s_fail = 0;
+    if (blockIdx.x == 0 && (int)threadIdx.x < P) {  // thread t writes our slot in rank t's mailbox
+        CandX x;
+        x.c = best;
+        x.lb = x.ub = x.x = x.cost = 0.0;
+        const int ql = best.j >= 0 && best.j < d.N ? loc_of(d, (int)best.j) : -1;
+        if (ql >= 0) {
+            x.lb = d.lb[ql];
+            x.ub = d.ub[ql];
+            x.x = d.xval[ql];
+            x.cost = d.cost[ql];
+        }
+        MboxRec* r = d.mpeers[threadIdx.x] + par * P + d.rank;
+        r->x = x;
+        __threadfence_system();
+        __hip_atomic_store(&r->seq, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < P) {  // thread t waits for rank t's record, then stages it in LDS
+        MboxRec* r = d.mbox + par * P + threadIdx.x;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        bool ok = true;
+        while (__hip_atomic_load(&r->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != want) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
+                ok = false;
+                break;
+            }
+        }
+        if (!ok) {
+            atomicOr(s_fail, 1);
+        } else {
+            __atomic_thread_fence(__ATOMIC_ACQUIRE);
+            CandX x;
+            x.c.score = __hip_atomic_load(&r->x.c.score, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            x.c.d = __hip_atomic_load(&r->x.c.d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            x.c.j = __hip_atomic_load(&r->x.c.j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            x.lb = __hip_atomic_load(&r->x.lb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            x.ub = __hip_atomic_load(&r->x.ub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            x.x = __hip_atomic_load(&r->x.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            x.cost = __hip_atomic_load(&r->x.cost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            s_rec[threadIdx.x] = x;
+        }
+    }
+    __syncthreads();
+    if (*s_fail) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) d.ctl->status = ST_COMMFAIL;
+        return false;
+    }
+    int win = 0;
+    for (int r = 1; r < P; ++r)
+        if (cand_better(s_rec[r].c, s_rec[win].c, bland)) win = r;
+    best = s_rec[win].c;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && best.j >= 0 && best.j < d.N) {
+        const int m = d.m;  // the column's scalars for k_ratio (sharded: read from pkt)
+        d.pkt[m] = s_rec[win].lb;
+        d.pkt[m + 1] = s_rec[win].ub;
+        d.pkt[m + 2] = s_rec[win].x;
+        d.pkt[m + 3] = s_rec[win].cost;
+    }
+    return true;
+}
+
 // Min-loc over this shard's tile candidates and the (replicated) slack
 // candidates.  One GPU: decide q and form a_R.  Sharded: write the local best
 // to cand_xchg[rank] for the all-gather (k_select_global decides).
@@ -739,7 +816,12 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles) {
     DevCtl* c = d.ctl;
     if (threadIdx.x == 0) c->applied_seq = c->plan_seq;  // the pricing launch applied it
     if (c->status != ST_RUN) return;
-    const Cand best = local_best(d, ntiles, red);
+    Cand best = local_best(d, ntiles, red);
+    if (d.p2p) {  // column-sharded: global min-loc over the xGMI mailbox
+        __shared__ CandX s_rec[MAX_P2P];
+        __shared__ int s_fail;
+        if (!p2p_exchange(d, best, c->bland, c->iter, c->mb_epoch, s_rec, &s_fail)) return;
+    }
     if (best.j < 0) {
         if (threadIdx.x == 0) c->status = ST_PHASE_OPT;
         return;
@@ -755,8 +837,8 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles) {
             return;
         }
     }
-    // one GPU: the full column is read in place by k_ftran_zr / k_update
-    gather_aR(d, q, q < d.N ? d.A + (size_t)(q - d.col0) * (size_t)d.m : nullptr);
+    // the full column is read in place by k_ftran_zr / k_update
+    gather_aR(d, q, q < d.N ? qcolumn(d, q) : nullptr);
 }
 
 // One GPU, fused select + FTRAN on the bump: every workgroup reduces the tile and
@@ -864,6 +946,11 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_u
         }
     }
     best = block_best<256>(best, bland, red);
+    if (d.p2p) {  // column-sharded: global min-loc over the xGMI mailbox
+        __shared__ CandX s_rec[MAX_P2P];
+        __shared__ int s_fail;
+        if (!p2p_exchange(d, best, bland, c->iter, c->mb_epoch, s_rec, &s_fail)) return;
+    }
     if (best.j < 0) {
         if (blockIdx.x == 0 && tid == 0) c->status = ST_PHASE_OPT;
         return;
@@ -881,7 +968,7 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_u
     if (q < d.N && d.csc) {
         scatter_aR_csc(d, q, aRs, k);
     } else if (q < d.N) {
-        const double* col = d.A + (size_t)(q - d.col0) * (size_t)d.m;
+        const double* col = qcolumn(d, q);
         if (pfr) {
             double g[PFR];
 #pragma unroll

@@ -115,6 +115,10 @@ class Problem:
                                            transport.c_allgather, transport.c_allreduce,
                                            transport.c_bcast, None), "elp_comm_init_host")
 
+    def comm_enable_p2p(self) -> None:
+        """xGMI mailbox min-loc (no collective launch per iteration); after comm_init*."""
+        check(self._lib.elp_comm_enable_p2p(self._h), "elp_comm_enable_p2p")
+
     def load_dense(self, A, dirs, rhs, obj, lo=None, up=None, maximize=False) -> None:
         m, n = self.m, self.n
         A = np.asfortranarray(np.asarray(A, dtype=np.float64).reshape(m, n))

@@ -190,6 +190,14 @@ int elp_get_trace(elp_handle* h, int64_t* pairs, int64_t capacity, int64_t* coun
 int elp_comm_unique_id(uint8_t id[128]);
 int elp_comm_init(elp_handle* h, const uint8_t id[128], int32_t world_size, int32_t rank);
 
+/* Per-iteration min-loc over xGMI without a collective launch: every rank
+ * allocates a small uncached mailbox, the IPC handles are exchanged once over
+ * the communicator, and from then on the select kernel writes its candidate
+ * record straight into every peer's mailbox and waits for theirs (2 s timeout
+ * -> ELP_E_COMM).  Call after elp_comm_init* and before elp_load_*; needs A
+ * replicated (elp_control.replicate).  No-op on one rank. */
+int elp_comm_enable_p2p(elp_handle* h);
+
 /* Same sharded algorithm over caller-provided host transports instead of RCCL
  * (every rank may then share one GPU; used by the multi-rank tests).  Buffers
  * are host memory; return 0 on success.  allgather: recv holds world*bytes.

@@ -8,10 +8,12 @@ if ROOT not in sys.path:
 
 
 def _init(rank, world, port):
+    from datetime import timedelta
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a failing rank must not leave its peers waiting for gloo's 30-minute default
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=120))
     return dist
 
 
@@ -51,9 +53,10 @@ def transport_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def sharded_solve_worker(rank, world, port, q, cases, replicate=0):
+def sharded_solve_worker(rank, world, port, q, cases, replicate=0, p2p=False):
     """GPU: every rank solves the same LPs on one shared GPU with the host transport.
-    replicate: elp_control.replicate (1 every rank holds all of A, 2 shards only)."""
+    replicate: elp_control.replicate (1 every rank holds all of A, 2 shards only);
+    p2p: the per-iteration min-loc over the IPC mailbox instead of the transport."""
     import numpy as np
     dist = _init(rank, world, port)
     import easylp_amd
@@ -66,12 +69,16 @@ def sharded_solve_worker(rank, world, port, q, cases, replicate=0):
             p = easylp_amd.Problem(m, n, replicate=replicate)
             p.set_trace(200000)
             p.comm_init_host(t)
+            if p2p:
+                p.comm_enable_p2p()
             p.load_generated(case["seed"])
         else:
             A, dirs, rhs, obj, lo, up, mx = case["lp"]
             p = easylp_amd.Problem(A.shape[0], A.shape[1], replicate=replicate)
             p.set_trace(200000)
             p.comm_init_host(t)
+            if p2p:
+                p.comm_enable_p2p()
             p.load_dense(A, dirs, rhs, obj, lo, up, mx)
         st = p.solve()
         sol = p.solution(st)

@@ -13,7 +13,7 @@ HEADER = os.path.join(ROOT, "include", "easylp_hip.h")
 
 def declared():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"\b(elp_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(elp_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_header_declares_expected_surface():

@@ -34,23 +34,27 @@ def _cases():
     ]
 
 
-@pytest.mark.parametrize("world,replicate", [(2, 1), (3, 1), (2, 2), (3, 2)])
-def test_sharded_matches_oracle(world, replicate):
+@pytest.mark.parametrize("world,replicate,p2p", [(2, 1, False), (3, 1, False), (2, 2, False),
+                                                 (3, 2, False), (2, 1, True), (3, 1, True)])
+def test_sharded_matches_oracle(world, replicate, p2p):
     """replicate 1: every rank holds all of A and only the min-loc record is
-    exchanged; 2: column shards only, the entering column is all-reduced."""
+    exchanged; 2: column shards only, the entering column is all-reduced.
+    p2p: the min-loc records travel through the IPC mailbox (the select kernel
+    writes into every peer's memory and waits for theirs) -- here all ranks
+    share one GPU, on the 8-GPU node the stores go over xGMI."""
     from dist_worker import sharded_solve_worker
     from oracle import generate_dense, solve_dense as orc
     cases = _cases()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=sharded_solve_worker, args=(r, world, port, q, cases, replicate))
+    procs = [ctx.Process(target=sharded_solve_worker, args=(r, world, port, q, cases, replicate, p2p))
              for r in range(world)]
     for p in procs:
         p.start()
     res = {}
     for _ in range(world):
-        r, results, errors = q.get(timeout=600)
+        r, results, errors = q.get(timeout=240)
         assert errors == 0
         res[r] = results
     for p in procs:
@@ -71,6 +75,35 @@ def test_sharded_matches_oracle(world, replicate):
             assert g["objval"] == o.objval
             np.testing.assert_array_equal(g["x"], o.x)
             assert g["stats"]["world_size"] == world
+
+
+def test_rccl_single_rank_p2p_mailbox(monkeypatch):
+    """The mailbox exchange on a 1-rank RCCL communicator: the select kernel
+    writes its record into its own mailbox and waits for it."""
+    monkeypatch.setenv("ELP_RCCL_SINGLE", "1")
+    import easylp_amd
+    from easylp_amd._lib import load
+    from oracle import generate_dense, solve_dense as orc
+    import ctypes
+    lib = load()
+    uid = ctypes.create_string_buffer(128)
+    assert lib.elp_comm_unique_id(uid) == 0, lib.elp_last_error()
+    m, n, seed = 250, 1000, 6
+    with easylp_amd.Problem(m, n, replicate=1) as p:
+        p.set_trace(100000)
+        p.comm_init(uid.raw, 1, 0)
+        p.comm_enable_p2p()
+        p.load_generated(seed)
+        st = p.solve()
+        g = p.solution(st)
+        # a second load on the same handle: new mailbox epoch, stale slots ignored
+        p.load_generated(seed)
+        g2 = p.solution(p.solve())
+    A, b, c = generate_dense(seed, m, n)
+    o = orc(A, np.ones(m, np.int32), b, c, maximize=True, trace_cap=100000)
+    assert g.status == o.status == 0
+    np.testing.assert_array_equal(g.trace, o.trace)
+    assert g.objval == o.objval == g2.objval
 
 
 def test_rccl_transport_single_rank(monkeypatch):
