@@ -61,6 +61,19 @@ def parse():
     return ap.parse_args()
 
 
+def enable_p2p(p, rank):
+    """xGMI mailbox for the min-loc; collective and agreed by all ranks, so on
+    failure every rank falls back to the RCCL all-gather together."""
+    from easylp_amd._lib import ElpError
+    try:
+        p.comm_enable_p2p()
+        return True
+    except ElpError as e:
+        if rank == 0:
+            print(f"xGMI mailbox unavailable ({e}); RCCL all-gather min-loc", file=sys.stderr)
+        return False
+
+
 def cpu_baseline(args):
     """The CPU oracle (same algorithm, 1 thread) on a bounded sample of the same LP."""
     import numpy as np
@@ -110,7 +123,7 @@ def c4_rate(args, lib, world, rank, local, barrier, dist):
         from easylp_amd.dist import share_unique_id
         p.comm_init(share_unique_id(lib, rank), world, rank)
         if args.p2p:
-            p.comm_enable_p2p()
+            enable_p2p(p, rank)
     t_load = time.perf_counter()
     p.load_generated(args.seed)
     barrier()
@@ -230,7 +243,7 @@ def main():
         from easylp_amd.dist import share_unique_id
         p.comm_init(share_unique_id(lib, rank), world, rank)
         if args.p2p:
-            p.comm_enable_p2p()
+            args.p2p = int(enable_p2p(p, rank))
 
     p.load_generated(args.seed)
 

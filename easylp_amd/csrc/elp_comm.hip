@@ -47,39 +47,67 @@ int Comm::init_host(int world_size, int rank_, elp_host_allgather_fn ag, elp_hos
     return 0;
 }
 
+// Collective over the communicator: every rank takes every step (the handle
+// all-gather and the final agreement), so a rank that fails to allocate or to
+// map a peer does not strand the others; if any rank failed, none uses p2p.
 int Comm::enable_p2p(size_t rec_bytes, hipStream_t st) {
     if (kind == 0) return ELP_E_STATE;
     if (p2p) return 0;
     const size_t bytes = 2 * (size_t)world * rec_bytes;
-    // uncached: a peer's remote store and this rank's polling load meet in memory
-    if (hipExtMallocWithFlags(&mbox, bytes, hipDeviceMallocUncached) != hipSuccess) return ELP_E_NOMEM;
-    if (hipMemset(mbox, 0, bytes) != hipSuccess) return ELP_E_HIP;
+    int ok = 1;
     hipIpcMemHandle_t mine;
-    if (hipIpcGetMemHandle(&mine, mbox) != hipSuccess) return ELP_E_HIP;
+    std::memset(&mine, 0, sizeof(mine));
+    // uncached: a peer's remote store and this rank's polling load meet in memory
+    if (hipExtMallocWithFlags(&mbox, bytes, hipDeviceMallocUncached) != hipSuccess) {
+        mbox = nullptr;
+        ok = 0;
+    }
+    if (ok && hipMemset(mbox, 0, bytes) != hipSuccess) ok = 0;
+    if (ok && hipIpcGetMemHandle(&mine, mbox) != hipSuccess) ok = 0;
     static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
     unsigned char* dstage = nullptr;
-    if (hipMalloc((void**)&dstage, 64 * ((size_t)world + 1)) != hipSuccess) return ELP_E_NOMEM;
+    if (hipMalloc((void**)&dstage, 64 * ((size_t)world + 1) + sizeof(int32_t)) != hipSuccess) return ELP_E_NOMEM;
     std::vector<unsigned char> all(64 * (size_t)world);
     int rc = hipMemcpy(dstage + 64 * world, &mine, 64, hipMemcpyHostToDevice) == hipSuccess ? 0 : ELP_E_HIP;
     if (!rc) rc = allgather(dstage + 64 * world, dstage, 64, st);
     if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = ELP_E_HIP;
     if (!rc && hipMemcpy(all.data(), dstage, all.size(), hipMemcpyDeviceToHost) != hipSuccess) rc = ELP_E_HIP;
-    (void)hipFree(dstage);
-    if (rc) return rc;
     std::vector<void*> ptrs((size_t)world, nullptr);
-    for (int r = 0; r < world; ++r) {
+    for (int r = 0; !rc && ok && r < world; ++r) {
         if (r == rank) {
             ptrs[r] = mbox;
             continue;
         }
         hipIpcMemHandle_t hd;
         std::memcpy(&hd, all.data() + 64 * (size_t)r, 64);
-        if (hipIpcOpenMemHandle(&ptrs[r], hd, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return ELP_E_COMM;
+        if (hipIpcOpenMemHandle(&ptrs[r], hd, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+            ok = 0;
+            break;
+        }
         opened.push_back(ptrs[r]);
     }
-    if (hipMalloc((void**)&dpeers, sizeof(void*) * (size_t)world) != hipSuccess) return ELP_E_NOMEM;
-    if (hipMemcpy(dpeers, ptrs.data(), sizeof(void*) * (size_t)world, hipMemcpyHostToDevice) != hipSuccess)
-        return ELP_E_HIP;
+    if (!rc && ok) {
+        if (hipMalloc((void**)&dpeers, sizeof(void*) * (size_t)world) != hipSuccess) ok = 0;
+        else if (hipMemcpy(dpeers, ptrs.data(), sizeof(void*) * (size_t)world, hipMemcpyHostToDevice) != hipSuccess)
+            ok = 0;
+    }
+    // agreement: max over ranks of "failed"
+    int32_t failed = rc || !ok;
+    int32_t* dflag = reinterpret_cast<int32_t*>(dstage + 64 * ((size_t)world + 1));
+    if (!rc && hipMemcpy(dflag, &failed, sizeof(failed), hipMemcpyHostToDevice) != hipSuccess) rc = ELP_E_HIP;
+    if (!rc) rc = allreduce_max_i32(dflag, 1, st);
+    if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = ELP_E_HIP;
+    if (!rc && hipMemcpy(&failed, dflag, sizeof(failed), hipMemcpyDeviceToHost) != hipSuccess) rc = ELP_E_HIP;
+    (void)hipFree(dstage);
+    if (rc || failed) {
+        for (void* p : opened) (void)hipIpcCloseMemHandle(p);
+        opened.clear();
+        if (dpeers) (void)hipFree(dpeers);
+        if (mbox) (void)hipFree(mbox);
+        dpeers = nullptr;
+        mbox = nullptr;
+        return rc ? rc : ELP_E_COMM;
+    }
     p2p = 1;
     return 0;
 }
