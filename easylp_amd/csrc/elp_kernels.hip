@@ -849,7 +849,13 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_u
     extern __shared__ __attribute__((aligned(16))) double aRs[];  // [k]
     __shared__ Cand red[4];
     DevCtl* c = d.ctl;
-    if (blockIdx.x == 0 && threadIdx.x == 0) c->applied_seq = c->plan_seq;  // applied by k_price
+    // the control block first (vmcnt retires in issue order: the status test
+    // then waits for these loads only, not for the prefetch behind them)
+    const int32_t st0 = c->status;
+    const int bland = c->bland, ny = c->ny, k = c->k;
+    const double dtol = c->tol_dual;
+    const int64_t c_iter = c->iter, c_epoch = c->mb_epoch;
+    const int32_t c_seq = c->plan_seq;
     // Everything that does not depend on the control block or on q goes out
     // first (bounded by the host's k_ub / ny_ub, masked below): the tile
     // candidates, the Y slots' duals and rows, this wave's row of Minv, the R
@@ -884,11 +890,13 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_u
     }
 #pragma unroll
     for (int t = 0; t < PFR; ++t) rl[t] = ld_clamp(d.Rl, tid + 256 * t, k_ub);
+    __builtin_amdgcn_sched_barrier(0);  // all of the above issued before any use
+    if (blockIdx.x == 0 && threadIdx.x == 0) c->applied_seq = c_seq;  // applied by k_price
     // the slacks' status (second round trip: indexed by the Y rows; slots past
     // the real |Y| are stale, so the index is range-checked)
 #pragma unroll
     for (int t = 0; t < PFY; ++t) vs[t] = d.vstat[d.n + ((yl[t] >= 0 && yl[t] < d.m) ? yl[t] : 0)];
-    if (c->status != ST_RUN) {
+    if (st0 != ST_RUN) {
 #pragma unroll
         for (int t = 0; t < PFC; ++t) KEEP(cc[t].score);
 #pragma unroll
@@ -902,8 +910,6 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_u
         for (int t = 0; t < PFR; ++t) KEEP(rl[t]);
         return;
     }
-    const int bland = c->bland, ny = c->ny, k = c->k;
-    const double dtol = c->tol_dual;
     Cand best;
     best.j = -1;
     best.score = 0.0;
@@ -949,7 +955,7 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_u
     if (d.p2p) {  // column-sharded: global min-loc over the xGMI mailbox
         __shared__ CandX s_rec[MAX_P2P];
         __shared__ int s_fail;
-        if (!p2p_exchange(d, best, bland, c->iter, c->mb_epoch, s_rec, &s_fail)) return;
+        if (!p2p_exchange(d, best, bland, c_iter, c_epoch, s_rec, &s_fail)) return;
     }
     if (best.j < 0) {
         if (blockIdx.x == 0 && tid == 0) c->status = ST_PHASE_OPT;
@@ -1226,6 +1232,12 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
     // The first chunk's AS and alpha_S loads go out before the control block
     // arrives: they are in bounds for any k <= k_ub (host upper bound) and the
     // positions past the real k are dropped below.
+    // the control block first (vmcnt retires in issue order: the status test
+    // then waits for these loads only)
+    const DevCtl* c = d.ctl;
+    const int32_t st0 = c->status;
+    const int k = c->k, q = c->q, bland = c->bland;
+    const double sig = c->sig, ptol = c->tol_primal, pivtol = c->tol_pivot;
     const int ch0 = 2 * w + hh;
     double a0[ZCHUNK], s0[ZCHUNK];
     const bool row_tile = (int)blockIdx.x < nrt;
@@ -1249,10 +1261,17 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
         le = d.rlo[i];
         he = d.rhi[i];
     }
-    const DevCtl* c = d.ctl;
-    if (c->status != ST_RUN) return;
-    const int m = d.m, k = c->k, q = c->q, bland = c->bland;
-    const double sig = c->sig, ptol = c->tol_primal, pivtol = c->tol_pivot;
+    __builtin_amdgcn_sched_barrier(0);  // all of the above issued before any use
+    if (st0 != ST_RUN) {
+#pragma unroll
+        for (int t = 0; t < ZCHUNK; ++t) {
+            KEEP(a0[t]);
+            KEEP(s0[t]);
+        }
+        KEEP(xe);
+        return;
+    }
+    const int m = d.m;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         d.ctl->snap_k = k;
         d.ctl->snap_bland = bland;
@@ -1405,8 +1424,17 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         atomicMax(&d.dstamp[dslot * 16 + 8], t);
     }
     RSTAMP(0);
+    // ---- the control block first: vmcnt retires loads in issue order, so the
+    //      status test below then waits for these alone, not for the prefetch
+    DevCtl* c = d.ctl;
+    const int32_t st0 = c->status;
+    const int m = d.m, k = c->snap_k, q = c->q, ny = c->snap_ny, ncand = c->ncand;
+    const double sig = c->sig, dq = c->dq;
+    const int bland = c->snap_bland;
+    const int apos_c = c->snap_apos;
+    const bool lead = blockIdx.x == 0;
     // ---- loads that depend on neither the control block nor the decision go
-    //      out first (bounded by the host's k_ub, masked by the real k below):
+    //      out next (bounded by the host's k_ub, masked by the real k below):
     //      the pass-1 minima, this wave's row of MinvT (B^-1 row, cases B / D)
     //      and its bump row R_col (dual update)
     constexpr int PFB = 4, PFT = 8;
@@ -1424,8 +1452,8 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     }
     // entries of Rl past the real k are stale: range-checked before use
     const int rcol = ld_clamp(d.Rl, main_wg ? col : 0, k_ub);
-    DevCtl* c = d.ctl;
-    if (c->status != ST_RUN) {  // no plan this iteration: k_update must not re-apply one
+    __builtin_amdgcn_sched_barrier(0);  // all of the above issued before any use
+    if (st0 != ST_RUN) {  // no plan this iteration: k_update must not re-apply one
         if (blockIdx.x == 0 && threadIdx.x == 0) c->plan.action = ACT_NONE;
 #pragma unroll
         for (int t = 0; t < PFB; ++t) KEEP(bm[t]);
@@ -1434,10 +1462,6 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         KEEP(rcol);
         return;
     }
-    const int m = d.m, k = c->snap_k, q = c->q, ny = c->snap_ny, ncand = c->ncand;
-    const double sig = c->sig, dq = c->dq;
-    const int bland = c->snap_bland;
-    const bool lead = blockIdx.x == 0;
     RSTAMP(1);
     // workgroup 0 / thread 0 keeps the counters it updates in registers
     // (read once here instead of one dependent round trip per update)
@@ -1511,7 +1535,6 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     for (int t = 0; t < PFQ; ++t) rq[t] = ld_clamp(d.rcand, tid + 256 * t, ncand);
     // case D needs wave_dot(MinvT[apos, :], A[lrow, S]) in every workgroup: wave 0
     // fetches that row now (apos comes with the control block)
-    const int apos_c = c->snap_apos;
     double arow[PFT];
     {
         const double* row = d.MinvT + (size_t)(apos_c >= 0 ? apos_c : 0) * d.ldm;
