@@ -115,7 +115,7 @@ static void free_dev(elp_handle* h) {
                     d.cand,     d.pstamp, d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand,
                     d.pkt, d.objg, d.ract, d.cand_xchg, h->d_flag, d.cS, d.slo, d.shi, d.rlo, d.rhi,
                     (void*)d.cptr, (void*)d.rind, (void*)d.cval, (void*)d.rptr, (void*)d.cind,
-                    (void*)d.rval, d.qcol, d.dstamp};
+                    (void*)d.rval, d.qcol, d.dstamp, d.rowvs, d.yvs};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     h->A_owned = nullptr;
@@ -208,6 +208,8 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.cost, nv));
     A(dalloc(&d.xval, nv));
     A(dalloc(&d.vstat, nv));
+    A(dalloc(&d.rowvs, mm));
+    A(dalloc(&d.yvs, mm));
     A(dalloc(&d.asgn, mm));
     A(dalloc(&d.xr, mm));
     A(dalloc(&d.xs, mm));
@@ -770,6 +772,8 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
                 const unsigned long long* r = &v[(size_t)t * 16];
                 for (int i = 0; i < 11; ++i)
                     if (r[i]) h->stamp_sum[i] += 10.0 * (double)(long long)(r[i] - r[11]);  // ns (100 MHz)
+                for (int i = 13; i < 16; ++i)  // select kernel, relative to its workgroup 0's start
+                    if (r[i] && r[12]) h->stamp_sum[i] += 10.0 * (double)(long long)(r[i] - r[12]);
                 h->stamp_n++;
             }
         }
@@ -1239,7 +1243,9 @@ extern "C" void elp_destroy(elp_handle* h) {
         const char* nm[11] = {"wg0", "ctl", "pass1", "decide", "binv", "dual", "book", "end", "last_start",
                               "main_end", "ar_end"};
         for (int i = 0; i < 11; ++i) std::fprintf(stderr, " %s=%.2f", nm[i], h->stamp_sum[i] / h->stamp_n / 1e3);
-        std::fprintf(stderr, "\n");
+        std::fprintf(stderr, "\nk_select_ftran stamps (us after its workgroup 0 starts): ctl=%.2f decide=%.2f end=%.2f\n",
+                     h->stamp_sum[13] / h->stamp_n / 1e3, h->stamp_sum[14] / h->stamp_n / 1e3,
+                     h->stamp_sum[15] / h->stamp_n / 1e3);
     }
     if (!h) return;
     (void)hipSetDevice(h->dev);

@@ -66,6 +66,11 @@ struct DevCtl {
     // snapshot workgroup): |Y|, rpos / ypos of the entering slack's row, the
     // last Y row and its bump position
     int32_t snap_ny, snap_apos, snap_ypos0, snap_ylast, snap_rposyl, pad4;
+    // ... and the scalars of the pivot bookkeeping, so k_ratio reads them with
+    // the control block: q's (lb, ub, x, cost) and status; the last bump
+    // position's (cost, lo, hi), structural and row
+    double snap_lbq, snap_ubq, snap_xq, snap_cq, snap_csl, snap_slol, snap_shil;
+    int32_t snap_vsq, snap_sllast, snap_rllast, pad7;
     // pricing-kernel timer (Dev::ptimer): s_memrealtime ticks (100 MHz) from the
     // first workgroup's start to the last one's end, summed over timed passes
     unsigned long long price_ticks;
@@ -141,6 +146,9 @@ struct Dev {
     RCand* rcand;            // pass-2 candidates (capacity 2m)
     double *rlo, *rhi;       // per covered row: bounds of the covering unit variable
     int8_t* vstat;
+    int8_t* rowvs;  // per row: the status its slack has whenever it is nonbasic
+                    // (<=: lower, >=: upper, ==: fixed -- a slack never flips)
+    int8_t* yvs;    // per Y slot: rowvs of the slot's row (select reads it in slot order)
     int32_t *cover, *rpos, *Rl, *Sl, *spos, *Yl, *ypos, *perm, *pivstep, *nzlist, *nzcount;
     Cand* cand;
     unsigned long long* pstamp;  // [tile][2] start / end stamps of the last pricing pass

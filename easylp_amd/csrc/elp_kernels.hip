@@ -263,6 +263,7 @@ __global__ void k_init_rows(Dev d, const double* __restrict__ rhs_in) {
     d.asgn[i] = 1.0;
     const double r = bi - d.ract[i];
     const double sl = d.lb[sv], su = d.ub[sv];
+    d.rowvs[i] = sl == su ? VS_FIXED : sl > -HUGE_VAL ? VS_LOWER : VS_UPPER;
     if (r >= sl && r <= su) {
         d.vstat[sv] = VS_BASIC;
         d.cover[i] = svg;
@@ -312,6 +313,7 @@ __global__ void __launch_bounds__(1024) k_init_Y(Dev d) {
         if (f) {
             d.Yl[off + before] = i;
             d.ypos[i] = off + before;
+            d.yvs[off + before] = d.rowvs[i];
         }
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -674,6 +676,9 @@ DEV void price_timer_sum(const Dev& d, int ntiles, unsigned long long* red) {
 }
 
 // ============================================================== select
+// debug stamps (Dev::dstamp, ELP_STAMPS): s_memrealtime at the phases of workgroup 0
+#define RSTAMP(i) do { if (d.dstamp && blockIdx.x == 0 && threadIdx.x == 0) \
+    d.dstamp[dslot * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 constexpr int MAX_P2P = 64;  // ranks a mailbox exchange supports
 
 // xGMI mailbox min-loc (Dev::p2p, column-sharded with A replicated): workgroup
@@ -845,9 +850,10 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles) {
 // slack candidates itself (a total order: all agree), gathers a_R into LDS and
 // computes alpha_S for its 4 bump rows (one wave per row, wave order).
 // Workgroup 0 publishes q.  Saves a launch and the single-workgroup select.
-__global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_ub, int ny_ub) {
+__global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_ub, int ny_ub, int dslot) {
     extern __shared__ __attribute__((aligned(16))) double aRs[];  // [k]
     __shared__ Cand red[4];
+    RSTAMP(12);
     DevCtl* c = d.ctl;
     // the control block first (vmcnt retires in issue order: the status test
     // then waits for these loads only, not for the prefetch behind them)
@@ -882,6 +888,7 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_u
     for (int t = 0; t < PFY; ++t) {
         yl[t] = ld_clamp(d.Yl, tid + 256 * t, ny_ub);
         yv[t] = ld_clamp(d.yy, tid + 256 * t, ny_ub);
+        vs[t] = ld_clamp(d.yvs, tid + 256 * t, ny_ub);  // the slot's slack status
     }
     {
         const double* row = d.Minv + (size_t)(pr < k_ub ? pr : 0) * d.ldm;
@@ -892,10 +899,6 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_u
     for (int t = 0; t < PFR; ++t) rl[t] = ld_clamp(d.Rl, tid + 256 * t, k_ub);
     __builtin_amdgcn_sched_barrier(0);  // all of the above issued before any use
     if (blockIdx.x == 0 && threadIdx.x == 0) c->applied_seq = c_seq;  // applied by k_price
-    // the slacks' status (second round trip: indexed by the Y rows; slots past
-    // the real |Y| are stale, so the index is range-checked)
-#pragma unroll
-    for (int t = 0; t < PFY; ++t) vs[t] = d.vstat[d.n + ((yl[t] >= 0 && yl[t] < d.m) ? yl[t] : 0)];
     if (st0 != ST_RUN) {
 #pragma unroll
         for (int t = 0; t < PFC; ++t) KEEP(cc[t].score);
@@ -910,6 +913,7 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_u
         for (int t = 0; t < PFR; ++t) KEEP(rl[t]);
         return;
     }
+    RSTAMP(13);
     Cand best;
     best.j = -1;
     best.score = 0.0;
@@ -961,6 +965,7 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_u
         if (blockIdx.x == 0 && tid == 0) c->status = ST_PHASE_OPT;
         return;
     }
+    RSTAMP(14);
     const int q = (int)best.j;
     if (blockIdx.x == 0 && tid == 0) entering_chosen(d, best);
     if (d.ptimer && blockIdx.x == gridDim.x - 1) {  // the extra timer workgroup
@@ -1008,6 +1013,7 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_u
     }
     acc = wave_tree(acc);
     if (lane == 0) d.alS[pr] = acc;
+    RSTAMP(15);
 }
 
 __global__ void __launch_bounds__(1024) k_select_local(Dev d, int ntiles, int rank) {
@@ -1286,6 +1292,19 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
             cw->snap_ypos0 = i0 >= 0 ? d.ypos[i0] : -1;
             cw->snap_ylast = yl;
             cw->snap_rposyl = yl >= 0 ? d.rpos[yl] : -1;
+            const int ql = loc_of(d, q);
+            const bool pk = ql < 0 || (d.sharded && q < d.N);  // from the exchanged packet
+            const int m = d.m, last = k - 1;
+            cw->snap_lbq = pk ? d.pkt[m] : d.lb[ql];
+            cw->snap_ubq = pk ? d.pkt[m + 1] : d.ub[ql];
+            cw->snap_xq = pk ? d.pkt[m + 2] : d.xval[ql];
+            cw->snap_cq = pk ? d.pkt[m + 3] : d.cost[ql];
+            cw->snap_vsq = ql >= 0 ? d.vstat[ql] : VS_LOWER;
+            cw->snap_csl = last >= 0 ? d.cS[last] : 0.0;
+            cw->snap_slol = last >= 0 ? d.slo[last] : 0.0;
+            cw->snap_shil = last >= 0 ? d.shi[last] : 0.0;
+            cw->snap_sllast = last >= 0 ? d.Sl[last] : -1;
+            cw->snap_rllast = last >= 0 ? d.Rl[last] : -1;
         }
         return;
     }
@@ -1402,16 +1421,11 @@ enum { SI_VSQ, SI_RPOS0, SI_YPOS0, SI_YLAST, SI_SLLAST, SI_RLLAST, SI_RPOSYL, SI
 // Phase 2 (defer != 0): workgroups [nmain, gridDim.x) copy this pivot's AR rows
 // (the only update the next pricing sweep needs), workgroup 0 runs the loop-top
 // checks, and the rest of the update is deferred into the next pricing launch.
-// debug stamps (Dev::dstamp, ELP_STAMPS): s_memrealtime at the phases of workgroup 0
-#define RSTAMP(i) do { if (d.dstamp && blockIdx.x == 0 && threadIdx.x == 0) \
-    d.dstamp[dslot * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int lds_row, int defer,
                                                int nmain, int k_ub, int dslot) {
     extern __shared__ __attribute__((aligned(16))) double asrow_lds[];  // [k]: A[lrow, S]
     __shared__ double dred[4];
     __shared__ Leave lred[4];
-    __shared__ double sc[SC_N];
-    __shared__ int si[SI_N];
     __shared__ int s_action;
     __shared__ Plan s_plan;
     __shared__ double s_wd;
@@ -1433,6 +1447,11 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     const int bland = c->snap_bland;
     const int apos_c = c->snap_apos;
     const bool lead = blockIdx.x == 0;
+    // bookkeeping scalars, snapshot by k_ftran_zr (see DevCtl)
+    const double sv_lbq = c->snap_lbq, sv_ubq = c->snap_ubq, sv_xq = c->snap_xq, sv_cq = c->snap_cq;
+    const double sv_csl = c->snap_csl, sv_slol = c->snap_slol, sv_shil = c->snap_shil;
+    const int sv_vsq = c->snap_vsq, sv_sllast = c->snap_sllast, sv_rllast = c->snap_rllast;
+    const int sv_ypos0 = c->snap_ypos0, sv_ylast = c->snap_ylast, sv_rposyl = c->snap_rposyl;
     // ---- loads that depend on neither the control block nor the decision go
     //      out next (bounded by the host's k_ub, masked by the real k below):
     //      the pass-1 minima, this wave's row of MinvT (B^-1 row, cases B / D)
@@ -1452,6 +1471,12 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     }
     // entries of Rl past the real k are stale: range-checked before use
     const int rcol = ld_clamp(d.Rl, main_wg ? col : 0, k_ub);
+    // the pass-2 candidates k_ftran_zr emitted: the first 256 * PFQ slots of the
+    // list (capacity 2m), masked by the real count below
+    constexpr int PFQ = 4;
+    RCand rq[PFQ];
+#pragma unroll
+    for (int t = 0; t < PFQ; ++t) rq[t] = ld_clamp(d.rcand, tid + 256 * t, 2 * (m > 0 ? m : 1));
     __builtin_amdgcn_sched_barrier(0);  // all of the above issued before any use
     if (st0 != ST_RUN) {  // no plan this iteration: k_update must not re-apply one
         if (blockIdx.x == 0 && threadIdx.x == 0) c->plan.action = ACT_NONE;
@@ -1460,6 +1485,8 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
 #pragma unroll
         for (int t = 0; t < PFT; ++t) KEEP(trow[t]);
         KEEP(rcol);
+#pragma unroll
+        for (int t = 0; t < PFQ; ++t) KEEP(rq[t].r);
         return;
     }
     RSTAMP(1);
@@ -1487,52 +1514,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     const int ypos_r = d.ypos[rsafe];  // its Y slot (workgroup 0 rewrites no bump row's slot)
     // ---- parallel prefetch of bookkeeping scalars
     const int ql = loc_of(d, q);  // -1: the entering column lives on another shard
-    {
-        // thread t < SC_N loads double scalar t, thread SC_N + u int scalar u:
-        // addresses picked by selects, one unconditional load each
-        const bool pk = ql < 0 || (d.sharded && q < d.N);  // from the exchanged packet
-        const int ls = last >= 0 ? last : 0;
-        const double zero = 0.0;
-        const double* dp = &zero;
-        switch (tid) {
-            case SC_LBQ: dp = pk ? d.pkt + m : d.lb + ql; break;
-            case SC_UBQ: dp = pk ? d.pkt + m + 1 : d.ub + ql; break;
-            case SC_XVQ: dp = pk ? d.pkt + m + 2 : d.xval + ql; break;
-            case SC_CQ: dp = pk ? d.pkt + m + 3 : d.cost + ql; break;
-            case SC_CSL: dp = d.cS + ls; break;
-            case SC_SLOL: dp = d.slo + ls; break;
-            case SC_SHIL: dp = d.shi + ls; break;
-            default: break;
-        }
-        const int32_t neg = -1;
-        const int32_t* ip = &neg;
-        switch (tid - SC_N) {
-            case SI_SLLAST: ip = d.Sl + ls; break;
-            case SI_RLLAST: ip = d.Rl + ls; break;
-            default: break;
-        }
-        const int8_t* vp = d.vstat + (ql >= 0 ? ql : 0);
-        const double dv = *dp;
-        const int32_t iv = *ip;
-        const int8_t vv = *vp;
-        if (tid < SC_N) sc[tid] = (tid == SC_SLL || (last < 0 && tid >= SC_CSL)) ? 0.0 : dv;
-        switch (tid - SC_N) {
-            case SI_VSQ: si[SI_VSQ] = ql >= 0 ? vv : VS_LOWER; break;
-            case SI_RPOS0: si[SI_RPOS0] = c->snap_apos; break;
-            case SI_YPOS0: si[SI_YPOS0] = c->snap_ypos0; break;
-            case SI_YLAST: si[SI_YLAST] = c->snap_ylast; break;
-            case SI_SLLAST: si[SI_SLLAST] = last >= 0 ? iv : -1; break;
-            case SI_RLLAST: si[SI_RLLAST] = last >= 0 ? iv : -1; break;
-            case SI_RPOSYL: si[SI_RPOSYL] = c->snap_rposyl; break;
-            default: break;
-        }
-    }
-    // the pass-2 candidates (emitted by k_ftran_zr) go out with the rest
-    constexpr int PFQ = 4;  // per thread, held in registers (<= 1024 candidates)
     const bool pfq = ncand <= 256 * PFQ;
-    RCand rq[PFQ];
-#pragma unroll
-    for (int t = 0; t < PFQ; ++t) rq[t] = ld_clamp(d.rcand, tid + 256 * t, ncand);
     // case D needs wave_dot(MinvT[apos, :], A[lrow, S]) in every workgroup: wave 0
     // fetches that row now (apos comes with the control block)
     double arow[PFT];
@@ -1588,7 +1570,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         if (leave_better(lred[i], best, bland)) best = lred[i];
     RSTAMP(3);
     // ---- decision (uniform across the block)
-    const double lbq = sc[SC_LBQ], ubq = sc[SC_UBQ];
+    const double lbq = sv_lbq, ubq = sv_ubq;
     const double theta = best.var >= 0 ? (best.r > 0.0 ? best.r : 0.0) : INF;
     const double flip = (lbq > -INF && ubq < INF) ? ubq - lbq : INF;
     int action;
@@ -1624,7 +1606,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     if (action == ACT_FLIP) {
         if (lead && tid == 0) {
             if (ql >= 0) {  // the shard that stores q's status
-                if (si[SI_VSQ] == VS_LOWER) {
+                if (sv_vsq == VS_LOWER) {
                     d.vstat[ql] = VS_UPPER;
                     d.xval[ql] = ubq;
                 } else {
@@ -1663,9 +1645,9 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
                 ap_row = lrow;
             }
         } else {  // C, D, E: row i0 leaves Y; D: the leaving slack's row joins it
-            rm_slot = si[SI_YPOS0];
+            rm_slot = sv_ypos0;
             rm_last = ny - 1;
-            if (si[SI_RPOS0] >= 0 && lrow >= 0 && !leave_art) {
+            if (apos_c >= 0 && lrow >= 0 && !leave_art) {
                 ap_slot = ny - 1;
                 ap_row = lrow;
             }
@@ -1688,7 +1670,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     double vcol = 0.0;  // vvec[col] (cases B, D)
     // pivot case as workgroup 0's bookkeeping will classify it
     const int lposx = best.e >= m ? best.e - m : -1;
-    const int apos = si[SI_RPOS0];
+    const int apos = apos_c;
     const int pcx = q < d.N ? (lposx >= 0 ? PC_A : PC_B) : apos < 0 ? PC_E : lposx >= 0 ? PC_C : PC_D;
     // operands of the dual update that need the decision (cases A, C)
     const bool upd = phase == 2 && lane == 0 && col < k && pcx != PC_E &&
@@ -1702,6 +1684,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     double vr[PFV], ca[PFV];
     double t0_piv = 0.0, t0_ymoved = 0.0;
     int t0_yposl = -1;
+    int8_t t0_rowvs = VS_FIXED, t0_yvslast = VS_FIXED;
     {  // (straight-line; workgroup 0 uses them, the others discard them)
         const size_t rv = (size_t)(lposx >= 0 ? lposx : 0) * d.ldm, ra = (size_t)(apos >= 0 ? apos : 0) * d.ldm;
 #pragma unroll
@@ -1711,7 +1694,9 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         }
         t0_piv = d.Minv[rv + (apos >= 0 ? apos : 0)];
         t0_yposl = d.ypos[lrow_all >= 0 ? lrow_all : 0];
-        const int moved = si[SI_YLAST];
+        t0_rowvs = d.rowvs[lrow_all >= 0 ? lrow_all : 0];
+        t0_yvslast = d.yvs[ny > 0 ? ny - 1 : 0];
+        const int moved = sv_ylast;
         t0_ymoved = d.y[moved >= 0 ? moved : 0];
     }
     if (lrow_all >= 0 && k > 0) {
@@ -1772,7 +1757,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         // the last Y row moves into the slot of row i0 (cases C, D)
         // (workgroup 0 rewrites ypos only for rows that are not bump rows, the
         //  entering slack's row -- excluded above -- and the moved last row)
-        const int slot = (pcx == PC_C || pcx == PC_D) && row == si[SI_YLAST] ? si[SI_YPOS0] : ypos_r;
+        const int slot = (pcx == PC_C || pcx == PC_D) && row == sv_ylast ? sv_ypos0 : ypos_r;
         if (slot >= 0) d.yy[slot] = yn;
     }
     RSTAMP(5);
@@ -1794,7 +1779,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         const int lv = best.var;
         const int lrow = best.e < m ? best.e : -1;
         const int lpos = best.e < m ? -1 : best.e - m;
-        const double xq = sc[SC_XVQ] + sig * theta;
+        const double xq = sv_xq + sig * theta;
         const bool at_lower = best.g > 0.0;
         const bool leave_art = lv >= d.N + m;
         const int lvl = loc_of(d, lv);
@@ -1808,7 +1793,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
             d.xval[lvl] = at_lower ? best.l : best.u;
         }
         if (ql >= 0) d.vstat[ql] = VS_BASIC;
-        const double cq = sc[SC_CQ];
+        const double cq = sv_cq;
         Plan P;
         P.action = ACT_PIVOT;
         P.k_old = k;
@@ -1852,12 +1837,13 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
                     P.y_ap_row = i;
                     d.Yl[nny] = i;
                     d.ypos[i] = nny;
+                    d.yvs[nny] = t0_rowvs;
                     nny++;
                 }
             }
         } else {
             const int i0 = q - d.N;
-            const int a = si[SI_RPOS0];
+            const int a = apos_c;
             if (a < 0) {  // case E
                 P.pcase = PC_E;
                 if (lrow != i0) c->status = ST_NUMFAIL;
@@ -1869,13 +1855,13 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
                 P.last = last;
                 P.piv = t0_piv;  // Minv[b][a]
                 if (b != last) {
-                    d.Sl[b] = si[SI_SLLAST];
-                    d.cS[b] = sc[SC_CSL];
-                    d.slo[b] = sc[SC_SLOL];
-                    d.shi[b] = sc[SC_SHIL];
+                    d.Sl[b] = sv_sllast;
+                    d.cS[b] = sv_csl;
+                    d.slo[b] = sv_slol;
+                    d.shi[b] = sv_shil;
                 }
                 if (a != last) {
-                    const int rl = si[SI_RLLAST];
+                    const int rl = sv_rllast;
                     d.Rl[a] = rl;
                     d.rpos[rl] = a;
                 }
@@ -1897,13 +1883,14 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
             d.rlo[i0] = lbq;
             d.rhi[i0] = ubq;
             // row i0 leaves Y (its slack is basic now) ...
-            const int sl = si[SI_YPOS0], ylast = nny - 1;
+            const int sl = sv_ypos0, ylast = nny - 1;
             P.y_rm_slot = sl;
             P.y_rm_last = ylast;
             if (sl != ylast) {
-                const int moved = si[SI_YLAST];
+                const int moved = sv_ylast;
                 d.Yl[sl] = moved;
                 d.ypos[moved] = sl;
+                d.yvs[sl] = t0_yvslast;
             }
             d.ypos[i0] = -1;
             nny--;
@@ -1913,6 +1900,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
                 P.y_ap_row = lrow;
                 d.Yl[nny] = lrow;
                 d.ypos[lrow] = nny;
+                d.yvs[nny] = t0_rowvs;
                 nny++;
             }
         }
@@ -1921,7 +1909,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
             // artificial left: no append) the slot it already had
             int yslot = P.y_ap_slot >= 0 ? P.y_ap_slot : t0_yposl;
             if (P.y_ap_slot < 0 && P.pcase >= PC_C && P.y_rm_slot != P.y_rm_last &&
-                P.lrow == si[SI_YLAST])
+                P.lrow == sv_ylast)
                 yslot = P.y_rm_slot;  // the leaving row was the last Y row: moved into i0's slot
             if (P.pcase == PC_B) {
                 const double yn = dq / P.piv;
@@ -1935,9 +1923,9 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
                 }
             }
             if (P.pcase >= PC_C) {  // C, D, E removed row i0 from Y
-                const int sl = si[SI_YPOS0], moved = si[SI_YLAST];
+                const int sl = sv_ypos0, moved = sv_ylast;
                 // the owner wave of a bump row wrote its moved slot already
-                const bool owned = P.pcase != PC_E && si[SI_RPOSYL] >= 0;
+                const bool owned = P.pcase != PC_E && sv_rposyl >= 0;
                 const bool special = P.pcase == PC_D && moved == P.row;
                 if (sl != ny - 1 && !owned && !special) d.yy[sl] = t0_ymoved;
             }
@@ -2635,7 +2623,7 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
         const size_t ldsz = lds > 64 ? lds : 64;  // the timer workgroup reduces in it
         // + the timer workgroup, + the CSC column-scatter workgroup
         const unsigned g = cdiv(k_ub > 0 ? k_ub : 1, 4) + (d.ptimer ? 1 : 0) + (d.csc ? 1 : 0);
-        k_select_ftran<<<g, 256, ldsz, st>>>(d, ntiles, k_ub, ny_ub);
+        k_select_ftran<<<g, 256, ldsz, st>>>(d, ntiles, k_ub, ny_ub, dslot);
         return launch_iteration_tail(d, k_ub, phase, st, false, dslot);
     }
     k_select<<<1, 1024, 0, st>>>(d, ntiles);
