@@ -58,7 +58,13 @@ def parse():
     ap.add_argument("--sparse-n", type=int, default=10000)
     ap.add_argument("--sparse-steps", type=int, default=1000)
     ap.add_argument("--sparse-cpu-iters", type=int, default=200)
-    return ap.parse_args()
+    ap.add_argument("--pricing", choices=["devex", "dantzig"], default="devex",
+                    help="pricing rule (elp_control.pricing; devex is lp_solve's default)")
+    ap.add_argument("--compare-rules", type=int, default=1,
+                    help="N=1: also solve the LP to optimality with the other pricing rule")
+    a = ap.parse_args()
+    a.rule = 1 if a.pricing == "devex" else 0
+    return a
 
 
 def enable_p2p(p, rank):
@@ -80,7 +86,7 @@ def cpu_baseline(args):
     from oracle import generate_dense, solve_dense
     A, b, c = generate_dense(args.seed, args.m, args.n)
     t0 = time.time()
-    r = solve_dense(A, np.ones(args.m, np.int32), b, c, maximize=True,
+    r = solve_dense(A, np.ones(args.m, np.int32), b, c, maximize=True, price_rule=args.rule,
                     max_iter=args.warmup + args.cpu_iters, t_mark_iter=args.warmup)
     wall = time.time() - t0
     it = r.stats["iterations"] - args.warmup
@@ -118,7 +124,7 @@ def c4_rate(args, lib, world, rank, local, barrier, dist):
     import torch
     from easylp_amd import Problem
     m, n = 10000, 500000
-    p = Problem(m, n, device=local)
+    p = Problem(m, n, device=local, pricing=args.rule)
     if world > 1 or args.force_sharded:
         from easylp_amd.dist import share_unique_id
         p.comm_init(share_unique_id(lib, rank), world, rank)
@@ -151,7 +157,7 @@ def c4_rate(args, lib, world, rank, local, barrier, dist):
 def sparse_rate(args, local, with_cpu):
     """BASELINE config 5 on the CSC path: a seeded sparse LP of Netlib-like shape
     (easylp_amd.synth.sparse_packing, 5 nonzeros per column) plus the Klee-Minty
-    cube n=12 (4095 Dantzig pivots).  Same step definition; the CPU leg is the
+    cube n=12 (4095 pivots under Dantzig, a few dozen under Devex).  Same step definition; the CPU leg is the
     oracle in its CSC order (price_mode 1) over a bounded window."""
     import numpy as np
     from easylp_amd import Problem
@@ -159,7 +165,7 @@ def sparse_rate(args, local, with_cpu):
     m, n = args.sparse_m, args.sparse_n
     cp, ri, v, b, c = sparse_packing(args.seed, m, n, 5)
     dirs = np.ones(m, np.int32)
-    p = Problem(m, n, device=local)
+    p = Problem(m, n, device=local, pricing=args.rule)
     p.load_csc(cp, ri, v, dirs, b, c, maximize=True)
     p.iterate(args.warmup)
     s0 = p.stats()
@@ -189,7 +195,7 @@ def sparse_rate(args, local, with_cpu):
     K = sp.csc_matrix((vals, (rows, cols)), shape=(km, km))
     kb = np.array([5.0 ** (i + 1) for i in range(km)])
     kc = np.array([2.0 ** (km - 1 - j) for j in range(km)])
-    with Problem(km, km, device=local) as pk:
+    with Problem(km, km, device=local, pricing=args.rule) as pk:
         pk.load_csc(K.indptr, K.indices, K.data, np.ones(km, np.int32), kb, kc, maximize=True)
         kst = pk.solve()
         ks = pk.stats()
@@ -200,14 +206,15 @@ def sparse_rate(args, local, with_cpu):
         from oracle import solve_dense
         A = dense_of(cp, ri, v, m, n)
         w = args.warmup
-        r = solve_dense(A, dirs, b, c, maximize=True, price_mode=1,
+        r = solve_dense(A, dirs, b, c, maximize=True, price_mode=1, price_rule=args.rule,
                         max_iter=w + args.sparse_cpu_iters, t_mark_iter=w)
         cit = r.stats["iterations"] - w
         out["cpu_baseline"] = {"value": cit / r.stats["seconds_at_mark"], "unit": "iterations/s",
                                "cores": 1, "kind": "port",
                                "sample": "oracle/ (C, -O3, 1 thread, CSC order) iterations [%d, %d)" % (w, w + cit)}
         t0 = time.perf_counter()
-        rk = solve_dense(K.toarray(), np.ones(km, np.int32), kb, kc, maximize=True, price_mode=1)
+        rk = solve_dense(K.toarray(), np.ones(km, np.int32), kb, kc, maximize=True, price_mode=1,
+                         price_rule=args.rule)
         out["klee_minty"]["cpu_seconds"] = time.perf_counter() - t0
         out["klee_minty"]["cpu_iterations"] = rk.stats["iterations"]
     return out
@@ -238,7 +245,7 @@ def main():
 
     lib = load()
     verbose = ELP_PROFILE_PRICE if args.profile_price else 0
-    p = Problem(args.m, args.n, device=local, verbose=verbose)
+    p = Problem(args.m, args.n, device=local, verbose=verbose, pricing=args.rule)
     if world > 1 or args.force_sharded:
         from easylp_amd.dist import share_unique_id
         p.comm_init(share_unique_id(lib, rank), world, rank)
@@ -294,6 +301,18 @@ def main():
 
     traffic, traffic_src = committed_traffic(args) if world == 1 else (None, None)
 
+    other = None  # the same LP to optimality under the other pricing rule
+    if args.compare_rules and world == 1 and not args.no_optimal and not args.force_sharded:
+        p.close()
+        q = Problem(args.m, args.n, device=local, pricing=1 - args.rule)
+        q.load_generated(args.seed)
+        qst = q.solve()
+        qs = q.stats()
+        other = {"pricing": "dantzig" if args.rule else "devex", "status": qst,
+                 "objective": q.solution(qst).objval, "iterations_to_optimal": qs["iterations"],
+                 "time_to_optimal_s": qs["seconds_loop"]}
+        q.close()
+
     c4 = None
     if args.c4:
         p.close()  # free the 5000x50000 problem first
@@ -327,11 +346,13 @@ def main():
                 "parallelism": ("column-shard x%d, %s min-loc" % (world, "xGMI mailbox" if args.p2p else "RCCL all-gather")
                                 if world > 1 or args.force_sharded else "single GPU"),
                 "iterations_timed": iters,
+                "pricing": args.pricing,
             },
             "time_to_optimal_s": tto,
             "final": final,
+            "other_pricing": other,
             "roofline": {
-                "kernel": "k_price (pricing sweep + Dantzig argmin)",
+                "kernel": "k_price (pricing sweep + %s argmin)" % args.pricing,
                 "bound": "hbm",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,

@@ -51,7 +51,8 @@ class ElpControl(ctypes.Structure):
         ("refactor_mode", ctypes.c_int32),
         ("replicate", ctypes.c_int32),
         ("max_nodes", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 4),
+        ("pricing", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 3),
     ]
 
 

@@ -100,6 +100,7 @@ extern "C" void elp_default_control(elp_control* c) {
     c->device = 0;
     c->sync_every = 32;
     c->verbose = 0;
+    c->pricing = ELP_PRICE_DEVEX;
 }
 
 extern "C" const char* elp_last_error(void) { return g_err.c_str(); }
@@ -115,7 +116,7 @@ static void free_dev(elp_handle* h) {
                     d.cand,     d.pstamp, d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand,
                     d.pkt, d.objg, d.ract, d.cand_xchg, h->d_flag, d.cS, d.slo, d.shi, d.rlo, d.rhi,
                     (void*)d.cptr, (void*)d.rind, (void*)d.cval, (void*)d.rptr, (void*)d.cind,
-                    (void*)d.rval, d.qcol, d.dstamp, d.rowvs, d.yvs};
+                    (void*)d.rval, d.qcol, d.dstamp, d.rowvs, d.yvs, d.dw, d.dprev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     h->A_owned = nullptr;
@@ -135,6 +136,8 @@ extern "C" int elp_create(elp_handle** out, int64_t m, int64_t n, const elp_cont
     *out = nullptr;
     if (m < 0 || n < 1) return fail(ELP_E_ARG, "elp_create: need m >= 0 and n >= 1");
     if (m > 0x3fffffff || n > 0x3fffffff) return fail(ELP_E_ARG, "elp_create: dimension too large");
+    if (ctl && ctl->pricing != ELP_PRICE_DANTZIG && ctl->pricing != ELP_PRICE_DEVEX)
+        return fail(ELP_E_ARG, "elp_create: pricing must be ELP_PRICE_DANTZIG or ELP_PRICE_DEVEX");
     elp_handle* h = new elp_handle();
     if (ctl) h->ctl = *ctl;
     else elp_default_control(&h->ctl);
@@ -210,6 +213,8 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.vstat, nv));
     A(dalloc(&d.rowvs, mm));
     A(dalloc(&d.yvs, mm));
+    A(dalloc(&d.dw, (size_t)(n + m)));
+    A(dalloc(&d.dprev, (size_t)(n + m)));
     A(dalloc(&d.asgn, mm));
     A(dalloc(&d.xr, mm));
     A(dalloc(&d.xs, mm));
@@ -399,6 +404,8 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
     c.unb_var = -1;
     c.qcol_var = -1;
     c.mb_epoch = ++h->mb_epoch;
+    c.devex = h->ctl.pricing == ELP_PRICE_DEVEX;
+    c.dv_lv = -1;
     *h->hctl = c;
     HIPCHK(hipMemcpyAsync(d.ctl, h->hctl, sizeof(DevCtl), hipMemcpyHostToDevice, h->st));
     if (d.qcol) HIPCHK(hipMemsetAsync(d.qcol, 0, (size_t)std::max<int64_t>(m, 1) * sizeof(double), h->st));
@@ -408,6 +415,7 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
         if (rc) return rc;
     }
     HIPCHK(launch_init_rows(d, drhs, h->st));
+    HIPCHK(launch_devex_reset(d, h->st));
     HIPCHK(hipMemcpyAsync(h->hctl, d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
     HIPCHK(hipStreamSynchronize(h->st));
     {

@@ -65,7 +65,11 @@ struct DevCtl {
     // likewise the bookkeeping entries k_ratio's dual update reads (k_ftran_zr's
     // snapshot workgroup): |Y|, rpos / ypos of the entering slack's row, the
     // last Y row and its bump position
-    int32_t snap_ny, snap_apos, snap_ypos0, snap_ylast, snap_rposyl, pad4;
+    int32_t snap_ny, snap_apos, snap_ypos0, snap_ylast, snap_rposyl;
+    // the status k_ratio's workgroups act on: workgroup 0 may already have
+    // written the next loop-top status (refactor / stop / cap) when another
+    // workgroup of the same launch starts and reads the control block
+    int32_t snap_status;
     // ... and the scalars of the pivot bookkeeping, so k_ratio reads them with
     // the control block: q's (lb, ub, x, cost) and status; the last bump
     // position's (cost, lo, hi), structural and row
@@ -83,6 +87,14 @@ struct DevCtl {
     // a poll (k_update) -- see DESIGN.md "Iteration pipeline"
     int32_t plan_seq, applied_seq;
     int64_t mb_epoch;  // xGMI mailbox: loads so far (seq = epoch << 40 | iteration + 1)
+    // Devex pricing (elp_control.pricing): the last pivot as the next pricing
+    // pass needs it -- entering reduced cost and weight, leaving variable;
+    // dv_valid: 0 no update (phase start, bound flip), 1 update from the last
+    // pivot, 2 the reference framework restarts (oracle run_phase)
+    int32_t devex, dv_valid;
+    int32_t dv_lv, pad8;
+    double dv_dq, dv_wq;
+    double wq;  // weight of the entering candidate (select kernels)
 };
 
 // Harris pass-2 candidate (a superset of the global candidates: exact ratio
@@ -93,8 +105,8 @@ struct RCand {
 };
 
 struct Cand {
-    double score, d;
-    int64_t j;  // -1: none
+    double score, d, w;  // w: the column's Devex weight (1 under Dantzig)
+    int64_t j;           // -1: none
 };
 
 // a rank's best candidate as exchanged between shards: with every rank holding
@@ -176,6 +188,9 @@ struct Dev {
     MboxRec* mbox;          // this rank's mailbox [2 parities][world]
     MboxRec* const* mpeers; // every rank's mailbox as mapped in this process
     int32_t p2p, rank;
+    // Devex: weight and last reduced cost per local structural (j < n) and
+    // slack (n + i)
+    double *dw, *dprev;
 };
 
 // ---------------------------------------------------------------- launches
@@ -216,7 +231,8 @@ hipError_t launch_refactor_gj(const Dev& d, int k, hipStream_t st);
 hipError_t launch_btran_exact(const Dev& d, int k, hipStream_t st);  // phase-2 duals
 hipError_t launch_refactor_primal(const Dev& d, int k, hipStream_t st);  // needs ract
 hipError_t launch_nzlist(const Dev& d, hipStream_t st);
-hipError_t launch_phase2(const Dev& d, hipStream_t st);
+hipError_t launch_phase2(const Dev& d, hipStream_t st);  // (includes devex_reset)
+hipError_t launch_devex_reset(const Dev& d, hipStream_t st);  // weights 1, dv_valid 0
 // sensitivity (final basis, k = bump dimension): dred[n] reduced costs; TR
 // (k x n), plo/phi (k x ceil(n/64)), qlo/qhi (k x ceil(m/64)) work; out4 =
 // [olo(k) ohi(k) rlo(k) rhi(k)]: intervals of delta c_{S_p} and delta b_{R_c}

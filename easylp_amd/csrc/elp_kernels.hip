@@ -104,23 +104,33 @@ DEV Cand shfl_cand(const Cand& c, int off) {
     Cand o;
     o.score = __shfl_xor(c.score, off);
     o.d = __shfl_xor(c.d, off);
+    o.w = __shfl_xor(c.w, off);
     o.j = __shfl_xor((long long)c.j, off);
     return o;
+}
+// field-wise select (a whole-struct conditional copy of Cand was observed to
+// be miscompiled on gfx950: the d field kept its old value)
+DEV void cand_take(Cand& c, const Cand& o, bool take) {
+    c.score = take ? o.score : c.score;
+    c.d = take ? o.d : c.d;
+    c.w = take ? o.w : c.w;
+    c.j = take ? o.j : c.j;
 }
 // block-wide argmax of candidates; result valid in every thread
 template <int NT>
 DEV Cand block_best(Cand c, int bland, Cand* lds) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
-        Cand o = shfl_cand(c, off);
-        if (cand_better(o, c, bland)) c = o;
+        const Cand o = shfl_cand(c, off);
+        cand_take(c, o, cand_better(o, c, bland));
     }
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (lane == 0) lds[w] = c;
     __syncthreads();
-    Cand r = lds[0];
+    int win = 0;  // the winning wave, then one copy of its record
     for (int i = 1; i < NT / 64; ++i)
-        if (cand_better(lds[i], r, bland)) r = lds[i];
+        if (cand_better(lds[i], lds[win], bland)) win = i;
+    const Cand r = lds[win];
     __syncthreads();
     return r;
 }
@@ -453,6 +463,87 @@ DEV bool apply_role(const Dev& d, int napply, int nb_minv) {
 }
 
 // ============================================================== pricing
+// Devex reference weights (oracle run_phase, price_rule 1): the last pivot's
+// ratio alpha_rj / alpha_rq = (d_j - d_j') / d_q from this pass's d_j' and the
+// previous pass's d_j, w_j = max(w_j, (alpha_rj / alpha_rq)^2 w_q) (capped);
+// the leaving variable's weight was set by k_ratio and is not updated here.
+// DevCtl::dv_valid: 0 no update (phase start, bound flip), 1 update, 2 the
+// framework restarts (every priced weight back to 1).
+constexpr double DEVEX_WMAX = 1e20;
+constexpr double DEVEX_RESET = 1e6;  // entering weight above this: new reference framework
+struct DevexIn {
+    int32_t valid, lv;
+    double dq, wq;
+};
+DEV DevexIn devex_in(const DevCtl* c) {
+    DevexIn x;
+    x.valid = c->dv_valid;
+    x.lv = c->dv_lv;
+    x.dq = c->dv_dq;
+    x.wq = c->dv_wq;
+    return x;
+}
+// jl: local id (dw / dprev index), jg: global id
+DEV double devex_weight(const Dev& d, const DevexIn& x, int64_t jl, int64_t jg, double dj) {
+    double wj = d.dw[jl];
+    if (x.valid == 2) {  // framework restart (k_ratio): weight 1, no update
+        wj = 1.0;
+        d.dw[jl] = 1.0;
+    } else if (x.valid == 1 && jg != x.lv) {
+        const double r = (d.dprev[jl] - dj) / x.dq;
+        double wn = (r * r) * x.wq;
+        if (wn > DEVEX_WMAX) wn = DEVEX_WMAX;
+        if (wn > wj) {
+            wj = wn;
+            d.dw[jl] = wj;
+        }
+    }
+    d.dprev[jl] = dj;
+    return wj;
+}
+// candidate of a priced column: Dantzig score |d|, Devex d^2 / w
+DEV Cand price_cand(int8_t vs, double dj, double wj, int devex, double dtol, int64_t jg) {
+    Cand o;
+    o.j = -1;
+    o.score = 0.0;
+    o.d = dj;
+    o.w = wj;
+    if ((vs == VS_LOWER || vs == VS_FREE) && dj < -dtol) {
+        o.j = jg;
+        o.score = devex ? (dj * dj) / wj : -dj;
+    } else if ((vs == VS_UPPER || vs == VS_FREE) && dj > dtol) {
+        o.j = jg;
+        o.score = devex ? (dj * dj) / wj : dj;
+    }
+    return o;
+}
+// The slack candidates (replicated on every rank; a slack's cost is 0, so
+// d = -y on the Y slots, in slot order): one extra workgroup of the pricing
+// launch, written as candidate [ntiles] next to the tiles'
+template <int NT>
+DEV void price_slacks(const Dev& d, int64_t slot, Cand* red) {
+    const DevCtl* c = d.ctl;
+    const int ny = c->ny, bland = c->bland, devex = c->devex;
+    const double dtol = c->tol_dual;
+    const DevexIn dx = devex_in(c);
+    Cand best;
+    best.j = -1;
+    best.score = 0.0;
+    best.d = 0.0;
+    best.w = 1.0;
+    for (int p = threadIdx.x; p < ny; p += NT) {
+        const int8_t v = d.yvs[p];
+        if (v == VS_FIXED) continue;
+        const int i = d.Yl[p];
+        const double dj = 0.0 - d.yy[p];
+        const double wj = devex ? devex_weight(d, dx, d.n + i, d.N + i, dj) : 1.0;
+        const Cand o = price_cand(v, dj, wj, devex, dtol, d.N + i);
+        cand_take(best, o, cand_better(o, best, bland));
+    }
+    best = block_best<NT>(best, bland, red);
+    if (threadIdx.x == 0) d.cand[slot] = best;
+}
+
 // One workgroup = 8 waves = 128 columns x all Y slots.  Wave w sweeps slot
 // chunk w (PRICE_SPLIT contiguous chunks), lane l owns columns 2l, 2l+1 of the
 // tile (16-byte loads, 1 KiB per wave instruction, row-major AR so every load
@@ -466,6 +557,11 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int napply, int 
     if (apply_role(d, napply, nb_minv)) return;
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
+    const int64_t ntiles = gridDim.x - napply - 1;
+    if ((int64_t)blockIdx.x == ntiles) {  // the slack workgroup
+        price_slacks<PRICE_THREADS>(d, ntiles, red);
+        return;
+    }
     if (d.ptimer && threadIdx.x == 0) d.pstamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     const int ny = c->ny, bland = c->bland;
     const int lane = threadIdx.x & 63;
@@ -513,6 +609,7 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int napply, int 
     best.j = -1;
     best.score = 0.0;
     best.d = 0.0;
+    best.w = 1.0;
     if (threadIdx.x < TILE_COLS) {
         const int64_t j = (int64_t)blockIdx.x * TILE_COLS + threadIdx.x;
         if (j < d.n) {
@@ -522,16 +619,9 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int napply, int 
 #pragma unroll
                 for (int ww = 0; ww < PRICE_SPLIT; ++ww) tot = tot + part[ww][threadIdx.x];
                 const double dj = d.cost[j] - tot;
-                const double dtol = c->tol_dual;
-                if ((vs == VS_LOWER || vs == VS_FREE) && dj < -dtol) {
-                    best.j = d.col0 + j;
-                    best.score = -dj;
-                    best.d = dj;
-                } else if ((vs == VS_UPPER || vs == VS_FREE) && dj > dtol) {
-                    best.j = d.col0 + j;
-                    best.score = dj;
-                    best.d = dj;
-                }
+                const int devex = c->devex;
+                const double wj = devex ? devex_weight(d, devex_in(c), j, d.col0 + j, dj) : 1.0;
+                best = price_cand(vs, dj, wj, devex, c->tol_dual, d.col0 + j);
             }
         }
     }
@@ -545,9 +635,11 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int napply, int 
 // algorithmic bytes of one pricing pass.  Dense: the AR sweep (8|Y|n), c and
 // status (9n), y_Y and Yl (12|Y|).  CSC: row index + value per nonzero (12 nnz),
 // column pointer, c, status (17n); the y gathers hit L2 (m doubles)
-DEV double price_pass_bytes(const Dev& d, int ny) {
-    if (d.csc) return 12.0 * (double)d.nnz + 17.0 * (double)d.n + 8.0 * (double)d.m;
-    return 8.0 * (double)ny * (double)d.n + 9.0 * (double)d.n + 12.0 * (double)ny;
+DEV double price_pass_bytes(const Dev& d, int ny, int devex) {
+    // Devex adds w and the previous d per column: read both, write d (24n)
+    const double dvx = devex ? 24.0 * (double)d.n : 0.0;
+    if (d.csc) return 12.0 * (double)d.nnz + 17.0 * (double)d.n + 8.0 * (double)d.m + dvx;
+    return 8.0 * (double)ny * (double)d.n + 9.0 * (double)d.n + 12.0 * (double)ny + dvx;
 }
 
 // CSC pricing: one workgroup = one tile of TILE_COLS columns, one thread per
@@ -563,6 +655,11 @@ __global__ void __launch_bounds__(TILE_COLS) k_price_csc(Dev d, int napply, int 
     if (apply_role(d, napply, nb_minv)) return;
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
+    const int64_t ntiles = gridDim.x - napply - 1;
+    if ((int64_t)blockIdx.x == ntiles) {  // the slack workgroup
+        price_slacks<TILE_COLS>(d, ntiles, red);
+        return;
+    }
     if (d.ptimer && threadIdx.x == 0) d.pstamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     const int bland = c->bland;
     const int64_t j0 = (int64_t)blockIdx.x * TILE_COLS;
@@ -590,20 +687,14 @@ __global__ void __launch_bounds__(TILE_COLS) k_price_csc(Dev d, int napply, int 
     best.j = -1;
     best.score = 0.0;
     best.d = 0.0;
+    best.w = 1.0;
     if (j < d.n) {
         const int8_t vs = d.vstat[j];
         if (vs != VS_BASIC && vs != VS_FIXED) {
             const double dj = d.cost[j] - acc;
-            const double dtol = c->tol_dual;
-            if ((vs == VS_LOWER || vs == VS_FREE) && dj < -dtol) {
-                best.j = d.col0 + j;
-                best.score = -dj;
-                best.d = dj;
-            } else if ((vs == VS_UPPER || vs == VS_FREE) && dj > dtol) {
-                best.j = d.col0 + j;
-                best.score = dj;
-                best.d = dj;
-            }
+            const int devex = c->devex;
+            const double wj = devex ? devex_weight(d, devex_in(c), j, d.col0 + j, dj) : 1.0;
+            best = price_cand(vs, dj, wj, devex, c->tol_dual, d.col0 + j);
         }
     }
     best = block_best<TILE_COLS>(best, bland, red);
@@ -671,7 +762,7 @@ DEV void price_timer_sum(const Dev& d, int ntiles, unsigned long long* red) {
         const int ny = c->ny;
         c->price_ticks += hi - lo;
         c->price_timed++;
-        c->price_tbytes += price_pass_bytes(d, ny);
+        c->price_tbytes += price_pass_bytes(d, ny, c->devex);
     }
 }
 
@@ -729,6 +820,7 @@ DEV bool p2p_exchange(const Dev& d, Cand& best, int bland, int64_t iter, int64_t
             CandX x;
             x.c.score = __hip_atomic_load(&r->x.c.score, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             x.c.d = __hip_atomic_load(&r->x.c.d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            x.c.w = __hip_atomic_load(&r->x.c.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             x.c.j = __hip_atomic_load(&r->x.c.j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             x.lb = __hip_atomic_load(&r->x.lb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             x.ub = __hip_atomic_load(&r->x.ub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -761,34 +853,15 @@ DEV bool p2p_exchange(const Dev& d, Cand& best, int bland, int64_t iter, int64_t
 // to cand_xchg[rank] for the all-gather (k_select_global decides).
 DEV Cand local_best(const Dev& d, int ntiles, Cand* red) {
     const DevCtl* c = d.ctl;
-    const int bland = c->bland, ny = c->ny;
+    const int bland = c->bland;
     Cand best;
     best.j = -1;
     best.score = 0.0;
     best.d = 0.0;
-    for (int t = threadIdx.x; t < ntiles; t += 1024) {
+    best.w = 1.0;
+    for (int t = threadIdx.x; t <= ntiles; t += 1024) {  // [ntiles]: the slacks
         const Cand o = d.cand[t];
-        if (cand_better(o, best, bland)) best = o;
-    }
-    const double dtol = c->tol_dual;
-    for (int p = threadIdx.x; p < ny; p += 1024) {
-        const int i = d.Yl[p];
-        const int jl = d.n + i;  // local slack id
-        const int8_t vs = d.vstat[jl];
-        if (vs == VS_FIXED) continue;
-        const double dj = d.cost[jl] - d.yy[p];
-        Cand o;
-        o.j = -1;
-        if ((vs == VS_LOWER || vs == VS_FREE) && dj < -dtol) {
-            o.j = d.N + i;
-            o.score = -dj;
-            o.d = dj;
-        } else if ((vs == VS_UPPER || vs == VS_FREE) && dj > dtol) {
-            o.j = d.N + i;
-            o.score = dj;
-            o.d = dj;
-        }
-        if (cand_better(o, best, bland)) best = o;
+        cand_take(best, o, cand_better(o, best, bland));
     }
     return block_best<1024>(best, bland, red);
 }
@@ -798,10 +871,11 @@ DEV void entering_chosen(const Dev& d, const Cand& best) {
     const int ny = c->ny;
     c->ncand = 0;
     // algorithmic bytes of this pricing pass: AR sweep + c + status + y_Y + Yl
-    c->price_bytes += price_pass_bytes(d, ny);
+    c->price_bytes += price_pass_bytes(d, ny, c->devex);
     c->price_passes++;
     c->q = (int)best.j;
     c->dq = best.d;
+    c->wq = best.w;
     c->sig = best.d < 0.0 ? 1.0 : -1.0;
 }
 
@@ -850,7 +924,7 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles) {
 // slack candidates itself (a total order: all agree), gathers a_R into LDS and
 // computes alpha_S for its 4 bump rows (one wave per row, wave order).
 // Workgroup 0 publishes q.  Saves a launch and the single-workgroup select.
-__global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_ub, int ny_ub, int dslot) {
+__global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_ub, int dslot) {
     extern __shared__ __attribute__((aligned(16))) double aRs[];  // [k]
     __shared__ Cand red[4];
     RSTAMP(12);
@@ -858,38 +932,29 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_u
     // the control block first (vmcnt retires in issue order: the status test
     // then waits for these loads only, not for the prefetch behind them)
     const int32_t st0 = c->status;
-    const int bland = c->bland, ny = c->ny, k = c->k;
-    const double dtol = c->tol_dual;
+    const int bland = c->bland, k = c->k;
     const int64_t c_iter = c->iter, c_epoch = c->mb_epoch;
     const int32_t c_seq = c->plan_seq;
     // Everything that does not depend on the control block or on q goes out
-    // first (bounded by the host's k_ub / ny_ub, masked below): the tile
-    // candidates, the Y slots' duals and rows, this wave's row of Minv, the R
-    // list.  After the min-loc only the a_R gather is left.
+    // first (bounded by the host's k_ub, masked below): the candidates of the
+    // tiles and of the slacks (candidate [ntiles], k_price's slack workgroup),
+    // this wave's row of Minv, the R list.  After the min-loc only the a_R
+    // gather is left.
     constexpr int PFM = 8;  // Minv values per lane held in registers (k <= 512)
     constexpr int PFR = 4;  // R-list entries per thread (k <= 1024)
-    constexpr int PFC = 4;  // tile candidates per thread (<= 1024 tiles)
-    constexpr int PFY = 4;  // Y slots per thread (|Y| <= 1024)
+    constexpr int PFC = 4;  // candidates per thread (<= 1023 tiles)
+    const int ncand = ntiles + 1;
     const int pr = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63, tid = threadIdx.x;
     const bool pfm = k_ub <= 64 * PFM, pfr = k_ub <= 256 * PFR;
-    const bool pfc = ntiles <= 256 * PFC, pfy = ny_ub <= 256 * PFY;
+    const bool pfc = ncand <= 256 * PFC;
     double mrow[PFM];
     int rl[PFR];
     Cand cc[PFC];
-    int yl[PFY];
-    double yv[PFY];
-    int8_t vs[PFY];
     // (unconditional, no branch around them: a load inside a conditional block
     //  is drained at the block's end; masks are applied where values are used)
 #pragma unroll
-    for (int t = 0; t < PFC; ++t) cc[t] = ld_clamp(d.cand, tid + 256 * t, ntiles);
-#pragma unroll
-    for (int t = 0; t < PFY; ++t) {
-        yl[t] = ld_clamp(d.Yl, tid + 256 * t, ny_ub);
-        yv[t] = ld_clamp(d.yy, tid + 256 * t, ny_ub);
-        vs[t] = ld_clamp(d.yvs, tid + 256 * t, ny_ub);  // the slot's slack status
-    }
+    for (int t = 0; t < PFC; ++t) cc[t] = ld_clamp(d.cand, tid + 256 * t, ncand);
     {
         const double* row = d.Minv + (size_t)(pr < k_ub ? pr : 0) * d.ldm;
 #pragma unroll
@@ -903,11 +968,6 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_u
 #pragma unroll
         for (int t = 0; t < PFC; ++t) KEEP(cc[t].score);
 #pragma unroll
-        for (int t = 0; t < PFY; ++t) {
-            KEEP(yv[t]);
-            KEEP((int)vs[t]);
-        }
-#pragma unroll
         for (int t = 0; t < PFM; ++t) KEEP(mrow[t]);
 #pragma unroll
         for (int t = 0; t < PFR; ++t) KEEP(rl[t]);
@@ -918,41 +978,15 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_u
     best.j = -1;
     best.score = 0.0;
     best.d = 0.0;
+    best.w = 1.0;
     if (pfc) {
 #pragma unroll
         for (int t = 0; t < PFC; ++t)
-            if (tid + 256 * t < ntiles && cand_better(cc[t], best, bland)) best = cc[t];
+            cand_take(best, cc[t], tid + 256 * t < ncand && cand_better(cc[t], best, bland));
     } else {
-        for (int t = tid; t < ntiles; t += 256) {
+        for (int t = tid; t < ncand; t += 256) {
             const Cand o = d.cand[t];
-            if (cand_better(o, best, bland)) best = o;
-        }
-    }
-    // slack candidates (a slack's cost is 0: d = -y)
-    auto slack = [&](int p, int i, double yp, int8_t v) {
-        if (v == VS_FIXED) return;
-        const double dj = 0.0 - yp;
-        Cand o;
-        o.j = -1;
-        if ((v == VS_LOWER || v == VS_FREE) && dj < -dtol) {
-            o.j = d.N + i;
-            o.score = -dj;
-            o.d = dj;
-        } else if ((v == VS_UPPER || v == VS_FREE) && dj > dtol) {
-            o.j = d.N + i;
-            o.score = dj;
-            o.d = dj;
-        }
-        if (cand_better(o, best, bland)) best = o;
-    };
-    if (pfy) {
-#pragma unroll
-        for (int t = 0; t < PFY; ++t)
-            if (tid + 256 * t < ny) slack(tid + 256 * t, yl[t], yv[t], vs[t]);  // (< ny: valid)
-    } else {
-        for (int p = tid; p < ny; p += 256) {
-            const int i = d.Yl[p];
-            slack(p, i, d.yy[p], d.vstat[d.n + i]);
+            cand_take(best, o, cand_better(o, best, bland));
         }
     }
     best = block_best<256>(best, bland, red);
@@ -1046,7 +1080,7 @@ __global__ void __launch_bounds__(256) k_select_global(Dev d) {
     const int bland = c->bland;
     Cand best = d.cand_xchg[0].c;
     for (int r = 1; r < d.world; ++r)
-        if (cand_better(d.cand_xchg[r].c, best, bland)) best = d.cand_xchg[r].c;
+        cand_take(best, d.cand_xchg[r].c, cand_better(d.cand_xchg[r].c, best, bland));
     const int m = d.m;
     if (best.j < 0) {
         for (int i = threadIdx.x; i < m + 4; i += 256) d.pkt[i] = 0.0;
@@ -1268,6 +1302,7 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
         he = d.rhi[i];
     }
     __builtin_amdgcn_sched_barrier(0);  // all of the above issued before any use
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) d.ctl->snap_status = st0;  // for k_ratio
     if (st0 != ST_RUN) {
 #pragma unroll
         for (int t = 0; t < ZCHUNK; ++t) {
@@ -1395,6 +1430,16 @@ DEV bool leave_better(const Leave& a, const Leave& b, int bland) {
     if (bland) return a.r < b.r || (a.r == b.r && a.var < b.var);
     return a.ag > b.ag || (a.ag == b.ag && a.var < b.var);
 }
+// field-wise select (see cand_take)
+DEV void leave_take(Leave& c, const Leave& o, bool take) {
+    c.ag = take ? o.ag : c.ag;
+    c.r = take ? o.r : c.r;
+    c.g = take ? o.g : c.g;
+    c.l = take ? o.l : c.l;
+    c.u = take ? o.u : c.u;
+    c.var = take ? o.var : c.var;
+    c.e = take ? o.e : c.e;
+}
 DEV Leave shfl_leave(const Leave& x, int off) {
     Leave o;
     o.ag = __shfl_xor(x.ag, off);
@@ -1441,10 +1486,10 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     // ---- the control block first: vmcnt retires loads in issue order, so the
     //      status test below then waits for these alone, not for the prefetch
     DevCtl* c = d.ctl;
-    const int32_t st0 = c->status;
+    const int32_t st0 = c->snap_status;  // (not c->status: see DevCtl::snap_status)
     const int m = d.m, k = c->snap_k, q = c->q, ny = c->snap_ny, ncand = c->ncand;
-    const double sig = c->sig, dq = c->dq;
-    const int bland = c->snap_bland;
+    const double sig = c->sig, dq = c->dq, wq = c->wq;
+    const int bland = c->snap_bland, devex = c->devex;
     const int apos_c = c->snap_apos;
     const bool lead = blockIdx.x == 0;
     // bookkeeping scalars, snapshot by k_ftran_zr (see DevCtl)
@@ -1549,7 +1594,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         o.l = cd.l;
         o.u = cd.u;
         o.e = cd.e;
-        if (leave_better(o, best, bland)) best = o;
+        leave_take(best, o, leave_better(o, best, bland));
     };
     if (pfq) {
 #pragma unroll
@@ -1561,13 +1606,16 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         Leave o = shfl_leave(best, off);
-        if (leave_better(o, best, bland)) best = o;
+        leave_take(best, o, leave_better(o, best, bland));
     }
     if ((tid & 63) == 0) lred[tid >> 6] = best;
     __syncthreads();  // also publishes the prefetched scalars
-    best = lred[0];
-    for (int i = 1; i < 4; ++i)
-        if (leave_better(lred[i], best, bland)) best = lred[i];
+    {
+        int win = 0;
+        for (int i = 1; i < 4; ++i)
+            if (leave_better(lred[i], lred[win], bland)) win = i;
+        best = lred[win];
+    }
     RSTAMP(3);
     // ---- decision (uniform across the block)
     const double lbq = sv_lbq, ubq = sv_ubq;
@@ -1617,6 +1665,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
             c->flips = cs_flips + 1;
             c->ndegen = 0;
             c->bland = 0;
+            c->dv_valid = 0;  // a flip changes no reduced cost
             Plan P;
             P.action = ACT_FLIP;
             P.pcase = PC_NONE;
@@ -1793,6 +1842,22 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
             d.xval[lvl] = at_lower ? best.l : best.u;
         }
         if (ql >= 0) d.vstat[ql] = VS_BASIC;
+        if (devex && wq > DEVEX_RESET) {
+            // restart the framework (oracle: every weight 1 now): the next pass
+            // sets the weight of each column it prices; a column basic now is
+            // priced again only after it leaves, which sets its weight (below)
+            if (!leave_art && lvl >= 0) d.dw[lvl] = 1.0;
+            c->dv_valid = 2;
+        } else if (devex) {  // the leaving variable's weight; this pivot for the next pass
+            double wl = wq / (best.g * best.g);
+            if (wl < 1.0) wl = 1.0;
+            if (wl > DEVEX_WMAX) wl = DEVEX_WMAX;
+            if (!leave_art && lvl >= 0) d.dw[lvl] = wl;
+            c->dv_valid = 1;
+            c->dv_lv = lv;
+            c->dv_dq = dq;
+            c->dv_wq = wq;
+        }
         const double cq = sv_cq;
         Plan P;
         P.action = ACT_PIVOT;
@@ -2229,6 +2294,13 @@ __global__ void __launch_bounds__(1024) k_ns_store(Dev d, int k) {
 }
 
 // ============================================================== phase 2 / extract
+// a phase start: the reference framework is the current nonbasic set
+__global__ void k_devex_reset(Dev d) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < (int64_t)d.n + d.m) d.dw[j] = 1.0;
+    if (j == 0) d.ctl->dv_valid = 0;
+}
+
 __global__ void k_phase2(Dev d) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t < d.m) {
@@ -2562,8 +2634,9 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int phase, hipStrea
     unsigned nb_minv = 0, napply = 0;
     if (phase == 2) update_grid(d, k_ub, false, &nb_minv, &napply);
     if (ev0) (void)hipEventRecord(ev0, st);
-    if (d.csc) k_price_csc<<<ntiles + napply, TILE_COLS, 0, st>>>(d, (int)napply, (int)nb_minv);
-    else k_price<<<ntiles + napply, PRICE_THREADS, 0, st>>>(d, (int)napply, (int)nb_minv);
+    // + 1: the slack workgroup (candidate [ntiles])
+    if (d.csc) k_price_csc<<<ntiles + 1 + napply, TILE_COLS, 0, st>>>(d, (int)napply, (int)nb_minv);
+    else k_price<<<ntiles + 1 + napply, PRICE_THREADS, 0, st>>>(d, (int)napply, (int)nb_minv);
     if (ev1) (void)hipEventRecord(ev1, st);
     return hipGetLastError();
 }
@@ -2615,6 +2688,7 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
 
 hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStream_t st,
                             hipEvent_t ev0, hipEvent_t ev1, int dslot) {
+    (void)ny_ub;
     hipError_t e = launch_btran_price(d, k_ub, phase, st, ev0, ev1);
     if (e != hipSuccess) return e;
     const int ntiles = (int)cdiv(d.n, TILE_COLS);
@@ -2623,7 +2697,7 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
         const size_t ldsz = lds > 64 ? lds : 64;  // the timer workgroup reduces in it
         // + the timer workgroup, + the CSC column-scatter workgroup
         const unsigned g = cdiv(k_ub > 0 ? k_ub : 1, 4) + (d.ptimer ? 1 : 0) + (d.csc ? 1 : 0);
-        k_select_ftran<<<g, 256, ldsz, st>>>(d, ntiles, k_ub, ny_ub, dslot);
+        k_select_ftran<<<g, 256, ldsz, st>>>(d, ntiles, k_ub, dslot);
         return launch_iteration_tail(d, k_ub, phase, st, false, dslot);
     }
     k_select<<<1, 1024, 0, st>>>(d, ntiles);
@@ -2709,11 +2783,16 @@ hipError_t launch_refactor_primal(const Dev& d, int k, hipStream_t st) {
     return hipGetLastError();
 }
 
+hipError_t launch_devex_reset(const Dev& d, hipStream_t st) {
+    k_devex_reset<<<cdiv((int64_t)d.n + d.m, 256), 256, 0, st>>>(d);
+    return hipGetLastError();
+}
+
 hipError_t launch_phase2(const Dev& d, hipStream_t st) {
     const int64_t mx = d.m > d.n ? d.m : d.n;
     k_phase2<<<cdiv(mx, 256), 256, 0, st>>>(d);
     if (d.m > 0) k_phase2_cS<<<cdiv(d.m, 256), 256, 0, st>>>(d);
-    return hipGetLastError();
+    return launch_devex_reset(d, st);
 }
 
 hipError_t launch_extract(const Dev& d, double* xout, hipStream_t st) {

@@ -51,6 +51,9 @@ extern "C" {
 
 typedef struct elp_handle elp_handle;
 
+#define ELP_PRICE_DANTZIG 0 /* elp_control.pricing */
+#define ELP_PRICE_DEVEX 1
+
 typedef struct elp_control {
     double tol_primal;       /* Harris primal feasibility tolerance    (1e-9)  */
     double tol_dual;         /* optimality tolerance on |d_j|          (1e-9)  */
@@ -72,7 +75,11 @@ typedef struct elp_control {
                                 (each rank holds its shard, the entering column
                                 travels in an all-reduce) */
     int32_t max_nodes;       /* branch and bound: node limit, <= 0 unlimited   */
-    int32_t reserved[4];
+    int32_t pricing;         /* ELP_PRICE_DEVEX (default): largest d_j^2 / w_j
+                                with Devex reference weights, lp_solve's default
+                                pricer (lp.control(pivoting = "devex"));
+                                ELP_PRICE_DANTZIG: largest |d_j|               */
+    int32_t reserved[3];
 } elp_control;
 
 typedef struct elp_stats {

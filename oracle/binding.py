@@ -30,6 +30,8 @@ class OrcControl(ctypes.Structure):
         ("t_mark_iter", ctypes.c_int64),
         ("refactor_mode", ctypes.c_int32),
         ("price_mode", ctypes.c_int32),
+        ("price_rule", ctypes.c_int32),
+        ("pad0", ctypes.c_int32),
     ]
 
 
@@ -46,6 +48,7 @@ class OrcStats(ctypes.Structure):
         ("price_bytes", ctypes.c_double),
         ("seconds_at_mark", ctypes.c_double),
         ("gj_refactors", ctypes.c_int64),
+        ("devex_resets", ctypes.c_int64),
     ]
 
 

@@ -25,7 +25,12 @@
  *     updated by rank-one / bordered formulas (cases A-E below);
  *   - dual y is zero on slack-covered rows, so pricing sweeps only the
  *     rows Y = {i : slack i nonbasic}, kept as a row-major copy AR;
- *   - Dantzig pricing (largest |d_j|, lowest index on ties), Harris
+ *   - Devex pricing (price_rule 1, the default: largest d_j^2 / w_j with
+ *     reference weights w updated from consecutive passes' reduced costs,
+ *     run_phase) or Dantzig (price_rule 0: largest |d_j|); lowest index on
+ *     ties.  lp_solve's default pricer is DEVEX (lp_solve 5.5 set_pivoting,
+ *     PRICER_DEVEX + PRICE_ADAPTIVE); its exact weight recurrences are not in
+ *     the reference, so this restatement defines the arithmetic.  Harris
  *     two-pass ratio test (largest |alpha|, lowest variable id on ties),
  *     bound flips, Bland fallback after a run of degenerate pivots,
  *     Gauss-Jordan refactor of M every refactor_period pivots;
@@ -46,6 +51,8 @@
 #define PRICE_SPLIT 8
 #define ZCHUNK 32
 #define WAVE 64
+#define DEVEX_WMAX 1e20   /* Devex weight cap (both sides of the parity contract) */
+#define DEVEX_RESET 1e6   /* entering weight above this: new reference framework */
 
 /* ------------------------------------------------------------------ */
 /* synthetic generator (bit-identical in HIP and numpy)                */
@@ -109,6 +116,8 @@ typedef struct {
     int64_t *cp, *ri; /* price_mode 1: nonzero pattern of A by column      */
     int64_t gj_count; /* refactors that needed a fresh Gauss-Jordan */
     int refactor_mode;
+    double *dw, *dprev; /* price_rule 1: Devex weight and last reduced cost
+                           of each structural and slack (n + m)            */
 } orc_t;
 
 static double* dalloc(size_t n) { return (double*)calloc(n ? n : 1, sizeof(double)); }
@@ -332,6 +341,21 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
      * phase start and after every refactor.  Optimality found with updated
      * duals is re-checked after a refactor (recheck: no loop-top checks). */
     int y_valid = 0, recheck = 0;
+    /* Devex (price_rule 1): reference framework = the nonbasic set at the
+     * phase start (all weights 1).  After a pivot with entering q (reduced
+     * cost d_q, weight w_q) the next pricing pass has d_j' = d_j - (d_q /
+     * alpha_rq) alpha_rj, so the pivot-row ratio alpha_rj / alpha_rq is
+     * (d_j - d_j') / d_q -- read off the two passes' reduced costs without
+     * forming the pivot row -- and w_j = max(w_j, (alpha_rj / alpha_rq)^2 w_q);
+     * the leaving variable takes max(w_q / alpha_rq^2, 1).  Bound flips change
+     * no d (dv_valid = 0).  Weights are capped at DEVEX_WMAX; a pivot whose
+     * entering weight exceeds DEVEX_RESET restarts the framework (all 1). */
+    const int devex = ctl->price_rule == 1;
+    int dv_valid = 0;
+    int64_t dv_lv = -1;
+    double dv_dq = 1.0, dv_wq = 1.0;
+    if (devex)
+        for (int64_t j = 0; j < n + m; ++j) s->dw[j] = 1.0;
     for (;;) {
         if (*iter == ctl->t_mark_iter && st->seconds_at_mark == 0.0) {
             struct timespec tm;
@@ -403,7 +427,7 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
         st->price_bytes += 8.0 * ((double)ny * (double)n + (double)n + (double)ny);
         }
         int64_t q = -1;
-        double qscore = 0.0, dq = 0.0;
+        double qscore = 0.0, dq = 0.0, qw = 1.0;
         const double dtol = ctl->tol_dual;
         for (int64_t j = 0; j < n + m; ++j) {
             const int8_t vs = s->vstat[j];
@@ -416,19 +440,38 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
             } else {
                 d = s->cost[j] - s->y[j - n];
             }
+            double wj = 1.0;
+            if (devex) { /* every priced column, eligible or not */
+                wj = s->dw[j];
+                if (dv_valid && j != dv_lv) {
+                    const double r = (s->dprev[j] - d) / dv_dq;
+                    double wn = (r * r) * dv_wq;
+                    if (wn > DEVEX_WMAX) wn = DEVEX_WMAX;
+                    if (wn > wj) {
+                        wj = wn;
+                        s->dw[j] = wj;
+                    }
+                }
+                s->dprev[j] = d;
+            }
             double score = 0.0;
-            if ((vs == VS_LOWER || vs == VS_FREE) && d < -dtol) score = -d;
-            else if ((vs == VS_UPPER || vs == VS_FREE) && d > dtol) score = d;
+            if ((vs == VS_LOWER || vs == VS_FREE) && d < -dtol) score = devex ? (d * d) / wj : -d;
+            else if ((vs == VS_UPPER || vs == VS_FREE) && d > dtol) score = devex ? (d * d) / wj : d;
             else continue;
-            if (bland) {
-                q = j;
-                dq = d;
-                break;
+            if (bland) { /* lowest eligible index (Devex keeps updating weights) */
+                if (q < 0) {
+                    q = j;
+                    dq = d;
+                    qw = wj;
+                }
+                if (!devex) break;
+                continue;
             }
             if (score > qscore) {
                 qscore = score;
                 q = j;
                 dq = d;
+                qw = wj;
             }
         }
         if (q < 0) {
@@ -512,6 +555,7 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
                 trace[2 * (*iter - 1)] = q;
                 trace[2 * (*iter - 1) + 1] = -1;
             }
+            dv_valid = 0;
             ndegen = 0;
             bland = 0;
             continue;
@@ -528,6 +572,22 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
         if (trace && *iter - 1 < trace_cap) {
             trace[2 * (*iter - 1)] = q;
             trace[2 * (*iter - 1) + 1] = lv;
+        }
+        if (devex && qw > DEVEX_RESET) {
+            /* the weights have outgrown the framework: restart it from the
+             * current nonbasic set (all weights 1, no update next pass) */
+            for (int64_t j = 0; j < n + m; ++j) s->dw[j] = 1.0;
+            dv_valid = 0;
+            st->devex_resets++;
+        } else if (devex) { /* the leaving variable's weight; this pivot for the next pass */
+            double wl = qw / (lg * lg);
+            if (wl < 1.0) wl = 1.0;
+            if (wl > DEVEX_WMAX) wl = DEVEX_WMAX;
+            if (lv < n + m) s->dw[lv] = wl;
+            dv_valid = 1;
+            dv_lv = lv;
+            dv_dq = dq;
+            dv_wq = qw;
         }
         if (theta == 0.0) {
             st->degenerate++;
@@ -829,6 +889,8 @@ void orc_default_control(orc_control* c) {
     c->t_mark_iter = -1;
     c->refactor_mode = 0;
     c->price_mode = 0;
+    c->price_rule = 1;
+    c->pad0 = 0;
 }
 
 static int cmp_i64(const void* a, const void* b) {
@@ -915,6 +977,8 @@ int orc_solve_dense_sens(int64_t m, int64_t n, const double* A, const int32_t* d
     s->part = dalloc((size_t)PRICE_SPLIT * (size_t)n);
     s->used = (int8_t*)calloc((size_t)mm, 1);
     s->perm = ialloc((size_t)mm);
+    s->dw = dalloc((size_t)(n + m));
+    s->dprev = dalloc((size_t)(n + m));
 
     int status = 0;
     int64_t unb_var = -1;
@@ -1050,6 +1114,7 @@ int orc_solve_dense_sens(int64_t m, int64_t n, const double* A, const int32_t* d
     free(s->xr); free(s->xs); free(s->Minv); free(s->Yl); free(s->ypos); free(s->AR);
     free(s->y); free(s->t); free(s->yR); free(s->yy); free(s->acol); free(s->aR);
     free(s->alS); free(s->alU); free(s->z); free(s->v); free(s->tmp); free(s->part);
+    free(s->dw); free(s->dprev);
     free(s->used); free(s->perm); free(s->cp); free(s->ri);
     return status;
 }

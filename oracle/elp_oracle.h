@@ -43,6 +43,9 @@ typedef struct orc_control {
     int32_t price_mode;    /* 0 dense: chunked AR sweep over the Y rows;
                               1 CSC path: one fma chain per column over its
                               nonzero rows in ascending order (elp_load_csc)  */
+    int32_t price_rule;    /* 0 Dantzig (largest |d_j|), 1 Devex reference
+                              weights (largest d_j^2 / w_j; run_phase)        */
+    int32_t pad0;
 } orc_control;
 
 typedef struct orc_stats {
@@ -57,6 +60,7 @@ typedef struct orc_stats {
     double price_bytes;    /* sum over iterations of 8*(|Y|*n + n + |Y|)      */
     double seconds_at_mark;
     int64_t gj_refactors;  /* refactors that fell back to Gauss-Jordan      */
+    int64_t devex_resets;  /* Devex reference-framework restarts            */
 } orc_stats;
 
 void orc_default_control(orc_control* c);

@@ -53,10 +53,12 @@ def transport_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def sharded_solve_worker(rank, world, port, q, cases, replicate=0, p2p=False):
+def sharded_solve_worker(rank, world, port, q, cases, replicate=0, p2p=False, ctl=None):
     """GPU: every rank solves the same LPs on one shared GPU with the host transport.
     replicate: elp_control.replicate (1 every rank holds all of A, 2 shards only);
-    p2p: the per-iteration min-loc over the IPC mailbox instead of the transport."""
+    p2p: the per-iteration min-loc over the IPC mailbox instead of the transport;
+    ctl: further elp_control fields (e.g. pricing)."""
+    ctl = dict(ctl or {})
     import numpy as np
     dist = _init(rank, world, port)
     import easylp_amd
@@ -66,7 +68,7 @@ def sharded_solve_worker(rank, world, port, q, cases, replicate=0, p2p=False):
     for case in cases:
         if case["kind"] == "generated":
             m, n = case["m"], case["n"]
-            p = easylp_amd.Problem(m, n, replicate=replicate)
+            p = easylp_amd.Problem(m, n, replicate=replicate, **ctl)
             p.set_trace(200000)
             p.comm_init_host(t)
             if p2p:
@@ -74,7 +76,7 @@ def sharded_solve_worker(rank, world, port, q, cases, replicate=0, p2p=False):
             p.load_generated(case["seed"])
         else:
             A, dirs, rhs, obj, lo, up, mx = case["lp"]
-            p = easylp_amd.Problem(A.shape[0], A.shape[1], replicate=replicate)
+            p = easylp_amd.Problem(A.shape[0], A.shape[1], replicate=replicate, **ctl)
             p.set_trace(200000)
             p.comm_init_host(t)
             if p2p:

@@ -59,15 +59,21 @@ def test_known_answers_csc(gpu, rec):
     _same(g, o)
 
 
-def test_klee_minty_12(gpu):
-    """Degenerate-path case: 2^12 - 1 Dantzig pivots to the optimum 5^12."""
+@pytest.mark.parametrize("rule", [0, 1], ids=["dantzig", "devex"])
+def test_klee_minty_12(gpu, rule):
+    """Degenerate-path case: 2^12 - 1 Dantzig pivots to the optimum 5^12;
+    Devex weights take a short path to it."""
     from make_sparse import klee_minty
     from oracle import solve_dense as orc
     A, dirs, rhs, obj, lo, up, mx = klee_minty(12)
-    g = gpu.solve_sparse(A, dirs, rhs, obj, lo, up, mx, trace=10000)
-    o = orc(A.toarray(), dirs, rhs, obj, lo, up, mx, trace_cap=10000, price_mode=1)
+    g = gpu.solve_sparse(A, dirs, rhs, obj, lo, up, mx, trace=10000, pricing=rule)
+    o = orc(A.toarray(), dirs, rhs, obj, lo, up, mx, trace_cap=10000, price_mode=1, price_rule=rule)
     _same(g, o)
-    assert g.objval == 5.0 ** 12 and g.stats["iterations"] == 2 ** 12 - 1
+    assert g.objval == 5.0 ** 12
+    if rule == 0:
+        assert g.stats["iterations"] == 2 ** 12 - 1
+    else:
+        assert g.stats["iterations"] < 2 ** 12 // 8
 
 
 @pytest.mark.parametrize("kind", ["packing", "general"])

@@ -14,10 +14,11 @@ KNOWN = load_known_answers()
 DENSE = load_dense_lps()
 
 
+@pytest.mark.parametrize("rule", [1, 0], ids=["devex", "dantzig"])
 @pytest.mark.parametrize("rec", KNOWN, ids=[r["name"] for r in KNOWN])
-def test_known_answer(rec):
+def test_known_answer(rec, rule):
     r = solve_dense(rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"],
-                    rec["maximize"])
+                    rec["maximize"], price_rule=rule)
     exp = rec["expected"]
     assert r.status == exp["status"]
     if r.status == 3:
@@ -39,10 +40,11 @@ def test_known_answer(rec):
 
 @pytest.mark.parametrize("rec", [d for d in DENSE if d["m"] <= 500],
                          ids=[f"s{d['seed']}_{d['m']}x{d['n']}" for d in DENSE if d["m"] <= 500])
-def test_dense_vs_highs(rec):
+@pytest.mark.parametrize("rule", [1, 0], ids=["devex", "dantzig"])
+def test_dense_vs_highs(rec, rule):
     m, n = rec["m"], rec["n"]
     A, b, c = generate_dense(rec["seed"], m, n)
-    r = solve_dense(A, np.ones(m, np.int32), b, c, maximize=True)
+    r = solve_dense(A, np.ones(m, np.int32), b, c, maximize=True, price_rule=rule)
     assert r.status == 0
     assert abs(r.objval - rec["objective"]) <= 1e-8 * abs(rec["objective"])
     x = np.zeros(n)

@@ -34,9 +34,14 @@ def test_known_answers_column_order(rec):
 
 @pytest.mark.parametrize("n", [4, 7, 10])
 def test_klee_minty_exponential_path(n):
-    """Dantzig's rule walks all 2^n vertices of the Klee-Minty cube."""
+    """Dantzig's rule walks all 2^n vertices of the Klee-Minty cube; Devex
+    weights (the default) take a short path to the same optimum."""
     from oracle import solve_dense as orc
     rec = next(r for r in SPARSE if r["name"] == f"klee_minty_{n}")
-    o = orc(rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], True, price_mode=1)
+    args = (rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], True)
+    o = orc(*args, price_mode=1, price_rule=0)
     assert o.status == 0 and o.objval == 5.0 ** n
     assert o.stats["iterations"] == 2 ** n - 1
+    v = orc(*args, price_mode=1)
+    assert v.status == 0 and v.objval == 5.0 ** n
+    assert v.stats["iterations"] <= 6 * n  # 9, 21, 51 for n = 4, 7, 10
