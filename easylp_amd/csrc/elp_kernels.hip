@@ -483,14 +483,16 @@ DEV DevexIn devex_in(const DevCtl* c) {
     x.wq = c->dv_wq;
     return x;
 }
-// jl: local id (dw / dprev index), jg: global id
-DEV double devex_weight(const Dev& d, const DevexIn& x, int64_t jl, int64_t jg, double dj) {
-    double wj = d.dw[jl];
+// jl: local id (dw / dprev index), jg: global id; w0 / dp0: dw[jl], dprev[jl]
+// as loaded by the caller (issued early, off the dependent tail)
+DEV double devex_weight(const Dev& d, const DevexIn& x, int64_t jl, int64_t jg, double dj, double w0,
+                        double dp0) {
+    double wj = w0;
     if (x.valid == 2) {  // framework restart (k_ratio): weight 1, no update
         wj = 1.0;
         d.dw[jl] = 1.0;
     } else if (x.valid == 1 && jg != x.lv) {
-        const double r = (d.dprev[jl] - dj) / x.dq;
+        const double r = (dp0 - dj) / x.dq;
         double wn = (r * r) * x.wq;
         if (wn > DEVEX_WMAX) wn = DEVEX_WMAX;
         if (wn > wj) {
@@ -536,7 +538,7 @@ DEV void price_slacks(const Dev& d, int64_t slot, Cand* red) {
         if (v == VS_FIXED) continue;
         const int i = d.Yl[p];
         const double dj = 0.0 - d.yy[p];
-        const double wj = devex ? devex_weight(d, dx, d.n + i, d.N + i, dj) : 1.0;
+        const double wj = devex ? devex_weight(d, dx, d.n + i, d.N + i, dj, d.dw[d.n + i], d.dprev[d.n + i]) : 1.0;
         const Cand o = price_cand(v, dj, wj, devex, dtol, d.N + i);
         cand_take(best, o, cand_better(o, best, bland));
     }
@@ -566,6 +568,16 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int napply, int 
     const int ny = c->ny, bland = c->bland;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // the tile's per-column operands of the epilogue (status, cost, Devex weight
+    // and previous d) go out before the sweep, so the epilogue waits for none
+    // of them (every wave loads, clamped: no branch to drain; waves 0-1 use them)
+    const int64_t jt = (int64_t)blockIdx.x * TILE_COLS + (threadIdx.x & (TILE_COLS - 1));
+    const int64_t jc = jt < d.n ? jt : 0;
+    const int devex = c->devex;
+    const DevexIn dx = devex_in(c);
+    const double dtol = c->tol_dual;
+    const int8_t pf_vs = d.vstat[jc];
+    const double pf_c = d.cost[jc], pf_w = d.dw[jc], pf_dp = d.dprev[jc];
     const int L = (ny + PRICE_SPLIT - 1) / PRICE_SPLIT;
     const int p0 = w * L;
     const int p1 = min(ny, p0 + L);
@@ -611,17 +623,16 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int napply, int 
     best.d = 0.0;
     best.w = 1.0;
     if (threadIdx.x < TILE_COLS) {
-        const int64_t j = (int64_t)blockIdx.x * TILE_COLS + threadIdx.x;
+        const int64_t j = jt;
         if (j < d.n) {
-            const int8_t vs = d.vstat[j];
+            const int8_t vs = pf_vs;
             if (vs != VS_BASIC && vs != VS_FIXED) {
                 double tot = 0.0;
 #pragma unroll
                 for (int ww = 0; ww < PRICE_SPLIT; ++ww) tot = tot + part[ww][threadIdx.x];
-                const double dj = d.cost[j] - tot;
-                const int devex = c->devex;
-                const double wj = devex ? devex_weight(d, devex_in(c), j, d.col0 + j, dj) : 1.0;
-                best = price_cand(vs, dj, wj, devex, c->tol_dual, d.col0 + j);
+                const double dj = pf_c - tot;
+                const double wj = devex ? devex_weight(d, dx, j, d.col0 + j, dj, pf_w, pf_dp) : 1.0;
+                best = price_cand(vs, dj, wj, devex, dtol, d.col0 + j);
             }
         }
     }
@@ -693,7 +704,7 @@ __global__ void __launch_bounds__(TILE_COLS) k_price_csc(Dev d, int napply, int 
         if (vs != VS_BASIC && vs != VS_FIXED) {
             const double dj = d.cost[j] - acc;
             const int devex = c->devex;
-            const double wj = devex ? devex_weight(d, devex_in(c), j, d.col0 + j, dj) : 1.0;
+            const double wj = devex ? devex_weight(d, devex_in(c), j, d.col0 + j, dj, d.dw[j], d.dprev[j]) : 1.0;
             best = price_cand(vs, dj, wj, devex, c->tol_dual, d.col0 + j);
         }
     }
