@@ -248,7 +248,8 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.pivstep, mm));
     A(dalloc(&d.nzlist, n));
     A(dalloc(&d.nzcount, 1));
-    A(dalloc(&d.cand, (size_t)((n + TILE_COLS - 1) / TILE_COLS) + 64));
+    // tile candidates + the slack workgroups' (|Y| <= m, >= 128 slots each)
+    A(dalloc(&d.cand, (size_t)((n + TILE_COLS - 1) / TILE_COLS) + (size_t)((mm + TILE_COLS - 1) / TILE_COLS) + 64));
     A(dalloc(&d.pstamp, 2 * ((size_t)((n + TILE_COLS - 1) / TILE_COLS) + 64)));
     if (h->csc) A(dalloc(&d.qcol, mm));
     if (std::getenv("ELP_STAMPS")) A(dalloc(&d.dstamp, 16 * 64));

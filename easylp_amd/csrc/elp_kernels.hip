@@ -520,10 +520,11 @@ DEV Cand price_cand(int8_t vs, double dj, double wj, int devex, double dtol, int
     return o;
 }
 // The slack candidates (replicated on every rank; a slack's cost is 0, so
-// d = -y on the Y slots, in slot order): one extra workgroup of the pricing
-// launch, written as candidate [ntiles] next to the tiles'
+// d = -y on the Y slots, in slot order): nsw extra workgroups of the pricing
+// launch (the host sizes them from its bound on |Y|: one slot per thread),
+// workgroup s writing candidate [ntiles + s] next to the tiles'
 template <int NT>
-DEV void price_slacks(const Dev& d, int64_t slot, Cand* red) {
+DEV void price_slacks(const Dev& d, int64_t ntiles, int s, int nsw, Cand* red) {
     const DevCtl* c = d.ctl;
     const int ny = c->ny, bland = c->bland, devex = c->devex;
     const double dtol = c->tol_dual;
@@ -533,7 +534,7 @@ DEV void price_slacks(const Dev& d, int64_t slot, Cand* red) {
     best.score = 0.0;
     best.d = 0.0;
     best.w = 1.0;
-    for (int p = threadIdx.x; p < ny; p += NT) {
+    for (int p = s * NT + threadIdx.x; p < ny; p += nsw * NT) {
         const int8_t v = d.yvs[p];
         if (v == VS_FIXED) continue;
         const int i = d.Yl[p];
@@ -543,7 +544,7 @@ DEV void price_slacks(const Dev& d, int64_t slot, Cand* red) {
         cand_take(best, o, cand_better(o, best, bland));
     }
     best = block_best<NT>(best, bland, red);
-    if (threadIdx.x == 0) d.cand[slot] = best;
+    if (threadIdx.x == 0) d.cand[ntiles + s] = best;
 }
 
 // One workgroup = 8 waves = 128 columns x all Y slots.  Wave w sweeps slot
@@ -553,15 +554,15 @@ DEV void price_slacks(const Dev& d, int64_t slot, Cand* red) {
 // contiguous yy[] written by BTRAN (wave-uniform scalar loads).  The chunk
 // partials are combined in LDS in chunk order, then the tile's argmin.
 constexpr int PRICE_THREADS = 64 * PRICE_SPLIT;
-__global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int napply, int nb_minv) {
+__global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int napply, int nb_minv, int nsw) {
     __shared__ double part[PRICE_SPLIT][TILE_COLS];
     __shared__ Cand red[PRICE_SPLIT];
     if (apply_role(d, napply, nb_minv)) return;
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
-    const int64_t ntiles = gridDim.x - napply - 1;
-    if ((int64_t)blockIdx.x == ntiles) {  // the slack workgroup
-        price_slacks<PRICE_THREADS>(d, ntiles, red);
+    const int64_t ntiles = gridDim.x - napply - nsw;
+    if ((int64_t)blockIdx.x >= ntiles) {  // a slack workgroup
+        price_slacks<PRICE_THREADS>(d, ntiles, (int)(blockIdx.x - ntiles), nsw, red);
         return;
     }
     if (d.ptimer && threadIdx.x == 0) d.pstamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -660,15 +661,15 @@ DEV double price_pass_bytes(const Dev& d, int ny, int devex) {
 // row order (oracle price_mode 1).  Tiles with more than CSC_STAGE nonzeros
 // read straight from global memory (same order).
 constexpr int CSC_STAGE = 2048;  // staged nonzeros per tile: 32 KiB of LDS
-__global__ void __launch_bounds__(TILE_COLS) k_price_csc(Dev d, int napply, int nb_minv) {
+__global__ void __launch_bounds__(TILE_COLS) k_price_csc(Dev d, int napply, int nb_minv, int nsw) {
     __shared__ double sv[CSC_STAGE], sy[CSC_STAGE];
     __shared__ Cand red[TILE_COLS / 64];
     if (apply_role(d, napply, nb_minv)) return;
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
-    const int64_t ntiles = gridDim.x - napply - 1;
-    if ((int64_t)blockIdx.x == ntiles) {  // the slack workgroup
-        price_slacks<TILE_COLS>(d, ntiles, red);
+    const int64_t ntiles = gridDim.x - napply - nsw;
+    if ((int64_t)blockIdx.x >= ntiles) {  // a slack workgroup
+        price_slacks<TILE_COLS>(d, ntiles, (int)(blockIdx.x - ntiles), nsw, red);
         return;
     }
     if (d.ptimer && threadIdx.x == 0) d.pstamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -862,7 +863,7 @@ DEV bool p2p_exchange(const Dev& d, Cand& best, int bland, int64_t iter, int64_t
 // Min-loc over this shard's tile candidates and the (replicated) slack
 // candidates.  One GPU: decide q and form a_R.  Sharded: write the local best
 // to cand_xchg[rank] for the all-gather (k_select_global decides).
-DEV Cand local_best(const Dev& d, int ntiles, Cand* red) {
+DEV Cand local_best(const Dev& d, int ncand, Cand* red) {
     const DevCtl* c = d.ctl;
     const int bland = c->bland;
     Cand best;
@@ -870,7 +871,7 @@ DEV Cand local_best(const Dev& d, int ntiles, Cand* red) {
     best.score = 0.0;
     best.d = 0.0;
     best.w = 1.0;
-    for (int t = threadIdx.x; t <= ntiles; t += 1024) {  // [ntiles]: the slacks
+    for (int t = threadIdx.x; t < ncand; t += 1024) {  // tiles, then the slack workgroups'
         const Cand o = d.cand[t];
         cand_take(best, o, cand_better(o, best, bland));
     }
@@ -901,12 +902,12 @@ DEV void gather_aR(const Dev& d, int q, const double* qcol) {
     }
 }
 
-__global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles) {
+__global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles, int nsw) {
     __shared__ Cand red[16];
     DevCtl* c = d.ctl;
     if (threadIdx.x == 0) c->applied_seq = c->plan_seq;  // the pricing launch applied it
     if (c->status != ST_RUN) return;
-    Cand best = local_best(d, ntiles, red);
+    Cand best = local_best(d, ntiles + nsw, red);
     if (d.p2p) {  // column-sharded: global min-loc over the xGMI mailbox
         __shared__ CandX s_rec[MAX_P2P];
         __shared__ int s_fail;
@@ -935,7 +936,7 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles) {
 // slack candidates itself (a total order: all agree), gathers a_R into LDS and
 // computes alpha_S for its 4 bump rows (one wave per row, wave order).
 // Workgroup 0 publishes q.  Saves a launch and the single-workgroup select.
-__global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_ub, int dslot) {
+__global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw, int k_ub, int dslot) {
     extern __shared__ __attribute__((aligned(16))) double aRs[];  // [k]
     __shared__ Cand red[4];
     RSTAMP(12);
@@ -948,13 +949,13 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_u
     const int32_t c_seq = c->plan_seq;
     // Everything that does not depend on the control block or on q goes out
     // first (bounded by the host's k_ub, masked below): the candidates of the
-    // tiles and of the slacks (candidate [ntiles], k_price's slack workgroup),
+    // tiles and of the slacks (candidates [ntiles, ntiles + nsw), k_price's slack workgroups),
     // this wave's row of Minv, the R list.  After the min-loc only the a_R
     // gather is left.
     constexpr int PFM = 8;  // Minv values per lane held in registers (k <= 512)
     constexpr int PFR = 4;  // R-list entries per thread (k <= 1024)
     constexpr int PFC = 4;  // candidates per thread (<= 1023 tiles)
-    const int ncand = ntiles + 1;
+    const int ncand = ntiles + nsw;
     const int pr = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63, tid = threadIdx.x;
     const bool pfm = k_ub <= 64 * PFM, pfr = k_ub <= 256 * PFR;
@@ -1061,12 +1062,12 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int k_u
     RSTAMP(15);
 }
 
-__global__ void __launch_bounds__(1024) k_select_local(Dev d, int ntiles, int rank) {
+__global__ void __launch_bounds__(1024) k_select_local(Dev d, int ntiles, int nsw, int rank) {
     __shared__ Cand red[16];
     DevCtl* c = d.ctl;
     if (threadIdx.x == 0) c->applied_seq = c->plan_seq;  // applied by k_price
     if (c->status != ST_RUN) return;
-    const Cand best = local_best(d, ntiles, red);
+    const Cand best = local_best(d, ntiles + nsw, red);
     if (threadIdx.x == 0) {
         CandX x;
         x.c = best;
@@ -2625,7 +2626,12 @@ static void update_grid(const Dev& d, int k_ub, bool with_ar, unsigned* nb_minv,
     *nb = *nb_minv + nb_copy;
 }
 
-static hipError_t launch_btran_price(const Dev& d, int k_ub, int phase, hipStream_t st,
+// slack workgroups of the pricing launch for |Y| <= ny_ub
+static int slack_wgs(const Dev& d, int ny_ub) {
+    return (int)cdiv(ny_ub > 0 ? ny_ub : 1, d.csc ? TILE_COLS : PRICE_THREADS);
+}
+
+static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phase, hipStream_t st,
                                      hipEvent_t ev0, hipEvent_t ev1) {
     const int m = d.m;
     const double* tv = d.cS;
@@ -2645,9 +2651,10 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int phase, hipStrea
     unsigned nb_minv = 0, napply = 0;
     if (phase == 2) update_grid(d, k_ub, false, &nb_minv, &napply);
     if (ev0) (void)hipEventRecord(ev0, st);
-    // + 1: the slack workgroup (candidate [ntiles])
-    if (d.csc) k_price_csc<<<ntiles + 1 + napply, TILE_COLS, 0, st>>>(d, (int)napply, (int)nb_minv);
-    else k_price<<<ntiles + 1 + napply, PRICE_THREADS, 0, st>>>(d, (int)napply, (int)nb_minv);
+    // + nsw: the slack workgroups (candidates [ntiles, ntiles + nsw))
+    const int nsw = slack_wgs(d, ny_ub);
+    if (d.csc) k_price_csc<<<ntiles + nsw + napply, TILE_COLS, 0, st>>>(d, (int)napply, (int)nb_minv, nsw);
+    else k_price<<<ntiles + nsw + napply, PRICE_THREADS, 0, st>>>(d, (int)napply, (int)nb_minv, nsw);
     if (ev1) (void)hipEventRecord(ev1, st);
     return hipGetLastError();
 }
@@ -2699,28 +2706,26 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
 
 hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStream_t st,
                             hipEvent_t ev0, hipEvent_t ev1, int dslot) {
-    (void)ny_ub;
-    hipError_t e = launch_btran_price(d, k_ub, phase, st, ev0, ev1);
+    hipError_t e = launch_btran_price(d, k_ub, ny_ub, phase, st, ev0, ev1);
     if (e != hipSuccess) return e;
-    const int ntiles = (int)cdiv(d.n, TILE_COLS);
+    const int ntiles = (int)cdiv(d.n, TILE_COLS), nsw = slack_wgs(d, ny_ub);
     const size_t lds = (size_t)k_ub * sizeof(double);
     if (lds <= 48 * 1024 && !d.force_select) {  // fused select + bump FTRAN
         const size_t ldsz = lds > 64 ? lds : 64;  // the timer workgroup reduces in it
         // + the timer workgroup, + the CSC column-scatter workgroup
         const unsigned g = cdiv(k_ub > 0 ? k_ub : 1, 4) + (d.ptimer ? 1 : 0) + (d.csc ? 1 : 0);
-        k_select_ftran<<<g, 256, ldsz, st>>>(d, ntiles, k_ub, dslot);
+        k_select_ftran<<<g, 256, ldsz, st>>>(d, ntiles, nsw, k_ub, dslot);
         return launch_iteration_tail(d, k_ub, phase, st, false, dslot);
     }
-    k_select<<<1, 1024, 0, st>>>(d, ntiles);
+    k_select<<<1, 1024, 0, st>>>(d, ntiles, nsw);
     return launch_iteration_tail(d, k_ub, phase, st, true, dslot);
 }
 
 hipError_t launch_iteration_head(const Dev& d, int k_ub, int ny_ub, int phase, int rank,
                                  hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
-    (void)ny_ub;
-    hipError_t e = launch_btran_price(d, k_ub, phase, st, ev0, ev1);
+    hipError_t e = launch_btran_price(d, k_ub, ny_ub, phase, st, ev0, ev1);
     if (e != hipSuccess) return e;
-    k_select_local<<<1, 1024, 0, st>>>(d, (int)cdiv(d.n, TILE_COLS), rank);
+    k_select_local<<<1, 1024, 0, st>>>(d, (int)cdiv(d.n, TILE_COLS), slack_wgs(d, ny_ub), rank);
     return hipGetLastError();
 }
 
