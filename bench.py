@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--sparse-cpu-iters", type=int, default=200)
     ap.add_argument("--pricing", choices=["devex", "dantzig"], default="devex",
                     help="pricing rule (elp_control.pricing; devex is lp_solve's default)")
+    ap.add_argument("--sync-every", type=int, default=32,
+                    help="iterations enqueued between host polls (elp_control.sync_every)")
     ap.add_argument("--compare-rules", type=int, default=1,
                     help="N=1: also solve the LP to optimality with the other pricing rule")
     a = ap.parse_args()
@@ -245,7 +247,7 @@ def main():
 
     lib = load()
     verbose = ELP_PROFILE_PRICE if args.profile_price else 0
-    p = Problem(args.m, args.n, device=local, verbose=verbose, pricing=args.rule)
+    p = Problem(args.m, args.n, device=local, verbose=verbose, pricing=args.rule, sync_every=args.sync_every)
     if world > 1 or args.force_sharded:
         from easylp_amd.dist import share_unique_id
         p.comm_init(share_unique_id(lib, rank), world, rank)
@@ -304,7 +306,7 @@ def main():
     other = None  # the same LP to optimality under the other pricing rule
     if args.compare_rules and world == 1 and not args.no_optimal and not args.force_sharded:
         p.close()
-        q = Problem(args.m, args.n, device=local, pricing=1 - args.rule)
+        q = Problem(args.m, args.n, device=local, pricing=1 - args.rule, sync_every=args.sync_every)
         q.load_generated(args.seed)
         qst = q.solve()
         qs = q.stats()

@@ -9,7 +9,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libeasylp_hip.so")
+LIB_PATH = os.environ.get("ELP_LIB_PATH") or os.path.join(HERE, "lib", "libeasylp_hip.so")
 
 ELP_LE, ELP_GE, ELP_EQ = 1, 2, 3
 ELP_OPTIMAL, ELP_SUBOPTIMAL, ELP_INFEASIBLE, ELP_UNBOUNDED = 0, 1, 2, 3

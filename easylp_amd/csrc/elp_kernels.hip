@@ -554,6 +554,10 @@ DEV void price_slacks(const Dev& d, int64_t ntiles, int s, int nsw, Cand* red) {
 // contiguous yy[] written by BTRAN (wave-uniform scalar loads).  The chunk
 // partials are combined in LDS in chunk order, then the tile's argmin.
 constexpr int PRICE_THREADS = 64 * PRICE_SPLIT;
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+// plain (cached) loads: the live AR rows (~80 MB at 5000x50000) stay in the
+// 256 MiB Infinity Cache between passes; non-temporal loads measured 10% slower
+#define AR_LOAD(ptr) (*reinterpret_cast<const dbl2*>(ptr))
 __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int napply, int nb_minv, int nsw) {
     __shared__ double part[PRICE_SPLIT][TILE_COLS];
     __shared__ Cand red[PRICE_SPLIT];
@@ -589,10 +593,10 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int napply, int 
     int p = p0;
     constexpr int UNR = 16;  // rows in flight per wave: 16 KiB (32 measured slower)
     for (; p + UNR <= p1; p += UNR) {
-        double2 v[UNR];
+        dbl2 v[UNR];
 #pragma unroll
         for (int u = 0; u < UNR; ++u)
-            v[u] = *reinterpret_cast<const double2*>(col + (size_t)(p + u) * TILE_COLS);
+            v[u] = AR_LOAD(col + (size_t)(p + u) * TILE_COLS);
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
             const double yv = yy[p + u];
@@ -601,11 +605,10 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int napply, int 
         }
     }
     if (p < p1) {  // remainder: same order, loads issued together
-        double2 v[UNR];
+        dbl2 v[UNR];
 #pragma unroll
         for (int u = 0; u < UNR; ++u)
-            v[u] = (p + u < p1) ? *reinterpret_cast<const double2*>(col + (size_t)(p + u) * TILE_COLS)
-                                : make_double2(0.0, 0.0);
+            v[u] = (p + u < p1) ? AR_LOAD(col + (size_t)(p + u) * TILE_COLS) : dbl2{0.0, 0.0};
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
             if (p + u < p1) {
