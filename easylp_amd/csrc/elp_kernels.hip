@@ -591,7 +591,10 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int napply, int 
     const double* __restrict__ yy = d.yy;
     double acc0 = 0.0, acc1 = 0.0;
     int p = p0;
-    constexpr int UNR = 16;  // rows in flight per wave: 16 KiB (32 measured slower)
+#ifndef ELP_PRICE_UNR
+#define ELP_PRICE_UNR 16
+#endif
+    constexpr int UNR = ELP_PRICE_UNR;  // rows in flight per wave: 16 KiB (32 measured slower)
     for (; p + UNR <= p1; p += UNR) {
         dbl2 v[UNR];
 #pragma unroll
