@@ -2622,12 +2622,16 @@ hipError_t launch_init_rows(const Dev& d, const double* rhs, hipStream_t st) {
 
 // workgroups of a plan application for bumps up to k_ub: nb_minv for Minv /
 // MinvT, the rest for x_B, AS (and AR rows: with_ar)
-static void update_grid(const Dev& d, int k_ub, bool with_ar, unsigned* nb_minv, unsigned* nb) {
+// apply_plan grid: nb_minv workgroups for Minv / MinvT (per_thread elements
+// per thread), then the x_B / AS (/ AR) copy workgroups; threads = the
+// launch's workgroup size
+static void update_grid(const Dev& d, int k_ub, bool with_ar, unsigned* nb_minv, unsigned* nb,
+                        int threads = 256, int per_thread = 1) {
     const int64_t kk = 2 * (int64_t)(k_ub + 1) * (k_ub + 1);
-    *nb_minv = cdiv(kk, 256);
+    *nb_minv = cdiv(kk, threads * per_thread);
     if (*nb_minv > 2048) *nb_minv = 2048;
     const int64_t cw = with_ar ? (d.m > d.n ? d.m : d.n) : (d.m > k_ub + 1 ? d.m : k_ub + 1);
-    unsigned nb_copy = cdiv(cw, 256);
+    unsigned nb_copy = cdiv(cw, threads);
     if (nb_copy > 1024) nb_copy = 1024;
     *nb = *nb_minv + nb_copy;
 }
@@ -2655,7 +2659,9 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phas
     // phase 2: the previous iteration's plan is applied by trailing workgroups
     // of the pricing launch (it touches nothing the sweep reads)
     unsigned nb_minv = 0, napply = 0;
-    if (phase == 2) update_grid(d, k_ub, false, &nb_minv, &napply);
+    // (the apply workgroups ride beside the sweep: a few elements per thread
+    // keeps their count, and the launch's dispatch tail, small)
+    if (phase == 2) update_grid(d, k_ub, false, &nb_minv, &napply, d.csc ? TILE_COLS : PRICE_THREADS, 4);
     if (ev0) (void)hipEventRecord(ev0, st);
     // + nsw: the slack workgroups (candidates [ntiles, ntiles + nsw))
     const int nsw = slack_wgs(d, ny_ub);
