@@ -27,7 +27,11 @@ enum : int32_t {
 enum : int32_t { PC_NONE = 0, PC_A = 1, PC_B = 2, PC_C = 3, PC_D = 4, PC_E = 5 };
 enum : int32_t { ACT_NONE = 0, ACT_FLIP = 1, ACT_PIVOT = 2 };
 
-constexpr int PRICE_SPLIT = 8;  // slot chunks per pricing tile (one per wave)
+#ifndef ELP_PRICE_SPLIT
+#define ELP_PRICE_SPLIT 2
+#endif
+// slot chunks per pricing tile (one per wave); the oracle's PRICE_SPLIT must match
+constexpr int PRICE_SPLIT = ELP_PRICE_SPLIT;
 constexpr int ZCHUNK = 32;      // bump positions per FTRAN-z partial
 constexpr int TILE_COLS = 128;  // columns per pricing workgroup (2 per lane)
 

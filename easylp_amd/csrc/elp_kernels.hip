@@ -547,7 +547,7 @@ DEV void price_slacks(const Dev& d, int64_t ntiles, int s, int nsw, Cand* red) {
     if (threadIdx.x == 0) d.cand[ntiles + s] = best;
 }
 
-// One workgroup = 8 waves = 128 columns x all Y slots.  Wave w sweeps slot
+// One workgroup = PRICE_SPLIT waves = 128 columns x all Y slots.  Wave w sweeps slot
 // chunk w (PRICE_SPLIT contiguous chunks), lane l owns columns 2l, 2l+1 of the
 // tile (16-byte loads, 1 KiB per wave instruction, row-major AR so every load
 // is fully coalesced), 16 rows in flight per wave; y_Y comes from the
@@ -2661,7 +2661,10 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phas
     unsigned nb_minv = 0, napply = 0;
     // (the apply workgroups ride beside the sweep: a few elements per thread
     // keeps their count, and the launch's dispatch tail, small)
-    if (phase == 2) update_grid(d, k_ub, false, &nb_minv, &napply, d.csc ? TILE_COLS : PRICE_THREADS, 4);
+    #ifndef ELP_APPLY_PT
+#define ELP_APPLY_PT 4
+#endif
+    if (phase == 2) update_grid(d, k_ub, false, &nb_minv, &napply, d.csc ? TILE_COLS : PRICE_THREADS, ELP_APPLY_PT);
     if (ev0) (void)hipEventRecord(ev0, st);
     // + nsw: the slack workgroups (candidates [ntiles, ntiles + nsw))
     const int nsw = slack_wgs(d, ny_ub);

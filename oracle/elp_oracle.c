@@ -6,7 +6,7 @@
  * so that the HIP kernels (also -ffp-contract=off, explicit fma) produce
  * the same bits.  Reduction orders follow DESIGN.md "Reduction order
  * contract":
- *   price  : 8 contiguous slot chunks, fma chain per chunk, then the
+ *   price  : PRICE_SPLIT (2) contiguous slot chunks, fma chain per chunk, then the
  *            partials added in chunk order starting from 0.0 (PRICE_SPLIT)
  *   wave   : 64 lane-strided fma chains + butterfly 32,16,..,1 (wave_dot):
  *            FTRAN / BTRAN / B^-1 rows, phase-1 c_S correction, phase-1 sum
@@ -48,7 +48,9 @@
 #define VS_UPPER 2
 #define VS_FREE 3
 
-#define PRICE_SPLIT 8
+#ifndef PRICE_SPLIT
+#define PRICE_SPLIT 2 /* = the HIP side's ELP_PRICE_SPLIT */
+#endif
 #define ZCHUNK 32
 #define WAVE 64
 #define DEVEX_WMAX 1e20   /* Devex weight cap (both sides of the parity contract) */
