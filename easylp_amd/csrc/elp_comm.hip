@@ -47,6 +47,43 @@ int Comm::init_host(int world_size, int rank_, elp_host_allgather_fn ag, elp_hos
     return 0;
 }
 
+// Round-trip probe of freshly mapped mailboxes: thread t stores a reserved
+// sequence word into this rank's slots (both parities) of rank t's mailbox,
+// then waits (2 s at most) for rank t's word in its own.  Proves, before the
+// first solve, that remote stores land and become visible to the polling
+// loads (p2p_exchange's protocol); the reserved word can never equal a real
+// iteration's sequence (epoch << 40 | iteration + 1).
+constexpr int64_t MBOX_PROBE_SEQ = INT64_MAX;
+__global__ void k_mbox_probe(void* const* peers, void* mine, int P, int rank, int64_t rec, int* ok_out) {
+    __shared__ int fail;
+    const int t = threadIdx.x;
+    if (t == 0) fail = 0;
+    __syncthreads();
+    if (t < P) {
+        __threadfence_system();
+        for (int par = 0; par < 2; ++par) {
+            int64_t* s = reinterpret_cast<int64_t*>(static_cast<char*>(peers[t]) + (par * P + rank) * rec + rec - 8);
+            __hip_atomic_store(s, MBOX_PROBE_SEQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    __syncthreads();
+    if (t < P) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        for (int par = 0; par < 2; ++par) {
+            int64_t* s = reinterpret_cast<int64_t*>(static_cast<char*>(mine) + (par * P + t) * rec + rec - 8);
+            while (__hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != MBOX_PROBE_SEQ) {
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
+                    atomicOr(&fail, 1);
+                    break;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (t == 0) *ok_out = fail ? 0 : 1;
+}
+
 // Collective over the communicator: every rank takes every step (the handle
 // all-gather and the final agreement), so a rank that fails to allocate or to
 // map a peer does not strand the others; if any rank failed, none uses p2p.
@@ -89,6 +126,17 @@ int Comm::enable_p2p(size_t rec_bytes, hipStream_t st) {
     if (!rc && ok) {
         if (hipMalloc((void**)&dpeers, sizeof(void*) * (size_t)world) != hipSuccess) ok = 0;
         else if (hipMemcpy(dpeers, ptrs.data(), sizeof(void*) * (size_t)world, hipMemcpyHostToDevice) != hipSuccess)
+            ok = 0;
+    }
+    // every rank that mapped all peers probes the round trip (a rank that did
+    // not leaves its peers' probes to time out: they fail the agreement too)
+    if (!rc && ok) {
+        int32_t* dok = reinterpret_cast<int32_t*>(dstage);
+        int32_t hok = 0;
+        hipLaunchKernelGGL(k_mbox_probe, dim3(1), dim3(64), 0, st, (void* const*)dpeers, mbox, world, rank,
+                           (int64_t)rec_bytes, dok);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess ||
+            hipMemcpy(&hok, dok, sizeof(hok), hipMemcpyDeviceToHost) != hipSuccess || !hok)
             ok = 0;
     }
     // agreement: max over ranks of "failed"
