@@ -126,7 +126,8 @@ def c4_rate(args, lib, world, rank, local, barrier, dist):
     import torch
     from easylp_amd import Problem
     m, n = 10000, 500000
-    p = Problem(m, n, device=local, pricing=args.rule)
+    from easylp_amd._lib import ELP_PROFILE_PRICE
+    p = Problem(m, n, device=local, pricing=args.rule, verbose=ELP_PROFILE_PRICE if args.profile_price else 0)
     if world > 1 or args.force_sharded:
         from easylp_amd.dist import share_unique_id
         p.comm_init(share_unique_id(lib, rank), world, rank)
@@ -150,7 +151,17 @@ def c4_rate(args, lib, world, rank, local, barrier, dist):
         el = float(tt.item())
     it = s1["iterations"] - s0["iterations"]
     p.close()
+    # this rank's pricing sweep over its column shard (device clock, as the headline roofline)
+    price_s = s1["price_seconds"] - s0["price_seconds"]
+    price_b = s1["price_timed_bytes"] - s0["price_timed_bytes"]
+    price_n = s1["price_timed_launches"] - s0["price_timed_launches"]
+    sweep = None
+    if price_s > 0 and price_n > 0:
+        gbs = price_b / price_s / 1e9
+        sweep = {"achieved": gbs, "peak": 8000.0, "unit": "GB/s", "frac": gbs / 8000.0,
+                 "bytes_per_launch": price_b / price_n, "avg_sweep_us": 1e6 * price_s / price_n, "rank": rank}
     return {"workload": "dense random LP m=10000 n=500000 (SURVEY config 4), columns sharded x%d" % world,
+            "price_sweep": sweep,
             "value": it / el if el > 0 else None, "unit": "iterations/s", "iterations_timed": it,
             "warmup": args.c4_warmup, "ms_per_step": 1e3 * el / max(it, 1),
             "bump_dim": s1["bump_dim"], "y_rows": s1["y_rows"], "load_s": t_load}

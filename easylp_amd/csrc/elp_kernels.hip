@@ -1001,10 +1001,13 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw
 #pragma unroll
         for (int t = 0; t < PFC; ++t)
             cand_take(best, cc[t], tid + 256 * t < ncand && cand_better(cc[t], best, bland));
-    } else {
-        for (int t = tid; t < ncand; t += 256) {
-            const Cand o = d.cand[t];
-            cand_take(best, o, cand_better(o, best, bland));
+    } else {  // many tiles (one GPU holding n = 500 000): batches of 8 loads in flight
+        for (int t0 = tid; t0 < ncand; t0 += 256 * 8) {
+            Cand o[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) o[u] = ld_clamp(d.cand, t0 + 256 * u, ncand);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) cand_take(best, o[u], t0 + 256 * u < ncand && cand_better(o[u], best, bland));
         }
     }
     best = block_best<256>(best, bland, red);
@@ -1275,10 +1278,14 @@ DEV void emit_cand(const Dev& d, int var, int e, double g, double x, double l, d
     d.rcand[slot] = cd;
 }
 
-constexpr int ZR_WAVES = 8;   // waves per row tile of k_ftran_zr
+// waves per row tile of k_ftran_zr (ZR_WAVES): 8, or 4 when the row tiles
+// outnumber the CUs and every chunk still gets its own half-wave (the kernel
+// holds one 8-wave workgroup per CU -- 175 VGPRs -- so 4-wave tiles run two
+// per CU: one round of workgroups at m = 10 000 instead of two).  Which wave
+// forms a chunk does not change the arithmetic (chunk sums added in order).
 constexpr int ZR_ROWS = 32;   // rows per row tile: lane = row + 32 * half; each
                               // half-wave runs whole ZCHUNK chains (its own chunk)
-template <bool LDSZ>
+template <bool LDSZ, int ZR_WAVES>
 __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int k_ub) {
     extern __shared__ __attribute__((aligned(16))) double zlds[];  // [nch][ZR_ROWS]
     __shared__ double red[ZR_WAVES];
@@ -2686,15 +2693,17 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     const int m = d.m;
     if (bump_ftran && k_ub > 0) k_ftran_bump<<<cdiv(k_ub, 4), 256, 0, st>>>(d, d.aR, d.alS, 1);
     const int nrt = (int)cdiv(m > 0 ? m : 1, ZR_ROWS);
-    const int nbt = (int)cdiv(k_ub, 64 * ZR_WAVES);
+    // z partials: 256 B per chunk of ZCHUNK bump positions in LDS (<= 64 KiB,
+    // k <= 8192); larger bumps use a private slice of zpart per row tile
+    const size_t lds = (size_t)cdiv(k_ub, ZCHUNK) * ZR_ROWS * sizeof(double);
+    const bool ldsz = lds <= 64 * 1024 && !d.force_select;
+    const int zw = (ldsz && nrt > 256 && cdiv(k_ub, ZCHUNK) <= 8) ? 4 : 8;  // waves per row tile
+    const int nbt = (int)cdiv(k_ub, 64 * zw);
     {
-        // z partials: 256 B per chunk of ZCHUNK bump positions in LDS (<= 64 KiB,
-        // k <= 8192); larger bumps use a private slice of zpart per row tile
-        const size_t lds = (size_t)cdiv(k_ub, ZCHUNK) * ZR_ROWS * sizeof(double);
         // + 1: the snapshot workgroup
-        if (lds <= 64 * 1024 && !d.force_select)
-            k_ftran_zr<true><<<nrt + nbt + 1, 64 * ZR_WAVES, lds, st>>>(d, nrt, k_ub);
-        else k_ftran_zr<false><<<nrt + nbt + 1, 64 * ZR_WAVES, 0, st>>>(d, nrt, k_ub);
+        if (zw == 4) k_ftran_zr<true, 4><<<nrt + nbt + 1, 256, lds, st>>>(d, nrt, k_ub);
+        else if (ldsz) k_ftran_zr<true, 8><<<nrt + nbt + 1, 512, lds, st>>>(d, nrt, k_ub);
+        else k_ftran_zr<false, 8><<<nrt + nbt + 1, 512, 0, st>>>(d, nrt, k_ub);
     }
     // ratio test + (cases B/D) B^-1 row: one workgroup per 4 bump columns;
     // phase 2 adds the AR-copy workgroups and defers the rest of the update
