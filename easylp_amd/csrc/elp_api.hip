@@ -113,7 +113,7 @@ static void free_dev(elp_handle* h) {
                     d.t,        d.acol, d.aR,   d.alS,   d.alU,  d.zz,    d.zpart, d.vrow,
                     d.vvec,     d.colA, d.rhs,  d.vstat, d.cover, d.rpos, d.Rl,    d.Sl,
                     d.Yl,  d.ypos,  d.perm,  d.pivstep, d.nzlist, d.nzcount,
-                    d.cand,     d.pstamp, d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand,
+                    d.cand,     d.pstamp, d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand, d.rseg,
                     d.pkt, d.objg, d.ract, d.cand_xchg, h->d_flag, d.cS, d.slo, d.shi, d.rlo, d.rhi,
                     (void*)d.cptr, (void*)d.rind, (void*)d.cval, (void*)d.rptr, (void*)d.cind,
                     (void*)d.rval, d.qcol, d.dstamp, d.rowvs, d.yvs, d.dw, d.dprev};
@@ -221,7 +221,11 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.y, mm));
     A(dalloc(&d.yy, mm));
     A(dalloc(&d.blockmin, (size_t)(mm / 32 + mm / 256 + 4)));  // k_ftran_zr row + bump tiles
-    A(dalloc(&d.rcand, (size_t)(2 * mm + 2)));
+    // a segment holds the candidates of every RSEG-th k_ftran_zr workgroup: at most
+    // 32 per row tile and 512 per bump tile, i.e. <= (m + k) / RSEG + 544 (k <= m)
+    d.rsegcap = (int32_t)(2 * mm / RSEG + 1024);
+    A(dalloc(&d.rcand, (size_t)RSEG * (size_t)d.rsegcap));
+    A(dalloc(&d.rseg, (size_t)RSEG * RSEG_STRIDE));
     A(dalloc(&d.pkt, (size_t)(mm + 4)));
     A(dalloc(&d.objg, (size_t)h->n));
     A(dalloc(&d.ract, mm));
@@ -262,6 +266,7 @@ static int alloc_all(elp_handle* h) {
     A(hipHostMalloc((void**)&h->hctl, sizeof(DevCtl)));
     // (AR padding columns [n, ldr) are read by the 128-column tiles but their
     //  results are discarded, so AR needs no clearing); Minv / work start clean
+    A(hipMemsetAsync(d.rseg, 0, (size_t)RSEG * RSEG_STRIDE * sizeof(int32_t), h->st));
     A(hipMemsetAsync(d.Minv, 0, (size_t)mm * (size_t)mm * sizeof(double), h->st));
     A(hipMemsetAsync(d.MinvT, 0, (size_t)mm * (size_t)mm * sizeof(double), h->st));
     if (d.qcol) A(hipMemsetAsync(d.qcol, 0, (size_t)mm * sizeof(double), h->st));

@@ -33,6 +33,11 @@ enum : int32_t { ACT_NONE = 0, ACT_FLIP = 1, ACT_PIVOT = 2 };
 // slot chunks per pricing tile (one per wave); the oracle's PRICE_SPLIT must match
 constexpr int PRICE_SPLIT = ELP_PRICE_SPLIT;
 constexpr int ZCHUNK = 32;      // bump positions per FTRAN-z partial
+// k_ftran_zr's Harris pass-2 candidates go to RSEG lists by workgroup index
+// (blockIdx % RSEG), each with its own counter line: RSEG times fewer atomics
+// queue on one address than with a single list (the result is the same: the
+// leaving variable is chosen by a total order)
+constexpr int RSEG = 8, RSEG_STRIDE = 32;
 constexpr int TILE_COLS = 128;  // columns per pricing workgroup (2 per lane)
 
 struct Plan {
@@ -63,7 +68,7 @@ struct DevCtl {
     double price_bytes;    // algorithmic bytes of every pricing pass that ran
     int64_t price_passes;
     unsigned long long ns_emax_bits;  // max|I - M Minv| of the last refactor (bits of a double >= 0)
-    int32_t ncand, pad2;              // Harris pass-2 candidate count (k_ftran_zr)
+    int32_t pad2, pad3;
     int32_t snap_k, snap_bland;       // k, bland as k_ratio's workgroups must see them
                                       // (workgroup 0 rewrites k / bland meanwhile)
     // likewise the bookkeeping entries k_ratio's dual update reads (k_ftran_zr's
@@ -159,7 +164,9 @@ struct Dev {
     double* objg;            // global objective (N), for c_S of foreign basic columns
     double* ract;            // row activities sum_j a_ij x_j of nonzero nonbasic columns
     CandX* cand_xchg;        // [world] local best candidates (all-gathered)
-    RCand* rcand;            // pass-2 candidates (capacity 2m)
+    RCand* rcand;            // pass-2 candidates: RSEG segments of rsegcap each
+    int32_t* rseg;           // their counts, one per 128-byte line (stride RSEG_STRIDE)
+    int32_t rsegcap;
     double *rlo, *rhi;       // per covered row: bounds of the covering unit variable
     int8_t* vstat;
     int8_t* rowvs;  // per row: the status its slack has whenever it is nonbasic

@@ -899,7 +899,7 @@ DEV Cand local_best(const Dev& d, int ncand, Cand* red) {
 DEV void entering_chosen(const Dev& d, const Cand& best) {
     DevCtl* c = d.ctl;
     const int ny = c->ny;
-    c->ncand = 0;
+    for (int sg = 0; sg < RSEG; ++sg) d.rseg[sg * RSEG_STRIDE] = 0;  // k_ftran_zr's candidate lists
     // algorithmic bytes of this pricing pass: AR sweep + c + status + y_Y + Yl
     c->price_bytes += price_pass_bytes(d, ny, c->devex);
     c->price_passes++;
@@ -1279,7 +1279,8 @@ DEV void emit_cand(const Dev& d, int var, int e, double g, double x, double l, d
     if (var < 0) return;
     const double r = harris2(g, x, l, u, pivtol);
     if (!(r <= bmin) || r == HUGE_VAL) return;
-    const int slot = atomicAdd(&d.ctl->ncand, 1);
+    const int seg = blockIdx.x & (RSEG - 1);
+    const int slot = atomicAdd(&d.rseg[seg * RSEG_STRIDE], 1);
     RCand cd;
     cd.g = g;
     cd.r = r;
@@ -1287,7 +1288,7 @@ DEV void emit_cand(const Dev& d, int var, int e, double g, double x, double l, d
     cd.u = u;
     cd.var = var;
     cd.e = e;
-    d.rcand[slot] = cd;
+    d.rcand[(size_t)seg * d.rsegcap + slot] = cd;
 }
 
 // waves per row tile of k_ftran_zr (ZR_WAVES): 8, or 4 when the row tiles
@@ -1524,7 +1525,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     //      status test below then waits for these alone, not for the prefetch
     DevCtl* c = d.ctl;
     const int32_t st0 = c->snap_status;  // (not c->status: see DevCtl::snap_status)
-    const int m = d.m, k = c->snap_k, q = c->q, ny = c->snap_ny, ncand = c->ncand;
+    const int m = d.m, k = c->snap_k, q = c->q, ny = c->snap_ny;
     const double sig = c->sig, dq = c->dq, wq = c->wq;
     const int bland = c->snap_bland, devex = c->devex;
     const int apos_c = c->snap_apos;
@@ -1553,12 +1554,16 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     }
     // entries of Rl past the real k are stale: range-checked before use
     const int rcol = ld_clamp(d.Rl, main_wg ? col : 0, k_ub);
-    // the pass-2 candidates k_ftran_zr emitted: the first 256 * PFQ slots of the
-    // list (capacity 2m), masked by the real count below
+    // the pass-2 candidates k_ftran_zr emitted: RSEG lists, 32 threads per list
+    // (256 = RSEG * 32), the first 32 * PFQ entries of each, masked by its count
     constexpr int PFQ = 4;
+    static_assert(RSEG * 32 == 256, "k_ratio: 32 threads per candidate list");
+    const int sg = tid & (RSEG - 1), si = tid >> 3;
+    const RCand* segp = d.rcand + (size_t)sg * d.rsegcap;
+    const int scnt = d.rseg[sg * RSEG_STRIDE];
     RCand rq[PFQ];
 #pragma unroll
-    for (int t = 0; t < PFQ; ++t) rq[t] = ld_clamp(d.rcand, tid + 256 * t, 2 * (m > 0 ? m : 1));
+    for (int t = 0; t < PFQ; ++t) rq[t] = ld_clamp(segp, si + 32 * t, d.rsegcap);
     __builtin_amdgcn_sched_barrier(0);  // all of the above issued before any use
     if (st0 != ST_RUN) {  // no plan this iteration: k_update must not re-apply one
         if (blockIdx.x == 0 && threadIdx.x == 0) c->plan.action = ACT_NONE;
@@ -1596,7 +1601,6 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     const int ypos_r = d.ypos[rsafe];  // its Y slot (workgroup 0 rewrites no bump row's slot)
     // ---- parallel prefetch of bookkeeping scalars
     const int ql = loc_of(d, q);  // -1: the entering column lives on another shard
-    const bool pfq = ncand <= 256 * PFQ;
     // case D needs wave_dot(MinvT[apos, :], A[lrow, S]) in every workgroup: wave 0
     // fetches that row now (apos comes with the control block)
     double arow[PFT];
@@ -1633,13 +1637,10 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         o.e = cd.e;
         leave_take(best, o, leave_better(o, best, bland));
     };
-    if (pfq) {
 #pragma unroll
-        for (int t = 0; t < PFQ; ++t)
-            if (tid + 256 * t < ncand) consider(rq[t]);
-    } else {
-        for (int t = tid; t < ncand; t += 256) consider(d.rcand[t]);
-    }
+    for (int t = 0; t < PFQ; ++t)
+        if (si + 32 * t < scnt) consider(rq[t]);
+    for (int t = si + 32 * PFQ; t < scnt; t += 32) consider(segp[t]);  // long lists
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         Leave o = shfl_leave(best, off);
