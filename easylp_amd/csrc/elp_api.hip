@@ -113,7 +113,7 @@ static void free_dev(elp_handle* h) {
                     d.t,        d.acol, d.aR,   d.alS,   d.alU,  d.zz,    d.zpart, d.vrow,
                     d.vvec,     d.colA, d.rhs,  d.vstat, d.cover, d.rpos, d.Rl,    d.Sl,
                     d.Yl,  d.ypos,  d.perm,  d.pivstep, d.nzlist, d.nzcount,
-                    d.cand,     d.pstamp, d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand, d.rseg,
+                    d.cand,     d.pstamp, d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand, d.rseg, d.AT,
                     d.pkt, d.objg, d.ract, d.cand_xchg, h->d_flag, d.cS, d.slo, d.shi, d.rlo, d.rhi,
                     (void*)d.cptr, (void*)d.rind, (void*)d.cval, (void*)d.rptr, (void*)d.cind,
                     (void*)d.rval, d.qcol, d.dstamp, d.rowvs, d.yvs, d.dw, d.dprev};
@@ -428,6 +428,19 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
         const int rc = ensure_ar(h, (int64_t)h->hctl->ny + 64);
         if (rc) return rc;
     }
+    // dense A: a row-major copy for the AR row copies (contiguous reads); without
+    // the memory for it they read A's rows in place
+    // (only while the AR rows could still grow to a full copy of A beside it)
+    size_t mem_free = 0, mem_total = 0;
+    const size_t at_bytes = (size_t)m * (size_t)nl * sizeof(double);
+    if (!d.csc && d.A && !d.AT && at_bytes > 0 && hipMemGetInfo(&mem_free, &mem_total) == hipSuccess &&
+        mem_free > 2 * at_bytes + ((size_t)1 << 30)) {
+        if (hipMalloc((void**)&d.AT, at_bytes) != hipSuccess) {
+            d.AT = nullptr;
+            (void)hipGetLastError();
+        }
+    }
+    if (d.AT) HIPCHK(launch_transpose_A(d, h->st));
     HIPCHK(launch_fill_AR(h->d, h->st));
     (void)hipFree(dlo);
     (void)hipFree(dup);

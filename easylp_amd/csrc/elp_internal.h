@@ -147,6 +147,7 @@ struct Dev {
     int64_t ldr;   // n rounded up to TILE_COLS
     int64_t arcap; // AR rows per column tile (capacity)
     const double* A;  // column-major m x n (this shard's columns)
+    double* AT;       // its row-major copy (m x n, ld n): AR row copies read it contiguously
     const double* Afull;  // sharded + replicated: all N columns (A = Afull + col0*m);
                           // null: the entering column comes in the exchanged pkt
     double* AR;       // Y rows, tile-major: [ldr/128 tiles][arcap rows][128 cols]
@@ -242,6 +243,7 @@ hipError_t launch_refactor_gj(const Dev& d, int k, hipStream_t st);
 hipError_t launch_btran_exact(const Dev& d, int k, hipStream_t st);  // phase-2 duals
 hipError_t launch_refactor_primal(const Dev& d, int k, hipStream_t st);  // needs ract
 hipError_t launch_nzlist(const Dev& d, hipStream_t st);
+hipError_t launch_transpose_A(const Dev& d, hipStream_t st);
 hipError_t launch_phase2(const Dev& d, hipStream_t st);  // (includes devex_reset)
 hipError_t launch_devex_reset(const Dev& d, hipStream_t st);  // weights 1, dv_valid 0
 // sensitivity (final basis, k = bump dimension): dred[n] reduced costs; TR

@@ -353,6 +353,28 @@ __global__ void __launch_bounds__(1024) k_init_Y(Dev d) {
     }
 }
 
+// a_ij of this shard, read along a row (AR row copies): the row-major copy when
+// there is one (contiguous over j), else the column-major A (one line per element)
+DEV double a_row(const Dev& d, int64_t i, int64_t j) {
+    return d.AT ? d.AT[(size_t)i * (size_t)d.n + (size_t)j] : d.A[(size_t)j * (size_t)d.m + (size_t)i];
+}
+
+// AT = A^T through 64 x 64 LDS tiles (reads down columns, writes along rows)
+__global__ void __launch_bounds__(256) k_transpose_A(Dev d) {
+    __shared__ double t[64][65];
+    const int64_t j0 = (int64_t)blockIdx.x * 64, i0 = (int64_t)blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < 64; r += 4) {
+        const int64_t j = j0 + r, i = i0 + tx;
+        if (j < d.n && i < d.m) t[r][tx] = d.A[(size_t)j * (size_t)d.m + (size_t)i];
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {
+        const int64_t i = i0 + r, j = j0 + tx;
+        if (i < d.m && j < d.n) d.AT[(size_t)i * (size_t)d.n + (size_t)j] = t[tx][r];
+    }
+}
+
 // element (row p, column j) of the tile-major AR
 DEV size_t ar_at(const Dev& d, int64_t p, int64_t j) {
     return ((size_t)(j / TILE_COLS) * (size_t)d.arcap + (size_t)p) * TILE_COLS + (size_t)(j % TILE_COLS);
@@ -364,7 +386,7 @@ __global__ void k_fill_AR(Dev d) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= d.n) return;
     for (int p = blockIdx.y; p < ny; p += gridDim.y)
-        d.AR[ar_at(d, p, j)] = d.A[(size_t)j * (size_t)d.m + (size_t)d.Yl[p]];
+        d.AR[ar_at(d, p, j)] = a_row(d, d.Yl[p], j);
 }
 
 // grow AR: rows [0, rows) of every tile into the new capacity
@@ -1743,7 +1765,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         const int64_t tstride = (int64_t)(gridDim.x - nmain) * blockDim.x;
         for (int64_t j = (int64_t)(blockIdx.x - nmain) * blockDim.x + tid; j < d.n; j += tstride) {
             if (rm_slot >= 0 && rm_slot != rm_last) d.AR[ar_at(d, rm_slot, j)] = d.AR[ar_at(d, rm_last, j)];
-            if (ap_slot >= 0) d.AR[ar_at(d, ap_slot, j)] = d.A[(size_t)j * (size_t)m + ap_row];
+            if (ap_slot >= 0) d.AR[ar_at(d, ap_slot, j)] = a_row(d, ap_row, j);
         }
         if (d.dstamp) {
             __syncthreads();
@@ -2157,7 +2179,7 @@ DEV void apply_plan(const Dev& d, const Plan& P, int blk, int nb, int nb_minv, b
         for (int64_t j = t0; j < d.n; j += tstride) {
             if (P.y_rm_slot >= 0 && P.y_rm_slot != P.y_rm_last)
                 d.AR[ar_at(d, P.y_rm_slot, j)] = d.AR[ar_at(d, P.y_rm_last, j)];
-            if (P.y_ap_slot >= 0) d.AR[ar_at(d, P.y_ap_slot, j)] = d.A[(size_t)j * m + P.y_ap_row];
+            if (P.y_ap_slot >= 0) d.AR[ar_at(d, P.y_ap_slot, j)] = a_row(d, P.y_ap_row, j);
         }
     }
 }
@@ -2616,6 +2638,12 @@ hipError_t launch_fill_AR(const Dev& d, hipStream_t st) {
 hipError_t launch_ar_relayout(const Dev& d, const double* old_ar, int64_t old_cap, int rows,
                               hipStream_t st) {
     if (rows > 0) k_ar_relayout<<<2048, 256, 0, st>>>(d, old_ar, old_cap, rows);
+    return hipGetLastError();
+}
+
+hipError_t launch_transpose_A(const Dev& d, hipStream_t st) {
+    if (d.m > 0 && d.n > 0)
+        k_transpose_A<<<dim3((unsigned)cdiv(d.n, 64), (unsigned)cdiv(d.m, 64)), 256, 0, st>>>(d);
     return hipGetLastError();
 }
 
