@@ -2755,8 +2755,11 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
         const unsigned nmain = cdiv(k_ub > 0 ? k_ub : 1, 4);
         unsigned nar = 0;
         if (defer && !d.csc) {
+#ifndef ELP_NAR_MAX
+#define ELP_NAR_MAX 512
+#endif
             nar = cdiv(d.n, 256);
-            if (nar > 512) nar = 512;
+            if (nar > ELP_NAR_MAX) nar = ELP_NAR_MAX;
         }
         k_ratio<<<nmain + nar, 256, lds_row ? lds : 0, st>>>(d, phase, nrt + nbt, lds_row, defer, (int)nmain,
                                                            k_ub, dslot);
