@@ -112,7 +112,7 @@ static void free_dev(elp_handle* h) {
                     d.lb,       d.ub,  d.cost,  d.xval,  d.asgn, d.xr,    d.xs,    d.y,
                     d.t,        d.acol, d.aR,   d.alS,   d.alU,  d.zz,    d.zpart, d.vrow,
                     d.vvec,     d.colA, d.rhs,  d.vstat, d.cover, d.rpos, d.Rl,    d.Sl,
-                    d.Yl,  d.ypos,  d.perm,  d.pivstep, d.nzlist, d.nzcount,
+                    d.Yl,  d.ypos,  d.perm,  d.pivstep, d.nzlist, d.nzcount, d.nzchunk,
                     d.cand,     d.pstamp, d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand, d.rseg, d.AT,
                     d.pkt, d.objg, d.ract, d.cand_xchg, h->d_flag, d.cS, d.slo, d.shi, d.rlo, d.rhi,
                     (void*)d.cptr, (void*)d.rind, (void*)d.cval, (void*)d.rptr, (void*)d.cind,
@@ -251,6 +251,7 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.perm, mm));
     A(dalloc(&d.pivstep, mm));
     A(dalloc(&d.nzlist, n));
+    A(dalloc(&d.nzchunk, n / (1024 * 16) + 2));
     A(dalloc(&d.nzcount, 1));
     // tile candidates + the slack workgroups' (|Y| <= m, >= 128 slots each)
     A(dalloc(&d.cand, (size_t)((n + TILE_COLS - 1) / TILE_COLS) + (size_t)((mm + TILE_COLS - 1) / TILE_COLS) + 64));

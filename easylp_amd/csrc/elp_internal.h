@@ -174,6 +174,7 @@ struct Dev {
                     // (<=: lower, >=: upper, ==: fixed -- a slack never flips)
     int8_t* yvs;    // per Y slot: rowvs of the slot's row (select reads it in slot order)
     int32_t *cover, *rpos, *Rl, *Sl, *spos, *Yl, *ypos, *perm, *pivstep, *nzlist, *nzcount;
+    int32_t* nzchunk;  // per-chunk counts of the nzlist compaction
     Cand* cand;
     unsigned long long* pstamp;  // [tile][2] start / end stamps of the last pricing pass
     int32_t ptimer, pad3;        // 1: k_price stamps, the select kernels sum them

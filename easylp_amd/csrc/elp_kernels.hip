@@ -195,44 +195,79 @@ __global__ void k_init_cols(Dev d, const double* __restrict__ lo, const double* 
     }
 }
 
-// ordered compaction (single block): nzlist = { j < n : vstat != BASIC && xval != 0 }.
-// Thread t owns NZ_RUN consecutive columns of each 1024 * NZ_RUN chunk (flags in
-// a bit mask, loads all in flight), a wave scan + the waves' totals give its
-// output offset: two barriers per 16 384 columns (n = 500 000: 31 chunks)
-constexpr int NZ_RUN = 16;
-__global__ void __launch_bounds__(1024) k_nzlist(Dev d) {
-    __shared__ int wsum[16];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int base = 0;
-    for (int64_t j0 = 0; j0 < d.n; j0 += 1024 * NZ_RUN) {
-        const int64_t js = j0 + (int64_t)threadIdx.x * NZ_RUN;
-        unsigned mask = 0;
+// ordered compaction: nzlist = { j < n : vstat != BASIC && xval != 0 }, ascending.
+// One workgroup per chunk of 1024 * NZ_RUN columns; thread t owns NZ_RUN
+// consecutive columns (a bit mask of flags, loads all in flight).  Pass 1
+// counts each chunk; pass 2 offsets the chunk by the counts before it (a wave
+// scan + the waves' totals inside the chunk) and writes.
+constexpr int NZ_RUN = 16, NZ_CHUNK = 1024 * NZ_RUN;
+DEV unsigned nz_flags(const Dev& d, int64_t js) {
+    unsigned mask = 0;
+    if (js + NZ_RUN <= d.n) {  // whole run: one 16-byte status load, 8 value loads
+        const int4 v4 = *reinterpret_cast<const int4*>(d.vstat + js);  // (hipMalloc base, js % 16 == 0)
+        double2 xv[NZ_RUN / 2];
 #pragma unroll
+        for (int u = 0; u < NZ_RUN / 2; ++u) xv[u] = *reinterpret_cast<const double2*>(d.xval + js + 2 * u);
+        const int8_t* vb = reinterpret_cast<const int8_t*>(&v4);
+#pragma unroll
+        for (int u = 0; u < NZ_RUN; ++u) {
+            const double x = (u & 1) ? xv[u >> 1].y : xv[u >> 1].x;
+            mask |= (unsigned)((vb[u] != VS_BASIC) & (x != 0.0)) << u;
+        }
+    } else {
         for (int u = 0; u < NZ_RUN; ++u) {
             const int64_t j = js + u;
             const bool f = j < d.n && d.vstat[j] != VS_BASIC && d.xval[j] != 0.0;
             mask |= (unsigned)f << u;
         }
-        const int cnt = __popc(mask);
-        int incl = cnt;  // inclusive scan over the wave
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int v = __shfl_up(incl, off);
-            if (lane >= off) incl += v;
-        }
-        if (lane == 63) wsum[w] = incl;
-        __syncthreads();
-        int pos = base + incl - cnt, tot = 0;
-        for (int i = 0; i < 16; ++i) {
-            if (i < w) pos += wsum[i];
-            tot += wsum[i];
-        }
-        for (int u = 0; u < NZ_RUN; ++u)
-            if (mask >> u & 1u) d.nzlist[pos++] = (int)(js + u);
-        base += tot;
-        __syncthreads();  // wsum is rewritten by the next chunk
     }
-    if (threadIdx.x == 0) *d.nzcount = base;
+    return mask;
+}
+__global__ void __launch_bounds__(1024) k_nzlist_count(Dev d) {
+    __shared__ int wsum[16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t js = (int64_t)blockIdx.x * NZ_CHUNK + (int64_t)threadIdx.x * NZ_RUN;
+    int cnt = __popc(nz_flags(d, js));
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
+    if (lane == 0) wsum[w] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int i = 0; i < 16; ++i) t += wsum[i];
+        d.nzchunk[blockIdx.x] = t;
+    }
+}
+__global__ void __launch_bounds__(1024) k_nzlist(Dev d) {
+    __shared__ int wsum[16];
+    __shared__ int s_base;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t js = (int64_t)blockIdx.x * NZ_CHUNK + (int64_t)threadIdx.x * NZ_RUN;
+    const unsigned mask = nz_flags(d, js);
+    if (threadIdx.x < 64) {  // the counts of the chunks before this one
+        int b = 0;
+        for (int c = lane; c < (int)blockIdx.x; c += 64) b += d.nzchunk[c];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) b += __shfl_xor(b, off);
+        if (lane == 0) s_base = b;
+    }
+    const int cnt = __popc(mask);
+    int incl = cnt;  // inclusive scan over the wave
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(incl, off);
+        if (lane >= off) incl += v;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int pos = s_base + incl - cnt, tot = s_base;
+    for (int i = 0; i < 16; ++i) {
+        if (i < w) pos += wsum[i];
+        tot += wsum[i];
+    }
+    for (int u = 0; u < NZ_RUN; ++u)
+        if (mask >> u & 1u) d.nzlist[pos++] = (int)(js + u);
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *d.nzcount = tot;
 }
 
 // ract_i = chain(ract_i, a_ij x_j over this shard's nonzero nonbasic columns,
@@ -2623,8 +2658,7 @@ hipError_t launch_generate(const Dev& d, uint64_t seed, int64_t col0, int64_t n_
 
 hipError_t launch_init_cols(const Dev& d, const double* lo, const double* up, hipStream_t st) {
     k_init_cols<<<cdiv(d.n, 256), 256, 0, st>>>(d, lo, up);
-    k_nzlist<<<1, 1024, 0, st>>>(d);
-    return hipGetLastError();
+    return launch_nzlist(d, st);
 }
 
 hipError_t launch_fill_AR(const Dev& d, hipStream_t st) {
@@ -2648,7 +2682,9 @@ hipError_t launch_transpose_A(const Dev& d, hipStream_t st) {
 }
 
 hipError_t launch_nzlist(const Dev& d, hipStream_t st) {
-    k_nzlist<<<1, 1024, 0, st>>>(d);
+    const unsigned nb = (unsigned)cdiv(d.n > 0 ? d.n : 1, NZ_CHUNK);
+    k_nzlist_count<<<nb, 1024, 0, st>>>(d);
+    k_nzlist<<<nb, 1024, 0, st>>>(d);
     return hipGetLastError();
 }
 
