@@ -16,6 +16,8 @@ ELP_OPTIMAL, ELP_SUBOPTIMAL, ELP_INFEASIBLE, ELP_UNBOUNDED = 0, 1, 2, 3
 ELP_NUMFAILURE, ELP_TIMEOUT = 5, 7
 ELP_PROFILE_PRICE = 2   # device-clock pricing timer
 ELP_PROFILE_EVENTS = 4  # HIP-event pricing timer
+ELP_SCALE_GEOMETRIC, ELP_SCALE_EQUILIBRATE = 4, 64
+ABI_VERSION = 2
 
 # every entry point the header declares (checked by tests/test_abi.py)
 EXPORTS = (
@@ -52,7 +54,11 @@ class ElpControl(ctypes.Structure):
         ("replicate", ctypes.c_int32),
         ("max_nodes", ctypes.c_int32),
         ("pricing", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 3),
+        ("ngpu", ctypes.c_int32),
+        ("scaling", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
+        ("tol_singular", ctypes.c_double),
+        ("mailbox_timeout", ctypes.c_double),
     ]
 
 

@@ -69,6 +69,7 @@ struct elp_handle {
     std::vector<double> lo_h, up_h;  // column bounds as loaded (MIP root)
     std::vector<int32_t> is_int;     // integer columns (elp_set_int); empty: LP
     bool in_bnb = false;             // node reloads keep is_int / root bounds
+    int64_t bnb_iter_left = 0;       // branch and bound: LP iterations left (max_iter > 0)
     bool mip = false;                // the last elp_solve ran branch and bound
     int64_t mip_nodes = 0, mip_iters = 0;
     elp_stats stats{};
@@ -101,6 +102,10 @@ extern "C" void elp_default_control(elp_control* c) {
     c->sync_every = 32;
     c->verbose = 0;
     c->pricing = ELP_PRICE_DEVEX;
+    c->ngpu = 1;
+    c->scaling = 0;
+    c->tol_singular = 1e-13;
+    c->mailbox_timeout = 2.0;
 }
 
 extern "C" const char* elp_last_error(void) { return g_err.c_str(); }
@@ -145,6 +150,9 @@ extern "C" int elp_create(elp_handle** out, int64_t m, int64_t n, const elp_cont
     if (h->ctl.degen_switch <= 0) h->ctl.degen_switch = 50;
     if (h->ctl.sync_every <= 0) h->ctl.sync_every = 32;
     if (!(h->ctl.infinity > 0)) h->ctl.infinity = 1e30;
+    if (!(h->ctl.tol_singular >= 0)) h->ctl.tol_singular = 1e-13;
+    if (!(h->ctl.mailbox_timeout > 0)) h->ctl.mailbox_timeout = 2.0;
+    if (h->ctl.ngpu < 1) h->ctl.ngpu = 1;
     h->m = m;
     h->n = n;
     h->col0 = 0;
@@ -177,6 +185,8 @@ static int alloc_all(elp_handle* h) {
     d.ldm = mm;
     d.ldr = ((n + TILE_COLS - 1) / TILE_COLS) * TILE_COLS;
     d.infinity = h->ctl.infinity;
+    d.tol_singular = h->ctl.tol_singular;
+    d.mb_ticks = (int64_t)(h->ctl.mailbox_timeout * 1e8);  // s_memrealtime: 100 MHz
     d.ptimer = (h->ctl.verbose & ELP_PROFILE_PRICE) ? 1 : 0;
     d.csc = h->csc ? 1 : 0;
     d.p2p = h->comm.p2p;
@@ -401,6 +411,8 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
     c.status = ST_RUN;
     c.phase = 1;
     c.iter_limit = h->ctl.max_iter > 0 ? h->ctl.max_iter : 100 * (m + n) + 10000;
+    // branch and bound: max_iter bounds the whole tree, not each node
+    if (h->in_bnb && h->ctl.max_iter > 0) c.iter_limit = std::max<int64_t>(h->bnb_iter_left, 0);
     c.iter_stop = INT64_MAX;
     c.refactor_period = h->ctl.refactor_period;
     c.degen_switch = h->ctl.degen_switch;
@@ -716,6 +728,14 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             h->stats.seconds_loop += now_s() - t_loop0;
             return 0;
         }
+        if (c->status == ST_RUN && h->phase == 2 && c->iter >= c->iter_limit) {
+            // the phase-2 loop top (oracle run_phase) before any k_ratio has
+            // checked the cap: a budget spent in phase 1 or a branch-and-bound
+            // budget of 0
+            h->done = true;
+            h->final_status = ELP_SUBOPTIMAL;
+            break;
+        }
         if (c->status == ST_RUN && h->phase == 2 && c->since_refactor >= period &&
             c->iter < c->iter_limit) {
             rc = do_refactor(h, c->k);
@@ -808,7 +828,8 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
         h->dbg_wait += now_s() - t_enq1;
         h->stats.host_polls++;
         const int32_t s = c->status;
-        if (s == ST_COMMFAIL) return fail(ELP_E_COMM, "xGMI mailbox: a peer's record did not arrive within 2 s");
+        if (s == ST_COMMFAIL)
+            return fail(ELP_E_COMM, "xGMI mailbox: a peer's record did not arrive within elp_control.mailbox_timeout");
         if (prof && s == ST_RUN) {  // every launch of the chunk did work
             for (int t = 0; t < chunk; ++t) {
                 float ms = 0.f;
@@ -931,9 +952,17 @@ static int reload_bounds(elp_handle* h, const std::vector<double>& lo, const std
 
 // Depth-first branch and bound over LP relaxations; the rules are
 // oracle/elp_oracle.c orc_solve_mip's, so both explore the same tree.
+// max_iter (total LP iterations) and time_limit (seconds since the branch and
+// bound started) bound the whole tree.  A node LP that stops on a limit ends
+// the search; one that fails numerically is skipped but makes the result
+// incomplete.  Status: unbounded relaxation -> 3; incumbent -> 0, or 1 when the
+// tree was not fully explored (a limit, max_nodes, a failed node); no
+// incumbent -> the failed node's status (1 iteration cap, 5, 7), 1 at the node
+// limit, else 2 (lp_solve's SUBOPTIMAL / TIMEOUT / NUMFAILURE conventions).
 static int run_bnb(elp_handle* h, int32_t* out_status) {
     const int64_t n = h->n;
     const double INF = HUGE_VAL, BIG = h->ctl.infinity;
+    const double t_bnb = now_s();
     std::vector<double> l0 = h->lo_h, u0 = h->up_h;
     for (int64_t j = 0; j < n; ++j) {
         if (l0[j] <= -BIG) l0[j] = -INF;
@@ -949,6 +978,7 @@ static int run_bnb(elp_handle* h, int32_t* out_status) {
     double best = INF;
     Node best_node;
     bool have = false, limit = false, unbounded = false;
+    int32_t failed = -1;  // status of the first node LP that did not finish (incomplete tree)
     int64_t nodes = 0, iters = 0;
     std::vector<double> x((size_t)n);
     while (!stack.empty()) {
@@ -959,8 +989,16 @@ static int run_bnb(elp_handle* h, int32_t* out_status) {
             continue;
         }
         nodes++;
-        int rc = nodes == 1 && h->lo_h == nd.lo && h->up_h == nd.up ? 0 : reload_bounds(h, nd.lo, nd.up);
+        h->bnb_iter_left = h->ctl.max_iter - iters;
+        if (h->ctl.max_iter > 0 && h->bnb_iter_left <= 0) {  // budget spent: as the oracle
+            failed = failed < 0 ? ELP_SUBOPTIMAL : failed;
+            break;
+        }
+        int rc = 0;
+        if (!(nodes == 1 && h->lo_h == nd.lo && h->up_h == nd.up)) rc = reload_bounds(h, nd.lo, nd.up);
         if (rc) return rc;
+        h->t_solve_start = t_bnb;  // time_limit counts from the start of the tree
+        h->timing_started = true;
         int32_t s = 0;
         rc = run_loop(h, INT64_MAX, &s);
         if (rc) return rc;
@@ -973,6 +1011,11 @@ static int run_bnb(elp_handle* h, int32_t* out_status) {
         if (s == ELP_UNBOUNDED) {
             unbounded = true;
             break;
+        }
+        if (s != ELP_OPTIMAL && s != ELP_INFEASIBLE) {  // limit or numerical failure
+            if (failed < 0) failed = s;
+            if (s == ELP_SUBOPTIMAL || s == ELP_TIMEOUT) break;  // the tree's budget is spent
+            continue;
         }
         if (s != ELP_OPTIMAL) continue;
         double z = 0.0;
@@ -1001,13 +1044,18 @@ static int run_bnb(elp_handle* h, int32_t* out_status) {
     }
     int32_t status;
     if (unbounded) status = ELP_UNBOUNDED;
-    else if (have) status = limit ? ELP_SUBOPTIMAL : ELP_OPTIMAL;
+    else if (have) status = (limit || failed >= 0) ? ELP_SUBOPTIMAL : ELP_OPTIMAL;
+    else if (failed >= 0) status = failed;
     else status = limit ? ELP_SUBOPTIMAL : ELP_INFEASIBLE;
     if (have && !unbounded) {  // leave the incumbent's LP on the handle for elp_get_solution
+        // (the incumbent's node was solved within the limits once: no limits now)
+        h->bnb_iter_left = INT64_MAX / 4;
+        const double tl = h->ctl.time_limit;
+        h->ctl.time_limit = 0.0;
         int rc = reload_bounds(h, best_node.lo, best_node.up);
-        if (rc) return rc;
         int32_t s = 0;
-        rc = run_loop(h, INT64_MAX, &s);
+        if (!rc) rc = run_loop(h, INT64_MAX, &s);
+        h->ctl.time_limit = tl;
         if (rc) return rc;
     }
     h->final_status = status;
@@ -1305,7 +1353,7 @@ extern "C" int elp_comm_enable_p2p(elp_handle* h) {
     if (h->comm.kind == 0) return 0;  // one rank: nothing to exchange
     if (h->comm.world > 64) return fail(ELP_E_UNSUPPORTED, "elp_comm_enable_p2p: more than 64 ranks");
     HIPCHK(hipSetDevice(h->dev));
-    const int rc = h->comm.enable_p2p(sizeof(MboxRec), h->st);
+    const int rc = h->comm.enable_p2p(sizeof(MboxRec), h->st, h->ctl.mailbox_timeout);
     return rc ? fail(rc, "elp_comm_enable_p2p: mailbox allocation / IPC exchange failed") : 0;
 }
 

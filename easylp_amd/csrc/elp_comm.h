@@ -32,7 +32,11 @@ struct Comm {
     void** dpeers = nullptr;           // device array: every rank's mailbox, mapped here
     std::vector<void*> opened;         // IPC-opened peer mailboxes
     int p2p = 0;
-    int enable_p2p(size_t rec_bytes, hipStream_t st);
+    // device scratch for setup collectives (enable_p2p), allocated at init
+    static constexpr int SCRATCH_RANKS = 64;
+    static constexpr size_t SCRATCH_BYTES = 64 * (SCRATCH_RANKS + 1) + 64;
+    void* scratch = nullptr;
+    int enable_p2p(size_t rec_bytes, hipStream_t st, double timeout_s);
 
     static int unique_id(uint8_t id[128]);
     int init_rccl(const uint8_t id[128], int world_size, int rank_);

@@ -27,6 +27,10 @@ int Comm::init_rccl(const uint8_t id[128], int world_size, int rank_) {
     }
     ncclUniqueId u;
     std::memcpy(&u, id, 128);
+    if (!scratch && hipMalloc(&scratch, SCRATCH_BYTES) != hipSuccess) {
+        scratch = nullptr;
+        return ELP_E_NOMEM;
+    }
     ncclComm_t c = nullptr;
     if (ncclCommInitRank(&c, world, u, rank) != ncclSuccess) return ELP_E_COMM;
     nccl = c;
@@ -40,6 +44,10 @@ int Comm::init_host(int world_size, int rank_, elp_host_allgather_fn ag, elp_hos
     world = world_size;
     rank = rank_;
     kind = world > 1 ? 2 : 0;
+    if (!scratch && hipMalloc(&scratch, SCRATCH_BYTES) != hipSuccess) {
+        scratch = nullptr;
+        return ELP_E_NOMEM;
+    }
     h_allgather = ag;
     h_allreduce = ar;
     h_bcast = bc;
@@ -49,12 +57,13 @@ int Comm::init_host(int world_size, int rank_, elp_host_allgather_fn ag, elp_hos
 
 // Round-trip probe of freshly mapped mailboxes: thread t stores a reserved
 // sequence word into this rank's slots (both parities) of rank t's mailbox,
-// then waits (2 s at most) for rank t's word in its own.  Proves, before the
+// then waits (the mailbox timeout at most) for rank t's word in its own.  Proves, before the
 // first solve, that remote stores land and become visible to the polling
 // loads (p2p_exchange's protocol); the reserved word can never equal a real
 // iteration's sequence (epoch << 40 | iteration + 1).
 constexpr int64_t MBOX_PROBE_SEQ = INT64_MAX;
-__global__ void k_mbox_probe(void* const* peers, void* mine, int P, int rank, int64_t rec, int* ok_out) {
+__global__ void k_mbox_probe(void* const* peers, void* mine, int P, int rank, int64_t rec, int* ok_out,
+                             unsigned long long ticks) {
     __shared__ int fail;
     const int t = threadIdx.x;
     if (t == 0) fail = 0;
@@ -73,7 +82,7 @@ __global__ void k_mbox_probe(void* const* peers, void* mine, int P, int rank, in
             int64_t* s = reinterpret_cast<int64_t*>(static_cast<char*>(mine) + (par * P + t) * rec + rec - 8);
             while (__hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != MBOX_PROBE_SEQ) {
                 __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
+                if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {  // 100 MHz clock
                     atomicOr(&fail, 1);
                     break;
                 }
@@ -87,7 +96,7 @@ __global__ void k_mbox_probe(void* const* peers, void* mine, int P, int rank, in
 // Collective over the communicator: every rank takes every step (the handle
 // all-gather and the final agreement), so a rank that fails to allocate or to
 // map a peer does not strand the others; if any rank failed, none uses p2p.
-int Comm::enable_p2p(size_t rec_bytes, hipStream_t st) {
+int Comm::enable_p2p(size_t rec_bytes, hipStream_t st, double timeout_s) {
     if (kind == 0) return ELP_E_STATE;
     if (p2p) return 0;
     const size_t bytes = 2 * (size_t)world * rec_bytes;
@@ -102,8 +111,10 @@ int Comm::enable_p2p(size_t rec_bytes, hipStream_t st) {
     if (ok && hipMemset(mbox, 0, bytes) != hipSuccess) ok = 0;
     if (ok && hipIpcGetMemHandle(&mine, mbox) != hipSuccess) ok = 0;
     static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
-    unsigned char* dstage = nullptr;
-    if (hipMalloc((void**)&dstage, 64 * ((size_t)world + 1) + sizeof(int32_t)) != hipSuccess) return ELP_E_NOMEM;
+    // staging of the two collectives below: the scratch buffer allocated with
+    // the communicator, so no allocation here can make this rank skip them
+    if (!scratch || world > SCRATCH_RANKS) return ELP_E_STATE;
+    unsigned char* dstage = static_cast<unsigned char*>(scratch);
     std::vector<unsigned char> all(64 * (size_t)world);
     int rc = hipMemcpy(dstage + 64 * world, &mine, 64, hipMemcpyHostToDevice) == hipSuccess ? 0 : ELP_E_HIP;
     if (!rc) rc = allgather(dstage + 64 * world, dstage, 64, st);
@@ -133,8 +144,9 @@ int Comm::enable_p2p(size_t rec_bytes, hipStream_t st) {
     if (!rc && ok) {
         int32_t* dok = reinterpret_cast<int32_t*>(dstage);
         int32_t hok = 0;
+        const double secs = timeout_s > 0 ? timeout_s : 2.0;
         hipLaunchKernelGGL(k_mbox_probe, dim3(1), dim3(64), 0, st, (void* const*)dpeers, mbox, world, rank,
-                           (int64_t)rec_bytes, dok);
+                           (int64_t)rec_bytes, dok, (unsigned long long)(secs * 1e8));
         if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess ||
             hipMemcpy(&hok, dok, sizeof(hok), hipMemcpyDeviceToHost) != hipSuccess || !hok)
             ok = 0;
@@ -146,7 +158,6 @@ int Comm::enable_p2p(size_t rec_bytes, hipStream_t st) {
     if (!rc) rc = allreduce_max_i32(dflag, 1, st);
     if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = ELP_E_HIP;
     if (!rc && hipMemcpy(&failed, dflag, sizeof(failed), hipMemcpyDeviceToHost) != hipSuccess) rc = ELP_E_HIP;
-    (void)hipFree(dstage);
     if (rc || failed) {
         for (void* p : opened) (void)hipIpcCloseMemHandle(p);
         opened.clear();
@@ -169,6 +180,8 @@ void Comm::destroy() {
     mbox = nullptr;
     p2p = 0;
     if (kind == 1 && nccl) ncclCommDestroy((ncclComm_t)nccl);
+    if (scratch) (void)hipFree(scratch);
+    scratch = nullptr;
     nccl = nullptr;
     kind = 0;
     world = 1;

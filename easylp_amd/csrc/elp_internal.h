@@ -182,6 +182,8 @@ struct Dev {
     int64_t* trace;
     int32_t maximize, pad2;
     double infinity;
+    double tol_singular;  // Gauss-Jordan: |pivot| <= this -> ST_NUMFAIL (elp_control)
+    int64_t mb_ticks;     // xGMI mailbox wait limit in s_memrealtime ticks (100 MHz)
     // CSC input (elp_load_csc, one GPU): A is null, columns live in cptr/rind/cval
     // (rows ascending), a CSR copy serves the row activities, and the entering
     // column is scattered into the dense qcol each iteration

@@ -865,7 +865,8 @@ constexpr int MAX_P2P = 64;  // ranks a mailbox exchange supports
 // every rank's mailbox (fields, system-scope fence, then the sequence word);
 // every workgroup waits until all slots of this iteration carry its sequence
 // number and reduces them with the candidate total order, so all ranks agree.
-// Returns false (status ST_COMMFAIL) if a peer stays silent for 2 s.
+// Returns false (status ST_COMMFAIL) if a peer stays silent for Dev::mb_ticks
+// (elp_control.mailbox_timeout).
 DEV bool p2p_exchange(const Dev& d, Cand& best, int bland, int64_t iter, int64_t epoch, CandX* s_rec,
                       int* s_fail) {
     const int P = d.world;
@@ -895,7 +896,7 @@ DEV bool p2p_exchange(const Dev& d, Cand& best, int bland, int64_t iter, int64_t
         bool ok = true;
         while (__hip_atomic_load(&r->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != want) {
             __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
+            if (__builtin_amdgcn_s_memrealtime() - t0 > (unsigned long long)d.mb_ticks) {  // 100 MHz clock
                 ok = false;
                 break;
             }
@@ -2285,7 +2286,7 @@ __global__ void __launch_bounds__(256) k_gj_step(Dev d, int k, int col, const do
         if (blockIdx.x == 0) {
             d.perm[col] = r;
             d.pivstep[r] = col;
-            if (!(fabs(s_piv) > 1e-13)) d.ctl->status = ST_NUMFAIL;
+            if (!(fabs(s_piv) > d.tol_singular)) d.ctl->status = ST_NUMFAIL;
         }
     }
     __syncthreads();

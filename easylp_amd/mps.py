@@ -13,7 +13,8 @@ MPS dialects are read (whitespace-separated fields; names without spaces):
 The result maps onto the C ABI's arrays: a ranged row becomes two rows (>= and
 <=) because elp_load_* takes one direction per row; the objective constant is
 returned separately (EasyLP adds its `objective_add` outside the solver too,
-R/class.R:593-597).  The first N row is the objective; other N rows are dropped.
+R/class.R:593-597).  The first N row is the objective; other N rows (free rows)
+are dropped, and their COLUMNS / RHS / RANGES entries with them.
 """
 from __future__ import annotations
 
@@ -79,6 +80,7 @@ def read_mps(path_or_text: str, *, text: bool = False) -> MpsProblem:
     row_type = []      # 'L' 'G' 'E'
     row_names = []
     obj_row = None
+    free_rows = set()  # N rows after the first: dropped with their entries
     cols = {}          # name -> index
     col_names = []
     entries = []       # (row, col, value)
@@ -125,6 +127,8 @@ def read_mps(path_or_text: str, *, text: bool = False) -> MpsProblem:
             if t == "N":
                 if obj_row is None:
                     obj_row = rn
+                else:
+                    free_rows.add(rn)
                 continue
             if t not in ("L", "G", "E"):
                 raise MpsError(f"line {lineno}: row type {t!r}")
@@ -157,6 +161,8 @@ def read_mps(path_or_text: str, *, text: bool = False) -> MpsProblem:
                     obj[j] += v
                 elif rn in rows:
                     entries.append((rows[rn], j, v))
+                elif rn in free_rows:
+                    continue
                 else:
                     raise MpsError(f"line {lineno}: unknown row {rn!r}")
         elif section in ("RHS", "RANGES"):
@@ -167,6 +173,8 @@ def read_mps(path_or_text: str, *, text: bool = False) -> MpsProblem:
                     obj_const = -v
                 elif rn in rows:
                     (rhs_vals if section == "RHS" else rng_vals)[rows[rn]] = v
+                elif rn in free_rows or rn == obj_row:
+                    continue
                 else:
                     raise MpsError(f"line {lineno}: unknown row {rn!r}")
         elif section == "BOUNDS":

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define ELP_ABI_VERSION 1
+#define ELP_ABI_VERSION 2
 
 /* row directions, mirroring R/class.R:272 ("==" -> "=") and the "<"/">"
  * spellings accepted by R/methods.R:215-219 */
@@ -79,8 +79,26 @@ typedef struct elp_control {
                                 with Devex reference weights, lp_solve's default
                                 pricer (lp.control(pivoting = "devex"));
                                 ELP_PRICE_DANTZIG: largest |d_j|               */
-    int32_t reserved[3];
+    int32_t ngpu;            /* devices this handle drives in ONE process (the
+                                R caller stays one process): <= 1 one GPU; P > 1
+                                shards the columns over devices device ..
+                                device+P-1 (mod the visible count) with one host
+                                thread per device and an in-process
+                                communicator (RCCL over xGMI when the devices
+                                are distinct).  Excludes elp_comm_init*.       */
+    int32_t scaling;         /* ELP_SCALE_* bits (lp.control(scaling = ...)):
+                                0 none; ELP_SCALE_GEOMETRIC | ELP_SCALE_EQUILIBRATE
+                                (default, lp_solve's "geometric" + "equilibrate");
+                                factors are powers of 2 so scaling is exact     */
+    int32_t reserved0;
+    double tol_singular;     /* |pivot| <= this in a Gauss-Jordan refactor is a
+                                singular basis -> status 5            (1e-13)  */
+    double mailbox_timeout;  /* xGMI mailbox: seconds a rank waits for a peer's
+                                record before the solve fails (ELP_E_COMM) (2) */
 } elp_control;
+
+#define ELP_SCALE_GEOMETRIC 4   /* elp_control.scaling bits (lp_solve's numbering) */
+#define ELP_SCALE_EQUILIBRATE 64
 
 typedef struct elp_stats {
     int64_t iterations;        /* simplex iterations, both phases             */

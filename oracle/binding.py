@@ -15,6 +15,9 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _SO = os.path.join(_HERE, "_build", "libelp_oracle.so")
+# ELP_ORACLE_SO: another build of the same source (the ASan/UBSan one of
+# `make sanitize`, run_sanitized_tests.sh)
+_SO = os.environ.get("ELP_ORACLE_SO") or _SO
 _lib = None
 
 
@@ -32,6 +35,7 @@ class OrcControl(ctypes.Structure):
         ("price_mode", ctypes.c_int32),
         ("price_rule", ctypes.c_int32),
         ("pad0", ctypes.c_int32),
+        ("tol_singular", ctypes.c_double),
     ]
 
 

@@ -118,6 +118,7 @@ typedef struct {
     int64_t *cp, *ri; /* price_mode 1: nonzero pattern of A by column      */
     int64_t gj_count; /* refactors that needed a fresh Gauss-Jordan */
     int refactor_mode;
+    double tol_singular;
     double *dw, *dprev; /* price_rule 1: Devex weight and last reduced cost
                            of each structural and slack (n + m)            */
 } orc_t;
@@ -223,7 +224,7 @@ static int gauss_jordan(orc_t* s) {
                 p = r;
             }
         const double piv = W[p * k + c];
-        if (!(fabs(piv) > 1e-13)) return -1;
+        if (!(fabs(piv) > s->tol_singular)) return -1;
         s->perm[c] = p;
         for (int64_t r = 0; r < k; ++r) {
             if (r == p) {
@@ -893,6 +894,7 @@ void orc_default_control(orc_control* c) {
     c->price_mode = 0;
     c->price_rule = 1;
     c->pad0 = 0;
+    c->tol_singular = 1e-13;
 }
 
 static int cmp_i64(const void* a, const void* b) {
@@ -946,6 +948,7 @@ int orc_solve_dense_sens(int64_t m, int64_t n, const double* A, const int32_t* d
         s->cp[j + 1] = t;
     }
     s->refactor_mode = ctl.refactor_mode;
+    s->tol_singular = ctl.tol_singular;
     const int64_t nv = s->nv, mm = m > 0 ? m : 1;
     s->b = dalloc((size_t)mm);
     s->lb = dalloc((size_t)nv);
@@ -1131,7 +1134,11 @@ int orc_solve_dense_sens(int64_t m, int64_t n, const double* A, const int32_t* d
 /*   1e-9 |best|) -> prune (zmin: objective in minimisation form);         */
 /*   branch on the lowest-index integer column with |x - round(x)| > 1e-7  */
 /*   (lp_solve's epsint); ceiling branch explored first (lp_solve's        */
-/*   default floor_first = CEILING); LIFO stack.                            */
+/*   default floor_first = CEILING); LIFO stack.  ctl->max_iter > 0 bounds  */
+/*   the LP iterations of the whole tree: a node that hits it ends the      */
+/*   search; a node that fails numerically is skipped.  Either makes the    */
+/*   tree incomplete: incumbent -> 1 (sub-optimal), none -> that node's     */
+/*   status.                                                               */
 typedef struct { double* lo; double* up; } bnb_node;
 
 int orc_solve_mip(int64_t m, int64_t n, const double* A, const int32_t* dir, const double* rhs,
@@ -1161,8 +1168,11 @@ int orc_solve_mip(int64_t m, int64_t n, const double* A, const int32_t* dir, con
     double best = INF;
     double* xbest = dalloc((size_t)n);
     double* x = dalloc((size_t)n);
-    int have = 0, status = -1;
+    int have = 0, status = -1, failed = -1;
     orc_stats st;
+    orc_control nctl;
+    if (ctl) nctl = *ctl;
+    else orc_default_control(&nctl);
     while (top > 0) {
         bnb_node nd = stack[--top];
         if (max_nodes > 0 && nodes >= max_nodes) {
@@ -1173,10 +1183,25 @@ int orc_solve_mip(int64_t m, int64_t n, const double* A, const int32_t* dir, con
         }
         nodes++;
         double z = 0.0;
-        const int s = orc_solve_dense(m, n, A, dir, rhs, obj, nd.lo, nd.up, maximize, ctl, &z, x,
-                                      NULL, NULL, NULL, 0, &st);
+        if (ctl && ctl->max_iter > 0) nctl.max_iter = ctl->max_iter - iters > 0 ? ctl->max_iter - iters : 0;
+        /* (max_iter 0 would mean "default": a spent budget runs no iteration) */
+        int s;
+        if (ctl && ctl->max_iter > 0 && nctl.max_iter == 0) {
+            s = 1;
+            memset(&st, 0, sizeof st);
+        } else {
+            s = orc_solve_dense(m, n, A, dir, rhs, obj, nd.lo, nd.up, maximize, &nctl, &z, x, NULL, NULL,
+                                NULL, 0, &st);
+        }
         iters += st.iterations;
         int branched = 0;
+        if (s != 0 && s != 2 && s != 3) { /* iteration budget or numerical failure */
+            if (failed < 0) failed = s;
+            free(nd.lo);
+            free(nd.up);
+            if (s == 1) break;
+            continue;
+        }
         if (s == 3) {
             status = 3;
             free(nd.lo);
@@ -1229,7 +1254,17 @@ int orc_solve_mip(int64_t m, int64_t n, const double* A, const int32_t* dir, con
             free(nd.up);
         }
     }
-    if (status != 3) status = have ? (status == 1 ? 1 : 0) : (status == 1 ? 1 : 2);
+    while (top > 0) { /* a limit ended the search */
+        --top;
+        free(stack[top].lo);
+        free(stack[top].up);
+    }
+    if (status != 3) {
+        const int limit = status == 1;
+        if (have) status = (limit || failed >= 0) ? 1 : 0;
+        else if (failed >= 0) status = failed;
+        else status = limit ? 1 : 2;
+    }
     if (have && status != 3) {
         if (xout) memcpy(xout, xbest, (size_t)n * sizeof(double));
         if (objval) {

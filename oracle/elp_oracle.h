@@ -46,6 +46,7 @@ typedef struct orc_control {
     int32_t price_rule;    /* 0 Dantzig (largest |d_j|), 1 Devex reference
                               weights (largest d_j^2 / w_j; run_phase)        */
     int32_t pad0;
+    double tol_singular;   /* Gauss-Jordan |pivot| <= this: numerical failure */
 } orc_control;
 
 typedef struct orc_stats {

@@ -30,19 +30,36 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version_and_defaults():
-    from easylp_amd._lib import ElpControl, load
+    from easylp_amd._lib import ABI_VERSION, ElpControl, load
     lib = load()
-    assert lib.elp_abi_version() == 1
+    assert lib.elp_abi_version() == ABI_VERSION == 2
     c = ElpControl()
     lib.elp_default_control(ctypes.byref(c))
     assert c.infinity == 1e30 and c.refactor_period == 100 and c.sync_every == 32
+    assert c.tol_singular == 1e-13 and c.mailbox_timeout == 2.0 and c.ngpu == 1
 
 
-def test_control_struct_size_matches_header():
-    # 5 doubles + int64 + 8 int32 fields + 4 reserved int32 = 96 bytes
+def _c_layout(struct, fields, tmp_path):
+    """sizeof / offsetof of a header struct, from gcc (the ctypes mirror must match)."""
+    import subprocess
+    src = tmp_path / "lay.c"
+    body = "".join(f'printf("%zu\\n", offsetof({struct}, {f}));' for f in fields)
+    src.write_text(f'#include <stdio.h>\n#include <stddef.h>\n#include "{HEADER}"\n'
+                   f'int main(void){{printf("%zu\\n", sizeof({struct}));{body}return 0;}}\n')
+    exe = tmp_path / "lay"
+    subprocess.run(["gcc", "-o", str(exe), str(src)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
+    return int(out[0]), [int(v) for v in out[1:]]
+
+
+@pytest.mark.parametrize("which", ["elp_control", "elp_stats"])
+def test_struct_layout_matches_header(which, tmp_path):
     from easylp_amd._lib import ElpControl, ElpStats
-    assert ctypes.sizeof(ElpControl) == 96
-    assert ctypes.sizeof(ElpStats) == 8 * 8 + 4 * 8 + 4 + 4 + 16 + 8 + 8 + 8 + 8 + 16
+    cls = ElpControl if which == "elp_control" else ElpStats
+    names = [f for f, _ in cls._fields_]
+    size, offs = _c_layout(which, names, tmp_path)
+    assert ctypes.sizeof(cls) == size
+    assert [getattr(cls, f).offset for f in names] == offs
 
 
 def test_usage_errors_without_gpu():

@@ -76,3 +76,39 @@ ENDATA
     p, g = solve_mps(str(f))
     assert g.status == 0 and g.objval == 20.0  # b + c
     np.testing.assert_array_equal(g.x, [0, 1, 1])
+
+
+@pytest.mark.parametrize("name", ["students", "cyingair", "investments"])
+def test_mip_iteration_budget_matches_oracle(gpu, name):
+    """max_iter bounds the whole tree on the GPU as in the oracle: same status,
+    node count, LP iterations and incumbent for budgets that end the search at
+    different depths."""
+    from oracle import solve_mip
+    rec = next(r for r in MIP if r["name"] == name)
+    args = (rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], rec["maximize"])
+    total = solve_mip(*args, rec["is_int"]).stats["lp_iterations"]
+    for cap in sorted({1, 3, max(1, total // 3), max(1, total // 2), max(1, total - 1), total + 5}):
+        o = solve_mip(*args, rec["is_int"], max_iter=cap)
+        g = gpu.solve_dense(*args, is_int=rec["is_int"], max_iter=cap)
+        assert (g.status, g.stats["mip_nodes"], g.stats["mip_lp_iterations"]) == (
+            o.status, o.stats["nodes"], o.stats["lp_iterations"]), cap
+        assert o.stats["lp_iterations"] <= cap
+        if o.status in (0, 1) and g.status in (0, 1) and o.objval != 0.0:
+            assert g.objval == o.objval
+
+
+def test_mip_time_limit_bounds_the_whole_tree(gpu):
+    """time_limit counts from the start of the branch and bound: a tree that
+    needs many nodes stops with 1 (incumbent) or 7 (none) instead of running on."""
+    import time
+    rng = np.random.default_rng(7)
+    m, n = 30, 60
+    A = rng.integers(1, 40, (m, n)).astype(float)
+    b = A.sum(axis=1) * 0.37
+    c = rng.integers(1, 60, n).astype(float)
+    t0 = time.time()
+    g = gpu.solve_dense(A, np.ones(m, np.int32), b, c, np.zeros(n), np.full(n, 3.0), True,
+                        is_int=np.ones(n, np.int32), time_limit=0.05)
+    el = time.time() - t0
+    assert g.status in (1, 7)
+    assert el < 5.0

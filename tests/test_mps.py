@@ -127,3 +127,32 @@ def test_errors():
         read_mps("NAME X\nROWS\n N obj\nCOLUMNS\n    x nope 1\nENDATA\n", text=True)
     with pytest.raises(MpsError, match="bad number"):
         read_mps("NAME X\nROWS\n N obj\n L r\nCOLUMNS\n    x r abc\nENDATA\n", text=True)
+
+
+def test_free_rows_dropped_with_their_entries():
+    """N rows after the first are free rows: their COLUMNS / RHS / RANGES
+    entries are skipped, not reported as unknown rows."""
+    t = """NAME FREE
+ROWS
+ N obj
+ N FREE
+ L c1
+ N FREE2
+COLUMNS
+    x obj 1 FREE 7
+    x c1 1 FREE2 -2
+    y obj 2 c1 1
+    y FREE 3
+RHS
+    rhs c1 4 FREE 9
+RANGES
+    rng FREE2 1
+ENDATA
+"""
+    p = read_mps(t, text=True)
+    assert p.row_names == ["c1"]
+    np.testing.assert_array_equal(p.obj, [1.0, 2.0])
+    np.testing.assert_array_equal(p.rhs, [4.0])
+    np.testing.assert_array_equal(p.dense(), [[1.0, 1.0]])
+    with pytest.raises(MpsError, match="unknown row"):
+        read_mps(t.replace("y FREE 3", "y NOPE 3"), text=True)

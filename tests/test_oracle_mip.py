@@ -51,3 +51,27 @@ def test_infeasible_and_node_limit():
     o = solve_mip(rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"],
                   rec["maximize"], rec["is_int"], max_nodes=5)
     assert o.status == 1 and o.stats["nodes"] == 5
+
+
+def test_iteration_budget_bounds_the_whole_tree():
+    """ctl.max_iter caps the LP iterations of the whole branch and bound (not each
+    node): the search stops when a node hits it; with an incumbent the result is
+    sub-optimal (1), without one the failed node's status (1)."""
+    from oracle import solve_mip
+    rec = next(r for r in MIP if r["name"] == "students")
+    args = (rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], rec["maximize"],
+            rec["is_int"])
+    full = solve_mip(*args)
+    assert full.status == 0 and full.stats["nodes"] > 1
+    total = full.stats["lp_iterations"]
+    # a budget inside the first node: no incumbent, the node's status
+    o = solve_mip(*args, max_iter=3)
+    assert o.status == 1 and o.stats["lp_iterations"] <= 3 and o.stats["nodes"] == 1
+    # a budget that runs out later in the tree: never more iterations than allowed
+    for cap in (total // 2, total - 1):
+        o = solve_mip(*args, max_iter=cap)
+        assert o.status == 1
+        assert o.stats["lp_iterations"] <= cap
+    # a budget above the total changes nothing
+    o = solve_mip(*args, max_iter=total + 10)
+    assert o.status == 0 and o.objval == full.objval and o.stats["nodes"] == full.stats["nodes"]
