@@ -1,25 +1,32 @@
 #!/usr/bin/env python3
-"""bench.py -- simplex iterations/s on the dense random LP of BASELINE.json.
+"""bench.py -- simplex iterations/s + time-to-optimal on the dense LP of BASELINE.json.
 
 Workload (BASELINE.json configs[2], the config its metric is quoted on):
 maximize c'x s.t. A x <= b, x >= 0, A dense 5000 x 50000 fp64 with
-A_ij, c_j ~ U[0,1), b_i = n/8 + U n/4, generated on the device
-by the counter-based generator (data: synthetic).  A "step" is one simplex
-iteration (BTRAN, pricing sweep + argmin, FTRAN, ratio test, basis update;
-periodic refactor included).  Inputs are resident in HBM before timing.
+A_ij, c_j ~ U[0,1), b_i = n/8 + U n/4, generated into HBM once
+by the counter-based generator (data: synthetic; generation is not timed).
+
+A "step" is ONE FULL SOLVE: elp_load_dense_device (canonicalisation, the
+row-major copy of A, the Y-row copy, phase decision) + elp_solve to
+optimality, from A already resident in HBM -- what easylp$solve() does per
+call (R/class.R:260-278).  `value` = simplex iterations of the K timed solves /
+their wall time, i.e. the whole-solve iteration rate, and `time_to_optimal_s`
+= wall time per solve (load included, generation excluded).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
-Rank 0 prints one JSON line.  With N > 1 (torchrun) the columns of A are
-sharded across ranks (one process per GPU, RCCL min-loc + entering-column
-exchange per iteration) and all ranks run the same iterations: value is the
-iteration rate of the one LP (strong scaling).
+Rank 0 prints one JSON line.  With N > 1 (torchrun; without a launcher
+bench.py starts torchrun itself) the columns are sharded across ranks (one
+process per GPU, per-iteration RCCL min-loc) and every rank runs the same
+solve: `value` is the iteration rate of the one LP (strong scaling).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
+import subprocess
 import sys
 import time
 
@@ -33,23 +40,20 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=10, help="timed full solves")
+    ap.add_argument("--warmup", type=int, default=2, help="untimed full solves")
     ap.add_argument("--m", type=int, default=5000)
     ap.add_argument("--n", type=int, default=50000)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--cpu-iters", type=int, default=300,
-                    help="iterations of the CPU oracle sample (after --warmup)")
+    ap.add_argument("--cpu-iters", type=int, default=0,
+                    help="cap on the CPU oracle's iterations (0: one full solve, ~20 s)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-optimal", action="store_true", help="skip the run to optimality")
     ap.add_argument("--profile-price", type=int, default=1,
-                    help="HIP events around the pricing kernel (roofline)")
+                    help="device-clock timer over every pricing launch (roofline)")
     ap.add_argument("--c4", type=int, default=1,
-                    help="also time the 10000x500000 column-sharded config (SURVEY config 4)")
-    ap.add_argument("--c4-steps", type=int, default=300)
-    ap.add_argument("--c4-warmup", type=int, default=100)
-    ap.add_argument("--p2p", type=int, default=1,
-                    help="N>1: per-iteration min-loc through the xGMI mailbox (0: RCCL all-gather)")
+                    help="also solve the 10000x500000 column-sharded config (SURVEY config 4) to optimality")
+    ap.add_argument("--p2p", type=int, default=0,
+                    help="N>1: per-iteration min-loc through the xGMI mailbox (default: RCCL all-gather)")
     ap.add_argument("--force-sharded", action="store_true",
                     help="N=1: run the sharded pipeline on a 1-rank RCCL communicator (overhead probe)")
     ap.add_argument("--sparse", type=int, default=1,
@@ -64,9 +68,36 @@ def parse():
                     help="iterations enqueued between host polls (elp_control.sync_every)")
     ap.add_argument("--compare-rules", type=int, default=1,
                     help="N=1: also solve the LP to optimality with the other pricing rule")
+    ap.add_argument("--window", type=int, default=1,
+                    help="also report the steady-state rate over iterations [100, 1100) of one solve")
     a = ap.parse_args()
     a.rule = 1 if a.pricing == "devex" else 0
     return a
+
+
+def relaunch_under_torchrun(args) -> int:
+    """--gpus N > 1 without a launcher: start torchrun as a child before any GPU
+    call (never exec from this process) and return its exit code."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def host_info():
+    model = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model, os.cpu_count()
 
 
 def enable_p2p(p, rank):
@@ -82,96 +113,131 @@ def enable_p2p(p, rank):
         return False
 
 
+def make_problem(args, lib, m, n, world, rank, local, **ctl):
+    from easylp_amd import Problem
+    from easylp_amd._lib import ELP_PROFILE_PRICE
+    p = Problem(m, n, device=local, verbose=ELP_PROFILE_PRICE if args.profile_price else 0,
+                pricing=args.rule, sync_every=args.sync_every, **ctl)
+    p2p = False
+    if world > 1 or args.force_sharded:
+        from easylp_amd.dist import share_unique_id
+        p.comm_init(share_unique_id(lib, rank), world, rank)
+        if args.p2p:
+            p2p = enable_p2p(p, rank)
+    return p, p2p
+
+
+def full_solves(p, A, b, c, count, barrier):
+    """`count` full solves (load from HBM + solve to optimality); per-solve stats."""
+    import numpy as np
+    dirs = np.ones(len(b), np.int32)
+    recs = []
+    for _ in range(count):
+        t0 = time.perf_counter()
+        p.load_dense_device(A.data_ptr(), dirs, b, c, maximize=True)
+        st = p.solve()
+        el = time.perf_counter() - t0
+        recs.append((st, el, p.stats()))
+    barrier()
+    return recs
+
+
+def price_roofline(stats_list):
+    """Pricing-launch roofline over the given solves: algorithmic sweep bytes /
+    device-clock launch time (every workgroup of each timed launch)."""
+    secs = sum(s["price_seconds"] for s in stats_list)
+    byts = sum(s["price_timed_bytes"] for s in stats_list)
+    nl = sum(s["price_timed_launches"] for s in stats_list)
+    ach = byts / secs / 1e9 if secs > 0 else None
+    return {"achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": ach / HBM_PEAK_GBS if ach else None,
+            "bytes_per_launch": byts / nl if nl else None,
+            "avg_launch_us": 1e6 * secs / nl if nl else None, "launches_timed": nl}
+
+
 def cpu_baseline(args):
-    """The CPU oracle (same algorithm, 1 thread) on a bounded sample of the same LP."""
+    """The CPU oracle (same algorithm, 1 thread) solving the same LP: one full
+    solve by default (about 20 s on one EPYC core), else the first --cpu-iters."""
     import numpy as np
     from oracle import generate_dense, solve_dense
     A, b, c = generate_dense(args.seed, args.m, args.n)
-    t0 = time.time()
-    r = solve_dense(A, np.ones(args.m, np.int32), b, c, maximize=True, price_rule=args.rule,
-                    max_iter=args.warmup + args.cpu_iters, t_mark_iter=args.warmup)
-    wall = time.time() - t0
-    it = r.stats["iterations"] - args.warmup
-    secs = r.stats["seconds_at_mark"]
+    kw = {"max_iter": args.cpu_iters} if args.cpu_iters > 0 else {}
+    r = solve_dense(A, np.ones(args.m, np.int32), b, c, maximize=True, price_rule=args.rule, **kw)
+    it, secs = r.stats["iterations"], r.stats["seconds"]
+    model, ncpu = host_info()
+    full = r.status == 0
     return {
         "value": it / secs if secs > 0 else None,
         "unit": "iterations/s",
         "cores": 1,
         "kind": "port",
-        "sample": (f"oracle/ (C, -O3, 1 thread) on the same LP, iterations "
-                   f"[{args.warmup}, {args.warmup + it}) timed; {wall:.1f}s wall incl. "
-                   f"iterations [0,{args.warmup})"),
+        "time_to_optimal_s": secs if full else None,
+        "iterations": it,
+        "sample": ("oracle/ (C, -O3, 1 thread) %s of the same LP: %d iterations in %.1f s "
+                   "(setup included, generation excluded)" % (
+                       "one full solve" if full else "the first iterations", it, secs)),
+        "host": {"cpu": model, "nproc": ncpu},
     }
 
 
 def committed_traffic(args):
-    """HBM traffic per pricing launch from the committed rocprofv3 --pmc FETCH_SIZE
-    pass of this same command (tools/gpu_check.sh -> profiles/pmc_traffic.json);
-    only used when that pass measured the same LP and iteration window."""
+    """HBM traffic per pricing launch from the committed rocprofv3 --pmc
+    FETCH_SIZE pass of this same command (tools/gpu_check.sh ->
+    profiles/pmc_traffic.json); used only when that pass ran the same LP,
+    steps and warmup."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         t = json.load(open(path))
     except (OSError, ValueError):
         return None, None
-    same = (t.get("m"), t.get("n"), t.get("warmup"), t.get("steps")) == (
-        args.m, args.n, args.warmup, args.steps)
+    same = (t.get("m"), t.get("n"), t.get("warmup"), t.get("steps"), t.get("step")) == (
+        args.m, args.n, args.warmup, args.steps, "full solve")
     if not same:
         return None, None
     return t["traffic_bytes_per_launch"], "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE, x2 gfx950)"
 
 
-def c4_rate(args, lib, world, rank, local, barrier, dist):
-    """Iterations/s of the north-star scaling config: dense LP m=10000 n=500000,
-    columns sharded over the ranks.  Same step definition."""
+def c4_config(args, lib, world, rank, local, barrier, dist):
+    """BASELINE config 4: dense LP m=10000 n=500000 (40 GB), columns sharded over
+    the ranks, solved to optimality from A resident in HBM."""
+    import numpy as np
     import torch
-    from easylp_amd import Problem
+    from easylp_amd import generate_dense_device
     m, n = 10000, 500000
-    from easylp_amd._lib import ELP_PROFILE_PRICE
-    p = Problem(m, n, device=local, pricing=args.rule, verbose=ELP_PROFILE_PRICE if args.profile_price else 0)
-    if world > 1 or args.force_sharded:
-        from easylp_amd.dist import share_unique_id
-        p.comm_init(share_unique_id(lib, rank), world, rank)
-        if args.p2p:
-            enable_p2p(p, rank)
-    t_load = time.perf_counter()
-    p.load_generated(args.seed)
+    A, b, c = generate_dense_device(args.seed, m, n, local)
+    p, _ = make_problem(args, lib, m, n, world, rank, local)
     barrier()
-    t_load = time.perf_counter() - t_load
-    p.iterate(args.c4_warmup)
-    barrier()
-    s0 = p.stats()
     t0 = time.perf_counter()
-    p.iterate(args.c4_steps)
+    p.load_dense_device(A.data_ptr(), np.ones(m, np.int32), b, c, maximize=True)
+    barrier()
+    t_load = time.perf_counter() - t0
+    st = p.solve()
     barrier()
     el = time.perf_counter() - t0
-    s1 = p.stats()
-    if world > 1:
-        tt = torch.tensor([el], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
-    it = s1["iterations"] - s0["iterations"]
+    s = p.stats()
+    obj = p.solution(st).objval
     p.close()
-    # this rank's pricing sweep over its column shard (device clock, as the headline roofline)
-    price_s = s1["price_seconds"] - s0["price_seconds"]
-    price_b = s1["price_timed_bytes"] - s0["price_timed_bytes"]
-    price_n = s1["price_timed_launches"] - s0["price_timed_launches"]
-    sweep = None
-    if price_s > 0 and price_n > 0:
-        gbs = price_b / price_s / 1e9
-        sweep = {"achieved": gbs, "peak": 8000.0, "unit": "GB/s", "frac": gbs / 8000.0,
-                 "bytes_per_launch": price_b / price_n, "avg_sweep_us": 1e6 * price_s / price_n, "rank": rank}
+    del A
+    torch.cuda.empty_cache()
+    if world > 1:
+        tt = torch.tensor([el, t_load], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el, t_load = float(tt[0]), float(tt[1])
+    sweep = price_roofline([s])
+    sweep["rank"] = rank
     return {"workload": "dense random LP m=10000 n=500000 (SURVEY config 4), columns sharded x%d" % world,
-            "price_sweep": sweep,
-            "value": it / el if el > 0 else None, "unit": "iterations/s", "iterations_timed": it,
-            "warmup": args.c4_warmup, "ms_per_step": 1e3 * el / max(it, 1),
-            "bump_dim": s1["bump_dim"], "y_rows": s1["y_rows"], "load_s": t_load}
+            "status": st, "objective": obj, "iterations_to_optimal": s["iterations"],
+            "time_to_optimal_s": el, "load_s": t_load,
+            "value": s["iterations"] / el if el > 0 else None, "unit": "iterations/s (whole solve)",
+            "bump_dim": s["bump_dim"], "y_rows": s["y_rows"], "refactors": s["refactors"],
+            "price_sweep": sweep}
 
 
 def sparse_rate(args, local, with_cpu):
     """BASELINE config 5 on the CSC path: a seeded sparse LP of Netlib-like shape
     (easylp_amd.synth.sparse_packing, 5 nonzeros per column) plus the Klee-Minty
-    cube n=12 (4095 pivots under Dantzig, a few dozen under Devex).  Same step definition; the CPU leg is the
-    oracle in its CSC order (price_mode 1) over a bounded window."""
+    cube n=12 (4095 pivots under Dantzig, a few dozen under Devex).  The CPU leg
+    is the oracle in its CSC order (price_mode 1) over a bounded window."""
     import numpy as np
     from easylp_amd import Problem
     from easylp_amd.synth import dense_of, sparse_packing
@@ -179,25 +245,27 @@ def sparse_rate(args, local, with_cpu):
     cp, ri, v, b, c = sparse_packing(args.seed, m, n, 5)
     dirs = np.ones(m, np.int32)
     p = Problem(m, n, device=local, pricing=args.rule)
+    t0 = time.perf_counter()
     p.load_csc(cp, ri, v, dirs, b, c, maximize=True)
-    p.iterate(args.warmup)
+    st = p.solve()
+    tto = time.perf_counter() - t0
+    s2 = p.stats()
+    sol = p.solution(st)
+    p.load_csc(cp, ri, v, dirs, b, c, maximize=True)  # steady-state window [100, 100 + steps)
+    p.iterate(100)
     s0 = p.stats()
     t0 = time.perf_counter()
     p.iterate(args.sparse_steps)
     el = time.perf_counter() - t0
     s1 = p.stats()
-    st = p.solve()
-    s2 = p.stats()
-    sol = p.solution(st)
     p.close()
     it = s1["iterations"] - s0["iterations"]
     out = {"workload": "sparse LP m=%d n=%d nnz=%d (CSC, BASELINE configs[4])" % (m, n, int(cp[-1])),
-           "value": it / el if el > 0 else None, "unit": "iterations/s", "iterations_timed": it,
-           "warmup": args.warmup, "ms_per_step": 1e3 * el / max(it, 1),
-           "time_to_optimal_s": s2["seconds_loop"], "status": st, "objective": sol.objval,
-           "iterations_to_optimal": s2["iterations"], "bump_dim": s2["bump_dim"]}
-    # Klee-Minty cube (degenerate-path case): time to optimal on the GPU
-    km = 12
+           "value": s2["iterations"] / tto, "unit": "iterations/s (whole solve)",
+           "time_to_optimal_s": tto, "status": st, "objective": sol.objval,
+           "iterations_to_optimal": s2["iterations"], "bump_dim": s2["bump_dim"],
+           "window": {"iterations": [100, 100 + it], "value": it / el if el > 0 else None}}
+    km = 12  # Klee-Minty cube (degenerate-path case)
     rows, cols, vals = [], [], []
     for i in range(km):
         for j in range(i + 1):
@@ -209,16 +277,18 @@ def sparse_rate(args, local, with_cpu):
     kb = np.array([5.0 ** (i + 1) for i in range(km)])
     kc = np.array([2.0 ** (km - 1 - j) for j in range(km)])
     with Problem(km, km, device=local, pricing=args.rule) as pk:
+        t0 = time.perf_counter()
         pk.load_csc(K.indptr, K.indices, K.data, np.ones(km, np.int32), kb, kc, maximize=True)
         kst = pk.solve()
+        kt = time.perf_counter() - t0
         ks = pk.stats()
         kobj = pk.solution(kst).objval
-    out["klee_minty"] = {"n": km, "iterations": ks["iterations"], "seconds": ks["seconds_loop"],
+    out["klee_minty"] = {"n": km, "iterations": ks["iterations"], "seconds": kt,
                          "objective": kobj, "expected": 5.0 ** km}
     if with_cpu:
         from oracle import solve_dense
         A = dense_of(cp, ri, v, m, n)
-        w = args.warmup
+        w = 100
         r = solve_dense(A, dirs, b, c, maximize=True, price_mode=1, price_rule=args.rule,
                         max_iter=w + args.sparse_cpu_iters, t_mark_iter=w)
         cit = r.stats["iterations"] - w
@@ -236,9 +306,11 @@ def sparse_rate(args, local, with_cpu):
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_under_torchrun(args))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
+    if args.gpus != world:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
 
     import torch
@@ -253,83 +325,78 @@ def main():
         dist.init_process_group("gloo", init_method="env://", rank=0, world_size=1)
     torch.cuda.set_device(local)
 
-    from easylp_amd import Problem
-    from easylp_amd._lib import ELP_PROFILE_PRICE, load
+    from easylp_amd import generate_dense_device
+    from easylp_amd._lib import load
 
     lib = load()
-    verbose = ELP_PROFILE_PRICE if args.profile_price else 0
-    p = Problem(args.m, args.n, device=local, verbose=verbose, pricing=args.rule, sync_every=args.sync_every)
-    if world > 1 or args.force_sharded:
-        from easylp_amd.dist import share_unique_id
-        p.comm_init(share_unique_id(lib, rank), world, rank)
-        if args.p2p:
-            args.p2p = int(enable_p2p(p, rank))
-
-    p.load_generated(args.seed)
 
     def barrier():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
 
-    # warmup (untimed)
-    st = p.iterate(args.warmup)
+    A, b, c = generate_dense_device(args.seed, args.m, args.n, local)  # resident in HBM, untimed
+    p, p2p = make_problem(args, lib, args.m, args.n, world, rank, local)
+
+    full_solves(p, A, b, c, args.warmup, barrier)  # warmup (untimed)
     barrier()
-    s0 = p.stats()
     t0 = time.perf_counter()
-    st = p.iterate(args.steps)
-    barrier()
-    t1 = time.perf_counter()
-    s1 = p.stats()
-    elapsed = t1 - t0
+    recs = full_solves(p, A, b, c, args.steps, barrier)  # (ends with a barrier)
+    elapsed = time.perf_counter() - t0
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    iters = s1["iterations"] - s0["iterations"]
+    stats = [r[2] for r in recs]
+    iters = sum(s["iterations"] for s in stats)
     value = iters / elapsed if elapsed > 0 else 0.0
+    roof = price_roofline(stats)
+    last = stats[-1] if stats else p.stats()
+    final = {"status": recs[-1][0] if recs else None, "iterations_to_optimal": last["iterations"],
+             "objective": p.solution(recs[-1][0]).objval if recs else None,
+             "bump_dim": last["bump_dim"], "y_rows": last["y_rows"], "refactors": last["refactors"],
+             "load_s": sum(s["seconds_load"] for s in stats) / max(len(stats), 1),
+             "price_launches_per_solve": last["price_launches"]}
 
-    price_dev_bytes = (s1["price_bytes"] - s0["price_bytes"]) / max(iters, 1)
-    price_s = s1["price_seconds"] - s0["price_seconds"]
-    price_b = s1["price_timed_bytes"] - s0["price_timed_bytes"]
-    price_n = s1["price_timed_launches"] - s0["price_timed_launches"]
-    achieved = price_b / price_s / 1e9 if price_s > 0 else None
-
-    # run on to optimality: time-to-optimal (device generation excluded)
-    tto = None
-    final = None
-    if not args.no_optimal:
-        st = p.solve()
+    window = None  # steady state of one solve: iterations [100, 1100)
+    if args.window:
+        import numpy as np
+        p.load_dense_device(A.data_ptr(), np.ones(args.m, np.int32), b, c, maximize=True)
+        p.iterate(100)
         barrier()
-        s2 = p.stats()
-        sol = p.solution(st)
-        tto = s2["seconds_loop"]
-        final = {"status": st, "iterations_to_optimal": s2["iterations"],
-                 "objective": sol.objval, "bump_dim": s2["bump_dim"], "y_rows": s2["y_rows"],
-                 "refactors": s2["refactors"]}
-        if world > 1:
-            tt = torch.tensor([tto], dtype=torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            tto = float(tt.item())
+        w0 = p.stats()
+        tw = time.perf_counter()
+        p.iterate(1000)
+        barrier()
+        tw = time.perf_counter() - tw
+        w1 = p.stats()
+        wit = w1["iterations"] - w0["iterations"]
+        wr = price_roofline([{k: w1[k] - w0[k] for k in ("price_seconds", "price_timed_bytes",
+                                                         "price_timed_launches")}])
+        window = {"iterations": [100, 100 + wit], "value": wit / tw if tw > 0 else None,
+                  "us_per_iteration": 1e6 * tw / max(wit, 1), "price_frac": wr["frac"],
+                  "price_avg_launch_us": wr["avg_launch_us"]}
 
     traffic, traffic_src = committed_traffic(args) if world == 1 else (None, None)
 
     other = None  # the same LP to optimality under the other pricing rule
-    if args.compare_rules and world == 1 and not args.no_optimal and not args.force_sharded:
-        p.close()
-        q = Problem(args.m, args.n, device=local, pricing=1 - args.rule, sync_every=args.sync_every)
-        q.load_generated(args.seed)
-        qst = q.solve()
-        qs = q.stats()
-        other = {"pricing": "dantzig" if args.rule else "devex", "status": qst,
-                 "objective": q.solution(qst).objval, "iterations_to_optimal": qs["iterations"],
-                 "time_to_optimal_s": qs["seconds_loop"]}
-        q.close()
+    if args.compare_rules and world == 1 and not args.force_sharded:
+        from easylp_amd import Problem
+        import numpy as np
+        with Problem(args.m, args.n, device=local, pricing=1 - args.rule, sync_every=args.sync_every) as q:
+            tq = time.perf_counter()
+            q.load_dense_device(A.data_ptr(), np.ones(args.m, np.int32), b, c, maximize=True)
+            qst = q.solve()
+            tq = time.perf_counter() - tq
+            qs = q.stats()
+            other = {"pricing": "dantzig" if args.rule else "devex", "status": qst,
+                     "objective": q.solution(qst).objval, "iterations_to_optimal": qs["iterations"],
+                     "time_to_optimal_s": tq}
+    p.close()
+    del A
+    torch.cuda.empty_cache()
 
-    c4 = None
-    if args.c4:
-        p.close()  # free the 5000x50000 problem first
-        c4 = c4_rate(args, lib, world, rank, local, barrier, dist)
+    c4 = c4_config(args, lib, world, rank, local, barrier, dist) if args.c4 else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -347,42 +414,37 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": 1e3 * elapsed / max(iters, 1),
+            "ms_per_step": 1e3 * elapsed / max(args.steps, 1),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (counter-based generator on device, seed %d)" % args.seed,
+            "data": "synthetic (counter-based generator into HBM, seed %d)" % args.seed,
             "config": {
-                "workload": "dense random LP m=%d n=%d (BASELINE configs[2])" % (args.m, args.n),
+                "workload": "dense random LP m=%d n=%d (BASELINE configs[2]), step = one full solve "
+                            "(load from HBM + solve to optimality)" % (args.m, args.n),
                 "m": args.m, "n": args.n, "seed": args.seed,
-                "parallelism": ("column-shard x%d, %s min-loc" % (world, "xGMI mailbox" if args.p2p else "RCCL all-gather")
+                "parallelism": ("column-shard x%d, %s min-loc" % (world, "xGMI mailbox" if p2p else "RCCL all-gather")
                                 if world > 1 or args.force_sharded else "single GPU"),
                 "iterations_timed": iters,
                 "pricing": args.pricing,
             },
-            "time_to_optimal_s": tto,
+            "time_to_optimal_s": elapsed / max(args.steps, 1),
             "final": final,
+            "steady_state": window,
             "other_pricing": other,
             "roofline": {
-                "kernel": "k_price (pricing sweep + %s argmin)" % args.pricing,
+                "kernel": "k_price (pricing sweep + %s argmin + deferred update)" % args.pricing,
                 "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                **roof,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "bytes_per_launch": price_b / price_n if price_n else price_dev_bytes,
-                "avg_launch_us": 1e6 * price_s / price_n if price_n else None,
-                "launches_timed": price_n,
             },
             "cpu_baseline": cpu,
             "scaling_config": c4,
             "sparse_config": sparse,
         }
         print(json.dumps(line), flush=True)
-    p.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -6,8 +6,9 @@ easylp$solve() (/root/reference/R/class.R:251-302): dense A (`solve_dense`),
 sparse A through the CSC path (`solve_sparse`).
 """
 from .solver import (  # noqa: F401
-    STATUS_TEXT, Problem, Solution, csc_arrays, dir_codes, large_to_infinity, solve_dense,
-    solve_sparse, status_text,
+    STATUS_TEXT, Problem, Solution, csc_arrays, dir_codes, generate_dense_device, large_to_infinity,
+    solve_dense, solve_sparse, status_text,
 )
 
-__all__ = ["Problem", "Solution", "solve_dense", "solve_sparse", "csc_arrays", "large_to_infinity", "status_text", "STATUS_TEXT"]
+__all__ = ["Problem", "Solution", "solve_dense", "solve_sparse", "csc_arrays", "generate_dense_device",
+           "large_to_infinity", "status_text", "STATUS_TEXT"]

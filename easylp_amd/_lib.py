@@ -22,7 +22,7 @@ ABI_VERSION = 2
 # every entry point the header declares (checked by tests/test_abi.py)
 EXPORTS = (
     "elp_default_control", "elp_create", "elp_load_dense", "elp_load_dense_device",
-    "elp_load_generated", "elp_load_csc", "elp_set_int", "elp_solve", "elp_iterate", "elp_get_solution",
+    "elp_load_generated", "elp_generate_dense", "elp_load_csc", "elp_set_int", "elp_solve", "elp_iterate", "elp_get_solution",
     "elp_get_stats", "elp_sensitivity",
     "elp_set_trace", "elp_get_trace", "elp_comm_unique_id", "elp_comm_init", "elp_comm_init_host", "elp_comm_enable_p2p",
     "elp_destroy", "elp_last_error", "elp_abi_version",
@@ -86,6 +86,7 @@ class ElpStats(ctypes.Structure):
         ("gj_refactors", ctypes.c_int64),
         ("mip_nodes", ctypes.c_int64),
         ("mip_lp_iterations", ctypes.c_int64),
+        ("price_launches", ctypes.c_int64),
     ]
 
 
@@ -113,6 +114,7 @@ def load(path: str | None = None):
     lib.elp_load_dense.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32]
     lib.elp_load_dense_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32]
     lib.elp_load_generated.argtypes = [vp, ctypes.c_uint64]
+    lib.elp_generate_dense.argtypes = [i32, ctypes.c_uint64, i64, i64, vp, vp, vp]
     lib.elp_load_csc.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32]
     lib.elp_set_int.argtypes = [vp, vp]
     lib.elp_solve.argtypes = [vp, P(i32)]
@@ -131,6 +133,7 @@ def load(path: str | None = None):
     lib.elp_last_error.restype = ctypes.c_char_p
     lib.elp_abi_version.restype = i32
     for name in ("elp_create", "elp_load_dense", "elp_load_dense_device", "elp_load_generated",
+                 "elp_generate_dense",
                  "elp_load_csc", "elp_sensitivity", "elp_set_int",
                  "elp_solve", "elp_iterate", "elp_get_solution", "elp_get_stats",
                  "elp_set_trace", "elp_get_trace", "elp_comm_unique_id", "elp_comm_init",

@@ -265,7 +265,9 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.nzcount, 1));
     // tile candidates + the slack workgroups' (|Y| <= m, >= 128 slots each)
     A(dalloc(&d.cand, (size_t)((n + TILE_COLS - 1) / TILE_COLS) + (size_t)((mm + TILE_COLS - 1) / TILE_COLS) + 64));
-    A(dalloc(&d.pstamp, 2 * ((size_t)((n + TILE_COLS - 1) / TILE_COLS) + 64)));
+    // one stamp pair per pricing workgroup: tiles, slack workgroups (<= m / 128 + 1)
+    // and the apply workgroups (<= 2048 + 1024, launch_btran_price)
+    A(dalloc(&d.pstamp, 2 * ((size_t)((n + TILE_COLS - 1) / TILE_COLS) + (size_t)(mm / 128 + 1) + 3072 + 64)));
     if (h->csc) A(dalloc(&d.qcol, mm));
     if (std::getenv("ELP_STAMPS")) A(dalloc(&d.dstamp, 16 * 64));
     A(dalloc(&d.ctl, 1));
@@ -653,6 +655,30 @@ extern "C" int elp_load_generated(elp_handle* h, uint64_t seed) {
     return rc;
 }
 
+extern "C" int elp_generate_dense(int32_t device, uint64_t seed, int64_t m, int64_t n, double* dA,
+                                  double* b, double* c) {
+    if (m < 0 || n < 1 || m > 0x3fffffff || n > 0x3fffffff) return fail(ELP_E_ARG, "elp_generate_dense: bad size");
+    if (m > 0 && !dA) return fail(ELP_E_ARG, "elp_generate_dense: dA is NULL");
+    HIPCHK(hipSetDevice(device));
+    hipStream_t st = nullptr;
+    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    double *db = nullptr, *dc = nullptr;
+    hipError_t e = dalloc(&db, (size_t)(m > 0 ? m : 1));
+    if (e == hipSuccess) e = dalloc(&dc, (size_t)n);
+    Dev g{};
+    g.m = (int32_t)m;
+    g.n = (int32_t)n;
+    if (e == hipSuccess) e = launch_generate(g, seed, 0, n, m > 0 ? dA : nullptr, db, dc, st);
+    if (e == hipSuccess && b && m) e = hipMemcpyAsync(b, db, (size_t)m * sizeof(double), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess && c) e = hipMemcpyAsync(c, dc, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (db) (void)hipFree(db);
+    if (dc) (void)hipFree(dc);
+    (void)hipStreamDestroy(st);
+    if (e != hipSuccess) return fail(ELP_E_HIP, std::string("elp_generate_dense: ") + hipGetErrorString(e));
+    return 0;
+}
+
 static int push_ctl_fields(elp_handle* h) {
     // host-owned fields are written as one block (the device is idle at a poll)
     HIPCHK(hipMemcpyAsync(h->d.ctl, h->hctl, sizeof(DevCtl), hipMemcpyHostToDevice, h->st));
@@ -772,6 +798,7 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             const int kub = (int)std::min<int64_t>(h->m, (int64_t)k0 + t);
             const int nyub = (int)std::min<int64_t>(h->m, (int64_t)ny0 + t);
             hipEvent_t e0 = prof ? h->ev[2 * t] : nullptr, e1 = prof ? h->ev[2 * t + 1] : nullptr;
+            h->stats.price_launches++;
             if (h->comm.kind == 0 || h->comm.p2p) {  // (p2p: min-loc inside the select kernel)
                 HIPCHK(launch_iteration(h->d, kub, nyub, h->phase, h->st, e0, e1, t));
             } else {
@@ -987,6 +1014,18 @@ static int run_bnb(elp_handle* h, int32_t* out_status) {
         if (h->ctl.max_nodes > 0 && nodes >= h->ctl.max_nodes) {
             limit = true;
             continue;
+        }
+        if (h->ctl.time_limit > 0) {
+            // (a node LP checks the clock at its polls; small nodes finish
+            // before their first poll, so the tree checks it between nodes too;
+            // all ranks of a sharded solve take the same decision)
+            int over = 0;
+            const int rc = any_rank(h, now_s() - t_bnb > h->ctl.time_limit, &over);
+            if (rc) return rc;
+            if (over) {
+                failed = failed < 0 ? ELP_TIMEOUT : failed;
+                break;
+            }
         }
         nodes++;
         h->bnb_iter_left = h->ctl.max_iter - iters;

@@ -68,7 +68,7 @@ struct DevCtl {
     double price_bytes;    // algorithmic bytes of every pricing pass that ran
     int64_t price_passes;
     unsigned long long ns_emax_bits;  // max|I - M Minv| of the last refactor (bits of a double >= 0)
-    int32_t pad2, pad3;
+    int32_t price_grid, pad3;         // workgroups of the last pricing launch (Dev::ptimer)
     int32_t snap_k, snap_bland;       // k, bland as k_ratio's workgroups must see them
                                       // (workgroup 0 rewrites k / bland meanwhile)
     // likewise the bookkeeping entries k_ratio's dual update reads (k_ftran_zr's
@@ -85,7 +85,9 @@ struct DevCtl {
     double snap_lbq, snap_ubq, snap_xq, snap_cq, snap_csl, snap_slol, snap_shil;
     int32_t snap_vsq, snap_sllast, snap_rllast, pad7;
     // pricing-kernel timer (Dev::ptimer): s_memrealtime ticks (100 MHz) from the
-    // first workgroup's start to the last one's end, summed over timed passes
+    // first workgroup's start to the last one's end -- every workgroup of the
+    // launch: tiles, slack candidates and the deferred-update appliers, i.e. what
+    // a kernel trace times -- summed over timed passes
     unsigned long long price_ticks;
     int64_t price_timed;
     double price_tbytes;
@@ -176,7 +178,7 @@ struct Dev {
     int32_t *cover, *rpos, *Rl, *Sl, *spos, *Yl, *ypos, *perm, *pivstep, *nzlist, *nzcount;
     int32_t* nzchunk;  // per-chunk counts of the nzlist compaction
     Cand* cand;
-    unsigned long long* pstamp;  // [tile][2] start / end stamps of the last pricing pass
+    unsigned long long* pstamp;  // [workgroup][2] start / end stamps of the last pricing launch
     int32_t ptimer, pad3;        // 1: k_price stamps, the select kernels sum them
     DevCtl* ctl;
     int64_t* trace;

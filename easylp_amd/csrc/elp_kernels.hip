@@ -627,7 +627,7 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
 // plain (cached) loads: the live AR rows (~80 MB at 5000x50000) stay in the
 // 256 MiB Infinity Cache between passes; non-temporal loads measured 10% slower
 #define AR_LOAD(ptr) (*reinterpret_cast<const dbl2*>(ptr))
-__global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int napply, int nb_minv, int nsw) {
+DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
     __shared__ double part[PRICE_SPLIT][TILE_COLS];
     __shared__ Cand red[PRICE_SPLIT];
     if (apply_role(d, napply, nb_minv)) return;
@@ -638,7 +638,6 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int napply, int 
         price_slacks<PRICE_THREADS>(d, ntiles, (int)(blockIdx.x - ntiles), nsw, red);
         return;
     }
-    if (d.ptimer && threadIdx.x == 0) d.pstamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     const int ny = c->ny, bland = c->bland;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -713,10 +712,28 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int napply, int 
         }
     }
     best = block_best<PRICE_THREADS>(best, bland, red);
-    if (threadIdx.x == 0) {
-        d.cand[blockIdx.x] = best;
-        if (d.ptimer) d.pstamp[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) d.cand[blockIdx.x] = best;
+}
+
+// the pricing-launch timer (Dev::ptimer): every workgroup stamps its start and
+// its end (after all its waves), so first start -> last end is the launch
+template <int NT>
+DEV void pstamp_begin(const Dev& d) {
+    if (d.ptimer && threadIdx.x == 0) {
+        d.pstamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+        if (blockIdx.x == 0) d.ctl->price_grid = (int32_t)gridDim.x;
     }
+}
+DEV void pstamp_end(const Dev& d) {
+    if (!d.ptimer) return;
+    __syncthreads();  // (every return path of the bodies is workgroup-uniform)
+    if (threadIdx.x == 0) d.pstamp[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+}
+
+__global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int napply, int nb_minv, int nsw) {
+    pstamp_begin<PRICE_THREADS>(d);
+    price_body(d, napply, nb_minv, nsw);
+    pstamp_end(d);
 }
 
 // algorithmic bytes of one pricing pass.  Dense: the AR sweep (8|Y|n), c and
@@ -736,7 +753,13 @@ DEV double price_pass_bytes(const Dev& d, int ny, int devex) {
 // row order (oracle price_mode 1).  Tiles with more than CSC_STAGE nonzeros
 // read straight from global memory (same order).
 constexpr int CSC_STAGE = 2048;  // staged nonzeros per tile: 32 KiB of LDS
+DEV void price_csc_body(const Dev& d, int napply, int nb_minv, int nsw);
 __global__ void __launch_bounds__(TILE_COLS) k_price_csc(Dev d, int napply, int nb_minv, int nsw) {
+    pstamp_begin<TILE_COLS>(d);
+    price_csc_body(d, napply, nb_minv, nsw);
+    pstamp_end(d);
+}
+DEV void price_csc_body(const Dev& d, int napply, int nb_minv, int nsw) {
     __shared__ double sv[CSC_STAGE], sy[CSC_STAGE];
     __shared__ Cand red[TILE_COLS / 64];
     if (apply_role(d, napply, nb_minv)) return;
@@ -747,7 +770,6 @@ __global__ void __launch_bounds__(TILE_COLS) k_price_csc(Dev d, int napply, int 
         price_slacks<TILE_COLS>(d, ntiles, (int)(blockIdx.x - ntiles), nsw, red);
         return;
     }
-    if (d.ptimer && threadIdx.x == 0) d.pstamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     const int bland = c->bland;
     const int64_t j0 = (int64_t)blockIdx.x * TILE_COLS;
     const int64_t j = j0 + threadIdx.x;
@@ -785,10 +807,7 @@ __global__ void __launch_bounds__(TILE_COLS) k_price_csc(Dev d, int napply, int 
         }
     }
     best = block_best<TILE_COLS>(best, bland, red);
-    if (threadIdx.x == 0) {
-        d.cand[blockIdx.x] = best;
-        if (d.ptimer) d.pstamp[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-    }
+    if (threadIdx.x == 0) d.cand[blockIdx.x] = best;
 }
 
 // CSC: a_R[p] = A[R_p, q] by scattering column q's nonzeros through rpos
@@ -820,13 +839,15 @@ DEV void scatter_qcol_csc(const Dev& d, int q) {
     if (threadIdx.x == 0) c->qcol_var = q;
 }
 
-// Pricing-pass timer: first start to last end over the tiles' stamps (one
-// workgroup of NT threads), added to the control block with the pass's bytes.
+// Pricing-launch timer: first start to last end over the stamps of every
+// workgroup of the last pricing launch (one workgroup of NT threads), added to
+// the control block with the pass's bytes.
 template <int NT>
-DEV void price_timer_sum(const Dev& d, int ntiles, unsigned long long* red) {
+DEV void price_timer_sum(const Dev& d, unsigned long long* red) {
     __syncthreads();  // red may still be read by the preceding reduction
+    const int nwg = d.ctl->price_grid;
     unsigned long long lo = ~0ull, hi = 0;
-    for (int t = threadIdx.x; t < ntiles; t += NT) {
+    for (int t = threadIdx.x; t < nwg; t += NT) {
         lo = min(lo, d.pstamp[2 * t]);
         hi = max(hi, d.pstamp[2 * t + 1]);
     }
@@ -995,7 +1016,7 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles, int nsw) {
     }
     const int q = (int)best.j;
     if (threadIdx.x == 0) entering_chosen(d, best);
-    if (d.ptimer) price_timer_sum<1024>(d, ntiles, reinterpret_cast<unsigned long long*>(red));
+    if (d.ptimer) price_timer_sum<1024>(d, reinterpret_cast<unsigned long long*>(red));
     if (d.csc) {  // dense copy of the entering column + a_R through rpos
         scatter_qcol_csc(d, q);
         if (q < d.N) {
@@ -1094,7 +1115,7 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw
     const int q = (int)best.j;
     if (blockIdx.x == 0 && tid == 0) entering_chosen(d, best);
     if (d.ptimer && blockIdx.x == gridDim.x - 1) {  // the extra timer workgroup
-        price_timer_sum<256>(d, ntiles, reinterpret_cast<unsigned long long*>(aRs));
+        price_timer_sum<256>(d, reinterpret_cast<unsigned long long*>(aRs));
         return;
     }
     if (d.csc && blockIdx.x == gridDim.x - 1 - d.ptimer) {  // CSC: dense entering column
@@ -1160,7 +1181,7 @@ __global__ void __launch_bounds__(1024) k_select_local(Dev d, int ntiles, int ns
         }
         d.cand_xchg[rank] = x;
     }
-    if (d.ptimer) price_timer_sum<1024>(d, ntiles, reinterpret_cast<unsigned long long*>(red));
+    if (d.ptimer) price_timer_sum<1024>(d, reinterpret_cast<unsigned long long*>(red));
 }
 
 // after the all-gather: global min-loc (same total order on every rank); the

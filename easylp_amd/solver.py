@@ -222,6 +222,22 @@ class Problem:
         return Solution(status, obj.value, x, y[:m], basis[:m], self.stats(), tr)
 
 
+def generate_dense_device(seed: int, m: int, n: int, device: int = 0):
+    """The synthetic LP of SURVEY.md 8d (maximize c'x, A x <= b, x >= 0) with A
+    generated straight into HBM (elp_generate_dense): returns (A, b, c), A a
+    torch float64 tensor of m*n elements on cuda:device (column-major, lda = m),
+    b and c numpy arrays.  Pass A.data_ptr() to Problem.load_dense_device."""
+    import torch
+    lib = load()
+    A = torch.empty(max(m * n, 1), dtype=torch.float64, device=f"cuda:{device}")
+    b = np.zeros(max(m, 1))
+    c = np.zeros(n)
+    torch.cuda.synchronize(device)
+    check(lib.elp_generate_dense(int(device), int(seed), int(m), int(n), ctypes.c_void_p(A.data_ptr()),
+                                 b.ctypes.data, c.ctypes.data), "elp_generate_dense")
+    return A, b[:m], c
+
+
 def csc_arrays(A):
     """(colptr, rowind, val) of a scipy.sparse matrix or dense array: canonical
     CSC (duplicates summed, rows sorted), explicit zeros kept."""

@@ -127,6 +127,8 @@ typedef struct elp_stats {
     int64_t gj_refactors;      /* refactors that needed a Gauss-Jordan rebuild */
     int64_t mip_nodes;         /* branch-and-bound nodes (LP relaxations) solved */
     int64_t mip_lp_iterations; /* simplex iterations over all of them           */
+    int64_t price_launches;    /* pricing-kernel launches enqueued (profilers:
+                                  the dispatches of this handle's pricing kernel) */
 } elp_stats;
 
 #define ELP_PROFILE_PRICE 2   /* elp_control.verbose bit: device-clock pricing timer */
@@ -168,6 +170,14 @@ int elp_load_csc(elp_handle* h, const int64_t* colptr, const int32_t* rowind, co
  * counter-based (seed, stream, global index) so every rank / the oracle
  * regenerate the same numbers. */
 int elp_load_generated(elp_handle* h, uint64_t seed);
+
+/* The same synthetic LP written into caller memory instead of a handle (bench
+ * and tests: A stays resident in HBM and every solve loads it with
+ * elp_load_dense_device, so load is timed and generation is not).  dA: device
+ * memory on `device`, m x n column-major (lda = m); b[m], c[n]: host arrays
+ * (either may be NULL). */
+int elp_generate_dense(int32_t device, uint64_t seed, int64_t m, int64_t n, double* dA, double* b,
+                       double* c);
 
 /* set.type(prob, columns, "integer" | "binary")        R/class.R:265
  * is_int[n] != 0 marks integer columns (binary = integer with bounds [0, 1]);

@@ -91,6 +91,14 @@ def load():
         ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
     ]
+    lib.orc_solve_generated.restype = ctypes.c_int
+    lib.orc_solve_generated.argtypes = [
+        ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, P(OrcControl), ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, P(OrcStats),
+    ]
+    lib.orc_generate_rows.restype = None
+    lib.orc_generate_rows.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                                      ctypes.c_int64, ctypes.c_void_p]
     _lib = lib
     return lib
 
@@ -187,3 +195,36 @@ def solve_mip(A, dir, rhs, obj, lo, up, maximize, is_int, max_nodes=0, **ctl):
                                ctypes.byref(nodes), ctypes.byref(iters))
     return OracleResult(status, objval.value, x, np.zeros(m), np.zeros(0, np.int64),
                         np.zeros((0, 2), np.int64), {"nodes": nodes.value, "lp_iterations": iters.value})
+
+
+def solve_generated(seed, m, n, trace_cap=0, **ctl):
+    """orc_solve_generated: the synthetic LP of generate_dense(seed, m, n) solved
+    without materialising A (entries regenerated on read)."""
+    lib = load()
+    c = OrcControl()
+    lib.orc_default_control(ctypes.byref(c))
+    for key, val in ctl.items():
+        setattr(c, key, val)
+    x = np.zeros(n)
+    y = np.zeros(max(m, 1))
+    basis = np.zeros(max(m, 1), dtype=np.int64)
+    trace = np.full(2 * max(trace_cap, 1), -2, dtype=np.int64)
+    objval = ctypes.c_double(0.0)
+    st = OrcStats()
+    status = lib.orc_solve_generated(seed, m, n, ctypes.byref(c), ctypes.addressof(objval), x.ctypes.data,
+                                     y.ctypes.data, basis.ctypes.data,
+                                     trace.ctypes.data if trace_cap else None, trace_cap, ctypes.byref(st))
+    if status < 0:
+        raise ValueError(f"orc_solve_generated usage error {status}")
+    stats = {f: getattr(st, f) for f, _ in OrcStats._fields_}
+    it = min(stats["iterations"], trace_cap)
+    return OracleResult(status, objval.value, x, y[:m], basis[:m], trace[: 2 * it].reshape(-1, 2), stats)
+
+
+def generate_rows(seed, m, n, rows):
+    """Rows `rows` of the generate_dense(seed, m, n) matrix, row-major."""
+    lib = load()
+    rows = np.ascontiguousarray(rows, dtype=np.int64)
+    out = np.zeros((len(rows), n))
+    lib.orc_generate_rows(seed, m, n, rows.ctypes.data, len(rows), out.ctypes.data)
+    return out

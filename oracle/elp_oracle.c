@@ -88,12 +88,22 @@ void orc_generate_dense(uint64_t seed, int64_t m, int64_t n, int64_t col0, int64
     }
 }
 
+void orc_generate_rows(uint64_t seed, int64_t m, int64_t n, const int64_t* rows, int64_t nrows,
+                       double* out) {
+    (void)n;
+    for (int64_t r = 0; r < nrows; ++r)
+        for (int64_t j = 0; j < n; ++j)
+            out[(size_t)r * (size_t)n + (size_t)j] =
+                gen_u01(seed, 0, (uint64_t)rows[r] + (uint64_t)j * (uint64_t)m);
+}
+
 /* ------------------------------------------------------------------ */
 /* solver state                                                        */
 /* ------------------------------------------------------------------ */
 typedef struct {
     int64_t m, n, nv;
-    const double* A; /* column-major m x n */
+    const double* A; /* column-major m x n; NULL: generated on the fly (gen_seed) */
+    uint64_t gen_seed;
     double* b;
     double *lb, *ub, *cost, *xval;
     int8_t* vstat;
@@ -121,13 +131,29 @@ typedef struct {
     double tol_singular;
     double *dw, *dprev; /* price_rule 1: Devex weight and last reduced cost
                            of each structural and slack (n + m)            */
+    int64_t* nzl;       /* n: nz_nonbasic list                              */
+    double* colbuf;     /* m: a generated column (Acol)                     */
 } orc_t;
 
 static double* dalloc(size_t n) { return (double*)calloc(n ? n : 1, sizeof(double)); }
 static int64_t* ialloc(size_t n) { return (int64_t*)calloc(n ? n : 1, sizeof(int64_t)); }
 
 static inline double Aat(const orc_t* s, int64_t i, int64_t j) {
+    if (!s->A) return gen_u01(s->gen_seed, 0, (uint64_t)i + (uint64_t)j * (uint64_t)s->m);
     return s->A[(size_t)j * (size_t)s->m + (size_t)i];
+}
+/* column j of A (in place, or generated into buf) */
+static inline const double* Acol(const orc_t* s, int64_t j, double* buf) {
+    if (s->A) return &s->A[(size_t)j * (size_t)s->m];
+    for (int64_t i = 0; i < s->m; ++i) buf[i] = Aat(s, i, j);
+    return buf;
+}
+/* ascending list of nonbasic structurals with x_j != 0 (row activities) */
+static int64_t nz_nonbasic(const orc_t* s, int64_t* list) {
+    int64_t c = 0;
+    for (int64_t j = 0; j < s->n; ++j)
+        if (s->vstat[j] != VS_BASIC && s->xval[j] != 0.0) list[c++] = j;
+    return c;
 }
 static inline double unit_sign(const orc_t* s, int64_t var) {
     return var >= s->n + s->m ? s->asgn[var - s->n - s->m] : 1.0;
@@ -282,10 +308,11 @@ static int refactor(orc_t* s) {
         if (gauss_jordan(s)) return -1;
     }
     /* primal values: rhs_i = (b_i - sum_{j nonbasic struct, x_j != 0} a_ij x_j) - s_i */
+    const int64_t nz = nz_nonbasic(s, s->nzl);
+    (void)n;
     for (int64_t i = 0; i < m; ++i) {
         double acc = 0.0;
-        for (int64_t j = 0; j < n; ++j)
-            if (s->vstat[j] != VS_BASIC && s->xval[j] != 0.0) acc = fma(Aat(s, i, j), s->xval[j], acc);
+        for (int64_t t = 0; t < nz; ++t) acc = fma(Aat(s, i, s->nzl[t]), s->xval[s->nzl[t]], acc);
         double r = s->b[i] - acc;
         if (s->vstat[n + i] != VS_BASIC) r = r - s->xval[n + i];
         s->acol[i] = r;
@@ -388,7 +415,7 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
          * wave order over all m rows with y = 0 on uncovered rows */
         if (phase == 1) {
             for (int64_t p = 0; p < k; ++p)
-                s->t[p] = s->cost[s->Sl[p]] - wave_dot(m, &s->A[(size_t)s->Sl[p] * (size_t)m], s->y);
+                s->t[p] = s->cost[s->Sl[p]] - wave_dot(m, Acol(s, s->Sl[p], s->colbuf), s->y);
         } else {
             for (int64_t p = 0; p < k; ++p) s->t[p] = s->cost[s->Sl[p]];
         }
@@ -409,7 +436,7 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
             for (int w = 1; w < PRICE_SPLIT; ++w)
                 for (int64_t j = 0; j < n; ++j) s->part[(size_t)w * (size_t)n + (size_t)j] = 0.0;
             for (int64_t j = 0; j < n; ++j) {
-                const double* col = &s->A[(size_t)j * (size_t)m];
+                const double* col = Acol(s, j, s->colbuf);
                 double acc = 0.0;
                 for (int64_t t = s->cp[j]; t < s->cp[j + 1]; ++t)  /* ascending rows */
                     acc = fma(col[s->ri[t]], s->y[s->ri[t]], acc);
@@ -764,7 +791,7 @@ static void sensitivity(orc_t* s, const orc_control* ctl, const int32_t* dir, in
     double *dfrom = duals + (m + n), *dtill = dfrom + (m + n);
     double* d = dalloc((size_t)(n + m));
     for (int64_t j = 0; j < n; ++j) {
-        const double* col = &s->A[(size_t)j * (size_t)m];
+        const double* col = Acol(s, j, s->colbuf);
         double dot = 0.0;
         if (ctl->price_mode == 1) {
             for (int64_t i = 0; i < m; ++i)
@@ -910,12 +937,45 @@ int orc_solve_dense(int64_t m, int64_t n, const double* A, const int32_t* dir, c
                                 yout, basis, trace, trace_cap, st_out, NULL);
 }
 
+static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, const int32_t* dir,
+                      const double* rhs, const double* obj, const double* lo, const double* up,
+                      int32_t maximize, const orc_control* ctl_in, double* objval, double* xout,
+                      double* yout, int64_t* basis, int64_t* trace, int64_t trace_cap,
+                      orc_stats* st_out, double* sens);
+
 int orc_solve_dense_sens(int64_t m, int64_t n, const double* A, const int32_t* dir,
                          const double* rhs, const double* obj, const double* lo,
                          const double* up, int32_t maximize, const orc_control* ctl_in,
                          double* objval, double* xout, double* yout, int64_t* basis,
                          int64_t* trace, int64_t trace_cap, orc_stats* st_out, double* sens) {
-    if (m < 0 || n <= 0 || (m > 0 && (!A || !dir || !rhs)) || !obj) return -1;
+    if (m > 0 && !A) return -1;
+    return solve_core(m, n, A, 0, dir, rhs, obj, lo, up, maximize, ctl_in, objval, xout, yout, basis,
+                      trace, trace_cap, st_out, sens);
+}
+
+int orc_solve_generated(uint64_t seed, int64_t m, int64_t n, const orc_control* ctl, double* objval,
+                        double* x, double* y, int64_t* basis, int64_t* trace, int64_t trace_cap,
+                        orc_stats* st) {
+    if (m < 0 || n <= 0 || (ctl && ctl->price_mode != 0)) return -1;
+    double* b = dalloc((size_t)(m > 0 ? m : 1));
+    double* c = dalloc((size_t)n);
+    int32_t* dir = (int32_t*)malloc((size_t)(m > 0 ? m : 1) * sizeof(int32_t));
+    orc_generate_dense(seed, m, n, 0, n, NULL, b, c);
+    for (int64_t i = 0; i < m; ++i) dir[i] = 1;
+    const int r = solve_core(m, n, NULL, seed, dir, b, c, NULL, NULL, 1, ctl, objval, x, y, basis, trace,
+                             trace_cap, st, NULL);
+    free(b);
+    free(c);
+    free(dir);
+    return r;
+}
+
+static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, const int32_t* dir,
+                      const double* rhs, const double* obj, const double* lo, const double* up,
+                      int32_t maximize, const orc_control* ctl_in, double* objval, double* xout,
+                      double* yout, int64_t* basis, int64_t* trace, int64_t trace_cap,
+                      orc_stats* st_out, double* sens) {
+    if (m < 0 || n <= 0 || (m > 0 && (!dir || !rhs)) || !obj) return -1;
     for (int64_t i = 0; i < m; ++i)
         if (dir[i] < 1 || dir[i] > 3) return -2;
     orc_control ctl;
@@ -938,15 +998,22 @@ int orc_solve_dense_sens(int64_t m, int64_t n, const double* A, const int32_t* d
     s->n = n;
     s->nv = n + 2 * m;
     s->A = A;
+    s->gen_seed = gen_seed;
     s->nnz = 0;
-    for (size_t t = 0; t < (size_t)m * (size_t)n; ++t) s->nnz += A[t] != 0.0;
     s->cp = ialloc((size_t)n + 1);
-    s->ri = ialloc((size_t)s->nnz);
-    for (int64_t j = 0, t = 0; j < n; ++j) {
-        for (int64_t i = 0; i < m; ++i)
-            if (A[(size_t)j * (size_t)m + (size_t)i] != 0.0) s->ri[t++] = i;
-        s->cp[j + 1] = t;
+    if (ctl.price_mode == 1) { /* the column pattern (CSC order) */
+        for (size_t t = 0; t < (size_t)m * (size_t)n; ++t) s->nnz += A[t] != 0.0;
+        s->ri = ialloc((size_t)s->nnz);
+        for (int64_t j = 0, t = 0; j < n; ++j) {
+            for (int64_t i = 0; i < m; ++i)
+                if (A[(size_t)j * (size_t)m + (size_t)i] != 0.0) s->ri[t++] = i;
+            s->cp[j + 1] = t;
+        }
+    } else {
+        s->ri = ialloc(1);
     }
+    s->nzl = ialloc((size_t)n);
+    s->colbuf = dalloc((size_t)(m > 0 ? m : 1));
     s->refactor_mode = ctl.refactor_mode;
     s->tol_singular = ctl.tol_singular;
     const int64_t nv = s->nv, mm = m > 0 ? m : 1;
@@ -1013,6 +1080,7 @@ int orc_solve_dense_sens(int64_t m, int64_t n, const double* A, const int32_t* d
     int64_t iter = 0;
     if (status == 0) {
         int any_art = 0;
+        int64_t nzc = 0;
         for (int64_t i = 0; i < m; ++i) {
             double bi = rhs[i];
             if (bi <= -BIG) bi = -INF;
@@ -1027,9 +1095,9 @@ int orc_solve_dense_sens(int64_t m, int64_t n, const double* A, const int32_t* d
             s->vstat[av] = VS_LOWER;
             s->rpos[i] = -1;
             s->ypos[i] = -1;
+            if (i == 0) nzc = nz_nonbasic(s, s->nzl); /* (no basic structural yet) */
             double acc = 0.0;
-            for (int64_t j = 0; j < n; ++j)
-                if (s->xval[j] != 0.0) acc = fma(Aat(s, i, j), s->xval[j], acc);
+            for (int64_t t = 0; t < nzc; ++t) acc = fma(Aat(s, i, s->nzl[t]), s->xval[s->nzl[t]], acc);
             const double r = s->b[i] - acc;
             if (r >= s->lb[sv] && r <= s->ub[sv]) {
                 s->vstat[sv] = VS_BASIC;
@@ -1120,7 +1188,7 @@ int orc_solve_dense_sens(int64_t m, int64_t n, const double* A, const int32_t* d
     free(s->y); free(s->t); free(s->yR); free(s->yy); free(s->acol); free(s->aR);
     free(s->alS); free(s->alU); free(s->z); free(s->v); free(s->tmp); free(s->part);
     free(s->dw); free(s->dprev);
-    free(s->used); free(s->perm); free(s->cp); free(s->ri);
+    free(s->used); free(s->perm); free(s->cp); free(s->ri); free(s->nzl); free(s->colbuf);
     return status;
 }
 

@@ -90,6 +90,15 @@ int orc_solve_dense_sens(int64_t m, int64_t n, const double* A, const int32_t* d
                          double* objval, double* x, double* y, int64_t* basis,
                          int64_t* trace, int64_t trace_cap, orc_stats* st, double* sens);
 
+/* orc_solve_dense on the synthetic LP of orc_generate_dense(seed, m, n) (all
+ * rows <=, x >= 0, maximize) without materialising A: every entry is
+ * regenerated from the counter-based generator when the algorithm reads it, so
+ * the 10000 x 500000 config (40 GB) runs in the memory of its Y rows (AR), the
+ * bump inverse and O(m + n) vectors.  Dense pricing order only (price_mode 0). */
+int orc_solve_generated(uint64_t seed, int64_t m, int64_t n, const orc_control* ctl, double* objval,
+                        double* x, double* y, int64_t* basis, int64_t* trace, int64_t trace_cap,
+                        orc_stats* st);
+
 /* Mixed-integer LP (is_int[n] != 0: integer column; binary = integer in
  * [0, 1]) by depth-first branch and bound over orc_solve_dense relaxations
  * (rules in elp_oracle.c).  max_nodes <= 0: unlimited.  Returns 0 optimal,
@@ -105,6 +114,10 @@ int orc_solve_mip(int64_t m, int64_t n, const double* A, const int32_t* dir, con
  * (column-major, lda = m).  c (ncols) and b (m) may be NULL. */
 void orc_generate_dense(uint64_t seed, int64_t m, int64_t n, int64_t col0,
                         int64_t ncols, double* A, double* b, double* c);
+
+/* Rows rows[0..nrows) of the same instance, row-major (out[r * n + j]). */
+void orc_generate_rows(uint64_t seed, int64_t m, int64_t n, const int64_t* rows, int64_t nrows,
+                       double* out);
 
 #ifdef __cplusplus
 }

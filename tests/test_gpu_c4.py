@@ -1,0 +1,70 @@
+"""BASELINE config 4 at full size on one GPU: the dense 10 000 x 500 000 LP
+(40 GB of A, generated in HBM) solved to optimality.
+
+The answer is checked without ever materialising A on the host:
+  * an optimality certificate, blockwise from the counter-based generator --
+    primal feasibility (the basic columns regenerated), dual feasibility (the
+    reduced costs of all 500 000 columns from the |Y| rows where y != 0,
+    regenerated in blocks) and strong duality c'x = b'y;
+  * the pivot path: the first 300 iterations bit for bit against the oracle's
+    generated-A entry point (oracle/elp_oracle.c orc_solve_generated, which
+    regenerates every entry it reads instead of holding A).
+Reference: the solve that R/class.R:276-278 hands to lp_solve."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+M, N, SEED = 10000, 500000, 1
+CAP = 300  # pivot-trace window compared with the oracle
+
+
+@pytest.fixture(scope="module")
+def c4(gpu):
+    with gpu.Problem(M, N) as p:
+        p.set_trace(CAP)
+        p.load_generated(SEED)
+        st = p.solve()
+        sol = p.solution(st)
+    return sol
+
+
+def test_c4_optimality_certificate(c4):
+    from oracle import generate_dense, generate_rows
+    sol = c4
+    assert sol.status == 0
+    _, b, c = generate_dense(SEED, M, N, want_A=False)
+    x, y = sol.x, sol.y
+    assert (x >= -1e-12).all()
+    # primal: A x <= b over the basic columns (every other x_j is 0)
+    J = np.nonzero(x)[0]
+    assert len(J) <= sol.stats["bump_dim"]
+    Ax = np.zeros(M)
+    for j in J:
+        col, _, _ = generate_dense(SEED, M, N, col0=int(j), ncols=1)
+        Ax += col[:, 0] * x[j]
+    assert (Ax <= b + 1e-9 * np.abs(b).max()).all()
+    # dual: y >= 0 (slack reduced costs) and c - A'y <= tol on every column,
+    # the rows with y != 0 regenerated 32 at a time
+    tol_dual = 1e-9  # elp_control.tol_dual
+    assert (y >= -tol_dual).all()
+    Y = np.nonzero(y)[0]
+    assert 0 < len(Y) <= sol.stats["y_rows"]
+    aty = np.zeros(N)
+    for r0 in range(0, len(Y), 32):
+        rows = Y[r0:r0 + 32]
+        aty += y[rows] @ generate_rows(SEED, M, N, rows)
+    assert (c - aty <= 2 * tol_dual).all()
+    # strong duality and the reported objective
+    cx = c @ x
+    assert abs(cx - b @ y) <= 1e-10 * abs(cx)
+    assert abs(sol.objval - cx) <= 1e-10 * abs(cx)
+    assert int((sol.basis < N).sum()) == sol.stats["bump_dim"]
+
+
+def test_c4_trace_matches_oracle(c4):
+    from oracle import solve_generated
+    o = solve_generated(SEED, M, N, trace_cap=CAP, max_iter=CAP)
+    assert o.status == 1 and o.stats["iterations"] == CAP
+    assert c4.stats["iterations"] > CAP
+    np.testing.assert_array_equal(c4.trace, o.trace)

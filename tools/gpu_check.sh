@@ -1,18 +1,26 @@
 #!/bin/bash
-# One GPU-box session: parity tests, smoke, the full bench line, then the
-# profiles committed under profiles/: a rocprofv3 kernel trace + stats of the
-# bench's timed window only (no run to optimality, no secondary configs), the
-# per-iteration timeline of that trace, and a separate PMC pass (FETCH_SIZE)
-# for the pricing kernel's HBM traffic over the same window.
+# One GPU-box session: parity tests, smoke, the bench line exactly as the
+# driver runs it (`bench.py --gpus 1 --steps 20 --warmup 5`), then the
+# profiles committed under profiles/:
+#   * rocprofv3 --kernel-trace --stats of the same timed region (the same 25
+#     full solves, without the secondary configs: every solve is identical, so
+#     the per-kernel averages are the timed window's);
+#   * a separate PMC pass (FETCH_SIZE) over the same command for the pricing
+#     kernel's HBM traffic per launch (timed dispatches only);
+#   * a per-iteration timeline over iterations [100, 1100) of one solve.
+# Traces go to /tmp on the box (too large to bring back); summaries to gpurun_out/.
 # Each GPU step has its own time limit; a crash / fault / timeout ends the script.
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"
 OUT="$ROOT/gpurun_out"
 mkdir -p "$OUT"
-TAG=${1:-r01}
-STEPS=${STEPS:-1000}
+TAG=${1:-r02}
 SKIP_TESTS=${SKIP_TESTS:-0}
+STEPS=${STEPS:-20}
+WARM=${WARM:-5}
+TMP=/tmp/elp_prof_$TAG
+mkdir -p "$TMP"
 echo "== host: $(nproc) cpus; $(grep -m1 'model name' /proc/cpuinfo)" | tee "$OUT/host_$TAG.txt"
 
 if [ "$SKIP_TESTS" = "0" ]; then
@@ -24,13 +32,18 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smo
 cat "$OUT/smoke_$TAG.log"
 fi
 
-timeout -k 10 400 python bench.py --steps "$STEPS" > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err" || { echo "bench failed rc=$?"; tail -20 "$OUT/bench_$TAG.err"; exit 4; }
+timeout -k 10 600 python bench.py --gpus 1 --steps "$STEPS" --warmup "$WARM" > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err" || { echo "bench failed rc=$?"; tail -20 "$OUT/bench_$TAG.err"; exit 4; }
 cat "$OUT/bench_$TAG.json"
 
-WIN="--steps $STEPS --warmup 100 --no-cpu --no-optimal --c4 0 --sparse 0"
+REG="--steps $STEPS --warmup $WARM --c4 0 --sparse 0 --no-cpu --compare-rules 0 --window 0"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- python3 "$ROOT/bench.py" $WIN > "$OUT/prof_bench_$TAG.json" 2> "$OUT/prof_bench_$TAG.err" || { echo "rocprof failed rc=$?"; tail -20 "$OUT/prof_bench_$TAG.err"; exit 5; }
-python3 "$ROOT/tools/timeline.py" $(find "$OUT/prof_$TAG" -name "*kernel_trace.csv") 100 "$STEPS" > "$OUT/timeline_$TAG.txt" && cat "$OUT/timeline_$TAG.txt"
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_price --output-format csv -d "$OUT/pmc_$TAG" -o run -- python3 "$ROOT/bench.py" $WIN --profile-price 0 > "$OUT/pmc_bench_$TAG.json" 2> "$OUT/pmc_bench_$TAG.err" || { echo "rocprof pmc failed rc=$?"; tail -20 "$OUT/pmc_bench_$TAG.err"; exit 6; }
-python3 "$ROOT/tools/pmc_traffic.py" "$OUT/pmc_$TAG/run_counter_collection.csv" "$OUT/pmc_bench_$TAG.json" 100 "$STEPS" > "$OUT/pmc_traffic_$TAG.json" && cat "$OUT/pmc_traffic_$TAG.json"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$TMP/kt" -o run -- python3 "$ROOT/bench.py" $REG > "$OUT/prof_bench_$TAG.json" 2> "$OUT/prof_bench_$TAG.err" || { echo "rocprof failed rc=$?"; tail -20 "$OUT/prof_bench_$TAG.err"; exit 5; }
+cp "$(find "$TMP/kt" -name '*kernel_stats.csv' | head -1)" "$OUT/kernel_stats_$TAG.csv"
+python3 "$ROOT/tools/window_stats.py" "$(find "$TMP/kt" -name '*kernel_trace.csv' | head -1)" "$OUT/prof_bench_$TAG.json" > "$OUT/window_stats_$TAG.json" && cat "$OUT/window_stats_$TAG.json"
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_price --output-format csv -d "$TMP/pmc" -o run -- python3 "$ROOT/bench.py" $REG > "$OUT/pmc_bench_$TAG.json" 2> "$OUT/pmc_bench_$TAG.err" || { echo "rocprof pmc failed rc=$?"; tail -20 "$OUT/pmc_bench_$TAG.err"; exit 6; }
+python3 "$ROOT/tools/pmc_traffic.py" "$(find "$TMP/pmc" -name '*counter_collection.csv' | head -1)" "$OUT/pmc_bench_$TAG.json" > "$OUT/pmc_traffic_$TAG.json" && cat "$OUT/pmc_traffic_$TAG.json"
+WIN="--steps 0 --warmup 0 --window 1 --c4 0 --sparse 0 --no-cpu --compare-rules 0"
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$TMP/tl" -o run -- python3 "$ROOT/bench.py" $WIN > "$OUT/tl_bench_$TAG.json" 2>&1 || { echo "rocprof timeline failed"; exit 7; }
+python3 "$ROOT/tools/timeline.py" "$(find "$TMP/tl" -name '*kernel_trace.csv' | head -1)" 100 1000 > "$OUT/timeline_$TAG.txt" && cat "$OUT/timeline_$TAG.txt"
+rm -rf "$TMP"
 echo done

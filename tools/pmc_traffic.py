@@ -2,29 +2,36 @@
 
 FETCH_SIZE is in KiB and, on gfx950, reports half the bytes of a wide
 coalesced streaming read (MI355X_MICROARCH.md, HBM section): bytes =
-2 * 1024 * FETCH_SIZE.  The PMC pass runs `bench.py --steps K --warmup W`;
-the timed launches are dispatches W+1 .. W+K of k_price (launch 0-based W..W+K-1).
-Usage: python tools/pmc_traffic.py <counter_collection.csv> <bench.json> W K
+2 * 1024 * FETCH_SIZE.  The PMC pass runs `bench.py --steps K --warmup W`
+(steps are full solves, each of L pricing launches -- bench's
+final.price_launches_per_solve): the timed launches are k_price dispatches
+[W*L, (W+K)*L) in dispatch order.
+Usage: python tools/pmc_traffic.py <counter_collection.csv> <bench.json>
 """
 import csv
 import json
 import sys
 
 
-def main(csv_path, bench_json, warmup, steps):
+def main(csv_path, bench_json):
+    b = json.loads(open(bench_json).read().strip().splitlines()[-1])
+    W, K = b["warmup"], b["steps"]
+    L = b["final"]["price_launches_per_solve"]
     rows = [r for r in csv.DictReader(open(csv_path))
             if r["Counter_Name"] == "FETCH_SIZE" and "k_price" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    win = rows[warmup:warmup + steps]
+    win = rows[W * L:(W + K) * L]
     fetch = [2 * 1024 * float(r["Counter_Value"]) for r in win]
-    b = json.loads(open(bench_json).read().strip().splitlines()[-1])
     alg = b["roofline"]["bytes_per_launch"]
     out = {
-        "warmup": warmup,
-        "steps": steps,
+        "step": "full solve",
+        "warmup": W,
+        "steps": K,
         "m": b["config"]["m"],
         "n": b["config"]["n"],
+        "launches_per_solve": L,
         "launches": len(win),
+        "dispatches_in_pass": len(rows),
         "traffic_bytes_per_launch": sum(fetch) / len(fetch),
         "algorithmic_bytes_per_launch": alg,
         "traffic_over_algorithmic": (sum(fetch) / len(fetch)) / alg if alg else None,
@@ -34,4 +41,4 @@ def main(csv_path, bench_json, warmup, steps):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]))
+    main(sys.argv[1], sys.argv[2])
