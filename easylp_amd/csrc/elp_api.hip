@@ -14,7 +14,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
+#include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/easylp_hip.h"
@@ -86,6 +89,14 @@ struct elp_handle {
     // ELP_STAMPS debug: k_ratio phase stamps, summed over polled chunks
     std::vector<double> stamp_sum;
     int64_t stamp_n = 0;
+    // single-process multi-device (elp_control.ngpu > 1): this handle drives one
+    // rank handle per device (see "ngpu" below); empty for an ordinary handle
+    std::vector<elp_handle*> ranks;
+    std::vector<int> rank_dev;
+    std::unique_ptr<elp::ThreadGroup> tgroup;  // ranks sharing a device
+    std::vector<elp::ThreadRank> tranks;
+    std::vector<double*> peer_A;  // elp_load_dense_device: A copied to the other devices
+    size_t peer_A_count = 0;
 };
 
 extern "C" void elp_default_control(elp_control* c) {
@@ -126,6 +137,7 @@ static void free_dev(elp_handle* h) {
         if (p) (void)hipFree(p);
     h->A_owned = nullptr;
     h->d_flag = nullptr;
+    h->w_cap = 0;  // (W0 / W1 went with the rest)
     d = Dev{};
     if (h->hctl) (void)hipHostFree(h->hctl);
     h->hctl = nullptr;
@@ -134,6 +146,95 @@ static void free_dev(elp_handle* h) {
 template <class T>
 static hipError_t dalloc(T** p, size_t count) {
     return hipMalloc((void**)p, (count ? count : 1) * sizeof(T));
+}
+
+// ---------------------------------------------------------------- ngpu
+// Single-process multi-device (elp_control.ngpu = P > 1; SURVEY.md 8b
+// "Threading": the R caller stays one synchronous process): the handle the
+// caller holds drives P rank handles, one per device, each the column-sharded
+// solver of one rank (elp_comm_* semantics).  Every API call runs on all ranks
+// at once -- rank 0 on the calling thread, the others on one host thread each
+// -- and returns when all are done.  Ranks on distinct devices share an RCCL
+// communicator from ncclCommInitAll (xGMI); ranks that share a device (fewer
+// devices than P, e.g. a one-GPU box) use the in-process ThreadGroup.
+static bool is_group(const elp_handle* h) { return h && !h->ranks.empty(); }
+
+template <class F>
+static int fan_out(elp_handle* g, F&& f) {
+    const int P = (int)g->ranks.size();
+    if (g->tgroup) g->tgroup->reset();
+    std::vector<int> rc(P, 0);
+    std::vector<std::string> err(P);
+    std::atomic<int> first{-1};
+    auto run = [&](int r) {
+        rc[r] = f(g->ranks[r], r);
+        if (rc[r] < 0) {
+            err[r] = g_err;
+            int none = -1;
+            first.compare_exchange_strong(none, r);
+            if (g->tgroup) g->tgroup->abort();  // release the ranks waiting in a collective
+        }
+    };
+    std::vector<std::thread> th;
+    th.reserve((size_t)P);
+    for (int r = 1; r < P; ++r) th.emplace_back(run, r);
+    run(0);
+    for (auto& t : th) t.join();
+    const int r = first.load();
+    if (r >= 0) return fail(rc[r], "rank " + std::to_string(r) + ": " + err[r]);
+    return rc[0];
+}
+
+static void destroy_group(elp_handle* g) {
+    for (size_t r = 0; r < g->peer_A.size(); ++r)
+        if (g->peer_A[r]) {
+            (void)hipSetDevice(g->rank_dev[r]);
+            (void)hipFree(g->peer_A[r]);
+        }
+    g->peer_A.clear();
+    for (elp_handle* r : g->ranks)
+        if (r) elp_destroy(r);
+    g->ranks.clear();
+    g->tgroup.reset();
+}
+
+static int create_group(elp_handle* g) {
+    const int P = g->ctl.ngpu;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail(ELP_E_HIP, "elp_create: no HIP device");
+    g->rank_dev.resize(P);
+    for (int r = 0; r < P; ++r) g->rank_dev[r] = (g->ctl.device + r) % ndev;
+    const bool distinct = P <= ndev && !std::getenv("ELP_NGPU_THREADS");
+    g->ranks.assign(P, nullptr);
+    for (int r = 0; r < P; ++r) {
+        elp_control c = g->ctl;
+        c.ngpu = 1;
+        c.device = g->rank_dev[r];
+        const int rc = elp_create(&g->ranks[r], g->m, g->n, &c);
+        if (rc) return rc;
+    }
+    if (distinct) {
+        std::vector<void*> comms;
+        int rc = Comm::init_all(comms, g->rank_dev);
+        if (rc) return fail(rc, "elp_create: ncclCommInitAll failed");
+        for (int r = 0; r < P; ++r) {
+            HIPCHK(hipSetDevice(g->rank_dev[r]));
+            rc = g->ranks[r]->comm.adopt_rccl(comms[r], P, r);
+            if (rc) return fail(rc, "elp_create: communicator set-up failed");
+        }
+    } else {
+        g->tgroup = std::make_unique<ThreadGroup>(P);
+        g->tranks.resize(P);
+        for (int r = 0; r < P; ++r) {
+            g->tranks[r] = ThreadRank{g->tgroup.get(), r};
+            HIPCHK(hipSetDevice(g->rank_dev[r]));
+            const int rc = g->ranks[r]->comm.init_host(P, r, ThreadGroup::allgather, ThreadGroup::allreduce,
+                                                       ThreadGroup::bcast, &g->tranks[r]);
+            if (rc) return fail(rc, "elp_create: in-process transport set-up failed");
+        }
+    }
+    g->peer_A.assign(P, nullptr);
+    return 0;
 }
 
 extern "C" int elp_create(elp_handle** out, int64_t m, int64_t n, const elp_control* ctl) {
@@ -165,6 +266,14 @@ extern "C" int elp_create(elp_handle** out, int64_t m, int64_t n, const elp_cont
     if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess) {
         delete h;
         return fail(ELP_E_HIP, "elp_create: stream creation failed");
+    }
+    if (h->ctl.ngpu > 1) {
+        const int rc = create_group(h);
+        if (rc) {
+            const std::string msg = g_err;
+            elp_destroy(h);
+            return fail(rc, msg);
+        }
     }
     *out = h;
     return 0;
@@ -521,6 +630,8 @@ static int prep_load(elp_handle* h, bool csc = false) {
 
 extern "C" int elp_load_dense(elp_handle* h, const double* A, const int32_t* dir, const double* rhs,
                               const double* obj, const double* lo, const double* up, int32_t maximize) {
+    if (is_group(h))
+        return fan_out(h, [&](elp_handle* r, int) { return elp_load_dense(r, A, dir, rhs, obj, lo, up, maximize); });
     const double t0 = now_s();
     if (!h || !obj || (h->m > 0 && (!A || !dir || !rhs))) return fail(ELP_E_ARG, "elp_load_dense: NULL input");
     int rc = prep_load(h);
@@ -541,6 +652,28 @@ extern "C" int elp_load_dense(elp_handle* h, const double* A, const int32_t* dir
 extern "C" int elp_load_dense_device(elp_handle* h, const double* dA, const int32_t* dir,
                                      const double* rhs, const double* obj, const double* lo,
                                      const double* up, int32_t maximize) {
+    if (is_group(h)) {
+        // every rank reads A from its own HBM: ranks on other devices get a copy
+        const size_t cnt = (size_t)h->m * (size_t)h->n;
+        const size_t have = h->peer_A_count;
+        h->peer_A_count = std::max(have, cnt);
+        return fan_out(h, [&](elp_handle* r, int k) {
+            const double* src = dA;
+            if (cnt && h->rank_dev[k] != h->rank_dev[0]) {
+                if (hipSetDevice(h->rank_dev[k]) != hipSuccess) return fail(ELP_E_HIP, "hipSetDevice");
+                if (!h->peer_A[k] || have < cnt) {
+                    if (h->peer_A[k]) (void)hipFree(h->peer_A[k]);
+                    h->peer_A[k] = nullptr;
+                    if (dalloc(&h->peer_A[k], cnt) != hipSuccess) return fail(ELP_E_NOMEM, "copy of A");
+                }
+                if (hipMemcpyPeer(h->peer_A[k], h->rank_dev[k], dA, h->rank_dev[0], cnt * sizeof(double)) !=
+                    hipSuccess)
+                    return fail(ELP_E_HIP, "hipMemcpyPeer of A");
+                src = h->peer_A[k];
+            }
+            return elp_load_dense_device(r, src, dir, rhs, obj, lo, up, maximize);
+        });
+    }
     const double t0 = now_s();
     if (!h || !obj || (h->m > 0 && (!dA || !dir || !rhs)))
         return fail(ELP_E_ARG, "elp_load_dense_device: NULL input");
@@ -557,6 +690,7 @@ extern "C" int elp_load_dense_device(elp_handle* h, const double* dA, const int3
 extern "C" int elp_load_csc(elp_handle* h, const int64_t* colptr, const int32_t* rowind,
                             const double* val, const int32_t* dir, const double* rhs,
                             const double* obj, const double* lo, const double* up, int32_t maximize) {
+    if (is_group(h)) return fail(ELP_E_UNSUPPORTED, "elp_load_csc: not with ngpu > 1 (column-sharded CSC)");
     const double t0 = now_s();
     if (!h || !obj || !colptr || (h->m > 0 && (!dir || !rhs))) return fail(ELP_E_ARG, "elp_load_csc: NULL input");
     const int64_t m = h->m, n = h->n;
@@ -623,6 +757,7 @@ extern "C" int elp_load_csc(elp_handle* h, const int64_t* colptr, const int32_t*
 }
 
 extern "C" int elp_load_generated(elp_handle* h, uint64_t seed) {
+    if (is_group(h)) return fan_out(h, [&](elp_handle* r, int) { return elp_load_generated(r, seed); });
     const double t0 = now_s();
     int rc = prep_load(h);
     if (rc) return rc;
@@ -956,6 +1091,7 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
 }
 
 extern "C" int elp_set_int(elp_handle* h, const int32_t* is_int) {
+    if (is_group(h)) return fan_out(h, [&](elp_handle* r, int) { return elp_set_int(r, is_int); });
     if (!h || !h->loaded) return fail(ELP_E_STATE, "elp_set_int: no problem loaded");
     h->is_int.clear();
     if (is_int) {
@@ -1108,6 +1244,12 @@ static int run_bnb(elp_handle* h, int32_t* out_status) {
 
 extern "C" int elp_solve(elp_handle* h, int32_t* lp_status) {
     if (!h || !lp_status) return fail(ELP_E_ARG, "elp_solve: NULL argument");
+    if (is_group(h)) {
+        std::vector<int32_t> st(h->ranks.size(), 0);
+        const int rc = fan_out(h, [&](elp_handle* r, int k) { return elp_solve(r, &st[k]); });
+        *lp_status = st[0];
+        return rc;
+    }
     if (!h->loaded) return fail(ELP_E_STATE, "elp_solve: no problem loaded");
     HIPCHK(hipSetDevice(h->dev));
     const double t0 = now_s();
@@ -1123,6 +1265,12 @@ extern "C" int elp_solve(elp_handle* h, int32_t* lp_status) {
 
 extern "C" int elp_iterate(elp_handle* h, int64_t iters, int32_t* lp_status) {
     if (!h || !lp_status || iters < 0) return fail(ELP_E_ARG, "elp_iterate: bad argument");
+    if (is_group(h)) {
+        std::vector<int32_t> st(h->ranks.size(), 0);
+        const int rc = fan_out(h, [&](elp_handle* r, int k) { return elp_iterate(r, iters, &st[k]); });
+        *lp_status = st[0];
+        return rc;
+    }
     if (!h->loaded) return fail(ELP_E_STATE, "elp_iterate: no problem loaded");
     HIPCHK(hipSetDevice(h->dev));
     const double t0 = now_s();
@@ -1132,6 +1280,11 @@ extern "C" int elp_iterate(elp_handle* h, int64_t iters, int32_t* lp_status) {
 }
 
 extern "C" int elp_get_solution(elp_handle* h, double* objval, double* x, double* y, int64_t* basis) {
+    if (is_group(h))  // (collective: every rank takes part, rank 0 reports)
+        return fan_out(h, [&](elp_handle* r, int k) {
+            return k == 0 ? elp_get_solution(r, objval, x, y, basis)
+                          : elp_get_solution(r, nullptr, nullptr, nullptr, nullptr);
+        });
     if (!h || !h->loaded) return fail(ELP_E_STATE, "elp_get_solution: no problem loaded");
     HIPCHK(hipSetDevice(h->dev));
     const int64_t m = h->m, n = h->n, nl = h->nloc;
@@ -1200,6 +1353,7 @@ extern "C" int elp_get_solution(elp_handle* h, double* objval, double* x, double
 // oracle/elp_oracle.c sensitivity() line by line.
 extern "C" int elp_sensitivity(elp_handle* h, double* objfrom, double* objtill, double* duals,
                                double* dualsfrom, double* dualstill) {
+    if (is_group(h)) return fail(ELP_E_UNSUPPORTED, "elp_sensitivity: column-sharded solves (ngpu > 1)");
     if (!h || !h->loaded) return fail(ELP_E_STATE, "elp_sensitivity: no problem loaded");
     if (!h->done || h->final_status != ELP_OPTIMAL)
         return fail(ELP_E_STATE, "elp_sensitivity: problem is not optimal");
@@ -1304,6 +1458,7 @@ extern "C" int elp_sensitivity(elp_handle* h, double* objfrom, double* objtill, 
 }
 
 extern "C" int elp_get_stats(elp_handle* h, elp_stats* st) {
+    if (is_group(h)) return elp_get_stats(h->ranks[0], st);
     if (!h || !st) return fail(ELP_E_ARG, "elp_get_stats: NULL argument");
     if (h->loaded) {
         HIPCHK(hipSetDevice(h->dev));
@@ -1330,6 +1485,8 @@ extern "C" int elp_get_stats(elp_handle* h, elp_stats* st) {
 }
 
 extern "C" int elp_set_trace(elp_handle* h, int64_t capacity) {
+    if (is_group(h) && capacity >= 0)
+        return fan_out(h, [&](elp_handle* r, int) { return elp_set_trace(r, capacity); });
     if (!h || capacity < 0) return fail(ELP_E_ARG, "elp_set_trace: bad argument");
     if (h->loaded) return fail(ELP_E_STATE, "elp_set_trace: call before elp_load_*");
     h->trace_cap = capacity;
@@ -1337,6 +1494,7 @@ extern "C" int elp_set_trace(elp_handle* h, int64_t capacity) {
 }
 
 extern "C" int elp_get_trace(elp_handle* h, int64_t* pairs, int64_t capacity, int64_t* count) {
+    if (is_group(h)) return elp_get_trace(h->ranks[0], pairs, capacity, count);
     if (!h || !count) return fail(ELP_E_ARG, "elp_get_trace: NULL argument");
     if (!h->loaded) return fail(ELP_E_STATE, "elp_get_trace: no problem loaded");
     HIPCHK(hipSetDevice(h->dev));
@@ -1363,6 +1521,7 @@ extern "C" void elp_destroy(elp_handle* h) {
                      h->stamp_sum[15] / h->stamp_n / 1e3);
     }
     if (!h) return;
+    destroy_group(h);
     (void)hipSetDevice(h->dev);
     if (h->st) (void)hipStreamSynchronize(h->st);
     if (getenv("ELP_DEBUG_ENQUEUE"))
@@ -1378,6 +1537,7 @@ extern "C" void elp_destroy(elp_handle* h) {
 extern "C" int elp_comm_unique_id(uint8_t id[128]) { return elp::Comm::unique_id(id); }
 
 extern "C" int elp_comm_init(elp_handle* h, const uint8_t id[128], int32_t world_size, int32_t rank) {
+    if (is_group(h)) return fail(ELP_E_STATE, "an ngpu > 1 handle owns its communicator");
     if (!h || !id || world_size < 1 || rank < 0 || rank >= world_size)
         return fail(ELP_E_ARG, "elp_comm_init: bad argument");
     if (h->loaded) return fail(ELP_E_STATE, "elp_comm_init: call before elp_load_*");
@@ -1387,6 +1547,7 @@ extern "C" int elp_comm_init(elp_handle* h, const uint8_t id[128], int32_t world
 }
 
 extern "C" int elp_comm_enable_p2p(elp_handle* h) {
+    if (is_group(h)) return fail(ELP_E_STATE, "an ngpu > 1 handle owns its communicator");
     if (!h) return fail(ELP_E_ARG, "elp_comm_enable_p2p: NULL handle");
     if (h->loaded) return fail(ELP_E_STATE, "elp_comm_enable_p2p: call before elp_load_*");
     if (h->comm.kind == 0) return 0;  // one rank: nothing to exchange
@@ -1399,6 +1560,7 @@ extern "C" int elp_comm_enable_p2p(elp_handle* h) {
 extern "C" int elp_comm_init_host(elp_handle* h, int32_t world_size, int32_t rank,
                                   elp_host_allgather_fn ag, elp_host_allreduce_fn ar,
                                   elp_host_bcast_fn bc, void* user) {
+    if (is_group(h)) return fail(ELP_E_STATE, "an ngpu > 1 handle owns its communicator");
     if (!h || world_size < 1 || rank < 0 || rank >= world_size)
         return fail(ELP_E_ARG, "elp_comm_init_host: bad argument");
     if (h->loaded) return fail(ELP_E_STATE, "elp_comm_init_host: call before elp_load_*");

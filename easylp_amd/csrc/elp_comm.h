@@ -10,11 +10,41 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <condition_variable>
+#include <mutex>
 #include <vector>
 
 #include "../../include/easylp_hip.h"
 
 namespace elp {
+
+// In-process transport of a single-process multi-device handle
+// (elp_control.ngpu) whose ranks share a device: the ranks are host threads of
+// one process and exchange host copies through a shared staging area, a
+// generation-counted barrier between the phases of each collective.  The
+// reductions run in rank order on every rank, so all ranks hold identical
+// bits.  abort() releases every waiting rank (their collectives fail).
+struct ThreadGroup {
+    int world;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    bool aborted = false;
+    std::vector<unsigned char> buf;
+    explicit ThreadGroup(int P) : world(P) {}
+    bool barrier();
+    void abort();
+    void reset();
+    // elp_host_*_fn callbacks; user = &ranks[r] (a ThreadRank)
+    static int allgather(const void* send, void* recv, size_t bytes, void* user);
+    static int allreduce(void* buf, size_t count, int32_t dtype, void* user);
+    static int bcast(void* buf, size_t bytes, int32_t root, void* user);
+};
+struct ThreadRank {
+    ThreadGroup* g;
+    int rank;
+};
 
 struct Comm {
     int world = 1, rank = 0;
@@ -40,6 +70,10 @@ struct Comm {
 
     static int unique_id(uint8_t id[128]);
     int init_rccl(const uint8_t id[128], int world_size, int rank_);
+    // a communicator of ncclCommInitAll (single-process multi-device): taken over
+    int adopt_rccl(void* comm, int world_size, int rank_);
+    // ncclCommInitAll over devs (one communicator per device, rank = position)
+    static int init_all(std::vector<void*>& comms, const std::vector<int>& devs);
     int init_host(int world_size, int rank_, elp_host_allgather_fn ag, elp_host_allreduce_fn ar,
                   elp_host_bcast_fn bc, void* user);
     void destroy();

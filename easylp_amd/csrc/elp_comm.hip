@@ -3,6 +3,7 @@
 
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -36,6 +37,106 @@ int Comm::init_rccl(const uint8_t id[128], int world_size, int rank_) {
     nccl = c;
     kind = 1;
     return 0;
+}
+
+int Comm::adopt_rccl(void* comm, int world_size, int rank_) {
+    world = world_size;
+    rank = rank_;
+    if (!scratch && hipMalloc(&scratch, SCRATCH_BYTES) != hipSuccess) {
+        scratch = nullptr;
+        return ELP_E_NOMEM;
+    }
+    nccl = comm;
+    kind = 1;
+    return 0;
+}
+
+int Comm::init_all(std::vector<void*>& comms, const std::vector<int>& devs) {
+    std::vector<ncclComm_t> c(devs.size(), nullptr);
+    if (ncclCommInitAll(c.data(), (int)devs.size(), devs.data()) != ncclSuccess) return ELP_E_COMM;
+    comms.assign(c.begin(), c.end());
+    return 0;
+}
+
+// ---------------------------------------------------------------- threads
+bool ThreadGroup::barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    if (aborted) return false;
+    const uint64_t my = gen;
+    if (++arrived == world) {
+        arrived = 0;
+        ++gen;
+        cv.notify_all();
+        return true;
+    }
+    cv.wait(lk, [&] { return gen != my || aborted; });
+    return !aborted || gen != my;
+}
+
+void ThreadGroup::abort() {
+    std::lock_guard<std::mutex> lk(mu);
+    aborted = true;
+    cv.notify_all();
+}
+
+void ThreadGroup::reset() {
+    std::lock_guard<std::mutex> lk(mu);
+    aborted = false;
+    arrived = 0;
+}
+
+// every collective: (rank 0 sizes the area) barrier, deposit, barrier, read,
+// barrier -- the last one keeps the area intact until every rank has read it
+int ThreadGroup::allgather(const void* send, void* recv, size_t bytes, void* user) {
+    ThreadRank* tr = static_cast<ThreadRank*>(user);
+    ThreadGroup& g = *tr->g;
+    if (!g.barrier()) return 1;
+    if (tr->rank == 0) g.buf.resize(bytes * (size_t)g.world);
+    if (!g.barrier()) return 1;
+    std::memcpy(g.buf.data() + bytes * (size_t)tr->rank, send, bytes);
+    if (!g.barrier()) return 1;
+    std::memcpy(recv, g.buf.data(), bytes * (size_t)g.world);
+    return g.barrier() ? 0 : 1;
+}
+
+int ThreadGroup::allreduce(void* buf, size_t count, int32_t dtype, void* user) {
+    ThreadRank* tr = static_cast<ThreadRank*>(user);
+    ThreadGroup& g = *tr->g;
+    const size_t es = dtype == 0 ? sizeof(double) : sizeof(int32_t);
+    const size_t bytes = count * es;
+    if (!g.barrier()) return 1;
+    if (tr->rank == 0) g.buf.resize(bytes * (size_t)g.world);
+    if (!g.barrier()) return 1;
+    std::memcpy(g.buf.data() + bytes * (size_t)tr->rank, buf, bytes);
+    if (!g.barrier()) return 1;
+    if (dtype == 0) {  // f64 sum in rank order
+        double* out = static_cast<double*>(buf);
+        const double* all = reinterpret_cast<const double*>(g.buf.data());
+        for (size_t i = 0; i < count; ++i) {
+            double acc = all[i];
+            for (int r = 1; r < g.world; ++r) acc = acc + all[(size_t)r * count + i];
+            out[i] = acc;
+        }
+    } else {  // i32 max
+        int32_t* out = static_cast<int32_t*>(buf);
+        const int32_t* all = reinterpret_cast<const int32_t*>(g.buf.data());
+        for (size_t i = 0; i < count; ++i) {
+            int32_t v = all[i];
+            for (int r = 1; r < g.world; ++r) v = std::max(v, all[(size_t)r * count + i]);
+            out[i] = v;
+        }
+    }
+    return g.barrier() ? 0 : 1;
+}
+
+int ThreadGroup::bcast(void* buf, size_t bytes, int32_t root, void* user) {
+    ThreadRank* tr = static_cast<ThreadRank*>(user);
+    ThreadGroup& g = *tr->g;
+    if (!g.barrier()) return 1;
+    if (tr->rank == root) g.buf.assign(static_cast<unsigned char*>(buf), static_cast<unsigned char*>(buf) + bytes);
+    if (!g.barrier()) return 1;
+    if (tr->rank != root) std::memcpy(buf, g.buf.data(), bytes);
+    return g.barrier() ? 0 : 1;
 }
 
 int Comm::init_host(int world_size, int rank_, elp_host_allgather_fn ag, elp_host_allreduce_fn ar,

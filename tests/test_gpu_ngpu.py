@@ -1,0 +1,92 @@
+"""Single-process multi-device (elp_control.ngpu > 1, SURVEY.md 8b "Threading":
+the R caller stays one process): one handle drives P rank handles from P host
+threads.  On the one-GPU test box the ranks share the device and talk over the
+in-process ThreadGroup; on a node with P devices the same handle builds an
+RCCL communicator with ncclCommInitAll.  The column-sharded solve must walk the
+oracle's pivot path bit for bit, for A replicated or sharded, and for every
+load entry point."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _general_lp():
+    rng = np.random.default_rng(5)
+    m, n = 40, 90
+    A = rng.uniform(-1, 1, (m, n))
+    x0 = rng.uniform(0, 2, n)
+    dirs = rng.integers(1, 4, m).astype(np.int32)
+    rhs = A @ x0 + np.where(dirs == 1, 1.0, np.where(dirs == 2, -1.0, 0.0))
+    lo = np.where(rng.random(n) < 0.3, -3.0, 0.0)
+    up = np.full(n, 5.0)
+    obj = rng.uniform(-1, 1, n)
+    return A, dirs, rhs, obj, lo, up
+
+
+def _same(g, o, ngpu):
+    assert g.status == o.status
+    np.testing.assert_array_equal(g.trace, o.trace)
+    np.testing.assert_array_equal(g.basis, o.basis)
+    assert g.objval == o.objval
+    np.testing.assert_array_equal(g.x, o.x)
+    assert g.stats["world_size"] == ngpu
+
+
+@pytest.mark.parametrize("ngpu,replicate", [(2, 1), (3, 1), (2, 2), (3, 2), (4, 0)])
+def test_ngpu_generated_matches_oracle(gpu, ngpu, replicate):
+    from oracle import generate_dense, solve_dense as orc
+    m, n, seed = 300, 1201, 11
+    with gpu.Problem(m, n, ngpu=ngpu, replicate=replicate) as p:
+        p.set_trace(200000)
+        p.load_generated(seed)
+        g = p.solution(p.solve())
+    A, b, c = generate_dense(seed, m, n)
+    o = orc(A, np.ones(m, np.int32), b, c, maximize=True, trace_cap=200000)
+    assert o.status == 0
+    _same(g, o, ngpu)
+
+
+@pytest.mark.parametrize("ngpu", [2, 3])
+def test_ngpu_general_lp_matches_oracle(gpu, ngpu):
+    """free / boxed columns, >= and == rows, phase 1 -- through elp_load_dense."""
+    from oracle import solve_dense as orc
+    A, dirs, rhs, obj, lo, up = _general_lp()
+    g = gpu.solve_dense(A, dirs, rhs, obj, lo, up, maximize=True, trace=200000, ngpu=ngpu)
+    o = orc(A, dirs, rhs, obj, lo, up, True, trace_cap=200000)
+    _same(g, o, ngpu)
+
+
+def test_ngpu_device_resident_input(gpu):
+    """elp_load_dense_device on an ngpu handle (A in HBM of the first device;
+    ranks on other devices would get a copy), solved twice on one handle."""
+    from oracle import solve_dense as orc
+    m, n, seed = 250, 1000, 4
+    A, b, c = gpu.generate_dense_device(seed, m, n, 0)
+    with gpu.Problem(m, n, ngpu=2) as p:
+        p.set_trace(100000)
+        for _ in range(2):
+            p.load_dense_device(A.data_ptr(), np.ones(m, np.int32), b, c, maximize=True)
+            g = p.solution(p.solve())
+    Ah = A.cpu().numpy().reshape(n, m).T
+    o = orc(Ah, np.ones(m, np.int32), b, c, maximize=True, trace_cap=100000)
+    _same(g, o, 2)
+
+
+def test_ngpu_mip_and_refusals(gpu):
+    from easylp_amd._lib import ElpError
+    from conftest import load_mip_known_answers
+    from oracle import solve_mip
+    rec = next(r for r in load_mip_known_answers() if r["name"] == "investments")
+    args = (rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], rec["maximize"])
+    g = gpu.solve_dense(*args, is_int=rec["is_int"], ngpu=2)
+    o = solve_mip(*args, rec["is_int"])
+    assert g.status == o.status == 0 and g.objval == o.objval
+    assert g.stats["mip_nodes"] == o.stats["nodes"]
+    with gpu.Problem(2, 2, ngpu=2) as p:
+        with pytest.raises(ElpError, match="owns its communicator"):
+            p.comm_init(bytes(128), 2, 0)
+        p.load_dense(np.eye(2), [1, 1], [1.0, 1.0], [1.0, 1.0], maximize=True)
+        assert p.solve() == 0
+        with pytest.raises(ElpError, match="ngpu"):
+            p.sensitivity()
