@@ -49,7 +49,7 @@ def parse():
                     help="cap on the CPU oracle's iterations (0: one full solve, ~20 s)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-price", type=int, default=1,
-                    help="device-clock timer over every pricing launch (roofline)")
+                    help="HIP events on the pricing dispatches of every 8th chunk (roofline)")
     ap.add_argument("--c4", type=int, default=1,
                     help="also solve the 10000x500000 column-sharded config (SURVEY config 4) to optimality")
     ap.add_argument("--p2p", type=int, default=0,
@@ -115,8 +115,8 @@ def enable_p2p(p, rank):
 
 def make_problem(args, lib, m, n, world, rank, local, **ctl):
     from easylp_amd import Problem
-    from easylp_amd._lib import ELP_PROFILE_PRICE
-    p = Problem(m, n, device=local, verbose=ELP_PROFILE_PRICE if args.profile_price else 0,
+    from easylp_amd._lib import ELP_PROFILE_SAMPLE
+    p = Problem(m, n, device=local, verbose=ELP_PROFILE_SAMPLE if args.profile_price else 0,
                 pricing=args.rule, sync_every=args.sync_every, **ctl)
     p2p = False
     if world > 1 or args.force_sharded:
@@ -144,7 +144,7 @@ def full_solves(p, A, b, c, count, barrier):
 
 def price_roofline(stats_list):
     """Pricing-launch roofline over the given solves: algorithmic sweep bytes /
-    device-clock launch time (every workgroup of each timed launch)."""
+    the launches' time (HIP events bound to each timed pricing dispatch)."""
     secs = sum(s["price_seconds"] for s in stats_list)
     byts = sum(s["price_timed_bytes"] for s in stats_list)
     nl = sum(s["price_timed_launches"] for s in stats_list)
@@ -350,7 +350,11 @@ def main():
     stats = [r[2] for r in recs]
     iters = sum(s["iterations"] for s in stats)
     value = iters / elapsed if elapsed > 0 else 0.0
-    roof = price_roofline(stats)
+    # the pricing kernel's time: HIP events bound to the pricing dispatches
+    # (hipExtLaunchKernelGGL, on the solver's stream) of every 8th chunk of
+    # iterations between host polls in the timed solves -- a uniform sample, so
+    # the markers stay off most dispatches (events on all of them cost ~9 %)
+    roof = dict(price_roofline(stats), timer="HIP events on the pricing dispatches of every 8th chunk of the timed solves")
     last = stats[-1] if stats else p.stats()
     final = {"status": recs[-1][0] if recs else None, "iterations_to_optimal": last["iterations"],
              "objective": p.solution(recs[-1][0]).objval if recs else None,

@@ -15,7 +15,8 @@ ELP_LE, ELP_GE, ELP_EQ = 1, 2, 3
 ELP_OPTIMAL, ELP_SUBOPTIMAL, ELP_INFEASIBLE, ELP_UNBOUNDED = 0, 1, 2, 3
 ELP_NUMFAILURE, ELP_TIMEOUT = 5, 7
 ELP_PROFILE_PRICE = 2   # device-clock pricing timer
-ELP_PROFILE_EVENTS = 4  # HIP-event pricing timer
+ELP_PROFILE_EVENTS = 4  # HIP events on every pricing dispatch
+ELP_PROFILE_SAMPLE = 8  # ... on those of every 8th chunk between host polls
 ELP_SCALE_GEOMETRIC, ELP_SCALE_EQUILIBRATE = 4, 64
 ABI_VERSION = 2
 

@@ -81,6 +81,7 @@ struct elp_handle {
     int64_t trace_cap = 0;
     elp::Comm comm;  // multi-GPU (world 1 = no-op)
     std::vector<hipEvent_t> ev;  // pricing-kernel timing pairs (profile mode)
+    int64_t prof_chunks = 0;     // chunks seen by ELP_PROFILE_SAMPLE
     int32_t* d_flag = nullptr;   // one int for cross-rank decisions
     int64_t ar_rows = 0;         // AR capacity in rows (grown at polls)
     bool replicated = false;     // sharded, every rank holds all of A (Dev::Afull)
@@ -875,7 +876,11 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
     int rc = push_ctl_fields(h);
     if (rc) return rc;
     const int period = h->ctl.refactor_period;
-    const bool prof = (h->ctl.verbose & ELP_PROFILE_EVENTS) != 0;
+    // ELP_PROFILE_EVENTS: events on the pricing dispatches of every chunk;
+    // ELP_PROFILE_SAMPLE: of every 8th chunk only (a uniform sample of the solve
+    // that leaves the other chunks' dispatches untouched)
+    const bool prof_all = (h->ctl.verbose & ELP_PROFILE_EVENTS) != 0;
+    const bool prof = prof_all || (h->ctl.verbose & ELP_PROFILE_SAMPLE) != 0;
     if (prof && (int)h->ev.size() < 2 * h->ctl.sync_every) {
         for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
         h->ev.assign(2 * h->ctl.sync_every, nullptr);
@@ -929,10 +934,11 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             HIPCHK(hipStreamSynchronize(h->st));
         }
         const double t_enq0 = now_s();
+        const bool prof_chunk = prof && (prof_all || h->prof_chunks++ % 8 == 0);
         for (int t = 0; t < chunk; ++t) {
             const int kub = (int)std::min<int64_t>(h->m, (int64_t)k0 + t);
             const int nyub = (int)std::min<int64_t>(h->m, (int64_t)ny0 + t);
-            hipEvent_t e0 = prof ? h->ev[2 * t] : nullptr, e1 = prof ? h->ev[2 * t + 1] : nullptr;
+            hipEvent_t e0 = prof_chunk ? h->ev[2 * t] : nullptr, e1 = prof_chunk ? h->ev[2 * t + 1] : nullptr;
             h->stats.price_launches++;
             if (h->comm.kind == 0 || h->comm.p2p) {  // (p2p: min-loc inside the select kernel)
                 HIPCHK(launch_iteration(h->d, kub, nyub, h->phase, h->st, e0, e1, t));
@@ -992,7 +998,7 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
         const int32_t s = c->status;
         if (s == ST_COMMFAIL)
             return fail(ELP_E_COMM, "xGMI mailbox: a peer's record did not arrive within elp_control.mailbox_timeout");
-        if (prof && s == ST_RUN) {  // every launch of the chunk did work
+        if (prof_chunk && s == ST_RUN) {  // every launch of the chunk did work
             for (int t = 0; t < chunk; ++t) {
                 float ms = 0.f;
                 HIPCHK(hipEventElapsedTime(&ms, h->ev[2 * t], h->ev[2 * t + 1]));

@@ -17,6 +17,7 @@
 // running, so the host can enqueue several iterations between polls.
 #include "elp_internal.h"
 
+#include <hip/hip_ext.h>
 #include <math.h>
 
 namespace elp {
@@ -616,74 +617,101 @@ DEV void price_slacks(const Dev& d, int64_t ntiles, int s, int nsw, Cand* red) {
     if (threadIdx.x == 0) d.cand[ntiles + s] = best;
 }
 
-// One workgroup = PRICE_SPLIT waves = 128 columns x all Y slots.  Wave w sweeps slot
-// chunk w (PRICE_SPLIT contiguous chunks), lane l owns columns 2l, 2l+1 of the
-// tile (16-byte loads, 1 KiB per wave instruction, row-major AR so every load
-// is fully coalesced), 16 rows in flight per wave; y_Y comes from the
-// contiguous yy[] written by BTRAN (wave-uniform scalar loads).  The chunk
-// partials are combined in LDS in chunk order, then the tile's argmin.
+// Pricing (k_price): see price_body.  The chunk partials are combined in LDS in
+// chunk order, then the tile's argmin.
 constexpr int PRICE_THREADS = 64 * PRICE_SPLIT;
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 // plain (cached) loads: the live AR rows (~80 MB at 5000x50000) stay in the
 // 256 MiB Infinity Cache between passes; non-temporal loads measured 10% slower
 #define AR_LOAD(ptr) (*reinterpret_cast<const dbl2*>(ptr))
-DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
-    __shared__ double part[PRICE_SPLIT][TILE_COLS];
-    __shared__ Cand red[PRICE_SPLIT];
-    if (apply_role(d, napply, nb_minv)) return;
-    const DevCtl* c = d.ctl;
-    if (c->status != ST_RUN) return;
-    const int64_t ntiles = gridDim.x - napply - nsw;
-    if ((int64_t)blockIdx.x >= ntiles) {  // a slack workgroup
-        price_slacks<PRICE_THREADS>(d, ntiles, (int)(blockIdx.x - ntiles), nsw, red);
-        return;
-    }
-    const int ny = c->ny, bland = c->bland;
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // the tile's per-column operands of the epilogue (status, cost, Devex weight
-    // and previous d) go out before the sweep, so the epilogue waits for none
-    // of them (every wave loads, clamped: no branch to drain; waves 0-1 use them)
-    const int64_t jt = (int64_t)blockIdx.x * TILE_COLS + (threadIdx.x & (TILE_COLS - 1));
-    const int64_t jc = jt < d.n ? jt : 0;
-    const int devex = c->devex;
-    const DevexIn dx = devex_in(c);
-    const double dtol = c->tol_dual;
-    const int8_t pf_vs = d.vstat[jc];
-    const double pf_c = d.cost[jc], pf_w = d.dw[jc], pf_dp = d.dprev[jc];
-    const int L = (ny + PRICE_SPLIT - 1) / PRICE_SPLIT;
-    const int p0 = w * L;
-    const int p1 = min(ny, p0 + L);
-    // this tile's rows are contiguous: row p at col + p * TILE_COLS
-    const double* col = d.AR + (size_t)blockIdx.x * (size_t)d.arcap * TILE_COLS + 2 * lane;
-    const double* __restrict__ yy = d.yy;
-    double acc0 = 0.0, acc1 = 0.0;
-    int p = p0;
 #ifndef ELP_PRICE_UNR
 #define ELP_PRICE_UNR 16
 #endif
+// One tile workgroup = PRICE_SPLIT waves = 128 columns x all Y slots.  Wave w
+// sweeps the slots p = w, w + PRICE_SPLIT, w + 2 PRICE_SPLIT, ... (an fma chain
+// in slot order; the oracle's price order): its first UNR rows do not depend
+// on |Y|, so they go out with the epilogue operands BEFORE the control block
+// arrives (rows past |Y| are masked when it does), and the sweep overlaps the
+// control-block round trip instead of following it.
+DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
+    __shared__ double part[PRICE_SPLIT][TILE_COLS];
+    __shared__ Cand red[PRICE_SPLIT];
+    const int64_t ntiles = gridDim.x - napply - nsw;
+    if ((int64_t)blockIdx.x >= ntiles) {
+        if (apply_role(d, napply, nb_minv)) return;
+        if (d.ctl->status != ST_RUN) return;
+        price_slacks<PRICE_THREADS>(d, ntiles, (int)(blockIdx.x - ntiles), nsw, red);  // a slack workgroup
+        return;
+    }
+    constexpr int S = PRICE_SPLIT;
     constexpr int UNR = ELP_PRICE_UNR;  // rows in flight per wave: 16 KiB (32 measured slower)
-    for (; p + UNR <= p1; p += UNR) {
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // the tile's per-column operands of the epilogue (status, cost, Devex weight
+    // and previous d): every wave loads, clamped, no branch to drain; waves 0-1
+    // use them
+    const int64_t jt = (int64_t)blockIdx.x * TILE_COLS + (threadIdx.x & (TILE_COLS - 1));
+    const int64_t jc = jt < d.n ? jt : 0;
+    const int8_t pf_vs = d.vstat[jc];
+    const double pf_c = d.cost[jc], pf_w = d.dw[jc], pf_dp = d.dprev[jc];
+    // this tile's rows are contiguous: row p at col + p * TILE_COLS
+    const double* col = d.AR + (size_t)blockIdx.x * (size_t)d.arcap * TILE_COLS + 2 * lane;
+    const double* __restrict__ yy = d.yy;
+    const int cap = (int)d.arcap;
+    dbl2 v0[UNR];
+    double y0[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {  // slot w + S u, clamped into AR
+        const int pp = min(w + S * u, cap - 1);
+        v0[u] = AR_LOAD(col + (size_t)pp * TILE_COLS);
+        y0[u] = yy[pp];
+    }
+    __builtin_amdgcn_sched_barrier(0);  // all of the above issued before any use
+    const DevCtl* c = d.ctl;
+    const int32_t st0 = c->status;
+    const int ny = c->ny, bland = c->bland;
+    if (st0 != ST_RUN) {
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            KEEP(v0[u].x);
+            KEEP(y0[u]);
+        }
+        KEEP(pf_c);
+        return;
+    }
+    const int devex = c->devex;
+    const DevexIn dx = devex_in(c);
+    const double dtol = c->tol_dual;
+    double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+        if (w + S * u < ny) {
+            acc0 = fma(v0[u].x, y0[u], acc0);
+            acc1 = fma(v0[u].y, y0[u], acc1);
+        }
+    }
+    int p = w + S * UNR;
+    for (; p + S * (UNR - 1) < ny; p += S * UNR) {
         dbl2 v[UNR];
 #pragma unroll
         for (int u = 0; u < UNR; ++u)
-            v[u] = AR_LOAD(col + (size_t)(p + u) * TILE_COLS);
+            v[u] = AR_LOAD(col + (size_t)(p + S * u) * TILE_COLS);
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
-            const double yv = yy[p + u];
+            const double yv = yy[p + S * u];
             acc0 = fma(v[u].x, yv, acc0);
             acc1 = fma(v[u].y, yv, acc1);
         }
     }
-    if (p < p1) {  // remainder: same order, loads issued together
+    if (p < ny) {  // remainder: same order, loads issued together
         dbl2 v[UNR];
 #pragma unroll
         for (int u = 0; u < UNR; ++u)
-            v[u] = (p + u < p1) ? AR_LOAD(col + (size_t)(p + u) * TILE_COLS) : dbl2{0.0, 0.0};
+            v[u] = (p + S * u < ny) ? AR_LOAD(col + (size_t)(p + S * u) * TILE_COLS) : dbl2{0.0, 0.0};
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
-            if (p + u < p1) {
-                const double yv = yy[p + u];
+            if (p + S * u < ny) {
+                const double yv = yy[p + S * u];
                 acc0 = fma(v[u].x, yv, acc0);
                 acc1 = fma(v[u].y, yv, acc1);
             }
@@ -1618,7 +1646,13 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     //      out next (bounded by the host's k_ub, masked by the real k below):
     //      the pass-1 minima, this wave's row of MinvT (B^-1 row, cases B / D)
     //      and its bump row R_col (dual update)
-    constexpr int PFB = 4, PFT = 8;
+#ifndef ELP_RATIO_PFT
+#define ELP_RATIO_PFT 8
+#endif
+#ifndef ELP_RATIO_PFQ
+#define ELP_RATIO_PFQ 1  // (4: +0.5 us of k_ratio, rocprof A/B r02)
+#endif
+    constexpr int PFB = 4, PFT = ELP_RATIO_PFT;
     const bool main_wg = (int)blockIdx.x < nmain;
     const bool pfb = nblk <= 256 * PFB, pft = k_ub <= 64 * PFT;
     double bm[PFB], trow[PFT];
@@ -1635,7 +1669,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     const int rcol = ld_clamp(d.Rl, main_wg ? col : 0, k_ub);
     // the pass-2 candidates k_ftran_zr emitted: RSEG lists, 32 threads per list
     // (256 = RSEG * 32), the first 32 * PFQ entries of each, masked by its count
-    constexpr int PFQ = 4;
+    constexpr int PFQ = ELP_RATIO_PFQ;
     static_assert(RSEG * 32 == 256, "k_ratio: 32 threads per candidate list");
     const int sg = tid & (RSEG - 1), si = tid >> 3;
     const RCand* segp = d.rcand + (size_t)sg * d.rsegcap;
@@ -2771,12 +2805,23 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phas
 #define ELP_APPLY_PT 4
 #endif
     if (phase == 2) update_grid(d, k_ub, false, &nb_minv, &napply, d.csc ? TILE_COLS : PRICE_THREADS, ELP_APPLY_PT);
-    if (ev0) (void)hipEventRecord(ev0, st);
     // + nsw: the slack workgroups (candidates [ntiles, ntiles + nsw))
     const int nsw = slack_wgs(d, ny_ub);
-    if (d.csc) k_price_csc<<<ntiles + nsw + napply, TILE_COLS, 0, st>>>(d, (int)napply, (int)nb_minv, nsw);
-    else k_price<<<ntiles + nsw + napply, PRICE_THREADS, 0, st>>>(d, (int)napply, (int)nb_minv, nsw);
-    if (ev1) (void)hipEventRecord(ev1, st);
+    const unsigned grid = ntiles + nsw + napply;
+    if (ev0) {
+        // profiling (ELP_PROFILE_EVENTS): events bound to the dispatch itself
+        // (the CP's start / end timestamps of this launch, as a kernel trace
+        // reports them; no marker packets between the kernels)
+        if (d.csc)
+            hipExtLaunchKernelGGL(k_price_csc, dim3(grid), dim3(TILE_COLS), 0, st, ev0, ev1, 0, d, (int)napply,
+                                  (int)nb_minv, nsw);
+        else
+            hipExtLaunchKernelGGL(k_price, dim3(grid), dim3(PRICE_THREADS), 0, st, ev0, ev1, 0, d, (int)napply,
+                                  (int)nb_minv, nsw);
+        return hipGetLastError();
+    }
+    if (d.csc) k_price_csc<<<grid, TILE_COLS, 0, st>>>(d, (int)napply, (int)nb_minv, nsw);
+    else k_price<<<grid, PRICE_THREADS, 0, st>>>(d, (int)napply, (int)nb_minv, nsw);
     return hipGetLastError();
 }
 

@@ -116,11 +116,13 @@ typedef struct elp_stats {
     int32_t world_size;        /* ranks sharing the column partition           */
     int32_t rank;
     int64_t col0, ncols;       /* this rank's column shard                     */
-    /* pricing-kernel timing (control.verbose & ELP_PROFILE_PRICE): every
-     * workgroup of the pricing kernel stamps s_memrealtime (the GPU's 100 MHz
-     * constant clock) at start and end; first start -> last end is summed per
-     * pricing pass that chose an entering variable.  With ELP_PROFILE_EVENTS
-     * instead: HIP events around every pricing launch of completed chunks. */
+    /* pricing-kernel timing.  control.verbose & ELP_PROFILE_EVENTS: HIP events
+     * bound to every pricing dispatch (hipExtLaunchKernelGGL: the launch's
+     * start / end timestamps, as a kernel trace reports them) of the chunks
+     * between host polls in which every launch priced.  ELP_PROFILE_PRICE
+     * instead: every workgroup of the pricing kernel stamps s_memrealtime (the
+     * GPU's 100 MHz constant clock) at start and end; first start -> last end
+     * per pass that chose an entering variable. */
     double price_seconds;      /* sum of timed pricing-kernel durations        */
     double price_timed_bytes;  /* algorithmic bytes of those launches          */
     int64_t price_timed_launches;
@@ -132,7 +134,8 @@ typedef struct elp_stats {
 } elp_stats;
 
 #define ELP_PROFILE_PRICE 2   /* elp_control.verbose bit: device-clock pricing timer */
-#define ELP_PROFILE_EVENTS 4  /* elp_control.verbose bit: HIP-event pricing timer  */
+#define ELP_PROFILE_EVENTS 4  /* elp_control.verbose bit: HIP events on each pricing dispatch */
+#define ELP_PROFILE_SAMPLE 8  /* elp_control.verbose bit: the same on every 8th chunk between polls */
 
 /* Fill *c with defaults. */
 void elp_default_control(elp_control* c);

@@ -6,8 +6,9 @@
  * so that the HIP kernels (also -ffp-contract=off, explicit fma) produce
  * the same bits.  Reduction orders follow DESIGN.md "Reduction order
  * contract":
- *   price  : PRICE_SPLIT (2) contiguous slot chunks, fma chain per chunk, then the
- *            partials added in chunk order starting from 0.0 (PRICE_SPLIT)
+ *   price  : PRICE_SPLIT (2) slot classes p = w (mod PRICE_SPLIT), an fma chain per
+ *            class in slot order, then the partials added in class order starting
+ *            from 0.0 (PRICE_SPLIT)
  *   wave   : 64 lane-strided fma chains + butterfly 32,16,..,1 (wave_dot):
  *            FTRAN / BTRAN / B^-1 rows, phase-1 c_S correction, phase-1 sum
  *   zchunk : chunks of 32 bump positions, fma chain, sequential sum
@@ -429,7 +430,6 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
         /* ---- pricing over structurals (AR sweep) and slacks ---- */
         const int64_t ny = s->ny;
         for (int64_t p = 0; p < ny; ++p) s->yy[p] = s->y[s->Yl[p]];
-        const int64_t L = (ny + PRICE_SPLIT - 1) / PRICE_SPLIT;
         if (ctl->price_mode == 1) {
             /* column chains (CSC): the sum lands in part[0], part[1..] stay 0
              * and add exactly */
@@ -447,8 +447,8 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
         for (int w = 0; w < PRICE_SPLIT; ++w) {
             double* pw = s->part + (size_t)w * (size_t)n;
             for (int64_t j = 0; j < n; ++j) pw[j] = 0.0;
-            const int64_t p0 = (int64_t)w * L, p1 = p0 + L < ny ? p0 + L : ny;
-            for (int64_t p = p0; p < p1; ++p) {
+            /* chunk w = the slots p = w (mod PRICE_SPLIT), in slot order */
+            for (int64_t p = w; p < ny; p += PRICE_SPLIT) {
                 const double yp = s->yy[p];
                 const double* row = s->AR + (size_t)p * (size_t)n;
                 for (int64_t j = 0; j < n; ++j) pw[j] = fma(row[j], yp, pw[j]);

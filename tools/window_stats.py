@@ -35,7 +35,7 @@ def main(trace, bench_json):
     kp = kern.get("k_price", {})
     out = {"timed_solves": K, "price_launches_per_solve": L, "window_wall_ms": wall / 1e6,
            "k_price_avg_us_rocprof": kp.get("avg_us"),
-           "k_price_avg_us_bench_device_clock": b["roofline"]["avg_launch_us"],
+           "k_price_avg_us_bench": b["roofline"]["avg_launch_us"], "bench_timer": b["roofline"].get("timer"),
            "bytes_per_launch": b["roofline"]["bytes_per_launch"],
            "frac_from_rocprof": (b["roofline"]["bytes_per_launch"] / (kp["avg_us"] * 1e-6) / 8e12) if kp else None,
            "kernels": kern}
