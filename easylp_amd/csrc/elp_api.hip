@@ -98,6 +98,9 @@ struct elp_handle {
     std::vector<elp::ThreadRank> tranks;
     std::vector<double*> peer_A;  // elp_load_dense_device: A copied to the other devices
     size_t peer_A_count = 0;
+    // scaling (elp_control.scaling): the solver works on A~ = 2^srow A 2^scol
+    // (exponents per row and per GLOBAL column; empty: unscaled)
+    std::vector<int32_t> srow_h, scol_h;
 };
 
 extern "C" void elp_default_control(elp_control* c) {
@@ -115,7 +118,7 @@ extern "C" void elp_default_control(elp_control* c) {
     c->verbose = 0;
     c->pricing = ELP_PRICE_DEVEX;
     c->ngpu = 1;
-    c->scaling = 0;
+    c->scaling = ELP_SCALE_GEOMETRIC | ELP_SCALE_EQUILIBRATE;  // lp_solve's default scaling
     c->tol_singular = 1e-13;
     c->mailbox_timeout = 2.0;
 }
@@ -474,6 +477,117 @@ static int any_rank(elp_handle* h, int v, int* out) {
     return 0;
 }
 
+static bool scaling_on(const elp_handle* h) { return (h->ctl.scaling & (ELP_SCALE_GEOMETRIC | ELP_SCALE_EQUILIBRATE)) != 0; }
+static double unscale_col(const elp_handle* h, double v, int64_t j, int sgn) {
+    return h->scol_h.empty() ? v : std::ldexp(v, sgn * h->scol_h[(size_t)j]);
+}
+static double unscale_row(const elp_handle* h, double v, int64_t i, int sgn) {
+    return h->srow_h.empty() ? v : std::ldexp(v, sgn * h->srow_h[(size_t)i]);
+}
+
+// Scale the m x ncols column-major A (all N columns: one GPU or replicated) in
+// place on the device (launch_scale_*; oracle/elp_oracle.c scale_factors) and
+// keep the exponents on the host.
+static int scale_dense(elp_handle* h, double* A, int64_t ncols) {
+    h->srow_h.clear();
+    h->scol_h.clear();
+    if (!scaling_on(h)) return 0;
+    const int m = (int)h->m;
+    int32_t *rho = nullptr, *gam = nullptr, *rmn = nullptr, *rmx = nullptr, *chg = nullptr;
+    hipError_t e = dalloc(&rho, (size_t)std::max(m, 1));
+    if (e == hipSuccess) e = dalloc(&gam, (size_t)ncols);
+    if (e == hipSuccess) e = dalloc(&rmn, (size_t)std::max(m, 1));
+    if (e == hipSuccess) e = dalloc(&rmx, (size_t)std::max(m, 1));
+    if (e == hipSuccess) e = dalloc(&chg, 1);
+    if (e == hipSuccess) e = launch_scale_init(m, ncols, rho, gam, rmn, rmx, h->st);
+    if (h->ctl.scaling & ELP_SCALE_GEOMETRIC)
+        for (int pass = 0; pass < SCALE_PASSES && e == hipSuccess; ++pass) {
+            int32_t moved = 0;
+            e = hipMemsetAsync(chg, 0, sizeof(int32_t), h->st);
+            if (e == hipSuccess) e = launch_scale_rows(m, ncols, A, gam, rmn, rmx, h->st);
+            if (e == hipSuccess) e = launch_scale_row_final(m, rmn, rmx, rho, chg, h->st);
+            if (e == hipSuccess) e = launch_scale_cols(m, ncols, A, rho, gam, 0, chg, h->st);
+            if (e == hipSuccess) e = hipMemcpyAsync(&moved, chg, sizeof(int32_t), hipMemcpyDeviceToHost, h->st);
+            if (e == hipSuccess) e = hipStreamSynchronize(h->st);
+            if (!moved) break;
+        }
+    if (e == hipSuccess && (h->ctl.scaling & ELP_SCALE_EQUILIBRATE))
+        e = launch_scale_cols(m, ncols, A, rho, gam, 1, chg, h->st);
+    if (e == hipSuccess) e = launch_scale_apply(m, ncols, A, rho, gam, h->st);
+    h->srow_h.assign((size_t)m, 0);
+    h->scol_h.assign((size_t)ncols, 0);
+    if (e == hipSuccess && m)
+        e = hipMemcpyAsync(h->srow_h.data(), rho, (size_t)m * sizeof(int32_t), hipMemcpyDeviceToHost, h->st);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(h->scol_h.data(), gam, (size_t)ncols * sizeof(int32_t), hipMemcpyDeviceToHost, h->st);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->st);
+    for (int32_t* p : {rho, gam, rmn, rmx, chg})
+        if (p) (void)hipFree(p);
+    if (e != hipSuccess) return fail(ELP_E_HIP, std::string("scaling: ") + hipGetErrorString(e));
+    return 0;
+}
+
+// The same factors from CSC arrays on the host (nonzeros only: explicit zeros
+// are skipped exactly as the dense kernels skip zero entries); val is scaled in place.
+static int ilogb_i(double a) { return std::ilogb(a); }
+static int floor_half_h(int v) { return v >= 0 ? v / 2 : -((1 - v) / 2); }
+static void scale_csc(elp_handle* h, const int64_t* cp, const int32_t* ri, double* val) {
+    h->srow_h.clear();
+    h->scol_h.clear();
+    if (!scaling_on(h)) return;
+    const int64_t m = h->m, n = h->n;
+    constexpr int EMN = 0x3fffffff, EMX = -0x3fffffff;
+    std::vector<int32_t> rho((size_t)m, 0), gam((size_t)n, 0);
+    auto col_pass = [&](bool equil) {
+        bool changed = false;
+        for (int64_t j = 0; j < n; ++j) {
+            int mn = EMN, mx = EMX;
+            for (int64_t t = cp[j]; t < cp[j + 1]; ++t) {
+                if (val[t] == 0.0) continue;
+                const int e = ilogb_i(val[t]) + rho[(size_t)ri[t]];
+                mn = std::min(mn, e);
+                mx = std::max(mx, e);
+            }
+            const int g = mx == EMX ? 0 : equil ? -(mx + 1) : -floor_half_h(mn + mx);
+            if (g != gam[(size_t)j]) {
+                gam[(size_t)j] = g;
+                changed = true;
+            }
+        }
+        return changed;
+    };
+    auto row_pass = [&]() {
+        std::vector<int> mn((size_t)m, EMN), mx((size_t)m, EMX);
+        for (int64_t j = 0; j < n; ++j)
+            for (int64_t t = cp[j]; t < cp[j + 1]; ++t) {
+                if (val[t] == 0.0) continue;
+                const int e = ilogb_i(val[t]) + gam[(size_t)j];
+                const size_t i = (size_t)ri[t];
+                mn[i] = std::min(mn[i], e);
+                mx[i] = std::max(mx[i], e);
+            }
+        bool changed = false;
+        for (int64_t i = 0; i < m; ++i) {
+            const int r = mx[(size_t)i] == EMX ? 0 : -floor_half_h(mn[(size_t)i] + mx[(size_t)i]);
+            if (r != rho[(size_t)i]) {
+                rho[(size_t)i] = r;
+                changed = true;
+            }
+        }
+        return changed;
+    };
+    if (h->ctl.scaling & ELP_SCALE_GEOMETRIC)
+        for (int pass = 0; pass < SCALE_PASSES; ++pass) {
+            const bool ch = row_pass();
+            if (!(col_pass(false) | ch)) break;
+        }
+    if (h->ctl.scaling & ELP_SCALE_EQUILIBRATE) col_pass(true);
+    for (int64_t j = 0; j < n; ++j)
+        for (int64_t t = cp[j]; t < cp[j + 1]; ++t) val[t] = std::ldexp(val[t], rho[(size_t)ri[t]] + gam[(size_t)j]);
+    h->srow_h = std::move(rho);
+    h->scol_h = std::move(gam);
+}
+
 // common tail of elp_load_*: bounds, rows, control block, phase decision
 static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, const double* obj,
                        const double* lo, const double* up, int32_t maximize) {
@@ -496,12 +610,18 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
         h->is_int.clear();
         h->mip = false;
     }
-    // host-side staging of the small vectors (local column shard)
-    std::vector<double> lo_h(nl), up_h(nl), slb(m), sub(m);
+    // host-side staging of the small vectors (local column shard), scaled:
+    // bounds by 2^-scol, costs by 2^scol, rhs by 2^srow (infinite values first
+    // become +-inf, so they stay infinite)
+    const double BIG = h->ctl.infinity;
+    auto fin = [&](double v) { return v <= -BIG ? -HUGE_VAL : v >= BIG ? HUGE_VAL : v; };
+    std::vector<double> lo_h(nl), up_h(nl), slb(m), sub(m), rhs_s(m), obj_s(n);
     for (int64_t j = 0; j < nl; ++j) {
-        lo_h[j] = lo ? lo[n0 + j] : 0.0;
-        up_h[j] = up ? up[n0 + j] : HUGE_VAL;
+        lo_h[j] = unscale_col(h, fin(lo ? lo[n0 + j] : 0.0), n0 + j, -1);
+        up_h[j] = unscale_col(h, fin(up ? up[n0 + j] : HUGE_VAL), n0 + j, -1);
     }
+    for (int64_t i = 0; i < m; ++i) rhs_s[i] = unscale_row(h, fin(rhs[i]), i, 1);
+    for (int64_t j = 0; j < n; ++j) obj_s[j] = unscale_col(h, obj[j], j, 1);
     for (int64_t i = 0; i < m; ++i) {
         slb[i] = dir[i] == ELP_GE ? -HUGE_VAL : 0.0;
         sub[i] = dir[i] == ELP_LE ? HUGE_VAL : 0.0;
@@ -513,12 +633,12 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
     HIPCHK(hipMemcpyAsync(dlo, lo_h.data(), nl * sizeof(double), hipMemcpyHostToDevice, h->st));
     HIPCHK(hipMemcpyAsync(dup, up_h.data(), nl * sizeof(double), hipMemcpyHostToDevice, h->st));
     if (m) {
-        HIPCHK(hipMemcpyAsync(drhs, rhs, m * sizeof(double), hipMemcpyHostToDevice, h->st));
+        HIPCHK(hipMemcpyAsync(drhs, rhs_s.data(), m * sizeof(double), hipMemcpyHostToDevice, h->st));
         HIPCHK(hipMemcpyAsync(d.lb + nl, slb.data(), m * sizeof(double), hipMemcpyHostToDevice, h->st));
         HIPCHK(hipMemcpyAsync(d.ub + nl, sub.data(), m * sizeof(double), hipMemcpyHostToDevice, h->st));
     }
-    HIPCHK(hipMemcpyAsync(d.obj, obj + n0, nl * sizeof(double), hipMemcpyHostToDevice, h->st));
-    HIPCHK(hipMemcpyAsync(d.objg, obj, n * sizeof(double), hipMemcpyHostToDevice, h->st));
+    HIPCHK(hipMemcpyAsync(d.obj, obj_s.data() + n0, nl * sizeof(double), hipMemcpyHostToDevice, h->st));
+    HIPCHK(hipMemcpyAsync(d.objg, obj_s.data(), n * sizeof(double), hipMemcpyHostToDevice, h->st));
     DevCtl c{};
     c.status = ST_RUN;
     c.phase = 1;
@@ -626,6 +746,8 @@ static int prep_load(elp_handle* h, bool csc = false) {
                     (h->ctl.replicate == 1 || (h->ctl.replicate == 0 && abytes <= 64.0 * (1ull << 30)));
     if (h->comm.p2p && !h->replicated)
         return fail(ELP_E_UNSUPPORTED, "xGMI mailbox exchange needs A replicated on every rank");
+    if (scaling_on(h) && h->comm.kind != 0 && !h->replicated)
+        return fail(ELP_E_UNSUPPORTED, "scaling needs all of A on every rank (elp_control.replicate) or scaling = 0");
     return alloc_all(h);
 }
 
@@ -643,6 +765,8 @@ extern "C" int elp_load_dense(elp_handle* h, const double* A, const int32_t* dir
     if (cnt)
         HIPCHK(hipMemcpyAsync(h->A_owned, A + (size_t)c0 * (size_t)h->m, cnt * sizeof(double),
                               hipMemcpyHostToDevice, h->st));
+    rc = scale_dense(h, h->A_owned, nc);
+    if (rc) return rc;
     h->d.A = h->A_owned + (size_t)(h->col0 - c0) * (size_t)h->m;
     h->d.Afull = h->replicated ? h->A_owned : nullptr;
     rc = load_common(h, dir, rhs, obj, lo, up, maximize);
@@ -680,6 +804,17 @@ extern "C" int elp_load_dense_device(elp_handle* h, const double* dA, const int3
         return fail(ELP_E_ARG, "elp_load_dense_device: NULL input");
     int rc = prep_load(h);
     if (rc) return rc;
+    if (scaling_on(h)) {  // the caller's A is read-only: scale a copy of it
+        const size_t cnt = (size_t)h->m * (size_t)h->n;
+        HIPCHK(dalloc(&h->A_owned, cnt));
+        if (cnt) HIPCHK(hipMemcpyAsync(h->A_owned, dA, cnt * sizeof(double), hipMemcpyDeviceToDevice, h->st));
+        rc = scale_dense(h, h->A_owned, h->n);
+        if (rc) return rc;
+        dA = h->A_owned;
+    } else {
+        h->srow_h.clear();
+        h->scol_h.clear();
+    }
     h->d.A = dA + (size_t)h->col0 * (size_t)h->m;
     h->d.Afull = h->replicated ? dA : nullptr;
     rc = load_common(h, dir, rhs, obj, lo, up, maximize);
@@ -710,6 +845,9 @@ extern "C" int elp_load_csc(elp_handle* h, const int64_t* colptr, const int32_t*
     }
     int rc = prep_load(h, true);
     if (rc) return rc;
+    std::vector<double> sval(val, val + nnz);  // scaled in place (scaling on)
+    scale_csc(h, colptr, rowind, sval.data());
+    val = sval.data();
     // CSR copy: a counting sort by row keeps the columns ascending within a row
     std::vector<int64_t> rp((size_t)m + 1, 0);
     for (int64_t t = 0; t < nnz; ++t) rp[(size_t)rowind[t] + 1]++;
@@ -784,6 +922,8 @@ extern "C" int elp_load_generated(elp_handle* h, uint64_t seed) {
     HIPCHK(hipStreamSynchronize(h->st));
     (void)hipFree(db);
     (void)hipFree(dc);
+    rc = scale_dense(h, h->A_owned, nc);
+    if (rc) return rc;
     h->d.A = h->A_owned + (size_t)(h->col0 - c0) * (size_t)m;
     h->d.Afull = h->replicated ? h->A_owned : nullptr;
     rc = load_common(h, dir.data(), b.data(), c.data(), lo.data(), up.data(), 1);
@@ -1312,6 +1452,7 @@ extern "C" int elp_get_solution(elp_handle* h, double* objval, double* x, double
     (void)nl;
     const DevCtl& c = *h->hctl;
     const double BIG = h->ctl.infinity;
+    for (int64_t j = 0; j < n; ++j) xs[j] = unscale_col(h, xs[j], j, 1);  // (exact)
     const bool unb = h->done && h->final_status == ELP_UNBOUNDED;
     // the unbounded variable's global id (shard-local q -> global)
     const int64_t uvar = unb ? (int64_t)c.unb_var : -1;  // global id
@@ -1332,8 +1473,7 @@ extern "C" int elp_get_solution(elp_handle* h, double* objval, double* x, double
     if (y && m) {
         HIPCHK(hipMemcpyAsync(y, h->d.y, m * sizeof(double), hipMemcpyDeviceToHost, h->st));
         HIPCHK(hipStreamSynchronize(h->st));
-        if (h->maximize)
-            for (int64_t i = 0; i < m; ++i) y[i] = -y[i];
+        for (int64_t i = 0; i < m; ++i) y[i] = unscale_row(h, h->maximize ? -y[i] : y[i], i, 1);
     }
     if (basis && m) {
         std::vector<int32_t> cover(m), Sl(std::max(c.k, 1));
@@ -1413,9 +1553,10 @@ extern "C" int elp_sensitivity(elp_handle* h, double* objfrom, double* objtill, 
     auto clip = [&](double v) { return v <= -INF ? -BIG : v >= INF ? BIG : v; };
     const bool mx = h->maximize != 0;
     const double sg = mx ? -1.0 : 1.0;
+    // (the assembly runs on the scaled problem; every output is unscaled)
     if (duals) {
-        for (int64_t i = 0; i < m; ++i) duals[i] = sg * y[i];
-        for (int64_t j = 0; j < n; ++j) duals[m + j] = sg * dr[j];
+        for (int64_t i = 0; i < m; ++i) duals[i] = unscale_row(h, sg * y[i], i, 1);
+        for (int64_t j = 0; j < n; ++j) duals[m + j] = unscale_col(h, sg * dr[j], j, -1);
     }
     std::vector<int> spos(n, -1);
     for (int p = 0; p < k; ++p) spos[Sl[p]] = p;
@@ -1434,8 +1575,8 @@ extern "C" int elp_sensitivity(elp_handle* h, double* objfrom, double* objtill, 
         } else {
             lo = hi = c;
         }
-        if (objfrom) objfrom[j] = clip(mx ? -hi : lo);
-        if (objtill) objtill[j] = clip(mx ? -lo : hi);
+        if (objfrom) objfrom[j] = clip(unscale_col(h, mx ? -hi : lo, j, -1));
+        if (objtill) objtill[j] = clip(unscale_col(h, mx ? -lo : hi, j, -1));
     }
     for (int64_t i = 0; i < m && (dualsfrom || dualstill); ++i) {
         double lo = -INF, hi = INF;
@@ -1453,8 +1594,8 @@ extern "C" int elp_sensitivity(elp_handle* h, double* objfrom, double* objtill, 
             lo = bi + o4[2 * (size_t)k + c];
             hi = bi + o4[3 * (size_t)k + c];
         }
-        if (dualsfrom) dualsfrom[i] = clip(lo);
-        if (dualstill) dualstill[i] = clip(hi);
+        if (dualsfrom) dualsfrom[i] = clip(unscale_row(h, lo, i, -1));
+        if (dualstill) dualstill[i] = clip(unscale_row(h, hi, i, -1));
     }
     for (int64_t j = 0; j < n; ++j) {
         if (dualsfrom) dualsfrom[m + j] = -BIG;

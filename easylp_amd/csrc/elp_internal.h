@@ -249,6 +249,18 @@ hipError_t launch_btran_exact(const Dev& d, int k, hipStream_t st);  // phase-2 
 hipError_t launch_refactor_primal(const Dev& d, int k, hipStream_t st);  // needs ract
 hipError_t launch_nzlist(const Dev& d, hipStream_t st);
 hipError_t launch_transpose_A(const Dev& d, hipStream_t st);
+// scaling (elp_control.scaling): exponents rho (m rows), gamma (ncols columns);
+// rmn / rmx: per-row min / max work (m each); changed: set when a pass moved a factor
+constexpr int SCALE_PASSES = 20;  // geometric row + column passes at most
+hipError_t launch_scale_init(int m, int64_t ncols, int32_t* rho, int32_t* gam, int32_t* rmn, int32_t* rmx,
+                             hipStream_t st);
+hipError_t launch_scale_rows(int m, int64_t ncols, const double* A, const int32_t* gam, int32_t* rmn, int32_t* rmx,
+                             hipStream_t st);
+hipError_t launch_scale_row_final(int m, int32_t* rmn, int32_t* rmx, int32_t* rho, int32_t* changed, hipStream_t st);
+hipError_t launch_scale_cols(int m, int64_t ncols, const double* A, const int32_t* rho, int32_t* gam, int equilibrate,
+                             int32_t* changed, hipStream_t st);
+hipError_t launch_scale_apply(int m, int64_t ncols, double* A, const int32_t* rho, const int32_t* gam,
+                              hipStream_t st);
 hipError_t launch_phase2(const Dev& d, hipStream_t st);  // (includes devex_reset)
 hipError_t launch_devex_reset(const Dev& d, hipStream_t st);  // weights 1, dv_valid 0
 // sensitivity (final basis, k = bump dimension): dred[n] reduced costs; TR

@@ -411,6 +411,120 @@ __global__ void __launch_bounds__(256) k_transpose_A(Dev d) {
     }
 }
 
+// ============================================================== scaling
+// lp_solve-style scaling (elp_control.scaling; oracle scale_factors): every
+// factor is a power of two, so the scaled problem is exact and unscaling is
+// exact.  On the integer exponents e_ij = ilogb|a_ij| of the nonzeros,
+// geometric passes set row then column exponents to -floor((min + max) / 2) of
+// the currently scaled entries (lp_solve's sqrt(min * max) in the log domain);
+// equilibrate sets each column's to -(max + 1), so its largest scaled |a| lies
+// in [1/2, 1).  Integer min / max: identical on the GPU and the oracle.
+DEV int floor_half(int s) { return s >= 0 ? s / 2 : -((1 - s) / 2); }
+constexpr int SCALE_EMPTY_MIN = 0x3fffffff, SCALE_EMPTY_MAX = -0x3fffffff;
+
+// column pass: one workgroup per column (grid-stride), rows strided by thread
+__global__ void __launch_bounds__(256) k_scale_col(int m, int64_t ncols, const double* __restrict__ A,
+                                                   const int32_t* __restrict__ rho, int32_t* __restrict__ gam,
+                                                   int equilibrate, int32_t* changed) {
+    __shared__ int smn[4], smx[4];
+    for (int64_t j = blockIdx.x; j < ncols; j += gridDim.x) {
+        const double* col = A + (size_t)j * (size_t)m;
+        int mn = SCALE_EMPTY_MIN, mx = SCALE_EMPTY_MAX;
+        for (int i = threadIdx.x; i < m; i += 256) {
+            const double a = col[i];
+            if (a != 0.0) {
+                const int e = ilogb(a) + rho[i];
+                mn = min(mn, e);
+                mx = max(mx, e);
+            }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            mn = min(mn, __shfl_xor(mn, off));
+            mx = max(mx, __shfl_xor(mx, off));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            smn[threadIdx.x >> 6] = mn;
+            smx[threadIdx.x >> 6] = mx;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int w = 1; w < 4; ++w) {
+                mn = min(mn, smn[w]);
+                mx = max(mx, smx[w]);
+            }
+            int g = 0;
+            if (mx != SCALE_EMPTY_MAX) g = equilibrate ? -(mx + 1) : -floor_half(mn + mx);
+            if (g != gam[j]) {
+                gam[j] = g;
+                *changed = 1;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// row pass, part 1: thread = row, a chunk of SCALE_RCOLS columns per workgroup
+// row; per-row min / max of e_ij + gamma_j into rmn / rmx (integer atomics)
+constexpr int SCALE_RCOLS = 512;
+__global__ void __launch_bounds__(256) k_scale_row_part(int m, int64_t ncols, const double* __restrict__ A,
+                                                        const int32_t* __restrict__ gam, int32_t* rmn,
+                                                        int32_t* rmx) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    const int64_t j0 = (int64_t)blockIdx.y * SCALE_RCOLS;
+    const int64_t j1 = j0 + SCALE_RCOLS < ncols ? j0 + SCALE_RCOLS : ncols;
+    int mn = SCALE_EMPTY_MIN, mx = SCALE_EMPTY_MAX;
+    for (int64_t j = j0; j < j1; ++j) {
+        const double a = A[(size_t)j * (size_t)m + i];
+        if (a != 0.0) {
+            const int e = ilogb(a) + gam[j];
+            mn = min(mn, e);
+            mx = max(mx, e);
+        }
+    }
+    if (mx != SCALE_EMPTY_MAX) {
+        atomicMin(&rmn[i], mn);
+        atomicMax(&rmx[i], mx);
+    }
+}
+
+// row pass, part 2: rho_i from the row's min / max
+__global__ void k_scale_row_final(int m, int32_t* rmn, int32_t* rmx, int32_t* rho, int32_t* changed) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    const int mn = rmn[i], mx = rmx[i];
+    const int r = mx == SCALE_EMPTY_MAX ? 0 : -floor_half(mn + mx);
+    if (r != rho[i]) {
+        rho[i] = r;
+        *changed = 1;
+    }
+    rmn[i] = SCALE_EMPTY_MIN;  // ready for the next pass
+    rmx[i] = SCALE_EMPTY_MAX;
+}
+
+__global__ void k_scale_init(int m, int64_t ncols, int32_t* rho, int32_t* gam, int32_t* rmn, int32_t* rmx) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t < m) {
+        rho[t] = 0;
+        rmn[t] = SCALE_EMPTY_MIN;
+        rmx[t] = SCALE_EMPTY_MAX;
+    }
+    if (t < ncols) gam[t] = 0;
+}
+
+// A_ij *= 2^(rho_i + gamma_j) (exact)
+__global__ void k_scale_apply(int m, int64_t ncols, double* __restrict__ A, const int32_t* __restrict__ rho,
+                              const int32_t* __restrict__ gam) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    const int r = rho[i];
+    for (int64_t j = blockIdx.y; j < ncols; j += gridDim.y) {
+        double* a = A + (size_t)j * (size_t)m + i;
+        *a = ldexp(*a, r + gam[j]);
+    }
+}
+
 // element (row p, column j) of the tile-major AR
 DEV size_t ar_at(const Dev& d, int64_t p, int64_t j) {
     return ((size_t)(j / TILE_COLS) * (size_t)d.arcap + (size_t)p) * TILE_COLS + (size_t)(j % TILE_COLS);
@@ -2728,6 +2842,39 @@ hipError_t launch_fill_AR(const Dev& d, hipStream_t st) {
 hipError_t launch_ar_relayout(const Dev& d, const double* old_ar, int64_t old_cap, int rows,
                               hipStream_t st) {
     if (rows > 0) k_ar_relayout<<<2048, 256, 0, st>>>(d, old_ar, old_cap, rows);
+    return hipGetLastError();
+}
+
+hipError_t launch_scale_init(int m, int64_t ncols, int32_t* rho, int32_t* gam, int32_t* rmn, int32_t* rmx,
+                             hipStream_t st) {
+    const int64_t mx = m > ncols ? m : ncols;
+    k_scale_init<<<cdiv(mx > 0 ? mx : 1, 256), 256, 0, st>>>(m, ncols, rho, gam, rmn, rmx);
+    return hipGetLastError();
+}
+hipError_t launch_scale_rows(int m, int64_t ncols, const double* A, const int32_t* gam, int32_t* rmn, int32_t* rmx,
+                             hipStream_t st) {
+    if (m > 0 && ncols > 0)
+        k_scale_row_part<<<dim3(cdiv(m, 256), cdiv(ncols, SCALE_RCOLS)), 256, 0, st>>>(m, ncols, A, gam, rmn, rmx);
+    return hipGetLastError();
+}
+hipError_t launch_scale_row_final(int m, int32_t* rmn, int32_t* rmx, int32_t* rho, int32_t* changed, hipStream_t st) {
+    if (m > 0) k_scale_row_final<<<cdiv(m, 256), 256, 0, st>>>(m, rmn, rmx, rho, changed);
+    return hipGetLastError();
+}
+hipError_t launch_scale_cols(int m, int64_t ncols, const double* A, const int32_t* rho, int32_t* gam, int equilibrate,
+                             int32_t* changed, hipStream_t st) {
+    if (m > 0 && ncols > 0) {
+        const unsigned g = (unsigned)(ncols < 65536 ? ncols : 65536);
+        k_scale_col<<<g, 256, 0, st>>>(m, ncols, A, rho, gam, equilibrate, changed);
+    }
+    return hipGetLastError();
+}
+hipError_t launch_scale_apply(int m, int64_t ncols, double* A, const int32_t* rho, const int32_t* gam,
+                              hipStream_t st) {
+    if (m > 0 && ncols > 0) {
+        dim3 g(cdiv(m, 256), (unsigned)(ncols < 65535 ? ncols : 65535));
+        k_scale_apply<<<g, 256, 0, st>>>(m, ncols, A, rho, gam);
+    }
     return hipGetLastError();
 }
 

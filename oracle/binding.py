@@ -34,7 +34,7 @@ class OrcControl(ctypes.Structure):
         ("refactor_mode", ctypes.c_int32),
         ("price_mode", ctypes.c_int32),
         ("price_rule", ctypes.c_int32),
-        ("pad0", ctypes.c_int32),
+        ("scaling", ctypes.c_int32),
         ("tol_singular", ctypes.c_double),
     ]
 
@@ -96,6 +96,9 @@ def load():
         ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, P(OrcControl), ctypes.c_void_p, ctypes.c_void_p,
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, P(OrcStats),
     ]
+    lib.orc_scale_factors.restype = None
+    lib.orc_scale_factors.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
+                                      ctypes.c_void_p, ctypes.c_void_p]
     lib.orc_generate_rows.restype = None
     lib.orc_generate_rows.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                                       ctypes.c_int64, ctypes.c_void_p]
@@ -228,3 +231,14 @@ def generate_rows(seed, m, n, rows):
     out = np.zeros((len(rows), n))
     lib.orc_generate_rows(seed, m, n, rows.ctypes.data, len(rows), out.ctypes.data)
     return out
+
+
+def scale_factors(A, mode=4 | 64):
+    """(rho, gamma): the integer scaling exponents the solver applies to A."""
+    lib = load()
+    A = np.asfortranarray(np.asarray(A, dtype=np.float64))
+    m, n = A.shape
+    rho = np.zeros(max(m, 1), np.int32)
+    gam = np.zeros(n, np.int32)
+    lib.orc_scale_factors(m, n, A.ctypes.data, mode, rho.ctypes.data, gam.ctypes.data)
+    return rho[:m], gam

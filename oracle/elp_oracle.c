@@ -89,6 +89,12 @@ void orc_generate_dense(uint64_t seed, int64_t m, int64_t n, int64_t col0, int64
     }
 }
 
+/* scaling exponents of a dense column-major A (test access to scale_factors) */
+static void scale_factors_dense(int64_t m, int64_t n, const double* A, int mode, int32_t* rho, int32_t* gam);
+void orc_scale_factors(int64_t m, int64_t n, const double* A, int32_t mode, int32_t* rho, int32_t* gam) {
+    scale_factors_dense(m, n, A, mode, rho, gam);
+}
+
 void orc_generate_rows(uint64_t seed, int64_t m, int64_t n, const int64_t* rows, int64_t nrows,
                        double* out) {
     (void)n;
@@ -105,6 +111,10 @@ typedef struct {
     int64_t m, n, nv;
     const double* A; /* column-major m x n; NULL: generated on the fly (gen_seed) */
     uint64_t gen_seed;
+    int32_t *srow, *scol; /* scaling exponents (NULL: unscaled): the solver sees
+                             a_ij * 2^(srow_i + scol_j) */
+    int a_scaled;         /* A (a scaled copy) already holds those values   */
+    double* A_copy;       /* that copy (freed at the end)                   */
     double* b;
     double *lb, *ub, *cost, *xval;
     int8_t* vstat;
@@ -136,18 +146,106 @@ typedef struct {
     double* colbuf;     /* m: a generated column (Acol)                     */
 } orc_t;
 
+/* v * 2^(sgn * exponent) of column j / row i (scaling; exact, inf stays inf) */
+#define SC_COL(v, j, sgn) (s->scol ? ldexp((v), (sgn) * s->scol[j]) : (v))
+#define SC_ROW(v, i, sgn) (s->srow ? ldexp((v), (sgn) * s->srow[i]) : (v))
+
 static double* dalloc(size_t n) { return (double*)calloc(n ? n : 1, sizeof(double)); }
 static int64_t* ialloc(size_t n) { return (int64_t*)calloc(n ? n : 1, sizeof(int64_t)); }
 
-static inline double Aat(const orc_t* s, int64_t i, int64_t j) {
+static inline double Araw(const orc_t* s, int64_t i, int64_t j) {
     if (!s->A) return gen_u01(s->gen_seed, 0, (uint64_t)i + (uint64_t)j * (uint64_t)s->m);
     return s->A[(size_t)j * (size_t)s->m + (size_t)i];
 }
-/* column j of A (in place, or generated into buf) */
+/* the matrix the simplex works on: A scaled (exactly: powers of 2) */
+static inline double Aat(const orc_t* s, int64_t i, int64_t j) {
+    const double a = Araw(s, i, j);
+    return s->srow && !s->a_scaled ? ldexp(a, s->srow[i] + s->scol[j]) : a;
+}
+/* column j of the scaled A (in place when materialised, else built in buf) */
 static inline const double* Acol(const orc_t* s, int64_t j, double* buf) {
-    if (s->A) return &s->A[(size_t)j * (size_t)s->m];
+    if (s->A && (!s->srow || s->a_scaled)) return &s->A[(size_t)j * (size_t)s->m];
     for (int64_t i = 0; i < s->m; ++i) buf[i] = Aat(s, i, j);
     return buf;
+}
+
+/* ------------------------------------------------------------------ */
+/* scaling (the HIP side's k_scale_*): on the integer exponents            */
+/* e_ij = ilogb|a_ij| of the nonzeros, geometric passes (at most 20, row    */
+/* pass then column pass, until no factor moves) set each exponent to       */
+/* -floor((min + max) / 2) of the currently scaled entries (lp_solve's      */
+/* SCALE_GEOMETRIC, sqrt(min * max), in the log domain); equilibrate sets    */
+/* each column's to -(max + 1) so its largest |a| lies in [1/2, 1)          */
+/* (SCALE_EQUILIBRATE).  lp_solve's own scaling loop is not in the          */
+/* reference: this arithmetic is the contract both sides implement.         */
+#define SCALE_PASSES 20
+#define SC_EMPTY_MIN 0x3fffffff
+#define SC_EMPTY_MAX (-0x3fffffff)
+static int floor_half(int v) { return v >= 0 ? v / 2 : -((1 - v) / 2); }
+static int col_pass(const orc_t* s, int32_t* rho, int32_t* gam, int equilibrate) {
+    int changed = 0;
+    for (int64_t j = 0; j < s->n; ++j) {
+        int mn = SC_EMPTY_MIN, mx = SC_EMPTY_MAX;
+        for (int64_t i = 0; i < s->m; ++i) {
+            const double a = Araw(s, i, j);
+            if (a == 0.0) continue;
+            const int e = ilogb(a) + rho[i];
+            if (e < mn) mn = e;
+            if (e > mx) mx = e;
+        }
+        const int g = mx == SC_EMPTY_MAX ? 0 : equilibrate ? -(mx + 1) : -floor_half(mn + mx);
+        if (g != gam[j]) {
+            gam[j] = g;
+            changed = 1;
+        }
+    }
+    return changed;
+}
+static int row_pass(const orc_t* s, int32_t* rho, const int32_t* gam) {
+    const int64_t m = s->m, n = s->n;
+    int* mn = (int*)malloc((size_t)(m > 0 ? m : 1) * sizeof(int));
+    int* mx = (int*)malloc((size_t)(m > 0 ? m : 1) * sizeof(int));
+    for (int64_t i = 0; i < m; ++i) {
+        mn[i] = SC_EMPTY_MIN;
+        mx[i] = SC_EMPTY_MAX;
+    }
+    for (int64_t j = 0; j < n; ++j)
+        for (int64_t i = 0; i < m; ++i) {
+            const double a = Araw(s, i, j);
+            if (a == 0.0) continue;
+            const int e = ilogb(a) + gam[j];
+            if (e < mn[i]) mn[i] = e;
+            if (e > mx[i]) mx[i] = e;
+        }
+    int changed = 0;
+    for (int64_t i = 0; i < m; ++i) {
+        const int r = mx[i] == SC_EMPTY_MAX ? 0 : -floor_half(mn[i] + mx[i]);
+        if (r != rho[i]) {
+            rho[i] = r;
+            changed = 1;
+        }
+    }
+    free(mn);
+    free(mx);
+    return changed;
+}
+static void scale_factors(const orc_t* s, int mode, int32_t* rho, int32_t* gam) {
+    for (int64_t i = 0; i < s->m; ++i) rho[i] = 0;
+    for (int64_t j = 0; j < s->n; ++j) gam[j] = 0;
+    if (mode & 4)
+        for (int pass = 0; pass < SCALE_PASSES; ++pass) {
+            const int ch = row_pass(s, rho, gam);
+            if (!(col_pass(s, rho, gam, 0) | ch)) break;
+        }
+    if (mode & 64) col_pass(s, rho, gam, 1);
+}
+static void scale_factors_dense(int64_t m, int64_t n, const double* A, int mode, int32_t* rho, int32_t* gam) {
+    orc_t t;
+    memset(&t, 0, sizeof t);
+    t.m = m;
+    t.n = n;
+    t.A = A;
+    scale_factors(&t, mode, rho, gam);
 }
 /* ascending list of nonbasic structurals with x_j != 0 (row activities) */
 static int64_t nz_nonbasic(const orc_t* s, int64_t* list) {
@@ -803,8 +901,9 @@ static void sensitivity(orc_t* s, const orc_control* ctl, const int32_t* dir, in
     }
     for (int64_t i = 0; i < m; ++i) d[n + i] = s->vstat[n + i] == VS_BASIC ? 0.0 : -s->y[i];
     const double sg = maximize ? -1.0 : 1.0;
-    for (int64_t i = 0; i < m; ++i) duals[i] = sg * s->y[i];
-    for (int64_t j = 0; j < n; ++j) duals[m + j] = sg * d[j];
+    /* (everything below is in the scaled problem; outputs are unscaled) */
+    for (int64_t i = 0; i < m; ++i) duals[i] = SC_ROW(sg * s->y[i], i, 1);
+    for (int64_t j = 0; j < n; ++j) duals[m + j] = SC_COL(sg * d[j], j, -1);
     /* ---- objective ranging (internal min-form costs) */
     for (int64_t j = 0; j < n; ++j) {
         double lo = -INF, hi = INF;
@@ -849,7 +948,7 @@ static void sensitivity(orc_t* s, const orc_control* ctl, const int32_t* dir, in
             lo = hi = c;
         }
         /* user sense: max negated the costs */
-        const double ulo = maximize ? -hi : lo, uhi = maximize ? -lo : hi;
+        const double ulo = SC_COL(maximize ? -hi : lo, j, -1), uhi = SC_COL(maximize ? -lo : hi, j, -1);
         objfrom[j] = ulo <= -INF ? -BIG : ulo >= INF ? BIG : ulo;
         objtill[j] = uhi <= -INF ? -BIG : uhi >= INF ? BIG : uhi;
     }
@@ -898,6 +997,8 @@ static void sensitivity(orc_t* s, const orc_control* ctl, const int32_t* dir, in
             lo = b + glo;
             hi = b + ghi;
         }
+        lo = SC_ROW(lo, i, -1);
+        hi = SC_ROW(hi, i, -1);
         dfrom[i] = lo <= -INF ? -BIG : lo >= INF ? BIG : lo;
         dtill[i] = hi <= -INF ? -BIG : hi >= INF ? BIG : hi;
     }
@@ -920,7 +1021,7 @@ void orc_default_control(orc_control* c) {
     c->refactor_mode = 0;
     c->price_mode = 0;
     c->price_rule = 1;
-    c->pad0 = 0;
+    c->scaling = 4 | 64; /* = elp_default_control: geometric + equilibrate */
     c->tol_singular = 1e-13;
 }
 
@@ -1014,6 +1115,22 @@ static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, 
     }
     s->nzl = ialloc((size_t)n);
     s->colbuf = dalloc((size_t)(m > 0 ? m : 1));
+    s->srow = s->scol = NULL;
+    if (ctl.scaling & (4 | 64)) {
+        s->srow = (int32_t*)calloc((size_t)(m > 0 ? m : 1), sizeof(int32_t));
+        s->scol = (int32_t*)calloc((size_t)n, sizeof(int32_t));
+        scale_factors(s, ctl.scaling, s->srow, s->scol);
+        if (A) { /* a materialised input: scale a copy once (exact) */
+            s->A_copy = (double*)malloc((size_t)m * (size_t)n * sizeof(double) + 8);
+            for (int64_t j = 0; j < n; ++j)
+                for (int64_t i = 0; i < m; ++i)
+                    s->A_copy[(size_t)j * (size_t)m + (size_t)i] =
+                        ldexp(A[(size_t)j * (size_t)m + (size_t)i], s->srow[i] + s->scol[j]);
+            s->A = s->A_copy;
+            s->a_scaled = 1;
+        }
+    }
+    /* scaled vectors: infinite values stay infinite (|v| >= infinity first) */
     s->refactor_mode = ctl.refactor_mode;
     s->tol_singular = ctl.tol_singular;
     const int64_t nv = s->nv, mm = m > 0 ? m : 1;
@@ -1061,6 +1178,8 @@ static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, 
         double l = lo ? lo[j] : 0.0, u = up ? up[j] : INF;
         if (l <= -BIG) l = -INF;
         if (u >= BIG) u = INF;
+        l = SC_COL(l, j, -1);
+        u = SC_COL(u, j, -1);
         s->lb[j] = l;
         s->ub[j] = u;
         s->cost[j] = 0.0;
@@ -1085,6 +1204,7 @@ static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, 
             double bi = rhs[i];
             if (bi <= -BIG) bi = -INF;
             if (bi >= BIG) bi = INF;
+            bi = SC_ROW(bi, i, 1);
             s->b[i] = bi;
             if (fabs(bi) < INF && fabs(bi) > bmax) bmax = fabs(bi);
             const int64_t sv = n + i, av = n + m + i;
@@ -1132,7 +1252,7 @@ static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, 
                 s->lb[av] = 0.0;
                 s->ub[av] = 0.0;
             }
-            for (int64_t j = 0; j < n; ++j) s->cost[j] = maximize ? -obj[j] : obj[j];
+            for (int64_t j = 0; j < n; ++j) s->cost[j] = SC_COL(maximize ? -obj[j] : obj[j], j, 1);
             if (any_art && refactor(s)) status = 5;
         }
         if (status == 0) {
@@ -1145,9 +1265,10 @@ static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, 
     }
 
     /* ---- outputs (get.objective / get.variables, R/class.R:277-278) ---- */
+    /* (unscaled: x_j = 2^scol_j x~_j, y_i = 2^srow_i y~_i -- exact) */
     if (xout)
         for (int64_t j = 0; j < n; ++j) {
-            double v = s->vstat[j] == VS_BASIC ? s->xs[s->spos[j]] : s->xval[j];
+            double v = SC_COL(s->vstat[j] == VS_BASIC ? s->xs[s->spos[j]] : s->xval[j], j, 1);
             if (status == 3 && j == unb_var) v = unb_sigma > 0 ? BIG : -BIG;
             xout[j] = v;
         }
@@ -1156,14 +1277,14 @@ static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, 
         else {
             double acc = 0.0;
             for (int64_t j = 0; j < n; ++j) {
-                const double v = s->vstat[j] == VS_BASIC ? s->xs[s->spos[j]] : s->xval[j];
+                const double v = SC_COL(s->vstat[j] == VS_BASIC ? s->xs[s->spos[j]] : s->xval[j], j, 1);
                 acc = fma(obj[j], v, acc);
             }
             *objval = acc;
         }
     }
     if (yout)
-        for (int64_t i = 0; i < m; ++i) yout[i] = maximize ? -s->y[i] : s->y[i];
+        for (int64_t i = 0; i < m; ++i) yout[i] = SC_ROW(maximize ? -s->y[i] : s->y[i], i, 1);
     if (basis) {
         int64_t c = 0;
         for (int64_t i = 0; i < m; ++i)
@@ -1189,6 +1310,7 @@ static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, 
     free(s->alS); free(s->alU); free(s->z); free(s->v); free(s->tmp); free(s->part);
     free(s->dw); free(s->dprev);
     free(s->used); free(s->perm); free(s->cp); free(s->ri); free(s->nzl); free(s->colbuf);
+    free(s->srow); free(s->scol); free(s->A_copy);
     return status;
 }
 

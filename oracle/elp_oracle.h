@@ -45,7 +45,8 @@ typedef struct orc_control {
                               nonzero rows in ascending order (elp_load_csc)  */
     int32_t price_rule;    /* 0 Dantzig (largest |d_j|), 1 Devex reference
                               weights (largest d_j^2 / w_j; run_phase)        */
-    int32_t pad0;
+    int32_t scaling;       /* 4 geometric | 64 equilibrate (elp_control.scaling):
+                              power-of-2 factors, scale_factors()           */
     double tol_singular;   /* Gauss-Jordan |pivot| <= this: numerical failure */
 } orc_control;
 
@@ -114,6 +115,10 @@ int orc_solve_mip(int64_t m, int64_t n, const double* A, const int32_t* dir, con
  * (column-major, lda = m).  c (ncols) and b (m) may be NULL. */
 void orc_generate_dense(uint64_t seed, int64_t m, int64_t n, int64_t col0,
                         int64_t ncols, double* A, double* b, double* c);
+
+/* Scaling exponents (control.scaling bits: 4 geometric, 64 equilibrate) of a
+ * dense column-major m x n A: the solver works on a_ij * 2^(rho_i + gam_j). */
+void orc_scale_factors(int64_t m, int64_t n, const double* A, int32_t mode, int32_t* rho, int32_t* gam);
 
 /* Rows rows[0..nrows) of the same instance, row-major (out[r * n + j]). */
 void orc_generate_rows(uint64_t seed, int64_t m, int64_t n, const int64_t* rows, int64_t nrows,

@@ -113,3 +113,18 @@ def load_mip_known_answers():
         r["dir"] = np.array(r["dir"], dtype=np.int32)
         r["is_int"] = np.array(r["is_int"], dtype=np.int32)
     return recs
+
+
+def load_robust_lps():
+    """tests/golden/robust_lps.json (make_robust.py): badly scaled, nearly
+    dependent, degenerate transport / assignment and wide-range LPs with the
+    HiGHS optimum."""
+    with open(os.path.join(GOLDEN, "robust_lps.json")) as f:
+        recs = json.load(f)
+    for r in recs:
+        r["A"] = np.array(r["A_rowmajor"], dtype=np.float64).reshape(r["m"], r["n"])
+        for k in ("rhs", "lo", "up"):
+            r[k] = np.array([_dec(v) for v in r[k]], dtype=np.float64)
+        r["obj"] = np.array(r["obj"], dtype=np.float64)
+        r["dir"] = np.array(r["dir"], dtype=np.int32)
+    return recs

@@ -21,7 +21,9 @@ CAP = 300  # pivot-trace window compared with the oracle
 
 @pytest.fixture(scope="module")
 def c4(gpu):
-    with gpu.Problem(M, N) as p:
+    # scaling off: the oracle's generated-A entry point would need passes over
+    # all 5e9 regenerated entries to reproduce the factors
+    with gpu.Problem(M, N, scaling=0) as p:
         p.set_trace(CAP)
         p.load_generated(SEED)
         st = p.solve()
@@ -64,7 +66,7 @@ def test_c4_optimality_certificate(c4):
 
 def test_c4_trace_matches_oracle(c4):
     from oracle import solve_generated
-    o = solve_generated(SEED, M, N, trace_cap=CAP, max_iter=CAP)
+    o = solve_generated(SEED, M, N, trace_cap=CAP, max_iter=CAP, scaling=0)
     assert o.status == 1 and o.stats["iterations"] == CAP
     assert c4.stats["iterations"] > CAP
     np.testing.assert_array_equal(c4.trace, o.trace)

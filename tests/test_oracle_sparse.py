@@ -34,14 +34,18 @@ def test_known_answers_column_order(rec):
 
 @pytest.mark.parametrize("n", [4, 7, 10])
 def test_klee_minty_exponential_path(n):
-    """Dantzig's rule walks all 2^n vertices of the Klee-Minty cube; Devex
-    weights (the default) take a short path to the same optimum."""
+    """Unscaled, Dantzig's rule walks all 2^n vertices of the Klee-Minty cube
+    and Devex weights take a short path; the default scaling (geometric +
+    equilibrate) breaks the construction, and every variant reaches 5^n."""
     from oracle import solve_dense as orc
     rec = next(r for r in SPARSE if r["name"] == f"klee_minty_{n}")
     args = (rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], True)
-    o = orc(*args, price_mode=1, price_rule=0)
+    o = orc(*args, price_mode=1, price_rule=0, scaling=0)
     assert o.status == 0 and o.objval == 5.0 ** n
     assert o.stats["iterations"] == 2 ** n - 1
-    v = orc(*args, price_mode=1)
+    v = orc(*args, price_mode=1, scaling=0)
     assert v.status == 0 and v.objval == 5.0 ** n
     assert v.stats["iterations"] <= 6 * n  # 9, 21, 51 for n = 4, 7, 10
+    for rule in (0, 1):
+        sc = orc(*args, price_mode=1, price_rule=rule)
+        assert sc.status == 0 and abs(sc.objval - 5.0 ** n) <= 1e-12 * 5.0 ** n
