@@ -485,44 +485,70 @@ static double unscale_row(const elp_handle* h, double v, int64_t i, int sgn) {
     return h->srow_h.empty() ? v : std::ldexp(v, sgn * h->srow_h[(size_t)i]);
 }
 
-// Scale the m x ncols column-major A (all N columns: one GPU or replicated) in
-// place on the device (launch_scale_*; oracle/elp_oracle.c scale_factors) and
-// keep the exponents on the host.
-static int scale_dense(elp_handle* h, double* A, int64_t ncols) {
+// Scale the m x ncols column-major A in place on the device (launch_scale_*;
+// oracle/elp_oracle.c scale_factors) and keep the exponents on the host.  A
+// holds columns [c0, c0 + ncols): all N of them (one GPU, replicated shards:
+// every rank computes the same factors alone), or this rank's shard only --
+// then the row passes combine the shards' maxima with an all-reduce and the
+// column exponents are gathered (exact f64 sum of a zero-filled vector).
+static int scale_dense(elp_handle* h, double* A, int64_t c0, int64_t ncols) {
     h->srow_h.clear();
     h->scol_h.clear();
     if (!scaling_on(h)) return 0;
     const int m = (int)h->m;
-    int32_t *rho = nullptr, *gam = nullptr, *rmn = nullptr, *rmx = nullptr, *chg = nullptr;
+    const bool shards = ncols < h->n && h->comm.kind != 0;
+    int32_t *rho = nullptr, *gam = nullptr, *rw = nullptr, *chg = nullptr;
+    double* gg = nullptr;
     hipError_t e = dalloc(&rho, (size_t)std::max(m, 1));
-    if (e == hipSuccess) e = dalloc(&gam, (size_t)ncols);
-    if (e == hipSuccess) e = dalloc(&rmn, (size_t)std::max(m, 1));
-    if (e == hipSuccess) e = dalloc(&rmx, (size_t)std::max(m, 1));
+    if (e == hipSuccess) e = dalloc(&gam, (size_t)std::max<int64_t>(ncols, 1));
+    if (e == hipSuccess) e = dalloc(&rw, 2 * (size_t)std::max(m, 1));  // [rnm | rmx]
     if (e == hipSuccess) e = dalloc(&chg, 1);
+    int32_t *rmn = rw, *rmx = rw + std::max(m, 1);
     if (e == hipSuccess) e = launch_scale_init(m, ncols, rho, gam, rmn, rmx, h->st);
+    int rc = 0;
     if (h->ctl.scaling & ELP_SCALE_GEOMETRIC)
-        for (int pass = 0; pass < SCALE_PASSES && e == hipSuccess; ++pass) {
+        for (int pass = 0; pass < SCALE_PASSES && e == hipSuccess && !rc; ++pass) {
             int32_t moved = 0;
             e = hipMemsetAsync(chg, 0, sizeof(int32_t), h->st);
             if (e == hipSuccess) e = launch_scale_rows(m, ncols, A, gam, rmn, rmx, h->st);
-            if (e == hipSuccess) e = launch_scale_row_final(m, rmn, rmx, rho, chg, h->st);
-            if (e == hipSuccess) e = launch_scale_cols(m, ncols, A, rho, gam, 0, chg, h->st);
-            if (e == hipSuccess) e = hipMemcpyAsync(&moved, chg, sizeof(int32_t), hipMemcpyDeviceToHost, h->st);
-            if (e == hipSuccess) e = hipStreamSynchronize(h->st);
+            if (e == hipSuccess && shards) rc = h->comm.allreduce_max_i32(rw, 2 * (size_t)std::max(m, 1), h->st);
+            if (e == hipSuccess && !rc) e = launch_scale_row_final(m, rmn, rmx, rho, chg, h->st);
+            if (e == hipSuccess && !rc) e = launch_scale_cols(m, ncols, A, rho, gam, 0, chg, h->st);
+            if (e == hipSuccess && !rc && shards) rc = h->comm.allreduce_max_i32(chg, 1, h->st);
+            if (e == hipSuccess && !rc) e = hipMemcpyAsync(&moved, chg, sizeof(int32_t), hipMemcpyDeviceToHost, h->st);
+            if (e == hipSuccess && !rc) e = hipStreamSynchronize(h->st);
             if (!moved) break;
         }
-    if (e == hipSuccess && (h->ctl.scaling & ELP_SCALE_EQUILIBRATE))
+    if (e == hipSuccess && !rc && (h->ctl.scaling & ELP_SCALE_EQUILIBRATE))
         e = launch_scale_cols(m, ncols, A, rho, gam, 1, chg, h->st);
-    if (e == hipSuccess) e = launch_scale_apply(m, ncols, A, rho, gam, h->st);
+    if (e == hipSuccess && !rc) e = launch_scale_apply(m, ncols, A, rho, gam, h->st);
     h->srow_h.assign((size_t)m, 0);
-    h->scol_h.assign((size_t)ncols, 0);
-    if (e == hipSuccess && m)
+    h->scol_h.assign((size_t)h->n, 0);
+    std::vector<int32_t> gl((size_t)ncols);
+    if (e == hipSuccess && !rc && m)
         e = hipMemcpyAsync(h->srow_h.data(), rho, (size_t)m * sizeof(int32_t), hipMemcpyDeviceToHost, h->st);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(h->scol_h.data(), gam, (size_t)ncols * sizeof(int32_t), hipMemcpyDeviceToHost, h->st);
-    if (e == hipSuccess) e = hipStreamSynchronize(h->st);
-    for (int32_t* p : {rho, gam, rmn, rmx, chg})
+    if (e == hipSuccess && !rc && ncols)
+        e = hipMemcpyAsync(gl.data(), gam, (size_t)ncols * sizeof(int32_t), hipMemcpyDeviceToHost, h->st);
+    if (e == hipSuccess && !rc) e = hipStreamSynchronize(h->st);
+    if (e == hipSuccess && !rc) {
+        if (!shards) {
+            std::copy(gl.begin(), gl.end(), h->scol_h.begin() + c0);
+        } else {  // every rank's column exponents
+            std::vector<double> gv((size_t)h->n, 0.0);
+            for (int64_t j = 0; j < ncols; ++j) gv[(size_t)(c0 + j)] = (double)gl[(size_t)j];
+            e = dalloc(&gg, (size_t)h->n);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(gg, gv.data(), gv.size() * sizeof(double), hipMemcpyHostToDevice, h->st);
+            if (e == hipSuccess) rc = h->comm.allreduce_sum_f64(gg, (size_t)h->n, h->st);
+            if (e == hipSuccess && !rc)
+                e = hipMemcpyAsync(gv.data(), gg, gv.size() * sizeof(double), hipMemcpyDeviceToHost, h->st);
+            if (e == hipSuccess && !rc) e = hipStreamSynchronize(h->st);
+            for (int64_t j = 0; j < h->n; ++j) h->scol_h[(size_t)j] = (int32_t)gv[(size_t)j];
+        }
+    }
+    for (void* p : {(void*)rho, (void*)gam, (void*)rw, (void*)chg, (void*)gg})
         if (p) (void)hipFree(p);
+    if (rc) return fail(rc, "scaling: shard exchange failed");
     if (e != hipSuccess) return fail(ELP_E_HIP, std::string("scaling: ") + hipGetErrorString(e));
     return 0;
 }
@@ -746,8 +772,6 @@ static int prep_load(elp_handle* h, bool csc = false) {
                     (h->ctl.replicate == 1 || (h->ctl.replicate == 0 && abytes <= 64.0 * (1ull << 30)));
     if (h->comm.p2p && !h->replicated)
         return fail(ELP_E_UNSUPPORTED, "xGMI mailbox exchange needs A replicated on every rank");
-    if (scaling_on(h) && h->comm.kind != 0 && !h->replicated)
-        return fail(ELP_E_UNSUPPORTED, "scaling needs all of A on every rank (elp_control.replicate) or scaling = 0");
     return alloc_all(h);
 }
 
@@ -765,7 +789,7 @@ extern "C" int elp_load_dense(elp_handle* h, const double* A, const int32_t* dir
     if (cnt)
         HIPCHK(hipMemcpyAsync(h->A_owned, A + (size_t)c0 * (size_t)h->m, cnt * sizeof(double),
                               hipMemcpyHostToDevice, h->st));
-    rc = scale_dense(h, h->A_owned, nc);
+    rc = scale_dense(h, h->A_owned, c0, nc);
     if (rc) return rc;
     h->d.A = h->A_owned + (size_t)(h->col0 - c0) * (size_t)h->m;
     h->d.Afull = h->replicated ? h->A_owned : nullptr;
@@ -804,13 +828,16 @@ extern "C" int elp_load_dense_device(elp_handle* h, const double* dA, const int3
         return fail(ELP_E_ARG, "elp_load_dense_device: NULL input");
     int rc = prep_load(h);
     if (rc) return rc;
-    if (scaling_on(h)) {  // the caller's A is read-only: scale a copy of it
-        const size_t cnt = (size_t)h->m * (size_t)h->n;
+    if (scaling_on(h)) {  // the caller's A is read-only: scale a copy of (this rank's part of) it
+        const int64_t c0 = h->replicated ? 0 : h->col0, nc = h->replicated ? h->n : h->nloc;
+        const size_t cnt = (size_t)h->m * (size_t)nc;
         HIPCHK(dalloc(&h->A_owned, cnt));
-        if (cnt) HIPCHK(hipMemcpyAsync(h->A_owned, dA, cnt * sizeof(double), hipMemcpyDeviceToDevice, h->st));
-        rc = scale_dense(h, h->A_owned, h->n);
+        if (cnt)
+            HIPCHK(hipMemcpyAsync(h->A_owned, dA + (size_t)c0 * (size_t)h->m, cnt * sizeof(double),
+                                  hipMemcpyDeviceToDevice, h->st));
+        rc = scale_dense(h, h->A_owned, c0, nc);
         if (rc) return rc;
-        dA = h->A_owned;
+        dA = h->A_owned - (size_t)c0 * (size_t)h->m;  // (only columns [c0, c0 + nc) are read)
     } else {
         h->srow_h.clear();
         h->scol_h.clear();
@@ -922,7 +949,7 @@ extern "C" int elp_load_generated(elp_handle* h, uint64_t seed) {
     HIPCHK(hipStreamSynchronize(h->st));
     (void)hipFree(db);
     (void)hipFree(dc);
-    rc = scale_dense(h, h->A_owned, nc);
+    rc = scale_dense(h, h->A_owned, c0, nc);
     if (rc) return rc;
     h->d.A = h->A_owned + (size_t)(h->col0 - c0) * (size_t)m;
     h->d.Afull = h->replicated ? h->A_owned : nullptr;

@@ -250,7 +250,9 @@ hipError_t launch_refactor_primal(const Dev& d, int k, hipStream_t st);  // need
 hipError_t launch_nzlist(const Dev& d, hipStream_t st);
 hipError_t launch_transpose_A(const Dev& d, hipStream_t st);
 // scaling (elp_control.scaling): exponents rho (m rows), gamma (ncols columns);
-// rmn / rmx: per-row min / max work (m each); changed: set when a pass moved a factor
+// rmn / rmx: per-row work (m each: max of -e, max of e; rmx must follow rmn in
+// one 2m buffer so shards combine them with one all-reduce max); changed: set
+// when a pass moved a factor
 constexpr int SCALE_PASSES = 20;  // geometric row + column passes at most
 hipError_t launch_scale_init(int m, int64_t ncols, int32_t* rho, int32_t* gam, int32_t* rmn, int32_t* rmx,
                              hipStream_t st);

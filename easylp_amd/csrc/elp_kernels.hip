@@ -465,7 +465,8 @@ __global__ void __launch_bounds__(256) k_scale_col(int m, int64_t ncols, const d
 }
 
 // row pass, part 1: thread = row, a chunk of SCALE_RCOLS columns per workgroup
-// row; per-row min / max of e_ij + gamma_j into rmn / rmx (integer atomics)
+// row; per-row max of -(e_ij + gamma_j) and of e_ij + gamma_j into rnm / rmx
+// (integer atomics; both maxima, so shards combine with one all-reduce max)
 constexpr int SCALE_RCOLS = 512;
 __global__ void __launch_bounds__(256) k_scale_row_part(int m, int64_t ncols, const double* __restrict__ A,
                                                         const int32_t* __restrict__ gam, int32_t* rmn,
@@ -484,7 +485,7 @@ __global__ void __launch_bounds__(256) k_scale_row_part(int m, int64_t ncols, co
         }
     }
     if (mx != SCALE_EMPTY_MAX) {
-        atomicMin(&rmn[i], mn);
+        atomicMax(&rmn[i], -mn);
         atomicMax(&rmx[i], mx);
     }
 }
@@ -493,13 +494,13 @@ __global__ void __launch_bounds__(256) k_scale_row_part(int m, int64_t ncols, co
 __global__ void k_scale_row_final(int m, int32_t* rmn, int32_t* rmx, int32_t* rho, int32_t* changed) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= m) return;
-    const int mn = rmn[i], mx = rmx[i];
+    const int mn = -rmn[i], mx = rmx[i];
     const int r = mx == SCALE_EMPTY_MAX ? 0 : -floor_half(mn + mx);
     if (r != rho[i]) {
         rho[i] = r;
         *changed = 1;
     }
-    rmn[i] = SCALE_EMPTY_MIN;  // ready for the next pass
+    rmn[i] = SCALE_EMPTY_MAX;  // ready for the next pass
     rmx[i] = SCALE_EMPTY_MAX;
 }
 
@@ -507,7 +508,7 @@ __global__ void k_scale_init(int m, int64_t ncols, int32_t* rho, int32_t* gam, i
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t < m) {
         rho[t] = 0;
-        rmn[t] = SCALE_EMPTY_MIN;
+        rmn[t] = SCALE_EMPTY_MAX;
         rmx[t] = SCALE_EMPTY_MAX;
     }
     if (t < ncols) gam[t] = 0;
