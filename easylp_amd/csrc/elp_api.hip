@@ -477,6 +477,17 @@ static int any_rank(elp_handle* h, int v, int* out) {
     return 0;
 }
 
+// ELP_DEBUG_LOAD: phase times of elp_load_* on stderr (device synchronised)
+static void load_mark(elp_handle* h, const char* what) {
+    static const bool on = std::getenv("ELP_DEBUG_LOAD") != nullptr;
+    if (!on) return;
+    (void)hipStreamSynchronize(h->st);
+    static thread_local double t_last = 0.0;
+    const double t = now_s();
+    if (what) std::fprintf(stderr, "elp load: %-18s %8.2f ms\n", what, 1e3 * (t - t_last));
+    t_last = t;
+}
+
 static bool scaling_on(const elp_handle* h) { return (h->ctl.scaling & (ELP_SCALE_GEOMETRIC | ELP_SCALE_EQUILIBRATE)) != 0; }
 static double unscale_col(const elp_handle* h, double v, int64_t j, int sgn) {
     return h->scol_h.empty() ? v : std::ldexp(v, sgn * h->scol_h[(size_t)j]);
@@ -505,9 +516,11 @@ static int scale_dense(elp_handle* h, double* A, int64_t c0, int64_t ncols) {
     if (e == hipSuccess) e = dalloc(&chg, 1);
     int32_t *rmn = rw, *rmx = rw + std::max(m, 1);
     if (e == hipSuccess) e = launch_scale_init(m, ncols, rho, gam, rmn, rmx, h->st);
-    int rc = 0;
+    int rc = 0, passes = 0;
+    const double t_sc = now_s();
     if (h->ctl.scaling & ELP_SCALE_GEOMETRIC)
         for (int pass = 0; pass < SCALE_PASSES && e == hipSuccess && !rc; ++pass) {
+            passes++;
             int32_t moved = 0;
             e = hipMemsetAsync(chg, 0, sizeof(int32_t), h->st);
             if (e == hipSuccess) e = launch_scale_rows(m, ncols, A, gam, rmn, rmx, h->st);
@@ -550,6 +563,9 @@ static int scale_dense(elp_handle* h, double* A, int64_t c0, int64_t ncols) {
         if (p) (void)hipFree(p);
     if (rc) return fail(rc, "scaling: shard exchange failed");
     if (e != hipSuccess) return fail(ELP_E_HIP, std::string("scaling: ") + hipGetErrorString(e));
+    if (std::getenv("ELP_DEBUG_SCALE"))
+        std::fprintf(stderr, "elp scaling: %d geometric passes, %.2f ms (m %lld, %lld columns)\n", passes,
+                     1e3 * (now_s() - t_sc), (long long)m, (long long)ncols);
     return 0;
 }
 
@@ -619,6 +635,7 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
                        const double* lo, const double* up, int32_t maximize) {
     const int64_t m = h->m, n = h->n, n0 = h->col0, nl = h->nloc;
     Dev& d = h->d;
+    load_mark(h, "A + scaling");
     for (int64_t i = 0; i < m; ++i)
         if (dir[i] < ELP_LE || dir[i] > ELP_EQ) return fail(ELP_E_ARG, "dir must be 1 (<=), 2 (>=) or 3 (==)");
     h->maximize = maximize ? 1 : 0;
@@ -699,6 +716,7 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
         const int rc = ensure_ar(h, (int64_t)h->hctl->ny + 64);
         if (rc) return rc;
     }
+    load_mark(h, "cols / rows / Y");
     // dense A: a row-major copy for the AR row copies (contiguous reads); without
     // the memory for it they read A's rows in place
     // (only while the AR rows could still grow to a full copy of A beside it)
@@ -711,7 +729,9 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
             (void)hipGetLastError();
         }
     }
+    load_mark(h, "A^T alloc");
     if (d.AT) HIPCHK(launch_transpose_A(d, h->st));
+    load_mark(h, d.AT ? "A^T copy" : "A^T (none)");
     HIPCHK(launch_fill_AR(h->d, h->st));
     (void)hipFree(dlo);
     (void)hipFree(dup);
@@ -755,7 +775,9 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
 static int prep_load(elp_handle* h, bool csc = false) {
     if (!h) return fail(ELP_E_ARG, "NULL handle");
     HIPCHK(hipSetDevice(h->dev));
+    load_mark(h, nullptr);
     if (h->loaded) free_dev(h);
+    load_mark(h, "free previous");
     h->loaded = false;
     h->csc = csc;
     if (csc && h->comm.kind != 0)
@@ -772,7 +794,9 @@ static int prep_load(elp_handle* h, bool csc = false) {
                     (h->ctl.replicate == 1 || (h->ctl.replicate == 0 && abytes <= 64.0 * (1ull << 30)));
     if (h->comm.p2p && !h->replicated)
         return fail(ELP_E_UNSUPPORTED, "xGMI mailbox exchange needs A replicated on every rank");
-    return alloc_all(h);
+    const int rc = alloc_all(h);
+    load_mark(h, "alloc");
+    return rc;
 }
 
 extern "C" int elp_load_dense(elp_handle* h, const double* A, const int32_t* dir, const double* rhs,
