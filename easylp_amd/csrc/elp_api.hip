@@ -136,7 +136,8 @@ static void free_dev(elp_handle* h) {
                     d.cand,     d.pstamp, d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand, d.rseg, d.AT,
                     d.pkt, d.objg, d.ract, d.cand_xchg, h->d_flag, d.cS, d.slo, d.shi, d.rlo, d.rhi,
                     (void*)d.cptr, (void*)d.rind, (void*)d.cval, (void*)d.rptr, (void*)d.cind,
-                    (void*)d.rval, d.qcol, d.dstamp, d.rowvs, d.yvs, d.dw, d.dprev};
+                    (void*)d.rval, d.qcol, d.dstamp, d.rowvs, d.yvs, d.dw, d.dprev, (void*)d.srow,
+                    (void*)d.scol};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     h->A_owned = nullptr;
@@ -502,7 +503,7 @@ static double unscale_row(const elp_handle* h, double v, int64_t i, int sgn) {
 // every rank computes the same factors alone), or this rank's shard only --
 // then the row passes combine the shards' maxima with an all-reduce and the
 // column exponents are gathered (exact f64 sum of a zero-filled vector).
-static int scale_dense(elp_handle* h, double* A, int64_t c0, int64_t ncols) {
+static int scale_dense(elp_handle* h, double* A, int64_t c0, int64_t ncols, bool apply = true) {
     h->srow_h.clear();
     h->scol_h.clear();
     if (!scaling_on(h)) return 0;
@@ -534,7 +535,7 @@ static int scale_dense(elp_handle* h, double* A, int64_t c0, int64_t ncols) {
         }
     if (e == hipSuccess && !rc && (h->ctl.scaling & ELP_SCALE_EQUILIBRATE))
         e = launch_scale_cols(m, ncols, A, rho, gam, 1, chg, h->st);
-    if (e == hipSuccess && !rc) e = launch_scale_apply(m, ncols, A, rho, gam, h->st);
+    if (e == hipSuccess && !rc && apply) e = launch_scale_apply(m, ncols, A, rho, gam, h->st);
     h->srow_h.assign((size_t)m, 0);
     h->scol_h.assign((size_t)h->n, 0);
     std::vector<int32_t> gl((size_t)ncols);
@@ -852,16 +853,21 @@ extern "C" int elp_load_dense_device(elp_handle* h, const double* dA, const int3
         return fail(ELP_E_ARG, "elp_load_dense_device: NULL input");
     int rc = prep_load(h);
     if (rc) return rc;
-    if (scaling_on(h)) {  // the caller's A is read-only: scale a copy of (this rank's part of) it
+    if (scaling_on(h)) {
+        // the caller's A is read-only and may be large (40 GB at 10 000 x 500 000):
+        // the factors come from read-only passes and every kernel scales what it
+        // reads on the fly (Dev::srow / scol; exact, the values of a scaled copy)
         const int64_t c0 = h->replicated ? 0 : h->col0, nc = h->replicated ? h->n : h->nloc;
-        const size_t cnt = (size_t)h->m * (size_t)nc;
-        HIPCHK(dalloc(&h->A_owned, cnt));
-        if (cnt)
-            HIPCHK(hipMemcpyAsync(h->A_owned, dA + (size_t)c0 * (size_t)h->m, cnt * sizeof(double),
-                                  hipMemcpyDeviceToDevice, h->st));
-        rc = scale_dense(h, h->A_owned, c0, nc);
+        rc = scale_dense(h, const_cast<double*>(dA) + (size_t)c0 * (size_t)h->m, c0, nc, false);
         if (rc) return rc;
-        dA = h->A_owned - (size_t)c0 * (size_t)h->m;  // (only columns [c0, c0 + nc) are read)
+        int32_t *sr = nullptr, *scg = nullptr;
+        HIPCHK(dalloc(&sr, (size_t)std::max<int64_t>(h->m, 1)));
+        HIPCHK(dalloc(&scg, (size_t)h->n));
+        h->d.srow = sr;
+        h->d.scol = scg;
+        if (h->m)
+            HIPCHK(hipMemcpyAsync(sr, h->srow_h.data(), (size_t)h->m * sizeof(int32_t), hipMemcpyHostToDevice, h->st));
+        HIPCHK(hipMemcpyAsync(scg, h->scol_h.data(), (size_t)h->n * sizeof(int32_t), hipMemcpyHostToDevice, h->st));
     } else {
         h->srow_h.clear();
         h->scol_h.clear();

@@ -28,7 +28,7 @@ enum : int32_t { PC_NONE = 0, PC_A = 1, PC_B = 2, PC_C = 3, PC_D = 4, PC_E = 5 }
 enum : int32_t { ACT_NONE = 0, ACT_FLIP = 1, ACT_PIVOT = 2 };
 
 #ifndef ELP_PRICE_SPLIT
-#define ELP_PRICE_SPLIT 2
+#define ELP_PRICE_SPLIT 4
 #endif
 // slot chunks per pricing tile (one per wave); the oracle's PRICE_SPLIT must match
 constexpr int PRICE_SPLIT = ELP_PRICE_SPLIT;
@@ -185,6 +185,12 @@ struct Dev {
     int32_t maximize, pad2;
     double infinity;
     double tol_singular;  // Gauss-Jordan: |pivot| <= this -> ST_NUMFAIL (elp_control)
+    // on-the-fly scaling (elp_load_dense_device with scaling on: the caller's A
+    // is read-only and is not copied): every read of A / Afull / the exchanged
+    // column multiplies by 2^(srow[i] + scol[j]) (j global; exact, so the values
+    // are those of a scaled copy); null when A itself holds the scaled values
+    const int32_t* srow;
+    const int32_t* scol;
     int64_t mb_ticks;     // xGMI mailbox wait limit in s_memrealtime ticks (100 MHz)
     // CSC input (elp_load_csc, one GPU): A is null, columns live in cptr/rind/cval
     // (rows ascending), a CSR copy serves the row activities, and the entering

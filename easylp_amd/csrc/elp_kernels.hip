@@ -74,6 +74,16 @@ DEV int loc_of(const Dev& d, int g) {
     }
     return d.n + (g - d.N);
 }
+// an element of A as the solver sees it: scaled on the fly when A is the
+// caller's unscaled matrix (Dev::srow / scol), as stored otherwise
+DEV double sca(const Dev& d, double a, int64_t i, int64_t jg) {
+    return d.srow ? ldexp(a, d.srow[i] + d.scol[jg]) : a;
+}
+// element i of the entering column q (a column pointer of qcolumn): the
+// exchanged packet and the CSC scatter hold scaled values already
+DEV double qcol_at(const Dev& d, const double* col, int q, int64_t i) {
+    return col == d.pkt || d.csc ? col[i] : sca(d, col[i], i, q);
+}
 // the entering structural column q (global id): read in place on one GPU or
 // from the replicated A, else from the exchanged packet
 DEV const double* qcolumn(const Dev& d, int q) {
@@ -280,7 +290,7 @@ __global__ void k_row_chain(Dev d) {
     double acc = d.ract[i];
     for (int t = 0; t < nz; ++t) {
         const int j = d.nzlist[t];
-        acc = fma(d.A[(size_t)j * (size_t)d.m + (size_t)i], d.xval[j], acc);
+        acc = fma(sca(d, d.A[(size_t)j * (size_t)d.m + (size_t)i], i, d.col0 + j), d.xval[j], acc);
     }
     d.ract[i] = acc;
 }
@@ -392,7 +402,8 @@ __global__ void __launch_bounds__(1024) k_init_Y(Dev d) {
 // a_ij of this shard, read along a row (AR row copies): the row-major copy when
 // there is one (contiguous over j), else the column-major A (one line per element)
 DEV double a_row(const Dev& d, int64_t i, int64_t j) {
-    return d.AT ? d.AT[(size_t)i * (size_t)d.n + (size_t)j] : d.A[(size_t)j * (size_t)d.m + (size_t)i];
+    return d.AT ? d.AT[(size_t)i * (size_t)d.n + (size_t)j]  // (scaled by k_transpose_A)
+                : sca(d, d.A[(size_t)j * (size_t)d.m + (size_t)i], i, d.col0 + j);
 }
 
 // AT = A^T through 64 x 64 LDS tiles (reads down columns, writes along rows)
@@ -402,7 +413,7 @@ __global__ void __launch_bounds__(256) k_transpose_A(Dev d) {
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     for (int r = ty; r < 64; r += 4) {
         const int64_t j = j0 + r, i = i0 + tx;
-        if (j < d.n && i < d.m) t[r][tx] = d.A[(size_t)j * (size_t)d.m + (size_t)i];
+        if (j < d.n && i < d.m) t[r][tx] = sca(d, d.A[(size_t)j * (size_t)d.m + (size_t)i], i, d.col0 + j);
     }
     __syncthreads();
     for (int r = ty; r < 64; r += 4) {
@@ -1135,7 +1146,7 @@ DEV void entering_chosen(const Dev& d, const Cand& best) {
 DEV void gather_aR(const Dev& d, int q, const double* qcol) {
     const int k = d.ctl->k;
     if (q < d.N) {
-        for (int p = threadIdx.x; p < k; p += blockDim.x) d.aR[p] = qcol[d.Rl[p]];
+        for (int p = threadIdx.x; p < k; p += blockDim.x) d.aR[p] = qcol_at(d, qcol, q, d.Rl[p]);
     } else {
         const int i0 = q - d.N;
         for (int p = threadIdx.x; p < k; p += blockDim.x) d.aR[p] = d.Rl[p] == i0 ? 1.0 : 0.0;
@@ -1275,9 +1286,9 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw
             for (int t = 0; t < PFR; ++t) g[t] = col[tid + 256 * t < k ? rl[t] : 0];  // straight-line
 #pragma unroll
             for (int t = 0; t < PFR; ++t)
-                if (tid + 256 * t < k) aRs[tid + 256 * t] = g[t];
+                if (tid + 256 * t < k) aRs[tid + 256 * t] = d.srow && col != d.pkt ? sca(d, g[t], rl[t], q) : g[t];
         } else {
-            for (int p = tid; p < k; p += 256) aRs[p] = col[d.Rl[p]];
+            for (int p = tid; p < k; p += 256) aRs[p] = qcol_at(d, col, q, d.Rl[p]);
         }
     } else {
         const int i0 = q - d.N;
@@ -1357,7 +1368,7 @@ __global__ void __launch_bounds__(256) k_select_global(Dev d) {
         }
     } else if (own) {
         const double* col = d.A + (size_t)ql * (size_t)m;
-        for (int i = threadIdx.x; i < m; i += 256) d.pkt[i] = col[i];
+        for (int i = threadIdx.x; i < m; i += 256) d.pkt[i] = sca(d, col[i], i, q);
         if (threadIdx.x == 0) {
             d.pkt[m] = d.lb[ql];
             d.pkt[m + 1] = d.ub[ql];
@@ -1405,7 +1416,7 @@ __global__ void __launch_bounds__(256) k_select_xftran(Dev d) {
     }
     if (q < d.N) {
         const double* col = d.Afull + (size_t)q * (size_t)m;
-        for (int p = threadIdx.x; p < k; p += 256) aRs[p] = col[d.Rl[p]];
+        for (int p = threadIdx.x; p < k; p += 256) aRs[p] = sca(d, col[d.Rl[p]], d.Rl[p], q);
     } else {
         const int i0 = q - d.N;
         for (int p = threadIdx.x; p < k; p += 256) aRs[p] = d.Rl[p] == i0 ? 1.0 : 0.0;
@@ -1608,7 +1619,7 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
     double* zp = LDSZ ? zlds : d.zpart + (size_t)blockIdx.x * ZR_ROWS * (size_t)nch;
     if (row_tile) {
         double aiq = 0.0;
-        if (u >= 0) aiq = q >= d.N ? (i == q - d.N ? 1.0 : 0.0) : qcolumn(d, q)[i];
+        if (u >= 0) aiq = q >= d.N ? (i == q - d.N ? 1.0 : 0.0) : qcol_at(d, qcolumn(d, q), q, i);
         if (ch0 < nch) {  // the prefetched chunk: fma chain over its real positions
             double acc = 0.0;
             if (i < m) {
@@ -2376,7 +2387,7 @@ DEV void apply_plan(const Dev& d, const Plan& P, int blk, int nb, int nb_minv, b
     for (int64_t t = t0; t < d.m; t += tstride) {
         if (P.pcase == PC_A || P.pcase == PC_B) {
             const int pos = P.pcase == PC_A ? P.p : k;
-            d.AS[(size_t)pos * m + t] = qcolumn(d, P.q)[t];
+            d.AS[(size_t)pos * m + t] = qcol_at(d, qcolumn(d, P.q), P.q, t);
         } else if (P.pcase == PC_C && P.b != P.last) {
             d.AS[(size_t)P.b * m + t] = d.AS[(size_t)P.last * m + t];
         }
@@ -2626,7 +2637,7 @@ __global__ void __launch_bounds__(256) k_sens_redcost(Dev d, double* __restrict_
     if (j >= d.n) return;
     const double* col = d.A + (size_t)j * (size_t)d.m;
     double acc = 0.0;
-    for (int i = lane; i < d.m; i += 64) acc = fma(col[i], d.y[i], acc);
+    for (int i = lane; i < d.m; i += 64) acc = fma(sca(d, col[i], i, d.col0 + j), d.y[i], acc);
     acc = wave_tree(acc);
     if (lane == 0) dred[j] = d.vstat[j] == VS_BASIC ? 0.0 : d.cost[j] - acc;
 }
@@ -2642,7 +2653,7 @@ __global__ void k_sens_gather_rows(Dev d, double* __restrict__ TR, int k) {
         return;
     }
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d.n; j += (int64_t)gridDim.x * blockDim.x)
-        TR[(size_t)c * (size_t)d.n + (size_t)j] = d.A[(size_t)j * (size_t)d.m + (size_t)i];
+        TR[(size_t)c * (size_t)d.n + (size_t)j] = sca(d, d.A[(size_t)j * (size_t)d.m + (size_t)i], i, d.col0 + j);
 }
 
 // ratio-interval update: keep l <= x + t g <= u  ->  t in [lo, hi]

@@ -50,7 +50,7 @@
 #define VS_FREE 3
 
 #ifndef PRICE_SPLIT
-#define PRICE_SPLIT 2 /* = the HIP side's ELP_PRICE_SPLIT */
+#define PRICE_SPLIT 4 /* = the HIP side's ELP_PRICE_SPLIT */
 #endif
 #define ZCHUNK 32
 #define WAVE 64

@@ -57,13 +57,16 @@ def test_ngpu_general_lp_matches_oracle(gpu, ngpu):
     _same(g, o, ngpu)
 
 
-def test_ngpu_device_resident_input(gpu):
+@pytest.mark.parametrize("replicate", [1, 2])
+def test_ngpu_device_resident_input(gpu, replicate):
     """elp_load_dense_device on an ngpu handle (A in HBM of the first device;
-    ranks on other devices would get a copy), solved twice on one handle."""
+    ranks on other devices would get a copy), solved twice on one handle; the
+    default scaling is applied on the fly (the caller's A is not copied), also
+    to the entering column that travels between column-only shards."""
     from oracle import solve_dense as orc
     m, n, seed = 250, 1000, 4
     A, b, c = gpu.generate_dense_device(seed, m, n, 0)
-    with gpu.Problem(m, n, ngpu=2) as p:
+    with gpu.Problem(m, n, ngpu=2, replicate=replicate) as p:
         p.set_trace(100000)
         for _ in range(2):
             p.load_dense_device(A.data_ptr(), np.ones(m, np.int32), b, c, maximize=True)
