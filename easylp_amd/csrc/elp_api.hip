@@ -111,7 +111,7 @@ extern "C" void elp_default_control(elp_control* c) {
     c->infinity = 1e30;
     c->time_limit = 0.0;
     c->max_iter = 0;
-    c->refactor_period = 100;
+    c->refactor_period = 250;  // lp_solve's default set_maxpivot
     c->degen_switch = 50;
     c->device = 0;
     c->sync_every = 32;
@@ -252,7 +252,7 @@ extern "C" int elp_create(elp_handle** out, int64_t m, int64_t n, const elp_cont
     elp_handle* h = new elp_handle();
     if (ctl) h->ctl = *ctl;
     else elp_default_control(&h->ctl);
-    if (h->ctl.refactor_period <= 0) h->ctl.refactor_period = 100;
+    if (h->ctl.refactor_period <= 0) h->ctl.refactor_period = 250;
     if (h->ctl.degen_switch <= 0) h->ctl.degen_switch = 50;
     if (h->ctl.sync_every <= 0) h->ctl.sync_every = 32;
     if (!(h->ctl.infinity > 0)) h->ctl.infinity = 1e30;

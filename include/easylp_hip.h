@@ -61,7 +61,7 @@ typedef struct elp_control {
     double infinity;         /* lp_solve infinity                      (1e30)  */
     double time_limit;       /* seconds, <= 0: none   (lp.control timeout)     */
     int64_t max_iter;        /* <= 0: 100*(m+n)+10000                          */
-    int32_t refactor_period; /* pivots between Gauss-Jordan refactors  (100)   */
+    int32_t refactor_period; /* pivots between refactors (250, lp_solve maxpivot) */
     int32_t degen_switch;    /* degenerate pivots before Bland's rule  (50)    */
     int32_t device;          /* HIP device ordinal for this handle     (0)     */
     int32_t sync_every;      /* iterations launched between host polls (32)    */

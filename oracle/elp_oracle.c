@@ -1015,7 +1015,7 @@ void orc_default_control(orc_control* c) {
     c->tol_pivot = 1e-9;
     c->infinity = 1e30;
     c->max_iter = 0;
-    c->refactor_period = 100;
+    c->refactor_period = 250;  // lp_solve's default set_maxpivot
     c->degen_switch = 50;
     c->t_mark_iter = -1;
     c->refactor_mode = 0;
@@ -1082,7 +1082,7 @@ static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, 
     orc_control ctl;
     if (ctl_in) ctl = *ctl_in;
     else orc_default_control(&ctl);
-    if (ctl.refactor_period <= 0) ctl.refactor_period = 100;
+    if (ctl.refactor_period <= 0) ctl.refactor_period = 250;
     if (ctl.degen_switch <= 0) ctl.degen_switch = 50;
     const int64_t max_iter = ctl.max_iter > 0 ? ctl.max_iter : 100 * (m + n) + 10000;
     const double INF = HUGE_VAL, BIG = ctl.infinity;

@@ -35,7 +35,7 @@ def test_abi_version_and_defaults():
     assert lib.elp_abi_version() == ABI_VERSION == 2
     c = ElpControl()
     lib.elp_default_control(ctypes.byref(c))
-    assert c.infinity == 1e30 and c.refactor_period == 100 and c.sync_every == 32
+    assert c.infinity == 1e30 and c.refactor_period == 250 and c.sync_every == 32
     assert c.tol_singular == 1e-13 and c.mailbox_timeout == 2.0 and c.ngpu == 1
 
 
