@@ -133,7 +133,7 @@ static void free_dev(elp_handle* h) {
                     d.t,        d.acol, d.aR,   d.alS,   d.alU,  d.zz,    d.zpart, d.vrow,
                     d.vvec,     d.colA, d.rhs,  d.vstat, d.cover, d.rpos, d.Rl,    d.Sl,
                     d.Yl,  d.ypos,  d.perm,  d.pivstep, d.nzlist, d.nzcount, d.nzchunk,
-                    d.cand,     d.pstamp, d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand, d.rseg, d.AT,
+                    d.cand,     d.pstamp, d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand, d.rcnt, d.AT,
                     d.pkt, d.objg, d.ract, d.cand_xchg, h->d_flag, d.cS, d.slo, d.shi, d.rlo, d.rhi,
                     (void*)d.cptr, (void*)d.rind, (void*)d.cval, (void*)d.rptr, (void*)d.cind,
                     (void*)d.rval, d.qcol, d.dstamp, d.rowvs, d.yvs, d.dw, d.dprev, (void*)d.srow,
@@ -345,11 +345,11 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.y, mm));
     A(dalloc(&d.yy, mm));
     A(dalloc(&d.blockmin, (size_t)(mm / 32 + mm / 256 + 4)));  // k_ftran_zr row + bump tiles
-    // a segment holds the candidates of every RSEG-th k_ftran_zr workgroup: at most
-    // 32 per row tile and 512 per bump tile, i.e. <= (m + k) / RSEG + 544 (k <= m)
-    d.rsegcap = (int32_t)(2 * mm / RSEG + 1024);
-    A(dalloc(&d.rcand, (size_t)RSEG * (size_t)d.rsegcap));
-    A(dalloc(&d.rseg, (size_t)RSEG * RSEG_STRIDE));
+    // pass-2 candidate regions: one per row tile (32 rows) and one per bump-tile
+    // wave (64 positions): <= m/32 + k/64 + 8 (k <= m)
+    d.rregs = (int32_t)(mm / 32 + mm / 64 + 10);
+    A(dalloc(&d.rcand, (size_t)d.rregs * RREG));
+    A(dalloc(&d.rcnt, (size_t)d.rregs));
     A(dalloc(&d.pkt, (size_t)(mm + 4)));
     A(dalloc(&d.objg, (size_t)h->n));
     A(dalloc(&d.ract, mm));
@@ -381,7 +381,11 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.cand, (size_t)((n + TILE_COLS - 1) / TILE_COLS) + (size_t)((mm + TILE_COLS - 1) / TILE_COLS) + 64));
     // one stamp pair per pricing workgroup: tiles, slack workgroups (<= m / 128 + 1)
     // and the apply workgroups (<= 2048 + 1024, launch_btran_price)
+#ifdef ELP_PDBG
+    A(dalloc(&d.pstamp, 4 * ((size_t)((n + TILE_COLS - 1) / TILE_COLS) + (size_t)(mm / 128 + 1) + 3072 + 64)));
+#else
     A(dalloc(&d.pstamp, 2 * ((size_t)((n + TILE_COLS - 1) / TILE_COLS) + (size_t)(mm / 128 + 1) + 3072 + 64)));
+#endif
     if (h->csc) A(dalloc(&d.qcol, mm));
     if (std::getenv("ELP_STAMPS")) A(dalloc(&d.dstamp, 16 * 64));
     A(dalloc(&d.ctl, 1));
@@ -393,7 +397,7 @@ static int alloc_all(elp_handle* h) {
     A(hipHostMalloc((void**)&h->hctl, sizeof(DevCtl)));
     // (AR padding columns [n, ldr) are read by the 128-column tiles but their
     //  results are discarded, so AR needs no clearing); Minv / work start clean
-    A(hipMemsetAsync(d.rseg, 0, (size_t)RSEG * RSEG_STRIDE * sizeof(int32_t), h->st));
+    A(hipMemsetAsync(d.rcnt, 0, (size_t)d.rregs * sizeof(int32_t), h->st));
     A(hipMemsetAsync(d.Minv, 0, (size_t)mm * (size_t)mm * sizeof(double), h->st));
     A(hipMemsetAsync(d.MinvT, 0, (size_t)mm * (size_t)mm * sizeof(double), h->st));
     if (d.qcol) A(hipMemsetAsync(d.qcol, 0, (size_t)mm * sizeof(double), h->st));
@@ -1052,6 +1056,37 @@ static int do_refactor(elp_handle* h, int k) {
     return 0;
 }
 
+#ifdef ELP_PDBG
+// diagnostic: the stamps of the last pricing launch of a chunk, appended to
+// $ELP_PDBG_FILE at the first poll at or past each multiple of $ELP_PDBG_ITER
+static void pdbg_dump(elp_handle* h, const DevCtl* c) {
+    const char* fe = getenv("ELP_PDBG_FILE");
+    const char* ie = getenv("ELP_PDBG_ITER");
+    if (!fe || !ie || !h->d.ptimer || h->phase != 2 || c->status != ST_RUN) return;
+    const int64_t every = atoll(ie);
+    static int64_t next = 0;
+    if (c->iter < next || every <= 0) return;
+    next = (c->iter / every + 1) * every;
+    const int grid = c->price_grid;
+    std::vector<unsigned long long> v((size_t)4 * grid);
+    if (hipMemcpy(v.data(), h->d.pstamp, v.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    unsigned long long t0 = ~0ull;
+    for (int b = 0; b < grid; ++b) t0 = std::min(t0, v[4 * b]);
+    FILE* f = fopen(fe, "a");
+    if (!f) return;
+    fprintf(f, "# iter %lld ny %d k %d grid %d ntiles %lld\n", (long long)c->iter, c->ny, c->k, grid,
+            (long long)((h->n + TILE_COLS - 1) / TILE_COLS));
+    for (int b = 0; b < grid; ++b) {
+        const unsigned long long* r = &v[4 * b];
+        const bool tile = r[1] > 16;
+        fprintf(f, "%d %s %lld %lld %lld %lld\n", b, tile ? "tile" : r[1] == 1 ? "apply" : "slack",
+                10 * (long long)(r[0] - t0), tile ? 10 * (long long)(r[1] - t0) : -1,
+                tile ? 10 * (long long)(r[2] - t0) : -1, 10 * (long long)(r[3] - t0));
+    }
+    fclose(f);
+}
+#endif
+
 // the polling loop; budget = iterations allowed in this call
 static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
     if (h->done) {
@@ -1192,6 +1227,9 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
         }
         h->dbg_wait += now_s() - t_enq1;
         h->stats.host_polls++;
+#ifdef ELP_PDBG
+        pdbg_dump(h, c);
+#endif
         const int32_t s = c->status;
         if (s == ST_COMMFAIL)
             return fail(ELP_E_COMM, "xGMI mailbox: a peer's record did not arrive within elp_control.mailbox_timeout");

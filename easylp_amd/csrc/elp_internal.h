@@ -33,11 +33,7 @@ enum : int32_t { ACT_NONE = 0, ACT_FLIP = 1, ACT_PIVOT = 2 };
 // slot chunks per pricing tile (one per wave); the oracle's PRICE_SPLIT must match
 constexpr int PRICE_SPLIT = ELP_PRICE_SPLIT;
 constexpr int ZCHUNK = 32;      // bump positions per FTRAN-z partial
-// k_ftran_zr's Harris pass-2 candidates go to RSEG lists by workgroup index
-// (blockIdx % RSEG), each with its own counter line: RSEG times fewer atomics
-// queue on one address than with a single list (the result is the same: the
-// leaving variable is chosen by a total order)
-constexpr int RSEG = 8, RSEG_STRIDE = 32;
+constexpr int RREG = 64;  // pass-2 candidate slots per k_ftran_zr wave region
 constexpr int TILE_COLS = 128;  // columns per pricing workgroup (2 per lane)
 
 struct Plan {
@@ -167,9 +163,10 @@ struct Dev {
     double* objg;            // global objective (N), for c_S of foreign basic columns
     double* ract;            // row activities sum_j a_ij x_j of nonzero nonbasic columns
     CandX* cand_xchg;        // [world] local best candidates (all-gathered)
-    RCand* rcand;            // pass-2 candidates: RSEG segments of rsegcap each
-    int32_t* rseg;           // their counts, one per 128-byte line (stride RSEG_STRIDE)
-    int32_t rsegcap;
+    RCand* rcand;            // pass-2 candidates: one region of RREG slots per emitting
+                             // k_ftran_zr wave (row tile: wave 0; bump tile: every wave)
+    int32_t* rcnt;           // candidates in each region (written every iteration, no atomics)
+    int32_t rregs;           // regions allocated
     double *rlo, *rhi;       // per covered row: bounds of the covering unit variable
     int8_t* vstat;
     int8_t* rowvs;  // per row: the status its slack has whenever it is nonbasic

@@ -659,6 +659,17 @@ DEV bool apply_role(const Dev& d, int napply, int nb_minv) {
 }
 
 // ============================================================== pricing
+// ELP_PDBG (diagnostic builds only, tools/build_variant.sh): four stamps per
+// pricing workgroup -- start, control block in, sweep done, end -- so the host
+// can dump one launch's timeline (ELP_PDBG_ITER); slot 1 holds the role of a
+// non-tile workgroup (1 apply, 2 slacks)
+#ifdef ELP_PDBG
+constexpr int PSTRIDE = 4;
+#define PDBG(slot, v) do { if (d.ptimer && threadIdx.x == 0) d.pstamp[PSTRIDE * blockIdx.x + (slot)] = (v); } while (0)
+#else
+constexpr int PSTRIDE = 2;
+#define PDBG(slot, v) do {} while (0)
+#endif
 // Devex reference weights (oracle run_phase, price_rule 1): the last pivot's
 // ratio alpha_rj / alpha_rq = (d_j - d_j') / d_q from this pass's d_j' and the
 // previous pass's d_j, w_j = max(w_j, (alpha_rj / alpha_rq)^2 w_q) (capped);
@@ -764,6 +775,8 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
     __shared__ Cand red[PRICE_SPLIT];
     const int64_t ntiles = gridDim.x - napply - nsw;
     if ((int64_t)blockIdx.x >= ntiles) {
+        PDBG(1, (int)blockIdx.x >= (int)gridDim.x - napply ? 1ull : 2ull);
+        PDBG(2, 0ull);
         if (apply_role(d, napply, nb_minv)) return;
         if (d.ctl->status != ST_RUN) return;
         price_slacks<PRICE_THREADS>(d, ntiles, (int)(blockIdx.x - ntiles), nsw, red);  // a slack workgroup
@@ -805,6 +818,7 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
         KEEP(pf_c);
         return;
     }
+    PDBG(1, __builtin_amdgcn_s_memrealtime());
     const int devex = c->devex;
     const DevexIn dx = devex_in(c);
     const double dtol = c->tol_dual;
@@ -830,19 +844,24 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
         }
     }
     if (p < ny) {  // remainder: same order, loads issued together
+        // (y at clamped rows, unconditional: a load under the row test is
+        //  drained at the end of its block -- one round trip per row)
         dbl2 v[UNR];
+        double yv[UNR];
 #pragma unroll
-        for (int u = 0; u < UNR; ++u)
+        for (int u = 0; u < UNR; ++u) {
             v[u] = (p + S * u < ny) ? AR_LOAD(col + (size_t)(p + S * u) * TILE_COLS) : dbl2{0.0, 0.0};
+            yv[u] = yy[min(p + S * u, ny - 1)];
+        }
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
             if (p + S * u < ny) {
-                const double yv = yy[p + S * u];
-                acc0 = fma(v[u].x, yv, acc0);
-                acc1 = fma(v[u].y, yv, acc1);
+                acc0 = fma(v[u].x, yv[u], acc0);
+                acc1 = fma(v[u].y, yv[u], acc1);
             }
         }
     }
+    PDBG(2, __builtin_amdgcn_s_memrealtime());
     part[w][2 * lane] = acc0;
     part[w][2 * lane + 1] = acc1;
     __syncthreads();
@@ -874,14 +893,14 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
 template <int NT>
 DEV void pstamp_begin(const Dev& d) {
     if (d.ptimer && threadIdx.x == 0) {
-        d.pstamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+        d.pstamp[PSTRIDE * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
         if (blockIdx.x == 0) d.ctl->price_grid = (int32_t)gridDim.x;
     }
 }
 DEV void pstamp_end(const Dev& d) {
     if (!d.ptimer) return;
     __syncthreads();  // (every return path of the bodies is workgroup-uniform)
-    if (threadIdx.x == 0) d.pstamp[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) d.pstamp[PSTRIDE * blockIdx.x + PSTRIDE - 1] = __builtin_amdgcn_s_memrealtime();
 }
 
 __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int napply, int nb_minv, int nsw) {
@@ -1002,8 +1021,8 @@ DEV void price_timer_sum(const Dev& d, unsigned long long* red) {
     const int nwg = d.ctl->price_grid;
     unsigned long long lo = ~0ull, hi = 0;
     for (int t = threadIdx.x; t < nwg; t += NT) {
-        lo = min(lo, d.pstamp[2 * t]);
-        hi = max(hi, d.pstamp[2 * t + 1]);
+        lo = min(lo, d.pstamp[PSTRIDE * t]);
+        hi = max(hi, d.pstamp[PSTRIDE * t + PSTRIDE - 1]);
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
@@ -1132,7 +1151,6 @@ DEV Cand local_best(const Dev& d, int ncand, Cand* red) {
 DEV void entering_chosen(const Dev& d, const Cand& best) {
     DevCtl* c = d.ctl;
     const int ny = c->ny;
-    for (int sg = 0; sg < RSEG; ++sg) d.rseg[sg * RSEG_STRIDE] = 0;  // k_ftran_zr's candidate lists
     // algorithmic bytes of this pricing pass: AR sweep + c + status + y_Y + Yl
     c->price_bytes += price_pass_bytes(d, ny, c->devex);
     c->price_passes++;
@@ -1196,7 +1214,8 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw
     // then waits for these loads only, not for the prefetch behind them)
     const int32_t st0 = c->status;
     const int bland = c->bland, k = c->k;
-    const int64_t c_iter = c->iter, c_epoch = c->mb_epoch;
+    // (iter / mb_epoch are read by the p2p path only, after the min-loc: loaded
+    //  here, their registers were reused before the loads retired -> a full wait)
     const int32_t c_seq = c->plan_seq;
     // Everything that does not depend on the control block or on q goes out
     // first (bounded by the host's k_ub, masked below): the candidates of the
@@ -1259,7 +1278,7 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw
     if (d.p2p) {  // column-sharded: global min-loc over the xGMI mailbox
         __shared__ CandX s_rec[MAX_P2P];
         __shared__ int s_fail;
-        if (!p2p_exchange(d, best, bland, c_iter, c_epoch, s_rec, &s_fail)) return;
+        if (!p2p_exchange(d, best, bland, c->iter, c->mb_epoch, s_rec, &s_fail)) return;
     }
     if (best.j < 0) {
         if (blockIdx.x == 0 && tid == 0) c->status = ST_PHASE_OPT;
@@ -1506,22 +1525,27 @@ DEV double harris2(double g, double x, double l, double u, double pivtol) {
     return HUGE_VAL;
 }
 // keep entry e as a pass-2 candidate if its exact ratio <= the workgroup's
-// pass-1 minimum (the global minimum can only be smaller)
-DEV void emit_cand(const Dev& d, int var, int e, double g, double x, double l, double u, double bmin,
+// pass-1 minimum (the global minimum can only be smaller).  Wave-collective:
+// the wave's kept entries are compacted by ballot into its own region and the
+// count stored alongside -- no atomic, so nothing waits for a reply.
+DEV void emit_wave(const Dev& d, int region, int var, int e, double g, double x, double l, double u, double bmin,
                    double pivtol) {
-    if (var < 0) return;
-    const double r = harris2(g, x, l, u, pivtol);
-    if (!(r <= bmin) || r == HUGE_VAL) return;
-    const int seg = blockIdx.x & (RSEG - 1);
-    const int slot = atomicAdd(&d.rseg[seg * RSEG_STRIDE], 1);
-    RCand cd;
-    cd.g = g;
-    cd.r = r;
-    cd.l = l;
-    cd.u = u;
-    cd.var = var;
-    cd.e = e;
-    d.rcand[(size_t)seg * d.rsegcap + slot] = cd;
+    const double r = var >= 0 ? harris2(g, x, l, u, pivtol) : HUGE_VAL;
+    const bool keep = var >= 0 && r <= bmin && r != HUGE_VAL;
+    const unsigned long long mask = __ballot(keep);
+    const int lane = threadIdx.x & 63;
+    if (keep) {
+        const int slot = __popcll(mask & ((1ull << lane) - 1ull));
+        RCand cd;
+        cd.g = g;
+        cd.r = r;
+        cd.l = l;
+        cd.u = u;
+        cd.var = var;
+        cd.e = e;
+        d.rcand[(size_t)region * RREG + slot] = cd;
+    }
+    if (lane == 0) d.rcnt[region] = __popcll(mask);
 }
 
 // waves per row tile of k_ftran_zr (ZR_WAVES): 8, or 4 when the row tiles
@@ -1666,7 +1690,7 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
 #pragma unroll
             for (int off = 32; off >= 1; off >>= 1) bmin = fmin(bmin, __shfl_xor(bmin, off));
             if (lane == 0) d.blockmin[blockIdx.x] = bmin;
-            emit_cand(d, ve, i, ge, xe, le, he, bmin, pivtol);
+            emit_wave(d, blockIdx.x, ve, i, ge, xe, le, he, bmin, pivtol);  // region = row tile
         }
     } else {
         const int p = (blockIdx.x - nrt) * (64 * ZR_WAVES) + threadIdx.x;
@@ -1686,7 +1710,8 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
         bmin = red[0];
         for (int ww = 1; ww < ZR_WAVES; ++ww) bmin = fmin(bmin, red[ww]);
         if (threadIdx.x == 0) d.blockmin[blockIdx.x] = bmin;
-        emit_cand(d, ve, m + p, ge, xe, le, he, bmin, pivtol);
+        // region: nrt + (bump tile) * ZR_WAVES + wave
+        emit_wave(d, nrt + (blockIdx.x - nrt) * ZR_WAVES + w, ve, m + p, ge, xe, le, he, bmin, pivtol);
     }
 }
 
@@ -1738,7 +1763,7 @@ enum { SI_VSQ, SI_RPOS0, SI_YPOS0, SI_YLAST, SI_SLLAST, SI_RLLAST, SI_RPOSYL, SI
 // (the only update the next pricing sweep needs), workgroup 0 runs the loop-top
 // checks, and the rest of the update is deferred into the next pricing launch.
 __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int lds_row, int defer,
-                                               int nmain, int k_ub, int dslot) {
+                                               int nmain, int k_ub, int dslot, int nreg) {
     extern __shared__ __attribute__((aligned(16))) double asrow_lds[];  // [k]: A[lrow, S]
     __shared__ double dred[4];
     __shared__ Leave lred[4];
@@ -1758,7 +1783,8 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     //      status test below then waits for these alone, not for the prefetch
     DevCtl* c = d.ctl;
     const int32_t st0 = c->snap_status;  // (not c->status: see DevCtl::snap_status)
-    const int m = d.m, k = c->snap_k, q = c->q, ny = c->snap_ny;
+    const int m = d.m, k = c->snap_k, ny = c->snap_ny;
+    int q = c->q;  // (pinned below)
     const double sig = c->sig, dq = c->dq, wq = c->wq;
     const int bland = c->snap_bland, devex = c->devex;
     const int apos_c = c->snap_apos;
@@ -1793,17 +1819,23 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     }
     // entries of Rl past the real k are stale: range-checked before use
     const int rcol = ld_clamp(d.Rl, main_wg ? col : 0, k_ub);
-    // the pass-2 candidates k_ftran_zr emitted: RSEG lists, 32 threads per list
-    // (256 = RSEG * 32), the first 32 * PFQ entries of each, masked by its count
-    constexpr int PFQ = ELP_RATIO_PFQ;
-    static_assert(RSEG * 32 == 256, "k_ratio: 32 threads per candidate list");
-    const int sg = tid & (RSEG - 1), si = tid >> 3;
-    const RCand* segp = d.rcand + (size_t)sg * d.rsegcap;
-    const int scnt = d.rseg[sg * RSEG_STRIDE];
-    RCand rq[PFQ];
+    // the pass-2 candidates k_ftran_zr emitted, one region per emitting wave:
+    // thread t takes regions t and t + 256 (PFR), count and first PFQ entries
+    // prefetched (clamped, masked by the count at use)
+    constexpr int PFQ = ELP_RATIO_PFQ, PFR = 2;
+    int rcn[PFR];
+    RCand rq[PFR][PFQ];
 #pragma unroll
-    for (int t = 0; t < PFQ; ++t) rq[t] = ld_clamp(segp, si + 32 * t, d.rsegcap);
+    for (int s = 0; s < PFR; ++s) {
+        const int reg = min(tid + 256 * s, nreg - 1);
+        rcn[s] = d.rcnt[reg];
+#pragma unroll
+        for (int t = 0; t < PFQ; ++t) rq[s][t] = d.rcand[(size_t)reg * RREG + t];
+    }
     __builtin_amdgcn_sched_barrier(0);  // all of the above issued before any use
+    // q stays a vector value up to here: its scalar copy (loc_of) would otherwise
+    // be scheduled above the prefetch, which then waits for the control block
+    asm volatile("" : "+v"(q));
     if (st0 != ST_RUN) {  // no plan this iteration: k_update must not re-apply one
         if (blockIdx.x == 0 && threadIdx.x == 0) c->plan.action = ACT_NONE;
 #pragma unroll
@@ -1812,7 +1844,11 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         for (int t = 0; t < PFT; ++t) KEEP(trow[t]);
         KEEP(rcol);
 #pragma unroll
-        for (int t = 0; t < PFQ; ++t) KEEP(rq[t].r);
+        for (int s = 0; s < PFR; ++s) {
+            KEEP(rcn[s]);
+#pragma unroll
+            for (int t = 0; t < PFQ; ++t) KEEP(rq[s][t].r);
+        }
         return;
     }
     RSTAMP(1);
@@ -1877,9 +1913,18 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         leave_take(best, o, leave_better(o, best, bland));
     };
 #pragma unroll
-    for (int t = 0; t < PFQ; ++t)
-        if (si + 32 * t < scnt) consider(rq[t]);
-    for (int t = si + 32 * PFQ; t < scnt; t += 32) consider(segp[t]);  // long lists
+    for (int s = 0; s < PFR; ++s) {
+        const int reg = tid + 256 * s;
+        if (reg >= nreg) continue;
+#pragma unroll
+        for (int t = 0; t < PFQ; ++t)
+            if (t < rcn[s]) consider(rq[s][t]);
+        for (int t = PFQ; t < rcn[s]; ++t) consider(d.rcand[(size_t)reg * RREG + t]);  // long regions
+    }
+    for (int reg = tid + 256 * PFR; reg < nreg; reg += 256) {  // (huge m)
+        const int cnt = d.rcnt[reg];
+        for (int t = 0; t < cnt; ++t) consider(d.rcand[(size_t)reg * RREG + t]);
+    }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         Leave o = shfl_leave(best, off);
@@ -3024,7 +3069,7 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
             if (nar > ELP_NAR_MAX) nar = ELP_NAR_MAX;
         }
         k_ratio<<<nmain + nar, 256, lds_row ? lds : 0, st>>>(d, phase, nrt + nbt, lds_row, defer, (int)nmain,
-                                                           k_ub, dslot);
+                                                           k_ub, dslot, nrt + nbt * zw);
     }
     if (!defer) {
         unsigned nb_minv, nb;

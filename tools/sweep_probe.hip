@@ -86,6 +86,52 @@ __global__ void __launch_bounds__(64 * S) k_split(const double* __restrict__ AR,
     }
 }
 
+// one wave per column strip of 128/G*... columns: the G lane groups take the
+// row classes p = g (mod G) (the tile kernel's S waves folded into one wave),
+// W such waves per workgroup (independent strips).  Strip width = 128 / (G/... )
+// = 2 * 64 / G columns; dispatch granularity = W waves.
+template <int G, int UNR, int W>
+__global__ void __launch_bounds__(64 * W) k_strip(const double* __restrict__ AR, const double* __restrict__ yy,
+                                                 int ny, int cap, int nstrips, double* __restrict__ out) {
+    constexpr int LPR = 64 / G, SW = 2 * LPR, SPT = TC / SW;
+    __shared__ double part[W][G][SW];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int s = blockIdx.x * W + wv;
+    if (s >= nstrips) return;
+    const int tile = s / SPT, sub = s % SPT, g = lane / LPR, cl = lane % LPR;
+    const double* col = AR + (size_t)tile * cap * TC + sub * SW + 2 * cl;
+    double a0 = 0.0, a1 = 0.0;
+    int pb = 0;
+    for (; pb + G * UNR <= ny; pb += G * UNR) {
+        dbl2 v[UNR];
+        double y[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            v[u] = *reinterpret_cast<const dbl2*>(col + (size_t)(pb + g + G * u) * TC);
+            y[u] = yy[pb + g + G * u];
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            a0 = fma(v[u].x, y[u], a0);
+            a1 = fma(v[u].y, y[u], a1);
+        }
+    }
+    for (int p = pb + g; p < ny; p += G) {
+        const dbl2 v = *reinterpret_cast<const dbl2*>(col + (size_t)p * TC);
+        a0 = fma(v.x, yy[p], a0);
+        a1 = fma(v.y, yy[p], a1);
+    }
+    part[wv][g][2 * cl] = a0;
+    part[wv][g][2 * cl + 1] = a1;
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    if (lane < SW) {
+        double t = 0.0;
+        for (int i = 0; i < G; ++i) t += part[wv][i][lane];
+        out[(size_t)tile * TC + sub * SW + lane] = t;
+    }
+}
+
 // plain streaming read of the same bytes (copy-rate reference): grid-stride dbl2
 __global__ void k_stream(const dbl2* __restrict__ a, size_t n2, double* out) {
     double acc = 0.0;
@@ -116,7 +162,7 @@ static double time_us(F launch, int reps = 200) {
 
 int main(int argc, char** argv) {
     const int n = argc > 1 ? atoi(argv[1]) : 50000;
-    const int nys[] = {100, 268, 500};
+    const int nys[] = {100, 268, 500};  // (ny multiple of 4: the strip kernels' remainder is per group)
     const int cap = 1024;
     const int ntiles = (n + TC - 1) / TC;
     const size_t elems = (size_t)ntiles * cap * TC;
@@ -139,6 +185,15 @@ int main(int argc, char** argv) {
         rep("tile S8 U16", time_us([&] { k_tile<8, 16><<<ntiles, 512>>>(AR, yy, ny, cap, out); }));
         rep("tile S4 U8", time_us([&] { k_tile<4, 8><<<ntiles, 256>>>(AR, yy, ny, cap, out); }));
         rep("tile S2 U32", time_us([&] { k_tile<2, 32><<<ntiles, 128>>>(AR, yy, ny, cap, out); }));
+        {
+            const int ns4 = ntiles * 4, ns8 = ntiles * 8;
+            rep("strip G4 U16 W1", time_us([&] { k_strip<4, 16, 1><<<ns4, 64>>>(AR, yy, ny, cap, ns4, out); }));
+            rep("strip G4 U8 W1", time_us([&] { k_strip<4, 8, 1><<<ns4, 64>>>(AR, yy, ny, cap, ns4, out); }));
+            rep("strip G4 U16 W2", time_us([&] { k_strip<4, 16, 2><<<(ns4 + 1) / 2, 128>>>(AR, yy, ny, cap, ns4, out); }));
+            rep("strip G8 U16 W1", time_us([&] { k_strip<8, 16, 1><<<ns8, 64>>>(AR, yy, ny, cap, ns8, out); }));
+            rep("strip G8 U8 W1", time_us([&] { k_strip<8, 8, 1><<<ns8, 64>>>(AR, yy, ny, cap, ns8, out); }));
+            rep("strip G2 U16 W1", time_us([&] { k_strip<2, 16, 1><<<ntiles * 2, 64>>>(AR, yy, ny, cap, ntiles * 2, out); }));
+        }
         for (int R : {2, 3, 4, 6, 8})
             for (int s = 0; s < 2; ++s) {
                 char nm[64];
