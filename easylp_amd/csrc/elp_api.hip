@@ -382,7 +382,7 @@ static int alloc_all(elp_handle* h) {
     // one stamp pair per pricing workgroup: tiles, slack workgroups (<= m / 128 + 1)
     // and the apply workgroups (<= 2048 + 1024, launch_btran_price)
 #ifdef ELP_PDBG
-    A(dalloc(&d.pstamp, 4 * ((size_t)((n + TILE_COLS - 1) / TILE_COLS) + (size_t)(mm / 128 + 1) + 3072 + 64)));
+    A(dalloc(&d.pstamp, 6 * ((size_t)((n + TILE_COLS - 1) / TILE_COLS) + (size_t)(mm / 128 + 1) + 3072 + 64)));
 #else
     A(dalloc(&d.pstamp, 2 * ((size_t)((n + TILE_COLS - 1) / TILE_COLS) + (size_t)(mm / 128 + 1) + 3072 + 64)));
 #endif
@@ -1068,20 +1068,20 @@ static void pdbg_dump(elp_handle* h, const DevCtl* c) {
     if (c->iter < next || every <= 0) return;
     next = (c->iter / every + 1) * every;
     const int grid = c->price_grid;
-    std::vector<unsigned long long> v((size_t)4 * grid);
+    std::vector<unsigned long long> v((size_t)6 * grid);
     if (hipMemcpy(v.data(), h->d.pstamp, v.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
     unsigned long long t0 = ~0ull;
-    for (int b = 0; b < grid; ++b) t0 = std::min(t0, v[4 * b]);
+    for (int b = 0; b < grid; ++b) t0 = std::min(t0, v[6 * b]);
     FILE* f = fopen(fe, "a");
     if (!f) return;
     fprintf(f, "# iter %lld ny %d k %d grid %d ntiles %lld\n", (long long)c->iter, c->ny, c->k, grid,
             (long long)((h->n + TILE_COLS - 1) / TILE_COLS));
     for (int b = 0; b < grid; ++b) {
-        const unsigned long long* r = &v[4 * b];
+        const unsigned long long* r = &v[6 * b];
         const bool tile = r[1] > 16;
-        fprintf(f, "%d %s %lld %lld %lld %lld\n", b, tile ? "tile" : r[1] == 1 ? "apply" : "slack",
-                10 * (long long)(r[0] - t0), tile ? 10 * (long long)(r[1] - t0) : -1,
-                tile ? 10 * (long long)(r[2] - t0) : -1, 10 * (long long)(r[3] - t0));
+        auto rel = [&](int s) { return tile ? 10 * (long long)(r[s] - t0) : -1ll; };
+        fprintf(f, "%d %s %lld %lld %lld %lld %lld %lld\n", b, tile ? "tile" : r[1] == 1 ? "apply" : "slack",
+                10 * (long long)(r[0] - t0), rel(1), rel(2), rel(3), rel(4), 10 * (long long)(r[5] - t0));
     }
     fclose(f);
 }

@@ -111,14 +111,6 @@ DEV bool cand_better(const Cand& a, const Cand& b, int bland) {
     if (bland) return a.j < b.j;
     return a.score > b.score || (a.score == b.score && a.j < b.j);
 }
-DEV Cand shfl_cand(const Cand& c, int off) {
-    Cand o;
-    o.score = __shfl_xor(c.score, off);
-    o.d = __shfl_xor(c.d, off);
-    o.w = __shfl_xor(c.w, off);
-    o.j = __shfl_xor((long long)c.j, off);
-    return o;
-}
 // field-wise select (a whole-struct conditional copy of Cand was observed to
 // be miscompiled on gfx950: the d field kept its old value)
 DEV void cand_take(Cand& c, const Cand& o, bool take) {
@@ -127,14 +119,121 @@ DEV void cand_take(Cand& c, const Cand& o, bool take) {
     c.w = take ? o.w : c.w;
     c.j = take ? o.j : c.j;
 }
+// Cross-lane moves without LDS: DPP inside a row of 16 lanes (xor 1, xor 2,
+// half-row mirror, row mirror -- a butterfly over 16 lanes when each step
+// follows a full reduction of the previous group), ds_swizzle for xor 16, then
+// the two halves by readlane.
+template <int CTRL>
+DEV double dpp_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+DEV double swz16_f64(double v) {  // lane ^ 16 inside each half-wave
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_swizzle((int)b, 0x401F);
+    const int hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), 0x401F);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+DEV double readlane_f64(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+DEV long long readlane_i64(long long v, int l) {
+    const int lo = __builtin_amdgcn_readlane((int)v, l), hi = __builtin_amdgcn_readlane((int)(v >> 32), l);
+    return ((long long)hi << 32) | (long long)(unsigned)lo;
+}
+// wave-wide max (the result is uniform)
+DEV double wave_max_f64(double v) {
+    v = fmax(v, dpp_f64<0xB1>(v));   // quad_perm [1,0,3,2]: lane ^ 1
+    v = fmax(v, dpp_f64<0x4E>(v));   // quad_perm [2,3,0,1]: lane ^ 2
+    v = fmax(v, dpp_f64<0x141>(v));  // row_half_mirror: the other quad of the 8
+    v = fmax(v, dpp_f64<0x140>(v));  // row_mirror: the other 8 of the 16
+    v = fmax(v, swz16_f64(v));
+    return fmax(readlane_f64(v, 0), readlane_f64(v, 32));
+}
+// The best candidate of a wave whose candidate indices increase with the lane
+// (a pricing tile: lane l holds the better of its columns 2l, 2l+1).  The same
+// total order as cand_better: the highest score, then the lowest index -- the
+// lowest lane among the highest scores; Bland: the lowest valid lane.
+DEV Cand wave_best_mono(const Cand& c, int bland) {
+    const bool valid = c.j >= 0;
+    const unsigned long long vm = __ballot(valid);
+    Cand r;
+    r.j = -1;
+    r.score = 0.0;
+    r.d = 0.0;
+    r.w = 1.0;
+    if (vm == 0ull) return r;
+    int win;
+    if (bland) {
+        win = __ffsll((long long)vm) - 1;
+    } else {
+        const double smax = wave_max_f64(valid ? c.score : -1.0);
+        win = __ffsll((long long)__ballot(valid && c.score == smax)) - 1;
+    }
+    win = __builtin_amdgcn_readfirstlane(win);
+    r.score = readlane_f64(c.score, win);
+    r.d = readlane_f64(c.d, win);
+    r.w = readlane_f64(c.w, win);
+    r.j = readlane_i64((long long)c.j, win);
+    return r;
+}
+// wave-wide min (uniform result)
+DEV double wave_min_f64(double v) {
+    v = fmin(v, dpp_f64<0xB1>(v));
+    v = fmin(v, dpp_f64<0x4E>(v));
+    v = fmin(v, dpp_f64<0x141>(v));
+    v = fmin(v, dpp_f64<0x140>(v));
+    v = fmin(v, swz16_f64(v));
+    return fmin(readlane_f64(v, 0), readlane_f64(v, 32));
+}
+DEV int wave_min_i32(int v) {
+    v = min(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_ds_swizzle(v, 0x401F));
+    return min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 32));
+}
+// The lane holding the lowest index among the lanes of `mask` (non-empty):
+// usually one lane (no tie), else a min-reduction of the indices
+DEV int lowest_index_lane(unsigned long long mask, bool in, int idx) {
+    if (__popcll(mask) == 1) return __ffsll((long long)mask) - 1;
+    const int im = wave_min_i32(in ? idx : 0x7fffffff);
+    return __ffsll((long long)__ballot(in && idx == im)) - 1;
+}
+// the best candidate of a wave in cand_better's total order (highest score,
+// then lowest index; Bland: lowest index), without LDS
+DEV Cand wave_best(const Cand& c, int bland) {
+    const bool valid = c.j >= 0;
+    const unsigned long long vm = __ballot(valid);
+    Cand r;
+    r.j = -1;
+    r.score = 0.0;
+    r.d = 0.0;
+    r.w = 1.0;
+    if (vm == 0ull) return r;
+    unsigned long long mask = vm;
+    bool in = valid;
+    if (!bland) {
+        const double smax = wave_max_f64(valid ? c.score : -1.0);
+        in = valid && c.score == smax;
+        mask = __ballot(in);
+    }
+    const int win = __builtin_amdgcn_readfirstlane(lowest_index_lane(mask, in, (int)c.j));
+    r.score = readlane_f64(c.score, win);
+    r.d = readlane_f64(c.d, win);
+    r.w = readlane_f64(c.w, win);
+    r.j = readlane_i64((long long)c.j, win);
+    return r;
+}
 // block-wide argmax of candidates; result valid in every thread
 template <int NT>
 DEV Cand block_best(Cand c, int bland, Cand* lds) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const Cand o = shfl_cand(c, off);
-        cand_take(c, o, cand_better(o, c, bland));
-    }
+    c = wave_best(c, bland);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (lane == 0) lds[w] = c;
     __syncthreads();
@@ -147,8 +246,7 @@ DEV Cand block_best(Cand c, int bland, Cand* lds) {
 }
 template <int NT>
 DEV double block_min(double v, double* lds) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = fmin(v, __shfl_xor(v, off));
+    v = wave_min_f64(v);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (lane == 0) lds[w] = v;
     __syncthreads();
@@ -659,12 +757,13 @@ DEV bool apply_role(const Dev& d, int napply, int nb_minv) {
 }
 
 // ============================================================== pricing
-// ELP_PDBG (diagnostic builds only, tools/build_variant.sh): four stamps per
-// pricing workgroup -- start, control block in, sweep done, end -- so the host
+// ELP_PDBG (diagnostic builds only, tools/build_variant.sh): six stamps per
+// pricing workgroup -- start, control block in, wave 0's sweep done, every
+// wave's sweep done, epilogue before the argmin, end -- so the host
 // can dump one launch's timeline (ELP_PDBG_ITER); slot 1 holds the role of a
 // non-tile workgroup (1 apply, 2 slacks)
 #ifdef ELP_PDBG
-constexpr int PSTRIDE = 4;
+constexpr int PSTRIDE = 6;
 #define PDBG(slot, v) do { if (d.ptimer && threadIdx.x == 0) d.pstamp[PSTRIDE * blockIdx.x + (slot)] = (v); } while (0)
 #else
 constexpr int PSTRIDE = 2;
@@ -777,6 +876,8 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
     if ((int64_t)blockIdx.x >= ntiles) {
         PDBG(1, (int)blockIdx.x >= (int)gridDim.x - napply ? 1ull : 2ull);
         PDBG(2, 0ull);
+        PDBG(3, 0ull);
+        PDBG(4, 0ull);
         if (apply_role(d, napply, nb_minv)) return;
         if (d.ctl->status != ST_RUN) return;
         price_slacks<PRICE_THREADS>(d, ntiles, (int)(blockIdx.x - ntiles), nsw, red);  // a slack workgroup
@@ -786,13 +887,14 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
     constexpr int UNR = ELP_PRICE_UNR;  // rows in flight per wave: 16 KiB (32 measured slower)
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // the tile's per-column operands of the epilogue (status, cost, Devex weight
-    // and previous d): every wave loads, clamped, no branch to drain; waves 0-1
-    // use them
-    const int64_t jt = (int64_t)blockIdx.x * TILE_COLS + (threadIdx.x & (TILE_COLS - 1));
-    const int64_t jc = jt < d.n ? jt : 0;
-    const int8_t pf_vs = d.vstat[jc];
-    const double pf_c = d.cost[jc], pf_w = d.dw[jc], pf_dp = d.dprev[jc];
+    // the epilogue's per-column operands (status, cost, Devex weight, previous
+    // d) of columns 2 lane, 2 lane + 1 -- wave 0's: the other waves load element
+    // 0 (one line); clamped, no branch to drain
+    const int64_t jA = (int64_t)blockIdx.x * TILE_COLS + 2 * lane;
+    const int64_t jc0 = (w == 0 && jA < d.n) ? jA : 0, jc1 = (w == 0 && jA + 1 < d.n) ? jA + 1 : 0;
+    const int8_t pf_vs0 = d.vstat[jc0], pf_vs1 = d.vstat[jc1];
+    const double pf_c0 = d.cost[jc0], pf_w0 = d.dw[jc0], pf_dp0 = d.dprev[jc0];
+    const double pf_c1 = d.cost[jc1], pf_w1 = d.dw[jc1], pf_dp1 = d.dprev[jc1];
     // this tile's rows are contiguous: row p at col + p * TILE_COLS
     const double* col = d.AR + (size_t)blockIdx.x * (size_t)d.arcap * TILE_COLS + 2 * lane;
     const double* __restrict__ yy = d.yy;
@@ -815,7 +917,8 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
             KEEP(v0[u].x);
             KEEP(y0[u]);
         }
-        KEEP(pf_c);
+        KEEP(pf_c0);
+        KEEP(pf_c1);
         return;
     }
     PDBG(1, __builtin_amdgcn_s_memrealtime());
@@ -865,27 +968,35 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
     part[w][2 * lane] = acc0;
     part[w][2 * lane + 1] = acc1;
     __syncthreads();
-    Cand best;
-    best.j = -1;
-    best.score = 0.0;
-    best.d = 0.0;
-    best.w = 1.0;
-    if (threadIdx.x < TILE_COLS) {
-        const int64_t j = jt;
-        if (j < d.n) {
-            const int8_t vs = pf_vs;
-            if (vs != VS_BASIC && vs != VS_FIXED) {
-                double tot = 0.0;
+    PDBG(3, __builtin_amdgcn_s_memrealtime());
+    // the epilogue is wave 0's: lane l finishes columns 2l, 2l+1 (the classes
+    // added in order), takes the better of the two, and the wave reduces
+    // without LDS or a barrier
+    if (w != 0) return;
+    Cand cb[2];
 #pragma unroll
-                for (int ww = 0; ww < PRICE_SPLIT; ++ww) tot = tot + part[ww][threadIdx.x];
-                const double dj = pf_c - tot;
-                const double wj = devex ? devex_weight(d, dx, j, d.col0 + j, dj, pf_w, pf_dp) : 1.0;
-                best = price_cand(vs, dj, wj, devex, dtol, d.col0 + j);
-            }
+    for (int h = 0; h < 2; ++h) {
+        cb[h].j = -1;
+        cb[h].score = 0.0;
+        cb[h].d = 0.0;
+        cb[h].w = 1.0;
+        const int64_t j = jA + h;
+        const int8_t vs = h ? pf_vs1 : pf_vs0;
+        if (j < d.n && vs != VS_BASIC && vs != VS_FIXED) {
+            double tot = 0.0;
+#pragma unroll
+            for (int ww = 0; ww < PRICE_SPLIT; ++ww) tot = tot + part[ww][2 * lane + h];
+            const double dj = (h ? pf_c1 : pf_c0) - tot;
+            const double wj = devex ? devex_weight(d, dx, j, d.col0 + j, dj, h ? pf_w1 : pf_w0, h ? pf_dp1 : pf_dp0)
+                                    : 1.0;
+            cb[h] = price_cand(vs, dj, wj, devex, dtol, d.col0 + j);
         }
     }
-    best = block_best<PRICE_THREADS>(best, bland, red);
-    if (threadIdx.x == 0) d.cand[blockIdx.x] = best;
+    Cand best = cb[0];
+    cand_take(best, cb[1], cand_better(cb[1], cb[0], bland));
+    PDBG(4, __builtin_amdgcn_s_memrealtime());
+    best = wave_best_mono(best, bland);
+    if (lane == 0) d.cand[blockIdx.x] = best;
 }
 
 // the pricing-launch timer (Dev::ptimer): every workgroup stamps its start and
@@ -1736,16 +1847,29 @@ DEV void leave_take(Leave& c, const Leave& o, bool take) {
     c.var = take ? o.var : c.var;
     c.e = take ? o.e : c.e;
 }
-DEV Leave shfl_leave(const Leave& x, int off) {
-    Leave o;
-    o.ag = __shfl_xor(x.ag, off);
-    o.r = __shfl_xor(x.r, off);
-    o.g = __shfl_xor(x.g, off);
-    o.l = __shfl_xor(x.l, off);
-    o.u = __shfl_xor(x.u, off);
-    o.var = __shfl_xor(x.var, off);
-    o.e = __shfl_xor(x.e, off);
-    return o;
+// the best leaving candidate of a wave in leave_better's total order, without LDS
+DEV Leave wave_best_leave(const Leave& x, int bland) {
+    const bool valid = x.var >= 0;
+    const unsigned long long vm = __ballot(valid);
+    if (vm == 0ull) return x;  // every lane holds "none"
+    bool in;
+    if (bland) {
+        const double rmin = wave_min_f64(valid ? x.r : HUGE_VAL);
+        in = valid && x.r == rmin;
+    } else {
+        const double amax = wave_max_f64(valid ? x.ag : -1.0);
+        in = valid && x.ag == amax;
+    }
+    const int win = __builtin_amdgcn_readfirstlane(lowest_index_lane(__ballot(in), in, x.var));
+    Leave r;
+    r.ag = readlane_f64(x.ag, win);
+    r.r = readlane_f64(x.r, win);
+    r.g = readlane_f64(x.g, win);
+    r.l = readlane_f64(x.l, win);
+    r.u = readlane_f64(x.u, win);
+    r.var = __builtin_amdgcn_readlane(x.var, win);
+    r.e = __builtin_amdgcn_readlane(x.e, win);
+    return r;
 }
 
 // Scalars the pivot bookkeeping needs, fetched in parallel at kernel start.
@@ -1925,11 +2049,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         const int cnt = d.rcnt[reg];
         for (int t = 0; t < cnt; ++t) consider(d.rcand[(size_t)reg * RREG + t]);
     }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        Leave o = shfl_leave(best, off);
-        leave_take(best, o, leave_better(o, best, bland));
-    }
+    best = wave_best_leave(best, bland);
     if ((tid & 63) == 0) lred[tid >> 6] = best;
     __syncthreads();  // also publishes the prefetched scalars
     {

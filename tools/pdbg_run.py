@@ -38,14 +38,19 @@ for block in open(out).read().split("# ")[1:]:
     t0 = np.array([int(r[2]) for r in tile])
     t1 = np.array([int(r[3]) for r in tile])
     t2 = np.array([int(r[4]) for r in tile])
-    t3 = np.array([int(r[5]) for r in tile])
-    ap = np.array([int(r[5]) for r in rows if r[1] == "apply"])
+    t2a = np.array([int(r[5]) for r in tile])
+    t2b = np.array([int(r[6]) for r in tile])
+    t3 = np.array([int(r[7]) for r in tile])
+    ap = np.array([int(r[7]) for r in rows if r[1] == "apply"])
     ap0 = np.array([int(r[2]) for r in rows if r[1] == "apply"])
-    sl = np.array([int(r[5]) for r in rows if r[1] == "slack"])
+    sl = np.array([int(r[7]) for r in rows if r[1] == "slack"])
     print(head)
     print("  tile start  p50 %.2f max %.2f | ctl in p50 %.2f max %.2f | sweep done p50 %.2f p90 %.2f max %.2f |"
           " end p50 %.2f max %.2f (us)" % (pct(t0, 50), pct(t0, 100), pct(t1, 50), pct(t1, 100), pct(t2, 50),
                                             pct(t2, 90), pct(t2, 100), pct(t3, 50), pct(t3, 100)))
+    print("  all waves done - wave 0 p50 %.2f max %.2f | devex epilogue p50 %.2f max %.2f | argmin+store p50 %.2f max %.2f"
+          % (pct(t2a - t2, 50), pct(t2a - t2, 100), pct(t2b - t2a, 50), pct(t2b - t2a, 100), pct(t3 - t2b, 50),
+             pct(t3 - t2b, 100)))
     print("  sweep per tile (ctl in -> done) p50 %.2f max %.2f | apply n %d start max %.2f end p50 %.2f max %.2f |"
           " slack end max %.2f" % (pct(t2 - t1, 50), pct(t2 - t1, 100), len(ap), pct(ap0, 100), pct(ap, 50),
                                    pct(ap, 100), pct(sl, 100)))
