@@ -58,10 +58,22 @@ __global__ void k_gen_bc(uint64_t seed, int m, int64_t ncols, int64_t col0, int6
 }
 
 // ------------------------------------------------------------ helpers
-DEV double wave_tree(double v) {  // butterfly 32..1; lane 0 == oracle wave_dot tree
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off);
-    return v;
+// wave sum in the oracle's wave_dot tree (pairs of lanes, then pairs of pairs,
+// ... : offsets 1, 2, 4, ..., 32 ascending): DPP inside 16-lane rows (after
+// the quad sums every lane of a quad holds the same value, so the mirrors pair
+// whole groups like xor 4 / xor 8 would), ds_swizzle for xor 16, the halves by
+// readlane.  Uniform result.
+template <int CTRL>
+DEV double dpp_f64(double v);
+DEV double swz16_f64(double v);
+DEV double readlane_f64(double v, int l);
+DEV double wave_tree(double v) {
+    v = v + dpp_f64<0xB1>(v);
+    v = v + dpp_f64<0x4E>(v);
+    v = v + dpp_f64<0x141>(v);
+    v = v + dpp_f64<0x140>(v);
+    v = v + swz16_f64(v);
+    return readlane_f64(v, 0) + readlane_f64(v, 32);
 }
 DEV double unit_sign(const Dev& d, int var, int row) {  // var: global id
     return var >= d.N + d.m ? d.asgn[row] : 1.0;
@@ -1797,9 +1809,7 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
                 ve = u;
                 tmin = harris1(ge, xe, le, he, ptol, pivtol, bland);
             }
-            double bmin = tmin;
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) bmin = fmin(bmin, __shfl_xor(bmin, off));
+            const double bmin = wave_min_f64(tmin);
             if (lane == 0) d.blockmin[blockIdx.x] = bmin;
             emit_wave(d, blockIdx.x, ve, i, ge, xe, le, he, bmin, pivtol);  // region = row tile
         }
@@ -1813,9 +1823,7 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
             ve = d.Sl[p];
             tmin = harris1(ge, xe, le, he, ptol, pivtol, bland);
         }
-        double bmin = tmin;
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) bmin = fmin(bmin, __shfl_xor(bmin, off));
+        double bmin = wave_min_f64(tmin);
         if (lane == 0) red[w] = bmin;
         __syncthreads();
         bmin = red[0];

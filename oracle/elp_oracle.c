@@ -6,10 +6,10 @@
  * so that the HIP kernels (also -ffp-contract=off, explicit fma) produce
  * the same bits.  Reduction orders follow DESIGN.md "Reduction order
  * contract":
- *   price  : PRICE_SPLIT (2) slot classes p = w (mod PRICE_SPLIT), an fma chain per
+ *   price  : PRICE_SPLIT (4) slot classes p = w (mod PRICE_SPLIT), an fma chain per
  *            class in slot order, then the partials added in class order starting
  *            from 0.0 (PRICE_SPLIT)
- *   wave   : 64 lane-strided fma chains + butterfly 32,16,..,1 (wave_dot):
+ *   wave   : 64 lane-strided fma chains + pairwise tree, offsets 1,2,..,32 (wave_dot):
  *            FTRAN / BTRAN / B^-1 rows, phase-1 c_S correction, phase-1 sum
  *   zchunk : chunks of 32 bump positions, fma chain, sequential sum
  *   seq    : one fma chain in index order (row activities)
@@ -261,7 +261,15 @@ static inline double* MI(orc_t* s, int64_t r, int64_t c) {
     return &s->Minv[(size_t)r * (size_t)s->ldm + (size_t)c];
 }
 
-/* wave order: 64 lane-strided fma chains, then butterfly tree */
+/* the GPU's wave sum (elp_kernels.hip wave_tree): pairs of lanes, then pairs
+   of pairs, ... -- offsets 1, 2, 4, ..., 32 ascending; lane 0's value */
+static double wave_tree(double* lane) {
+    for (int off = 1; off < WAVE; off <<= 1)
+        for (int l = 0; l + off < WAVE; l += 2 * off) lane[l] = lane[l] + lane[l + off];
+    return lane[0];
+}
+
+/* wave order: 64 lane-strided fma chains, then the wave tree */
 static double wave_dot(int64_t len, const double* a, const double* b) {
     double lane[WAVE];
     for (int l = 0; l < WAVE; ++l) {
@@ -269,9 +277,7 @@ static double wave_dot(int64_t len, const double* a, const double* b) {
         for (int64_t i = l; i < len; i += WAVE) acc = fma(a[i], b[i], acc);
         lane[l] = acc;
     }
-    for (int off = WAVE / 2; off >= 1; off >>= 1)
-        for (int l = 0; l < off; ++l) lane[l] = lane[l] + lane[l + off];
-    return lane[0];
+    return wave_tree(lane);
 }
 
 /* z_i = sum_p A[i, S_p] * w_p in ZCHUNK order */
@@ -437,9 +443,7 @@ static double art_sum(const orc_t* s) {
             if (s->cover[i] >= s->n + s->m) acc = acc + s->xr[i];
         lane[l] = acc;
     }
-    for (int off = WAVE / 2; off >= 1; off >>= 1)
-        for (int l = 0; l < off; ++l) lane[l] = lane[l] + lane[l + off];
-    return lane[0];
+    return wave_tree(lane);
 }
 
 /* basic entry e: covered row e (< m) or bump position e - m */
