@@ -265,7 +265,7 @@ def sparse_rate(args, local, with_cpu):
            "time_to_optimal_s": tto, "status": st, "objective": sol.objval,
            "iterations_to_optimal": s2["iterations"], "bump_dim": s2["bump_dim"],
            "window": {"iterations": [100, 100 + it], "value": it / el if el > 0 else None}}
-    km = 12  # Klee-Minty cube (degenerate-path case)
+    km = 12  # Klee-Minty cube: Dantzig's exponential path (2^n - 1 pivots) on the unscaled cube
     rows, cols, vals = [], [], []
     for i in range(km):
         for j in range(i + 1):
@@ -276,15 +276,16 @@ def sparse_rate(args, local, with_cpu):
     K = sp.csc_matrix((vals, (rows, cols)), shape=(km, km))
     kb = np.array([5.0 ** (i + 1) for i in range(km)])
     kc = np.array([2.0 ** (km - 1 - j) for j in range(km)])
-    with Problem(km, km, device=local, pricing=args.rule) as pk:
+    with Problem(km, km, device=local, pricing=0, scaling=0) as pk:
         t0 = time.perf_counter()
         pk.load_csc(K.indptr, K.indices, K.data, np.ones(km, np.int32), kb, kc, maximize=True)
         kst = pk.solve()
         kt = time.perf_counter() - t0
         ks = pk.stats()
         kobj = pk.solution(kst).objval
-    out["klee_minty"] = {"n": km, "iterations": ks["iterations"], "seconds": kt,
-                         "objective": kobj, "expected": 5.0 ** km}
+    out["klee_minty"] = {"n": km, "pricing": "dantzig", "scaling": "off", "iterations": ks["iterations"],
+                         "expected_iterations": 2 ** km - 1, "seconds": kt, "objective": kobj,
+                         "expected": 5.0 ** km}
     if with_cpu:
         from oracle import solve_dense
         A = dense_of(cp, ri, v, m, n)
@@ -297,7 +298,7 @@ def sparse_rate(args, local, with_cpu):
                                "sample": "oracle/ (C, -O3, 1 thread, CSC order) iterations [%d, %d)" % (w, w + cit)}
         t0 = time.perf_counter()
         rk = solve_dense(K.toarray(), np.ones(km, np.int32), kb, kc, maximize=True, price_mode=1,
-                         price_rule=args.rule)
+                         price_rule=0, scaling=0)
         out["klee_minty"]["cpu_seconds"] = time.perf_counter() - t0
         out["klee_minty"]["cpu_iterations"] = rk.stats["iterations"]
     return out

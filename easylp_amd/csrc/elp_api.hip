@@ -58,6 +58,12 @@ struct elp_handle {
     hipStream_t st = nullptr;
     Dev d{};
     double* A_owned = nullptr;
+    // large buffers kept across reloads of the handle (a fresh hipMalloc of
+    // tens of GB right after a hipFree of the same size measured 0.4-3.7 s)
+    double* keep_A = nullptr;
+    size_t keep_A_bytes = 0, A_owned_bytes = 0;
+    double* keep_AT = nullptr;
+    size_t keep_AT_bytes = 0, AT_bytes = 0;
     size_t w_cap = 0;
     bool loaded = false, done = false;
     int maximize = 0;
@@ -126,8 +132,25 @@ extern "C" void elp_default_control(elp_control* c) {
 extern "C" const char* elp_last_error(void) { return g_err.c_str(); }
 extern "C" int32_t elp_abi_version(void) { return ELP_ABI_VERSION; }
 
-static void free_dev(elp_handle* h) {
+static void release_kept(elp_handle* h) {
+    if (h->keep_A) (void)hipFree(h->keep_A);
+    if (h->keep_AT) (void)hipFree(h->keep_AT);
+    h->keep_A = h->keep_AT = nullptr;
+    h->keep_A_bytes = h->keep_AT_bytes = 0;
+}
+
+// keep_big: a reload -- A's copy and A^T stay allocated for the next load
+static void free_dev(elp_handle* h, bool keep_big = false) {
     Dev& d = h->d;
+    if (keep_big) {
+        release_kept(h);
+        h->keep_A = h->A_owned;
+        h->keep_A_bytes = h->A_owned ? h->A_owned_bytes : 0;
+        h->keep_AT = d.AT;
+        h->keep_AT_bytes = d.AT ? h->AT_bytes : 0;
+        h->A_owned = nullptr;
+        d.AT = nullptr;
+    }
     void* ptrs[] = {h->A_owned, d.AR,  d.AS,    d.Minv,  d.W0,   d.W1,    d.b,     d.obj,
                     d.lb,       d.ub,  d.cost,  d.xval,  d.asgn, d.xr,    d.xs,    d.y,
                     d.t,        d.acol, d.aR,   d.alS,   d.alU,  d.zz,    d.zpart, d.vrow,
@@ -151,6 +174,20 @@ static void free_dev(elp_handle* h) {
 template <class T>
 static hipError_t dalloc(T** p, size_t count) {
     return hipMalloc((void**)p, (count ? count : 1) * sizeof(T));
+}
+
+// a buffer of `bytes`, the kept one when it is exactly that size
+static hipError_t take_or_alloc(double** p, size_t bytes, double** keep, size_t* keep_bytes) {
+    if (*keep && *keep_bytes == bytes) {
+        *p = *keep;
+        *keep = nullptr;
+        *keep_bytes = 0;
+        return hipSuccess;
+    }
+    if (*keep) (void)hipFree(*keep);
+    *keep = nullptr;
+    *keep_bytes = 0;
+    return hipMalloc((void**)p, bytes ? bytes : sizeof(double));  // (m = 0: kernels read element 0)
 }
 
 // ---------------------------------------------------------------- ngpu
@@ -727,6 +764,16 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
     // (only while the AR rows could still grow to a full copy of A beside it)
     size_t mem_free = 0, mem_total = 0;
     const size_t at_bytes = (size_t)m * (size_t)nl * sizeof(double);
+    if (!d.csc && d.A && !d.AT && at_bytes > 0 && h->keep_AT && h->keep_AT_bytes == at_bytes) {
+        d.AT = h->keep_AT;  // a reload of the same shape
+        h->keep_AT = nullptr;
+        h->keep_AT_bytes = 0;
+    }
+    if (h->keep_AT) {
+        (void)hipFree(h->keep_AT);
+        h->keep_AT = nullptr;
+        h->keep_AT_bytes = 0;
+    }
     if (!d.csc && d.A && !d.AT && at_bytes > 0 && hipMemGetInfo(&mem_free, &mem_total) == hipSuccess &&
         mem_free > 2 * at_bytes + ((size_t)1 << 30)) {
         if (hipMalloc((void**)&d.AT, at_bytes) != hipSuccess) {
@@ -734,6 +781,8 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
             (void)hipGetLastError();
         }
     }
+    h->AT_bytes = d.AT ? at_bytes : 0;
+    release_kept(h);  // whatever this load did not take
     load_mark(h, "A^T alloc");
     if (d.AT) HIPCHK(launch_transpose_A(d, h->st));
     load_mark(h, d.AT ? "A^T copy" : "A^T (none)");
@@ -781,7 +830,7 @@ static int prep_load(elp_handle* h, bool csc = false) {
     if (!h) return fail(ELP_E_ARG, "NULL handle");
     HIPCHK(hipSetDevice(h->dev));
     load_mark(h, nullptr);
-    if (h->loaded) free_dev(h);
+    if (h->loaded) free_dev(h, true);
     load_mark(h, "free previous");
     h->loaded = false;
     h->csc = csc;
@@ -814,7 +863,8 @@ extern "C" int elp_load_dense(elp_handle* h, const double* A, const int32_t* dir
     if (rc) return rc;
     const int64_t c0 = h->replicated ? 0 : h->col0, nc = h->replicated ? h->n : h->nloc;
     const size_t cnt = (size_t)h->m * (size_t)nc;
-    HIPCHK(dalloc(&h->A_owned, cnt));
+    HIPCHK(take_or_alloc(&h->A_owned, cnt * sizeof(double), &h->keep_A, &h->keep_A_bytes));
+    h->A_owned_bytes = cnt * sizeof(double);
     if (cnt)
         HIPCHK(hipMemcpyAsync(h->A_owned, A + (size_t)c0 * (size_t)h->m, cnt * sizeof(double),
                               hipMemcpyHostToDevice, h->st));
@@ -963,7 +1013,8 @@ extern "C" int elp_load_generated(elp_handle* h, uint64_t seed) {
     if (rc) return rc;
     const int64_t m = h->m, n = h->n;
     const int64_t c0 = h->replicated ? 0 : h->col0, nc = h->replicated ? n : h->nloc;
-    HIPCHK(dalloc(&h->A_owned, (size_t)m * (size_t)nc));
+    HIPCHK(take_or_alloc(&h->A_owned, (size_t)m * (size_t)nc * sizeof(double), &h->keep_A, &h->keep_A_bytes));
+    h->A_owned_bytes = (size_t)m * (size_t)nc * sizeof(double);
     double *db = nullptr, *dc = nullptr;
     HIPCHK(dalloc(&db, m));
     HIPCHK(dalloc(&dc, n));
@@ -1770,6 +1821,7 @@ extern "C" void elp_destroy(elp_handle* h) {
         fprintf(stderr, "elp: host enqueue %.4f s, poll wait %.4f s, polls %lld\n", h->dbg_enqueue,
                 h->dbg_wait, (long long)h->stats.host_polls);
     free_dev(h);
+    release_kept(h);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     h->comm.destroy();
     if (h->st) (void)hipStreamDestroy(h->st);

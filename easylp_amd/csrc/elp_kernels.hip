@@ -184,7 +184,8 @@ DEV Cand wave_best_mono(const Cand& c, int bland) {
         win = __ffsll((long long)vm) - 1;
     } else {
         const double smax = wave_max_f64(valid ? c.score : -1.0);
-        win = __ffsll((long long)__ballot(valid && c.score == smax)) - 1;
+        const unsigned long long mm = __ballot(valid && c.score == smax);
+        win = __ffsll((long long)(mm ? mm : vm)) - 1;  // (NaN scores only: the lowest valid lane)
     }
     win = __builtin_amdgcn_readfirstlane(win);
     r.score = readlane_f64(c.score, win);
@@ -234,6 +235,10 @@ DEV Cand wave_best(const Cand& c, int bland) {
         const double smax = wave_max_f64(valid ? c.score : -1.0);
         in = valid && c.score == smax;
         mask = __ballot(in);
+        if (mask == 0ull) {  // (NaN scores only) the lowest index among the valid lanes
+            in = valid;
+            mask = vm;
+        }
     }
     const int win = __builtin_amdgcn_readfirstlane(lowest_index_lane(mask, in, (int)c.j));
     r.score = readlane_f64(c.score, win);
@@ -1868,7 +1873,12 @@ DEV Leave wave_best_leave(const Leave& x, int bland) {
         const double amax = wave_max_f64(valid ? x.ag : -1.0);
         in = valid && x.ag == amax;
     }
-    const int win = __builtin_amdgcn_readfirstlane(lowest_index_lane(__ballot(in), in, x.var));
+    unsigned long long mask = __ballot(in);
+    if (mask == 0ull) {  // (NaN ratios only) the lowest variable among the valid lanes
+        in = valid;
+        mask = vm;
+    }
+    const int win = __builtin_amdgcn_readfirstlane(lowest_index_lane(mask, in, x.var));
     Leave r;
     r.ag = readlane_f64(x.ag, win);
     r.r = readlane_f64(x.r, win);
