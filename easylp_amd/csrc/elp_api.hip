@@ -424,7 +424,10 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.pstamp, 2 * ((size_t)((n + TILE_COLS - 1) / TILE_COLS) + (size_t)(mm / 128 + 1) + 3072 + 64)));
 #endif
     if (h->csc) A(dalloc(&d.qcol, mm));
-    if (std::getenv("ELP_STAMPS")) A(dalloc(&d.dstamp, 16 * 64));
+    if (std::getenv("ELP_STAMPS")) {
+        A(dalloc(&d.dstamp, 16 * 64));
+        d.stamp_wide = std::atoi(std::getenv("ELP_STAMPS")) >= 2;
+    }
     A(dalloc(&d.ctl, 1));
     A(dalloc(&d.trace, (size_t)(h->trace_cap > 0 ? 2 * h->trace_cap : 2)));
     if (e != hipSuccess) {
@@ -774,7 +777,11 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
         h->keep_AT = nullptr;
         h->keep_AT_bytes = 0;
     }
-    if (!d.csc && d.A && !d.AT && at_bytes > 0 && hipMemGetInfo(&mem_free, &mem_total) == hipSuccess &&
+    // the row-major copy for AR row appends: off unless ELP_USE_AT=1 -- r02 measured no
+    // difference with and without it (C3 and C4), and it doubles A's footprint (40 GB at
+    // C4, whose allocation alone took 0.4-3.7 s on some loads)
+    static const bool no_at = std::getenv("ELP_USE_AT") == nullptr;
+    if (!no_at && !d.csc && d.A && !d.AT && at_bytes > 0 && hipMemGetInfo(&mem_free, &mem_total) == hipSuccess &&
         mem_free > 2 * at_bytes + ((size_t)1 << 30)) {
         if (hipMalloc((void**)&d.AT, at_bytes) != hipSuccess) {
             d.AT = nullptr;
@@ -1269,8 +1276,10 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             if (h->stamp_sum.empty()) h->stamp_sum.assign(16, 0.0);
             for (int t = 0; t < chunk; ++t) {
                 const unsigned long long* r = &v[(size_t)t * 16];
+                // time base: the first workgroup's start (ELP_STAMPS=2), else workgroup 0's
+                const unsigned long long base = r[11] != ~0ull ? r[11] : r[0];
                 for (int i = 0; i < 11; ++i)
-                    if (r[i]) h->stamp_sum[i] += 10.0 * (double)(long long)(r[i] - r[11]);  // ns (100 MHz)
+                    if (r[i]) h->stamp_sum[i] += 10.0 * (double)(long long)(r[i] - base);  // ns (100 MHz)
                 for (int i = 13; i < 16; ++i)  // select kernel, relative to its workgroup 0's start
                     if (r[i] && r[12]) h->stamp_sum[i] += 10.0 * (double)(long long)(r[i] - r[12]);
                 h->stamp_n++;
@@ -1804,7 +1813,7 @@ extern "C" int elp_get_trace(elp_handle* h, int64_t* pairs, int64_t capacity, in
 
 extern "C" void elp_destroy(elp_handle* h) {
     if (h && h->stamp_n) {
-        std::fprintf(stderr, "k_ratio stamps (us after the first workgroup start, %lld iterations):",
+        std::fprintf(stderr, "k_ratio stamps (us after workgroup 0's start; ELP_STAMPS=2: the first workgroup's; %lld iterations):",
                      (long long)h->stamp_n);
         const char* nm[11] = {"wg0", "ctl", "pass1", "decide", "binv", "dual", "book", "end", "last_start",
                               "main_end", "ar_end"};

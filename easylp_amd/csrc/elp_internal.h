@@ -203,6 +203,7 @@ struct Dev {
     double* qcol;
     // debug (ELP_STAMPS): s_memrealtime stamps of k_ratio, 16 per chunk slot
     unsigned long long* dstamp;
+    int32_t stamp_wide, pad_sw;  // ELP_STAMPS=2: also the grid-wide (atomic) stamps
     // xGMI mailbox exchange (Comm::enable_p2p): the select kernel publishes this
     // rank's best candidate into every peer's slot and waits for all of them
     MboxRec* mbox;          // this rank's mailbox [2 parities][world]

@@ -1915,7 +1915,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     const int tid = threadIdx.x;
     const int col = blockIdx.x * 4 + (tid >> 6);
     const int lane = tid & 63;
-    if (d.dstamp && tid == 0) {
+    if (d.stamp_wide && tid == 0) {  // (ELP_STAMPS=2: grid-wide stamps, contended atomics)
         const unsigned long long t = __builtin_amdgcn_s_memrealtime();
         atomicMin(&d.dstamp[dslot * 16 + 11], t);
         atomicMax(&d.dstamp[dslot * 16 + 8], t);
@@ -2167,7 +2167,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
             if (rm_slot >= 0 && rm_slot != rm_last) d.AR[ar_at(d, rm_slot, j)] = d.AR[ar_at(d, rm_last, j)];
             if (ap_slot >= 0) d.AR[ar_at(d, ap_slot, j)] = a_row(d, ap_row, j);
         }
-        if (d.dstamp) {
+        if (d.stamp_wide) {
             __syncthreads();
             if (tid == 0) atomicMax(&d.dstamp[dslot * 16 + 10], __builtin_amdgcn_s_memrealtime());
         }
@@ -2270,7 +2270,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         if (slot >= 0) d.yy[slot] = yn;
     }
     RSTAMP(5);
-    if (d.dstamp) {
+    if (d.stamp_wide) {
         __syncthreads();
         if (tid == 0) atomicMax(&d.dstamp[dslot * 16 + 9], __builtin_amdgcn_s_memrealtime());
     }
