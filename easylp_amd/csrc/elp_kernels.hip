@@ -1909,8 +1909,6 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     extern __shared__ __attribute__((aligned(16))) double asrow_lds[];  // [k]: A[lrow, S]
     __shared__ double dred[4];
     __shared__ Leave lred[4];
-    __shared__ int s_action;
-    __shared__ Plan s_plan;
     __shared__ double s_wd;
     const int tid = threadIdx.x;
     const int col = blockIdx.x * 4 + (tid >> 6);
@@ -2275,6 +2273,32 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         if (tid == 0) atomicMax(&d.dstamp[dslot * 16 + 9], __builtin_amdgcn_s_memrealtime());
     }
     if (!lead) return;
+    // ---- the rows the deferred update reads -- vrow = Minv row p (A) / b (C)
+    //      over the pivot, colA = MinvT row a (C, D) -- by the whole workgroup,
+    //      from the rows prefetched at the decision, before thread 0's
+    //      bookkeeping (which they do not depend on) instead of after it
+    {
+        const int pc = pcx;
+        const double piv = pc == PC_A ? best.g * sig : t0_piv;  // the plan's piv (A: alS[p]; C: Minv[b][a])
+        if (pfv) {
+#pragma unroll
+            for (int t = 0; t < PFV; ++t) {
+                const int j = tid + 256 * t;
+                if (j >= k) continue;
+                if (pc == PC_A || pc == PC_C) d.vrow[j] = vr[t] / piv;
+                if (pc == PC_C || pc == PC_D) d.colA[j] = ca[t];
+            }
+        } else if (pc == PC_A) {
+            for (int j = tid; j < k; j += 256) d.vrow[j] = d.Minv[(size_t)lposx * d.ldm + j] / piv;
+        } else if (pc == PC_C) {
+            for (int j = tid; j < k; j += 256) {
+                d.vrow[j] = d.Minv[(size_t)lposx * d.ldm + j] / piv;
+                d.colA[j] = d.MinvT[(size_t)apos * d.ldm + j];
+            }
+        } else if (pc == PC_D) {
+            for (int j = tid; j < k; j += 256) d.colA[j] = d.MinvT[(size_t)apos * d.ldm + j];
+        }
+    }
     // ---- pivot: bookkeeping by thread 0 (stores only, plus Minv[b][a] in case C)
     if (tid == 0) {
         if (theta == 0.0) {
@@ -2461,35 +2485,8 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         c->plan = P;
         c->plan_seq = cs_seq + 1;
         if (defer) loop_top(P.pcase == PC_E && lrow != q - d.N ? ST_NUMFAIL : ST_RUN, cs_iter + 1, cs_since + 1);
-        s_plan = P;
-        s_action = P.pcase;
     }
     RSTAMP(6);
-    __syncthreads();
-    const Plan P = s_plan;
-    const int pc = s_action;
-    if (pfv) {  // rows prefetched after the decision (P.p = P.b = lpos, P.a = apos)
-#pragma unroll
-        for (int t = 0; t < PFV; ++t) {
-            const int j = tid + 256 * t;
-            if (j >= k) continue;
-            if (pc == PC_A || pc == PC_C) d.vrow[j] = vr[t] / P.piv;
-            if (pc == PC_C || pc == PC_D) d.colA[j] = ca[t];
-        }
-    } else if (pc == PC_A) {
-        for (int j = tid; j < k; j += 256) d.vrow[j] = d.Minv[(size_t)P.p * d.ldm + j] / P.piv;
-    } else if (pc == PC_C) {
-        for (int j = tid; j < k; j += 256) {
-            d.vrow[j] = d.Minv[(size_t)P.b * d.ldm + j] / P.piv;
-            d.colA[j] = d.MinvT[(size_t)P.a * d.ldm + j];
-        }
-    } else if (pc == PC_D) {
-        for (int j = tid; j < k; j += 256) d.colA[j] = d.MinvT[(size_t)P.a * d.ldm + j];
-    }
-    if (d.dstamp) {
-        __syncthreads();
-        RSTAMP(7);
-    }
 }
 
 // new value of bump-inverse element (i, j); old(r, c) reads the pre-update matrix
