@@ -1950,15 +1950,13 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     double bm[PFB], trow[PFT];
     // (unconditional, no branch around them: a load inside a conditional block
     //  is drained at the block's end; masks are applied where the values are used)
-#pragma unroll
-    for (int t = 0; t < PFB; ++t) bm[t] = ld_clamp(d.blockmin, tid + 256 * t, nblk);
-    {  // (AR-copy workgroups fetch row 0: harmless)
-        const double* row = d.MinvT + (size_t)(main_wg && col < k_ub ? col : 0) * d.ldm;
-#pragma unroll
-        for (int t = 0; t < PFT; ++t) trow[t] = ld_clamp(row, lane + 64 * t, k_ub);
-    }
+    // Issue order = the order of first use (vmcnt retires in issue order): Rl
+    // (its y is read right after the control block), the pass-1 minima, the
+    // pass-2 candidates, then this wave's MinvT row (the B^-1 row, last)
     // entries of Rl past the real k are stale: range-checked before use
     const int rcol = ld_clamp(d.Rl, main_wg ? col : 0, k_ub);
+#pragma unroll
+    for (int t = 0; t < PFB; ++t) bm[t] = ld_clamp(d.blockmin, tid + 256 * t, nblk);
     // the pass-2 candidates k_ftran_zr emitted, one region per emitting wave:
     // thread t takes regions t and t + 256 (PFR), count and first PFQ entries
     // prefetched (clamped, masked by the count at use)
@@ -1971,6 +1969,11 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         rcn[s] = d.rcnt[reg];
 #pragma unroll
         for (int t = 0; t < PFQ; ++t) rq[s][t] = d.rcand[(size_t)reg * RREG + t];
+    }
+    {  // (AR-copy workgroups fetch row 0: harmless)
+        const double* row = d.MinvT + (size_t)(main_wg && col < k_ub ? col : 0) * d.ldm;
+#pragma unroll
+        for (int t = 0; t < PFT; ++t) trow[t] = ld_clamp(row, lane + 64 * t, k_ub);
     }
     __builtin_amdgcn_sched_barrier(0);  // all of the above issued before any use
     // q stays a vector value up to here: its scalar copy (loc_of) would otherwise
