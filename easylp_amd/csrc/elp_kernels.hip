@@ -2302,15 +2302,18 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
             for (int j = tid; j < k; j += 256) d.colA[j] = d.MinvT[(size_t)apos * d.ldm + j];
         }
     }
-    // ---- pivot: bookkeeping by thread 0 (stores only, plus Minv[b][a] in case C)
-    if (tid == 0) {
+    // ---- pivot: bookkeeping, its stores split by destination over the four waves
+    //      (a store chain per wave; stores to one address stay in one wave, in order)
+    if ((tid & 63) == 0) {  // thread 0 of each wave: the same decisions, a quarter of the stores
+        const int wv = tid >> 6;  // (0: counters / statuses / control block, 1: bump lists,
+                                  //  2: Y list and covers, 3: plan record and duals)
         if (theta == 0.0) {
-            c->degenerate = cs_degen + 1;
-            c->ndegen = cs_ndegen + 1;
-            if (cs_ndegen + 1 >= cs_dswitch) c->bland = 1;
+            if (wv == 0) { c->degenerate = cs_degen + 1; }
+            if (wv == 0) { c->ndegen = cs_ndegen + 1; }
+            if (wv == 0) { if (cs_ndegen + 1 >= cs_dswitch) c->bland = 1; }
         } else {
-            c->ndegen = 0;
-            c->bland = 0;
+            if (wv == 0) { c->ndegen = 0; }
+            if (wv == 0) { c->bland = 0; }
         }
         const int lv = best.var;
         const int lrow = best.e < m ? best.e : -1;
@@ -2320,30 +2323,30 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         const bool leave_art = lv >= d.N + m;
         const int lvl = loc_of(d, lv);
         if (leave_art) {
-            d.lb[lvl] = 0.0;
-            d.ub[lvl] = 0.0;
-            d.vstat[lvl] = VS_FIXED;
-            d.xval[lvl] = 0.0;
+            if (wv == 0) { d.lb[lvl] = 0.0; }
+            if (wv == 0) { d.ub[lvl] = 0.0; }
+            if (wv == 0) { d.vstat[lvl] = VS_FIXED; }
+            if (wv == 0) { d.xval[lvl] = 0.0; }
         } else if (lvl >= 0) {  // a structural of another shard keeps no status here
-            d.vstat[lvl] = best.l == best.u ? VS_FIXED : at_lower ? VS_LOWER : VS_UPPER;
-            d.xval[lvl] = at_lower ? best.l : best.u;
+            if (wv == 0) { d.vstat[lvl] = best.l == best.u ? VS_FIXED : at_lower ? VS_LOWER : VS_UPPER; }
+            if (wv == 0) { d.xval[lvl] = at_lower ? best.l : best.u; }
         }
-        if (ql >= 0) d.vstat[ql] = VS_BASIC;
+        if (wv == 0) { if (ql >= 0) d.vstat[ql] = VS_BASIC; }
         if (devex && wq > DEVEX_RESET) {
             // restart the framework (oracle: every weight 1 now): the next pass
             // sets the weight of each column it prices; a column basic now is
             // priced again only after it leaves, which sets its weight (below)
-            if (!leave_art && lvl >= 0) d.dw[lvl] = 1.0;
-            c->dv_valid = 2;
+            if (wv == 0) { if (!leave_art && lvl >= 0) d.dw[lvl] = 1.0; }
+            if (wv == 0) { c->dv_valid = 2; }
         } else if (devex) {  // the leaving variable's weight; this pivot for the next pass
             double wl = wq / (best.g * best.g);
             if (wl < 1.0) wl = 1.0;
             if (wl > DEVEX_WMAX) wl = DEVEX_WMAX;
-            if (!leave_art && lvl >= 0) d.dw[lvl] = wl;
-            c->dv_valid = 1;
-            c->dv_lv = lv;
-            c->dv_dq = dq;
-            c->dv_wq = wq;
+            if (wv == 0) { if (!leave_art && lvl >= 0) d.dw[lvl] = wl; }
+            if (wv == 0) { c->dv_valid = 1; }
+            if (wv == 0) { c->dv_lv = lv; }
+            if (wv == 0) { c->dv_dq = dq; }
+            if (wv == 0) { c->dv_wq = wq; }
         }
         const double cq = sv_cq;
         Plan P;
@@ -2365,10 +2368,10 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
                 P.pcase = PC_A;
                 P.p = lpos;
                 P.piv = best.g * sig;  // alS[lpos]
-                d.Sl[lpos] = q;
-                d.cS[lpos] = cq;
-                d.slo[lpos] = lbq;
-                d.shi[lpos] = ubq;
+                if (wv == 1) { d.Sl[lpos] = q; }
+                if (wv == 1) { d.cS[lpos] = cq; }
+                if (wv == 1) { d.slo[lpos] = lbq; }
+                if (wv == 1) { d.shi[lpos] = ubq; }
             } else {  // case B
                 const int i = lrow;
                 P.pcase = PC_B;
@@ -2376,20 +2379,20 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
                 P.p = k;
                 // delta = acol_i - z_i = sigma_u * alU_i = sigma_u * sig * g (exact)
                 P.piv = unit_sign(d, lv, i) * (sig * best.g);
-                d.Rl[k] = i;
-                d.rpos[i] = k;
-                d.Sl[k] = q;
-                d.cS[k] = cq;
-                d.slo[k] = lbq;
-                d.shi[k] = ubq;
-                d.cover[i] = -1;
+                if (wv == 1) { d.Rl[k] = i; }
+                if (wv == 1) { d.rpos[i] = k; }
+                if (wv == 1) { d.Sl[k] = q; }
+                if (wv == 1) { d.cS[k] = cq; }
+                if (wv == 1) { d.slo[k] = lbq; }
+                if (wv == 1) { d.shi[k] = ubq; }
+                if (wv == 1) { d.cover[i] = -1; }
                 newk = k + 1;
                 if (!leave_art) {
                     P.y_ap_slot = nny;
                     P.y_ap_row = i;
-                    d.Yl[nny] = i;
-                    d.ypos[i] = nny;
-                    d.yvs[nny] = t0_rowvs;
+                    if (wv == 2) { d.Yl[nny] = i; }
+                    if (wv == 2) { d.ypos[i] = nny; }
+                    if (wv == 2) { d.yvs[nny] = t0_rowvs; }
                     nny++;
                 }
             }
@@ -2398,7 +2401,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
             const int a = apos_c;
             if (a < 0) {  // case E
                 P.pcase = PC_E;
-                if (lrow != i0) c->status = ST_NUMFAIL;
+                if (wv == 0) { if (lrow != i0) c->status = ST_NUMFAIL; }
             } else if (lpos >= 0) {  // case C
                 const int b = lpos;
                 P.pcase = PC_C;
@@ -2407,52 +2410,52 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
                 P.last = last;
                 P.piv = t0_piv;  // Minv[b][a]
                 if (b != last) {
-                    d.Sl[b] = sv_sllast;
-                    d.cS[b] = sv_csl;
-                    d.slo[b] = sv_slol;
-                    d.shi[b] = sv_shil;
+                    if (wv == 1) { d.Sl[b] = sv_sllast; }
+                    if (wv == 1) { d.cS[b] = sv_csl; }
+                    if (wv == 1) { d.slo[b] = sv_slol; }
+                    if (wv == 1) { d.shi[b] = sv_shil; }
                 }
                 if (a != last) {
                     const int rl = sv_rllast;
-                    d.Rl[a] = rl;
-                    d.rpos[rl] = a;
+                    if (wv == 1) { d.Rl[a] = rl; }
+                    if (wv == 1) { d.rpos[rl] = a; }
                 }
-                d.rpos[i0] = -1;
+                if (wv == 1) { d.rpos[i0] = -1; }
                 newk = k - 1;
             } else {  // case D
                 const int i1 = lrow;
                 P.pcase = PC_D;
                 P.a = a;
                 P.row = i1;
-                d.Rl[a] = i1;
-                d.rpos[i1] = a;
-                d.rpos[i0] = -1;
-                d.cover[i1] = -1;
+                if (wv == 1) { d.Rl[a] = i1; }
+                if (wv == 1) { d.rpos[i1] = a; }
+                if (wv == 1) { d.rpos[i0] = -1; }
+                if (wv == 1) { d.cover[i1] = -1; }
             }
             // the entering slack covers row i0
             P.i0 = i0;
-            d.cover[i0] = q;
-            d.rlo[i0] = lbq;
-            d.rhi[i0] = ubq;
+            if (wv == 2) { d.cover[i0] = q; }
+            if (wv == 2) { d.rlo[i0] = lbq; }
+            if (wv == 2) { d.rhi[i0] = ubq; }
             // row i0 leaves Y (its slack is basic now) ...
             const int sl = sv_ypos0, ylast = nny - 1;
             P.y_rm_slot = sl;
             P.y_rm_last = ylast;
             if (sl != ylast) {
                 const int moved = sv_ylast;
-                d.Yl[sl] = moved;
-                d.ypos[moved] = sl;
-                d.yvs[sl] = t0_yvslast;
+                if (wv == 2) { d.Yl[sl] = moved; }
+                if (wv == 2) { d.ypos[moved] = sl; }
+                if (wv == 2) { d.yvs[sl] = t0_yvslast; }
             }
-            d.ypos[i0] = -1;
+            if (wv == 2) { d.ypos[i0] = -1; }
             nny--;
             // ... and in case D the leaving slack's row joins it
             if (P.pcase == PC_D && !leave_art) {
                 P.y_ap_slot = nny;
                 P.y_ap_row = lrow;
-                d.Yl[nny] = lrow;
-                d.ypos[lrow] = nny;
-                d.yvs[nny] = t0_rowvs;
+                if (wv == 2) { d.Yl[nny] = lrow; }
+                if (wv == 2) { d.ypos[lrow] = nny; }
+                if (wv == 2) { d.yvs[nny] = t0_rowvs; }
                 nny++;
             }
         }
@@ -2465,13 +2468,13 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
                 yslot = P.y_rm_slot;  // the leaving row was the last Y row: moved into i0's slot
             if (P.pcase == PC_B) {
                 const double yn = dq / P.piv;
-                d.y[P.row] = yn;
-                d.yy[yslot] = yn;
+                if (wv == 3) { d.y[P.row] = yn; }
+                if (wv == 3) { d.yy[yslot] = yn; }
             } else if (P.pcase == PC_C || P.pcase == PC_D) {
-                d.y[P.i0] = 0.0;
+                if (wv == 3) { d.y[P.i0] = 0.0; }
                 if (P.pcase == PC_D) {
-                    d.y[P.row] = -wD;
-                    d.yy[yslot] = -wD;
+                    if (wv == 3) { d.y[P.row] = -wD; }
+                    if (wv == 3) { d.yy[yslot] = -wD; }
                 }
             }
             if (P.pcase >= PC_C) {  // C, D, E removed row i0 from Y
@@ -2479,15 +2482,15 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
                 // the owner wave of a bump row wrote its moved slot already
                 const bool owned = P.pcase != PC_E && sv_rposyl >= 0;
                 const bool special = P.pcase == PC_D && moved == P.row;
-                if (sl != ny - 1 && !owned && !special) d.yy[sl] = t0_ymoved;
+                if (wv == 3) { if (sl != ny - 1 && !owned && !special) d.yy[sl] = t0_ymoved; }
             }
         }
-        c->k = newk;
-        c->ny = nny;
-        c->since_refactor = cs_since + 1;
-        c->plan = P;
-        c->plan_seq = cs_seq + 1;
-        if (defer) loop_top(P.pcase == PC_E && lrow != q - d.N ? ST_NUMFAIL : ST_RUN, cs_iter + 1, cs_since + 1);
+        if (wv == 0) { c->k = newk; }
+        if (wv == 0) { c->ny = nny; }
+        if (wv == 0) { c->since_refactor = cs_since + 1; }
+        if (wv == 3) { c->plan = P; }
+        if (wv == 0) { c->plan_seq = cs_seq + 1; }
+        if (wv == 0) { if (defer) loop_top(P.pcase == PC_E && lrow != q - d.N ? ST_NUMFAIL : ST_RUN, cs_iter + 1, cs_since + 1); }
     }
     RSTAMP(6);
 }
