@@ -93,3 +93,25 @@ def test_ngpu_mip_and_refusals(gpu):
         assert p.solve() == 0
         with pytest.raises(ElpError, match="ngpu"):
             p.sensitivity()
+
+
+@pytest.mark.parametrize("replicate", [1, 2])
+def test_ngpu_larger_capped_window(gpu, replicate):
+    """the column-only variant (replicate = 2: the entering
+    column is exchanged every iteration) beyond toy sizes -- 2000 x 20000 on two
+    ranks, the first 400 pivots against the oracle's generated-A solve (scaled,
+    the default), plus the state both reach at the cap."""
+    from oracle import solve_generated
+    m, n, seed, cap = 2000, 20000, 9, 400
+    with gpu.Problem(m, n, ngpu=2, replicate=replicate, max_iter=cap) as p:
+        p.set_trace(cap)
+        p.load_generated(seed)
+        st = p.solve()
+        g = p.solution(st)
+        s = p.stats()
+    o = solve_generated(seed, m, n, trace_cap=cap, max_iter=cap)
+    assert st == o.status == 1  # the iteration cap: sub-optimal
+    assert s["iterations"] == o.stats["iterations"] == cap
+    np.testing.assert_array_equal(g.trace, o.trace)
+    np.testing.assert_array_equal(g.basis, o.basis)
+    assert g.objval == o.objval
