@@ -425,7 +425,7 @@ static int alloc_all(elp_handle* h) {
 #endif
     if (h->csc) A(dalloc(&d.qcol, mm));
     if (std::getenv("ELP_STAMPS")) {
-        A(dalloc(&d.dstamp, 16 * 64));
+        A(dalloc(&d.dstamp, DSTAMP_STRIDE * 64));
         d.stamp_wide = std::atoi(std::getenv("ELP_STAMPS")) >= 2;
     }
     A(dalloc(&d.ctl, 1));
@@ -1218,8 +1218,8 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
         if (chunk < 1) chunk = 1;
         const double bytes0 = c->price_bytes;
         if (h->d.dstamp) {  // debug: min-start slot at +inf, maxima at 0
-            std::vector<unsigned long long> init(16 * 64, 0ull);
-            for (int t = 0; t < 64; ++t) init[t * 16 + 11] = ~0ull;
+            std::vector<unsigned long long> init(DSTAMP_STRIDE * 64, 0ull);
+            for (int t = 0; t < 64; ++t) init[t * DSTAMP_STRIDE + 11] = ~0ull;
             HIPCHK(hipMemcpyAsync(h->d.dstamp, init.data(), init.size() * 8, hipMemcpyHostToDevice, h->st));
             HIPCHK(hipStreamSynchronize(h->st));
         }
@@ -1271,17 +1271,19 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
         }
         h->dbg_enqueue += t_enq1 - t_enq0;
         if (h->d.dstamp && c->status == ST_RUN && h->phase == 2) {
-            std::vector<unsigned long long> v(16 * 64);
+            std::vector<unsigned long long> v(DSTAMP_STRIDE * 64);
             HIPCHK(hipMemcpy(v.data(), h->d.dstamp, v.size() * 8, hipMemcpyDeviceToHost));
-            if (h->stamp_sum.empty()) h->stamp_sum.assign(16, 0.0);
+            if (h->stamp_sum.empty()) h->stamp_sum.assign(DSTAMP_STRIDE, 0.0);
             for (int t = 0; t < chunk; ++t) {
-                const unsigned long long* r = &v[(size_t)t * 16];
+                const unsigned long long* r = &v[(size_t)t * DSTAMP_STRIDE];
                 // time base: the first workgroup's start (ELP_STAMPS=2), else workgroup 0's
                 const unsigned long long base = r[11] != ~0ull ? r[11] : r[0];
                 for (int i = 0; i < 11; ++i)
                     if (r[i]) h->stamp_sum[i] += 10.0 * (double)(long long)(r[i] - base);  // ns (100 MHz)
                 for (int i = 13; i < 16; ++i)  // select kernel, relative to its workgroup 0's start
                     if (r[i] && r[12]) h->stamp_sum[i] += 10.0 * (double)(long long)(r[i] - r[12]);
+                for (int i = 17; i < 20; ++i)  // FTRAN-z, relative to its workgroup 0's start
+                    if (r[i] && r[16]) h->stamp_sum[i] += 10.0 * (double)(long long)(r[i] - r[16]);
                 h->stamp_n++;
             }
         }
@@ -1821,6 +1823,9 @@ extern "C" void elp_destroy(elp_handle* h) {
         std::fprintf(stderr, "\nk_select_ftran stamps (us after its workgroup 0 starts): ctl=%.2f decide=%.2f end=%.2f\n",
                      h->stamp_sum[13] / h->stamp_n / 1e3, h->stamp_sum[14] / h->stamp_n / 1e3,
                      h->stamp_sum[15] / h->stamp_n / 1e3);
+        std::fprintf(stderr, "k_ftran_zr stamps (us after its workgroup 0 starts): ctl=%.2f z=%.2f emitted=%.2f\n",
+                     h->stamp_sum[17] / h->stamp_n / 1e3, h->stamp_sum[18] / h->stamp_n / 1e3,
+                     h->stamp_sum[19] / h->stamp_n / 1e3);
     }
     if (!h) return;
     destroy_group(h);

@@ -1178,7 +1178,7 @@ DEV void price_timer_sum(const Dev& d, unsigned long long* red) {
 // ============================================================== select
 // debug stamps (Dev::dstamp, ELP_STAMPS): s_memrealtime at the phases of workgroup 0
 #define RSTAMP(i) do { if (d.dstamp && blockIdx.x == 0 && threadIdx.x == 0) \
-    d.dstamp[dslot * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+    d.dstamp[dslot * DSTAMP_STRIDE + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 constexpr int MAX_P2P = 64;  // ranks a mailbox exchange supports
 
 // xGMI mailbox min-loc (Dev::p2p, column-sharded with A replicated): workgroup
@@ -1341,7 +1341,7 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw
     // the control block first (vmcnt retires in issue order: the status test
     // then waits for these loads only, not for the prefetch behind them)
     const int32_t st0 = c->status;
-    const int bland = c->bland, k = c->k;
+    int bland = c->bland, k = c->k;  // (pinned below)
     // (iter / mb_epoch are read by the p2p path only, after the min-loc: loaded
     //  here, their registers were reused before the loads retired -> a full wait)
     const int32_t c_seq = c->plan_seq;
@@ -1373,6 +1373,7 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw
 #pragma unroll
     for (int t = 0; t < PFR; ++t) rl[t] = ld_clamp(d.Rl, tid + 256 * t, k_ub);
     __builtin_amdgcn_sched_barrier(0);  // all of the above issued before any use
+    asm volatile("" : "+v"(bland), "+v"(k));  // (their scalar copies stay below the prefetch)
     if (blockIdx.x == 0 && threadIdx.x == 0) c->applied_seq = c_seq;  // applied by k_price
     if (st0 != ST_RUN) {
 #pragma unroll
@@ -1684,9 +1685,10 @@ DEV void emit_wave(const Dev& d, int region, int var, int e, double g, double x,
 constexpr int ZR_ROWS = 32;   // rows per row tile: lane = row + 32 * half; each
                               // half-wave runs whole ZCHUNK chains (its own chunk)
 template <bool LDSZ, int ZR_WAVES>
-__global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int k_ub) {
+__global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int k_ub, int dslot) {
     extern __shared__ __attribute__((aligned(16))) double zlds[];  // [nch][ZR_ROWS]
     __shared__ double red[ZR_WAVES];
+    RSTAMP(16);
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r = lane & (ZR_ROWS - 1), hh = lane >> 5;
@@ -1699,7 +1701,7 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
     // then waits for these loads only)
     const DevCtl* c = d.ctl;
     const int32_t st0 = c->status;
-    const int k = c->k, q = c->q, bland = c->bland;
+    int k = c->k, q = c->q, bland = c->bland;  // (pinned below)
     const double sig = c->sig, ptol = c->tol_primal, pivtol = c->tol_pivot;
     const int ch0 = 2 * w + hh;
     double a0[ZCHUNK], s0[ZCHUNK];
@@ -1725,6 +1727,10 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
         he = d.rhi[i];
     }
     __builtin_amdgcn_sched_barrier(0);  // all of the above issued before any use
+    // the control-block integers stay vector values up to here: their scalar
+    // copies would otherwise be scheduled above the prefetch, which then waits
+    // for the control block's round trip (measured: 2.7 us to the status test)
+    asm volatile("" : "+v"(k), "+v"(q), "+v"(bland));
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) d.ctl->snap_status = st0;  // for k_ratio
     if (st0 != ST_RUN) {
 #pragma unroll
@@ -1735,6 +1741,7 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
         KEEP(xe);
         return;
     }
+    RSTAMP(17);
     const int m = d.m;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         d.ctl->snap_k = k;
@@ -1803,6 +1810,7 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
             }
             zp[ch * ZR_ROWS + r] = acc;
         }
+        RSTAMP(18);
         __syncthreads();
         if (w == 0) {
             if (hh == 0 && i < m && u >= 0) {
@@ -1817,6 +1825,7 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
             const double bmin = wave_min_f64(tmin);
             if (lane == 0) d.blockmin[blockIdx.x] = bmin;
             emit_wave(d, blockIdx.x, ve, i, ge, xe, le, he, bmin, pivtol);  // region = row tile
+            RSTAMP(19);
         }
     } else {
         const int p = (blockIdx.x - nrt) * (64 * ZR_WAVES) + threadIdx.x;
@@ -1915,8 +1924,8 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     const int lane = tid & 63;
     if (d.stamp_wide && tid == 0) {  // (ELP_STAMPS=2: grid-wide stamps, contended atomics)
         const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-        atomicMin(&d.dstamp[dslot * 16 + 11], t);
-        atomicMax(&d.dstamp[dslot * 16 + 8], t);
+        atomicMin(&d.dstamp[dslot * DSTAMP_STRIDE + 11], t);
+        atomicMax(&d.dstamp[dslot * DSTAMP_STRIDE + 8], t);
     }
     RSTAMP(0);
     // ---- the control block first: vmcnt retires loads in issue order, so the
@@ -2170,7 +2179,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         }
         if (d.stamp_wide) {
             __syncthreads();
-            if (tid == 0) atomicMax(&d.dstamp[dslot * 16 + 10], __builtin_amdgcn_s_memrealtime());
+            if (tid == 0) atomicMax(&d.dstamp[dslot * DSTAMP_STRIDE + 10], __builtin_amdgcn_s_memrealtime());
         }
         return;
     }
@@ -2273,7 +2282,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     RSTAMP(5);
     if (d.stamp_wide) {
         __syncthreads();
-        if (tid == 0) atomicMax(&d.dstamp[dslot * 16 + 9], __builtin_amdgcn_s_memrealtime());
+        if (tid == 0) atomicMax(&d.dstamp[dslot * DSTAMP_STRIDE + 9], __builtin_amdgcn_s_memrealtime());
     }
     if (!lead) return;
     // ---- the rows the deferred update reads -- vrow = Minv row p (A) / b (C)
@@ -3190,9 +3199,9 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     const int nbt = (int)cdiv(k_ub, 64 * zw);
     {
         // + 1: the snapshot workgroup
-        if (zw == 4) k_ftran_zr<true, 4><<<nrt + nbt + 1, 256, lds, st>>>(d, nrt, k_ub);
-        else if (ldsz) k_ftran_zr<true, 8><<<nrt + nbt + 1, 512, lds, st>>>(d, nrt, k_ub);
-        else k_ftran_zr<false, 8><<<nrt + nbt + 1, 512, 0, st>>>(d, nrt, k_ub);
+        if (zw == 4) k_ftran_zr<true, 4><<<nrt + nbt + 1, 256, lds, st>>>(d, nrt, k_ub, dslot);
+        else if (ldsz) k_ftran_zr<true, 8><<<nrt + nbt + 1, 512, lds, st>>>(d, nrt, k_ub, dslot);
+        else k_ftran_zr<false, 8><<<nrt + nbt + 1, 512, 0, st>>>(d, nrt, k_ub, dslot);
     }
     // ratio test + (cases B/D) B^-1 row: one workgroup per 4 bump columns;
     // phase 2 adds the AR-copy workgroups and defers the rest of the update
