@@ -1333,6 +1333,7 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles, int nsw) {
 // slack candidates itself (a total order: all agree), gathers a_R into LDS and
 // computes alpha_S for its 4 bump rows (one wave per row, wave order).
 // Workgroup 0 publishes q.  Saves a launch and the single-workgroup select.
+template <int PFM>  // Minv values per lane held in registers (k <= 64 PFM): 8 or 16 by the host's bound
 __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw, int k_ub, int dslot) {
     extern __shared__ __attribute__((aligned(16))) double aRs[];  // [k]
     __shared__ Cand red[4];
@@ -1350,7 +1351,6 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw
     // tiles and of the slacks (candidates [ntiles, ntiles + nsw), k_price's slack workgroups),
     // this wave's row of Minv, the R list.  After the min-loc only the a_R
     // gather is left.
-    constexpr int PFM = 8;  // Minv values per lane held in registers (k <= 512)
     constexpr int PFR = 4;  // R-list entries per thread (k <= 1024)
     constexpr int PFC = 4;  // candidates per thread (<= 1023 tiles)
     const int ncand = ntiles + nsw;
@@ -1684,9 +1684,13 @@ DEV void emit_wave(const Dev& d, int region, int var, int e, double g, double x,
 // forms a chunk does not change the arithmetic (chunk sums added in order).
 constexpr int ZR_ROWS = 32;   // rows per row tile: lane = row + 32 * half; each
                               // half-wave runs whole ZCHUNK chains (its own chunk)
-template <bool LDSZ, int ZR_WAVES>
+// ALS: alpha_S staged once per workgroup in LDS (after the z partials) instead
+// of every lane loading the chunk's 32 values itself (half the VMEM instructions
+// and 64 fewer VGPRs); needs k_ub <= ZR_PA * threads
+constexpr int ZR_PA = 4;
+template <bool LDSZ, int ZR_WAVES, bool ALS>
 __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int k_ub, int dslot) {
-    extern __shared__ __attribute__((aligned(16))) double zlds[];  // [nch][ZR_ROWS]
+    extern __shared__ __attribute__((aligned(16))) double zlds[];  // [nch_ub][ZR_ROWS], then (ALS) [k_ub] alpha_S
     __shared__ double red[ZR_WAVES];
     RSTAMP(16);
     const int lane = threadIdx.x & 63;
@@ -1704,15 +1708,19 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
     int k = c->k, q = c->q, bland = c->bland;  // (pinned below)
     const double sig = c->sig, ptol = c->tol_primal, pivtol = c->tol_pivot;
     const int ch0 = 2 * w + hh;
-    double a0[ZCHUNK], s0[ZCHUNK];
+    double a0[ZCHUNK], s0[ALS ? 1 : ZCHUNK], pa[ALS ? ZR_PA : 1];
     const bool row_tile = (int)blockIdx.x < nrt;
+    if constexpr (ALS) {  // this thread's share of alpha_S, staged in LDS below
+#pragma unroll
+        for (int t = 0; t < ZR_PA; ++t) pa[t] = ld_clamp(d.alS, (int)threadIdx.x + (int)blockDim.x * t, k_ub);
+    }
     if (row_tile && ch0 * ZCHUNK < k_ub && i < d.m) {
         const double* col = d.AS + (size_t)(ch0 * ZCHUNK) * mm + i;
 #pragma unroll
         for (int t = 0; t < ZCHUNK; ++t) {
             const bool in = ch0 * ZCHUNK + t < k_ub;
             a0[t] = in ? col[(size_t)t * mm] : 0.0;
-            s0[t] = in ? d.alS[ch0 * ZCHUNK + t] : 0.0;
+            if constexpr (!ALS) s0[t] = in ? d.alS[ch0 * ZCHUNK + t] : 0.0;
         }
     }
     // likewise wave 0's epilogue operands (independent of q and z)
@@ -1734,9 +1742,13 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) d.ctl->snap_status = st0;  // for k_ratio
     if (st0 != ST_RUN) {
 #pragma unroll
-        for (int t = 0; t < ZCHUNK; ++t) {
-            KEEP(a0[t]);
-            KEEP(s0[t]);
+        for (int t = 0; t < ZCHUNK; ++t) KEEP(a0[t]);
+        if constexpr (!ALS) {
+#pragma unroll
+            for (int t = 0; t < ZCHUNK; ++t) KEEP(s0[t]);
+        } else {
+#pragma unroll
+            for (int t = 0; t < ZR_PA; ++t) KEEP(pa[t]);
         }
         KEEP(xe);
         return;
@@ -1776,6 +1788,15 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
     const int nch = (k + ZCHUNK - 1) / ZCHUNK;
     // z partials of this tile's rows: LDS, or (huge bumps) a private slice of zpart
     double* zp = LDSZ ? zlds : d.zpart + (size_t)blockIdx.x * ZR_ROWS * (size_t)nch;
+    double* als = zlds + (size_t)((k_ub + ZCHUNK - 1) / ZCHUNK) * ZR_ROWS;  // (ALS)
+    if constexpr (ALS) {
+#pragma unroll
+        for (int t = 0; t < ZR_PA; ++t) {
+            const int p = (int)threadIdx.x + (int)blockDim.x * t;
+            if (p < k) als[p] = pa[t];
+        }
+        __syncthreads();
+    }
     if (row_tile) {
         double aiq = 0.0;
         if (u >= 0) aiq = q >= d.N ? (i == q - d.N ? 1.0 : 0.0) : qcol_at(d, qcolumn(d, q), q, i);
@@ -1785,30 +1806,29 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
                 const int len = min(ZCHUNK, k - ch0 * ZCHUNK);
 #pragma unroll
                 for (int t = 0; t < ZCHUNK; ++t)
-                    if (t < len) acc = fma(a0[t], s0[t], acc);
+                    if (t < len) acc = fma(a0[t], ALS ? als[ch0 * ZCHUNK + t] : s0[t], acc);
             }
             zp[ch0 * ZR_ROWS + r] = acc;
         }
+        // later chunks (k > 2 ZR_WAVES ZCHUNK): every load unconditional at a
+        // clamped row / position -- a load under a lane or position test is
+        // drained at the end of its block, one round trip per position in the
+        // last, partial chunk (measured: FTRAN-z 21 us at 10 000 x 500 000, k 529)
         for (int ch = ch0 + 2 * ZR_WAVES; ch < nch; ch += 2 * ZR_WAVES) {
-            const int c0 = ch * ZCHUNK, c1 = min(k, c0 + ZCHUNK);
-            double acc = 0.0;
-            if (i < m) {
-                const double* col = d.AS + (size_t)c0 * mm + i;
-                double a[ZCHUNK];  // the whole chunk in flight
-                if (c1 - c0 == ZCHUNK) {
+            const int c0 = ch * ZCHUNK, len = min(ZCHUNK, k - c0);
+            const double* col = d.AS + (size_t)c0 * mm + (i < m ? i : 0);
+            double a[ZCHUNK], s[ALS ? 1 : ZCHUNK];  // the whole chunk in flight
 #pragma unroll
-                    for (int t = 0; t < ZCHUNK; ++t) a[t] = col[(size_t)t * mm];
-#pragma unroll
-                    for (int t = 0; t < ZCHUNK; ++t) acc = fma(a[t], d.alS[c0 + t], acc);
-                } else {
-#pragma unroll
-                    for (int t = 0; t < ZCHUNK; ++t) a[t] = (c0 + t < c1) ? col[(size_t)t * mm] : 0.0;
-#pragma unroll
-                    for (int t = 0; t < ZCHUNK; ++t)
-                        if (c0 + t < c1) acc = fma(a[t], d.alS[c0 + t], acc);
-                }
+            for (int t = 0; t < ZCHUNK; ++t) {
+                const int tt = t < len ? t : len - 1;
+                a[t] = col[(size_t)tt * mm];
+                if constexpr (!ALS) s[t] = d.alS[c0 + tt];
             }
-            zp[ch * ZR_ROWS + r] = acc;
+            double acc = 0.0;
+#pragma unroll
+            for (int t = 0; t < ZCHUNK; ++t)
+                if (t < len) acc = fma(a[t], ALS ? als[c0 + t] : s[t], acc);
+            zp[ch * ZR_ROWS + r] = i < m ? acc : 0.0;
         }
         RSTAMP(18);
         __syncthreads();
@@ -1913,6 +1933,9 @@ enum { SI_VSQ, SI_RPOS0, SI_YPOS0, SI_YLAST, SI_SLLAST, SI_RLLAST, SI_RPOSYL, SI
 // Phase 2 (defer != 0): workgroups [nmain, gridDim.x) copy this pivot's AR rows
 // (the only update the next pricing sweep needs), workgroup 0 runs the loop-top
 // checks, and the rest of the update is deferred into the next pricing launch.
+// PFT: B^-1 row values per lane held in registers (k <= 64 PFT), 8 or 16 by the
+// host's bound on k (a longer row is read in a loop)
+template <int PFT>
 __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int lds_row, int defer,
                                                int nmain, int k_ub, int dslot, int nreg) {
     extern __shared__ __attribute__((aligned(16))) double asrow_lds[];  // [k]: A[lrow, S]
@@ -1932,11 +1955,12 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     //      status test below then waits for these alone, not for the prefetch
     DevCtl* c = d.ctl;
     const int32_t st0 = c->snap_status;  // (not c->status: see DevCtl::snap_status)
-    const int m = d.m, k = c->snap_k, ny = c->snap_ny;
-    int q = c->q;  // (pinned below)
+    const int m = d.m;
+    int k = c->snap_k, ny = c->snap_ny, q = c->q;  // (these five pinned below)
     const double sig = c->sig, dq = c->dq, wq = c->wq;
-    const int bland = c->snap_bland, devex = c->devex;
-    const int apos_c = c->snap_apos;
+    int bland = c->snap_bland;
+    const int devex = c->devex;
+    int apos_c = c->snap_apos;
     const bool lead = blockIdx.x == 0;
     // bookkeeping scalars, snapshot by k_ftran_zr (see DevCtl)
     const double sv_lbq = c->snap_lbq, sv_ubq = c->snap_ubq, sv_xq = c->snap_xq, sv_cq = c->snap_cq;
@@ -1947,13 +1971,10 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     //      out next (bounded by the host's k_ub, masked by the real k below):
     //      the pass-1 minima, this wave's row of MinvT (B^-1 row, cases B / D)
     //      and its bump row R_col (dual update)
-#ifndef ELP_RATIO_PFT
-#define ELP_RATIO_PFT 8
-#endif
 #ifndef ELP_RATIO_PFQ
 #define ELP_RATIO_PFQ 1  // (4: +0.5 us of k_ratio, rocprof A/B r02)
 #endif
-    constexpr int PFB = 4, PFT = ELP_RATIO_PFT;
+    constexpr int PFB = 4;
     const bool main_wg = (int)blockIdx.x < nmain;
     const bool pfb = nblk <= 256 * PFB, pft = k_ub <= 64 * PFT;
     double bm[PFB], trow[PFT];
@@ -1985,9 +2006,10 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         for (int t = 0; t < PFT; ++t) trow[t] = ld_clamp(row, lane + 64 * t, k_ub);
     }
     __builtin_amdgcn_sched_barrier(0);  // all of the above issued before any use
-    // q stays a vector value up to here: its scalar copy (loc_of) would otherwise
-    // be scheduled above the prefetch, which then waits for the control block
-    asm volatile("" : "+v"(q));
+    // the control-block integers stay vector values up to here: their scalar
+    // copies (loc_of, loop bounds) would otherwise be scheduled above the
+    // prefetch, which then waits for the control block
+    asm volatile("" : "+v"(q), "+v"(k), "+v"(ny), "+v"(bland), "+v"(apos_c));
     if (st0 != ST_RUN) {  // no plan this iteration: k_update must not re-apply one
         if (blockIdx.x == 0 && threadIdx.x == 0) c->plan.action = ACT_NONE;
 #pragma unroll
@@ -2221,7 +2243,14 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
     if (lrow_all >= 0 && k > 0) {
         // huge bumps: every workgroup writes the same values to d.vrow (benign)
         double* asrow = lds_row ? asrow_lds : d.vrow;
-        for (int j = tid; j < k; j += 256) asrow[j] = d.AS[(size_t)j * (size_t)m + lrow_all];
+        for (int j0 = tid; j0 < k; j0 += 1024) {  // 4 loads in flight per thread (k <= 1024: one pass)
+            double v[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) v[t] = d.AS[(size_t)min(j0 + 256 * t, k - 1) * (size_t)m + lrow_all];
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (j0 + 256 * t < k) asrow[j0 + 256 * t] = v[t];
+        }
         __syncthreads();
         if (col < k) {
             double acc = 0.0;
@@ -3195,13 +3224,29 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     // k <= 8192); larger bumps use a private slice of zpart per row tile
     const size_t lds = (size_t)cdiv(k_ub, ZCHUNK) * ZR_ROWS * sizeof(double);
     const bool ldsz = lds <= 64 * 1024 && !d.force_select;
-    const int zw = (ldsz && nrt > 256 && cdiv(k_ub, ZCHUNK) <= 8) ? 4 : 8;  // waves per row tile
+    static const int zw_env = getenv("ELP_ZW") ? atoi(getenv("ELP_ZW")) : 0;  // A/B override
+    int zw = (ldsz && nrt > 256 && cdiv(k_ub, ZCHUNK) <= 8) ? 4 : 8;  // waves per row tile
+    if (ldsz && (zw_env == 4 || zw_env == 8)) zw = zw_env;
     const int nbt = (int)cdiv(k_ub, 64 * zw);
+    // alpha_S in LDS beside the z partials when the half-waves run more than one
+    // chunk each (k_ub > 2 zw ZCHUNK) and it fits the prefetch (ZR_PA per thread):
+    // 10 000 x 500 000 at k 529: 18.8 -> 16.3 us; with one chunk per half-wave the
+    // registers win (the LDS round trip cost 0.8 us at 5000 x 50000, r02)
+    static const bool no_als = getenv("ELP_NO_ALS") != nullptr;  // A/B
+    const size_t lds_als = lds + (size_t)k_ub * sizeof(double);
+    const bool als = !no_als && ldsz && k_ub > 2 * zw * ZCHUNK && k_ub <= ZR_PA * 64 * zw && lds_als <= 64 * 1024;
     {
         // + 1: the snapshot workgroup
-        if (zw == 4) k_ftran_zr<true, 4><<<nrt + nbt + 1, 256, lds, st>>>(d, nrt, k_ub, dslot);
-        else if (ldsz) k_ftran_zr<true, 8><<<nrt + nbt + 1, 512, lds, st>>>(d, nrt, k_ub, dslot);
-        else k_ftran_zr<false, 8><<<nrt + nbt + 1, 512, 0, st>>>(d, nrt, k_ub, dslot);
+        if (als) {
+            if (zw == 4) k_ftran_zr<true, 4, true><<<nrt + nbt + 1, 256, lds_als, st>>>(d, nrt, k_ub, dslot);
+            else k_ftran_zr<true, 8, true><<<nrt + nbt + 1, 512, lds_als, st>>>(d, nrt, k_ub, dslot);
+        } else if (zw == 4) {
+            k_ftran_zr<true, 4, false><<<nrt + nbt + 1, 256, lds, st>>>(d, nrt, k_ub, dslot);
+        } else if (ldsz) {
+            k_ftran_zr<true, 8, false><<<nrt + nbt + 1, 512, lds, st>>>(d, nrt, k_ub, dslot);
+        } else {
+            k_ftran_zr<false, 8, false><<<nrt + nbt + 1, 512, 0, st>>>(d, nrt, k_ub, dslot);
+        }
     }
     // ratio test + (cases B/D) B^-1 row: one workgroup per 4 bump columns;
     // phase 2 adds the AR-copy workgroups and defers the rest of the update
@@ -3218,8 +3263,10 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
             nar = cdiv(d.n, 256);
             if (nar > ELP_NAR_MAX) nar = ELP_NAR_MAX;
         }
-        k_ratio<<<nmain + nar, 256, lds_row ? lds : 0, st>>>(d, phase, nrt + nbt, lds_row, defer, (int)nmain,
-                                                           k_ub, dslot, nrt + nbt * zw);
+        // (8 B^-1 values per lane in registers: 16 for k > 512 measured slower at
+        //  10 000 x 500 000, 16.5 vs 14.7 us -- the longer rows go through the loop)
+        k_ratio<8><<<nmain + nar, 256, lds_row ? lds : 0, st>>>(d, phase, nrt + nbt, lds_row, defer, (int)nmain,
+                                                               k_ub, dslot, nrt + nbt * zw);
     }
     if (!defer) {
         unsigned nb_minv, nb;
@@ -3239,7 +3286,7 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
         const size_t ldsz = lds > 64 ? lds : 64;  // the timer workgroup reduces in it
         // + the timer workgroup, + the CSC column-scatter workgroup
         const unsigned g = cdiv(k_ub > 0 ? k_ub : 1, 4) + (d.ptimer ? 1 : 0) + (d.csc ? 1 : 0);
-        k_select_ftran<<<g, 256, ldsz, st>>>(d, ntiles, nsw, k_ub, dslot);
+        k_select_ftran<8><<<g, 256, ldsz, st>>>(d, ntiles, nsw, k_ub, dslot);  // (16 measured no faster)
         return launch_iteration_tail(d, k_ub, phase, st, false, dslot);
     }
     k_select<<<1, 1024, 0, st>>>(d, ntiles, nsw);
