@@ -58,6 +58,22 @@ __global__ void k_gen_bc(uint64_t seed, int m, int64_t ncols, int64_t col0, int6
 }
 
 // ------------------------------------------------------------ helpers
+// lane-strided fma chain over x[0:len) . y[0:len) (lane l: x[l] y[l], then +64,
+// ... in order -- the oracle's wave_dot lanes), loads issued 8 at a time: a
+// plain loop waited for each load before issuing the next (k > 512 bumps)
+DEV double lane_chain(const double* __restrict__ x, const double* y, int len) {
+    const int lane = threadIdx.x & 63;
+    double acc = 0.0;
+    for (int j0 = lane; j0 < len; j0 += 64 * 8) {
+        double v[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = x[min(j0 + 64 * t, len - 1)];
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            if (j0 + 64 * t < len) acc = fma(v[t], y[j0 + 64 * t], acc);
+    }
+    return acc;
+}
 // wave sum in the oracle's wave_dot tree (pairs of lanes, then pairs of pairs,
 // ... : offsets 1, 2, 4, ..., 32 ascending): DPP inside 16-lane rows (after
 // the quad sums every lane of a quad holds the same value, so the mirrors pair
@@ -1457,7 +1473,7 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw
             if (lane + 64 * t < k) acc = fma(mrow[t], aRs[lane + 64 * t], acc);
     } else {
         const double* row = d.Minv + (size_t)pr * d.ldm;
-        for (int i = lane; i < k; i += 64) acc = fma(row[i], aRs[i], acc);
+        acc = lane_chain(row, aRs, k);
     }
     acc = wave_tree(acc);
     if (lane == 0) d.alS[pr] = acc;
@@ -1574,8 +1590,7 @@ __global__ void __launch_bounds__(256) k_select_xftran(Dev d) {
     const int lane = threadIdx.x & 63;
     if (p >= k) return;
     const double* row = d.Minv + (size_t)p * d.ldm;
-    double acc = 0.0;
-    for (int i = lane; i < k; i += 64) acc = fma(row[i], aRs[i], acc);
+    double acc = lane_chain(row, aRs, k);
     acc = wave_tree(acc);
     if (lane == 0) d.alS[p] = acc;
 }
@@ -2260,7 +2275,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
                     if (lane + 64 * t < k) acc = fma(trow[t], asrow[lane + 64 * t], acc);
             } else {
                 const double* row = d.MinvT + (size_t)col * d.ldm;
-                for (int j = lane; j < k; j += 64) acc = fma(row[j], asrow[j], acc);
+                acc = lane_chain(row, asrow, k);
             }
             acc = wave_tree(acc);
             // case B delta = acol_i - z_i = sigma_u * sig * g (exact)
@@ -2276,7 +2291,7 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
                     if (lane + 64 * t < k) acc = fma(arow[t], asrow[lane + 64 * t], acc);
             } else {
                 const double* row = d.MinvT + (size_t)apos * d.ldm;
-                for (int j = lane; j < k; j += 64) acc = fma(row[j], asrow[j], acc);
+                acc = lane_chain(row, asrow, k);
             }
             acc = wave_tree(acc);
             if (tid == 0) s_wd = dq / acc;
