@@ -572,12 +572,22 @@ __global__ void __launch_bounds__(256) k_scale_col(int m, int64_t ncols, const d
     for (int64_t j = blockIdx.x; j < ncols; j += gridDim.x) {
         const double* col = A + (size_t)j * (size_t)m;
         int mn = SCALE_EMPTY_MIN, mx = SCALE_EMPTY_MAX;
-        for (int i = threadIdx.x; i < m; i += 256) {
-            const double a = col[i];
-            if (a != 0.0) {
-                const int e = ilogb(a) + rho[i];
-                mn = min(mn, e);
-                mx = max(mx, e);
+        for (int i0 = threadIdx.x; i0 < m; i0 += 256 * 8) {  // 8 loads in flight per thread
+            double a[8];
+            int r[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int ii = min(i0 + 256 * u, m - 1);
+                a[u] = col[ii];
+                r[u] = rho[ii];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (i0 + 256 * u < m && a[u] != 0.0) {
+                    const int e = ilogb(a[u]) + r[u];
+                    mn = min(mn, e);
+                    mx = max(mx, e);
+                }
             }
         }
 #pragma unroll
@@ -618,12 +628,22 @@ __global__ void __launch_bounds__(256) k_scale_row_part(int m, int64_t ncols, co
     const int64_t j0 = (int64_t)blockIdx.y * SCALE_RCOLS;
     const int64_t j1 = j0 + SCALE_RCOLS < ncols ? j0 + SCALE_RCOLS : ncols;
     int mn = SCALE_EMPTY_MIN, mx = SCALE_EMPTY_MAX;
-    for (int64_t j = j0; j < j1; ++j) {
-        const double a = A[(size_t)j * (size_t)m + i];
-        if (a != 0.0) {
-            const int e = ilogb(a) + gam[j];
-            mn = min(mn, e);
-            mx = max(mx, e);
+    for (int64_t j = j0; j < j1; j += 8) {  // 8 loads in flight per thread
+        double a[8];
+        int g[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t jj = j + u < j1 ? j + u : j1 - 1;
+            a[u] = A[(size_t)jj * (size_t)m + i];
+            g[u] = gam[jj];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (j + u < j1 && a[u] != 0.0) {
+                const int e = ilogb(a[u]) + g[u];
+                mn = min(mn, e);
+                mx = max(mx, e);
+            }
         }
     }
     if (mx != SCALE_EMPTY_MAX) {
