@@ -230,6 +230,7 @@ def c4_config(args, lib, world, rank, local, barrier, dist):
             "time_to_optimal_s": el, "load_s": t_load,
             "value": s["iterations"] / el if el > 0 else None, "unit": "iterations/s (whole solve)",
             "bump_dim": s["bump_dim"], "y_rows": s["y_rows"], "refactors": s["refactors"],
+            "gj_refactors": s["gj_refactors"], "max_inv_resid": s["max_inv_resid"],
             "price_sweep": sweep}
 
 
@@ -360,6 +361,7 @@ def main():
     final = {"status": recs[-1][0] if recs else None, "iterations_to_optimal": last["iterations"],
              "objective": p.solution(recs[-1][0]).objval if recs else None,
              "bump_dim": last["bump_dim"], "y_rows": last["y_rows"], "refactors": last["refactors"],
+             "gj_refactors": last["gj_refactors"], "max_inv_resid": last["max_inv_resid"],
              "load_s": sum(s["seconds_load"] for s in stats) / max(len(stats), 1),
              "price_launches_per_solve": last["price_launches"]}
 

@@ -88,6 +88,7 @@ class ElpStats(ctypes.Structure):
         ("mip_nodes", ctypes.c_int64),
         ("mip_lp_iterations", ctypes.c_int64),
         ("price_launches", ctypes.c_int64),
+        ("max_inv_resid", ctypes.c_double),
     ]
 
 

@@ -1096,6 +1096,7 @@ static int do_refactor(elp_handle* h, int k) {
         bits = h->hctl->ns_emax_bits;
         double emax;
         std::memcpy(&emax, &bits, sizeof(emax));
+        if (h->ctl.refactor_mode == 0 && emax > h->stats.max_inv_resid) h->stats.max_inv_resid = emax;
         if (emax <= NS_TOL && h->ctl.refactor_mode == 0) {
             HIPCHK(launch_refactor_ns_update(h->d, k, h->st));
         } else {

@@ -131,6 +131,9 @@ typedef struct elp_stats {
     int64_t mip_lp_iterations; /* simplex iterations over all of them           */
     int64_t price_launches;    /* pricing-kernel launches enqueued (profilers:
                                   the dispatches of this handle's pricing kernel) */
+    double max_inv_resid;      /* drift of the maintained bump inverse: the
+                                  largest max|I - M Minv| a refactor measured
+                                  before correcting it (refactor_mode 0)        */
 } elp_stats;
 
 #define ELP_PROFILE_PRICE 2   /* elp_control.verbose bit: device-clock pricing timer */

@@ -53,6 +53,7 @@ class OrcStats(ctypes.Structure):
         ("seconds_at_mark", ctypes.c_double),
         ("gj_refactors", ctypes.c_int64),
         ("devex_resets", ctypes.c_int64),
+        ("max_inv_resid", ctypes.c_double),
     ]
 
 

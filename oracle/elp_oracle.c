@@ -138,6 +138,7 @@ typedef struct {
     int64_t nnz;      /* nonzeros of A (price_mode 1 byte count)          */
     int64_t *cp, *ri; /* price_mode 1: nonzero pattern of A by column      */
     int64_t gj_count; /* refactors that needed a fresh Gauss-Jordan */
+    double emax_max;  /* largest Newton-Schulz residual max|E| seen  */
     int refactor_mode;
     double tol_singular;
     double *dw, *dprev; /* price_rule 1: Devex weight and last reduced cost
@@ -392,6 +393,7 @@ static int newton_schulz(orc_t* s) {
             E[i * k + j] = e;
             if (fabs(e) > emax) emax = fabs(e);
         }
+    if (emax > s->emax_max) s->emax_max = emax;
     if (!(emax <= NS_TOL)) return 0;
     /* Minv_new[i][j] = Minv[i][j] + sum_l Minv[i][l] E[l][j]  (seq, from Minv[i][j]) */
     double* Nw = Mk;
@@ -1300,6 +1302,7 @@ static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, 
     clock_gettime(CLOCK_MONOTONIC, &t1);
     st.iterations = iter;
     st.gj_refactors = s->gj_count;
+    st.max_inv_resid = s->emax_max;
     st.bump_dim = s->k;
     st.y_rows = s->ny;
     st.seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);

@@ -63,6 +63,7 @@ typedef struct orc_stats {
     double seconds_at_mark;
     int64_t gj_refactors;  /* refactors that fell back to Gauss-Jordan      */
     int64_t devex_resets;  /* Devex reference-framework restarts            */
+    double max_inv_resid;  /* largest max|I - M Minv| a refactor measured    */
 } orc_stats;
 
 void orc_default_control(orc_control* c);

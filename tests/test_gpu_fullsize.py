@@ -55,6 +55,9 @@ def test_c3_trace_matches_oracle(c3):
     np.testing.assert_array_equal(sol.trace, o.trace)
     np.testing.assert_array_equal(sol.basis, o.basis)
     assert sol.objval == o.objval
+    # the maintained bump inverse drifts the same way on both sides (bit-identical E)
+    assert sol.stats["max_inv_resid"] == o.stats["max_inv_resid"] <= 1e-6
+    assert sol.stats["gj_refactors"] == o.stats["gj_refactors"] == 0
 
 
 def test_c3_vs_highs_fixture(c3):

@@ -18,6 +18,7 @@ def _cmp(g, o, rel=1e-12):
     assert g.status == o.status
     if hasattr(o, "stats") and "gj_refactors" in o.stats:
         assert g.stats["gj_refactors"] == o.stats["gj_refactors"]
+        assert g.stats["max_inv_resid"] == o.stats["max_inv_resid"]  # same E, bit for bit
         assert g.stats["refactors"] >= o.stats["refactors"]
     if g.status in (0, 1):
         assert abs(g.objval - o.objval) <= rel * max(1.0, abs(o.objval))
