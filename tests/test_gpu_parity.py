@@ -176,3 +176,23 @@ def test_ar_growth_during_solve(gpu, monkeypatch):
     assert o.stats["y_rows"] > 16
     _cmp(g, o)
     np.testing.assert_array_equal(g.trace, o.trace)
+
+
+def test_bump_past_1024_vs_oracle(gpu):
+    """Diagonally dominant LP whose optimal basis is all structural: the bump
+    grows by one per pivot to k = 1050, past the register-resident limits of
+    the latency kernels (B^-1 rows and bump FTRAN by lane-strided chains past
+    512, the ratio test's row loops and two-pass A[lrow, S] gather past 1024,
+    alpha_S staged in LDS for FTRAN-z)."""
+    from oracle import solve_dense as orc
+    m = n = 1050
+    rng = np.random.default_rng(7)
+    A = np.eye(m) + rng.uniform(0, 1.0 / m, (m, n))
+    b = rng.uniform(1, 2, m)
+    c = rng.uniform(1, 2, n)
+    dirs = np.ones(m, np.int32)
+    g = gpu.solve_dense(A, dirs, b, c, maximize=True, trace=100000)
+    o = orc(A, dirs, b, c, maximize=True, trace_cap=100000)
+    assert o.stats["bump_dim"] > 1024, o.stats
+    _cmp(g, o)
+    np.testing.assert_array_equal(g.trace, o.trace)
