@@ -55,8 +55,8 @@ def test_fuzz_dense(gpu, name, gctl, octl, sub):
     for rec, rid in zip(FUZZ[sub], IDS[sub]):
         try:
             seen.add(_run(gpu, rec, gctl=gctl, octl=octl).status)
-        except AssertionError as e:
-            raise AssertionError(f"{rid}: {e}") from None
+        except Exception as e:  # name the LP
+            raise AssertionError(f"{rid}: {type(e).__name__}: {e}") from None
     assert {0, 2, 3} <= seen, seen
 
 
@@ -65,8 +65,8 @@ def test_fuzz_csc(gpu):
     for rec, rid in zip(FUZZ, IDS):
         try:
             seen.add(_run(gpu, rec, sparse=True).status)
-        except AssertionError as e:
-            raise AssertionError(f"{rid}: {e}") from None
+        except Exception as e:  # name the LP
+            raise AssertionError(f"{rid}: {type(e).__name__}: {e}") from None
     assert {0, 2, 3} <= seen, seen
 
 
@@ -76,6 +76,6 @@ def test_fuzz_two_ranks(gpu):
     for rec, rid in list(zip(FUZZ, IDS))[::4]:
         try:
             g = _run(gpu, rec, gctl={"ngpu": 2})
-        except AssertionError as e:
-            raise AssertionError(f"{rid}: {e}") from None
+        except Exception as e:  # name the LP
+            raise AssertionError(f"{rid}: {type(e).__name__}: {e}") from None
         assert g.stats["world_size"] == 2
