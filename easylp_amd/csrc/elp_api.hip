@@ -310,6 +310,10 @@ extern "C" int elp_create(elp_handle** out, int64_t m, int64_t n, const elp_cont
         return fail(ELP_E_HIP, "elp_create: stream creation failed");
     }
     if (h->ctl.ngpu > 1) {
+        if (n < h->ctl.ngpu) {  // (prep_load's rule for column shards)
+            elp_destroy(h);
+            return fail(ELP_E_ARG, "elp_create: ngpu exceeds n (every rank prices at least one column)");
+        }
         const int rc = create_group(h);
         if (rc) {
             const std::string msg = g_err;
@@ -845,6 +849,9 @@ static int prep_load(elp_handle* h, bool csc = false) {
         return fail(ELP_E_UNSUPPORTED, "elp_load_csc: column-sharded CSC solves are not supported");
     if (h->comm.world > 1) {
         const int64_t P = h->comm.world, r = h->comm.rank;
+        if (h->n < P)  // every rank prices at least one column
+            return fail(ELP_E_ARG, "column-sharded solve: n (" + std::to_string(h->n) + ") is below the rank count (" +
+                                       std::to_string(P) + ")");
         h->col0 = r * h->n / P;
         h->nloc = (r + 1) * h->n / P - h->col0;
     }

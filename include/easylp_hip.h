@@ -85,7 +85,8 @@ typedef struct elp_control {
                                 device+P-1 (mod the visible count) with one host
                                 thread per device and an in-process
                                 communicator (RCCL over xGMI when the devices
-                                are distinct).  Excludes elp_comm_init*.       */
+                                are distinct).  Excludes elp_comm_init*.
+                                P > n: ELP_E_ARG (a rank prices >= 1 column). */
     int32_t scaling;         /* ELP_SCALE_* bits (lp.control(scaling = ...)):
                                 0 none; ELP_SCALE_GEOMETRIC | ELP_SCALE_EQUILIBRATE
                                 (default, lp_solve's "geometric" + "equilibrate");

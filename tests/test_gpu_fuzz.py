@@ -71,9 +71,14 @@ def test_fuzz_csc(gpu):
 
 
 def test_fuzz_two_ranks(gpu):
-    """ngpu = 2: columns split over two rank handles (sharing the test GPU),
-    one-column models included (rank 1 then owns no column)."""
+    """ngpu = 2: columns split over two rank handles (sharing the test GPU);
+    a one-column model cannot be split and is refused (ELP_E_ARG)."""
     for rec, rid in list(zip(FUZZ, IDS))[::4]:
+        if rec["n"] < 2:
+            from easylp_amd._lib import ElpError
+            with pytest.raises(ElpError, match="ngpu exceeds n"):
+                _run(gpu, rec, gctl={"ngpu": 2})
+            continue
         try:
             g = _run(gpu, rec, gctl={"ngpu": 2})
         except Exception as e:  # name the LP
