@@ -108,3 +108,34 @@ def fuzz_lp(seed):
 
 def fuzz_set(count, start=0):
     return [fuzz_lp(s) for s in range(start, start + count)]
+
+
+def fuzz_mip(seed):
+    """A small MIP (branch and bound stays at a few hundred nodes): integer
+    coefficients, every column boxed or bounded by a packing row, a random
+    subset of the columns integer; one in five is integer-infeasible by
+    construction (an equality row 2 x_0 + 2 x_1 = odd over integer columns)."""
+    rng = np.random.default_rng(5000 + seed)
+    m, n = int(rng.integers(1, 9)), int(rng.integers(2, 11))
+    A = rng.integers(-2, 6, (m, n)).astype(np.float64)
+    dirs = rng.integers(1, 4, m).astype(np.int32)
+    dirs[0] = 1
+    A[0, :] = rng.integers(1, 6, n)  # a packing row bounds every column
+    lo = np.zeros(n)
+    up = np.where(rng.random(n) < 0.5, rng.integers(1, 8, n).astype(np.float64), INF)
+    x0 = np.floor(rng.uniform(0, 1, n) * np.where(np.isfinite(up), up + 1, 4.0))
+    act = A @ x0
+    rhs = np.where(dirs == 1, act + rng.integers(0, 4, m), np.where(dirs == 2, act - rng.integers(0, 4, m), act))
+    is_int = (rng.random(n) < 0.7).astype(np.int32)
+    infeasible = seed % 5 == 4
+    if infeasible:
+        is_int[:2] = 1
+        A = np.vstack([A, np.zeros(n)])
+        A[-1, :2] = 2.0
+        dirs = np.append(dirs, np.int32(3))
+        rhs = np.append(rhs, 2.0 * (x0[0] + x0[1]) + 1.0)
+        m += 1
+    obj = rng.integers(-4, 9, n).astype(np.float64)
+    return {"A": A, "dir": dirs, "rhs": rhs.astype(np.float64), "obj": obj, "lo": lo, "up": up,
+            "maximize": bool(rng.random() < 0.7), "is_int": is_int, "m": m, "n": n, "seed": seed,
+            "kind": "infeasible" if infeasible else "feasible"}

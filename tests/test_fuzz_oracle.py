@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 from conftest import feasible
-from fuzz_lps import fuzz_set
+from fuzz_lps import fuzz_mip, fuzz_set
 
 FUZZ = fuzz_set(120)
 HIGHS_STATUS = {0: 0, 2: 2, 3: 3}  # linprog status -> elp status
@@ -63,3 +63,35 @@ def test_fuzz_set_covers_every_outcome():
     assert {0, 2, 3} <= seen, seen
     assert {r["style"] for r in FUZZ} == {0, 1, 2, 3}
     assert any(r["m"] == 0 for r in FUZZ) and any(r["n"] == 1 for r in FUZZ)
+
+
+MIPS = [fuzz_mip(s) for s in range(40)]
+
+
+def _highs_milp(rec):
+    from scipy.optimize import Bounds, LinearConstraint, milp
+    A, d, b = rec["A"], rec["dir"], rec["rhs"]
+    lo_r = np.where(d == 1, -np.inf, b)
+    up_r = np.where(d == 2, np.inf, b)
+    sgn = -1.0 if rec["maximize"] else 1.0
+    r = milp(sgn * rec["obj"], constraints=[LinearConstraint(A, lo_r, up_r)],
+             integrality=rec["is_int"], bounds=Bounds(rec["lo"], rec["up"]))
+    return r.status, (sgn * r.fun if r.status == 0 else None)
+
+
+@pytest.mark.parametrize("rec", MIPS, ids=[f"mip{r['seed']}_{r['m']}x{r['n']}_{r['kind'][:3]}" for r in MIPS])
+def test_oracle_mip_vs_highs(rec):
+    """Branch and bound over the oracle's LPs (orc_solve_mip, the rules of
+    lp_solve's defaults: DESIGN.md section 11) against HiGHS' MILP optimum."""
+    from oracle import solve_mip
+    o = solve_mip(rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], rec["maximize"],
+                  rec["is_int"])
+    hs, hobj = _highs_milp(rec)
+    if rec["kind"] == "infeasible":
+        assert o.status == 2 and hs == 2, (o.status, hs)
+        return
+    assert hs == 0 and o.status == 0, (o.status, hs)
+    assert abs(o.objval - hobj) <= 1e-7 * max(1.0, abs(hobj)), (o.objval, hobj)
+    xi = o.x[rec["is_int"] == 1]
+    assert np.all(np.abs(xi - np.round(xi)) <= 1e-7)
+    assert feasible(rec["A"], rec["dir"], rec["rhs"], o.x, rec["lo"], rec["up"], tol=1e-7)
