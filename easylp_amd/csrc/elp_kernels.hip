@@ -916,6 +916,9 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
 #ifndef ELP_PRICE_UNR
 #define ELP_PRICE_UNR 16
 #endif
+#ifndef ELP_PRICE_PRE
+#define ELP_PRICE_PRE ELP_PRICE_UNR
+#endif
 // One tile workgroup = PRICE_SPLIT waves = 128 columns x all Y slots.  Wave w
 // sweeps the slots p = w, w + PRICE_SPLIT, w + 2 PRICE_SPLIT, ... (an fma chain
 // in slot order; the oracle's price order): its first UNR rows do not depend
@@ -938,6 +941,8 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
     }
     constexpr int S = PRICE_SPLIT;
     constexpr int UNR = ELP_PRICE_UNR;  // rows in flight per wave: 16 KiB (32 measured slower)
+    constexpr int PRE = ELP_PRICE_PRE;  // rows issued before the control block / y arrive
+                                        // (24 / 32: 35.1 -> 35.5-36.4 us per iteration, r02m A/B)
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // the epilogue's per-column operands (status, cost, Devex weight, previous
@@ -952,10 +957,10 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
     const double* col = d.AR + (size_t)blockIdx.x * (size_t)d.arcap * TILE_COLS + 2 * lane;
     const double* __restrict__ yy = d.yy;
     const int cap = (int)d.arcap;
-    dbl2 v0[UNR];
-    double y0[UNR];
+    dbl2 v0[PRE];
+    double y0[PRE];
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {  // slot w + S u, clamped into AR
+    for (int u = 0; u < PRE; ++u) {  // slot w + S u, clamped into AR
         const int pp = min(w + S * u, cap - 1);
         v0[u] = AR_LOAD(col + (size_t)pp * TILE_COLS);
         y0[u] = yy[pp];
@@ -966,7 +971,7 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
     const int ny = c->ny, bland = c->bland;
     if (st0 != ST_RUN) {
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) {
+        for (int u = 0; u < PRE; ++u) {
             KEEP(v0[u].x);
             KEEP(y0[u]);
         }
@@ -980,13 +985,13 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
     const double dtol = c->tol_dual;
     double acc0 = 0.0, acc1 = 0.0;
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
+    for (int u = 0; u < PRE; ++u) {
         if (w + S * u < ny) {
             acc0 = fma(v0[u].x, y0[u], acc0);
             acc1 = fma(v0[u].y, y0[u], acc1);
         }
     }
-    int p = w + S * UNR;
+    int p = w + S * PRE;
     for (; p + S * (UNR - 1) < ny; p += S * UNR) {
         dbl2 v[UNR];
 #pragma unroll
