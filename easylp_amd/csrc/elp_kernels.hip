@@ -916,15 +916,21 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
 #ifndef ELP_PRICE_UNR
 #define ELP_PRICE_UNR 16
 #endif
-#ifndef ELP_PRICE_PRE
-#define ELP_PRICE_PRE ELP_PRICE_UNR
+#ifndef ELP_PRICE_YLANE
+#define ELP_PRICE_YLANE 1  // (0: one uniform y load per row, 16 more vector-memory instructions per block)
 #endif
+// lane l's double, read by every lane (v_readlane pair)
+DEV double lane_bcast(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
 // One tile workgroup = PRICE_SPLIT waves = 128 columns x all Y slots.  Wave w
 // sweeps the slots p = w, w + PRICE_SPLIT, w + 2 PRICE_SPLIT, ... (an fma chain
 // in slot order; the oracle's price order): its first UNR rows do not depend
-// on |Y|, so they go out with the epilogue operands BEFORE the control block
-// arrives (rows past |Y| are masked when it does), and the sweep overlaps the
-// control-block round trip instead of following it.
+// on |Y|, so they go out right behind the control-block loads, before the
+// control block arrives (rows past |Y| are masked when it does), and the sweep
+// overlaps the control-block round trip instead of following it.
 DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
     __shared__ double part[PRICE_SPLIT][TILE_COLS];
     __shared__ Cand red[PRICE_SPLIT];
@@ -939,12 +945,48 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
         price_slacks<PRICE_THREADS>(d, ntiles, (int)(blockIdx.x - ntiles), nsw, red);  // a slack workgroup
         return;
     }
+    // Software-pipelined sweep: the control block is loaded FIRST (vmcnt
+    // retires in issue order, so the status test and the loop bound wait for
+    // it alone, not for the rows issued behind it), then the first UNR rows
+    // (independent of |Y|), then the epilogue operands; each loop step issues
+    // the next UNR rows before it consumes the current ones, so a wave keeps
+    // rows in flight through the whole sweep instead of draining them every
+    // UNR rows.  Consumption order -- one fma chain per slot class in slot
+    // order -- is the oracle's, unchanged.  With y read once per block (one
+    // lane per row, v_readlane at the fma) instead of one uniform load per row,
+    // r02m A/B at 5000x50000: launch 20.5 -> 19.6 us, 35.4 -> 34.6 us per
+    // iteration (pipelining alone: no change; 8 / 12 rows per block: same);
+    // at 10 000 x 500 000, HBM-bound, unchanged (338 vs 341 us, one run each).
     constexpr int S = PRICE_SPLIT;
-    constexpr int UNR = ELP_PRICE_UNR;  // rows in flight per wave: 16 KiB (32 measured slower)
-    constexpr int PRE = ELP_PRICE_PRE;  // rows issued before the control block / y arrive
-                                        // (24 / 32: 35.1 -> 35.5-36.4 us per iteration, r02m A/B)
+    constexpr int UNR = ELP_PRICE_UNR;
+    constexpr int SU = S * UNR;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const DevCtl* c = d.ctl;
+    int32_t st0 = c->status;
+    int ny = c->ny, bland = c->bland, devex = c->devex;
+    DevexIn dx = devex_in(c);
+    double dtol = c->tol_dual;
+    __builtin_amdgcn_sched_barrier(0);
+    const double* col = d.AR + (size_t)blockIdx.x * (size_t)d.arcap * TILE_COLS + 2 * lane;
+    const double* __restrict__ yy = d.yy;
+    const int cap = (int)d.arcap;
+    dbl2 va[UNR], vb[UNR];
+#if ELP_PRICE_YLANE
+    // y of a block: lane l loads slot p + S (l mod UNR), the fma takes it by readlane
+    double ya, yb;
+    ya = yy[min(w + S * (lane % UNR), cap - 1)];
+#else
+    double ya[UNR], yb[UNR];
+#endif
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {  // slot w + S u, clamped into AR (masked by |Y| at use)
+        const int pp = min(w + S * u, cap - 1);
+        va[u] = AR_LOAD(col + (size_t)pp * TILE_COLS);
+#if !ELP_PRICE_YLANE
+        ya[u] = yy[pp];
+#endif
+    }
     // the epilogue's per-column operands (status, cost, Devex weight, previous
     // d) of columns 2 lane, 2 lane + 1 -- wave 0's: the other waves load element
     // 0 (one line); clamped, no branch to drain
@@ -953,75 +995,86 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
     const int8_t pf_vs0 = d.vstat[jc0], pf_vs1 = d.vstat[jc1];
     const double pf_c0 = d.cost[jc0], pf_w0 = d.dw[jc0], pf_dp0 = d.dprev[jc0];
     const double pf_c1 = d.cost[jc1], pf_w1 = d.dw[jc1], pf_dp1 = d.dprev[jc1];
-    // this tile's rows are contiguous: row p at col + p * TILE_COLS
-    const double* col = d.AR + (size_t)blockIdx.x * (size_t)d.arcap * TILE_COLS + 2 * lane;
-    const double* __restrict__ yy = d.yy;
-    const int cap = (int)d.arcap;
-    dbl2 v0[PRE];
-    double y0[PRE];
-#pragma unroll
-    for (int u = 0; u < PRE; ++u) {  // slot w + S u, clamped into AR
-        const int pp = min(w + S * u, cap - 1);
-        v0[u] = AR_LOAD(col + (size_t)pp * TILE_COLS);
-        y0[u] = yy[pp];
-    }
     __builtin_amdgcn_sched_barrier(0);  // all of the above issued before any use
-    const DevCtl* c = d.ctl;
-    const int32_t st0 = c->status;
-    const int ny = c->ny, bland = c->bland;
+    // (the control-block values stay vector values up to here -- their scalar
+    //  copies would otherwise be made above the row loads, which would then
+    //  wait for the control block; the wait here is for the control block only)
+    asm volatile("" : "+v"(st0), "+v"(ny), "+v"(bland), "+v"(devex), "+v"(dx.valid), "+v"(dx.lv));
+    asm volatile("" : "+v"(dx.dq), "+v"(dx.wq), "+v"(dtol));
     if (st0 != ST_RUN) {
 #pragma unroll
-        for (int u = 0; u < PRE; ++u) {
-            KEEP(v0[u].x);
-            KEEP(y0[u]);
-        }
+        for (int u = 0; u < UNR; ++u) KEEP(va[u].x);
+#if ELP_PRICE_YLANE
+        KEEP(ya);
+#else
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) KEEP(ya[u]);
+#endif
         KEEP(pf_c0);
         KEEP(pf_c1);
         return;
     }
     PDBG(1, __builtin_amdgcn_s_memrealtime());
-    const int devex = c->devex;
-    const DevexIn dx = devex_in(c);
-    const double dtol = c->tol_dual;
+    const int nys = __builtin_amdgcn_readfirstlane(ny);
     double acc0 = 0.0, acc1 = 0.0;
-#pragma unroll
-    for (int u = 0; u < PRE; ++u) {
-        if (w + S * u < ny) {
-            acc0 = fma(v0[u].x, y0[u], acc0);
-            acc1 = fma(v0[u].y, y0[u], acc1);
-        }
-    }
-    int p = w + S * PRE;
-    for (; p + S * (UNR - 1) < ny; p += S * UNR) {
-        dbl2 v[UNR];
-#pragma unroll
-        for (int u = 0; u < UNR; ++u)
-            v[u] = AR_LOAD(col + (size_t)(p + S * u) * TILE_COLS);
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            const double yv = yy[p + S * u];
-            acc0 = fma(v[u].x, yv, acc0);
-            acc1 = fma(v[u].y, yv, acc1);
-        }
-    }
-    if (p < ny) {  // remainder: same order, loads issued together
-        // (y at clamped rows, unconditional: a load under the row test is
-        //  drained at the end of its block -- one round trip per row)
-        dbl2 v[UNR];
-        double yv[UNR];
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            v[u] = (p + S * u < ny) ? AR_LOAD(col + (size_t)(p + S * u) * TILE_COLS) : dbl2{0.0, 0.0};
-            yv[u] = yy[min(p + S * u, ny - 1)];
-        }
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            if (p + S * u < ny) {
-                acc0 = fma(v[u].x, yv[u], acc0);
-                acc1 = fma(v[u].y, yv[u], acc1);
+    // rows of a block at or past |Y| re-read the block's first row (p < |Y|;
+    // an L1/L2 hit) and are masked when consumed
+#if ELP_PRICE_YLANE
+#define PIPE_ISSUE(V, Y, P)                                                          \
+    do {                                                                             \
+        _Pragma("unroll") for (int u = 0; u < UNR; ++u) {                            \
+            const int r_ = (P) + S * u < nys ? (P) + S * u : (P);                    \
+            V[u] = AR_LOAD(col + (size_t)r_ * TILE_COLS);                            \
+        }                                                                            \
+        const int ry_ = (P) + S * (lane % UNR);                                      \
+        Y = yy[ry_ < nys ? ry_ : (P)];                                               \
+    } while (0)
+#define PIPE_Y(Y, u) lane_bcast(Y, u)
+#else
+#define PIPE_ISSUE(V, Y, P)                                                          \
+    do {                                                                             \
+        _Pragma("unroll") for (int u = 0; u < UNR; ++u) {                            \
+            const int r_ = (P) + S * u < nys ? (P) + S * u : (P);                    \
+            V[u] = AR_LOAD(col + (size_t)r_ * TILE_COLS);                            \
+            Y[u] = yy[r_];                                                           \
+        }                                                                            \
+    } while (0)
+#define PIPE_Y(Y, u) Y[u]
+#endif
+#define PIPE_CONSUME(V, Y, P)                                                        \
+    do {                                                                             \
+        _Pragma("unroll") for (int u = 0; u < UNR; ++u) {                            \
+            if ((P) + S * u < nys) {                                                 \
+                const double y_ = PIPE_Y(Y, u);                                      \
+                acc0 = fma(V[u].x, y_, acc0);                                        \
+                acc1 = fma(V[u].y, y_, acc1);                                        \
+            }                                                                        \
+        }                                                                            \
+    } while (0)
+    int p = w;
+    if (p < nys) {
+        for (;;) {
+            if (p + SU >= nys) {
+                PIPE_CONSUME(va, ya, p);
+                break;
             }
+            PIPE_ISSUE(vb, yb, p + SU);
+            __builtin_amdgcn_sched_barrier(0);
+            PIPE_CONSUME(va, ya, p);
+            p += SU;
+            if (p + SU >= nys) {
+                PIPE_CONSUME(vb, yb, p);
+                break;
+            }
+            PIPE_ISSUE(va, ya, p + SU);
+            __builtin_amdgcn_sched_barrier(0);
+            PIPE_CONSUME(vb, yb, p);
+            p += SU;
         }
     }
+#undef PIPE_ISSUE
+#undef PIPE_CONSUME
+#undef PIPE_Y
     PDBG(2, __builtin_amdgcn_s_memrealtime());
     part[w][2 * lane] = acc0;
     part[w][2 * lane + 1] = acc1;
