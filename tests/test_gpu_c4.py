@@ -70,3 +70,28 @@ def test_c4_trace_matches_oracle(c4):
     assert o.status == 1 and o.stats["iterations"] == CAP
     assert c4.stats["iterations"] > CAP
     np.testing.assert_array_equal(c4.trace, o.trace)
+
+
+def test_c4_eight_column_shards_match_oracle(c4, gpu):
+    """The 8-rank column-sharded solve of BASELINE config 4 at full size
+    (SURVEY.md 8e), rehearsed in one process on the test GPU: ngpu = 8 rank
+    handles share the device over the in-process transport, A column-only
+    (replicate = 2: 62 500 columns, 5 GB per rank, the entering column
+    exchanged every iteration), solved to optimality -- the first 300 pivots
+    identical to the oracle's, and iterations, basis, objective and x
+    identical to the single-GPU solve above."""
+    from oracle import solve_generated
+    with gpu.Problem(M, N, ngpu=8, replicate=2, scaling=0) as p:
+        p.set_trace(CAP)
+        p.load_generated(SEED)
+        st = p.solve()
+        g = p.solution(st)
+        s = p.stats()
+    assert s["world_size"] == 8
+    o = solve_generated(SEED, M, N, trace_cap=CAP, max_iter=CAP, scaling=0)
+    np.testing.assert_array_equal(g.trace, o.trace)
+    assert st == c4.status == 0
+    assert s["iterations"] == c4.stats["iterations"]
+    np.testing.assert_array_equal(g.basis, c4.basis)
+    assert g.objval == c4.objval
+    np.testing.assert_array_equal(g.x, c4.x)
