@@ -1781,10 +1781,6 @@ constexpr int ZR_ROWS = 32;   // rows per row tile: lane = row + 32 * half; each
 // of every lane loading the chunk's 32 values itself (half the VMEM instructions
 // and 64 fewer VGPRs); needs k_ub <= ZR_PA * threads
 constexpr int ZR_PA = 4;
-#ifndef ELP_ZR_SLANE
-#define ELP_ZR_SLANE 0
-#endif
-constexpr bool ZR_SLANE = ELP_ZR_SLANE;
 template <bool LDSZ, int ZR_WAVES, bool ALS>
 __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int k_ub, int dslot) {
     extern __shared__ __attribute__((aligned(16))) double zlds[];  // [nch_ub][ZR_ROWS], then (ALS) [k_ub] alpha_S
@@ -1805,19 +1801,11 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
     int k = c->k, q = c->q, bland = c->bland;  // (pinned below)
     const double sig = c->sig, ptol = c->tol_primal, pivtol = c->tol_pivot;
     const int ch0 = 2 * w + hh;
-    // ZR_SLANE: the first chunk's alpha_S read once per half-wave (lane r loads
-    // position r; the fma takes position t from lane t of its half by readlane)
-    // instead of one half-uniform load per position
-    constexpr bool SL = ZR_SLANE && !ALS;
-    double a0[ZCHUNK], s0[(ALS || SL) ? 1 : ZCHUNK], pa[ALS ? ZR_PA : 1];
-    double sv = 0.0;
+    double a0[ZCHUNK], s0[ALS ? 1 : ZCHUNK], pa[ALS ? ZR_PA : 1];
     const bool row_tile = (int)blockIdx.x < nrt;
     if constexpr (ALS) {  // this thread's share of alpha_S, staged in LDS below
 #pragma unroll
         for (int t = 0; t < ZR_PA; ++t) pa[t] = ld_clamp(d.alS, (int)threadIdx.x + (int)blockDim.x * t, k_ub);
-    }
-    if constexpr (SL) {  // (every lane of the half: rows past m too)
-        if (row_tile && ch0 * ZCHUNK < k_ub) sv = d.alS[min(ch0 * ZCHUNK + r, k_ub - 1)];
     }
     if (row_tile && ch0 * ZCHUNK < k_ub && i < d.m) {
         const double* col = d.AS + (size_t)(ch0 * ZCHUNK) * mm + i;
@@ -1825,7 +1813,7 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
         for (int t = 0; t < ZCHUNK; ++t) {
             const bool in = ch0 * ZCHUNK + t < k_ub;
             a0[t] = in ? col[(size_t)t * mm] : 0.0;
-            if constexpr (!ALS && !SL) s0[t] = in ? d.alS[ch0 * ZCHUNK + t] : 0.0;
+            if constexpr (!ALS) s0[t] = in ? d.alS[ch0 * ZCHUNK + t] : 0.0;
         }
     }
     // likewise wave 0's epilogue operands (independent of q and z)
@@ -1848,9 +1836,7 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
     if (st0 != ST_RUN) {
 #pragma unroll
         for (int t = 0; t < ZCHUNK; ++t) KEEP(a0[t]);
-        if constexpr (SL) {
-            KEEP(sv);
-        } else if constexpr (!ALS) {
+        if constexpr (!ALS) {
 #pragma unroll
             for (int t = 0; t < ZCHUNK; ++t) KEEP(s0[t]);
         } else {
@@ -1912,15 +1898,8 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
             if (i < m) {
                 const int len = min(ZCHUNK, k - ch0 * ZCHUNK);
 #pragma unroll
-                for (int t = 0; t < ZCHUNK; ++t) {
-                    if (t < len) {
-                        double st;
-                        if constexpr (ALS) st = als[ch0 * ZCHUNK + t];
-                        else if constexpr (SL) st = hh ? lane_bcast(sv, 32 + t) : lane_bcast(sv, t);
-                        else st = s0[t];
-                        acc = fma(a0[t], st, acc);
-                    }
-                }
+                for (int t = 0; t < ZCHUNK; ++t)
+                    if (t < len) acc = fma(a0[t], ALS ? als[ch0 * ZCHUNK + t] : s0[t], acc);
             }
             zp[ch0 * ZR_ROWS + r] = acc;
         }
