@@ -1269,7 +1269,12 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
         const double t_enq1 = now_s();
         HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
         HIPCHK(hipStreamSynchronize(h->st));
-        if (c->plan_seq != c->applied_seq) {
+        // a poll that just queues the next chunk (phase 2 running, no budget, cap,
+        // refactor or time-limit stop due) leaves the last plan to the next chunk's
+        // first pricing launch, as inside a chunk; any other poll may read the basis
+        const bool plain_next = c->status == ST_RUN && h->phase == 2 && c->iter < c->iter_stop &&
+                                c->iter < c->iter_limit && c->since_refactor < period && !(h->ctl.time_limit > 0);
+        if (c->plan_seq != c->applied_seq && !plain_next) {
             // phase 2 defers each iteration's update into the next pricing launch:
             // apply the last one now (phase 1 applied its plans in place)
             if (h->phase == 2) HIPCHK(launch_apply_pending(h->d, std::max(k0, c->k), h->st));
