@@ -155,6 +155,21 @@ def price_roofline(stats_list):
             "avg_launch_us": 1e6 * secs / nl if nl else None, "launches_timed": nl}
 
 
+def iteration_roofline(stats_list):
+    """Whole-iteration roofline (SURVEY.md 8d "report both per phase"): the
+    iterations' algorithmic bytes (pricing sweep + select 8k^2 + FTRAN-z 8mk +
+    ratio test 8k^2 + 16n + deferred update 32k^2 + 16m, accumulated on the
+    device at the k of each iteration) / the simplex-loop wall time."""
+    byts = sum(s["iter_bytes"] for s in stats_list)
+    secs = sum(s["seconds_loop"] for s in stats_list)
+    its = sum(s["iterations"] for s in stats_list)
+    ach = byts / secs / 1e9 if secs > 0 else None
+    return {"achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": ach / HBM_PEAK_GBS if ach else None,
+            "bytes_per_iteration": byts / its if its else None,
+            "timer": "host wall clock of the simplex loops of the timed solves (load excluded)"}
+
+
 def cpu_baseline(args):
     """The CPU oracle (same algorithm, 1 thread) solving the same LP: one full
     solve by default (about 20 s on one EPYC core), else the first --cpu-iters."""
@@ -447,6 +462,7 @@ def main():
                 "traffic": traffic,
                 "traffic_source": traffic_src,
             },
+            "iteration_roofline": iteration_roofline(stats),
             "cpu_baseline": cpu,
             "scaling_config": c4,
             "sparse_config": sparse,

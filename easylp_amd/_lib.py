@@ -89,6 +89,7 @@ class ElpStats(ctypes.Structure):
         ("mip_lp_iterations", ctypes.c_int64),
         ("price_launches", ctypes.c_int64),
         ("max_inv_resid", ctypes.c_double),
+        ("iter_bytes", ctypes.c_double),
     ]
 
 

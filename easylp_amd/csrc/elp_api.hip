@@ -1791,6 +1791,7 @@ extern "C" int elp_get_stats(elp_handle* h, elp_stats* st) {
         h->stats.mip_nodes = h->mip ? h->mip_nodes : 0;
         h->stats.mip_lp_iterations = h->mip ? h->mip_iters : 0;
         h->stats.price_bytes = c.price_bytes;
+        h->stats.iter_bytes = c.iter_bytes;
         if (h->d.ptimer) {
             h->stats.price_seconds = 1e-8 * (double)c.price_ticks;
             h->stats.price_timed_launches = c.price_timed;

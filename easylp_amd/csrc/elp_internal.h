@@ -64,6 +64,7 @@ struct DevCtl {
     int32_t infeasible_bounds, pad1;
     double price_bytes;    // algorithmic bytes of every pricing pass that ran
     int64_t price_passes;
+    double iter_bytes;     // algorithmic bytes of the whole iterations
     unsigned long long ns_emax_bits;  // max|I - M Minv| of the last refactor (bits of a double >= 0)
     int32_t price_grid, pad3;         // workgroups of the last pricing launch (Dev::ptimer)
     int32_t snap_k, snap_bland;       // k, bland as k_ratio's workgroups must see them

@@ -1374,8 +1374,13 @@ DEV void entering_chosen(const Dev& d, const Cand& best) {
     DevCtl* c = d.ctl;
     const int ny = c->ny;
     // algorithmic bytes of this pricing pass: AR sweep + c + status + y_Y + Yl
-    c->price_bytes += price_pass_bytes(d, ny, c->devex);
+    const double pb = price_pass_bytes(d, ny, c->devex);
+    c->price_bytes += pb;
     c->price_passes++;
+    // the whole iteration: + select 8k^2, FTRAN-z 8mk, ratio
+    // 8k^2 + 16n, deferred update 32k^2 + 16m
+    const double kk = (double)c->k, mm = (double)d.m, nn = (double)d.n;
+    c->iter_bytes += pb + 48.0 * kk * kk + 8.0 * mm * kk + 16.0 * nn + 16.0 * mm;
     c->q = (int)best.j;
     c->dq = best.d;
     c->wq = best.w;

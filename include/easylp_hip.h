@@ -135,6 +135,9 @@ typedef struct elp_stats {
     double max_inv_resid;      /* drift of the maintained bump inverse: the
                                   largest max|I - M Minv| a refactor measured
                                   before correcting it (refactor_mode 0)        */
+    double iter_bytes;         /* algorithmic bytes of the whole iterations:
+                                  price_bytes + 48k^2 + 8mk + 16n + 16m each
+                                  (select, FTRAN-z, ratio test, update)         */
 } elp_stats;
 
 #define ELP_PROFILE_PRICE 2   /* elp_control.verbose bit: device-clock pricing timer */
