@@ -18,7 +18,7 @@ ELP_PROFILE_PRICE = 2   # device-clock pricing timer
 ELP_PROFILE_EVENTS = 4  # HIP events on every pricing dispatch
 ELP_PROFILE_SAMPLE = 8  # ... on those of every 8th chunk between host polls
 ELP_SCALE_GEOMETRIC, ELP_SCALE_EQUILIBRATE = 4, 64
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # every entry point the header declares (checked by tests/test_abi.py)
 EXPORTS = (

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define ELP_ABI_VERSION 2
+#define ELP_ABI_VERSION 3  /* 3: elp_stats.iter_bytes appended */
 
 /* row directions, mirroring R/class.R:272 ("==" -> "=") and the "<"/">"
  * spellings accepted by R/methods.R:215-219 */
