@@ -142,6 +142,9 @@ def load(path: str | None = None):
                  "elp_set_trace", "elp_get_trace", "elp_comm_unique_id", "elp_comm_init",
                  "elp_comm_init_host", "elp_comm_enable_p2p"):
         getattr(lib, name).restype = ctypes.c_int
+    if lib.elp_abi_version() != ABI_VERSION:  # (struct layouts would disagree)
+        raise ElpError(f"{path} has ABI {lib.elp_abi_version()}, this binding expects {ABI_VERSION}: "
+                       "rebuild it with `python -m easylp_amd.build`")
     _lib = lib
     return lib
 
