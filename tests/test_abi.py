@@ -11,6 +11,15 @@ from conftest import ROOT
 HEADER = os.path.join(ROOT, "include", "easylp_hip.h")
 
 
+def _torch_first():
+    """On a GPU box torch must start the HIP runtime before the library is
+    loaded (the gpu fixture's rule, tests/conftest.py): loading the library
+    first breaks every later GPU test of the same process."""
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.init()
+
+
 def declared():
     txt = open(HEADER).read()
     return sorted(set(re.findall(r"\b(elp_[a-z0-9_]+)\s*\(", txt)))
@@ -23,6 +32,7 @@ def test_header_declares_expected_surface():
 
 def test_library_exports_every_declared_symbol():
     from easylp_amd import build
+    _torch_first()
     lib_path = build.build()
     lib = ctypes.CDLL(lib_path)
     missing = [s for s in declared() if not hasattr(lib, s)]
@@ -31,6 +41,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_defaults():
     from easylp_amd._lib import ABI_VERSION, ElpControl, load
+    _torch_first()
     lib = load()
     assert lib.elp_abi_version() == ABI_VERSION == 3
     c = ElpControl()
@@ -64,6 +75,7 @@ def test_struct_layout_matches_header(which, tmp_path):
 
 def test_usage_errors_without_gpu():
     from easylp_amd._lib import load
+    _torch_first()
     lib = load()
     h = ctypes.c_void_p()
     assert lib.elp_create(ctypes.byref(h), -1, 5, None) == -1
