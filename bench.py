@@ -15,10 +15,17 @@ their wall time, i.e. the whole-solve iteration rate, and `time_to_optimal_s`
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
-Rank 0 prints one JSON line.  With N > 1 (torchrun; without a launcher
-bench.py starts torchrun itself) the columns are sharded across ranks (one
-process per GPU, per-iteration RCCL min-loc) and every rank runs the same
-solve: `value` is the iteration rate of the one LP (strong scaling).
+Rank 0 prints one JSON line.  With N > 1 the columns are sharded over N
+GPUs (strong scaling: `value` is the iteration rate of the one LP).  Default
+`--mode ngpu`: ONE process drives the N devices through one handle
+(elp_control.ngpu = N) -- what the R `.Call` path runs (R stays one synchronous
+process) -- with the per-iteration min-loc through the direct
+peer mailbox; A is generated on every device (untimed) and each rank reads its
+own copy (elp_load_dense_device_multi).  When the driver starts N processes
+under torchrun, rank 0 runs that one-process solve over all N devices and the
+other ranks only take part in the barriers around the timed region (they
+process no columns).  `--mode procs` keeps one process per GPU (elp_comm_init,
+RCCL all-gather or, with --p2p 1, the IPC mailbox).
 """
 from __future__ import annotations
 
@@ -52,8 +59,16 @@ def parse():
                     help="HIP events on the pricing dispatches of every 8th chunk (roofline)")
     ap.add_argument("--c4", type=int, default=1,
                     help="also solve the 10000x500000 column-sharded config (SURVEY config 4) to optimality")
+    ap.add_argument("--mode", choices=["ngpu", "procs"], default="ngpu",
+                    help="N>1: one process driving N devices (ngpu, the R path) or one process per GPU")
     ap.add_argument("--p2p", type=int, default=0,
-                    help="N>1: per-iteration min-loc through the xGMI mailbox (default: RCCL all-gather)")
+                    help="--mode procs, N>1: per-iteration min-loc through the IPC mailbox (default: RCCL all-gather)")
+    ap.add_argument("--exchange", type=int, default=0,
+                    help="--mode ngpu: elp_control.exchange (0 peer mailbox when it probes, 1 collective)")
+    ap.add_argument("--host-input", type=int, default=1,
+                    help="also time the solve from A in host memory (elp_load_dense, what .Call pays)")
+    ap.add_argument("--host-c4", type=int, default=1,
+                    help="with --host-input: also the 10000x500000 LP from a 40 GB host array (N=1)")
     ap.add_argument("--force-sharded", action="store_true",
                     help="N=1: run the sharded pipeline on a 1-rank RCCL communicator (overhead probe)")
     ap.add_argument("--sparse", type=int, default=1,
@@ -113,32 +128,105 @@ def enable_p2p(p, rank):
         return False
 
 
-def make_problem(args, lib, m, n, world, rank, local, **ctl):
+class Ctx:
+    """Where the bench runs.  procs: `world` processes, one GPU each (ngpu 1).
+    ngpu: one working process (rank 0) whose handle drives `ngpu` devices;
+    torchrun's other ranks (if any) only join the barriers."""
+
+    def __init__(self, args, world, rank, local, dist):
+        import torch
+        self.args, self.world, self.rank, self.local, self.dist = args, world, rank, local, dist
+        self.mode = args.mode if args.gpus > 1 else "single"
+        self.ngpu = args.gpus if self.mode == "ngpu" else 1
+        ndev = torch.cuda.device_count()
+        self.devices = [(local + r) % max(ndev, 1) for r in range(self.ngpu)]
+        self.works = self.mode != "ngpu" or rank == 0
+
+    def sync(self):
+        import torch
+        for dv in self.devices:
+            torch.cuda.synchronize(dv)
+
+    def barrier(self):
+        self.sync()
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max_over_ranks(self, v):
+        if self.world == 1:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def parallelism(self, p2p, stats):
+        if self.mode == "single":
+            return "force-sharded x1, RCCL" if self.args.force_sharded else "single GPU"
+        if self.mode == "procs":
+            return "column-shard x%d processes, %s min-loc" % (self.world, "IPC mailbox" if p2p else "RCCL all-gather")
+        ex = {1: "peer mailbox", 2: "collective (%s)" % ("RCCL" if len(set(self.devices)) == len(self.devices)
+                                                      else "in-process")}.get(stats.get("exchange"), "?")
+        return "ngpu x%d (one process), %s" % (self.ngpu, ex)
+
+
+def enable_p2p(p, rank):
+    """xGMI mailbox for the min-loc; collective and agreed by all ranks, so on
+    failure every rank falls back to the RCCL all-gather together."""
+    from easylp_amd._lib import ElpError
+    try:
+        p.comm_enable_p2p()
+        return True
+    except ElpError as e:
+        if rank == 0:
+            print(f"xGMI mailbox unavailable ({e}); RCCL all-gather min-loc", file=sys.stderr)
+        return False
+
+
+def make_problem(args, lib, m, n, ctx, **ctl):
     from easylp_amd import Problem
     from easylp_amd._lib import ELP_PROFILE_SAMPLE
-    p = Problem(m, n, device=local, verbose=ELP_PROFILE_SAMPLE if args.profile_price else 0,
-                pricing=args.rule, sync_every=args.sync_every, **ctl)
+    p = Problem(m, n, device=ctx.local, verbose=ELP_PROFILE_SAMPLE if args.profile_price else 0,
+                pricing=args.rule, sync_every=args.sync_every, ngpu=ctx.ngpu, exchange=args.exchange, **ctl)
     p2p = False
-    if world > 1 or args.force_sharded:
+    if ctx.mode == "procs" or args.force_sharded:
         from easylp_amd.dist import share_unique_id
-        p.comm_init(share_unique_id(lib, rank), world, rank)
+        p.comm_init(share_unique_id(lib, ctx.rank), ctx.world, ctx.rank)
         if args.p2p:
-            p2p = enable_p2p(p, rank)
+            p2p = enable_p2p(p, ctx.rank)
     return p, p2p
 
 
-def full_solves(p, A, b, c, count, barrier):
-    """`count` full solves (load from HBM + solve to optimality); per-solve stats."""
+def place_A(seed, m, n, ctx):
+    """The synthetic LP resident in HBM before anything is timed: on every device
+    of the handle (each rank reads its own copy)."""
+    from easylp_amd import generate_dense_device
+    As = []
+    for dv in ctx.devices:
+        A, b, c = generate_dense_device(seed, m, n, dv)
+        As.append(A)
+    return As, b, c
+
+
+def load_resident(p, As, b, c):
     import numpy as np
     dirs = np.ones(len(b), np.int32)
+    if len(As) > 1:
+        p.load_dense_device_multi([A.data_ptr() for A in As], dirs, b, c, maximize=True)
+    else:
+        p.load_dense_device(As[0].data_ptr(), dirs, b, c, maximize=True)
+
+
+def full_solves(p, As, b, c, count, ctx):
+    """`count` full solves (load from HBM + solve to optimality); per-solve stats."""
     recs = []
     for _ in range(count):
         t0 = time.perf_counter()
-        p.load_dense_device(A.data_ptr(), dirs, b, c, maximize=True)
+        load_resident(p, As, b, c)
         st = p.solve()
         el = time.perf_counter() - t0
         recs.append((st, el, p.stats()))
-    barrier()
+    ctx.sync()
     return recs
 
 
@@ -212,41 +300,76 @@ def committed_traffic(args):
     return t["traffic_bytes_per_launch"], "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE, x2 gfx950)"
 
 
-def c4_config(args, lib, world, rank, local, barrier, dist):
+def c4_config(args, lib, ctx):
     """BASELINE config 4: dense LP m=10000 n=500000 (40 GB), columns sharded over
     the ranks, solved to optimality from A resident in HBM."""
-    import numpy as np
     import torch
-    from easylp_amd import generate_dense_device
     m, n = 10000, 500000
-    A, b, c = generate_dense_device(args.seed, m, n, local)
-    p, _ = make_problem(args, lib, m, n, world, rank, local)
-    barrier()
+    As, b, c = place_A(args.seed, m, n, ctx)
+    p, _ = make_problem(args, lib, m, n, ctx)
+    if ctx.mode == "procs":
+        ctx.barrier()
+    else:  # (torchrun's idle ranks of the ngpu mode only join the timed region's barriers)
+        ctx.sync()
     t0 = time.perf_counter()
-    p.load_dense_device(A.data_ptr(), np.ones(m, np.int32), b, c, maximize=True)
-    barrier()
+    load_resident(p, As, b, c)
+    ctx.sync()
     t_load = time.perf_counter() - t0
     st = p.solve()
-    barrier()
+    ctx.sync()
     el = time.perf_counter() - t0
     s = p.stats()
     obj = p.solution(st).objval
     p.close()
-    del A
+    del As
     torch.cuda.empty_cache()
-    if world > 1:
-        tt = torch.tensor([el, t_load], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el, t_load = float(tt[0]), float(tt[1])
+    if ctx.mode == "procs":
+        el, t_load = ctx.max_over_ranks(el), ctx.max_over_ranks(t_load)
     sweep = price_roofline([s])
-    sweep["rank"] = rank
-    return {"workload": "dense random LP m=10000 n=500000 (SURVEY config 4), columns sharded x%d" % world,
+    sweep["rank"] = ctx.rank
+    return {"workload": "dense random LP m=10000 n=500000 (SURVEY config 4), columns sharded x%d" % max(ctx.world, ctx.ngpu),
+            "parallelism": ctx.parallelism(False, s),
             "status": st, "objective": obj, "iterations_to_optimal": s["iterations"],
             "time_to_optimal_s": el, "load_s": t_load,
             "value": s["iterations"] / el if el > 0 else None, "unit": "iterations/s (whole solve)",
             "bump_dim": s["bump_dim"], "y_rows": s["y_rows"], "refactors": s["refactors"],
             "gj_refactors": s["gj_refactors"], "max_inv_resid": s["max_inv_resid"],
             "price_sweep": sweep}
+
+
+def host_input(args, lib, ctx, m, n, label, reps):
+    """Time-to-optimal with A in host memory (incl. H2D, excl.
+    generation): elp_load_dense from a numpy array -- the entry point the R glue
+    calls -- through the pinned staging pipeline, to every device
+    of the handle from one pass over host memory."""
+    import numpy as np
+    import torch
+    from easylp_amd import generate_dense_device
+    A, b, c = generate_dense_device(args.seed, m, n, ctx.devices[0])
+    Ah = A.cpu().numpy().reshape(n, m).T  # column-major (m, n) view: no copy at load
+    del A
+    torch.cuda.empty_cache()
+    p, _ = make_problem(args, lib, m, n, ctx)
+    dirs = np.ones(m, np.int32)
+    out = []
+    for _ in range(reps):
+        ctx.sync()
+        t0 = time.perf_counter()
+        p.load_dense(Ah, dirs, b, c, maximize=True)
+        t_load = time.perf_counter() - t0
+        st = p.solve()
+        el = time.perf_counter() - t0
+        s = p.stats()
+        out.append({"status": st, "time_to_optimal_s": el, "load_s": t_load, "h2d_s": s["seconds_h2d"],
+                    "h2d_GBps": s["h2d_bytes"] / s["seconds_h2d"] / 1e9 if s["seconds_h2d"] > 0 else None,
+                    "iterations": s["iterations"]})
+    obj = p.solution(out[-1]["status"]).objval
+    p.close()
+    del Ah
+    best = min(out, key=lambda r: r["time_to_optimal_s"])
+    return {"workload": "%s from host memory (elp_load_dense, pageable numpy A)" % label,
+            "parallelism": ctx.parallelism(False, {"exchange": 0}) if ctx.ngpu == 1 else "ngpu x%d" % ctx.ngpu,
+            "h2d_bytes": 8.0 * m * n, "objective": obj, "runs": out, "best": best}
 
 
 def sparse_rate(args, local, with_cpu):
@@ -323,11 +446,11 @@ def sparse_rate(args, local, with_cpu):
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    if args.mode == "procs" and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(relaunch_under_torchrun(args))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world:
+    if world > 1 and args.gpus != world:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
 
     import torch
@@ -340,30 +463,32 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group("gloo", init_method="env://", rank=0, world_size=1)
+    ctx = Ctx(args, world, rank, local, dist)
+    if not ctx.works:
+        # torchrun rank of the ngpu mode: rank 0's one process drives every GPU;
+        # this rank joins the barriers around the timed region and the max, then
+        # waits for the end (it touches no GPU)
+        dist.barrier()
+        dist.barrier()
+        ctx.max_over_ranks(0.0)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     torch.cuda.set_device(local)
 
-    from easylp_amd import generate_dense_device
     from easylp_amd._lib import load
 
     lib = load()
 
-    def barrier():
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
+    As, b, c = place_A(args.seed, args.m, args.n, ctx)  # resident in HBM, untimed
+    p, p2p = make_problem(args, lib, args.m, args.n, ctx)
 
-    A, b, c = generate_dense_device(args.seed, args.m, args.n, local)  # resident in HBM, untimed
-    p, p2p = make_problem(args, lib, args.m, args.n, world, rank, local)
-
-    full_solves(p, A, b, c, args.warmup, barrier)  # warmup (untimed)
-    barrier()
+    full_solves(p, As, b, c, args.warmup, ctx)  # warmup (untimed)
+    ctx.barrier()
     t0 = time.perf_counter()
-    recs = full_solves(p, A, b, c, args.steps, barrier)  # (ends with a barrier)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    recs = full_solves(p, As, b, c, args.steps, ctx)
+    ctx.barrier()
+    elapsed = ctx.max_over_ranks(time.perf_counter() - t0)
     stats = [r[2] for r in recs]
     iters = sum(s["iterations"] for s in stats)
     value = iters / elapsed if elapsed > 0 else 0.0
@@ -382,14 +507,13 @@ def main():
 
     window = None  # steady state of one solve: iterations [100, 1100)
     if args.window:
-        import numpy as np
-        p.load_dense_device(A.data_ptr(), np.ones(args.m, np.int32), b, c, maximize=True)
+        load_resident(p, As, b, c)
         p.iterate(100)
-        barrier()
+        ctx.sync()
         w0 = p.stats()
         tw = time.perf_counter()
         p.iterate(1000)
-        barrier()
+        ctx.sync()
         tw = time.perf_counter() - tw
         w1 = p.stats()
         wit = w1["iterations"] - w0["iterations"]
@@ -399,33 +523,42 @@ def main():
                   "us_per_iteration": 1e6 * tw / max(wit, 1), "price_frac": wr["frac"],
                   "price_avg_launch_us": wr["avg_launch_us"]}
 
-    traffic, traffic_src = committed_traffic(args) if world == 1 else (None, None)
+    traffic, traffic_src = committed_traffic(args) if max(world, ctx.ngpu) == 1 else (None, None)
 
     other = None  # the same LP to optimality under the other pricing rule
-    if args.compare_rules and world == 1 and not args.force_sharded:
+    if args.compare_rules and max(world, ctx.ngpu) == 1 and not args.force_sharded:
         from easylp_amd import Problem
         import numpy as np
         with Problem(args.m, args.n, device=local, pricing=1 - args.rule, sync_every=args.sync_every) as q:
             tq = time.perf_counter()
-            q.load_dense_device(A.data_ptr(), np.ones(args.m, np.int32), b, c, maximize=True)
+            q.load_dense_device(As[0].data_ptr(), np.ones(args.m, np.int32), b, c, maximize=True)
             qst = q.solve()
             tq = time.perf_counter() - tq
             qs = q.stats()
             other = {"pricing": "dantzig" if args.rule else "devex", "status": qst,
                      "objective": q.solution(qst).objval, "iterations_to_optimal": qs["iterations"],
                      "time_to_optimal_s": tq}
+    parallelism = ctx.parallelism(p2p, last)
     p.close()
-    del A
+    del As
     torch.cuda.empty_cache()
 
-    c4 = c4_config(args, lib, world, rank, local, barrier, dist) if args.c4 else None
+    hosted = None
+    if args.host_input and ctx.mode != "procs":
+        hosted = {"c3": host_input(args, lib, ctx, args.m, args.n, "dense LP m=%d n=%d" % (args.m, args.n), 3)}
+        torch.cuda.empty_cache()
+
+    c4 = c4_config(args, lib, ctx) if args.c4 else None
+    if hosted is not None and args.host_c4 and args.c4 and ctx.ngpu == 1:
+        hosted["c4"] = host_input(args, lib, ctx, 10000, 500000, "dense LP m=10000 n=500000", 1)
+        torch.cuda.empty_cache()
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and max(world, ctx.ngpu) == 1 and not args.no_cpu:
         cpu = cpu_baseline(args)
 
     sparse = None
-    if args.sparse and world == 1:
+    if args.sparse and max(world, ctx.ngpu) == 1:
         sparse = sparse_rate(args, local, rank == 0 and not args.no_cpu)
 
     if rank == 0:
@@ -433,7 +566,7 @@ def main():
             "metric": METRIC,
             "value": value,
             "unit": "iterations/s",
-            "n_gpus": world,
+            "n_gpus": max(world, ctx.ngpu),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / max(args.steps, 1),
@@ -446,8 +579,7 @@ def main():
                 "workload": "dense random LP m=%d n=%d (BASELINE configs[2]), step = one full solve "
                             "(load from HBM + solve to optimality)" % (args.m, args.n),
                 "m": args.m, "n": args.n, "seed": args.seed,
-                "parallelism": ("column-shard x%d, %s min-loc" % (world, "xGMI mailbox" if p2p else "RCCL all-gather")
-                                if world > 1 or args.force_sharded else "single GPU"),
+                "parallelism": parallelism,
                 "iterations_timed": iters,
                 "pricing": args.pricing,
             },
@@ -463,12 +595,15 @@ def main():
                 "traffic_source": traffic_src,
             },
             "iteration_roofline": iteration_roofline(stats),
+            "host_input": hosted,
             "cpu_baseline": cpu,
             "scaling_config": c4,
             "sparse_config": sparse,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
+        if ctx.mode == "ngpu":
+            dist.barrier()
         dist.destroy_process_group()
 
 

@@ -18,11 +18,11 @@ ELP_PROFILE_PRICE = 2   # device-clock pricing timer
 ELP_PROFILE_EVENTS = 4  # HIP events on every pricing dispatch
 ELP_PROFILE_SAMPLE = 8  # ... on those of every 8th chunk between host polls
 ELP_SCALE_GEOMETRIC, ELP_SCALE_EQUILIBRATE = 4, 64
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # every entry point the header declares (checked by tests/test_abi.py)
 EXPORTS = (
-    "elp_default_control", "elp_create", "elp_load_dense", "elp_load_dense_device",
+    "elp_default_control", "elp_create", "elp_load_dense", "elp_load_dense_device", "elp_load_dense_device_multi",
     "elp_load_generated", "elp_generate_dense", "elp_load_csc", "elp_set_int", "elp_solve", "elp_iterate", "elp_get_solution",
     "elp_get_stats", "elp_sensitivity",
     "elp_set_trace", "elp_get_trace", "elp_comm_unique_id", "elp_comm_init", "elp_comm_init_host", "elp_comm_enable_p2p",
@@ -57,7 +57,7 @@ class ElpControl(ctypes.Structure):
         ("pricing", ctypes.c_int32),
         ("ngpu", ctypes.c_int32),
         ("scaling", ctypes.c_int32),
-        ("reserved0", ctypes.c_int32),
+        ("exchange", ctypes.c_int32),
         ("tol_singular", ctypes.c_double),
         ("mailbox_timeout", ctypes.c_double),
     ]
@@ -90,6 +90,10 @@ class ElpStats(ctypes.Structure):
         ("price_launches", ctypes.c_int64),
         ("max_inv_resid", ctypes.c_double),
         ("iter_bytes", ctypes.c_double),
+        ("exchange", ctypes.c_int32),
+        ("reserved1", ctypes.c_int32),
+        ("seconds_h2d", ctypes.c_double),
+        ("h2d_bytes", ctypes.c_double),
     ]
 
 
@@ -100,6 +104,41 @@ class ElpError(RuntimeError):
 _lib = None
 
 
+def hip_runtime_files() -> list[str]:
+    """The HIP / HSA runtime files mapped into this process (/proc/self/maps)."""
+    out = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                p = line.split()[-1]
+                if "libamdhip64" in p or "libhsa-runtime64" in p:
+                    out.add(p)
+    except OSError:
+        pass
+    return sorted(out)
+
+
+def _one_runtime() -> None:
+    """One HIP runtime per process.  torch bundles its own ROCm (7.0) under the
+    same SONAMEs the library needs (libamdhip64.so.7, libhsa-runtime64.so.1); if
+    the library loaded first it would start /opt/rocm's runtime and a later
+    torch would start a second HSA runtime beside it -- the r02 `elp_create:
+    hipSetDevice failed` (tools/runtime_probe.py: lib_first).  Sharing
+    /opt/rocm's runtime with torch works but aborts at exit (preload_all).  So a
+    Python process that has torch binds the library to torch's runtime: torch
+    is imported first (no device call), and the library's NEEDED entries then
+    resolve to the runtime already loaded.  Processes without torch (R, the C
+    driver, ELP_NO_TORCH=1) use /opt/rocm's runtime through the RUNPATH."""
+    if os.environ.get("ELP_NO_TORCH"):
+        return
+    if any("libamdhip64" in p for p in hip_runtime_files()):
+        return  # a runtime is already there: bind to it
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load(path: str | None = None):
     """Load the HIP library; raises (loudly) if it is absent."""
     global _lib
@@ -108,6 +147,7 @@ def load(path: str | None = None):
     path = path or LIB_PATH
     if not os.path.exists(path):
         raise ElpError(f"{path} not built: run `python -m easylp_amd.build` (no CPU fallback)")
+    _one_runtime()
     lib = ctypes.CDLL(path)
     P, vp = ctypes.POINTER, ctypes.c_void_p
     i64, i32, dbl = ctypes.c_int64, ctypes.c_int32, ctypes.c_double
@@ -116,6 +156,7 @@ def load(path: str | None = None):
     lib.elp_create.argtypes = [P(vp), i64, i64, P(ElpControl)]
     lib.elp_load_dense.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32]
     lib.elp_load_dense_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32]
+    lib.elp_load_dense_device_multi.argtypes = [vp, P(vp), i32, vp, vp, vp, vp, vp, i32]
     lib.elp_load_generated.argtypes = [vp, ctypes.c_uint64]
     lib.elp_generate_dense.argtypes = [i32, ctypes.c_uint64, i64, i64, vp, vp, vp]
     lib.elp_load_csc.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32]
@@ -135,7 +176,8 @@ def load(path: str | None = None):
     lib.elp_destroy.restype = None
     lib.elp_last_error.restype = ctypes.c_char_p
     lib.elp_abi_version.restype = i32
-    for name in ("elp_create", "elp_load_dense", "elp_load_dense_device", "elp_load_generated",
+    for name in ("elp_create", "elp_load_dense", "elp_load_dense_device", "elp_load_dense_device_multi",
+                 "elp_load_generated",
                  "elp_generate_dense",
                  "elp_load_csc", "elp_sensitivity", "elp_set_int",
                  "elp_solve", "elp_iterate", "elp_get_solution", "elp_get_stats",

@@ -15,7 +15,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <atomic>
+#include <condition_variable>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -103,7 +105,8 @@ struct elp_handle {
     std::unique_ptr<elp::ThreadGroup> tgroup;  // ranks sharing a device
     std::vector<elp::ThreadRank> tranks;
     std::vector<double*> peer_A;  // elp_load_dense_device: A copied to the other devices
-    size_t peer_A_count = 0;
+    std::vector<size_t> peer_A_bytes;  // (elements held by each copy)
+    bool broken = false;          // a rank failed and the RCCL communicators were aborted
     // scaling (elp_control.scaling): the solver works on A~ = 2^srow A 2^scol
     // (exponents per row and per GLOBAL column; empty: unscaled)
     std::vector<int32_t> srow_h, scol_h;
@@ -203,6 +206,9 @@ static bool is_group(const elp_handle* h) { return h && !h->ranks.empty(); }
 
 template <class F>
 static int fan_out(elp_handle* g, F&& f) {
+    if (g->broken)
+        return fail(ELP_E_STATE, "ngpu handle: a rank failed earlier and the communicators were aborted; "
+                                 "destroy the handle");
     const int P = (int)g->ranks.size();
     if (g->tgroup) g->tgroup->reset();
     std::vector<int> rc(P, 0);
@@ -214,7 +220,15 @@ static int fan_out(elp_handle* g, F&& f) {
             err[r] = g_err;
             int none = -1;
             first.compare_exchange_strong(none, r);
-            if (g->tgroup) g->tgroup->abort();  // release the ranks waiting in a collective
+            // release the ranks waiting in a collective: the in-process transport
+            // fails its waiters; distinct devices abort every RCCL communicator
+            // (the handle is unusable afterwards: later calls fail ELP_E_STATE)
+            if (g->tgroup) {
+                g->tgroup->abort();
+            } else if (none < 0) {
+                for (elp_handle* rh : g->ranks) rh->comm.abort_rccl();
+                g->broken = true;
+            }
         }
     };
     std::vector<std::thread> th;
@@ -238,6 +252,80 @@ static void destroy_group(elp_handle* g) {
         if (r) elp_destroy(r);
     g->ranks.clear();
     g->tgroup.reset();
+}
+
+// ngpu: the per-iteration min-loc over a direct peer mailbox.
+// One process drives every rank, so no IPC: each rank's mailbox is uncached
+// memory on its own device, every device enables peer access to every other
+// one, and each rank gets a device array of the P raw mailbox pointers -- the
+// same store / poll protocol as the multi-process mailbox (p2p_exchange).  The
+// P probes run concurrently (one per rank stream); only when every round trip
+// arrives do the ranks adopt the mailboxes, else everything is released and
+// the collective stays (returns 0 either way; errors of the set-up are not
+// fatal).  Ranks that share a device (the one-GPU test box) use same-device
+// pointers; their streams must land on distinct hardware queues, which the
+// probe checks (spinning kernels behind each other on one queue never meet).
+static void enable_group_p2p(elp_handle* g) {
+    const int P = (int)g->ranks.size();
+    if (P > 64 || g->ctl.exchange == 1) return;
+    if (const char* e = std::getenv("ELP_NGPU_MAILBOX"))
+        if (std::atoi(e) == 0) return;
+    const size_t rec = sizeof(MboxRec), bytes = 2 * (size_t)P * rec;
+    std::vector<void*> mb(P, nullptr);
+    std::vector<void**> dp(P, nullptr);
+    std::vector<int32_t*> dok(P, nullptr);
+    bool ok = true;
+    for (int r = 0; r < P && ok; ++r)
+        for (int t = 0; t < P && ok; ++t) {
+            const int a = g->rank_dev[r], b = g->rank_dev[t];
+            if (a == b) continue;
+            int can = 0;
+            if (hipSetDevice(a) != hipSuccess || hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) {
+                ok = false;
+                break;
+            }
+            const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) ok = false;
+            (void)hipGetLastError();
+        }
+    for (int r = 0; r < P && ok; ++r) {
+        ok = hipSetDevice(g->rank_dev[r]) == hipSuccess &&
+             hipExtMallocWithFlags(&mb[r], bytes, hipDeviceMallocUncached) == hipSuccess &&
+             hipMemset(mb[r], 0, bytes) == hipSuccess && hipMalloc((void**)&dok[r], sizeof(int32_t)) == hipSuccess &&
+             hipMemset(dok[r], 0, sizeof(int32_t)) == hipSuccess;
+    }
+    for (int r = 0; r < P && ok; ++r) {
+        ok = hipSetDevice(g->rank_dev[r]) == hipSuccess && hipMalloc((void**)&dp[r], sizeof(void*) * P) == hipSuccess &&
+             hipMemcpy(dp[r], mb.data(), sizeof(void*) * P, hipMemcpyHostToDevice) == hipSuccess;
+    }
+    if (ok) {
+        // a probe round trip takes microseconds once every kernel runs: a short
+        // limit keeps a doomed set-up (shared hardware queues) cheap
+        const double secs = std::min(g->ctl.mailbox_timeout, 0.5);
+        int launched = 0;
+        for (int r = 0; r < P && ok; ++r, ++launched)
+            ok = hipSetDevice(g->rank_dev[r]) == hipSuccess &&
+                 launch_mbox_probe((void* const*)dp[r], mb[r], P, r, (int64_t)rec, dok[r],
+                                   (unsigned long long)(secs * 1e8), g->ranks[r]->st) == hipSuccess;
+        for (int r = 0; r < launched; ++r) {  // every launched probe drains (bounded by its limit)
+            int32_t v = 0;
+            const bool got = hipSetDevice(g->rank_dev[r]) == hipSuccess &&
+                             hipStreamSynchronize(g->ranks[r]->st) == hipSuccess &&
+                             hipMemcpy(&v, dok[r], sizeof(v), hipMemcpyDeviceToHost) == hipSuccess;
+            ok = ok && got && v == 1;
+        }
+    }
+    for (int r = 0; r < P; ++r) {
+        (void)hipSetDevice(g->rank_dev[r]);
+        if (dok[r]) (void)hipFree(dok[r]);
+        if (ok) {
+            g->ranks[r]->comm.adopt_p2p(mb[r], dp[r]);
+        } else {
+            if (mb[r]) (void)hipFree(mb[r]);
+            if (dp[r]) (void)hipFree(dp[r]);
+        }
+    }
+    (void)hipGetLastError();
 }
 
 static int create_group(elp_handle* g) {
@@ -276,6 +364,8 @@ static int create_group(elp_handle* g) {
         }
     }
     g->peer_A.assign(P, nullptr);
+    g->peer_A_bytes.assign(P, 0);
+    enable_group_p2p(g);
     return 0;
 }
 
@@ -344,7 +434,9 @@ static int alloc_all(elp_handle* h) {
     d.mb_ticks = (int64_t)(h->ctl.mailbox_timeout * 1e8);  // s_memrealtime: 100 MHz
     d.ptimer = (h->ctl.verbose & ELP_PROFILE_PRICE) ? 1 : 0;
     d.csc = h->csc ? 1 : 0;
-    d.p2p = h->comm.p2p;
+    // the mailbox carries the min-loc record only: with A not replicated the
+    // entering column must travel, so that load uses the collective
+    d.p2p = h->comm.p2p && h->replicated ? 1 : 0;
     d.rank = h->comm.rank;
     d.mbox = (MboxRec*)h->comm.mbox;
     d.mpeers = (MboxRec* const*)h->comm.dpeers;
@@ -634,7 +726,7 @@ static void scale_csc(elp_handle* h, const int64_t* cp, const int32_t* ri, doubl
         for (int64_t j = 0; j < n; ++j) {
             int mn = EMN, mx = EMX;
             for (int64_t t = cp[j]; t < cp[j + 1]; ++t) {
-                if (val[t] == 0.0) continue;
+                if (val[t] == 0.0) continue;  // (elp_load_csc rejects non-finite values)
                 const int e = ilogb_i(val[t]) + rho[(size_t)ri[t]];
                 mn = std::min(mn, e);
                 mx = std::max(mx, e);
@@ -817,6 +909,7 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
     h->stats.rank = h->comm.rank;
     h->stats.col0 = h->col0;
     h->stats.ncols = h->nloc;
+    h->stats.exchange = h->comm.kind == 0 ? 0 : d.p2p ? 1 : 2;
     h->timing_started = false;
     if (infeasible) {  // R/class.R:297-298: lower > upper -> "unfeasible"
         h->done = true;
@@ -835,6 +928,172 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
         HIPCHK(hipStreamSynchronize(h->st));
     }
     return 0;
+}
+
+// ---------------------------------------------------------------- host -> device
+// elp_load_dense's copy of A from the caller's pageable memory (the R matrix,
+// the one H2D copy that replaces the add.constraint loop).  A
+// pageable hipMemcpy stages through the runtime's own small pinned buffers one
+// at a time; here host threads copy chunk c into pinned buffer c % STAGE_BUFS
+// while the DMA engines move the chunks before it, and every device that needs
+// a range of A (all ranks of an ngpu handle) receives each chunk from the same
+// pinned buffer -- A is read from host memory once however many devices get it.
+namespace {
+constexpr size_t STAGE_BYTES = (size_t)16 << 20;  // per chunk
+constexpr int STAGE_BUFS = 6;
+constexpr size_t STAGE_MIN = (size_t)8 << 20;     // below this: one plain copy
+
+struct H2DTarget {
+    int dev;
+    hipStream_t st;
+    double* dst;    // receives source elements [e0, e1)
+    size_t e0, e1;
+};
+
+// persistent pinned chunks (process lifetime: pinning 96 MB costs more than
+// most loads); one staged upload at a time
+std::mutex g_stage_mu;
+void* g_stage[STAGE_BUFS] = {};
+
+// memcpy of one chunk split over T host threads (memory-bandwidth bound: one
+// thread reaches ~1/4 of what the DMA engines take)
+struct CopyPool {
+    int T;
+    std::vector<std::thread> th;
+    std::mutex mu;
+    std::condition_variable cv, done;
+    const char* src = nullptr;
+    char* dst = nullptr;
+    size_t bytes = 0;
+    uint64_t gen = 0;
+    int pending = 0;
+    bool quit = false;
+    explicit CopyPool(int t) : T(t) {
+        for (int i = 0; i < T; ++i) th.emplace_back([this, i] { work(i); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            quit = true;
+        }
+        cv.notify_all();
+        for (auto& t : th) t.join();
+    }
+    void work(int i) {
+        uint64_t seen = 0;
+        for (;;) {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return quit || gen != seen; });
+            if (quit) return;
+            seen = gen;
+            const char* s = src;
+            char* d = dst;
+            const size_t b = bytes;
+            lk.unlock();
+            size_t per = (b + (size_t)T - 1) / (size_t)T;
+            per = (per + 4095) & ~(size_t)4095;
+            const size_t o = (size_t)i * per;
+            if (o < b) std::memcpy(d + o, s + o, std::min(per, b - o));
+            lk.lock();
+            if (--pending == 0) done.notify_one();
+        }
+    }
+    void copy(void* d, const void* s, size_t b) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            src = static_cast<const char*>(s);
+            dst = static_cast<char*>(d);
+            bytes = b;
+            pending = T;
+            ++gen;
+        }
+        cv.notify_all();
+        std::unique_lock<std::mutex> lk(mu);
+        done.wait(lk, [&] { return pending == 0; });
+    }
+};
+}  // namespace
+
+// copy src[e0, e1) of every target to its device; returns after every DMA is done
+static int h2d_staged(const double* src, std::vector<H2DTarget>& tg) {
+    size_t lo = SIZE_MAX, hi = 0;
+    for (const H2DTarget& t : tg)
+        if (t.e1 > t.e0) {
+            lo = std::min(lo, t.e0);
+            hi = std::max(hi, t.e1);
+        }
+    if (hi <= lo) return 0;
+    if ((hi - lo) * sizeof(double) < STAGE_MIN) {
+        for (const H2DTarget& t : tg)
+            if (t.e1 > t.e0) {
+                HIPCHK(hipSetDevice(t.dev));
+                HIPCHK(hipMemcpyAsync(t.dst, src + t.e0, (t.e1 - t.e0) * sizeof(double), hipMemcpyHostToDevice,
+                                      t.st));
+                HIPCHK(hipStreamSynchronize(t.st));
+            }
+        return 0;
+    }
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    for (int b = 0; b < STAGE_BUFS; ++b)
+        if (!g_stage[b] && hipHostMalloc(&g_stage[b], STAGE_BYTES, hipHostMallocDefault) != hipSuccess) {
+            g_stage[b] = nullptr;
+            return fail(ELP_E_NOMEM, "elp_load_dense: pinned staging allocation failed");
+        }
+    const size_t P = tg.size();
+    std::vector<hipEvent_t> ev(P * STAGE_BUFS, nullptr);
+    std::vector<char> used(P * STAGE_BUFS, 0);
+    int rc = 0;
+    for (size_t t = 0; t < P && !rc; ++t)
+        for (int b = 0; b < STAGE_BUFS && !rc; ++b)
+            if (hipSetDevice(tg[t].dev) != hipSuccess ||
+                hipEventCreateWithFlags(&ev[t * STAGE_BUFS + b], hipEventDisableTiming) != hipSuccess)
+                rc = fail(ELP_E_HIP, "elp_load_dense: event creation failed");
+    if (!rc) {
+        const unsigned hw = std::thread::hardware_concurrency();
+        CopyPool pool((int)std::max(1u, std::min(8u, hw ? hw : 1u)));
+        const size_t ce = STAGE_BYTES / sizeof(double);
+        size_t c = 0;
+        for (size_t e = lo; e < hi && !rc; e += ce, ++c) {
+            const size_t f = std::min(hi, e + ce);
+            const int b = (int)(c % STAGE_BUFS);
+            for (size_t t = 0; t < P && !rc; ++t)  // buffer b's last DMAs are done
+                if (used[t * STAGE_BUFS + b] && hipEventSynchronize(ev[t * STAGE_BUFS + b]) != hipSuccess)
+                    rc = fail(ELP_E_HIP, "elp_load_dense: staging wait failed");
+            if (rc) break;
+            pool.copy(g_stage[b], src + e, (f - e) * sizeof(double));
+            for (size_t t = 0; t < P && !rc; ++t) {
+                const size_t a0 = std::max(e, tg[t].e0), a1 = std::min(f, tg[t].e1);
+                if (a1 <= a0) continue;
+                if (hipSetDevice(tg[t].dev) != hipSuccess ||
+                    hipMemcpyAsync(tg[t].dst + (a0 - tg[t].e0), static_cast<double*>(g_stage[b]) + (a0 - e),
+                                   (a1 - a0) * sizeof(double), hipMemcpyHostToDevice, tg[t].st) != hipSuccess ||
+                    hipEventRecord(ev[t * STAGE_BUFS + b], tg[t].st) != hipSuccess)
+                    rc = fail(ELP_E_HIP, "elp_load_dense: staged copy failed");
+                used[t * STAGE_BUFS + b] = 1;
+            }
+        }
+    }
+    for (size_t t = 0; t < P; ++t) {
+        (void)hipSetDevice(tg[t].dev);
+        if (hipStreamSynchronize(tg[t].st) != hipSuccess && !rc) rc = fail(ELP_E_HIP, "elp_load_dense: H2D failed");
+        for (int b = 0; b < STAGE_BUFS; ++b)
+            if (ev[t * STAGE_BUFS + b]) (void)hipEventDestroy(ev[t * STAGE_BUFS + b]);
+    }
+    return rc;
+}
+
+// will this rank hold all of A (prep_load's rule, before prep_load ran)?
+static bool will_replicate(const elp_handle* h) {
+    const double abytes = 8.0 * (double)h->m * (double)h->n;
+    return h->comm.kind != 0 && (h->ctl.replicate == 1 || (h->ctl.replicate == 0 && abytes <= 64.0 * (1ull << 30)));
+}
+static int64_t shard_col0(const elp_handle* h) {
+    return h->comm.world > 1 ? (int64_t)h->comm.rank * h->n / h->comm.world : 0;
+}
+static int64_t shard_ncols(const elp_handle* h) {
+    if (h->comm.world <= 1) return h->n;
+    const int64_t P = h->comm.world, r = h->comm.rank;
+    return (r + 1) * h->n / P - r * h->n / P;
 }
 
 static int prep_load(elp_handle* h, bool csc = false) {
@@ -860,34 +1119,76 @@ static int prep_load(elp_handle* h, bool csc = false) {
     const double abytes = 8.0 * (double)h->m * (double)h->n;
     h->replicated = h->comm.kind != 0 &&
                     (h->ctl.replicate == 1 || (h->ctl.replicate == 0 && abytes <= 64.0 * (1ull << 30)));
-    if (h->comm.p2p && !h->replicated)
-        return fail(ELP_E_UNSUPPORTED, "xGMI mailbox exchange needs A replicated on every rank");
     const int rc = alloc_all(h);
     load_mark(h, "alloc");
     return rc;
 }
 
-extern "C" int elp_load_dense(elp_handle* h, const double* A, const int32_t* dir, const double* rhs,
-                              const double* obj, const double* lo, const double* up, int32_t maximize) {
-    if (is_group(h))
-        return fan_out(h, [&](elp_handle* r, int) { return elp_load_dense(r, A, dir, rhs, obj, lo, up, maximize); });
-    const double t0 = now_s();
-    if (!h || !obj || (h->m > 0 && (!A || !dir || !rhs))) return fail(ELP_E_ARG, "elp_load_dense: NULL input");
+// elp_load_dense, part 1: the device copy of A this rank owns (all of A when
+// replicated, else its column shard), allocated but not yet filled
+static int dense_host_prepare(elp_handle* h) {
     int rc = prep_load(h);
     if (rc) return rc;
-    const int64_t c0 = h->replicated ? 0 : h->col0, nc = h->replicated ? h->n : h->nloc;
+    const int64_t nc = h->replicated ? h->n : h->nloc;
     const size_t cnt = (size_t)h->m * (size_t)nc;
     HIPCHK(take_or_alloc(&h->A_owned, cnt * sizeof(double), &h->keep_A, &h->keep_A_bytes));
     h->A_owned_bytes = cnt * sizeof(double);
-    if (cnt)
-        HIPCHK(hipMemcpyAsync(h->A_owned, A + (size_t)c0 * (size_t)h->m, cnt * sizeof(double),
-                              hipMemcpyHostToDevice, h->st));
-    rc = scale_dense(h, h->A_owned, c0, nc);
+    return 0;
+}
+// the source range [e0, e1) of the column-major host A this rank receives
+static H2DTarget dense_host_target(elp_handle* h) {
+    const int64_t c0 = h->replicated ? 0 : h->col0, nc = h->replicated ? h->n : h->nloc;
+    return H2DTarget{h->dev, h->st, h->A_owned, (size_t)c0 * (size_t)h->m, (size_t)(c0 + nc) * (size_t)h->m};
+}
+// part 2 (A uploaded): scaling in place, then the common tail
+static int dense_host_finish(elp_handle* h, const int32_t* dir, const double* rhs, const double* obj,
+                             const double* lo, const double* up, int32_t maximize) {
+    HIPCHK(hipSetDevice(h->dev));
+    const int64_t c0 = h->replicated ? 0 : h->col0, nc = h->replicated ? h->n : h->nloc;
+    int rc = scale_dense(h, h->A_owned, c0, nc);
     if (rc) return rc;
     h->d.A = h->A_owned + (size_t)(h->col0 - c0) * (size_t)h->m;
     h->d.Afull = h->replicated ? h->A_owned : nullptr;
-    rc = load_common(h, dir, rhs, obj, lo, up, maximize);
-    h->stats.seconds_load = now_s() - t0;
+    return load_common(h, dir, rhs, obj, lo, up, maximize);
+}
+
+extern "C" int elp_load_dense(elp_handle* h, const double* A, const int32_t* dir, const double* rhs,
+                              const double* obj, const double* lo, const double* up, int32_t maximize) {
+    const double t0 = now_s();
+    if (!h || !obj || (h->m > 0 && (!A || !dir || !rhs))) return fail(ELP_E_ARG, "elp_load_dense: NULL input");
+    std::vector<elp_handle*> rk;
+    if (is_group(h)) {
+        rk = h->ranks;
+        int rc = fan_out(h, [&](elp_handle* r, int) { return dense_host_prepare(r); });
+        if (rc) return rc;
+    } else {
+        rk.push_back(h);
+        int rc = dense_host_prepare(h);
+        if (rc) return rc;
+    }
+    // A crosses PCIe once per device that needs it, from one pass over host memory
+    std::vector<H2DTarget> tg;
+    double hbytes = 0.0;
+    size_t lo_e = SIZE_MAX, hi_e = 0;
+    for (elp_handle* r : rk) {
+        tg.push_back(dense_host_target(r));
+        lo_e = std::min(lo_e, tg.back().e0);
+        hi_e = std::max(hi_e, tg.back().e1);
+    }
+    if (hi_e > lo_e) hbytes = (double)(hi_e - lo_e) * sizeof(double);
+    const double t1 = now_s();
+    int rc = h2d_staged(A, tg);
+    const double th2d = now_s() - t1;
+    if (rc) return rc;
+    if (is_group(h))
+        rc = fan_out(h, [&](elp_handle* r, int) { return dense_host_finish(r, dir, rhs, obj, lo, up, maximize); });
+    else
+        rc = dense_host_finish(h, dir, rhs, obj, lo, up, maximize);
+    for (elp_handle* r : rk) {
+        r->stats.seconds_load = now_s() - t0;
+        r->stats.seconds_h2d = th2d;
+        r->stats.h2d_bytes = hbytes;
+    }
     return rc;
 }
 
@@ -896,22 +1197,26 @@ extern "C" int elp_load_dense_device(elp_handle* h, const double* dA, const int3
                                      const double* up, int32_t maximize) {
     if (is_group(h)) {
         // every rank reads A from its own HBM: ranks on other devices get a copy
-        const size_t cnt = (size_t)h->m * (size_t)h->n;
-        const size_t have = h->peer_A_count;
-        h->peer_A_count = std::max(have, cnt);
+        // of what they read -- all of A when replicated, else their column shard
+        // (addressed through the full-shape base, so d.A = base + col0 * m)
         return fan_out(h, [&](elp_handle* r, int k) {
             const double* src = dA;
+            const int64_t c0 = will_replicate(r) ? 0 : shard_col0(r);
+            const int64_t nc = will_replicate(r) ? r->n : shard_ncols(r);
+            const size_t cnt = (size_t)h->m * (size_t)nc;
             if (cnt && h->rank_dev[k] != h->rank_dev[0]) {
                 if (hipSetDevice(h->rank_dev[k]) != hipSuccess) return fail(ELP_E_HIP, "hipSetDevice");
-                if (!h->peer_A[k] || have < cnt) {
+                if (!h->peer_A[k] || h->peer_A_bytes[k] != cnt) {
                     if (h->peer_A[k]) (void)hipFree(h->peer_A[k]);
                     h->peer_A[k] = nullptr;
+                    h->peer_A_bytes[k] = 0;
                     if (dalloc(&h->peer_A[k], cnt) != hipSuccess) return fail(ELP_E_NOMEM, "copy of A");
+                    h->peer_A_bytes[k] = cnt;
                 }
-                if (hipMemcpyPeer(h->peer_A[k], h->rank_dev[k], dA, h->rank_dev[0], cnt * sizeof(double)) !=
-                    hipSuccess)
+                if (hipMemcpyPeer(h->peer_A[k], h->rank_dev[k], dA + (size_t)c0 * (size_t)h->m, h->rank_dev[0],
+                                  cnt * sizeof(double)) != hipSuccess)
                     return fail(ELP_E_HIP, "hipMemcpyPeer of A");
-                src = h->peer_A[k];
+                src = h->peer_A[k] - (size_t)c0 * (size_t)h->m;
             }
             return elp_load_dense_device(r, src, dir, rhs, obj, lo, up, maximize);
         });
@@ -945,6 +1250,18 @@ extern "C" int elp_load_dense_device(elp_handle* h, const double* dA, const int3
     rc = load_common(h, dir, rhs, obj, lo, up, maximize);
     h->stats.seconds_load = now_s() - t0;
     return rc;
+}
+
+extern "C" int elp_load_dense_device_multi(elp_handle* h, const double* const* dA, int32_t count,
+                                           const int32_t* dir, const double* rhs, const double* obj,
+                                           const double* lo, const double* up, int32_t maximize) {
+    if (!h || !dA) return fail(ELP_E_ARG, "elp_load_dense_device_multi: NULL argument");
+    const int P = is_group(h) ? (int)h->ranks.size() : 1;
+    if (count != P)
+        return fail(ELP_E_ARG, "elp_load_dense_device_multi: count must equal the handle's rank count (" +
+                                   std::to_string(P) + ")");
+    if (!is_group(h)) return elp_load_dense_device(h, dA[0], dir, rhs, obj, lo, up, maximize);
+    return fan_out(h, [&](elp_handle* r, int k) { return elp_load_dense_device(r, dA[k], dir, rhs, obj, lo, up, maximize); });
 }
 
 // CSC input: validate, build the CSR copy on the host (row activities), upload.
@@ -1238,7 +1555,7 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             const int nyub = (int)std::min<int64_t>(h->m, (int64_t)ny0 + t);
             hipEvent_t e0 = prof_chunk ? h->ev[2 * t] : nullptr, e1 = prof_chunk ? h->ev[2 * t + 1] : nullptr;
             h->stats.price_launches++;
-            if (h->comm.kind == 0 || h->comm.p2p) {  // (p2p: min-loc inside the select kernel)
+            if (h->comm.kind == 0 || h->d.p2p) {  // (p2p: min-loc inside the select kernel)
                 HIPCHK(launch_iteration(h->d, kub, nyub, h->phase, h->st, e0, e1, t));
             } else {
                 // sharded: local min-loc -> all-gather -> global min-loc.  Replicated

@@ -67,6 +67,16 @@ struct Comm {
     static constexpr size_t SCRATCH_BYTES = 64 * (SCRATCH_RANKS + 1) + 64;
     void* scratch = nullptr;
     int enable_p2p(size_t rec_bytes, hipStream_t st, double timeout_s);
+    // single-process multi-device (elp_control.ngpu): the group allocated this
+    // rank's mailbox and the device array of every rank's mailbox (raw peer
+    // pointers after hipDeviceEnablePeerAccess, no IPC) and proved the round
+    // trip; the communicator takes ownership of both
+    void adopt_p2p(void* mine, void** dpeers_dev);
+    // ngpu on distinct devices: a rank failed while its peers may wait inside an
+    // RCCL collective -- ncclCommAbort releases them; the communicator is then
+    // unusable (every later collective fails)
+    void abort_rccl();
+    bool aborted = false;
 
     static int unique_id(uint8_t id[128]);
     int init_rccl(const uint8_t id[128], int world_size, int rank_);
@@ -83,5 +93,12 @@ struct Comm {
     int allreduce_max_i32(int32_t* dbuf, size_t count, hipStream_t st);
     int bcast_f64(double* dbuf, size_t count, int root, hipStream_t st);
 };
+
+// Mailbox round-trip probe (k_mbox_probe): thread t stores the reserved
+// sequence word into this rank's slots of peers[t]'s mailbox and waits (ticks
+// of the 100 MHz clock at most) for rank t's word in `mine`; *ok = 1 when all
+// arrived.  Every rank's probe must be in flight at the same time.
+hipError_t launch_mbox_probe(void* const* dpeers, void* mine, int P, int rank, int64_t rec_bytes, int32_t* ok,
+                             unsigned long long ticks, hipStream_t st);
 
 }  // namespace elp

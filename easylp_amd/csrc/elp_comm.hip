@@ -194,12 +194,36 @@ __global__ void k_mbox_probe(void* const* peers, void* mine, int P, int rank, in
     if (t == 0) *ok_out = fail ? 0 : 1;
 }
 
+hipError_t launch_mbox_probe(void* const* dpeers, void* mine, int P, int rank, int64_t rec_bytes, int32_t* ok,
+                             unsigned long long ticks, hipStream_t st) {
+    hipLaunchKernelGGL(k_mbox_probe, dim3(1), dim3(64), 0, st, dpeers, mine, P, rank, rec_bytes, ok, ticks);
+    return hipGetLastError();
+}
+
+void Comm::adopt_p2p(void* mine, void** dpeers_dev) {
+    mbox = mine;
+    dpeers = dpeers_dev;
+    p2p = 1;
+}
+
+void Comm::abort_rccl() {
+    if (kind == 1 && nccl && !aborted) {
+        (void)ncclCommAbort((ncclComm_t)nccl);
+        nccl = nullptr;
+        aborted = true;
+    }
+}
+
 // Collective over the communicator: every rank takes every step (the handle
 // all-gather and the final agreement), so a rank that fails to allocate or to
 // map a peer does not strand the others; if any rank failed, none uses p2p.
 int Comm::enable_p2p(size_t rec_bytes, hipStream_t st, double timeout_s) {
     if (kind == 0) return ELP_E_STATE;
     if (p2p) return 0;
+    // staging of the two collectives below: the scratch buffer allocated with
+    // the communicator, so no allocation here can make this rank skip them
+    // (checked before anything is allocated: callers keep world <= 64)
+    if (!scratch || world > SCRATCH_RANKS) return ELP_E_STATE;
     const size_t bytes = 2 * (size_t)world * rec_bytes;
     int ok = 1;
     hipIpcMemHandle_t mine;
@@ -212,9 +236,6 @@ int Comm::enable_p2p(size_t rec_bytes, hipStream_t st, double timeout_s) {
     if (ok && hipMemset(mbox, 0, bytes) != hipSuccess) ok = 0;
     if (ok && hipIpcGetMemHandle(&mine, mbox) != hipSuccess) ok = 0;
     static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
-    // staging of the two collectives below: the scratch buffer allocated with
-    // the communicator, so no allocation here can make this rank skip them
-    if (!scratch || world > SCRATCH_RANKS) return ELP_E_STATE;
     unsigned char* dstage = static_cast<unsigned char*>(scratch);
     std::vector<unsigned char> all(64 * (size_t)world);
     int rc = hipMemcpy(dstage + 64 * world, &mine, 64, hipMemcpyHostToDevice) == hipSuccess ? 0 : ELP_E_HIP;
@@ -246,9 +267,9 @@ int Comm::enable_p2p(size_t rec_bytes, hipStream_t st, double timeout_s) {
         int32_t* dok = reinterpret_cast<int32_t*>(dstage);
         int32_t hok = 0;
         const double secs = timeout_s > 0 ? timeout_s : 2.0;
-        hipLaunchKernelGGL(k_mbox_probe, dim3(1), dim3(64), 0, st, (void* const*)dpeers, mbox, world, rank,
-                           (int64_t)rec_bytes, dok, (unsigned long long)(secs * 1e8));
-        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess ||
+        if (launch_mbox_probe((void* const*)dpeers, mbox, world, rank, (int64_t)rec_bytes, dok,
+                              (unsigned long long)(secs * 1e8), st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess ||
             hipMemcpy(&hok, dok, sizeof(hok), hipMemcpyDeviceToHost) != hipSuccess || !hok)
             ok = 0;
     }
@@ -280,7 +301,8 @@ void Comm::destroy() {
     dpeers = nullptr;
     mbox = nullptr;
     p2p = 0;
-    if (kind == 1 && nccl) ncclCommDestroy((ncclComm_t)nccl);
+    if (kind == 1 && nccl && !aborted) ncclCommDestroy((ncclComm_t)nccl);
+    aborted = false;
     if (scratch) (void)hipFree(scratch);
     scratch = nullptr;
     nccl = nullptr;
@@ -289,6 +311,7 @@ void Comm::destroy() {
 }
 
 int Comm::allgather(const void* dsend, void* drecv, size_t bytes, hipStream_t st) {
+    if (aborted) return ELP_E_COMM;
     if (kind == 0) {
         if (dsend != drecv && hipMemcpyAsync(drecv, dsend, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
             return ELP_E_HIP;
@@ -316,6 +339,7 @@ static int host_allreduce(Comm& c, void* dbuf, size_t count, size_t esize, int d
 }
 
 int Comm::allreduce_sum_f64(double* dbuf, size_t count, hipStream_t st) {
+    if (aborted) return ELP_E_COMM;
     if (kind == 0) return 0;
     if (kind == 1)
         return ncclAllReduce(dbuf, dbuf, count, ncclFloat64, ncclSum, (ncclComm_t)nccl, st) == ncclSuccess
@@ -324,6 +348,7 @@ int Comm::allreduce_sum_f64(double* dbuf, size_t count, hipStream_t st) {
 }
 
 int Comm::allreduce_max_i32(int32_t* dbuf, size_t count, hipStream_t st) {
+    if (aborted) return ELP_E_COMM;
     if (kind == 0) return 0;
     if (kind == 1)
         return ncclAllReduce(dbuf, dbuf, count, ncclInt32, ncclMax, (ncclComm_t)nccl, st) == ncclSuccess
@@ -332,6 +357,7 @@ int Comm::allreduce_max_i32(int32_t* dbuf, size_t count, hipStream_t st) {
 }
 
 int Comm::bcast_f64(double* dbuf, size_t count, int root, hipStream_t st) {
+    if (aborted) return ELP_E_COMM;
     if (kind == 0) return 0;
     if (kind == 1)
         return ncclBroadcast(dbuf, dbuf, count, ncclFloat64, root, (ncclComm_t)nccl, st) == ncclSuccess

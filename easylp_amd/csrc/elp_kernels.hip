@@ -315,9 +315,9 @@ DEV double wave_art_sum(const Dev& d) {
 __global__ void k_init_cols(Dev d, const double* __restrict__ lo, const double* __restrict__ up) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= d.n) return;
-    double l = lo ? lo[j] : 0.0, u = up ? up[j] : HUGE_VAL;
-    if (l <= -d.infinity) l = -HUGE_VAL;
-    if (u >= d.infinity) u = HUGE_VAL;
+    // (the host mapped |v| >= elp_control.infinity to +-inf BEFORE scaling; a
+    //  finite bound that crosses 1e30 once scaled stays finite, as in the oracle)
+    const double l = lo ? lo[j] : 0.0, u = up ? up[j] : HUGE_VAL;
     d.lb[j] = l;
     d.ub[j] = u;
     d.cost[j] = 0.0;
@@ -444,9 +444,7 @@ __global__ void k_row_chain_csr(Dev d) {
 __global__ void k_init_rows(Dev d, const double* __restrict__ rhs_in) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= d.m) return;
-    double bi = rhs_in[i];
-    if (bi <= -d.infinity) bi = -HUGE_VAL;
-    if (bi >= d.infinity) bi = HUGE_VAL;
+    const double bi = rhs_in[i];  // (infinite values mapped by the host before scaling)
     d.b[i] = bi;
     const int n = d.n, m = d.m, sv = n + i, av = n + m + i;  // local ids
     const int svg = d.N + i, avg = d.N + m + i;                 // global ids
@@ -583,7 +581,7 @@ __global__ void __launch_bounds__(256) k_scale_col(int m, int64_t ncols, const d
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                if (i0 + 256 * u < m && a[u] != 0.0) {
+                if (i0 + 256 * u < m && a[u] != 0.0 && isfinite(a[u])) {  // (non-finite: no exponent)
                     const int e = ilogb(a[u]) + r[u];
                     mn = min(mn, e);
                     mx = max(mx, e);
@@ -639,7 +637,7 @@ __global__ void __launch_bounds__(256) k_scale_row_part(int m, int64_t ncols, co
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            if (j + u < j1 && a[u] != 0.0) {
+            if (j + u < j1 && a[u] != 0.0 && isfinite(a[u])) {
                 const int e = ilogb(a[u]) + g[u];
                 mn = min(mn, e);
                 mx = max(mx, e);

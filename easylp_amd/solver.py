@@ -145,6 +145,22 @@ class Problem:
             self._h, ctypes.c_void_p(int(dA_ptr)), d.ctypes.data, rhs.ctypes.data, obj.ctypes.data,
             lo.ctypes.data, up.ctypes.data, int(bool(maximize))), "elp_load_dense_device")
 
+    def load_dense_device_multi(self, dA_ptrs, dirs, rhs, obj, lo=None, up=None, maximize=False):
+        """ngpu handle, A resident on every device: dA_ptrs[r] is A (m*n float64,
+        column-major) on rank r's device (device + r); each rank reads its own copy
+        (elp_load_dense_device_multi)."""
+        m, n = self.m, self.n
+        d = dir_codes(dirs)
+        rhs = np.ascontiguousarray(rhs, dtype=np.float64).reshape(m)
+        obj = np.ascontiguousarray(obj, dtype=np.float64).reshape(n)
+        lo = np.zeros(n) if lo is None else np.ascontiguousarray(lo, dtype=np.float64)
+        up = np.full(n, np.inf) if up is None else np.ascontiguousarray(up, dtype=np.float64)
+        ptrs = (ctypes.c_void_p * len(dA_ptrs))(*[int(p) for p in dA_ptrs])
+        self._keep = (d, rhs, obj, lo, up, ptrs)
+        check(self._lib.elp_load_dense_device_multi(
+            self._h, ptrs, len(dA_ptrs), d.ctypes.data, rhs.ctypes.data, obj.ctypes.data,
+            lo.ctypes.data, up.ctypes.data, int(bool(maximize))), "elp_load_dense_device_multi")
+
     def load_csc(self, colptr, rowind, val, dirs, rhs, obj, lo=None, up=None, maximize=False) -> None:
         """Sparse A in compressed sparse columns (rows strictly increasing per column)."""
         m, n = self.m, self.n

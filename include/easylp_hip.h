@@ -25,7 +25,8 @@
 extern "C" {
 #endif
 
-#define ELP_ABI_VERSION 3  /* 3: elp_stats.iter_bytes appended */
+#define ELP_ABI_VERSION 4  /* 3: elp_stats.iter_bytes appended; 4: elp_control.exchange,
+                             elp_load_dense_device_multi, elp_stats.exchange / h2d_bytes */
 
 /* row directions, mirroring R/class.R:272 ("==" -> "=") and the "<"/">"
  * spellings accepted by R/methods.R:215-219 */
@@ -91,7 +92,18 @@ typedef struct elp_control {
                                 0 none; ELP_SCALE_GEOMETRIC | ELP_SCALE_EQUILIBRATE
                                 (default, lp_solve's "geometric" + "equilibrate");
                                 factors are powers of 2 so scaling is exact     */
-    int32_t reserved0;
+    int32_t exchange;        /* per-iteration min-loc of a column-sharded solve
+                                with A replicated:  0 (default) -- an ngpu
+                                handle writes each rank's record straight into
+                                every peer's device memory (peer access, no IPC)
+                                and polls its own mailbox inside the select
+                                kernel, when every device maps every peer and a
+                                probe round trip succeeds at elp_create; else,
+                                and with A not replicated, the collective
+                                (RCCL all-gather / in-process transport).
+                                Multi-process handles (elp_comm_init*) use the
+                                collective unless elp_comm_enable_p2p.
+                                1: always the collective */
     double tol_singular;     /* |pivot| <= this in a Gauss-Jordan refactor is a
                                 singular basis -> status 5            (1e-13)  */
     double mailbox_timeout;  /* xGMI mailbox: seconds a rank waits for a peer's
@@ -138,6 +150,12 @@ typedef struct elp_stats {
     double iter_bytes;         /* algorithmic bytes of the whole iterations:
                                   price_bytes + 48k^2 + 8mk + 16n + 16m each
                                   (select, FTRAN-z, ratio test, update)         */
+    int32_t exchange;          /* min-loc transport of the last load: 0 none
+                                  (one rank), 1 peer mailbox, 2 collective      */
+    int32_t reserved1;
+    double seconds_h2d;        /* elp_load_dense: host -> device copy of A     */
+    double h2d_bytes;          /* bytes of A read from host memory (once, also
+                                  when several devices receive them)            */
 } elp_stats;
 
 #define ELP_PROFILE_PRICE 2   /* elp_control.verbose bit: device-clock pricing timer */
@@ -164,6 +182,17 @@ int elp_load_dense(elp_handle* h, const double* A, const int32_t* dir, const dou
 int elp_load_dense_device(elp_handle* h, const double* dA, const int32_t* dir, const double* rhs,
                           const double* obj, const double* lo, const double* up,
                           int32_t maximize);
+
+/* Single-process multi-device (elp_control.ngpu = P > 1) with A already
+ * resident on every device: dA[r] is the full m x n column-major A (lda = m)
+ * in the memory of rank r's device (device + r mod the visible count), count =
+ * P.  Rank r reads its copy in place -- all of it when A is replicated
+ * (elp_control.replicate), else only its column shard -- so no device-to-device
+ * copy happens at load.  The caller keeps every dA[r] alive until elp_destroy.
+ * On a one-device handle count must be 1 (then = elp_load_dense_device). */
+int elp_load_dense_device_multi(elp_handle* h, const double* const* dA, int32_t count, const int32_t* dir,
+                                const double* rhs, const double* obj, const double* lo, const double* up,
+                                int32_t maximize);
 
 /* Sparse A in compressed sparse columns (BASELINE config 5):
  * colptr[n+1] (colptr[0] = 0, colptr[n] = nnz), rowind[nnz] strictly increasing

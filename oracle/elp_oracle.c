@@ -189,7 +189,7 @@ static int col_pass(const orc_t* s, int32_t* rho, int32_t* gam, int equilibrate)
         int mn = SC_EMPTY_MIN, mx = SC_EMPTY_MAX;
         for (int64_t i = 0; i < s->m; ++i) {
             const double a = Araw(s, i, j);
-            if (a == 0.0) continue;
+            if (a == 0.0 || !isfinite(a)) continue; /* (non-finite: no exponent) */
             const int e = ilogb(a) + rho[i];
             if (e < mn) mn = e;
             if (e > mx) mx = e;
@@ -213,7 +213,7 @@ static int row_pass(const orc_t* s, int32_t* rho, const int32_t* gam) {
     for (int64_t j = 0; j < n; ++j)
         for (int64_t i = 0; i < m; ++i) {
             const double a = Araw(s, i, j);
-            if (a == 0.0) continue;
+            if (a == 0.0 || !isfinite(a)) continue;
             const int e = ilogb(a) + gam[j];
             if (e < mn[i]) mn[i] = e;
             if (e > mx[i]) mx[i] = e;

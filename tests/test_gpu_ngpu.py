@@ -5,10 +5,27 @@ in-process ThreadGroup; on a node with P devices the same handle builds an
 RCCL communicator with ncclCommInitAll.  The column-sharded solve must walk the
 oracle's pivot path bit for bit, for A replicated or sharded, and for every
 load entry point."""
+import os
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def run_child(tmp_path, *args, hw_queues=16, timeout=600):
+    """tests/ngpu_child.py in a fresh process with one hardware queue per rank
+    stream (GPU_MAX_HW_QUEUES, set before HIP starts); returns its npz."""
+    out = str(tmp_path / "res.npz")
+    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(hw_queues))
+    r = subprocess.run([sys.executable, os.path.join(HERE, "ngpu_child.py"), out, *map(str, args)],
+                       capture_output=True, text=True, timeout=timeout, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    return dict(np.load(out))
 
 
 def _general_lp():
@@ -115,3 +132,76 @@ def test_ngpu_larger_capped_window(gpu, replicate):
     np.testing.assert_array_equal(g.trace, o.trace)
     np.testing.assert_array_equal(g.basis, o.basis)
     assert g.objval == o.objval
+
+
+@pytest.mark.parametrize("ngpu", [2, 3, 8])
+def test_ngpu_peer_mailbox_matches_oracle(tmp_path, ngpu):
+    """the ngpu handle's per-iteration min-loc through the direct
+    peer mailbox (each rank's select kernel stores its record into every peer's
+    device memory and polls its own; peer access, no IPC, no collective launch),
+    here with all P ranks on the test GPU (same-device peer pointers; on an
+    8-GPU node the stores cross xGMI).  Bit-identical to the oracle's pivot
+    path; a second load on the same handle (new sequence epoch) too."""
+    from oracle import generate_dense, solve_dense as orc
+    m, n, seed = 300, 1201, 11
+    g = run_child(tmp_path, "generated", m, n, seed, ngpu, 1, 200000)
+    assert int(g["exchange"]) == 1  # the mailbox, not the collective fallback
+    assert int(g["world"]) == ngpu
+    A, b, c = generate_dense(seed, m, n)
+    o = orc(A, np.ones(m, np.int32), b, c, maximize=True, trace_cap=200000)
+    assert int(g["status"]) == o.status == 0
+    np.testing.assert_array_equal(g["trace"], o.trace)
+    np.testing.assert_array_equal(g["basis"], o.basis)
+    assert float(g["objval"]) == o.objval == float(g["objval2"])
+    np.testing.assert_array_equal(g["x"], o.x)
+
+
+def test_ngpu_mailbox_in_process(gpu):
+    """The same in the test process (box default of 4 hardware queues): two ranks
+    use the mailbox when their probe round trip succeeds, else the in-process
+    collective -- either way bit-identical; column-only A (replicate = 2) always
+    takes the collective (the entering column must travel)."""
+    from oracle import generate_dense, solve_dense as orc
+    m, n, seed = 300, 1201, 11
+    A, b, c = generate_dense(seed, m, n)
+    o = orc(A, np.ones(m, np.int32), b, c, maximize=True, trace_cap=200000)
+    for replicate in (1, 2):
+        with gpu.Problem(m, n, ngpu=2, replicate=replicate) as p:
+            p.set_trace(200000)
+            p.load_generated(seed)
+            g = p.solution(p.solve())
+        assert g.stats["exchange"] in ((1, 2) if replicate == 1 else (2,))
+        _same(g, o, 2)
+
+
+def test_ngpu_exchange_collective_forced(gpu):
+    """elp_control.exchange = 1 keeps the collective."""
+    from oracle import generate_dense, solve_dense as orc
+    m, n, seed = 200, 900, 3
+    with gpu.Problem(m, n, ngpu=2, replicate=1, exchange=1) as p:
+        p.set_trace(100000)
+        p.load_generated(seed)
+        g = p.solution(p.solve())
+    assert g.stats["exchange"] == 2
+    A, b, c = generate_dense(seed, m, n)
+    _same(g, orc(A, np.ones(m, np.int32), b, c, maximize=True, trace_cap=100000), 2)
+
+
+def test_ngpu_host_load_once(gpu):
+    """elp_load_dense on an ngpu handle: A is read from host memory once (the
+    pinned staging pipeline feeds every rank's device), replicated or column-
+    only; larger than the staging threshold so the chunked path runs."""
+    from oracle import generate_dense, solve_dense as orc
+    m, n, seed = 400, 6000, 2  # 19.2 MB of A: two 16 MB chunks
+    A, b, c = generate_dense(seed, m, n)
+    o = orc(A, np.ones(m, np.int32), b, c, maximize=True, trace_cap=100000)
+    for ngpu, replicate in ((1, 0), (2, 1), (3, 2)):
+        g = gpu.solve_dense(A, np.ones(m, np.int32), b, c, maximize=True, trace=100000, ngpu=ngpu,
+                            replicate=replicate)
+        assert g.stats["h2d_bytes"] == 8.0 * m * n
+        assert g.stats["seconds_h2d"] > 0
+        if ngpu == 1:
+            assert g.status == o.status and g.objval == o.objval
+            np.testing.assert_array_equal(g.trace, o.trace)
+        else:
+            _same(g, o, ngpu)
