@@ -18,6 +18,7 @@ ELP_PROFILE_PRICE = 2   # device-clock pricing timer
 ELP_PROFILE_EVENTS = 4  # HIP events on every pricing dispatch
 ELP_PROFILE_SAMPLE = 8  # ... on those of every 8th chunk between host polls
 ELP_SCALE_GEOMETRIC, ELP_SCALE_EQUILIBRATE = 4, 64
+ELP_BASIS_AUTO, ELP_BASIS_INVERSE, ELP_BASIS_LU = 0, 1, 2
 ABI_VERSION = 4
 
 # every entry point the header declares (checked by tests/test_abi.py)
@@ -60,6 +61,8 @@ class ElpControl(ctypes.Structure):
         ("exchange", ctypes.c_int32),
         ("tol_singular", ctypes.c_double),
         ("mailbox_timeout", ctypes.c_double),
+        ("basis", ctypes.c_int32),
+        ("reserved2", ctypes.c_int32),
     ]
 
 
@@ -94,6 +97,10 @@ class ElpStats(ctypes.Structure):
         ("reserved1", ctypes.c_int32),
         ("seconds_h2d", ctypes.c_double),
         ("h2d_bytes", ctypes.c_double),
+        ("lu_nnz", ctypes.c_int64),
+        ("eta_nnz", ctypes.c_int64),
+        ("basis", ctypes.c_int32),
+        ("reserved2", ctypes.c_int32),
     ]
 
 

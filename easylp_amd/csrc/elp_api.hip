@@ -25,6 +25,7 @@
 #include "../../include/easylp_hip.h"
 #include "elp_comm.h"
 #include "elp_internal.h"
+#include "elp_lu_factor.h"
 
 using namespace elp;
 
@@ -110,6 +111,18 @@ struct elp_handle {
     // scaling (elp_control.scaling): the solver works on A~ = 2^srow A 2^scol
     // (exponents per row and per GLOBAL column; empty: unscaled)
     std::vector<int32_t> srow_h, scol_h;
+    // sparse-LU engine (elp_control.basis, CSC input): host copy of the scaled
+    // CSC (the refactor builds B from it), artificial signs, the last factors,
+    // the device descriptor and its buffers (grown as needed, kept across loads)
+    bool lu = false;
+    LuDev ld{};
+    LuFactors luf;
+    std::vector<int64_t> lu_cp;
+    std::vector<int32_t> lu_ri;
+    std::vector<double> lu_cv, lu_asgn;
+    std::vector<void*> lub;
+    std::vector<size_t> lubcap;
+    int64_t lu_nnz_max = 0;
 };
 
 extern "C" void elp_default_control(elp_control* c) {
@@ -166,6 +179,13 @@ static void free_dev(elp_handle* h, bool keep_big = false) {
                     (void*)d.scol};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    for (void*& p : h->lub)
+        if (p) {
+            (void)hipFree(p);
+            p = nullptr;
+        }
+    h->lubcap.assign(h->lub.size(), 0);
+    h->ld = LuDev{};
     h->A_owned = nullptr;
     h->d_flag = nullptr;
     h->w_cap = 0;  // (W0 / W1 went with the rest)
@@ -453,9 +473,11 @@ static int alloc_all(elp_handle* h) {
     if (h->csc) h->ar_rows = 1;  // CSC prices from the columns: no AR
     d.arcap = h->ar_rows;
     A(dalloc(&d.AR, (size_t)h->ar_rows * (size_t)d.ldr));
-    A(dalloc(&d.AS, (size_t)mm * (size_t)mm));
-    A(dalloc(&d.Minv, (size_t)mm * (size_t)mm));
-    A(dalloc(&d.MinvT, (size_t)mm * (size_t)mm));
+    // the explicit bump inverse's m x m buffers (none with the sparse LU)
+    const size_t msq = h->lu ? 1 : (size_t)mm * (size_t)mm;
+    A(dalloc(&d.AS, msq));
+    A(dalloc(&d.Minv, msq));
+    A(dalloc(&d.MinvT, msq));
     A(dalloc(&d.cS, mm));
     A(dalloc(&d.slo, mm));
     A(dalloc(&d.shi, mm));
@@ -494,7 +516,7 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.alS, mm));
     A(dalloc(&d.alU, mm));
     A(dalloc(&d.zz, mm));
-    A(dalloc(&d.zpart, (size_t)(mm + 64) * (size_t)((mm + ZCHUNK - 1) / ZCHUNK)));
+    A(dalloc(&d.zpart, h->lu ? 1 : (size_t)(mm + 64) * (size_t)((mm + ZCHUNK - 1) / ZCHUNK)));
     A(dalloc(&d.vrow, mm));
     A(dalloc(&d.vvec, mm));
     A(dalloc(&d.colA, mm));
@@ -534,8 +556,8 @@ static int alloc_all(elp_handle* h) {
     // (AR padding columns [n, ldr) are read by the 128-column tiles but their
     //  results are discarded, so AR needs no clearing); Minv / work start clean
     A(hipMemsetAsync(d.rcnt, 0, (size_t)d.rregs * sizeof(int32_t), h->st));
-    A(hipMemsetAsync(d.Minv, 0, (size_t)mm * (size_t)mm * sizeof(double), h->st));
-    A(hipMemsetAsync(d.MinvT, 0, (size_t)mm * (size_t)mm * sizeof(double), h->st));
+    A(hipMemsetAsync(d.Minv, 0, msq * sizeof(double), h->st));
+    A(hipMemsetAsync(d.MinvT, 0, msq * sizeof(double), h->st));
     if (d.qcol) A(hipMemsetAsync(d.qcol, 0, (size_t)mm * sizeof(double), h->st));
     // index lists: entries past k / |Y| are read speculatively (and discarded):
     // start them at -1 rather than whatever the allocator hands out
@@ -910,6 +932,7 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
     h->stats.col0 = h->col0;
     h->stats.ncols = h->nloc;
     h->stats.exchange = h->comm.kind == 0 ? 0 : d.p2p ? 1 : 2;
+    h->stats.basis = h->lu ? ELP_BASIS_LU : ELP_BASIS_INVERSE;
     h->timing_started = false;
     if (infeasible) {  // R/class.R:297-298: lower > upper -> "unfeasible"
         h->done = true;
@@ -1096,6 +1119,7 @@ static int64_t shard_ncols(const elp_handle* h) {
     return (r + 1) * h->n / P - r * h->n / P;
 }
 
+static int lu_start(elp_handle* h);
 static int prep_load(elp_handle* h, bool csc = false) {
     if (!h) return fail(ELP_E_ARG, "NULL handle");
     HIPCHK(hipSetDevice(h->dev));
@@ -1104,6 +1128,11 @@ static int prep_load(elp_handle* h, bool csc = false) {
     load_mark(h, "free previous");
     h->loaded = false;
     h->csc = csc;
+    if (!csc) {
+        if (h->ctl.basis == ELP_BASIS_LU)
+            return fail(ELP_E_UNSUPPORTED, "elp_control.basis = ELP_BASIS_LU needs CSC input (elp_load_csc)");
+        h->lu = false;
+    }
     if (csc && h->comm.kind != 0)
         return fail(ELP_E_UNSUPPORTED, "elp_load_csc: column-sharded CSC solves are not supported");
     if (h->comm.world > 1) {
@@ -1285,6 +1314,8 @@ extern "C" int elp_load_csc(elp_handle* h, const int64_t* colptr, const int32_t*
             if (!std::isfinite(val[t])) return fail(ELP_E_ARG, "elp_load_csc: non-finite coefficient");
         }
     }
+    // the basis representation: the sparse LU unless the explicit inverse is asked for
+    h->lu = h->ctl.basis != ELP_BASIS_INVERSE;
     int rc = prep_load(h, true);
     if (rc) return rc;
     std::vector<double> sval(val, val + nnz);  // scaled in place (scaling on)
@@ -1331,7 +1362,13 @@ extern "C" int elp_load_csc(elp_handle* h, const int64_t* colptr, const int32_t*
         HIPCHK(hipMemcpyAsync(drv, rv.data(), (size_t)nnz * sizeof(double), hipMemcpyHostToDevice, h->st));
     }
     d.A = nullptr;
+    if (h->lu) {  // the refactors build B from the scaled CSC on the host
+        h->lu_cp.assign(colptr, colptr + n + 1);
+        h->lu_ri.assign(rowind, rowind + nnz);
+        h->lu_cv.assign(val, val + nnz);
+    }
     rc = load_common(h, dir, rhs, obj, lo, up, maximize);
+    if (!rc && h->lu) rc = lu_start(h);
     HIPCHK(hipStreamSynchronize(h->st));  // the host CSR staging goes out of scope
     h->stats.seconds_load = now_s() - t0;
     return rc;
@@ -1470,8 +1507,10 @@ static void pdbg_dump(elp_handle* h, const DevCtl* c) {
 }
 #endif
 
+static int lu_run_loop(elp_handle* h, int64_t budget, int32_t* lp_status);
 // the polling loop; budget = iterations allowed in this call
 static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
+    if (h->lu) return lu_run_loop(h, budget, lp_status);
     if (h->done) {
         *lp_status = h->final_status;
         return 0;
@@ -1723,6 +1762,263 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
     return 0;
 }
 
+// ---------------------------------------------------------------- sparse LU
+// The CSC path's sparse-LU engine (elp_control.basis): the host
+// factors the basis at every refactor (elp_lu_factor.cpp, the oracle's
+// Markowitz rule), uploads the factors and their level schedules, and the
+// device runs the iterations (launch_lu_iteration: BTRAN, pricing, select +
+// FTRAN + ratio test + update + eta).  The loop mirrors
+// oracle/elp_oracle_lu.c run_phase_lu.
+enum LuBuf {
+    LB_PROW, LB_PCOL, LB_RSTEP, LB_UD,
+    LB_SCHED,  // 4 schedules x (lvptr, row, ptr, j, v)
+    LB_EP = LB_SCHED + 20, LB_EPIV, LB_EI, LB_EPV, LB_EV, LB_HEAD, LB_BPOS, LB_XB, LB_ALPHA, LB_VEC, LB_ACOL,
+    LB_COUNT
+};
+
+// device buffer `id` of at least `bytes` (grown, never shrunk)
+static int lu_buf(elp_handle* h, int id, size_t bytes, void** out) {
+    if (h->lub.size() < (size_t)LB_COUNT) {
+        h->lub.resize(LB_COUNT, nullptr);
+        h->lubcap.resize(LB_COUNT, 0);
+    }
+    bytes = std::max<size_t>(bytes, 16);
+    if (h->lubcap[(size_t)id] < bytes) {
+        if (h->lub[(size_t)id]) (void)hipFree(h->lub[(size_t)id]);
+        h->lub[(size_t)id] = nullptr;
+        h->lubcap[(size_t)id] = 0;
+        if (hipMalloc(&h->lub[(size_t)id], bytes) != hipSuccess) {
+            h->lub[(size_t)id] = nullptr;
+            return fail(ELP_E_NOMEM, "sparse LU: device allocation failed");
+        }
+        h->lubcap[(size_t)id] = bytes;
+    }
+    *out = h->lub[(size_t)id];
+    return 0;
+}
+
+template <class T>
+static int lu_upload(elp_handle* h, int id, const std::vector<T>& v, const T** dst) {
+    void* p = nullptr;
+    int rc = lu_buf(h, id, v.size() * sizeof(T), &p);
+    if (rc) return rc;
+    if (!v.empty()) HIPCHK(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, h->st));
+    *dst = static_cast<const T*>(p);
+    return 0;
+}
+
+static int lu_upload_sched(elp_handle* h, int k, const LuSched& sc, LuSchedDev* sd) {
+    const int b = LB_SCHED + 5 * k;
+    int rc = lu_upload(h, b, sc.lvptr, &sd->lvptr);
+    if (!rc) rc = lu_upload(h, b + 1, sc.row, &sd->row);
+    if (!rc) rc = lu_upload(h, b + 2, sc.ptr, &sd->ptr);
+    if (!rc) rc = lu_upload(h, b + 3, sc.j, &sd->j);
+    if (!rc) rc = lu_upload(h, b + 4, sc.v, &sd->v);
+    sd->nlev = sc.nlev();
+    return rc;
+}
+
+// Refactor: B from head (downloaded), Markowitz LU on the host, factors and
+// schedules to the device, empty eta file; with_xb: x_B = B^-1 (b - N x_N).
+// *singular = true when the basis has no LU (numerical failure).
+static int lu_refactor(elp_handle* h, bool with_xb, bool* singular) {
+    const int64_t m = h->m;
+    *singular = false;
+    std::vector<int32_t> head((size_t)std::max<int64_t>(m, 1));
+    if (m) HIPCHK(hipMemcpyAsync(head.data(), h->ld.head, (size_t)m * sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    const LuColumns a{m, h->n, h->lu_cp.data(), h->lu_ri.data(), h->lu_cv.data(), h->lu_asgn.data()};
+    if (lu_factor(h->luf, a, head.data(), h->ctl.tol_singular)) {
+        *singular = true;
+        return 0;
+    }
+    lu_schedules(h->luf);
+    h->lu_nnz_max = std::max(h->lu_nnz_max, h->luf.nnz());
+    LuDev& u = h->ld;
+    int rc = lu_upload(h, LB_PROW, h->luf.prow, &u.prow);
+    if (!rc) rc = lu_upload(h, LB_PCOL, h->luf.pcol, &u.pcol);
+    if (!rc) rc = lu_upload(h, LB_RSTEP, h->luf.rstep, &u.rstep);
+    if (!rc) rc = lu_upload(h, LB_UD, h->luf.ud, &u.ud);
+    if (!rc) rc = lu_upload_sched(h, 0, h->luf.sL, &u.sL);
+    if (!rc) rc = lu_upload_sched(h, 1, h->luf.sU, &u.sU);
+    if (!rc) rc = lu_upload_sched(h, 2, h->luf.sUT, &u.sUT);
+    if (!rc) rc = lu_upload_sched(h, 3, h->luf.sLT, &u.sLT);
+    if (rc) return rc;
+    h->hctl->lu_ne = 0;
+    h->hctl->lu_enz = 0;
+    HIPCHK(hipMemcpyAsync(&h->d.ctl->lu_ne, &h->hctl->lu_ne, sizeof(int32_t), hipMemcpyHostToDevice, h->st));
+    HIPCHK(hipMemcpyAsync(&h->d.ctl->lu_enz, &h->hctl->lu_enz, sizeof(int64_t), hipMemcpyHostToDevice, h->st));
+    if (with_xb) {
+        rc = row_chain(h);
+        if (rc) return rc;
+        HIPCHK(launch_lu_xb(h->d, u, h->st));
+    }
+    HIPCHK(hipStreamSynchronize(h->st));  // (the host factors are reused as upload sources)
+    return 0;
+}
+
+// after load_common on a CSC load with the sparse LU: the engine's state from
+// the slack / artificial basis, its (diagonal) LU, the phase-start checks
+static int lu_start(elp_handle* h) {
+    const int64_t m = h->m, nv = h->n + 2 * m;
+    LuDev& u = h->ld;
+    u.m = (int32_t)m;
+    u.lds = m <= lu_lds_max_m() ? 1 : 0;
+    if (const char* e = std::getenv("ELP_LU_GLOBAL"))  // test hook: the global-memory vector
+        if (std::atoi(e)) u.lds = 0;
+    const int64_t period = std::max<int64_t>(h->ctl.refactor_period, 1);
+    u.ecap = period + 2;
+    u.enzcap = std::max<int64_t>(m, 1) * (period + 1);
+    void* p = nullptr;
+    const size_t mm = (size_t)std::max<int64_t>(m, 1);
+    int rc = lu_buf(h, LB_EP, (size_t)(u.ecap + 1) * sizeof(int64_t), &p);
+    u.ep = (int64_t*)p;
+    if (!rc) rc = lu_buf(h, LB_EPIV, (size_t)u.ecap * sizeof(int32_t), &p), u.epiv = (int32_t*)p;
+    if (!rc) rc = lu_buf(h, LB_EPV, (size_t)u.ecap * sizeof(double), &p), u.epv = (double*)p;
+    if (!rc) rc = lu_buf(h, LB_EI, (size_t)u.enzcap * sizeof(int32_t), &p), u.ei = (int32_t*)p;
+    if (!rc) rc = lu_buf(h, LB_EV, (size_t)u.enzcap * sizeof(double), &p), u.ev = (double*)p;
+    if (!rc) rc = lu_buf(h, LB_HEAD, mm * sizeof(int32_t), &p), u.head = (int32_t*)p;
+    if (!rc) rc = lu_buf(h, LB_BPOS, (size_t)nv * sizeof(int32_t), &p), u.bpos = (int32_t*)p;
+    if (!rc) rc = lu_buf(h, LB_XB, mm * sizeof(double), &p), u.xB = (double*)p;
+    if (!rc) rc = lu_buf(h, LB_ALPHA, mm * sizeof(double), &p), u.alpha = (double*)p;
+    if (!rc) rc = lu_buf(h, LB_VEC, mm * sizeof(double), &p), u.vec = (double*)p;
+    if (!rc) rc = lu_buf(h, LB_ACOL, mm * sizeof(double), &p), u.acol = (double*)p;
+    if (rc) return rc;
+    h->lu_nnz_max = 0;
+    h->stats.basis = ELP_BASIS_LU;
+    if (h->done) return 0;  // lower > upper: nothing to solve
+    HIPCHK(launch_lu_init(h->d, u, h->st));
+    h->lu_asgn.assign(mm, 1.0);
+    if (m) HIPCHK(hipMemcpyAsync(h->lu_asgn.data(), h->d.asgn, (size_t)m * sizeof(double), hipMemcpyDeviceToHost, h->st));
+    bool singular = false;
+    rc = lu_refactor(h, false, &singular);  // (the oracle's initial lu_factor: x_B stays)
+    if (rc) return rc;
+    if (singular) {
+        h->done = true;
+        h->final_status = ELP_NUMFAILURE;
+        return 0;
+    }
+    HIPCHK(launch_lu_looptop(h->d, u, h->phase, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    return 0;
+}
+
+static int lu_run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
+    if (h->done) {
+        *lp_status = h->final_status;
+        return 0;
+    }
+    const double t_loop0 = now_s();
+    if (!h->timing_started) {
+        h->t_solve_start = t_loop0;
+        h->timing_started = true;
+    }
+    DevCtl* c = h->hctl;
+    HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    c->iter_stop = budget >= INT64_MAX - c->iter ? INT64_MAX : c->iter + budget;
+    if (c->status == ST_STOP) c->status = ST_RUN;
+    c->phase = h->phase;
+    int rc = push_ctl_fields(h);
+    if (rc) return rc;
+    auto refactor_now = [&](bool* numfail) -> int {
+        bool singular = false;
+        const int r = lu_refactor(h, true, &singular);
+        if (r) return r;
+        *numfail = singular;
+        h->stats.refactors++;
+        return 0;
+    };
+    for (;;) {
+        if (c->status == ST_RUN && c->iter >= c->iter_stop && c->iter < c->iter_limit) {
+            *lp_status = ELP_SUBOPTIMAL;
+            h->stats.seconds_loop += now_s() - t_loop0;
+            return 0;
+        }
+        for (int t = 0; t < h->ctl.sync_every; ++t) {
+            h->stats.price_launches++;
+            HIPCHK(launch_lu_iteration(h->d, h->ld, h->phase, h->st));
+        }
+        HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+        HIPCHK(hipStreamSynchronize(h->st));
+        h->stats.host_polls++;
+        const int32_t s = c->status;
+        if (s == ST_RUN) {
+            if (h->ctl.time_limit > 0 && now_s() - h->t_solve_start > h->ctl.time_limit) {
+                h->done = true;
+                h->final_status = ELP_TIMEOUT;
+                break;
+            }
+            continue;
+        }
+        if (s == ST_STOP) {
+            *lp_status = ELP_SUBOPTIMAL;
+            h->stats.seconds_loop += now_s() - t_loop0;
+            return 0;
+        }
+        const bool recheck = s == ST_PHASE_OPT && h->phase == 2 && c->since_refactor > 0;
+        if (s == ST_REFACTOR || recheck) {
+            bool nf = false;
+            rc = refactor_now(&nf);
+            if (rc) return rc;
+            if (nf) {
+                h->done = true;
+                h->final_status = ELP_NUMFAILURE;
+                break;
+            }
+            c->since_refactor = 0;
+            c->lu_ne = 0;
+            c->lu_enz = 0;
+            c->status = ST_RUN;  // (a re-check skips the loop-top checks, as the oracle's)
+            rc = push_ctl_fields(h);
+            if (rc) return rc;
+            continue;
+        }
+        if ((s == ST_PHASE_OPT || s == ST_P1DONE) && h->phase == 1) {
+            if (s == ST_PHASE_OPT && c->art_sum > c->tol_inf) {
+                h->done = true;
+                h->final_status = ELP_INFEASIBLE;
+                break;
+            }
+            HIPCHK(launch_lu_phase2(h->d, h->st));
+            HIPCHK(launch_devex_reset(h->d, h->st));
+            h->phase = 2;
+            bool nf = false;
+            rc = refactor_now(&nf);
+            if (rc) return rc;
+            if (nf) {
+                h->done = true;
+                h->final_status = ELP_NUMFAILURE;
+                break;
+            }
+            HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+            HIPCHK(hipStreamSynchronize(h->st));
+            c->phase = 2;
+            c->since_refactor = 0;
+            c->ndegen = 0;
+            c->bland = 0;
+            c->lu_ne = 0;
+            c->lu_enz = 0;
+            c->status = ST_RUN;
+            rc = push_ctl_fields(h);
+            if (rc) return rc;
+            HIPCHK(launch_lu_looptop(h->d, h->ld, 2, h->st));
+            HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+            HIPCHK(hipStreamSynchronize(h->st));
+            continue;
+        }
+        h->done = true;
+        if (s == ST_PHASE_OPT) h->final_status = ELP_OPTIMAL;
+        else if (s == ST_UNBOUNDED) h->final_status = ELP_UNBOUNDED;
+        else if (s == ST_ITERCAP) h->final_status = ELP_SUBOPTIMAL;
+        else h->final_status = ELP_NUMFAILURE;
+        break;
+    }
+    h->stats.seconds_loop += now_s() - t_loop0;
+    *lp_status = h->final_status;
+    return 0;
+}
+
 extern "C" int elp_set_int(elp_handle* h, const int32_t* is_int) {
     if (is_group(h)) return fan_out(h, [&](elp_handle* r, int) { return elp_set_int(r, is_int); });
     if (!h || !h->loaded) return fail(ELP_E_STATE, "elp_set_int: no problem loaded");
@@ -1741,7 +2037,8 @@ static int reload_bounds(elp_handle* h, const std::vector<double>& lo, const std
     const std::vector<int32_t> dir = h->dir_h;
     const std::vector<double> rhs = h->rhs_h, obj = h->obj_h;
     h->in_bnb = true;
-    const int rc = load_common(h, dir.data(), rhs.data(), obj.data(), lo.data(), up.data(), h->maximize);
+    int rc = load_common(h, dir.data(), rhs.data(), obj.data(), lo.data(), up.data(), h->maximize);
+    if (!rc && h->lu) rc = lu_start(h);
     h->in_bnb = false;
     return rc;
 }
@@ -1928,7 +2225,8 @@ extern "C" int elp_get_solution(elp_handle* h, double* objval, double* x, double
     double* dx = nullptr;
     HIPCHK(dalloc(&dx, n));
     HIPCHK(hipMemsetAsync(dx, 0, (size_t)n * sizeof(double), h->st));
-    HIPCHK(launch_extract(h->d, dx + h->col0, h->st));
+    if (h->lu) HIPCHK(launch_lu_extract(h->d, h->ld, dx, h->st));
+    else HIPCHK(launch_extract(h->d, dx + h->col0, h->st));
     {
         const int rc = h->comm.allreduce_sum_f64(dx, (size_t)n, h->st);
         if (rc) return fail(rc, "solution all-reduce failed");
@@ -1962,7 +2260,14 @@ extern "C" int elp_get_solution(elp_handle* h, double* objval, double* x, double
         HIPCHK(hipStreamSynchronize(h->st));
         for (int64_t i = 0; i < m; ++i) y[i] = unscale_row(h, h->maximize ? -y[i] : y[i], i, 1);
     }
-    if (basis && m) {
+    if (basis && m && h->lu) {
+        std::vector<int32_t> head((size_t)m);
+        HIPCHK(hipMemcpyAsync(head.data(), h->ld.head, (size_t)m * sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
+        HIPCHK(hipStreamSynchronize(h->st));
+        std::vector<int64_t> bv(head.begin(), head.end());
+        std::sort(bv.begin(), bv.end());
+        for (int64_t t = 0; t < m; ++t) basis[t] = bv[(size_t)t];
+    } else if (basis && m) {
         std::vector<int32_t> cover(m), Sl(std::max(c.k, 1));
         HIPCHK(hipMemcpyAsync(cover.data(), h->d.cover, m * sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
         if (c.k)
@@ -1991,6 +2296,9 @@ extern "C" int elp_sensitivity(elp_handle* h, double* objfrom, double* objtill, 
     if (!h->done || h->final_status != ELP_OPTIMAL)
         return fail(ELP_E_STATE, "elp_sensitivity: problem is not optimal");
     if (h->comm.kind != 0) return fail(ELP_E_UNSUPPORTED, "elp_sensitivity: column-sharded solves");
+    if (h->lu)
+        return fail(ELP_E_UNSUPPORTED, "elp_sensitivity: the sparse-LU basis (load with elp_control.basis = "
+                                       "ELP_BASIS_INVERSE for a sensitivity report)");
     if (h->mip || !h->is_int.empty())  // R/class.R:617-618, :634-635
         return fail(ELP_E_STATE, "Sensitivity unavailable for problems with integer/binary variables");
     HIPCHK(hipSetDevice(h->dev));
@@ -2109,6 +2417,20 @@ extern "C" int elp_get_stats(elp_handle* h, elp_stats* st) {
         h->stats.mip_lp_iterations = h->mip ? h->mip_iters : 0;
         h->stats.price_bytes = c.price_bytes;
         h->stats.iter_bytes = c.iter_bytes;
+        if (h->lu) {  // basic structurals, factor and eta-file sizes
+            std::vector<int32_t> head((size_t)std::max<int64_t>(h->m, 1));
+            if (h->m) {
+                HIPCHK(hipMemcpyAsync(head.data(), h->ld.head, (size_t)h->m * sizeof(int32_t), hipMemcpyDeviceToHost,
+                                      h->st));
+                HIPCHK(hipStreamSynchronize(h->st));
+            }
+            int64_t k = 0;
+            for (int64_t p = 0; p < h->m; ++p) k += head[(size_t)p] < h->n;
+            h->stats.bump_dim = k;
+            h->stats.y_rows = 0;
+            h->stats.lu_nnz = h->lu_nnz_max;
+            h->stats.eta_nnz = c.lu_enz_max;
+        }
         if (h->d.ptimer) {
             h->stats.price_seconds = 1e-8 * (double)c.price_ticks;
             h->stats.price_timed_launches = c.price_timed;

@@ -25,8 +25,9 @@
 extern "C" {
 #endif
 
-#define ELP_ABI_VERSION 4  /* 3: elp_stats.iter_bytes appended; 4: elp_control.exchange,
-                             elp_load_dense_device_multi, elp_stats.exchange / h2d_bytes */
+#define ELP_ABI_VERSION 4  /* 3: elp_stats.iter_bytes appended; 4: elp_control.exchange /
+                             basis, elp_load_dense_device_multi, elp_stats.exchange /
+                             h2d_bytes / lu_nnz / eta_nnz / basis */
 
 /* row directions, mirroring R/class.R:272 ("==" -> "=") and the "<"/">"
  * spellings accepted by R/methods.R:215-219 */
@@ -108,7 +109,21 @@ typedef struct elp_control {
                                 singular basis -> status 5            (1e-13)  */
     double mailbox_timeout;  /* xGMI mailbox: seconds a rank waits for a peer's
                                 record before the solve fails (ELP_E_COMM) (2) */
+    int32_t basis;           /* basis representation (lp_solve's bfp):
+                                ELP_BASIS_AUTO (default): dense input keeps the
+                                explicit bump inverse, CSC input the sparse LU;
+                                ELP_BASIS_INVERSE: unit columns + explicit
+                                inverse of the structural bump (O(m^2) device
+                                memory); ELP_BASIS_LU (CSC input only): a
+                                Markowitz LU of the whole basis at each refactor
+                                plus a product-form eta file, O(nnz(L+U)) device
+                                memory (the role LUSOL plays for lp_solve) */
+    int32_t reserved2;
 } elp_control;
+
+#define ELP_BASIS_AUTO 0     /* elp_control.basis */
+#define ELP_BASIS_INVERSE 1
+#define ELP_BASIS_LU 2
 
 #define ELP_SCALE_GEOMETRIC 4   /* elp_control.scaling bits (lp_solve's numbering) */
 #define ELP_SCALE_EQUILIBRATE 64
@@ -156,6 +171,11 @@ typedef struct elp_stats {
     double seconds_h2d;        /* elp_load_dense: host -> device copy of A     */
     double h2d_bytes;          /* bytes of A read from host memory (once, also
                                   when several devices receive them)            */
+    int64_t lu_nnz;            /* ELP_BASIS_LU: largest nnz(L) + nnz(U) + m    */
+    int64_t eta_nnz;           /* ELP_BASIS_LU: largest eta-file nonzeros      */
+    int32_t basis;             /* the representation the last load used
+                                  (ELP_BASIS_INVERSE or ELP_BASIS_LU)           */
+    int32_t reserved2;
 } elp_stats;
 
 #define ELP_PROFILE_PRICE 2   /* elp_control.verbose bit: device-clock pricing timer */
@@ -194,7 +214,9 @@ int elp_load_dense_device_multi(elp_handle* h, const double* const* dA, int32_t 
                                 const double* rhs, const double* obj, const double* lo, const double* up,
                                 int32_t maximize);
 
-/* Sparse A in compressed sparse columns (BASELINE config 5):
+/* Sparse A in compressed sparse columns (BASELINE config 5;
+ * with elp_control.basis AUTO or LU the solver keeps a sparse LU of the basis,
+ * see elp_control.basis; sensitivity then needs ELP_BASIS_INVERSE):
  * colptr[n+1] (colptr[0] = 0, colptr[n] = nnz), rowind[nnz] strictly increasing
  * within each column, val[nnz] finite.  Same problem semantics as
  * elp_load_dense; pricing then sweeps the nonzeros (12 bytes each) instead of

@@ -88,6 +88,7 @@ int main(int argc, char** argv) {
         elp_handle* h = NULL;
         int32_t st = -1;
         double z = 0.0;
+        ctl.ngpu = ngpu < n ? ngpu : (int)n; /* a rank prices at least one column */
         int rc = elp_create(&h, m, n, &ctl);
         if (!rc && cap > 0) rc = elp_set_trace(h, cap);
         if (!rc) rc = elp_load_dense(h, A, dir, rhs, obj, lo, up, mx);

@@ -128,3 +128,11 @@ def load_robust_lps():
         r["obj"] = np.array(r["obj"], dtype=np.float64)
         r["dir"] = np.array(r["dir"], dtype=np.int32)
     return recs
+
+
+def load_sparse_lu():
+    """tests/golden/sparse_lu.json (make_sparse_lu.py): the larger sparse LPs of
+    the sparse-LU engine -- generator spec + HiGHS optimum (or the optimum by
+    construction)."""
+    with open(os.path.join(GOLDEN, "sparse_lu.json")) as f:
+        return json.load(f)

@@ -117,7 +117,7 @@ def test_c_driver_host_input_matches_oracle(tmp_path, ngpu):
     assert len(out) == len(cases)
     for g, (lp, exp, name) in zip(out, cases):
         _check(g, lp, exp, name)
-        if ngpu > 1:
+        if ngpu > 1 and lp[0].shape[1] >= 2:  # (n = 1: the driver runs one rank)
             assert g["exchange"] in (1, 2)
 
 

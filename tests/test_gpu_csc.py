@@ -32,6 +32,7 @@ def _same(g, o):
 
 
 def _gpu_csc(gpu, rec, **ctl):
+    ctl.setdefault("basis", 1)  # ELP_BASIS_INVERSE: the bump inverse, oracle price_mode 1
     return gpu.solve_sparse(rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"],
                             rec["maximize"], trace=200000, **ctl)
 
@@ -67,7 +68,7 @@ def test_klee_minty_12(gpu, rule):
     from make_sparse import klee_minty
     from oracle import solve_dense as orc
     A, dirs, rhs, obj, lo, up, mx = klee_minty(12)
-    g = gpu.solve_sparse(A, dirs, rhs, obj, lo, up, mx, trace=10000, pricing=rule, scaling=0)
+    g = gpu.solve_sparse(A, dirs, rhs, obj, lo, up, mx, trace=10000, pricing=rule, scaling=0, basis=1)
     o = orc(A.toarray(), dirs, rhs, obj, lo, up, mx, trace_cap=10000, price_mode=1, price_rule=rule,
             scaling=0)
     _same(g, o)
@@ -84,7 +85,7 @@ def test_larger_sparse_vs_oracle(gpu, kind):
     from oracle import solve_dense as orc
     gen = sparse_packing if kind == "packing" else sparse_general
     A, dirs, rhs, obj, lo, up, mx = gen(31, 600, 3000, 5)
-    g = gpu.solve_sparse(A, dirs, rhs, obj, lo, up, mx, trace=100000)
+    g = gpu.solve_sparse(A, dirs, rhs, obj, lo, up, mx, trace=100000, basis=1)
     o = orc(A.toarray(), dirs, rhs, obj, lo, up, mx, trace_cap=100000, price_mode=1)
     assert g.status == 0
     _same(g, o)
@@ -122,12 +123,14 @@ def test_mps_file_through_csc(gpu, tmp_path):
     """An MPS file (ranges, bounds, sense, objective constant) read by
     easylp_amd.mps and solved on the GPU: same pivots as the oracle."""
     from easylp_amd.mps import read_mps, solve_mps
-    from oracle import solve_dense as orc
+    from easylp_amd.solver import csc_arrays
+    from oracle import solve_lu
     from test_mps import TEXT
     f = tmp_path / "t.mps"
     f.write_text(TEXT)
-    p, g = solve_mps(str(f))
-    o = orc(p.dense(), p.dirs, p.rhs, p.obj, p.lo, p.up, p.maximize, price_mode=1)
+    p, g = solve_mps(str(f))  # (CSC input: the sparse-LU basis by default)
+    cp, ri, v, _ = csc_arrays(p.dense())
+    o = solve_lu(cp, ri, v, p.dirs, p.rhs, p.obj, p.lo, p.up, p.maximize)
     assert g.status == o.status == 0
     assert g.objval == o.objval
     np.testing.assert_array_equal(g.basis, o.basis)

@@ -44,7 +44,7 @@ def _run(gpu, rec, sparse=False, gctl=None, octl=None):
     from oracle import solve_dense as orc
     args = (rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], rec["maximize"])
     solve = gpu.solve_sparse if sparse else gpu.solve_dense
-    g = solve(*args, trace=100000, **(gctl or {}))
+    g = solve(*args, trace=100000, **(gctl or {}), **({"basis": 1} if sparse else {}))
     o = orc(*args, trace_cap=100000, **(octl or {}), **({"price_mode": 1} if sparse else {}))
     _same(g, o)
     return g
@@ -124,7 +124,7 @@ def test_fuzz_mip(gpu, path):
         rec = fuzz_mip(s)
         args = (rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], rec["maximize"])
         solve = gpu.solve_dense if path == "dense" else gpu.solve_sparse
-        g = solve(*args, is_int=rec["is_int"])
+        g = solve(*args, is_int=rec["is_int"], **({"basis": 1} if path == "csc" else {}))
         o = solve_mip(*args, rec["is_int"], price_mode=1 if path == "csc" else 0)
         assert (g.status, g.stats["mip_nodes"], g.stats["mip_lp_iterations"]) == (
             o.status, o.stats["nodes"], o.stats["lp_iterations"]), f"mip{s}"

@@ -18,7 +18,7 @@ def test_reference_mips_gpu(gpu, rec, path):
     from oracle import solve_mip
     args = (rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], rec["maximize"])
     solve = gpu.solve_dense if path == "dense" else gpu.solve_sparse
-    g = solve(*args, is_int=rec["is_int"])
+    g = solve(*args, is_int=rec["is_int"], **({"basis": 1} if path == "csc" else {}))
     o = solve_mip(*args, rec["is_int"], price_mode=1 if path == "csc" else 0)
     exp = rec["expected"]
     assert g.status == o.status == exp["status"]

@@ -92,7 +92,7 @@ def test_csc_path(gpu, rule, name):
     assert len(recs) == len(names)
     for rec in recs:
         args = (rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], rec["maximize"])
-        g = gpu.solve_sparse(*args, trace=100000, pricing=rule)
+        g = gpu.solve_sparse(*args, trace=100000, pricing=rule, basis=1)
         o = orc(*args, trace_cap=100000, price_mode=1, price_rule=rule)
         _same(g, o)
 

@@ -38,7 +38,7 @@ def test_robust_dense_vs_oracle_and_highs(gpu, rec):
 @pytest.mark.parametrize("rec", ROBUST[::2], ids=[r["name"] for r in ROBUST[::2]])
 def test_robust_csc_vs_oracle(gpu, rec):
     from oracle import solve_dense as orc
-    g = gpu.solve_sparse(*_args(rec), trace=100000)
+    g = gpu.solve_sparse(*_args(rec), trace=100000, basis=1)
     o = orc(*_args(rec), trace_cap=100000, price_mode=1)
     _same(g, o)
 

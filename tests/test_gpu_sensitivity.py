@@ -61,7 +61,7 @@ def test_dense_sensitivity(gpu, rec):
 def test_csc_sensitivity(gpu, rec):
     from oracle import solve_dense as orc
     g = gpu.solve_sparse(rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"],
-                         rec["maximize"], sensitivity=True)
+                         rec["maximize"], sensitivity=True, basis=1)
     o = orc(rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], rec["maximize"],
             sens=True, price_mode=1)
     _check(g, o)
