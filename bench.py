@@ -373,13 +373,53 @@ def host_input(args, lib, ctx, m, n, label, reps):
 
 
 def sparse_rate(args, local, with_cpu):
-    """BASELINE config 5 on the CSC path: a seeded sparse LP of Netlib-like shape
-    (easylp_amd.synth.sparse_packing, 5 nonzeros per column) plus the Klee-Minty
-    cube n=12 (4095 pivots under Dantzig, a few dozen under Devex).  The CPU leg
-    is the oracle in its CSC order (price_mode 1) over a bounded window."""
+    """BASELINE config 5 on the CSC path with the sparse-LU basis (elp_control
+    basis AUTO -> LU for CSC input):
+      * "Netlib scale": the 20 000 x 100 000 LP of easylp_amd.synth.sparse_kkt
+        (5 nonzeros per column, boxed columns, optimum known by construction
+        and pinned by HiGHS in tests/golden/sparse_lu.json) to optimality;
+      * the seeded 1000 x 10 000 packing LP (sparse_packing) to optimality and
+        a steady-state window;
+      * the Klee-Minty cube n = 12 (4095 Dantzig pivots on the unscaled cube).
+    The CPU leg is the oracle's LU engine (orc_solve_lu, same algorithm, one
+    thread) over a bounded number of iterations of the same LPs."""
+    import json as _json
     import numpy as np
     from easylp_amd import Problem
-    from easylp_amd.synth import dense_of, sparse_packing
+    from easylp_amd.synth import sparse_kkt, sparse_packing
+    out = {}
+    fx = {f["name"]: f for f in _json.load(open(os.path.join(ROOT, "tests", "golden", "sparse_lu.json")))}
+    # ---- Netlib scale: 20 000 x 100 000 ----
+    k = fx["kkt_20000x100000"]
+    cp, ri, v, b, c, u, obj = sparse_kkt(k["seed"], k["m"], k["n"], k["k"])
+    m, n = k["m"], k["n"]
+    dirs, lo = np.ones(m, np.int32), np.zeros(n)
+    with Problem(m, n, device=local, pricing=args.rule) as p:
+        t0 = time.perf_counter()
+        p.load_csc(cp, ri, v, dirs, b, c, lo, u, maximize=True)
+        st = p.solve()
+        tto = time.perf_counter() - t0
+        s = p.stats()
+        z = p.solution(st).objval
+    big = {"workload": "sparse LP m=%d n=%d nnz=%d (sparse_kkt, boxed; BASELINE configs[4] at Netlib scale)"
+                       % (m, n, int(cp[-1])),
+           "basis": "sparse LU (Markowitz + product-form etas)", "status": st, "objective": z,
+           "objective_highs": k["highs_objective"], "rel_err_vs_highs": abs(z - k["highs_objective"]) / abs(k["highs_objective"]),
+           "iterations_to_optimal": s["iterations"], "bound_flips": s["bound_flips"], "refactors": s["refactors"],
+           "time_to_optimal_s": tto, "load_s": s["seconds_load"],
+           "value": s["iterations"] / tto if tto > 0 else None, "unit": "iterations/s (whole solve)",
+           "lu_nnz": s["lu_nnz"], "eta_nnz": s["eta_nnz"], "basic_structurals": s["bump_dim"],
+           "dense_inverse_bytes_avoided": 3 * 8 * m * m}
+    if with_cpu:
+        from oracle import solve_lu
+        w = args.sparse_cpu_iters
+        r = solve_lu(cp, ri, v, dirs, b, c, lo, u, maximize=True, max_iter=w, price_rule=args.rule)
+        big["cpu_baseline"] = {"value": r.stats["iterations"] / r.stats["seconds"], "unit": "iterations/s",
+                               "cores": 1, "kind": "port",
+                               "sample": "oracle/elp_oracle_lu.c (C, -O3, 1 thread) first %d iterations, setup "
+                                         "included" % r.stats["iterations"]}
+    out["netlib_scale"] = big
+    # ---- 1000 x 10 000 packing ----
     m, n = args.sparse_m, args.sparse_n
     cp, ri, v, b, c = sparse_packing(args.seed, m, n, 5)
     dirs = np.ones(m, np.int32)
@@ -399,11 +439,12 @@ def sparse_rate(args, local, with_cpu):
     s1 = p.stats()
     p.close()
     it = s1["iterations"] - s0["iterations"]
-    out = {"workload": "sparse LP m=%d n=%d nnz=%d (CSC, BASELINE configs[4])" % (m, n, int(cp[-1])),
-           "value": s2["iterations"] / tto, "unit": "iterations/s (whole solve)",
-           "time_to_optimal_s": tto, "status": st, "objective": sol.objval,
-           "iterations_to_optimal": s2["iterations"], "bump_dim": s2["bump_dim"],
-           "window": {"iterations": [100, 100 + it], "value": it / el if el > 0 else None}}
+    out.update({"workload": "sparse LP m=%d n=%d nnz=%d (CSC, sparse LU)" % (m, n, int(cp[-1])),
+                "value": s2["iterations"] / tto, "unit": "iterations/s (whole solve)",
+                "time_to_optimal_s": tto, "status": st, "objective": sol.objval,
+                "iterations_to_optimal": s2["iterations"], "basic_structurals": s2["bump_dim"],
+                "lu_nnz": s2["lu_nnz"], "eta_nnz": s2["eta_nnz"],
+                "window": {"iterations": [100, 100 + it], "value": it / el if el > 0 else None}})
     km = 12  # Klee-Minty cube: Dantzig's exponential path (2^n - 1 pivots) on the unscaled cube
     rows, cols, vals = [], [], []
     for i in range(km):
@@ -426,18 +467,16 @@ def sparse_rate(args, local, with_cpu):
                          "expected_iterations": 2 ** km - 1, "seconds": kt, "objective": kobj,
                          "expected": 5.0 ** km}
     if with_cpu:
-        from oracle import solve_dense
-        A = dense_of(cp, ri, v, m, n)
-        w = 100
-        r = solve_dense(A, dirs, b, c, maximize=True, price_mode=1, price_rule=args.rule,
-                        max_iter=w + args.sparse_cpu_iters, t_mark_iter=w)
-        cit = r.stats["iterations"] - w
-        out["cpu_baseline"] = {"value": cit / r.stats["seconds_at_mark"], "unit": "iterations/s",
+        from oracle import solve_lu
+        r = solve_lu(cp, ri, v, dirs, b, c, maximize=True, price_rule=args.rule,
+                     max_iter=100 + args.sparse_cpu_iters)
+        out["cpu_baseline"] = {"value": r.stats["iterations"] / r.stats["seconds"], "unit": "iterations/s",
                                "cores": 1, "kind": "port",
-                               "sample": "oracle/ (C, -O3, 1 thread, CSC order) iterations [%d, %d)" % (w, w + cit)}
+                               "sample": "oracle/elp_oracle_lu.c (C, -O3, 1 thread) first %d iterations"
+                                         % r.stats["iterations"]}
         t0 = time.perf_counter()
-        rk = solve_dense(K.toarray(), np.ones(km, np.int32), kb, kc, maximize=True, price_mode=1,
-                         price_rule=0, scaling=0)
+        rk = solve_lu(K.indptr, K.indices, K.data, np.ones(km, np.int32), kb, kc, maximize=True, price_rule=0,
+                      scaling=0)
         out["klee_minty"]["cpu_seconds"] = time.perf_counter() - t0
         out["klee_minty"]["cpu_iterations"] = rk.stats["iterations"]
     return out

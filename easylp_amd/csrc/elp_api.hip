@@ -114,6 +114,7 @@ struct elp_handle {
     // sparse-LU engine (elp_control.basis, CSC input): host copy of the scaled
     // CSC (the refactor builds B from it), artificial signs, the last factors,
     // the device descriptor and its buffers (grown as needed, kept across loads)
+    int64_t kcap = 0;  // bump capacity: AS m x kcap, Minv / MinvT kcap x kcap (grown at polls)
     bool lu = false;
     LuDev ld{};
     LuFactors luf;
@@ -447,7 +448,13 @@ static int alloc_all(elp_handle* h) {
     d.world = h->comm.world;
     d.sharded = h->comm.kind != 0;
     d.nv = (int32_t)(n + 2 * m);
-    d.ldm = mm;
+    // bump capacity: the explicit inverse needs O(m k + k^2), not O(m^2) -- k (the
+    // basic structurals) starts at 0 and grows by at most one per iteration, so
+    // the buffers start small and double at a poll (ensure_k)
+    h->kcap = std::min<int64_t>(mm, 256);
+    if (const char* e = std::getenv("ELP_KCAP_INIT"))  // test hook: force growth
+        h->kcap = std::max<int64_t>(1, std::min<int64_t>(mm, std::atoll(e)));
+    d.ldm = h->kcap;
     d.ldr = ((n + TILE_COLS - 1) / TILE_COLS) * TILE_COLS;
     d.infinity = h->ctl.infinity;
     d.tol_singular = h->ctl.tol_singular;
@@ -474,8 +481,8 @@ static int alloc_all(elp_handle* h) {
     d.arcap = h->ar_rows;
     A(dalloc(&d.AR, (size_t)h->ar_rows * (size_t)d.ldr));
     // the explicit bump inverse's m x m buffers (none with the sparse LU)
-    const size_t msq = h->lu ? 1 : (size_t)mm * (size_t)mm;
-    A(dalloc(&d.AS, msq));
+    const size_t msq = h->lu ? 1 : (size_t)h->kcap * (size_t)h->kcap;
+    A(dalloc(&d.AS, h->lu ? 1 : (size_t)mm * (size_t)h->kcap));
     A(dalloc(&d.Minv, msq));
     A(dalloc(&d.MinvT, msq));
     A(dalloc(&d.cS, mm));
@@ -516,7 +523,7 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.alS, mm));
     A(dalloc(&d.alU, mm));
     A(dalloc(&d.zz, mm));
-    A(dalloc(&d.zpart, h->lu ? 1 : (size_t)(mm + 64) * (size_t)((mm + ZCHUNK - 1) / ZCHUNK)));
+    A(dalloc(&d.zpart, h->lu ? 1 : (size_t)(mm + 64) * (size_t)((h->kcap + ZCHUNK - 1) / ZCHUNK + 1)));
     A(dalloc(&d.vrow, mm));
     A(dalloc(&d.vvec, mm));
     A(dalloc(&d.colA, mm));
@@ -591,6 +598,51 @@ static int ensure_ar(elp_handle* h, int64_t rows) {
     HIPCHK(launch_ar_relayout(h->d, old, old_cap, (int)std::min<int64_t>(old_cap, h->hctl->ny), h->st));
     HIPCHK(hipStreamSynchronize(h->st));
     (void)hipFree(old);
+    return 0;
+}
+
+// Grow the bump buffers to hold at least `need` positions (device idle: called
+// at a poll): AS keeps its first k columns (ld m), Minv / MinvT their k x k
+// block (ld kcap -> the new kcap); zpart is scratch.
+static int ensure_k(elp_handle* h, int64_t need) {
+    if (h->lu) return 0;
+    const int64_t mm = std::max<int64_t>(h->m, 1);
+    need = std::min<int64_t>(need, mm);
+    if (need <= h->kcap) return 0;
+    const int64_t cap = std::min<int64_t>(mm, std::max<int64_t>(need, 2 * h->kcap));
+    HIPCHK(hipMemcpyAsync(h->hctl, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    const int64_t k = std::min<int64_t>(h->hctl->k + 1, h->kcap);  // (+1: a pending case-B plan's row)
+    Dev& d = h->d;
+    double *as = nullptr, *mi = nullptr, *mt = nullptr, *zp = nullptr;
+    hipError_t e = dalloc(&as, (size_t)mm * (size_t)cap);
+    if (e == hipSuccess) e = dalloc(&mi, (size_t)cap * (size_t)cap);
+    if (e == hipSuccess) e = dalloc(&mt, (size_t)cap * (size_t)cap);
+    if (e == hipSuccess) e = dalloc(&zp, (size_t)(mm + 64) * (size_t)((cap + ZCHUNK - 1) / ZCHUNK + 1));
+    if (e != hipSuccess) {
+        for (double* p : {as, mi, mt, zp})
+            if (p) (void)hipFree(p);
+        return fail(ELP_E_NOMEM, "bump growth failed (k = " + std::to_string(need) + ")");
+    }
+    const size_t sq = (size_t)cap * (size_t)cap * sizeof(double);
+    HIPCHK(hipMemsetAsync(mi, 0, sq, h->st));
+    HIPCHK(hipMemsetAsync(mt, 0, sq, h->st));
+    if (k > 0) {
+        HIPCHK(hipMemcpyAsync(as, d.AS, (size_t)k * (size_t)mm * sizeof(double), hipMemcpyDeviceToDevice, h->st));
+        const size_t w = (size_t)k * sizeof(double);
+        HIPCHK(hipMemcpy2DAsync(mi, (size_t)cap * sizeof(double), d.Minv, (size_t)h->kcap * sizeof(double), w,
+                                (size_t)k, hipMemcpyDeviceToDevice, h->st));
+        HIPCHK(hipMemcpy2DAsync(mt, (size_t)cap * sizeof(double), d.MinvT, (size_t)h->kcap * sizeof(double), w,
+                                (size_t)k, hipMemcpyDeviceToDevice, h->st));
+    }
+    HIPCHK(hipStreamSynchronize(h->st));
+    for (double* p : {d.AS, d.Minv, d.MinvT, d.zpart}) (void)hipFree(p);
+    d.AS = as;
+    d.Minv = mi;
+    d.MinvT = mt;
+    d.zpart = zp;
+    d.ldm = cap;
+    h->kcap = cap;
     return 0;
 }
 
@@ -1314,8 +1366,9 @@ extern "C" int elp_load_csc(elp_handle* h, const int64_t* colptr, const int32_t*
             if (!std::isfinite(val[t])) return fail(ELP_E_ARG, "elp_load_csc: non-finite coefficient");
         }
     }
-    // the basis representation: the sparse LU unless the explicit inverse is asked for
-    h->lu = h->ctl.basis != ELP_BASIS_INVERSE;
+    // the basis representation: the explicit bump inverse (grown with k) unless
+    // the sparse LU is asked for (the LU engine is latency-bound)
+    h->lu = h->ctl.basis == ELP_BASIS_LU;
     int rc = prep_load(h, true);
     if (rc) return rc;
     std::vector<double> sval(val, val + nnz);  // scaled in place (scaling on)
@@ -1574,6 +1627,8 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
         const int k0 = c->k, ny0 = c->ny;
         int chunk = h->ctl.sync_every;
         rc = ensure_ar(h, (int64_t)ny0 + chunk + 1);  // |Y| grows by <= 1 per iteration
+        if (rc) return rc;
+        rc = ensure_k(h, (int64_t)k0 + chunk + 2);  // so does k
         if (rc) return rc;
         const int to_refactor = period - c->since_refactor;
         if (to_refactor > 0 && to_refactor < chunk) chunk = to_refactor;

@@ -3587,20 +3587,55 @@ DEV void lu_sched_solve(const LuSchedDev& sc, const double* __restrict__ ud, dou
     }
 }
 
+// Eta entries prefetched per thread: the next eta's pivot, value, range and
+// first LU_EPF entries per thread are loaded while the current eta computes
+// (none of them depends on x); longer etas load the rest on the spot.
+constexpr int LU_EPF = 4;
+struct EtaPf {
+    int p;
+    double pv;
+    int64_t b, en;
+    int i[LU_EPF];
+    double v[LU_EPF];
+};
+DEV void eta_load_head(const LuDev& u, int e, bool on, EtaPf& f) {
+    f.p = on ? u.epiv[e] : 0;
+    f.pv = on ? u.epv[e] : 1.0;
+    f.b = on ? u.ep[e] : 0;
+    f.en = on ? u.ep[e + 1] : 0;
+}
+DEV void eta_load_body(const LuDev& u, EtaPf& f) {
+#pragma unroll
+    for (int k = 0; k < LU_EPF; ++k) {
+        const int64_t kk = f.b + threadIdx.x + (int64_t)k * LU_NT;
+        const bool in = kk < f.en;
+        f.i[k] = in ? u.ei[kk] : 0;
+        f.v[k] = in ? u.ev[kk] : 0.0;
+    }
+}
+
 // FTRAN through the eta file: x_p /= pivot, then x_i -= alpha_i x_p
 DEV void lu_eta_ftran(const LuDev& u, int ne, double* x) {
+    if (ne <= 0) return;
+    EtaPf cur, nxt;
+    eta_load_head(u, 0, true, cur);
+    eta_load_body(u, cur);
     for (int e = 0; e < ne; ++e) {
-        const int p = u.epiv[e];
-        const double pv = u.epv[e];
-        const int64_t b = u.ep[e], en = u.ep[e + 1];
-        const double xp = x[p] / pv;
+        const bool more = e + 1 < ne;
+        eta_load_head(u, e + 1, more, nxt);
+        const double xp = x[cur.p] / cur.pv;
         __syncthreads();
-        if (threadIdx.x == 0) x[p] = xp;
-        for (int64_t k = b + threadIdx.x; k < en; k += LU_NT) {
+        if (threadIdx.x == 0) x[cur.p] = xp;
+#pragma unroll
+        for (int k = 0; k < LU_EPF; ++k)
+            if (cur.b + threadIdx.x + (int64_t)k * LU_NT < cur.en) x[cur.i[k]] = fma(-cur.v[k], xp, x[cur.i[k]]);
+        for (int64_t k = cur.b + threadIdx.x + (int64_t)LU_EPF * LU_NT; k < cur.en; k += LU_NT) {
             const int i = u.ei[k];
             x[i] = fma(-u.ev[k], xp, x[i]);
         }
+        eta_load_body(u, nxt);
         __syncthreads();
+        cur = nxt;
     }
 }
 
@@ -3608,18 +3643,27 @@ DEV void lu_eta_ftran(const LuDev& u, int ne, double* x) {
 // the sum in the oracle's lane_dot256 order (256 lane-strided chains, then the
 // pairwise tree: each wave's tree, then (w0 + w1) + (w2 + w3))
 DEV void lu_eta_btran(const LuDev& u, int ne, double* x, double* red) {
+    if (ne <= 0) return;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    EtaPf cur, nxt;
+    eta_load_head(u, ne - 1, true, cur);
+    eta_load_body(u, cur);
     for (int e = ne - 1; e >= 0; --e) {
-        const int p = u.epiv[e];
-        const double pv = u.epv[e];
-        const int64_t b = u.ep[e], en = u.ep[e + 1];
+        const bool more = e > 0;
+        eta_load_head(u, e - 1, more, nxt);
         double acc = 0.0;
-        for (int64_t k = b + threadIdx.x; k < en; k += LU_NT) acc = fma(u.ev[k], x[u.ei[k]], acc);
+#pragma unroll
+        for (int k = 0; k < LU_EPF; ++k)
+            if (cur.b + threadIdx.x + (int64_t)k * LU_NT < cur.en) acc = fma(cur.v[k], x[cur.i[k]], acc);
+        for (int64_t k = cur.b + threadIdx.x + (int64_t)LU_EPF * LU_NT; k < cur.en; k += LU_NT)
+            acc = fma(u.ev[k], x[u.ei[k]], acc);
         acc = wave_tree(acc);
         if (lane == 0) red[w] = acc;
+        eta_load_body(u, nxt);
         __syncthreads();
-        if (threadIdx.x == 0) x[p] = (x[p] - ((red[0] + red[1]) + (red[2] + red[3]))) / pv;
+        if (threadIdx.x == 0) x[cur.p] = (x[cur.p] - ((red[0] + red[1]) + (red[2] + red[3]))) / cur.pv;
         __syncthreads();
+        cur = nxt;
     }
 }
 

@@ -110,14 +110,15 @@ typedef struct elp_control {
     double mailbox_timeout;  /* xGMI mailbox: seconds a rank waits for a peer's
                                 record before the solve fails (ELP_E_COMM) (2) */
     int32_t basis;           /* basis representation (lp_solve's bfp):
-                                ELP_BASIS_AUTO (default): dense input keeps the
-                                explicit bump inverse, CSC input the sparse LU;
-                                ELP_BASIS_INVERSE: unit columns + explicit
-                                inverse of the structural bump (O(m^2) device
-                                memory); ELP_BASIS_LU (CSC input only): a
-                                Markowitz LU of the whole basis at each refactor
-                                plus a product-form eta file, O(nnz(L+U)) device
-                                memory (the role LUSOL plays for lp_solve) */
+                                ELP_BASIS_AUTO (default) = ELP_BASIS_INVERSE:
+                                unit columns + the explicit inverse of the
+                                structural bump (k basic structurals: O(m k +
+                                k^2) device memory, grown with k);
+                                ELP_BASIS_LU (CSC input only): a Markowitz LU of
+                                the whole basis at each refactor plus a
+                                product-form eta file, O(nnz(L+U) + etas) device
+                                memory (the role LUSOL plays for lp_solve);
+                                latency-bound on the GPU */
     int32_t reserved2;
 } elp_control;
 
@@ -215,8 +216,8 @@ int elp_load_dense_device_multi(elp_handle* h, const double* const* dA, int32_t 
                                 int32_t maximize);
 
 /* Sparse A in compressed sparse columns (BASELINE config 5;
- * with elp_control.basis AUTO or LU the solver keeps a sparse LU of the basis,
- * see elp_control.basis; sensitivity then needs ELP_BASIS_INVERSE):
+ * elp_control.basis = ELP_BASIS_LU keeps a sparse LU of the basis instead of
+ * the bump inverse; sensitivity then needs ELP_BASIS_INVERSE):
  * colptr[n+1] (colptr[0] = 0, colptr[n] = nnz), rowind[nnz] strictly increasing
  * within each column, val[nnz] finite.  Same problem semantics as
  * elp_load_dense; pricing then sweeps the nonzeros (12 bytes each) instead of
