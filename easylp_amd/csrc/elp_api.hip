@@ -455,7 +455,25 @@ static int alloc_all(elp_handle* h) {
     if (const char* e = std::getenv("ELP_KCAP_INIT"))  // test hook: force growth
         h->kcap = std::max<int64_t>(1, std::min<int64_t>(mm, std::atoll(e)));
     d.ldm = h->kcap;
-    d.ldr = ((n + TILE_COLS - 1) / TILE_COLS) * TILE_COLS;
+    // pricing tiles (price_body): TILE_COLS columns.  ELP_TILE_BAL=1 (A/B
+    // switch): once there are 256+ tiles, as many as the next multiple of
+    // 2 x 256 (two resident per CU), narrower, so every CU sweeps the same
+    // share -- measured slower at 5000 x 50000 (21.6 vs 19.9 us per launch,
+    // r03: idle lanes and more row loads cost more than the imbalance)
+    {
+        const int64_t t0 = (n + TILE_COLS - 1) / TILE_COLS;
+        int64_t tw = TILE_COLS;
+        const char* bal = std::getenv("ELP_TILE_BAL");
+        if (!h->csc && t0 >= 256 && bal && std::atoi(bal) == 1) {
+            const int64_t t1 = (t0 + 511) / 512 * 512;
+            tw = 2 * ((n + 2 * t1 - 1) / (2 * t1));
+        }
+        if (const char* e = std::getenv("ELP_TILE_W"))  // A/B switch
+            if (!h->csc) tw = std::max<int64_t>(2, std::min<int64_t>(TILE_COLS, std::atoll(e) & ~1ll));
+        d.tile_w = (int32_t)tw;
+        d.ntiles = (int32_t)std::max<int64_t>(1, (n + tw - 1) / tw);
+    }
+    d.ldr = (int64_t)d.ntiles * TILE_COLS;
     d.infinity = h->ctl.infinity;
     d.tol_singular = h->ctl.tol_singular;
     d.mb_ticks = (int64_t)(h->ctl.mailbox_timeout * 1e8);  // s_memrealtime: 100 MHz
@@ -540,13 +558,13 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.nzchunk, n / (1024 * 16) + 2));
     A(dalloc(&d.nzcount, 1));
     // tile candidates + the slack workgroups' (|Y| <= m, >= 128 slots each)
-    A(dalloc(&d.cand, (size_t)((n + TILE_COLS - 1) / TILE_COLS) + (size_t)((mm + TILE_COLS - 1) / TILE_COLS) + 64));
+    A(dalloc(&d.cand, (size_t)d.ntiles + (size_t)((mm + TILE_COLS - 1) / TILE_COLS) + 64));
     // one stamp pair per pricing workgroup: tiles, slack workgroups (<= m / 128 + 1)
     // and the apply workgroups (<= 2048 + 1024, launch_btran_price)
 #ifdef ELP_PDBG
-    A(dalloc(&d.pstamp, 6 * ((size_t)((n + TILE_COLS - 1) / TILE_COLS) + (size_t)(mm / 128 + 1) + 3072 + 64)));
+    A(dalloc(&d.pstamp, 6 * ((size_t)d.ntiles + (size_t)(mm / 128 + 1) + 3072 + 64)));
 #else
-    A(dalloc(&d.pstamp, 2 * ((size_t)((n + TILE_COLS - 1) / TILE_COLS) + (size_t)(mm / 128 + 1) + 3072 + 64)));
+    A(dalloc(&d.pstamp, 2 * ((size_t)d.ntiles + (size_t)(mm / 128 + 1) + 3072 + 64)));
 #endif
     if (h->csc) A(dalloc(&d.qcol, mm));
     if (std::getenv("ELP_STAMPS")) {

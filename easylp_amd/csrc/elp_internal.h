@@ -147,7 +147,8 @@ struct Dev {
     int32_t world;        // ranks sharing the columns
     int32_t sharded;      // 1: column-sharded solve (world > 1 or a test transport)
     int64_t ldm;   // Minv leading dimension (= max(m,1))
-    int64_t ldr;   // n rounded up to TILE_COLS
+    int64_t ldr;   // AR row length: ntiles x TILE_COLS (a tile's rows are TILE_COLS apart)
+    int32_t tile_w, ntiles;  // pricing tiles: tile_w (even, <= TILE_COLS) columns each
     int64_t arcap; // AR rows per column tile (capacity)
     const double* A;  // column-major m x n (this shard's columns)
     double* AT;       // its row-major copy (m x n, ld n): AR row copies read it contiguously

@@ -688,7 +688,8 @@ __global__ void k_scale_apply(int m, int64_t ncols, double* __restrict__ A, cons
 
 // element (row p, column j) of the tile-major AR
 DEV size_t ar_at(const Dev& d, int64_t p, int64_t j) {
-    return ((size_t)(j / TILE_COLS) * (size_t)d.arcap + (size_t)p) * TILE_COLS + (size_t)(j % TILE_COLS);
+    const int64_t tw = d.tile_w;  // columns per tile (<= TILE_COLS; rows of a tile stay TILE_COLS apart)
+    return ((size_t)(j / tw) * (size_t)d.arcap + (size_t)p) * TILE_COLS + (size_t)(j % tw);
 }
 
 // AR[p][j] = A[Yl[p]][j] for p < ny (initial fill)
@@ -795,6 +796,8 @@ DEV void btran_body(const Dev& d, int phase, const double* __restrict__ tv) {
 // deferred update (phase 2): defined with k_update below
 struct Plan;
 DEV void apply_plan(const Dev& d, const Plan& P, int blk, int nb, int nb_minv, bool do_ar);
+DEV void apply_minv(const Dev& d, const Plan& P, int64_t e0, int64_t estride);
+DEV void apply_copy(const Dev& d, const Plan& P, int64_t t0, int64_t tstride, bool do_ar);
 DEV bool plan_pending(const DevCtl* c) { return c->plan_seq != c->applied_seq && c->plan.action != ACT_NONE; }
 // the pricing launch's trailing `napply` workgroups apply the pending plan
 DEV bool apply_role(const Dev& d, int napply, int nb_minv) {
@@ -929,20 +932,39 @@ DEV double lane_bcast(double v, int l) {
 // on |Y|, so they go out right behind the control-block loads, before the
 // control block arrives (rows past |Y| are masked when it does), and the sweep
 // overlaps the control-block round trip instead of following it.
-DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
+// waves 1..3 of tile `tile` apply their share of the pending deferred plan
+// (whatever the loop status: the next select kernel marks the plan applied)
+DEV void tile_apply(const Dev& d, int64_t tile, int64_t ntiles) {
+    const DevCtl* cc = d.ctl;
+    if (!plan_pending(cc) || cc->status == ST_NUMFAIL) return;
+    const Plan P = cc->plan;
+    const int64_t vt = tile * (PRICE_THREADS - 64) + ((int)threadIdx.x - 64);
+    const int64_t VT = ntiles * (PRICE_THREADS - 64);
+    apply_minv(d, P, vt, VT);
+    apply_copy(d, P, vt, VT, false);
+}
+
+// Grid (r03): [nsw slack workgroups][d.ntiles column tiles of d.tile_w columns]
+// (tile_w = 128, or narrower balanced tiles under ELP_TILE_BAL=1, alloc_all);
+// the slack workgroups go first (their candidates are needed as soon as the
+// tiles'), and the deferred update of the last pivot is applied by waves 1..3
+// of every tile once their sweep is done (phase 2; nothing the sweep reads)
+// instead of by trailing workgroups that started only as tiles retired.
+DEV void price_body(const Dev& d, int nsw, int apply) {
     __shared__ double part[PRICE_SPLIT][TILE_COLS];
     __shared__ Cand red[PRICE_SPLIT];
-    const int64_t ntiles = gridDim.x - napply - nsw;
-    if ((int64_t)blockIdx.x >= ntiles) {
-        PDBG(1, (int)blockIdx.x >= (int)gridDim.x - napply ? 1ull : 2ull);
+    const int64_t ntiles = d.ntiles;
+    if ((int)blockIdx.x < nsw) {
+        PDBG(1, 2ull);
         PDBG(2, 0ull);
         PDBG(3, 0ull);
         PDBG(4, 0ull);
-        if (apply_role(d, napply, nb_minv)) return;
         if (d.ctl->status != ST_RUN) return;
-        price_slacks<PRICE_THREADS>(d, ntiles, (int)(blockIdx.x - ntiles), nsw, red);  // a slack workgroup
+        price_slacks<PRICE_THREADS>(d, ntiles, (int)blockIdx.x, nsw, red);  // a slack workgroup
         return;
     }
+    const int64_t tile = (int64_t)blockIdx.x - nsw;
+    const int tw = d.tile_w;
     // Software-pipelined sweep: the control block is loaded FIRST (vmcnt
     // retires in issue order, so the status test and the loop bound wait for
     // it alone, not for the rows issued behind it), then the first UNR rows
@@ -966,7 +988,9 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
     DevexIn dx = devex_in(c);
     double dtol = c->tol_dual;
     __builtin_amdgcn_sched_barrier(0);
-    const double* col = d.AR + (size_t)blockIdx.x * (size_t)d.arcap * TILE_COLS + 2 * lane;
+    // lanes past the tile's width read their last valid pair again (same line: no traffic)
+    const int lcol = 2 * lane < tw ? 2 * lane : ((tw - 1) & ~1);
+    const double* col = d.AR + (size_t)tile * (size_t)d.arcap * TILE_COLS + lcol;
     const double* __restrict__ yy = d.yy;
     const int cap = (int)d.arcap;
     dbl2 va[UNR], vb[UNR];
@@ -988,8 +1012,9 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
     // the epilogue's per-column operands (status, cost, Devex weight, previous
     // d) of columns 2 lane, 2 lane + 1 -- wave 0's: the other waves load element
     // 0 (one line); clamped, no branch to drain
-    const int64_t jA = (int64_t)blockIdx.x * TILE_COLS + 2 * lane;
-    const int64_t jc0 = (w == 0 && jA < d.n) ? jA : 0, jc1 = (w == 0 && jA + 1 < d.n) ? jA + 1 : 0;
+    const int64_t jA = tile * tw + 2 * lane;
+    const bool inA = 2 * lane < tw, inB = 2 * lane + 1 < tw;  // (tile widths are even: both)
+    const int64_t jc0 = (w == 0 && inA && jA < d.n) ? jA : 0, jc1 = (w == 0 && inB && jA + 1 < d.n) ? jA + 1 : 0;
     const int8_t pf_vs0 = d.vstat[jc0], pf_vs1 = d.vstat[jc1];
     const double pf_c0 = d.cost[jc0], pf_w0 = d.dw[jc0], pf_dp0 = d.dprev[jc0];
     const double pf_c1 = d.cost[jc1], pf_w1 = d.dw[jc1], pf_dp1 = d.dprev[jc1];
@@ -1010,6 +1035,7 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
 #endif
         KEEP(pf_c0);
         KEEP(pf_c1);
+        if (apply && w != 0) tile_apply(d, tile, ntiles);
         return;
     }
     PDBG(1, __builtin_amdgcn_s_memrealtime());
@@ -1080,8 +1106,11 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
     PDBG(3, __builtin_amdgcn_s_memrealtime());
     // the epilogue is wave 0's: lane l finishes columns 2l, 2l+1 (the classes
     // added in order), takes the better of the two, and the wave reduces
-    // without LDS or a barrier
-    if (w != 0) return;
+    // without LDS or a barrier; waves 1..3 apply the pending plan meanwhile
+    if (w != 0) {
+        if (apply) tile_apply(d, tile, ntiles);  // (phase 2 only: phase 1 applies in k_update)
+        return;
+    }
     Cand cb[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1091,7 +1120,7 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
         cb[h].w = 1.0;
         const int64_t j = jA + h;
         const int8_t vs = h ? pf_vs1 : pf_vs0;
-        if (j < d.n && vs != VS_BASIC && vs != VS_FIXED) {
+        if ((h ? inB : inA) && j < d.n && vs != VS_BASIC && vs != VS_FIXED) {
             double tot = 0.0;
 #pragma unroll
             for (int ww = 0; ww < PRICE_SPLIT; ++ww) tot = tot + part[ww][2 * lane + h];
@@ -1105,7 +1134,7 @@ DEV void price_body(const Dev& d, int napply, int nb_minv, int nsw) {
     cand_take(best, cb[1], cand_better(cb[1], cb[0], bland));
     PDBG(4, __builtin_amdgcn_s_memrealtime());
     best = wave_best_mono(best, bland);
-    if (lane == 0) d.cand[blockIdx.x] = best;
+    if (lane == 0) d.cand[tile] = best;
 }
 
 // the pricing-launch timer (Dev::ptimer): every workgroup stamps its start and
@@ -1123,9 +1152,9 @@ DEV void pstamp_end(const Dev& d) {
     if (threadIdx.x == 0) d.pstamp[PSTRIDE * blockIdx.x + PSTRIDE - 1] = __builtin_amdgcn_s_memrealtime();
 }
 
-__global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int napply, int nb_minv, int nsw) {
+__global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int nsw, int apply) {
     pstamp_begin<PRICE_THREADS>(d);
-    price_body(d, napply, nb_minv, nsw);
+    price_body(d, nsw, apply);
     pstamp_end(d);
 }
 
@@ -2661,32 +2690,31 @@ DEV double minv_new(const Dev& d, const Plan& P, int i, int j, const OldM& old) 
 // The plan k_ratio made: Minv and MinvT update (blocks [0, nb_minv)) + primal
 // update x_B -= step*alpha and AS copies (blocks [nb_minv, nb)); with do_ar also
 // the AR row copies (phase 1, where nothing is deferred).  Flips only update x_B.
-DEV void apply_plan(const Dev& d, const Plan& P, int blk, int nb, int nb_minv, bool do_ar) {
+// the Minv / MinvT part of a plan: element e0, e0 + estride, ... of the 2 kk^2
+DEV void apply_minv(const Dev& d, const Plan& P, int64_t e0, int64_t estride) {
+    if (P.action != ACT_PIVOT || P.pcase == PC_E) return;
     const int k = P.k_old;
     const size_t ldm = (size_t)d.ldm;
-    if (blk < nb_minv) {
-        if (P.action != ACT_PIVOT || P.pcase == PC_E) return;
-        const int kk = P.pcase == PC_B ? k + 1 : P.pcase == PC_C ? k - 1 : k;
-        const int64_t nel = (int64_t)kk * kk;
-        const int64_t e0 = (int64_t)blk * blockDim.x + threadIdx.x;
-        const int64_t estride = (int64_t)nb_minv * blockDim.x;
-        const OldM oM{d.Minv, ldm, false}, oT{d.MinvT, ldm, true};
-        for (int64_t e = e0; e < 2 * nel; e += estride) {
-            if (e < nel) {
-                const int i = (int)(e / kk), j = (int)(e % kk);
-                d.Minv[(size_t)i * ldm + j] = minv_new(d, P, i, j, oM);
-            } else {
-                const int64_t f = e - nel;  // MinvT element (j, i) = new Minv (i, j)
-                const int j = (int)(f / kk), i = (int)(f % kk);
-                d.MinvT[(size_t)j * ldm + i] = minv_new(d, P, i, j, oT);
-            }
+    const int kk = P.pcase == PC_B ? k + 1 : P.pcase == PC_C ? k - 1 : k;
+    const int64_t nel = (int64_t)kk * kk;
+    const OldM oM{d.Minv, ldm, false}, oT{d.MinvT, ldm, true};
+    for (int64_t e = e0; e < 2 * nel; e += estride) {
+        if (e < nel) {
+            const int i = (int)(e / kk), j = (int)(e % kk);
+            d.Minv[(size_t)i * ldm + j] = minv_new(d, P, i, j, oM);
+        } else {
+            const int64_t f = e - nel;  // MinvT element (j, i) = new Minv (i, j)
+            const int j = (int)(f / kk), i = (int)(f % kk);
+            d.MinvT[(size_t)j * ldm + i] = minv_new(d, P, i, j, oT);
         }
-        return;
     }
+}
+
+// the primal update and the AS (/ AR) copies of a plan: thread t0 of tstride
+DEV void apply_copy(const Dev& d, const Plan& P, int64_t t0, int64_t tstride, bool do_ar) {
+    const int k = P.k_old;
     // ---- primal update (oracle order: x -= step * (sig * alpha), then the
     //      entering value / compaction of the pivot case)
-    const int64_t t0 = (int64_t)(blk - nb_minv) * blockDim.x + threadIdx.x;
-    const int64_t tstride = (int64_t)(nb - nb_minv) * blockDim.x;
     const size_t m = (size_t)d.m;
     const double step = P.step, sg = P.sig;
     for (int64_t t = t0; t < d.m; t += tstride) {
@@ -2719,6 +2747,15 @@ DEV void apply_plan(const Dev& d, const Plan& P, int blk, int nb, int nb_minv, b
             if (P.y_ap_slot >= 0) d.AR[ar_at(d, P.y_ap_slot, j)] = a_row(d, P.y_ap_row, j);
         }
     }
+}
+
+DEV void apply_plan(const Dev& d, const Plan& P, int blk, int nb, int nb_minv, bool do_ar) {
+    if (blk < nb_minv) {
+        apply_minv(d, P, (int64_t)blk * blockDim.x + threadIdx.x, (int64_t)nb_minv * blockDim.x);
+        return;
+    }
+    apply_copy(d, P, (int64_t)(blk - nb_minv) * blockDim.x + threadIdx.x, (int64_t)(nb - nb_minv) * blockDim.x,
+               do_ar);
 }
 
 // Standalone update.  mode 0 (phase 1): the plan k_ratio just made, AR included.
@@ -3283,10 +3320,11 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phas
     #ifndef ELP_APPLY_PT
 #define ELP_APPLY_PT 4
 #endif
-    if (phase == 2) update_grid(d, k_ub, false, &nb_minv, &napply, d.csc ? TILE_COLS : PRICE_THREADS, ELP_APPLY_PT);
-    // + nsw: the slack workgroups (candidates [ntiles, ntiles + nsw))
+    if (phase == 2 && d.csc) update_grid(d, k_ub, false, &nb_minv, &napply, TILE_COLS, ELP_APPLY_PT);
+    // + nsw: the slack workgroups (candidates [ntiles, ntiles + nsw)); the dense
+    // sweep applies the deferred plan inside its tiles (price_body)
     const int nsw = slack_wgs(d, ny_ub);
-    const unsigned grid = ntiles + nsw + napply;
+    const unsigned grid = (d.csc ? ntiles + napply : (unsigned)d.ntiles) + nsw;
     if (ev0) {
         // profiling (ELP_PROFILE_EVENTS): events bound to the dispatch itself
         // (the CP's start / end timestamps of this launch, as a kernel trace
@@ -3295,12 +3333,12 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phas
             hipExtLaunchKernelGGL(k_price_csc, dim3(grid), dim3(TILE_COLS), 0, st, ev0, ev1, 0, d, (int)napply,
                                   (int)nb_minv, nsw);
         else
-            hipExtLaunchKernelGGL(k_price, dim3(grid), dim3(PRICE_THREADS), 0, st, ev0, ev1, 0, d, (int)napply,
-                                  (int)nb_minv, nsw);
+            hipExtLaunchKernelGGL(k_price, dim3(grid), dim3(PRICE_THREADS), 0, st, ev0, ev1, 0, d, nsw,
+                                  phase == 2 ? 1 : 0);
         return hipGetLastError();
     }
     if (d.csc) k_price_csc<<<grid, TILE_COLS, 0, st>>>(d, (int)napply, (int)nb_minv, nsw);
-    else k_price<<<grid, PRICE_THREADS, 0, st>>>(d, (int)napply, (int)nb_minv, nsw);
+    else k_price<<<grid, PRICE_THREADS, 0, st>>>(d, nsw, phase == 2 ? 1 : 0);
     return hipGetLastError();
 }
 
@@ -3376,7 +3414,7 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
                             hipEvent_t ev0, hipEvent_t ev1, int dslot) {
     hipError_t e = launch_btran_price(d, k_ub, ny_ub, phase, st, ev0, ev1);
     if (e != hipSuccess) return e;
-    const int ntiles = (int)cdiv(d.n, TILE_COLS), nsw = slack_wgs(d, ny_ub);
+    const int ntiles = d.ntiles, nsw = slack_wgs(d, ny_ub);
     const size_t lds = (size_t)k_ub * sizeof(double);
     if (lds <= 48 * 1024 && !d.force_select) {  // fused select + bump FTRAN
         const size_t ldsz = lds > 64 ? lds : 64;  // the timer workgroup reduces in it
@@ -3393,7 +3431,7 @@ hipError_t launch_iteration_head(const Dev& d, int k_ub, int ny_ub, int phase, i
                                  hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
     hipError_t e = launch_btran_price(d, k_ub, ny_ub, phase, st, ev0, ev1);
     if (e != hipSuccess) return e;
-    k_select_local<<<1, 1024, 0, st>>>(d, (int)cdiv(d.n, TILE_COLS), slack_wgs(d, ny_ub), rank);
+    k_select_local<<<1, 1024, 0, st>>>(d, d.ntiles, slack_wgs(d, ny_ub), rank);
     return hipGetLastError();
 }
 
