@@ -128,6 +128,34 @@ def enable_p2p(p, rank):
         return False
 
 
+def ngpu_probe(args, local):
+    """Torchrun-launched N > 1 in the default ngpu mode: before anything is
+    timed, rank 0 checks that one handle can drive the N devices (RCCL
+    communicator, peer mailbox probe, a small LP solved to optimality).  On
+    failure every rank falls back to --mode procs (one process per GPU), so a
+    node where the single-process path cannot run still yields a line."""
+    import numpy as np
+    from easylp_amd import Problem
+    from easylp_amd._lib import ELP_OPTIMAL
+    rng = np.random.default_rng(7)
+    m, n = 64, 64 * args.gpus * 4
+    A = np.asfortranarray(rng.random((m, n)))
+    b = n / 8 + rng.random(m) * n / 4
+    c = rng.random(n)
+    try:
+        if os.environ.get("ELP_BENCH_FAIL_NGPU"):  # (rehearses the fallback on a one-GPU box)
+            raise RuntimeError("ELP_BENCH_FAIL_NGPU set")
+        with Problem(m, n, device=local, ngpu=args.gpus, exchange=args.exchange) as p:
+            p.load_dense(A, np.ones(m, np.int32), b, c, maximize=True)
+            ok = p.solve() == ELP_OPTIMAL
+            if not ok:
+                print("ngpu probe: the probe LP did not solve to optimality", file=sys.stderr)
+            return ok
+    except Exception as e:  # (any failure: fall back, report it)
+        print(f"ngpu probe failed ({e}); falling back to --mode procs", file=sys.stderr)
+        return False
+
+
 class Ctx:
     """Where the bench runs.  procs: `world` processes, one GPU each (ngpu 1).
     ngpu: one working process (rank 0) whose handle drives `ngpu` devices;
@@ -170,23 +198,10 @@ class Ctx:
         return "ngpu x%d (one process), %s" % (self.ngpu, ex)
 
 
-def enable_p2p(p, rank):
-    """xGMI mailbox for the min-loc; collective and agreed by all ranks, so on
-    failure every rank falls back to the RCCL all-gather together."""
-    from easylp_amd._lib import ElpError
-    try:
-        p.comm_enable_p2p()
-        return True
-    except ElpError as e:
-        if rank == 0:
-            print(f"xGMI mailbox unavailable ({e}); RCCL all-gather min-loc", file=sys.stderr)
-        return False
-
-
 def make_problem(args, lib, m, n, ctx, **ctl):
     from easylp_amd import Problem
     from easylp_amd._lib import ELP_PROFILE_SAMPLE
-    p = Problem(m, n, device=ctx.local, verbose=ELP_PROFILE_SAMPLE if args.profile_price else 0,
+    p = Problem(m, n, device=ctx.devices[0], verbose=ELP_PROFILE_SAMPLE if args.profile_price else 0,
                 pricing=args.rule, sync_every=args.sync_every, ngpu=ctx.ngpu, exchange=args.exchange, **ctl)
     p2p = False
     if ctx.mode == "procs" or args.force_sharded:
@@ -497,6 +512,12 @@ def main():
 
     if world > 1:
         dist.init_process_group("gloo", init_method="env://")
+        if args.mode == "ngpu":
+            ok = torch.tensor([1 if rank != 0 else (1 if ngpu_probe(args, local) else 0)], dtype=torch.int32)
+            dist.broadcast(ok, 0)
+            if not int(ok.item()):
+                args.mode = "procs"
+                args.fallback = "ngpu probe failed on rank 0: one process per GPU"
     elif args.force_sharded:
         os.environ["ELP_RCCL_SINGLE"] = "1"
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -513,7 +534,7 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
         return
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(ctx.devices[0])
 
     from easylp_amd._lib import load
 
@@ -619,6 +640,7 @@ def main():
                             "(load from HBM + solve to optimality)" % (args.m, args.n),
                 "m": args.m, "n": args.n, "seed": args.seed,
                 "parallelism": parallelism,
+                "fallback": getattr(args, "fallback", None),
                 "iterations_timed": iters,
                 "pricing": args.pricing,
             },

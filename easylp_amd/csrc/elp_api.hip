@@ -108,6 +108,7 @@ struct elp_handle {
     std::vector<double*> peer_A;  // elp_load_dense_device: A copied to the other devices
     std::vector<size_t> peer_A_bytes;  // (elements held by each copy)
     bool broken = false;          // a rank failed and the RCCL communicators were aborted
+    int32_t sel_cap = 0;          // Dev::sel_cap (rank handles sharing a device)
     // scaling (elp_control.scaling): the solver works on A~ = 2^srow A 2^scol
     // (exponents per row and per GLOBAL column; empty: unscaled)
     std::vector<int32_t> srow_h, scol_h;
@@ -378,6 +379,7 @@ static int create_group(elp_handle* g) {
         g->tranks.resize(P);
         for (int r = 0; r < P; ++r) {
             g->tranks[r] = ThreadRank{g->tgroup.get(), r};
+            g->ranks[r]->sel_cap = 32;  // (Dev::sel_cap: P - 1 spinning grids of <= 32 workgroups)
             HIPCHK(hipSetDevice(g->rank_dev[r]));
             const int rc = g->ranks[r]->comm.init_host(P, r, ThreadGroup::allgather, ThreadGroup::allreduce,
                                                        ThreadGroup::bcast, &g->tranks[r]);
@@ -486,6 +488,7 @@ static int alloc_all(elp_handle* h) {
     d.mbox = (MboxRec*)h->comm.mbox;
     d.mpeers = (MboxRec* const*)h->comm.dpeers;
     d.force_select = std::getenv("ELP_FORCE_SELECT") ? 1 : 0;  // test hook
+    d.sel_cap = h->sel_cap;
     const size_t nv = (size_t)(n + 2 * m);
     hipError_t e = hipSuccess;
     auto A = [&](hipError_t x) {

@@ -199,6 +199,11 @@ struct Dev {
     // (rows ascending), a CSR copy serves the row activities, and the entering
     // column is scattered into the dense qcol each iteration
     int32_t csc, force_select;  // force_select: test hook (ELP_FORCE_SELECT), large-bump launch shape
+    // bump-row workgroups of the fused select kernel, at most (0: one per 4 rows):
+    // ranks that share a device (ngpu on fewer devices) spin in that kernel on
+    // the peer mailbox, and P - 1 ranks' spinning grids must leave the device
+    // room for the last rank's pricing launch (else it never starts)
+    int32_t sel_cap, sel_pad;
     int64_t nnz;
     const int64_t* cptr;
     const int32_t* rind;

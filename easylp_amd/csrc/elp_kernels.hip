@@ -913,7 +913,11 @@ constexpr int PRICE_THREADS = 64 * PRICE_SPLIT;
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 // plain (cached) loads: the live AR rows (~80 MB at 5000x50000) stay in the
 // 256 MiB Infinity Cache between passes; non-temporal loads measured 10% slower
-#define AR_LOAD(ptr) (*reinterpret_cast<const dbl2*>(ptr))
+// there.  NTL (host's choice, sweep_nt): non-temporal loads once the sweep is
+// larger than the Infinity Cache anyway (10 000 x 500 000), so it does not evict
+// the bump (AS, Minv) the latency kernels re-read every iteration
+#define AR_LOAD(ptr) (NTL ? __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(ptr)) \
+                          : *reinterpret_cast<const dbl2*>(ptr))
 #ifndef ELP_PRICE_UNR
 #define ELP_PRICE_UNR 16
 #endif
@@ -950,6 +954,7 @@ DEV void tile_apply(const Dev& d, int64_t tile, int64_t ntiles) {
 // tiles'), and the deferred update of the last pivot is applied by waves 1..3
 // of every tile once their sweep is done (phase 2; nothing the sweep reads)
 // instead of by trailing workgroups that started only as tiles retired.
+template <int NTL>
 DEV void price_body(const Dev& d, int nsw, int apply) {
     __shared__ double part[PRICE_SPLIT][TILE_COLS];
     __shared__ Cand red[PRICE_SPLIT];
@@ -1152,9 +1157,10 @@ DEV void pstamp_end(const Dev& d) {
     if (threadIdx.x == 0) d.pstamp[PSTRIDE * blockIdx.x + PSTRIDE - 1] = __builtin_amdgcn_s_memrealtime();
 }
 
+template <int NTL>
 __global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int nsw, int apply) {
     pstamp_begin<PRICE_THREADS>(d);
-    price_body(d, nsw, apply);
+    price_body<NTL>(d, nsw, apply);
     pstamp_end(d);
 }
 
@@ -1459,8 +1465,10 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles, int nsw) {
 // slack candidates itself (a total order: all agree), gathers a_R into LDS and
 // computes alpha_S for its 4 bump rows (one wave per row, wave order).
 // Workgroup 0 publishes q.  Saves a launch and the single-workgroup select.
+// nrw: the bump-row workgroups (the host's cdiv(k_ub, 4), or Dev::sel_cap):
+// workgroup b forms rows 4b + wave, 4b + wave + 4 nrw, ...
 template <int PFM>  // Minv values per lane held in registers (k <= 64 PFM): 8 or 16 by the host's bound
-__global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw, int k_ub, int dslot) {
+__global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw, int k_ub, int dslot, int nrw) {
     extern __shared__ __attribute__((aligned(16))) double aRs[];  // [k]
     __shared__ Cand red[4];
     RSTAMP(12);
@@ -1587,6 +1595,12 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw
     }
     acc = wave_tree(acc);
     if (lane == 0) d.alS[pr] = acc;
+    // (capped grid only) the rows past the first 4 nrw, from memory
+    for (int p2 = pr + 4 * nrw; p2 < k; p2 += 4 * nrw) {
+        double a2 = lane_chain(d.Minv + (size_t)p2 * d.ldm, aRs, k);
+        a2 = wave_tree(a2);
+        if (lane == 0) d.alS[p2] = a2;
+    }
     RSTAMP(15);
 }
 
@@ -3297,6 +3311,18 @@ static int slack_wgs(const Dev& d, int ny_ub) {
     return (int)cdiv(ny_ub > 0 ? ny_ub : 1, d.csc ? TILE_COLS : PRICE_THREADS);
 }
 
+// non-temporal sweep loads above this many sweep bytes (ELP_SWEEP_NT: 0 never,
+// 1 always, unset: 192 MB -- beyond the Infinity Cache's share the sweep can keep)
+static bool sweep_nt(double bytes) {
+    static const double thr = [] {
+        const char* e = std::getenv("ELP_SWEEP_NT");
+        if (!e) return 192.0e6;
+        const int v = std::atoi(e);
+        return v == 0 ? 1e300 : v == 1 ? 0.0 : (double)v * 1e6;
+    }();
+    return bytes > thr;
+}
+
 static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phase, hipStream_t st,
                                      hipEvent_t ev0, hipEvent_t ev1) {
     const int m = d.m;
@@ -3325,6 +3351,7 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phas
     // sweep applies the deferred plan inside its tiles (price_body)
     const int nsw = slack_wgs(d, ny_ub);
     const unsigned grid = (d.csc ? ntiles + napply : (unsigned)d.ntiles) + nsw;
+    const bool nt = !d.csc && sweep_nt(8.0 * (double)ny_ub * (double)d.n);
     if (ev0) {
         // profiling (ELP_PROFILE_EVENTS): events bound to the dispatch itself
         // (the CP's start / end timestamps of this launch, as a kernel trace
@@ -3332,13 +3359,17 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phas
         if (d.csc)
             hipExtLaunchKernelGGL(k_price_csc, dim3(grid), dim3(TILE_COLS), 0, st, ev0, ev1, 0, d, (int)napply,
                                   (int)nb_minv, nsw);
+        else if (nt)
+            hipExtLaunchKernelGGL(k_price<1>, dim3(grid), dim3(PRICE_THREADS), 0, st, ev0, ev1, 0, d, nsw,
+                                  phase == 2 ? 1 : 0);
         else
-            hipExtLaunchKernelGGL(k_price, dim3(grid), dim3(PRICE_THREADS), 0, st, ev0, ev1, 0, d, nsw,
+            hipExtLaunchKernelGGL(k_price<0>, dim3(grid), dim3(PRICE_THREADS), 0, st, ev0, ev1, 0, d, nsw,
                                   phase == 2 ? 1 : 0);
         return hipGetLastError();
     }
     if (d.csc) k_price_csc<<<grid, TILE_COLS, 0, st>>>(d, (int)napply, (int)nb_minv, nsw);
-    else k_price<<<grid, PRICE_THREADS, 0, st>>>(d, nsw, phase == 2 ? 1 : 0);
+    else if (nt) k_price<1><<<grid, PRICE_THREADS, 0, st>>>(d, nsw, phase == 2 ? 1 : 0);
+    else k_price<0><<<grid, PRICE_THREADS, 0, st>>>(d, nsw, phase == 2 ? 1 : 0);
     return hipGetLastError();
 }
 
@@ -3419,8 +3450,10 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
     if (lds <= 48 * 1024 && !d.force_select) {  // fused select + bump FTRAN
         const size_t ldsz = lds > 64 ? lds : 64;  // the timer workgroup reduces in it
         // + the timer workgroup, + the CSC column-scatter workgroup
-        const unsigned g = cdiv(k_ub > 0 ? k_ub : 1, 4) + (d.ptimer ? 1 : 0) + (d.csc ? 1 : 0);
-        k_select_ftran<8><<<g, 256, ldsz, st>>>(d, ntiles, nsw, k_ub, dslot);  // (16 measured no faster)
+        unsigned nrw = cdiv(k_ub > 0 ? k_ub : 1, 4);
+        if (d.sel_cap > 0 && nrw > (unsigned)d.sel_cap) nrw = (unsigned)d.sel_cap;
+        const unsigned g = nrw + (d.ptimer ? 1 : 0) + (d.csc ? 1 : 0);
+        k_select_ftran<8><<<g, 256, ldsz, st>>>(d, ntiles, nsw, k_ub, dslot, (int)nrw);  // (16 measured no faster)
         return launch_iteration_tail(d, k_ub, phase, st, false, dslot);
     }
     k_select<<<1, 1024, 0, st>>>(d, ntiles, nsw);

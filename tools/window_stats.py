@@ -32,7 +32,13 @@ def main(trace, bench_json):
     wall = rows[hi][1] - rows[lo][0]
     kern = {k: {"calls": n[k], "avg_us": dur[k] / n[k] / 1e3, "total_ms": dur[k] / 1e6}
             for k in sorted(dur, key=lambda k: -dur[k])}
-    kp = kern.get("k_price", {})
+    # k_price<0> / k_price<1> (cached / non-temporal sweep loads): one figure
+    kps = [k for k in kern if k.split("<")[0] == "k_price"]
+    kp = {}
+    if kps:
+        calls = sum(kern[k]["calls"] for k in kps)
+        tot = sum(kern[k]["total_ms"] for k in kps)
+        kp = {"calls": calls, "avg_us": tot * 1e3 / calls, "total_ms": tot}
     out = {"timed_solves": K, "price_launches_per_solve": L, "window_wall_ms": wall / 1e6,
            "k_price_avg_us_rocprof": kp.get("avg_us"),
            "k_price_avg_us_bench": b["roofline"]["avg_launch_us"], "bench_timer": b["roofline"].get("timer"),
