@@ -109,6 +109,10 @@ struct elp_handle {
     std::vector<size_t> peer_A_bytes;  // (elements held by each copy)
     bool broken = false;          // a rank failed and the RCCL communicators were aborted
     int32_t sel_cap = 0;          // Dev::sel_cap (rank handles sharing a device)
+    // buffers replaced by a growth at a poll, freed at the next load / destroy
+    // (ranks sharing a device: hipFree waits for the device to drain, and the
+    // other ranks' select kernels spin on this rank's next mailbox record)
+    std::vector<void*> retired;
     // scaling (elp_control.scaling): the solver works on A~ = 2^srow A 2^scol
     // (exponents per row and per GLOBAL column; empty: unscaled)
     std::vector<int32_t> srow_h, scol_h;
@@ -177,10 +181,12 @@ static void free_dev(elp_handle* h, bool keep_big = false) {
                     d.cand,     d.pstamp, d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand, d.rcnt, d.AT,
                     d.pkt, d.objg, d.ract, d.cand_xchg, h->d_flag, d.cS, d.slo, d.shi, d.rlo, d.rhi,
                     (void*)d.cptr, (void*)d.rind, (void*)d.cval, (void*)d.rptr, (void*)d.cind,
-                    (void*)d.rval, d.qcol, d.dstamp, d.rowvs, d.yvs, d.dw, d.dprev, (void*)d.srow,
+                    (void*)d.rval, d.qcol, d.qz, d.dstamp, d.rowvs, d.yvs, d.dw, d.dprev, (void*)d.srow,
                     (void*)d.scol};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    for (void* p : h->retired) (void)hipFree(p);
+    h->retired.clear();
     for (void*& p : h->lub)
         if (p) {
             (void)hipFree(p);
@@ -194,6 +200,13 @@ static void free_dev(elp_handle* h, bool keep_big = false) {
     d = Dev{};
     if (h->hctl) (void)hipHostFree(h->hctl);
     h->hctl = nullptr;
+}
+
+// a buffer a growth replaced (see elp_handle::retired)
+static void retire(elp_handle* h, void* p) {
+    if (!p) return;
+    if (h->sel_cap > 0) h->retired.push_back(p);
+    else (void)hipFree(p);
 }
 
 template <class T>
@@ -570,6 +583,7 @@ static int alloc_all(elp_handle* h) {
     A(dalloc(&d.pstamp, 2 * ((size_t)d.ntiles + (size_t)(mm / 128 + 1) + 3072 + 64)));
 #endif
     if (h->csc) A(dalloc(&d.qcol, mm));
+    else if (!std::getenv("ELP_NO_QZ")) A(dalloc(&d.qz, mm));  // (ELP_NO_QZ: A/B switch)
     if (std::getenv("ELP_STAMPS")) {
         A(dalloc(&d.dstamp, DSTAMP_STRIDE * 64));
         d.stamp_wide = std::atoi(std::getenv("ELP_STAMPS")) >= 2;
@@ -618,7 +632,7 @@ static int ensure_ar(elp_handle* h, int64_t rows) {
     HIPCHK(hipStreamSynchronize(h->st));
     HIPCHK(launch_ar_relayout(h->d, old, old_cap, (int)std::min<int64_t>(old_cap, h->hctl->ny), h->st));
     HIPCHK(hipStreamSynchronize(h->st));
-    (void)hipFree(old);
+    retire(h, old);
     return 0;
 }
 
@@ -657,7 +671,7 @@ static int ensure_k(elp_handle* h, int64_t need) {
                                 (size_t)k, hipMemcpyDeviceToDevice, h->st));
     }
     HIPCHK(hipStreamSynchronize(h->st));
-    for (double* p : {d.AS, d.Minv, d.MinvT, d.zpart}) (void)hipFree(p);
+    for (double* p : {d.AS, d.Minv, d.MinvT, d.zpart}) retire(h, p);
     d.AS = as;
     d.Minv = mi;
     d.MinvT = mt;
@@ -670,8 +684,8 @@ static int ensure_k(elp_handle* h, int64_t need) {
 static int ensure_w(elp_handle* h, int k) {
     const size_t need = (size_t)k * (size_t)k;
     if (need <= h->w_cap && h->d.W0) return 0;
-    if (h->d.W0) (void)hipFree(h->d.W0);
-    if (h->d.W1) (void)hipFree(h->d.W1);
+    retire(h, h->d.W0);
+    retire(h, h->d.W1);
     h->d.W0 = h->d.W1 = nullptr;
     size_t cap = std::max<size_t>(need, 64 * 64);
     cap = std::max(cap, h->w_cap * 2);

@@ -212,6 +212,11 @@ struct Dev {
     const int32_t* cind;
     const double* rval;
     double* qcol;
+    // dense, one-GPU select path: the entering column as FTRAN-z reads it
+    // (a_iq per row, scaled; the unit column of an entering slack), written by
+    // the select kernel's staging workgroups so k_ftran_zr can load it at
+    // kernel start instead of one round trip after its control block
+    double* qz;
     // debug (ELP_STAMPS): s_memrealtime stamps of k_ratio, 16 per chunk slot
     unsigned long long* dstamp;
     int32_t stamp_wide, pad_sw;  // ELP_STAMPS=2: also the grid-wide (atomic) stamps
@@ -276,7 +281,7 @@ hipError_t launch_apply_pending(const Dev& d, int k_ub, hipStream_t st);
 bool launch_select_xftran(const Dev& d, int k_ub, hipStream_t st, hipError_t* err);
 hipError_t launch_select_finish(const Dev& d, hipStream_t st);
 hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t st,
-                                 bool bump_ftran = true, int dslot = 0);
+                                 bool bump_ftran = true, int dslot = 0, int qz = 0);
 // row activities: ract = chain(ract, local nonzero nonbasic columns)
 hipError_t launch_row_chain(const Dev& d, hipStream_t st);
 // refactor = ns_resid; (host reads ns_emax) ns_update | gauss_jordan; primal

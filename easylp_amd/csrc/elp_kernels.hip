@@ -1467,8 +1467,11 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles, int nsw) {
 // Workgroup 0 publishes q.  Saves a launch and the single-workgroup select.
 // nrw: the bump-row workgroups (the host's cdiv(k_ub, 4), or Dev::sel_cap):
 // workgroup b forms rows 4b + wave, 4b + wave + 4 nrw, ...
+// nqz: the staging workgroups after them (Dev::qz; 0: none), QZ_PT rows per thread
+constexpr int QZ_PT = 8;
 template <int PFM>  // Minv values per lane held in registers (k <= 64 PFM): 8 or 16 by the host's bound
-__global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw, int k_ub, int dslot, int nrw) {
+__global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw, int k_ub, int dslot, int nrw,
+                                                      int nqz) {
     extern __shared__ __attribute__((aligned(16))) double aRs[];  // [k]
     __shared__ Cand red[4];
     RSTAMP(12);
@@ -1488,7 +1491,8 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw
     constexpr int PFR = 4;  // R-list entries per thread (k <= 1024)
     constexpr int PFC = 4;  // candidates per thread (<= 1023 tiles)
     const int ncand = ntiles + nsw;
-    const int pr = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const bool qzw = (int)blockIdx.x >= nrw && (int)blockIdx.x < nrw + nqz;  // a staging workgroup
+    const int pr = qzw ? k_ub : blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63, tid = threadIdx.x;
     const bool pfm = k_ub <= 64 * PFM, pfr = k_ub <= 256 * PFR;
     const bool pfc = ncand <= 256 * PFC;
@@ -1556,6 +1560,28 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw
     }
     if (d.csc && blockIdx.x == gridDim.x - 1 - d.ptimer) {  // CSC: dense entering column
         scatter_qcol_csc(d, q);
+        return;
+    }
+    if (qzw) {  // stage the entering column for k_ftran_zr (QZ_PT loads in flight)
+        const int m = d.m;
+        const int i0 = (int)(blockIdx.x - nrw) * 256 * QZ_PT + tid;
+        if (q < d.N) {
+            const double* col = qcolumn(d, q);
+            double v[QZ_PT];
+#pragma unroll
+            for (int t = 0; t < QZ_PT; ++t) v[t] = col[min(i0 + 256 * t, m - 1)];
+#pragma unroll
+            for (int t = 0; t < QZ_PT; ++t) {
+                const int i = i0 + 256 * t;
+                if (i < m) d.qz[i] = col == d.pkt ? v[t] : sca(d, v[t], i, q);
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < QZ_PT; ++t) {
+                const int i = i0 + 256 * t;
+                if (i < m) d.qz[i] = i == q - d.N ? 1.0 : 0.0;
+            }
+        }
         return;
     }
     if (q < d.N && d.csc) {
@@ -1828,7 +1854,7 @@ constexpr int ZR_ROWS = 32;   // rows per row tile: lane = row + 32 * half; each
 // and 64 fewer VGPRs); needs k_ub <= ZR_PA * threads
 constexpr int ZR_PA = 4;
 template <bool LDSZ, int ZR_WAVES, bool ALS>
-__global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int k_ub, int dslot) {
+__global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int k_ub, int dslot, int qz) {
     extern __shared__ __attribute__((aligned(16))) double zlds[];  // [nch_ub][ZR_ROWS], then (ALS) [k_ub] alpha_S
     __shared__ double red[ZR_WAVES];
     RSTAMP(16);
@@ -1867,11 +1893,13 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
     double ge = 0.0, xe = 0.0, le = 0.0, he = 0.0;
     int ve = -1;
     int u = -1;
+    double pq = 0.0;  // (qz) a_iq as the select kernel staged it
     if (row_tile && w == 0 && hh == 0 && i < d.m) {
         u = d.cover[i];
         xe = d.xr[i];
         le = d.rlo[i];
         he = d.rhi[i];
+        pq = (qz ? d.qz : d.xr)[i];
     }
     __builtin_amdgcn_sched_barrier(0);  // all of the above issued before any use
     // the control-block integers stay vector values up to here: their scalar
@@ -1890,6 +1918,7 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
             for (int t = 0; t < ZR_PA; ++t) KEEP(pa[t]);
         }
         KEEP(xe);
+        KEEP(pq);
         return;
     }
     RSTAMP(17);
@@ -1938,7 +1967,7 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int 
     }
     if (row_tile) {
         double aiq = 0.0;
-        if (u >= 0) aiq = q >= d.N ? (i == q - d.N ? 1.0 : 0.0) : qcol_at(d, qcolumn(d, q), q, i);
+        if (u >= 0) aiq = qz ? pq : q >= d.N ? (i == q - d.N ? 1.0 : 0.0) : qcol_at(d, qcolumn(d, q), q, i);
         if (ch0 < nch) {  // the prefetched chunk: fma chain over its real positions
             double acc = 0.0;
             if (i < m) {
@@ -3381,7 +3410,7 @@ hipError_t launch_apply_pending(const Dev& d, int k_ub, hipStream_t st) {
 }
 
 hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t st, bool bump_ftran,
-                                 int dslot) {
+                                 int dslot, int qz) {
     const int m = d.m;
     if (bump_ftran && k_ub > 0) k_ftran_bump<<<cdiv(k_ub, 4), 256, 0, st>>>(d, d.aR, d.alS, 1);
     const int nrt = (int)cdiv(m > 0 ? m : 1, ZR_ROWS);
@@ -3403,14 +3432,14 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     {
         // + 1: the snapshot workgroup
         if (als) {
-            if (zw == 4) k_ftran_zr<true, 4, true><<<nrt + nbt + 1, 256, lds_als, st>>>(d, nrt, k_ub, dslot);
-            else k_ftran_zr<true, 8, true><<<nrt + nbt + 1, 512, lds_als, st>>>(d, nrt, k_ub, dslot);
+            if (zw == 4) k_ftran_zr<true, 4, true><<<nrt + nbt + 1, 256, lds_als, st>>>(d, nrt, k_ub, dslot, qz);
+            else k_ftran_zr<true, 8, true><<<nrt + nbt + 1, 512, lds_als, st>>>(d, nrt, k_ub, dslot, qz);
         } else if (zw == 4) {
-            k_ftran_zr<true, 4, false><<<nrt + nbt + 1, 256, lds, st>>>(d, nrt, k_ub, dslot);
+            k_ftran_zr<true, 4, false><<<nrt + nbt + 1, 256, lds, st>>>(d, nrt, k_ub, dslot, qz);
         } else if (ldsz) {
-            k_ftran_zr<true, 8, false><<<nrt + nbt + 1, 512, lds, st>>>(d, nrt, k_ub, dslot);
+            k_ftran_zr<true, 8, false><<<nrt + nbt + 1, 512, lds, st>>>(d, nrt, k_ub, dslot, qz);
         } else {
-            k_ftran_zr<false, 8, false><<<nrt + nbt + 1, 512, 0, st>>>(d, nrt, k_ub, dslot);
+            k_ftran_zr<false, 8, false><<<nrt + nbt + 1, 512, 0, st>>>(d, nrt, k_ub, dslot, qz);
         }
     }
     // ratio test + (cases B/D) B^-1 row: one workgroup per 4 bump columns;
@@ -3452,9 +3481,11 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
         // + the timer workgroup, + the CSC column-scatter workgroup
         unsigned nrw = cdiv(k_ub > 0 ? k_ub : 1, 4);
         if (d.sel_cap > 0 && nrw > (unsigned)d.sel_cap) nrw = (unsigned)d.sel_cap;
-        const unsigned g = nrw + (d.ptimer ? 1 : 0) + (d.csc ? 1 : 0);
-        k_select_ftran<8><<<g, 256, ldsz, st>>>(d, ntiles, nsw, k_ub, dslot, (int)nrw);  // (16 measured no faster)
-        return launch_iteration_tail(d, k_ub, phase, st, false, dslot);
+        const unsigned nqz = d.qz && !d.csc ? cdiv(d.m, 256 * QZ_PT) : 0;
+        const unsigned g = nrw + nqz + (d.ptimer ? 1 : 0) + (d.csc ? 1 : 0);
+        k_select_ftran<8><<<g, 256, ldsz, st>>>(d, ntiles, nsw, k_ub, dslot, (int)nrw,
+                                                (int)nqz);  // (16 measured no faster)
+        return launch_iteration_tail(d, k_ub, phase, st, false, dslot, nqz > 0 ? 1 : 0);
     }
     k_select<<<1, 1024, 0, st>>>(d, ntiles, nsw);
     return launch_iteration_tail(d, k_ub, phase, st, true, dslot);

@@ -96,3 +96,19 @@ def test_scaled_mip_vs_oracle(gpu):
         g = gpu.solve_dense(*args, is_int=rec["is_int"])
         o = solve_mip(*args, rec["is_int"])
         assert (g.status, g.objval, g.stats["mip_nodes"]) == (o.status, o.objval, o.stats["nodes"])
+
+
+def test_large_finite_bound_and_rhs_survive_scaling(gpu):
+    """A finite bound / rhs that crosses 1e30 only after scaling stays finite
+    (clamped once, before scaling, as the oracle does): column 1's
+    coefficients are ~1e3 (its bound is scaled up ~2^10), row 1's ~1e-3 (its rhs
+    too).  The re-clamp this guards against turned both infinite: unbounded."""
+    from oracle import solve_dense as orc
+    A = np.array([[1e3, -1e3, 0.0], [0.0, 0.0, 1e-3]])
+    args = (A, np.ones(2, np.int32), np.array([5.0, 1e27]), np.array([1.0, 0.0, 1.0]),
+            np.zeros(3), np.array([np.inf, 1e27, np.inf]), True)
+    g = gpu.solve_dense(*args, trace=1000)
+    o = orc(*args, trace_cap=1000)
+    _same(g, o)
+    assert g.status == 0
+    assert g.x[1] == 1e27
