@@ -488,7 +488,7 @@ static int alloc_all(elp_handle* h) {
         d.tile_w = (int32_t)tw;
         d.ntiles = (int32_t)std::max<int64_t>(1, (n + tw - 1) / tw);
     }
-    d.ldr = (int64_t)d.ntiles * TILE_COLS;
+    d.ldr = (int64_t)d.ntiles * d.tile_w;  // AR: [tile][row][tile_w], rows packed
     d.infinity = h->ctl.infinity;
     d.tol_singular = h->ctl.tol_singular;
     d.mb_ticks = (int64_t)(h->ctl.mailbox_timeout * 1e8);  // s_memrealtime: 100 MHz

@@ -147,14 +147,14 @@ struct Dev {
     int32_t world;        // ranks sharing the columns
     int32_t sharded;      // 1: column-sharded solve (world > 1 or a test transport)
     int64_t ldm;   // Minv leading dimension (= max(m,1))
-    int64_t ldr;   // AR row length: ntiles x TILE_COLS (a tile's rows are TILE_COLS apart)
+    int64_t ldr;   // AR row length: ntiles x tile_w (a tile's rows are tile_w apart)
     int32_t tile_w, ntiles;  // pricing tiles: tile_w (even, <= TILE_COLS) columns each
     int64_t arcap; // AR rows per column tile (capacity)
     const double* A;  // column-major m x n (this shard's columns)
     double* AT;       // its row-major copy (m x n, ld n): AR row copies read it contiguously
     const double* Afull;  // sharded + replicated: all N columns (A = Afull + col0*m);
                           // null: the entering column comes in the exchanged pkt
-    double* AR;       // Y rows, tile-major: [ldr/128 tiles][arcap rows][128 cols]
+    double* AR;       // Y rows, tile-major: [ntiles][arcap rows][tile_w cols]
                       // (a pricing wave streams one contiguous run of rows)
     double* AS;       // basic structural columns, column-major (m x m capacity)
     double* Minv;     // bump inverse, row-major ldm x ldm

@@ -688,8 +688,8 @@ __global__ void k_scale_apply(int m, int64_t ncols, double* __restrict__ A, cons
 
 // element (row p, column j) of the tile-major AR
 DEV size_t ar_at(const Dev& d, int64_t p, int64_t j) {
-    const int64_t tw = d.tile_w;  // columns per tile (<= TILE_COLS; rows of a tile stay TILE_COLS apart)
-    return ((size_t)(j / tw) * (size_t)d.arcap + (size_t)p) * TILE_COLS + (size_t)(j % tw);
+    const int64_t tw = d.tile_w;  // columns per tile (<= TILE_COLS), also the row stride inside a tile
+    return ((size_t)(j / tw) * (size_t)d.arcap + (size_t)p) * (size_t)tw + (size_t)(j % tw);
 }
 
 // AR[p][j] = A[Yl[p]][j] for p < ny (initial fill)
@@ -703,13 +703,13 @@ __global__ void k_fill_AR(Dev d) {
 
 // grow AR: rows [0, rows) of every tile into the new capacity
 __global__ void k_ar_relayout(Dev d, const double* __restrict__ old_ar, int64_t old_cap, int rows) {
-    const int64_t ntiles = d.ldr / TILE_COLS;
-    const int64_t total = ntiles * (int64_t)rows * TILE_COLS;
+    const int64_t tw = d.tile_w, ntiles = d.ldr / tw;
+    const int64_t total = ntiles * (int64_t)rows * tw;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
          e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t t = e / ((int64_t)rows * TILE_COLS);
-        const int64_t r = e % ((int64_t)rows * TILE_COLS);
-        d.AR[(size_t)t * (size_t)d.arcap * TILE_COLS + (size_t)r] = old_ar[(size_t)t * (size_t)old_cap * TILE_COLS + (size_t)r];
+        const int64_t t = e / ((int64_t)rows * tw);
+        const int64_t r = e % ((int64_t)rows * tw);
+        d.AR[(size_t)t * (size_t)d.arcap * tw + (size_t)r] = old_ar[(size_t)t * (size_t)old_cap * tw + (size_t)r];
     }
 }
 
@@ -995,7 +995,7 @@ DEV void price_body(const Dev& d, int nsw, int apply) {
     __builtin_amdgcn_sched_barrier(0);
     // lanes past the tile's width read their last valid pair again (same line: no traffic)
     const int lcol = 2 * lane < tw ? 2 * lane : ((tw - 1) & ~1);
-    const double* col = d.AR + (size_t)tile * (size_t)d.arcap * TILE_COLS + lcol;
+    const double* col = d.AR + (size_t)tile * (size_t)d.arcap * (size_t)tw + lcol;  // rows tw apart
     const double* __restrict__ yy = d.yy;
     const int cap = (int)d.arcap;
     dbl2 va[UNR], vb[UNR];
@@ -1009,7 +1009,7 @@ DEV void price_body(const Dev& d, int nsw, int apply) {
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {  // slot w + S u, clamped into AR (masked by |Y| at use)
         const int pp = min(w + S * u, cap - 1);
-        va[u] = AR_LOAD(col + (size_t)pp * TILE_COLS);
+        va[u] = AR_LOAD(col + (size_t)pp * (size_t)tw);
 #if !ELP_PRICE_YLANE
         ya[u] = yy[pp];
 #endif
@@ -1053,7 +1053,7 @@ DEV void price_body(const Dev& d, int nsw, int apply) {
     do {                                                                             \
         _Pragma("unroll") for (int u = 0; u < UNR; ++u) {                            \
             const int r_ = (P) + S * u < nys ? (P) + S * u : (P);                    \
-            V[u] = AR_LOAD(col + (size_t)r_ * TILE_COLS);                            \
+            V[u] = AR_LOAD(col + (size_t)r_ * (size_t)tw);                           \
         }                                                                            \
         const int ry_ = (P) + S * (lane % UNR);                                      \
         Y = yy[ry_ < nys ? ry_ : (P)];                                               \
@@ -1064,7 +1064,7 @@ DEV void price_body(const Dev& d, int nsw, int apply) {
     do {                                                                             \
         _Pragma("unroll") for (int u = 0; u < UNR; ++u) {                            \
             const int r_ = (P) + S * u < nys ? (P) + S * u : (P);                    \
-            V[u] = AR_LOAD(col + (size_t)r_ * TILE_COLS);                            \
+            V[u] = AR_LOAD(col + (size_t)r_ * (size_t)tw);                           \
             Y[u] = yy[r_];                                                           \
         }                                                                            \
     } while (0)

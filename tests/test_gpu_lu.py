@@ -109,8 +109,8 @@ def test_lu_packing_2000x10000_trace(gpu):
     """a 2000 x 10 000 sparse LP (5 nonzeros per column): the
     first 1500 pivots bit for bit against the oracle (a capped solve: the
     oracle's dense vectors make the whole solve minutes on one core), and the
-    GPU's own solve to optimality at the HiGHS optimum of
-    tests/golden/sparse_lu.json."""
+    GPU's own solve to optimality (default basis: the bump inverse) at the
+    HiGHS optimum of tests/golden/sparse_lu.json."""
     import easylp_amd
     from easylp_amd.synth import sparse_packing
     from oracle import solve_lu
@@ -135,11 +135,11 @@ def test_lu_packing_2000x10000_trace(gpu):
         full = p.solution(st)
     assert st == 0
     assert abs(full.objval - fx["objective"]) <= 1e-8 * abs(fx["objective"])
-    assert full.stats["lu_nnz"] > 0
+    assert full.stats["basis"] == 1  # ELP_BASIS_AUTO solves with the bump inverse
 
 
 def test_lu_mip_matches_oracle_optimum(gpu):
-    """Branch and bound over sparse-LU relaxations (the CSC default): the
+    """Branch and bound over sparse-LU relaxations (basis = ELP_BASIS_LU): the
     reference's MIP tests at their known optima."""
     import easylp_amd
     from conftest import load_mip_known_answers

@@ -1,7 +1,7 @@
 set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread -p no:cacheprovider --durations=20 > gpurun_out/pytest_gpu_r03b.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v ${PYTEST_EXTRA:-} --timeout 400 --timeout-method thread -p no:cacheprovider --durations=20 > gpurun_out/pytest_gpu_r03b.log 2>&1
 rc=$?; tail -30 gpurun_out/pytest_gpu_r03b.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_r03b.log 2>&1 || { echo "smoke failed"; cat gpurun_out/smoke_r03b.log; exit 3; }
 cat gpurun_out/smoke_r03b.log

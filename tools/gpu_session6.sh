@@ -1,13 +1,23 @@
-# C4 (10000 x 500000): cached vs non-temporal pricing sweep, per-kernel
-# averages over the last 2000 iterations (rocprofv3 kernel trace)
+# (1) C3 pricing: 128-column tiles vs balanced packed tiles (ELP_TILE_BAL=1);
+# (2) C4 (10000 x 500000): cached vs non-temporal pricing sweep, per-kernel
+#     averages over the last 2000 iterations (rocprofv3 kernel trace);
+# (3) ELP_STAMPS phase stamps at C3 and C4
 set -u
 R="$GRAFT_REPO_ROOT"
 mkdir -p "$R/gpurun_out"
+cd "$R"
+Q="--steps 10 --warmup 2 --c4 0 --sparse 0 --no-cpu --compare-rules 0 --host-input 0"
+for v in w128 bal w128b balb; do
+  case $v in bal*) export ELP_TILE_BAL=1;; *) unset ELP_TILE_BAL;; esac
+  timeout -k 10 300 python -u bench.py $Q > gpurun_out/b6_$v.json 2> gpurun_out/b6_$v.err || { echo "bench $v failed"; tail -5 gpurun_out/b6_$v.err; exit 4; }
+  python -c "import json;d=json.load(open('gpurun_out/b6_$v.json'));r=d['roofline'];w=d['steady_state'];print('$v', round(d['value']), 'it/s tto', round(d['time_to_optimal_s'],4), 'price us', round(r['avg_launch_us'],2), 'frac', round(r['frac'],3), 'window us/it', round(w['us_per_iteration'],2))"
+done
+unset ELP_TILE_BAL
 cd /tmp && export TMPDIR=/tmp
 Q="--steps 0 --warmup 0 --c4 1 --sparse 0 --no-cpu --compare-rules 0 --window 0 --host-input 0"
-for v in ${VARIANTS:-nt0 ntauto}; do
+for v in nt0 ntauto; do
   if [ $v = nt0 ]; then export ELP_SWEEP_NT=0; else unset ELP_SWEEP_NT; fi
-  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d /tmp/c4_$v -o run -- python3 "$R/bench.py" $Q > "$R/gpurun_out/c4_$v.json" 2> "$R/gpurun_out/c4_$v.err" || { echo "c4 $v failed"; tail -5 "$R/gpurun_out/c4_$v.err"; exit 4; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d /tmp/c4_$v -o run -- python3 "$R/bench.py" $Q > "$R/gpurun_out/c4_$v.json" 2> "$R/gpurun_out/c4_$v.err" || { echo "c4 $v failed"; tail -5 "$R/gpurun_out/c4_$v.err"; exit 5; }
   python3 "$R/tools/c4_kernels.py" "$(find /tmp/c4_$v -name '*kernel_trace.csv' | head -1)" 2000 > "$R/gpurun_out/c4k_$v.txt"
   head -8 "$R/gpurun_out/c4k_$v.txt"
   python3 -c "import json;d=json.load(open('$R/gpurun_out/c4_$v.json'));s=d['scaling_config'];print('$v', s['iterations_to_optimal'], round(s['time_to_optimal_s'],3), s['objective'])"
@@ -16,5 +26,5 @@ done
 unset ELP_SWEEP_NT
 cd "$R"
 S="--steps 1 --warmup 0 --sparse 0 --no-cpu --compare-rules 0 --window 0 --host-input 0"
-ELP_STAMPS=1 timeout -k 10 300 python bench.py $S --c4 1 > gpurun_out/stamps_r03.json 2> gpurun_out/stamps_r03.err || { echo "stamps run failed"; tail -5 gpurun_out/stamps_r03.err; exit 5; }
+ELP_STAMPS=1 timeout -k 10 300 python bench.py $S --c4 1 > gpurun_out/stamps_r03.json 2> gpurun_out/stamps_r03.err || { echo "stamps run failed"; tail -5 gpurun_out/stamps_r03.err; exit 6; }
 grep -A2 "k_ratio stamps" gpurun_out/stamps_r03.err
