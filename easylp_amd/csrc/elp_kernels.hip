@@ -3483,8 +3483,13 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
         if (d.sel_cap > 0 && nrw > (unsigned)d.sel_cap) nrw = (unsigned)d.sel_cap;
         const unsigned nqz = d.qz && !d.csc ? cdiv(d.m, 256 * QZ_PT) : 0;
         const unsigned g = nrw + nqz + (d.ptimer ? 1 : 0) + (d.csc ? 1 : 0);
-        k_select_ftran<8><<<g, 256, ldsz, st>>>(d, ntiles, nsw, k_ub, dslot, (int)nrw,
-                                                (int)nqz);  // (16 measured no faster)
+        // Minv row values per lane in registers: 8 (k <= 512), 10 (k <= 640: the
+        // last 4 000 iterations of 10 000 x 500 000, k 529; 16 measured no faster
+        // there, r01 -- fewer waves per SIMD), else the row is read after a_R
+        if (k_ub > 512 && k_ub <= 640)
+            k_select_ftran<10><<<g, 256, ldsz, st>>>(d, ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz);
+        else
+            k_select_ftran<8><<<g, 256, ldsz, st>>>(d, ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz);
         return launch_iteration_tail(d, k_ub, phase, st, false, dslot, nqz > 0 ? 1 : 0);
     }
     k_select<<<1, 1024, 0, st>>>(d, ntiles, nsw);
