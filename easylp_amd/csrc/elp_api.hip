@@ -113,6 +113,11 @@ struct elp_handle {
     // (ranks sharing a device: hipFree waits for the device to drain, and the
     // other ranks' select kernels spin on this rank's next mailbox record)
     std::vector<void*> retired;
+    // device copy of Dev for the per-iteration kernels (Dev::self) and its
+    // pinned staging copy, which also remembers what was last uploaded
+    Dev* d_dev = nullptr;
+    Dev* h_dev = nullptr;
+    bool dev_uploaded = false;
     // scaling (elp_control.scaling): the solver works on A~ = 2^srow A 2^scol
     // (exponents per row and per GLOBAL column; empty: unscaled)
     std::vector<int32_t> srow_h, scol_h;
@@ -200,6 +205,30 @@ static void free_dev(elp_handle* h, bool keep_big = false) {
     d = Dev{};
     if (h->hctl) (void)hipHostFree(h->hctl);
     h->hctl = nullptr;
+}
+
+// Dev::self: upload h->d when it changed since the last upload (loads and
+// growths change it; a chunk usually finds it as it was)
+static int upload_dev(elp_handle* h) {
+    if (!h->d_dev) {
+        if (hipMalloc((void**)&h->d_dev, sizeof(Dev)) != hipSuccess) {
+            h->d_dev = nullptr;
+            return fail(ELP_E_NOMEM, "device Dev allocation failed");
+        }
+        if (hipHostMalloc((void**)&h->h_dev, sizeof(Dev), hipHostMallocDefault) != hipSuccess) {
+            h->h_dev = nullptr;
+            return fail(ELP_E_NOMEM, "pinned Dev allocation failed");
+        }
+        h->dev_uploaded = false;
+    }
+    h->d.self = h->d_dev;
+    if (h->dev_uploaded && std::memcmp(h->h_dev, &h->d, sizeof(Dev)) == 0) return 0;
+    // the staging copy may still feed the previous upload: let it land first
+    HIPCHK(hipStreamSynchronize(h->st));
+    std::memcpy((void*)h->h_dev, (const void*)&h->d, sizeof(Dev));
+    HIPCHK(hipMemcpyAsync(h->d_dev, h->h_dev, sizeof(Dev), hipMemcpyHostToDevice, h->st));
+    h->dev_uploaded = true;
+    return 0;
 }
 
 // a buffer a growth replaced (see elp_handle::retired)
@@ -1677,6 +1706,7 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             HIPCHK(hipMemcpyAsync(h->d.dstamp, init.data(), init.size() * 8, hipMemcpyHostToDevice, h->st));
             HIPCHK(hipStreamSynchronize(h->st));
         }
+        if ((rc = upload_dev(h))) return rc;  // (Dev::self for this chunk's launches)
         const double t_enq0 = now_s();
         const bool prof_chunk = prof && (prof_all || h->prof_chunks++ % 8 == 0);
         for (int t = 0; t < chunk; ++t) {
@@ -2579,6 +2609,8 @@ extern "C" void elp_destroy(elp_handle* h) {
                 h->dbg_wait, (long long)h->stats.host_polls);
     free_dev(h);
     release_kept(h);
+    if (h->d_dev) (void)hipFree(h->d_dev);
+    if (h->h_dev) (void)hipHostFree(h->h_dev);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     h->comm.destroy();
     if (h->st) (void)hipStreamDestroy(h->st);

@@ -204,6 +204,11 @@ struct Dev {
     // the peer mailbox, and P - 1 ranks' spinning grids must leave the device
     // room for the last rank's pricing launch (else it never starts)
     int32_t sel_cap, sel_pad;
+    // device copy of this struct (elp_api upload_dev, refreshed at every chunk
+    // when it changed): the four per-iteration kernels take it by pointer
+    // (ELP_DEV_PTR) so their prologues read it through the scalar cache / L2
+    // instead of ~800 B of fresh kernel arguments per launch
+    const Dev* self;
     int64_t nnz;
     const int64_t* cptr;
     const int32_t* rind;

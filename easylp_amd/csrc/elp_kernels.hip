@@ -20,6 +20,21 @@
 #include <hip/hip_ext.h>
 #include <math.h>
 
+// The per-iteration kernels read Dev through a pointer to its device copy
+// (Dev::self) or, with ELP_DEV_PTR 0, by value from the kernel arguments.
+#ifndef ELP_DEV_PTR
+#define ELP_DEV_PTR 1
+#endif
+#if ELP_DEV_PTR
+#define DEV_PARAM const Dev* __restrict__ dp_
+#define DEV_BIND const Dev& d = *dp_;
+#define DEV_ARG(x) ((x).self)
+#else
+#define DEV_PARAM Dev d
+#define DEV_BIND
+#define DEV_ARG(x) (x)
+#endif
+
 namespace elp {
 
 #define DEV __device__ __forceinline__
@@ -1158,7 +1173,8 @@ DEV void pstamp_end(const Dev& d) {
 }
 
 template <int NTL>
-__global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int nsw, int apply) {
+__global__ void __launch_bounds__(PRICE_THREADS) k_price(DEV_PARAM, int nsw, int apply) {
+    DEV_BIND
     pstamp_begin<PRICE_THREADS>(d);
     price_body<NTL>(d, nsw, apply);
     pstamp_end(d);
@@ -1470,8 +1486,9 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles, int nsw) {
 // nqz: the staging workgroups after them (Dev::qz; 0: none), QZ_PT rows per thread
 constexpr int QZ_PT = 8;
 template <int PFM>  // Minv values per lane held in registers (k <= 64 PFM): 8 or 16 by the host's bound
-__global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw, int k_ub, int dslot, int nrw,
+__global__ void __launch_bounds__(256) k_select_ftran(DEV_PARAM, int ntiles, int nsw, int k_ub, int dslot, int nrw,
                                                       int nqz) {
+    DEV_BIND
     extern __shared__ __attribute__((aligned(16))) double aRs[];  // [k]
     __shared__ Cand red[4];
     RSTAMP(12);
@@ -1854,7 +1871,8 @@ constexpr int ZR_ROWS = 32;   // rows per row tile: lane = row + 32 * half; each
 // and 64 fewer VGPRs); needs k_ub <= ZR_PA * threads
 constexpr int ZR_PA = 4;
 template <bool LDSZ, int ZR_WAVES, bool ALS>
-__global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int k_ub, int dslot, int qz) {
+__global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(DEV_PARAM, int nrt, int k_ub, int dslot, int qz) {
+    DEV_BIND
     extern __shared__ __attribute__((aligned(16))) double zlds[];  // [nch_ub][ZR_ROWS], then (ALS) [k_ub] alpha_S
     __shared__ double red[ZR_WAVES];
     RSTAMP(16);
@@ -2104,8 +2122,9 @@ enum { SI_VSQ, SI_RPOS0, SI_YPOS0, SI_YLAST, SI_SLLAST, SI_RLLAST, SI_RPOSYL, SI
 // PFT: B^-1 row values per lane held in registers (k <= 64 PFT), 8 or 16 by the
 // host's bound on k (a longer row is read in a loop)
 template <int PFT>
-__global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int lds_row, int defer,
+__global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, int lds_row, int defer,
                                                int nmain, int k_ub, int dslot, int nreg) {
+    DEV_BIND
     extern __shared__ __attribute__((aligned(16))) double asrow_lds[];  // [k]: A[lrow, S]
     __shared__ double dred[4];
     __shared__ Leave lred[4];
@@ -3389,16 +3408,16 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phas
             hipExtLaunchKernelGGL(k_price_csc, dim3(grid), dim3(TILE_COLS), 0, st, ev0, ev1, 0, d, (int)napply,
                                   (int)nb_minv, nsw);
         else if (nt)
-            hipExtLaunchKernelGGL(k_price<1>, dim3(grid), dim3(PRICE_THREADS), 0, st, ev0, ev1, 0, d, nsw,
+            hipExtLaunchKernelGGL(k_price<1>, dim3(grid), dim3(PRICE_THREADS), 0, st, ev0, ev1, 0, DEV_ARG(d), nsw,
                                   phase == 2 ? 1 : 0);
         else
-            hipExtLaunchKernelGGL(k_price<0>, dim3(grid), dim3(PRICE_THREADS), 0, st, ev0, ev1, 0, d, nsw,
+            hipExtLaunchKernelGGL(k_price<0>, dim3(grid), dim3(PRICE_THREADS), 0, st, ev0, ev1, 0, DEV_ARG(d), nsw,
                                   phase == 2 ? 1 : 0);
         return hipGetLastError();
     }
     if (d.csc) k_price_csc<<<grid, TILE_COLS, 0, st>>>(d, (int)napply, (int)nb_minv, nsw);
-    else if (nt) k_price<1><<<grid, PRICE_THREADS, 0, st>>>(d, nsw, phase == 2 ? 1 : 0);
-    else k_price<0><<<grid, PRICE_THREADS, 0, st>>>(d, nsw, phase == 2 ? 1 : 0);
+    else if (nt) k_price<1><<<grid, PRICE_THREADS, 0, st>>>(DEV_ARG(d), nsw, phase == 2 ? 1 : 0);
+    else k_price<0><<<grid, PRICE_THREADS, 0, st>>>(DEV_ARG(d), nsw, phase == 2 ? 1 : 0);
     return hipGetLastError();
 }
 
@@ -3432,14 +3451,14 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     {
         // + 1: the snapshot workgroup
         if (als) {
-            if (zw == 4) k_ftran_zr<true, 4, true><<<nrt + nbt + 1, 256, lds_als, st>>>(d, nrt, k_ub, dslot, qz);
-            else k_ftran_zr<true, 8, true><<<nrt + nbt + 1, 512, lds_als, st>>>(d, nrt, k_ub, dslot, qz);
+            if (zw == 4) k_ftran_zr<true, 4, true><<<nrt + nbt + 1, 256, lds_als, st>>>(DEV_ARG(d), nrt, k_ub, dslot, qz);
+            else k_ftran_zr<true, 8, true><<<nrt + nbt + 1, 512, lds_als, st>>>(DEV_ARG(d), nrt, k_ub, dslot, qz);
         } else if (zw == 4) {
-            k_ftran_zr<true, 4, false><<<nrt + nbt + 1, 256, lds, st>>>(d, nrt, k_ub, dslot, qz);
+            k_ftran_zr<true, 4, false><<<nrt + nbt + 1, 256, lds, st>>>(DEV_ARG(d), nrt, k_ub, dslot, qz);
         } else if (ldsz) {
-            k_ftran_zr<true, 8, false><<<nrt + nbt + 1, 512, lds, st>>>(d, nrt, k_ub, dslot, qz);
+            k_ftran_zr<true, 8, false><<<nrt + nbt + 1, 512, lds, st>>>(DEV_ARG(d), nrt, k_ub, dslot, qz);
         } else {
-            k_ftran_zr<false, 8, false><<<nrt + nbt + 1, 512, 0, st>>>(d, nrt, k_ub, dslot, qz);
+            k_ftran_zr<false, 8, false><<<nrt + nbt + 1, 512, 0, st>>>(DEV_ARG(d), nrt, k_ub, dslot, qz);
         }
     }
     // ratio test + (cases B/D) B^-1 row: one workgroup per 4 bump columns;
@@ -3459,7 +3478,7 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
         }
         // (8 B^-1 values per lane in registers: 16 for k > 512 measured slower at
         //  10 000 x 500 000, 16.5 vs 14.7 us -- the longer rows go through the loop)
-        k_ratio<8><<<nmain + nar, 256, lds_row ? lds : 0, st>>>(d, phase, nrt + nbt, lds_row, defer, (int)nmain,
+        k_ratio<8><<<nmain + nar, 256, lds_row ? lds : 0, st>>>(DEV_ARG(d), phase, nrt + nbt, lds_row, defer, (int)nmain,
                                                                k_ub, dslot, nrt + nbt * zw);
     }
     if (!defer) {
@@ -3487,9 +3506,9 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
         // last 4 000 iterations of 10 000 x 500 000, k 529; 16 measured no faster
         // there, r01 -- fewer waves per SIMD), else the row is read after a_R
         if (k_ub > 512 && k_ub <= 640)
-            k_select_ftran<10><<<g, 256, ldsz, st>>>(d, ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz);
+            k_select_ftran<10><<<g, 256, ldsz, st>>>(DEV_ARG(d), ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz);
         else
-            k_select_ftran<8><<<g, 256, ldsz, st>>>(d, ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz);
+            k_select_ftran<8><<<g, 256, ldsz, st>>>(DEV_ARG(d), ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz);
         return launch_iteration_tail(d, k_ub, phase, st, false, dslot, nqz > 0 ? 1 : 0);
     }
     k_select<<<1, 1024, 0, st>>>(d, ntiles, nsw);
