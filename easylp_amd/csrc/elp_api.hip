@@ -521,7 +521,7 @@ static int alloc_all(elp_handle* h) {
     d.infinity = h->ctl.infinity;
     d.tol_singular = h->ctl.tol_singular;
     d.mb_ticks = (int64_t)(h->ctl.mailbox_timeout * 1e8);  // s_memrealtime: 100 MHz
-    d.ptimer = (h->ctl.verbose & ELP_PROFILE_PRICE) ? 1 : 0;
+    d.ptimer = ELP_DIAG && (h->ctl.verbose & ELP_PROFILE_PRICE) ? 1 : 0;  // (diagnostic builds)
     d.csc = h->csc ? 1 : 0;
     // the mailbox carries the min-loc record only: with A not replicated the
     // entering column must travel, so that load uses the collective
@@ -613,7 +613,7 @@ static int alloc_all(elp_handle* h) {
 #endif
     if (h->csc) A(dalloc(&d.qcol, mm));
     else if (!std::getenv("ELP_NO_QZ")) A(dalloc(&d.qz, mm));  // (ELP_NO_QZ: A/B switch)
-    if (std::getenv("ELP_STAMPS")) {
+    if (ELP_DIAG && std::getenv("ELP_STAMPS")) {  // (diagnostic builds)
         A(dalloc(&d.dstamp, DSTAMP_STRIDE * 64));
         d.stamp_wide = std::atoi(std::getenv("ELP_STAMPS")) >= 2;
     }
@@ -1706,7 +1706,7 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             HIPCHK(hipMemcpyAsync(h->d.dstamp, init.data(), init.size() * 8, hipMemcpyHostToDevice, h->st));
             HIPCHK(hipStreamSynchronize(h->st));
         }
-        if ((rc = upload_dev(h))) return rc;  // (Dev::self for this chunk's launches)
+        if (ELP_DEV_PTR && (rc = upload_dev(h))) return rc;  // (Dev::self for this chunk's launches)
         const double t_enq0 = now_s();
         const bool prof_chunk = prof && (prof_all || h->prof_chunks++ % 8 == 0);
         for (int t = 0; t < chunk; ++t) {

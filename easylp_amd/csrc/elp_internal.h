@@ -4,6 +4,18 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Diagnostic builds (tools/build_variant.sh NAME "-DELP_DIAG=1"): the
+// ELP_STAMPS phase stamps and the ELP_PROFILE_PRICE device-clock pricing
+// timer.  Off in the product build: their run-time tests sat at the head of
+// the latency kernels, each a dependent scalar load before the control block.
+#ifndef ELP_DIAG
+#define ELP_DIAG 0
+#endif
+// Dev by pointer for the per-iteration kernels (A/B switch, see elp_kernels.hip)
+#ifndef ELP_DEV_PTR
+#define ELP_DEV_PTR 0
+#endif
+
 namespace elp {
 
 // variable status (same codes as oracle/elp_oracle.c)

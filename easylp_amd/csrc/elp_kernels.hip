@@ -20,11 +20,12 @@
 #include <hip/hip_ext.h>
 #include <math.h>
 
-// The per-iteration kernels read Dev through a pointer to its device copy
-// (Dev::self) or, with ELP_DEV_PTR 0, by value from the kernel arguments.
-#ifndef ELP_DEV_PTR
-#define ELP_DEV_PTR 1
-#endif
+// The per-iteration kernels read Dev by value from the kernel arguments or,
+// with ELP_DEV_PTR 1, through a pointer to its device copy (Dev::self).  The
+// pointer form measured slower (r03: 38.3-38.9 against 36.8-37.3 us per C3
+// iteration): pointers loaded from memory lose their global address space,
+// so the control-block reads became flat loads that wait for every load in
+// flight; kernel-argument pointers stay global.
 #if ELP_DEV_PTR
 #define DEV_PARAM const Dev* __restrict__ dp_
 #define DEV_BIND const Dev& d = *dp_;
@@ -833,7 +834,7 @@ DEV bool apply_role(const Dev& d, int napply, int nb_minv) {
 // non-tile workgroup (1 apply, 2 slacks)
 #ifdef ELP_PDBG
 constexpr int PSTRIDE = 6;
-#define PDBG(slot, v) do { if (d.ptimer && threadIdx.x == 0) d.pstamp[PSTRIDE * blockIdx.x + (slot)] = (v); } while (0)
+#define PDBG(slot, v) do { if (ELP_DIAG && d.ptimer && threadIdx.x == 0) d.pstamp[PSTRIDE * blockIdx.x + (slot)] = (v); } while (0)
 #else
 constexpr int PSTRIDE = 2;
 #define PDBG(slot, v) do {} while (0)
@@ -1161,13 +1162,13 @@ DEV void price_body(const Dev& d, int nsw, int apply) {
 // its end (after all its waves), so first start -> last end is the launch
 template <int NT>
 DEV void pstamp_begin(const Dev& d) {
-    if (d.ptimer && threadIdx.x == 0) {
+    if (ELP_DIAG && d.ptimer && threadIdx.x == 0) {
         d.pstamp[PSTRIDE * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
         if (blockIdx.x == 0) d.ctl->price_grid = (int32_t)gridDim.x;
     }
 }
 DEV void pstamp_end(const Dev& d) {
-    if (!d.ptimer) return;
+    if (!ELP_DIAG || !d.ptimer) return;
     __syncthreads();  // (every return path of the bodies is workgroup-uniform)
     if (threadIdx.x == 0) d.pstamp[PSTRIDE * blockIdx.x + PSTRIDE - 1] = __builtin_amdgcn_s_memrealtime();
 }
@@ -1320,7 +1321,7 @@ DEV void price_timer_sum(const Dev& d, unsigned long long* red) {
 
 // ============================================================== select
 // debug stamps (Dev::dstamp, ELP_STAMPS): s_memrealtime at the phases of workgroup 0
-#define RSTAMP(i) do { if (d.dstamp && blockIdx.x == 0 && threadIdx.x == 0) \
+#define RSTAMP(i) do { if (ELP_DIAG && d.dstamp && blockIdx.x == 0 && threadIdx.x == 0) \
     d.dstamp[dslot * DSTAMP_STRIDE + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 constexpr int MAX_P2P = 64;  // ranks a mailbox exchange supports
 
@@ -1464,7 +1465,7 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles, int nsw) {
     }
     const int q = (int)best.j;
     if (threadIdx.x == 0) entering_chosen(d, best);
-    if (d.ptimer) price_timer_sum<1024>(d, reinterpret_cast<unsigned long long*>(red));
+    if (ELP_DIAG && d.ptimer) price_timer_sum<1024>(d, reinterpret_cast<unsigned long long*>(red));
     if (d.csc) {  // dense copy of the entering column + a_R through rpos
         scatter_qcol_csc(d, q);
         if (q < d.N) {
@@ -1571,11 +1572,11 @@ __global__ void __launch_bounds__(256) k_select_ftran(DEV_PARAM, int ntiles, int
     RSTAMP(14);
     const int q = (int)best.j;
     if (blockIdx.x == 0 && tid == 0) entering_chosen(d, best);
-    if (d.ptimer && blockIdx.x == gridDim.x - 1) {  // the extra timer workgroup
+    if (ELP_DIAG && d.ptimer && blockIdx.x == gridDim.x - 1) {  // the extra timer workgroup
         price_timer_sum<256>(d, reinterpret_cast<unsigned long long*>(aRs));
         return;
     }
-    if (d.csc && blockIdx.x == gridDim.x - 1 - d.ptimer) {  // CSC: dense entering column
+    if (d.csc && blockIdx.x == gridDim.x - 1 - (ELP_DIAG ? d.ptimer : 0)) {  // CSC: dense entering column
         scatter_qcol_csc(d, q);
         return;
     }
@@ -1666,7 +1667,7 @@ __global__ void __launch_bounds__(1024) k_select_local(Dev d, int ntiles, int ns
         }
         d.cand_xchg[rank] = x;
     }
-    if (d.ptimer) price_timer_sum<1024>(d, reinterpret_cast<unsigned long long*>(red));
+    if (ELP_DIAG && d.ptimer) price_timer_sum<1024>(d, reinterpret_cast<unsigned long long*>(red));
 }
 
 // after the all-gather: global min-loc (same total order on every rank); the
@@ -2132,7 +2133,7 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
     const int tid = threadIdx.x;
     const int col = blockIdx.x * 4 + (tid >> 6);
     const int lane = tid & 63;
-    if (d.stamp_wide && tid == 0) {  // (ELP_STAMPS=2: grid-wide stamps, contended atomics)
+    if (ELP_DIAG && d.stamp_wide && tid == 0) {  // (ELP_STAMPS=2: grid-wide stamps, contended atomics)
         const unsigned long long t = __builtin_amdgcn_s_memrealtime();
         atomicMin(&d.dstamp[dslot * DSTAMP_STRIDE + 11], t);
         atomicMax(&d.dstamp[dslot * DSTAMP_STRIDE + 8], t);
@@ -2386,7 +2387,7 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
             if (rm_slot >= 0 && rm_slot != rm_last) d.AR[ar_at(d, rm_slot, j)] = d.AR[ar_at(d, rm_last, j)];
             if (ap_slot >= 0) d.AR[ar_at(d, ap_slot, j)] = a_row(d, ap_row, j);
         }
-        if (d.stamp_wide) {
+        if (ELP_DIAG && d.stamp_wide) {
             __syncthreads();
             if (tid == 0) atomicMax(&d.dstamp[dslot * DSTAMP_STRIDE + 10], __builtin_amdgcn_s_memrealtime());
         }
@@ -2496,7 +2497,7 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
         if (slot >= 0) d.yy[slot] = yn;
     }
     RSTAMP(5);
-    if (d.stamp_wide) {
+    if (ELP_DIAG && d.stamp_wide) {
         __syncthreads();
         if (tid == 0) atomicMax(&d.dstamp[dslot * DSTAMP_STRIDE + 9], __builtin_amdgcn_s_memrealtime());
     }
