@@ -77,6 +77,8 @@ def parse():
     ap.add_argument("--sparse-n", type=int, default=10000)
     ap.add_argument("--sparse-steps", type=int, default=1000)
     ap.add_argument("--sparse-cpu-iters", type=int, default=200)
+    ap.add_argument("--sparse-window", type=int, default=5000,
+                    help="iterations of the phase-1 Netlib-scale LP timed from its start")
     ap.add_argument("--pricing", choices=["devex", "dantzig"], default="devex",
                     help="pricing rule (elp_control.pricing; devex is lp_solve's default)")
     ap.add_argument("--sync-every", type=int, default=32,
@@ -388,25 +390,28 @@ def host_input(args, lib, ctx, m, n, label, reps):
 
 
 def sparse_rate(args, local, with_cpu):
-    """BASELINE config 5 on the CSC path with the sparse-LU basis (elp_control
-    basis AUTO -> LU for CSC input):
-      * "Netlib scale": the 20 000 x 100 000 LP of easylp_amd.synth.sparse_kkt
+    """BASELINE config 5 on the CSC path (basis AUTO = the explicit bump
+    inverse with k-sized buffers):
+      * "Netlib scale": the 20 000 x 100 000 LPs of easylp_amd.synth.sparse_kkt
         (5 nonzeros per column, boxed columns, optimum known by construction
-        and pinned by HiGHS in tests/golden/sparse_lu.json) to optimality;
+        and pinned by HiGHS in tests/golden/sparse_lu.json): the feasible-start
+        one to optimality, the phase-1 one over its first `sparse_window`
+        iterations (it needs ~70 000 primal pivots: minutes, DESIGN.md 9.1);
       * the seeded 1000 x 10 000 packing LP (sparse_packing) to optimality and
         a steady-state window;
       * the Klee-Minty cube n = 12 (4095 Dantzig pivots on the unscaled cube).
-    The CPU leg is the oracle's LU engine (orc_solve_lu, same algorithm, one
-    thread) over a bounded number of iterations of the same LPs."""
+    The CPU leg is the oracle's LU engine (orc_solve_lu, one thread) over a
+    bounded number of iterations of the same LPs."""
     import json as _json
     import numpy as np
     from easylp_amd import Problem
     from easylp_amd.synth import sparse_kkt, sparse_packing
     out = {}
     fx = {f["name"]: f for f in _json.load(open(os.path.join(ROOT, "tests", "golden", "sparse_lu.json")))}
-    # ---- Netlib scale: 20 000 x 100 000 ----
-    k = fx["kkt_20000x100000"]
-    cp, ri, v, b, c, u, obj = sparse_kkt(k["seed"], k["m"], k["n"], k["k"])
+    basis_name = {1: "explicit bump inverse (k-sized buffers)", 2: "sparse LU (Markowitz + product-form etas)"}
+    # ---- Netlib scale: 20 000 x 100 000, feasible start, to optimality ----
+    k = fx["kkt_feasible_20000x100000"]
+    cp, ri, v, b, c, u, obj = sparse_kkt(k["seed"], k["m"], k["n"], k["k"], feasible_start=True)
     m, n = k["m"], k["n"]
     dirs, lo = np.ones(m, np.int32), np.zeros(n)
     with Problem(m, n, device=local, pricing=args.rule) as p:
@@ -416,15 +421,15 @@ def sparse_rate(args, local, with_cpu):
         tto = time.perf_counter() - t0
         s = p.stats()
         z = p.solution(st).objval
-    big = {"workload": "sparse LP m=%d n=%d nnz=%d (sparse_kkt, boxed; BASELINE configs[4] at Netlib scale)"
-                       % (m, n, int(cp[-1])),
-           "basis": "sparse LU (Markowitz + product-form etas)", "status": st, "objective": z,
-           "objective_highs": k["highs_objective"], "rel_err_vs_highs": abs(z - k["highs_objective"]) / abs(k["highs_objective"]),
+    big = {"workload": "sparse LP m=%d n=%d nnz=%d (sparse_kkt feasible_start, boxed; BASELINE configs[4] at "
+                       "Netlib scale)" % (m, n, int(cp[-1])),
+           "basis": basis_name.get(s["basis"], s["basis"]), "status": st, "objective": z,
+           "objective_constructed": obj, "objective_highs": k["highs_objective"],
+           "rel_err_vs_highs": abs(z - k["highs_objective"]) / abs(k["highs_objective"]),
            "iterations_to_optimal": s["iterations"], "bound_flips": s["bound_flips"], "refactors": s["refactors"],
            "time_to_optimal_s": tto, "load_s": s["seconds_load"],
            "value": s["iterations"] / tto if tto > 0 else None, "unit": "iterations/s (whole solve)",
-           "lu_nnz": s["lu_nnz"], "eta_nnz": s["eta_nnz"], "basic_structurals": s["bump_dim"],
-           "dense_inverse_bytes_avoided": 3 * 8 * m * m}
+           "basic_structurals": s["bump_dim"], "dense_inverse_bytes_avoided": 3 * 8 * m * m}
     if with_cpu:
         from oracle import solve_lu
         w = args.sparse_cpu_iters
@@ -434,6 +439,23 @@ def sparse_rate(args, local, with_cpu):
                                "sample": "oracle/elp_oracle_lu.c (C, -O3, 1 thread) first %d iterations, setup "
                                          "included" % r.stats["iterations"]}
     out["netlib_scale"] = big
+    # ---- the phase-1 LP of the same size: a window from the start ----
+    k = fx["kkt_20000x100000"]
+    cp, ri, v, b, c, u, obj = sparse_kkt(k["seed"], k["m"], k["n"], k["k"])
+    with Problem(m, n, device=local, pricing=args.rule) as p:
+        t0 = time.perf_counter()
+        p.load_csc(cp, ri, v, dirs, b, c, lo, u, maximize=True)
+        st = p.iterate(args.sparse_window)
+        el = time.perf_counter() - t0
+        s = p.stats()
+    out["netlib_scale_phase1"] = {
+        "workload": "sparse LP m=%d n=%d nnz=%d (sparse_kkt: %d rows with b < 0, one column in ten at its "
+                    "upper bound in the optimum)" % (m, n, int(cp[-1]), int((b < 0).sum())),
+        "iterations": s["iterations"], "phase1_iterations": s["phase1_iterations"], "status": st,
+        "basic_structurals": s["bump_dim"], "seconds": el, "load_s": s["seconds_load"],
+        "value": s["iterations"] / el if el > 0 else None, "unit": "iterations/s (first iterations, load included)",
+        "note": "not solved to optimality here: ~70 000 primal pivots with up to ~8 800 basic structurals "
+                "(DESIGN.md 9.1); HiGHS dual simplex needs %d" % k["highs_iterations"]}
     # ---- 1000 x 10 000 packing ----
     m, n = args.sparse_m, args.sparse_n
     cp, ri, v, b, c = sparse_packing(args.seed, m, n, 5)
@@ -454,7 +476,8 @@ def sparse_rate(args, local, with_cpu):
     s1 = p.stats()
     p.close()
     it = s1["iterations"] - s0["iterations"]
-    out.update({"workload": "sparse LP m=%d n=%d nnz=%d (CSC, sparse LU)" % (m, n, int(cp[-1])),
+    out.update({"workload": "sparse LP m=%d n=%d nnz=%d (CSC)" % (m, n, int(cp[-1])),
+                "basis": basis_name.get(s2["basis"], s2["basis"]),
                 "value": s2["iterations"] / tto, "unit": "iterations/s (whole solve)",
                 "time_to_optimal_s": tto, "status": st, "objective": sol.objval,
                 "iterations_to_optimal": s2["iterations"], "basic_structurals": s2["bump_dim"],

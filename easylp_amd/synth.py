@@ -40,7 +40,7 @@ def dense_of(colptr, rowind, val, m: int, n: int) -> np.ndarray:
     return A
 
 
-def sparse_kkt(seed: int, m: int, n: int, k: int, per_col: int = 5):
+def sparse_kkt(seed: int, m: int, n: int, k: int, per_col: int = 5, feasible_start: bool = False):
     """A sparse boxed LP of Netlib-like size whose optimum is known by
     construction (a KKT point), for the sparse-LU engine at scales no offline
     reference solver finishes here:
@@ -54,7 +54,14 @@ def sparse_kkt(seed: int, m: int, n: int, k: int, per_col: int = 5):
     b = A x* on R and A x* + U[0.1, 1) elsewhere; c_j = a_j'y* on S and
     a_j'y* -+ U[0.05, 1) on the columns at 0 / at u, so (x*, y*) is primal and
     dual feasible and complementary: optimal.  Returns colptr, rowind, val, b,
-    c, u, objective (c'x*, computed here in float64)."""
+    c, u, objective (c'x*, computed here in float64).
+
+    feasible_start: every entry positive and no column at its upper bound in
+    x*, so b >= 0 and the slack basis is feasible (no phase 1) and no column
+    has to cross the basis on its way to u.  The default LP needs a phase 1
+    over the rows with b_i < 0 and moves one column in ten to its upper bound
+    through the basis: a primal simplex walks ~70 000 pivots on it at
+    20 000 x 100 000 with up to ~8 800 basic structurals."""
     rng = np.random.default_rng(seed)
     R = np.sort(rng.choice(m, k, replace=False))
     S = np.sort(rng.choice(n, k, replace=False))
@@ -76,6 +83,8 @@ def sparse_kkt(seed: int, m: int, n: int, k: int, per_col: int = 5):
     np.cumsum(counts, out=colptr[1:])
     rowind = np.concatenate([np.asarray(cc, dtype=np.int32) for cc in cols])
     val = rng.uniform(0.1, 1.0, size=rowind.size) * rng.choice([-1.0, 1.0], size=rowind.size, p=[0.3, 0.7])
+    if feasible_start:
+        val = np.abs(val)
     colid = np.repeat(np.arange(n), counts)
     rpos = np.full(m, -1)
     rpos[R] = np.arange(k)
@@ -86,6 +95,8 @@ def sparse_kkt(seed: int, m: int, n: int, k: int, per_col: int = 5):
     u = rng.uniform(1.0, 10.0, size=n)
     x = np.zeros(n)
     at_up = rng.random(n) < 0.1
+    if feasible_start:
+        at_up[:] = False
     x[at_up] = u[at_up]
     x[S] = u[S] * rng.uniform(0.2, 0.8, size=k)
     at_up[S] = False

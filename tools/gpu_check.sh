@@ -21,10 +21,15 @@ STEPS=${STEPS:-20}
 WARM=${WARM:-5}
 TMP=/tmp/elp_prof_$TAG
 mkdir -p "$TMP"
+# heartbeat: single GPU tests and solves can run minutes without printing;
+# every step below has its own time limit
+(while sleep 30; do date +%T >> "$OUT/hb_$TAG.txt"; done) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 echo "== host: $(nproc) cpus; $(grep -m1 'model name' /proc/cpuinfo)" | tee "$OUT/host_$TAG.txt"
 
 if [ "$SKIP_TESTS" = "0" ]; then
-timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --durations=12 --timeout 300 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_gpu_$TAG.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -x --durations=25 --timeout 300 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_gpu_$TAG.log" 2>&1
 rc=$?
 tail -5 "$OUT/pytest_gpu_$TAG.log"
 if [ $rc -ne 0 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi
