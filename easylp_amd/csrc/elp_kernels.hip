@@ -1871,6 +1871,13 @@ constexpr int ZR_ROWS = 32;   // rows per row tile: lane = row + 32 * half; each
 // of every lane loading the chunk's 32 values itself (half the VMEM instructions
 // and 64 fewer VGPRs); needs k_ub <= ZR_PA * threads
 constexpr int ZR_PA = 4;
+// XPF: chunks past the 2 ZR_WAVES half-waves' first ones (k > 512 with 8-wave
+// tiles: 529 at the end of 10 000 x 500 000 is 17 chunks on 16 half-waves)
+// whose values every thread of the row tile prefetches cooperatively (ZR_XR
+// per thread, 256-B row segments) before the control block, parked in LDS; the
+// owning half-wave then runs its chain from LDS instead of paying a second
+// dependent round trip to AS.  Same chain, same order: same bits.
+constexpr int ZR_XPF = 2;
 template <bool LDSZ, int ZR_WAVES, bool ALS>
 __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(DEV_PARAM, int nrt, int k_ub, int dslot, int qz) {
     DEV_BIND
@@ -1894,9 +1901,23 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(DEV_PARAM, int nrt, 
     const int ch0 = 2 * w + hh;
     double a0[ZCHUNK], s0[ALS ? 1 : ZCHUNK], pa[ALS ? ZR_PA : 1];
     const bool row_tile = (int)blockIdx.x < nrt;
+    constexpr int XR = ALS ? ZR_XPF * ZCHUNK * ZR_ROWS / (64 * ZR_WAVES) : 1;
+    double xv[XR];
+    const int nch_ub = (k_ub + ZCHUNK - 1) / ZCHUNK;
+    const int nxp = ALS ? min(max(nch_ub - 2 * ZR_WAVES, 0), ZR_XPF) : 0;  // prefetched extra chunks
     if constexpr (ALS) {  // this thread's share of alpha_S, staged in LDS below
 #pragma unroll
         for (int t = 0; t < ZR_PA; ++t) pa[t] = ld_clamp(d.alS, (int)threadIdx.x + (int)blockDim.x * t, k_ub);
+        // the extra chunks: value v = [chunk x][position][row], rows fastest
+        // (clamped addresses, masked when used)
+        const int rb = blockIdx.x * ZR_ROWS, mlast = d.m - 1;
+#pragma unroll
+        for (int t = 0; t < XR; ++t) {
+            const int v = (int)threadIdx.x + (int)blockDim.x * t;
+            const int x = v / (ZCHUNK * ZR_ROWS), pos = (v / ZR_ROWS) % ZCHUNK, row = v % ZR_ROWS;
+            const int cpos = min((2 * ZR_WAVES + x) * ZCHUNK + pos, k_ub - 1);
+            xv[t] = d.AS[(size_t)cpos * mm + min(rb + row, mlast)];
+        }
     }
     if (row_tile && ch0 * ZCHUNK < k_ub && i < d.m) {
         const double* col = d.AS + (size_t)(ch0 * ZCHUNK) * mm + i;
@@ -1935,6 +1956,8 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(DEV_PARAM, int nrt, 
         } else {
 #pragma unroll
             for (int t = 0; t < ZR_PA; ++t) KEEP(pa[t]);
+#pragma unroll
+            for (int t = 0; t < XR; ++t) KEEP(xv[t]);
         }
         KEEP(xe);
         KEEP(pq);
@@ -1975,12 +1998,18 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(DEV_PARAM, int nrt, 
     const int nch = (k + ZCHUNK - 1) / ZCHUNK;
     // z partials of this tile's rows: LDS, or (huge bumps) a private slice of zpart
     double* zp = LDSZ ? zlds : d.zpart + (size_t)blockIdx.x * ZR_ROWS * (size_t)nch;
-    double* als = zlds + (size_t)((k_ub + ZCHUNK - 1) / ZCHUNK) * ZR_ROWS;  // (ALS)
+    double* als = zlds + (size_t)nch_ub * ZR_ROWS;  // (ALS)
+    double* xz = als + k_ub;                         // (ALS) [nxp][ZCHUNK][ZR_ROWS]
     if constexpr (ALS) {
 #pragma unroll
         for (int t = 0; t < ZR_PA; ++t) {
             const int p = (int)threadIdx.x + (int)blockDim.x * t;
             if (p < k) als[p] = pa[t];
+        }
+#pragma unroll
+        for (int t = 0; t < XR; ++t) {
+            const int v = (int)threadIdx.x + (int)blockDim.x * t;
+            if (v < nxp * ZCHUNK * ZR_ROWS) xz[v] = xv[t];
         }
         __syncthreads();
     }
@@ -2003,6 +2032,13 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(DEV_PARAM, int nrt, 
         // last, partial chunk (measured: FTRAN-z 21 us at 10 000 x 500 000, k 529)
         for (int ch = ch0 + 2 * ZR_WAVES; ch < nch; ch += 2 * ZR_WAVES) {
             const int c0 = ch * ZCHUNK, len = min(ZCHUNK, k - c0);
+            if (ALS && ch - 2 * ZR_WAVES < nxp) {  // a prefetched extra chunk: from LDS
+                const double* xc = xz + (size_t)(ch - 2 * ZR_WAVES) * ZCHUNK * ZR_ROWS + r;
+                double acc = 0.0;
+                for (int t = 0; t < len; ++t) acc = fma(xc[t * ZR_ROWS], als[c0 + t], acc);
+                zp[ch * ZR_ROWS + r] = i < m ? acc : 0.0;
+                continue;
+            }
             const double* col = d.AS + (size_t)c0 * mm + (i < m ? i : 0);
             double a[ZCHUNK], s[ALS ? 1 : ZCHUNK];  // the whole chunk in flight
 #pragma unroll
@@ -3447,7 +3483,8 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     // 10 000 x 500 000 at k 529: 18.8 -> 16.3 us; with one chunk per half-wave the
     // registers win (the LDS round trip cost 0.8 us at 5000 x 50000, r02)
     static const bool no_als = getenv("ELP_NO_ALS") != nullptr;  // A/B
-    const size_t lds_als = lds + (size_t)k_ub * sizeof(double);
+    const int nxp = (int)std::min<int64_t>(std::max<int64_t>((int64_t)cdiv(k_ub, ZCHUNK) - 2 * zw, 0), ZR_XPF);
+    const size_t lds_als = lds + (size_t)k_ub * sizeof(double) + (size_t)nxp * ZCHUNK * ZR_ROWS * sizeof(double);
     const bool als = !no_als && ldsz && k_ub > 2 * zw * ZCHUNK && k_ub <= ZR_PA * 64 * zw && lds_als <= 64 * 1024;
     {
         // + 1: the snapshot workgroup
@@ -3477,8 +3514,10 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
             nar = cdiv(d.n, 256);
             if (nar > ELP_NAR_MAX) nar = ELP_NAR_MAX;
         }
-        // (8 B^-1 values per lane in registers: 16 for k > 512 measured slower at
-        //  10 000 x 500 000, 16.5 vs 14.7 us -- the longer rows go through the loop)
+        // (8 B^-1 values per lane in registers; for k > 512 the row is read in a
+        //  loop after the decision -- 16 per lane measured slower at 10 000 x
+        //  500 000 (16.5 vs 14.7 us, r01), 10 as well (12.01 vs 11.75 us at k
+        //  529, r03 A/B over the last 2000 iterations))
         k_ratio<8><<<nmain + nar, 256, lds_row ? lds : 0, st>>>(DEV_ARG(d), phase, nrt + nbt, lds_row, defer, (int)nmain,
                                                                k_ub, dslot, nrt + nbt * zw);
     }
