@@ -15,6 +15,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <atomic>
+#include <map>
+#include <unordered_map>
 #include <condition_variable>
 #include <memory>
 #include <mutex>
@@ -93,6 +95,8 @@ struct elp_handle {
     int64_t prof_chunks = 0;     // chunks seen by ELP_PROFILE_SAMPLE
     int32_t* d_flag = nullptr;   // one int for cross-rank decisions
     int64_t ar_rows = 0;         // AR capacity in rows (grown at polls)
+    int64_t shape_m = -1, shape_n = -1;  // the previous load's shape (reloads start at its grown capacities)
+    bool shape_csc = false;
     bool replicated = false;     // sharded, every rank holds all of A (Dev::Afull)
     bool csc = false;            // A given in CSC (elp_load_csc)
     int64_t mb_epoch = 0;        // loads so far (xGMI mailbox sequence epoch)
@@ -113,6 +117,11 @@ struct elp_handle {
     // (ranks sharing a device: hipFree waits for the device to drain, and the
     // other ranks' select kernels spin on this rank's next mailbox record)
     std::vector<void*> retired;
+    // buffers of the last load kept for the next one (free_dev on a reload):
+    // alloc_all's allocations by size; a reload of the same shape takes them
+    // back instead of ~80 hipFree + hipMalloc pairs (1.8 ms at 5000 x 50000)
+    std::unordered_map<void*, size_t> asize;
+    std::multimap<size_t, void*> pool;
     // device copy of Dev for the per-iteration kernels (Dev::self) and its
     // pinned staging copy, which also remembers what was last uploaded
     Dev* d_dev = nullptr;
@@ -166,7 +175,13 @@ static void release_kept(elp_handle* h) {
     h->keep_A_bytes = h->keep_AT_bytes = 0;
 }
 
-// keep_big: a reload -- A's copy and A^T stay allocated for the next load
+static void drain_pool(elp_handle* h) {
+    for (auto& kv : h->pool) (void)hipFree(kv.second);
+    h->pool.clear();
+}
+
+// keep_big: a reload -- A's copy and A^T stay allocated for the next load, the
+// other buffers go to the handle's pool (dalloc inside alloc_all takes them back)
 static void free_dev(elp_handle* h, bool keep_big = false) {
     Dev& d = h->d;
     if (keep_big) {
@@ -178,6 +193,12 @@ static void free_dev(elp_handle* h, bool keep_big = false) {
         h->A_owned = nullptr;
         d.AT = nullptr;
     }
+    auto release = [&](void* p) {
+        const auto it = h->asize.find(p);
+        if (keep_big && it != h->asize.end()) h->pool.emplace(it->second, p);
+        else (void)hipFree(p);
+        if (it != h->asize.end()) h->asize.erase(it);
+    };
     void* ptrs[] = {h->A_owned, d.AR,  d.AS,    d.Minv,  d.W0,   d.W1,    d.b,     d.obj,
                     d.lb,       d.ub,  d.cost,  d.xval,  d.asgn, d.xr,    d.xs,    d.y,
                     d.t,        d.acol, d.aR,   d.alS,   d.alU,  d.zz,    d.zpart, d.vrow,
@@ -189,7 +210,8 @@ static void free_dev(elp_handle* h, bool keep_big = false) {
                     (void*)d.rval, d.qcol, d.qz, d.dstamp, d.rowvs, d.yvs, d.dw, d.dprev, (void*)d.srow,
                     (void*)d.scol};
     for (void* p : ptrs)
-        if (p) (void)hipFree(p);
+        if (p) release(p);
+    if (!keep_big) drain_pool(h);
     for (void* p : h->retired) (void)hipFree(p);
     h->retired.clear();
     for (void*& p : h->lub)
@@ -203,8 +225,10 @@ static void free_dev(elp_handle* h, bool keep_big = false) {
     h->d_flag = nullptr;
     h->w_cap = 0;  // (W0 / W1 went with the rest)
     d = Dev{};
-    if (h->hctl) (void)hipHostFree(h->hctl);
-    h->hctl = nullptr;
+    if (h->hctl && !keep_big) {  // (a reload keeps the pinned control-block copy)
+        (void)hipHostFree(h->hctl);
+        h->hctl = nullptr;
+    }
 }
 
 // Dev::self: upload h->d when it changed since the last upload (loads and
@@ -234,13 +258,29 @@ static int upload_dev(elp_handle* h) {
 // a buffer a growth replaced (see elp_handle::retired)
 static void retire(elp_handle* h, void* p) {
     if (!p) return;
+    h->asize.erase(p);  // (never pooled: a growth replaced it)
     if (h->sel_cap > 0) h->retired.push_back(p);
     else (void)hipFree(p);
 }
 
+// the handle whose alloc_all is running on this thread (ngpu ranks load on
+// threads of their own): dalloc then draws on and records into its pool
+static thread_local elp_handle* t_alloc_h = nullptr;
 template <class T>
 static hipError_t dalloc(T** p, size_t count) {
-    return hipMalloc((void**)p, (count ? count : 1) * sizeof(T));
+    const size_t bytes = (count ? count : 1) * sizeof(T);
+    elp_handle* h = t_alloc_h;
+    if (!h) return hipMalloc((void**)p, bytes);
+    const auto it = h->pool.find(bytes);
+    if (it != h->pool.end()) {
+        *p = static_cast<T*>(it->second);
+        h->pool.erase(it);
+    } else {
+        const hipError_t e = hipMalloc((void**)p, bytes);
+        if (e != hipSuccess) return e;
+    }
+    h->asize[*p] = bytes;
+    return hipSuccess;
 }
 
 // a buffer of `bytes`, the kept one when it is exactly that size
@@ -481,7 +521,15 @@ extern "C" int elp_create(elp_handle** out, int64_t m, int64_t n, const elp_cont
 }
 
 // Allocate every device buffer for the local shard (called by elp_load_*).
+static int alloc_all_body(elp_handle* h);
 static int alloc_all(elp_handle* h) {
+    t_alloc_h = h;
+    const int rc = alloc_all_body(h);
+    t_alloc_h = nullptr;
+    drain_pool(h);  // what this shape did not take back
+    return rc;
+}
+static int alloc_all_body(elp_handle* h) {
     Dev& d = h->d;
     const int64_t m = h->m, n = h->nloc;
     const int64_t mm = m > 0 ? m : 1;
@@ -495,7 +543,14 @@ static int alloc_all(elp_handle* h) {
     // bump capacity: the explicit inverse needs O(m k + k^2), not O(m^2) -- k (the
     // basic structurals) starts at 0 and grows by at most one per iteration, so
     // the buffers start small and double at a poll (ensure_k)
-    h->kcap = std::min<int64_t>(mm, 256);
+    // a reload of the same shape starts at the capacities the last solve grew
+    // to (the values never depend on them), so it does not grow again
+    const bool same_shape = h->shape_m == m && h->shape_n == n && h->shape_csc == h->csc;
+    const int64_t kcap_prev = same_shape ? h->kcap : 0, ar_prev = same_shape ? h->ar_rows : 0;
+    h->shape_m = m;
+    h->shape_n = n;
+    h->shape_csc = h->csc;
+    h->kcap = std::min<int64_t>(mm, std::max<int64_t>(256, kcap_prev));
     if (const char* e = std::getenv("ELP_KCAP_INIT"))  // test hook: force growth
         h->kcap = std::max<int64_t>(1, std::min<int64_t>(mm, std::atoll(e)));
     d.ldm = h->kcap;
@@ -537,7 +592,7 @@ static int alloc_all(elp_handle* h) {
         if (e == hipSuccess) e = x;
     };
     // AR holds only the |Y| live rows: start small, grow at polls (ensure_ar)
-    h->ar_rows = std::min<int64_t>(mm, 1024);
+    h->ar_rows = std::min<int64_t>(mm, std::max<int64_t>(1024, ar_prev));
     if (const char* e = std::getenv("ELP_AR_INIT_ROWS"))  // test hook: force growth
         h->ar_rows = std::max<int64_t>(1, std::min<int64_t>(mm, std::atoll(e)));
     if (h->csc) h->ar_rows = 1;  // CSC prices from the columns: no AR
@@ -623,7 +678,7 @@ static int alloc_all(elp_handle* h) {
         free_dev(h);
         return fail(ELP_E_NOMEM, std::string("device allocation failed: ") + hipGetErrorString(e));
     }
-    A(hipHostMalloc((void**)&h->hctl, sizeof(DevCtl)));
+    if (!h->hctl) A(hipHostMalloc((void**)&h->hctl, sizeof(DevCtl)));
     // (AR padding columns [n, ldr) are read by the 128-column tiles but their
     //  results are discarded, so AR needs no clearing); Minv / work start clean
     A(hipMemsetAsync(d.rcnt, 0, (size_t)d.rregs * sizeof(int32_t), h->st));
