@@ -20,6 +20,8 @@
 #include <hip/hip_ext.h>
 #include <math.h>
 
+#include <type_traits>
+
 // The per-iteration kernels read Dev by value from the kernel arguments or,
 // with ELP_DEV_PTR 1, through a pointer to its device copy (Dev::self).  The
 // pointer form measured slower (r03: 38.3-38.9 against 36.8-37.3 us per C3
@@ -2566,9 +2568,13 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
     }
     // ---- pivot: bookkeeping, its stores split by destination over the four waves
     //      (a store chain per wave; stores to one address stay in one wave, in order)
-    if ((tid & 63) == 0) {  // thread 0 of each wave: the same decisions, a quarter of the stores
-        const int wv = tid >> 6;  // (0: counters / statuses / control block, 1: bump lists,
-                                  //  2: Y list and covers, 3: plan record and duals)
+    // (each wave's code specialised to its own stores -- wv is a compile-time
+    //  constant per instance, so a wave evaluates only what it writes: the
+    //  single-lane tail of the kernel is shorter)
+    auto book = [&](auto WVc) {
+        constexpr int wv = decltype(WVc)::value;  // (0: counters / statuses / control block,
+                                                  //  1: bump lists, 2: Y list and covers,
+                                                  //  3: plan record and duals)
         if (theta == 0.0) {
             if (wv == 0) { c->degenerate = cs_degen + 1; }
             if (wv == 0) { c->ndegen = cs_ndegen + 1; }
@@ -2753,6 +2759,14 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
         if (wv == 3) { c->plan = P; }
         if (wv == 0) { c->plan_seq = cs_seq + 1; }
         if (wv == 0) { if (defer) loop_top(P.pcase == PC_E && lrow != q - d.N ? ST_NUMFAIL : ST_RUN, cs_iter + 1, cs_since + 1); }
+        };
+    if ((tid & 63) == 0) {  // thread 0 of each wave: the same decisions, a quarter of the stores
+        switch (tid >> 6) {
+            case 0: book(std::integral_constant<int, 0>{}); break;
+            case 1: book(std::integral_constant<int, 1>{}); break;
+            case 2: book(std::integral_constant<int, 2>{}); break;
+            default: book(std::integral_constant<int, 3>{}); break;
+        }
     }
     RSTAMP(6);
 }
