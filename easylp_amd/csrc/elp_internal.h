@@ -84,7 +84,7 @@ struct DevCtl {
     // likewise the bookkeeping entries k_ratio's dual update reads (k_ftran_zr's
     // snapshot workgroup): |Y|, rpos / ypos of the entering slack's row, the
     // last Y row and its bump position
-    int32_t snap_ny, snap_apos, snap_ypos0, snap_ylast, snap_rposyl;
+    int32_t snap_ny, snap_apos, snap_ypos0, snap_ylast, snap_pad;
     // the status k_ratio's workgroups act on: workgroup 0 may already have
     // written the next loop-top status (refactor / stop / cap) when another
     // workgroup of the same launch starts and reads the control block

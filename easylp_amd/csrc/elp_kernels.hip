@@ -1422,7 +1422,11 @@ DEV Cand local_best(const Dev& d, int ncand, Cand* red) {
     return block_best<1024>(best, bland, red);
 }
 
-DEV void entering_chosen(const Dev& d, const Cand& best) {
+// the statistics of this iteration's pricing pass and of the whole iteration:
+// read-modify-writes of control-block fields, so the thread that runs them
+// waits a round trip -- kept off the select kernel's critical path (after its
+// own bump rows)
+DEV void entering_stats(const Dev& d) {
     DevCtl* c = d.ctl;
     const int ny = c->ny;
     // algorithmic bytes of this pricing pass: AR sweep + c + status + y_Y + Yl
@@ -1433,6 +1437,9 @@ DEV void entering_chosen(const Dev& d, const Cand& best) {
     // 8k^2 + 16n, deferred update 32k^2 + 16m
     const double kk = (double)c->k, mm = (double)d.m, nn = (double)d.n;
     c->iter_bytes += pb + 48.0 * kk * kk + 8.0 * mm * kk + 16.0 * nn + 16.0 * mm;
+}
+DEV void entering_chosen(const Dev& d, const Cand& best) {
+    DevCtl* c = d.ctl;
     c->q = (int)best.j;
     c->dq = best.d;
     c->wq = best.w;
@@ -1466,7 +1473,10 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles, int nsw) {
         return;
     }
     const int q = (int)best.j;
-    if (threadIdx.x == 0) entering_chosen(d, best);
+    if (threadIdx.x == 0) {
+        entering_chosen(d, best);
+        entering_stats(d);
+    }
     if (ELP_DIAG && d.ptimer) price_timer_sum<1024>(d, reinterpret_cast<unsigned long long*>(red));
     if (d.csc) {  // dense copy of the entering column + a_R through rpos
         scatter_qcol_csc(d, q);
@@ -1629,7 +1639,11 @@ __global__ void __launch_bounds__(256) k_select_ftran(DEV_PARAM, int ntiles, int
         }
     }
     __syncthreads();
-    if (pr >= k) return;
+    const bool stats_here = blockIdx.x == 0 && tid == 0;
+    if (pr >= k) {
+        if (stats_here) entering_stats(d);
+        return;
+    }
     double acc = 0.0;
     if (pfm) {
 #pragma unroll
@@ -1647,6 +1661,7 @@ __global__ void __launch_bounds__(256) k_select_ftran(DEV_PARAM, int ntiles, int
         a2 = wave_tree(a2);
         if (lane == 0) d.alS[p2] = a2;
     }
+    if (stats_here) entering_stats(d);
     RSTAMP(15);
 }
 
@@ -1712,7 +1727,10 @@ __global__ void __launch_bounds__(256) k_select_global(Dev d) {
     } else {
         for (int i = threadIdx.x; i < m + 4; i += 256) d.pkt[i] = 0.0;
     }
-    if (threadIdx.x == 0) entering_chosen(d, best);
+    if (threadIdx.x == 0) {
+        entering_chosen(d, best);
+        entering_stats(d);
+    }
 }
 
 // after the all-reduce of pkt: a_R from the exchanged column
@@ -1747,6 +1765,7 @@ __global__ void __launch_bounds__(256) k_select_xftran(Dev d) {
         d.pkt[m + 2] = x.x;
         d.pkt[m + 3] = x.cost;
         entering_chosen(d, best);
+        entering_stats(d);
     }
     if (q < d.N) {
         const double* col = d.Afull + (size_t)q * (size_t)m;
@@ -1979,8 +1998,7 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(DEV_PARAM, int nrt, 
             cw->snap_ny = ny;
             cw->snap_apos = i0 >= 0 ? d.rpos[i0] : -1;
             cw->snap_ypos0 = i0 >= 0 ? d.ypos[i0] : -1;
-            cw->snap_ylast = yl;
-            cw->snap_rposyl = yl >= 0 ? d.rpos[yl] : -1;
+            cw->snap_ylast = yl;  // (rpos[yl]: k_ratio loads it itself, one round trip fewer here)
             const int ql = loc_of(d, q);
             const bool pk = ql < 0 || (d.sharded && q < d.N);  // from the exchanged packet
             const int m = d.m, last = k - 1;
@@ -2192,7 +2210,7 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
     const double sv_lbq = c->snap_lbq, sv_ubq = c->snap_ubq, sv_xq = c->snap_xq, sv_cq = c->snap_cq;
     const double sv_csl = c->snap_csl, sv_slol = c->snap_slol, sv_shil = c->snap_shil;
     const int sv_vsq = c->snap_vsq, sv_sllast = c->snap_sllast, sv_rllast = c->snap_rllast;
-    const int sv_ypos0 = c->snap_ypos0, sv_ylast = c->snap_ylast, sv_rposyl = c->snap_rposyl;
+    const int sv_ypos0 = c->snap_ypos0, sv_ylast = c->snap_ylast;
     // ---- loads that depend on neither the control block nor the decision go
     //      out next (bounded by the host's k_ub, masked by the real k below):
     //      the pass-1 minima, this wave's row of MinvT (B^-1 row, cases B / D)
@@ -2274,6 +2292,10 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
     const int rsafe = (rcol >= 0 && rcol < m) ? rcol : 0;
     const double yold = d.y[rsafe];
     const int ypos_r = d.ypos[rsafe];  // its Y slot (workgroup 0 rewrites no bump row's slot)
+    // rpos of the last Y row (the bookkeeping's moved-slot rule): read here, off
+    // the snapshot kernel's critical path, and consumed before the barrier
+    // below, ahead of the bookkeeping's own rpos stores
+    int sv_rposyl = d.rpos[sv_ylast >= 0 ? sv_ylast : 0];
     // ---- parallel prefetch of bookkeeping scalars
     const int ql = loc_of(d, q);  // -1: the entering column lives on another shard
     // case D needs wave_dot(MinvT[apos, :], A[lrow, S]) in every workgroup: wave 0
@@ -2327,6 +2349,8 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
     }
     best = wave_best_leave(best, bland);
     if ((tid & 63) == 0) lred[tid >> 6] = best;
+    if (sv_ylast < 0) sv_rposyl = -1;
+    asm volatile("" : "+v"(sv_rposyl));  // (waited for here, before any rpos store)
     __syncthreads();  // also publishes the prefetched scalars
     {
         int win = 0;
