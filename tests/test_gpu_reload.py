@@ -44,3 +44,33 @@ def test_reload_reuses_buffers(gpu, m):
                 from oracle import solve_dense as orc
                 o = orc(A, np.ones(m, np.int32), np.full(m, 10.0), c, up=up, maximize=True)
                 assert sol.objval == o.objval
+
+
+def test_reload_pool_alternating_inputs(gpu, monkeypatch):
+    """The reload pool (free_dev keeps the last load's buffers by size for the
+    next alloc_all): one handle loads dense LPs of one shape, a CSC LP and dense
+    again, with the bump and AR capacities forced to grow inside each solve
+    (grown buffers are never pooled) -- every pivot trace is the oracle's."""
+    import scipy.sparse as sp
+    from oracle import generate_dense, solve_dense as orc
+    monkeypatch.setenv("ELP_KCAP_INIT", "3")
+    monkeypatch.setenv("ELP_AR_INIT_ROWS", "4")
+    m, n = 120, 700
+    dirs = np.ones(m, np.int32)
+    with gpu.Problem(m, n) as p:
+        p.set_trace(100000)
+        for step, seed in enumerate((3, 4, 5, 6, 7)):
+            A, b, c = generate_dense(seed, m, n)
+            if step == 2:  # a CSC load between the dense ones
+                A = A * (np.random.default_rng(seed).random((m, n)) < 0.2)
+                S = sp.csc_matrix(A)
+                p.load_csc(S.indptr, S.indices, S.data, dirs, b, c, maximize=True)
+                o = orc(A, dirs, b, c, maximize=True, trace_cap=100000, price_mode=1)
+            else:
+                p.load_dense(A, dirs, b, c, maximize=True)
+                o = orc(A, dirs, b, c, maximize=True, trace_cap=100000)
+            g = p.solution(p.solve())
+            assert g.status == o.status == 0, step
+            assert g.stats["bump_dim"] > 3
+            np.testing.assert_array_equal(g.trace, o.trace)
+            assert g.objval == o.objval
