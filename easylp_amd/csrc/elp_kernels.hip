@@ -3549,7 +3549,15 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
 #ifndef ELP_NAR_MAX
 #define ELP_NAR_MAX 512
 #endif
-            nar = cdiv(d.n, 256);
+#ifndef ELP_NAR_COLS
+#define ELP_NAR_COLS 768
+#endif
+            // the AR-copy workgroups work only when Y changes, but every one of
+            // them prefetches and repeats the decision: 3 columns per thread
+            // (66 workgroups at n = 50 000, was 196 -- +1-2 % over the C3
+            // solve, r03 A/B) and at most 512 (n = 500 000, where a copy that
+            // long wants the parallelism)
+            nar = cdiv(d.n, ELP_NAR_COLS);
             if (nar > ELP_NAR_MAX) nar = ELP_NAR_MAX;
         }
         // (8 B^-1 values per lane in registers; for k > 512 the row is read in a
