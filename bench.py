@@ -10,8 +10,11 @@ A "step" is ONE FULL SOLVE: elp_load_dense_device (canonicalisation, the
 row-major copy of A, the Y-row copy, phase decision) + elp_solve to
 optimality, from A already resident in HBM -- what easylp$solve() does per
 call (R/class.R:260-278).  `value` = simplex iterations of the K timed solves /
-their wall time, i.e. the whole-solve iteration rate, and `time_to_optimal_s`
-= wall time per solve (load included, generation excluded).
+their wall time, i.e. the whole-solve iteration rate (A resident in HBM).
+`time_to_optimal_s` follows SURVEY.md 8d (H2D included, generation excluded):
+the best of three solves from A in host memory through elp_load_dense, the
+entry point the R glue calls (`host_input.c3`); the HBM-resident time per
+solve is `time_to_optimal_hbm_s`.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
@@ -55,6 +58,8 @@ def parse():
     ap.add_argument("--cpu-iters", type=int, default=0,
                     help="cap on the CPU oracle's iterations (0: one full solve, ~20 s)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--highs", type=int, default=1,
+                    help="N=1: SciPy HiGHS (highs-ds) CPU leg in a child process (cpu_baseline_highs)")
     ap.add_argument("--profile-price", type=int, default=1,
                     help="HIP events on the pricing dispatches of every 8th chunk (roofline)")
     ap.add_argument("--c4", type=int, default=1,
@@ -300,6 +305,91 @@ def cpu_baseline(args):
     }
 
 
+def highs_child(argv):
+    """`python bench.py --highs-child OUT M N SEED`: the second CPU stand-in of
+    SURVEY.md 8d -- SciPy's HiGHS dual simplex (linprog method="highs-ds",
+    presolve off), in its own process with OMP_NUM_THREADS=1 -- on the same LPs:
+    configs[1] (500 x 2000) to optimality, configs[2] (M x N) over 1 and 21
+    iterations (its set-up from the dense matrix alone takes over a minute, so
+    the rate is the 20 iterations between the two runs), and the phase-1
+    Netlib-scale sparse LP (kkt_20000x100000) to optimality.  Writes JSON to OUT."""
+    import numpy as np
+    import scipy
+    import scipy.sparse as sp
+    from scipy.optimize import linprog
+    from oracle import generate_dense
+    from easylp_amd.synth import sparse_kkt
+    out_path, m3, n3, seed = argv[0], int(argv[1]), int(argv[2]), int(argv[3])
+    res = {"solver": "SciPy %s HiGHS dual simplex (linprog highs-ds, presolve off, OMP_NUM_THREADS=1)"
+                     % scipy.__version__}
+
+    def run(Acsc, b, c, bounds, cap=None):
+        opts = {"presolve": False}
+        if cap:
+            opts["maxiter"] = cap
+        t = time.perf_counter()
+        r = linprog(-c, A_ub=Acsc, b_ub=b, bounds=bounds, method="highs-ds", options=opts)
+        return r, time.perf_counter() - t
+
+    A, b, c = generate_dense(seed, 500, 2000)
+    r, t = run(sp.csc_matrix(A), b, c, (0, None))
+    res["c2"] = {"workload": "dense LP m=500 n=2000 seed %d, to optimality" % seed, "status": int(r.status),
+                 "iterations": int(r.nit), "time_to_optimal_s": t, "value": r.nit / t, "unit": "iterations/s",
+                 "objective": -float(r.fun)}
+    fx = {f["name"]: f for f in json.load(open(os.path.join(ROOT, "tests", "golden", "sparse_lu.json")))}
+    k = fx["kkt_20000x100000"]
+    cp, ri, v, bk, ck, u, obj = sparse_kkt(k["seed"], k["m"], k["n"], k["k"])
+    r, t = run(sp.csc_matrix((v, ri, cp), shape=(k["m"], k["n"])), bk, ck, list(zip(np.zeros(k["n"]), u)))
+    res["kkt_20000x100000"] = {"workload": "sparse_kkt phase-1 LP m=20000 n=100000, to optimality",
+                               "status": int(r.status), "iterations": int(r.nit), "time_to_optimal_s": t,
+                               "value": r.nit / t, "unit": "iterations/s", "objective": -float(r.fun)}
+    with open(out_path, "w") as f:  # (what is there so far, should the long leg be cut)
+        json.dump(res, f)
+    A, b, c = generate_dense(seed, m3, n3)
+    Ac = sp.csc_matrix(A)
+    del A
+    r1, t1 = run(Ac, b, c, (0, None), cap=1)
+    r21, t21 = run(Ac, b, c, (0, None), cap=21)
+    it = int(r21.nit) - int(r1.nit)
+    res["c3"] = {"workload": "dense LP m=%d n=%d seed %d, capped" % (m3, n3, seed),
+                 "seconds_1_iteration": t1, "seconds_21_iterations": t21, "iterations": it,
+                 "value": it / (t21 - t1) if t21 > t1 and it > 0 else None, "unit": "iterations/s",
+                 "note": "set-up from the dense matrix (~%.0f s) excluded: rate over the iterations between "
+                         "the 1- and 21-iteration runs" % t1}
+    with open(out_path, "w") as f:
+        json.dump(res, f)
+
+
+class HighsLeg:
+    """The HiGHS child, started when the timed region is over (one CPU core, in
+    parallel with the remaining GPU legs), collected at the end."""
+
+    def __init__(self, args):
+        import tempfile
+        self.path = os.path.join(tempfile.mkdtemp(prefix="elp_highs_"), "highs.json")
+        env = dict(os.environ, OMP_NUM_THREADS="1", ELP_NO_TORCH="1")
+        self.proc = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--highs-child", self.path,
+                                      str(args.m), str(args.n), str(args.seed)], env=env,
+                                     stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+
+    def result(self, timeout):
+        try:
+            _, err = self.proc.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            self.proc.kill()
+            self.proc.communicate()
+            err = b"timed out"
+        try:
+            r = json.load(open(self.path))
+        except (OSError, ValueError):
+            return {"error": (err or b"").decode(errors="replace")[-400:]}
+        if self.proc.returncode:
+            r["error"] = "incomplete (exit %s): %s" % (self.proc.returncode, (err or b"")[-200:].decode(errors="replace"))
+        model, ncpu = host_info()
+        r.update({"cores": 1, "kind": "port", "host": {"cpu": model, "nproc": ncpu}})
+        return r
+
+
 def committed_traffic(args):
     """HBM traffic per pricing launch from the committed rocprofv3 --pmc
     FETCH_SIZE pass of this same command (tools/gpu_check.sh ->
@@ -521,6 +611,8 @@ def sparse_rate(args, local, with_cpu):
 
 
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--highs-child":
+        return highs_child(sys.argv[2:])
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.mode == "procs" and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -607,6 +699,7 @@ def main():
                   "price_avg_launch_us": wr["avg_launch_us"]}
 
     traffic, traffic_src = committed_traffic(args) if max(world, ctx.ngpu) == 1 else (None, None)
+    highs = HighsLeg(args) if rank == 0 and max(world, ctx.ngpu) == 1 and args.highs and not args.no_cpu else None
 
     other = None  # the same LP to optimality under the other pricing rule
     if args.compare_rules and max(world, ctx.ngpu) == 1 and not args.force_sharded:
@@ -644,6 +737,21 @@ def main():
     if args.sparse and max(world, ctx.ngpu) == 1:
         sparse = sparse_rate(args, local, rank == 0 and not args.no_cpu)
 
+    highs_res = highs.result(timeout=400) if highs is not None else None
+    # time to optimal includes the H2D copy of A (what .Call pays:
+    # elp_load_dense from host memory); the HBM-resident figure stays beside it
+    tto_hbm = elapsed / max(args.steps, 1)
+    from_host = bool(hosted and hosted.get("c3"))
+    tto = hosted["c3"]["best"]["time_to_optimal_s"] if from_host else tto_hbm
+    amdahl = None
+    if max(world, ctx.ngpu) > 1 and window:  # (the first multi-GPU record explains itself)
+        sweep_us = window.get("price_avg_launch_us")
+        amdahl = {"us_per_iteration": window["us_per_iteration"], "per_rank_sweep_us": sweep_us,
+                  "replicated_chain_us": (window["us_per_iteration"] - sweep_us) if sweep_us else None,
+                  "exchange": last.get("exchange"), "exchange_rtt_us": last.get("exchange_rtt_us"),
+                  "note": "steady-state window [100, 1100) on rank 0: the sweep from HIP events on its pricing "
+                          "dispatches, the chain = the rest of the iteration (select, FTRAN-z, ratio test, "
+                          "exchange); exchange_rtt_us: one all-rank mailbox round measured by the set-up probe"}
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -667,7 +775,10 @@ def main():
                 "iterations_timed": iters,
                 "pricing": args.pricing,
             },
-            "time_to_optimal_s": elapsed / max(args.steps, 1),
+            "time_to_optimal_s": tto,
+            "time_to_optimal_source": "host_input.c3.best (elp_load_dense from host memory, H2D included)"
+                                      if from_host else "the timed solves (A resident in HBM)",
+            "time_to_optimal_hbm_s": tto_hbm,
             "final": final,
             "steady_state": window,
             "other_pricing": other,
@@ -681,6 +792,8 @@ def main():
             "iteration_roofline": iteration_roofline(stats),
             "host_input": hosted,
             "cpu_baseline": cpu,
+            "cpu_baseline_highs": highs_res,
+            "amdahl": amdahl,
             "scaling_config": c4,
             "sparse_config": sparse,
         }

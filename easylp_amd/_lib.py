@@ -19,7 +19,8 @@ ELP_PROFILE_EVENTS = 4  # HIP events on every pricing dispatch
 ELP_PROFILE_SAMPLE = 8  # ... on those of every 8th chunk between host polls
 ELP_SCALE_GEOMETRIC, ELP_SCALE_EQUILIBRATE = 4, 64
 ELP_BASIS_AUTO, ELP_BASIS_INVERSE, ELP_BASIS_LU = 0, 1, 2
-ABI_VERSION = 4
+ABI_VERSION = 5
+ELP_SIMPLEX_PRIMAL_PRIMAL, ELP_SIMPLEX_DUAL_PRIMAL = 5, 6
 
 # every entry point the header declares (checked by tests/test_abi.py)
 EXPORTS = (
@@ -62,7 +63,7 @@ class ElpControl(ctypes.Structure):
         ("tol_singular", ctypes.c_double),
         ("mailbox_timeout", ctypes.c_double),
         ("basis", ctypes.c_int32),
-        ("reserved2", ctypes.c_int32),
+        ("simplex", ctypes.c_int32),
     ]
 
 
@@ -100,7 +101,9 @@ class ElpStats(ctypes.Structure):
         ("lu_nnz", ctypes.c_int64),
         ("eta_nnz", ctypes.c_int64),
         ("basis", ctypes.c_int32),
-        ("reserved2", ctypes.c_int32),
+        ("simplex", ctypes.c_int32),
+        ("exchange_rtt_us", ctypes.c_double),
+        ("dual_iterations", ctypes.c_int64),
     ]
 
 
@@ -142,7 +145,7 @@ def _one_runtime() -> None:
         return  # a runtime is already there: bind to it
     try:
         import torch  # noqa: F401
-    except ImportError:
+    except Exception:  # (absent, or its bundled ROCm libraries failed: /opt/rocm's runtime then)
         pass
 
 

@@ -132,7 +132,8 @@ struct elp_handle {
     std::vector<int32_t> srow_h, scol_h;
     // sparse-LU engine (elp_control.basis, CSC input): host copy of the scaled
     // CSC (the refactor builds B from it), artificial signs, the last factors,
-    // the device descriptor and its buffers (grown as needed, kept across loads)
+    // the device descriptor and its buffers (grown as needed within a load, freed by
+    // every load: free_dev)
     int64_t kcap = 0;  // bump capacity: AS m x kcap, Minv / MinvT kcap x kcap (grown at polls)
     bool lu = false;
     LuDev ld{};
@@ -308,8 +309,17 @@ static hipError_t take_or_alloc(double** p, size_t bytes, double** keep, size_t*
 // devices than P, e.g. a one-GPU box) use the in-process ThreadGroup.
 static bool is_group(const elp_handle* h) { return h && !h->ranks.empty(); }
 
+// collective = false: the call issues no collective (elp_set_int, elp_set_trace,
+// elp_sensitivity), so a failing rank never strands a peer and nothing is aborted.
+// Otherwise a rank failure releases the peers that wait in a collective: the
+// in-process transport fails its waiters at once (and is reset at the next
+// call); RCCL communicators (distinct devices) are aborted -- for good: later
+// calls fail ELP_E_STATE -- only when a peer is still running a grace period
+// after the failure, i.e. actually waiting for the failed rank (a uniform
+// argument / state error returns on every rank before any collective, and
+// leaves the handle usable: ADVICE r03).
 template <class F>
-static int fan_out(elp_handle* g, F&& f) {
+static int fan_out(elp_handle* g, F&& f, bool collective = true) {
     if (g->broken)
         return fail(ELP_E_STATE, "ngpu handle: a rank failed earlier and the communicators were aborted; "
                                  "destroy the handle");
@@ -318,27 +328,42 @@ static int fan_out(elp_handle* g, F&& f) {
     std::vector<int> rc(P, 0);
     std::vector<std::string> err(P);
     std::atomic<int> first{-1};
+    std::mutex mu;
+    std::condition_variable cv;
+    int running = P;
     auto run = [&](int r) {
         rc[r] = f(g->ranks[r], r);
         if (rc[r] < 0) {
             err[r] = g_err;
             int none = -1;
             first.compare_exchange_strong(none, r);
-            // release the ranks waiting in a collective: the in-process transport
-            // fails its waiters; distinct devices abort every RCCL communicator
-            // (the handle is unusable afterwards: later calls fail ELP_E_STATE)
-            if (g->tgroup) {
-                g->tgroup->abort();
-            } else if (none < 0) {
-                for (elp_handle* rh : g->ranks) rh->comm.abort_rccl();
-                g->broken = true;
-            }
+            if (collective && g->tgroup) g->tgroup->abort();
         }
+        std::lock_guard<std::mutex> lk(mu);
+        --running;
+        cv.notify_all();
     };
     std::vector<std::thread> th;
     th.reserve((size_t)P);
     for (int r = 1; r < P; ++r) th.emplace_back(run, r);
     run(0);
+    if (collective && !g->tgroup) {
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            if (running == 0) break;
+            if (first.load() < 0) {
+                cv.wait(lk);
+                continue;
+            }
+            // a rank failed: give the others the mailbox timeout to return on their own
+            const double grace = std::max(1.0, g->ctl.mailbox_timeout);
+            if (cv.wait_for(lk, std::chrono::duration<double>(grace), [&] { return running == 0; })) break;
+            lk.unlock();
+            for (elp_handle* rh : g->ranks) rh->comm.abort_rccl();
+            g->broken = true;
+            break;
+        }
+    }
     for (auto& t : th) t.join();
     const int r = first.load();
     if (r >= 0) return fail(rc[r], "rank " + std::to_string(r) + ": " + err[r]);
@@ -395,8 +420,8 @@ static void enable_group_p2p(elp_handle* g) {
     for (int r = 0; r < P && ok; ++r) {
         ok = hipSetDevice(g->rank_dev[r]) == hipSuccess &&
              hipExtMallocWithFlags(&mb[r], bytes, hipDeviceMallocUncached) == hipSuccess &&
-             hipMemset(mb[r], 0, bytes) == hipSuccess && hipMalloc((void**)&dok[r], sizeof(int32_t)) == hipSuccess &&
-             hipMemset(dok[r], 0, sizeof(int32_t)) == hipSuccess;
+             hipMemset(mb[r], 0, bytes) == hipSuccess && hipMalloc((void**)&dok[r], 2 * sizeof(int32_t)) == hipSuccess &&
+             hipMemset(dok[r], 0, 2 * sizeof(int32_t)) == hipSuccess;
     }
     for (int r = 0; r < P && ok; ++r) {
         ok = hipSetDevice(g->rank_dev[r]) == hipSuccess && hipMalloc((void**)&dp[r], sizeof(void*) * P) == hipSuccess &&
@@ -412,11 +437,12 @@ static void enable_group_p2p(elp_handle* g) {
                  launch_mbox_probe((void* const*)dp[r], mb[r], P, r, (int64_t)rec, dok[r],
                                    (unsigned long long)(secs * 1e8), g->ranks[r]->st) == hipSuccess;
         for (int r = 0; r < launched; ++r) {  // every launched probe drains (bounded by its limit)
-            int32_t v = 0;
+            int32_t v[2] = {0, 0};
             const bool got = hipSetDevice(g->rank_dev[r]) == hipSuccess &&
                              hipStreamSynchronize(g->ranks[r]->st) == hipSuccess &&
-                             hipMemcpy(&v, dok[r], sizeof(v), hipMemcpyDeviceToHost) == hipSuccess;
-            ok = ok && got && v == 1;
+                             hipMemcpy(v, dok[r], sizeof(v), hipMemcpyDeviceToHost) == hipSuccess;
+            ok = ok && got && v[0] == 1;
+            if (got && v[0] == 1) g->ranks[r]->comm.rtt_us = mbox_rtt_us(v[1]);
         }
     }
     for (int r = 0; r < P; ++r) {
@@ -2195,7 +2221,7 @@ static int lu_run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
 }
 
 extern "C" int elp_set_int(elp_handle* h, const int32_t* is_int) {
-    if (is_group(h)) return fan_out(h, [&](elp_handle* r, int) { return elp_set_int(r, is_int); });
+    if (is_group(h)) return fan_out(h, [&](elp_handle* r, int) { return elp_set_int(r, is_int); }, false);
     if (!h || !h->loaded) return fail(ELP_E_STATE, "elp_set_int: no problem loaded");
     h->is_int.clear();
     if (is_int) {
@@ -2350,6 +2376,7 @@ static int run_bnb(elp_handle* h, int32_t* out_status) {
 extern "C" int elp_solve(elp_handle* h, int32_t* lp_status) {
     if (!h || !lp_status) return fail(ELP_E_ARG, "elp_solve: NULL argument");
     if (is_group(h)) {
+        if (!h->ranks[0]->loaded) return fail(ELP_E_STATE, "elp_solve: no problem loaded");
         std::vector<int32_t> st(h->ranks.size(), 0);
         const int rc = fan_out(h, [&](elp_handle* r, int k) { return elp_solve(r, &st[k]); });
         *lp_status = st[0];
@@ -2371,6 +2398,7 @@ extern "C" int elp_solve(elp_handle* h, int32_t* lp_status) {
 extern "C" int elp_iterate(elp_handle* h, int64_t iters, int32_t* lp_status) {
     if (!h || !lp_status || iters < 0) return fail(ELP_E_ARG, "elp_iterate: bad argument");
     if (is_group(h)) {
+        if (!h->ranks[0]->loaded) return fail(ELP_E_STATE, "elp_iterate: no problem loaded");
         std::vector<int32_t> st(h->ranks.size(), 0);
         const int rc = fan_out(h, [&](elp_handle* r, int k) { return elp_iterate(r, iters, &st[k]); });
         *lp_status = st[0];
@@ -2385,6 +2413,7 @@ extern "C" int elp_iterate(elp_handle* h, int64_t iters, int32_t* lp_status) {
 }
 
 extern "C" int elp_get_solution(elp_handle* h, double* objval, double* x, double* y, int64_t* basis) {
+    if (is_group(h) && !h->ranks[0]->loaded) return fail(ELP_E_STATE, "elp_get_solution: no problem loaded");
     if (is_group(h))  // (collective: every rank takes part, rank 0 reports)
         return fan_out(h, [&](elp_handle* r, int k) {
             return k == 0 ? elp_get_solution(r, objval, x, y, basis)
@@ -2464,26 +2493,30 @@ extern "C" int elp_get_solution(elp_handle* h, double* objval, double* x, double
 // basis: the reduced costs and the two MFMA contractions run on the device
 // (launch_sensitivity), the per-variable assembly here mirrors
 // oracle/elp_oracle.c sensitivity() line by line.
-extern "C" int elp_sensitivity(elp_handle* h, double* objfrom, double* objtill, double* duals,
-                               double* dualsfrom, double* dualstill) {
-    if (is_group(h)) return fail(ELP_E_UNSUPPORTED, "elp_sensitivity: column-sharded solves (ngpu > 1)");
-    if (!h || !h->loaded) return fail(ELP_E_STATE, "elp_sensitivity: no problem loaded");
-    if (!h->done || h->final_status != ELP_OPTIMAL)
-        return fail(ELP_E_STATE, "elp_sensitivity: problem is not optimal");
-    if (h->comm.kind != 0) return fail(ELP_E_UNSUPPORTED, "elp_sensitivity: column-sharded solves");
-    if (h->lu)
-        return fail(ELP_E_UNSUPPORTED, "elp_sensitivity: the sparse-LU basis (load with elp_control.basis = "
-                                       "ELP_BASIS_INVERSE for a sensitivity report)");
-    if (h->mip || !h->is_int.empty())  // R/class.R:617-618, :634-635
-        return fail(ELP_E_STATE, "Sensitivity unavailable for problems with integer/binary variables");
+//
+// Column-sharded handles (ngpu > 1): every rank runs the same
+// launch on its own shard -- reduced costs and the objective-ranging product
+// alpha_p. = Minv A[R, shard] over its columns, the rhs ranging (replicated
+// A[:, S] Minv) in full -- and the host merges: the interval of a basic
+// structural's cost is the intersection of the ranks' intervals (max of the
+// lower, min of the upper limits: the same values the single-GPU reduction
+// takes, in any order), the per-column entries come from the owning rank.
+struct SensPart {
+    int64_t col0 = 0, ncols = 0;  // this rank's structurals
+    int k = 0;
+    std::vector<double> dr, o4, cost, lb, ub, xr, y, b;
+    std::vector<int8_t> vs;  // ncols structurals, then m slacks
+    std::vector<int32_t> Sl, cover, rpos;
+};
+
+static int sens_part(elp_handle* h, SensPart& sp) {
     HIPCHK(hipSetDevice(h->dev));
     HIPCHK(hipMemcpyAsync(h->hctl, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
     HIPCHK(hipStreamSynchronize(h->st));
     const Dev& d = h->d;
-    const int64_t m = h->m, n = h->n;
+    const int64_t m = h->m, n = d.n;  // (n: this shard's columns)
     const int k = h->hctl->k;
     const int64_t ntc = (n + 63) / 64, ntr = (m + 63) / 64;
-    const double INF = HUGE_VAL, BIG = h->ctl.infinity;
     double *dred = nullptr, *TR = nullptr, *plo = nullptr, *phi = nullptr, *qlo = nullptr,
            *qhi = nullptr, *out4 = nullptr;
     auto release = [&]() {
@@ -2498,71 +2531,103 @@ extern "C" int elp_sensitivity(elp_handle* h, double* objfrom, double* objtill, 
         return fail(ELP_E_NOMEM, "elp_sensitivity: work allocation failed");
     }
     hipError_t e = launch_sensitivity(d, k, dred, TR, plo, phi, qlo, qhi, out4, h->st);
-    std::vector<double> dr(n), o4(4 * (size_t)k), cost(n), lb(n), ub(n), xr(m), y(m), b(m);
-    std::vector<int8_t> vs(n + m);
-    std::vector<int32_t> Sl(k), Rl(k), cover(m), rpos(m);
+    sp.col0 = h->col0;
+    sp.ncols = n;
+    sp.k = k;
+    sp.dr.resize(n);
+    sp.o4.resize(4 * (size_t)k);
+    sp.cost.resize(n);
+    sp.lb.resize(n);
+    sp.ub.resize(n);
+    sp.xr.resize(m);
+    sp.y.resize(m);
+    sp.b.resize(m);
+    sp.vs.resize(n + m);
+    sp.Sl.resize(k);
+    sp.cover.resize(m);
+    sp.rpos.resize(m);
     auto d2h = [&](void* dst, const void* src, size_t bytes) {
         if (e == hipSuccess && bytes) e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->st);
     };
-    d2h(dr.data(), dred, n * sizeof(double));
-    d2h(o4.data(), out4, 4 * (size_t)k * sizeof(double));
-    d2h(cost.data(), d.cost, n * sizeof(double));
-    d2h(lb.data(), d.lb, n * sizeof(double));
-    d2h(ub.data(), d.ub, n * sizeof(double));
-    d2h(vs.data(), d.vstat, (n + m) * sizeof(int8_t));
-    d2h(Sl.data(), d.Sl, k * sizeof(int32_t));
-    d2h(Rl.data(), d.Rl, k * sizeof(int32_t));
-    d2h(cover.data(), d.cover, m * sizeof(int32_t));
-    d2h(rpos.data(), d.rpos, m * sizeof(int32_t));
-    d2h(xr.data(), d.xr, m * sizeof(double));
-    d2h(y.data(), d.y, m * sizeof(double));
-    d2h(b.data(), d.b, m * sizeof(double));
+    d2h(sp.dr.data(), dred, n * sizeof(double));
+    d2h(sp.o4.data(), out4, 4 * (size_t)k * sizeof(double));
+    d2h(sp.cost.data(), d.cost, n * sizeof(double));
+    d2h(sp.lb.data(), d.lb, n * sizeof(double));
+    d2h(sp.ub.data(), d.ub, n * sizeof(double));
+    d2h(sp.vs.data(), d.vstat, (n + m) * sizeof(int8_t));
+    d2h(sp.Sl.data(), d.Sl, k * sizeof(int32_t));
+    d2h(sp.cover.data(), d.cover, m * sizeof(int32_t));
+    d2h(sp.rpos.data(), d.rpos, m * sizeof(int32_t));
+    d2h(sp.xr.data(), d.xr, m * sizeof(double));
+    d2h(sp.y.data(), d.y, m * sizeof(double));
+    d2h(sp.b.data(), d.b, m * sizeof(double));
     if (e == hipSuccess) e = hipStreamSynchronize(h->st);
     release();
     if (e != hipSuccess) return fail(ELP_E_HIP, std::string("elp_sensitivity: ") + hipGetErrorString(e));
+    return 0;
+}
+
+// h: a handle of the solve (rank 0 of a group: scaling, rows, sense are replicated)
+static void sens_assemble(const elp_handle* h, const std::vector<SensPart>& parts, double* objfrom,
+                          double* objtill, double* duals, double* dualsfrom, double* dualstill) {
+    const SensPart& p0 = parts[0];
+    const int64_t m = h->m, n = h->n;
+    const int k = p0.k;
+    const double INF = HUGE_VAL, BIG = h->ctl.infinity;
     auto clip = [&](double v) { return v <= -INF ? -BIG : v >= INF ? BIG : v; };
     const bool mx = h->maximize != 0;
     const double sg = mx ? -1.0 : 1.0;
-    // (the assembly runs on the scaled problem; every output is unscaled)
-    if (duals) {
-        for (int64_t i = 0; i < m; ++i) duals[i] = unscale_row(h, sg * y[i], i, 1);
-        for (int64_t j = 0; j < n; ++j) duals[m + j] = unscale_col(h, sg * dr[j], j, -1);
-    }
-    std::vector<int> spos(n, -1);
-    for (int p = 0; p < k; ++p) spos[Sl[p]] = p;
-    for (int64_t j = 0; j < n && (objfrom || objtill); ++j) {
-        double lo = -INF, hi = INF;
-        const double c = cost[j];
-        if (vs[j] == VS_BASIC) {
-            const int p = spos[j];
-            lo = c + o4[p];
-            hi = c + o4[k + p];
-        } else if (lb[j] == ub[j]) {
-        } else if (vs[j] == VS_LOWER) {
-            lo = c - dr[j];
-        } else if (vs[j] == VS_UPPER) {
-            hi = c - dr[j];
-        } else {
-            lo = hi = c;
+    // objective-ranging intervals of the basic structurals: intersection over shards
+    std::vector<double> olo(p0.o4.begin(), p0.o4.begin() + k), ohi(p0.o4.begin() + k, p0.o4.begin() + 2 * k);
+    for (size_t r = 1; r < parts.size(); ++r)
+        for (int p = 0; p < k; ++p) {
+            olo[p] = std::fmax(olo[p], parts[r].o4[p]);
+            ohi[p] = std::fmin(ohi[p], parts[r].o4[k + p]);
         }
-        if (objfrom) objfrom[j] = clip(unscale_col(h, mx ? -hi : lo, j, -1));
-        if (objtill) objtill[j] = clip(unscale_col(h, mx ? -lo : hi, j, -1));
-    }
+    std::vector<int> spos((size_t)n, -1);
+    for (int p = 0; p < k; ++p) spos[(size_t)p0.Sl[p]] = p;  // (Sl holds global ids)
+    // (the assembly runs on the scaled problem; every output is unscaled)
+    if (duals)
+        for (int64_t i = 0; i < m; ++i) duals[i] = unscale_row(h, sg * p0.y[i], i, 1);
+    for (const SensPart& sp : parts)
+        for (int64_t jj = 0; jj < sp.ncols; ++jj) {
+            const int64_t j = sp.col0 + jj;
+            const double dr = sp.dr[jj];
+            if (duals) duals[m + j] = unscale_col(h, sg * dr, j, -1);
+            if (!objfrom && !objtill) continue;
+            double lo = -INF, hi = INF;
+            const double c = sp.cost[jj];
+            const int8_t vs = sp.vs[jj];
+            if (vs == VS_BASIC) {
+                const int p = spos[j];
+                lo = c + olo[p];
+                hi = c + ohi[p];
+            } else if (sp.lb[jj] == sp.ub[jj]) {
+            } else if (vs == VS_LOWER) {
+                lo = c - dr;
+            } else if (vs == VS_UPPER) {
+                hi = c - dr;
+            } else {
+                lo = hi = c;
+            }
+            if (objfrom) objfrom[j] = clip(unscale_col(h, mx ? -hi : lo, j, -1));
+            if (objtill) objtill[j] = clip(unscale_col(h, mx ? -lo : hi, j, -1));
+        }
     for (int64_t i = 0; i < m && (dualsfrom || dualstill); ++i) {
         double lo = -INF, hi = INF;
-        const double bi = b[i];
-        const int u = cover[i];
+        const double bi = p0.b[i];
+        const int u = p0.cover[i];
         if (u == (int)(n + i)) {
-            const double act = bi - xr[i];
+            const double act = bi - p0.xr[i];
             if (h->dir_h[i] == ELP_LE) lo = act;
             else if (h->dir_h[i] == ELP_GE) hi = act;
             else lo = hi = bi;
         } else if (u >= (int)(n + m)) {
             lo = hi = bi;
         } else {
-            const int c = rpos[i];
-            lo = bi + o4[2 * (size_t)k + c];
-            hi = bi + o4[3 * (size_t)k + c];
+            const int c = p0.rpos[i];
+            lo = bi + p0.o4[2 * (size_t)k + c];
+            hi = bi + p0.o4[3 * (size_t)k + c];
         }
         if (dualsfrom) dualsfrom[i] = clip(unscale_row(h, lo, i, -1));
         if (dualstill) dualstill[i] = clip(unscale_row(h, hi, i, -1));
@@ -2571,6 +2636,43 @@ extern "C" int elp_sensitivity(elp_handle* h, double* objfrom, double* objtill, 
         if (dualsfrom) dualsfrom[m + j] = -BIG;
         if (dualstill) dualstill[m + j] = BIG;
     }
+}
+
+// the state checks of a rank handle (every rank of a group holds the same)
+static int sens_check(elp_handle* h) {
+    if (!h || !h->loaded) return fail(ELP_E_STATE, "elp_sensitivity: no problem loaded");
+    if (!h->done || h->final_status != ELP_OPTIMAL)
+        return fail(ELP_E_STATE, "elp_sensitivity: problem is not optimal");
+    if (h->lu)
+        return fail(ELP_E_UNSUPPORTED, "elp_sensitivity: the sparse-LU basis (load with elp_control.basis = "
+                                       "ELP_BASIS_INVERSE for a sensitivity report)");
+    if (h->mip || !h->is_int.empty())  // R/class.R:617-618, :634-635
+        return fail(ELP_E_STATE, "Sensitivity unavailable for problems with integer/binary variables");
+    return 0;
+}
+
+extern "C" int elp_sensitivity(elp_handle* h, double* objfrom, double* objtill, double* duals,
+                               double* dualsfrom, double* dualstill) {
+    if (is_group(h)) {
+        // (no collective: the ranks' reports meet in this process's memory)
+        for (elp_handle* r : h->ranks) {
+            const int rc = sens_check(r);
+            if (rc) return rc;
+        }
+        std::vector<SensPart> parts(h->ranks.size());
+        const int rc = fan_out(h, [&](elp_handle* r, int k) { return sens_part(r, parts[(size_t)k]); }, false);
+        if (rc) return rc;
+        sens_assemble(h->ranks[0], parts, objfrom, objtill, duals, dualsfrom, dualstill);
+        return 0;
+    }
+    const int rc0 = sens_check(h);
+    if (rc0) return rc0;
+    if (h->comm.kind != 0)
+        return fail(ELP_E_UNSUPPORTED, "elp_sensitivity: multi-process column-sharded solves (use elp_control.ngpu)");
+    std::vector<SensPart> parts(1);
+    const int rc = sens_part(h, parts[0]);
+    if (rc) return rc;
+    sens_assemble(h, parts, objfrom, objtill, duals, dualsfrom, dualstill);
     return 0;
 }
 
@@ -2592,6 +2694,7 @@ extern "C" int elp_get_stats(elp_handle* h, elp_stats* st) {
         h->stats.mip_lp_iterations = h->mip ? h->mip_iters : 0;
         h->stats.price_bytes = c.price_bytes;
         h->stats.iter_bytes = c.iter_bytes;
+        h->stats.exchange_rtt_us = h->comm.p2p ? h->comm.rtt_us : 0.0;
         if (h->lu) {  // basic structurals, factor and eta-file sizes
             std::vector<int32_t> head((size_t)std::max<int64_t>(h->m, 1));
             if (h->m) {
@@ -2618,7 +2721,7 @@ extern "C" int elp_get_stats(elp_handle* h, elp_stats* st) {
 
 extern "C" int elp_set_trace(elp_handle* h, int64_t capacity) {
     if (is_group(h) && capacity >= 0)
-        return fan_out(h, [&](elp_handle* r, int) { return elp_set_trace(r, capacity); });
+        return fan_out(h, [&](elp_handle* r, int) { return elp_set_trace(r, capacity); }, false);
     if (!h || capacity < 0) return fail(ELP_E_ARG, "elp_set_trace: bad argument");
     if (h->loaded) return fail(ELP_E_STATE, "elp_set_trace: call before elp_load_*");
     h->trace_cap = capacity;

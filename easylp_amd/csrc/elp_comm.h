@@ -10,6 +10,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <mutex>
 #include <vector>
@@ -72,11 +73,15 @@ struct Comm {
     // pointers after hipDeviceEnablePeerAccess, no IPC) and proved the round
     // trip; the communicator takes ownership of both
     void adopt_p2p(void* mine, void** dpeers_dev);
-    // ngpu on distinct devices: a rank failed while its peers may wait inside an
+    double rtt_us = 0.0;  // the probe's measured exchange round (k_mbox_probe), 0 when none
+    // ngpu on distinct devices: a rank failed while its peers wait inside an
     // RCCL collective -- ncclCommAbort releases them; the communicator is then
-    // unusable (every later collective fails)
+    // unusable (every later collective fails).  Called from another rank's
+    // thread: `aborted` is atomic and every collective tests it before it
+    // touches `nccl`, which abort_rccl never clears (the handle stays valid to
+    // read; RCCL fails the calls on an aborted communicator)
     void abort_rccl();
-    bool aborted = false;
+    std::atomic<bool> aborted{false};
 
     static int unique_id(uint8_t id[128]);
     int init_rccl(const uint8_t id[128], int world_size, int rank_);
@@ -96,9 +101,12 @@ struct Comm {
 
 // Mailbox round-trip probe (k_mbox_probe): thread t stores the reserved
 // sequence word into this rank's slots of peers[t]'s mailbox and waits (ticks
-// of the 100 MHz clock at most) for rank t's word in `mine`; *ok = 1 when all
-// arrived.  Every rank's probe must be in flight at the same time.
+// of the 100 MHz clock at most) for rank t's word in `mine`; ok[0] = 1 when all
+// arrived, ok[1] = 100 MHz ticks of MBOX_ROUNDS timed exchange rounds after it
+// (mbox_rtt_us: microseconds per round).  Every rank's probe must be in flight
+// at the same time; ok holds 2 ints.
 hipError_t launch_mbox_probe(void* const* dpeers, void* mine, int P, int rank, int64_t rec_bytes, int32_t* ok,
                              unsigned long long ticks, hipStream_t st);
+double mbox_rtt_us(int32_t ticks);
 
 }  // namespace elp

@@ -160,38 +160,57 @@ int Comm::init_host(int world_size, int rank_, elp_host_allgather_fn ag, elp_hos
 // sequence word into this rank's slots (both parities) of rank t's mailbox,
 // then waits (the mailbox timeout at most) for rank t's word in its own.  Proves, before the
 // first solve, that remote stores land and become visible to the polling
-// loads (p2p_exchange's protocol); the reserved word can never equal a real
-// iteration's sequence (epoch << 40 | iteration + 1).
+// loads (p2p_exchange's protocol); the reserved words can never equal a real
+// iteration's sequence (epoch << 40 | iteration + 1).  Then MBOX_ROUNDS
+// exchange rounds of the solver's shape (store this round's word into every
+// peer's slot of the round's parity, wait for every peer's): ok_out[1] = the
+// 100 MHz ticks they took on thread 0, i.e. the per-iteration cost of the
+// exchange with every kernel already running.
 constexpr int64_t MBOX_PROBE_SEQ = INT64_MAX;
+constexpr int MBOX_ROUNDS = 64;
 __global__ void k_mbox_probe(void* const* peers, void* mine, int P, int rank, int64_t rec, int* ok_out,
                              unsigned long long ticks) {
     __shared__ int fail;
     const int t = threadIdx.x;
     if (t == 0) fail = 0;
     __syncthreads();
-    if (t < P) {
-        __threadfence_system();
-        for (int par = 0; par < 2; ++par) {
-            int64_t* s = reinterpret_cast<int64_t*>(static_cast<char*>(peers[t]) + (par * P + rank) * rec + rec - 8);
-            __hip_atomic_store(s, MBOX_PROBE_SEQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
-    __syncthreads();
-    if (t < P) {
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        for (int par = 0; par < 2; ++par) {
-            int64_t* s = reinterpret_cast<int64_t*>(static_cast<char*>(mine) + (par * P + t) * rec + rec - 8);
-            while (__hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != MBOX_PROBE_SEQ) {
-                __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {  // 100 MHz clock
-                    atomicOr(&fail, 1);
-                    break;
-                }
+    auto slot = [&](void* base, int par, int r) {
+        return reinterpret_cast<int64_t*>(static_cast<char*>(base) + (par * P + r) * rec + rec - 8);
+    };
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    auto wait_for = [&](int64_t* s, int64_t want) {
+        while (__hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != want) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {  // 100 MHz clock
+                atomicOr(&fail, 1);
+                return;
             }
         }
+    };
+    if (t < P) {
+        __threadfence_system();
+        for (int par = 0; par < 2; ++par)
+            __hip_atomic_store(slot(peers[t], par, rank), MBOX_PROBE_SEQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __syncthreads();
-    if (t == 0) *ok_out = fail ? 0 : 1;
+    if (t < P)
+        for (int par = 0; par < 2; ++par) wait_for(slot(mine, par, t), MBOX_PROBE_SEQ);
+    __syncthreads();
+    unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+    for (int r = 1; r <= MBOX_ROUNDS && !fail; ++r) {
+        const int par = r & 1;
+        const int64_t want = MBOX_PROBE_SEQ - r;
+        if (t < P) {
+            __threadfence_system();
+            __hip_atomic_store(slot(peers[t], par, rank), want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            wait_for(slot(mine, par, t), want);
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        ok_out[0] = fail ? 0 : 1;
+        ok_out[1] = fail ? 0 : (int)(__builtin_amdgcn_s_memrealtime() - r0);
+    }
 }
 
 hipError_t launch_mbox_probe(void* const* dpeers, void* mine, int P, int rank, int64_t rec_bytes, int32_t* ok,
@@ -200,6 +219,8 @@ hipError_t launch_mbox_probe(void* const* dpeers, void* mine, int P, int rank, i
     return hipGetLastError();
 }
 
+double mbox_rtt_us(int32_t ticks) { return ticks > 0 ? 10.0 * 1e-3 * (double)ticks / MBOX_ROUNDS : 0.0; }
+
 void Comm::adopt_p2p(void* mine, void** dpeers_dev) {
     mbox = mine;
     dpeers = dpeers_dev;
@@ -207,11 +228,8 @@ void Comm::adopt_p2p(void* mine, void** dpeers_dev) {
 }
 
 void Comm::abort_rccl() {
-    if (kind == 1 && nccl && !aborted) {
-        (void)ncclCommAbort((ncclComm_t)nccl);
-        nccl = nullptr;
-        aborted = true;
-    }
+    bool expect = false;
+    if (kind == 1 && nccl && aborted.compare_exchange_strong(expect, true)) (void)ncclCommAbort((ncclComm_t)nccl);
 }
 
 // Collective over the communicator: every rank takes every step (the handle
@@ -265,13 +283,15 @@ int Comm::enable_p2p(size_t rec_bytes, hipStream_t st, double timeout_s) {
     // not leaves its peers' probes to time out: they fail the agreement too)
     if (!rc && ok) {
         int32_t* dok = reinterpret_cast<int32_t*>(dstage);
-        int32_t hok = 0;
+        int32_t hok[2] = {0, 0};
         const double secs = timeout_s > 0 ? timeout_s : 2.0;
         if (launch_mbox_probe((void* const*)dpeers, mbox, world, rank, (int64_t)rec_bytes, dok,
                               (unsigned long long)(secs * 1e8), st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess ||
-            hipMemcpy(&hok, dok, sizeof(hok), hipMemcpyDeviceToHost) != hipSuccess || !hok)
+            hipMemcpy(hok, dok, sizeof(hok), hipMemcpyDeviceToHost) != hipSuccess || !hok[0])
             ok = 0;
+        else
+            rtt_us = mbox_rtt_us(hok[1]);
     }
     // agreement: max over ranks of "failed"
     int32_t failed = rc || !ok;

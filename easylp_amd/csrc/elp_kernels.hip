@@ -3586,7 +3586,9 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
         // + the timer workgroup, + the CSC column-scatter workgroup
         unsigned nrw = cdiv(k_ub > 0 ? k_ub : 1, 4);
         if (d.sel_cap > 0 && nrw > (unsigned)d.sel_cap) nrw = (unsigned)d.sel_cap;
-        const unsigned nqz = d.qz && !d.csc ? cdiv(d.m, 256 * QZ_PT) : 0;
+        // (ranks sharing a device, sel_cap > 0: no staging workgroups -- they would
+        //  spin on the mailbox beside the capped bump rows; FTRAN-z reads the column)
+        const unsigned nqz = d.qz && !d.csc && d.sel_cap == 0 ? cdiv(d.m, 256 * QZ_PT) : 0;
         const unsigned g = nrw + nqz + (d.ptimer ? 1 : 0) + (d.csc ? 1 : 0);
         // Minv row values per lane in registers: 8 (k <= 512), 10 (k <= 640: the
         // last 4 000 iterations of 10 000 x 500 000, k 529; 16 measured no faster

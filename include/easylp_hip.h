@@ -25,9 +25,10 @@
 extern "C" {
 #endif
 
-#define ELP_ABI_VERSION 4  /* 3: elp_stats.iter_bytes appended; 4: elp_control.exchange /
+#define ELP_ABI_VERSION 5  /* 3: elp_stats.iter_bytes appended; 4: elp_control.exchange /
                              basis, elp_load_dense_device_multi, elp_stats.exchange /
-                             h2d_bytes / lu_nnz / eta_nnz / basis */
+                             h2d_bytes / lu_nnz / eta_nnz / basis; 5: elp_control.simplex,
+                             elp_stats.exchange_rtt_us / dual_iterations / simplex */
 
 /* row directions, mirroring R/class.R:272 ("==" -> "=") and the "<"/">"
  * spellings accepted by R/methods.R:215-219 */
@@ -119,8 +120,16 @@ typedef struct elp_control {
                                 product-form eta file, O(nnz(L+U) + etas) device
                                 memory (the role LUSOL plays for lp_solve);
                                 latency-bound on the GPU */
-    int32_t reserved2;
+    int32_t simplex;         /* lp.control(simplextype = ...), lp_solve's
+                                set_simplextype numbering: ELP_SIMPLEX_DUAL_PRIMAL
+                                (6) -- phase 1 by the dual simplex when the slack
+                                basis is primal infeasible, phase 2 primal;
+                                ELP_SIMPLEX_PRIMAL_PRIMAL (5) -- phase 1 primal on
+                                artificials.  0: the default    */
 } elp_control;
+
+#define ELP_SIMPLEX_PRIMAL_PRIMAL 5  /* elp_control.simplex (lp_solve's SIMPLEX_*) */
+#define ELP_SIMPLEX_DUAL_PRIMAL 6
 
 #define ELP_BASIS_AUTO 0     /* elp_control.basis */
 #define ELP_BASIS_INVERSE 1
@@ -176,7 +185,12 @@ typedef struct elp_stats {
     int64_t eta_nnz;           /* ELP_BASIS_LU: largest eta-file nonzeros      */
     int32_t basis;             /* the representation the last load used
                                   (ELP_BASIS_INVERSE or ELP_BASIS_LU)           */
-    int32_t reserved2;
+    int32_t simplex;           /* the phase-1 method the last solve ran
+                                  (ELP_SIMPLEX_DUAL_PRIMAL / _PRIMAL_PRIMAL)    */
+    double exchange_rtt_us;    /* peer mailbox (exchange 1): one exchange round
+                                  between all ranks, measured by the set-up
+                                  probe with every rank's kernel running        */
+    int64_t dual_iterations;   /* iterations of the dual simplex (phase 1)     */
 } elp_stats;
 
 #define ELP_PROFILE_PRICE 2   /* elp_control.verbose bit: device-clock pricing timer */
@@ -266,7 +280,9 @@ int elp_get_stats(elp_handle* h, elp_stats* st);
 
 /* get.sensitivity.obj / get.sensitivity.rhs             R/class.R:613-646
  * Sensitivity report of the final basis of an OPTIMAL solve (ELP_E_STATE
- * otherwise, as R's stop("Problem is not optimal"); one GPU only).  Any output
+ * otherwise, as R's stop("Problem is not optimal"); one GPU or an ngpu handle --
+ * each rank ranges its own columns, the report is the one-GPU report bit for
+ * bit; ELP_E_UNSUPPORTED after elp_comm_init*).  Any output
  * may be NULL.  objfrom[n] / objtill[n]: range of each objective coefficient
  * over which the basis stays optimal; duals[m+n]: constraint duals then reduced
  * costs (user sense); dualsfrom / dualstill[m+n]: range of each constraint's rhs

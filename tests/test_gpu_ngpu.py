@@ -106,10 +106,55 @@ def test_ngpu_mip_and_refusals(gpu):
     with gpu.Problem(2, 2, ngpu=2) as p:
         with pytest.raises(ElpError, match="owns its communicator"):
             p.comm_init(bytes(128), 2, 0)
+        with pytest.raises(ElpError, match="no problem loaded"):
+            p.solve()  # a uniform state error: no rank waits, the handle stays usable
+        with pytest.raises(ElpError, match="no problem loaded"):
+            p.set_int([1, 1])  # (every rank fails alike; nothing is aborted)
         p.load_dense(np.eye(2), [1, 1], [1.0, 1.0], [1.0, 1.0], maximize=True)
         assert p.solve() == 0
-        with pytest.raises(ElpError, match="ngpu"):
-            p.sensitivity()
+        p.set_int([1, 1])
+        assert p.solve() == 0
+        with pytest.raises(ElpError, match="integer"):
+            p.sensitivity()  # R/class.R:617-618
+
+
+def _sens_equal(g, o, exact=False):
+    """ngpu reports against the single-GPU / oracle reports: +-1e30 exactly,
+    finite entries to 1e-9 (or bit for bit against one GPU)."""
+    for key in ("objfrom", "objtill", "duals", "dualsfrom", "dualstill"):
+        a, b = np.asarray(g[key]), np.asarray(o[key])
+        if exact:
+            np.testing.assert_array_equal(a, b, err_msg=key)
+            continue
+        ia, ib = np.abs(a) >= 1e30, np.abs(b) >= 1e30
+        np.testing.assert_array_equal(ia, ib, err_msg=key)
+        np.testing.assert_array_equal(a[ia], b[ib], err_msg=key)
+        scale = max(1.0, float(np.abs(b[~ib]).max(initial=0.0)))
+        np.testing.assert_allclose(a[~ia], b[~ib], rtol=1e-9, atol=1e-9 * scale, err_msg=key)
+
+
+@pytest.mark.parametrize("ngpu,replicate", [(2, 1), (3, 1), (2, 2), (3, 2)])
+def test_ngpu_sensitivity(gpu, ngpu, replicate):
+    """get.sensitivity.obj / .rhs (R/class.R:613-646) after a
+    column-sharded solve -- each rank ranges its own columns, the host merges --
+    equal to the oracle's report to 1e-9 (+-1e30 exactly) and to the
+    single-GPU report bit for bit; a dense generated LP and a general LP (free
+    / boxed columns, >= and == rows, phase 1)."""
+    from oracle import generate_dense, solve_dense as orc
+    m, n, seed = 120, 700, 3
+    A, b, c = generate_dense(seed, m, n)
+    d = np.ones(m, np.int32)
+    cases = [(A, d, b, c, None, None, True), _general_lp() + (True,)]
+    for (A_, d_, r_, c_, lo_, up_, mx) in cases:
+        o = orc(A_, d_, r_, c_, lo_, up_, mx, sens=True)
+        one = gpu.solve_dense(A_, d_, r_, c_, lo_, up_, maximize=mx, sensitivity=True)
+        g = gpu.solve_dense(A_, d_, r_, c_, lo_, up_, maximize=mx, sensitivity=True, ngpu=ngpu,
+                            replicate=replicate)
+        assert g.status == one.status == o.status == 0
+        assert g.stats["world_size"] == ngpu
+        np.testing.assert_array_equal(g.basis, o.basis)
+        _sens_equal(g.sens, o.sens)
+        _sens_equal(g.sens, one.sens, exact=True)
 
 
 @pytest.mark.parametrize("replicate", [1, 2])
