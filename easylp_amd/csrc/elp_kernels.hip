@@ -972,11 +972,14 @@ DEV void tile_apply(const Dev& d, int64_t tile, int64_t ntiles) {
 // tiles'), and the deferred update of the last pivot is applied by waves 1..3
 // of every tile once their sweep is done (phase 2; nothing the sweep reads)
 // instead of by trailing workgroups that started only as tiles retired.
+// napply > 0 (A/B switch ELP_TRAIL_APPLY=1, r02's layout): the plan is applied
+// by napply trailing workgroups instead (apply = 0 then)
 template <int NTL>
-DEV void price_body(const Dev& d, int nsw, int apply) {
+DEV void price_body(const Dev& d, int nsw, int apply, int napply, int nb_minv) {
     __shared__ double part[PRICE_SPLIT][TILE_COLS];
     __shared__ Cand red[PRICE_SPLIT];
     const int64_t ntiles = d.ntiles;
+    if (napply > 0 && apply_role(d, napply, nb_minv)) return;
     if ((int)blockIdx.x < nsw) {
         PDBG(1, 2ull);
         PDBG(2, 0ull);
@@ -1176,10 +1179,10 @@ DEV void pstamp_end(const Dev& d) {
 }
 
 template <int NTL>
-__global__ void __launch_bounds__(PRICE_THREADS) k_price(DEV_PARAM, int nsw, int apply) {
+__global__ void __launch_bounds__(PRICE_THREADS) k_price(DEV_PARAM, int nsw, int apply, int napply, int nb_minv) {
     DEV_BIND
     pstamp_begin<PRICE_THREADS>(d);
-    price_body<NTL>(d, nsw, apply);
+    price_body<NTL>(d, nsw, apply, napply, nb_minv);
     pstamp_end(d);
 }
 
@@ -3470,10 +3473,19 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phas
 #define ELP_APPLY_PT 4
 #endif
     if (phase == 2 && d.csc) update_grid(d, k_ub, false, &nb_minv, &napply, TILE_COLS, ELP_APPLY_PT);
+    // ELP_TRAIL_APPLY=1 (A/B): the dense deferred plan in
+    // trailing workgroups of the launch (r02) instead of the tiles' waves 1-3
+    static const bool trail = [] {
+        const char* e = std::getenv("ELP_TRAIL_APPLY");
+        return e && std::atoi(e) == 1;
+    }();
+    unsigned dnapply = 0, dnb_minv = 0;
+    if (phase == 2 && !d.csc && trail) update_grid(d, k_ub, false, &dnb_minv, &dnapply, PRICE_THREADS, ELP_APPLY_PT);
+    const int dapply = phase == 2 && !trail ? 1 : 0;
     // + nsw: the slack workgroups (candidates [ntiles, ntiles + nsw)); the dense
     // sweep applies the deferred plan inside its tiles (price_body)
     const int nsw = slack_wgs(d, ny_ub);
-    const unsigned grid = (d.csc ? ntiles + napply : (unsigned)d.ntiles) + nsw;
+    const unsigned grid = (d.csc ? ntiles + napply : (unsigned)d.ntiles + dnapply) + nsw;
     const bool nt = !d.csc && sweep_nt(8.0 * (double)ny_ub * (double)d.n);
     if (ev0) {
         // profiling (ELP_PROFILE_EVENTS): events bound to the dispatch itself
@@ -3484,15 +3496,15 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phas
                                   (int)nb_minv, nsw);
         else if (nt)
             hipExtLaunchKernelGGL(k_price<1>, dim3(grid), dim3(PRICE_THREADS), 0, st, ev0, ev1, 0, DEV_ARG(d), nsw,
-                                  phase == 2 ? 1 : 0);
+                                  dapply, (int)dnapply, (int)dnb_minv);
         else
             hipExtLaunchKernelGGL(k_price<0>, dim3(grid), dim3(PRICE_THREADS), 0, st, ev0, ev1, 0, DEV_ARG(d), nsw,
-                                  phase == 2 ? 1 : 0);
+                                  dapply, (int)dnapply, (int)dnb_minv);
         return hipGetLastError();
     }
     if (d.csc) k_price_csc<<<grid, TILE_COLS, 0, st>>>(d, (int)napply, (int)nb_minv, nsw);
-    else if (nt) k_price<1><<<grid, PRICE_THREADS, 0, st>>>(DEV_ARG(d), nsw, phase == 2 ? 1 : 0);
-    else k_price<0><<<grid, PRICE_THREADS, 0, st>>>(DEV_ARG(d), nsw, phase == 2 ? 1 : 0);
+    else if (nt) k_price<1><<<grid, PRICE_THREADS, 0, st>>>(DEV_ARG(d), nsw, dapply, (int)dnapply, (int)dnb_minv);
+    else k_price<0><<<grid, PRICE_THREADS, 0, st>>>(DEV_ARG(d), nsw, dapply, (int)dnapply, (int)dnb_minv);
     return hipGetLastError();
 }
 

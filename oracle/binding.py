@@ -36,6 +36,8 @@ class OrcControl(ctypes.Structure):
         ("price_rule", ctypes.c_int32),
         ("scaling", ctypes.c_int32),
         ("tol_singular", ctypes.c_double),
+        ("simplex", ctypes.c_int32),
+        ("pad0", ctypes.c_int32),
     ]
 
 
@@ -56,6 +58,8 @@ class OrcStats(ctypes.Structure):
         ("max_inv_resid", ctypes.c_double),
         ("lu_nnz", ctypes.c_int64),
         ("eta_nnz", ctypes.c_int64),
+        ("dual_iterations", ctypes.c_int64),
+        ("flattened", ctypes.c_int64),
     ]
 
 

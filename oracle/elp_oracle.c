@@ -145,6 +145,14 @@ typedef struct {
                            of each structural and slack (n + m)            */
     int64_t* nzl;       /* n: nz_nonbasic list                              */
     double* colbuf;     /* m: a generated column (Acol)                     */
+    /* dual simplex (run_dual): the pivot row's class partials, rho_r dense
+     * (m) and on the Y slots, the pass's reduced costs / pivot row (n + m) */
+    double *apart, *rho, *rhoY, *dvec, *avec;
+    /* its bound-flipping ratio test: candidate id, exact ratio, Harris bound,
+     * |alpha|, u - l (inf: not boxed), alive; the flipped ids; a_F, B^-1 a_F */
+    int64_t *cj, *flips;
+    double *ct, *cb, *ca, *cr, *aF, *fS;
+    int8_t* calive;
 } orc_t;
 
 /* v * 2^(sgn * exponent) of column j / row i (scaling; exact, inf stays inf) */
@@ -434,7 +442,7 @@ static int refactor(orc_t* s) {
 /* ------------------------------------------------------------------ */
 /* one phase of the simplex                                           */
 /* ------------------------------------------------------------------ */
-enum { PH_OPTIMAL = 0, PH_UNBOUNDED = 3, PH_NUMFAIL = 5, PH_ITERCAP = 1, PH_P1DONE = 10 };
+enum { PH_OPTIMAL = 0, PH_UNBOUNDED = 3, PH_NUMFAIL = 5, PH_ITERCAP = 1, PH_P1DONE = 10, PH_INFEAS = 2 };
 
 /* phase-1 infeasibility sum, in wave order (one 64-lane wave on the GPU) */
 static double art_sum(const orc_t* s) {
@@ -463,6 +471,158 @@ static inline int basic_entry(const orc_t* s, int64_t e, double sig, int64_t* va
         *x = s->xs[p];
     }
     return 1;
+}
+
+/* y = B^-T c_B: covered rows take their unit variable's cost, the R rows
+ * y_R = Minv' t with t_p = c_{S_p} - A[:,S_p]' y_cov (phase 1; y_cov = 0 in
+ * phase 2 and in the dual, whose unit variables are the zero-cost slacks) */
+static void btran(orc_t* s, int phase) {
+    const int64_t m = s->m, k = s->k;
+    for (int64_t i = 0; i < m; ++i) {
+        const int64_t u = s->cover[i];
+        s->y[i] = u >= 0 ? unit_sign(s, u) * s->cost[u] : 0.0;
+    }
+    /* wave order over all m rows with y = 0 on uncovered rows */
+    if (phase == 1) {
+        for (int64_t p = 0; p < k; ++p)
+            s->t[p] = s->cost[s->Sl[p]] - wave_dot(m, Acol(s, s->Sl[p], s->colbuf), s->y);
+    } else {
+        for (int64_t p = 0; p < k; ++p) s->t[p] = s->cost[s->Sl[p]];
+    }
+    /* y_R = Minv' t: one wave per p over row p of Minv^T */
+    for (int64_t p = 0; p < k; ++p) {
+        for (int64_t q = 0; q < k; ++q) s->tmp[q] = *MI(s, q, p);
+        s->yR[p] = wave_dot(k, s->tmp, s->t);
+    }
+    for (int64_t p = 0; p < k; ++p) s->y[s->Rl[p]] = s->yR[p];
+}
+
+/* Basis change after a pivot: entering q (now basic, value xq), leaving lv
+ * (covered row lrow or bump position lpos); cases A-E of the header, the
+ * bump inverse update, and -- phase 2 -- the dual update y += theta_d rho_r
+ * with theta_d = dq / alpha_rq (run_phase and run_dual share it).  Returns
+ * -1 on a numerical failure (case E off its row, AR growth). */
+static int basis_change(orc_t* s, int phase, int64_t q, int64_t lv, int64_t lrow, int64_t lpos, double dq,
+                        double xq) {
+    const int64_t m = s->m, n = s->n, k = s->k;
+    const int leave_art = lv >= n + m;
+    /* ---- basis change ---- */
+    if (q < n) {
+        if (lpos >= 0) {
+            /* case A: structural replaces structural at bump position lpos */
+            const int64_t p = lpos;
+            const double piv = s->alS[p];
+            for (int64_t j = 0; j < k; ++j) s->v[j] = *MI(s, p, j) / piv;
+            if (phase == 2) /* dual update: rho_r = Minv row p, theta_d = dq / piv */
+                for (int64_t j = 0; j < k; ++j) s->y[s->Rl[j]] = fma(dq, s->v[j], s->y[s->Rl[j]]);
+            for (int64_t i = 0; i < k; ++i) {
+                if (i == p) continue;
+                const double wi = s->alS[i];
+                for (int64_t j = 0; j < k; ++j) *MI(s, i, j) = fma(-wi, s->v[j], *MI(s, i, j));
+            }
+            for (int64_t j = 0; j < k; ++j) *MI(s, p, j) = s->v[j];
+            s->spos[lv] = -1;
+            s->Sl[p] = q;
+            s->spos[q] = p;
+            s->xs[p] = xq;
+        } else {
+            /* case B: structural enters, unit var of row lrow leaves; bump grows */
+            const int64_t i = lrow;
+            const double delta = s->acol[i] - s->z[i];
+            row_times_minv(s, i, s->v);
+            for (int64_t c = 0; c < k; ++c) s->v[c] = s->v[c] / delta;
+            if (phase == 2) { /* dual update: row i joins R with y_i = dq / delta */
+                for (int64_t c = 0; c < k; ++c) s->y[s->Rl[c]] = fma(-dq, s->v[c], s->y[s->Rl[c]]);
+                s->y[i] = dq / delta;
+            }
+            for (int64_t a = 0; a < k; ++a) {
+                const double wa = s->alS[a];
+                for (int64_t c = 0; c < k; ++c) *MI(s, a, c) = fma(wa, s->v[c], *MI(s, a, c));
+            }
+            for (int64_t a = 0; a < k; ++a) *MI(s, a, k) = -(s->alS[a] / delta);
+            for (int64_t c = 0; c < k; ++c) *MI(s, k, c) = -s->v[c];
+            *MI(s, k, k) = 1.0 / delta;
+            s->Rl[k] = i;
+            s->rpos[i] = k;
+            s->Sl[k] = q;
+            s->spos[q] = k;
+            s->xs[k] = xq;
+            s->cover[i] = -1;
+            s->k = k + 1;
+            if (!leave_art && y_append(s, i)) return -1;
+        }
+    } else {
+        const int64_t i0 = q - n;
+        const int64_t a = s->rpos[i0];
+        if (a < 0) {
+            /* case E: slack replaces the artificial covering the same row */
+            if (lrow != i0) return -1;
+            s->cover[i0] = q;
+            s->xr[i0] = xq;
+        } else if (lpos >= 0) {
+            /* case C: slack of row i0 (in R) enters, structural at lpos leaves */
+            const int64_t b = lpos, last = k - 1;
+            const double piv = *MI(s, b, a);
+            for (int64_t c = 0; c < k; ++c) s->v[c] = *MI(s, b, c) / piv;
+            if (phase == 2) { /* dual update; row i0 leaves R (y = 0) */
+                for (int64_t c = 0; c < k; ++c)
+                    if (c != a) s->y[s->Rl[c]] = fma(dq, s->v[c], s->y[s->Rl[c]]);
+                s->y[i0] = 0.0;
+            }
+            for (int64_t r = 0; r < k; ++r) {
+                if (r == b) continue;
+                const double f = *MI(s, r, a);
+                for (int64_t c = 0; c < k; ++c)
+                    if (c != a) *MI(s, r, c) = fma(-f, s->v[c], *MI(s, r, c));
+            }
+            if (b != last) {
+                for (int64_t c = 0; c < k; ++c) *MI(s, b, c) = *MI(s, last, c);
+                s->Sl[b] = s->Sl[last];
+                s->spos[s->Sl[b]] = b;
+                s->xs[b] = s->xs[last];
+            }
+            if (a != last) {
+                for (int64_t r = 0; r < k; ++r) *MI(s, r, a) = *MI(s, r, last);
+                s->Rl[a] = s->Rl[last];
+                s->rpos[s->Rl[a]] = a;
+            }
+            s->spos[lv] = -1;
+            s->rpos[i0] = -1;
+            s->cover[i0] = q;
+            s->xr[i0] = xq;
+            s->k = k - 1;
+        } else {
+            /* case D: slack of row i0 (in R) enters, unit var of row i1 leaves */
+            const int64_t i1 = lrow;
+            row_times_minv(s, i1, s->v);
+            const double piv = s->v[a];
+            if (phase == 2) { /* dual update; row i1 takes position a */
+                const double w = dq / piv;
+                for (int64_t c = 0; c < k; ++c)
+                    if (c != a) s->y[s->Rl[c]] = fma(w, s->v[c], s->y[s->Rl[c]]);
+                s->y[i0] = 0.0;
+                s->y[i1] = -w;
+            }
+            for (int64_t r = 0; r < k; ++r) s->t[r] = *MI(s, r, a) / piv;
+            for (int64_t r = 0; r < k; ++r) {
+                const double f = s->t[r];
+                for (int64_t c = 0; c < k; ++c)
+                    if (c != a) *MI(s, r, c) = fma(-f, s->v[c], *MI(s, r, c));
+                *MI(s, r, a) = f;
+            }
+            s->Rl[a] = i1;
+            s->rpos[i1] = a;
+            s->rpos[i0] = -1;
+            s->cover[i1] = -1;
+            s->cover[i0] = q;
+            s->xr[i0] = xq;
+        }
+        y_remove(s, i0);
+        if (a >= 0 && lpos < 0 && !leave_art) {
+            if (y_append(s, lrow)) return -1;
+        }
+    }
+    return 0;
 }
 
 static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter, int64_t max_iter,
@@ -511,25 +671,8 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
         const int64_t k = s->k;
         /* ---- BTRAN (phase 1: every iteration) ---- */
         if (phase == 1 || !y_valid) {
-        y_valid = 1;
-        for (int64_t i = 0; i < m; ++i) {
-            const int64_t u = s->cover[i];
-            s->y[i] = u >= 0 ? unit_sign(s, u) * s->cost[u] : 0.0;
-        }
-        /* t_p = c_{S_p} - A[:,S_p]' y_cov   (phase 1 only: y_cov = 0 in phase 2),
-         * wave order over all m rows with y = 0 on uncovered rows */
-        if (phase == 1) {
-            for (int64_t p = 0; p < k; ++p)
-                s->t[p] = s->cost[s->Sl[p]] - wave_dot(m, Acol(s, s->Sl[p], s->colbuf), s->y);
-        } else {
-            for (int64_t p = 0; p < k; ++p) s->t[p] = s->cost[s->Sl[p]];
-        }
-        /* y_R = Minv' t: one wave per p over row p of Minv^T */
-        for (int64_t p = 0; p < k; ++p) {
-            for (int64_t q = 0; q < k; ++q) s->tmp[q] = *MI(s, q, p);
-            s->yR[p] = wave_dot(k, s->tmp, s->t);
-        }
-        for (int64_t p = 0; p < k; ++p) s->y[s->Rl[p]] = s->yR[p];
+            y_valid = 1;
+            btran(s, phase);
         }
         /* ---- pricing over structurals (AR sweep) and slacks ---- */
         const int64_t ny = s->ny;
@@ -748,123 +891,342 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
             s->xval[lv] = at_lower ? s->lb[lv] : s->ub[lv];
         }
         s->vstat[q] = VS_BASIC;
-        /* ---- basis change ---- */
-        if (q < n) {
-            if (lpos >= 0) {
-                /* case A: structural replaces structural at bump position lpos */
-                const int64_t p = lpos;
-                const double piv = s->alS[p];
-                for (int64_t j = 0; j < k; ++j) s->v[j] = *MI(s, p, j) / piv;
-                if (phase == 2) /* dual update: rho_r = Minv row p, theta_d = dq / piv */
-                    for (int64_t j = 0; j < k; ++j) s->y[s->Rl[j]] = fma(dq, s->v[j], s->y[s->Rl[j]]);
-                for (int64_t i = 0; i < k; ++i) {
-                    if (i == p) continue;
-                    const double wi = s->alS[i];
-                    for (int64_t j = 0; j < k; ++j) *MI(s, i, j) = fma(-wi, s->v[j], *MI(s, i, j));
-                }
-                for (int64_t j = 0; j < k; ++j) *MI(s, p, j) = s->v[j];
-                s->spos[lv] = -1;
-                s->Sl[p] = q;
-                s->spos[q] = p;
-                s->xs[p] = xq;
-            } else {
-                /* case B: structural enters, unit var of row lrow leaves; bump grows */
-                const int64_t i = lrow;
-                const double delta = s->acol[i] - s->z[i];
-                row_times_minv(s, i, s->v);
-                for (int64_t c = 0; c < k; ++c) s->v[c] = s->v[c] / delta;
-                if (phase == 2) { /* dual update: row i joins R with y_i = dq / delta */
-                    for (int64_t c = 0; c < k; ++c) s->y[s->Rl[c]] = fma(-dq, s->v[c], s->y[s->Rl[c]]);
-                    s->y[i] = dq / delta;
-                }
-                for (int64_t a = 0; a < k; ++a) {
-                    const double wa = s->alS[a];
-                    for (int64_t c = 0; c < k; ++c) *MI(s, a, c) = fma(wa, s->v[c], *MI(s, a, c));
-                }
-                for (int64_t a = 0; a < k; ++a) *MI(s, a, k) = -(s->alS[a] / delta);
-                for (int64_t c = 0; c < k; ++c) *MI(s, k, c) = -s->v[c];
-                *MI(s, k, k) = 1.0 / delta;
-                s->Rl[k] = i;
-                s->rpos[i] = k;
-                s->Sl[k] = q;
-                s->spos[q] = k;
-                s->xs[k] = xq;
-                s->cover[i] = -1;
-                s->k = k + 1;
-                if (!leave_art && y_append(s, i)) return PH_NUMFAIL;
-            }
-        } else {
-            const int64_t i0 = q - n;
-            const int64_t a = s->rpos[i0];
-            if (a < 0) {
-                /* case E: slack replaces the artificial covering the same row */
-                if (lrow != i0) return PH_NUMFAIL;
-                s->cover[i0] = q;
-                s->xr[i0] = xq;
-            } else if (lpos >= 0) {
-                /* case C: slack of row i0 (in R) enters, structural at lpos leaves */
-                const int64_t b = lpos, last = k - 1;
-                const double piv = *MI(s, b, a);
-                for (int64_t c = 0; c < k; ++c) s->v[c] = *MI(s, b, c) / piv;
-                if (phase == 2) { /* dual update; row i0 leaves R (y = 0) */
-                    for (int64_t c = 0; c < k; ++c)
-                        if (c != a) s->y[s->Rl[c]] = fma(dq, s->v[c], s->y[s->Rl[c]]);
-                    s->y[i0] = 0.0;
-                }
-                for (int64_t r = 0; r < k; ++r) {
-                    if (r == b) continue;
-                    const double f = *MI(s, r, a);
-                    for (int64_t c = 0; c < k; ++c)
-                        if (c != a) *MI(s, r, c) = fma(-f, s->v[c], *MI(s, r, c));
-                }
-                if (b != last) {
-                    for (int64_t c = 0; c < k; ++c) *MI(s, b, c) = *MI(s, last, c);
-                    s->Sl[b] = s->Sl[last];
-                    s->spos[s->Sl[b]] = b;
-                    s->xs[b] = s->xs[last];
-                }
-                if (a != last) {
-                    for (int64_t r = 0; r < k; ++r) *MI(s, r, a) = *MI(s, r, last);
-                    s->Rl[a] = s->Rl[last];
-                    s->rpos[s->Rl[a]] = a;
-                }
-                s->spos[lv] = -1;
-                s->rpos[i0] = -1;
-                s->cover[i0] = q;
-                s->xr[i0] = xq;
-                s->k = k - 1;
-            } else {
-                /* case D: slack of row i0 (in R) enters, unit var of row i1 leaves */
-                const int64_t i1 = lrow;
-                row_times_minv(s, i1, s->v);
-                const double piv = s->v[a];
-                if (phase == 2) { /* dual update; row i1 takes position a */
-                    const double w = dq / piv;
-                    for (int64_t c = 0; c < k; ++c)
-                        if (c != a) s->y[s->Rl[c]] = fma(w, s->v[c], s->y[s->Rl[c]]);
-                    s->y[i0] = 0.0;
-                    s->y[i1] = -w;
-                }
-                for (int64_t r = 0; r < k; ++r) s->t[r] = *MI(s, r, a) / piv;
-                for (int64_t r = 0; r < k; ++r) {
-                    const double f = s->t[r];
-                    for (int64_t c = 0; c < k; ++c)
-                        if (c != a) *MI(s, r, c) = fma(-f, s->v[c], *MI(s, r, c));
-                    *MI(s, r, a) = f;
-                }
-                s->Rl[a] = i1;
-                s->rpos[i1] = a;
-                s->rpos[i0] = -1;
-                s->cover[i1] = -1;
-                s->cover[i0] = q;
-                s->xr[i0] = xq;
-            }
-            y_remove(s, i0);
-            if (a >= 0 && lpos < 0 && !leave_art) {
-                if (y_append(s, lrow)) return PH_NUMFAIL;
+        if (basis_change(s, phase, q, lv, lrow, lpos, dq, xq)) return PH_NUMFAIL;
+        since_refactor++;
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* dual simplex phase 1 (lp_solve's default SIMPLEX_DUAL_PRIMAL: the dual */
+/* simplex while the basis is primal infeasible, then the primal; reached */
+/* through R/class.R:262 lp.control and :276 solve).  lp_solve's own dual */
+/* loop is not in the reference (third-party, absent): this restatement   */
+/* defines the arithmetic and the HIP side reproduces it bit for bit.     */
+/*   start: the slack basis with every boxed column at the bound its cost */
+/*     sign makes dual feasible; a column that no bound makes dual        */
+/*     feasible (one-sided or free with the wrong-signed cost) has its    */
+/*     cost zeroed for the phase (solve_core);                            */
+/*   CHUZR: the basic variable most out of its bounds by delta^2 / w      */
+/*     (dual Devex reference weights w per basic variable, all 1 at the   */
+/*     start) or by delta (price_rule 0), lowest variable id on ties;     */
+/*   rho_r = row r of B^-1: Minv row p for bump position p; for the slack */
+/*     covering row i: sigma (e_i - (A[i,S] Minv) on R);                  */
+/*   pivot row alpha_j = rho_r' a_j and d_j = c_j - y' a_j in ONE sweep of */
+/*     the Y rows (the pricing order: PRICE_SPLIT slot classes), the       */
+/*     covered leaving row's own entry added last (fma(sigma, a_ij, .)); */
+/*     CSC (price_mode 1): one column chain each over the dense rho / y;  */
+/*   Harris dual ratio test: with s = +1 (x_r below its lower bound) or   */
+/*     -1 and ah = s alpha_j, columns at lower (or free with ah < 0) need */
+/*     ah < -tol_pivot and bound (d_j + tol_dual) / -ah, at upper (or     */
+/*     free with ah > 0) ah > tol_pivot and (tol_dual - d_j) / ah; pass 2 */
+/*     takes the largest |alpha_j| among exact ratios <= the minimum      */
+/*     bound, lowest id on ties (after degen_switch dual-degenerate       */
+/*     pivots: Bland -- the lowest infeasible variable, the smallest      */
+/*     exact ratio); no candidate: primal infeasible;                     */
+/*   FTRAN of a_q, primal step |x_r - beta_r| / |alpha_rq| (column value) */
+/*     in the entering direction, leaving variable to beta_r, then the    */
+/*     primal simplex's basis change and dual update y += (d_q/a_rq) rho; */
+/*   dual Devex: w_e = max(w_e, (alpha_eq / alpha_rq)^2 w_r) for the other */
+/*     basic entries, w_q = max(w_r / alpha_rq^2, 1); restart (all 1)     */
+/*     when w_q > DEVEX_RESET.                                            */
+/* Returns PH_P1DONE (primal feasible), PH_INFEAS, PH_ITERCAP, PH_NUMFAIL. */
+static int run_dual(orc_t* s, const orc_control* ctl, int64_t* iter, int64_t max_iter, int64_t* trace,
+                    int64_t trace_cap, orc_stats* st) {
+    const int64_t m = s->m, n = s->n;
+    const double ptol = ctl->tol_primal, dtol = ctl->tol_dual, pivtol = ctl->tol_pivot, INF = HUGE_VAL;
+    const int devex = ctl->price_rule == 1;
+    int64_t since_refactor = 0, ndegen = 0;
+    int bland = 0, recheck = 0;
+    for (int64_t j = 0; j < n + m; ++j) s->dw[j] = 1.0;
+    btran(s, 2);
+    for (;;) {
+        if (!recheck) {
+            if (*iter >= max_iter) return PH_ITERCAP;
+            if (since_refactor >= ctl->refactor_period) {
+                if (refactor(s)) return PH_NUMFAIL;
+                st->refactors++;
+                since_refactor = 0;
+                btran(s, 2);
             }
         }
-        since_refactor++;
+        recheck = 0;
+        const int64_t k = s->k;
+        /* ---- CHUZR ---- */
+        int64_t rv = -1, re = -1;
+        double rscore = 0.0, rx = 0.0, rbeta = 0.0;
+        int rs = 0;
+        for (int64_t e = 0; e < m + k; ++e) {
+            int64_t var;
+            double x;
+            if (e < m) {
+                if (s->cover[e] < 0) continue;
+                var = s->cover[e];
+                x = s->xr[e];
+            } else {
+                var = s->Sl[e - m];
+                x = s->xs[e - m];
+            }
+            const double l = s->lb[var], u = s->ub[var];
+            double delta, beta;
+            int sd;
+            if (x < l - ptol) {
+                delta = l - x;
+                beta = l;
+                sd = 1;
+            } else if (x > u + ptol) {
+                delta = x - u;
+                beta = u;
+                sd = -1;
+            } else {
+                continue;
+            }
+            const double score = devex ? (delta * delta) / s->dw[var] : delta;
+            int take;
+            if (rv < 0) take = 1;
+            else if (bland) take = var < rv;
+            else take = score > rscore || (score == rscore && var < rv);
+            if (take) {
+                rv = var;
+                re = e;
+                rscore = score;
+                rx = x;
+                rbeta = beta;
+                rs = sd;
+            }
+        }
+        if (rv < 0) {
+            if (since_refactor > 0) { /* updated values: confirm on a fresh x_B */
+                if (refactor(s)) return PH_NUMFAIL;
+                st->refactors++;
+                since_refactor = 0;
+                btran(s, 2);
+                recheck = 1;
+                continue;
+            }
+            return PH_P1DONE;
+        }
+        /* ---- rho_r on the R rows (position order) and the covered row ---- */
+        int64_t xrow = -1;
+        double xsig = 0.0;
+        if (re >= m) {
+            for (int64_t c = 0; c < k; ++c) s->v[c] = *MI(s, re - m, c);
+        } else {
+            xrow = re;
+            xsig = unit_sign(s, s->cover[re]);
+            row_times_minv(s, re, s->v);
+            for (int64_t c = 0; c < k; ++c) s->v[c] = -(xsig * s->v[c]);
+        }
+        for (int64_t i = 0; i < m; ++i) s->rho[i] = 0.0;
+        for (int64_t c = 0; c < k; ++c) s->rho[s->Rl[c]] = s->v[c];
+        if (xrow >= 0) s->rho[xrow] = xsig;
+        /* ---- one sweep: d_j (y) and alpha_j (rho) ---- */
+        const int64_t ny = s->ny;
+        for (int64_t p = 0; p < ny; ++p) {
+            s->yy[p] = s->y[s->Yl[p]];
+            s->rhoY[p] = s->rho[s->Yl[p]];
+        }
+        if (ctl->price_mode == 1) {
+            for (int64_t j = 0; j < n; ++j) {
+                const double* col = Acol(s, j, s->colbuf);
+                double ad = 0.0, aa = 0.0;
+                for (int64_t t = s->cp[j]; t < s->cp[j + 1]; ++t) { /* ascending rows */
+                    ad = fma(col[s->ri[t]], s->y[s->ri[t]], ad);
+                    aa = fma(col[s->ri[t]], s->rho[s->ri[t]], aa);
+                }
+                s->dvec[j] = s->cost[j] - ad;
+                s->avec[j] = aa;
+            }
+            st->price_bytes += 12.0 * (double)s->nnz + 17.0 * (double)n;
+        } else {
+            for (int w = 0; w < PRICE_SPLIT; ++w) {
+                double* pw = s->part + (size_t)w * (size_t)n;
+                double* qw = s->apart + (size_t)w * (size_t)n;
+                for (int64_t j = 0; j < n; ++j) pw[j] = qw[j] = 0.0;
+                for (int64_t p = w; p < ny; p += PRICE_SPLIT) {
+                    const double yp = s->yy[p], rp = s->rhoY[p];
+                    const double* row = s->AR + (size_t)p * (size_t)n;
+                    for (int64_t j = 0; j < n; ++j) {
+                        pw[j] = fma(row[j], yp, pw[j]);
+                        qw[j] = fma(row[j], rp, qw[j]);
+                    }
+                }
+            }
+            for (int64_t j = 0; j < n; ++j) {
+                double td = 0.0, ta = 0.0;
+                for (int w = 0; w < PRICE_SPLIT; ++w) {
+                    td = td + s->part[(size_t)w * (size_t)n + (size_t)j];
+                    ta = ta + s->apart[(size_t)w * (size_t)n + (size_t)j];
+                }
+                s->dvec[j] = s->cost[j] - td;
+                s->avec[j] = xrow >= 0 ? fma(xsig, Aat(s, xrow, j), ta) : ta;
+            }
+            st->price_bytes += 8.0 * ((double)ny * (double)n + (double)n + (double)ny);
+        }
+        for (int64_t i = 0; i < m; ++i) {
+            s->dvec[n + i] = s->cost[n + i] - s->y[i];
+            s->avec[n + i] = s->rho[i];
+        }
+        /* ---- bound-flipping Harris ratio test ---- */
+        int64_t nc = 0;
+        for (int64_t j = 0; j < n + m; ++j) { /* candidates, ascending id */
+            const int8_t vs = s->vstat[j];
+            if (vs == VS_BASIC || s->lb[j] == s->ub[j]) continue;
+            const double a = s->avec[j], ah = rs * a, dj = s->dvec[j];
+            int side = 0;
+            if (vs == VS_LOWER || (vs == VS_FREE && ah < 0.0)) side = ah < -pivtol ? 1 : 0;
+            else if (vs == VS_UPPER || (vs == VS_FREE && ah > 0.0)) side = ah > pivtol ? -1 : 0;
+            if (!side) continue;
+            s->cj[nc] = j;
+            s->ct[nc] = side > 0 ? dj / (-ah) : (-dj) / ah;
+            s->cb[nc] = bland ? s->ct[nc] : side > 0 ? (dj + dtol) / (-ah) : (dtol - dj) / ah;
+            s->ca[nc] = fabs(a);
+            s->cr[nc] = (s->lb[j] > -INF && s->ub[j] < INF) ? s->ub[j] - s->lb[j] : INF;
+            s->calive[nc] = 1;
+            nc++;
+        }
+        /* bunches: the candidates whose exact ratio is within the Harris bound
+         * of the ones left are flipped together while every one of them is
+         * boxed and the slope (the primal infeasibility of x_r) stays
+         * positive past them (their |alpha| (u - l) summed in ascending id);
+         * otherwise the largest |alpha| of the bunch enters */
+        double slope = fabs(rx - rbeta);
+        int64_t q = -1, nflip = 0;
+        double qt = 0.0, qa = 0.0;
+        for (;;) {
+            double thmax = INF;
+            int any = 0;
+            for (int64_t c = 0; c < nc; ++c)
+                if (s->calive[c]) {
+                    any = 1;
+                    if (s->cb[c] < thmax) thmax = s->cb[c];
+                }
+            if (!any) break;
+            double sum = 0.0;
+            int allbox = 1;
+            for (int64_t c = 0; c < nc; ++c)
+                if (s->calive[c] && s->ct[c] <= thmax) {
+                    if (s->cr[c] == INF) allbox = 0;
+                    else sum = fma(s->ca[c], s->cr[c], sum);
+                }
+            if (allbox && sum < slope) {
+                slope = slope - sum;
+                for (int64_t c = 0; c < nc; ++c)
+                    if (s->calive[c] && s->ct[c] <= thmax) {
+                        s->calive[c] = 0;
+                        s->flips[nflip++] = s->cj[c];
+                    }
+                continue;
+            }
+            int64_t qc = -1;
+            for (int64_t c = 0; c < nc; ++c) {
+                if (!s->calive[c] || !(s->ct[c] <= thmax)) continue;
+                int take;
+                if (qc < 0) take = 1;
+                else if (bland) take = s->ct[c] < s->ct[qc] || (s->ct[c] == s->ct[qc] && s->cj[c] < s->cj[qc]);
+                else take = s->ca[c] > s->ca[qc] || (s->ca[c] == s->ca[qc] && s->cj[c] < s->cj[qc]);
+                if (take) qc = c;
+            }
+            q = s->cj[qc];
+            qt = s->ct[qc];
+            qa = s->avec[q];
+            break;
+        }
+        (*iter)++;
+        st->phase1_iterations++;
+        st->dual_iterations++;
+        if (q < 0) { /* dual unbounded: every move of the nonbasics leaves x_r infeasible */
+            if (trace && *iter - 1 < trace_cap) {
+                trace[2 * (*iter - 1)] = -2;
+                trace[2 * (*iter - 1) + 1] = rv;
+            }
+            return PH_INFEAS;
+        }
+        /* ---- the flips: a_F = sum_j a_j dx_j (ascending j), x_B -= B^-1 a_F ---- */
+        if (nflip > 0) {
+            for (int64_t i = 0; i < m; ++i) s->aF[i] = 0.0;
+            for (int64_t f = 0; f < nflip; ++f) {
+                const int64_t j = s->flips[f];
+                const double dx = s->vstat[j] == VS_LOWER ? s->ub[j] - s->lb[j] : s->lb[j] - s->ub[j];
+                for (int64_t i = 0; i < m; ++i) s->aF[i] = fma(Aat(s, i, j), dx, s->aF[i]);
+                s->vstat[j] = s->vstat[j] == VS_LOWER ? VS_UPPER : VS_LOWER;
+                s->xval[j] = s->vstat[j] == VS_LOWER ? s->lb[j] : s->ub[j];
+            }
+            for (int64_t p = 0; p < k; ++p) s->aR[p] = s->aF[s->Rl[p]];
+            for (int64_t p = 0; p < k; ++p) s->fS[p] = wave_dot(k, MI(s, p, 0), s->aR);
+            for (int64_t i = 0; i < m; ++i)
+                if (s->cover[i] >= 0)
+                    s->xr[i] = s->xr[i] - unit_sign(s, s->cover[i]) * (s->aF[i] - zchunk_row(s, i, s->fS));
+            for (int64_t p = 0; p < k; ++p) s->xs[p] = s->xs[p] - s->fS[p];
+            st->bound_flips += nflip;
+            rx = re < m ? s->xr[re] : s->xs[re - m];
+        }
+        {
+            const double dq = s->dvec[q];
+            const double sig = (s->vstat[q] == VS_LOWER || (s->vstat[q] == VS_FREE && rs * qa < 0.0)) ? 1.0 : -1.0;
+            /* ---- FTRAN ---- */
+            for (int64_t i = 0; i < m; ++i) s->acol[i] = (q < n) ? Aat(s, i, q) : (i == q - n ? 1.0 : 0.0);
+            for (int64_t p = 0; p < k; ++p) s->aR[p] = s->acol[s->Rl[p]];
+            for (int64_t p = 0; p < k; ++p) s->alS[p] = wave_dot(k, MI(s, p, 0), s->aR);
+            for (int64_t i = 0; i < m; ++i) {
+                if (s->cover[i] < 0) continue;
+                s->z[i] = zchunk_row(s, i, s->alS);
+                s->alU[i] = unit_sign(s, s->cover[i]) * (s->acol[i] - s->z[i]);
+            }
+            const double arq = re < m ? s->alU[re] : s->alS[re - m];
+            const double step = fabs((rx - rbeta) / arq);
+            if (trace && *iter - 1 < trace_cap) {
+                trace[2 * (*iter - 1)] = q;
+                trace[2 * (*iter - 1) + 1] = rv;
+            }
+            /* ---- dual Devex weights of the basic entries (old basis) ---- */
+            if (devex) {
+                const double wr = s->dw[rv];
+                for (int64_t e = 0; e < m + k; ++e) {
+                    if (e == re) continue;
+                    int64_t var;
+                    double ae;
+                    if (e < m) {
+                        if (s->cover[e] < 0) continue;
+                        var = s->cover[e];
+                        ae = s->alU[e];
+                    } else {
+                        var = s->Sl[e - m];
+                        ae = s->alS[e - m];
+                    }
+                    const double r = ae / arq;
+                    double wn = (r * r) * wr;
+                    if (wn > DEVEX_WMAX) wn = DEVEX_WMAX;
+                    if (wn > s->dw[var]) s->dw[var] = wn;
+                }
+                double wq = wr / (arq * arq);
+                if (wq < 1.0) wq = 1.0;
+                if (wq > DEVEX_WMAX) wq = DEVEX_WMAX;
+                if (wq > DEVEX_RESET) {
+                    for (int64_t j = 0; j < n + m; ++j) s->dw[j] = 1.0;
+                    st->devex_resets++;
+                } else {
+                    s->dw[q] = wq;
+                }
+            }
+            if (!(qt > 0.0)) {
+                st->degenerate++;
+                if (++ndegen >= ctl->degen_switch) bland = 1;
+            } else {
+                ndegen = 0;
+                bland = 0;
+            }
+            /* ---- primal update: x_B -= step sig alpha, x_r to its bound ---- */
+            for (int64_t i = 0; i < m; ++i)
+                if (s->cover[i] >= 0) s->xr[i] = fma(-step, sig * s->alU[i], s->xr[i]);
+            for (int64_t p = 0; p < k; ++p) s->xs[p] = fma(-step, sig * s->alS[p], s->xs[p]);
+            const double xq = s->xval[q] + sig * step;
+            const int at_lower = rs > 0;
+            s->vstat[rv] = at_lower ? VS_LOWER : VS_UPPER;
+            s->xval[rv] = rbeta;
+            s->vstat[q] = VS_BASIC;
+            if (basis_change(s, 2, q, rv, re < m ? re : -1, re < m ? -1 : re - m, dq, xq)) return PH_NUMFAIL;
+            since_refactor++;
+        }
     }
 }
 
@@ -1015,6 +1377,10 @@ static void sensitivity(orc_t* s, const orc_control* ctl, const int32_t* dir, in
     free(d);
 }
 
+/* elp_control.simplex's default (include/easylp_hip.h): 0 means it */
+#define ORC_SIMPLEX_DEFAULT 5
+static int simplex_type(const orc_control* c) { return c->simplex == 0 ? ORC_SIMPLEX_DEFAULT : c->simplex; }
+
 void orc_default_control(orc_control* c) {
     c->tol_primal = 1e-9;
     c->tol_dual = 1e-9;
@@ -1029,6 +1395,8 @@ void orc_default_control(orc_control* c) {
     c->price_rule = 1;
     c->scaling = 4 | 64; /* = elp_default_control: geometric + equilibrate */
     c->tol_singular = 1e-13;
+    c->simplex = 0;
+    c->pad0 = 0;
 }
 
 static int cmp_i64(const void* a, const void* b) {
@@ -1174,6 +1542,20 @@ static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, 
     s->perm = ialloc((size_t)mm);
     s->dw = dalloc((size_t)(n + m));
     s->dprev = dalloc((size_t)(n + m));
+    s->apart = dalloc((size_t)PRICE_SPLIT * (size_t)n);
+    s->rho = dalloc((size_t)mm);
+    s->rhoY = dalloc((size_t)mm);
+    s->dvec = dalloc((size_t)(n + m));
+    s->avec = dalloc((size_t)(n + m));
+    s->cj = ialloc((size_t)(n + m));
+    s->flips = ialloc((size_t)(n + m));
+    s->ct = dalloc((size_t)(n + m));
+    s->cb = dalloc((size_t)(n + m));
+    s->ca = dalloc((size_t)(n + m));
+    s->cr = dalloc((size_t)(n + m));
+    s->aF = dalloc((size_t)mm);
+    s->fS = dalloc((size_t)mm);
+    s->calive = (int8_t*)calloc((size_t)(n + m), 1);
 
     int status = 0;
     int64_t unb_var = -1;
@@ -1204,8 +1586,8 @@ static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, 
     }
     int64_t iter = 0;
     if (status == 0) {
-        int any_art = 0;
-        int64_t nzc = 0;
+        int any_art = 0, dual = 0;
+        int64_t nzc = nz_nonbasic(s, s->nzl); /* (no basic structural yet) */
         for (int64_t i = 0; i < m; ++i) {
             double bi = rhs[i];
             if (bi <= -BIG) bi = -INF;
@@ -1221,11 +1603,42 @@ static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, 
             s->vstat[av] = VS_LOWER;
             s->rpos[i] = -1;
             s->ypos[i] = -1;
-            if (i == 0) nzc = nz_nonbasic(s, s->nzl); /* (no basic structural yet) */
+        }
+        /* SIMPLEX_DUAL_PRIMAL: is the slack basis primal infeasible? */
+        if (simplex_type(&ctl) == 6)
+            for (int64_t i = 0; i < m && !dual; ++i) {
+                double acc = 0.0;
+                for (int64_t t = 0; t < nzc; ++t) acc = fma(Aat(s, i, s->nzl[t]), s->xval[s->nzl[t]], acc);
+                const double r = s->b[i] - acc;
+                dual = !(r >= s->lb[n + i] && r <= s->ub[n + i]);
+            }
+        if (dual) {
+            /* dual-feasible start: boxed columns at the bound their cost sign
+             * asks for; columns no bound makes dual feasible lose their cost
+             * for the phase (run_dual) */
+            for (int64_t j = 0; j < n; ++j) {
+                const double cj = SC_COL(maximize ? -obj[j] : obj[j], j, 1);
+                s->cost[j] = cj;
+                const double l = s->lb[j], u = s->ub[j];
+                if (l > -INF && u < INF && l != u) {
+                    s->vstat[j] = cj < 0.0 ? VS_UPPER : VS_LOWER;
+                    s->xval[j] = cj < 0.0 ? u : l;
+                }
+                const int8_t vs = s->vstat[j];
+                if (l != u && ((vs == VS_LOWER && cj < 0.0) || (vs == VS_UPPER && cj > 0.0) ||
+                               (vs == VS_FREE && cj != 0.0))) {
+                    s->cost[j] = 0.0;
+                    st.flattened++;
+                }
+            }
+            nzc = nz_nonbasic(s, s->nzl);
+        }
+        for (int64_t i = 0; i < m; ++i) {
+            const int64_t sv = n + i, av = n + m + i;
             double acc = 0.0;
             for (int64_t t = 0; t < nzc; ++t) acc = fma(Aat(s, i, s->nzl[t]), s->xval[s->nzl[t]], acc);
             const double r = s->b[i] - acc;
-            if (r >= s->lb[sv] && r <= s->ub[sv]) {
+            if (dual || (r >= s->lb[sv] && r <= s->ub[sv])) {  /* (dual: the slack, feasible or not) */
                 s->vstat[sv] = VS_BASIC;
                 s->cover[i] = sv;
                 s->xr[i] = r;
@@ -1245,7 +1658,12 @@ static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, 
             }
         }
         s->tol_inf = 1e-9 * (1.0 + bmax);
-        if (any_art && status == 0) {
+        if (dual) {
+            int ph = run_dual(s, &ctl, &iter, max_iter, trace, trace_cap, &st);
+            if (ph == PH_NUMFAIL) status = 5;
+            else if (ph == PH_ITERCAP) status = 1;
+            else if (ph == PH_INFEAS) status = 2;
+        } else if (any_art && status == 0) {
             int ph = run_phase(s, 1, &ctl, &iter, max_iter, trace, trace_cap, &st, &unb_var, &unb_sigma);
             if (ph == PH_NUMFAIL) status = 5;
             else if (ph == PH_ITERCAP) status = 1;
@@ -1259,7 +1677,7 @@ static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, 
                 s->ub[av] = 0.0;
             }
             for (int64_t j = 0; j < n; ++j) s->cost[j] = SC_COL(maximize ? -obj[j] : obj[j], j, 1);
-            if (any_art && refactor(s)) status = 5;
+            if ((any_art || dual) && refactor(s)) status = 5;
         }
         if (status == 0) {
             int ph = run_phase(s, 2, &ctl, &iter, max_iter, trace, trace_cap, &st, &unb_var, &unb_sigma);
@@ -1316,6 +1734,9 @@ static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, 
     free(s->y); free(s->t); free(s->yR); free(s->yy); free(s->acol); free(s->aR);
     free(s->alS); free(s->alU); free(s->z); free(s->v); free(s->tmp); free(s->part);
     free(s->dw); free(s->dprev);
+    free(s->apart); free(s->rho); free(s->rhoY); free(s->dvec); free(s->avec);
+    free(s->cj); free(s->flips); free(s->ct); free(s->cb); free(s->ca); free(s->cr); free(s->aF); free(s->fS);
+    free(s->calive);
     free(s->used); free(s->perm); free(s->cp); free(s->ri); free(s->nzl); free(s->colbuf);
     free(s->srow); free(s->scol); free(s->A_copy);
     return status;

@@ -48,6 +48,11 @@ typedef struct orc_control {
     int32_t scaling;       /* 4 geometric | 64 equilibrate (elp_control.scaling):
                               power-of-2 factors, scale_factors()           */
     double tol_singular;   /* Gauss-Jordan |pivot| <= this: numerical failure */
+    int32_t simplex;       /* phase 1 when the slack basis is infeasible:
+                              6 dual simplex (lp_solve SIMPLEX_DUAL_PRIMAL),
+                              5 primal on artificials (SIMPLEX_PRIMAL_PRIMAL);
+                              0: the default (= elp_control.simplex's)       */
+    int32_t pad0;
 } orc_control;
 
 typedef struct orc_stats {
@@ -66,6 +71,8 @@ typedef struct orc_stats {
     double max_inv_resid;  /* largest max|I - M Minv| a refactor measured    */
     int64_t lu_nnz;        /* orc_solve_lu: largest nnz(L) + nnz(U) + m      */
     int64_t eta_nnz;       /* orc_solve_lu: largest eta-file nonzeros         */
+    int64_t dual_iterations; /* phase-1 iterations of the dual simplex        */
+    int64_t flattened;     /* columns whose cost the dual phase zeroed        */
 } orc_stats;
 
 void orc_default_control(orc_control* c);
