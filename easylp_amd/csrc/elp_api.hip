@@ -144,7 +144,11 @@ struct elp_handle {
     std::vector<void*> lub;
     std::vector<size_t> lubcap;
     int64_t lu_nnz_max = 0;
+    bool dual_used = false;  // the last load's phase 1 is the dual simplex (phase 3)
 };
+
+// elp_control.simplex = 0 (include/easylp_hip.h)
+#define ELP_SIMPLEX_DEFAULT ELP_SIMPLEX_PRIMAL_PRIMAL
 
 extern "C" void elp_default_control(elp_control* c) {
     std::memset(c, 0, sizeof(*c));
@@ -209,7 +213,8 @@ static void free_dev(elp_handle* h, bool keep_big = false) {
                     d.pkt, d.objg, d.ract, d.cand_xchg, h->d_flag, d.cS, d.slo, d.shi, d.rlo, d.rhi,
                     (void*)d.cptr, (void*)d.rind, (void*)d.cval, (void*)d.rptr, (void*)d.cind,
                     (void*)d.rval, d.qcol, d.qz, d.dstamp, d.rowvs, d.yvs, d.dw, d.dprev, (void*)d.srow,
-                    (void*)d.scol};
+                    (void*)d.scol, d.rhoR, d.rr, d.dchz, d.dcand, d.dcnt, d.dcomp, d.dalive, d.dflip,
+                    d.dflipdx, d.aF, d.fS};
     for (void* p : ptrs)
         if (p) release(p);
     if (!keep_big) drain_pool(h);
@@ -507,6 +512,8 @@ extern "C" int elp_create(elp_handle** out, int64_t m, int64_t n, const elp_cont
     if (m > 0x3fffffff || n > 0x3fffffff) return fail(ELP_E_ARG, "elp_create: dimension too large");
     if (ctl && ctl->pricing != ELP_PRICE_DANTZIG && ctl->pricing != ELP_PRICE_DEVEX)
         return fail(ELP_E_ARG, "elp_create: pricing must be ELP_PRICE_DANTZIG or ELP_PRICE_DEVEX");
+    if (ctl && ctl->simplex != 0 && ctl->simplex != ELP_SIMPLEX_PRIMAL_PRIMAL && ctl->simplex != ELP_SIMPLEX_DUAL_PRIMAL)
+        return fail(ELP_E_ARG, "elp_create: simplex must be 0, ELP_SIMPLEX_PRIMAL_PRIMAL or ELP_SIMPLEX_DUAL_PRIMAL");
     elp_handle* h = new elp_handle();
     if (ctl) h->ctl = *ctl;
     else elp_default_control(&h->ctl);
@@ -700,6 +707,23 @@ static int alloc_all_body(elp_handle* h) {
     }
     A(dalloc(&d.ctl, 1));
     A(dalloc(&d.trace, (size_t)(h->trace_cap > 0 ? 2 * h->trace_cap : 2)));
+    // dual simplex phase 1 (one GPU; elp_kernels.hip "dual simplex"): regions =
+    // the pricing tiles + the slack workgroups (<= m / 128 + 1), DREG slots each
+    if (!d.sharded && !h->lu) {
+        d.dregs = d.ntiles + (int32_t)((mm + TILE_COLS - 1) / TILE_COLS) + 2;
+        d.dchzn = (int32_t)((2 * mm + 255) / 256 + 2);
+        A(dalloc(&d.rhoR, mm));
+        A(dalloc(&d.rr, mm));
+        A(dalloc(&d.dchz, (size_t)d.dchzn));
+        A(dalloc(&d.dcand, (size_t)d.dregs * DREG));
+        A(dalloc(&d.dcnt, (size_t)d.dregs));
+        A(dalloc(&d.dcomp, (size_t)(n + m)));
+        A(dalloc(&d.dalive, (size_t)(n + m)));
+        A(dalloc(&d.dflip, (size_t)(n + m)));
+        A(dalloc(&d.dflipdx, (size_t)(n + m)));
+        A(dalloc(&d.aF, mm));
+        A(dalloc(&d.fS, mm));
+    }
     if (e != hipSuccess) {
         free_dev(h);
         return fail(ELP_E_NOMEM, std::string("device allocation failed: ") + hipGetErrorString(e));
@@ -990,6 +1014,16 @@ static void scale_csc(elp_handle* h, const int64_t* cp, const int32_t* ri, doubl
     h->scol_h = std::move(gam);
 }
 
+// the phase-1 method (elp_control.simplex; lp_solve's set_simplextype): the
+// dual simplex on one GPU with the bump inverse; column-sharded solves and the
+// sparse-LU engine keep the primal phase 1 on artificials
+static int simplex_type(const elp_handle* h) {
+    return h->ctl.simplex == 0 ? ELP_SIMPLEX_DEFAULT : h->ctl.simplex;
+}
+static bool dual_phase1(const elp_handle* h) {
+    return simplex_type(h) == ELP_SIMPLEX_DUAL_PRIMAL && h->comm.kind == 0 && !h->lu && h->d.dcand;
+}
+
 // common tail of elp_load_*: bounds, rows, control block, phase decision
 static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, const double* obj,
                        const double* lo, const double* up, int32_t maximize) {
@@ -1136,7 +1170,31 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
         h->final_status = ELP_INFEASIBLE;
         return 0;
     }
-    if (h->any_art) {
+    h->dual_used = false;
+    if (h->any_art && dual_phase1(h)) {
+        // SIMPLEX_DUAL_PRIMAL (oracle solve_core): the slack basis is infeasible,
+        // so the phase-1 method is the dual simplex from a dual-feasible start --
+        // boxed columns at the bound their cost sign asks for, the costs no bound
+        // makes dual feasible zeroed, every row covered by its slack
+        HIPCHK(launch_dual_setup_cols(d, h->st));
+        HIPCHK(hipMemsetAsync(d.ract, 0, (size_t)std::max<int64_t>(m, 1) * sizeof(double), h->st));
+        {
+            const int rc = row_chain(h);
+            if (rc) return rc;
+        }
+        HIPCHK(launch_dual_init_rows(d, h->st));
+        HIPCHK(launch_btran_exact(d, 0, h->st));  // slack basis: y = 0
+        HIPCHK(hipMemcpyAsync(h->hctl, d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+        HIPCHK(hipStreamSynchronize(h->st));
+        h->hctl->phase = 2;
+        h->hctl->devex = 0;  // (the primal Devex weights: dw holds the dual ones)
+        h->hctl->ddevex = h->ctl.pricing == ELP_PRICE_DEVEX;
+        HIPCHK(hipMemcpyAsync(d.ctl, h->hctl, sizeof(DevCtl), hipMemcpyHostToDevice, h->st));
+        HIPCHK(hipStreamSynchronize(h->st));
+        h->phase = 3;
+        h->any_art = false;
+        h->dual_used = true;
+    } else if (h->any_art) {
         h->phase = 1;
     } else {
         HIPCHK(launch_phase2(d, h->st));
@@ -1669,7 +1727,7 @@ static int do_refactor(elp_handle* h, int k) {
         if (rc) return rc;
     }
     HIPCHK(launch_refactor_primal(h->d, k, h->st));
-    if (h->phase == 2) HIPCHK(launch_btran_exact(h->d, k, h->st));  // exact duals again
+    if (h->phase >= 2) HIPCHK(launch_btran_exact(h->d, k, h->st));  // exact duals again (phase 3: the dual's costs)
     h->stats.refactors++;
     return 0;
 }
@@ -1746,7 +1804,7 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             h->stats.seconds_loop += now_s() - t_loop0;
             return 0;
         }
-        if (c->status == ST_RUN && h->phase == 2 && c->iter >= c->iter_limit) {
+        if (c->status == ST_RUN && h->phase >= 2 && c->iter >= c->iter_limit) {
             // the phase-2 loop top (oracle run_phase) before any k_ratio has
             // checked the cap: a budget spent in phase 1 or a branch-and-bound
             // budget of 0
@@ -1754,7 +1812,7 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             h->final_status = ELP_SUBOPTIMAL;
             break;
         }
-        if (c->status == ST_RUN && h->phase == 2 && c->since_refactor >= period &&
+        if (c->status == ST_RUN && h->phase >= 2 && c->since_refactor >= period &&
             c->iter < c->iter_limit) {
             rc = do_refactor(h, c->k);
             if (rc) return rc;
@@ -1795,7 +1853,9 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             const int nyub = (int)std::min<int64_t>(h->m, (int64_t)ny0 + t);
             hipEvent_t e0 = prof_chunk ? h->ev[2 * t] : nullptr, e1 = prof_chunk ? h->ev[2 * t + 1] : nullptr;
             h->stats.price_launches++;
-            if (h->comm.kind == 0 || h->d.p2p) {  // (p2p: min-loc inside the select kernel)
+            if (h->phase == 3) {  // the dual simplex phase 1 (one GPU)
+                HIPCHK(launch_dual_iteration(h->d, kub, nyub, h->st));
+            } else if (h->comm.kind == 0 || h->d.p2p) {  // (p2p: min-loc inside the select kernel)
                 HIPCHK(launch_iteration(h->d, kub, nyub, h->phase, h->st, e0, e1, t));
             } else {
                 // sharded: local min-loc -> all-gather -> global min-loc.  Replicated
@@ -1907,6 +1967,40 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             *lp_status = ELP_SUBOPTIMAL;
             h->stats.seconds_loop += now_s() - t_loop0;
             return 0;
+        }
+        if (s == ST_DUALINF && h->phase == 3) {  // the dual ray: no nonbasic can repair the leaving row
+            h->done = true;
+            h->final_status = ELP_INFEASIBLE;
+            break;
+        }
+        if (s == ST_PHASE_OPT && h->phase == 3) {
+            // primal feasible: confirm on a fresh x_B after updates (oracle run_dual),
+            // else the real costs and the primal phase 2 from this basis
+            const bool recheck = c->since_refactor > 0;
+            if (!recheck) {
+                HIPCHK(launch_phase2(h->d, h->st));
+                h->phase = 2;
+            }
+            rc = do_refactor(h, c->k);
+            if (rc) return rc;
+            HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+            HIPCHK(hipStreamSynchronize(h->st));
+            if (c->status == ST_NUMFAIL) {
+                h->done = true;
+                h->final_status = ELP_NUMFAILURE;
+                break;
+            }
+            c->phase = 2;
+            c->since_refactor = 0;
+            if (!recheck) {
+                c->ndegen = 0;
+                c->bland = 0;
+                c->devex = h->ctl.pricing == ELP_PRICE_DEVEX;
+            }
+            c->status = ST_RUN;
+            rc = push_ctl_fields(h);
+            if (rc) return rc;
+            continue;
         }
         if ((s == ST_PHASE_OPT || s == ST_P1DONE) && h->phase == 1) {
             if (s == ST_PHASE_OPT && c->art_sum > c->tol_inf) {
@@ -2171,6 +2265,40 @@ static int lu_run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             c->lu_ne = 0;
             c->lu_enz = 0;
             c->status = ST_RUN;  // (a re-check skips the loop-top checks, as the oracle's)
+            rc = push_ctl_fields(h);
+            if (rc) return rc;
+            continue;
+        }
+        if (s == ST_DUALINF && h->phase == 3) {  // the dual ray: no nonbasic can repair the leaving row
+            h->done = true;
+            h->final_status = ELP_INFEASIBLE;
+            break;
+        }
+        if (s == ST_PHASE_OPT && h->phase == 3) {
+            // primal feasible: confirm on a fresh x_B after updates (oracle run_dual),
+            // else the real costs and the primal phase 2 from this basis
+            const bool recheck = c->since_refactor > 0;
+            if (!recheck) {
+                HIPCHK(launch_phase2(h->d, h->st));
+                h->phase = 2;
+            }
+            rc = do_refactor(h, c->k);
+            if (rc) return rc;
+            HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+            HIPCHK(hipStreamSynchronize(h->st));
+            if (c->status == ST_NUMFAIL) {
+                h->done = true;
+                h->final_status = ELP_NUMFAILURE;
+                break;
+            }
+            c->phase = 2;
+            c->since_refactor = 0;
+            if (!recheck) {
+                c->ndegen = 0;
+                c->bland = 0;
+                c->devex = h->ctl.pricing == ELP_PRICE_DEVEX;
+            }
+            c->status = ST_RUN;
             rc = push_ctl_fields(h);
             if (rc) return rc;
             continue;
@@ -2695,6 +2823,8 @@ extern "C" int elp_get_stats(elp_handle* h, elp_stats* st) {
         h->stats.price_bytes = c.price_bytes;
         h->stats.iter_bytes = c.iter_bytes;
         h->stats.exchange_rtt_us = h->comm.p2p ? h->comm.rtt_us : 0.0;
+        h->stats.dual_iterations = c.dual_iters;
+        h->stats.simplex = h->dual_used ? ELP_SIMPLEX_DUAL_PRIMAL : ELP_SIMPLEX_PRIMAL_PRIMAL;
         if (h->lu) {  // basic structurals, factor and eta-file sizes
             std::vector<int32_t> head((size_t)std::max<int64_t>(h->m, 1));
             if (h->m) {

@@ -33,6 +33,7 @@ enum : int32_t {
     ST_NUMFAIL = 6,
     ST_STOP = 7,       // elp_iterate budget reached at loop top
     ST_COMMFAIL = 8,   // xGMI mailbox: a peer's record did not arrive in time
+    ST_DUALINF = 9,    // dual simplex: no entering candidate for the leaving row (primal infeasible)
 };
 
 // pivot cases (oracle/elp_oracle.c "case A".."case E")
@@ -59,6 +60,11 @@ struct Plan {
     int32_t y_ap_slot, y_ap_row;  // -1: no append
     double piv;                   // A: alS[p]; B: delta; C: Minv[b][a]
     double xq;
+    // dual simplex (phase 3): dual Devex weights of the basic entries are
+    // updated with the plan (apply_copy): w_r of the leaving variable, the
+    // pivot alpha_rq of the FTRAN column, the leaving entry (row / m + position)
+    int32_t dual, dre;
+    double dwr, darq;
 };
 
 struct DevCtl {
@@ -119,7 +125,30 @@ struct DevCtl {
     // sparse-LU engine (ELP_BASIS_LU): etas in the file, their entries
     int32_t lu_ne, lu_pad;
     int64_t lu_enz, lu_enz_max;
+    // dual simplex phase 1 (h->phase 3, oracle run_dual): the leaving row of
+    // this iteration as k_dual_row chose it -- basic variable, entry (covered
+    // row, or m + bump position), direction s (+1 below its lower bound), the
+    // covered row whose own entry the pivot row adds (-1: a bump position) and
+    // its sign; value, target bound, bounds, dual Devex weight
+    int32_t dr_var, dr_e, dr_s, dr_xrow;
+    double dr_x, dr_beta, dr_lb, dr_ub, dr_w, dr_xsig;
+    double dq_t;              // the entering column's exact dual ratio (<= 0: degenerate)
+    int32_t nflip, ddevex;    // bound flips of this iteration; dual Devex pricing on
+    int64_t dual_iters, dflat;  // dual iterations; columns whose cost the phase zeroed
 };
+
+// dual simplex candidates (k_dual_price -> k_dual_bfrt): exact ratio t, Harris
+// bound b, pivot-row alpha (signed), range u - l (+inf: not boxed), reduced cost
+struct DualCand {
+    double t, b, a, r, d;
+    int32_t j, side;  // global id; +1 acts at its lower bound, -1 at its upper
+};
+// a dual CHUZR partial (k_dual_chuzr, one per workgroup)
+struct ChzRec {
+    double score, x, beta;
+    int32_t var, e, s, pad;
+};
+constexpr int DREG = 256;  // DualCand slots per k_dual_price region (one region per workgroup)
 
 // Harris pass-2 candidate (a superset of the global candidates: exact ratio
 // <= its workgroup's pass-1 minimum)
@@ -243,8 +272,21 @@ struct Dev {
     MboxRec* const* mpeers; // every rank's mailbox as mapped in this process
     int32_t p2p, rank;
     // Devex: weight and last reduced cost per local structural (j < n) and
-    // slack (n + i)
+    // slack (n + i); the dual phase keeps its reference weights of the basic
+    // variables in dw
     double *dw, *dprev;
+    // dual simplex phase 1 (single GPU): rho_r on the bump positions and on the
+    // Y slots, the CHUZR partials, the ratio-test candidate regions and their
+    // counts, the compacted candidates and their live flags, the bound flips
+    // (ids, dx), the flip column a_F and its bump FTRAN
+    double *rhoR, *rr;
+    ChzRec* dchz;
+    DualCand *dcand, *dcomp;
+    int32_t* dcnt;
+    int8_t* dalive;
+    int32_t* dflip;
+    double *dflipdx, *aF, *fS;
+    int32_t dregs, dchzn;
 };
 
 // Sparse-LU engine of the CSC path (elp_control.basis = ELP_BASIS_LU, DESIGN.md
@@ -350,5 +392,15 @@ hipError_t launch_lu_phase2(const Dev& d, hipStream_t st);
 hipError_t launch_lu_extract(const Dev& d, const LuDev& u, double* xout, hipStream_t st);
 // largest m whose working vector fits the LDS of one workgroup (0: query failed)
 int lu_lds_max_m();
+
+// dual simplex phase 1 (elp_kernels.hip "dual simplex" section; oracle run_dual)
+// load: the dual-feasible start -- boxed columns at the bound their cost sign
+// asks for, costs of the columns no bound makes dual feasible zeroed (run
+// before the row activities), then every row covered by its slack
+hipError_t launch_dual_setup_cols(const Dev& d, hipStream_t st);
+hipError_t launch_dual_init_rows(const Dev& d, hipStream_t st);
+// one iteration: CHUZR, rho_r, pivot row + pricing, bound-flipping ratio test,
+// the flips' FTRAN and x_B update, FTRAN of a_q, pivot bookkeeping, update
+hipError_t launch_dual_iteration(const Dev& d, int k_ub, int ny_ub, hipStream_t st);
 
 }  // namespace elp

@@ -1460,7 +1460,9 @@ DEV void gather_aR(const Dev& d, int q, const double* qcol) {
     }
 }
 
-__global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles, int nsw) {
+// dual != 0 (the dual phase): q is k_dual_bfrt's (candidate 0), which also set
+// the control block's entering fields and the statistics
+__global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles, int nsw, int dual) {
     __shared__ Cand red[16];
     DevCtl* c = d.ctl;
     if (threadIdx.x == 0) c->applied_seq = c->plan_seq;  // the pricing launch applied it
@@ -1476,7 +1478,7 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles, int nsw) {
         return;
     }
     const int q = (int)best.j;
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && !dual) {
         entering_chosen(d, best);
         entering_stats(d);
     }
@@ -1503,7 +1505,7 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles, int nsw) {
 constexpr int QZ_PT = 8;
 template <int PFM>  // Minv values per lane held in registers (k <= 64 PFM): 8 or 16 by the host's bound
 __global__ void __launch_bounds__(256) k_select_ftran(DEV_PARAM, int ntiles, int nsw, int k_ub, int dslot, int nrw,
-                                                      int nqz) {
+                                                      int nqz, int dual) {
     DEV_BIND
     extern __shared__ __attribute__((aligned(16))) double aRs[];  // [k]
     __shared__ Cand red[4];
@@ -1586,7 +1588,7 @@ __global__ void __launch_bounds__(256) k_select_ftran(DEV_PARAM, int ntiles, int
     }
     RSTAMP(14);
     const int q = (int)best.j;
-    if (blockIdx.x == 0 && tid == 0) entering_chosen(d, best);
+    if (blockIdx.x == 0 && tid == 0 && !dual) entering_chosen(d, best);  // (dual: k_dual_bfrt chose q)
     if (ELP_DIAG && d.ptimer && blockIdx.x == gridDim.x - 1) {  // the extra timer workgroup
         price_timer_sum<256>(d, reinterpret_cast<unsigned long long*>(aRs));
         return;
@@ -1642,7 +1644,7 @@ __global__ void __launch_bounds__(256) k_select_ftran(DEV_PARAM, int ntiles, int
         }
     }
     __syncthreads();
-    const bool stats_here = blockIdx.x == 0 && tid == 0;
+    const bool stats_here = blockIdx.x == 0 && tid == 0 && !dual;
     if (pr >= k) {
         if (stats_here) entering_stats(d);
         return;
@@ -2181,7 +2183,12 @@ enum { SI_VSQ, SI_RPOS0, SI_YPOS0, SI_YLAST, SI_SLLAST, SI_RLLAST, SI_RPOSYL, SI
 // checks, and the rest of the update is deferred into the next pricing launch.
 // PFT: B^-1 row values per lane held in registers (k <= 64 PFT), 8 or 16 by the
 // host's bound on k (a longer row is read in a loop)
-template <int PFT>
+// DUAL (the dual simplex phase, oracle run_dual): no primal ratio test -- the
+// leaving entry is k_dual_row's, the step |x_r - beta_r| / |alpha_rq| on the
+// FTRAN column, the leaving variable goes to beta_r; the bookkeeping, the B^-1
+// row and the dual update are the primal's (phase 2), the plan carries the dual
+// Devex update and the loop-top checks run here (no deferral).
+template <int PFT, bool DUAL = false>
 __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, int lds_row, int defer,
                                                int nmain, int k_ub, int dslot, int nreg) {
     DEV_BIND
@@ -2362,10 +2369,27 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
         best = lred[win];
     }
     RSTAMP(3);
+    double dual_acol = 0.0;
+    int dual_s = 0;
+    double dual_qt = 0.0;
+    if constexpr (DUAL) {  // the dual's leaving entry replaces the primal decision
+        const int e = c->dr_e;
+        dual_acol = e < m ? d.alU[e] : d.alS[e - m];
+        const double xe = e < m ? d.xr[e] : d.xs[e - m];  // (after this iteration's flips)
+        best.var = c->dr_var;
+        best.e = e;
+        best.g = sig * dual_acol;
+        best.ag = fabs(best.g);
+        best.l = c->dr_lb;
+        best.u = c->dr_ub;
+        best.r = fabs((xe - c->dr_beta) / dual_acol);
+        dual_s = c->dr_s;
+        dual_qt = c->dq_t;
+    }
     // ---- decision (uniform across the block)
     const double lbq = sv_lbq, ubq = sv_ubq;
     const double theta = best.var >= 0 ? (best.r > 0.0 ? best.r : 0.0) : INF;
-    const double flip = (lbq > -INF && ubq < INF) ? ubq - lbq : INF;
+    const double flip = !DUAL && (lbq > -INF && ubq < INF) ? ubq - lbq : INF;
     int action;
     double step;
     if (flip < INF && flip <= theta) {
@@ -2381,7 +2405,8 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
     if (lead && tid == 0) {
         const int64_t it = cs_iter;
         c->iter = it + 1;
-        if (phase == 1) c->phase1_iters = cs_p1 + 1;
+        if (phase == 1 || DUAL) c->phase1_iters = cs_p1 + 1;
+        if (DUAL) c->dual_iters++;
         if (action == ACT_NONE) {
             c->status = ST_UNBOUNDED;
             c->unb_var = q;
@@ -2422,6 +2447,8 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
             P.y_rm_slot = P.y_rm_last = P.y_ap_slot = P.y_ap_row = -1;
             P.piv = 0.0;
             P.xq = 0.0;
+            P.dual = P.dre = 0;
+            P.dwr = P.darq = 0.0;
             c->plan = P;
             c->plan_seq = cs_seq + 1;
             if (defer) loop_top(ST_RUN, cs_iter + 1, cs_since);
@@ -2602,7 +2629,8 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
         constexpr int wv = decltype(WVc)::value;  // (0: counters / statuses / control block,
                                                   //  1: bump lists, 2: Y list and covers,
                                                   //  3: plan record and duals)
-        if (theta == 0.0) {
+        // (dual: degenerate when the entering column's dual ratio is not positive)
+        if (DUAL ? !(dual_qt > 0.0) : theta == 0.0) {
             if (wv == 0) { c->degenerate = cs_degen + 1; }
             if (wv == 0) { c->ndegen = cs_ndegen + 1; }
             if (wv == 0) { if (cs_ndegen + 1 >= cs_dswitch) c->bland = 1; }
@@ -2614,7 +2642,7 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
         const int lrow = best.e < m ? best.e : -1;
         const int lpos = best.e < m ? -1 : best.e - m;
         const double xq = sv_xq + sig * theta;
-        const bool at_lower = best.g > 0.0;
+        const bool at_lower = DUAL ? dual_s > 0 : best.g > 0.0;
         const bool leave_art = lv >= d.N + m;
         const int lvl = loc_of(d, lv);
         if (leave_art) {
@@ -2656,6 +2684,10 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
         P.sig = sig;
         P.y_rm_slot = P.y_rm_last = P.y_ap_slot = P.y_ap_row = -1;
         P.piv = 0.0;
+        P.dual = DUAL && c->ddevex ? 1 : 0;
+        P.dre = best.e;
+        P.dwr = DUAL ? c->dr_w : 0.0;
+        P.darq = dual_acol;
         int nny = ny;
         int newk = k;
         if (q < d.N) {
@@ -2785,7 +2817,7 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
         if (wv == 0) { c->since_refactor = cs_since + 1; }
         if (wv == 3) { c->plan = P; }
         if (wv == 0) { c->plan_seq = cs_seq + 1; }
-        if (wv == 0) { if (defer) loop_top(P.pcase == PC_E && lrow != q - d.N ? ST_NUMFAIL : ST_RUN, cs_iter + 1, cs_since + 1); }
+        if (wv == 0) { if (defer || DUAL) loop_top(P.pcase == PC_E && lrow != q - d.N ? ST_NUMFAIL : ST_RUN, cs_iter + 1, cs_since + 1); }
         };
     if ((tid & 63) == 0) {  // thread 0 of each wave: the same decisions, a quarter of the stores
         switch (tid >> 6) {
@@ -2853,6 +2885,40 @@ DEV void apply_minv(const Dev& d, const Plan& P, int64_t e0, int64_t estride) {
 // the primal update and the AS (/ AR) copies of a plan: thread t0 of tstride
 DEV void apply_copy(const Dev& d, const Plan& P, int64_t t0, int64_t tstride, bool do_ar) {
     const int k = P.k_old;
+    if (P.dual && P.action == ACT_PIVOT) {
+        // dual Devex (oracle run_dual): the basic entries of the old basis other
+        // than the leaving one take max(w, (alpha_e / alpha_rq)^2 w_r), the
+        // entering variable max(w_r / alpha_rq^2, 1); above DEVEX_RESET every
+        // weight restarts at 1.  Entries are read through the new lists (k_ratio
+        // rewrote them): the entering slack's row (i0) and the removed bump
+        // position are skipped, case C's moved position keeps alpha_S[last].
+        const double wr = P.dwr, arq = P.darq;
+        double wq = wr / (arq * arq);
+        if (wq < 1.0) wq = 1.0;
+        if (wq > DEVEX_WMAX) wq = DEVEX_WMAX;
+        if (wq > DEVEX_RESET) {
+            for (int64_t t = t0; t < (int64_t)d.n + d.m; t += tstride) d.dw[t] = 1.0;
+        } else {
+            auto upd = [&](int var, double ae) {
+                const double r = ae / arq;
+                double wn = (r * r) * wr;
+                if (wn > DEVEX_WMAX) wn = DEVEX_WMAX;
+                const int lv = loc_of(d, var);
+                if (wn > d.dw[lv]) d.dw[lv] = wn;
+            };
+            for (int64_t t = t0; t < d.m; t += tstride) {
+                if (t == P.i0 || t == P.lrow) continue;
+                const int u = d.cover[t];
+                if (u >= 0) upd(u, d.alU[t]);
+            }
+            for (int64_t p = t0; p < k; p += tstride) {
+                if (p == P.lpos) continue;  // (A, C: the leaving structural)
+                if (P.pcase == PC_C && p == P.last) upd(d.Sl[P.b], d.alS[P.last]);  // (moved to b)
+                else upd(d.Sl[p], d.alS[p]);
+            }
+            if (t0 == 0) d.dw[loc_of(d, P.q)] = wq;
+        }
+    }
     // ---- primal update (oracle order: x -= step * (sig * alpha), then the
     //      entering value / compaction of the pivot case)
     const size_t m = (size_t)d.m;
@@ -3319,6 +3385,658 @@ __global__ void k_sens_final(Dev d, int k, int ntc, int ntr, const double* __res
     }
 }
 
+// ============================================================== dual simplex
+// Phase 1 by the dual simplex (lp_solve's default SIMPLEX_DUAL_PRIMAL; oracle
+// run_dual, whose arithmetic every kernel here reproduces bit for bit).  One
+// iteration (launch_dual_iteration): k_dual_chuzr (leaving-row partials) ->
+// k_dual_row (leaving row, rho_r on the bump positions) -> k_dual_price (ONE
+// sweep of the Y rows for both d_j = c_j - y'a_j and the pivot row alpha_j =
+// rho_r'a_j, Harris candidates compacted per tile) -> k_dual_bfrt (bound-
+// flipping ratio test over the compacted candidates, one workgroup) ->
+// k_dual_flip_* (a_F = sum of the flipped columns, its FTRAN, x_B -= B^-1 a_F)
+// -> the primal iteration's select-FTRAN, FTRAN-z and k_ratio (DUAL: the
+// leaving entry is the dual's) -> k_update (also the dual Devex weights).
+
+// oracle solve_core's dual start: cost (minimisation form), boxed columns at
+// the bound their cost sign asks for, zero cost where no bound is dual feasible
+__global__ void k_dual_setup_cols(Dev d) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= d.n) return;
+    const double cj = d.maximize ? -d.obj[j] : d.obj[j];
+    d.cost[j] = cj;
+    const double l = d.lb[j], u = d.ub[j];
+    if (l > -HUGE_VAL && u < HUGE_VAL && l != u) {
+        d.vstat[j] = cj < 0.0 ? VS_UPPER : VS_LOWER;
+        d.xval[j] = cj < 0.0 ? u : l;
+    }
+    const int8_t vs = d.vstat[j];
+    if (l != u && ((vs == VS_LOWER && cj < 0.0) || (vs == VS_UPPER && cj > 0.0) || (vs == VS_FREE && cj != 0.0))) {
+        d.cost[j] = 0.0;
+        atomicAdd(reinterpret_cast<unsigned long long*>(&d.ctl->dflat), 1ull);
+    }
+}
+
+// every row covered by its slack, feasible or not (after k_init_rows and the
+// row activities of the placement above); no artificial, Y empty
+__global__ void k_dual_init_rows(Dev d) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= d.m) return;
+    const int n = d.n, m = d.m, sv = n + i, av = n + m + i;
+    d.vstat[sv] = VS_BASIC;
+    d.cover[i] = d.N + i;
+    d.xr[i] = d.b[i] - d.ract[i];
+    d.xval[sv] = 0.0;
+    d.rlo[i] = d.lb[sv];
+    d.rhi[i] = d.ub[sv];
+    d.lb[av] = 0.0;
+    d.ub[av] = 0.0;
+    d.cost[av] = 0.0;
+    d.vstat[av] = VS_FIXED;
+    d.xval[av] = 0.0;
+    d.asgn[i] = 1.0;
+    d.rpos[i] = -1;
+    d.ypos[i] = -1;
+    if (i == 0) {
+        d.ctl->ny = 0;
+        d.ctl->k = 0;
+    }
+}
+
+// CHUZR total order: the larger infeasibility score, then the lower variable
+// id; Bland: the lower variable id
+DEV bool chz_better(const ChzRec& a, const ChzRec& b, int bland) {
+    if (a.var < 0) return false;
+    if (b.var < 0) return true;
+    if (bland) return a.var < b.var;
+    return a.score > b.score || (a.score == b.score && a.var < b.var);
+}
+DEV void chz_take(ChzRec& c, const ChzRec& o, bool take) {  // (field-wise, see cand_take)
+    c.score = take ? o.score : c.score;
+    c.x = take ? o.x : c.x;
+    c.beta = take ? o.beta : c.beta;
+    c.var = take ? o.var : c.var;
+    c.e = take ? o.e : c.e;
+    c.s = take ? o.s : c.s;
+}
+DEV void chz_none(ChzRec& r) {
+    r.score = r.x = r.beta = 0.0;
+    r.var = r.e = -1;
+    r.s = r.pad = 0;
+}
+// block-wide best of NT records (tree in LDS; a total order, so any tree agrees)
+template <int NT>
+DEV ChzRec block_best_chz(ChzRec r, int bland, ChzRec* lds) {
+    const int t = threadIdx.x;
+    lds[t] = r;
+    __syncthreads();
+    for (int h = NT / 2; h >= 1; h >>= 1) {
+        if (t < h && chz_better(lds[t + h], lds[t], bland)) lds[t] = lds[t + h];
+        __syncthreads();
+    }
+    const ChzRec out = lds[0];
+    __syncthreads();
+    return out;
+}
+
+// CHUZR partials: one basic entry per thread (covered rows, then bump positions)
+__global__ void __launch_bounds__(256) k_dual_chuzr(Dev d) {
+    __shared__ ChzRec red[256];
+    const DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    const int m = d.m, k = c->k, bland = c->bland, dvx = c->ddevex;
+    const double ptol = c->tol_primal;
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    ChzRec r;
+    chz_none(r);
+    int var = -1;
+    double x = 0.0, l = 0.0, u = 0.0;
+    if (e < m) {
+        const int cv = d.cover[e];
+        if (cv >= 0) {
+            var = cv;
+            x = d.xr[e];
+            l = d.rlo[e];
+            u = d.rhi[e];
+        }
+    } else if (e - m < k) {
+        const int p = e - m;
+        var = d.Sl[p];
+        x = d.xs[p];
+        l = d.slo[p];
+        u = d.shi[p];
+    }
+    if (var >= 0) {
+        double delta = 0.0, beta = 0.0;
+        int sd = 0;
+        if (x < l - ptol) {
+            delta = l - x;
+            beta = l;
+            sd = 1;
+        } else if (x > u + ptol) {
+            delta = x - u;
+            beta = u;
+            sd = -1;
+        }
+        if (sd) {
+            r.var = var;
+            r.e = e;
+            r.x = x;
+            r.beta = beta;
+            r.s = sd;
+            r.score = dvx ? (delta * delta) / d.dw[loc_of(d, var)] : delta;
+        }
+    }
+    r = block_best_chz<256>(r, bland, red);
+    if (threadIdx.x == 0) d.dchz[blockIdx.x] = r;
+}
+
+// The leaving row (every workgroup reduces the CHUZR partials: a total order,
+// all agree) and rho_r on the bump positions, one wave per position:
+// Minv row p for bump position p; -sigma (A[i,S] Minv)_c for the slack covering
+// row i (the oracle's row_times_minv in wave order).  Written in position order
+// (rhoR) and on the Y slots (rr, the dense sweep's operand).
+__global__ void __launch_bounds__(256) k_dual_row(Dev d, int nchz, int lds_row) {
+    extern __shared__ __attribute__((aligned(16))) double asrow_lds[];  // [k]: A[i, S]
+    __shared__ ChzRec red[256];
+    DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    const int m = d.m, k = c->k, bland = c->bland;
+    const int tid = threadIdx.x, lane = tid & 63;
+    ChzRec r;
+    chz_none(r);
+    for (int t = tid; t < nchz; t += 256) {
+        const ChzRec o = d.dchz[t];
+        chz_take(r, o, chz_better(o, r, bland));
+    }
+    r = block_best_chz<256>(r, bland, red);
+    if (r.var < 0) {  // primal feasible: the dual phase is done (the host re-checks)
+        if (blockIdx.x == 0 && tid == 0) c->status = ST_PHASE_OPT;
+        return;
+    }
+    const int xrow = r.e < m ? r.e : -1;
+    const double xsig = xrow >= 0 ? unit_sign(d, r.var, xrow) : 0.0;
+    if (blockIdx.x == 0 && tid == 0) {
+        const int lv = loc_of(d, r.var);
+        c->dr_var = r.var;
+        c->dr_e = r.e;
+        c->dr_s = r.s;
+        c->dr_xrow = xrow;
+        c->dr_x = r.x;
+        c->dr_beta = r.beta;
+        c->dr_lb = d.lb[lv];
+        c->dr_ub = d.ub[lv];
+        c->dr_w = d.dw[lv];
+        c->dr_xsig = xsig;
+    }
+    double* asrow = lds_row ? asrow_lds : d.vrow;  // (huge bumps: every workgroup writes the same values)
+    if (xrow >= 0) {
+        for (int p = tid; p < k; p += 256) asrow[p] = d.AS[(size_t)p * (size_t)m + xrow];
+        __syncthreads();
+    }
+    const int lrp = r.e - m;  // (bump position of a leaving structural)
+    for (int cc = blockIdx.x * 4 + (tid >> 6); cc < k; cc += gridDim.x * 4) {
+        double v;
+        if (xrow >= 0) {
+            double acc = lane_chain(d.MinvT + (size_t)cc * d.ldm, asrow, k);
+            acc = wave_tree(acc);
+            v = -(xsig * acc);
+        } else {
+            v = d.Minv[(size_t)lrp * d.ldm + cc];
+        }
+        if (lane == 0) {
+            d.rhoR[cc] = v;
+            const int slot = d.ypos[d.Rl[cc]];  // (R = Y in the dual phase: every R row has a slot)
+            if (slot >= 0) d.rr[slot] = v;
+        }
+    }
+}
+
+// a priced column's ratio-test record (oracle run_dual): side +1 acts at its
+// lower bound (needs ah < -tol_pivot), -1 at its upper (ah > tol_pivot)
+DEV bool dual_candidate(int8_t vs, double a, double dj, double lb, double ub, int rs, int bland, double dtol,
+                        double pivtol, int j, DualCand& o) {
+    if (vs == VS_BASIC || vs == VS_FIXED) return false;
+    const double ah = rs * a;
+    int side = 0;
+    if (vs == VS_LOWER || (vs == VS_FREE && ah < 0.0)) side = ah < -pivtol ? 1 : 0;
+    else if (vs == VS_UPPER || (vs == VS_FREE && ah > 0.0)) side = ah > pivtol ? -1 : 0;
+    if (!side) return false;
+    o.t = side > 0 ? dj / (-ah) : (-dj) / ah;
+    o.b = bland ? o.t : side > 0 ? (dj + dtol) / (-ah) : (dtol - dj) / ah;
+    o.a = a;
+    o.r = (lb > -HUGE_VAL && ub < HUGE_VAL) ? ub - lb : HUGE_VAL;
+    o.d = dj;
+    o.j = j;
+    o.side = side;
+    return true;
+}
+
+// ordered emission of a workgroup's candidates into its region: `flag` per
+// thread in thread order (plus a second one right behind it: two columns per
+// lane), counts per wave in LDS
+template <int NT>
+DEV void emit_region(const Dev& d, int region, bool f0, const DualCand& c0, bool f1, const DualCand& c1,
+                     int* wcnt) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long b0 = __ballot(f0), b1 = __ballot(f1);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const int before = __popcll(b0 & below) + __popcll(b1 & below);
+    if (lane == 0) wcnt[w] = __popcll(b0) + __popcll(b1);
+    __syncthreads();
+    int off = 0, tot = 0;
+    for (int i = 0; i < NT / 64; ++i) {
+        if (i < w) off += wcnt[i];
+        tot += wcnt[i];
+    }
+    DualCand* base = d.dcand + (size_t)region * DREG;
+    if (f0) base[off + before] = c0;
+    if (f1) base[off + before + (f0 ? 1 : 0)] = c1;
+    if (threadIdx.x == 0) d.dcnt[region] = tot;
+}
+
+// the slack columns of the Y rows (cost 0: d = -y, alpha = rho on the slot)
+template <int NT>
+DEV void dual_slacks(const Dev& d, int region, int s, int nsw, int* wcnt) {
+    const DevCtl* c = d.ctl;
+    const int ny = c->ny, bland = c->bland, rs = c->dr_s;
+    const double dtol = c->tol_dual, pivtol = c->tol_pivot;
+    const int p = s * NT + threadIdx.x;  // (the host sizes nsw for one slot per thread)
+    DualCand o;
+    bool f = false;
+    if (p < ny) {
+        const int8_t v = d.yvs[p];
+        const int i = d.Yl[p];
+        const int sv = d.n + i;
+        f = dual_candidate(v, d.rr[p], 0.0 - d.yy[p], d.lb[sv], d.ub[sv], rs, bland, dtol, pivtol, d.N + i, o);
+    }
+    emit_region<NT>(d, region, f, o, false, o, wcnt);
+}
+
+// Dense pivot row + pricing: one sweep of the tile's Y rows with both y and
+// rho (wave w: slot class p = w mod 4, fma chains in slot order; the classes
+// added in order), then wave 0 finishes columns 2 lane, 2 lane + 1: d_j,
+// alpha_j (+ sigma a_ij of a covered leaving row i, last), the candidates.
+// Grid: [nsw slack workgroups][ntiles tiles].
+__global__ void __launch_bounds__(PRICE_THREADS) k_dual_price(Dev d, int nsw) {
+    __shared__ double pd[PRICE_SPLIT][TILE_COLS], pa[PRICE_SPLIT][TILE_COLS];
+    __shared__ int wcnt[PRICE_SPLIT];
+    const DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    if ((int)blockIdx.x < nsw) {
+        dual_slacks<PRICE_THREADS>(d, d.ntiles + blockIdx.x, blockIdx.x, nsw, wcnt);
+        return;
+    }
+    const int64_t tile = (int64_t)blockIdx.x - nsw;
+    const int tw = d.tile_w, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int ny = c->ny;
+    const int lcol = 2 * lane < tw ? 2 * lane : ((tw - 1) & ~1);
+    const double* col = d.AR + (size_t)tile * (size_t)d.arcap * (size_t)tw + lcol;
+    double d0 = 0.0, d1 = 0.0, a0 = 0.0, a1 = 0.0;
+    constexpr int U = 8;
+    int p = w;
+    for (; p + PRICE_SPLIT * (U - 1) < ny; p += PRICE_SPLIT * U) {
+        dbl2 v[U];
+        double yv[U], rv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            v[u] = *reinterpret_cast<const dbl2*>(col + (size_t)(p + PRICE_SPLIT * u) * (size_t)tw);
+            yv[u] = d.yy[p + PRICE_SPLIT * u];
+            rv[u] = d.rr[p + PRICE_SPLIT * u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            d0 = fma(v[u].x, yv[u], d0);
+            d1 = fma(v[u].y, yv[u], d1);
+            a0 = fma(v[u].x, rv[u], a0);
+            a1 = fma(v[u].y, rv[u], a1);
+        }
+    }
+    for (; p < ny; p += PRICE_SPLIT) {
+        const dbl2 v = *reinterpret_cast<const dbl2*>(col + (size_t)p * (size_t)tw);
+        const double yv = d.yy[p], rv = d.rr[p];
+        d0 = fma(v.x, yv, d0);
+        d1 = fma(v.y, yv, d1);
+        a0 = fma(v.x, rv, a0);
+        a1 = fma(v.y, rv, a1);
+    }
+    pd[w][2 * lane] = d0;
+    pd[w][2 * lane + 1] = d1;
+    pa[w][2 * lane] = a0;
+    pa[w][2 * lane + 1] = a1;
+    __syncthreads();
+    if (w != 0) {
+        __syncthreads();  // (emit_region's barrier)
+        return;
+    }
+    const int xrow = c->dr_xrow, rs = c->dr_s, bland = c->bland;
+    const double xsig = c->dr_xsig, dtol = c->tol_dual, pivtol = c->tol_pivot;
+    DualCand o[2];
+    bool f[2] = {false, false};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int64_t j = tile * tw + 2 * lane + h;
+        if (2 * lane + h >= tw || j >= d.n) continue;
+        const int8_t vs = d.vstat[j];
+        if (vs == VS_BASIC || vs == VS_FIXED) continue;
+        double td = 0.0, ta = 0.0;
+#pragma unroll
+        for (int ww = 0; ww < PRICE_SPLIT; ++ww) {
+            td = td + pd[ww][2 * lane + h];
+            ta = ta + pa[ww][2 * lane + h];
+        }
+        const double dj = d.cost[j] - td;
+        const double aj = xrow >= 0 ? fma(xsig, a_row(d, xrow, j), ta) : ta;
+        f[h] = dual_candidate(vs, aj, dj, d.lb[j], d.ub[j], rs, bland, dtol, pivtol, (int)(d.col0 + j), o[h]);
+    }
+    emit_region<64>(d, (int)tile, f[0], o[0], f[1], o[1], wcnt);
+}
+
+// CSC pivot row + pricing: one column chain per thread over its nonzeros in
+// ascending rows with the dense y and rho (rho_i from the bump positions
+// through rpos, sigma on a covered leaving row)
+__global__ void __launch_bounds__(TILE_COLS) k_dual_price_csc(Dev d, int nsw) {
+    __shared__ int wcnt[TILE_COLS / 64];
+    const DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    if ((int)blockIdx.x < nsw) {
+        dual_slacks<TILE_COLS>(d, d.ntiles + blockIdx.x, blockIdx.x, nsw, wcnt);
+        return;
+    }
+    const int64_t tile = (int64_t)blockIdx.x - nsw;
+    const int64_t j = tile * TILE_COLS + threadIdx.x;
+    const int xrow = c->dr_xrow, rs = c->dr_s, bland = c->bland;
+    const double xsig = c->dr_xsig, dtol = c->tol_dual, pivtol = c->tol_pivot;
+    DualCand o;
+    bool f = false;
+    if (j < d.n) {
+        const int8_t vs = d.vstat[j];
+        if (vs != VS_BASIC && vs != VS_FIXED) {
+            double ad = 0.0, aa = 0.0;
+            for (int64_t t = d.cptr[j]; t < d.cptr[j + 1]; ++t) {
+                const int i = d.rind[t];
+                const double v = d.cval[t];
+                const int rp = d.rpos[i];
+                const double rho = rp >= 0 ? d.rhoR[rp] : (i == xrow ? xsig : 0.0);
+                ad = fma(v, d.y[i], ad);
+                aa = fma(v, rho, aa);
+            }
+            f = dual_candidate(vs, aa, d.cost[j] - ad, d.lb[j], d.ub[j], rs, bland, dtol, pivtol, (int)j, o);
+        }
+    }
+    emit_region<TILE_COLS>(d, (int)tile, f, o, false, o, wcnt);
+}
+
+// exclusive block scan of one int per thread (NT threads); returns the total
+template <int NT>
+DEV int block_scan_excl(int v, int* excl, int* lds) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int u = __shfl_up(incl, off);
+        if (lane >= off) incl += u;
+    }
+    if (lane == 63) lds[w] = incl;
+    __syncthreads();
+    int base = 0, tot = 0;
+    for (int i = 0; i < NT / 64; ++i) {
+        if (i < w) base += lds[i];
+        tot += lds[i];
+    }
+    __syncthreads();
+    *excl = base + incl - v;
+    return tot;
+}
+
+// Bound-flipping Harris ratio test (oracle run_dual), one workgroup: compacts
+// the regions' candidates (region order = ascending structural id, then the
+// slacks), then takes bunches -- the live candidates whose exact ratio is
+// within the smallest Harris bound -- flipping a bunch while all of it is boxed
+// and the slope (x_r's infeasibility) stays positive past the sum of its
+// |alpha| (u - l) in ascending id, else letting the bunch's largest |alpha|
+// enter (Bland: the smallest ratio).  Each thread owns a contiguous run of the
+// compacted candidates, so ordered compactions are one block scan.
+constexpr int BF_NT = 1024;
+__global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg) {
+    __shared__ int scan_lds[BF_NT / 64];
+    __shared__ double red[BF_NT / 64];
+    __shared__ int s_int[4];
+    __shared__ double s_dbl[2];
+    DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    const int tid = threadIdx.x;
+    const int bland = c->bland;
+    // ---- compaction: region counts scanned in chunks of BF_NT regions
+    int total = 0;
+    for (int r0 = 0; r0 < nreg; r0 += BF_NT) {
+        const int r = r0 + tid;
+        const int cnt = r < nreg ? d.dcnt[r] : 0;
+        int excl;
+        const int tot = block_scan_excl<BF_NT>(cnt, &excl, scan_lds);
+        if (r < nreg) {
+            const DualCand* src = d.dcand + (size_t)r * DREG;
+            for (int t = 0; t < cnt; ++t) d.dcomp[total + excl + t] = src[t];
+        }
+        total += tot;
+    }
+    __syncthreads();  // (the compacted array is read by other threads below)
+    const int N = total;
+    const int run = (N + BF_NT - 1) / BF_NT;  // this thread's candidates [lo, hi)
+    const int lo = min(N, tid * run), hi = min(N, lo + run);
+    for (int t = lo; t < hi; ++t) d.dalive[t] = 1;
+    double slope = fabs(c->dr_x - c->dr_beta);
+    const double INF = HUGE_VAL;
+    int nflip = 0, qidx = -1;
+    for (;;) {
+        // smallest Harris bound among the live candidates
+        double bmin = INF;
+        int live = 0;
+        for (int t = lo; t < hi; ++t)
+            if (d.dalive[t]) {
+                live = 1;
+                bmin = fmin(bmin, d.dcomp[t].b);
+            }
+        const double thmax = block_min<BF_NT>(bmin, red);
+        if (tid == 0) s_int[0] = 0;
+        __syncthreads();
+        if (live) s_int[0] = 1;
+        __syncthreads();
+        if (!s_int[0]) break;  // nothing left: the dual ray (q = -1)
+        // the bunch, in order, into dflip[nflip ...) (a flip list in the making)
+        int cnt = 0, allbox = 1;
+        for (int t = lo; t < hi; ++t)
+            if (d.dalive[t] && d.dcomp[t].t <= thmax) {
+                cnt++;
+                if (d.dcomp[t].r == INF) allbox = 0;
+            }
+        int excl;
+        const int nq = block_scan_excl<BF_NT>(cnt, &excl, scan_lds);
+        if (tid == 0) s_int[1] = 1;
+        __syncthreads();
+        if (!allbox) s_int[1] = 0;
+        for (int t = lo, o = nflip + excl; t < hi; ++t)
+            if (d.dalive[t] && d.dcomp[t].t <= thmax) d.dflip[o++] = t;  // (compact index for now)
+        __syncthreads();
+        if (tid == 0) {  // |alpha| (u - l) summed in ascending id (the bunch's order)
+            double sum = 0.0;
+            if (s_int[1])
+                for (int t = 0; t < nq; ++t) {
+                    const DualCand& o = d.dcomp[d.dflip[nflip + t]];
+                    sum = fma(fabs(o.a), o.r, sum);
+                }
+            s_dbl[0] = sum;
+        }
+        __syncthreads();
+        const double sum = s_dbl[0];
+        if (nq == 0) break;  // (NaN ratios only: no candidate qualifies -- the ray)
+        if (s_int[1] && sum < slope) {  // flip the bunch
+            slope = slope - sum;
+            for (int t = nflip + tid; t < nflip + nq; t += BF_NT) d.dalive[d.dflip[t]] = 0;
+            nflip += nq;
+            __syncthreads();
+            continue;
+        }
+        // the bunch's best enters: largest |alpha| (Bland: smallest ratio), lowest id
+        int best = -1;
+        for (int t = nflip + tid; t < nflip + nq; t += BF_NT) {
+            const int ci = d.dflip[t];
+            if (best < 0) {
+                best = ci;
+                continue;
+            }
+            const DualCand& o = d.dcomp[ci];
+            const DualCand& b = d.dcomp[best];
+            const bool take = bland ? (o.t < b.t || (o.t == b.t && o.j < b.j))
+                                    : (fabs(o.a) > fabs(b.a) || (fabs(o.a) == fabs(b.a) && o.j < b.j));
+            if (take) best = ci;
+        }
+        // block argmax in the same total order (candidate indices through LDS)
+        __shared__ int s_best[BF_NT];
+        s_best[tid] = best;
+        __syncthreads();
+        for (int h = BF_NT / 2; h >= 1; h >>= 1) {
+            if (tid < h) {
+                const int x = s_best[tid], y = s_best[tid + h];
+                if (x < 0) s_best[tid] = y;
+                else if (y >= 0) {
+                    const DualCand& o = d.dcomp[y];
+                    const DualCand& b = d.dcomp[x];
+                    const bool take = bland ? (o.t < b.t || (o.t == b.t && o.j < b.j))
+                                            : (fabs(o.a) > fabs(b.a) || (fabs(o.a) == fabs(b.a) && o.j < b.j));
+                    if (take) s_best[tid] = y;
+                }
+            }
+            __syncthreads();
+        }
+        qidx = s_best[0];
+        break;
+    }
+    __syncthreads();
+    // the flips: compact indices -> ids and dx (before their status changes)
+    for (int t = tid; t < nflip; t += BF_NT) {
+        const DualCand o = d.dcomp[d.dflip[t]];
+        const int jl = loc_of(d, o.j);
+        const double l = d.lb[jl], u = d.ub[jl];
+        const bool at_lower = o.side > 0;  // (boxed columns act at their current bound)
+        d.dflipdx[t] = at_lower ? u - l : l - u;
+        d.dflip[t] = o.j;
+    }
+    __syncthreads();
+    for (int t = tid; t < nflip; t += BF_NT) {
+        const int jl = loc_of(d, d.dflip[t]);
+        const bool up = d.dflipdx[t] > 0.0;
+        d.vstat[jl] = up ? VS_UPPER : VS_LOWER;
+        d.xval[jl] = up ? d.ub[jl] : d.lb[jl];
+    }
+    if (tid != 0) return;
+    const int64_t it = c->iter;
+    if (qidx < 0) {  // dual unbounded: the LP is infeasible (oracle: trace -2, the leaving variable)
+        c->iter = it + 1;
+        c->phase1_iters++;
+        c->dual_iters++;
+        if (it < c->trace_cap) {
+            d.trace[2 * it] = -2;
+            d.trace[2 * it + 1] = c->dr_var;
+        }
+        c->nflip = 0;
+        c->status = ST_DUALINF;
+        return;
+    }
+    const DualCand q = d.dcomp[qidx];
+    c->q = q.j;
+    c->dq = q.d;
+    c->wq = 1.0;
+    c->sig = q.side > 0 ? 1.0 : -1.0;
+    c->dq_t = q.t;
+    c->nflip = nflip;
+    c->flips += nflip;
+    Cand e;
+    e.score = 1.0;
+    e.d = q.d;
+    e.w = 1.0;
+    e.j = q.j;
+    d.cand[0] = e;
+    // (statistics: the pricing pass and the whole iteration's bytes)
+    const double kk = (double)c->k, mm = (double)d.m;
+    const double pb = price_pass_bytes(d, c->ny, 0) + 8.0 * (double)c->ny;  // (+ rho on the slots)
+    c->price_bytes += pb;
+    c->price_passes++;
+    c->iter_bytes += pb + 48.0 * kk * kk + 8.0 * mm * kk * (nflip > 0 ? 2.0 : 1.0) + 16.0 * (double)d.n + 16.0 * mm;
+}
+
+// a_F = sum over the flips (in list order) of a_j dx_j: dense, one row per
+// thread (the oracle's per-row fma chain); CSC, one workgroup scattering the
+// flipped columns one after the other (rows of a column are distinct, so each
+// row sees the same chain)
+__global__ void __launch_bounds__(256) k_dual_flip_col(Dev d) {
+    const DevCtl* c = d.ctl;
+    const int nf = c->nflip;
+    if (c->status != ST_RUN || nf == 0) return;
+    const int m = d.m;
+    if (d.csc) {
+        for (int i = threadIdx.x; i < m; i += blockDim.x) d.aF[i] = 0.0;
+        __syncthreads();
+        for (int f = 0; f < nf; ++f) {
+            const int j = d.dflip[f];
+            const double dx = d.dflipdx[f];
+            for (int64_t t = d.cptr[j] + threadIdx.x; t < d.cptr[j + 1]; t += blockDim.x) {
+                const int i = d.rind[t];
+                d.aF[i] = fma(d.cval[t], dx, d.aF[i]);
+            }
+            __syncthreads();
+        }
+        return;
+    }
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    double acc = 0.0;
+    for (int f = 0; f < nf; ++f) {
+        const int j = d.dflip[f];
+        acc = fma(sca(d, d.A[(size_t)(j - d.col0) * (size_t)m + i], i, j), d.dflipdx[f], acc);
+    }
+    d.aF[i] = acc;
+}
+
+// fS = Minv a_F[R] (one wave per bump row, wave order)
+__global__ void __launch_bounds__(256) k_dual_flip_bump(Dev d, int lds_row) {
+    extern __shared__ __attribute__((aligned(16))) double afr_lds[];
+    const DevCtl* c = d.ctl;
+    if (c->status != ST_RUN || c->nflip == 0) return;
+    const int k = c->k;
+    double* afr = lds_row ? afr_lds : d.zz;  // (huge bumps: every workgroup writes the same values)
+    for (int p = threadIdx.x; p < k; p += 256) afr[p] = d.aF[d.Rl[p]];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    for (int p = blockIdx.x * 4 + (threadIdx.x >> 6); p < k; p += gridDim.x * 4) {
+        double acc = lane_chain(d.Minv + (size_t)p * d.ldm, afr, k);
+        acc = wave_tree(acc);
+        if (lane == 0) d.fS[p] = acc;
+    }
+}
+
+// x_B -= B^-1 a_F: covered rows x -= sigma (a_F,i - A[i,S] fS) (zchunk order),
+// bump positions x -= fS
+__global__ void __launch_bounds__(256) k_dual_flip_apply(Dev d) {
+    const DevCtl* c = d.ctl;
+    if (c->status != ST_RUN || c->nflip == 0) return;
+    const int m = d.m, k = c->k;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t < m) {
+        const int u = d.cover[t];
+        if (u < 0) return;
+        double tot = 0.0;
+        for (int c0 = 0; c0 < k; c0 += ZCHUNK) {
+            double acc = 0.0;
+            const int c1 = min(k, c0 + ZCHUNK);
+            for (int p = c0; p < c1; ++p) acc = fma(d.AS[(size_t)p * (size_t)m + t], d.fS[p], acc);
+            tot = tot + acc;
+        }
+        d.xr[t] = d.xr[t] - unit_sign(d, u, t) * (d.aF[t] - tot);
+    } else if (t - m < k) {
+        d.xs[t - m] = d.xs[t - m] - d.fS[t - m];
+    }
+}
+
 // ============================================================== launchers
 static inline unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
 
@@ -3551,7 +4269,7 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     }
     // ratio test + (cases B/D) B^-1 row: one workgroup per 4 bump columns;
     // phase 2 adds the AR-copy workgroups and defers the rest of the update
-    const int defer = phase == 2;
+    const int defer = phase == 2;  // (phase 3, the dual: applied right away by k_update)
     {
         const size_t lds = (size_t)k_ub * sizeof(double);
         const int lds_row = lds <= 48 * 1024 && !d.force_select;
@@ -3576,8 +4294,12 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
         //  loop after the decision -- 16 per lane measured slower at 10 000 x
         //  500 000 (16.5 vs 14.7 us, r01), 10 as well (12.01 vs 11.75 us at k
         //  529, r03 A/B over the last 2000 iterations))
-        k_ratio<8><<<nmain + nar, 256, lds_row ? lds : 0, st>>>(DEV_ARG(d), phase, nrt + nbt, lds_row, defer, (int)nmain,
-                                                               k_ub, dslot, nrt + nbt * zw);
+        if (phase == 3)
+            k_ratio<8, true><<<nmain, 256, lds_row ? lds : 0, st>>>(DEV_ARG(d), 2, nrt + nbt, lds_row, 0, (int)nmain, k_ub,
+                                                                   dslot, nrt + nbt * zw);
+        else
+            k_ratio<8><<<nmain + nar, 256, lds_row ? lds : 0, st>>>(DEV_ARG(d), phase, nrt + nbt, lds_row, defer,
+                                                                   (int)nmain, k_ub, dslot, nrt + nbt * zw);
     }
     if (!defer) {
         unsigned nb_minv, nb;
@@ -3606,13 +4328,54 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
         // last 4 000 iterations of 10 000 x 500 000, k 529; 16 measured no faster
         // there, r01 -- fewer waves per SIMD), else the row is read after a_R
         if (k_ub > 512 && k_ub <= 640)
-            k_select_ftran<10><<<g, 256, ldsz, st>>>(DEV_ARG(d), ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz);
+            k_select_ftran<10><<<g, 256, ldsz, st>>>(DEV_ARG(d), ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz, 0);
         else
-            k_select_ftran<8><<<g, 256, ldsz, st>>>(DEV_ARG(d), ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz);
+            k_select_ftran<8><<<g, 256, ldsz, st>>>(DEV_ARG(d), ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz, 0);
         return launch_iteration_tail(d, k_ub, phase, st, false, dslot, nqz > 0 ? 1 : 0);
     }
-    k_select<<<1, 1024, 0, st>>>(d, ntiles, nsw);
+    k_select<<<1, 1024, 0, st>>>(d, ntiles, nsw, 0);
     return launch_iteration_tail(d, k_ub, phase, st, true, dslot);
+}
+
+hipError_t launch_dual_setup_cols(const Dev& d, hipStream_t st) {
+    if (d.n > 0) k_dual_setup_cols<<<cdiv(d.n, 256), 256, 0, st>>>(d);
+    return hipGetLastError();
+}
+
+hipError_t launch_dual_init_rows(const Dev& d, hipStream_t st) {
+    if (d.m > 0) k_dual_init_rows<<<cdiv(d.m, 256), 256, 0, st>>>(d);
+    return hipGetLastError();
+}
+
+hipError_t launch_dual_iteration(const Dev& d, int k_ub, int ny_ub, hipStream_t st) {
+    const int m = d.m;
+    const unsigned nchz = cdiv((int64_t)m + k_ub, 256);
+    k_dual_chuzr<<<nchz, 256, 0, st>>>(d);
+    const size_t lds = (size_t)k_ub * sizeof(double);
+    const int lds_row = lds <= 48 * 1024;
+    unsigned nrw = cdiv(k_ub > 0 ? k_ub : 1, 4);
+    if (nrw > 1024) nrw = 1024;
+    k_dual_row<<<nrw, 256, lds_row ? lds : 0, st>>>(d, (int)nchz, lds_row);
+    const int nsw = slack_wgs(d, ny_ub);
+    if (d.csc) k_dual_price_csc<<<d.ntiles + nsw, TILE_COLS, 0, st>>>(d, nsw);
+    else k_dual_price<<<d.ntiles + nsw, PRICE_THREADS, 0, st>>>(d, nsw);
+    k_dual_bfrt<<<1, BF_NT, 0, st>>>(d, d.ntiles + nsw);
+    k_dual_flip_col<<<d.csc ? 1u : cdiv(m > 0 ? m : 1, 256), 256, 0, st>>>(d);
+    if (k_ub > 0) k_dual_flip_bump<<<nrw, 256, lds_row ? lds : 0, st>>>(d, lds_row);
+    k_dual_flip_apply<<<cdiv((int64_t)m + k_ub, 256), 256, 0, st>>>(d);
+    // the entering column q (k_dual_bfrt's, candidate 0): a_R, alpha_S (+ staging)
+    if (lds <= 48 * 1024 && !d.force_select) {
+        const size_t ldsz = lds > 64 ? lds : 64;
+        const unsigned nqz = d.qz && !d.csc ? cdiv(m, 256 * QZ_PT) : 0;
+        const unsigned g = nrw + nqz + (d.csc ? 1 : 0);
+        if (k_ub > 512 && k_ub <= 640)
+            k_select_ftran<10><<<g, 256, ldsz, st>>>(DEV_ARG(d), 1, 0, k_ub, 0, (int)nrw, (int)nqz, 1);
+        else
+            k_select_ftran<8><<<g, 256, ldsz, st>>>(DEV_ARG(d), 1, 0, k_ub, 0, (int)nrw, (int)nqz, 1);
+        return launch_iteration_tail(d, k_ub, 3, st, false, 0, nqz > 0 ? 1 : 0);
+    }
+    k_select<<<1, 1024, 0, st>>>(d, 1, 0, 1);
+    return launch_iteration_tail(d, k_ub, 3, st, true, 0);
 }
 
 hipError_t launch_iteration_head(const Dev& d, int k_ub, int ny_ub, int phase, int rank,

@@ -1102,12 +1102,14 @@ static int run_dual(orc_t* s, const orc_control* ctl, int64_t* iter, int64_t max
                 }
             if (!any) break;
             double sum = 0.0;
-            int allbox = 1;
+            int allbox = 1, nq = 0;
             for (int64_t c = 0; c < nc; ++c)
                 if (s->calive[c] && s->ct[c] <= thmax) {
+                    nq++;
                     if (s->cr[c] == INF) allbox = 0;
                     else sum = fma(s->ca[c], s->cr[c], sum);
                 }
+            if (nq == 0) break; /* (NaN ratios only: no candidate qualifies -- the ray) */
             if (allbox && sum < slope) {
                 slope = slope - sum;
                 for (int64_t c = 0; c < nc; ++c)

@@ -1,0 +1,112 @@
+"""GPU dual simplex phase 1 (elp_control.simplex = ELP_SIMPLEX_DUAL_PRIMAL,
+lp_solve's default behind R/class.R:262 lp.control / :276 solve) against the
+oracle's run_dual: on every fixture whose slack basis is infeasible the dual
+walks the oracle's path bit for bit -- pivot trace (entering, leaving; -2 for
+the infeasibility ray), basis, status, objective and x -- dense and CSC,
+Devex and Dantzig; the Netlib-shaped KKT LPs (bound flips) included, and the
+20 000 x 100 000 phase-1 LP the primal never finished solved to the HiGHS
+optimum (tests/golden/sparse_lu.json)."""
+import numpy as np
+import pytest
+
+from conftest import load_known_answers, load_robust_lps, load_sparse_lu, load_sparse_lps
+from fuzz_lps import fuzz_set
+
+pytestmark = pytest.mark.gpu
+
+DUAL = 6
+FUZZ = fuzz_set(120)
+KNOWN = load_known_answers()
+ROBUST = load_robust_lps()
+SPARSE = load_sparse_lps()
+
+
+def _same(g, o, tag):
+    assert g.status == o.status, (tag, g.status, o.status)
+    np.testing.assert_array_equal(g.trace, o.trace, err_msg=tag)
+    assert g.stats["dual_iterations"] == o.stats["dual_iterations"], tag
+    assert g.stats["bound_flips"] == o.stats["bound_flips"], tag
+    if g.status in (0, 1):
+        np.testing.assert_array_equal(g.basis, o.basis, err_msg=tag)
+        assert abs(g.objval - o.objval) <= 1e-12 * max(1.0, abs(o.objval)), tag
+        if len(o.x):
+            np.testing.assert_allclose(g.x, o.x, rtol=1e-12, atol=1e-12 * max(1.0, np.abs(o.x).max()), err_msg=tag)
+
+
+def _run(gpu, rec, sparse=False, rule=1, tag=""):
+    from oracle import solve_dense as orc
+    args = (rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], rec["maximize"])
+    solve = gpu.solve_sparse if sparse else gpu.solve_dense
+    g = solve(*args, trace=100000, simplex=DUAL, pricing=rule, **({"basis": 1} if sparse else {}))
+    o = orc(*args, trace_cap=100000, simplex=DUAL, price_rule=rule, **({"price_mode": 1} if sparse else {}))
+    _same(g, o, tag)
+    return g, o
+
+
+@pytest.mark.parametrize("sparse", [False, True], ids=["dense", "csc"])
+def test_dual_known_and_robust(gpu, sparse):
+    used = 0
+    for rec in KNOWN + ROBUST:
+        g, o = _run(gpu, rec, sparse=sparse, tag=rec["name"])
+        used += o.stats["dual_iterations"] > 0
+        if o.stats["dual_iterations"] > 0:
+            assert g.stats["simplex"] == DUAL
+    assert used >= 8, used
+
+
+@pytest.mark.parametrize("sparse,rule", [(False, 1), (False, 0), (True, 1)], ids=["dense", "dense-dantzig", "csc"])
+def test_dual_fuzz(gpu, sparse, rule):
+    seen, used = set(), 0
+    for rec in FUZZ:
+        g, o = _run(gpu, rec, sparse=sparse, rule=rule, tag=f"f{rec['seed']}_{rec['m']}x{rec['n']}")
+        seen.add(g.status)
+        used += o.stats["dual_iterations"] > 0
+    assert {0, 2, 3} <= seen, seen
+    assert used >= 60, used
+
+
+def test_dual_sparse_fixtures(gpu):
+    for rec in SPARSE:
+        _run(gpu, rec, sparse=True, tag=rec["name"])
+
+
+def _kkt(name):
+    from easylp_amd.synth import sparse_kkt
+    k = next(f for f in load_sparse_lu() if f["name"] == name)
+    cp, ri, v, b, c, u, obj = sparse_kkt(k["seed"], k["m"], k["n"], k["k"], feasible_start=k["feasible_start"])
+    return k, cp, ri, v, b, c, u
+
+
+def test_dual_kkt_2000x10000_matches_oracle(gpu):
+    """Boxed, one column in ten at u in the optimum: bound flips every few
+    pivots; the GPU's flips, trace and optimum are the oracle's."""
+    from easylp_amd.synth import dense_of
+    from oracle import solve_dense as orc
+    k, cp, ri, v, b, c, u = _kkt("kkt_2000x10000")
+    m, n = k["m"], k["n"]
+    dirs, lo = np.ones(m, np.int32), np.zeros(n)
+    with gpu.Problem(m, n, simplex=DUAL, basis=1) as p:
+        p.set_trace(100000)
+        p.load_csc(cp, ri, v, dirs, b, c, lo, u, maximize=True)
+        g = p.solution(p.solve())
+    o = orc(dense_of(cp, ri, v, m, n), dirs, b, c, lo, u, True, simplex=DUAL, price_mode=1, trace_cap=100000)
+    assert o.stats["bound_flips"] > 0
+    _same(g, o, "kkt_2000x10000")
+    assert abs(g.objval - k["highs_objective"]) <= 1e-9 * abs(k["highs_objective"])
+
+
+def test_dual_kkt_20000x100000_optimum(gpu):
+    """the phase-1 Netlib-scale LP (3 455 rows with b < 0) that
+    the primal phase 1 walked ~70 000 pivots on is solved to the HiGHS optimum
+    (1e-8 relative) by the dual phase 1 + primal phase 2."""
+    k, cp, ri, v, b, c, u = _kkt("kkt_20000x100000")
+    m, n = k["m"], k["n"]
+    with gpu.Problem(m, n, simplex=DUAL) as p:
+        p.load_csc(cp, ri, v, np.ones(m, np.int32), b, c, np.zeros(n), u, maximize=True)
+        st = p.solve()
+        s = p.stats()
+        z = p.solution(st).objval
+    assert st == 0
+    assert s["dual_iterations"] > 0 and s["simplex"] == DUAL
+    assert abs(z - k["highs_objective"]) <= 1e-8 * abs(k["highs_objective"]), (z, k["highs_objective"])
+    assert s["iterations"] <= 4 * k["highs_iterations"], s["iterations"]
