@@ -82,8 +82,8 @@ def parse():
     ap.add_argument("--sparse-n", type=int, default=10000)
     ap.add_argument("--sparse-steps", type=int, default=1000)
     ap.add_argument("--sparse-cpu-iters", type=int, default=200)
-    ap.add_argument("--sparse-window", type=int, default=5000,
-                    help="iterations of the phase-1 Netlib-scale LP timed from its start")
+    ap.add_argument("--sparse-window", type=int, default=2000,
+                    help="iterations of the phase-1 Netlib-scale LP's primal phase 1 timed from its start")
     ap.add_argument("--pricing", choices=["devex", "dantzig"], default="devex",
                     help="pricing rule (elp_control.pricing; devex is lp_solve's default)")
     ap.add_argument("--sync-every", type=int, default=32,
@@ -529,23 +529,40 @@ def sparse_rate(args, local, with_cpu):
                                "sample": "oracle/elp_oracle_lu.c (C, -O3, 1 thread) first %d iterations, setup "
                                          "included" % r.stats["iterations"]}
     out["netlib_scale"] = big
-    # ---- the phase-1 LP of the same size: a window from the start ----
+    # ---- the phase-1 LP of the same size: the dual simplex phase 1 (lp_solve's
+    #      SIMPLEX_DUAL_PRIMAL) to optimality; the primal phase 1 on artificials
+    #      (~70 000 pivots) over a window from its start ----
     k = fx["kkt_20000x100000"]
     cp, ri, v, b, c, u, obj = sparse_kkt(k["seed"], k["m"], k["n"], k["k"])
-    with Problem(m, n, device=local, pricing=args.rule) as p:
+    with Problem(m, n, device=local, pricing=args.rule, simplex=6) as p:
+        t0 = time.perf_counter()
+        p.load_csc(cp, ri, v, dirs, b, c, lo, u, maximize=True)
+        st = p.solve()
+        tto = time.perf_counter() - t0
+        s = p.stats()
+        z = p.solution(st).objval
+    out["netlib_scale_phase1"] = {
+        "workload": "sparse LP m=%d n=%d nnz=%d (sparse_kkt: %d rows with b < 0, one column in ten at its "
+                    "upper bound in the optimum), dual simplex phase 1 + primal phase 2" % (
+                        m, n, int(cp[-1]), int((b < 0).sum())),
+        "simplex": "dual-primal" if s["simplex"] == 6 else "primal-primal",
+        "status": st, "objective": z, "objective_highs": k["highs_objective"],
+        "rel_err_vs_highs": abs(z - k["highs_objective"]) / abs(k["highs_objective"]),
+        "iterations_to_optimal": s["iterations"], "dual_iterations": s["dual_iterations"],
+        "bound_flips": s["bound_flips"], "refactors": s["refactors"], "basic_structurals": s["bump_dim"],
+        "time_to_optimal_s": tto, "load_s": s["seconds_load"],
+        "value": s["iterations"] / tto if tto > 0 else None, "unit": "iterations/s (whole solve)",
+        "highs_iterations": k["highs_iterations"]}
+    with Problem(m, n, device=local, pricing=args.rule, simplex=5) as p:
         t0 = time.perf_counter()
         p.load_csc(cp, ri, v, dirs, b, c, lo, u, maximize=True)
         st = p.iterate(args.sparse_window)
         el = time.perf_counter() - t0
         s = p.stats()
-    out["netlib_scale_phase1"] = {
-        "workload": "sparse LP m=%d n=%d nnz=%d (sparse_kkt: %d rows with b < 0, one column in ten at its "
-                    "upper bound in the optimum)" % (m, n, int(cp[-1]), int((b < 0).sum())),
-        "iterations": s["iterations"], "phase1_iterations": s["phase1_iterations"], "status": st,
-        "basic_structurals": s["bump_dim"], "seconds": el, "load_s": s["seconds_load"],
-        "value": s["iterations"] / el if el > 0 else None, "unit": "iterations/s (first iterations, load included)",
-        "note": "not solved to optimality here: ~70 000 primal pivots with up to ~8 800 basic structurals "
-                "(DESIGN.md 9.1); HiGHS dual simplex needs %d" % k["highs_iterations"]}
+    out["netlib_scale_phase1"]["primal_phase1_window"] = {
+        "iterations": s["iterations"], "status": st, "basic_structurals": s["bump_dim"], "seconds": el,
+        "note": "the primal phase 1 on artificials over its first iterations: ~70 000 pivots to optimality "
+                "(DESIGN.md 9.1)"}
     # ---- 1000 x 10 000 packing ----
     m, n = args.sparse_m, args.sparse_n
     cp, ri, v, b, c = sparse_packing(args.seed, m, n, 5)

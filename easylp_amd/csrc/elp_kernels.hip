@@ -3647,7 +3647,7 @@ DEV void dual_slacks(const Dev& d, int region, int s, int nsw, int* wcnt) {
         const int8_t v = d.yvs[p];
         const int i = d.Yl[p];
         const int sv = d.n + i;
-        f = dual_candidate(v, d.rr[p], 0.0 - d.yy[p], d.lb[sv], d.ub[sv], rs, bland, dtol, pivtol, d.N + i, o);
+        f = dual_candidate(v, d.rr[p], d.cost[sv] - d.yy[p], d.lb[sv], d.ub[sv], rs, bland, dtol, pivtol, d.N + i, o);
     }
     emit_region<NT>(d, region, f, o, false, o, wcnt);
 }
@@ -3792,8 +3792,8 @@ DEV int block_scan_excl(int v, int* excl, int* lds) {
 // the regions' candidates (region order = ascending structural id, then the
 // slacks), then takes bunches -- the live candidates whose exact ratio is
 // within the smallest Harris bound -- flipping a bunch while all of it is boxed
-// and the slope (x_r's infeasibility) stays positive past the sum of its
-// |alpha| (u - l) in ascending id, else letting the bunch's largest |alpha|
+// and the slope (x_r's infeasibility) stays above tol_primal past the sum of
+// its |alpha| (u - l) in ascending id, else letting the bunch's largest |alpha|
 // enter (Bland: the smallest ratio).  Each thread owns a contiguous run of the
 // compacted candidates, so ordered compactions are one block scan.
 constexpr int BF_NT = 1024;
@@ -3869,7 +3869,7 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg) {
         __syncthreads();
         const double sum = s_dbl[0];
         if (nq == 0) break;  // (NaN ratios only: no candidate qualifies -- the ray)
-        if (s_int[1] && sum < slope) {  // flip the bunch
+        if (s_int[1] && sum < slope - c->tol_primal) {  // flip the bunch (x_r still out past it)
             slope = slope - sum;
             for (int t = nflip + tid; t < nflip + nq; t += BF_NT) d.dalive[d.dflip[t]] = 0;
             nflip += nq;

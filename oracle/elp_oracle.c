@@ -896,6 +896,61 @@ static int run_phase(orc_t* s, int phase, const orc_control* ctl, int64_t* iter,
     }
 }
 
+/* The dual's pricing pass (run_dual, warm_core): ONE sweep of the Y rows
+ * (PRICE_SPLIT slot classes, the pricing order) for d_j = c_j - y'a_j and the
+ * pivot row alpha_j = rho'a_j, the covered leaving row xrow's own entry added
+ * last; CSC (price_mode 1): column chains over the dense y and rho.  Slacks:
+ * d = c - y_i, alpha = rho_i.  Results in dvec / avec (n + m). */
+static void dual_sweep(orc_t* s, const orc_control* ctl, orc_stats* st, int64_t xrow, double xsig) {
+    const int64_t m = s->m, n = s->n;
+    const int64_t ny = s->ny;
+    for (int64_t p = 0; p < ny; ++p) {
+        s->yy[p] = s->y[s->Yl[p]];
+        s->rhoY[p] = s->rho[s->Yl[p]];
+    }
+    if (ctl->price_mode == 1) {
+        for (int64_t j = 0; j < n; ++j) {
+            const double* col = Acol(s, j, s->colbuf);
+            double ad = 0.0, aa = 0.0;
+            for (int64_t t = s->cp[j]; t < s->cp[j + 1]; ++t) { /* ascending rows */
+                ad = fma(col[s->ri[t]], s->y[s->ri[t]], ad);
+                aa = fma(col[s->ri[t]], s->rho[s->ri[t]], aa);
+            }
+            s->dvec[j] = s->cost[j] - ad;
+            s->avec[j] = aa;
+        }
+        st->price_bytes += 12.0 * (double)s->nnz + 17.0 * (double)n;
+    } else {
+        for (int w = 0; w < PRICE_SPLIT; ++w) {
+            double* pw = s->part + (size_t)w * (size_t)n;
+            double* qw = s->apart + (size_t)w * (size_t)n;
+            for (int64_t j = 0; j < n; ++j) pw[j] = qw[j] = 0.0;
+            for (int64_t p = w; p < ny; p += PRICE_SPLIT) {
+                const double yp = s->yy[p], rp = s->rhoY[p];
+                const double* row = s->AR + (size_t)p * (size_t)n;
+                for (int64_t j = 0; j < n; ++j) {
+                    pw[j] = fma(row[j], yp, pw[j]);
+                    qw[j] = fma(row[j], rp, qw[j]);
+                }
+            }
+        }
+        for (int64_t j = 0; j < n; ++j) {
+            double td = 0.0, ta = 0.0;
+            for (int w = 0; w < PRICE_SPLIT; ++w) {
+                td = td + s->part[(size_t)w * (size_t)n + (size_t)j];
+                ta = ta + s->apart[(size_t)w * (size_t)n + (size_t)j];
+            }
+            s->dvec[j] = s->cost[j] - td;
+            s->avec[j] = xrow >= 0 ? fma(xsig, Aat(s, xrow, j), ta) : ta;
+        }
+        st->price_bytes += 8.0 * ((double)ny * (double)n + (double)n + (double)ny);
+    }
+    for (int64_t i = 0; i < m; ++i) {
+        s->dvec[n + i] = s->cost[n + i] - s->y[i];
+        s->avec[n + i] = s->rho[i];
+    }
+}
+
 /* ------------------------------------------------------------------ */
 /* dual simplex phase 1 (lp_solve's default SIMPLEX_DUAL_PRIMAL: the dual */
 /* simplex while the basis is primal infeasible, then the primal; reached */
@@ -1020,52 +1075,7 @@ static int run_dual(orc_t* s, const orc_control* ctl, int64_t* iter, int64_t max
         for (int64_t c = 0; c < k; ++c) s->rho[s->Rl[c]] = s->v[c];
         if (xrow >= 0) s->rho[xrow] = xsig;
         /* ---- one sweep: d_j (y) and alpha_j (rho) ---- */
-        const int64_t ny = s->ny;
-        for (int64_t p = 0; p < ny; ++p) {
-            s->yy[p] = s->y[s->Yl[p]];
-            s->rhoY[p] = s->rho[s->Yl[p]];
-        }
-        if (ctl->price_mode == 1) {
-            for (int64_t j = 0; j < n; ++j) {
-                const double* col = Acol(s, j, s->colbuf);
-                double ad = 0.0, aa = 0.0;
-                for (int64_t t = s->cp[j]; t < s->cp[j + 1]; ++t) { /* ascending rows */
-                    ad = fma(col[s->ri[t]], s->y[s->ri[t]], ad);
-                    aa = fma(col[s->ri[t]], s->rho[s->ri[t]], aa);
-                }
-                s->dvec[j] = s->cost[j] - ad;
-                s->avec[j] = aa;
-            }
-            st->price_bytes += 12.0 * (double)s->nnz + 17.0 * (double)n;
-        } else {
-            for (int w = 0; w < PRICE_SPLIT; ++w) {
-                double* pw = s->part + (size_t)w * (size_t)n;
-                double* qw = s->apart + (size_t)w * (size_t)n;
-                for (int64_t j = 0; j < n; ++j) pw[j] = qw[j] = 0.0;
-                for (int64_t p = w; p < ny; p += PRICE_SPLIT) {
-                    const double yp = s->yy[p], rp = s->rhoY[p];
-                    const double* row = s->AR + (size_t)p * (size_t)n;
-                    for (int64_t j = 0; j < n; ++j) {
-                        pw[j] = fma(row[j], yp, pw[j]);
-                        qw[j] = fma(row[j], rp, qw[j]);
-                    }
-                }
-            }
-            for (int64_t j = 0; j < n; ++j) {
-                double td = 0.0, ta = 0.0;
-                for (int w = 0; w < PRICE_SPLIT; ++w) {
-                    td = td + s->part[(size_t)w * (size_t)n + (size_t)j];
-                    ta = ta + s->apart[(size_t)w * (size_t)n + (size_t)j];
-                }
-                s->dvec[j] = s->cost[j] - td;
-                s->avec[j] = xrow >= 0 ? fma(xsig, Aat(s, xrow, j), ta) : ta;
-            }
-            st->price_bytes += 8.0 * ((double)ny * (double)n + (double)n + (double)ny);
-        }
-        for (int64_t i = 0; i < m; ++i) {
-            s->dvec[n + i] = s->cost[n + i] - s->y[i];
-            s->avec[n + i] = s->rho[i];
-        }
+        dual_sweep(s, ctl, st, xrow, xsig);
         /* ---- bound-flipping Harris ratio test ---- */
         int64_t nc = 0;
         for (int64_t j = 0; j < n + m; ++j) { /* candidates, ascending id */
@@ -1086,8 +1096,8 @@ static int run_dual(orc_t* s, const orc_control* ctl, int64_t* iter, int64_t max
         }
         /* bunches: the candidates whose exact ratio is within the Harris bound
          * of the ones left are flipped together while every one of them is
-         * boxed and the slope (the primal infeasibility of x_r) stays
-         * positive past them (their |alpha| (u - l) summed in ascending id);
+         * boxed and the slope (the primal infeasibility of x_r) stays above
+         * tol_primal past them (their |alpha| (u - l) summed in ascending id);
          * otherwise the largest |alpha| of the bunch enters */
         double slope = fabs(rx - rbeta);
         int64_t q = -1, nflip = 0;
@@ -1110,7 +1120,7 @@ static int run_dual(orc_t* s, const orc_control* ctl, int64_t* iter, int64_t max
                     else sum = fma(s->ca[c], s->cr[c], sum);
                 }
             if (nq == 0) break; /* (NaN ratios only: no candidate qualifies -- the ray) */
-            if (allbox && sum < slope) {
+            if (allbox && sum < slope - ptol) { /* (x_r still out by more than tol_primal past them) */
                 slope = slope - sum;
                 for (int64_t c = 0; c < nc; ++c)
                     if (s->calive[c] && s->ct[c] <= thmax) {
@@ -1418,7 +1428,7 @@ static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, 
                       const double* rhs, const double* obj, const double* lo, const double* up,
                       int32_t maximize, const orc_control* ctl_in, double* objval, double* xout,
                       double* yout, int64_t* basis, int64_t* trace, int64_t trace_cap,
-                      orc_stats* st_out, double* sens);
+                      orc_stats* st_out, double* sens, orc_t* keep);
 
 int orc_solve_dense_sens(int64_t m, int64_t n, const double* A, const int32_t* dir,
                          const double* rhs, const double* obj, const double* lo,
@@ -1427,7 +1437,7 @@ int orc_solve_dense_sens(int64_t m, int64_t n, const double* A, const int32_t* d
                          int64_t* trace, int64_t trace_cap, orc_stats* st_out, double* sens) {
     if (m > 0 && !A) return -1;
     return solve_core(m, n, A, 0, dir, rhs, obj, lo, up, maximize, ctl_in, objval, xout, yout, basis,
-                      trace, trace_cap, st_out, sens);
+                      trace, trace_cap, st_out, sens, NULL);
 }
 
 int orc_solve_generated(uint64_t seed, int64_t m, int64_t n, const orc_control* ctl, double* objval,
@@ -1440,18 +1450,56 @@ int orc_solve_generated(uint64_t seed, int64_t m, int64_t n, const orc_control* 
     orc_generate_dense(seed, m, n, 0, n, NULL, b, c);
     for (int64_t i = 0; i < m; ++i) dir[i] = 1;
     const int r = solve_core(m, n, NULL, seed, dir, b, c, NULL, NULL, 1, ctl, objval, x, y, basis, trace,
-                             trace_cap, st, NULL);
+                             trace_cap, st, NULL, NULL);
     free(b);
     free(c);
     free(dir);
     return r;
 }
 
+static void free_state(orc_t* s) {
+    free(s->b); free(s->lb); free(s->ub); free(s->cost); free(s->xval); free(s->vstat);
+    free(s->asgn); free(s->cover); free(s->rpos); free(s->Rl); free(s->Sl); free(s->spos);
+    free(s->xr); free(s->xs); free(s->Minv); free(s->Yl); free(s->ypos); free(s->AR);
+    free(s->y); free(s->t); free(s->yR); free(s->yy); free(s->acol); free(s->aR);
+    free(s->alS); free(s->alU); free(s->z); free(s->v); free(s->tmp); free(s->part);
+    free(s->dw); free(s->dprev);
+    free(s->apart); free(s->rho); free(s->rhoY); free(s->dvec); free(s->avec);
+    free(s->cj); free(s->flips); free(s->ct); free(s->cb); free(s->ca); free(s->cr); free(s->aF); free(s->fS);
+    free(s->calive);
+    free(s->used); free(s->perm); free(s->cp); free(s->ri); free(s->nzl); free(s->colbuf);
+    free(s->srow); free(s->scol); free(s->A_copy);
+}
+
+/* get.objective / get.variables (R/class.R:277-278), unscaled exactly
+ * (x_j = 2^scol_j x~_j); unbounded: the ray's variable and the objective +-BIG */
+static void emit_outputs(const orc_t* s, int status, int64_t unb_var, double unb_sigma, int32_t maximize,
+                         const double* obj, double BIG, double* objval, double* xout) {
+    const int64_t n = s->n;
+    if (xout)
+        for (int64_t j = 0; j < n; ++j) {
+            double v = SC_COL(s->vstat[j] == VS_BASIC ? s->xs[s->spos[j]] : s->xval[j], j, 1);
+            if (status == 3 && j == unb_var) v = unb_sigma > 0 ? BIG : -BIG;
+            xout[j] = v;
+        }
+    if (objval) {
+        if (status == 3) *objval = maximize ? BIG : -BIG;
+        else {
+            double acc = 0.0;
+            for (int64_t j = 0; j < n; ++j) {
+                const double v = SC_COL(s->vstat[j] == VS_BASIC ? s->xs[s->spos[j]] : s->xval[j], j, 1);
+                acc = fma(obj[j], v, acc);
+            }
+            *objval = acc;
+        }
+    }
+}
+
 static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, const int32_t* dir,
                       const double* rhs, const double* obj, const double* lo, const double* up,
                       int32_t maximize, const orc_control* ctl_in, double* objval, double* xout,
                       double* yout, int64_t* basis, int64_t* trace, int64_t trace_cap,
-                      orc_stats* st_out, double* sens) {
+                      orc_stats* st_out, double* sens, orc_t* keep) {
     if (m < 0 || n <= 0 || (m > 0 && (!dir || !rhs)) || !obj) return -1;
     for (int64_t i = 0; i < m; ++i)
         if (dir[i] < 1 || dir[i] > 3) return -2;
@@ -1691,24 +1739,7 @@ static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, 
     }
 
     /* ---- outputs (get.objective / get.variables, R/class.R:277-278) ---- */
-    /* (unscaled: x_j = 2^scol_j x~_j, y_i = 2^srow_i y~_i -- exact) */
-    if (xout)
-        for (int64_t j = 0; j < n; ++j) {
-            double v = SC_COL(s->vstat[j] == VS_BASIC ? s->xs[s->spos[j]] : s->xval[j], j, 1);
-            if (status == 3 && j == unb_var) v = unb_sigma > 0 ? BIG : -BIG;
-            xout[j] = v;
-        }
-    if (objval) {
-        if (status == 3) *objval = maximize ? BIG : -BIG;
-        else {
-            double acc = 0.0;
-            for (int64_t j = 0; j < n; ++j) {
-                const double v = SC_COL(s->vstat[j] == VS_BASIC ? s->xs[s->spos[j]] : s->xval[j], j, 1);
-                acc = fma(obj[j], v, acc);
-            }
-            *objval = acc;
-        }
-    }
+    emit_outputs(s, status, unb_var, unb_sigma, maximize, obj, BIG, objval, xout);
     if (yout)
         for (int64_t i = 0; i < m; ++i) yout[i] = SC_ROW(maximize ? -s->y[i] : s->y[i], i, 1);
     if (basis) {
@@ -1729,18 +1760,103 @@ static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, 
     if (st.seconds_at_mark != 0.0) /* -> seconds from the mark to the end */
         st.seconds_at_mark = ((double)t1.tv_sec + 1e-9 * (double)t1.tv_nsec) - st.seconds_at_mark;
     if (st_out) *st_out = st;
+    if (keep) *keep = S; /* the caller's warm_core continues from this state */
+    else free_state(s);
+    return status;
+}
 
-    free(s->b); free(s->lb); free(s->ub); free(s->cost); free(s->xval); free(s->vstat);
-    free(s->asgn); free(s->cover); free(s->rpos); free(s->Rl); free(s->Sl); free(s->spos);
-    free(s->xr); free(s->xs); free(s->Minv); free(s->Yl); free(s->ypos); free(s->AR);
-    free(s->y); free(s->t); free(s->yR); free(s->yy); free(s->acol); free(s->aR);
-    free(s->alS); free(s->alU); free(s->z); free(s->v); free(s->tmp); free(s->part);
-    free(s->dw); free(s->dprev);
-    free(s->apart); free(s->rho); free(s->rhoY); free(s->dvec); free(s->avec);
-    free(s->cj); free(s->flips); free(s->ct); free(s->cb); free(s->ca); free(s->cr); free(s->aF); free(s->fS);
-    free(s->calive);
-    free(s->used); free(s->perm); free(s->cp); free(s->ri); free(s->nzl); free(s->colbuf);
-    free(s->srow); free(s->scol); free(s->A_copy);
+/* Re-solve after a change of the column bounds, from the basis the state's
+ * last solve ended on (MIP node warm start, SIMPLEX_DUAL_PRIMAL; the HIP side's
+ * warm reload in elp_api.hip run_bnb).  The basis stays; costs are the real
+ * ones again; y = B^-T c_B; each nonbasic structural takes the new value of
+ * its bound (a status whose bound is gone moves to the finite one: lower,
+ * else upper, else free; a fixed column sits at lower), boxed columns whose
+ * reduced cost has the wrong sign for their bound move to the other one, and
+ * any other nonbasic column or slack that stays dual infeasible (beyond
+ * tol_dual) has its cost shifted by -d_j for the dual phase; then x_B from b,
+ * the dual phase (which returns at once when x_B is feasible), the real costs,
+ * and the primal phase 2 -- solve_core's sequence after its start. */
+static int warm_core(orc_t* s, const double* lo, const double* up, int32_t maximize, const double* obj,
+                     const orc_control* ctl_in, double* objval, double* xout, orc_stats* st_out) {
+    orc_control ctl = *ctl_in;
+    if (ctl.refactor_period <= 0) ctl.refactor_period = 250;
+    if (ctl.degen_switch <= 0) ctl.degen_switch = 50;
+    const int64_t m = s->m, n = s->n;
+    const int64_t max_iter = ctl.max_iter > 0 ? ctl.max_iter : 100 * (m + n) + 10000;
+    const double INF = HUGE_VAL, BIG = ctl.infinity, dtol = ctl.tol_dual;
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    orc_stats st;
+    memset(&st, 0, sizeof st);
+    int status = 0;
+    int64_t iter = 0, unb_var = -1;
+    double unb_sigma = 0.0;
+    for (int64_t j = 0; j < n; ++j) {
+        double l = lo ? lo[j] : 0.0, u = up ? up[j] : INF;
+        if (l <= -BIG) l = -INF;
+        if (u >= BIG) u = INF;
+        s->lb[j] = SC_COL(l, j, -1);
+        s->ub[j] = SC_COL(u, j, -1);
+        if (s->lb[j] > s->ub[j]) status = 2; /* R/class.R:297-298 */
+        s->cost[j] = SC_COL(maximize ? -obj[j] : obj[j], j, 1);
+    }
+    for (int64_t i = 0; i < m; ++i) s->cost[n + i] = 0.0;
+    if (status == 0) {
+        btran(s, 2);
+        for (int64_t i = 0; i < m; ++i) s->rho[i] = 0.0;
+        dual_sweep(s, &ctl, &st, -1, 0.0);
+        for (int64_t j = 0; j < n + m; ++j) {
+            int8_t vs = s->vstat[j];
+            if (vs == VS_BASIC) continue;
+            const double l = s->lb[j], u = s->ub[j], d = s->dvec[j];
+            if (j < n) {
+                const int lo_ok = l > -INF, up_ok = u < INF;
+                if (l == u) {
+                    s->vstat[j] = VS_LOWER;
+                    s->xval[j] = l;
+                    continue;
+                }
+                if (vs == VS_LOWER && !lo_ok) vs = up_ok ? VS_UPPER : VS_FREE;
+                else if (vs == VS_UPPER && !up_ok) vs = lo_ok ? VS_LOWER : VS_FREE;
+                else if (vs == VS_FREE && (lo_ok || up_ok)) vs = lo_ok ? VS_LOWER : VS_UPPER;
+                if (vs == VS_LOWER && d < -dtol && up_ok) vs = VS_UPPER;
+                else if (vs == VS_UPPER && d > dtol && lo_ok) vs = VS_LOWER;
+                s->vstat[j] = vs;
+                s->xval[j] = vs == VS_LOWER ? l : vs == VS_UPPER ? u : 0.0;
+            } else if (l == u) {
+                continue;
+            }
+            if ((vs == VS_LOWER && d < -dtol) || (vs == VS_UPPER && d > dtol) || (vs == VS_FREE && fabs(d) > dtol)) {
+                s->cost[j] = s->cost[j] - d;
+                st.flattened++;
+            }
+        }
+        if (refactor(s)) status = 5;
+    }
+    if (status == 0) {
+        int ph = run_dual(s, &ctl, &iter, max_iter, NULL, 0, &st);
+        if (ph == PH_NUMFAIL) status = 5;
+        else if (ph == PH_ITERCAP) status = 1;
+        else if (ph == PH_INFEAS) status = 2;
+    }
+    if (status == 0) {
+        for (int64_t j = 0; j < n; ++j) s->cost[j] = SC_COL(maximize ? -obj[j] : obj[j], j, 1);
+        for (int64_t i = 0; i < m; ++i) s->cost[n + i] = 0.0;
+        if (refactor(s)) status = 5;
+    }
+    if (status == 0) {
+        int ph = run_phase(s, 2, &ctl, &iter, max_iter, NULL, 0, &st, &unb_var, &unb_sigma);
+        if (ph == PH_NUMFAIL) status = 5;
+        else if (ph == PH_ITERCAP) status = 1;
+        else if (ph == PH_UNBOUNDED) status = 3;
+    }
+    emit_outputs(s, status, unb_var, unb_sigma, maximize, obj, BIG, objval, xout);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    st.iterations = iter;
+    st.bump_dim = s->k;
+    st.y_rows = s->ny;
+    st.seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    if (st_out) *st_out = st;
     return status;
 }
 
@@ -1749,7 +1865,9 @@ static int solve_core(int64_t m, int64_t n, const double* A, uint64_t gen_seed, 
 /* binary columns of R/class.R:123-128, set.type at :265).  Rules (shared  */
 /* with the HIP host driver, easylp_amd/csrc/elp_api.hip run_bnb):         */
 /*   integer bounds tightened to ceil(lo - 1e-9) / floor(up + 1e-9);       */
-/*   node LP solved cold; LP unbounded -> MIP status 3; infeasible or      */
+/*   node LP solved cold (SIMPLEX_PRIMAL_PRIMAL) or warm from the last    */
+/*   node's basis (SIMPLEX_DUAL_PRIMAL, warm_core); LP unbounded -> MIP    */
+/*   status 3; infeasible or      */
 /*   numerical failure -> prune; bound test zmin >= best - max(1e-11,      */
 /*   1e-9 |best|) -> prune (zmin: objective in minimisation form);         */
 /*   branch on the lowest-index integer column with |x - round(x)| > 1e-7  */
@@ -1793,6 +1911,12 @@ int orc_solve_mip(int64_t m, int64_t n, const double* A, const int32_t* dir, con
     orc_control nctl;
     if (ctl) nctl = *ctl;
     else orc_default_control(&nctl);
+    /* SIMPLEX_DUAL_PRIMAL: node LPs after the first continue from the basis of
+     * the node solved last (warm_core: the dual simplex repairs the bounds the
+     * branch changed), as lp_solve re-solves B&B nodes from a kept basis */
+    const int warm = simplex_type(&nctl) == 6 && m > 0;
+    orc_t state;
+    int have_state = 0;
     while (top > 0) {
         bnb_node nd = stack[--top];
         if (max_nodes > 0 && nodes >= max_nodes) {
@@ -1809,9 +1933,16 @@ int orc_solve_mip(int64_t m, int64_t n, const double* A, const int32_t* dir, con
         if (ctl && ctl->max_iter > 0 && nctl.max_iter == 0) {
             s = 1;
             memset(&st, 0, sizeof st);
+        } else if (warm && have_state) {
+            s = warm_core(&state, nd.lo, nd.up, maximize, obj, &nctl, &z, x, &st);
         } else {
-            s = orc_solve_dense(m, n, A, dir, rhs, obj, nd.lo, nd.up, maximize, &nctl, &z, x, NULL, NULL,
-                                NULL, 0, &st);
+            s = solve_core(m, n, A, 0, dir, rhs, obj, nd.lo, nd.up, maximize, &nctl, &z, x, NULL, NULL, NULL, 0,
+                           &st, NULL, warm ? &state : NULL);
+            have_state = warm;
+        }
+        if (have_state && s != 0 && s != 2 && s != 3) { /* (a failed node: the next one starts cold) */
+            free_state(&state);
+            have_state = 0;
         }
         iters += st.iterations;
         int branched = 0;
@@ -1893,6 +2024,7 @@ int orc_solve_mip(int64_t m, int64_t n, const double* A, const int32_t* dir, con
             *objval = acc;
         }
     }
+    if (have_state) free_state(&state);
     if (nodes_out) *nodes_out = nodes;
     if (lp_iters_out) *lp_iters_out = iters;
     free(xbest);
