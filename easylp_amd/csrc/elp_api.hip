@@ -145,6 +145,7 @@ struct elp_handle {
     std::vector<size_t> lubcap;
     int64_t lu_nnz_max = 0;
     bool dual_used = false;  // the last load's phase 1 is the dual simplex (phase 3)
+    std::vector<double> mip_x;   // branch and bound: the incumbent (elp_get_solution)
 };
 
 // elp_control.simplex = 0 (include/easylp_hip.h)
@@ -1177,7 +1178,6 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
         // boxed columns at the bound their cost sign asks for, the costs no bound
         // makes dual feasible zeroed, every row covered by its slack
         HIPCHK(launch_dual_setup_cols(d, h->st));
-        HIPCHK(hipMemsetAsync(d.ract, 0, (size_t)std::max<int64_t>(m, 1) * sizeof(double), h->st));
         {
             const int rc = row_chain(h);
             if (rc) return rc;
@@ -2372,6 +2372,80 @@ static int reload_bounds(elp_handle* h, const std::vector<double>& lo, const std
     return rc;
 }
 
+// A branch-and-bound node warm-started from the basis the last node ended on
+// (oracle warm_core; SIMPLEX_DUAL_PRIMAL on one GPU): the node's bounds, the
+// real costs, every nonbasic column re-placed for them (launch_warm_start), a
+// refactor (Minv correction, x_B from b), then the dual phase 1 from that
+// basis -- its first CHUZR ends it at once when x_B is feasible -- and the
+// primal phase 2.  Device memory, A, the rows and the lists all stay.
+static int reload_bounds_warm(elp_handle* h, const std::vector<double>& lo, const std::vector<double>& up) {
+    const int64_t n = h->n;
+    Dev& d = h->d;
+    const double BIG = h->ctl.infinity;
+    auto fin = [&](double v) { return v <= -BIG ? -HUGE_VAL : v >= BIG ? HUGE_VAL : v; };
+    std::vector<double> lo_s((size_t)n), up_s((size_t)n);
+    for (int64_t j = 0; j < n; ++j) {
+        lo_s[(size_t)j] = unscale_col(h, fin(lo[(size_t)j]), j, -1);
+        up_s[(size_t)j] = unscale_col(h, fin(up[(size_t)j]), j, -1);
+    }
+    double *dlo = nullptr, *dup = nullptr;
+    HIPCHK(dalloc(&dlo, n));
+    HIPCHK(dalloc(&dup, n));
+    HIPCHK(hipMemcpyAsync(dlo, lo_s.data(), (size_t)n * sizeof(double), hipMemcpyHostToDevice, h->st));
+    HIPCHK(hipMemcpyAsync(dup, up_s.data(), (size_t)n * sizeof(double), hipMemcpyHostToDevice, h->st));
+    // the control block of a fresh solve, the basis kept
+    HIPCHK(hipMemcpyAsync(h->hctl, d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    DevCtl& c = *h->hctl;
+    const int k = c.k, ny = c.ny;
+    c.status = ST_RUN;
+    c.phase = 2;
+    c.iter = 0;
+    c.iter_limit = h->ctl.max_iter > 0 ? std::max<int64_t>(h->bnb_iter_left, 0) : 100 * (h->m + n) + 10000;
+    c.iter_stop = INT64_MAX;
+    c.since_refactor = 0;
+    c.ndegen = c.bland = 0;
+    c.phase1_iters = c.flips = c.degenerate = 0;
+    c.unb_var = -1;
+    c.infeasible_bounds = 0;
+    c.price_bytes = c.iter_bytes = 0.0;
+    c.price_passes = 0;
+    c.plan.action = ACT_NONE;
+    c.plan_seq = c.applied_seq = 0;
+    c.devex = 0;
+    c.ddevex = h->ctl.pricing == ELP_PRICE_DEVEX;
+    c.dv_valid = 0;
+    c.dual_iters = c.dflat = 0;
+    HIPCHK(hipMemcpyAsync(d.ctl, h->hctl, sizeof(DevCtl), hipMemcpyHostToDevice, h->st));
+    HIPCHK(launch_warm_start(d, dlo, dup, k, ny, h->st));
+    HIPCHK(hipMemcpyAsync(h->hctl, d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    (void)hipFree(dlo);
+    (void)hipFree(dup);
+    h->stats = elp_stats{};
+    h->stats.world_size = h->comm.world;
+    h->stats.ncols = h->nloc;
+    h->stats.basis = ELP_BASIS_INVERSE;
+    h->timing_started = false;
+    h->done = false;
+    h->dual_used = true;
+    if (h->hctl->infeasible_bounds) {  // R/class.R:297-298 (as load_common)
+        h->done = true;
+        h->final_status = ELP_INFEASIBLE;
+        return 0;
+    }
+    h->phase = 3;
+    int rc = do_refactor(h, k);
+    if (rc) return rc;
+    HIPCHK(launch_devex_reset(d, h->st));  // (the dual phase's weights start at 1)
+    HIPCHK(hipMemcpyAsync(h->hctl, d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    h->hctl->since_refactor = 0;
+    h->hctl->dv_valid = 0;
+    h->stats.refactors = 0;
+    return push_ctl_fields(h);
+}
+
 // Depth-first branch and bound over LP relaxations; the rules are
 // oracle/elp_oracle.c orc_solve_mip's, so both explore the same tree.
 // max_iter (total LP iterations) and time_limit (seconds since the branch and
@@ -2402,7 +2476,11 @@ static int run_bnb(elp_handle* h, int32_t* out_status) {
     bool have = false, limit = false, unbounded = false;
     int32_t failed = -1;  // status of the first node LP that did not finish (incomplete tree)
     int64_t nodes = 0, iters = 0;
-    std::vector<double> x((size_t)n);
+    std::vector<double> x((size_t)n), best_x;
+    // SIMPLEX_DUAL_PRIMAL on one GPU: node LPs after the first continue from
+    // the basis of the node solved last (reload_bounds_warm; oracle warm_core)
+    const bool warm = dual_phase1(h) && h->m > 0;
+    bool warm_ok = false;
     while (!stack.empty()) {
         Node nd = std::move(stack.back());
         stack.pop_back();
@@ -2429,7 +2507,8 @@ static int run_bnb(elp_handle* h, int32_t* out_status) {
             break;
         }
         int rc = 0;
-        if (!(nodes == 1 && h->lo_h == nd.lo && h->up_h == nd.up)) rc = reload_bounds(h, nd.lo, nd.up);
+        if (warm_ok && nodes > 1) rc = reload_bounds_warm(h, nd.lo, nd.up);
+        else if (!(nodes == 1 && h->lo_h == nd.lo && h->up_h == nd.up)) rc = reload_bounds(h, nd.lo, nd.up);
         if (rc) return rc;
         h->t_solve_start = t_bnb;  // time_limit counts from the start of the tree
         h->timing_started = true;
@@ -2446,6 +2525,9 @@ static int run_bnb(elp_handle* h, int32_t* out_status) {
             unbounded = true;
             break;
         }
+        // (the oracle: a node that failed leaves no basis to continue from -- the
+        //  next one starts cold; so does a node the primal phase 1 solved)
+        warm_ok = warm && (s == ELP_OPTIMAL || s == ELP_INFEASIBLE || s == ELP_UNBOUNDED);
         if (s != ELP_OPTIMAL && s != ELP_INFEASIBLE) {  // limit or numerical failure
             if (failed < 0) failed = s;
             if (s == ELP_SUBOPTIMAL || s == ELP_TIMEOUT) break;  // the tree's budget is spent
@@ -2467,6 +2549,7 @@ static int run_bnb(elp_handle* h, int32_t* out_status) {
         if (jb < 0) {
             best = zmin;
             best_node = nd;
+            best_x = x;
             have = true;
             continue;
         }
@@ -2481,17 +2564,11 @@ static int run_bnb(elp_handle* h, int32_t* out_status) {
     else if (have) status = (limit || failed >= 0) ? ELP_SUBOPTIMAL : ELP_OPTIMAL;
     else if (failed >= 0) status = failed;
     else status = limit ? ELP_SUBOPTIMAL : ELP_INFEASIBLE;
-    if (have && !unbounded) {  // leave the incumbent's LP on the handle for elp_get_solution
-        // (the incumbent's node was solved within the limits once: no limits now)
-        h->bnb_iter_left = INT64_MAX / 4;
-        const double tl = h->ctl.time_limit;
-        h->ctl.time_limit = 0.0;
-        int rc = reload_bounds(h, best_node.lo, best_node.up);
-        int32_t s = 0;
-        if (!rc) rc = run_loop(h, INT64_MAX, &s);
-        h->ctl.time_limit = tl;
-        if (rc) return rc;
-    }
+    (void)best_node;
+    // elp_get_solution reports the incumbent as the tree found it (the oracle's
+    // xbest): no re-solve, whose warm start could end on another optimal vertex
+    h->mip_x.clear();
+    if (have && !unbounded) h->mip_x = best_x;
     h->final_status = status;
     h->done = true;
     h->mip = true;
@@ -2570,6 +2647,7 @@ extern "C" int elp_get_solution(elp_handle* h, double* objval, double* x, double
     const DevCtl& c = *h->hctl;
     const double BIG = h->ctl.infinity;
     for (int64_t j = 0; j < n; ++j) xs[j] = unscale_col(h, xs[j], j, 1);  // (exact)
+    if (h->mip && !h->mip_x.empty()) xs = h->mip_x;  // branch and bound: the incumbent as found
     const bool unb = h->done && h->final_status == ELP_UNBOUNDED;
     // the unbounded variable's global id (shard-local q -> global)
     const int64_t uvar = unb ? (int64_t)c.unb_var : -1;  // global id

@@ -402,5 +402,9 @@ hipError_t launch_dual_init_rows(const Dev& d, hipStream_t st);
 // one iteration: CHUZR, rho_r, pivot row + pricing, bound-flipping ratio test,
 // the flips' FTRAN and x_B update, FTRAN of a_q, pivot bookkeeping, update
 hipError_t launch_dual_iteration(const Dev& d, int k_ub, int ny_ub, hipStream_t st);
+// MIP node warm start (oracle warm_core): new column bounds lo / up (local,
+// scaled), real costs, y, and every nonbasic column re-placed for the node
+// (k, ny: the kept basis's bump dimension and |Y|); the host then refactors
+hipError_t launch_warm_start(const Dev& d, const double* lo, const double* up, int k, int ny, hipStream_t st);
 
 }  // namespace elp

@@ -3145,6 +3145,7 @@ __global__ void k_phase2(Dev d) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t < d.m) {
         const int av = d.n + d.m + t;
+        d.cost[d.n + t] = 0.0;  // (a MIP node's warm start may have shifted a slack's cost)
         d.cost[av] = 0.0;
         d.lb[av] = 0.0;
         d.ub[av] = 0.0;
@@ -3591,6 +3592,59 @@ __global__ void __launch_bounds__(256) k_dual_row(Dev d, int nchz, int lds_row) 
     }
 }
 
+// MIP node warm start (oracle warm_core): the nonbasic column's status and
+// value under its new bounds, then dual feasibility -- a boxed column whose
+// reduced cost has the wrong sign moves to its other bound, anything still
+// dual infeasible beyond tol_dual has its cost shifted by -d_j for the dual
+// phase (k_phase2 restores the costs).  Slacks: the shift only.
+DEV void warm_fix(const Dev& d, int jl, bool structural, double dj, double dtol) {
+    int8_t vs = d.vstat[jl];
+    if (vs == VS_BASIC) return;
+    const double l = d.lb[jl], u = d.ub[jl];
+    if (l == u) {
+        if (structural) {
+            d.vstat[jl] = VS_FIXED;
+            d.xval[jl] = l;
+        }
+        return;
+    }
+    if (structural) {
+        const bool lo_ok = l > -HUGE_VAL, up_ok = u < HUGE_VAL;
+        if (vs == VS_FIXED) vs = VS_LOWER;  // (fixed in the last node: the oracle's "lower")
+        if (vs == VS_LOWER && !lo_ok) vs = up_ok ? VS_UPPER : VS_FREE;
+        else if (vs == VS_UPPER && !up_ok) vs = lo_ok ? VS_LOWER : VS_FREE;
+        else if (vs == VS_FREE && (lo_ok || up_ok)) vs = lo_ok ? VS_LOWER : VS_UPPER;
+        if (vs == VS_LOWER && dj < -dtol && up_ok) vs = VS_UPPER;
+        else if (vs == VS_UPPER && dj > dtol && lo_ok) vs = VS_LOWER;
+        d.vstat[jl] = vs;
+        d.xval[jl] = vs == VS_LOWER ? l : vs == VS_UPPER ? u : 0.0;
+    }
+    if ((vs == VS_LOWER && dj < -dtol) || (vs == VS_UPPER && dj > dtol) || (vs == VS_FREE && fabs(dj) > dtol)) {
+        d.cost[jl] = d.cost[jl] - dj;
+        atomicAdd(reinterpret_cast<unsigned long long*>(&d.ctl->dflat), 1ull);
+    }
+}
+
+// the node's bounds of the local structurals (scaled), the real costs, and the
+// bump positions' cached bounds / costs; lower > upper flags the node infeasible
+__global__ void k_warm_bounds(Dev d, const double* __restrict__ lo, const double* __restrict__ up) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < d.n) {
+        d.lb[t] = lo[t];
+        d.ub[t] = up[t];
+        d.cost[t] = d.maximize ? -d.obj[t] : d.obj[t];
+        if (lo[t] > up[t]) atomicOr(&d.ctl->infeasible_bounds, 1);
+    }
+    if (t < d.m) d.cost[d.n + t] = 0.0;
+    if (t < d.ctl->k) {
+        const int j = d.Sl[t];  // (one GPU: global = local)
+        d.slo[t] = lo[j];
+        d.shi[t] = up[j];
+        const double o = d.objg[j];
+        d.cS[t] = d.maximize ? -o : o;
+    }
+}
+
 // a priced column's ratio-test record (oracle run_dual): side +1 acts at its
 // lower bound (needs ah < -tol_pivot), -1 at its upper (ah > tol_pivot)
 DEV bool dual_candidate(int8_t vs, double a, double dj, double lb, double ub, int rs, int bland, double dtol,
@@ -3636,13 +3690,20 @@ DEV void emit_region(const Dev& d, int region, bool f0, const DualCand& c0, bool
 
 // the slack columns of the Y rows (cost 0: d = -y, alpha = rho on the slot)
 template <int NT>
-DEV void dual_slacks(const Dev& d, int region, int s, int nsw, int* wcnt) {
+DEV void dual_slacks(const Dev& d, int region, int s, int nsw, int* wcnt, int warm) {
     const DevCtl* c = d.ctl;
     const int ny = c->ny, bland = c->bland, rs = c->dr_s;
     const double dtol = c->tol_dual, pivtol = c->tol_pivot;
     const int p = s * NT + threadIdx.x;  // (the host sizes nsw for one slot per thread)
     DualCand o;
     bool f = false;
+    if (warm) {
+        if (p < ny) {
+            const int sv = d.n + d.Yl[p];
+            warm_fix(d, sv, false, d.cost[sv] - d.yy[p], dtol);
+        }
+        return;
+    }
     if (p < ny) {
         const int8_t v = d.yvs[p];
         const int i = d.Yl[p];
@@ -3657,13 +3718,15 @@ DEV void dual_slacks(const Dev& d, int region, int s, int nsw, int* wcnt) {
 // added in order), then wave 0 finishes columns 2 lane, 2 lane + 1: d_j,
 // alpha_j (+ sigma a_ij of a covered leaving row i, last), the candidates.
 // Grid: [nsw slack workgroups][ntiles tiles].
-__global__ void __launch_bounds__(PRICE_THREADS) k_dual_price(Dev d, int nsw) {
+// warm != 0 (MIP node warm start): the same pass for d_j alone (rho = 0), each
+// nonbasic column re-placed by warm_fix instead of a candidate
+__global__ void __launch_bounds__(PRICE_THREADS) k_dual_price(Dev d, int nsw, int warm) {
     __shared__ double pd[PRICE_SPLIT][TILE_COLS], pa[PRICE_SPLIT][TILE_COLS];
     __shared__ int wcnt[PRICE_SPLIT];
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
     if ((int)blockIdx.x < nsw) {
-        dual_slacks<PRICE_THREADS>(d, d.ntiles + blockIdx.x, blockIdx.x, nsw, wcnt);
+        dual_slacks<PRICE_THREADS>(d, d.ntiles + blockIdx.x, blockIdx.x, nsw, wcnt, warm);
         return;
     }
     const int64_t tile = (int64_t)blockIdx.x - nsw;
@@ -3708,7 +3771,7 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_dual_price(Dev d, int nsw) {
         __syncthreads();  // (emit_region's barrier)
         return;
     }
-    const int xrow = c->dr_xrow, rs = c->dr_s, bland = c->bland;
+    const int xrow = warm ? -1 : c->dr_xrow, rs = c->dr_s, bland = c->bland;
     const double xsig = c->dr_xsig, dtol = c->tol_dual, pivtol = c->tol_pivot;
     DualCand o[2];
     bool f[2] = {false, false};
@@ -3717,6 +3780,14 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_dual_price(Dev d, int nsw) {
         const int64_t j = tile * tw + 2 * lane + h;
         if (2 * lane + h >= tw || j >= d.n) continue;
         const int8_t vs = d.vstat[j];
+        if (warm) {
+            if (vs == VS_BASIC) continue;
+            double td = 0.0;
+#pragma unroll
+            for (int ww = 0; ww < PRICE_SPLIT; ++ww) td = td + pd[ww][2 * lane + h];
+            warm_fix(d, (int)j, true, d.cost[j] - td, dtol);
+            continue;
+        }
         if (vs == VS_BASIC || vs == VS_FIXED) continue;
         double td = 0.0, ta = 0.0;
 #pragma unroll
@@ -3728,26 +3799,38 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_dual_price(Dev d, int nsw) {
         const double aj = xrow >= 0 ? fma(xsig, a_row(d, xrow, j), ta) : ta;
         f[h] = dual_candidate(vs, aj, dj, d.lb[j], d.ub[j], rs, bland, dtol, pivtol, (int)(d.col0 + j), o[h]);
     }
+    if (warm) {
+        __syncthreads();  // (the barrier emit_region would take)
+        return;
+    }
     emit_region<64>(d, (int)tile, f[0], o[0], f[1], o[1], wcnt);
 }
 
 // CSC pivot row + pricing: one column chain per thread over its nonzeros in
 // ascending rows with the dense y and rho (rho_i from the bump positions
 // through rpos, sigma on a covered leaving row)
-__global__ void __launch_bounds__(TILE_COLS) k_dual_price_csc(Dev d, int nsw) {
+__global__ void __launch_bounds__(TILE_COLS) k_dual_price_csc(Dev d, int nsw, int warm) {
     __shared__ int wcnt[TILE_COLS / 64];
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
     if ((int)blockIdx.x < nsw) {
-        dual_slacks<TILE_COLS>(d, d.ntiles + blockIdx.x, blockIdx.x, nsw, wcnt);
+        dual_slacks<TILE_COLS>(d, d.ntiles + blockIdx.x, blockIdx.x, nsw, wcnt, warm);
         return;
     }
     const int64_t tile = (int64_t)blockIdx.x - nsw;
     const int64_t j = tile * TILE_COLS + threadIdx.x;
-    const int xrow = c->dr_xrow, rs = c->dr_s, bland = c->bland;
+    const int xrow = warm ? -1 : c->dr_xrow, rs = c->dr_s, bland = c->bland;
     const double xsig = c->dr_xsig, dtol = c->tol_dual, pivtol = c->tol_pivot;
     DualCand o;
     bool f = false;
+    if (warm) {
+        if (j < d.n && d.vstat[j] != VS_BASIC) {
+            double ad = 0.0;
+            for (int64_t t = d.cptr[j]; t < d.cptr[j + 1]; ++t) ad = fma(d.cval[t], d.y[d.rind[t]], ad);
+            warm_fix(d, (int)j, true, d.cost[j] - ad, dtol);
+        }
+        return;
+    }
     if (j < d.n) {
         const int8_t vs = d.vstat[j];
         if (vs != VS_BASIC && vs != VS_FIXED) {
@@ -4339,7 +4422,7 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
 
 hipError_t launch_dual_setup_cols(const Dev& d, hipStream_t st) {
     if (d.n > 0) k_dual_setup_cols<<<cdiv(d.n, 256), 256, 0, st>>>(d);
-    return hipGetLastError();
+    return launch_nzlist(d, st);  // (columns moved to their upper bound: the row activities' list)
 }
 
 hipError_t launch_dual_init_rows(const Dev& d, hipStream_t st) {
@@ -4357,8 +4440,8 @@ hipError_t launch_dual_iteration(const Dev& d, int k_ub, int ny_ub, hipStream_t 
     if (nrw > 1024) nrw = 1024;
     k_dual_row<<<nrw, 256, lds_row ? lds : 0, st>>>(d, (int)nchz, lds_row);
     const int nsw = slack_wgs(d, ny_ub);
-    if (d.csc) k_dual_price_csc<<<d.ntiles + nsw, TILE_COLS, 0, st>>>(d, nsw);
-    else k_dual_price<<<d.ntiles + nsw, PRICE_THREADS, 0, st>>>(d, nsw);
+    if (d.csc) k_dual_price_csc<<<d.ntiles + nsw, TILE_COLS, 0, st>>>(d, nsw, 0);
+    else k_dual_price<<<d.ntiles + nsw, PRICE_THREADS, 0, st>>>(d, nsw, 0);
     k_dual_bfrt<<<1, BF_NT, 0, st>>>(d, d.ntiles + nsw);
     k_dual_flip_col<<<d.csc ? 1u : cdiv(m > 0 ? m : 1, 256), 256, 0, st>>>(d);
     if (k_ub > 0) k_dual_flip_bump<<<nrw, 256, lds_row ? lds : 0, st>>>(d, lds_row);
@@ -4376,6 +4459,17 @@ hipError_t launch_dual_iteration(const Dev& d, int k_ub, int ny_ub, hipStream_t 
     }
     k_select<<<1, 1024, 0, st>>>(d, 1, 0, 1);
     return launch_iteration_tail(d, k_ub, 3, st, true, 0);
+}
+
+hipError_t launch_warm_start(const Dev& d, const double* lo, const double* up, int k, int ny, hipStream_t st) {
+    const int64_t mx = std::max<int64_t>(std::max<int64_t>(d.n, d.m), 1);
+    k_warm_bounds<<<cdiv(mx, 256), 256, 0, st>>>(d, lo, up);
+    const hipError_t e = launch_btran_exact(d, k, st);  // y = B^-T c_B (the real costs)
+    if (e != hipSuccess) return e;
+    const int nsw = slack_wgs(d, ny);
+    if (d.csc) k_dual_price_csc<<<d.ntiles + nsw, TILE_COLS, 0, st>>>(d, nsw, 1);
+    else k_dual_price<<<d.ntiles + nsw, PRICE_THREADS, 0, st>>>(d, nsw, 1);
+    return hipGetLastError();
 }
 
 hipError_t launch_iteration_head(const Dev& d, int k_ub, int ny_ub, int phase, int rank,

@@ -110,3 +110,34 @@ def test_dual_kkt_20000x100000_optimum(gpu):
     assert s["dual_iterations"] > 0 and s["simplex"] == DUAL
     assert abs(z - k["highs_objective"]) <= 1e-8 * abs(k["highs_objective"]), (z, k["highs_objective"])
     assert s["iterations"] <= 4 * k["highs_iterations"], s["iterations"]
+
+
+@pytest.mark.parametrize("path", ["dense", "csc"])
+def test_warm_mip_trees_match_oracle(gpu, path):
+    """branch and bound with node LPs warm-started from the last
+    node's basis (reload_bounds_warm / the oracle's warm_core) -- the trees stay
+    node for node the oracle's on the 40 fuzz MIPs and the reference's three
+    MIP tests (investments, students, cyingair): status, nodes, LP iterations,
+    incumbent and objective; the LP iterations over all trees drop against the
+    cold primal trees."""
+    from conftest import load_mip_known_answers
+    from fuzz_lps import fuzz_mip
+    from oracle import solve_mip
+    recs = [fuzz_mip(s) for s in range(40)] + load_mip_known_answers()
+    warm_its = cold_its = 0
+    for i, rec in enumerate(recs):
+        args = (rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], rec["maximize"])
+        solve = gpu.solve_dense if path == "dense" else gpu.solve_sparse
+        extra = {"basis": 1} if path == "csc" else {}
+        g = solve(*args, is_int=rec["is_int"], simplex=DUAL, **extra)
+        o = solve_mip(*args, rec["is_int"], simplex=DUAL, price_mode=1 if path == "csc" else 0)
+        tag = rec.get("name", f"mip{i}")
+        assert (g.status, g.stats["mip_nodes"], g.stats["mip_lp_iterations"]) == (
+            o.status, o.stats["nodes"], o.stats["lp_iterations"]), tag
+        if o.status == 0:
+            assert g.objval == o.objval, tag
+            np.testing.assert_array_equal(g.x, o.x, err_msg=tag)
+        warm_its += g.stats["mip_lp_iterations"]
+        c = solve(*args, is_int=rec["is_int"], simplex=5, **extra)
+        cold_its += c.stats["mip_lp_iterations"]
+    assert warm_its < 0.5 * cold_its, (warm_its, cold_its)
