@@ -3767,10 +3767,8 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_dual_price(Dev d, int nsw, in
     pa[w][2 * lane] = a0;
     pa[w][2 * lane + 1] = a1;
     __syncthreads();
-    if (w != 0) {
-        __syncthreads();  // (emit_region's barrier)
-        return;
-    }
+    // wave 0 finishes the tile's columns; waves 1..3 only take part in the
+    // emission's barrier (no candidates of their own)
     const int xrow = warm ? -1 : c->dr_xrow, rs = c->dr_s, bland = c->bland;
     const double xsig = c->dr_xsig, dtol = c->tol_dual, pivtol = c->tol_pivot;
     DualCand o[2];
@@ -3778,7 +3776,7 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_dual_price(Dev d, int nsw, in
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int64_t j = tile * tw + 2 * lane + h;
-        if (2 * lane + h >= tw || j >= d.n) continue;
+        if (w != 0 || 2 * lane + h >= tw || j >= d.n) continue;
         const int8_t vs = d.vstat[j];
         if (warm) {
             if (vs == VS_BASIC) continue;
@@ -3799,11 +3797,8 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_dual_price(Dev d, int nsw, in
         const double aj = xrow >= 0 ? fma(xsig, a_row(d, xrow, j), ta) : ta;
         f[h] = dual_candidate(vs, aj, dj, d.lb[j], d.ub[j], rs, bland, dtol, pivtol, (int)(d.col0 + j), o[h]);
     }
-    if (warm) {
-        __syncthreads();  // (the barrier emit_region would take)
-        return;
-    }
-    emit_region<64>(d, (int)tile, f[0], o[0], f[1], o[1], wcnt);
+    if (warm) return;
+    emit_region<PRICE_THREADS>(d, (int)tile, f[0], o[0], f[1], o[1], wcnt);
 }
 
 // CSC pivot row + pricing: one column chain per thread over its nonzeros in
