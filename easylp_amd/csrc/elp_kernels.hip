@@ -974,23 +974,32 @@ DEV void tile_apply(const Dev& d, int64_t tile, int64_t ntiles) {
 // instead of by trailing workgroups that started only as tiles retired.
 // napply > 0 (A/B switch ELP_TRAIL_APPLY=1, r02's layout): the plan is applied
 // by napply trailing workgroups instead (apply = 0 then)
-template <int NTL>
+// TW: the tile width at compile time (TILE_COLS, the default layout: every AR
+// row offset a shift) or 0 (ELP_TILE_BAL's balanced tiles: d.tile_w at run time).
+// ELP_SLACK_LAST (build switch, default 1 since r04): the slack workgroups after
+// the tiles (r02's order; 0: first, r03).  r04 A/B, one session each: k_price
+// 17.94 us under rocprof against 18.83 with the slacks first.
+#ifndef ELP_SLACK_LAST
+#define ELP_SLACK_LAST 1
+#endif
+template <int NTL, int TW>
 DEV void price_body(const Dev& d, int nsw, int apply, int napply, int nb_minv) {
     __shared__ double part[PRICE_SPLIT][TILE_COLS];
     __shared__ Cand red[PRICE_SPLIT];
     const int64_t ntiles = d.ntiles;
     if (napply > 0 && apply_role(d, napply, nb_minv)) return;
-    if ((int)blockIdx.x < nsw) {
+    const int sw = ELP_SLACK_LAST ? (int)blockIdx.x - (int)ntiles : (int)blockIdx.x;  // slack workgroup index
+    if (sw >= 0 && sw < nsw) {
         PDBG(1, 2ull);
         PDBG(2, 0ull);
         PDBG(3, 0ull);
         PDBG(4, 0ull);
         if (d.ctl->status != ST_RUN) return;
-        price_slacks<PRICE_THREADS>(d, ntiles, (int)blockIdx.x, nsw, red);  // a slack workgroup
+        price_slacks<PRICE_THREADS>(d, ntiles, sw, nsw, red);  // a slack workgroup
         return;
     }
-    const int64_t tile = (int64_t)blockIdx.x - nsw;
-    const int tw = d.tile_w;
+    const int64_t tile = ELP_SLACK_LAST ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - nsw;
+    const int tw = TW ? TW : d.tile_w;
     // Software-pipelined sweep: the control block is loaded FIRST (vmcnt
     // retires in issue order, so the status test and the loop bound wait for
     // it alone, not for the rows issued behind it), then the first UNR rows
@@ -1178,11 +1187,11 @@ DEV void pstamp_end(const Dev& d) {
     if (threadIdx.x == 0) d.pstamp[PSTRIDE * blockIdx.x + PSTRIDE - 1] = __builtin_amdgcn_s_memrealtime();
 }
 
-template <int NTL>
+template <int NTL, int TW>
 __global__ void __launch_bounds__(PRICE_THREADS) k_price(DEV_PARAM, int nsw, int apply, int napply, int nb_minv) {
     DEV_BIND
     pstamp_begin<PRICE_THREADS>(d);
-    price_body<NTL>(d, nsw, apply, napply, nb_minv);
+    price_body<NTL, TW>(d, nsw, apply, napply, nb_minv);
     pstamp_end(d);
 }
 
@@ -4202,6 +4211,15 @@ hipError_t launch_row_chain(const Dev& d, hipStream_t st) {
     return hipGetLastError();
 }
 
+
+// the dense pricing kernel for a launch: non-temporal sweep loads or not, the
+// default tile width as a compile-time constant or ELP_TILE_BAL's at run time
+typedef void (*PriceFn)(DEV_PARAM, int, int, int, int);
+static PriceFn price_kernel(bool nt, int tw) {
+    if (tw == TILE_COLS) return nt ? k_price<1, TILE_COLS> : k_price<0, TILE_COLS>;
+    return nt ? k_price<1, 0> : k_price<0, 0>;
+}
+
 hipError_t launch_init_rows(const Dev& d, const double* rhs, hipStream_t st) {
     if (d.m > 0) {
         k_init_rows<<<cdiv(d.m, 256), 256, 0, st>>>(d, rhs);
@@ -4269,11 +4287,13 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phas
 #define ELP_APPLY_PT 4
 #endif
     if (phase == 2 && d.csc) update_grid(d, k_ub, false, &nb_minv, &napply, TILE_COLS, ELP_APPLY_PT);
-    // ELP_TRAIL_APPLY=1 (A/B): the dense deferred plan in
-    // trailing workgroups of the launch (r02) instead of the tiles' waves 1-3
+    // the dense deferred plan in trailing workgroups of the launch (r02's
+    // layout, the default again since r04: 3 x 3 interleaved A/B at 5000 x 50000,
+    // 25.4k against 24.7k iterations/s with the tiles' waves 1-3 applying it);
+    // ELP_TRAIL_APPLY=0 restores the waves (r03)
     static const bool trail = [] {
         const char* e = std::getenv("ELP_TRAIL_APPLY");
-        return e && std::atoi(e) == 1;
+        return !(e && std::atoi(e) == 0);
     }();
     unsigned dnapply = 0, dnb_minv = 0;
     if (phase == 2 && !d.csc && trail) update_grid(d, k_ub, false, &dnb_minv, &dnapply, PRICE_THREADS, ELP_APPLY_PT);
@@ -4290,17 +4310,14 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phas
         if (d.csc)
             hipExtLaunchKernelGGL(k_price_csc, dim3(grid), dim3(TILE_COLS), 0, st, ev0, ev1, 0, d, (int)napply,
                                   (int)nb_minv, nsw);
-        else if (nt)
-            hipExtLaunchKernelGGL(k_price<1>, dim3(grid), dim3(PRICE_THREADS), 0, st, ev0, ev1, 0, DEV_ARG(d), nsw,
-                                  dapply, (int)dnapply, (int)dnb_minv);
         else
-            hipExtLaunchKernelGGL(k_price<0>, dim3(grid), dim3(PRICE_THREADS), 0, st, ev0, ev1, 0, DEV_ARG(d), nsw,
-                                  dapply, (int)dnapply, (int)dnb_minv);
+            hipExtLaunchKernelGGL(price_kernel(nt, d.tile_w), dim3(grid), dim3(PRICE_THREADS), 0, st, ev0, ev1, 0,
+                                  DEV_ARG(d), nsw, dapply, (int)dnapply, (int)dnb_minv);
         return hipGetLastError();
     }
     if (d.csc) k_price_csc<<<grid, TILE_COLS, 0, st>>>(d, (int)napply, (int)nb_minv, nsw);
-    else if (nt) k_price<1><<<grid, PRICE_THREADS, 0, st>>>(DEV_ARG(d), nsw, dapply, (int)dnapply, (int)dnb_minv);
-    else k_price<0><<<grid, PRICE_THREADS, 0, st>>>(DEV_ARG(d), nsw, dapply, (int)dnapply, (int)dnb_minv);
+    else hipLaunchKernelGGL(price_kernel(nt, d.tile_w), dim3(grid), dim3(PRICE_THREADS), 0, st, DEV_ARG(d), nsw,
+                            dapply, (int)dnapply, (int)dnb_minv);
     return hipGetLastError();
 }
 
