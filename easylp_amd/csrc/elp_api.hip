@@ -215,7 +215,7 @@ static void free_dev(elp_handle* h, bool keep_big = false) {
                     (void*)d.cptr, (void*)d.rind, (void*)d.cval, (void*)d.rptr, (void*)d.cind,
                     (void*)d.rval, d.qcol, d.qz, d.dstamp, d.rowvs, d.yvs, d.dw, d.dprev, (void*)d.srow,
                     (void*)d.scol, d.rhoR, d.rr, d.dchz, d.dcand, d.dcnt, d.dcomp, d.dalive, d.dflip,
-                    d.dflipdx, d.aF, d.fS};
+                    d.dflipdx, d.aF, d.fS, d.ddw != d.dw ? (void*)d.ddw : nullptr, d.dsend, d.drecv};
     for (void* p : ptrs)
         if (p) release(p);
     if (!keep_big) drain_pool(h);
@@ -708,9 +708,13 @@ static int alloc_all_body(elp_handle* h) {
     }
     A(dalloc(&d.ctl, 1));
     A(dalloc(&d.trace, (size_t)(h->trace_cap > 0 ? 2 * h->trace_cap : 2)));
-    // dual simplex phase 1 (one GPU; elp_kernels.hip "dual simplex"): regions =
-    // the pricing tiles + the slack workgroups (<= m / 128 + 1), DREG slots each
-    if (!d.sharded && !h->lu) {
+    // dual simplex phase 1 (elp_kernels.hip "dual simplex"): regions = the
+    // pricing tiles + the slack workgroups (<= m / 128 + 1), DREG slots each.
+    // One GPU, or column-sharded ranks holding all of A (the flipped and the
+    // entering columns are read from the replicated copy); the ratio test sees
+    // every rank's candidates: up to N + m of them
+    if (!h->lu && (!d.sharded || (h->replicated && !h->csc))) {
+        const int64_t Ng = h->n;
         d.dregs = d.ntiles + (int32_t)((mm + TILE_COLS - 1) / TILE_COLS) + 2;
         d.dchzn = (int32_t)((2 * mm + 255) / 256 + 2);
         A(dalloc(&d.rhoR, mm));
@@ -718,13 +722,22 @@ static int alloc_all_body(elp_handle* h) {
         A(dalloc(&d.dchz, (size_t)d.dchzn));
         A(dalloc(&d.dcand, (size_t)d.dregs * DREG));
         A(dalloc(&d.dcnt, (size_t)d.dregs));
-        A(dalloc(&d.dcomp, (size_t)(n + m)));
-        A(dalloc(&d.dalive, (size_t)(n + m)));
-        A(dalloc(&d.dflip, (size_t)(n + m)));
-        A(dalloc(&d.dflipdx, (size_t)(n + m)));
+        A(dalloc(&d.dcomp, (size_t)(Ng + m)));
+        A(dalloc(&d.dalive, (size_t)(Ng + m)));
+        A(dalloc(&d.dflip, (size_t)(Ng + m)));
+        A(dalloc(&d.dflipdx, (size_t)(Ng + m)));
         A(dalloc(&d.aF, mm));
         A(dalloc(&d.fS, mm));
+        d.dslack = !d.sharded || h->comm.rank == h->comm.world - 1;
+        if (d.sharded) {
+            const int P = h->comm.world;
+            d.dcap = (int32_t)((Ng + P - 1) / P + m);  // a shard's columns (<= ceil(N / P)) + the slacks
+            A(dalloc(&d.dsend, (size_t)d.dcap + 1));
+            A(dalloc(&d.drecv, (size_t)P * ((size_t)d.dcap + 1)));
+            A(dalloc(&d.ddw, (size_t)(Ng + 2 * m)));
+        }
     }
+    if (!d.ddw) d.ddw = d.dw;  // (one GPU: local ids are the global ids)
     if (e != hipSuccess) {
         free_dev(h);
         return fail(ELP_E_NOMEM, std::string("device allocation failed: ") + hipGetErrorString(e));
@@ -1022,7 +1035,8 @@ static int simplex_type(const elp_handle* h) {
     return h->ctl.simplex == 0 ? ELP_SIMPLEX_DEFAULT : h->ctl.simplex;
 }
 static bool dual_phase1(const elp_handle* h) {
-    return simplex_type(h) == ELP_SIMPLEX_DUAL_PRIMAL && h->comm.kind == 0 && !h->lu && h->d.dcand;
+    return simplex_type(h) == ELP_SIMPLEX_DUAL_PRIMAL && !h->lu && h->d.dcand &&
+           (h->comm.kind == 0 || (h->replicated && !h->csc && h->d.dsend));
 }
 
 // common tail of elp_load_*: bounds, rows, control block, phase decision
@@ -1853,8 +1867,17 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             const int nyub = (int)std::min<int64_t>(h->m, (int64_t)ny0 + t);
             hipEvent_t e0 = prof_chunk ? h->ev[2 * t] : nullptr, e1 = prof_chunk ? h->ev[2 * t + 1] : nullptr;
             h->stats.price_launches++;
-            if (h->phase == 3) {  // the dual simplex phase 1 (one GPU)
+            if (h->phase == 3 && h->comm.kind == 0) {  // the dual simplex phase 1 (one GPU)
                 HIPCHK(launch_dual_iteration(h->d, kub, nyub, h->st));
+            } else if (h->phase == 3) {
+                // column-sharded: each rank prices its shard (the last rank also the
+                // slacks) and packs its ratio-test candidates; the all-gather hands
+                // every rank all of them in rank order, and every rank runs the same
+                // bound-flipping ratio test and update
+                HIPCHK(launch_dual_iteration_head(h->d, kub, nyub, h->st));
+                rc = h->comm.allgather(h->d.dsend, h->d.drecv, ((size_t)h->d.dcap + 1) * sizeof(DualCand), h->st);
+                if (rc) return fail(rc, "dual ratio-test candidate all-gather failed");
+                HIPCHK(launch_dual_iteration_tail(h->d, kub, h->st));
             } else if (h->comm.kind == 0 || h->d.p2p) {  // (p2p: min-loc inside the select kernel)
                 HIPCHK(launch_iteration(h->d, kub, nyub, h->phase, h->st, e0, e1, t));
             } else {
@@ -2479,7 +2502,7 @@ static int run_bnb(elp_handle* h, int32_t* out_status) {
     std::vector<double> x((size_t)n), best_x;
     // SIMPLEX_DUAL_PRIMAL on one GPU: node LPs after the first continue from
     // the basis of the node solved last (reload_bounds_warm; oracle warm_core)
-    const bool warm = dual_phase1(h) && h->m > 0;
+    const bool warm = dual_phase1(h) && h->comm.kind == 0 && h->m > 0;
     bool warm_ok = false;
     while (!stack.empty()) {
         Node nd = std::move(stack.back());

@@ -142,6 +142,9 @@ struct DevCtl {
 struct DualCand {
     double t, b, a, r, d;
     int32_t j, side;  // global id; +1 acts at its lower bound, -1 at its upper
+    // the column's bounds, value and cost (scaled): what the other shards need
+    // when it enters (column-sharded ranks exchange the candidates)
+    double lb, ub, x, c;
 };
 // a dual CHUZR partial (k_dual_chuzr, one per workgroup)
 struct ChzRec {
@@ -287,6 +290,17 @@ struct Dev {
     int32_t* dflip;
     double *dflipdx, *aF, *fS;
     int32_t dregs, dchzn;
+    // the dual Devex weights of the basic variables, indexed by GLOBAL variable
+    // id (N + 2m): dw itself on one GPU (local = global ids), a replicated array
+    // on column-sharded ranks (a basic structural may live on another shard)
+    double* ddw;
+    // column-sharded dual phase (replicated A): this rank's compacted ratio-test
+    // candidates [header][dcap records] (header.j = count) and every rank's,
+    // all-gathered in rank order; dslack: this rank emits the slack candidates
+    // (one GPU, or the last rank -- so the gathered order is the one-GPU order:
+    // structurals by ascending id, then the slacks)
+    DualCand *dsend, *drecv;
+    int32_t dcap, dslack;
 };
 
 // Sparse-LU engine of the CSC path (elp_control.basis = ELP_BASIS_LU, DESIGN.md
@@ -402,6 +416,12 @@ hipError_t launch_dual_init_rows(const Dev& d, hipStream_t st);
 // one iteration: CHUZR, rho_r, pivot row + pricing, bound-flipping ratio test,
 // the flips' FTRAN and x_B update, FTRAN of a_q, pivot bookkeeping, update
 hipError_t launch_dual_iteration(const Dev& d, int k_ub, int ny_ub, hipStream_t st);
+// column-sharded ranks (replicated A): head = CHUZR, rho_r, the pivot row and
+// pricing of this shard, its candidates packed into dsend; the host all-gathers
+// dsend into drecv; tail = the bound-flipping ratio test over every rank's
+// candidates (identical on all ranks) and the rest of the iteration
+hipError_t launch_dual_iteration_head(const Dev& d, int k_ub, int ny_ub, hipStream_t st);
+hipError_t launch_dual_iteration_tail(const Dev& d, int k_ub, hipStream_t st);
 // MIP node warm start (oracle warm_core): new column bounds lo / up (local,
 // scaled), real costs, y, and every nonbasic column re-placed for the node
 // (k, ny: the kept basis's bump dimension and |Y|); the host then refactors

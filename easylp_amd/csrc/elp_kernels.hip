@@ -1477,7 +1477,7 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles, int nsw, int
     if (threadIdx.x == 0) c->applied_seq = c->plan_seq;  // the pricing launch applied it
     if (c->status != ST_RUN) return;
     Cand best = local_best(d, ntiles + nsw, red);
-    if (d.p2p) {  // column-sharded: global min-loc over the xGMI mailbox
+    if (d.p2p && !dual) {  // column-sharded: global min-loc over the xGMI mailbox
         __shared__ CandX s_rec[MAX_P2P];
         __shared__ int s_fail;
         if (!p2p_exchange(d, best, c->bland, c->iter, c->mb_epoch, s_rec, &s_fail)) return;
@@ -1586,7 +1586,7 @@ __global__ void __launch_bounds__(256) k_select_ftran(DEV_PARAM, int ntiles, int
         }
     }
     best = block_best<256>(best, bland, red);
-    if (d.p2p) {  // column-sharded: global min-loc over the xGMI mailbox
+    if (d.p2p && !dual) {  // column-sharded: global min-loc over the xGMI mailbox
         __shared__ CandX s_rec[MAX_P2P];
         __shared__ int s_fail;
         if (!p2p_exchange(d, best, bland, c->iter, c->mb_epoch, s_rec, &s_fail)) return;
@@ -2906,14 +2906,13 @@ DEV void apply_copy(const Dev& d, const Plan& P, int64_t t0, int64_t tstride, bo
         if (wq < 1.0) wq = 1.0;
         if (wq > DEVEX_WMAX) wq = DEVEX_WMAX;
         if (wq > DEVEX_RESET) {
-            for (int64_t t = t0; t < (int64_t)d.n + d.m; t += tstride) d.dw[t] = 1.0;
+            for (int64_t t = t0; t < (int64_t)d.N + d.m; t += tstride) d.ddw[t] = 1.0;
         } else {
             auto upd = [&](int var, double ae) {
                 const double r = ae / arq;
                 double wn = (r * r) * wr;
                 if (wn > DEVEX_WMAX) wn = DEVEX_WMAX;
-                const int lv = loc_of(d, var);
-                if (wn > d.dw[lv]) d.dw[lv] = wn;
+                if (wn > d.ddw[var]) d.ddw[var] = wn;
             };
             for (int64_t t = t0; t < d.m; t += tstride) {
                 if (t == P.i0 || t == P.lrow) continue;
@@ -2925,7 +2924,7 @@ DEV void apply_copy(const Dev& d, const Plan& P, int64_t t0, int64_t tstride, bo
                 if (P.pcase == PC_C && p == P.last) upd(d.Sl[P.b], d.alS[P.last]);  // (moved to b)
                 else upd(d.Sl[p], d.alS[p]);
             }
-            if (t0 == 0) d.dw[loc_of(d, P.q)] = wq;
+            if (t0 == 0) d.ddw[P.q] = wq;
         }
     }
     // ---- primal update (oracle order: x -= step * (sig * alpha), then the
@@ -3147,6 +3146,7 @@ __global__ void __launch_bounds__(1024) k_ns_store(Dev d, int k) {
 __global__ void k_devex_reset(Dev d) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j < (int64_t)d.n + d.m) d.dw[j] = 1.0;
+    if (d.ddw && d.ddw != d.dw && j < (int64_t)d.N + d.m) d.ddw[j] = 1.0;  // (sharded: global ids)
     if (j == 0) d.ctl->dv_valid = 0;
 }
 
@@ -3533,7 +3533,7 @@ __global__ void __launch_bounds__(256) k_dual_chuzr(Dev d) {
             r.x = x;
             r.beta = beta;
             r.s = sd;
-            r.score = dvx ? (delta * delta) / d.dw[loc_of(d, var)] : delta;
+            r.score = dvx ? (delta * delta) / d.ddw[var] : delta;
         }
     }
     r = block_best_chz<256>(r, bland, red);
@@ -3566,6 +3566,8 @@ __global__ void __launch_bounds__(256) k_dual_row(Dev d, int nchz, int lds_row) 
     const int xrow = r.e < m ? r.e : -1;
     const double xsig = xrow >= 0 ? unit_sign(d, r.var, xrow) : 0.0;
     if (blockIdx.x == 0 && tid == 0) {
+        // (a leaving structural's bounds from its bump position: on column-sharded
+        //  ranks it may live on another shard; the values are the same)
         const int lv = loc_of(d, r.var);
         c->dr_var = r.var;
         c->dr_e = r.e;
@@ -3573,9 +3575,9 @@ __global__ void __launch_bounds__(256) k_dual_row(Dev d, int nchz, int lds_row) 
         c->dr_xrow = xrow;
         c->dr_x = r.x;
         c->dr_beta = r.beta;
-        c->dr_lb = d.lb[lv];
-        c->dr_ub = d.ub[lv];
-        c->dr_w = d.dw[lv];
+        c->dr_lb = xrow >= 0 ? d.lb[lv] : d.slo[r.e - m];
+        c->dr_ub = xrow >= 0 ? d.ub[lv] : d.shi[r.e - m];
+        c->dr_w = d.ddw[r.var];
         c->dr_xsig = xsig;
     }
     double* asrow = lds_row ? asrow_lds : d.vrow;  // (huge bumps: every workgroup writes the same values)
@@ -3657,7 +3659,7 @@ __global__ void k_warm_bounds(Dev d, const double* __restrict__ lo, const double
 // a priced column's ratio-test record (oracle run_dual): side +1 acts at its
 // lower bound (needs ah < -tol_pivot), -1 at its upper (ah > tol_pivot)
 DEV bool dual_candidate(int8_t vs, double a, double dj, double lb, double ub, int rs, int bland, double dtol,
-                        double pivtol, int j, DualCand& o) {
+                        double pivtol, int j, double xj, double cj, DualCand& o) {
     if (vs == VS_BASIC || vs == VS_FIXED) return false;
     const double ah = rs * a;
     int side = 0;
@@ -3671,6 +3673,10 @@ DEV bool dual_candidate(int8_t vs, double a, double dj, double lb, double ub, in
     o.d = dj;
     o.j = j;
     o.side = side;
+    o.lb = lb;
+    o.ub = ub;
+    o.x = xj;
+    o.c = cj;
     return true;
 }
 
@@ -3717,7 +3723,8 @@ DEV void dual_slacks(const Dev& d, int region, int s, int nsw, int* wcnt, int wa
         const int8_t v = d.yvs[p];
         const int i = d.Yl[p];
         const int sv = d.n + i;
-        f = dual_candidate(v, d.rr[p], d.cost[sv] - d.yy[p], d.lb[sv], d.ub[sv], rs, bland, dtol, pivtol, d.N + i, o);
+        f = dual_candidate(v, d.rr[p], d.cost[sv] - d.yy[p], d.lb[sv], d.ub[sv], rs, bland, dtol, pivtol, d.N + i,
+                           d.xval[sv], d.cost[sv], o);
     }
     emit_region<NT>(d, region, f, o, false, o, wcnt);
 }
@@ -3804,7 +3811,8 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_dual_price(Dev d, int nsw, in
         }
         const double dj = d.cost[j] - td;
         const double aj = xrow >= 0 ? fma(xsig, a_row(d, xrow, j), ta) : ta;
-        f[h] = dual_candidate(vs, aj, dj, d.lb[j], d.ub[j], rs, bland, dtol, pivtol, (int)(d.col0 + j), o[h]);
+        f[h] = dual_candidate(vs, aj, dj, d.lb[j], d.ub[j], rs, bland, dtol, pivtol, (int)(d.col0 + j), d.xval[j],
+                              d.cost[j], o[h]);
     }
     if (warm) return;
     emit_region<PRICE_THREADS>(d, (int)tile, f[0], o[0], f[1], o[1], wcnt);
@@ -3847,7 +3855,8 @@ __global__ void __launch_bounds__(TILE_COLS) k_dual_price_csc(Dev d, int nsw, in
                 ad = fma(v, d.y[i], ad);
                 aa = fma(v, rho, aa);
             }
-            f = dual_candidate(vs, aa, d.cost[j] - ad, d.lb[j], d.ub[j], rs, bland, dtol, pivtol, (int)j, o);
+            f = dual_candidate(vs, aa, d.cost[j] - ad, d.lb[j], d.ub[j], rs, bland, dtol, pivtol, (int)j, d.xval[j],
+                               d.cost[j], o);
         }
     }
     emit_region<TILE_COLS>(d, (int)tile, f, o, false, o, wcnt);
@@ -3884,16 +3893,10 @@ DEV int block_scan_excl(int v, int* excl, int* lds) {
 // enter (Bland: the smallest ratio).  Each thread owns a contiguous run of the
 // compacted candidates, so ordered compactions are one block scan.
 constexpr int BF_NT = 1024;
-__global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg) {
-    __shared__ int scan_lds[BF_NT / 64];
-    __shared__ double red[BF_NT / 64];
-    __shared__ int s_int[4];
-    __shared__ double s_dbl[2];
-    DevCtl* c = d.ctl;
-    if (c->status != ST_RUN) return;
+// the regions' candidates in region order into dst[0, total): region counts
+// scanned in chunks of BF_NT regions, each thread copying its own regions
+DEV int compact_regions(const Dev& d, int nreg, DualCand* dst, int* scan_lds) {
     const int tid = threadIdx.x;
-    const int bland = c->bland;
-    // ---- compaction: region counts scanned in chunks of BF_NT regions
     int total = 0;
     for (int r0 = 0; r0 < nreg; r0 += BF_NT) {
         const int r = r0 + tid;
@@ -3902,9 +3905,45 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg) {
         const int tot = block_scan_excl<BF_NT>(cnt, &excl, scan_lds);
         if (r < nreg) {
             const DualCand* src = d.dcand + (size_t)r * DREG;
-            for (int t = 0; t < cnt; ++t) d.dcomp[total + excl + t] = src[t];
+            for (int t = 0; t < cnt; ++t) dst[total + excl + t] = src[t];
         }
         total += tot;
+    }
+    return total;
+}
+
+// column-sharded ranks: this shard's candidates (and the last rank's slack
+// candidates) packed into dsend -- record 0 carries the count
+__global__ void __launch_bounds__(BF_NT) k_dual_pack(Dev d, int nreg) {
+    __shared__ int scan_lds[BF_NT / 64];
+    if (d.ctl->status != ST_RUN) return;
+    const int total = compact_regions(d, nreg, d.dsend + 1, scan_lds);
+    if (threadIdx.x == 0) d.dsend[0].j = total;
+}
+
+// gathered: P = world ranks' packed records in drecv (rank order) instead of
+// this launch's regions
+__global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gathered) {
+    __shared__ int scan_lds[BF_NT / 64];
+    __shared__ double red[BF_NT / 64];
+    __shared__ int s_int[4];
+    __shared__ double s_dbl[2];
+    DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    const int tid = threadIdx.x;
+    const int bland = c->bland;
+    // ---- compaction (one GPU: the regions; sharded: the ranks' records, in
+    //      rank order = ascending structural id, the last rank's slacks last)
+    int total = 0;
+    if (!gathered) {
+        total = compact_regions(d, nreg, d.dcomp, scan_lds);
+    } else {
+        for (int r = 0; r < d.world; ++r) {
+            const DualCand* src = d.drecv + (size_t)r * ((size_t)d.dcap + 1);
+            const int cnt = src[0].j;
+            for (int t = tid; t < cnt; t += BF_NT) d.dcomp[total + t] = src[1 + t];
+            total += cnt;
+        }
     }
     __syncthreads();  // (the compacted array is read by other threads below)
     const int N = total;
@@ -3999,18 +4038,17 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg) {
         break;
     }
     __syncthreads();
-    // the flips: compact indices -> ids and dx (before their status changes)
+    // the flips: compact indices -> ids and dx = +-(u - l) (the record's range)
     for (int t = tid; t < nflip; t += BF_NT) {
         const DualCand o = d.dcomp[d.dflip[t]];
-        const int jl = loc_of(d, o.j);
-        const double l = d.lb[jl], u = d.ub[jl];
         const bool at_lower = o.side > 0;  // (boxed columns act at their current bound)
-        d.dflipdx[t] = at_lower ? u - l : l - u;
+        d.dflipdx[t] = at_lower ? o.ub - o.lb : o.lb - o.ub;
         d.dflip[t] = o.j;
     }
     __syncthreads();
     for (int t = tid; t < nflip; t += BF_NT) {
         const int jl = loc_of(d, d.dflip[t]);
+        if (jl < 0) continue;  // (column-sharded: another shard's column)
         const bool up = d.dflipdx[t] > 0.0;
         d.vstat[jl] = up ? VS_UPPER : VS_LOWER;
         d.xval[jl] = up ? d.ub[jl] : d.lb[jl];
@@ -4030,6 +4068,12 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg) {
         return;
     }
     const DualCand q = d.dcomp[qidx];
+    if (d.sharded) {  // the entering column's scalars, wherever it lives (k_ftran_zr's snapshot)
+        d.pkt[d.m] = q.lb;
+        d.pkt[d.m + 1] = q.ub;
+        d.pkt[d.m + 2] = q.x;
+        d.pkt[d.m + 3] = q.c;
+    }
     c->q = q.j;
     c->dq = q.d;
     c->wq = 1.0;
@@ -4077,9 +4121,9 @@ __global__ void __launch_bounds__(256) k_dual_flip_col(Dev d) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
     double acc = 0.0;
-    for (int f = 0; f < nf; ++f) {
+    for (int f = 0; f < nf; ++f) {  // (qcolumn: this shard's A, or the replicated A when sharded)
         const int j = d.dflip[f];
-        acc = fma(sca(d, d.A[(size_t)(j - d.col0) * (size_t)m + i], i, j), d.dflipdx[f], acc);
+        acc = fma(qcol_at(d, qcolumn(d, j), j, i), d.dflipdx[f], acc);
     }
     d.aF[i] = acc;
 }
@@ -4442,7 +4486,9 @@ hipError_t launch_dual_init_rows(const Dev& d, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_dual_iteration(const Dev& d, int k_ub, int ny_ub, hipStream_t st) {
+// CHUZR, rho_r and the pivot row + pricing of this shard's columns (+ the
+// slack candidates where d.dslack); returns the candidate regions' count
+static int dual_head(const Dev& d, int k_ub, int ny_ub, hipStream_t st) {
     const int m = d.m;
     const unsigned nchz = cdiv((int64_t)m + k_ub, 256);
     k_dual_chuzr<<<nchz, 256, 0, st>>>(d);
@@ -4451,10 +4497,38 @@ hipError_t launch_dual_iteration(const Dev& d, int k_ub, int ny_ub, hipStream_t 
     unsigned nrw = cdiv(k_ub > 0 ? k_ub : 1, 4);
     if (nrw > 1024) nrw = 1024;
     k_dual_row<<<nrw, 256, lds_row ? lds : 0, st>>>(d, (int)nchz, lds_row);
-    const int nsw = slack_wgs(d, ny_ub);
+    const int nsw = d.dslack ? slack_wgs(d, ny_ub) : 0;
     if (d.csc) k_dual_price_csc<<<d.ntiles + nsw, TILE_COLS, 0, st>>>(d, nsw, 0);
     else k_dual_price<<<d.ntiles + nsw, PRICE_THREADS, 0, st>>>(d, nsw, 0);
-    k_dual_bfrt<<<1, BF_NT, 0, st>>>(d, d.ntiles + nsw);
+    return d.ntiles + nsw;
+}
+
+static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st);
+
+hipError_t launch_dual_iteration_head(const Dev& d, int k_ub, int ny_ub, hipStream_t st) {
+    const int nreg = dual_head(d, k_ub, ny_ub, st);
+    k_dual_pack<<<1, BF_NT, 0, st>>>(d, nreg);
+    return hipGetLastError();
+}
+
+hipError_t launch_dual_iteration_tail(const Dev& d, int k_ub, hipStream_t st) {
+    k_dual_bfrt<<<1, BF_NT, 0, st>>>(d, 0, 1);
+    return dual_tail(d, k_ub, st);
+}
+
+hipError_t launch_dual_iteration(const Dev& d, int k_ub, int ny_ub, hipStream_t st) {
+    const int nreg = dual_head(d, k_ub, ny_ub, st);
+    k_dual_bfrt<<<1, BF_NT, 0, st>>>(d, nreg, 0);
+    return dual_tail(d, k_ub, st);
+}
+
+// the bound flips' FTRAN and x_B update, then FTRAN of a_q and the pivot
+static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st) {
+    const int m = d.m;
+    const size_t lds = (size_t)k_ub * sizeof(double);
+    const int lds_row = lds <= 48 * 1024;
+    unsigned nrw = cdiv(k_ub > 0 ? k_ub : 1, 4);
+    if (nrw > 1024) nrw = 1024;
     k_dual_flip_col<<<d.csc ? 1u : cdiv(m > 0 ? m : 1, 256), 256, 0, st>>>(d);
     if (k_ub > 0) k_dual_flip_bump<<<nrw, 256, lds_row ? lds : 0, st>>>(d, lds_row);
     k_dual_flip_apply<<<cdiv((int64_t)m + k_ub, 256), 256, 0, st>>>(d);
@@ -4563,7 +4637,7 @@ hipError_t launch_refactor_primal(const Dev& d, int k, hipStream_t st) {
 }
 
 hipError_t launch_devex_reset(const Dev& d, hipStream_t st) {
-    k_devex_reset<<<cdiv((int64_t)d.n + d.m, 256), 256, 0, st>>>(d);
+    k_devex_reset<<<cdiv((int64_t)(d.N > d.n ? d.N : d.n) + d.m, 256), 256, 0, st>>>(d);
     return hipGetLastError();
 }
 

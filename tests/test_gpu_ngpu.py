@@ -250,3 +250,60 @@ def test_ngpu_host_load_once(gpu):
             np.testing.assert_array_equal(g.trace, o.trace)
         else:
             _same(g, o, ngpu)
+
+
+def _same_dual(g, o, tag):
+    assert g.status == o.status, (tag, g.status, o.status)
+    np.testing.assert_array_equal(g.trace, o.trace, err_msg=tag)
+    assert g.stats["dual_iterations"] == o.stats["dual_iterations"], tag
+    assert g.stats["bound_flips"] == o.stats["bound_flips"], tag
+    if g.status in (0, 1):
+        np.testing.assert_array_equal(g.basis, o.basis, err_msg=tag)
+        assert abs(g.objval - o.objval) <= 1e-12 * max(1.0, abs(o.objval)), tag
+        if len(o.x):
+            np.testing.assert_allclose(g.x, o.x, rtol=1e-12, atol=1e-12 * max(1.0, np.abs(o.x).max()), err_msg=tag)
+
+
+@pytest.mark.parametrize("ngpu", [2, 3])
+def test_ngpu_dual_matches_oracle(gpu, ngpu):
+    """SIMPLEX_DUAL_PRIMAL (lp_solve's default, R/class.R:262 / :276) on the
+    column-sharded ranks of one handle, A replicated: each rank prices its
+    shard and packs its ratio-test candidates (the last rank also the slacks),
+    the all-gather hands every rank all of them in one-GPU order, and the
+    bound-flipping ratio test runs identically on every rank -- the pivot
+    trace, flips and optimum are the oracle's run_dual bit for bit."""
+    from conftest import load_known_answers, load_robust_lps
+    from fuzz_lps import fuzz_set
+    from oracle import solve_dense as orc
+    used = 0
+    recs = load_known_answers() + load_robust_lps() + fuzz_set(60)
+    for rec in recs:
+        if len(rec["obj"]) < ngpu:
+            continue  # (every rank prices at least one column)
+        args = (rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], rec["maximize"])
+        tag = rec.get("name", "f%s" % rec.get("seed"))
+        g = gpu.solve_dense(*args, trace=100000, simplex=6, ngpu=ngpu)
+        o = orc(*args, trace_cap=100000, simplex=6)
+        _same_dual(g, o, tag)
+        used += o.stats["dual_iterations"] > 0
+        if o.stats["dual_iterations"] > 0:
+            assert g.stats["simplex"] == 6 and g.stats["world_size"] == ngpu, tag
+    assert used >= 30, used
+
+
+def test_ngpu_dual_kkt_flips(gpu):
+    """The Netlib-shaped KKT LP (boxed columns, bound flips every few pivots)
+    on 3 column shards: flips of columns on every shard, the trace and the
+    optimum the oracle's."""
+    from conftest import load_sparse_lu
+    from easylp_amd.synth import dense_of, sparse_kkt
+    from oracle import solve_dense as orc
+    k = next(f for f in load_sparse_lu() if f["name"] == "kkt_2000x10000")
+    cp, ri, v, b, c, u, obj = sparse_kkt(k["seed"], 600, 3000, 60)
+    m, n = 600, 3000
+    A = dense_of(cp, ri, v, m, n)
+    dirs, lo = np.ones(m, np.int32), np.zeros(n)
+    g = gpu.solve_dense(A, dirs, b, c, lo, u, True, trace=100000, simplex=6, ngpu=3)
+    o = orc(A, dirs, b, c, lo, u, True, trace_cap=100000, simplex=6)
+    assert o.stats["bound_flips"] > 0 and o.stats["dual_iterations"] > 0
+    _same_dual(g, o, "kkt600x3000")

@@ -77,6 +77,49 @@ def test_sharded_matches_oracle(world, replicate, p2p):
             assert g["stats"]["world_size"] == world
 
 
+@pytest.mark.parametrize("world,p2p", [(2, False), (3, False), (2, True)])
+def test_sharded_dual_matches_oracle(world, p2p):
+    """SIMPLEX_DUAL_PRIMAL across processes (host transport, A replicated): the
+    ranks all-gather their ratio-test candidates every dual iteration and walk
+    the oracle's run_dual path bit for bit; with the mailbox on (p2p) the dual
+    iterations skip it and the primal phase 2 uses it."""
+    from dist_worker import sharded_solve_worker
+    from fuzz_lps import fuzz_set
+    from oracle import solve_dense as orc
+    cases = [_cases()[1]] + [{"kind": "dense", "lp": (r["A"], r["dir"], r["rhs"], r["obj"], r["lo"], r["up"],
+                                                      r["maximize"])}
+                             for r in fuzz_set(40) if len(r["obj"]) >= world][:12]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=sharded_solve_worker, args=(r, world, port, q, cases, 1, p2p, {"simplex": 6}))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, results, errors = q.get(timeout=240)
+        assert errors == 0
+        res[r] = results
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    duals = 0
+    for ci, case in enumerate(cases):
+        A, dirs, rhs, obj, lo, up, mx = case["lp"]
+        o = orc(A, dirs, rhs, obj, lo, up, mx, trace_cap=200000, simplex=6)
+        duals += o.stats["dual_iterations"] > 0
+        for r in range(world):
+            g = res[r][ci]
+            assert g["status"] == o.status, ci
+            np.testing.assert_array_equal(g["trace"], o.trace)
+            assert g["stats"]["dual_iterations"] == o.stats["dual_iterations"]
+            if o.status == 0:
+                np.testing.assert_array_equal(g["basis"], o.basis)
+                assert abs(g["objval"] - o.objval) <= 1e-12 * max(1.0, abs(o.objval))
+    assert duals >= 5, duals
+
+
 def test_rccl_single_rank_p2p_mailbox(monkeypatch):
     """The mailbox exchange on a 1-rank RCCL communicator: the select kernel
     writes its record into its own mailbox and waits for it."""
