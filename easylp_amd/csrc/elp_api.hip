@@ -148,8 +148,9 @@ struct elp_handle {
     std::vector<double> mip_x;   // branch and bound: the incumbent (elp_get_solution)
 };
 
-// elp_control.simplex = 0 (include/easylp_hip.h)
-#define ELP_SIMPLEX_DEFAULT ELP_SIMPLEX_PRIMAL_PRIMAL
+// elp_control.simplex = 0 (include/easylp_hip.h): lp_solve's default,
+// SIMPLEX_DUAL_PRIMAL, wherever the dual phase exists (dual_phase1)
+#define ELP_SIMPLEX_DEFAULT ELP_SIMPLEX_DUAL_PRIMAL
 
 extern "C" void elp_default_control(elp_control* c) {
     std::memset(c, 0, sizeof(*c));
@@ -1029,8 +1030,9 @@ static void scale_csc(elp_handle* h, const int64_t* cp, const int32_t* ri, doubl
 }
 
 // the phase-1 method (elp_control.simplex; lp_solve's set_simplextype): the
-// dual simplex on one GPU with the bump inverse; column-sharded solves and the
-// sparse-LU engine keep the primal phase 1 on artificials
+// dual simplex with the bump inverse on one GPU or on column-sharded ranks that
+// hold all of A; ranks with column shards only and the sparse-LU engine keep the
+// primal phase 1 on artificials (elp_stats.simplex reports what ran)
 static int simplex_type(const elp_handle* h) {
     return h->ctl.simplex == 0 ? ELP_SIMPLEX_DEFAULT : h->ctl.simplex;
 }
@@ -2502,7 +2504,7 @@ static int run_bnb(elp_handle* h, int32_t* out_status) {
     std::vector<double> x((size_t)n), best_x;
     // SIMPLEX_DUAL_PRIMAL on one GPU: node LPs after the first continue from
     // the basis of the node solved last (reload_bounds_warm; oracle warm_core)
-    const bool warm = dual_phase1(h) && h->comm.kind == 0 && h->m > 0;
+    const bool warm = dual_phase1(h) && h->m > 0;
     bool warm_ok = false;
     while (!stack.empty()) {
         Node nd = std::move(stack.back());

@@ -3636,19 +3636,21 @@ DEV void warm_fix(const Dev& d, int jl, bool structural, double dj, double dtol)
     }
 }
 
-// the node's bounds of the local structurals (scaled), the real costs, and the
-// bump positions' cached bounds / costs; lower > upper flags the node infeasible
+// the node's bounds of the local structurals (scaled; lo / up hold all N
+// columns by global id), the real costs, and the bump positions' cached bounds /
+// costs; lower > upper on any column flags the node infeasible (every
+// column-sharded rank checks all N, so all agree)
 __global__ void k_warm_bounds(Dev d, const double* __restrict__ lo, const double* __restrict__ up) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t < d.n) {
-        d.lb[t] = lo[t];
-        d.ub[t] = up[t];
+        d.lb[t] = lo[d.col0 + t];
+        d.ub[t] = up[d.col0 + t];
         d.cost[t] = d.maximize ? -d.obj[t] : d.obj[t];
-        if (lo[t] > up[t]) atomicOr(&d.ctl->infeasible_bounds, 1);
     }
+    if (t < d.N && lo[t] > up[t]) atomicOr(&d.ctl->infeasible_bounds, 1);
     if (t < d.m) d.cost[d.n + t] = 0.0;
     if (t < d.ctl->k) {
-        const int j = d.Sl[t];  // (one GPU: global = local)
+        const int j = d.Sl[t];  // (a global id)
         d.slo[t] = lo[j];
         d.shi[t] = up[j];
         const double o = d.objg[j];
@@ -4548,7 +4550,7 @@ static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st) {
 }
 
 hipError_t launch_warm_start(const Dev& d, const double* lo, const double* up, int k, int ny, hipStream_t st) {
-    const int64_t mx = std::max<int64_t>(std::max<int64_t>(d.n, d.m), 1);
+    const int64_t mx = std::max<int64_t>(std::max<int64_t>(d.N, d.m), 1);
     k_warm_bounds<<<cdiv(mx, 256), 256, 0, st>>>(d, lo, up);
     const hipError_t e = launch_btran_exact(d, k, st);  // y = B^-T c_B (the real costs)
     if (e != hipSuccess) return e;

@@ -125,7 +125,11 @@ typedef struct elp_control {
                                 (6) -- phase 1 by the dual simplex when the slack
                                 basis is primal infeasible, phase 2 primal;
                                 ELP_SIMPLEX_PRIMAL_PRIMAL (5) -- phase 1 primal on
-                                artificials.  0: the default    */
+                                artificials.  0: the default = lp_solve's,
+                                DUAL_PRIMAL where the dual phase exists (one
+                                GPU, or column-sharded ranks holding all of A,
+                                with the bump inverse), else PRIMAL_PRIMAL;
+                                elp_stats.simplex reports what ran */
 } elp_control;
 
 #define ELP_SIMPLEX_PRIMAL_PRIMAL 5  /* elp_control.simplex (lp_solve's SIMPLEX_*) */

@@ -1389,8 +1389,9 @@ static void sensitivity(orc_t* s, const orc_control* ctl, const int32_t* dir, in
     free(d);
 }
 
-/* elp_control.simplex's default (include/easylp_hip.h): 0 means it */
-#define ORC_SIMPLEX_DEFAULT 5
+/* elp_control.simplex's default (include/easylp_hip.h): 0 means it --
+ * SIMPLEX_DUAL_PRIMAL, lp_solve's default (set_simplextype) */
+#define ORC_SIMPLEX_DEFAULT 6
 static int simplex_type(const orc_control* c) { return c->simplex == 0 ? ORC_SIMPLEX_DEFAULT : c->simplex; }
 
 void orc_default_control(orc_control* c) {

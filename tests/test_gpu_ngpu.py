@@ -145,11 +145,13 @@ def test_ngpu_sensitivity(gpu, ngpu, replicate):
     A, b, c = generate_dense(seed, m, n)
     d = np.ones(m, np.int32)
     cases = [(A, d, b, c, None, None, True), _general_lp() + (True,)]
+    # (column-only shards keep the primal phase 1: compare like with like)
+    sx = 5 if replicate == 2 else 0
     for (A_, d_, r_, c_, lo_, up_, mx) in cases:
-        o = orc(A_, d_, r_, c_, lo_, up_, mx, sens=True)
-        one = gpu.solve_dense(A_, d_, r_, c_, lo_, up_, maximize=mx, sensitivity=True)
+        o = orc(A_, d_, r_, c_, lo_, up_, mx, sens=True, simplex=sx)
+        one = gpu.solve_dense(A_, d_, r_, c_, lo_, up_, maximize=mx, sensitivity=True, simplex=sx)
         g = gpu.solve_dense(A_, d_, r_, c_, lo_, up_, maximize=mx, sensitivity=True, ngpu=ngpu,
-                            replicate=replicate)
+                            replicate=replicate, simplex=sx)
         assert g.status == one.status == o.status == 0
         assert g.stats["world_size"] == ngpu
         np.testing.assert_array_equal(g.basis, o.basis)

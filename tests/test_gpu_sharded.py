@@ -48,7 +48,10 @@ def test_sharded_matches_oracle(world, replicate, p2p):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=sharded_solve_worker, args=(r, world, port, q, cases, replicate, p2p))
+    # column-only shards (replicate 2) keep the primal phase 1 (SIMPLEX_PRIMAL_PRIMAL)
+    sx = 5 if replicate == 2 else 0
+    procs = [ctx.Process(target=sharded_solve_worker, args=(r, world, port, q, cases, replicate, p2p,
+                                                            {"simplex": sx}))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -66,7 +69,7 @@ def test_sharded_matches_oracle(world, replicate, p2p):
             o = orc(A, np.ones(case["m"], np.int32), b, c, maximize=True, trace_cap=200000)
         else:
             A, dirs, rhs, obj, lo, up, mx = case["lp"]
-            o = orc(A, dirs, rhs, obj, lo, up, mx, trace_cap=200000)
+            o = orc(A, dirs, rhs, obj, lo, up, mx, trace_cap=200000, simplex=sx)
         for r in range(world):
             g = res[r][ci]
             assert g["status"] == o.status
