@@ -714,7 +714,7 @@ static int alloc_all_body(elp_handle* h) {
     // One GPU, or column-sharded ranks holding all of A (the flipped and the
     // entering columns are read from the replicated copy); the ratio test sees
     // every rank's candidates: up to N + m of them
-    if (!h->lu && (!d.sharded || (h->replicated && !h->csc))) {
+    if (!h->lu && (!d.sharded || !h->csc)) {
         const int64_t Ng = h->n;
         d.dregs = d.ntiles + (int32_t)((mm + TILE_COLS - 1) / TILE_COLS) + 2;
         d.dchzn = (int32_t)((2 * mm + 255) / 256 + 2);
@@ -1030,15 +1030,15 @@ static void scale_csc(elp_handle* h, const int64_t* cp, const int32_t* ri, doubl
 }
 
 // the phase-1 method (elp_control.simplex; lp_solve's set_simplextype): the
-// dual simplex with the bump inverse on one GPU or on column-sharded ranks that
-// hold all of A; ranks with column shards only and the sparse-LU engine keep the
-// primal phase 1 on artificials (elp_stats.simplex reports what ran)
+// dual simplex with the bump inverse, on one GPU or column-sharded; the
+// sparse-LU engine keeps the primal phase 1 on artificials (elp_stats.simplex
+// reports what ran)
 static int simplex_type(const elp_handle* h) {
     return h->ctl.simplex == 0 ? ELP_SIMPLEX_DEFAULT : h->ctl.simplex;
 }
 static bool dual_phase1(const elp_handle* h) {
     return simplex_type(h) == ELP_SIMPLEX_DUAL_PRIMAL && !h->lu && h->d.dcand &&
-           (h->comm.kind == 0 || (h->replicated && !h->csc && h->d.dsend));
+           (h->comm.kind == 0 || (!h->csc && h->d.dsend));
 }
 
 // common tail of elp_load_*: bounds, rows, control block, phase decision
@@ -1879,7 +1879,22 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
                 HIPCHK(launch_dual_iteration_head(h->d, kub, nyub, h->st));
                 rc = h->comm.allgather(h->d.dsend, h->d.drecv, ((size_t)h->d.dcap + 1) * sizeof(DualCand), h->st);
                 if (rc) return fail(rc, "dual ratio-test candidate all-gather failed");
-                HIPCHK(launch_dual_iteration_tail(h->d, kub, h->st));
+                if (h->replicated) {
+                    HIPCHK(launch_dual_iteration_tail(h->d, kub, h->st));
+                } else {
+                    // column-only shards: the entering column travels (all-reduce of
+                    // the owner's copy), and a_F = sum of the flipped columns is one
+                    // per-row chain continued shard after shard (a broadcast each)
+                    HIPCHK(launch_dual_ratio_shards(h->d, h->st));
+                    rc = h->comm.allreduce_sum_f64(h->d.pkt, (size_t)h->m, h->st);
+                    if (rc) return fail(rc, "entering-column all-reduce failed");
+                    for (int r = 0; r < h->comm.world; ++r) {
+                        if (r == h->comm.rank) HIPCHK(launch_dual_flip_part(h->d, h->st));
+                        rc = h->comm.bcast_f64(h->d.aF, (size_t)h->m, r, h->st);
+                        if (rc) return fail(rc, "bound-flip column broadcast failed");
+                    }
+                    HIPCHK(launch_dual_iteration_finish(h->d, kub, h->st));
+                }
             } else if (h->comm.kind == 0 || h->d.p2p) {  // (p2p: min-loc inside the select kernel)
                 HIPCHK(launch_iteration(h->d, kub, nyub, h->phase, h->st, e0, e1, t));
             } else {

@@ -422,6 +422,12 @@ hipError_t launch_dual_iteration(const Dev& d, int k_ub, int ny_ub, hipStream_t 
 // candidates (identical on all ranks) and the rest of the iteration
 hipError_t launch_dual_iteration_head(const Dev& d, int k_ub, int ny_ub, hipStream_t st);
 hipError_t launch_dual_iteration_tail(const Dev& d, int k_ub, hipStream_t st);
+// column-only shards (A not replicated): ratio test + the owner's entering
+// column into pkt[0, m) (the host all-reduces it), then per rank in rank order
+// its part of a_F's chain (the host broadcasts a_F from that rank), then the rest
+hipError_t launch_dual_ratio_shards(const Dev& d, hipStream_t st);
+hipError_t launch_dual_flip_part(const Dev& d, hipStream_t st);
+hipError_t launch_dual_iteration_finish(const Dev& d, int k_ub, hipStream_t st);
 // MIP node warm start (oracle warm_core): new column bounds lo / up (local,
 // scaled), real costs, y, and every nonbasic column re-placed for the node
 // (k, ny: the kept basis's bump dimension and |Y|); the host then refactors

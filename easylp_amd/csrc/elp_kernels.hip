@@ -4130,6 +4130,41 @@ __global__ void __launch_bounds__(256) k_dual_flip_col(Dev d) {
     d.aF[i] = acc;
 }
 
+// column-only shards (no replicated A): the owner of a structural entering
+// column packs it (scaled) into pkt[0, m), every other rank zeros -- the host
+// all-reduces pkt[0, m), an exact copy; k_dual_bfrt wrote pkt[m, m + 4) on all
+// ranks.  a_F starts at 0 for the flips' chain (k_dual_flip_part)
+__global__ void __launch_bounds__(256) k_dual_qpack(Dev d) {
+    const DevCtl* c = d.ctl;
+    if (c->status != ST_RUN) return;
+    const int i = blockIdx.x * 256 + threadIdx.x, m = d.m;
+    if (i >= m) return;
+    const int q = c->q;
+    const int ql = q < d.N ? loc_of(d, q) : -1;
+    d.pkt[i] = ql >= 0 ? sca(d, d.A[(size_t)ql * (size_t)m + i], i, q) : 0.0;
+    d.aF[i] = 0.0;
+}
+
+// a_F's per-row chain over this shard's flips (the flip list ascends by
+// global id, so the shards' runs follow each other in rank order): continued
+// from the a_F the previous rank broadcast -- the one-GPU chain's bits
+__global__ void __launch_bounds__(256) k_dual_flip_part(Dev d) {
+    const DevCtl* c = d.ctl;
+    const int nf = c->nflip;
+    if (c->status != ST_RUN || nf == 0) return;
+    const int m = d.m;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    double acc = d.aF[i];
+    for (int f = 0; f < nf; ++f) {
+        const int j = d.dflip[f];
+        const int jl = loc_of(d, j);
+        if (jl < 0) continue;
+        acc = fma(sca(d, d.A[(size_t)jl * (size_t)m + i], i, j), d.dflipdx[f], acc);
+    }
+    d.aF[i] = acc;
+}
+
 // fS = Minv a_F[R] (one wave per bump row, wave order)
 __global__ void __launch_bounds__(256) k_dual_flip_bump(Dev d, int lds_row) {
     extern __shared__ __attribute__((aligned(16))) double afr_lds[];
@@ -4505,7 +4540,7 @@ static int dual_head(const Dev& d, int k_ub, int ny_ub, hipStream_t st) {
     return d.ntiles + nsw;
 }
 
-static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st);
+static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_col = true);
 
 hipError_t launch_dual_iteration_head(const Dev& d, int k_ub, int ny_ub, hipStream_t st) {
     const int nreg = dual_head(d, k_ub, ny_ub, st);
@@ -4518,6 +4553,21 @@ hipError_t launch_dual_iteration_tail(const Dev& d, int k_ub, hipStream_t st) {
     return dual_tail(d, k_ub, st);
 }
 
+// column-only shards: the ratio test over the gathered candidates, then the
+// owner's entering column into pkt[0, m) (others: zeros) and a_F cleared
+hipError_t launch_dual_ratio_shards(const Dev& d, hipStream_t st) {
+    k_dual_bfrt<<<1, BF_NT, 0, st>>>(d, 0, 1);
+    k_dual_qpack<<<cdiv(d.m > 0 ? d.m : 1, 256), 256, 0, st>>>(d);
+    return hipGetLastError();
+}
+hipError_t launch_dual_flip_part(const Dev& d, hipStream_t st) {
+    k_dual_flip_part<<<cdiv(d.m > 0 ? d.m : 1, 256), 256, 0, st>>>(d);
+    return hipGetLastError();
+}
+hipError_t launch_dual_iteration_finish(const Dev& d, int k_ub, hipStream_t st) {
+    return dual_tail(d, k_ub, st, false);
+}
+
 hipError_t launch_dual_iteration(const Dev& d, int k_ub, int ny_ub, hipStream_t st) {
     const int nreg = dual_head(d, k_ub, ny_ub, st);
     k_dual_bfrt<<<1, BF_NT, 0, st>>>(d, nreg, 0);
@@ -4525,13 +4575,14 @@ hipError_t launch_dual_iteration(const Dev& d, int k_ub, int ny_ub, hipStream_t 
 }
 
 // the bound flips' FTRAN and x_B update, then FTRAN of a_q and the pivot
-static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st) {
+// (flip_col false: a_F was formed by the column-only shards' chain already)
+static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_col) {
     const int m = d.m;
     const size_t lds = (size_t)k_ub * sizeof(double);
     const int lds_row = lds <= 48 * 1024;
     unsigned nrw = cdiv(k_ub > 0 ? k_ub : 1, 4);
     if (nrw > 1024) nrw = 1024;
-    k_dual_flip_col<<<d.csc ? 1u : cdiv(m > 0 ? m : 1, 256), 256, 0, st>>>(d);
+    if (flip_col) k_dual_flip_col<<<d.csc ? 1u : cdiv(m > 0 ? m : 1, 256), 256, 0, st>>>(d);
     if (k_ub > 0) k_dual_flip_bump<<<nrw, 256, lds_row ? lds : 0, st>>>(d, lds_row);
     k_dual_flip_apply<<<cdiv((int64_t)m + k_ub, 256), 256, 0, st>>>(d);
     // the entering column q (k_dual_bfrt's, candidate 0): a_R, alpha_S (+ staging)

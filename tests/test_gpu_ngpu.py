@@ -145,13 +145,11 @@ def test_ngpu_sensitivity(gpu, ngpu, replicate):
     A, b, c = generate_dense(seed, m, n)
     d = np.ones(m, np.int32)
     cases = [(A, d, b, c, None, None, True), _general_lp() + (True,)]
-    # (column-only shards keep the primal phase 1: compare like with like)
-    sx = 5 if replicate == 2 else 0
     for (A_, d_, r_, c_, lo_, up_, mx) in cases:
-        o = orc(A_, d_, r_, c_, lo_, up_, mx, sens=True, simplex=sx)
-        one = gpu.solve_dense(A_, d_, r_, c_, lo_, up_, maximize=mx, sensitivity=True, simplex=sx)
+        o = orc(A_, d_, r_, c_, lo_, up_, mx, sens=True)
+        one = gpu.solve_dense(A_, d_, r_, c_, lo_, up_, maximize=mx, sensitivity=True)
         g = gpu.solve_dense(A_, d_, r_, c_, lo_, up_, maximize=mx, sensitivity=True, ngpu=ngpu,
-                            replicate=replicate, simplex=sx)
+                            replicate=replicate)
         assert g.status == one.status == o.status == 0
         assert g.stats["world_size"] == ngpu
         np.testing.assert_array_equal(g.basis, o.basis)
@@ -266,14 +264,17 @@ def _same_dual(g, o, tag):
             np.testing.assert_allclose(g.x, o.x, rtol=1e-12, atol=1e-12 * max(1.0, np.abs(o.x).max()), err_msg=tag)
 
 
-@pytest.mark.parametrize("ngpu", [2, 3])
-def test_ngpu_dual_matches_oracle(gpu, ngpu):
+@pytest.mark.parametrize("ngpu,replicate", [(2, 0), (3, 0), (2, 2), (3, 2)])
+def test_ngpu_dual_matches_oracle(gpu, ngpu, replicate):
     """SIMPLEX_DUAL_PRIMAL (lp_solve's default, R/class.R:262 / :276) on the
     column-sharded ranks of one handle, A replicated: each rank prices its
     shard and packs its ratio-test candidates (the last rank also the slacks),
     the all-gather hands every rank all of them in one-GPU order, and the
     bound-flipping ratio test runs identically on every rank -- the pivot
-    trace, flips and optimum are the oracle's run_dual bit for bit."""
+    trace, flips and optimum are the oracle's run_dual bit for bit.  With
+    column-only shards (replicate 2) the entering column is all-reduced from
+    its owner and the flipped columns' sum a_F is one per-row chain continued
+    shard after shard."""
     from conftest import load_known_answers, load_robust_lps
     from fuzz_lps import fuzz_set
     from oracle import solve_dense as orc
@@ -284,7 +285,7 @@ def test_ngpu_dual_matches_oracle(gpu, ngpu):
             continue  # (every rank prices at least one column)
         args = (rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], rec["maximize"])
         tag = rec.get("name", "f%s" % rec.get("seed"))
-        g = gpu.solve_dense(*args, trace=100000, simplex=6, ngpu=ngpu)
+        g = gpu.solve_dense(*args, trace=100000, simplex=6, ngpu=ngpu, replicate=replicate)
         o = orc(*args, trace_cap=100000, simplex=6)
         _same_dual(g, o, tag)
         used += o.stats["dual_iterations"] > 0
@@ -305,7 +306,8 @@ def test_ngpu_dual_kkt_flips(gpu):
     m, n = 600, 3000
     A = dense_of(cp, ri, v, m, n)
     dirs, lo = np.ones(m, np.int32), np.zeros(n)
-    g = gpu.solve_dense(A, dirs, b, c, lo, u, True, trace=100000, simplex=6, ngpu=3)
     o = orc(A, dirs, b, c, lo, u, True, trace_cap=100000, simplex=6)
     assert o.stats["bound_flips"] > 0 and o.stats["dual_iterations"] > 0
-    _same_dual(g, o, "kkt600x3000")
+    for replicate in (1, 2):
+        g = gpu.solve_dense(A, dirs, b, c, lo, u, True, trace=100000, simplex=6, ngpu=3, replicate=replicate)
+        _same_dual(g, o, "kkt600x3000 replicate %d" % replicate)

@@ -48,10 +48,7 @@ def test_sharded_matches_oracle(world, replicate, p2p):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    # column-only shards (replicate 2) keep the primal phase 1 (SIMPLEX_PRIMAL_PRIMAL)
-    sx = 5 if replicate == 2 else 0
-    procs = [ctx.Process(target=sharded_solve_worker, args=(r, world, port, q, cases, replicate, p2p,
-                                                            {"simplex": sx}))
+    procs = [ctx.Process(target=sharded_solve_worker, args=(r, world, port, q, cases, replicate, p2p))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -69,7 +66,7 @@ def test_sharded_matches_oracle(world, replicate, p2p):
             o = orc(A, np.ones(case["m"], np.int32), b, c, maximize=True, trace_cap=200000)
         else:
             A, dirs, rhs, obj, lo, up, mx = case["lp"]
-            o = orc(A, dirs, rhs, obj, lo, up, mx, trace_cap=200000, simplex=sx)
+            o = orc(A, dirs, rhs, obj, lo, up, mx, trace_cap=200000)
         for r in range(world):
             g = res[r][ci]
             assert g["status"] == o.status
@@ -80,8 +77,9 @@ def test_sharded_matches_oracle(world, replicate, p2p):
             assert g["stats"]["world_size"] == world
 
 
-@pytest.mark.parametrize("world,p2p", [(2, False), (3, False), (2, True)])
-def test_sharded_dual_matches_oracle(world, p2p):
+@pytest.mark.parametrize("world,replicate,p2p", [(2, 1, False), (3, 1, False), (2, 1, True), (2, 2, False),
+                                                 (3, 2, False)])
+def test_sharded_dual_matches_oracle(world, replicate, p2p):
     """SIMPLEX_DUAL_PRIMAL across processes (host transport, A replicated): the
     ranks all-gather their ratio-test candidates every dual iteration and walk
     the oracle's run_dual path bit for bit; with the mailbox on (p2p) the dual
@@ -95,7 +93,8 @@ def test_sharded_dual_matches_oracle(world, p2p):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=sharded_solve_worker, args=(r, world, port, q, cases, 1, p2p, {"simplex": 6}))
+    procs = [ctx.Process(target=sharded_solve_worker, args=(r, world, port, q, cases, replicate, p2p,
+                                                            {"simplex": 6}))
              for r in range(world)]
     for p in procs:
         p.start()
