@@ -2197,6 +2197,9 @@ enum { SI_VSQ, SI_RPOS0, SI_YPOS0, SI_YLAST, SI_SLLAST, SI_RLLAST, SI_RPOSYL, SI
 // FTRAN column, the leaving variable goes to beta_r; the bookkeeping, the B^-1
 // row and the dual update are the primal's (phase 2), the plan carries the dual
 // Devex update and the loop-top checks run here (no deferral).
+#ifndef ELP_BOOK_WG
+#define ELP_BOOK_WG 1
+#endif
 template <int PFT, bool DUAL = false>
 __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, int lds_row, int defer,
                                                int nmain, int k_ub, int dslot, int nreg) {
@@ -2224,7 +2227,11 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
     int bland = c->snap_bland;
     const int devex = c->devex;
     int apos_c = c->snap_apos;
-    const bool lead = blockIdx.x == 0;
+    // the bookkeeping workgroup: a workgroup of its own (ELP_BOOK_WG, grid
+    // [nmain main][1 bookkeeping][AR copies]) that skips the B^-1 row and the dual
+    // update of bump positions, so its single-lane tail starts at the decision;
+    // 0: workgroup 0, after its share of those (r03)
+    const bool lead = ELP_BOOK_WG ? (int)blockIdx.x == nmain : blockIdx.x == 0;
     // bookkeeping scalars, snapshot by k_ftran_zr (see DevCtl)
     const double sv_lbq = c->snap_lbq, sv_ubq = c->snap_ubq, sv_xq = c->snap_xq, sv_cq = c->snap_cq;
     const double sv_csl = c->snap_csl, sv_slol = c->snap_slol, sv_shil = c->snap_shil;
@@ -2464,7 +2471,7 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
         }
         return;
     }
-    if ((int)blockIdx.x >= nmain) {  // deferred flow: this pivot's AR row copies
+    if ((int)blockIdx.x >= nmain + ELP_BOOK_WG) {  // deferred flow: this pivot's AR row copies
         if (d.csc) return;
         const int lrow = best.e < m ? best.e : -1;
         const bool leave_art = best.var >= d.N + m;
@@ -2483,8 +2490,8 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
             }
         }
         if (rm_slot < 0 && ap_slot < 0) return;
-        const int64_t tstride = (int64_t)(gridDim.x - nmain) * blockDim.x;
-        for (int64_t j = (int64_t)(blockIdx.x - nmain) * blockDim.x + tid; j < d.n; j += tstride) {
+        const int64_t tstride = (int64_t)(gridDim.x - nmain - ELP_BOOK_WG) * blockDim.x;
+        for (int64_t j = (int64_t)(blockIdx.x - nmain - ELP_BOOK_WG) * blockDim.x + tid; j < d.n; j += tstride) {
             if (rm_slot >= 0 && rm_slot != rm_last) d.AR[ar_at(d, rm_slot, j)] = d.AR[ar_at(d, rm_last, j)];
             if (ap_slot >= 0) d.AR[ar_at(d, ap_slot, j)] = a_row(d, ap_row, j);
         }
@@ -2529,7 +2536,9 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
         const int moved = sv_ylast;
         t0_ymoved = d.y[moved >= 0 ? moved : 0];
     }
-    if (lrow_all >= 0 && k > 0) {
+    // (a separate bookkeeping workgroup forms no B^-1 row entries; it needs
+    //  A[lrow, S] only for case D's vvec[a])
+    if (lrow_all >= 0 && k > 0 && !(ELP_BOOK_WG && lead && !(phase == 2 && pcx == PC_D))) {
         // huge bumps: every workgroup writes the same values to d.vrow (benign)
         double* asrow = lds_row ? asrow_lds : d.vrow;
         for (int j0 = tid; j0 < k; j0 += 1024) {  // 4 loads in flight per thread (k <= 1024: one pass)
@@ -4470,12 +4479,14 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
         //  loop after the decision -- 16 per lane measured slower at 10 000 x
         //  500 000 (16.5 vs 14.7 us, r01), 10 as well (12.01 vs 11.75 us at k
         //  529, r03 A/B over the last 2000 iterations))
+        const unsigned nbk = ELP_BOOK_WG;  // (the bookkeeping workgroup after the main ones)
         if (phase == 3)
-            k_ratio<8, true><<<nmain, 256, lds_row ? lds : 0, st>>>(DEV_ARG(d), 2, nrt + nbt, lds_row, 0, (int)nmain, k_ub,
-                                                                   dslot, nrt + nbt * zw);
+            k_ratio<8, true><<<nmain + nbk, 256, lds_row ? lds : 0, st>>>(DEV_ARG(d), 2, nrt + nbt, lds_row, 0,
+                                                                         (int)nmain, k_ub, dslot, nrt + nbt * zw);
         else
-            k_ratio<8><<<nmain + nar, 256, lds_row ? lds : 0, st>>>(DEV_ARG(d), phase, nrt + nbt, lds_row, defer,
-                                                                   (int)nmain, k_ub, dslot, nrt + nbt * zw);
+            k_ratio<8><<<nmain + nbk + nar, 256, lds_row ? lds : 0, st>>>(DEV_ARG(d), phase, nrt + nbt, lds_row,
+                                                                         defer, (int)nmain, k_ub, dslot,
+                                                                         nrt + nbt * zw);
     }
     if (!defer) {
         unsigned nb_minv, nb;
