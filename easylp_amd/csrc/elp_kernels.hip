@@ -2888,14 +2888,35 @@ DEV void apply_minv(const Dev& d, const Plan& P, int64_t e0, int64_t estride) {
     const int kk = P.pcase == PC_B ? k + 1 : P.pcase == PC_C ? k - 1 : k;
     const int64_t nel = (int64_t)kk * kk;
     const OldM oM{d.Minv, ldm, false}, oT{d.MinvT, ldm, true};
-    for (int64_t e = e0; e < 2 * nel; e += estride) {
-        if (e < nel) {
-            const int i = (int)(e / kk), j = (int)(e % kk);
-            d.Minv[(size_t)i * ldm + j] = minv_new(d, P, i, j, oM);
-        } else {
-            const int64_t f = e - nel;  // MinvT element (j, i) = new Minv (i, j)
-            const int j = (int)(f / kk), i = (int)(f % kk);
-            d.MinvT[(size_t)j * ldm + i] = minv_new(d, P, i, j, oT);
+    // element e -> (row, column) by one division per half, then carried along
+    // the stride (a 64-bit integer division is a long instruction sequence on
+    // the GPU; same elements, same values)
+    if (nel == 0) return;
+    const int64_t sq = estride / kk, sr = estride % kk;
+    int64_t e = e0;
+    if (e < nel) {
+        int64_t i = e / kk, j = e % kk;
+        for (; e < nel; e += estride) {
+            d.Minv[(size_t)i * ldm + (size_t)j] = minv_new(d, P, (int)i, (int)j, oM);
+            i += sq;
+            j += sr;
+            if (j >= kk) {
+                j -= kk;
+                ++i;
+            }
+        }
+    }
+    if (e < 2 * nel) {  // MinvT element (j, i) = new Minv (i, j), f = e - nel = j kk + i
+        const int64_t f = e - nel;
+        int64_t j = f / kk, i = f % kk;
+        for (; e < 2 * nel; e += estride) {
+            d.MinvT[(size_t)j * ldm + (size_t)i] = minv_new(d, P, (int)i, (int)j, oT);
+            j += sq;
+            i += sr;
+            if (i >= kk) {
+                i -= kk;
+                ++j;
+            }
         }
     }
 }
