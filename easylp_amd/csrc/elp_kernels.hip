@@ -3023,17 +3023,20 @@ __global__ void k_gj_init(Dev d, int k) {
     if (e < k) d.pivstep[e] = 0x7fffffff;
 }
 
-// one Gauss-Jordan column step: every block finds the pivot redundantly
-__global__ void __launch_bounds__(256) k_gj_step(Dev d, int k, int col, const double* __restrict__ W,
-                                                double* __restrict__ W2) {
-    __shared__ double sv[4];
-    __shared__ int sr[4];
-    __shared__ int s_p;
-    __shared__ double s_piv;
+// one Gauss-Jordan column step, two launches: k_gj_pivot (one workgroup) picks
+// the pivot row of column `col` -- largest |W[r][col]| among the rows not used
+// yet, the lowest row on ties (a total order) -- into perm[col]; k_gj_elim then
+// eliminates with it, GJ_PT consecutive elements per thread.  (r03 and before:
+// every elimination workgroup searched the pivot column again itself -- k
+// strided loads per workgroup, ~360 us per step at k = 2000.)
+constexpr int GJ_PT = 4;
+__global__ void __launch_bounds__(1024) k_gj_pivot(Dev d, int k, int col, const double* __restrict__ W) {
+    __shared__ double sv[16];
+    __shared__ int sr[16];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     double bv = -1.0;
     int br = 0x7fffffff;
-    for (int r = tid; r < k; r += 256) {
+    for (int r = tid; r < k; r += 1024) {
         if (d.pivstep[r] < col) continue;  // used in an earlier step
         const double v = fabs(W[(size_t)r * k + col]);
         if (v > bv || (v == bv && r < br)) {
@@ -3058,33 +3061,41 @@ __global__ void __launch_bounds__(256) k_gj_step(Dev d, int k, int col, const do
     if (tid == 0) {
         double v = sv[0];
         int r = sr[0];
-        for (int i = 1; i < 4; ++i)
+        for (int i = 1; i < 16; ++i)
             if (sv[i] > v || (sv[i] == v && sr[i] < r)) {
                 v = sv[i];
                 r = sr[i];
             }
-        s_p = r;
-        s_piv = W[(size_t)r * k + col];
-        if (blockIdx.x == 0) {
-            d.perm[col] = r;
-            d.pivstep[r] = col;
-            if (!(fabs(s_piv) > d.tol_singular)) d.ctl->status = ST_NUMFAIL;
+        d.perm[col] = r;
+        d.pivstep[r] = col;
+        if (!(fabs(W[(size_t)r * k + col]) > d.tol_singular)) d.ctl->status = ST_NUMFAIL;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_gj_elim(Dev d, int k, int col, const double* __restrict__ W,
+                                                 double* __restrict__ W2) {
+    const int p = d.perm[col];
+    const double piv = W[(size_t)p * k + col];
+    const int64_t kk = (int64_t)k * k;
+    const int64_t e0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * GJ_PT;
+    int r = (int)(e0 / k), j = (int)(e0 % k);
+#pragma unroll
+    for (int t = 0; t < GJ_PT; ++t, ++j) {
+        const int64_t e = e0 + t;
+        if (e >= kk) return;
+        if (j == k) {
+            j = 0;
+            ++r;
         }
+        double v;
+        if (r == p) {
+            v = (j == col) ? 1.0 / piv : W[(size_t)p * k + j] / piv;
+        } else {
+            const double f = W[(size_t)r * k + col];
+            v = (j == col) ? -(f / piv) : fma(-f, W[(size_t)p * k + j] / piv, W[(size_t)r * k + j]);
+        }
+        W2[e] = v;
     }
-    __syncthreads();
-    const int p = s_p;
-    const double piv = s_piv;
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + tid;
-    if (e >= (int64_t)k * k) return;
-    const int r = (int)(e / k), j = (int)(e % k);
-    double v;
-    if (r == p) {
-        v = (j == col) ? 1.0 / piv : W[(size_t)p * k + j] / piv;
-    } else {
-        const double f = W[(size_t)r * k + col];
-        v = (j == col) ? -(f / piv) : fma(-f, W[(size_t)p * k + j] / piv, W[(size_t)r * k + j]);
-    }
-    W2[e] = v;
 }
 
 __global__ void k_gj_final(Dev d, int k, const double* __restrict__ W) {
@@ -4212,26 +4223,48 @@ __global__ void __launch_bounds__(256) k_dual_flip_bump(Dev d, int lds_row) {
     }
 }
 
-// x_B -= B^-1 a_F: covered rows x -= sigma (a_F,i - A[i,S] fS) (zchunk order),
-// bump positions x -= fS
-__global__ void __launch_bounds__(256) k_dual_flip_apply(Dev d) {
+// x_B -= B^-1 a_F: covered rows x -= sigma (a_F,i - A[i,S] fS) (zchunk order:
+// a chain per 32-position chunk, the chunk sums added in order from 0), bump
+// positions x -= fS.  FTRAN-z's shape: row tiles of 32 rows x 8 waves, half-wave
+// h of wave w runs chunks 2w + h, + 16, ... with the chunk's AS values all in
+// flight, partials through LDS (LDSZ) or a slice of zpart (huge bumps); then
+// tiles of 512 bump positions.  (r03: one thread per row walking all k
+// positions -- ~90 workgroups, 317 us per call at m = 20 000, k <= 2000.)
+template <bool LDSZ>
+__global__ void __launch_bounds__(512) k_dual_flip_apply(Dev d, int nrt) {
+    extern __shared__ __attribute__((aligned(16))) double fzl[];  // [nch][32]
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN || c->nflip == 0) return;
     const int m = d.m, k = c->k;
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    if (t < m) {
-        const int u = d.cover[t];
-        if (u < 0) return;
-        double tot = 0.0;
-        for (int c0 = 0; c0 < k; c0 += ZCHUNK) {
-            double acc = 0.0;
-            const int c1 = min(k, c0 + ZCHUNK);
-            for (int p = c0; p < c1; ++p) acc = fma(d.AS[(size_t)p * (size_t)m + t], d.fS[p], acc);
-            tot = tot + acc;
+    if ((int)blockIdx.x >= nrt) {
+        const int p = (blockIdx.x - nrt) * 512 + threadIdx.x;
+        if (p < k) d.xs[p] = d.xs[p] - d.fS[p];
+        return;
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, hh = lane >> 5;
+    const int i = blockIdx.x * ZR_ROWS + r;
+    const int nch = (k + ZCHUNK - 1) / ZCHUNK;
+    double* zp = LDSZ ? fzl : d.zpart + (size_t)blockIdx.x * ZR_ROWS * (size_t)nch;
+    const double* col0 = d.AS + (i < m ? i : 0);
+    for (int ch = 2 * w + hh; ch < nch; ch += 16) {
+        const int c0 = ch * ZCHUNK, len = min(ZCHUNK, k - c0);
+        double a[ZCHUNK];
+#pragma unroll
+        for (int t = 0; t < ZCHUNK; ++t) a[t] = col0[(size_t)(c0 + (t < len ? t : len - 1)) * (size_t)m];
+        double acc = 0.0;
+#pragma unroll
+        for (int t = 0; t < ZCHUNK; ++t)
+            if (t < len) acc = fma(a[t], d.fS[c0 + t], acc);
+        zp[ch * ZR_ROWS + r] = acc;
+    }
+    __syncthreads();
+    if (w == 0 && hh == 0 && i < m) {
+        const int u = d.cover[i];
+        if (u >= 0) {
+            double tot = 0.0;
+            for (int ch = 0; ch < nch; ++ch) tot = tot + zp[ch * ZR_ROWS + r];
+            d.xr[i] = d.xr[i] - unit_sign(d, u, i) * (d.aF[i] - tot);
         }
-        d.xr[t] = d.xr[t] - unit_sign(d, u, t) * (d.aF[t] - tot);
-    } else if (t - m < k) {
-        d.xs[t - m] = d.xs[t - m] - d.fS[t - m];
     }
 }
 
@@ -4616,7 +4649,12 @@ static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_co
     if (nrw > 1024) nrw = 1024;
     if (flip_col) k_dual_flip_col<<<d.csc ? 1u : cdiv(m > 0 ? m : 1, 256), 256, 0, st>>>(d);
     if (k_ub > 0) k_dual_flip_bump<<<nrw, 256, lds_row ? lds : 0, st>>>(d, lds_row);
-    k_dual_flip_apply<<<cdiv((int64_t)m + k_ub, 256), 256, 0, st>>>(d);
+    {
+        const unsigned nrt = cdiv(m > 0 ? m : 1, ZR_ROWS), nbt = cdiv(k_ub > 0 ? k_ub : 1, 512);
+        const size_t zl = (size_t)cdiv(k_ub > 0 ? k_ub : 1, ZCHUNK) * ZR_ROWS * sizeof(double);
+        if (zl <= 48 * 1024) k_dual_flip_apply<true><<<nrt + nbt, 512, zl, st>>>(d, (int)nrt);
+        else k_dual_flip_apply<false><<<nrt + nbt, 512, 0, st>>>(d, (int)nrt);
+    }
     // the entering column q (k_dual_bfrt's, candidate 0): a_R, alpha_S (+ staging)
     if (lds <= 48 * 1024 && !d.force_select) {
         const size_t ldsz = lds > 64 ? lds : 64;
@@ -4690,7 +4728,8 @@ hipError_t launch_refactor_gj(const Dev& d, int k, hipStream_t st) {
     k_gj_init<<<cdiv(kk > k ? kk : k, 256), 256, 0, st>>>(d, k);
     double *W = d.W0, *W2 = d.W1;
     for (int c = 0; c < k; ++c) {
-        k_gj_step<<<cdiv(kk, 256), 256, 0, st>>>(d, k, c, W, W2);
+        k_gj_pivot<<<1, 1024, 0, st>>>(d, k, c, W);
+        k_gj_elim<<<cdiv(kk, 256 * GJ_PT), 256, 0, st>>>(d, k, c, W, W2);
         double* sw = W;
         W = W2;
         W2 = sw;
