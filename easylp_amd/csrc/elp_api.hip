@@ -214,7 +214,7 @@ static void free_dev(elp_handle* h, bool keep_big = false) {
                     d.cand,     d.pstamp, d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand, d.rcnt, d.AT,
                     d.pkt, d.objg, d.ract, d.cand_xchg, h->d_flag, d.cS, d.slo, d.shi, d.rlo, d.rhi,
                     (void*)d.cptr, (void*)d.rind, (void*)d.cval, (void*)d.rptr, (void*)d.cind,
-                    (void*)d.rval, d.qcol, d.qz, d.dstamp, d.rowvs, d.yvs, d.dw, d.dprev, (void*)d.srow,
+                    (void*)d.rval, d.qcol, d.qz, d.spos, d.dstamp, d.rowvs, d.yvs, d.dw, d.dprev, (void*)d.srow,
                     (void*)d.scol, d.rhoR, d.rr, d.dchz, d.dcand, d.dcnt, d.dcomp, d.dalive, d.dflip,
                     d.dflipdx, d.aF, d.fS, d.ddw != d.dw ? (void*)d.ddw : nullptr, d.dsend, d.drecv};
     for (void* p : ptrs)
@@ -702,6 +702,7 @@ static int alloc_all_body(elp_handle* h) {
     A(dalloc(&d.pstamp, 2 * ((size_t)d.ntiles + (size_t)(mm / 128 + 1) + 3072 + 64)));
 #endif
     if (h->csc) A(dalloc(&d.qcol, mm));
+    if (h->csc && !h->lu) A(dalloc(&d.spos, (size_t)(n > 0 ? n : 1)));  // (the sparse FTRAN-z's column -> position)
     else if (!std::getenv("ELP_NO_QZ")) A(dalloc(&d.qz, mm));  // (ELP_NO_QZ: A/B switch)
     if (ELP_DIAG && std::getenv("ELP_STAMPS")) {  // (diagnostic builds)
         A(dalloc(&d.dstamp, DSTAMP_STRIDE * 64));

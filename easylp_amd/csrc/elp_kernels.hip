@@ -336,6 +336,7 @@ __global__ void k_init_cols(Dev d, const double* __restrict__ lo, const double* 
     // (the host mapped |v| >= elp_control.infinity to +-inf BEFORE scaling; a
     //  finite bound that crosses 1e30 once scaled stays finite, as in the oracle)
     const double l = lo ? lo[j] : 0.0, u = up ? up[j] : HUGE_VAL;
+    if (d.spos) d.spos[j] = -1;  // (CSC: no basic structural at a fresh start)
     d.lb[j] = l;
     d.ub[j] = u;
     d.cost[j] = 0.0;
@@ -813,17 +814,20 @@ DEV void btran_body(const Dev& d, int phase, const double* __restrict__ tv) {
 
 // deferred update (phase 2): defined with k_update below
 struct Plan;
-DEV void apply_plan(const Dev& d, const Plan& P, int blk, int nb, int nb_minv, bool do_ar);
-DEV void apply_minv(const Dev& d, const Plan& P, int64_t e0, int64_t estride);
+DEV void apply_plan(const Dev& d, const Plan& P, int blk, int nb, int nb_minv, bool do_ar, bool batch = true);
+DEV void apply_minv(const Dev& d, const Plan& P, int64_t e0, int64_t estride, bool batch = true);
 DEV void apply_copy(const Dev& d, const Plan& P, int64_t t0, int64_t tstride, bool do_ar);
 DEV bool plan_pending(const DevCtl* c) { return c->plan_seq != c->applied_seq && c->plan.action != ACT_NONE; }
 // the pricing launch's trailing `napply` workgroups apply the pending plan
-DEV bool apply_role(const Dev& d, int napply, int nb_minv) {
+// batch: the inverse update's loads grouped ahead of its stores (apply_minv);
+// the dense pricing launch's trailing workgroups keep one element at a time
+// (batched, its launch measured 0.6-1.5 us longer at 5000 x 50000, r04k A/B)
+DEV bool apply_role(const Dev& d, int napply, int nb_minv, bool batch = true) {
     if ((int)blockIdx.x < (int)gridDim.x - napply) return false;
     const DevCtl* c = d.ctl;
     if (plan_pending(c) && c->status != ST_NUMFAIL) {
         const Plan P = c->plan;
-        apply_plan(d, P, blockIdx.x - (gridDim.x - napply), napply, nb_minv, false);
+        apply_plan(d, P, blockIdx.x - (gridDim.x - napply), napply, nb_minv, false, batch);
     }
     return true;
 }
@@ -987,7 +991,7 @@ DEV void price_body(const Dev& d, int nsw, int apply, int napply, int nb_minv) {
     __shared__ double part[PRICE_SPLIT][TILE_COLS];
     __shared__ Cand red[PRICE_SPLIT];
     const int64_t ntiles = d.ntiles;
-    if (napply > 0 && apply_role(d, napply, nb_minv)) return;
+    if (napply > 0 && apply_role(d, napply, nb_minv, false)) return;
     const int sw = ELP_SLACK_LAST ? (int)blockIdx.x - (int)ntiles : (int)blockIdx.x;  // slack workgroup index
     if (sw >= 0 && sw < nsw) {
         PDBG(1, 2ull);
@@ -1895,6 +1899,160 @@ DEV void emit_wave(const Dev& d, int region, int var, int e, double g, double x,
     if (lane == 0) d.rcnt[region] = __popcll(mask);
 }
 
+// the scalars k_ratio's bookkeeping needs, taken before anything of this
+// iteration rewrites them (FTRAN-z's last workgroup; see DevCtl)
+DEV void zr_snapshot(const Dev& d, int k, int q) {
+    DevCtl* cw = d.ctl;
+    const int ny = cw->ny, i0 = q - d.N;
+    const int yl = ny > 0 ? d.Yl[ny - 1] : -1;
+    cw->snap_ny = ny;
+    cw->snap_apos = i0 >= 0 ? d.rpos[i0] : -1;
+    cw->snap_ypos0 = i0 >= 0 ? d.ypos[i0] : -1;
+    cw->snap_ylast = yl;  // (rpos[yl]: k_ratio loads it itself, one round trip fewer here)
+    const int ql = loc_of(d, q);
+    const bool pk = ql < 0 || (d.sharded && q < d.N);  // from the exchanged packet
+    const int m = d.m, last = k - 1;
+    cw->snap_lbq = pk ? d.pkt[m] : d.lb[ql];
+    cw->snap_ubq = pk ? d.pkt[m + 1] : d.ub[ql];
+    cw->snap_xq = pk ? d.pkt[m + 2] : d.xval[ql];
+    cw->snap_cq = pk ? d.pkt[m + 3] : d.cost[ql];
+    cw->snap_vsq = ql >= 0 ? d.vstat[ql] : VS_LOWER;
+    cw->snap_csl = last >= 0 ? d.cS[last] : 0.0;
+    cw->snap_slol = last >= 0 ? d.slo[last] : 0.0;
+    cw->snap_shil = last >= 0 ? d.shi[last] : 0.0;
+    cw->snap_sllast = last >= 0 ? d.Sl[last] : -1;
+    cw->snap_rllast = last >= 0 ? d.Rl[last] : -1;
+}
+
+// CSC input (one GPU): z_i = A[i, S] x_S on a covered row from the row's
+// nonzeros in basic columns (CSR + Dev::spos) -- in bump-position order with
+// the oracle's zchunk grouping (an fma chain per 32-position chunk, the chunk
+// sums added in order): the zero entries the dense AS walk adds change no bit,
+// so this is the dense result at O(nnz of the row) instead of O(k).  A row
+// with more than SPZ_MAX basic entries walks AS densely instead.
+constexpr int SPZ_MAX = 16;
+DEV double csr_zrow(const Dev& d, int i, int k, const double* __restrict__ xs) {
+    int pp[SPZ_MAX];
+    double vv[SPZ_MAX];
+    int cnt = 0;
+    bool over = false;
+    const int64_t t1 = d.rptr[i + 1];
+    for (int64_t t0 = d.rptr[i]; t0 < t1 && !over; t0 += 8) {  // 8 entries' loads in flight
+        int jj[8], ps[8];
+        double vr[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t tt = t0 + u < t1 ? t0 + u : t1 - 1;
+            jj[u] = d.cind[tt];
+            vr[u] = d.rval[tt];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) ps[u] = d.spos[jj[u]];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (t0 + u >= t1 || ps[u] < 0) continue;
+            if (cnt == SPZ_MAX) {
+                over = true;
+                break;
+            }
+            pp[cnt] = ps[u];
+            vv[cnt] = vr[u];
+            ++cnt;
+        }
+    }
+    double z = 0.0;
+    if (over) {
+        const size_t m = (size_t)d.m;
+        for (int c0 = 0; c0 < k; c0 += ZCHUNK) {
+            double acc = 0.0;
+            const int c1 = min(k, c0 + ZCHUNK);
+            for (int p = c0; p < c1; ++p) acc = fma(d.AS[(size_t)p * m + i], xs[p], acc);
+            z = z + acc;
+        }
+        return z;
+    }
+    for (int a = 1; a < cnt; ++a) {  // insertion sort by position (a handful of entries)
+        const int p = pp[a];
+        const double v = vv[a];
+        int b = a - 1;
+        while (b >= 0 && pp[b] > p) {
+            pp[b + 1] = pp[b];
+            vv[b + 1] = vv[b];
+            --b;
+        }
+        pp[b + 1] = p;
+        vv[b + 1] = v;
+    }
+    double acc = 0.0;
+    int ch = -1;
+    for (int e = 0; e < cnt; ++e) {
+        const int pc = pp[e] / ZCHUNK;
+        if (pc != ch) {
+            if (ch >= 0) z = z + acc;
+            acc = 0.0;
+            ch = pc;
+        }
+        acc = fma(vv[e], xs[pp[e]], acc);
+    }
+    if (ch >= 0) z = z + acc;
+    return z;
+}
+
+// FTRAN-z + Harris pass 1 for CSC input: row tiles of 64 rows (one per lane,
+// csr_zrow), then bump tiles of 64 positions, then the snapshot workgroup --
+// k_ftran_zr's regions and minima with one wave per tile (zw = 1)
+__global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt) {
+    const DevCtl* c = d.ctl;
+    const int32_t st0 = c->status;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) d.ctl->snap_status = st0;  // for k_ratio
+    if (st0 != ST_RUN) return;
+    const int k = c->k, q = c->q, bland = c->bland, m = d.m, lane = threadIdx.x;
+    const double sig = c->sig, ptol = c->tol_primal, pivtol = c->tol_pivot;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        d.ctl->snap_k = k;
+        d.ctl->snap_bland = bland;
+    }
+    if (blockIdx.x == gridDim.x - 1) {
+        if (threadIdx.x == 0) zr_snapshot(d, k, q);
+        return;
+    }
+    double tmin = HUGE_VAL, ge = 0.0, xe = 0.0, le = 0.0, he = 0.0;
+    int ve = -1, e = 0, region;
+    if ((int)blockIdx.x < nrt) {
+        const int i = blockIdx.x * 64 + lane;
+        e = i;
+        region = blockIdx.x;
+        const int u = i < m ? d.cover[i] : -1;
+        if (u >= 0) {
+            const double z = csr_zrow(d, i, k, d.alS);
+            const double aiq = q >= d.N ? (i == q - d.N ? 1.0 : 0.0) : d.qcol[i];
+            const double alU = unit_sign(d, u, i) * (aiq - z);
+            d.alU[i] = alU;
+            ge = sig * alU;
+            xe = d.xr[i];
+            le = d.rlo[i];
+            he = d.rhi[i];
+            ve = u;
+            tmin = harris1(ge, xe, le, he, ptol, pivtol, bland);
+        }
+    } else {
+        const int p = (blockIdx.x - nrt) * 64 + lane;
+        e = m + p;
+        region = blockIdx.x;  // (= nrt + bump tile: one wave per tile)
+        if (p < k) {
+            ge = sig * d.alS[p];
+            xe = d.xs[p];
+            le = d.slo[p];
+            he = d.shi[p];
+            ve = d.Sl[p];
+            tmin = harris1(ge, xe, le, he, ptol, pivtol, bland);
+        }
+    }
+    const double bmin = wave_min_f64(tmin);
+    if (lane == 0) d.blockmin[blockIdx.x] = bmin;
+    emit_wave(d, region, ve, e, ge, xe, le, he, bmin, pivtol);
+}
+
 // waves per row tile of k_ftran_zr (ZR_WAVES): 8, or 4 when the row tiles
 // outnumber the CUs and every chunk still gets its own half-wave (the kernel
 // holds one 8-wave workgroup per CU -- 175 VGPRs -- so 4-wave tiles run two
@@ -2005,28 +2163,7 @@ __global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(DEV_PARAM, int nrt, 
         d.ctl->snap_bland = bland;
     }
     if (blockIdx.x == gridDim.x - 1) {  // the snapshot workgroup (see DevCtl)
-        if (threadIdx.x == 0) {
-            DevCtl* cw = d.ctl;
-            const int ny = cw->ny, i0 = q - d.N;
-            const int yl = ny > 0 ? d.Yl[ny - 1] : -1;
-            cw->snap_ny = ny;
-            cw->snap_apos = i0 >= 0 ? d.rpos[i0] : -1;
-            cw->snap_ypos0 = i0 >= 0 ? d.ypos[i0] : -1;
-            cw->snap_ylast = yl;  // (rpos[yl]: k_ratio loads it itself, one round trip fewer here)
-            const int ql = loc_of(d, q);
-            const bool pk = ql < 0 || (d.sharded && q < d.N);  // from the exchanged packet
-            const int m = d.m, last = k - 1;
-            cw->snap_lbq = pk ? d.pkt[m] : d.lb[ql];
-            cw->snap_ubq = pk ? d.pkt[m + 1] : d.ub[ql];
-            cw->snap_xq = pk ? d.pkt[m + 2] : d.xval[ql];
-            cw->snap_cq = pk ? d.pkt[m + 3] : d.cost[ql];
-            cw->snap_vsq = ql >= 0 ? d.vstat[ql] : VS_LOWER;
-            cw->snap_csl = last >= 0 ? d.cS[last] : 0.0;
-            cw->snap_slol = last >= 0 ? d.slo[last] : 0.0;
-            cw->snap_shil = last >= 0 ? d.shi[last] : 0.0;
-            cw->snap_sllast = last >= 0 ? d.Sl[last] : -1;
-            cw->snap_rllast = last >= 0 ? d.Rl[last] : -1;
-        }
+        if (threadIdx.x == 0) zr_snapshot(d, k, q);
         return;
     }
     const int nch = (k + ZCHUNK - 1) / ZCHUNK;
@@ -2714,6 +2851,7 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
                 P.p = lpos;
                 P.piv = best.g * sig;  // alS[lpos]
                 if (wv == 1) { d.Sl[lpos] = q; }
+                if (wv == 1) { if (d.spos) { d.spos[lv] = -1; d.spos[q] = lpos; } }
                 if (wv == 1) { d.cS[lpos] = cq; }
                 if (wv == 1) { d.slo[lpos] = lbq; }
                 if (wv == 1) { d.shi[lpos] = ubq; }
@@ -2727,6 +2865,7 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
                 if (wv == 1) { d.Rl[k] = i; }
                 if (wv == 1) { d.rpos[i] = k; }
                 if (wv == 1) { d.Sl[k] = q; }
+                if (wv == 1) { if (d.spos) d.spos[q] = k; }
                 if (wv == 1) { d.cS[k] = cq; }
                 if (wv == 1) { d.slo[k] = lbq; }
                 if (wv == 1) { d.shi[k] = ubq; }
@@ -2754,7 +2893,9 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
                 P.b = b;
                 P.last = last;
                 P.piv = t0_piv;  // Minv[b][a]
+                if (wv == 1) { if (d.spos) d.spos[lv] = -1; }
                 if (b != last) {
+                    if (wv == 1) { if (d.spos) d.spos[sv_sllast] = b; }
                     if (wv == 1) { d.Sl[b] = sv_sllast; }
                     if (wv == 1) { d.cS[b] = sv_csl; }
                     if (wv == 1) { d.slo[b] = sv_slol; }
@@ -2848,13 +2989,17 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
     RSTAMP(6);
 }
 
-// new value of bump-inverse element (i, j); old(r, c) reads the pre-update matrix
+// the pre-update bump inverse: old(r, c) (tr: read from the transpose)
 struct OldM {
     const double* M;
     size_t ld;
     bool tr;
     DEV double operator()(int r, int c) const { return tr ? M[(size_t)c * ld + r] : M[(size_t)r * ld + c]; }
 };
+// The plan k_ratio made: Minv and MinvT update (blocks [0, nb_minv)) + primal
+// update x_B -= step*alpha and AS copies (blocks [nb_minv, nb)); with do_ar also
+// the AR row copies (phase 1, where nothing is deferred).  Flips only update x_B.
+// new value of bump-inverse element (i, j) (the sequential path below)
 DEV double minv_new(const Dev& d, const Plan& P, int i, int j, const OldM& old) {
     const int k = P.k_old;
     switch (P.pcase) {
@@ -2876,22 +3021,12 @@ DEV double minv_new(const Dev& d, const Plan& P, int i, int j, const OldM& old) 
         }
     }
 }
-
-// The plan k_ratio made: Minv and MinvT update (blocks [0, nb_minv)) + primal
-// update x_B -= step*alpha and AS copies (blocks [nb_minv, nb)); with do_ar also
-// the AR row copies (phase 1, where nothing is deferred).  Flips only update x_B.
-// the Minv / MinvT part of a plan: element e0, e0 + estride, ... of the 2 kk^2
-DEV void apply_minv(const Dev& d, const Plan& P, int64_t e0, int64_t estride) {
-    if (P.action != ACT_PIVOT || P.pcase == PC_E) return;
-    const int k = P.k_old;
+// one element at a time (the dense pricing launch's trailing workgroups, where
+// the grouped form below measured slower, r04k / r04m)
+DEV void apply_minv_seq(const Dev& d, const Plan& P, int64_t e0, int64_t estride, int kk) {
     const size_t ldm = (size_t)d.ldm;
-    const int kk = P.pcase == PC_B ? k + 1 : P.pcase == PC_C ? k - 1 : k;
     const int64_t nel = (int64_t)kk * kk;
     const OldM oM{d.Minv, ldm, false}, oT{d.MinvT, ldm, true};
-    // element e -> (row, column) by one division per half, then carried along
-    // the stride (a 64-bit integer division is a long instruction sequence on
-    // the GPU; same elements, same values)
-    if (nel == 0) return;
     const int64_t sq = estride / kk, sr = estride % kk;
     int64_t e = e0;
     if (e < nel) {
@@ -2919,6 +3054,104 @@ DEV void apply_minv(const Dev& d, const Plan& P, int64_t e0, int64_t estride) {
             }
         }
     }
+}
+
+// the Minv / MinvT part of a plan: element e0, e0 + estride, ... of the 2 kk^2.
+// A thread takes its elements MINV_U at a time: every load of the group (the
+// old element, the two update operands) goes out before the group's stores --
+// the stores alias the old matrix for the compiler, so a plain loop paid one
+// memory round trip per element.  Element e -> (row, column) by one division per
+// half, then carried along the stride.  Per element (pivot cases A-D, oracle
+// update_inverse): A: new = (i == p) ? vrow_j : old - alS_i vrow_j; B (bordered):
+// old + alS_i vvec_j inside, -alS_i / piv, -vvec_j, 1 / piv on the border; C:
+// old(sr, sc) - colA_sr vrow_sc with the last row / column moved; D: colA_i / vvec_a
+// on column a, old - (colA_i / vvec_a) vvec_j elsewhere.
+constexpr int MINV_U = 4;  // elements per group
+template <bool TR, int U>  // TR false: Minv (row i, column j); true: MinvT, element (j, i)
+DEV void apply_minv_half(const Dev& d, const Plan& P, int64_t e, int64_t end, int64_t estride, int64_t base,
+                         int kk) {
+    const int k = P.k_old, pc = P.pcase;
+    const size_t ldm = (size_t)d.ldm;
+    double* M = TR ? d.MinvT : d.Minv;
+    const OldM old{M, ldm, TR};
+    const int64_t sq = estride / kk, sr = estride % kk;
+    const int64_t f = e - base;
+    int64_t a = f / kk, b = f % kk;  // position in the half's row-major order
+    const double va = pc == PC_D ? d.vvec[P.a] : 1.0;
+    const int kl = k > 0 ? k - 1 : 0;
+    while (e < end) {
+        int ii[U], jj[U];
+        bool ok[U];
+        double ov[U], x1[U], x2[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            ok[u] = e + (int64_t)u * estride < end;
+            ii[u] = (int)(TR ? b : a);
+            jj[u] = (int)(TR ? a : b);
+            a += sq;
+            b += sr;
+            if (b >= kk) {
+                b -= kk;
+                ++a;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {  // the loads (indices clamped; masked by ok at the store)
+            const int i = ok[u] ? ii[u] : 0, j = ok[u] ? jj[u] : 0;
+            int r = i, c = j;
+            int i1 = i, j2 = j;
+            if (pc == PC_C) {
+                r = (i == P.b) ? P.last : i;
+                c = (j == P.a) ? P.last : j;
+                i1 = r;
+                j2 = c;
+            } else if (pc == PC_B) {
+                r = i < k ? i : 0;
+                c = j < k ? j : 0;
+                i1 = i < k ? i : kl;
+                j2 = j < k ? j : kl;
+            }
+            ov[u] = old(r, c);
+            x1[u] = pc == PC_C || pc == PC_D ? d.colA[i1] : d.alS[i1];
+            x2[u] = pc == PC_B || pc == PC_D ? d.vvec[j2] : d.vrow[j2];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!ok[u]) continue;
+            const int i = ii[u], j = jj[u];
+            double v;
+            if (pc == PC_A) {
+                v = (i == P.p) ? x2[u] : fma(-x1[u], x2[u], ov[u]);
+            } else if (pc == PC_B) {
+                if (i < k && j < k) v = fma(x1[u], x2[u], ov[u]);
+                else if (i < k) v = -(x1[u] / P.piv);
+                else if (j < k) v = -x2[u];
+                else v = 1.0 / P.piv;
+            } else if (pc == PC_C) {
+                v = fma(-x1[u], x2[u], ov[u]);
+            } else {  // PC_D
+                const double ca = x1[u] / va;
+                v = (j == P.a) ? ca : fma(-ca, x2[u], ov[u]);
+            }
+            if (TR) M[(size_t)j * ldm + (size_t)i] = v;
+            else M[(size_t)i * ldm + (size_t)j] = v;
+        }
+        e += (int64_t)U * estride;
+    }
+}
+DEV void apply_minv(const Dev& d, const Plan& P, int64_t e0, int64_t estride, bool batch) {
+    if (P.action != ACT_PIVOT || P.pcase == PC_E) return;
+    const int k = P.k_old;
+    const int kk = P.pcase == PC_B ? k + 1 : P.pcase == PC_C ? k - 1 : k;
+    const int64_t nel = (int64_t)kk * kk;
+    if (nel == 0) return;
+    if (!batch) return apply_minv_seq(d, P, e0, estride, kk);
+    if (e0 < nel) {
+        apply_minv_half<false, MINV_U>(d, P, e0, nel, estride, 0, kk);
+        // this thread's first MinvT element: the first e0 + t estride >= nel
+        e0 += (nel - e0 + estride - 1) / estride * estride;
+    }
+    if (e0 < 2 * nel) apply_minv_half<true, MINV_U>(d, P, e0, 2 * nel, estride, nel, kk);
 }
 
 // the primal update and the AS (/ AR) copies of a plan: thread t0 of tstride
@@ -2993,9 +3226,9 @@ DEV void apply_copy(const Dev& d, const Plan& P, int64_t t0, int64_t tstride, bo
     }
 }
 
-DEV void apply_plan(const Dev& d, const Plan& P, int blk, int nb, int nb_minv, bool do_ar) {
+DEV void apply_plan(const Dev& d, const Plan& P, int blk, int nb, int nb_minv, bool do_ar, bool batch) {
     if (blk < nb_minv) {
-        apply_minv(d, P, (int64_t)blk * blockDim.x + threadIdx.x, (int64_t)nb_minv * blockDim.x);
+        apply_minv(d, P, (int64_t)blk * blockDim.x + threadIdx.x, (int64_t)nb_minv * blockDim.x, batch);
         return;
     }
     apply_copy(d, P, (int64_t)(blk - nb_minv) * blockDim.x + threadIdx.x, (int64_t)(nb - nb_minv) * blockDim.x,
@@ -4171,6 +4404,23 @@ __global__ void __launch_bounds__(256) k_dual_flip_col(Dev d) {
     d.aF[i] = acc;
 }
 
+// CSC: the same update with A[i, S] fS from the row's nonzeros (csr_zrow), one
+// thread per row, then the bump positions
+__global__ void __launch_bounds__(256) k_dual_flip_apply_sp(Dev d) {
+    const DevCtl* c = d.ctl;
+    if (c->status != ST_RUN || c->nflip == 0) return;
+    const int m = d.m, k = c->k;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t < m) {
+        const int u = d.cover[t];
+        if (u < 0) return;
+        const double tot = csr_zrow(d, t, k, d.fS);
+        d.xr[t] = d.xr[t] - unit_sign(d, u, t) * (d.aF[t] - tot);
+    } else if (t - m < k) {
+        d.xs[t - m] = d.xs[t - m] - d.fS[t - m];
+    }
+}
+
 // column-only shards (no replicated A): the owner of a structural entering
 // column packs it (scaled) into pkt[0, m), every other rank zeros -- the host
 // all-reduces pkt[0, m), an exact copy; k_dual_bfrt wrote pkt[m, m + 4) on all
@@ -4390,6 +4640,18 @@ static void update_grid(const Dev& d, int k_ub, bool with_ar, unsigned* nb_minv,
     *nb = *nb_minv + nb_copy;
 }
 
+// CSC: A[i, S] v from the rows' nonzeros (csr_zrow) once the dense walk over AS
+// would stream more than ELP_SPZ_MIN_MB (16) MB -- below that the dense walk's
+// independent loads beat the row walk's dependent ones (1000 x 10 000 packing
+// LP, k <= 877: 0.53 s dense against 0.85 s sparse, r04m)
+static bool use_spz(const Dev& d, int k_ub) {
+    static const double thr = [] {
+        const char* e = std::getenv("ELP_SPZ_MIN_MB");
+        return e ? std::atof(e) * 1e6 : 16e6;
+    }();
+    return d.csc && d.spos && 8.0 * (double)d.m * (double)k_ub > thr;
+}
+
 // slack workgroups of the pricing launch for |Y| <= ny_ub
 static int slack_wgs(const Dev& d, int ny_ub) {
     return (int)cdiv(ny_ub > 0 ? ny_ub : 1, d.csc ? TILE_COLS : PRICE_THREADS);
@@ -4476,7 +4738,10 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
                                  int dslot, int qz) {
     const int m = d.m;
     if (bump_ftran && k_ub > 0) k_ftran_bump<<<cdiv(k_ub, 4), 256, 0, st>>>(d, d.aR, d.alS, 1);
-    const int nrt = (int)cdiv(m > 0 ? m : 1, ZR_ROWS);
+    // CSC with a large bump: FTRAN-z from the rows of A (k_ftran_zr_sp: 64-row
+    // tiles, 64-position bump tiles); else k_ftran_zr's 32-row tiles over AS
+    const bool spz = use_spz(d, k_ub);
+    const int nrt = spz ? (int)cdiv(m > 0 ? m : 1, 64) : (int)cdiv(m > 0 ? m : 1, ZR_ROWS);
     // z partials: 256 B per chunk of ZCHUNK bump positions in LDS (<= 64 KiB,
     // k <= 8192); larger bumps use a private slice of zpart per row tile
     const size_t lds = (size_t)cdiv(k_ub, ZCHUNK) * ZR_ROWS * sizeof(double);
@@ -4484,6 +4749,7 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     static const int zw_env = getenv("ELP_ZW") ? atoi(getenv("ELP_ZW")) : 0;  // A/B override
     int zw = (ldsz && nrt > 256 && cdiv(k_ub, ZCHUNK) <= 8) ? 4 : 8;  // waves per row tile
     if (ldsz && (zw_env == 4 || zw_env == 8)) zw = zw_env;
+    if (spz) zw = 1;
     const int nbt = (int)cdiv(k_ub, 64 * zw);
     // alpha_S in LDS beside the z partials when the half-waves run more than one
     // chunk each (k_ub > 2 zw ZCHUNK) and it fits the prefetch (ZR_PA per thread):
@@ -4493,7 +4759,9 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     const int nxp = (int)std::min<int64_t>(std::max<int64_t>((int64_t)cdiv(k_ub, ZCHUNK) - 2 * zw, 0), ZR_XPF);
     const size_t lds_als = lds + (size_t)k_ub * sizeof(double) + (size_t)nxp * ZCHUNK * ZR_ROWS * sizeof(double);
     const bool als = !no_als && ldsz && k_ub > 2 * zw * ZCHUNK && k_ub <= ZR_PA * 64 * zw && lds_als <= 64 * 1024;
-    {
+    if (spz) {
+        k_ftran_zr_sp<<<nrt + nbt + 1, 64, 0, st>>>(d, nrt);
+    } else {
         // + 1: the snapshot workgroup
         if (als) {
             if (zw == 4) k_ftran_zr<true, 4, true><<<nrt + nbt + 1, 256, lds_als, st>>>(DEV_ARG(d), nrt, k_ub, dslot, qz);
@@ -4649,7 +4917,9 @@ static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_co
     if (nrw > 1024) nrw = 1024;
     if (flip_col) k_dual_flip_col<<<d.csc ? 1u : cdiv(m > 0 ? m : 1, 256), 256, 0, st>>>(d);
     if (k_ub > 0) k_dual_flip_bump<<<nrw, 256, lds_row ? lds : 0, st>>>(d, lds_row);
-    {
+    if (use_spz(d, k_ub)) {
+        k_dual_flip_apply_sp<<<cdiv((int64_t)m + k_ub, 256), 256, 0, st>>>(d);
+    } else {
         const unsigned nrt = cdiv(m > 0 ? m : 1, ZR_ROWS), nbt = cdiv(k_ub > 0 ? k_ub : 1, 512);
         const size_t zl = (size_t)cdiv(k_ub > 0 ? k_ub : 1, ZCHUNK) * ZR_ROWS * sizeof(double);
         if (zl <= 48 * 1024) k_dual_flip_apply<true><<<nrt + nbt, 512, zl, st>>>(d, (int)nrt);
