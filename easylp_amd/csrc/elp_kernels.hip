@@ -1215,7 +1215,13 @@ DEV double price_pass_bytes(const Dev& d, int ny, int devex) {
 // index), then each thread runs its column's fma chain from LDS in ascending
 // row order (oracle price_mode 1).  Tiles with more than CSC_STAGE nonzeros
 // read straight from global memory (same order).
-constexpr int CSC_STAGE = 2048;  // staged nonzeros per tile: 32 KiB of LDS
+// staged nonzeros per tile: 16 KiB of LDS (2048 / 32 KiB until r04: the LDS
+// limited the launch -- its deferred-update workgroups too -- to 2 waves per
+// SIMD; 1024 measured 5 % faster on the sparse LPs, r04q)
+#ifndef ELP_CSC_STAGE
+#define ELP_CSC_STAGE 1024
+#endif
+constexpr int CSC_STAGE = ELP_CSC_STAGE;
 DEV void price_csc_body(const Dev& d, int napply, int nb_minv, int nsw);
 __global__ void __launch_bounds__(TILE_COLS) k_price_csc(Dev d, int napply, int nb_minv, int nsw) {
     pstamp_begin<TILE_COLS>(d);
@@ -1937,19 +1943,20 @@ DEV double csr_zrow(const Dev& d, int i, int k, const double* __restrict__ xs) {
     int cnt = 0;
     bool over = false;
     const int64_t t1 = d.rptr[i + 1];
-    for (int64_t t0 = d.rptr[i]; t0 < t1 && !over; t0 += 8) {  // 8 entries' loads in flight
-        int jj[8], ps[8];
-        double vr[8];
+    constexpr int G = 16;  // entries whose loads are in flight together
+    for (int64_t t0 = d.rptr[i]; t0 < t1 && !over; t0 += G) {
+        int jj[G], ps[G];
+        double vr[G];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < G; ++u) {
             const int64_t tt = t0 + u < t1 ? t0 + u : t1 - 1;
             jj[u] = d.cind[tt];
             vr[u] = d.rval[tt];
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) ps[u] = d.spos[jj[u]];
+        for (int u = 0; u < G; ++u) ps[u] = d.spos[jj[u]];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < G; ++u) {
             if (t0 + u >= t1 || ps[u] < 0) continue;
             if (cnt == SPZ_MAX) {
                 over = true;
@@ -1983,16 +1990,21 @@ DEV double csr_zrow(const Dev& d, int i, int k, const double* __restrict__ xs) {
         pp[b + 1] = p;
         vv[b + 1] = v;
     }
+    double xv[SPZ_MAX];  // the x values, all loads in flight before the chain
+#pragma unroll
+    for (int e = 0; e < SPZ_MAX; ++e) xv[e] = xs[e < cnt ? pp[e] : 0];
     double acc = 0.0;
     int ch = -1;
-    for (int e = 0; e < cnt; ++e) {
+#pragma unroll
+    for (int e = 0; e < SPZ_MAX; ++e) {
+        if (e >= cnt) break;
         const int pc = pp[e] / ZCHUNK;
         if (pc != ch) {
             if (ch >= 0) z = z + acc;
             acc = 0.0;
             ch = pc;
         }
-        acc = fma(vv[e], xs[pp[e]], acc);
+        acc = fma(vv[e], xv[e], acc);
     }
     if (ch >= 0) z = z + acc;
     return z;
