@@ -3364,51 +3364,78 @@ __global__ void k_refactor_rhs(Dev d) {
 }
 
 // ------------------------------------------------------------ Newton-Schulz
-// E = I - M Minv with M[i][l] = AS[l][Rl[i]] (= A[R_i, S_l]); 32x32 output
-// tiles, every output an fma chain over l in order (oracle newton_schulz).
-__global__ void __launch_bounds__(1024) k_ns_resid(Dev d, int k) {
-    __shared__ double Mt[32][33];
-    __shared__ double Bt[32][33];
-    __shared__ double red[16];
-    const int tx = threadIdx.x, ty = threadIdx.y;
-    const int i = blockIdx.y * 32 + ty, j = blockIdx.x * 32 + tx;
-    double acc = 0.0;
-    for (int l0 = 0; l0 < k; l0 += 32) {
-        const int li = l0 + tx, lj = l0 + ty;
-        const int ri = blockIdx.y * 32 + ty;
-        Mt[ty][tx] = (ri < k && li < k) ? d.AS[(size_t)li * (size_t)d.m + d.Rl[ri]] : 0.0;
-        Bt[ty][tx] = (lj < k && j < k) ? d.Minv[(size_t)lj * d.ldm + j] : 0.0;
+// Register-blocked fp64 GEMMs (r04): a 64 x 64 output tile per 256-thread
+// workgroup, thread (tx, ty) owning outputs (ty + 16 u, tx + 16 v), u, v < 4;
+// operands staged through LDS 16 values of l at a time.  Every output is still
+// ONE fma chain over l in order (oracle newton_schulz: the same bits); per l the
+// thread reads 4 + 4 values for 16 fmas instead of 2 per fma (r03's 32 x 32
+// tiles, one output per thread: ~3 TFLOP/s, 5 ms at k = 2000).
+constexpr int NS_T = 64, NS_L = 16;
+template <int MODE>  // 0: E = I - M Minv (M[i][l] = AS[l][Rl[i]]) into W0; 1: W1 = Minv + Minv E
+__global__ void __launch_bounds__(256) k_ns_gemm(Dev d, int k) {
+    __shared__ double At[NS_L][NS_T + 1];  // At[l][r]: operand A(i0 + r, l0 + l)
+    __shared__ double Bt[NS_L][NS_T + 1];  // Bt[l][c]: operand B(l0 + l, j0 + c)
+    __shared__ double red[4];
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const int i0 = blockIdx.y * NS_T, j0 = blockIdx.x * NS_T;
+    const size_t ldm = (size_t)d.ldm, m = (size_t)d.m;
+    double acc[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int i = i0 + ty + 16 * u, j = j0 + tx + 16 * v;
+            acc[u][v] = (MODE == 1 && i < k && j < k) ? d.Minv[(size_t)i * ldm + j] : 0.0;
+        }
+    for (int l0 = 0; l0 < k; l0 += NS_L) {
+#pragma unroll
+        for (int t = 0; t < NS_T * NS_L / 256; ++t) {
+            const int e = tid + 256 * t;
+            const int r = e / NS_L, c = e % NS_L;  // A: row r, l c
+            const int i = i0 + r, l = l0 + c;
+            double a = 0.0;
+            if (i < k && l < k) a = MODE == 0 ? d.AS[(size_t)l * m + d.Rl[i]] : d.Minv[(size_t)i * ldm + l];
+            At[c][r] = a;
+            const int rb = e / NS_T, cb = e % NS_T;  // B: l rb, column cb
+            const int lb = l0 + rb, j = j0 + cb;
+            double b = 0.0;
+            if (lb < k && j < k) b = MODE == 0 ? d.Minv[(size_t)lb * ldm + j] : d.W0[(size_t)lb * k + j];
+            Bt[rb][cb] = b;
+        }
         __syncthreads();
-        const int lend = min(32, k - l0);
-        for (int ll = 0; ll < lend; ++ll) acc = fma(Mt[ty][ll], Bt[ll][tx], acc);
+        const int lend = min(NS_L, k - l0);
+        for (int ll = 0; ll < lend; ++ll) {
+            double a[4], b[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) a[u] = At[ll][ty + 16 * u];
+#pragma unroll
+            for (int v = 0; v < 4; ++v) b[v] = Bt[ll][tx + 16 * v];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) acc[u][v] = fma(a[u], b[v], acc[u][v]);
+        }
         __syncthreads();
     }
-    double e = 0.0;
-    if (i < k && j < k) {
-        e = (i == j ? 1.0 : 0.0) - acc;
-        d.W0[(size_t)i * k + j] = e;
+    double emax = 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int i = i0 + ty + 16 * u, j = j0 + tx + 16 * v;
+            if (i >= k || j >= k) continue;
+            if (MODE == 0) {
+                const double e = (i == j ? 1.0 : 0.0) - acc[u][v];
+                d.W0[(size_t)i * k + j] = e;
+                emax = fmax(emax, fabs(e));
+            } else {
+                d.W1[(size_t)i * k + j] = acc[u][v];
+            }
+        }
+    if (MODE == 0) {
+        const double am = block_max<256>(emax, red);
+        if (tid == 0) atomicMax(&d.ctl->ns_emax_bits, (unsigned long long)__double_as_longlong(am));
     }
-    const double am = block_max<1024>(fabs(e), red, ty * 32 + tx);
-    if (tx == 0 && ty == 0) atomicMax(&d.ctl->ns_emax_bits, (unsigned long long)__double_as_longlong(am));
-}
-
-// W1 = Minv + Minv E  (chain over l starting from Minv[i][j])
-__global__ void __launch_bounds__(1024) k_ns_update(Dev d, int k) {
-    __shared__ double At[32][33];
-    __shared__ double Et[32][33];
-    const int tx = threadIdx.x, ty = threadIdx.y;
-    const int i = blockIdx.y * 32 + ty, j = blockIdx.x * 32 + tx;
-    double acc = (i < k && j < k) ? d.Minv[(size_t)i * d.ldm + j] : 0.0;
-    for (int l0 = 0; l0 < k; l0 += 32) {
-        const int li = l0 + tx, lj = l0 + ty;
-        At[ty][tx] = (i < k && li < k) ? d.Minv[(size_t)i * d.ldm + li] : 0.0;
-        Et[ty][tx] = (lj < k && j < k) ? d.W0[(size_t)lj * k + j] : 0.0;
-        __syncthreads();
-        const int lend = min(32, k - l0);
-        for (int ll = 0; ll < lend; ++ll) acc = fma(At[ty][ll], Et[ll][tx], acc);
-        __syncthreads();
-    }
-    if (i < k && j < k) d.W1[(size_t)i * k + j] = acc;
 }
 
 // Minv = W1, MinvT = W1^T (transposed through LDS, both stores coalesced)
@@ -4991,15 +5018,15 @@ hipError_t launch_select_finish(const Dev& d, hipStream_t st) {
 
 hipError_t launch_refactor_ns_resid(const Dev& d, int k, hipStream_t st) {
     if (k <= 0) return hipSuccess;
-    dim3 g(cdiv(k, 32), cdiv(k, 32));
-    k_ns_resid<<<g, dim3(32, 32), 0, st>>>(d, k);
+    dim3 g(cdiv(k, NS_T), cdiv(k, NS_T));
+    k_ns_gemm<0><<<g, 256, 0, st>>>(d, k);
     return hipGetLastError();
 }
 
 hipError_t launch_refactor_ns_update(const Dev& d, int k, hipStream_t st) {
     if (k <= 0) return hipSuccess;
+    k_ns_gemm<1><<<dim3(cdiv(k, NS_T), cdiv(k, NS_T)), 256, 0, st>>>(d, k);
     dim3 g(cdiv(k, 32), cdiv(k, 32));
-    k_ns_update<<<g, dim3(32, 32), 0, st>>>(d, k);
     k_ns_store<<<g, dim3(32, 32), 0, st>>>(d, k);
     return hipGetLastError();
 }
