@@ -4672,7 +4672,10 @@ static void update_grid(const Dev& d, int k_ub, bool with_ar, unsigned* nb_minv,
                         int threads = 256, int per_thread = 1) {
     const int64_t kk = 2 * (int64_t)(k_ub + 1) * (k_ub + 1);
     *nb_minv = cdiv(kk, threads * per_thread);
-    if (*nb_minv > 2048) *nb_minv = 2048;
+#ifndef ELP_MINV_WG_MAX
+#define ELP_MINV_WG_MAX 2048
+#endif
+    if (*nb_minv > ELP_MINV_WG_MAX) *nb_minv = ELP_MINV_WG_MAX;  // (only large bumps reach it)
     const int64_t cw = with_ar ? (d.m > d.n ? d.m : d.n) : (d.m > k_ub + 1 ? d.m : k_ub + 1);
     unsigned nb_copy = cdiv(cw, threads);
     if (nb_copy > 1024) nb_copy = 1024;
