@@ -2885,6 +2885,79 @@ static void sens_assemble(const elp_handle* h, const std::vector<SensPart>& part
     }
 }
 
+// One process per GPU (elp_comm_init*): every rank ranged its own columns
+// (parts[0]); the ranks' column parts and bump intervals travel in one
+// all-gather of fixed-size records -- [col0, ncols, k][o4: 4k][dr, cost, lb, ub,
+// status: cap each], cap = ceil(N / P) -- so every rank assembles the full
+// report (the replicated rows, y and lists are its own), as an ngpu handle does
+// in one process.  A collective: every rank calls elp_sensitivity.
+static int sens_gather(elp_handle* h, std::vector<SensPart>& parts) {
+    const int P = h->comm.world;
+    const int64_t cap = (h->n + P - 1) / P;
+    const int k = parts[0].k;
+    const size_t R = 3 + 4 * (size_t)k + 5 * (size_t)cap;
+    std::vector<double> rec(R, 0.0), all((size_t)P * R);
+    {
+        const SensPart& sp = parts[0];
+        rec[0] = (double)sp.col0;
+        rec[1] = (double)sp.ncols;
+        rec[2] = (double)sp.k;
+        std::copy(sp.o4.begin(), sp.o4.end(), rec.begin() + 3);
+        double* c = rec.data() + 3 + 4 * (size_t)k;
+        for (int64_t j = 0; j < sp.ncols; ++j) {
+            c[j] = sp.dr[(size_t)j];
+            c[cap + j] = sp.cost[(size_t)j];
+            c[2 * cap + j] = sp.lb[(size_t)j];
+            c[3 * cap + j] = sp.ub[(size_t)j];
+            c[4 * cap + j] = (double)sp.vs[(size_t)j];
+        }
+    }
+    double *dsend = nullptr, *drecv = nullptr;
+    auto release = [&]() {
+        if (dsend) (void)hipFree(dsend);
+        if (drecv) (void)hipFree(drecv);
+    };
+    if (dalloc(&dsend, R) != hipSuccess || dalloc(&drecv, (size_t)P * R) != hipSuccess) {
+        release();
+        return fail(ELP_E_NOMEM, "elp_sensitivity: exchange buffers");
+    }
+    hipError_t e = hipMemcpyAsync(dsend, rec.data(), R * sizeof(double), hipMemcpyHostToDevice, h->st);
+    int rc = e == hipSuccess ? h->comm.allgather(dsend, drecv, R * sizeof(double), h->st) : 0;
+    if (e == hipSuccess && !rc)
+        e = hipMemcpyAsync(all.data(), drecv, (size_t)P * R * sizeof(double), hipMemcpyDeviceToHost, h->st);
+    if (e == hipSuccess && !rc) e = hipStreamSynchronize(h->st);
+    release();
+    if (rc) return fail(rc, "elp_sensitivity: the ranks' report all-gather failed");
+    if (e != hipSuccess) return fail(ELP_E_HIP, std::string("elp_sensitivity: ") + hipGetErrorString(e));
+    SensPart mine = std::move(parts[0]);  // (the replicated fields come from this rank)
+    parts.assign((size_t)P, SensPart{});
+    for (int r = 0; r < P; ++r) {
+        const double* x = all.data() + (size_t)r * R;
+        SensPart& sp = parts[(size_t)r];
+        sp.col0 = (int64_t)x[0];
+        sp.ncols = (int64_t)x[1];
+        sp.k = (int)x[2];
+        if (sp.k != k || sp.ncols > cap) return fail(ELP_E_STATE, "elp_sensitivity: the ranks' bases differ");
+        sp.o4.assign(x + 3, x + 3 + 4 * (size_t)k);
+        const double* c = x + 3 + 4 * (size_t)k;
+        sp.dr.assign(c, c + sp.ncols);
+        sp.cost.assign(c + cap, c + cap + sp.ncols);
+        sp.lb.assign(c + 2 * cap, c + 2 * cap + sp.ncols);
+        sp.ub.assign(c + 3 * cap, c + 3 * cap + sp.ncols);
+        sp.vs.resize((size_t)sp.ncols);
+        for (int64_t j = 0; j < sp.ncols; ++j) sp.vs[(size_t)j] = (int8_t)c[4 * cap + j];
+    }
+    // rank 0's slot carries the replicated rows / duals / lists (identical everywhere)
+    SensPart& p0 = parts[0];
+    p0.xr = std::move(mine.xr);
+    p0.y = std::move(mine.y);
+    p0.b = std::move(mine.b);
+    p0.Sl = std::move(mine.Sl);
+    p0.cover = std::move(mine.cover);
+    p0.rpos = std::move(mine.rpos);
+    return 0;
+}
+
 // the state checks of a rank handle (every rank of a group holds the same)
 static int sens_check(elp_handle* h) {
     if (!h || !h->loaded) return fail(ELP_E_STATE, "elp_sensitivity: no problem loaded");
@@ -2914,11 +2987,13 @@ extern "C" int elp_sensitivity(elp_handle* h, double* objfrom, double* objtill, 
     }
     const int rc0 = sens_check(h);
     if (rc0) return rc0;
-    if (h->comm.kind != 0)
-        return fail(ELP_E_UNSUPPORTED, "elp_sensitivity: multi-process column-sharded solves (use elp_control.ngpu)");
     std::vector<SensPart> parts(1);
     const int rc = sens_part(h, parts[0]);
     if (rc) return rc;
+    if (h->comm.kind != 0) {
+        const int rg = sens_gather(h, parts);
+        if (rg) return rg;
+    }
     sens_assemble(h, parts, objfrom, objtill, duals, dualsfrom, dualstill);
     return 0;
 }

@@ -1943,7 +1943,10 @@ DEV double csr_zrow(const Dev& d, int i, int k, const double* __restrict__ xs) {
     int cnt = 0;
     bool over = false;
     const int64_t t1 = d.rptr[i + 1];
-    constexpr int G = 16;  // entries whose loads are in flight together
+#ifndef ELP_SPZ_G
+#define ELP_SPZ_G 16
+#endif
+    constexpr int G = ELP_SPZ_G;  // entries whose loads are in flight together
     for (int64_t t0 = d.rptr[i]; t0 < t1 && !over; t0 += G) {
         int jj[G], ps[G];
         double vr[G];
@@ -4208,6 +4211,16 @@ DEV int block_scan_excl(int v, int* excl, int* lds) {
 // enter (Bland: the smallest ratio).  Each thread owns a contiguous run of the
 // compacted candidates, so ordered compactions are one block scan.
 constexpr int BF_NT = 1024;
+constexpr int BF_BUN = 1024;  // bunch entries staged in LDS for the flip sum (16 KiB)
+constexpr int BF_RR = 4;      // candidates per thread held in registers (N <= 4096)
+// ELP_BFRT_REG=0 (test hook): every candidate set takes the global-memory path
+static int bfrt_reg() {
+    static const int on = [] {
+        const char* e = std::getenv("ELP_BFRT_REG");
+        return e ? (std::atoi(e) != 0) : 1;
+    }();
+    return on;
+}
 // the regions' candidates in region order into dst[0, total): region counts
 // scanned in chunks of BF_NT regions, each thread copying its own regions
 DEV int compact_regions(const Dev& d, int nreg, DualCand* dst, int* scan_lds) {
@@ -4238,7 +4251,8 @@ __global__ void __launch_bounds__(BF_NT) k_dual_pack(Dev d, int nreg) {
 
 // gathered: P = world ranks' packed records in drecv (rank order) instead of
 // this launch's regions
-__global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gathered) {
+__global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gathered, int reg_ok) {
+    __shared__ double s_bun[2 * BF_BUN];
     __shared__ int scan_lds[BF_NT / 64];
     __shared__ double red[BF_NT / 64];
     __shared__ int s_int[4];
@@ -4264,7 +4278,31 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     const int N = total;
     const int run = (N + BF_NT - 1) / BF_NT;  // this thread's candidates [lo, hi)
     const int lo = min(N, tid * run), hi = min(N, lo + run);
-    for (int t = lo; t < hi; ++t) d.dalive[t] = 1;
+    // up to BF_RR candidates per thread (N <= BF_RR * BF_NT) are held in
+    // registers for the bunch rounds (fully unrolled: no scratch); larger
+    // candidate sets walk dcomp / dalive in global memory
+    const bool reg = reg_ok && run <= BF_RR;
+    double rt[BF_RR], rb[BF_RR], ra[BF_RR], rw[BF_RR];
+    int rj[BF_RR];
+    unsigned ral = 0;  // live mask of the register candidates
+    if (reg) {
+#pragma unroll
+        for (int q = 0; q < BF_RR; ++q) {
+            rt[q] = rb[q] = ra[q] = rw[q] = 0.0;
+            rj[q] = 0;
+            if (lo + q < hi) {
+                const DualCand& o = d.dcomp[lo + q];
+                rt[q] = o.t;
+                rb[q] = o.b;
+                ra[q] = fabs(o.a);
+                rw[q] = o.r;
+                rj[q] = o.j;
+                ral |= 1u << q;
+            }
+        }
+    } else {
+        for (int t = lo; t < hi; ++t) d.dalive[t] = 1;
+    }
     double slope = fabs(c->dr_x - c->dr_beta);
     const double INF = HUGE_VAL;
     int nflip = 0, qidx = -1;
@@ -4272,11 +4310,18 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
         // smallest Harris bound among the live candidates
         double bmin = INF;
         int live = 0;
-        for (int t = lo; t < hi; ++t)
-            if (d.dalive[t]) {
-                live = 1;
-                bmin = fmin(bmin, d.dcomp[t].b);
-            }
+        if (reg) {
+#pragma unroll
+            for (int q = 0; q < BF_RR; ++q)
+                if (ral >> q & 1u) bmin = fmin(bmin, rb[q]);
+            live = ral != 0;
+        } else {
+            for (int t = lo; t < hi; ++t)
+                if (d.dalive[t]) {
+                    live = 1;
+                    bmin = fmin(bmin, d.dcomp[t].b);
+                }
+        }
         const double thmax = block_min<BF_NT>(bmin, red);
         if (tid == 0) s_int[0] = 0;
         __syncthreads();
@@ -4285,25 +4330,83 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
         if (!s_int[0]) break;  // nothing left: the dual ray (q = -1)
         // the bunch, in order, into dflip[nflip ...) (a flip list in the making)
         int cnt = 0, allbox = 1;
-        for (int t = lo; t < hi; ++t)
-            if (d.dalive[t] && d.dcomp[t].t <= thmax) {
-                cnt++;
-                if (d.dcomp[t].r == INF) allbox = 0;
-            }
+        unsigned rbun = 0;  // (register path: the bunch's members)
+        if (reg) {
+#pragma unroll
+            for (int q = 0; q < BF_RR; ++q)
+                if ((ral >> q & 1u) && rt[q] <= thmax) {
+                    rbun |= 1u << q;
+                    cnt++;
+                    if (rw[q] == INF) allbox = 0;
+                }
+        } else {
+            for (int t = lo; t < hi; ++t)
+                if (d.dalive[t] && d.dcomp[t].t <= thmax) {
+                    cnt++;
+                    if (d.dcomp[t].r == INF) allbox = 0;
+                }
+        }
         int excl;
         const int nq = block_scan_excl<BF_NT>(cnt, &excl, scan_lds);
         if (tid == 0) s_int[1] = 1;
         __syncthreads();
         if (!allbox) s_int[1] = 0;
-        for (int t = lo, o = nflip + excl; t < hi; ++t)
-            if (d.dalive[t] && d.dcomp[t].t <= thmax) d.dflip[o++] = t;  // (compact index for now)
+        // the bunch's (|alpha|, u - l) in bunch order into LDS for thread 0's sum;
+        // this thread's best member (largest |alpha| (Bland: smallest ratio),
+        // lowest id -- a total order: ids are distinct) for the entering choice
+        double ba = -1.0, bt = INF;
+        int bj = -1, bi = -1;
+        if (reg) {
+            int o = nflip + excl;
+#pragma unroll
+            for (int q = 0; q < BF_RR; ++q)
+                if (rbun >> q & 1u) {
+                    if (o - nflip < BF_BUN) {
+                        s_bun[2 * (o - nflip)] = ra[q];
+                        s_bun[2 * (o - nflip) + 1] = rw[q];
+                    }
+                    d.dflip[o++] = lo + q;  // (compact index for now)
+                    const bool take = bi < 0 || (bland ? (rt[q] < bt || (rt[q] == bt && rj[q] < bj))
+                                                       : (ra[q] > ba || (ra[q] == ba && rj[q] < bj)));
+                    if (take) {
+                        ba = ra[q];
+                        bt = rt[q];
+                        bj = rj[q];
+                        bi = lo + q;
+                    }
+                }
+        } else {
+            for (int t = lo, o = nflip + excl; t < hi; ++t)
+                if (d.dalive[t] && d.dcomp[t].t <= thmax) {
+                    const DualCand& e = d.dcomp[t];
+                    const double ea = fabs(e.a);
+                    if (o - nflip < BF_BUN) {
+                        s_bun[2 * (o - nflip)] = ea;
+                        s_bun[2 * (o - nflip) + 1] = e.r;
+                    }
+                    d.dflip[o++] = t;
+                    const bool take = bi < 0 || (bland ? (e.t < bt || (e.t == bt && e.j < bj))
+                                                       : (ea > ba || (ea == ba && e.j < bj)));
+                    if (take) {
+                        ba = ea;
+                        bt = e.t;
+                        bj = e.j;
+                        bi = t;
+                    }
+                }
+        }
         __syncthreads();
-        if (tid == 0) {  // |alpha| (u - l) summed in ascending id (the bunch's order)
+        if (tid == 0) {  // |alpha| (u - l) summed in ascending id (the bunch's order): from LDS,
+                         // not two dependent global loads per entry (r03: ~1 us each)
             double sum = 0.0;
             if (s_int[1])
                 for (int t = 0; t < nq; ++t) {
-                    const DualCand& o = d.dcomp[d.dflip[nflip + t]];
-                    sum = fma(fabs(o.a), o.r, sum);
+                    if (t < BF_BUN) {
+                        sum = fma(s_bun[2 * t], s_bun[2 * t + 1], sum);
+                    } else {
+                        const DualCand& o = d.dcomp[d.dflip[nflip + t]];
+                        sum = fma(fabs(o.a), o.r, sum);
+                    }
                 }
             s_dbl[0] = sum;
         }
@@ -4312,44 +4415,43 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
         if (nq == 0) break;  // (NaN ratios only: no candidate qualifies -- the ray)
         if (s_int[1] && sum < slope - c->tol_primal) {  // flip the bunch (x_r still out past it)
             slope = slope - sum;
-            for (int t = nflip + tid; t < nflip + nq; t += BF_NT) d.dalive[d.dflip[t]] = 0;
+            if (reg) {
+                ral &= ~rbun;
+            } else {
+                for (int t = nflip + tid; t < nflip + nq; t += BF_NT) d.dalive[d.dflip[t]] = 0;
+            }
             nflip += nq;
             __syncthreads();
             continue;
         }
-        // the bunch's best enters: largest |alpha| (Bland: smallest ratio), lowest id
-        int best = -1;
-        for (int t = nflip + tid; t < nflip + nq; t += BF_NT) {
-            const int ci = d.dflip[t];
-            if (best < 0) {
-                best = ci;
-                continue;
-            }
-            const DualCand& o = d.dcomp[ci];
-            const DualCand& b = d.dcomp[best];
-            const bool take = bland ? (o.t < b.t || (o.t == b.t && o.j < b.j))
-                                    : (fabs(o.a) > fabs(b.a) || (fabs(o.a) == fabs(b.a) && o.j < b.j));
-            if (take) best = ci;
-        }
-        // block argmax in the same total order (candidate indices through LDS)
-        __shared__ int s_best[BF_NT];
-        s_best[tid] = best;
+        // the bunch's best enters: block argmax of the threads' best members
+        // in the same total order, keys through LDS (s_bun is free again)
+        __shared__ int s_bi[BF_NT], s_bj[BF_NT];
+        s_bun[tid] = ba;
+        s_bun[BF_NT + tid] = bt;
+        s_bi[tid] = bi;
+        s_bj[tid] = bj;
         __syncthreads();
         for (int h = BF_NT / 2; h >= 1; h >>= 1) {
             if (tid < h) {
-                const int x = s_best[tid], y = s_best[tid + h];
-                if (x < 0) s_best[tid] = y;
-                else if (y >= 0) {
-                    const DualCand& o = d.dcomp[y];
-                    const DualCand& b = d.dcomp[x];
-                    const bool take = bland ? (o.t < b.t || (o.t == b.t && o.j < b.j))
-                                            : (fabs(o.a) > fabs(b.a) || (fabs(o.a) == fabs(b.a) && o.j < b.j));
-                    if (take) s_best[tid] = y;
+                const int y = s_bi[tid + h];
+                if (y >= 0) {
+                    const double ya = s_bun[tid + h], yt = s_bun[BF_NT + tid + h];
+                    const int yj = s_bj[tid + h];
+                    const bool take = s_bi[tid] < 0 ||
+                                      (bland ? (yt < s_bun[BF_NT + tid] || (yt == s_bun[BF_NT + tid] && yj < s_bj[tid]))
+                                             : (ya > s_bun[tid] || (ya == s_bun[tid] && yj < s_bj[tid])));
+                    if (take) {
+                        s_bun[tid] = ya;
+                        s_bun[BF_NT + tid] = yt;
+                        s_bi[tid] = y;
+                        s_bj[tid] = yj;
+                    }
                 }
             }
             __syncthreads();
         }
-        qidx = s_best[0];
+        qidx = s_bi[0];
         break;
     }
     __syncthreads();
@@ -4924,14 +5026,14 @@ hipError_t launch_dual_iteration_head(const Dev& d, int k_ub, int ny_ub, hipStre
 }
 
 hipError_t launch_dual_iteration_tail(const Dev& d, int k_ub, hipStream_t st) {
-    k_dual_bfrt<<<1, BF_NT, 0, st>>>(d, 0, 1);
+    k_dual_bfrt<<<1, BF_NT, 0, st>>>(d, 0, 1, bfrt_reg());
     return dual_tail(d, k_ub, st);
 }
 
 // column-only shards: the ratio test over the gathered candidates, then the
 // owner's entering column into pkt[0, m) (others: zeros) and a_F cleared
 hipError_t launch_dual_ratio_shards(const Dev& d, hipStream_t st) {
-    k_dual_bfrt<<<1, BF_NT, 0, st>>>(d, 0, 1);
+    k_dual_bfrt<<<1, BF_NT, 0, st>>>(d, 0, 1, bfrt_reg());
     k_dual_qpack<<<cdiv(d.m > 0 ? d.m : 1, 256), 256, 0, st>>>(d);
     return hipGetLastError();
 }
@@ -4945,7 +5047,7 @@ hipError_t launch_dual_iteration_finish(const Dev& d, int k_ub, hipStream_t st) 
 
 hipError_t launch_dual_iteration(const Dev& d, int k_ub, int ny_ub, hipStream_t st) {
     const int nreg = dual_head(d, k_ub, ny_ub, st);
-    k_dual_bfrt<<<1, BF_NT, 0, st>>>(d, nreg, 0);
+    k_dual_bfrt<<<1, BF_NT, 0, st>>>(d, nreg, 0, bfrt_reg());
     return dual_tail(d, k_ub, st);
 }
 

@@ -284,9 +284,10 @@ int elp_get_stats(elp_handle* h, elp_stats* st);
 
 /* get.sensitivity.obj / get.sensitivity.rhs             R/class.R:613-646
  * Sensitivity report of the final basis of an OPTIMAL solve (ELP_E_STATE
- * otherwise, as R's stop("Problem is not optimal"); one GPU or an ngpu handle --
- * each rank ranges its own columns, the report is the one-GPU report bit for
- * bit; ELP_E_UNSUPPORTED after elp_comm_init*).  Any output
+ * otherwise, as R's stop("Problem is not optimal"); one GPU, an ngpu handle or
+ * a rank of elp_comm_init* -- each rank ranges its own columns, the report is
+ * the one-GPU report bit for bit; after elp_comm_init* it is a collective that
+ * every rank calls and each receives the full report).  Any output
  * may be NULL.  objfrom[n] / objtill[n]: range of each objective coefficient
  * over which the basis stays optimal; duals[m+n]: constraint duals then reduced
  * costs (user sense); dualsfrom / dualstill[m+n]: range of each constraint's rhs

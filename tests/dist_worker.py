@@ -84,8 +84,11 @@ def sharded_solve_worker(rank, world, port, q, cases, replicate=0, p2p=False, ct
             p.load_dense(A, dirs, rhs, obj, lo, up, mx)
         st = p.solve()
         sol = p.solution(st)
-        results.append({"status": sol.status, "objval": sol.objval, "x": sol.x,
-                        "basis": sol.basis, "trace": sol.trace, "stats": sol.stats})
+        res = {"status": sol.status, "objval": sol.objval, "x": sol.x,
+               "basis": sol.basis, "trace": sol.trace, "stats": sol.stats}
+        if case.get("sens") and st == 0:  # (a collective: every rank asks)
+            res["sens"] = p.sensitivity()
+        results.append(res)
         p.close()
     q.put((rank, results, t.errors))
     dist.barrier()

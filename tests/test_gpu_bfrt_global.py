@@ -1,0 +1,27 @@
+"""k_dual_bfrt's two storage paths for the candidates: up to 4 096 candidates
+the bunch rounds run from registers (each thread's run of the compacted
+candidates), above that from dcomp / dalive in global memory.  The fixtures
+mostly fit the register path, so the dual parity tests run again in a child
+process with ELP_BFRT_REG=0 (every BFRT takes the global-memory path) -- the
+traces, flips and pivots must still be the oracle's bit for bit, one GPU and
+column-sharded ngpu ranks (the gathered records)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def test_dual_parity_with_global_bfrt():
+    env = dict(os.environ, ELP_BFRT_REG="0")
+    cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", "-m", "gpu",
+           os.path.join(HERE, "test_gpu_dual.py"),
+           os.path.join(HERE, "test_gpu_ngpu.py") + "::test_ngpu_dual_matches_oracle",
+           os.path.join(HERE, "test_gpu_ngpu.py") + "::test_ngpu_dual_kkt_flips"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=os.path.dirname(HERE))
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-2000:])
+    assert " passed" in r.stdout

@@ -264,7 +264,7 @@ def _same_dual(g, o, tag):
             np.testing.assert_allclose(g.x, o.x, rtol=1e-12, atol=1e-12 * max(1.0, np.abs(o.x).max()), err_msg=tag)
 
 
-@pytest.mark.parametrize("ngpu,replicate", [(2, 0), (3, 0), (2, 2), (3, 2)])
+@pytest.mark.parametrize("ngpu,replicate", [(2, 0), (3, 0), (4, 0), (2, 2), (3, 2), (4, 2)])
 def test_ngpu_dual_matches_oracle(gpu, ngpu, replicate):
     """SIMPLEX_DUAL_PRIMAL (lp_solve's default, R/class.R:262 / :276) on the
     column-sharded ranks of one handle, A replicated: each rank prices its

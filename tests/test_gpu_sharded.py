@@ -122,6 +122,43 @@ def test_sharded_dual_matches_oracle(world, replicate, p2p):
     assert duals >= 5, duals
 
 
+@pytest.mark.parametrize("world,replicate", [(2, 1), (3, 2)])
+def test_sharded_sensitivity(world, replicate):
+    """elp_sensitivity after one process per rank (elp_comm_init*): a collective
+    -- each rank ranges its own columns, the parts are all-gathered -- and every
+    rank's report is the one-GPU report bit for bit (R/class.R:613-646 read
+    after a sharded solve)."""
+    import easylp_amd
+    from dist_worker import sharded_solve_worker
+    from oracle import generate_dense
+    A, b, c = generate_dense(3, 120, 700)
+    cases = [{"kind": "dense", "lp": (A, np.ones(120, np.int32), b, c, None, None, True), "sens": True},
+             dict(_cases()[1], sens=True)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=sharded_solve_worker, args=(r, world, port, q, cases, replicate, False))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, results, errors = q.get(timeout=240)
+        assert errors == 0
+        res[r] = results
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for ci, case in enumerate(cases):
+        one = easylp_amd.solve_dense(*case["lp"][:6], maximize=case["lp"][6], sensitivity=True)
+        assert one.status == 0
+        for r in range(world):
+            g = res[r][ci]
+            assert g["status"] == 0
+            for key in ("objfrom", "objtill", "duals", "dualsfrom", "dualstill"):
+                np.testing.assert_array_equal(g["sens"][key], one.sens[key], err_msg=(ci, r, key))
+
+
 def test_rccl_single_rank_p2p_mailbox(monkeypatch):
     """The mailbox exchange on a 1-rank RCCL communicator: the select kernel
     writes its record into its own mailbox and waits for it."""

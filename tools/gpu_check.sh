@@ -50,5 +50,10 @@ python3 "$ROOT/tools/pmc_traffic.py" "$(find "$TMP/pmc" -name '*counter_collecti
 WIN="--steps 0 --warmup 0 --window 1 --c4 0 --sparse 0 --no-cpu --compare-rules 0 --host-input 0 --host-c4 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$TMP/tl" -o run -- python3 "$ROOT/bench.py" $WIN > "$OUT/tl_bench_$TAG.json" 2>&1 || { echo "rocprof timeline failed"; exit 7; }
 python3 "$ROOT/tools/timeline.py" "$(find "$TMP/tl" -name '*kernel_trace.csv' | head -1)" 100 1000 > "$OUT/timeline_$TAG.txt" && cat "$OUT/timeline_$TAG.txt"
+# the sparse 20000 x 100000 LPs: probe times, then the per-kernel
+# stats of the phase-1 (dual simplex) solve
+timeout -k 10 300 python3 "$ROOT/tools/sparse_probe.py" > "$OUT/sparse_probe_$TAG.txt" 2>&1 && cat "$OUT/sparse_probe_$TAG.txt" || { echo "sparse probe failed"; exit 8; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$TMP/sp" -o run -- python3 "$ROOT/tools/sparse_probe.py" kkt_20000x100000 > "$OUT/sparse_prof_$TAG.txt" 2>&1 || { echo "sparse rocprof failed"; exit 9; }
+cp "$(find "$TMP/sp" -name '*kernel_stats.csv' | head -1)" "$OUT/sparse_kernel_stats_$TAG.csv"
 rm -rf "$TMP"
 echo done
