@@ -117,6 +117,11 @@ struct elp_handle {
     // (ranks sharing a device: hipFree waits for the device to drain, and the
     // other ranks' select kernels spin on this rank's next mailbox record)
     std::vector<void*> retired;
+    // a warm-started B&B node's bounds (reload_bounds_warm), n each: allocated at
+    // the first node and kept, so no node allocates or frees (a hipFree would
+    // wait for peers spinning on this rank's record when ranks share a device)
+    double* warm_lo = nullptr;
+    double* warm_up = nullptr;
     // buffers of the last load kept for the next one (free_dev on a reload):
     // alloc_all's allocations by size; a reload of the same shape takes them
     // back instead of ~80 hipFree + hipMalloc pairs (1.8 ms at 5000 x 50000)
@@ -222,6 +227,9 @@ static void free_dev(elp_handle* h, bool keep_big = false) {
     if (!keep_big) drain_pool(h);
     for (void* p : h->retired) (void)hipFree(p);
     h->retired.clear();
+    if (h->warm_lo) (void)hipFree(h->warm_lo);
+    if (h->warm_up) (void)hipFree(h->warm_up);
+    h->warm_lo = h->warm_up = nullptr;
     for (void*& p : h->lub)
         if (p) {
             (void)hipFree(p);
@@ -2429,9 +2437,9 @@ static int reload_bounds_warm(elp_handle* h, const std::vector<double>& lo, cons
         lo_s[(size_t)j] = unscale_col(h, fin(lo[(size_t)j]), j, -1);
         up_s[(size_t)j] = unscale_col(h, fin(up[(size_t)j]), j, -1);
     }
-    double *dlo = nullptr, *dup = nullptr;
-    HIPCHK(dalloc(&dlo, n));
-    HIPCHK(dalloc(&dup, n));
+    if (!h->warm_lo) HIPCHK(hipMalloc((void**)&h->warm_lo, (size_t)std::max<int64_t>(n, 1) * sizeof(double)));
+    if (!h->warm_up) HIPCHK(hipMalloc((void**)&h->warm_up, (size_t)std::max<int64_t>(n, 1) * sizeof(double)));
+    double *dlo = h->warm_lo, *dup = h->warm_up;
     HIPCHK(hipMemcpyAsync(dlo, lo_s.data(), (size_t)n * sizeof(double), hipMemcpyHostToDevice, h->st));
     HIPCHK(hipMemcpyAsync(dup, up_s.data(), (size_t)n * sizeof(double), hipMemcpyHostToDevice, h->st));
     // the control block of a fresh solve, the basis kept
@@ -2442,6 +2450,11 @@ static int reload_bounds_warm(elp_handle* h, const std::vector<double>& lo, cons
     c.status = ST_RUN;
     c.phase = 2;
     c.iter = 0;
+    // a new mailbox epoch, as every load: the iteration count restarts at 0, and
+    // the last node's final records (seq = epoch << 40 | iteration + 1) still sit
+    // in the peers' slots -- under the old epoch a rank reaching the same
+    // iteration number could take a stale record for its peer's
+    c.mb_epoch = ++h->mb_epoch;
     c.iter_limit = h->ctl.max_iter > 0 ? std::max<int64_t>(h->bnb_iter_left, 0) : 100 * (h->m + n) + 10000;
     c.iter_stop = INT64_MAX;
     c.since_refactor = 0;
@@ -2461,8 +2474,6 @@ static int reload_bounds_warm(elp_handle* h, const std::vector<double>& lo, cons
     HIPCHK(launch_warm_start(d, dlo, dup, k, ny, h->st));
     HIPCHK(hipMemcpyAsync(h->hctl, d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
     HIPCHK(hipStreamSynchronize(h->st));
-    (void)hipFree(dlo);
-    (void)hipFree(dup);
     h->stats = elp_stats{};
     h->stats.world_size = h->comm.world;
     h->stats.ncols = h->nloc;

@@ -4213,17 +4213,24 @@ DEV int block_scan_excl(int v, int* excl, int* lds) {
 constexpr int BF_NT = 1024;
 constexpr int BF_BUN = 1024;  // bunch entries staged in LDS for the flip sum (16 KiB)
 constexpr int BF_RR = 4;      // candidates per thread held in registers (N <= 4096)
-// ELP_BFRT_REG=0 (test hook): every candidate set takes the global-memory path
+// ELP_BFRT_REG (test hook): 0 every candidate set takes the workgroup path from
+// global memory, 1 the workgroup path from registers (up to 4096 candidates),
+// 2 (default) also the one-wave path for up to 64 * BF_RR candidates
 static int bfrt_reg() {
-    static const int on = [] {
+    static const int mode = [] {
         const char* e = std::getenv("ELP_BFRT_REG");
-        return e ? (std::atoi(e) != 0) : 1;
+        return e ? std::atoi(e) : 2;
     }();
-    return on;
+    return mode;
 }
 // the regions' candidates in region order into dst[0, total): region counts
-// scanned in chunks of BF_NT regions, each thread copying its own regions
+// scanned in chunks of BF_NT regions, then the chunk's records copied by the
+// whole workgroup (output slot o -> its region by a binary search over the
+// scanned offsets in LDS), so the copies are independent loads in flight
+// instead of one thread walking a region's records one after another (a
+// region holds up to DREG)
 DEV int compact_regions(const Dev& d, int nreg, DualCand* dst, int* scan_lds) {
+    __shared__ int s_off[BF_NT];
     const int tid = threadIdx.x;
     int total = 0;
     for (int r0 = 0; r0 < nreg; r0 += BF_NT) {
@@ -4231,11 +4238,21 @@ DEV int compact_regions(const Dev& d, int nreg, DualCand* dst, int* scan_lds) {
         const int cnt = r < nreg ? d.dcnt[r] : 0;
         int excl;
         const int tot = block_scan_excl<BF_NT>(cnt, &excl, scan_lds);
-        if (r < nreg) {
-            const DualCand* src = d.dcand + (size_t)r * DREG;
-            for (int t = 0; t < cnt; ++t) dst[total + excl + t] = src[t];
+        s_off[tid] = excl;
+        __syncthreads();
+        for (int o = tid; o < tot; o += BF_NT) {
+            // the last region whose offset is <= o (empty regions share their
+            // successor's offset; regions past nreg sit at tot > o)
+            int lo = 0, hi = BF_NT - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (s_off[mid] <= o) lo = mid;
+                else hi = mid - 1;
+            }
+            dst[total + o] = d.dcand[(size_t)(r0 + lo) * DREG + (o - s_off[lo])];
         }
         total += tot;
+        __syncthreads();  // (s_off is rewritten by the next chunk)
     }
     return total;
 }
@@ -4247,6 +4264,117 @@ __global__ void __launch_bounds__(BF_NT) k_dual_pack(Dev d, int nreg) {
     if (d.ctl->status != ST_RUN) return;
     const int total = compact_regions(d, nreg, d.dsend + 1, scan_lds);
     if (threadIdx.x == 0) d.dsend[0].j = total;
+}
+
+// Small candidate sets (N <= 64 * BF_RR, the usual case: ~36 candidates per
+// dual pivot on kkt_2000x10000, ~5 bunch rounds) run the bunch rounds in one
+// wave: lane l holds its run of the compacted candidates in registers, the
+// round's minimum, prefix count, all-boxed test and entering choice are wave
+// shuffles (no workgroup barrier per step), the flip sum is lane 0's in-order
+// fma chain over the bunch staged in LDS.  Same decisions as the block path.
+DEV void bfrt_wave(const Dev& d, int N, int bland, double ptol, double slope, double* s_bun, int* nflip_out,
+                   int* qidx_out) {
+    const int lane = threadIdx.x & 63;
+    const int run = (N + 63) / 64;
+    const int lo = min(N, lane * run), hi = min(N, lo + run);
+    const double INF = HUGE_VAL;
+    double rt[BF_RR], rb[BF_RR], ra[BF_RR], rw[BF_RR];
+    int rj[BF_RR];
+    unsigned ral = 0;
+#pragma unroll
+    for (int q = 0; q < BF_RR; ++q) {
+        rt[q] = rb[q] = ra[q] = rw[q] = 0.0;
+        rj[q] = 0;
+        if (lo + q < hi) {
+            const DualCand& o = d.dcomp[lo + q];
+            rt[q] = o.t;
+            rb[q] = o.b;
+            ra[q] = fabs(o.a);
+            rw[q] = o.r;
+            rj[q] = o.j;
+            ral |= 1u << q;
+        }
+    }
+    int nflip = 0, qidx = -1;
+    for (;;) {
+        double bmin = INF;
+#pragma unroll
+        for (int q = 0; q < BF_RR; ++q)
+            if (ral >> q & 1u) bmin = fmin(bmin, rb[q]);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) bmin = fmin(bmin, __shfl_xor(bmin, off));
+        if (!__any(ral != 0)) break;  // nothing left: the dual ray (q = -1)
+        const double thmax = bmin;
+        unsigned rbun = 0;
+        int cnt = 0, allbox = 1;
+#pragma unroll
+        for (int q = 0; q < BF_RR; ++q)
+            if ((ral >> q & 1u) && rt[q] <= thmax) {
+                rbun |= 1u << q;
+                cnt++;
+                if (rw[q] == INF) allbox = 0;
+            }
+        int incl = cnt;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int u = __shfl_up(incl, off);
+            if (lane >= off) incl += u;
+        }
+        const int nq = __shfl(incl, 63);
+        const bool boxed = __all(allbox);
+        // the bunch in order: (|alpha|, u - l) to LDS for the sum, compact
+        // indices to dflip; this lane's best member for the entering choice
+        double ba = -1.0, bt = INF;
+        int bj = -1, bi = -1;
+        int o = nflip + incl - cnt;
+#pragma unroll
+        for (int q = 0; q < BF_RR; ++q)
+            if (rbun >> q & 1u) {
+                s_bun[2 * (o - nflip)] = ra[q];
+                s_bun[2 * (o - nflip) + 1] = rw[q];
+                d.dflip[o++] = lo + q;
+                const bool take = bi < 0 || (bland ? (rt[q] < bt || (rt[q] == bt && rj[q] < bj))
+                                                   : (ra[q] > ba || (ra[q] == ba && rj[q] < bj)));
+                if (take) {
+                    ba = ra[q];
+                    bt = rt[q];
+                    bj = rj[q];
+                    bi = lo + q;
+                }
+            }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double sum = 0.0;
+        if (lane == 0 && boxed)  // |alpha| (u - l) in ascending id (nq <= N <= 64 BF_RR < BF_BUN)
+            for (int t = 0; t < nq; ++t) sum = fma(s_bun[2 * t], s_bun[2 * t + 1], sum);
+        sum = __shfl(sum, 0);
+        __builtin_amdgcn_wave_barrier();  // (s_bun is rewritten by the next round)
+        if (nq == 0) break;  // (NaN ratios only: no candidate qualifies -- the ray)
+        if (boxed && sum < slope - ptol) {  // flip the bunch
+            slope = slope - sum;
+            ral &= ~rbun;
+            nflip += nq;
+            continue;
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double ya = __shfl_xor(ba, off), yt = __shfl_xor(bt, off);
+            const int yj = __shfl_xor(bj, off), yi = __shfl_xor(bi, off);
+            const bool take = yi >= 0 && (bi < 0 || (bland ? (yt < bt || (yt == bt && yj < bj))
+                                                           : (ya > ba || (ya == ba && yj < bj))));
+            if (take) {
+                ba = ya;
+                bt = yt;
+                bj = yj;
+                bi = yi;
+            }
+        }
+        qidx = bi;
+        break;
+    }
+    *nflip_out = nflip;
+    *qidx_out = qidx;
 }
 
 // gathered: P = world ranks' packed records in drecv (rank order) instead of
@@ -4276,12 +4404,26 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     }
     __syncthreads();  // (the compacted array is read by other threads below)
     const int N = total;
-    const int run = (N + BF_NT - 1) / BF_NT;  // this thread's candidates [lo, hi)
+    const double ptol = c->tol_primal;
+    int nflip = 0, qidx = -1;
+    const bool wave = reg_ok >= 2 && N <= 64 * BF_RR;  // (bfrt_wave: the usual case)
+    if (wave) {
+        if (tid < 64) bfrt_wave(d, N, bland, ptol, fabs(c->dr_x - c->dr_beta), s_bun, &nflip, &qidx);
+        if (tid == 0) {
+            s_int[2] = nflip;
+            s_int[3] = qidx;
+        }
+        __syncthreads();
+        nflip = s_int[2];
+        qidx = s_int[3];
+    }
+    // the workgroup path: thread t's candidates [lo, hi) (none when the wave ran)
+    const int run = wave ? 0 : (N + BF_NT - 1) / BF_NT;
     const int lo = min(N, tid * run), hi = min(N, lo + run);
     // up to BF_RR candidates per thread (N <= BF_RR * BF_NT) are held in
     // registers for the bunch rounds (fully unrolled: no scratch); larger
     // candidate sets walk dcomp / dalive in global memory
-    const bool reg = reg_ok && run <= BF_RR;
+    const bool reg = reg_ok >= 1 && run <= BF_RR;
     double rt[BF_RR], rb[BF_RR], ra[BF_RR], rw[BF_RR];
     int rj[BF_RR];
     unsigned ral = 0;  // live mask of the register candidates
@@ -4305,8 +4447,8 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     }
     double slope = fabs(c->dr_x - c->dr_beta);
     const double INF = HUGE_VAL;
-    int nflip = 0, qidx = -1;
     for (;;) {
+        if (wave) break;
         // smallest Harris bound among the live candidates
         double bmin = INF;
         int live = 0;
@@ -4413,7 +4555,7 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
         __syncthreads();
         const double sum = s_dbl[0];
         if (nq == 0) break;  // (NaN ratios only: no candidate qualifies -- the ray)
-        if (s_int[1] && sum < slope - c->tol_primal) {  // flip the bunch (x_r still out past it)
+        if (s_int[1] && sum < slope - ptol) {  // flip the bunch (x_r still out past it)
             slope = slope - sum;
             if (reg) {
                 ral &= ~rbun;
@@ -4770,14 +4912,23 @@ hipError_t launch_init_rows(const Dev& d, const double* rhs, hipStream_t st) {
 // apply_plan grid: nb_minv workgroups for Minv / MinvT (per_thread elements
 // per thread), then the x_B / AS (/ AR) copy workgroups; threads = the
 // launch's workgroup size
+// Workgroup caps on the Minv / MinvT share (only large bumps reach them): the
+// pricing launch's trailing apply (ELP_APPLY_PT elements per thread) takes up
+// to ELP_MINV_WG_MAX -- 8192 (2048 until r04x) measured 2 % faster on the
+// 20 000 x 100 000 feasible-start LP (k 2000) -- while k_update (one element per
+// thread, its x_B / AS copy workgroups dispatched after them) keeps
+// ELP_UPDATE_WG_MAX = 2048: 8192 there slowed it 21.7 -> 28.1 us at k 2000
+#ifndef ELP_MINV_WG_MAX
+#define ELP_MINV_WG_MAX 8192
+#endif
+#ifndef ELP_UPDATE_WG_MAX
+#define ELP_UPDATE_WG_MAX 2048
+#endif
 static void update_grid(const Dev& d, int k_ub, bool with_ar, unsigned* nb_minv, unsigned* nb,
-                        int threads = 256, int per_thread = 1) {
+                        int threads = 256, int per_thread = 1, unsigned wg_max = ELP_UPDATE_WG_MAX) {
     const int64_t kk = 2 * (int64_t)(k_ub + 1) * (k_ub + 1);
     *nb_minv = cdiv(kk, threads * per_thread);
-#ifndef ELP_MINV_WG_MAX
-#define ELP_MINV_WG_MAX 2048
-#endif
-    if (*nb_minv > ELP_MINV_WG_MAX) *nb_minv = ELP_MINV_WG_MAX;  // (only large bumps reach it)
+    if (*nb_minv > wg_max) *nb_minv = wg_max;
     const int64_t cw = with_ar ? (d.m > d.n ? d.m : d.n) : (d.m > k_ub + 1 ? d.m : k_ub + 1);
     unsigned nb_copy = cdiv(cw, threads);
     if (nb_copy > 1024) nb_copy = 1024;
@@ -4836,7 +4987,7 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phas
     #ifndef ELP_APPLY_PT
 #define ELP_APPLY_PT 4
 #endif
-    if (phase == 2 && d.csc) update_grid(d, k_ub, false, &nb_minv, &napply, TILE_COLS, ELP_APPLY_PT);
+    if (phase == 2 && d.csc) update_grid(d, k_ub, false, &nb_minv, &napply, TILE_COLS, ELP_APPLY_PT, ELP_MINV_WG_MAX);
     // the dense deferred plan in trailing workgroups of the launch (r02's
     // layout, the default again since r04: 3 x 3 interleaved A/B at 5000 x 50000,
     // 25.4k against 24.7k iterations/s with the tiles' waves 1-3 applying it);
@@ -4846,7 +4997,7 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phas
         return !(e && std::atoi(e) == 0);
     }();
     unsigned dnapply = 0, dnb_minv = 0;
-    if (phase == 2 && !d.csc && trail) update_grid(d, k_ub, false, &dnb_minv, &dnapply, PRICE_THREADS, ELP_APPLY_PT);
+    if (phase == 2 && !d.csc && trail) update_grid(d, k_ub, false, &dnb_minv, &dnapply, PRICE_THREADS, ELP_APPLY_PT, ELP_MINV_WG_MAX);
     const int dapply = phase == 2 && !trail ? 1 : 0;
     // + nsw: the slack workgroups (candidates [ntiles, ntiles + nsw)); the dense
     // sweep applies the deferred plan inside its tiles (price_body)

@@ -1,10 +1,10 @@
-"""k_dual_bfrt's two storage paths for the candidates: up to 4 096 candidates
-the bunch rounds run from registers (each thread's run of the compacted
-candidates), above that from dcomp / dalive in global memory.  The fixtures
-mostly fit the register path, so the dual parity tests run again in a child
-process with ELP_BFRT_REG=0 (every BFRT takes the global-memory path) -- the
-traces, flips and pivots must still be the oracle's bit for bit, one GPU and
-column-sharded ngpu ranks (the gathered records)."""
+"""k_dual_bfrt's three paths for the bunch rounds: one wave with the candidates
+in registers (up to 256 candidates: what the fixtures mostly have), the whole
+workgroup from registers (up to 4 096), and the workgroup from dcomp / dalive
+in global memory.  The dual parity tests run again in a child process with
+ELP_BFRT_REG=1 (no one-wave path) and =0 (every BFRT from global memory) --
+the traces, flips and pivots must still be the oracle's bit for bit, one GPU
+and column-sharded ngpu ranks (the gathered records)."""
 import os
 import subprocess
 import sys
@@ -16,8 +16,9 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def test_dual_parity_with_global_bfrt():
-    env = dict(os.environ, ELP_BFRT_REG="0")
+@pytest.mark.parametrize("mode", ["1", "0"])
+def test_dual_parity_with_global_bfrt(mode):
+    env = dict(os.environ, ELP_BFRT_REG=mode)
     cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", "-m", "gpu",
            os.path.join(HERE, "test_gpu_dual.py"),
            os.path.join(HERE, "test_gpu_ngpu.py") + "::test_ngpu_dual_matches_oracle",
