@@ -2016,7 +2016,11 @@ DEV double csr_zrow(const Dev& d, int i, int k, const double* __restrict__ xs) {
 // FTRAN-z + Harris pass 1 for CSC input: row tiles of 64 rows (one per lane,
 // csr_zrow), then bump tiles of 64 positions, then the snapshot workgroup --
 // k_ftran_zr's regions and minima with one wave per tile (zw = 1)
-__global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt) {
+// flip (the dual phase): the bound flips' x_B update rides along -- covered rows
+// x -= sigma (a_F,i - A[i, S] fS) by a second row walk, bump positions x -= fS
+// (k_dual_flip_apply's arithmetic) -- before x_B is read; until r04 a launch of
+// its own (k_dual_flip_apply_sp, ~22 us per dual pivot at 20 000 x 100 000)
+__global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt, int flip) {
     const DevCtl* c = d.ctl;
     const int32_t st0 = c->status;
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) d.ctl->snap_status = st0;  // for k_ratio
@@ -2031,6 +2035,7 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt) {
         if (threadIdx.x == 0) zr_snapshot(d, k, q);
         return;
     }
+    const bool fl = flip && c->nflip > 0;
     double tmin = HUGE_VAL, ge = 0.0, xe = 0.0, le = 0.0, he = 0.0;
     int ve = -1, e = 0, region;
     if ((int)blockIdx.x < nrt) {
@@ -2045,6 +2050,11 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt) {
             d.alU[i] = alU;
             ge = sig * alU;
             xe = d.xr[i];
+            if (fl) {
+                const double tot = csr_zrow(d, i, k, d.fS);
+                xe = xe - unit_sign(d, u, i) * (d.aF[i] - tot);
+                d.xr[i] = xe;
+            }
             le = d.rlo[i];
             he = d.rhi[i];
             ve = u;
@@ -2057,6 +2067,10 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt) {
         if (p < k) {
             ge = sig * d.alS[p];
             xe = d.xs[p];
+            if (fl) {
+                xe = xe - d.fS[p];
+                d.xs[p] = xe;
+            }
             le = d.slo[p];
             he = d.shi[p];
             ve = d.Sl[p];
@@ -4612,6 +4626,22 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
         d.vstat[jl] = up ? VS_UPPER : VS_LOWER;
         d.xval[jl] = up ? d.ub[jl] : d.lb[jl];
     }
+    // CSC (one GPU): a_F = sum of the flipped columns times their dx here, in
+    // place of a one-workgroup k_dual_flip_col launch -- each row's entries in
+    // flip order, the same fma chain
+    if (d.csc && !gathered && qidx >= 0 && nflip > 0) {
+        for (int i = tid; i < d.m; i += BF_NT) d.aF[i] = 0.0;
+        __syncthreads();  // (also publishes the ids / dx above)
+        for (int f = 0; f < nflip; ++f) {
+            const int j = d.dflip[f];
+            const double dx = d.dflipdx[f];
+            for (int64_t t = d.cptr[j] + tid; t < d.cptr[j + 1]; t += BF_NT) {
+                const int i = d.rind[t];
+                d.aF[i] = fma(d.cval[t], dx, d.aF[i]);
+            }
+            __syncthreads();
+        }
+    }
     if (tid != 0) return;
     const int64_t it = c->iter;
     if (qidx < 0) {  // dual unbounded: the LP is infeasible (oracle: trace -2, the leaving variable)
@@ -4654,29 +4684,15 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     c->iter_bytes += pb + 48.0 * kk * kk + 8.0 * mm * kk * (nflip > 0 ? 2.0 : 1.0) + 16.0 * (double)d.n + 16.0 * mm;
 }
 
-// a_F = sum over the flips (in list order) of a_j dx_j: dense, one row per
-// thread (the oracle's per-row fma chain); CSC, one workgroup scattering the
-// flipped columns one after the other (rows of a column are distinct, so each
-// row sees the same chain)
+// a_F = sum over the flips (in list order) of a_j dx_j, dense A: one row per
+// thread (the oracle's per-row fma chain).  CSC: k_dual_bfrt's tail scatters
+// the flipped columns one after the other (rows of a column are distinct, so
+// each row sees the same chain)
 __global__ void __launch_bounds__(256) k_dual_flip_col(Dev d) {
     const DevCtl* c = d.ctl;
     const int nf = c->nflip;
     if (c->status != ST_RUN || nf == 0) return;
-    const int m = d.m;
-    if (d.csc) {
-        for (int i = threadIdx.x; i < m; i += blockDim.x) d.aF[i] = 0.0;
-        __syncthreads();
-        for (int f = 0; f < nf; ++f) {
-            const int j = d.dflip[f];
-            const double dx = d.dflipdx[f];
-            for (int64_t t = d.cptr[j] + threadIdx.x; t < d.cptr[j + 1]; t += blockDim.x) {
-                const int i = d.rind[t];
-                d.aF[i] = fma(d.cval[t], dx, d.aF[i]);
-            }
-            __syncthreads();
-        }
-        return;
-    }
+    const int m = d.m;  // (dense A only: CSC builds a_F in k_dual_bfrt)
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
     double acc = 0.0;
@@ -4685,23 +4701,6 @@ __global__ void __launch_bounds__(256) k_dual_flip_col(Dev d) {
         acc = fma(qcol_at(d, qcolumn(d, j), j, i), d.dflipdx[f], acc);
     }
     d.aF[i] = acc;
-}
-
-// CSC: the same update with A[i, S] fS from the row's nonzeros (csr_zrow), one
-// thread per row, then the bump positions
-__global__ void __launch_bounds__(256) k_dual_flip_apply_sp(Dev d) {
-    const DevCtl* c = d.ctl;
-    if (c->status != ST_RUN || c->nflip == 0) return;
-    const int m = d.m, k = c->k;
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    if (t < m) {
-        const int u = d.cover[t];
-        if (u < 0) return;
-        const double tot = csr_zrow(d, t, k, d.fS);
-        d.xr[t] = d.xr[t] - unit_sign(d, u, t) * (d.aF[t] - tot);
-    } else if (t - m < k) {
-        d.xs[t - m] = d.xs[t - m] - d.fS[t - m];
-    }
 }
 
 // column-only shards (no replicated A): the owner of a structural entering
@@ -5055,7 +5054,7 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     const size_t lds_als = lds + (size_t)k_ub * sizeof(double) + (size_t)nxp * ZCHUNK * ZR_ROWS * sizeof(double);
     const bool als = !no_als && ldsz && k_ub > 2 * zw * ZCHUNK && k_ub <= ZR_PA * 64 * zw && lds_als <= 64 * 1024;
     if (spz) {
-        k_ftran_zr_sp<<<nrt + nbt + 1, 64, 0, st>>>(d, nrt);
+        k_ftran_zr_sp<<<nrt + nbt + 1, 64, 0, st>>>(d, nrt, phase == 3 ? 1 : 0);
     } else {
         // + 1: the snapshot workgroup
         if (als) {
@@ -5210,10 +5209,10 @@ static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_co
     const int lds_row = lds <= 48 * 1024;
     unsigned nrw = cdiv(k_ub > 0 ? k_ub : 1, 4);
     if (nrw > 1024) nrw = 1024;
-    if (flip_col) k_dual_flip_col<<<d.csc ? 1u : cdiv(m > 0 ? m : 1, 256), 256, 0, st>>>(d);
+    if (flip_col && !d.csc) k_dual_flip_col<<<cdiv(m > 0 ? m : 1, 256), 256, 0, st>>>(d);  // (CSC: k_dual_bfrt)
     if (k_ub > 0) k_dual_flip_bump<<<nrw, 256, lds_row ? lds : 0, st>>>(d, lds_row);
     if (use_spz(d, k_ub)) {
-        k_dual_flip_apply_sp<<<cdiv((int64_t)m + k_ub, 256), 256, 0, st>>>(d);
+        // (the row-wise x_B update runs inside k_ftran_zr_sp, below)
     } else {
         const unsigned nrt = cdiv(m > 0 ? m : 1, ZR_ROWS), nbt = cdiv(k_ub > 0 ? k_ub : 1, 512);
         const size_t zl = (size_t)cdiv(k_ub > 0 ? k_ub : 1, ZCHUNK) * ZR_ROWS * sizeof(double);

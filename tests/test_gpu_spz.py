@@ -1,4 +1,4 @@
-"""The CSC path's row-wise FTRAN-z (k_ftran_zr_sp / k_dual_flip_apply_sp:
+"""The CSC path's row-wise FTRAN-z (k_ftran_zr_sp, with the dual flip update:
 A[i, S] v from the rows' nonzeros in bump-position order, the oracle's zchunk
 grouping).  The library switches to it once the dense walk over AS would stream
 more than ELP_SPZ_MIN_MB; the fixtures here are far below that, so the CSC
