@@ -1662,6 +1662,13 @@ __global__ void __launch_bounds__(256) k_select_ftran(DEV_PARAM, int ntiles, int
             for (int p = tid; p < k; p += 256) aRs[p] = d.Rl[p] == i0 ? 1.0 : 0.0;
         }
     }
+    // dual == 2 (CSC dual pivot with the row-wise flip update): the flips' bump
+    // FTRAN fS = Minv a_F[R] rides here too (k_dual_flip_bump's chains, the
+    // second k_ub doubles of LDS holding a_F[R])
+    const bool ffs = dual == 2 && c->nflip > 0;
+    double* afr = aRs + k_ub;
+    if (ffs)
+        for (int p = tid; p < k; p += 256) afr[p] = d.aF[d.Rl[p]];
     __syncthreads();
     const bool stats_here = blockIdx.x == 0 && tid == 0 && !dual;
     if (pr >= k) {
@@ -1679,11 +1686,19 @@ __global__ void __launch_bounds__(256) k_select_ftran(DEV_PARAM, int ntiles, int
     }
     acc = wave_tree(acc);
     if (lane == 0) d.alS[pr] = acc;
+    if (ffs) {
+        const double f = wave_tree(lane_chain(d.Minv + (size_t)pr * d.ldm, afr, k));
+        if (lane == 0) d.fS[pr] = f;
+    }
     // (capped grid only) the rows past the first 4 nrw, from memory
     for (int p2 = pr + 4 * nrw; p2 < k; p2 += 4 * nrw) {
         double a2 = lane_chain(d.Minv + (size_t)p2 * d.ldm, aRs, k);
         a2 = wave_tree(a2);
         if (lane == 0) d.alS[p2] = a2;
+        if (ffs) {
+            const double f = wave_tree(lane_chain(d.Minv + (size_t)p2 * d.ldm, afr, k));
+            if (lane == 0) d.fS[p2] = f;
+        }
     }
     if (stats_here) entering_stats(d);
     RSTAMP(15);
@@ -5210,8 +5225,12 @@ static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_co
     unsigned nrw = cdiv(k_ub > 0 ? k_ub : 1, 4);
     if (nrw > 1024) nrw = 1024;
     if (flip_col && !d.csc) k_dual_flip_col<<<cdiv(m > 0 ? m : 1, 256), 256, 0, st>>>(d);  // (CSC: k_dual_bfrt)
-    if (k_ub > 0) k_dual_flip_bump<<<nrw, 256, lds_row ? lds : 0, st>>>(d, lds_row);
-    if (use_spz(d, k_ub)) {
+    const bool spz = use_spz(d, k_ub);
+    // CSC with the row-wise update: the flips' bump FTRAN inside k_select_ftran
+    // (dual = 2; a_R and a_F[R] side by side in LDS)
+    const bool fold_fs = spz && 2 * lds <= 64 * 1024 && !d.force_select;
+    if (k_ub > 0 && !fold_fs) k_dual_flip_bump<<<nrw, 256, lds_row ? lds : 0, st>>>(d, lds_row);
+    if (spz) {
         // (the row-wise x_B update runs inside k_ftran_zr_sp, below)
     } else {
         const unsigned nrt = cdiv(m > 0 ? m : 1, ZR_ROWS), nbt = cdiv(k_ub > 0 ? k_ub : 1, 512);
@@ -5220,14 +5239,15 @@ static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_co
         else k_dual_flip_apply<false><<<nrt + nbt, 512, 0, st>>>(d, (int)nrt);
     }
     // the entering column q (k_dual_bfrt's, candidate 0): a_R, alpha_S (+ staging)
-    if (lds <= 48 * 1024 && !d.force_select) {
-        const size_t ldsz = lds > 64 ? lds : 64;
+    if (fold_fs || (lds <= 48 * 1024 && !d.force_select)) {
+        const size_t ldsz = fold_fs ? (2 * lds > 64 ? 2 * lds : 64) : (lds > 64 ? lds : 64);
+        const int dual = fold_fs ? 2 : 1;
         const unsigned nqz = d.qz && !d.csc ? cdiv(m, 256 * QZ_PT) : 0;
         const unsigned g = nrw + nqz + (d.csc ? 1 : 0);
         if (k_ub > 512 && k_ub <= 640)
-            k_select_ftran<10><<<g, 256, ldsz, st>>>(DEV_ARG(d), 1, 0, k_ub, 0, (int)nrw, (int)nqz, 1);
+            k_select_ftran<10><<<g, 256, ldsz, st>>>(DEV_ARG(d), 1, 0, k_ub, 0, (int)nrw, (int)nqz, dual);
         else
-            k_select_ftran<8><<<g, 256, ldsz, st>>>(DEV_ARG(d), 1, 0, k_ub, 0, (int)nrw, (int)nqz, 1);
+            k_select_ftran<8><<<g, 256, ldsz, st>>>(DEV_ARG(d), 1, 0, k_ub, 0, (int)nrw, (int)nqz, dual);
         return launch_iteration_tail(d, k_ub, 3, st, false, 0, nqz > 0 ? 1 : 0);
     }
     k_select<<<1, 1024, 0, st>>>(d, 1, 0, 1);
