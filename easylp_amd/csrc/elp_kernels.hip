@@ -2032,9 +2032,10 @@ DEV double csr_zrow(const Dev& d, int i, int k, const double* __restrict__ xs) {
 // csr_zrow), then bump tiles of 64 positions, then the snapshot workgroup --
 // k_ftran_zr's regions and minima with one wave per tile (zw = 1)
 // flip (the dual phase): the bound flips' x_B update rides along -- covered rows
-// x -= sigma (a_F,i - A[i, S] fS) by a second row walk, bump positions x -= fS
-// (k_dual_flip_apply's arithmetic) -- before x_B is read; until r04 a launch of
-// its own (k_dual_flip_apply_sp, ~22 us per dual pivot at 20 000 x 100 000)
+// x -= sigma (a_F,i - A[i, S] fS) by a row walk in nrt extra waves, bump
+// positions x -= fS (k_dual_flip_apply's arithmetic); the dual leaves on
+// k_dual_row's row, so no primal pass 1 runs.  Until r04 a launch of its own
+// (k_dual_flip_apply_sp, ~22 us per dual pivot at 20 000 x 100 000)
 __global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt, int flip) {
     const DevCtl* c = d.ctl;
     const int32_t st0 = c->status;
@@ -2051,6 +2052,18 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt, int flip) {
         return;
     }
     const bool fl = flip && c->nflip > 0;
+    if (flip && (int)blockIdx.x >= (int)gridDim.x - 1 - nrt) {  // the flip update's row waves
+        if (!fl) return;
+        const int i = (blockIdx.x - (gridDim.x - 1 - nrt)) * 64 + lane;
+        const int u = i < m ? d.cover[i] : -1;
+        if (u >= 0) {
+            const double tot = csr_zrow(d, i, k, d.fS);
+            d.xr[i] = d.xr[i] - unit_sign(d, u, i) * (d.aF[i] - tot);
+        }
+        return;
+    }
+    // (flip: the dual phase leaves with k_dual_row's row -- no primal pass 1,
+    //  and x_B is being updated beside this)
     double tmin = HUGE_VAL, ge = 0.0, xe = 0.0, le = 0.0, he = 0.0;
     int ve = -1, e = 0, region;
     if ((int)blockIdx.x < nrt) {
@@ -2063,33 +2076,30 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt, int flip) {
             const double aiq = q >= d.N ? (i == q - d.N ? 1.0 : 0.0) : d.qcol[i];
             const double alU = unit_sign(d, u, i) * (aiq - z);
             d.alU[i] = alU;
-            ge = sig * alU;
-            xe = d.xr[i];
-            if (fl) {
-                const double tot = csr_zrow(d, i, k, d.fS);
-                xe = xe - unit_sign(d, u, i) * (d.aF[i] - tot);
-                d.xr[i] = xe;
+            if (!flip) {
+                ge = sig * alU;
+                xe = d.xr[i];
+                le = d.rlo[i];
+                he = d.rhi[i];
+                ve = u;
+                tmin = harris1(ge, xe, le, he, ptol, pivtol, bland);
             }
-            le = d.rlo[i];
-            he = d.rhi[i];
-            ve = u;
-            tmin = harris1(ge, xe, le, he, ptol, pivtol, bland);
         }
     } else {
         const int p = (blockIdx.x - nrt) * 64 + lane;
         e = m + p;
         region = blockIdx.x;  // (= nrt + bump tile: one wave per tile)
         if (p < k) {
-            ge = sig * d.alS[p];
-            xe = d.xs[p];
-            if (fl) {
-                xe = xe - d.fS[p];
-                d.xs[p] = xe;
+            if (flip) {
+                if (fl) d.xs[p] = d.xs[p] - d.fS[p];
+            } else {
+                ge = sig * d.alS[p];
+                xe = d.xs[p];
+                le = d.slo[p];
+                he = d.shi[p];
+                ve = d.Sl[p];
+                tmin = harris1(ge, xe, le, he, ptol, pivtol, bland);
             }
-            le = d.slo[p];
-            he = d.shi[p];
-            ve = d.Sl[p];
-            tmin = harris1(ge, xe, le, he, ptol, pivtol, bland);
         }
     }
     const double bmin = wave_min_f64(tmin);
@@ -5069,7 +5079,8 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     const size_t lds_als = lds + (size_t)k_ub * sizeof(double) + (size_t)nxp * ZCHUNK * ZR_ROWS * sizeof(double);
     const bool als = !no_als && ldsz && k_ub > 2 * zw * ZCHUNK && k_ub <= ZR_PA * 64 * zw && lds_als <= 64 * 1024;
     if (spz) {
-        k_ftran_zr_sp<<<nrt + nbt + 1, 64, 0, st>>>(d, nrt, phase == 3 ? 1 : 0);
+        // (the dual phase: + nrt waves for the flips' x_B update, before the snapshot one)
+        k_ftran_zr_sp<<<nrt + nbt + (phase == 3 ? nrt : 0) + 1, 64, 0, st>>>(d, nrt, phase == 3 ? 1 : 0);
     } else {
         // + 1: the snapshot workgroup
         if (als) {
