@@ -78,12 +78,12 @@ def parse():
                     help="N=1: run the sharded pipeline on a 1-rank RCCL communicator (overhead probe)")
     ap.add_argument("--sparse", type=int, default=1,
                     help="also time the CSC path on a sparse LP (BASELINE config 5)")
+    ap.add_argument("--c2", type=int, default=1,
+                    help="N=1: also BASELINE configs[1] (500 x 2000) to optimality from host memory")
     ap.add_argument("--sparse-m", type=int, default=1000)
     ap.add_argument("--sparse-n", type=int, default=10000)
     ap.add_argument("--sparse-steps", type=int, default=1000)
     ap.add_argument("--sparse-cpu-iters", type=int, default=200)
-    ap.add_argument("--sparse-window", type=int, default=2000,
-                    help="iterations of the phase-1 Netlib-scale LP's primal phase 1 timed from its start")
     ap.add_argument("--pricing", choices=["devex", "dantzig"], default="devex",
                     help="pricing rule (elp_control.pricing; devex is lp_solve's default)")
     ap.add_argument("--sync-every", type=int, default=32,
@@ -254,15 +254,26 @@ def full_solves(p, As, b, c, count, ctx):
 
 def price_roofline(stats_list):
     """Pricing-launch roofline over the given solves: algorithmic sweep bytes /
-    the launches' time (HIP events bound to each timed pricing dispatch)."""
-    secs = sum(s["price_seconds"] for s in stats_list)
+    the launches' time.  The time is the kernel's own clock (every workgroup of
+    the sampled launches stamps s_memrealtime at entry and exit, first start ->
+    last end: `avg_launch_us`); HIP events bound to the same dispatches
+    (`avg_launch_us_events`) read the dispatch gap too and stay beside it."""
+    secs_ev = sum(s["price_seconds"] for s in stats_list)
+    secs = sum(s.get("price_seconds_stamps", 0.0) for s in stats_list)
+    ns = sum(s.get("price_stamped_launches", 0) for s in stats_list)
     byts = sum(s["price_timed_bytes"] for s in stats_list)
     nl = sum(s["price_timed_launches"] for s in stats_list)
+    src = "stamps"
+    if not (secs > 0 and ns == nl):  # (no stamped launches: the events)
+        secs, src = secs_ev, "events"
     ach = byts / secs / 1e9 if secs > 0 else None
     return {"achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": ach / HBM_PEAK_GBS if ach else None,
             "bytes_per_launch": byts / nl if nl else None,
-            "avg_launch_us": 1e6 * secs / nl if nl else None, "launches_timed": nl}
+            "avg_launch_us": 1e6 * secs / nl if nl else None, "launches_timed": nl,
+            "avg_launch_us_events": 1e6 * secs_ev / nl if nl else None,
+            "frac_events": byts / secs_ev / 1e9 / HBM_PEAK_GBS if secs_ev > 0 else None,
+            "launch_timer": src}
 
 
 def iteration_roofline(stats_list):
@@ -479,14 +490,48 @@ def host_input(args, lib, ctx, m, n, label, reps):
             "h2d_bytes": 8.0 * m * n, "objective": obj, "runs": out, "best": best}
 
 
+def c2_config(args, local, reps=5):
+    """BASELINE configs[1]: the dense 500 x 2000 LP (seed args.seed, the LP the
+    HiGHS leg times as cpu_baseline_highs.c2) to optimality from host memory
+    (elp_load_dense + elp_solve, what one easylp$solve() call pays): the best of
+    `reps` solves after one untimed warm-up."""
+    import numpy as np
+    import torch
+    from easylp_amd import Problem, generate_dense_device
+    m, n = 500, 2000
+    A, b, c = generate_dense_device(args.seed, m, n, local)
+    Ah = A.cpu().numpy().reshape(n, m).T  # column-major (m, n) view
+    del A
+    torch.cuda.empty_cache()
+    dirs = np.ones(m, np.int32)
+    runs = []
+    with Problem(m, n, device=local, pricing=args.rule) as p:
+        for r in range(reps + 1):
+            torch.cuda.synchronize(local)
+            t0 = time.perf_counter()
+            p.load_dense(Ah, dirs, b, c, maximize=True)
+            st = p.solve()
+            el = time.perf_counter() - t0
+            s = p.stats()
+            if r:
+                runs.append({"status": st, "time_to_optimal_s": el, "iterations": s["iterations"]})
+        obj = p.solution(st).objval
+    best = min(runs, key=lambda r: r["time_to_optimal_s"])
+    return {"workload": "dense random LP m=500 n=2000 seed %d (BASELINE configs[1]), from host memory" % args.seed,
+            "status": best["status"], "objective": obj, "iterations": best["iterations"],
+            "time_to_optimal_s": best["time_to_optimal_s"],
+            "value": best["iterations"] / best["time_to_optimal_s"], "unit": "iterations/s (whole solve)",
+            "runs": [r["time_to_optimal_s"] for r in runs]}
+
+
 def sparse_rate(args, local, with_cpu):
     """BASELINE config 5 on the CSC path (basis AUTO = the explicit bump
     inverse with k-sized buffers):
       * "Netlib scale": the 20 000 x 100 000 LPs of easylp_amd.synth.sparse_kkt
         (5 nonzeros per column, boxed columns, optimum known by construction
-        and pinned by HiGHS in tests/golden/sparse_lu.json): the feasible-start
-        one to optimality, the phase-1 one over its first `sparse_window`
-        iterations (it needs ~70 000 primal pivots: minutes, DESIGN.md 9.1);
+        and pinned by HiGHS in tests/golden/sparse_lu.json), both to
+        optimality: the feasible-start one (primal) and the phase-1 one (dual
+        simplex phase 1, lp_solve's SIMPLEX_DUAL_PRIMAL default);
       * the seeded 1000 x 10 000 packing LP (sparse_packing) to optimality and
         a steady-state window;
       * the Klee-Minty cube n = 12 (4095 Dantzig pivots on the unscaled cube).
@@ -530,8 +575,7 @@ def sparse_rate(args, local, with_cpu):
                                          "included" % r.stats["iterations"]}
     out["netlib_scale"] = big
     # ---- the phase-1 LP of the same size: the dual simplex phase 1 (lp_solve's
-    #      SIMPLEX_DUAL_PRIMAL) to optimality; the primal phase 1 on artificials
-    #      (~70 000 pivots) over a window from its start ----
+    #      SIMPLEX_DUAL_PRIMAL) to optimality ----
     k = fx["kkt_20000x100000"]
     cp, ri, v, b, c, u, obj = sparse_kkt(k["seed"], k["m"], k["n"], k["k"])
     with Problem(m, n, device=local, pricing=args.rule, simplex=6) as p:
@@ -553,16 +597,6 @@ def sparse_rate(args, local, with_cpu):
         "time_to_optimal_s": tto, "load_s": s["seconds_load"],
         "value": s["iterations"] / tto if tto > 0 else None, "unit": "iterations/s (whole solve)",
         "highs_iterations": k["highs_iterations"]}
-    with Problem(m, n, device=local, pricing=args.rule, simplex=5) as p:
-        t0 = time.perf_counter()
-        p.load_csc(cp, ri, v, dirs, b, c, lo, u, maximize=True)
-        st = p.iterate(args.sparse_window)
-        el = time.perf_counter() - t0
-        s = p.stats()
-    out["netlib_scale_phase1"]["primal_phase1_window"] = {
-        "iterations": s["iterations"], "status": st, "basic_structurals": s["bump_dim"], "seconds": el,
-        "note": "the primal phase 1 on artificials over its first iterations: ~70 000 pivots to optimality "
-                "(DESIGN.md 9.1)"}
     # ---- 1000 x 10 000 packing ----
     m, n = args.sparse_m, args.sparse_n
     cp, ri, v, b, c = sparse_packing(args.seed, m, n, 5)
@@ -624,6 +658,8 @@ def sparse_rate(args, local, with_cpu):
                       scaling=0)
         out["klee_minty"]["cpu_seconds"] = time.perf_counter() - t0
         out["klee_minty"]["cpu_iterations"] = rk.stats["iterations"]
+        # (> 1: the GPU is slower -- 4095 latency-bound pivots of a 12 x 12 LP)
+        out["klee_minty"]["gpu_over_cpu_time"] = kt / out["klee_minty"]["cpu_seconds"]
     return out
 
 
@@ -688,7 +724,9 @@ def main():
     # (hipExtLaunchKernelGGL, on the solver's stream) of every 8th chunk of
     # iterations between host polls in the timed solves -- a uniform sample, so
     # the markers stay off most dispatches (events on all of them cost ~9 %)
-    roof = dict(price_roofline(stats), timer="HIP events on the pricing dispatches of every 8th chunk of the timed solves")
+    roof = dict(price_roofline(stats), timer="the pricing kernel's own s_memrealtime stamps (first workgroup start -> "
+                "last workgroup end) on the pricing dispatches of every 8th chunk of the timed solves; HIP events "
+                "bound to the same dispatches in avg_launch_us_events")
     last = stats[-1] if stats else p.stats()
     final = {"status": recs[-1][0] if recs else None, "iterations_to_optimal": last["iterations"],
              "objective": p.solution(recs[-1][0]).objval if recs else None,
@@ -754,7 +792,17 @@ def main():
     if args.sparse and max(world, ctx.ngpu) == 1:
         sparse = sparse_rate(args, local, rank == 0 and not args.no_cpu)
 
+    c2 = c2_config(args, local) if args.c2 and max(world, ctx.ngpu) == 1 else None
+
     highs_res = highs.result(timeout=400) if highs is not None else None
+    # GPU / CPU on the same LPs (> 1: the GPU is faster)
+    if c2 and highs_res and highs_res.get("c2"):
+        c2["highs_time_to_optimal_s"] = highs_res["c2"]["time_to_optimal_s"]
+        c2["speedup_vs_highs"] = highs_res["c2"]["time_to_optimal_s"] / c2["time_to_optimal_s"]
+    if sparse and highs_res and highs_res.get("kkt_20000x100000"):
+        ph1 = sparse["netlib_scale_phase1"]
+        ph1["highs_time_to_optimal_s"] = highs_res["kkt_20000x100000"]["time_to_optimal_s"]
+        ph1["speedup_vs_highs"] = ph1["highs_time_to_optimal_s"] / ph1["time_to_optimal_s"]
     # time to optimal includes the H2D copy of A (what .Call pays:
     # elp_load_dense from host memory); the HBM-resident figure stays beside it
     tto_hbm = elapsed / max(args.steps, 1)
@@ -812,6 +860,7 @@ def main():
             "cpu_baseline_highs": highs_res,
             "amdahl": amdahl,
             "scaling_config": c4,
+            "c2": c2,
             "sparse_config": sparse,
         }
         print(json.dumps(line), flush=True)

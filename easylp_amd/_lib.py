@@ -19,7 +19,7 @@ ELP_PROFILE_EVENTS = 4  # HIP events on every pricing dispatch
 ELP_PROFILE_SAMPLE = 8  # ... on those of every 8th chunk between host polls
 ELP_SCALE_GEOMETRIC, ELP_SCALE_EQUILIBRATE = 4, 64
 ELP_BASIS_AUTO, ELP_BASIS_INVERSE, ELP_BASIS_LU = 0, 1, 2
-ABI_VERSION = 5
+ABI_VERSION = 6
 ELP_SIMPLEX_PRIMAL_PRIMAL, ELP_SIMPLEX_DUAL_PRIMAL = 5, 6
 
 # every entry point the header declares (checked by tests/test_abi.py)
@@ -104,6 +104,8 @@ class ElpStats(ctypes.Structure):
         ("simplex", ctypes.c_int32),
         ("exchange_rtt_us", ctypes.c_double),
         ("dual_iterations", ctypes.c_int64),
+        ("price_seconds_stamps", ctypes.c_double),
+        ("price_stamped_launches", ctypes.c_int64),
     ]
 
 

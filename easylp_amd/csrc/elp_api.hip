@@ -221,7 +221,8 @@ static void free_dev(elp_handle* h, bool keep_big = false) {
                     (void*)d.cptr, (void*)d.rind, (void*)d.cval, (void*)d.rptr, (void*)d.cind,
                     (void*)d.rval, d.qcol, d.qz, d.spos, d.dstamp, d.rowvs, d.yvs, d.dw, d.dprev, (void*)d.srow,
                     (void*)d.scol, d.rhoR, d.rr, d.dchz, d.dcand, d.dcnt, d.dcomp, d.dalive, d.dflip,
-                    d.dflipdx, d.aF, d.fS, d.ddw != d.dw ? (void*)d.ddw : nullptr, d.dsend, d.drecv};
+                    d.dflipdx, d.aF, d.fS, d.ddw != d.dw ? (void*)d.ddw : nullptr, d.dsend, d.drecv,
+                    d.afs, d.afl, d.aflv, d.ptst, d.ptgrid};
     for (void* p : ptrs)
         if (p) release(p);
     if (!keep_big) drain_pool(h);
@@ -318,14 +319,16 @@ static hipError_t take_or_alloc(double** p, size_t bytes, double** keep, size_t*
 // "Threading": the R caller stays one synchronous process): the handle the
 // caller holds drives P rank handles, one per device, each the column-sharded
 // solver of one rank (elp_comm_* semantics).  Every API call runs on all ranks
-// at once -- rank 0 on the calling thread, the others on one host thread each
-// -- and returns when all are done.  Ranks on distinct devices share an RCCL
+// at once -- one host thread per rank (RCCL ranks: the calling thread watches
+// them; in-process ranks: rank 0 runs on the calling thread) -- and returns
+// when all are done.  Ranks on distinct devices share an RCCL
 // communicator from ncclCommInitAll (xGMI); ranks that share a device (fewer
 // devices than P, e.g. a one-GPU box) use the in-process ThreadGroup.
 static bool is_group(const elp_handle* h) { return h && !h->ranks.empty(); }
 
 // collective = false: the call issues no collective (elp_set_int, elp_set_trace,
-// elp_sensitivity), so a failing rank never strands a peer and nothing is aborted.
+// the ngpu elp_sensitivity parts), so a failing rank never strands a peer and
+// nothing is aborted.
 // Otherwise a rank failure releases the peers that wait in a collective: the
 // in-process transport fails its waiters at once (and is reset at the next
 // call); RCCL communicators (distinct devices) are aborted -- for good: later
@@ -358,11 +361,16 @@ static int fan_out(elp_handle* g, F&& f, bool collective = true) {
         --running;
         cv.notify_all();
     };
+    // RCCL ranks (distinct devices): every rank on a worker thread and the
+    // calling thread the watchdog -- rank 0 itself may be the one blocked in a
+    // collective for a failed peer, and only an abort from outside releases it
+    // (ADVICE r04); otherwise rank 0 runs on the calling thread
+    const bool watch = collective && !g->tgroup;
     std::vector<std::thread> th;
     th.reserve((size_t)P);
-    for (int r = 1; r < P; ++r) th.emplace_back(run, r);
-    run(0);
-    if (collective && !g->tgroup) {
+    for (int r = watch ? 0 : 1; r < P; ++r) th.emplace_back(run, r);
+    if (!watch) run(0);
+    if (watch) {
         std::unique_lock<std::mutex> lk(mu);
         for (;;) {
             if (running == 0) break;
@@ -621,6 +629,15 @@ static int alloc_all_body(elp_handle* h) {
     d.mb_ticks = (int64_t)(h->ctl.mailbox_timeout * 1e8);  // s_memrealtime: 100 MHz
     d.ptimer = ELP_DIAG && (h->ctl.verbose & ELP_PROFILE_PRICE) ? 1 : 0;  // (diagnostic builds)
     d.csc = h->csc ? 1 : 0;
+    // CSC bumps above ELP_SPF_MIN (512) positions: sparse FTRAN and B^-1 rows
+    // (DESIGN.md 9); below it the dense chains' prefetched rows win
+    {
+        static const int spf = [] {
+            const char* s = std::getenv("ELP_SPF_MIN");
+            return s ? std::atoi(s) : 512;
+        }();
+        d.spf_min = h->csc && !h->lu && spf > 0 ? spf : 0;
+    }
     // the mailbox carries the min-loc record only: with A not replicated the
     // entering column must travel, so that load uses the collective
     d.p2p = h->comm.p2p && h->replicated ? 1 : 0;
@@ -711,11 +728,17 @@ static int alloc_all_body(elp_handle* h) {
 #endif
     if (h->csc) A(dalloc(&d.qcol, mm));
     if (h->csc && !h->lu) A(dalloc(&d.spos, (size_t)(n > 0 ? n : 1)));  // (the sparse FTRAN-z's column -> position)
-    else if (!std::getenv("ELP_NO_QZ")) A(dalloc(&d.qz, mm));  // (ELP_NO_QZ: A/B switch)
+    if (!h->csc && !std::getenv("ELP_NO_QZ")) A(dalloc(&d.qz, mm));  // (dense only; ELP_NO_QZ: A/B switch)
     if (ELP_DIAG && std::getenv("ELP_STAMPS")) {  // (diagnostic builds)
         A(dalloc(&d.dstamp, DSTAMP_STRIDE * 64));
         d.stamp_wide = std::atoi(std::getenv("ELP_STAMPS")) >= 2;
     }
+    // the release pricing timer's stamps (launch_btran_price's largest grid:
+    // tiles + slack workgroups + deferred-update workgroups)
+    d.ptslots = 64;
+    d.ptcap = (int32_t)(d.ntiles + (mm / 128 + 1) + 8192 + 1024 + 64);
+    A(dalloc(&d.ptst, 2 * (size_t)d.ptslots * (size_t)d.ptcap));
+    A(dalloc(&d.ptgrid, (size_t)d.ptslots));
     A(dalloc(&d.ctl, 1));
     A(dalloc(&d.trace, (size_t)(h->trace_cap > 0 ? 2 * h->trace_cap : 2)));
     // dual simplex phase 1 (elp_kernels.hip "dual simplex"): regions = the
@@ -738,6 +761,13 @@ static int alloc_all_body(elp_handle* h) {
         A(dalloc(&d.dflipdx, (size_t)(Ng + m)));
         A(dalloc(&d.aF, mm));
         A(dalloc(&d.fS, mm));
+        if (h->csc) {  // (a_F's support and sparse a_F[R], k_dual_bfrt's tail)
+            A(dalloc(&d.afs, (size_t)(1 + 1024)));
+            A(dalloc(&d.afl, (size_t)(AFL_POS + 256)));
+            A(dalloc(&d.aflv, (size_t)256));
+            A(hipMemsetAsync(d.afs, 0xff, sizeof(int32_t), h->st));  // -1: clear all of a_F first
+            A(hipMemsetAsync(d.afl, 0xff, sizeof(int32_t), h->st));  // -1: no list
+        }
         d.dslack = !d.sharded || h->comm.rank == h->comm.world - 1;
         if (d.sharded) {
             const int P = h->comm.world;
@@ -1873,6 +1903,9 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
         if (ELP_DEV_PTR && (rc = upload_dev(h))) return rc;  // (Dev::self for this chunk's launches)
         const double t_enq0 = now_s();
         const bool prof_chunk = prof && (prof_all || h->prof_chunks++ % 8 == 0);
+        // (the device-clock timer of the same launches: ticks before the chunk)
+        const unsigned long long ticks0 = c->price_ticks;
+        const int64_t timed0 = c->price_timed;
         for (int t = 0; t < chunk; ++t) {
             const int kub = (int)std::min<int64_t>(h->m, (int64_t)k0 + t);
             const int nyub = (int)std::min<int64_t>(h->m, (int64_t)ny0 + t);
@@ -1905,12 +1938,13 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
                     HIPCHK(launch_dual_iteration_finish(h->d, kub, h->st));
                 }
             } else if (h->comm.kind == 0 || h->d.p2p) {  // (p2p: min-loc inside the select kernel)
-                HIPCHK(launch_iteration(h->d, kub, nyub, h->phase, h->st, e0, e1, t));
+                HIPCHK(launch_iteration(h->d, kub, nyub, h->phase, h->st, e0, e1, t, prof_chunk ? t : -1));
             } else {
                 // sharded: local min-loc -> all-gather -> global min-loc.  Replicated
                 // A: a_R + bump FTRAN straight from the local copy -> tail.  Else the
                 // owner packs its column, all-reduce (non-owners contribute zeros).
-                HIPCHK(launch_iteration_head(h->d, kub, nyub, h->phase, h->comm.rank, h->st, e0, e1));
+                HIPCHK(launch_iteration_head(h->d, kub, nyub, h->phase, h->comm.rank, h->st, e0, e1,
+                                             prof_chunk ? t : -1));
                 rc = h->comm.allgather(h->d.cand_xchg + h->comm.rank, h->d.cand_xchg, sizeof(CandX), h->st);
                 if (rc) return fail(rc, "candidate all-gather failed");
                 if (h->replicated) {
@@ -1933,6 +1967,7 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             }
         }
         const double t_enq1 = now_s();
+        if (prof_chunk && h->phase == 2) HIPCHK(launch_ptimer_reduce(h->d, std::min(chunk, h->d.ptslots), h->st));
         HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
         HIPCHK(hipStreamSynchronize(h->st));
         // a poll that just queues the next chunk (phase 2 running, no budget, cap,
@@ -1982,6 +2017,8 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             }
             h->stats.price_timed_launches += chunk;
             h->stats.price_timed_bytes += c->price_bytes - bytes0;
+            h->stats.price_seconds_stamps += 1e-8 * (double)(c->price_ticks - ticks0);  // (100 MHz clock)
+            h->stats.price_stamped_launches += c->price_timed - timed0;
         }
         if (s == ST_RUN) {
             if (h->ctl.time_limit > 0) {
@@ -2717,6 +2754,13 @@ extern "C" int elp_get_solution(elp_handle* h, double* objval, double* x, double
             *objval = acc;
         }
     }
+    if (h->mip) {
+        // branch and bound: y and the basis belong to the last node LP, not to
+        // the incumbent -- reported as zeros / -1 (include/easylp_hip.h)
+        if (y && m) std::fill(y, y + m, 0.0);
+        if (basis && m) std::fill(basis, basis + m, (int64_t)-1);
+        return 0;
+    }
     if (y && m) {
         HIPCHK(hipMemcpyAsync(y, h->d.y, m * sizeof(double), hipMemcpyDeviceToHost, h->st));
         HIPCHK(hipStreamSynchronize(h->st));
@@ -2948,6 +2992,7 @@ static int sens_gather(elp_handle* h, std::vector<SensPart>& parts) {
         sp.col0 = (int64_t)x[0];
         sp.ncols = (int64_t)x[1];
         sp.k = (int)x[2];
+        if (sp.ncols < 0) return fail(ELP_E_STATE, "elp_sensitivity: rank " + std::to_string(r) + " failed its part");
         if (sp.k != k || sp.ncols > cap) return fail(ELP_E_STATE, "elp_sensitivity: the ranks' bases differ");
         sp.o4.assign(x + 3, x + 3 + 4 * (size_t)k);
         const double* c = x + 3 + 4 * (size_t)k;
@@ -3000,10 +3045,21 @@ extern "C" int elp_sensitivity(elp_handle* h, double* objfrom, double* objtill, 
     if (rc0) return rc0;
     std::vector<SensPart> parts(1);
     const int rc = sens_part(h, parts[0]);
-    if (rc) return rc;
     if (h->comm.kind != 0) {
+        // a collective: a rank whose part failed still joins the all-gather,
+        // its record flagged (ncols = -1), so every rank fails together and no
+        // peer waits for it; the record size follows the replicated k
+        const std::string err = g_err;
+        if (rc) {
+            parts[0] = SensPart{};
+            parts[0].k = h->hctl ? h->hctl->k : 0;
+            parts[0].ncols = -1;
+        }
         const int rg = sens_gather(h, parts);
+        if (rc) return fail(rc, err);
         if (rg) return rg;
+    } else if (rc) {
+        return rc;
     }
     sens_assemble(h, parts, objfrom, objtill, duals, dualsfrom, dualstill);
     return 0;

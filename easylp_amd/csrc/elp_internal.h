@@ -301,7 +301,25 @@ struct Dev {
     // structurals by ascending id, then the slacks)
     DualCand *dsend, *drecv;
     int32_t dcap, dslack;
+    // CSC dual phase (one GPU): the support of the last a_F (afs[0] rows, -1:
+    // unknown -- clear all m; the rows in afs[1 ..]) and a_F[R] as a
+    // lane-bucketed sparse list for the select kernel's fS (afl[0] = n, -1: use
+    // the dense a_F; afl[1 .. 66) bucket starts; afl[66 ..) positions; aflv the
+    // values), both written by k_dual_bfrt's tail
+    int32_t* afs;
+    int32_t* afl;
+    double* aflv;
+    // CSC: bumps above this many positions take the sparse FTRAN / B^-1-row
+    // paths (ELP_SPF_MIN; 0 never)
+    int32_t spf_min, spf_pad;
+    // release pricing timer (k_price<.., TIMED>): [ptslots][ptcap][start, end]
+    // s_memrealtime stamps per workgroup, the grid of each slot's launch
+    unsigned long long* ptst;
+    int32_t* ptgrid;
+    int32_t ptcap, ptslots;
 };
+constexpr int AFL_SB = 1;    // afl: bucket starts [1, 66)
+constexpr int AFL_POS = 66;  // afl: positions [66, 66 + SPL)
 
 // Sparse-LU engine of the CSC path (elp_control.basis = ELP_BASIS_LU, DESIGN.md
 // 9.1; oracle/elp_oracle_lu.c): the whole basis B (position p holds head[p])
@@ -339,13 +357,16 @@ hipError_t launch_fill_AR(const Dev& d, hipStream_t st);  // AR rows for the ini
 hipError_t launch_ar_relayout(const Dev& d, const double* old_ar, int64_t old_cap, int rows,
                               hipStream_t st);
 // ev0/ev1 (may be null): events recorded around the pricing kernel
+// tslot >= 0: the timed pricing variant into stamp slot tslot (launch_ptimer_reduce)
 hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStream_t st,
-                            hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, int dslot = 0);
+                            hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, int dslot = 0, int tslot = -1);
+// the pricing timer of the chunk's timed slots [0, nslots) into DevCtl::price_ticks
+hipError_t launch_ptimer_reduce(const Dev& d, int nslots, hipStream_t st);
 // sharded iteration: head (BTRAN, pricing, local min-loc into cand_xchg[rank]),
 // then the host all-gathers cand_xchg, select_global packs pkt, the host
 // all-reduces pkt, then tail (a_R, FTRAN, ratio test, update)
 hipError_t launch_iteration_head(const Dev& d, int k_ub, int ny_ub, int phase, int rank,
-                                 hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+                                 hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, int tslot = -1);
 hipError_t launch_select_global(const Dev& d, hipStream_t st);
 // phase 2, at a host poll: apply a plan the last iteration left pending
 hipError_t launch_apply_pending(const Dev& d, int k_ub, hipStream_t st);

@@ -320,6 +320,82 @@ DEV double block_max(double v, double* lds, int ltid = -1) {
     return r;
 }
 
+// exclusive block scan of one int per thread (NT threads); returns the total
+template <int NT>
+DEV int block_scan_excl(int v, int* excl, int* lds) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int u = __shfl_up(incl, off);
+        if (lane >= off) incl += u;
+    }
+    if (lane == 63) lds[w] = incl;
+    __syncthreads();
+    int base = 0, tot = 0;
+    for (int i = 0; i < NT / 64; ++i) {
+        if (i < w) base += lds[i];
+        tot += lds[i];
+    }
+    __syncthreads();
+    *excl = base + incl - v;
+    return tot;
+}
+
+// ---------------------------------------------------------- sparse operands
+// Hypersparse products against the bump inverse (CSC input, large bumps): the
+// operand of a wave_dot -- a_R, a_F[R] (FTRAN), A[i, S] (a row of B^-1) -- has
+// a handful of nonzeros among k positions.  A list of them, lane-bucketed
+// (sorted by (position mod 64, position); lsb[l] = first entry of lane l,
+// lsb[64] = n), lets lane l run exactly its chain of the dense lane_chain
+// (positions l, l + 64, ... ascending) over the nonzero terms only: every
+// skipped term is fma(x, 0, acc) = acc, so the value is the dense one bit for
+// bit, at O(n) loads per wave instead of O(k).
+constexpr int SPL = 256;  // entries per list at most (more: the dense path)
+// lane l's chain over its bucket, loads 4 at a time in flight
+DEV double sparse_lane_chain(const double* __restrict__ x, const int* lpos, const double* lval, const int* lsb) {
+    const int lane = threadIdx.x & 63;
+    const int s = lsb[lane], e = lsb[lane + 1];
+    double acc = 0.0;
+    for (int t0 = s; t0 < e; t0 += 4) {
+        double xv[4], vv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = t0 + u < e ? t0 + u : e - 1;
+            xv[u] = x[lpos[t]];
+            vv[u] = lval[t];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (t0 + u < e) acc = fma(xv[u], vv[u], acc);
+    }
+    return acc;
+}
+// Lane-bucketed list from one candidate entry per thread (NT threads; valid
+// entries carry distinct positions): compaction, rank by (p mod 64, p), bucket
+// starts.  lkey: NT ints of scratch.  Returns n (uniform); ends with a barrier.
+template <int NT>
+DEV int spl_build(bool valid, int p, double v, int* lpos, double* lval, int* lsb, int* lkey, int* scan) {
+    int excl;
+    const int n = block_scan_excl<NT>(valid ? 1 : 0, &excl, scan);
+    const int key = ((p & 63) << 25) | p;  // (positions < 2^25)
+    if (valid) lkey[excl] = key;
+    __syncthreads();
+    if (valid) {
+        int r = 0;
+        for (int t = 0; t < n; ++t) r += lkey[t] < key ? 1 : 0;
+        lpos[r] = p;
+        lval[r] = v;
+    }
+    if ((int)threadIdx.x <= 64) {
+        int b = 0;
+        for (int t = 0; t < n; ++t) b += (lkey[t] >> 25) < (int)threadIdx.x ? 1 : 0;
+        lsb[threadIdx.x] = b;
+    }
+    __syncthreads();
+    return n;
+}
+
 // wave-order phase-1 sum (oracle art_sum): executed by ONE wave
 DEV double wave_art_sum(const Dev& d) {
     const int lane = threadIdx.x & 63;
@@ -1191,12 +1267,60 @@ DEV void pstamp_end(const Dev& d) {
     if (threadIdx.x == 0) d.pstamp[PSTRIDE * blockIdx.x + PSTRIDE - 1] = __builtin_amdgcn_s_memrealtime();
 }
 
-template <int NTL, int TW>
-__global__ void __launch_bounds__(PRICE_THREADS) k_price(DEV_PARAM, int nsw, int apply, int napply, int nb_minv) {
+// The release build's pricing timer: on the sampled chunks
+// (ELP_PROFILE_SAMPLE / _EVENTS) the host launches the TIMED variant, whose
+// workgroups stamp s_memrealtime (the 100 MHz constant clock) at entry and,
+// after a barrier, at exit into slot tslot of Dev::ptst; k_ptimer_reduce then
+// adds first start -> last end of each slot to DevCtl::price_ticks.  Only the
+// sampled launches pay the end barrier and the two stores.
+DEV void tstamp_begin(const Dev& d, int tslot) {
+    if (threadIdx.x == 0 && (int)blockIdx.x < d.ptcap) {
+        d.ptst[2 * ((size_t)tslot * d.ptcap + blockIdx.x)] = __builtin_amdgcn_s_memrealtime();
+        if (blockIdx.x == 0) d.ptgrid[tslot] = (int32_t)gridDim.x;
+    }
+}
+DEV void tstamp_end(const Dev& d, int tslot) {
+    __syncthreads();  // (every return path of the bodies is workgroup-uniform)
+    if (threadIdx.x == 0 && (int)blockIdx.x < d.ptcap)
+        d.ptst[2 * ((size_t)tslot * d.ptcap + blockIdx.x) + 1] = __builtin_amdgcn_s_memrealtime();
+}
+
+template <int NTL, int TW, bool TIMED = false>
+__global__ void __launch_bounds__(PRICE_THREADS) k_price(DEV_PARAM, int nsw, int apply, int napply, int nb_minv,
+                                                         int tslot) {
     DEV_BIND
+    if (TIMED) tstamp_begin(d, tslot);
     pstamp_begin<PRICE_THREADS>(d);
     price_body<NTL, TW>(d, nsw, apply, napply, nb_minv);
     pstamp_end(d);
+    if (TIMED) tstamp_end(d, tslot);
+}
+
+// one workgroup per timed slot of the chunk: first start -> last end
+__global__ void __launch_bounds__(256) k_ptimer_reduce(Dev d) {
+    __shared__ unsigned long long slo[256], shi[256];
+    const int s = blockIdx.x, t = threadIdx.x;
+    const int g = min(d.ptgrid[s], d.ptcap);
+    unsigned long long lo = ~0ull, hi = 0ull;
+    for (int w = t; w < g; w += 256) {
+        const unsigned long long a = d.ptst[2 * ((size_t)s * d.ptcap + w)], b = d.ptst[2 * ((size_t)s * d.ptcap + w) + 1];
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    slo[t] = lo;
+    shi[t] = hi;
+    __syncthreads();
+    for (int h = 128; h >= 1; h >>= 1) {
+        if (t < h) {
+            slo[t] = slo[t + h] < slo[t] ? slo[t + h] : slo[t];
+            shi[t] = shi[t + h] > shi[t] ? shi[t + h] : shi[t];
+        }
+        __syncthreads();
+    }
+    if (t == 0 && shi[0] > slo[0]) {
+        atomicAdd(&d.ctl->price_ticks, shi[0] - slo[0]);
+        atomicAdd(reinterpret_cast<unsigned long long*>(&d.ctl->price_timed), 1ull);
+    }
 }
 
 // algorithmic bytes of one pricing pass.  Dense: the AR sweep (8|Y|n), c and
@@ -1223,10 +1347,13 @@ DEV double price_pass_bytes(const Dev& d, int ny, int devex) {
 #endif
 constexpr int CSC_STAGE = ELP_CSC_STAGE;
 DEV void price_csc_body(const Dev& d, int napply, int nb_minv, int nsw);
-__global__ void __launch_bounds__(TILE_COLS) k_price_csc(Dev d, int napply, int nb_minv, int nsw) {
+template <bool TIMED = false>
+__global__ void __launch_bounds__(TILE_COLS) k_price_csc(Dev d, int napply, int nb_minv, int nsw, int tslot) {
+    if (TIMED) tstamp_begin(d, tslot);
     pstamp_begin<TILE_COLS>(d);
     price_csc_body(d, napply, nb_minv, nsw);
     pstamp_end(d);
+    if (TIMED) tstamp_end(d, tslot);
 }
 DEV void price_csc_body(const Dev& d, int napply, int nb_minv, int nsw) {
     __shared__ double sv[CSC_STAGE], sy[CSC_STAGE];
@@ -1514,6 +1641,82 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles, int nsw, int
     gather_aR(d, q, q < d.N ? qcolumn(d, q) : nullptr);
 }
 
+// A[Rl[p], q] of a CSC column by binary search over its rows (ascending)
+DEV double csc_at(const Dev& d, int64_t jl, int row) {
+    int64_t lo = d.cptr[jl], hi = d.cptr[jl + 1] - 1;
+    while (lo <= hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        const int r = d.rind[mid];
+        if (r == row) return d.cval[mid];
+        if (r < row) lo = mid + 1;
+        else hi = mid - 1;
+    }
+    return 0.0;
+}
+
+// CSC, large bump (k_ub > Dev::spf_min): alpha_S = Minv a_R and (dual == 2 with
+// flips) fS = Minv a_F[R] from lane-bucketed sparse lists -- a_R from column
+// q's rows through rpos, a_F[R] from k_dual_bfrt's list -- one wave per bump
+// row (rows pr, pr + 4 nrw, ...), the dense chains' bits (sparse_lane_chain).
+// A column with more than SPL entries / no a_F list: the dense chain over an
+// operand staged in global memory (d.aR / d.zz; every workgroup writes the same
+// final values, no intermediate state)
+DEV void select_ftran_sparse(const Dev& d, int q, int k, int pr, int nrw, int dual) {
+    __shared__ int s_pos[2][SPL], s_key[SPL], s_sb[2][72], s_scan[4];
+    __shared__ double s_val[2][SPL];
+    const int tid = threadIdx.x, lane = tid & 63;
+    bool dense_a = false;
+    {
+        bool valid = false;
+        int p = 0;
+        double v = 0.0;
+        if (q < d.N) {
+            const int64_t jl = (int64_t)q - d.col0;
+            const int64_t t0 = d.cptr[jl], t1 = d.cptr[jl + 1];
+            dense_a = t1 - t0 > SPL;
+            if (!dense_a && tid < t1 - t0) {
+                const int i = d.rind[t0 + tid];
+                v = d.cval[t0 + tid];
+                p = d.rpos[i];
+                valid = p >= 0 && p < k;
+            }
+        } else if (tid == 0) {
+            p = d.rpos[q - d.N];
+            v = 1.0;
+            valid = p >= 0 && p < k;
+        }
+        if (dense_a) {
+            const int64_t jl = (int64_t)q - d.col0;
+            for (int pp = tid; pp < k; pp += 256) d.aR[pp] = csc_at(d, jl, d.Rl[pp]);
+        } else {
+            spl_build<256>(valid, p, v, s_pos[0], s_val[0], s_sb[0], s_key, s_scan);
+        }
+    }
+    const bool ffs = dual == 2 && d.ctl->nflip > 0;
+    const int nf = ffs ? d.afl[0] : -1;
+    if (ffs && nf >= 0) {
+        for (int t = tid; t < nf; t += 256) {
+            s_pos[1][t] = d.afl[AFL_POS + t];
+            s_val[1][t] = d.aflv[t];
+        }
+        if (tid <= 64) s_sb[1][tid] = d.afl[AFL_SB + tid];
+    } else if (ffs) {
+        for (int pp = tid; pp < k; pp += 256) d.zz[pp] = d.aF[d.Rl[pp]];
+    }
+    __syncthreads();
+    for (int p2 = pr; p2 < k; p2 += 4 * nrw) {
+        const double* row = d.Minv + (size_t)p2 * d.ldm;
+        const double a =
+            wave_tree(dense_a ? lane_chain(row, d.aR, k) : sparse_lane_chain(row, s_pos[0], s_val[0], s_sb[0]));
+        if (lane == 0) d.alS[p2] = a;
+        if (ffs) {
+            const double f =
+                wave_tree(nf >= 0 ? sparse_lane_chain(row, s_pos[1], s_val[1], s_sb[1]) : lane_chain(row, d.zz, k));
+            if (lane == 0) d.fS[p2] = f;
+        }
+    }
+}
+
 // One GPU, fused select + FTRAN on the bump: every workgroup reduces the tile and
 // slack candidates itself (a total order: all agree), gathers a_R into LDS and
 // computes alpha_S for its 4 bump rows (one wave per row, wave order).
@@ -1522,7 +1725,8 @@ __global__ void __launch_bounds__(1024) k_select(Dev d, int ntiles, int nsw, int
 // workgroup b forms rows 4b + wave, 4b + wave + 4 nrw, ...
 // nqz: the staging workgroups after them (Dev::qz; 0: none), QZ_PT rows per thread
 constexpr int QZ_PT = 8;
-template <int PFM>  // Minv values per lane held in registers (k <= 64 PFM): 8 or 16 by the host's bound
+// SP: the CSC sparse FTRAN (select_ftran_sparse) after the min-loc
+template <int PFM, bool SP = false>  // Minv values per lane held in registers (k <= 64 PFM): 8 or 16 by the host's bound
 __global__ void __launch_bounds__(256) k_select_ftran(DEV_PARAM, int ntiles, int nsw, int k_ub, int dslot, int nrw,
                                                       int nqz, int dual) {
     DEV_BIND
@@ -1636,6 +1840,11 @@ __global__ void __launch_bounds__(256) k_select_ftran(DEV_PARAM, int ntiles, int
                 if (i < m) d.qz[i] = i == q - d.N ? 1.0 : 0.0;
             }
         }
+        return;
+    }
+    if constexpr (SP) {
+        select_ftran_sparse(d, q, k, pr, nrw, dual);
+        if (blockIdx.x == 0 && tid == 0 && !dual) entering_stats(d);
         return;
     }
     if (q < d.N && d.csc) {
@@ -2461,7 +2670,14 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
 #pragma unroll
         for (int t = 0; t < PFQ; ++t) rq[s][t] = d.rcand[(size_t)reg * RREG + t];
     }
-    {  // (AR-copy workgroups fetch row 0: harmless)
+    // DUAL: the leaving entry's B^-1 row is k_dual_row's rho_r (same row, same
+    // k): its value on this wave's position replaces the MinvT row
+    double rho_col = 0.0;
+    if constexpr (DUAL) {
+        rho_col = ld_clamp(d.rhoR, main_wg ? col : 0, k_ub);
+#pragma unroll
+        for (int t = 0; t < PFT; ++t) trow[t] = 0.0;
+    } else {  // (AR-copy workgroups fetch row 0: harmless)
         const double* row = d.MinvT + (size_t)(main_wg && col < k_ub ? col : 0) * d.ldm;
 #pragma unroll
         for (int t = 0; t < PFT; ++t) trow[t] = ld_clamp(row, lane + 64 * t, k_ub);
@@ -2477,6 +2693,7 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
         for (int t = 0; t < PFB; ++t) KEEP(bm[t]);
 #pragma unroll
         for (int t = 0; t < PFT; ++t) KEEP(trow[t]);
+        KEEP(rho_col);
         KEEP(rcol);
 #pragma unroll
         for (int s = 0; s < PFR; ++s) {
@@ -2518,7 +2735,13 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
     // case D needs wave_dot(MinvT[apos, :], A[lrow, S]) in every workgroup: wave 0
     // fetches that row now (apos comes with the control block)
     double arow[PFT];
-    {
+    double rho_a = 0.0, dxsig = 0.0;  // DUAL: rho_r at position apos; the leaving row's sigma
+    if constexpr (DUAL) {
+        rho_a = d.rhoR[apos_c >= 0 ? apos_c : 0];
+        dxsig = c->dr_xsig;
+#pragma unroll
+        for (int t = 0; t < PFT; ++t) arow[t] = 0.0;
+    } else {
         const double* row = d.MinvT + (size_t)(apos_c >= 0 ? apos_c : 0) * d.ldm;
 #pragma unroll
         for (int t = 0; t < PFT; ++t) arow[t] = ld_clamp(row, lane + 64 * t, k);
@@ -2729,7 +2952,19 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
     }
     // (a separate bookkeeping workgroup forms no B^-1 row entries; it needs
     //  A[lrow, S] only for case D's vvec[a])
-    if (lrow_all >= 0 && k > 0 && !(ELP_BOOK_WG && lead && !(phase == 2 && pcx == PC_D))) {
+    if (DUAL && lrow_all >= 0 && k > 0) {
+        // the dual phase leaves on k_dual_row's covered row: rho_r = -(sigma v)
+        // with v = row_times_minv(lrow) (wave order), sigma = +-1, so
+        // v = -(sigma rho_r) exactly -- no second pass over MinvT
+        if (col < k && main_wg) {
+            const double acc = -(dxsig * rho_col);
+            const double delta = unit_sign(d, best.var, lrow_all) * (sig * best.g);
+            vcol = q < d.N ? acc / delta : acc;
+            if (lane == 0) d.vvec[col] = vcol;
+        }
+        if (pcx == PC_D && tid == 0) s_wd = dq / (-(dxsig * rho_a));
+        __syncthreads();
+    } else if (lrow_all >= 0 && k > 0 && !(ELP_BOOK_WG && lead && !(phase == 2 && pcx == PC_D))) {
         // huge bumps: every workgroup writes the same values to d.vrow (benign)
         double* asrow = lds_row ? asrow_lds : d.vrow;
         for (int j0 = tid; j0 < k; j0 += 1024) {  // 4 loads in flight per thread (k <= 1024: one pass)
@@ -3900,9 +4135,14 @@ __global__ void __launch_bounds__(256) k_dual_chuzr(Dev d) {
 // Minv row p for bump position p; -sigma (A[i,S] Minv)_c for the slack covering
 // row i (the oracle's row_times_minv in wave order).  Written in position order
 // (rhoR) and on the Y slots (rr, the dense sweep's operand).
-__global__ void __launch_bounds__(256) k_dual_row(Dev d, int nchz, int lds_row) {
+// sp (CSC, large bump): A[i, S] from row i's nonzeros in basic columns (CSR +
+// spos) as a sparse list, rho_c = sparse_lane_chain over row c of MinvT (the
+// dense chain's bits; a row with more than SPL entries takes the dense walk)
+__global__ void __launch_bounds__(256) k_dual_row(Dev d, int nchz, int lds_row, int sp) {
     extern __shared__ __attribute__((aligned(16))) double asrow_lds[];  // [k]: A[i, S]
     __shared__ ChzRec red[256];
+    __shared__ int s_pos[SPL], s_key[SPL], s_sb[72], s_scan[4];
+    __shared__ double s_val[SPL];
     DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
     const int m = d.m, k = c->k, bland = c->bland;
@@ -3936,7 +4176,23 @@ __global__ void __launch_bounds__(256) k_dual_row(Dev d, int nchz, int lds_row) 
         c->dr_xsig = xsig;
     }
     double* asrow = lds_row ? asrow_lds : d.vrow;  // (huge bumps: every workgroup writes the same values)
-    if (xrow >= 0) {
+    bool spl = false;
+    if (xrow >= 0 && sp) {
+        const int64_t t0 = d.rptr[xrow], t1 = d.rptr[xrow + 1];
+        spl = t1 - t0 <= SPL;
+        if (spl) {
+            bool valid = false;
+            int p = 0;
+            double v = 0.0;
+            if (tid < t1 - t0) {
+                v = d.rval[t0 + tid];
+                p = d.spos[d.cind[t0 + tid]];
+                valid = p >= 0 && p < k;
+            }
+            spl_build<256>(valid, p, v, s_pos, s_val, s_sb, s_key, s_scan);
+        }
+    }
+    if (xrow >= 0 && !spl) {
         for (int p = tid; p < k; p += 256) asrow[p] = d.AS[(size_t)p * (size_t)m + xrow];
         __syncthreads();
     }
@@ -3944,7 +4200,8 @@ __global__ void __launch_bounds__(256) k_dual_row(Dev d, int nchz, int lds_row) 
     for (int cc = blockIdx.x * 4 + (tid >> 6); cc < k; cc += gridDim.x * 4) {
         double v;
         if (xrow >= 0) {
-            double acc = lane_chain(d.MinvT + (size_t)cc * d.ldm, asrow, k);
+            const double* mrow = d.MinvT + (size_t)cc * d.ldm;
+            double acc = spl ? sparse_lane_chain(mrow, s_pos, s_val, s_sb) : lane_chain(mrow, asrow, k);
             acc = wave_tree(acc);
             v = -(xsig * acc);
         } else {
@@ -4219,28 +4476,6 @@ __global__ void __launch_bounds__(TILE_COLS) k_dual_price_csc(Dev d, int nsw, in
     emit_region<TILE_COLS>(d, (int)tile, f, o, false, o, wcnt);
 }
 
-// exclusive block scan of one int per thread (NT threads); returns the total
-template <int NT>
-DEV int block_scan_excl(int v, int* excl, int* lds) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int incl = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int u = __shfl_up(incl, off);
-        if (lane >= off) incl += u;
-    }
-    if (lane == 63) lds[w] = incl;
-    __syncthreads();
-    int base = 0, tot = 0;
-    for (int i = 0; i < NT / 64; ++i) {
-        if (i < w) base += lds[i];
-        tot += lds[i];
-    }
-    __syncthreads();
-    *excl = base + incl - v;
-    return tot;
-}
-
 // Bound-flipping Harris ratio test (oracle run_dual), one workgroup: compacts
 // the regions' candidates (region order = ascending structural id, then the
 // slacks), then takes bunches -- the live candidates whose exact ratio is
@@ -4414,6 +4649,101 @@ DEV void bfrt_wave(const Dev& d, int N, int bland, double ptol, double slope, do
     }
     *nflip_out = nflip;
     *qidx_out = qidx;
+}
+
+// CSC (one GPU): a_F = sum of the flipped columns times their dx, each row one
+// fma chain in flip order (oracle run_dual).  Up to AF_PAR entries of flipped
+// columns: one thread per entry, the first entry of each row runs that row's
+// chain over the entries after it (rows of a column are distinct, so the
+// entries in flip order are the chain's terms in order); only the last a_F's
+// support is cleared first (Dev::afs), and a_F[R] leaves as the select
+// kernel's sparse list (Dev::afl).  More: the flips one after the other, a
+// barrier each, after clearing all of a_F (r04's path).
+constexpr int AF_PAR = 256;
+DEV void bfrt_flip_column(const Dev& d, int nflip, int k) {
+    __shared__ int s_off[BF_NT], s_row[AF_PAR], s_lpos[SPL], s_lkey[SPL], s_lsb[72], s_scan[BF_NT / 64];
+    __shared__ double s_v[AF_PAR], s_dx[AF_PAR], s_lval[SPL];
+    const int tid = threadIdx.x, m = d.m;
+    __syncthreads();  // (the flip ids / dx written above)
+    int len = 0;
+    if (tid < nflip) {
+        const int j = d.dflip[tid];
+        len = (int)(d.cptr[j + 1] - d.cptr[j]);
+    }
+    int excl = 0, E = AF_PAR + 1;
+    if (nflip <= BF_NT) E = block_scan_excl<BF_NT>(len, &excl, s_scan);
+    const bool par = E <= AF_PAR;
+    const int pn = d.afs[0];
+    if (pn < 0 || !par) {
+        for (int i = tid; i < m; i += BF_NT) d.aF[i] = 0.0;
+    } else {
+        for (int t = tid; t < pn; t += BF_NT) d.aF[d.afs[1 + t]] = 0.0;
+    }
+    if (!par) {
+        __syncthreads();
+        for (int f = 0; f < nflip; ++f) {
+            const int j = d.dflip[f];
+            const double dx = d.dflipdx[f];
+            for (int64_t t = d.cptr[j] + tid; t < d.cptr[j + 1]; t += BF_NT) {
+                const int i = d.rind[t];
+                d.aF[i] = fma(d.cval[t], dx, d.aF[i]);
+            }
+            __syncthreads();
+        }
+        if (tid == 0) {
+            d.afs[0] = -1;
+            d.afl[0] = -1;
+        }
+        return;
+    }
+    if (tid < nflip) s_off[tid] = excl;
+    __syncthreads();  // (also orders the clear before the chains' stores)
+    int row = -1;
+    if (tid < E) {
+        int lo = 0, hi = nflip - 1;  // the last flip whose offset is <= tid
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_off[mid] <= tid) lo = mid;
+            else hi = mid - 1;
+        }
+        const int j = d.dflip[lo];
+        const int64_t t = d.cptr[j] + (tid - s_off[lo]);
+        row = d.rind[t];
+        s_row[tid] = row;
+        s_v[tid] = d.cval[t];
+        s_dx[tid] = d.dflipdx[lo];
+    }
+    __syncthreads();
+    bool lead = false;
+    double acc = 0.0;
+    int p = -1;
+    if (tid < E) {
+        lead = true;
+        for (int e = 0; e < tid; ++e)
+            if (s_row[e] == row) {
+                lead = false;
+                break;
+            }
+        if (lead) {
+            for (int e = tid; e < E; ++e)
+                if (s_row[e] == row) acc = fma(s_v[e], s_dx[e], acc);
+            d.aF[row] = acc;
+            p = d.rpos[row];
+        }
+    }
+    int lex;
+    const int nl = block_scan_excl<BF_NT>(lead ? 1 : 0, &lex, s_scan);
+    if (lead) d.afs[1 + lex] = row;
+    const int n = spl_build<BF_NT>(lead && p >= 0 && p < k, p, acc, s_lpos, s_lval, s_lsb, s_lkey, s_scan);
+    for (int t = tid; t < n; t += BF_NT) {
+        d.afl[AFL_POS + t] = s_lpos[t];
+        d.aflv[t] = s_lval[t];
+    }
+    if (tid <= 64) d.afl[AFL_SB + tid] = s_lsb[tid];
+    if (tid == 0) {
+        d.afs[0] = nl;
+        d.afl[0] = n;
+    }
 }
 
 // gathered: P = world ranks' packed records in drecv (rank order) instead of
@@ -4654,19 +4984,7 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     // CSC (one GPU): a_F = sum of the flipped columns times their dx here, in
     // place of a one-workgroup k_dual_flip_col launch -- each row's entries in
     // flip order, the same fma chain
-    if (d.csc && !gathered && qidx >= 0 && nflip > 0) {
-        for (int i = tid; i < d.m; i += BF_NT) d.aF[i] = 0.0;
-        __syncthreads();  // (also publishes the ids / dx above)
-        for (int f = 0; f < nflip; ++f) {
-            const int j = d.dflip[f];
-            const double dx = d.dflipdx[f];
-            for (int64_t t = d.cptr[j] + tid; t < d.cptr[j + 1]; t += BF_NT) {
-                const int i = d.rind[t];
-                d.aF[i] = fma(d.cval[t], dx, d.aF[i]);
-            }
-            __syncthreads();
-        }
-    }
+    if (d.csc && !gathered && qidx >= 0 && nflip > 0) bfrt_flip_column(d, nflip, c->k);
     if (tid != 0) return;
     const int64_t it = c->iter;
     if (qidx < 0) {  // dual unbounded: the LP is infeasible (oracle: trace -2, the leaving variable)
@@ -4915,10 +5233,19 @@ hipError_t launch_row_chain(const Dev& d, hipStream_t st) {
 
 // the dense pricing kernel for a launch: non-temporal sweep loads or not, the
 // default tile width as a compile-time constant or ELP_TILE_BAL's at run time
-typedef void (*PriceFn)(DEV_PARAM, int, int, int, int);
-static PriceFn price_kernel(bool nt, int tw) {
+typedef void (*PriceFn)(DEV_PARAM, int, int, int, int, int);
+static PriceFn price_kernel(bool nt, int tw, bool timed) {
+    if (timed) {
+        if (tw == TILE_COLS) return nt ? k_price<1, TILE_COLS, true> : k_price<0, TILE_COLS, true>;
+        return nt ? k_price<1, 0, true> : k_price<0, 0, true>;
+    }
     if (tw == TILE_COLS) return nt ? k_price<1, TILE_COLS> : k_price<0, TILE_COLS>;
     return nt ? k_price<1, 0> : k_price<0, 0>;
+}
+
+hipError_t launch_ptimer_reduce(const Dev& d, int nslots, hipStream_t st) {
+    if (nslots > 0 && d.ptst) k_ptimer_reduce<<<nslots, 256, 0, st>>>(d);
+    return hipGetLastError();
 }
 
 hipError_t launch_init_rows(const Dev& d, const double* rhs, hipStream_t st) {
@@ -4971,6 +5298,9 @@ static bool use_spz(const Dev& d, int k_ub) {
     return d.csc && d.spos && 8.0 * (double)d.m * (double)k_ub > thr;
 }
 
+// CSC: sparse FTRAN / B^-1 rows once the bump exceeds Dev::spf_min positions
+static bool use_spf(const Dev& d, int k_ub) { return d.csc && d.spf_min > 0 && k_ub > d.spf_min; }
+
 // slack workgroups of the pricing launch for |Y| <= ny_ub
 static int slack_wgs(const Dev& d, int ny_ub) {
     return (int)cdiv(ny_ub > 0 ? ny_ub : 1, d.csc ? TILE_COLS : PRICE_THREADS);
@@ -4989,7 +5319,7 @@ static bool sweep_nt(double bytes) {
 }
 
 static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phase, hipStream_t st,
-                                     hipEvent_t ev0, hipEvent_t ev1) {
+                                     hipEvent_t ev0, hipEvent_t ev1, int tslot) {
     const int m = d.m;
     const double* tv = d.cS;
     if (phase == 1) {
@@ -5028,21 +5358,28 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phas
     const int nsw = slack_wgs(d, ny_ub);
     const unsigned grid = (d.csc ? ntiles + napply : (unsigned)d.ntiles + dnapply) + nsw;
     const bool nt = !d.csc && sweep_nt(8.0 * (double)ny_ub * (double)d.n);
+    // tslot >= 0: the timed variant (in-kernel stamps, k_ptimer_reduce)
+    const bool timed = tslot >= 0 && d.ptst && tslot < d.ptslots;
+    if (!timed) tslot = 0;
     if (ev0) {
         // profiling (ELP_PROFILE_EVENTS): events bound to the dispatch itself
         // (the CP's start / end timestamps of this launch, as a kernel trace
         // reports them; no marker packets between the kernels)
         if (d.csc)
-            hipExtLaunchKernelGGL(k_price_csc, dim3(grid), dim3(TILE_COLS), 0, st, ev0, ev1, 0, d, (int)napply,
-                                  (int)nb_minv, nsw);
+            hipExtLaunchKernelGGL(timed ? k_price_csc<true> : k_price_csc<false>, dim3(grid), dim3(TILE_COLS), 0, st,
+                                  ev0, ev1, 0, d, (int)napply, (int)nb_minv, nsw, tslot);
         else
-            hipExtLaunchKernelGGL(price_kernel(nt, d.tile_w), dim3(grid), dim3(PRICE_THREADS), 0, st, ev0, ev1, 0,
-                                  DEV_ARG(d), nsw, dapply, (int)dnapply, (int)dnb_minv);
+            hipExtLaunchKernelGGL(price_kernel(nt, d.tile_w, timed), dim3(grid), dim3(PRICE_THREADS), 0, st, ev0,
+                                  ev1, 0, DEV_ARG(d), nsw, dapply, (int)dnapply, (int)dnb_minv, tslot);
         return hipGetLastError();
     }
-    if (d.csc) k_price_csc<<<grid, TILE_COLS, 0, st>>>(d, (int)napply, (int)nb_minv, nsw);
-    else hipLaunchKernelGGL(price_kernel(nt, d.tile_w), dim3(grid), dim3(PRICE_THREADS), 0, st, DEV_ARG(d), nsw,
-                            dapply, (int)dnapply, (int)dnb_minv);
+    if (d.csc) {
+        if (timed) k_price_csc<true><<<grid, TILE_COLS, 0, st>>>(d, (int)napply, (int)nb_minv, nsw, tslot);
+        else k_price_csc<false><<<grid, TILE_COLS, 0, st>>>(d, (int)napply, (int)nb_minv, nsw, tslot);
+    } else {
+        hipLaunchKernelGGL(price_kernel(nt, d.tile_w, timed), dim3(grid), dim3(PRICE_THREADS), 0, st, DEV_ARG(d),
+                           nsw, dapply, (int)dnapply, (int)dnb_minv, tslot);
+    }
     return hipGetLastError();
 }
 
@@ -5139,13 +5476,14 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
 }
 
 hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStream_t st,
-                            hipEvent_t ev0, hipEvent_t ev1, int dslot) {
-    hipError_t e = launch_btran_price(d, k_ub, ny_ub, phase, st, ev0, ev1);
+                            hipEvent_t ev0, hipEvent_t ev1, int dslot, int tslot) {
+    hipError_t e = launch_btran_price(d, k_ub, ny_ub, phase, st, ev0, ev1, tslot);
     if (e != hipSuccess) return e;
     const int ntiles = d.ntiles, nsw = slack_wgs(d, ny_ub);
     const size_t lds = (size_t)k_ub * sizeof(double);
-    if (lds <= 48 * 1024 && !d.force_select) {  // fused select + bump FTRAN
-        const size_t ldsz = lds > 64 ? lds : 64;  // the timer workgroup reduces in it
+    const bool sp = use_spf(d, k_ub);
+    if ((sp || lds <= 48 * 1024) && !d.force_select) {  // fused select + bump FTRAN
+        const size_t ldsz = sp ? 64 : lds > 64 ? lds : 64;  // the timer workgroup reduces in it
         // + the timer workgroup, + the CSC column-scatter workgroup
         unsigned nrw = cdiv(k_ub > 0 ? k_ub : 1, 4);
         if (d.sel_cap > 0 && nrw > (unsigned)d.sel_cap) nrw = (unsigned)d.sel_cap;
@@ -5156,7 +5494,9 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
         // Minv row values per lane in registers: 8 (k <= 512), 10 (k <= 640: the
         // last 4 000 iterations of 10 000 x 500 000, k 529; 16 measured no faster
         // there, r01 -- fewer waves per SIMD), else the row is read after a_R
-        if (k_ub > 512 && k_ub <= 640)
+        if (sp)
+            k_select_ftran<8, true><<<g, 256, ldsz, st>>>(DEV_ARG(d), ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz, 0);
+        else if (k_ub > 512 && k_ub <= 640)
             k_select_ftran<10><<<g, 256, ldsz, st>>>(DEV_ARG(d), ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz, 0);
         else
             k_select_ftran<8><<<g, 256, ldsz, st>>>(DEV_ARG(d), ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz, 0);
@@ -5186,7 +5526,8 @@ static int dual_head(const Dev& d, int k_ub, int ny_ub, hipStream_t st) {
     const int lds_row = lds <= 48 * 1024;
     unsigned nrw = cdiv(k_ub > 0 ? k_ub : 1, 4);
     if (nrw > 1024) nrw = 1024;
-    k_dual_row<<<nrw, 256, lds_row ? lds : 0, st>>>(d, (int)nchz, lds_row);
+    const int sp = use_spf(d, k_ub) ? 1 : 0;
+    k_dual_row<<<nrw, 256, lds_row && !sp ? lds : 0, st>>>(d, (int)nchz, lds_row && !sp, sp);
     const int nsw = d.dslack ? slack_wgs(d, ny_ub) : 0;
     if (d.csc) k_dual_price_csc<<<d.ntiles + nsw, TILE_COLS, 0, st>>>(d, nsw, 0);
     else k_dual_price<<<d.ntiles + nsw, PRICE_THREADS, 0, st>>>(d, nsw, 0);
@@ -5236,10 +5577,10 @@ static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_co
     unsigned nrw = cdiv(k_ub > 0 ? k_ub : 1, 4);
     if (nrw > 1024) nrw = 1024;
     if (flip_col && !d.csc) k_dual_flip_col<<<cdiv(m > 0 ? m : 1, 256), 256, 0, st>>>(d);  // (CSC: k_dual_bfrt)
-    const bool spz = use_spz(d, k_ub);
+    const bool spz = use_spz(d, k_ub), sp = use_spf(d, k_ub);
     // CSC with the row-wise update: the flips' bump FTRAN inside k_select_ftran
-    // (dual = 2; a_R and a_F[R] side by side in LDS)
-    const bool fold_fs = spz && 2 * lds <= 64 * 1024 && !d.force_select;
+    // (dual = 2; a_R and a_F[R] side by side in LDS, or sparse lists: sp)
+    const bool fold_fs = spz && (sp || 2 * lds <= 64 * 1024) && !d.force_select;
     if (k_ub > 0 && !fold_fs) k_dual_flip_bump<<<nrw, 256, lds_row ? lds : 0, st>>>(d, lds_row);
     if (spz) {
         // (the row-wise x_B update runs inside k_ftran_zr_sp, below)
@@ -5250,12 +5591,14 @@ static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_co
         else k_dual_flip_apply<false><<<nrt + nbt, 512, 0, st>>>(d, (int)nrt);
     }
     // the entering column q (k_dual_bfrt's, candidate 0): a_R, alpha_S (+ staging)
-    if (fold_fs || (lds <= 48 * 1024 && !d.force_select)) {
-        const size_t ldsz = fold_fs ? (2 * lds > 64 ? 2 * lds : 64) : (lds > 64 ? lds : 64);
+    if (fold_fs || ((sp || lds <= 48 * 1024) && !d.force_select)) {
+        const size_t ldsz = sp ? 64 : fold_fs ? (2 * lds > 64 ? 2 * lds : 64) : (lds > 64 ? lds : 64);
         const int dual = fold_fs ? 2 : 1;
         const unsigned nqz = d.qz && !d.csc ? cdiv(m, 256 * QZ_PT) : 0;
         const unsigned g = nrw + nqz + (d.csc ? 1 : 0);
-        if (k_ub > 512 && k_ub <= 640)
+        if (sp)
+            k_select_ftran<8, true><<<g, 256, ldsz, st>>>(DEV_ARG(d), 1, 0, k_ub, 0, (int)nrw, (int)nqz, dual);
+        else if (k_ub > 512 && k_ub <= 640)
             k_select_ftran<10><<<g, 256, ldsz, st>>>(DEV_ARG(d), 1, 0, k_ub, 0, (int)nrw, (int)nqz, dual);
         else
             k_select_ftran<8><<<g, 256, ldsz, st>>>(DEV_ARG(d), 1, 0, k_ub, 0, (int)nrw, (int)nqz, dual);
@@ -5277,8 +5620,8 @@ hipError_t launch_warm_start(const Dev& d, const double* lo, const double* up, i
 }
 
 hipError_t launch_iteration_head(const Dev& d, int k_ub, int ny_ub, int phase, int rank,
-                                 hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
-    hipError_t e = launch_btran_price(d, k_ub, ny_ub, phase, st, ev0, ev1);
+                                 hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, int tslot) {
+    hipError_t e = launch_btran_price(d, k_ub, ny_ub, phase, st, ev0, ev1, tslot);
     if (e != hipSuccess) return e;
     k_select_local<<<1, 1024, 0, st>>>(d, d.ntiles, slack_wgs(d, ny_ub), rank);
     return hipGetLastError();

@@ -43,7 +43,7 @@ def test_abi_version_and_defaults():
     from easylp_amd._lib import ABI_VERSION, ElpControl, load
     _torch_first()
     lib = load()
-    assert lib.elp_abi_version() == ABI_VERSION == 5
+    assert lib.elp_abi_version() == ABI_VERSION == 6
     c = ElpControl()
     lib.elp_default_control(ctypes.byref(c))
     assert c.infinity == 1e30 and c.refactor_period == 250 and c.sync_every == 32

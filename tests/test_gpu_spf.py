@@ -1,0 +1,37 @@
+"""The CSC path's hypersparse products against the bump inverse (DESIGN.md 9,
+"sparse FTRAN"): alpha_S = Minv a_R and fS = Minv a_F[R] in the select kernel,
+rho_r = A[i, S] Minv in k_dual_row, from lane-bucketed lists of the operand's
+nonzeros (sparse_lane_chain: each lane's chain of the dense wave_dot over the
+nonzero terms only).  The library takes them once the bump exceeds
+ELP_SPF_MIN (512) positions; the fixtures here are far smaller, so the CSC
+parity tests run again in a child process with the threshold at 1 (every CSC
+iteration with k > 1 takes the sparse kernels) and the row-wise FTRAN-z forced
+(so the dual pivots fold fS into the select kernel from k_dual_bfrt's a_F[R]
+list) -- every trace must still be the oracle's bit for bit."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.mark.parametrize("spz", ["0", "16"], ids=["rowwise", "default-zr"])
+def test_csc_parity_with_sparse_ftran(spz):
+    env = dict(os.environ, ELP_SPF_MIN="1", ELP_SPZ_MIN_MB=spz)
+    cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", "-m", "gpu",
+           os.path.join(HERE, "test_gpu_csc.py"),
+           os.path.join(HERE, "test_gpu_dual.py") + "::test_dual_known_and_robust",
+           os.path.join(HERE, "test_gpu_dual.py") + "::test_dual_fuzz",
+           os.path.join(HERE, "test_gpu_dual.py") + "::test_dual_sparse_fixtures",
+           os.path.join(HERE, "test_gpu_dual.py") + "::test_dual_kkt_2000x10000_matches_oracle",
+           os.path.join(HERE, "test_gpu_fuzz.py") + "::test_fuzz_csc",
+           os.path.join(HERE, "test_gpu_fuzz.py") + "::test_fuzz_mip",
+           os.path.join(HERE, "test_gpu_mip.py") + "::test_reference_mips_gpu",
+           "-k", "not dense"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=os.path.dirname(HERE))
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-2000:])
+    assert " passed" in r.stdout
