@@ -638,6 +638,13 @@ static int alloc_all_body(elp_handle* h) {
         }();
         d.spf_min = h->csc && !h->lu && spf > 0 ? spf : 0;
     }
+    {  // one GPU: the dual phase's update deferred into the next iteration (A/B: ELP_DUAL_DEFER=0)
+        static const bool dd = [] {
+            const char* s = std::getenv("ELP_DUAL_DEFER");
+            return !(s && std::atoi(s) == 0);
+        }();
+        d.dual_defer = dd && h->comm.kind == 0 ? 1 : 0;
+    }
     // the mailbox carries the min-loc record only: with A not replicated the
     // entering column must travel, so that load uses the collective
     d.p2p = h->comm.p2p && h->replicated ? 1 : 0;
@@ -1973,13 +1980,16 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
         // a poll that just queues the next chunk (phase 2 running, no budget, cap,
         // refactor or time-limit stop due) leaves the last plan to the next chunk's
         // first pricing launch, as inside a chunk; any other poll may read the basis
-        const bool plain_next = c->status == ST_RUN && h->phase == 2 && c->iter < c->iter_stop &&
+        const bool ddefer = h->phase == 3 && h->comm.kind == 0 && h->d.dual_defer;
+        const bool plain_next = c->status == ST_RUN && (h->phase == 2 || ddefer) && c->iter < c->iter_stop &&
                                 c->iter < c->iter_limit && c->since_refactor < period && !(h->ctl.time_limit > 0);
-        if (c->plan_seq != c->applied_seq && !plain_next) {
-            // phase 2 defers each iteration's update into the next pricing launch:
-            // apply the last one now (phase 1 applied its plans in place)
+        if ((c->plan_seq != c->applied_seq || (ddefer && c->plan_seq != c->copy_seq)) && !plain_next) {
+            // phase 2 defers each iteration's update into the next pricing launch,
+            // the one-GPU dual phase into the next iteration's launches: apply the
+            // last one now (phase 1 and sharded dual ranks applied theirs in place)
             if (h->phase == 2) HIPCHK(launch_apply_pending(h->d, std::max(k0, c->k), h->st));
-            c->applied_seq = c->plan_seq;
+            if (ddefer) HIPCHK(launch_apply_pending(h->d, std::max(k0, c->k) + 1, h->st, true));
+            c->applied_seq = c->copy_seq = c->plan_seq;
             rc = push_ctl_fields(h);
             if (rc) return rc;
         }
@@ -2502,7 +2512,7 @@ static int reload_bounds_warm(elp_handle* h, const std::vector<double>& lo, cons
     c.price_bytes = c.iter_bytes = 0.0;
     c.price_passes = 0;
     c.plan.action = ACT_NONE;
-    c.plan_seq = c.applied_seq = 0;
+    c.plan_seq = c.applied_seq = c.copy_seq = 0;
     c.devex = 0;
     c.ddevex = h->ctl.pricing == ELP_PRICE_DEVEX;
     c.dv_valid = 0;

@@ -113,6 +113,9 @@ struct DevCtl {
     // select kernel marks it applied; the host applies a plan still pending at
     // a poll (k_update) -- see DESIGN.md "Iteration pipeline"
     int32_t plan_seq, applied_seq;
+    // the dual phase's deferred update (one GPU): the plan whose x_B / dual
+    // Devex / AS part k_dual_chuzr applied (its inverse part: applied_seq)
+    int32_t copy_seq, pad9;
     int64_t mb_epoch;  // xGMI mailbox: loads so far (seq = epoch << 40 | iteration + 1)
     // Devex pricing (elp_control.pricing): the last pivot as the next pricing
     // pass needs it -- entering reduced cost and weight, leaving variable;
@@ -317,6 +320,10 @@ struct Dev {
     unsigned long long* ptst;
     int32_t* ptgrid;
     int32_t ptcap, ptslots;
+    // one GPU, dual phase: k_ratio's plan applied during the next iteration
+    // (k_dual_chuzr, the pricing / ratio-test launches' trailing workgroups)
+    // instead of by a k_update launch (ELP_DUAL_DEFER=0: the launch)
+    int32_t dual_defer, dd_pad;
 };
 constexpr int AFL_SB = 1;    // afl: bucket starts [1, 66)
 constexpr int AFL_POS = 66;  // afl: positions [66, 66 + SPL)
@@ -369,7 +376,8 @@ hipError_t launch_iteration_head(const Dev& d, int k_ub, int ny_ub, int phase, i
                                  hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, int tslot = -1);
 hipError_t launch_select_global(const Dev& d, hipStream_t st);
 // phase 2, at a host poll: apply a plan the last iteration left pending
-hipError_t launch_apply_pending(const Dev& d, int k_ub, hipStream_t st);
+// dual: the dual phase's deferred plan (the parts not applied yet, AR included)
+hipError_t launch_apply_pending(const Dev& d, int k_ub, hipStream_t st, bool dual = false);
 // replicated A: global min-loc + a_R + bump FTRAN in one launch (false: the
 // bump is too large for it; use select_global + select_finish + tail(bump_ftran))
 bool launch_select_xftran(const Dev& d, int k_ub, hipStream_t st, hipError_t* err);

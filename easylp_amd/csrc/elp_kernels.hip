@@ -3524,11 +3524,124 @@ DEV void apply_plan(const Dev& d, const Plan& P, int blk, int nb, int nb_minv, b
                do_ar);
 }
 
+// ---- the dual phase's deferred update (one GPU, Dev::dual_defer; DESIGN.md
+// 2.3).  k_ratio's plan of iteration t is applied during iteration t + 1: x_B,
+// the dual Devex weights, the AS column (dense: AR rows) in k_dual_chuzr, entry
+// by entry by the thread that then scores the entry (dual_copy_entry); MinvT in
+// trailing workgroups of the pricing launch and Minv in those of the ratio-test
+// launch (apply_minv_part); k_dual_row in between reads the new inverse on the
+// fly (minv_new: the update's own arithmetic, so the same bits).  copy_seq and
+// applied_seq mark the two parts applied (k_dual_row, the select kernel).
+DEV bool copy_pending(const DevCtl* c) {
+    return c->plan_seq != c->copy_seq && c->plan.action == ACT_PIVOT && c->status != ST_NUMFAIL;
+}
+DEV bool minv_pending(const DevCtl* c) {
+    return c->plan_seq != c->applied_seq && c->plan.action == ACT_PIVOT && c->plan.pcase != PC_E &&
+           c->status != ST_NUMFAIL;
+}
+// part 0: Minv, part 1: MinvT -- elements t0, t0 + tstride, ... of that half
+DEV void apply_minv_part(const Dev& d, const Plan& P, int part, int64_t t0, int64_t tstride) {
+    const int k = P.k_old;
+    const int kk = P.pcase == PC_B ? k + 1 : P.pcase == PC_C ? k - 1 : k;
+    const int64_t nel = (int64_t)kk * kk;
+    if (nel == 0 || t0 >= nel) return;
+    if (part == 0) apply_minv_half<false, MINV_U>(d, P, t0, nel, tstride, 0, kk);
+    else apply_minv_half<true, MINV_U>(d, P, nel + t0, 2 * nel, tstride, nel, kk);
+}
+// the dual Devex weight and x of the variable now basic at entry e (row e < m,
+// else bump position e - m of the new basis) -- apply_copy's arithmetic, per
+// entry: every basic variable but the entering one takes max(w, (alpha / a_rq)^2
+// w_r) from the alpha of its old entry (case C: position b's from alS[last]);
+// the entering one max(w_r / a_rq^2, 1); reset: every weight 1 (*wout = 1)
+DEV void dual_copy_entry(const Dev& d, const Plan& P, int e, int k_new, double* wout) {
+    const int m = d.m;
+    const double step = P.step, sg = P.sig;
+    const double wr = P.dwr, arq = P.darq;
+    double wq = wr / (arq * arq);
+    if (wq < 1.0) wq = 1.0;
+    if (wq > DEVEX_WMAX) wq = DEVEX_WMAX;
+    const bool reset = wq > DEVEX_RESET;
+    int var = -1;
+    double ae = 0.0;
+    if (e < m) {
+        const int t = e, u = d.cover[t];
+        if (t == P.i0) d.xr[t] = P.xq;
+        else if (t != P.lrow && u >= 0) d.xr[t] = fma(-step, sg * d.alU[t], d.xr[t]);
+        var = u;
+        if (u >= 0 && u != P.q) ae = d.alU[t];
+    } else if (e - m < k_new) {
+        const int p = e - m;
+        const bool moved = P.pcase == PC_C && p == P.b;  // (b != last: the last position moved to b)
+        if ((P.pcase == PC_A && p == P.lpos) || (P.pcase == PC_B && p == P.k_old)) d.xs[p] = P.xq;
+        else if (moved) d.xs[p] = fma(-step, sg * d.alS[P.last], d.xs[P.last]);
+        else d.xs[p] = fma(-step, sg * d.alS[p], d.xs[p]);
+        var = d.Sl[p];
+        if (var != P.q) ae = moved ? d.alS[P.last] : d.alS[p];
+    }
+    *wout = -1.0;  // (not updated: read d.ddw)
+    if (!P.dual || var < 0) return;
+    if (reset) {
+        *wout = 1.0;
+    } else if (var == P.q) {
+        d.ddw[var] = wq;
+        *wout = wq;
+    } else {
+        const double r = ae / arq;
+        double wn = (r * r) * wr;
+        if (wn > DEVEX_WMAX) wn = DEVEX_WMAX;
+        const double w0 = d.ddw[var];
+        const double w = wn > w0 ? wn : w0;
+        if (wn > w0) d.ddw[var] = wn;
+        *wout = w;
+    }
+}
+// the rest of the copy part, strided over the launch: the AS column (A, B: the
+// entering column at its position; C: the last column moved to b), AR rows
+// (dense), every dual Devex weight 1 on a reset
+DEV void dual_copy_rest(const Dev& d, const Plan& P, int64_t t0, int64_t tstride) {
+    const int64_t m = d.m;
+    const int k = P.k_old;
+    if (P.pcase == PC_A || P.pcase == PC_B) {
+        const int pos = P.pcase == PC_A ? P.p : k;
+        const double* qc = qcolumn(d, P.q);
+        for (int64_t t = t0; t < m; t += tstride) d.AS[(size_t)pos * m + t] = qcol_at(d, qc, P.q, t);
+    } else if (P.pcase == PC_C && P.b != P.last) {
+        for (int64_t t = t0; t < m; t += tstride) d.AS[(size_t)P.b * m + t] = d.AS[(size_t)P.last * m + t];
+    }
+    if (!d.csc && (P.y_rm_slot >= 0 || P.y_ap_slot >= 0)) {
+        for (int64_t j = t0; j < d.n; j += tstride) {
+            if (P.y_rm_slot >= 0 && P.y_rm_slot != P.y_rm_last)
+                d.AR[ar_at(d, P.y_rm_slot, j)] = d.AR[ar_at(d, P.y_rm_last, j)];
+            if (P.y_ap_slot >= 0) d.AR[ar_at(d, P.y_ap_slot, j)] = a_row(d, P.y_ap_row, j);
+        }
+    }
+    if (P.dual) {
+        double wq = P.dwr / (P.darq * P.darq);
+        if (wq < 1.0) wq = 1.0;
+        if (wq > DEVEX_WMAX) wq = DEVEX_WMAX;
+        if (wq > DEVEX_RESET)
+            for (int64_t t = t0; t < (int64_t)d.N + m; t += tstride) d.ddw[t] = 1.0;
+    }
+}
+
 // Standalone update.  mode 0 (phase 1): the plan k_ratio just made, AR included.
 // mode 1 (phase 2, host poll): a deferred plan still pending; its AR rows were
-// copied by k_ratio already.
+// copied by k_ratio already.  mode 2 (the dual phase's deferred plan at a host
+// poll): the parts k_dual_chuzr / the trailing workgroups have not applied.
 __global__ void __launch_bounds__(256) k_update(Dev d, int nb_minv, int mode) {
     const DevCtl* c = d.ctl;
+    if (mode == 2) {
+        const bool cp = copy_pending(c), mp = minv_pending(c);
+        const Plan P = c->plan;
+        const int blk = blockIdx.x, nb = gridDim.x;
+        if (blk < nb_minv) {
+            if (mp) apply_minv(d, P, (int64_t)blk * blockDim.x + threadIdx.x, (int64_t)nb_minv * blockDim.x);
+        } else if (cp) {
+            apply_copy(d, P, (int64_t)(blk - nb_minv) * blockDim.x + threadIdx.x,
+                       (int64_t)(nb - nb_minv) * blockDim.x, true);
+        }
+        return;
+    }
     if (mode == 1 && !plan_pending(c)) return;
     const Plan P = c->plan;
     if (P.action == ACT_NONE || c->status == ST_NUMFAIL) return;
@@ -4079,13 +4192,22 @@ DEV ChzRec block_best_chz(ChzRec r, int bland, ChzRec* lds) {
 }
 
 // CHUZR partials: one basic entry per thread (covered rows, then bump positions)
-__global__ void __launch_bounds__(256) k_dual_chuzr(Dev d) {
+// defer (Dev::dual_defer): first the last plan's x_B / dual Devex / AS part --
+// each thread updates the entry it scores (dual_copy_entry), the AS / AR
+// copies and a weight reset strided over the launch -- whatever the status
+__global__ void __launch_bounds__(256) k_dual_chuzr(Dev d, int defer) {
     __shared__ ChzRec red[256];
     const DevCtl* c = d.ctl;
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    double wnew = -1.0;  // the entry's updated dual Devex weight (-1: read ddw)
+    if (defer && copy_pending(c)) {
+        const Plan P = c->plan;
+        dual_copy_entry(d, P, e, c->k, &wnew);
+        dual_copy_rest(d, P, e, (int64_t)gridDim.x * 256);
+    }
     if (c->status != ST_RUN) return;
     const int m = d.m, k = c->k, bland = c->bland, dvx = c->ddevex;
     const double ptol = c->tol_primal;
-    const int e = blockIdx.x * 256 + threadIdx.x;
     ChzRec r;
     chz_none(r);
     int var = -1;
@@ -4123,7 +4245,7 @@ __global__ void __launch_bounds__(256) k_dual_chuzr(Dev d) {
             r.x = x;
             r.beta = beta;
             r.s = sd;
-            r.score = dvx ? (delta * delta) / d.ddw[var] : delta;
+            r.score = dvx ? (delta * delta) / (wnew >= 0.0 ? wnew : d.ddw[var]) : delta;
         }
     }
     r = block_best_chz<256>(r, bland, red);
@@ -4135,15 +4257,57 @@ __global__ void __launch_bounds__(256) k_dual_chuzr(Dev d) {
 // Minv row p for bump position p; -sigma (A[i,S] Minv)_c for the slack covering
 // row i (the oracle's row_times_minv in wave order).  Written in position order
 // (rhoR) and on the Y slots (rr, the dense sweep's operand).
+// lane_chain / sparse_lane_chain over x(j) computed by a functor (the deferred
+// update's new inverse, minv_new)
+template <class F>
+DEV double lane_chain_f(F x, const double* y, int len) {
+    const int lane = threadIdx.x & 63;
+    double acc = 0.0;
+    for (int j0 = lane; j0 < len; j0 += 64 * 8) {
+        double v[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = x(min(j0 + 64 * t, len - 1));
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            if (j0 + 64 * t < len) acc = fma(v[t], y[j0 + 64 * t], acc);
+    }
+    return acc;
+}
+template <class F>
+DEV double sparse_lane_chain_f(F x, const int* lpos, const double* lval, const int* lsb) {
+    const int lane = threadIdx.x & 63;
+    const int s = lsb[lane], e = lsb[lane + 1];
+    double acc = 0.0;
+    for (int t0 = s; t0 < e; t0 += 4) {
+        double xv[4], vv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = t0 + u < e ? t0 + u : e - 1;
+            xv[u] = x(lpos[t]);
+            vv[u] = lval[t];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (t0 + u < e) acc = fma(xv[u], vv[u], acc);
+    }
+    return acc;
+}
+
 // sp (CSC, large bump): A[i, S] from row i's nonzeros in basic columns (CSR +
 // spos) as a sparse list, rho_c = sparse_lane_chain over row c of MinvT (the
 // dense chain's bits; a row with more than SPL entries takes the dense walk)
-__global__ void __launch_bounds__(256) k_dual_row(Dev d, int nchz, int lds_row, int sp) {
+// defer (Dev::dual_defer): the last plan's inverse update is still pending --
+// rho_r reads the new inverse through minv_new -- and k_dual_chuzr applied its
+// copy part (copy_seq)
+__global__ void __launch_bounds__(256) k_dual_row(Dev d, int nchz, int lds_row, int sp, int defer) {
     extern __shared__ __attribute__((aligned(16))) double asrow_lds[];  // [k]: A[i, S]
     __shared__ ChzRec red[256];
     __shared__ int s_pos[SPL], s_key[SPL], s_sb[72], s_scan[4];
     __shared__ double s_val[SPL];
     DevCtl* c = d.ctl;
+    const bool pend = defer && minv_pending(c);
+    const Plan P = c->plan;
+    if (defer && blockIdx.x == 0 && threadIdx.x == 0) c->copy_seq = c->plan_seq;
     if (c->status != ST_RUN) return;
     const int m = d.m, k = c->k, bland = c->bland;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -4175,7 +4339,7 @@ __global__ void __launch_bounds__(256) k_dual_row(Dev d, int nchz, int lds_row, 
         c->dr_w = d.ddw[r.var];
         c->dr_xsig = xsig;
     }
-    double* asrow = lds_row ? asrow_lds : d.vrow;  // (huge bumps: every workgroup writes the same values)
+    double* asrow = lds_row ? asrow_lds : d.zz;  // (huge bumps: every workgroup writes the same values)
     bool spl = false;
     if (xrow >= 0 && sp) {
         const int64_t t0 = d.rptr[xrow], t1 = d.rptr[xrow + 1];
@@ -4200,12 +4364,19 @@ __global__ void __launch_bounds__(256) k_dual_row(Dev d, int nchz, int lds_row, 
     for (int cc = blockIdx.x * 4 + (tid >> 6); cc < k; cc += gridDim.x * 4) {
         double v;
         if (xrow >= 0) {
-            const double* mrow = d.MinvT + (size_t)cc * d.ldm;
-            double acc = spl ? sparse_lane_chain(mrow, s_pos, s_val, s_sb) : lane_chain(mrow, asrow, k);
+            double acc;
+            if (pend) {  // row cc of the new MinvT: element (q, cc) of the new Minv
+                const OldM oT{d.MinvT, (size_t)d.ldm, true};
+                auto xf = [&](int q) { return minv_new(d, P, q, cc, oT); };
+                acc = spl ? sparse_lane_chain_f(xf, s_pos, s_val, s_sb) : lane_chain_f(xf, asrow, k);
+            } else {
+                const double* mrow = d.MinvT + (size_t)cc * d.ldm;
+                acc = spl ? sparse_lane_chain(mrow, s_pos, s_val, s_sb) : lane_chain(mrow, asrow, k);
+            }
             acc = wave_tree(acc);
             v = -(xsig * acc);
         } else {
-            v = d.Minv[(size_t)lrp * d.ldm + cc];
+            v = pend ? minv_new(d, P, lrp, cc, OldM{d.Minv, (size_t)d.ldm, false}) : d.Minv[(size_t)lrp * d.ldm + cc];
         }
         if (lane == 0) {
             d.rhoR[cc] = v;
@@ -4350,10 +4521,17 @@ DEV void dual_slacks(const Dev& d, int region, int s, int nsw, int* wcnt, int wa
 // Grid: [nsw slack workgroups][ntiles tiles].
 // warm != 0 (MIP node warm start): the same pass for d_j alone (rho = 0), each
 // nonbasic column re-placed by warm_fix instead of a candidate
-__global__ void __launch_bounds__(PRICE_THREADS) k_dual_price(Dev d, int nsw, int warm) {
+// (+ napply trailing workgroups: the deferred plan's MinvT update, dual_defer)
+__global__ void __launch_bounds__(PRICE_THREADS) k_dual_price(Dev d, int nsw, int warm, int napply) {
     __shared__ double pd[PRICE_SPLIT][TILE_COLS], pa[PRICE_SPLIT][TILE_COLS];
     __shared__ int wcnt[PRICE_SPLIT];
     const DevCtl* c = d.ctl;
+    if (napply > 0 && (int)blockIdx.x >= (int)gridDim.x - napply) {
+        if (minv_pending(c))
+            apply_minv_part(d, c->plan, 1, (int64_t)(blockIdx.x - (gridDim.x - napply)) * blockDim.x + threadIdx.x,
+                            (int64_t)napply * blockDim.x);
+        return;
+    }
     if (c->status != ST_RUN) return;
     if ((int)blockIdx.x < nsw) {
         dual_slacks<PRICE_THREADS>(d, d.ntiles + blockIdx.x, blockIdx.x, nsw, wcnt, warm);
@@ -4435,9 +4613,15 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_dual_price(Dev d, int nsw, in
 // CSC pivot row + pricing: one column chain per thread over its nonzeros in
 // ascending rows with the dense y and rho (rho_i from the bump positions
 // through rpos, sigma on a covered leaving row)
-__global__ void __launch_bounds__(TILE_COLS) k_dual_price_csc(Dev d, int nsw, int warm) {
+__global__ void __launch_bounds__(TILE_COLS) k_dual_price_csc(Dev d, int nsw, int warm, int napply) {
     __shared__ int wcnt[TILE_COLS / 64];
     const DevCtl* c = d.ctl;
+    if (napply > 0 && (int)blockIdx.x >= (int)gridDim.x - napply) {
+        if (minv_pending(c))
+            apply_minv_part(d, c->plan, 1, (int64_t)(blockIdx.x - (gridDim.x - napply)) * blockDim.x + threadIdx.x,
+                            (int64_t)napply * blockDim.x);
+        return;
+    }
     if (c->status != ST_RUN) return;
     if ((int)blockIdx.x < nsw) {
         dual_slacks<TILE_COLS>(d, d.ntiles + blockIdx.x, blockIdx.x, nsw, wcnt, warm);
@@ -4748,6 +4932,7 @@ DEV void bfrt_flip_column(const Dev& d, int nflip, int k) {
 
 // gathered: P = world ranks' packed records in drecv (rank order) instead of
 // this launch's regions
+// (workgroups 1 .. gridDim.x - 1: the deferred plan's Minv update, dual_defer)
 __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gathered, int reg_ok) {
     __shared__ double s_bun[2 * BF_BUN];
     __shared__ int scan_lds[BF_NT / 64];
@@ -4755,6 +4940,12 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     __shared__ int s_int[4];
     __shared__ double s_dbl[2];
     DevCtl* c = d.ctl;
+    if (blockIdx.x > 0) {
+        if (minv_pending(c))
+            apply_minv_part(d, c->plan, 0, (int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x,
+                            (int64_t)(gridDim.x - 1) * blockDim.x);
+        return;
+    }
     if (c->status != ST_RUN) return;
     const int tid = threadIdx.x;
     const int bland = c->bland;
@@ -5383,16 +5574,20 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phas
     return hipGetLastError();
 }
 
-hipError_t launch_apply_pending(const Dev& d, int k_ub, hipStream_t st) {
+hipError_t launch_apply_pending(const Dev& d, int k_ub, hipStream_t st, bool dual) {
     unsigned nb_minv, nb;
-    update_grid(d, k_ub, false, &nb_minv, &nb);
-    k_update<<<nb, 256, 0, st>>>(d, (int)nb_minv, 1);
+    update_grid(d, k_ub, dual, &nb_minv, &nb);
+    k_update<<<nb, 256, 0, st>>>(d, (int)nb_minv, dual ? 2 : 1);
     return hipGetLastError();
 }
 
 hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t st, bool bump_ftran,
                                  int dslot, int qz) {
     const int m = d.m;
+    // phase 3: the dual phase (k_update applies its plan at once); 4: the dual
+    // phase with the plan deferred into the next iteration (Dev::dual_defer)
+    const bool dskip = phase == 4;
+    if (phase >= 3) phase = 3;
     if (bump_ftran && k_ub > 0) k_ftran_bump<<<cdiv(k_ub, 4), 256, 0, st>>>(d, d.aR, d.alS, 1);
     // CSC with a large bump: FTRAN-z from the rows of A (k_ftran_zr_sp: 64-row
     // tiles, 64-position bump tiles); else k_ftran_zr's 32-row tiles over AS
@@ -5467,7 +5662,7 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
                                                                          defer, (int)nmain, k_ub, dslot,
                                                                          nrt + nbt * zw);
     }
-    if (!defer) {
+    if (!defer && !dskip) {
         unsigned nb_minv, nb;
         update_grid(d, k_ub, true, &nb_minv, &nb);
         k_update<<<nb, 256, 0, st>>>(d, (int)nb_minv, 0);
@@ -5518,23 +5713,39 @@ hipError_t launch_dual_init_rows(const Dev& d, hipStream_t st) {
 
 // CHUZR, rho_r and the pivot row + pricing of this shard's columns (+ the
 // slack candidates where d.dslack); returns the candidate regions' count
-static int dual_head(const Dev& d, int k_ub, int ny_ub, hipStream_t st) {
+// the deferred inverse update's share of a launch (dual_defer): workgroups of
+// `threads` for one half (Minv or MinvT) of a bump up to k_ub + 1 positions,
+// MINV_U elements per thread per pass, at most `cap`
+static unsigned defer_wgs(int k_ub, int threads, unsigned cap) {
+    const int64_t kk = (int64_t)(k_ub + 1) * (k_ub + 1);
+    unsigned nb = cdiv(kk, (int64_t)threads * 4);
+    return nb > cap ? cap : nb;
+}
+
+// defer: the one-GPU dual_defer flow (the last plan applied by this
+// iteration's CHUZR and trailing workgroups, no k_update); 0 on sharded ranks
+static int dual_head(const Dev& d, int k_ub, int ny_ub, hipStream_t st, int defer = 0) {
     const int m = d.m;
     const unsigned nchz = cdiv((int64_t)m + k_ub, 256);
-    k_dual_chuzr<<<nchz, 256, 0, st>>>(d);
+    k_dual_chuzr<<<nchz, 256, 0, st>>>(d, defer);
     const size_t lds = (size_t)k_ub * sizeof(double);
     const int lds_row = lds <= 48 * 1024;
     unsigned nrw = cdiv(k_ub > 0 ? k_ub : 1, 4);
     if (nrw > 1024) nrw = 1024;
     const int sp = use_spf(d, k_ub) ? 1 : 0;
-    k_dual_row<<<nrw, 256, lds_row && !sp ? lds : 0, st>>>(d, (int)nchz, lds_row && !sp, sp);
+    k_dual_row<<<nrw, 256, lds_row && !sp ? lds : 0, st>>>(d, (int)nchz, lds_row && !sp, sp, defer);
     const int nsw = d.dslack ? slack_wgs(d, ny_ub) : 0;
-    if (d.csc) k_dual_price_csc<<<d.ntiles + nsw, TILE_COLS, 0, st>>>(d, nsw, 0);
-    else k_dual_price<<<d.ntiles + nsw, PRICE_THREADS, 0, st>>>(d, nsw, 0);
+    if (d.csc) {
+        const int na = defer ? (int)defer_wgs(k_ub, TILE_COLS, 8192) : 0;
+        k_dual_price_csc<<<d.ntiles + nsw + na, TILE_COLS, 0, st>>>(d, nsw, 0, na);
+    } else {
+        const int na = defer ? (int)defer_wgs(k_ub, PRICE_THREADS, 4096) : 0;
+        k_dual_price<<<d.ntiles + nsw + na, PRICE_THREADS, 0, st>>>(d, nsw, 0, na);
+    }
     return d.ntiles + nsw;
 }
 
-static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_col = true);
+static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_col = true, int defer = 0);
 
 hipError_t launch_dual_iteration_head(const Dev& d, int k_ub, int ny_ub, hipStream_t st) {
     const int nreg = dual_head(d, k_ub, ny_ub, st);
@@ -5563,14 +5774,16 @@ hipError_t launch_dual_iteration_finish(const Dev& d, int k_ub, hipStream_t st) 
 }
 
 hipError_t launch_dual_iteration(const Dev& d, int k_ub, int ny_ub, hipStream_t st) {
-    const int nreg = dual_head(d, k_ub, ny_ub, st);
-    k_dual_bfrt<<<1, BF_NT, 0, st>>>(d, nreg, 0, bfrt_reg());
-    return dual_tail(d, k_ub, st);
+    const int defer = d.dual_defer ? 1 : 0;
+    const int nreg = dual_head(d, k_ub, ny_ub, st, defer);
+    // (dual_defer: + the Minv half of the last plan's update beside the ratio test)
+    k_dual_bfrt<<<1 + (defer ? defer_wgs(k_ub, BF_NT, 1024) : 0), BF_NT, 0, st>>>(d, nreg, 0, bfrt_reg());
+    return dual_tail(d, k_ub, st, true, defer);
 }
 
 // the bound flips' FTRAN and x_B update, then FTRAN of a_q and the pivot
 // (flip_col false: a_F was formed by the column-only shards' chain already)
-static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_col) {
+static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_col, int defer) {
     const int m = d.m;
     const size_t lds = (size_t)k_ub * sizeof(double);
     const int lds_row = lds <= 48 * 1024;
@@ -5602,10 +5815,10 @@ static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_co
             k_select_ftran<10><<<g, 256, ldsz, st>>>(DEV_ARG(d), 1, 0, k_ub, 0, (int)nrw, (int)nqz, dual);
         else
             k_select_ftran<8><<<g, 256, ldsz, st>>>(DEV_ARG(d), 1, 0, k_ub, 0, (int)nrw, (int)nqz, dual);
-        return launch_iteration_tail(d, k_ub, 3, st, false, 0, nqz > 0 ? 1 : 0);
+        return launch_iteration_tail(d, k_ub, defer ? 4 : 3, st, false, 0, nqz > 0 ? 1 : 0);
     }
     k_select<<<1, 1024, 0, st>>>(d, 1, 0, 1);
-    return launch_iteration_tail(d, k_ub, 3, st, true, 0);
+    return launch_iteration_tail(d, k_ub, defer ? 4 : 3, st, true, 0);
 }
 
 hipError_t launch_warm_start(const Dev& d, const double* lo, const double* up, int k, int ny, hipStream_t st) {
@@ -5614,8 +5827,8 @@ hipError_t launch_warm_start(const Dev& d, const double* lo, const double* up, i
     const hipError_t e = launch_btran_exact(d, k, st);  // y = B^-T c_B (the real costs)
     if (e != hipSuccess) return e;
     const int nsw = slack_wgs(d, ny);
-    if (d.csc) k_dual_price_csc<<<d.ntiles + nsw, TILE_COLS, 0, st>>>(d, nsw, 1);
-    else k_dual_price<<<d.ntiles + nsw, PRICE_THREADS, 0, st>>>(d, nsw, 1);
+    if (d.csc) k_dual_price_csc<<<d.ntiles + nsw, TILE_COLS, 0, st>>>(d, nsw, 1, 0);
+    else k_dual_price<<<d.ntiles + nsw, PRICE_THREADS, 0, st>>>(d, nsw, 1, 0);
     return hipGetLastError();
 }
 
