@@ -4527,9 +4527,11 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_dual_price(Dev d, int nsw, in
     __shared__ int wcnt[PRICE_SPLIT];
     const DevCtl* c = d.ctl;
     if (napply > 0 && (int)blockIdx.x >= (int)gridDim.x - napply) {
-        if (minv_pending(c))
-            apply_minv_part(d, c->plan, 1, (int64_t)(blockIdx.x - (gridDim.x - napply)) * blockDim.x + threadIdx.x,
+        if (minv_pending(c)) {
+            const Plan P = c->plan;
+            apply_minv_part(d, P, 1, (int64_t)(blockIdx.x - (gridDim.x - napply)) * blockDim.x + threadIdx.x,
                             (int64_t)napply * blockDim.x);
+        }
         return;
     }
     if (c->status != ST_RUN) return;
@@ -4617,9 +4619,11 @@ __global__ void __launch_bounds__(TILE_COLS) k_dual_price_csc(Dev d, int nsw, in
     __shared__ int wcnt[TILE_COLS / 64];
     const DevCtl* c = d.ctl;
     if (napply > 0 && (int)blockIdx.x >= (int)gridDim.x - napply) {
-        if (minv_pending(c))
-            apply_minv_part(d, c->plan, 1, (int64_t)(blockIdx.x - (gridDim.x - napply)) * blockDim.x + threadIdx.x,
+        if (minv_pending(c)) {
+            const Plan P = c->plan;
+            apply_minv_part(d, P, 1, (int64_t)(blockIdx.x - (gridDim.x - napply)) * blockDim.x + threadIdx.x,
                             (int64_t)napply * blockDim.x);
+        }
         return;
     }
     if (c->status != ST_RUN) return;
@@ -4941,9 +4945,11 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     __shared__ double s_dbl[2];
     DevCtl* c = d.ctl;
     if (blockIdx.x > 0) {
-        if (minv_pending(c))
-            apply_minv_part(d, c->plan, 0, (int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x,
+        if (minv_pending(c)) {
+            const Plan P = c->plan;
+            apply_minv_part(d, P, 0, (int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x,
                             (int64_t)(gridDim.x - 1) * blockDim.x);
+        }
         return;
     }
     if (c->status != ST_RUN) return;
