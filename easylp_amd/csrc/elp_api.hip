@@ -27,7 +27,6 @@
 #include "../../include/easylp_hip.h"
 #include "elp_comm.h"
 #include "elp_internal.h"
-#include "elp_lu_factor.h"
 
 using namespace elp;
 
@@ -140,15 +139,7 @@ struct elp_handle {
     // the device descriptor and its buffers (grown as needed within a load, freed by
     // every load: free_dev)
     int64_t kcap = 0;  // bump capacity: AS m x kcap, Minv / MinvT kcap x kcap (grown at polls)
-    bool lu = false;
-    LuDev ld{};
-    LuFactors luf;
-    std::vector<int64_t> lu_cp;
-    std::vector<int32_t> lu_ri;
-    std::vector<double> lu_cv, lu_asgn;
-    std::vector<void*> lub;
-    std::vector<size_t> lubcap;
-    int64_t lu_nnz_max = 0;
+
     bool dual_used = false;  // the last load's phase 1 is the dual simplex (phase 3)
     std::vector<double> mip_x;   // branch and bound: the incumbent (elp_get_solution)
 };
@@ -231,13 +222,6 @@ static void free_dev(elp_handle* h, bool keep_big = false) {
     if (h->warm_lo) (void)hipFree(h->warm_lo);
     if (h->warm_up) (void)hipFree(h->warm_up);
     h->warm_lo = h->warm_up = nullptr;
-    for (void*& p : h->lub)
-        if (p) {
-            (void)hipFree(p);
-            p = nullptr;
-        }
-    h->lubcap.assign(h->lub.size(), 0);
-    h->ld = LuDev{};
     h->A_owned = nullptr;
     h->d_flag = nullptr;
     h->w_cap = 0;  // (W0 / W1 went with the rest)
@@ -636,7 +620,7 @@ static int alloc_all_body(elp_handle* h) {
             const char* s = std::getenv("ELP_SPF_MIN");
             return s ? std::atoi(s) : 512;
         }();
-        d.spf_min = h->csc && !h->lu && spf > 0 ? spf : 0;
+        d.spf_min = h->csc && spf > 0 ? spf : 0;
     }
     {  // one GPU: the dual phase's update deferred into the next iteration (A/B: ELP_DUAL_DEFER=0)
         static const bool dd = [] {
@@ -666,8 +650,8 @@ static int alloc_all_body(elp_handle* h) {
     d.arcap = h->ar_rows;
     A(dalloc(&d.AR, (size_t)h->ar_rows * (size_t)d.ldr));
     // the explicit bump inverse's m x m buffers (none with the sparse LU)
-    const size_t msq = h->lu ? 1 : (size_t)h->kcap * (size_t)h->kcap;
-    A(dalloc(&d.AS, h->lu ? 1 : (size_t)mm * (size_t)h->kcap));
+    const size_t msq = (size_t)h->kcap * (size_t)h->kcap;
+    A(dalloc(&d.AS, (size_t)mm * (size_t)h->kcap));
     A(dalloc(&d.Minv, msq));
     A(dalloc(&d.MinvT, msq));
     A(dalloc(&d.cS, mm));
@@ -708,7 +692,7 @@ static int alloc_all_body(elp_handle* h) {
     A(dalloc(&d.alS, mm));
     A(dalloc(&d.alU, mm));
     A(dalloc(&d.zz, mm));
-    A(dalloc(&d.zpart, h->lu ? 1 : (size_t)(mm + 64) * (size_t)((h->kcap + ZCHUNK - 1) / ZCHUNK + 1)));
+    A(dalloc(&d.zpart, (size_t)(mm + 64) * (size_t)((h->kcap + ZCHUNK - 1) / ZCHUNK + 1)));
     A(dalloc(&d.vrow, mm));
     A(dalloc(&d.vvec, mm));
     A(dalloc(&d.colA, mm));
@@ -734,7 +718,7 @@ static int alloc_all_body(elp_handle* h) {
     A(dalloc(&d.pstamp, 2 * ((size_t)d.ntiles + (size_t)(mm / 128 + 1) + 3072 + 64)));
 #endif
     if (h->csc) A(dalloc(&d.qcol, mm));
-    if (h->csc && !h->lu) A(dalloc(&d.spos, (size_t)(n > 0 ? n : 1)));  // (the sparse FTRAN-z's column -> position)
+    if (h->csc) A(dalloc(&d.spos, (size_t)(n > 0 ? n : 1)));  // (the sparse FTRAN-z's column -> position)
     if (!h->csc && !std::getenv("ELP_NO_QZ")) A(dalloc(&d.qz, mm));  // (dense only; ELP_NO_QZ: A/B switch)
     if (ELP_DIAG && std::getenv("ELP_STAMPS")) {  // (diagnostic builds)
         A(dalloc(&d.dstamp, DSTAMP_STRIDE * 64));
@@ -753,7 +737,7 @@ static int alloc_all_body(elp_handle* h) {
     // One GPU, or column-sharded ranks holding all of A (the flipped and the
     // entering columns are read from the replicated copy); the ratio test sees
     // every rank's candidates: up to N + m of them
-    if (!h->lu && (!d.sharded || !h->csc)) {
+    if (!d.sharded || !h->csc) {
         const int64_t Ng = h->n;
         d.dregs = d.ntiles + (int32_t)((mm + TILE_COLS - 1) / TILE_COLS) + 2;
         d.dchzn = (int32_t)((2 * mm + 255) / 256 + 2);
@@ -835,7 +819,6 @@ static int ensure_ar(elp_handle* h, int64_t rows) {
 // at a poll): AS keeps its first k columns (ld m), Minv / MinvT their k x k
 // block (ld kcap -> the new kcap); zpart is scratch.
 static int ensure_k(elp_handle* h, int64_t need) {
-    if (h->lu) return 0;
     const int64_t mm = std::max<int64_t>(h->m, 1);
     need = std::min<int64_t>(need, mm);
     if (need <= h->kcap) return 0;
@@ -1083,7 +1066,7 @@ static int simplex_type(const elp_handle* h) {
     return h->ctl.simplex == 0 ? ELP_SIMPLEX_DEFAULT : h->ctl.simplex;
 }
 static bool dual_phase1(const elp_handle* h) {
-    return simplex_type(h) == ELP_SIMPLEX_DUAL_PRIMAL && !h->lu && h->d.dcand &&
+    return simplex_type(h) == ELP_SIMPLEX_DUAL_PRIMAL && h->d.dcand &&
            (h->comm.kind == 0 || (!h->csc && h->d.dsend));
 }
 
@@ -1226,7 +1209,7 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
     h->stats.col0 = h->col0;
     h->stats.ncols = h->nloc;
     h->stats.exchange = h->comm.kind == 0 ? 0 : d.p2p ? 1 : 2;
-    h->stats.basis = h->lu ? ELP_BASIS_LU : ELP_BASIS_INVERSE;
+    h->stats.basis = ELP_BASIS_INVERSE;
     h->timing_started = false;
     if (infeasible) {  // R/class.R:297-298: lower > upper -> "unfeasible"
         h->done = true;
@@ -1436,7 +1419,6 @@ static int64_t shard_ncols(const elp_handle* h) {
     return (r + 1) * h->n / P - r * h->n / P;
 }
 
-static int lu_start(elp_handle* h);
 static int prep_load(elp_handle* h, bool csc = false) {
     if (!h) return fail(ELP_E_ARG, "NULL handle");
     HIPCHK(hipSetDevice(h->dev));
@@ -1445,11 +1427,9 @@ static int prep_load(elp_handle* h, bool csc = false) {
     load_mark(h, "free previous");
     h->loaded = false;
     h->csc = csc;
-    if (!csc) {
-        if (h->ctl.basis == ELP_BASIS_LU)
-            return fail(ELP_E_UNSUPPORTED, "elp_control.basis = ELP_BASIS_LU needs CSC input (elp_load_csc)");
-        h->lu = false;
-    }
+    if (h->ctl.basis == ELP_BASIS_LU)  // (the r03-r04 sparse-LU engine, removed in r05: DESIGN.md 9.1)
+        return fail(ELP_E_UNSUPPORTED, "elp_control.basis = ELP_BASIS_LU: the sparse-LU engine was removed "
+                                       "(150x slower than the bump inverse); use ELP_BASIS_AUTO / _INVERSE");
     if (csc && h->comm.kind != 0)
         return fail(ELP_E_UNSUPPORTED, "elp_load_csc: column-sharded CSC solves are not supported");
     if (h->comm.world > 1) {
@@ -1631,9 +1611,6 @@ extern "C" int elp_load_csc(elp_handle* h, const int64_t* colptr, const int32_t*
             if (!std::isfinite(val[t])) return fail(ELP_E_ARG, "elp_load_csc: non-finite coefficient");
         }
     }
-    // the basis representation: the explicit bump inverse (grown with k) unless
-    // the sparse LU is asked for (the LU engine is latency-bound)
-    h->lu = h->ctl.basis == ELP_BASIS_LU;
     int rc = prep_load(h, true);
     if (rc) return rc;
     std::vector<double> sval(val, val + nnz);  // scaled in place (scaling on)
@@ -1680,13 +1657,7 @@ extern "C" int elp_load_csc(elp_handle* h, const int64_t* colptr, const int32_t*
         HIPCHK(hipMemcpyAsync(drv, rv.data(), (size_t)nnz * sizeof(double), hipMemcpyHostToDevice, h->st));
     }
     d.A = nullptr;
-    if (h->lu) {  // the refactors build B from the scaled CSC on the host
-        h->lu_cp.assign(colptr, colptr + n + 1);
-        h->lu_ri.assign(rowind, rowind + nnz);
-        h->lu_cv.assign(val, val + nnz);
-    }
     rc = load_common(h, dir, rhs, obj, lo, up, maximize);
-    if (!rc && h->lu) rc = lu_start(h);
     HIPCHK(hipStreamSynchronize(h->st));  // the host CSR staging goes out of scope
     h->stats.seconds_load = now_s() - t0;
     return rc;
@@ -1825,10 +1796,8 @@ static void pdbg_dump(elp_handle* h, const DevCtl* c) {
 }
 #endif
 
-static int lu_run_loop(elp_handle* h, int64_t budget, int32_t* lp_status);
 // the polling loop; budget = iterations allowed in this call
 static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
-    if (h->lu) return lu_run_loop(h, budget, lp_status);
     if (h->done) {
         *lp_status = h->final_status;
         return 0;
@@ -2153,297 +2122,6 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
     return 0;
 }
 
-// ---------------------------------------------------------------- sparse LU
-// The CSC path's sparse-LU engine (elp_control.basis): the host
-// factors the basis at every refactor (elp_lu_factor.cpp, the oracle's
-// Markowitz rule), uploads the factors and their level schedules, and the
-// device runs the iterations (launch_lu_iteration: BTRAN, pricing, select +
-// FTRAN + ratio test + update + eta).  The loop mirrors
-// oracle/elp_oracle_lu.c run_phase_lu.
-enum LuBuf {
-    LB_PROW, LB_PCOL, LB_RSTEP, LB_UD,
-    LB_SCHED,  // 4 schedules x (lvptr, row, ptr, j, v)
-    LB_EP = LB_SCHED + 20, LB_EPIV, LB_EI, LB_EPV, LB_EV, LB_HEAD, LB_BPOS, LB_XB, LB_ALPHA, LB_VEC, LB_ACOL,
-    LB_COUNT
-};
-
-// device buffer `id` of at least `bytes` (grown, never shrunk)
-static int lu_buf(elp_handle* h, int id, size_t bytes, void** out) {
-    if (h->lub.size() < (size_t)LB_COUNT) {
-        h->lub.resize(LB_COUNT, nullptr);
-        h->lubcap.resize(LB_COUNT, 0);
-    }
-    bytes = std::max<size_t>(bytes, 16);
-    if (h->lubcap[(size_t)id] < bytes) {
-        if (h->lub[(size_t)id]) (void)hipFree(h->lub[(size_t)id]);
-        h->lub[(size_t)id] = nullptr;
-        h->lubcap[(size_t)id] = 0;
-        if (hipMalloc(&h->lub[(size_t)id], bytes) != hipSuccess) {
-            h->lub[(size_t)id] = nullptr;
-            return fail(ELP_E_NOMEM, "sparse LU: device allocation failed");
-        }
-        h->lubcap[(size_t)id] = bytes;
-    }
-    *out = h->lub[(size_t)id];
-    return 0;
-}
-
-template <class T>
-static int lu_upload(elp_handle* h, int id, const std::vector<T>& v, const T** dst) {
-    void* p = nullptr;
-    int rc = lu_buf(h, id, v.size() * sizeof(T), &p);
-    if (rc) return rc;
-    if (!v.empty()) HIPCHK(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, h->st));
-    *dst = static_cast<const T*>(p);
-    return 0;
-}
-
-static int lu_upload_sched(elp_handle* h, int k, const LuSched& sc, LuSchedDev* sd) {
-    const int b = LB_SCHED + 5 * k;
-    int rc = lu_upload(h, b, sc.lvptr, &sd->lvptr);
-    if (!rc) rc = lu_upload(h, b + 1, sc.row, &sd->row);
-    if (!rc) rc = lu_upload(h, b + 2, sc.ptr, &sd->ptr);
-    if (!rc) rc = lu_upload(h, b + 3, sc.j, &sd->j);
-    if (!rc) rc = lu_upload(h, b + 4, sc.v, &sd->v);
-    sd->nlev = sc.nlev();
-    return rc;
-}
-
-// Refactor: B from head (downloaded), Markowitz LU on the host, factors and
-// schedules to the device, empty eta file; with_xb: x_B = B^-1 (b - N x_N).
-// *singular = true when the basis has no LU (numerical failure).
-static int lu_refactor(elp_handle* h, bool with_xb, bool* singular) {
-    const int64_t m = h->m;
-    *singular = false;
-    std::vector<int32_t> head((size_t)std::max<int64_t>(m, 1));
-    if (m) HIPCHK(hipMemcpyAsync(head.data(), h->ld.head, (size_t)m * sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
-    HIPCHK(hipStreamSynchronize(h->st));
-    const LuColumns a{m, h->n, h->lu_cp.data(), h->lu_ri.data(), h->lu_cv.data(), h->lu_asgn.data()};
-    if (lu_factor(h->luf, a, head.data(), h->ctl.tol_singular)) {
-        *singular = true;
-        return 0;
-    }
-    lu_schedules(h->luf);
-    h->lu_nnz_max = std::max(h->lu_nnz_max, h->luf.nnz());
-    LuDev& u = h->ld;
-    int rc = lu_upload(h, LB_PROW, h->luf.prow, &u.prow);
-    if (!rc) rc = lu_upload(h, LB_PCOL, h->luf.pcol, &u.pcol);
-    if (!rc) rc = lu_upload(h, LB_RSTEP, h->luf.rstep, &u.rstep);
-    if (!rc) rc = lu_upload(h, LB_UD, h->luf.ud, &u.ud);
-    if (!rc) rc = lu_upload_sched(h, 0, h->luf.sL, &u.sL);
-    if (!rc) rc = lu_upload_sched(h, 1, h->luf.sU, &u.sU);
-    if (!rc) rc = lu_upload_sched(h, 2, h->luf.sUT, &u.sUT);
-    if (!rc) rc = lu_upload_sched(h, 3, h->luf.sLT, &u.sLT);
-    if (rc) return rc;
-    h->hctl->lu_ne = 0;
-    h->hctl->lu_enz = 0;
-    HIPCHK(hipMemcpyAsync(&h->d.ctl->lu_ne, &h->hctl->lu_ne, sizeof(int32_t), hipMemcpyHostToDevice, h->st));
-    HIPCHK(hipMemcpyAsync(&h->d.ctl->lu_enz, &h->hctl->lu_enz, sizeof(int64_t), hipMemcpyHostToDevice, h->st));
-    if (with_xb) {
-        rc = row_chain(h);
-        if (rc) return rc;
-        HIPCHK(launch_lu_xb(h->d, u, h->st));
-    }
-    HIPCHK(hipStreamSynchronize(h->st));  // (the host factors are reused as upload sources)
-    return 0;
-}
-
-// after load_common on a CSC load with the sparse LU: the engine's state from
-// the slack / artificial basis, its (diagonal) LU, the phase-start checks
-static int lu_start(elp_handle* h) {
-    const int64_t m = h->m, nv = h->n + 2 * m;
-    LuDev& u = h->ld;
-    u.m = (int32_t)m;
-    u.lds = m <= lu_lds_max_m() ? 1 : 0;
-    if (const char* e = std::getenv("ELP_LU_GLOBAL"))  // test hook: the global-memory vector
-        if (std::atoi(e)) u.lds = 0;
-    const int64_t period = std::max<int64_t>(h->ctl.refactor_period, 1);
-    u.ecap = period + 2;
-    u.enzcap = std::max<int64_t>(m, 1) * (period + 1);
-    void* p = nullptr;
-    const size_t mm = (size_t)std::max<int64_t>(m, 1);
-    int rc = lu_buf(h, LB_EP, (size_t)(u.ecap + 1) * sizeof(int64_t), &p);
-    u.ep = (int64_t*)p;
-    if (!rc) rc = lu_buf(h, LB_EPIV, (size_t)u.ecap * sizeof(int32_t), &p), u.epiv = (int32_t*)p;
-    if (!rc) rc = lu_buf(h, LB_EPV, (size_t)u.ecap * sizeof(double), &p), u.epv = (double*)p;
-    if (!rc) rc = lu_buf(h, LB_EI, (size_t)u.enzcap * sizeof(int32_t), &p), u.ei = (int32_t*)p;
-    if (!rc) rc = lu_buf(h, LB_EV, (size_t)u.enzcap * sizeof(double), &p), u.ev = (double*)p;
-    if (!rc) rc = lu_buf(h, LB_HEAD, mm * sizeof(int32_t), &p), u.head = (int32_t*)p;
-    if (!rc) rc = lu_buf(h, LB_BPOS, (size_t)nv * sizeof(int32_t), &p), u.bpos = (int32_t*)p;
-    if (!rc) rc = lu_buf(h, LB_XB, mm * sizeof(double), &p), u.xB = (double*)p;
-    if (!rc) rc = lu_buf(h, LB_ALPHA, mm * sizeof(double), &p), u.alpha = (double*)p;
-    if (!rc) rc = lu_buf(h, LB_VEC, mm * sizeof(double), &p), u.vec = (double*)p;
-    if (!rc) rc = lu_buf(h, LB_ACOL, mm * sizeof(double), &p), u.acol = (double*)p;
-    if (rc) return rc;
-    h->lu_nnz_max = 0;
-    h->stats.basis = ELP_BASIS_LU;
-    if (h->done) return 0;  // lower > upper: nothing to solve
-    HIPCHK(launch_lu_init(h->d, u, h->st));
-    h->lu_asgn.assign(mm, 1.0);
-    if (m) HIPCHK(hipMemcpyAsync(h->lu_asgn.data(), h->d.asgn, (size_t)m * sizeof(double), hipMemcpyDeviceToHost, h->st));
-    bool singular = false;
-    rc = lu_refactor(h, false, &singular);  // (the oracle's initial lu_factor: x_B stays)
-    if (rc) return rc;
-    if (singular) {
-        h->done = true;
-        h->final_status = ELP_NUMFAILURE;
-        return 0;
-    }
-    HIPCHK(launch_lu_looptop(h->d, u, h->phase, h->st));
-    HIPCHK(hipStreamSynchronize(h->st));
-    return 0;
-}
-
-static int lu_run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
-    if (h->done) {
-        *lp_status = h->final_status;
-        return 0;
-    }
-    const double t_loop0 = now_s();
-    if (!h->timing_started) {
-        h->t_solve_start = t_loop0;
-        h->timing_started = true;
-    }
-    DevCtl* c = h->hctl;
-    HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
-    HIPCHK(hipStreamSynchronize(h->st));
-    c->iter_stop = budget >= INT64_MAX - c->iter ? INT64_MAX : c->iter + budget;
-    if (c->status == ST_STOP) c->status = ST_RUN;
-    c->phase = h->phase;
-    int rc = push_ctl_fields(h);
-    if (rc) return rc;
-    auto refactor_now = [&](bool* numfail) -> int {
-        bool singular = false;
-        const int r = lu_refactor(h, true, &singular);
-        if (r) return r;
-        *numfail = singular;
-        h->stats.refactors++;
-        return 0;
-    };
-    for (;;) {
-        if (c->status == ST_RUN && c->iter >= c->iter_stop && c->iter < c->iter_limit) {
-            *lp_status = ELP_SUBOPTIMAL;
-            h->stats.seconds_loop += now_s() - t_loop0;
-            return 0;
-        }
-        for (int t = 0; t < h->ctl.sync_every; ++t) {
-            h->stats.price_launches++;
-            HIPCHK(launch_lu_iteration(h->d, h->ld, h->phase, h->st));
-        }
-        HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
-        HIPCHK(hipStreamSynchronize(h->st));
-        h->stats.host_polls++;
-        const int32_t s = c->status;
-        if (s == ST_RUN) {
-            if (h->ctl.time_limit > 0 && now_s() - h->t_solve_start > h->ctl.time_limit) {
-                h->done = true;
-                h->final_status = ELP_TIMEOUT;
-                break;
-            }
-            continue;
-        }
-        if (s == ST_STOP) {
-            *lp_status = ELP_SUBOPTIMAL;
-            h->stats.seconds_loop += now_s() - t_loop0;
-            return 0;
-        }
-        const bool recheck = s == ST_PHASE_OPT && h->phase == 2 && c->since_refactor > 0;
-        if (s == ST_REFACTOR || recheck) {
-            bool nf = false;
-            rc = refactor_now(&nf);
-            if (rc) return rc;
-            if (nf) {
-                h->done = true;
-                h->final_status = ELP_NUMFAILURE;
-                break;
-            }
-            c->since_refactor = 0;
-            c->lu_ne = 0;
-            c->lu_enz = 0;
-            c->status = ST_RUN;  // (a re-check skips the loop-top checks, as the oracle's)
-            rc = push_ctl_fields(h);
-            if (rc) return rc;
-            continue;
-        }
-        if (s == ST_DUALINF && h->phase == 3) {  // the dual ray: no nonbasic can repair the leaving row
-            h->done = true;
-            h->final_status = ELP_INFEASIBLE;
-            break;
-        }
-        if (s == ST_PHASE_OPT && h->phase == 3) {
-            // primal feasible: confirm on a fresh x_B after updates (oracle run_dual),
-            // else the real costs and the primal phase 2 from this basis
-            const bool recheck = c->since_refactor > 0;
-            if (!recheck) {
-                HIPCHK(launch_phase2(h->d, h->st));
-                h->phase = 2;
-            }
-            rc = do_refactor(h, c->k);
-            if (rc) return rc;
-            HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
-            HIPCHK(hipStreamSynchronize(h->st));
-            if (c->status == ST_NUMFAIL) {
-                h->done = true;
-                h->final_status = ELP_NUMFAILURE;
-                break;
-            }
-            c->phase = 2;
-            c->since_refactor = 0;
-            if (!recheck) {
-                c->ndegen = 0;
-                c->bland = 0;
-                c->devex = h->ctl.pricing == ELP_PRICE_DEVEX;
-            }
-            c->status = ST_RUN;
-            rc = push_ctl_fields(h);
-            if (rc) return rc;
-            continue;
-        }
-        if ((s == ST_PHASE_OPT || s == ST_P1DONE) && h->phase == 1) {
-            if (s == ST_PHASE_OPT && c->art_sum > c->tol_inf) {
-                h->done = true;
-                h->final_status = ELP_INFEASIBLE;
-                break;
-            }
-            HIPCHK(launch_lu_phase2(h->d, h->st));
-            HIPCHK(launch_devex_reset(h->d, h->st));
-            h->phase = 2;
-            bool nf = false;
-            rc = refactor_now(&nf);
-            if (rc) return rc;
-            if (nf) {
-                h->done = true;
-                h->final_status = ELP_NUMFAILURE;
-                break;
-            }
-            HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
-            HIPCHK(hipStreamSynchronize(h->st));
-            c->phase = 2;
-            c->since_refactor = 0;
-            c->ndegen = 0;
-            c->bland = 0;
-            c->lu_ne = 0;
-            c->lu_enz = 0;
-            c->status = ST_RUN;
-            rc = push_ctl_fields(h);
-            if (rc) return rc;
-            HIPCHK(launch_lu_looptop(h->d, h->ld, 2, h->st));
-            HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
-            HIPCHK(hipStreamSynchronize(h->st));
-            continue;
-        }
-        h->done = true;
-        if (s == ST_PHASE_OPT) h->final_status = ELP_OPTIMAL;
-        else if (s == ST_UNBOUNDED) h->final_status = ELP_UNBOUNDED;
-        else if (s == ST_ITERCAP) h->final_status = ELP_SUBOPTIMAL;
-        else h->final_status = ELP_NUMFAILURE;
-        break;
-    }
-    h->stats.seconds_loop += now_s() - t_loop0;
-    *lp_status = h->final_status;
-    return 0;
-}
-
 extern "C" int elp_set_int(elp_handle* h, const int32_t* is_int) {
     if (is_group(h)) return fan_out(h, [&](elp_handle* r, int) { return elp_set_int(r, is_int); }, false);
     if (!h || !h->loaded) return fail(ELP_E_STATE, "elp_set_int: no problem loaded");
@@ -2463,7 +2141,6 @@ static int reload_bounds(elp_handle* h, const std::vector<double>& lo, const std
     const std::vector<double> rhs = h->rhs_h, obj = h->obj_h;
     h->in_bnb = true;
     int rc = load_common(h, dir.data(), rhs.data(), obj.data(), lo.data(), up.data(), h->maximize);
-    if (!rc && h->lu) rc = lu_start(h);
     h->in_bnb = false;
     return rc;
 }
@@ -2733,8 +2410,7 @@ extern "C" int elp_get_solution(elp_handle* h, double* objval, double* x, double
     double* dx = nullptr;
     HIPCHK(dalloc(&dx, n));
     HIPCHK(hipMemsetAsync(dx, 0, (size_t)n * sizeof(double), h->st));
-    if (h->lu) HIPCHK(launch_lu_extract(h->d, h->ld, dx, h->st));
-    else HIPCHK(launch_extract(h->d, dx + h->col0, h->st));
+    HIPCHK(launch_extract(h->d, dx + h->col0, h->st));
     {
         const int rc = h->comm.allreduce_sum_f64(dx, (size_t)n, h->st);
         if (rc) return fail(rc, "solution all-reduce failed");
@@ -2776,14 +2452,7 @@ extern "C" int elp_get_solution(elp_handle* h, double* objval, double* x, double
         HIPCHK(hipStreamSynchronize(h->st));
         for (int64_t i = 0; i < m; ++i) y[i] = unscale_row(h, h->maximize ? -y[i] : y[i], i, 1);
     }
-    if (basis && m && h->lu) {
-        std::vector<int32_t> head((size_t)m);
-        HIPCHK(hipMemcpyAsync(head.data(), h->ld.head, (size_t)m * sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
-        HIPCHK(hipStreamSynchronize(h->st));
-        std::vector<int64_t> bv(head.begin(), head.end());
-        std::sort(bv.begin(), bv.end());
-        for (int64_t t = 0; t < m; ++t) basis[t] = bv[(size_t)t];
-    } else if (basis && m) {
+    if (basis && m) {
         std::vector<int32_t> cover(m), Sl(std::max(c.k, 1));
         HIPCHK(hipMemcpyAsync(cover.data(), h->d.cover, m * sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
         if (c.k)
@@ -3029,9 +2698,6 @@ static int sens_check(elp_handle* h) {
     if (!h || !h->loaded) return fail(ELP_E_STATE, "elp_sensitivity: no problem loaded");
     if (!h->done || h->final_status != ELP_OPTIMAL)
         return fail(ELP_E_STATE, "elp_sensitivity: problem is not optimal");
-    if (h->lu)
-        return fail(ELP_E_UNSUPPORTED, "elp_sensitivity: the sparse-LU basis (load with elp_control.basis = "
-                                       "ELP_BASIS_INVERSE for a sensitivity report)");
     if (h->mip || !h->is_int.empty())  // R/class.R:617-618, :634-635
         return fail(ELP_E_STATE, "Sensitivity unavailable for problems with integer/binary variables");
     return 0;
@@ -3096,20 +2762,6 @@ extern "C" int elp_get_stats(elp_handle* h, elp_stats* st) {
         h->stats.exchange_rtt_us = h->comm.p2p ? h->comm.rtt_us : 0.0;
         h->stats.dual_iterations = c.dual_iters;
         h->stats.simplex = h->dual_used ? ELP_SIMPLEX_DUAL_PRIMAL : ELP_SIMPLEX_PRIMAL_PRIMAL;
-        if (h->lu) {  // basic structurals, factor and eta-file sizes
-            std::vector<int32_t> head((size_t)std::max<int64_t>(h->m, 1));
-            if (h->m) {
-                HIPCHK(hipMemcpyAsync(head.data(), h->ld.head, (size_t)h->m * sizeof(int32_t), hipMemcpyDeviceToHost,
-                                      h->st));
-                HIPCHK(hipStreamSynchronize(h->st));
-            }
-            int64_t k = 0;
-            for (int64_t p = 0; p < h->m; ++p) k += head[(size_t)p] < h->n;
-            h->stats.bump_dim = k;
-            h->stats.y_rows = 0;
-            h->stats.lu_nnz = h->lu_nnz_max;
-            h->stats.eta_nnz = c.lu_enz_max;
-        }
         if (h->d.ptimer) {
             h->stats.price_seconds = 1e-8 * (double)c.price_ticks;
             h->stats.price_timed_launches = c.price_timed;

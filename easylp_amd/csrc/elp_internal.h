@@ -125,9 +125,6 @@ struct DevCtl {
     int32_t dv_lv, pad8;
     double dv_dq, dv_wq;
     double wq;  // weight of the entering candidate (select kernels)
-    // sparse-LU engine (ELP_BASIS_LU): etas in the file, their entries
-    int32_t lu_ne, lu_pad;
-    int64_t lu_enz, lu_enz_max;
     // dual simplex phase 1 (h->phase 3, oracle run_dual): the leaving row of
     // this iteration as k_dual_row chose it -- basic variable, entry (covered
     // row, or m + bump position), direction s (+1 below its lower bound), the
@@ -328,30 +325,6 @@ struct Dev {
 constexpr int AFL_SB = 1;    // afl: bucket starts [1, 66)
 constexpr int AFL_POS = 66;  // afl: positions [66, 66 + SPL)
 
-// Sparse-LU engine of the CSC path (elp_control.basis = ELP_BASIS_LU, DESIGN.md
-// 9.1; oracle/elp_oracle_lu.c): the whole basis B (position p holds head[p])
-// factored P B Q = L U on the host at a refactor (elp_lu_factor.cpp), a
-// product-form eta file appended on the device, FTRAN / BTRAN by one workgroup
-// walking level schedules (rows of a level are independent; each row is one
-// fma chain in ascending step order, as in the oracle).
-struct LuSchedDev {
-    int32_t nlev, pad;
-    const int32_t *lvptr, *row, *ptr, *j;
-    const double* v;
-};
-struct LuDev {
-    int32_t m, lds;  // lds: the working vector lives in LDS (8 m bytes fit)
-    int64_t ecap, enzcap;  // eta file capacity: etas, entries
-    const int32_t *prow, *pcol, *rstep;  // step -> pivot row / position; row -> step
-    const double* ud;                    // U diagonal per step
-    LuSchedDev sL, sU, sUT, sLT;         // L fwd, U bwd, U^T fwd, L^T bwd
-    int64_t* ep;                         // [ecap + 1] entry offsets of the etas
-    int32_t *epiv, *ei;                  // pivot position per eta; entry positions
-    double *epv, *ev;                    // pivot value per eta; entry values
-    int32_t *head, *bpos;                // position -> basic variable (global id); variable -> position
-    double *xB, *alpha, *vec, *acol;     // m each: basic values, FTRAN result, scratch, dense rhs
-};
-
 // ---------------------------------------------------------------- launches
 // Each returns hipGetLastError() of its launch.
 hipError_t launch_generate(const Dev& d, uint64_t seed, int64_t col0, int64_t n_global,
@@ -418,23 +391,6 @@ hipError_t launch_sensitivity(const Dev& d, int k, double* dred, double* TR, dou
                               double* phi, double* qlo, double* qhi, double* out4, hipStream_t st);
 // x of the local shard into xout[0:n) (basic values from the replicated S list)
 hipError_t launch_extract(const Dev& d, double* xout, hipStream_t st);
-
-// sparse-LU engine (elp_kernels.hip, "sparse LU" section)
-// one iteration: BTRAN (y = B^-T c_B), pricing (structural + slack tiles),
-// select + FTRAN + ratio test + update + eta + loop-top checks
-hipError_t launch_lu_iteration(const Dev& d, const LuDev& u, int phase, hipStream_t st);
-// phase-start loop-top checks (phase 1: artificial sum; iteration cap)
-hipError_t launch_lu_looptop(const Dev& d, const LuDev& u, int phase, hipStream_t st);
-// head / bpos / xB from the initial cover (after launch_init_rows)
-hipError_t launch_lu_init(const Dev& d, const LuDev& u, hipStream_t st);
-// after a refactor: acol = b - ract - (nonbasic slack), xB = B^-1 acol (no etas)
-hipError_t launch_lu_xb(const Dev& d, const LuDev& u, hipStream_t st);
-// phase 2 costs and artificial bounds
-hipError_t launch_lu_phase2(const Dev& d, hipStream_t st);
-// structural x into xout[0:n)
-hipError_t launch_lu_extract(const Dev& d, const LuDev& u, double* xout, hipStream_t st);
-// largest m whose working vector fits the LDS of one workgroup (0: query failed)
-int lu_lds_max_m();
 
 // dual simplex phase 1 (elp_kernels.hip "dual simplex" section; oracle run_dual)
 // load: the dual-feasible start -- boxed columns at the bound their cost sign

@@ -5957,663 +5957,4 @@ hipError_t launch_sensitivity(const Dev& d, int k, double* dred, double* TR, dou
     return hipGetLastError();
 }
 
-// ============================================================== sparse LU
-// The CSC path's sparse-LU engine (elp_control.basis = ELP_BASIS_LU; oracle
-// /elp_oracle_lu.c run_phase_lu).  One iteration = three
-// launches: k_lu_btran (one workgroup: y = B^-T c_B through the eta file and
-// the U^T / L^T schedules), k_lu_price (grid: structural and slack tiles),
-// k_lu_iter (one workgroup: select, FTRAN through L / U and the etas, the
-// Harris ratio test over the m positions, the update, the new eta, the
-// loop-top checks).  The FTRAN / BTRAN vector lives in LDS when 8 m bytes fit
-// (LDS = 1), else in global memory (LuDev::vec); every row of a level is one
-// fma chain in ascending step order -- the oracle's -- so the schedule does
-// not change a bit.
-constexpr int LU_NT = 256;  // threads of the single-workgroup kernels (= the oracle's LANES)
-constexpr int LU_PF = 4;    // entries of a scheduled row prefetched into registers
-
-// One triangular solve: t[s] = (t[s] - sum_e v_e t[j_e]) (/ ud[s]) for the
-// rows of each level, a barrier between levels.  The next level's row
-// descriptors and first LU_PF entries are loaded while the current level
-// computes (they depend on neither t nor the current level).
-DEV void lu_sched_solve(const LuSchedDev& sc, const double* __restrict__ ud, double* t) {
-    const int nlev = sc.nlev;
-    if (nlev <= 0) return;
-    const int tid = threadIdx.x;
-    int r1 = sc.lvptr[1];
-    int i = sc.lvptr[0] + tid;
-    bool has = i < r1;
-    int s = 0, b = 0, e = 0;
-    int pj[LU_PF];
-    double pv[LU_PF];
-    if (has) {
-        s = sc.row[i];
-        b = sc.ptr[i];
-        e = sc.ptr[i + 1];
-    }
-#pragma unroll
-    for (int k = 0; k < LU_PF; ++k) {
-        const bool in = has && b + k < e;
-        pj[k] = in ? sc.j[b + k] : 0;
-        pv[k] = in ? sc.v[b + k] : 0.0;
-    }
-    for (int l = 0; l < nlev; ++l) {
-        // next level's descriptors (in flight during this level)
-        const int nr1 = l + 1 < nlev ? sc.lvptr[l + 2] : r1;
-        const int ni = r1 + tid;
-        const bool nhas = l + 1 < nlev && ni < nr1;
-        int ns = 0, nb = 0, ne = 0;
-        if (nhas) {
-            ns = sc.row[ni];
-            nb = sc.ptr[ni];
-            ne = sc.ptr[ni + 1];
-        }
-        if (has) {
-            double acc = t[s];
-#pragma unroll
-            for (int k = 0; k < LU_PF; ++k)
-                if (b + k < e) acc = fma(-pv[k], t[pj[k]], acc);
-            for (int k = b + LU_PF; k < e; ++k) acc = fma(-sc.v[k], t[sc.j[k]], acc);
-            t[s] = ud ? acc / ud[s] : acc;
-        }
-        for (int i2 = i + LU_NT; i2 < r1; i2 += LU_NT) {  // wide levels: the other rows
-            const int s2 = sc.row[i2];
-            double acc = t[s2];
-            for (int k = sc.ptr[i2]; k < sc.ptr[i2 + 1]; ++k) acc = fma(-sc.v[k], t[sc.j[k]], acc);
-            t[s2] = ud ? acc / ud[s2] : acc;
-        }
-#pragma unroll
-        for (int k = 0; k < LU_PF; ++k) {  // the next rows' first entries
-            const bool in = nhas && nb + k < ne;
-            pj[k] = in ? sc.j[nb + k] : 0;
-            pv[k] = in ? sc.v[nb + k] : 0.0;
-        }
-        __syncthreads();
-        r1 = nr1;
-        i = ni;
-        has = nhas;
-        s = ns;
-        b = nb;
-        e = ne;
-    }
-}
-
-// Eta entries prefetched per thread: the next eta's pivot, value, range and
-// first LU_EPF entries per thread are loaded while the current eta computes
-// (none of them depends on x); longer etas load the rest on the spot.
-constexpr int LU_EPF = 4;
-struct EtaPf {
-    int p;
-    double pv;
-    int64_t b, en;
-    int i[LU_EPF];
-    double v[LU_EPF];
-};
-DEV void eta_load_head(const LuDev& u, int e, bool on, EtaPf& f) {
-    f.p = on ? u.epiv[e] : 0;
-    f.pv = on ? u.epv[e] : 1.0;
-    f.b = on ? u.ep[e] : 0;
-    f.en = on ? u.ep[e + 1] : 0;
-}
-DEV void eta_load_body(const LuDev& u, EtaPf& f) {
-#pragma unroll
-    for (int k = 0; k < LU_EPF; ++k) {
-        const int64_t kk = f.b + threadIdx.x + (int64_t)k * LU_NT;
-        const bool in = kk < f.en;
-        f.i[k] = in ? u.ei[kk] : 0;
-        f.v[k] = in ? u.ev[kk] : 0.0;
-    }
-}
-
-// FTRAN through the eta file: x_p /= pivot, then x_i -= alpha_i x_p
-DEV void lu_eta_ftran(const LuDev& u, int ne, double* x) {
-    if (ne <= 0) return;
-    EtaPf cur, nxt;
-    eta_load_head(u, 0, true, cur);
-    eta_load_body(u, cur);
-    for (int e = 0; e < ne; ++e) {
-        const bool more = e + 1 < ne;
-        eta_load_head(u, e + 1, more, nxt);
-        const double xp = x[cur.p] / cur.pv;
-        __syncthreads();
-        if (threadIdx.x == 0) x[cur.p] = xp;
-#pragma unroll
-        for (int k = 0; k < LU_EPF; ++k)
-            if (cur.b + threadIdx.x + (int64_t)k * LU_NT < cur.en) x[cur.i[k]] = fma(-cur.v[k], xp, x[cur.i[k]]);
-        for (int64_t k = cur.b + threadIdx.x + (int64_t)LU_EPF * LU_NT; k < cur.en; k += LU_NT) {
-            const int i = u.ei[k];
-            x[i] = fma(-u.ev[k], xp, x[i]);
-        }
-        eta_load_body(u, nxt);
-        __syncthreads();
-        cur = nxt;
-    }
-}
-
-// BTRAN through the eta file (last eta first): x_p = (x_p - sum alpha_i x_i) / pivot,
-// the sum in the oracle's lane_dot256 order (256 lane-strided chains, then the
-// pairwise tree: each wave's tree, then (w0 + w1) + (w2 + w3))
-DEV void lu_eta_btran(const LuDev& u, int ne, double* x, double* red) {
-    if (ne <= 0) return;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    EtaPf cur, nxt;
-    eta_load_head(u, ne - 1, true, cur);
-    eta_load_body(u, cur);
-    for (int e = ne - 1; e >= 0; --e) {
-        const bool more = e > 0;
-        eta_load_head(u, e - 1, more, nxt);
-        double acc = 0.0;
-#pragma unroll
-        for (int k = 0; k < LU_EPF; ++k)
-            if (cur.b + threadIdx.x + (int64_t)k * LU_NT < cur.en) acc = fma(cur.v[k], x[cur.i[k]], acc);
-        for (int64_t k = cur.b + threadIdx.x + (int64_t)LU_EPF * LU_NT; k < cur.en; k += LU_NT)
-            acc = fma(u.ev[k], x[u.ei[k]], acc);
-        acc = wave_tree(acc);
-        if (lane == 0) red[w] = acc;
-        eta_load_body(u, nxt);
-        __syncthreads();
-        if (threadIdx.x == 0) x[cur.p] = (x[cur.p] - ((red[0] + red[1]) + (red[2] + red[3]))) / cur.pv;
-        __syncthreads();
-        cur = nxt;
-    }
-}
-
-// the working vector of one workgroup: LDS (dynamic) or the global scratch
-template <bool LDS>
-DEV double* lu_vec(const LuDev& u, double* lds) {
-    return LDS ? lds : u.vec;
-}
-
-// y = B^-T c_B (c_B[p] = cost of head[p]): etas on x (positions), then t[s] =
-// x[pcol[s]] (through the global alpha scratch), U^T and L^T, y[prow[s]] = t[s]
-template <bool LDS>
-DEV void lu_btran_body(const Dev& d, const LuDev& u, double* x, double* red) {
-    const int m = u.m;
-    const int ne = d.ctl->lu_ne;
-    for (int p = threadIdx.x; p < m; p += LU_NT) x[p] = d.cost[loc_of(d, u.head[p])];
-    __syncthreads();
-    lu_eta_btran(u, ne, x, red);
-    double* tmp = u.alpha;  // (free between iterations)
-    for (int p = threadIdx.x; p < m; p += LU_NT) tmp[p] = x[p];
-    __syncthreads();
-    for (int s = threadIdx.x; s < m; s += LU_NT) x[s] = tmp[u.pcol[s]];
-    __syncthreads();
-    lu_sched_solve(u.sUT, u.ud, x);
-    lu_sched_solve(u.sLT, nullptr, x);
-    for (int s = threadIdx.x; s < m; s += LU_NT) d.y[u.prow[s]] = x[s];
-}
-
-template <bool LDS>
-__global__ void __launch_bounds__(LU_NT) k_lu_btran(Dev d, LuDev u) {
-    extern __shared__ __attribute__((aligned(16))) double lu_lds[];
-    __shared__ double red[4];
-    if (d.ctl->status != ST_RUN) return;
-    lu_btran_body<LDS>(d, u, lu_vec<LDS>(u, lu_lds), red);
-}
-
-// pricing: tiles of 128 structurals (column chain over the CSC nonzeros, y
-// dense), then tiles of 128 slacks (d = c - y_i); Devex as k_price_csc
-__global__ void __launch_bounds__(TILE_COLS) k_lu_price(Dev d, LuDev u, int nts) {
-    __shared__ Cand red[TILE_COLS / 64];
-    const DevCtl* c = d.ctl;
-    if (c->status != ST_RUN) return;
-    const int bland = c->bland, devex = c->devex;
-    const double dtol = c->tol_dual;
-    Cand best;
-    best.j = -1;
-    best.score = 0.0;
-    best.d = 0.0;
-    best.w = 1.0;
-    int64_t jl = -1, jg = -1;
-    double dj = 0.0;
-    if ((int)blockIdx.x < nts) {
-        const int64_t j = (int64_t)blockIdx.x * TILE_COLS + threadIdx.x;
-        if (j < d.n && d.vstat[j] != VS_BASIC && d.lb[j] != d.ub[j]) {
-            double acc = 0.0;
-            for (int64_t t = d.cptr[j]; t < d.cptr[j + 1]; ++t) acc = fma(d.cval[t], d.y[d.rind[t]], acc);
-            dj = d.cost[j] - acc;
-            jl = j;
-            jg = j;
-        }
-    } else {
-        const int64_t i = (int64_t)(blockIdx.x - nts) * TILE_COLS + threadIdx.x;
-        const int64_t v = d.n + i;
-        if (i < d.m && d.vstat[v] != VS_BASIC && d.lb[v] != d.ub[v]) {
-            dj = d.cost[v] - d.y[i];
-            jl = v;
-            jg = d.N + i;
-        }
-    }
-    if (jl >= 0) {
-        const double wj = devex ? devex_weight(d, devex_in(c), jl, jg, dj, d.dw[jl], d.dprev[jl]) : 1.0;
-        best = price_cand(d.vstat[jl], dj, wj, devex, dtol, jg);
-    }
-    best = block_best<TILE_COLS>(best, bland, red);
-    if (threadIdx.x == 0) d.cand[blockIdx.x] = best;
-}
-
-// phase-1 infeasibility in the oracle's wave order over positions (one wave)
-DEV double lu_art_sum(const Dev& d, const LuDev& u) {
-    const int lane = threadIdx.x & 63;
-    double acc = 0.0;
-    for (int p = lane; p < u.m; p += 64)
-        if (u.head[p] >= d.N + d.m) acc = acc + u.xB[p];
-    return wave_tree(acc);
-}
-
-// loop-top checks after an iteration (oracle run_phase_lu's loop top): the
-// artificial sum (phase 1), the iteration cap, the refactor period, the
-// elp_iterate budget.  Executed by wave 0 (the sum is a wave reduction).
-DEV void lu_looptop(const Dev& d, const LuDev& u, int phase) {
-    DevCtl* c = d.ctl;
-    const double as = phase == 1 ? lu_art_sum(d, u) : 0.0;
-    if (threadIdx.x != 0) return;
-    if (c->status != ST_RUN) return;
-    if (phase == 1 && as <= c->tol_inf) {
-        c->art_sum = as;
-        c->status = ST_P1DONE;
-    } else if (c->iter >= c->iter_limit) {
-        c->status = ST_ITERCAP;
-    } else if (c->since_refactor >= c->refactor_period) {
-        c->status = ST_REFACTOR;
-    } else if (c->iter >= c->iter_stop) {
-        c->status = ST_STOP;
-    }
-}
-
-__global__ void k_lu_looptop(Dev d, LuDev u, int phase) { lu_looptop(d, u, phase); }
-
-// L and U of the FTRAN on t (steps), then x (positions) = t[pcol], etas on x:
-// x ends in `x` (LDS or the global vec) and in u.alpha
-template <bool LDS>
-DEV void lu_ftran_body(const Dev& d, const LuDev& u, double* x) {
-    const int m = u.m;
-    lu_sched_solve(u.sL, nullptr, x);
-    lu_sched_solve(u.sU, u.ud, x);
-    for (int s = threadIdx.x; s < m; s += LU_NT) u.alpha[u.pcol[s]] = x[s];
-    __syncthreads();
-    for (int p = threadIdx.x; p < m; p += LU_NT) x[p] = u.alpha[p];
-    __syncthreads();
-    const int ne = d.ctl->lu_ne;
-    if (ne > 0) {
-        lu_eta_ftran(u, ne, x);
-        for (int p = threadIdx.x; p < m; p += LU_NT) u.alpha[p] = x[p];
-        __syncthreads();
-    }
-}
-
-struct LuLeave {
-    double ag, r, g;
-    int var, pos;
-};
-DEV bool lu_leave_better(const LuLeave& a, const LuLeave& b, int bland) {
-    if (a.var < 0) return false;
-    if (b.var < 0) return true;
-    if (bland) return a.r < b.r || (a.r == b.r && a.var < b.var);
-    return a.ag > b.ag || (a.ag == b.ag && a.var < b.var);
-}
-
-// select + FTRAN + ratio test + update + eta + loop-top checks (one workgroup)
-template <bool LDS>
-__global__ void __launch_bounds__(LU_NT) k_lu_iter(Dev d, LuDev u, int ncand, int phase) {
-    extern __shared__ __attribute__((aligned(16))) double lu_lds[];
-    __shared__ Cand cred[LU_NT / 64];
-    __shared__ double dred[LU_NT / 64];
-    __shared__ LuLeave lred[LU_NT / 64];
-    __shared__ int s_cnt[LU_NT];
-    __shared__ double s_step;
-    __shared__ int s_act, s_lpos;
-    DevCtl* c = d.ctl;
-    if (c->status != ST_RUN) return;
-    const int m = u.m, n = d.n, tid = threadIdx.x;
-    const int bland = c->bland;
-    double* x = lu_vec<LDS>(u, lu_lds);
-    // ---- select ----
-    Cand best;
-    best.j = -1;
-    best.score = 0.0;
-    best.d = 0.0;
-    best.w = 1.0;
-    for (int t = tid; t < ncand; t += LU_NT) {
-        const Cand o = d.cand[t];
-        cand_take(best, o, cand_better(o, best, bland));
-    }
-    best = block_best<LU_NT>(best, bland, cred);
-    if (best.j < 0) {  // no entering candidate: this phase is optimal (the host re-checks)
-        const double as = phase == 1 ? lu_art_sum(d, u) : 0.0;
-        if (tid == 0) {
-            c->art_sum = as;
-            c->status = ST_PHASE_OPT;
-        }
-        return;
-    }
-    const int q = (int)best.j;
-    const double dq = best.d, qw = best.w;
-    const double sig = dq < 0.0 ? 1.0 : -1.0;
-    if (tid == 0) {
-        const double pb = 12.0 * (double)d.nnz + 17.0 * (double)n + 8.0 * (double)m;
-        c->price_bytes += pb;
-        c->price_passes++;
-        c->q = q;
-        c->dq = dq;
-        c->wq = qw;
-        c->sig = sig;
-    }
-    // ---- FTRAN: the entering column scattered into t (steps) ----
-    for (int s = tid; s < m; s += LU_NT) x[s] = 0.0;
-    __syncthreads();
-    if (q < d.N) {
-        for (int64_t t = d.cptr[q] + tid; t < d.cptr[q + 1]; t += LU_NT) x[u.rstep[d.rind[t]]] = d.cval[t];
-    } else if (tid == 0) {
-        x[u.rstep[q - d.N]] = 1.0;
-    }
-    __syncthreads();
-    lu_ftran_body<LDS>(d, u, x);
-    // ---- ratio test (Harris two-pass; textbook under Bland) ----
-    const double ptol = c->tol_primal, pivtol = c->tol_pivot, INF = HUGE_VAL;
-    double tmin = INF;
-    for (int p = tid; p < m; p += LU_NT) {
-        const int var = u.head[p];
-        const int vl = loc_of(d, var);
-        const double g = sig * x[p], xb = u.xB[p], l = d.lb[vl], hi = d.ub[vl];
-        double r = INF;
-        if (g > pivtol && l > -INF) r = bland ? (xb - l) / g : (xb - l + ptol) / g;
-        else if (g < -pivtol && hi < INF) r = bland ? (hi - xb) / (-g) : (hi - xb + ptol) / (-g);
-        tmin = fmin(tmin, r);
-    }
-    const double theta_max = block_min<LU_NT>(tmin, dred);
-    LuLeave lb_;
-    lb_.var = -1;
-    lb_.pos = -1;
-    lb_.ag = lb_.r = lb_.g = 0.0;
-    for (int p = tid; p < m; p += LU_NT) {
-        const int var = u.head[p];
-        const int vl = loc_of(d, var);
-        const double g = sig * x[p], xb = u.xB[p], l = d.lb[vl], hi = d.ub[vl];
-        double r;
-        if (g > pivtol && l > -INF) r = (xb - l) / g;
-        else if (g < -pivtol && hi < INF) r = (hi - xb) / (-g);
-        else continue;
-        if (!(r <= theta_max)) continue;
-        LuLeave o;
-        o.ag = fabs(g);
-        o.r = r;
-        o.g = g;
-        o.var = var;
-        o.pos = p;
-        if (lu_leave_better(o, lb_, bland)) lb_ = o;
-    }
-    // block-wide best leaving entry (a total order: variable ids break ties)
-    {
-        const int w = tid >> 6;
-        // wave: reduce by shuffles of the whole record (64 lanes, log steps)
-        for (int off = 32; off >= 1; off >>= 1) {
-            LuLeave o;
-            o.ag = __shfl_xor(lb_.ag, off);
-            o.r = __shfl_xor(lb_.r, off);
-            o.g = __shfl_xor(lb_.g, off);
-            o.var = __shfl_xor(lb_.var, off);
-            o.pos = __shfl_xor(lb_.pos, off);
-            if (lu_leave_better(o, lb_, bland)) lb_ = o;
-        }
-        if ((tid & 63) == 0) lred[w] = lb_;
-        __syncthreads();
-        lb_ = lred[0];
-        for (int i = 1; i < LU_NT / 64; ++i)
-            if (lu_leave_better(lred[i], lb_, bland)) lb_ = lred[i];
-        __syncthreads();
-    }
-    // ---- decision (thread 0; the oracle's order of effects) ----
-    if (tid == 0) {
-        const int lv = lb_.var;
-        const double theta = lv >= 0 ? (lb_.r > 0.0 ? lb_.r : 0.0) : INF;
-        const int ql = loc_of(d, q);
-        const double lbq = d.lb[ql], ubq = d.ub[ql];
-        const double flip = (lbq > -INF && ubq < INF) ? ubq - lbq : INF;
-        const int64_t it = c->iter;
-        c->iter = it + 1;
-        if (phase == 1) c->phase1_iters++;
-        const bool tr = it < c->trace_cap;
-        if (flip < INF && flip <= theta) {
-            s_act = ACT_FLIP;
-            s_step = flip;
-            if (d.vstat[ql] == VS_LOWER) {
-                d.vstat[ql] = VS_UPPER;
-                d.xval[ql] = ubq;
-            } else {
-                d.vstat[ql] = VS_LOWER;
-                d.xval[ql] = lbq;
-            }
-            c->flips++;
-            if (tr) {
-                d.trace[2 * it] = q;
-                d.trace[2 * it + 1] = -1;
-            }
-            c->dv_valid = 0;
-            c->ndegen = 0;
-            c->bland = 0;
-        } else if (theta == INF) {
-            s_act = ACT_NONE;
-            if (tr) {
-                d.trace[2 * it] = q;
-                d.trace[2 * it + 1] = -2;
-            }
-            c->unb_var = q;
-            c->unb_sig = sig;
-            c->status = ST_UNBOUNDED;
-        } else {
-            s_act = ACT_PIVOT;
-            s_step = theta;
-            s_lpos = lb_.pos;
-            if (tr) {
-                d.trace[2 * it] = q;
-                d.trace[2 * it + 1] = lv;
-            }
-            if (c->devex && qw > DEVEX_RESET) {  // a new framework: every priced weight 1 next pass
-                c->dv_valid = 2;
-            } else if (c->devex) {
-                double wl = qw / (lb_.g * lb_.g);
-                if (wl < 1.0) wl = 1.0;
-                if (wl > DEVEX_WMAX) wl = DEVEX_WMAX;
-                if (lv < d.N + d.m) d.dw[loc_of(d, lv)] = wl;
-                c->dv_valid = 1;
-                c->dv_lv = lv;
-                c->dv_dq = dq;
-                c->dv_wq = qw;
-            }
-            if (theta == 0.0) {
-                c->degenerate++;
-                if (++c->ndegen >= c->degen_switch) c->bland = 1;
-            } else {
-                c->ndegen = 0;
-                c->bland = 0;
-            }
-        }
-    }
-    __syncthreads();
-    const int act = s_act;
-    if (act == ACT_NONE) return;
-    // ---- primal update of every basic value ----
-    const double step = s_step;
-    for (int p = tid; p < m; p += LU_NT) u.xB[p] = fma(-step, sig * x[p], u.xB[p]);
-    __syncthreads();
-    if (act == ACT_PIVOT) {
-        const int lpos = s_lpos;
-        if (tid == 0) {
-            const int lv = lb_.var, ql = loc_of(d, q), lvl = loc_of(d, lv);
-            const double xq = d.xval[ql] + sig * step;
-            if (lv >= d.N + d.m) {
-                d.lb[lvl] = 0.0;
-                d.ub[lvl] = 0.0;
-                d.vstat[lvl] = VS_LOWER;
-                d.xval[lvl] = 0.0;
-            } else {
-                const bool at_lower = lb_.g > 0.0;
-                d.vstat[lvl] = at_lower ? VS_LOWER : VS_UPPER;
-                d.xval[lvl] = at_lower ? d.lb[lvl] : d.ub[lvl];
-            }
-            d.vstat[ql] = VS_BASIC;
-            u.bpos[lvl] = -1;
-            u.bpos[ql] = lpos;
-            u.head[lpos] = q;
-            u.xB[lpos] = xq;
-            c->since_refactor++;
-        }
-        // the eta: alpha's nonzeros except the pivot, ascending position
-        // (thread t compacts the contiguous run [t C, (t + 1) C))
-        const int C = (m + LU_NT - 1) / LU_NT;
-        const int p0 = tid * C, p1 = min(m, p0 + C);
-        int cnt = 0;
-        for (int p = p0; p < p1; ++p) cnt += (p != lpos && x[p] != 0.0);
-        s_cnt[tid] = cnt;
-        __syncthreads();
-        if (tid == 0) {  // exclusive scan of the counts
-            int acc = 0;
-            for (int t = 0; t < LU_NT; ++t) {
-                const int v = s_cnt[t];
-                s_cnt[t] = acc;
-                acc += v;
-            }
-            const int ne = c->lu_ne;
-            const int64_t enz = c->lu_enz;
-            u.epiv[ne] = lpos;
-            u.epv[ne] = x[lpos];
-            u.ep[ne + 1] = enz + acc;
-            if (ne == 0) u.ep[0] = 0;
-        }
-        __syncthreads();
-        const int64_t base = c->lu_enz + s_cnt[tid];
-        int at = 0;
-        for (int p = p0; p < p1; ++p)
-            if (p != lpos && x[p] != 0.0) {
-                u.ei[base + at] = p;
-                u.ev[base + at] = x[p];
-                at++;
-            }
-        __syncthreads();
-        if (tid == 0) {
-            const int ne = c->lu_ne;
-            c->lu_enz = u.ep[ne + 1];
-            if (c->lu_enz > c->lu_enz_max) c->lu_enz_max = c->lu_enz;
-            c->lu_ne = ne + 1;
-        }
-        __syncthreads();
-    }
-    if (tid < 64) lu_looptop(d, u, phase);
-}
-
-// head / bpos / xB from the initial cover (k_init_rows); every structural nonbasic
-__global__ void k_lu_init(Dev d, LuDev u) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < d.n + 2 * d.m) u.bpos[i] = -1;
-    if (i < d.m) {
-        const int v = d.cover[i];
-        u.head[i] = v;
-        u.xB[i] = d.xr[i];
-    }
-}
-__global__ void k_lu_init_bpos(Dev d, LuDev u) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < d.m) u.bpos[loc_of(d, u.head[i])] = i;
-}
-
-// refactor: acol_i = (b_i - ract_i) - x_slack (slack nonbasic)
-__global__ void k_lu_rhs(Dev d, LuDev u) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= d.m) return;
-    double r = d.b[i] - d.ract[i];
-    const int sv = d.n + i;
-    if (d.vstat[sv] != VS_BASIC) r = r - d.xval[sv];
-    u.acol[i] = r;
-}
-
-// xB = B^-1 acol on fresh factors (no etas)
-template <bool LDS>
-__global__ void __launch_bounds__(LU_NT) k_lu_xb(Dev d, LuDev u) {
-    extern __shared__ __attribute__((aligned(16))) double lu_lds[];
-    double* x = lu_vec<LDS>(u, lu_lds);
-    const int m = u.m;
-    for (int s = threadIdx.x; s < m; s += LU_NT) x[s] = u.acol[u.prow[s]];
-    __syncthreads();
-    lu_sched_solve(u.sL, nullptr, x);
-    lu_sched_solve(u.sU, u.ud, x);
-    for (int s = threadIdx.x; s < m; s += LU_NT) u.xB[u.pcol[s]] = x[s];
-}
-
-__global__ void k_lu_phase2(Dev d) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < d.m) {
-        const int av = d.n + d.m + t;
-        d.cost[av] = 0.0;
-        d.lb[av] = 0.0;
-        d.ub[av] = 0.0;
-    }
-    if (t < d.n) d.cost[t] = d.maximize ? -d.obj[t] : d.obj[t];
-}
-
-__global__ void k_lu_extract(Dev d, LuDev u, double* __restrict__ xout) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= d.n) return;
-    xout[j] = d.vstat[j] == VS_BASIC ? u.xB[u.bpos[j]] : d.xval[j];
-}
-
-static size_t lu_lds_bytes(const LuDev& u) { return u.lds ? (size_t)u.m * sizeof(double) : 0; }
-
-int lu_lds_max_m() {
-    static int cached = -1;
-    if (cached >= 0) return cached;
-    int dev = 0, lim = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&lim, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess)
-        lim = 65536;
-    // (the kernels' static LDS -- reductions, counts -- stays below 4 KiB)
-    const int bytes = lim - 4096;
-    const void* fns[] = {(const void*)k_lu_btran<true>, (const void*)k_lu_iter<true>, (const void*)k_lu_xb<true>};
-    for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-    (void)hipGetLastError();
-    cached = bytes > 0 ? bytes / (int)sizeof(double) : 0;
-    return cached;
-}
-
-hipError_t launch_lu_iteration(const Dev& d, const LuDev& u, int phase, hipStream_t st) {
-    const int nts = (int)cdiv(d.n, TILE_COLS), ntr = (int)cdiv(d.m > 0 ? d.m : 1, TILE_COLS);
-    const size_t lb = lu_lds_bytes(u);
-    if (u.lds) hipLaunchKernelGGL(k_lu_btran<true>, dim3(1), dim3(LU_NT), lb, st, d, u);
-    else hipLaunchKernelGGL(k_lu_btran<false>, dim3(1), dim3(LU_NT), 0, st, d, u);
-    hipLaunchKernelGGL(k_lu_price, dim3(nts + ntr), dim3(TILE_COLS), 0, st, d, u, nts);
-    if (u.lds) hipLaunchKernelGGL(k_lu_iter<true>, dim3(1), dim3(LU_NT), lb, st, d, u, nts + ntr, phase);
-    else hipLaunchKernelGGL(k_lu_iter<false>, dim3(1), dim3(LU_NT), 0, st, d, u, nts + ntr, phase);
-    return hipGetLastError();
-}
-
-hipError_t launch_lu_looptop(const Dev& d, const LuDev& u, int phase, hipStream_t st) {
-    hipLaunchKernelGGL(k_lu_looptop, dim3(1), dim3(64), 0, st, d, u, phase);
-    return hipGetLastError();
-}
-
-hipError_t launch_lu_init(const Dev& d, const LuDev& u, hipStream_t st) {
-    const int64_t nv = (int64_t)d.n + 2 * (int64_t)d.m;
-    k_lu_init<<<cdiv(nv > 0 ? nv : 1, 256), 256, 0, st>>>(d, u);
-    if (d.m > 0) k_lu_init_bpos<<<cdiv(d.m, 256), 256, 0, st>>>(d, u);
-    return hipGetLastError();
-}
-
-hipError_t launch_lu_xb(const Dev& d, const LuDev& u, hipStream_t st) {
-    if (d.m <= 0) return hipSuccess;
-    k_lu_rhs<<<cdiv(d.m, 256), 256, 0, st>>>(d, u);
-    if (u.lds) hipLaunchKernelGGL(k_lu_xb<true>, dim3(1), dim3(LU_NT), lu_lds_bytes(u), st, d, u);
-    else hipLaunchKernelGGL(k_lu_xb<false>, dim3(1), dim3(LU_NT), 0, st, d, u);
-    return hipGetLastError();
-}
-
-hipError_t launch_lu_phase2(const Dev& d, hipStream_t st) {
-    const int64_t mx = d.m > d.n ? d.m : d.n;
-    k_lu_phase2<<<cdiv(mx > 0 ? mx : 1, 256), 256, 0, st>>>(d);
-    return hipGetLastError();
-}
-
-hipError_t launch_lu_extract(const Dev& d, const LuDev& u, double* xout, hipStream_t st) {
-    k_lu_extract<<<cdiv(d.n, 256), 256, 0, st>>>(d, u, xout);
-    return hipGetLastError();
-}
-
 }  // namespace elp

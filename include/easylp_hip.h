@@ -115,11 +115,10 @@ typedef struct elp_control {
                                 unit columns + the explicit inverse of the
                                 structural bump (k basic structurals: O(m k +
                                 k^2) device memory, grown with k);
-                                ELP_BASIS_LU (CSC input only): a Markowitz LU of
-                                the whole basis at each refactor plus a
-                                product-form eta file, O(nnz(L+U) + etas) device
-                                memory (the role LUSOL plays for lp_solve);
-                                latency-bound on the GPU */
+                                ELP_BASIS_LU: refused (ELP_E_UNSUPPORTED) -- the
+                                r03-r04 sparse-LU engine measured 150x slower
+                                than the bump inverse and was removed in r05
+                                 */
     int32_t simplex;         /* lp.control(simplextype = ...), lp_solve's
                                 set_simplextype numbering: ELP_SIMPLEX_DUAL_PRIMAL
                                 (6) -- phase 1 by the dual simplex when the slack
@@ -185,10 +184,10 @@ typedef struct elp_stats {
     double seconds_h2d;        /* elp_load_dense: host -> device copy of A     */
     double h2d_bytes;          /* bytes of A read from host memory (once, also
                                   when several devices receive them)            */
-    int64_t lu_nnz;            /* ELP_BASIS_LU: largest nnz(L) + nnz(U) + m    */
-    int64_t eta_nnz;           /* ELP_BASIS_LU: largest eta-file nonzeros      */
+    int64_t lu_nnz;            /* reserved (0; the removed sparse-LU engine)   */
+    int64_t eta_nnz;           /* reserved (0)                                 */
     int32_t basis;             /* the representation the last load used
-                                  (ELP_BASIS_INVERSE or ELP_BASIS_LU)           */
+                                  (ELP_BASIS_INVERSE)                           */
     int32_t simplex;           /* the phase-1 method the last solve ran
                                   (ELP_SIMPLEX_DUAL_PRIMAL / _PRIMAL_PRIMAL)    */
     double exchange_rtt_us;    /* peer mailbox (exchange 1): one exchange round
@@ -240,8 +239,7 @@ int elp_load_dense_device_multi(elp_handle* h, const double* const* dA, int32_t 
                                 int32_t maximize);
 
 /* Sparse A in compressed sparse columns (BASELINE config 5;
- * elp_control.basis = ELP_BASIS_LU keeps a sparse LU of the basis instead of
- * the bump inverse; sensitivity then needs ELP_BASIS_INVERSE):
+ * the bump inverse with hypersparse FTRAN / B^-1 rows):
  * colptr[n+1] (colptr[0] = 0, colptr[n] = nnz), rowind[nnz] strictly increasing
  * within each column, val[nnz] finite.  Same problem semantics as
  * elp_load_dense; pricing then sweeps the nonzeros (12 bytes each) instead of

@@ -107,11 +107,6 @@ def load():
     lib.orc_scale_factors.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
                                       ctypes.c_void_p, ctypes.c_void_p]
     vp, i64 = ctypes.c_void_p, ctypes.c_int64
-    lib.orc_solve_lu.restype = ctypes.c_int
-    lib.orc_solve_lu.argtypes = [i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int32, P(OrcControl),
-                                 vp, vp, vp, vp, vp, i64, P(OrcStats)]
-    lib.orc_lu_factor.restype = ctypes.c_int
-    lib.orc_lu_factor.argtypes = [i64, i64, vp, vp, vp, vp, ctypes.c_double, vp, vp, vp, vp, vp, vp]
     lib.orc_generate_rows.restype = None
     lib.orc_generate_rows.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                                       ctypes.c_int64, ctypes.c_void_p]
@@ -173,63 +168,6 @@ def solve_dense(A, dir, rhs, obj, lo=None, up=None, maximize=False, trace_cap=0,
               "dualsfrom": sbuf[3 * n + m:4 * n + 2 * m], "dualstill": sbuf[4 * n + 2 * m:]}
     return OracleResult(status, objval.value, x, y[:m], basis[:m],
                         trace[: 2 * it].reshape(-1, 2), stats, sd)
-
-
-def solve_lu(colptr, rowind, val, dir, rhs, obj, lo=None, up=None, maximize=False, trace_cap=0, **ctl):
-    """orc_solve_lu: the sparse-LU engine of the CSC path (elp_oracle_lu.c) on
-    CSC arrays (rows ascending within a column)."""
-    lib = load()
-    colptr = np.ascontiguousarray(colptr, dtype=np.int64)
-    n = colptr.shape[0] - 1
-    rowind = np.ascontiguousarray(rowind, dtype=np.int32)
-    val = np.ascontiguousarray(val, dtype=np.float64)
-    obj = np.ascontiguousarray(obj, dtype=np.float64)
-    rhs = np.ascontiguousarray(rhs, dtype=np.float64).reshape(-1)
-    m = rhs.shape[0]
-    dir = np.ascontiguousarray(dir, dtype=np.int32).reshape(-1)
-    lo = np.zeros(n) if lo is None else np.ascontiguousarray(lo, dtype=np.float64)
-    up = np.full(n, np.inf) if up is None else np.ascontiguousarray(up, dtype=np.float64)
-    c = OrcControl()
-    lib.orc_default_control(ctypes.byref(c))
-    for key, v in ctl.items():
-        setattr(c, key, v)
-    x = np.zeros(n)
-    y = np.zeros(max(m, 1))
-    basis = np.zeros(max(m, 1), dtype=np.int64)
-    trace = np.full(2 * max(trace_cap, 1), -2, dtype=np.int64)
-    objval = ctypes.c_double(0.0)
-    st = OrcStats()
-    status = lib.orc_solve_lu(m, n, colptr.ctypes.data, _ptr(rowind), _ptr(val), _ptr(dir) if m else None,
-                              _ptr(rhs) if m else None, obj.ctypes.data, lo.ctypes.data, up.ctypes.data,
-                              int(bool(maximize)), ctypes.byref(c), ctypes.addressof(objval), x.ctypes.data,
-                              y.ctypes.data, basis.ctypes.data, trace.ctypes.data if trace_cap else None,
-                              trace_cap, ctypes.byref(st))
-    if status < 0:
-        raise ValueError(f"orc_solve_lu usage error {status}")
-    stats = {f: getattr(st, f) for f, _ in OrcStats._fields_}
-    it = min(stats["iterations"], trace_cap)
-    return OracleResult(status, objval.value, x, y[:m], basis[:m], trace[: 2 * it].reshape(-1, 2), stats, None)
-
-
-def lu_factor(colptr, rowind, val, m, head, tol_singular=1e-13):
-    """orc_lu_factor: (prow, pcol, udiag, (nnzL, nnzU), (lsum, usum)) or None if singular."""
-    lib = load()
-    colptr = np.ascontiguousarray(colptr, dtype=np.int64)
-    n = colptr.shape[0] - 1
-    rowind = np.ascontiguousarray(rowind, dtype=np.int32)
-    val = np.ascontiguousarray(val, dtype=np.float64)
-    head = np.ascontiguousarray(head, dtype=np.int64)
-    prow = np.zeros(max(m, 1), np.int64)
-    pcol = np.zeros(max(m, 1), np.int64)
-    ud = np.zeros(max(m, 1))
-    nz = np.zeros(2, np.int64)
-    ls, us = ctypes.c_double(0), ctypes.c_double(0)
-    rc = lib.orc_lu_factor(m, n, colptr.ctypes.data, _ptr(rowind), _ptr(val), head.ctypes.data, tol_singular,
-                           prow.ctypes.data, pcol.ctypes.data, ud.ctypes.data, nz.ctypes.data,
-                           ctypes.addressof(ls), ctypes.addressof(us))
-    if rc:
-        return None
-    return prow[:m], pcol[:m], ud[:m], tuple(int(v) for v in nz), (ls.value, us.value)
 
 
 def generate_dense(seed, m, n, col0=0, ncols=None, want_A=True):

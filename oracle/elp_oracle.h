@@ -69,8 +69,8 @@ typedef struct orc_stats {
     int64_t gj_refactors;  /* refactors that fell back to Gauss-Jordan      */
     int64_t devex_resets;  /* Devex reference-framework restarts            */
     double max_inv_resid;  /* largest max|I - M Minv| a refactor measured    */
-    int64_t lu_nnz;        /* orc_solve_lu: largest nnz(L) + nnz(U) + m      */
-    int64_t eta_nnz;       /* orc_solve_lu: largest eta-file nonzeros         */
+    int64_t lu_nnz;        /* (reserved: the r03-r04 sparse-LU restatement)   */
+    int64_t eta_nnz;       /* (reserved)                                       */
     int64_t dual_iterations; /* phase-1 iterations of the dual simplex        */
     int64_t flattened;     /* columns whose cost the dual phase zeroed        */
 } orc_stats;
@@ -131,21 +131,6 @@ void orc_generate_dense(uint64_t seed, int64_t m, int64_t n, int64_t col0,
 void orc_scale_factors(int64_t m, int64_t n, const double* A, int32_t mode, int32_t* rho, int32_t* gam);
 
 /* Rows rows[0..nrows) of the same instance, row-major (out[r * n + j]). */
-/* The sparse-LU engine of the CSC path (elp_oracle_lu.c; the HIP side's
- * elp_control.basis = ELP_BASIS_LU): CSC input (colptr[n+1], rowind rows
- * ascending per column, val), the rest as orc_solve_dense.  Pricing is the
- * column chain (price_mode 1); ctl->refactor_mode is unused. */
-int orc_solve_lu(int64_t m, int64_t n, const int64_t* colptr, const int32_t* rowind, const double* val,
-                 const int32_t* dir, const double* rhs, const double* obj, const double* lo, const double* up,
-                 int32_t maximize, const orc_control* ctl, double* objval, double* x, double* y,
-                 int64_t* basis, int64_t* trace, int64_t trace_cap, orc_stats* st);
-
-/* Its Markowitz factorization alone (tests): pivot rows / positions and the
- * U diagonal per step, nnz(L), nnz(U) and order-sensitive value checksums. */
-int orc_lu_factor(int64_t m, int64_t n, const int64_t* colptr, const int32_t* rowind, const double* val,
-                  const int64_t* head, double tol_singular, int64_t* prow, int64_t* pcol, double* ud,
-                  int64_t* nnz_lu, double* lsum, double* usum);
-
 void orc_generate_rows(uint64_t seed, int64_t m, int64_t n, const int64_t* rows, int64_t nrows,
                        double* out);
 

@@ -1,5 +1,5 @@
-"""Fixtures of the sparse-LU engine (tests/test_gpu_lu.py, bench.py's sparse
-config): generator specs plus the optimum each is pinned to.
+"""Fixtures of the Netlib-scale CSC LPs (tests/test_gpu_basis.py, test_gpu_dual.py,
+bench.py's sparse config): generator specs plus the optimum each is pinned to.
 
   packing_2000x10000   easylp_amd.synth.sparse_packing(1, 2000, 10000, 5):
                        HiGHS dual simplex optimum (scipy.optimize.linprog,

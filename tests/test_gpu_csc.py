@@ -124,13 +124,12 @@ def test_mps_file_through_csc(gpu, tmp_path):
     easylp_amd.mps and solved on the GPU: same pivots as the oracle."""
     from easylp_amd.mps import read_mps, solve_mps
     from easylp_amd.solver import csc_arrays
-    from oracle import solve_lu
+    from oracle import solve_dense as orc
     from test_mps import TEXT
     f = tmp_path / "t.mps"
     f.write_text(TEXT)
-    p, g = solve_mps(str(f))  # (CSC input: the sparse-LU basis by default)
-    cp, ri, v, _ = csc_arrays(p.dense())
-    o = solve_lu(cp, ri, v, p.dirs, p.rhs, p.obj, p.lo, p.up, p.maximize)
+    p, g = solve_mps(str(f))  # (CSC input)
+    o = orc(p.dense(), p.dirs, p.rhs, p.obj, p.lo, p.up, p.maximize, price_mode=1)
     assert g.status == o.status == 0
     assert g.objval == o.objval
     np.testing.assert_array_equal(g.basis, o.basis)
