@@ -2154,56 +2154,39 @@ DEV void zr_snapshot(const Dev& d, int k, int q) {
     cw->snap_rllast = last >= 0 ? d.Rl[last] : -1;
 }
 
-// CSC input (one GPU): z_i = A[i, S] x_S on a covered row from the row's
-// nonzeros in basic columns (CSR + Dev::spos) -- in bump-position order with
-// the oracle's zchunk grouping (an fma chain per 32-position chunk, the chunk
-// sums added in order): the zero entries the dense AS walk adds change no bit,
-// so this is the dense result at O(nnz of the row) instead of O(k).  A row
-// with more than SPZ_MAX basic entries walks AS densely instead.
-constexpr int SPZ_MAX = 16;
-DEV double csr_zrow(const Dev& d, int i, int k, const double* __restrict__ xs) {
-    int pp[SPZ_MAX];
-    double vv[SPZ_MAX];
+constexpr int SPZ_MAX = 16;  // basic entries of a row the CSC row walk keeps (more: the dense AS walk)
+
+// Row i's entries in basic columns (CSR + spos) as (bump position, value),
+// sorted by position: the row's extent r0 / r1 comes preloaded, ZB entries'
+// column / value loads go out together and then their spos loads (two
+// dependent round trips for a row of <= ZB nonzeros).  *over: more than
+// SPZ_MAX basic entries (the caller walks AS densely).
+constexpr int ZB = 32;
+DEV int csr_basic(const Dev& d, int64_t r0, int64_t r1, int* pp, double* vv, bool* over) {
     int cnt = 0;
-    bool over = false;
-    const int64_t t1 = d.rptr[i + 1];
-#ifndef ELP_SPZ_G
-#define ELP_SPZ_G 16
-#endif
-    constexpr int G = ELP_SPZ_G;  // entries whose loads are in flight together
-    for (int64_t t0 = d.rptr[i]; t0 < t1 && !over; t0 += G) {
-        int jj[G], ps[G];
-        double vr[G];
+    *over = false;
+    for (int64_t t0 = r0; t0 < r1 && !*over; t0 += ZB) {
+        int jj[ZB], ps[ZB];
+        double vr[ZB];
 #pragma unroll
-        for (int u = 0; u < G; ++u) {
-            const int64_t tt = t0 + u < t1 ? t0 + u : t1 - 1;
+        for (int u = 0; u < ZB; ++u) {
+            const int64_t tt = t0 + u < r1 ? t0 + u : r1 - 1;
             jj[u] = d.cind[tt];
             vr[u] = d.rval[tt];
         }
 #pragma unroll
-        for (int u = 0; u < G; ++u) ps[u] = d.spos[jj[u]];
+        for (int u = 0; u < ZB; ++u) ps[u] = d.spos[jj[u]];
 #pragma unroll
-        for (int u = 0; u < G; ++u) {
-            if (t0 + u >= t1 || ps[u] < 0) continue;
+        for (int u = 0; u < ZB; ++u) {
+            if (t0 + u >= r1 || ps[u] < 0) continue;
             if (cnt == SPZ_MAX) {
-                over = true;
+                *over = true;
                 break;
             }
             pp[cnt] = ps[u];
             vv[cnt] = vr[u];
             ++cnt;
         }
-    }
-    double z = 0.0;
-    if (over) {
-        const size_t m = (size_t)d.m;
-        for (int c0 = 0; c0 < k; c0 += ZCHUNK) {
-            double acc = 0.0;
-            const int c1 = min(k, c0 + ZCHUNK);
-            for (int p = c0; p < c1; ++p) acc = fma(d.AS[(size_t)p * m + i], xs[p], acc);
-            z = z + acc;
-        }
-        return z;
     }
     for (int a = 1; a < cnt; ++a) {  // insertion sort by position (a handful of entries)
         const int p = pp[a];
@@ -2216,6 +2199,24 @@ DEV double csr_zrow(const Dev& d, int i, int k, const double* __restrict__ xs) {
         }
         pp[b + 1] = p;
         vv[b + 1] = v;
+    }
+    return cnt;
+}
+// z = A[i, S] xs from csr_basic's entries in the oracle's zchunk order (an fma
+// chain per 32-position chunk, the chunk sums added in order from 0) -- the
+// dense AS walk's bits (its zero terms change nothing); over: the dense walk
+DEV double zrow_chain(const Dev& d, int i, int k, const int* pp, const double* vv, int cnt, bool over,
+                      const double* __restrict__ xs) {
+    double z = 0.0;
+    if (over) {
+        const size_t m = (size_t)d.m;
+        for (int c0 = 0; c0 < k; c0 += ZCHUNK) {
+            double acc = 0.0;
+            const int c1 = min(k, c0 + ZCHUNK);
+            for (int p = c0; p < c1; ++p) acc = fma(d.AS[(size_t)p * m + i], xs[p], acc);
+            z = z + acc;
+        }
+        return z;
     }
     double xv[SPZ_MAX];  // the x values, all loads in flight before the chain
 #pragma unroll
@@ -2237,21 +2238,47 @@ DEV double csr_zrow(const Dev& d, int i, int k, const double* __restrict__ xs) {
     return z;
 }
 
-// FTRAN-z + Harris pass 1 for CSC input: row tiles of 64 rows (one per lane,
-// csr_zrow), then bump tiles of 64 positions, then the snapshot workgroup --
-// k_ftran_zr's regions and minima with one wave per tile (zw = 1)
-// flip (the dual phase): the bound flips' x_B update rides along -- covered rows
-// x -= sigma (a_F,i - A[i, S] fS) by a row walk in nrt extra waves, bump
-// positions x -= fS (k_dual_flip_apply's arithmetic); the dual leaves on
-// k_dual_row's row, so no primal pass 1 runs.  Until r04 a launch of its own
-// (k_dual_flip_apply_sp, ~22 us per dual pivot at 20 000 x 100 000)
+// FTRAN-z + Harris pass 1 for CSC input: row tiles of 64 rows (one per lane:
+// csr_basic + zrow_chain), then bump tiles of 64 positions, then the snapshot
+// workgroup -- k_ftran_zr's regions and minima with one wave per tile (zw = 1).
+// Everything that depends on neither the control block nor this iteration's
+// decision (the row extent, cover, the entering column's and a_F's entry) is
+// loaded before the status test.
+// flip (the dual phase): the bound flips' x_B update rides along -- a covered
+// row's lane also forms A[i, S] fS from the same entries and updates
+// x -= sigma (a_F,i - A[i, S] fS); bump positions x -= fS (k_dual_flip_apply's
+// arithmetic); the dual leaves on k_dual_row's row, so no primal pass 1 runs.
+// (r04: the flips' row walk in waves of its own; until then a launch of its own)
 __global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt, int flip) {
     const DevCtl* c = d.ctl;
     const int32_t st0 = c->status;
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) d.ctl->snap_status = st0;  // for k_ratio
-    if (st0 != ST_RUN) return;
-    const int k = c->k, q = c->q, bland = c->bland, m = d.m, lane = threadIdx.x;
+    int k = c->k, q = c->q;
+    const int bland = c->bland, m = d.m, lane = threadIdx.x;
     const double sig = c->sig, ptol = c->tol_primal, pivtol = c->tol_pivot;
+    const int nfl = c->nflip;
+    const bool roww = (int)blockIdx.x < nrt;
+    const int i = roww ? (int)blockIdx.x * 64 + lane : 0;
+    const int ic = i < m ? i : (m > 0 ? m - 1 : 0);
+    int64_t r0 = 0, r1 = 0;
+    int u = -1;
+    double qi = 0.0, afi = 0.0;
+    if (m > 0) {  // (straight-line, masked at use)
+        r0 = d.rptr[ic];
+        r1 = d.rptr[ic + 1];
+        u = d.cover[ic];
+        qi = d.qcol[ic];
+        afi = d.aF ? d.aF[ic] : 0.0;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" : "+v"(k), "+v"(q));
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) d.ctl->snap_status = st0;  // for k_ratio
+    if (st0 != ST_RUN) {
+        KEEP(r0);
+        KEEP(u);
+        KEEP(qi);
+        KEEP(afi);
+        return;
+    }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         d.ctl->snap_k = k;
         d.ctl->snap_bland = bland;
@@ -2260,31 +2287,26 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt, int flip) {
         if (threadIdx.x == 0) zr_snapshot(d, k, q);
         return;
     }
-    const bool fl = flip && c->nflip > 0;
-    if (flip && (int)blockIdx.x >= (int)gridDim.x - 1 - nrt) {  // the flip update's row waves
-        if (!fl) return;
-        const int i = (blockIdx.x - (gridDim.x - 1 - nrt)) * 64 + lane;
-        const int u = i < m ? d.cover[i] : -1;
-        if (u >= 0) {
-            const double tot = csr_zrow(d, i, k, d.fS);
-            d.xr[i] = d.xr[i] - unit_sign(d, u, i) * (d.aF[i] - tot);
-        }
-        return;
-    }
-    // (flip: the dual phase leaves with k_dual_row's row -- no primal pass 1,
-    //  and x_B is being updated beside this)
+    const bool fl = flip && nfl > 0;
     double tmin = HUGE_VAL, ge = 0.0, xe = 0.0, le = 0.0, he = 0.0;
     int ve = -1, e = 0, region;
-    if ((int)blockIdx.x < nrt) {
-        const int i = blockIdx.x * 64 + lane;
+    if (roww) {
         e = i;
         region = blockIdx.x;
-        const int u = i < m ? d.cover[i] : -1;
-        if (u >= 0) {
-            const double z = csr_zrow(d, i, k, d.alS);
-            const double aiq = q >= d.N ? (i == q - d.N ? 1.0 : 0.0) : d.qcol[i];
-            const double alU = unit_sign(d, u, i) * (aiq - z);
+        if (i < m && u >= 0) {
+            int pp[SPZ_MAX];
+            double vv[SPZ_MAX];
+            bool over;
+            const int cnt = csr_basic(d, r0, r1, pp, vv, &over);
+            const double z = zrow_chain(d, i, k, pp, vv, cnt, over, d.alS);
+            const double aiq = q >= d.N ? (i == q - d.N ? 1.0 : 0.0) : qi;
+            const double sg = unit_sign(d, u, i);
+            const double alU = sg * (aiq - z);
             d.alU[i] = alU;
+            if (fl) {
+                const double tot = zrow_chain(d, i, k, pp, vv, cnt, over, d.fS);
+                d.xr[i] = d.xr[i] - sg * (afi - tot);
+            }
             if (!flip) {
                 ge = sig * alU;
                 xe = d.xr[i];
@@ -5483,7 +5505,7 @@ static void update_grid(const Dev& d, int k_ub, bool with_ar, unsigned* nb_minv,
     *nb = *nb_minv + nb_copy;
 }
 
-// CSC: A[i, S] v from the rows' nonzeros (csr_zrow) once the dense walk over AS
+// CSC: A[i, S] v from the rows' nonzeros (csr_basic + zrow_chain) once the dense walk over AS
 // would stream more than ELP_SPZ_MIN_MB (16) MB -- below that the dense walk's
 // independent loads beat the row walk's dependent ones (1000 x 10 000 packing
 // LP, k <= 877: 0.53 s dense against 0.85 s sparse, r04m)
@@ -5618,7 +5640,7 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     const bool als = !no_als && ldsz && k_ub > 2 * zw * ZCHUNK && k_ub <= ZR_PA * 64 * zw && lds_als <= 64 * 1024;
     if (spz) {
         // (the dual phase: + nrt waves for the flips' x_B update, before the snapshot one)
-        k_ftran_zr_sp<<<nrt + nbt + (phase == 3 ? nrt : 0) + 1, 64, 0, st>>>(d, nrt, phase == 3 ? 1 : 0);
+        k_ftran_zr_sp<<<nrt + nbt + 1, 64, 0, st>>>(d, nrt, phase == 3 ? 1 : 0);
     } else {
         // + 1: the snapshot workgroup
         if (als) {
