@@ -629,6 +629,13 @@ static int alloc_all_body(elp_handle* h) {
         }();
         d.dual_defer = dd && h->comm.kind == 0 ? 1 : 0;
     }
+    {  // CSC: no MinvT (ELP_CSC_MINVT=1 keeps it, A/B)
+        static const bool keep = [] {
+            const char* s = std::getenv("ELP_CSC_MINVT");
+            return s && std::atoi(s) != 0;
+        }();
+        d.noT = h->csc && !keep ? 1 : 0;
+    }
     // the mailbox carries the min-loc record only: with A not replicated the
     // entering column must travel, so that load uses the collective
     d.p2p = h->comm.p2p && h->replicated ? 1 : 0;
@@ -653,7 +660,7 @@ static int alloc_all_body(elp_handle* h) {
     const size_t msq = (size_t)h->kcap * (size_t)h->kcap;
     A(dalloc(&d.AS, (size_t)mm * (size_t)h->kcap));
     A(dalloc(&d.Minv, msq));
-    A(dalloc(&d.MinvT, msq));
+    if (!d.noT) A(dalloc(&d.MinvT, msq));
     A(dalloc(&d.cS, mm));
     A(dalloc(&d.slo, mm));
     A(dalloc(&d.shi, mm));
@@ -778,7 +785,7 @@ static int alloc_all_body(elp_handle* h) {
     //  results are discarded, so AR needs no clearing); Minv / work start clean
     A(hipMemsetAsync(d.rcnt, 0, (size_t)d.rregs * sizeof(int32_t), h->st));
     A(hipMemsetAsync(d.Minv, 0, msq * sizeof(double), h->st));
-    A(hipMemsetAsync(d.MinvT, 0, msq * sizeof(double), h->st));
+    if (d.MinvT) A(hipMemsetAsync(d.MinvT, 0, msq * sizeof(double), h->st));
     if (d.qcol) A(hipMemsetAsync(d.qcol, 0, (size_t)mm * sizeof(double), h->st));
     // index lists: entries past k / |Y| are read speculatively (and discarded):
     // start them at -1 rather than whatever the allocator hands out
@@ -830,7 +837,7 @@ static int ensure_k(elp_handle* h, int64_t need) {
     double *as = nullptr, *mi = nullptr, *mt = nullptr, *zp = nullptr;
     hipError_t e = dalloc(&as, (size_t)mm * (size_t)cap);
     if (e == hipSuccess) e = dalloc(&mi, (size_t)cap * (size_t)cap);
-    if (e == hipSuccess) e = dalloc(&mt, (size_t)cap * (size_t)cap);
+    if (e == hipSuccess && d.MinvT) e = dalloc(&mt, (size_t)cap * (size_t)cap);  // (none: CSC, d.noT)
     if (e == hipSuccess) e = dalloc(&zp, (size_t)(mm + 64) * (size_t)((cap + ZCHUNK - 1) / ZCHUNK + 1));
     if (e != hipSuccess) {
         for (double* p : {as, mi, mt, zp})
@@ -839,14 +846,15 @@ static int ensure_k(elp_handle* h, int64_t need) {
     }
     const size_t sq = (size_t)cap * (size_t)cap * sizeof(double);
     HIPCHK(hipMemsetAsync(mi, 0, sq, h->st));
-    HIPCHK(hipMemsetAsync(mt, 0, sq, h->st));
+    if (mt) HIPCHK(hipMemsetAsync(mt, 0, sq, h->st));
     if (k > 0) {
         HIPCHK(hipMemcpyAsync(as, d.AS, (size_t)k * (size_t)mm * sizeof(double), hipMemcpyDeviceToDevice, h->st));
         const size_t w = (size_t)k * sizeof(double);
         HIPCHK(hipMemcpy2DAsync(mi, (size_t)cap * sizeof(double), d.Minv, (size_t)h->kcap * sizeof(double), w,
                                 (size_t)k, hipMemcpyDeviceToDevice, h->st));
-        HIPCHK(hipMemcpy2DAsync(mt, (size_t)cap * sizeof(double), d.MinvT, (size_t)h->kcap * sizeof(double), w,
-                                (size_t)k, hipMemcpyDeviceToDevice, h->st));
+        if (mt)
+            HIPCHK(hipMemcpy2DAsync(mt, (size_t)cap * sizeof(double), d.MinvT, (size_t)h->kcap * sizeof(double), w,
+                                    (size_t)k, hipMemcpyDeviceToDevice, h->st));
     }
     HIPCHK(hipStreamSynchronize(h->st));
     for (double* p : {d.AS, d.Minv, d.MinvT, d.zpart}) retire(h, p);

@@ -320,7 +320,12 @@ struct Dev {
     // one GPU, dual phase: k_ratio's plan applied during the next iteration
     // (k_dual_chuzr, the pricing / ratio-test launches' trailing workgroups)
     // instead of by a k_update launch (ELP_DUAL_DEFER=0: the launch)
-    int32_t dual_defer, dd_pad;
+    int32_t dual_defer;
+    // CSC loads keep no MinvT (ELP_CSC_MINVT=1 restores it): every product
+    // that read a row of MinvT reads a column of Minv -- a handful of entries
+    // (sparse lists) or a gather -- and the per-pivot inverse update moves half
+    // the bytes; MinvT is then null
+    int32_t noT;
 };
 constexpr int AFL_SB = 1;    // afl: bucket starts [1, 66)
 constexpr int AFL_POS = 66;  // afl: positions [66, 66 + SPL)

@@ -371,6 +371,42 @@ DEV double sparse_lane_chain(const double* __restrict__ x, const int* lpos, cons
     }
     return acc;
 }
+// lane_chain / sparse_lane_chain over x(j) computed by a functor (the deferred
+// update's new inverse, minv_new)
+template <class F>
+DEV double lane_chain_f(F x, const double* y, int len) {
+    const int lane = threadIdx.x & 63;
+    double acc = 0.0;
+    for (int j0 = lane; j0 < len; j0 += 64 * 8) {
+        double v[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = x(min(j0 + 64 * t, len - 1));
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            if (j0 + 64 * t < len) acc = fma(v[t], y[j0 + 64 * t], acc);
+    }
+    return acc;
+}
+template <class F>
+DEV double sparse_lane_chain_f(F x, const int* lpos, const double* lval, const int* lsb) {
+    const int lane = threadIdx.x & 63;
+    const int s = lsb[lane], e = lsb[lane + 1];
+    double acc = 0.0;
+    for (int t0 = s; t0 < e; t0 += 4) {
+        double xv[4], vv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = t0 + u < e ? t0 + u : e - 1;
+            xv[u] = x(lpos[t]);
+            vv[u] = lval[t];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (t0 + u < e) acc = fma(xv[u], vv[u], acc);
+    }
+    return acc;
+}
+
 // Lane-bucketed list from one candidate entry per thread (NT threads; valid
 // entries carry distinct positions): compaction, rank by (p mod 64, p), bucket
 // starts.  lkey: NT ints of scratch.  Returns n (uniform); ends with a barrier.
@@ -875,10 +911,12 @@ DEV void btran_body(const Dev& d, int phase, const double* __restrict__ tv) {
         }
     }
     const int lane = threadIdx.x & 63;
+    // (row p of MinvT = column p of Minv: read with stride ldm when d.noT)
+    const int64_t ts = d.noT ? d.ldm : 1;
     for (int p = blockIdx.x * 4 + (threadIdx.x >> 6); p < k; p += gridDim.x * 4) {
-        const double* row = d.MinvT + (size_t)p * d.ldm;
+        const double* row = d.noT ? d.Minv + p : d.MinvT + (size_t)p * d.ldm;
         double acc = 0.0;
-        for (int q = lane; q < k; q += 64) acc = fma(row[q], tv[q], acc);
+        for (int q = lane; q < k; q += 64) acc = fma(row[q * ts], tv[q], acc);
         acc = wave_tree(acc);
         if (lane == 0) {
             const int i = d.Rl[p];
@@ -2161,7 +2199,18 @@ constexpr int SPZ_MAX = 16;  // basic entries of a row the CSC row walk keeps (m
 // column / value loads go out together and then their spos loads (two
 // dependent round trips for a row of <= ZB nonzeros).  *over: more than
 // SPZ_MAX basic entries (the caller walks AS densely).
-constexpr int ZB = 32;
+#ifndef ELP_ZB
+#define ELP_ZB 16
+#endif
+constexpr int ZB = ELP_ZB;
+// ELP_ZR_MERGE 1 (default): the flips' row walk in the same lane as alpha_U's,
+// from the same row entries (one set of row waves); 0: waves of their own
+// (r04's layout).  r05c A/B on the 20 000 x 100 000 phase-1 LP
+// (profiles/r05c_ab_zr_variants.txt): 24.4 us merged against 25.5 split, and
+// 28-31 us with 32 entries' loads per batch (ELP_ZB=32: 256 VGPRs)
+#ifndef ELP_ZR_MERGE
+#define ELP_ZR_MERGE 1
+#endif
 DEV int csr_basic(const Dev& d, int64_t r0, int64_t r1, int* pp, double* vv, bool* over) {
     int cnt = 0;
     *over = false;
@@ -2288,6 +2337,20 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt, int flip) {
         return;
     }
     const bool fl = flip && nfl > 0;
+    if (!ELP_ZR_MERGE && flip && (int)blockIdx.x >= (int)gridDim.x - 1 - nrt) {  // the flips' row waves
+        const int fi = (blockIdx.x - (gridDim.x - 1 - nrt)) * 64 + lane;
+        if (!fl || fi >= m) return;
+        const int fu = d.cover[fi];
+        if (fu >= 0) {
+            int pp[SPZ_MAX];
+            double vv[SPZ_MAX];
+            bool over;
+            const int cnt = csr_basic(d, d.rptr[fi], d.rptr[fi + 1], pp, vv, &over);
+            const double tot = zrow_chain(d, fi, k, pp, vv, cnt, over, d.fS);
+            d.xr[fi] = d.xr[fi] - unit_sign(d, fu, fi) * (d.aF[fi] - tot);
+        }
+        return;
+    }
     double tmin = HUGE_VAL, ge = 0.0, xe = 0.0, le = 0.0, he = 0.0;
     int ve = -1, e = 0, region;
     if (roww) {
@@ -2303,7 +2366,7 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt, int flip) {
             const double sg = unit_sign(d, u, i);
             const double alU = sg * (aiq - z);
             d.alU[i] = alU;
-            if (fl) {
+            if (ELP_ZR_MERGE && fl) {
                 const double tot = zrow_chain(d, i, k, pp, vv, cnt, over, d.fS);
                 d.xr[i] = d.xr[i] - sg * (afi - tot);
             }
@@ -2630,6 +2693,8 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
     __shared__ double dred[4];
     __shared__ Leave lred[4];
     __shared__ double s_wd;
+    __shared__ int s_lpos[SPL], s_lkey[SPL], s_lsb[72], s_lscan[4];  // (d.noT: A[lrow, S] as a sparse list)
+    __shared__ double s_lval[SPL];
     const int tid = threadIdx.x;
     const int col = blockIdx.x * 4 + (tid >> 6);
     const int lane = tid & 63;
@@ -2699,8 +2764,8 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
         rho_col = ld_clamp(d.rhoR, main_wg ? col : 0, k_ub);
 #pragma unroll
         for (int t = 0; t < PFT; ++t) trow[t] = 0.0;
-    } else {  // (AR-copy workgroups fetch row 0: harmless)
-        const double* row = d.MinvT + (size_t)(main_wg && col < k_ub ? col : 0) * d.ldm;
+    } else {  // (AR-copy workgroups fetch row 0: harmless; no MinvT: Minv, unused)
+        const double* row = (d.noT ? d.Minv : d.MinvT) + (size_t)(main_wg && col < k_ub ? col : 0) * d.ldm;
 #pragma unroll
         for (int t = 0; t < PFT; ++t) trow[t] = ld_clamp(row, lane + 64 * t, k_ub);
     }
@@ -2764,7 +2829,7 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
 #pragma unroll
         for (int t = 0; t < PFT; ++t) arow[t] = 0.0;
     } else {
-        const double* row = d.MinvT + (size_t)(apos_c >= 0 ? apos_c : 0) * d.ldm;
+        const double* row = (d.noT ? d.Minv : d.MinvT) + (size_t)(apos_c >= 0 ? apos_c : 0) * d.ldm;
 #pragma unroll
         for (int t = 0; t < PFT; ++t) arow[t] = ld_clamp(row, lane + 64 * t, k);
     }
@@ -2960,10 +3025,13 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
     int8_t t0_rowvs = VS_FIXED, t0_yvslast = VS_FIXED;
     {  // (straight-line; workgroup 0 uses them, the others discard them)
         const size_t rv = (size_t)(lposx >= 0 ? lposx : 0) * d.ldm, ra = (size_t)(apos >= 0 ? apos : 0) * d.ldm;
+        // (column a of Minv: row a of MinvT, or a gather with stride ldm without it)
+        const double* cab = d.noT ? d.Minv + (apos >= 0 ? apos : 0) : d.MinvT + ra;
+        const int64_t cas = d.noT ? d.ldm : 1;
 #pragma unroll
         for (int t = 0; t < PFV; ++t) {
             vr[t] = ld_clamp(d.Minv + rv, tid + 256 * t, k);
-            ca[t] = ld_clamp(d.MinvT + ra, tid + 256 * t, k);
+            ca[t] = cab[(int64_t)(tid + 256 * t < k ? tid + 256 * t : (k > 0 ? k - 1 : 0)) * cas];
         }
         t0_piv = d.Minv[rv + (apos >= 0 ? apos : 0)];
         t0_yposl = d.ypos[lrow_all >= 0 ? lrow_all : 0];
@@ -2985,6 +3053,45 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
             if (lane == 0) d.vvec[col] = vcol;
         }
         if (pcx == PC_D && tid == 0) s_wd = dq / (-(dxsig * rho_a));
+        __syncthreads();
+    } else if (d.noT && lrow_all >= 0 && k > 0 && !(ELP_BOOK_WG && lead && !(phase == 2 && pcx == PC_D))) {
+        // CSC without MinvT: A[lrow, S] as a sparse list from row lrow's CSR
+        // entries through spos (the bookkeeping's only spos store in cases B /
+        // D is q's, at position k: outside the list), each wave's chain over
+        // column col of Minv -- the dense chain's bits (sparse_lane_chain_f);
+        // a row with more than SPL entries walks the column with every term
+        const int64_t t0 = d.rptr[lrow_all], t1 = d.rptr[lrow_all + 1];
+        const bool sl = t1 - t0 <= SPL;
+        if (sl) {
+            bool valid = false;
+            int p = 0;
+            double v = 0.0;
+            if (tid < t1 - t0) {
+                v = d.rval[t0 + tid];
+                p = d.spos[d.cind[t0 + tid]];
+                valid = p >= 0 && p < k;
+            }
+            spl_build<256>(valid, p, v, s_lpos, s_lval, s_lsb, s_lkey, s_lscan);
+        } else {
+            double* asrow = lds_row ? asrow_lds : d.vrow;
+            for (int j = tid; j < k; j += 256) asrow[j] = d.AS[(size_t)j * (size_t)m + lrow_all];
+            __syncthreads();
+        }
+        const double* asrow = lds_row ? asrow_lds : d.vrow;
+        auto colchain = [&](int cc) {
+            auto xf = [&](int qq) { return d.Minv[(size_t)qq * d.ldm + cc]; };
+            return wave_tree(sl ? sparse_lane_chain_f(xf, s_lpos, s_lval, s_lsb) : lane_chain_f(xf, asrow, k));
+        };
+        if (col < k && main_wg) {
+            const double acc = colchain(col);
+            const double delta = unit_sign(d, best.var, lrow_all) * (sig * best.g);
+            vcol = q < d.N ? acc / delta : acc;
+            if (lane == 0) d.vvec[col] = vcol;
+        }
+        if (phase == 2 && pcx == PC_D && tid < 64) {  // vvec[a], redundantly per workgroup
+            const double acc = colchain(apos);
+            if (tid == 0) s_wd = dq / acc;
+        }
         __syncthreads();
     } else if (lrow_all >= 0 && k > 0 && !(ELP_BOOK_WG && lead && !(phase == 2 && pcx == PC_D))) {
         // huge bumps: every workgroup writes the same values to d.vrow (benign)
@@ -3080,10 +3187,11 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
         } else if (pc == PC_C) {
             for (int j = tid; j < k; j += 256) {
                 d.vrow[j] = d.Minv[(size_t)lposx * d.ldm + j] / piv;
-                d.colA[j] = d.MinvT[(size_t)apos * d.ldm + j];
+                d.colA[j] = d.noT ? d.Minv[(size_t)j * d.ldm + apos] : d.MinvT[(size_t)apos * d.ldm + j];
             }
         } else if (pc == PC_D) {
-            for (int j = tid; j < k; j += 256) d.colA[j] = d.MinvT[(size_t)apos * d.ldm + j];
+            for (int j = tid; j < k; j += 256)
+                d.colA[j] = d.noT ? d.Minv[(size_t)j * d.ldm + apos] : d.MinvT[(size_t)apos * d.ldm + j];
         }
     }
     // ---- pivot: bookkeeping, its stores split by destination over the four waves
@@ -3352,7 +3460,7 @@ DEV void apply_minv_seq(const Dev& d, const Plan& P, int64_t e0, int64_t estride
             }
         }
     }
-    if (e < 2 * nel) {  // MinvT element (j, i) = new Minv (i, j), f = e - nel = j kk + i
+    if (e < 2 * nel && !d.noT) {  // MinvT element (j, i) = new Minv (i, j), f = e - nel = j kk + i
         const int64_t f = e - nel;
         int64_t j = f / kk, i = f % kk;
         for (; e < 2 * nel; e += estride) {
@@ -3462,7 +3570,7 @@ DEV void apply_minv(const Dev& d, const Plan& P, int64_t e0, int64_t estride, bo
         // this thread's first MinvT element: the first e0 + t estride >= nel
         e0 += (nel - e0 + estride - 1) / estride * estride;
     }
-    if (e0 < 2 * nel) apply_minv_half<true, MINV_U>(d, P, e0, 2 * nel, estride, nel, kk);
+    if (e0 < 2 * nel && !d.noT) apply_minv_half<true, MINV_U>(d, P, e0, 2 * nel, estride, nel, kk);
 }
 
 // the primal update and the AS (/ AR) copies of a plan: thread t0 of tstride
@@ -3567,6 +3675,12 @@ DEV void apply_minv_part(const Dev& d, const Plan& P, int part, int64_t t0, int6
     const int kk = P.pcase == PC_B ? k + 1 : P.pcase == PC_C ? k - 1 : k;
     const int64_t nel = (int64_t)kk * kk;
     if (nel == 0 || t0 >= nel) return;
+    if (d.noT) {  // no MinvT: the two launches split Minv (rows [h, kk) here in part 0, [0, h) in part 1)
+        const int64_t h = (int64_t)(kk / 2) * kk;
+        if (part == 0) apply_minv_half<false, MINV_U>(d, P, h + t0, nel, tstride, 0, kk);
+        else if (t0 < h) apply_minv_half<false, MINV_U>(d, P, t0, h, tstride, 0, kk);
+        return;
+    }
     if (part == 0) apply_minv_half<false, MINV_U>(d, P, t0, nel, tstride, 0, kk);
     else apply_minv_half<true, MINV_U>(d, P, nel + t0, 2 * nel, tstride, nel, kk);
 }
@@ -3761,7 +3875,7 @@ __global__ void k_gj_final(Dev d, int k, const double* __restrict__ W) {
     const int a = (int)(e / k), cc = (int)(e % k);
     const double v = W[(size_t)d.perm[a] * k + cc];
     d.Minv[(size_t)a * d.ldm + d.perm[cc]] = v;
-    d.MinvT[(size_t)d.perm[cc] * d.ldm + a] = v;
+    if (!d.noT) d.MinvT[(size_t)d.perm[cc] * d.ldm + a] = v;
 }
 
 // rhs_i = (b_i - sum_{nz} a_ij x_j) - s_i  and a_R for the bump solve
@@ -3850,6 +3964,59 @@ __global__ void __launch_bounds__(256) k_ns_gemm(Dev d, int k) {
     }
 }
 
+// CSC: the same residual E = I - M Minv with M's row i = A[R_i, S] taken from
+// row R_i's CSR entries in basic columns (spos), ascending position: each
+// E[i][j] is k_ns_gemm<0>'s sequential fma chain over l without its zero terms
+// -- the same bits at O(nnz(M) k) instead of O(k^3).  One workgroup per row i,
+// a thread per column j (coalesced rows of Minv); a row with more than 256
+// basic entries runs every l.
+__global__ void __launch_bounds__(256) k_ns_resid_sp(Dev d, int k) {
+    __shared__ int s_l[256], s_scan[4];
+    __shared__ double s_v[256], red[4];
+    const int tid = threadIdx.x, i = blockIdx.x;
+    const int r = d.Rl[i];
+    const int64_t t0 = d.rptr[r], t1 = d.rptr[r + 1];
+    const bool sp = t1 - t0 <= 256;
+    int n = 0;
+    if (sp) {
+        int l = -1;
+        double v = 0.0;
+        if (tid < t1 - t0) {
+            v = d.rval[t0 + tid];
+            l = d.spos[d.cind[t0 + tid]];
+        }
+        const bool valid = l >= 0 && l < k;
+        int excl;
+        n = block_scan_excl<256>(valid ? 1 : 0, &excl, s_scan);
+        if (valid) s_l[excl] = l;
+        __syncthreads();
+        int rk = 0;
+        if (valid)
+            for (int t = 0; t < n; ++t) rk += s_l[t] < l ? 1 : 0;
+        __syncthreads();
+        if (valid) {
+            s_l[rk] = l;
+            s_v[rk] = v;
+        }
+        __syncthreads();
+    }
+    const size_t ldm = (size_t)d.ldm, m = (size_t)d.m;
+    double emax = 0.0;
+    for (int j = tid; j < k; j += 256) {
+        double acc = 0.0;
+        if (sp) {
+            for (int t = 0; t < n; ++t) acc = fma(s_v[t], d.Minv[(size_t)s_l[t] * ldm + j], acc);
+        } else {
+            for (int l = 0; l < k; ++l) acc = fma(d.AS[(size_t)l * m + r], d.Minv[(size_t)l * ldm + j], acc);
+        }
+        const double e = (i == j ? 1.0 : 0.0) - acc;
+        d.W0[(size_t)i * k + j] = e;
+        emax = fmax(emax, fabs(e));
+    }
+    const double am = block_max<256>(emax, red);
+    if (tid == 0) atomicMax(&d.ctl->ns_emax_bits, (unsigned long long)__double_as_longlong(am));
+}
+
 // Minv = W1, MinvT = W1^T (transposed through LDS, both stores coalesced)
 __global__ void __launch_bounds__(1024) k_ns_store(Dev d, int k) {
     __shared__ double T[32][33];
@@ -3863,7 +4030,7 @@ __global__ void __launch_bounds__(1024) k_ns_store(Dev d, int k) {
     T[ty][tx] = v;
     __syncthreads();
     const int ti = blockIdx.y * 32 + tx, tj = blockIdx.x * 32 + ty;  // MinvT[tj][ti]
-    if (ti < k && tj < k) d.MinvT[(size_t)tj * d.ldm + ti] = T[tx][ty];
+    if (ti < k && tj < k && !d.noT) d.MinvT[(size_t)tj * d.ldm + ti] = T[tx][ty];
 }
 
 // ============================================================== phase 2 / extract
@@ -4279,42 +4446,6 @@ __global__ void __launch_bounds__(256) k_dual_chuzr(Dev d, int defer) {
 // Minv row p for bump position p; -sigma (A[i,S] Minv)_c for the slack covering
 // row i (the oracle's row_times_minv in wave order).  Written in position order
 // (rhoR) and on the Y slots (rr, the dense sweep's operand).
-// lane_chain / sparse_lane_chain over x(j) computed by a functor (the deferred
-// update's new inverse, minv_new)
-template <class F>
-DEV double lane_chain_f(F x, const double* y, int len) {
-    const int lane = threadIdx.x & 63;
-    double acc = 0.0;
-    for (int j0 = lane; j0 < len; j0 += 64 * 8) {
-        double v[8];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] = x(min(j0 + 64 * t, len - 1));
-#pragma unroll
-        for (int t = 0; t < 8; ++t)
-            if (j0 + 64 * t < len) acc = fma(v[t], y[j0 + 64 * t], acc);
-    }
-    return acc;
-}
-template <class F>
-DEV double sparse_lane_chain_f(F x, const int* lpos, const double* lval, const int* lsb) {
-    const int lane = threadIdx.x & 63;
-    const int s = lsb[lane], e = lsb[lane + 1];
-    double acc = 0.0;
-    for (int t0 = s; t0 < e; t0 += 4) {
-        double xv[4], vv[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int t = t0 + u < e ? t0 + u : e - 1;
-            xv[u] = x(lpos[t]);
-            vv[u] = lval[t];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (t0 + u < e) acc = fma(xv[u], vv[u], acc);
-    }
-    return acc;
-}
-
 // sp (CSC, large bump): A[i, S] from row i's nonzeros in basic columns (CSR +
 // spos) as a sparse list, rho_c = sparse_lane_chain over row c of MinvT (the
 // dense chain's bits; a row with more than SPL entries takes the dense walk)
@@ -4363,7 +4494,7 @@ __global__ void __launch_bounds__(256) k_dual_row(Dev d, int nchz, int lds_row, 
     }
     double* asrow = lds_row ? asrow_lds : d.zz;  // (huge bumps: every workgroup writes the same values)
     bool spl = false;
-    if (xrow >= 0 && sp) {
+    if (xrow >= 0 && (sp || d.noT)) {  // (no MinvT: always the list when it fits)
         const int64_t t0 = d.rptr[xrow], t1 = d.rptr[xrow + 1];
         spl = t1 - t0 <= SPL;
         if (spl) {
@@ -4388,8 +4519,11 @@ __global__ void __launch_bounds__(256) k_dual_row(Dev d, int nchz, int lds_row, 
         if (xrow >= 0) {
             double acc;
             if (pend) {  // row cc of the new MinvT: element (q, cc) of the new Minv
-                const OldM oT{d.MinvT, (size_t)d.ldm, true};
+                const OldM oT = d.noT ? OldM{d.Minv, (size_t)d.ldm, false} : OldM{d.MinvT, (size_t)d.ldm, true};
                 auto xf = [&](int q) { return minv_new(d, P, q, cc, oT); };
+                acc = spl ? sparse_lane_chain_f(xf, s_pos, s_val, s_sb) : lane_chain_f(xf, asrow, k);
+            } else if (d.noT) {  // column cc of Minv
+                auto xf = [&](int q) { return d.Minv[(size_t)q * d.ldm + cc]; };
                 acc = spl ? sparse_lane_chain_f(xf, s_pos, s_val, s_sb) : lane_chain_f(xf, asrow, k);
             } else {
                 const double* mrow = d.MinvT + (size_t)cc * d.ldm;
@@ -5496,7 +5630,7 @@ hipError_t launch_init_rows(const Dev& d, const double* rhs, hipStream_t st) {
 #endif
 static void update_grid(const Dev& d, int k_ub, bool with_ar, unsigned* nb_minv, unsigned* nb,
                         int threads = 256, int per_thread = 1, unsigned wg_max = ELP_UPDATE_WG_MAX) {
-    const int64_t kk = 2 * (int64_t)(k_ub + 1) * (k_ub + 1);
+    const int64_t kk = (d.noT ? 1 : 2) * (int64_t)(k_ub + 1) * (k_ub + 1);
     *nb_minv = cdiv(kk, threads * per_thread);
     if (*nb_minv > wg_max) *nb_minv = wg_max;
     const int64_t cw = with_ar ? (d.m > d.n ? d.m : d.n) : (d.m > k_ub + 1 ? d.m : k_ub + 1);
@@ -5640,7 +5774,8 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     const bool als = !no_als && ldsz && k_ub > 2 * zw * ZCHUNK && k_ub <= ZR_PA * 64 * zw && lds_als <= 64 * 1024;
     if (spz) {
         // (the dual phase: + nrt waves for the flips' x_B update, before the snapshot one)
-        k_ftran_zr_sp<<<nrt + nbt + 1, 64, 0, st>>>(d, nrt, phase == 3 ? 1 : 0);
+        k_ftran_zr_sp<<<nrt + nbt + (phase == 3 && !ELP_ZR_MERGE ? nrt : 0) + 1, 64, 0, st>>>(d, nrt,
+                                                                                           phase == 3 ? 1 : 0);
     } else {
         // + 1: the snapshot workgroup
         if (als) {
@@ -5888,6 +6023,10 @@ hipError_t launch_select_finish(const Dev& d, hipStream_t st) {
 
 hipError_t launch_refactor_ns_resid(const Dev& d, int k, hipStream_t st) {
     if (k <= 0) return hipSuccess;
+    if (d.csc && d.spos) {  // (M is sparse: k_ns_resid_sp, the same bits)
+        k_ns_resid_sp<<<k, 256, 0, st>>>(d, k);
+        return hipGetLastError();
+    }
     dim3 g(cdiv(k, NS_T), cdiv(k, NS_T));
     k_ns_gemm<0><<<g, 256, 0, st>>>(d, k);
     return hipGetLastError();
