@@ -1896,7 +1896,7 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             hipEvent_t e0 = prof_chunk ? h->ev[2 * t] : nullptr, e1 = prof_chunk ? h->ev[2 * t + 1] : nullptr;
             h->stats.price_launches++;
             if (h->phase == 3 && h->comm.kind == 0) {  // the dual simplex phase 1 (one GPU)
-                HIPCHK(launch_dual_iteration(h->d, kub, nyub, h->st));
+                HIPCHK(launch_dual_iteration(h->d, kub, nyub, h->st, t));
             } else if (h->phase == 3) {
                 // column-sharded: each rank prices its shard (the last rank also the
                 // slacks) and packs its ratio-test candidates; the all-gather hands
@@ -1971,7 +1971,7 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             if (rc) return rc;
         }
         h->dbg_enqueue += t_enq1 - t_enq0;
-        if (h->d.dstamp && c->status == ST_RUN && h->phase == 2) {
+        if (h->d.dstamp && c->status == ST_RUN && (h->phase == 2 || h->phase == 3)) {
             std::vector<unsigned long long> v(DSTAMP_STRIDE * 64);
             HIPCHK(hipMemcpy(v.data(), h->d.dstamp, v.size() * 8, hipMemcpyDeviceToHost));
             if (h->stamp_sum.empty()) h->stamp_sum.assign(DSTAMP_STRIDE, 0.0);
@@ -1985,6 +1985,8 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
                     if (r[i] && r[12]) h->stamp_sum[i] += 10.0 * (double)(long long)(r[i] - r[12]);
                 for (int i = 17; i < 20; ++i)  // FTRAN-z, relative to its workgroup 0's start
                     if (r[i] && r[16]) h->stamp_sum[i] += 10.0 * (double)(long long)(r[i] - r[16]);
+                for (int i = 21; i < 24; ++i)  // the dual BFRT, relative to its start
+                    if (r[i] && r[20]) h->stamp_sum[i] += 10.0 * (double)(long long)(r[i] - r[20]);
                 h->stamp_n++;
             }
         }
@@ -2818,6 +2820,9 @@ extern "C" void elp_destroy(elp_handle* h) {
         std::fprintf(stderr, "k_ftran_zr stamps (us after its workgroup 0 starts): ctl=%.2f z=%.2f emitted=%.2f\n",
                      h->stamp_sum[17] / h->stamp_n / 1e3, h->stamp_sum[18] / h->stamp_n / 1e3,
                      h->stamp_sum[19] / h->stamp_n / 1e3);
+        std::fprintf(stderr, "k_dual_bfrt stamps (us after its start): compacted=%.2f decided=%.2f end=%.2f\n",
+                     h->stamp_sum[21] / h->stamp_n / 1e3, h->stamp_sum[22] / h->stamp_n / 1e3,
+                     h->stamp_sum[23] / h->stamp_n / 1e3);
     }
     if (!h) return;
     destroy_group(h);

@@ -46,7 +46,7 @@ enum : int32_t { ACT_NONE = 0, ACT_FLIP = 1, ACT_PIVOT = 2 };
 // slot chunks per pricing tile (one per wave); the oracle's PRICE_SPLIT must match
 constexpr int PRICE_SPLIT = ELP_PRICE_SPLIT;
 constexpr int ZCHUNK = 32;      // bump positions per FTRAN-z partial
-constexpr int DSTAMP_STRIDE = 24;  // ELP_STAMPS slots per chunk iteration (k_ratio 0-11, select 12-15, FTRAN-z 16-19)
+constexpr int DSTAMP_STRIDE = 24;  // ELP_STAMPS slots per chunk iteration (k_ratio 0-11, select 12-15, FTRAN-z 16-19, dual BFRT 20-23)
 constexpr int RREG = 64;  // pass-2 candidate slots per k_ftran_zr wave region
 constexpr int TILE_COLS = 128;  // columns per pricing workgroup (2 per lane)
 
@@ -405,7 +405,7 @@ hipError_t launch_dual_setup_cols(const Dev& d, hipStream_t st);
 hipError_t launch_dual_init_rows(const Dev& d, hipStream_t st);
 // one iteration: CHUZR, rho_r, pivot row + pricing, bound-flipping ratio test,
 // the flips' FTRAN and x_B update, FTRAN of a_q, pivot bookkeeping, update
-hipError_t launch_dual_iteration(const Dev& d, int k_ub, int ny_ub, hipStream_t st);
+hipError_t launch_dual_iteration(const Dev& d, int k_ub, int ny_ub, hipStream_t st, int dslot = 0);
 // column-sharded ranks (replicated A): head = CHUZR, rho_r, the pivot row and
 // pricing of this shard, its candidates packed into dsend; the host all-gathers
 // dsend into drecv; tail = the bound-flipping ratio test over every rank's

@@ -2298,7 +2298,8 @@ DEV double zrow_chain(const Dev& d, int i, int k, const int* pp, const double* v
 // x -= sigma (a_F,i - A[i, S] fS); bump positions x -= fS (k_dual_flip_apply's
 // arithmetic); the dual leaves on k_dual_row's row, so no primal pass 1 runs.
 // (r04: the flips' row walk in waves of its own; until then a launch of its own)
-__global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt, int flip) {
+__global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt, int flip, int dslot) {
+    RSTAMP(16);
     const DevCtl* c = d.ctl;
     const int32_t st0 = c->status;
     int k = c->k, q = c->q;
@@ -2328,6 +2329,7 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt, int flip) {
         KEEP(afi);
         return;
     }
+    RSTAMP(17);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         d.ctl->snap_k = k;
         d.ctl->snap_bland = bland;
@@ -2366,6 +2368,7 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt, int flip) {
             const double sg = unit_sign(d, u, i);
             const double alU = sg * (aiq - z);
             d.alU[i] = alU;
+            RSTAMP(18);
             if (ELP_ZR_MERGE && fl) {
                 const double tot = zrow_chain(d, i, k, pp, vv, cnt, over, d.fS);
                 d.xr[i] = d.xr[i] - sg * (afi - tot);
@@ -2399,6 +2402,7 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt, int flip) {
     const double bmin = wave_min_f64(tmin);
     if (lane == 0) d.blockmin[blockIdx.x] = bmin;
     emit_wave(d, region, ve, e, ge, xe, le, he, bmin, pivtol);
+    RSTAMP(19);
 }
 
 // waves per row tile of k_ftran_zr (ZR_WAVES): 8, or 4 when the row tiles
@@ -5093,7 +5097,7 @@ DEV void bfrt_flip_column(const Dev& d, int nflip, int k) {
 // gathered: P = world ranks' packed records in drecv (rank order) instead of
 // this launch's regions
 // (workgroups 1 .. gridDim.x - 1: the deferred plan's Minv update, dual_defer)
-__global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gathered, int reg_ok) {
+__global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gathered, int reg_ok, int dslot) {
     __shared__ double s_bun[2 * BF_BUN];
     __shared__ int scan_lds[BF_NT / 64];
     __shared__ double red[BF_NT / 64];
@@ -5108,6 +5112,7 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
         }
         return;
     }
+    RSTAMP(20);
     if (c->status != ST_RUN) return;
     const int tid = threadIdx.x;
     const int bland = c->bland;
@@ -5125,6 +5130,7 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
         }
     }
     __syncthreads();  // (the compacted array is read by other threads below)
+    RSTAMP(21);
     const int N = total;
     const double ptol = c->tol_primal;
     int nflip = 0, qidx = -1;
@@ -5319,6 +5325,7 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
         break;
     }
     __syncthreads();
+    RSTAMP(22);
     // the flips: compact indices -> ids and dx = +-(u - l) (the record's range)
     for (int t = tid; t < nflip; t += BF_NT) {
         const DualCand o = d.dcomp[d.dflip[t]];
@@ -5339,6 +5346,7 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     // flip order, the same fma chain
     if (d.csc && !gathered && qidx >= 0 && nflip > 0) bfrt_flip_column(d, nflip, c->k);
     if (tid != 0) return;
+    RSTAMP(23);
     const int64_t it = c->iter;
     if (qidx < 0) {  // dual unbounded: the LP is infeasible (oracle: trace -2, the leaving variable)
         c->iter = it + 1;
@@ -5774,8 +5782,8 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     const bool als = !no_als && ldsz && k_ub > 2 * zw * ZCHUNK && k_ub <= ZR_PA * 64 * zw && lds_als <= 64 * 1024;
     if (spz) {
         // (the dual phase: + nrt waves for the flips' x_B update, before the snapshot one)
-        k_ftran_zr_sp<<<nrt + nbt + (phase == 3 && !ELP_ZR_MERGE ? nrt : 0) + 1, 64, 0, st>>>(d, nrt,
-                                                                                           phase == 3 ? 1 : 0);
+        k_ftran_zr_sp<<<nrt + nbt + (phase == 3 && !ELP_ZR_MERGE ? nrt : 0) + 1, 64, 0, st>>>(
+            d, nrt, phase == 3 ? 1 : 0, dslot);
     } else {
         // + 1: the snapshot workgroup
         if (als) {
@@ -5908,7 +5916,7 @@ static int dual_head(const Dev& d, int k_ub, int ny_ub, hipStream_t st, int defe
     return d.ntiles + nsw;
 }
 
-static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_col = true, int defer = 0);
+static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_col = true, int defer = 0, int dslot = 0);
 
 hipError_t launch_dual_iteration_head(const Dev& d, int k_ub, int ny_ub, hipStream_t st) {
     const int nreg = dual_head(d, k_ub, ny_ub, st);
@@ -5917,14 +5925,14 @@ hipError_t launch_dual_iteration_head(const Dev& d, int k_ub, int ny_ub, hipStre
 }
 
 hipError_t launch_dual_iteration_tail(const Dev& d, int k_ub, hipStream_t st) {
-    k_dual_bfrt<<<1, BF_NT, 0, st>>>(d, 0, 1, bfrt_reg());
+    k_dual_bfrt<<<1, BF_NT, 0, st>>>(d, 0, 1, bfrt_reg(), 0);
     return dual_tail(d, k_ub, st);
 }
 
 // column-only shards: the ratio test over the gathered candidates, then the
 // owner's entering column into pkt[0, m) (others: zeros) and a_F cleared
 hipError_t launch_dual_ratio_shards(const Dev& d, hipStream_t st) {
-    k_dual_bfrt<<<1, BF_NT, 0, st>>>(d, 0, 1, bfrt_reg());
+    k_dual_bfrt<<<1, BF_NT, 0, st>>>(d, 0, 1, bfrt_reg(), 0);
     k_dual_qpack<<<cdiv(d.m > 0 ? d.m : 1, 256), 256, 0, st>>>(d);
     return hipGetLastError();
 }
@@ -5936,17 +5944,17 @@ hipError_t launch_dual_iteration_finish(const Dev& d, int k_ub, hipStream_t st) 
     return dual_tail(d, k_ub, st, false);
 }
 
-hipError_t launch_dual_iteration(const Dev& d, int k_ub, int ny_ub, hipStream_t st) {
+hipError_t launch_dual_iteration(const Dev& d, int k_ub, int ny_ub, hipStream_t st, int dslot) {
     const int defer = d.dual_defer ? 1 : 0;
     const int nreg = dual_head(d, k_ub, ny_ub, st, defer);
     // (dual_defer: + the Minv half of the last plan's update beside the ratio test)
-    k_dual_bfrt<<<1 + (defer ? defer_wgs(k_ub, BF_NT, 1024) : 0), BF_NT, 0, st>>>(d, nreg, 0, bfrt_reg());
-    return dual_tail(d, k_ub, st, true, defer);
+    k_dual_bfrt<<<1 + (defer ? defer_wgs(k_ub, BF_NT, 1024) : 0), BF_NT, 0, st>>>(d, nreg, 0, bfrt_reg(), dslot);
+    return dual_tail(d, k_ub, st, true, defer, dslot);
 }
 
 // the bound flips' FTRAN and x_B update, then FTRAN of a_q and the pivot
 // (flip_col false: a_F was formed by the column-only shards' chain already)
-static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_col, int defer) {
+static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_col, int defer, int dslot) {
     const int m = d.m;
     const size_t lds = (size_t)k_ub * sizeof(double);
     const int lds_row = lds <= 48 * 1024;
@@ -5977,11 +5985,11 @@ static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_co
         else if (k_ub > 512 && k_ub <= 640)
             k_select_ftran<10><<<g, 256, ldsz, st>>>(DEV_ARG(d), 1, 0, k_ub, 0, (int)nrw, (int)nqz, dual);
         else
-            k_select_ftran<8><<<g, 256, ldsz, st>>>(DEV_ARG(d), 1, 0, k_ub, 0, (int)nrw, (int)nqz, dual);
-        return launch_iteration_tail(d, k_ub, defer ? 4 : 3, st, false, 0, nqz > 0 ? 1 : 0);
+            k_select_ftran<8><<<g, 256, ldsz, st>>>(DEV_ARG(d), 1, 0, k_ub, dslot, (int)nrw, (int)nqz, dual);
+        return launch_iteration_tail(d, k_ub, defer ? 4 : 3, st, false, dslot, nqz > 0 ? 1 : 0);
     }
     k_select<<<1, 1024, 0, st>>>(d, 1, 0, 1);
-    return launch_iteration_tail(d, k_ub, defer ? 4 : 3, st, true, 0);
+    return launch_iteration_tail(d, k_ub, defer ? 4 : 3, st, true, dslot);
 }
 
 hipError_t launch_warm_start(const Dev& d, const double* lo, const double* up, int k, int ny, hipStream_t st) {
