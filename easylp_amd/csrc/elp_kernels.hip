@@ -2405,6 +2405,166 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt, int flip, in
     RSTAMP(19);
 }
 
+// The same with four lanes per row (ELP_ZR_LPR = 4, the default since r05):
+// a wave takes 16 rows; each lane loads an interleaved quarter of its row's
+// entries (<= ZQB per batch: one batch of column / value loads, then one of
+// spos loads, for rows of <= 32 nonzeros -- r05e stamps: the one-lane walk's
+// two batches of 16 scattered loads each took ~19 us of the kernel), the
+// quad's basic entries meet in LDS, and the quad's lane 0 forms alpha_U
+// (and the Harris pass-1 entry) while lane 1 forms the flips' x_B update --
+// each from the sorted list, the zchunk chains of zrow_chain: the same bits.
+constexpr int ZLPR = 4, ZRPW = 64 / ZLPR, ZQB = 8;
+__global__ void __launch_bounds__(64) k_ftran_zr_sq(Dev d, int nrt, int flip, int dslot) {
+    __shared__ int s_p[ZRPW][SPZ_MAX];
+    __shared__ double s_v[ZRPW][SPZ_MAX];
+    RSTAMP(16);
+    const DevCtl* c = d.ctl;
+    const int32_t st0 = c->status;
+    int k = c->k, q = c->q;
+    const int bland = c->bland, m = d.m, lane = threadIdx.x;
+    const double sig = c->sig, ptol = c->tol_primal, pivtol = c->tol_pivot;
+    const int nfl = c->nflip;
+    const int r = lane / ZLPR, sub = lane % ZLPR;
+    const bool roww = (int)blockIdx.x < nrt;
+    const int i = roww ? (int)blockIdx.x * ZRPW + r : 0;
+    const int ic = i < m ? i : (m > 0 ? m - 1 : 0);
+    int64_t r0 = 0, r1 = 0;
+    int u = -1;
+    double qi = 0.0, afi = 0.0;
+    if (m > 0) {  // (straight-line, masked at use)
+        r0 = d.rptr[ic];
+        r1 = d.rptr[ic + 1];
+        u = d.cover[ic];
+        qi = d.qcol[ic];
+        afi = d.aF ? d.aF[ic] : 0.0;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" : "+v"(k), "+v"(q));
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) d.ctl->snap_status = st0;  // for k_ratio
+    if (st0 != ST_RUN) {
+        KEEP(r0);
+        KEEP(u);
+        KEEP(qi);
+        KEEP(afi);
+        return;
+    }
+    RSTAMP(17);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        d.ctl->snap_k = k;
+        d.ctl->snap_bland = bland;
+    }
+    if (blockIdx.x == gridDim.x - 1) {
+        if (threadIdx.x == 0) zr_snapshot(d, k, q);
+        return;
+    }
+    const bool fl = flip && nfl > 0;
+    double tmin = HUGE_VAL, ge = 0.0, xe = 0.0, le = 0.0, he = 0.0;
+    int ve = -1, e = 0, region = blockIdx.x;
+    if (roww) {
+        const bool act = i < m && u >= 0;
+        int cnt = 0;
+        for (int64_t t0 = r0; t0 < r1; t0 += ZLPR * ZQB) {  // (trip counts differ per quad)
+            int jj[ZQB], ps[ZQB];
+            double vr[ZQB];
+#pragma unroll
+            for (int b = 0; b < ZQB; ++b) {
+                const int64_t tt = t0 + sub + ZLPR * b;
+                const int64_t tc = tt < r1 ? tt : r1 - 1;
+                jj[b] = d.cind[tc];
+                vr[b] = d.rval[tc];
+            }
+#pragma unroll
+            for (int b = 0; b < ZQB; ++b) ps[b] = d.spos[jj[b]];
+            int mine = 0;
+#pragma unroll
+            for (int b = 0; b < ZQB; ++b) mine += (t0 + sub + ZLPR * b < r1 && ps[b] >= 0 && ps[b] < k) ? 1 : 0;
+            // the quad's offsets: lanes 4r .. 4r + 3 (readlane-free: shuffles within the quad)
+            const int qb = lane & ~(ZLPR - 1);
+            int off = 0, tot = 0;
+#pragma unroll
+            for (int s2 = 0; s2 < ZLPR; ++s2) {
+                const int v = __shfl(mine, qb + s2);
+                off += s2 < sub ? v : 0;
+                tot += v;
+            }
+            int o = cnt + off;
+#pragma unroll
+            for (int b = 0; b < ZQB; ++b)
+                if (t0 + sub + ZLPR * b < r1 && ps[b] >= 0 && ps[b] < k) {
+                    if (o < SPZ_MAX) {
+                        s_p[r][o] = ps[b];
+                        s_v[r][o] = vr[b];
+                    }
+                    ++o;
+                }
+            cnt += tot;
+        }
+        __syncthreads();  // (one wave: the quad's entries in LDS)
+        const bool over = cnt > SPZ_MAX;
+        if (act && (sub == 0 || (sub == 1 && fl))) {
+            int pp[SPZ_MAX];
+            double vv[SPZ_MAX];
+            const int nc = over ? 0 : cnt;
+#pragma unroll
+            for (int t = 0; t < SPZ_MAX; ++t) {
+                pp[t] = t < nc ? s_p[r][t] : 0;
+                vv[t] = t < nc ? s_v[r][t] : 0.0;
+            }
+            for (int a = 1; a < nc; ++a) {  // insertion sort by position (a handful of entries)
+                const int p = pp[a];
+                const double v = vv[a];
+                int b = a - 1;
+                while (b >= 0 && pp[b] > p) {
+                    pp[b + 1] = pp[b];
+                    vv[b + 1] = vv[b];
+                    --b;
+                }
+                pp[b + 1] = p;
+                vv[b + 1] = v;
+            }
+            const double sg = unit_sign(d, u, i);
+            if (sub == 0) {
+                const double z = zrow_chain(d, i, k, pp, vv, nc, over, d.alS);
+                const double aiq = q >= d.N ? (i == q - d.N ? 1.0 : 0.0) : qi;
+                const double alU = sg * (aiq - z);
+                d.alU[i] = alU;
+                RSTAMP(18);
+                if (!flip) {
+                    ge = sig * alU;
+                    xe = d.xr[i];
+                    le = d.rlo[i];
+                    he = d.rhi[i];
+                    ve = u;
+                    tmin = harris1(ge, xe, le, he, ptol, pivtol, bland);
+                }
+            } else {
+                const double tot = zrow_chain(d, i, k, pp, vv, nc, over, d.fS);
+                d.xr[i] = d.xr[i] - sg * (afi - tot);
+            }
+        }
+        e = i;
+    } else {
+        const int p = (blockIdx.x - nrt) * 64 + lane;
+        e = m + p;
+        if (p < k) {
+            if (flip) {
+                if (fl) d.xs[p] = d.xs[p] - d.fS[p];
+            } else {
+                ge = sig * d.alS[p];
+                xe = d.xs[p];
+                le = d.slo[p];
+                he = d.shi[p];
+                ve = d.Sl[p];
+                tmin = harris1(ge, xe, le, he, ptol, pivtol, bland);
+            }
+        }
+    }
+    const double bmin = wave_min_f64(tmin);
+    if (lane == 0) d.blockmin[blockIdx.x] = bmin;
+    emit_wave(d, region, ve, e, ge, xe, le, he, bmin, pivtol);
+    RSTAMP(19);
+}
+
 // waves per row tile of k_ftran_zr (ZR_WAVES): 8, or 4 when the row tiles
 // outnumber the CUs and every chunk still gets its own half-wave (the kernel
 // holds one 8-wave workgroup per CU -- 175 VGPRs -- so 4-wave tiles run two
@@ -5762,7 +5922,11 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     // CSC with a large bump: FTRAN-z from the rows of A (k_ftran_zr_sp: 64-row
     // tiles, 64-position bump tiles); else k_ftran_zr's 32-row tiles over AS
     const bool spz = use_spz(d, k_ub);
-    const int nrt = spz ? (int)cdiv(m > 0 ? m : 1, 64) : (int)cdiv(m > 0 ? m : 1, ZR_ROWS);
+#ifndef ELP_ZR_LPR
+#define ELP_ZR_LPR 4
+#endif
+    // (k_ftran_zr_sq: 16 rows per wave; ELP_ZR_LPR=1: k_ftran_zr_sp's 64)
+    const int nrt = spz ? (int)cdiv(m > 0 ? m : 1, ELP_ZR_LPR == 4 ? ZRPW : 64) : (int)cdiv(m > 0 ? m : 1, ZR_ROWS);
     // z partials: 256 B per chunk of ZCHUNK bump positions in LDS (<= 64 KiB,
     // k <= 8192); larger bumps use a private slice of zpart per row tile
     const size_t lds = (size_t)cdiv(k_ub, ZCHUNK) * ZR_ROWS * sizeof(double);
@@ -5782,8 +5946,11 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     const bool als = !no_als && ldsz && k_ub > 2 * zw * ZCHUNK && k_ub <= ZR_PA * 64 * zw && lds_als <= 64 * 1024;
     if (spz) {
         // (the dual phase: + nrt waves for the flips' x_B update, before the snapshot one)
-        k_ftran_zr_sp<<<nrt + nbt + (phase == 3 && !ELP_ZR_MERGE ? nrt : 0) + 1, 64, 0, st>>>(
-            d, nrt, phase == 3 ? 1 : 0, dslot);
+        if (ELP_ZR_LPR == 4)
+            k_ftran_zr_sq<<<nrt + nbt + 1, 64, 0, st>>>(d, nrt, phase == 3 ? 1 : 0, dslot);
+        else
+            k_ftran_zr_sp<<<nrt + nbt + (phase == 3 && !ELP_ZR_MERGE ? nrt : 0) + 1, 64, 0, st>>>(
+                d, nrt, phase == 3 ? 1 : 0, dslot);
     } else {
         // + 1: the snapshot workgroup
         if (als) {
