@@ -5055,11 +5055,12 @@ __global__ void __launch_bounds__(BF_NT) k_dual_pack(Dev d, int nreg) {
 // shuffles (no workgroup barrier per step), the flip sum is lane 0's in-order
 // fma chain over the bunch staged in LDS.  Same decisions as the block path.
 DEV void bfrt_wave(const Dev& d, int N, int bland, double ptol, double slope, double* s_bun, int* nflip_out,
-                   int* qidx_out) {
+                   int* qidx_out, int* s_flip) {
     const int lane = threadIdx.x & 63;
     const int run = (N + 63) / 64;
     const int lo = min(N, lane * run), hi = min(N, lo + run);
     const double INF = HUGE_VAL;
+    const unsigned long long below = (1ull << lane) - 1ull;
     double rt[BF_RR], rb[BF_RR], ra[BF_RR], rw[BF_RR];
     int rj[BF_RR];
     unsigned ral = 0;
@@ -5079,42 +5080,42 @@ DEV void bfrt_wave(const Dev& d, int N, int bland, double ptol, double slope, do
     }
     int nflip = 0, qidx = -1;
     for (;;) {
+        if (!__any(ral != 0)) break;  // nothing left: the dual ray (q = -1)
         double bmin = INF;
 #pragma unroll
         for (int q = 0; q < BF_RR; ++q)
             if (ral >> q & 1u) bmin = fmin(bmin, rb[q]);
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) bmin = fmin(bmin, __shfl_xor(bmin, off));
-        if (!__any(ral != 0)) break;  // nothing left: the dual ray (q = -1)
-        const double thmax = bmin;
+        const double thmax = wave_min_f64(bmin);  // (DPP; uniform)
         unsigned rbun = 0;
-        int cnt = 0, allbox = 1;
+        int allbox = 1;
 #pragma unroll
         for (int q = 0; q < BF_RR; ++q)
             if ((ral >> q & 1u) && rt[q] <= thmax) {
                 rbun |= 1u << q;
-                cnt++;
                 if (rw[q] == INF) allbox = 0;
             }
-        int incl = cnt;
+        // the bunch in order (lane-major runs = ascending id): this lane's
+        // members' ranks from one ballot per register slot
+        int before = 0, nq = 0;
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int u = __shfl_up(incl, off);
-            if (lane >= off) incl += u;
+        for (int q = 0; q < BF_RR; ++q) {
+            const unsigned long long bq = __ballot((rbun >> q & 1u) != 0u);
+            before += __popcll(bq & below);
+            nq += __popcll(bq);
         }
-        const int nq = __shfl(incl, 63);
         const bool boxed = __all(allbox);
-        // the bunch in order: (|alpha|, u - l) to LDS for the sum, compact
-        // indices to dflip; this lane's best member for the entering choice
+        // (|alpha|, u - l) to LDS for the sum, compact indices to the flip list
+        // in LDS; this lane's best member for the entering choice
         double ba = -1.0, bt = INF;
         int bj = -1, bi = -1;
-        int o = nflip + incl - cnt;
+        int o = before;
 #pragma unroll
         for (int q = 0; q < BF_RR; ++q)
             if (rbun >> q & 1u) {
-                s_bun[2 * (o - nflip)] = ra[q];
-                s_bun[2 * (o - nflip) + 1] = rw[q];
-                d.dflip[o++] = lo + q;
+                s_bun[2 * o] = ra[q];
+                s_bun[2 * o + 1] = rw[q];
+                s_flip[nflip + o] = lo + q;
+                ++o;
                 const bool take = bi < 0 || (bland ? (rt[q] < bt || (rt[q] == bt && rj[q] < bj))
                                                    : (ra[q] > ba || (ra[q] == ba && rj[q] < bj)));
                 if (take) {
@@ -5124,35 +5125,33 @@ DEV void bfrt_wave(const Dev& d, int N, int bland, double ptol, double slope, do
                     bi = lo + q;
                 }
             }
+        if (nq == 0) break;  // (NaN ratios only: no candidate qualifies -- the ray)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         double sum = 0.0;
         if (lane == 0 && boxed)  // |alpha| (u - l) in ascending id (nq <= N <= 64 BF_RR < BF_BUN)
             for (int t = 0; t < nq; ++t) sum = fma(s_bun[2 * t], s_bun[2 * t + 1], sum);
-        sum = __shfl(sum, 0);
+        sum = readlane_f64(sum, 0);
         __builtin_amdgcn_wave_barrier();  // (s_bun is rewritten by the next round)
-        if (nq == 0) break;  // (NaN ratios only: no candidate qualifies -- the ray)
         if (boxed && sum < slope - ptol) {  // flip the bunch
             slope = slope - sum;
             ral &= ~rbun;
             nflip += nq;
             continue;
         }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const double ya = __shfl_xor(ba, off), yt = __shfl_xor(bt, off);
-            const int yj = __shfl_xor(bj, off), yi = __shfl_xor(bi, off);
-            const bool take = yi >= 0 && (bi < 0 || (bland ? (yt < bt || (yt == bt && yj < bj))
-                                                           : (ya > ba || (ya == ba && yj < bj))));
-            if (take) {
-                ba = ya;
-                bt = yt;
-                bj = yj;
-                bi = yi;
-            }
-        }
-        qidx = bi;
+        // the bunch's best enters: the largest |alpha| (Bland: the smallest
+        // ratio), then the lowest id -- each lane holds its own runs' best, and
+        // ids ascend with the lane, so the lowest lane among the best values
+        const bool has = bi >= 0;
+        const double key = has ? (bland ? -bt : ba) : -INF;
+        const double kmax = wave_max_f64(key);
+        // (the lowest id among the lanes at the best value: slack candidates
+        //  follow the Y slots, not ascending id)
+        const bool at = has && key == kmax;
+        const unsigned long long w = __ballot(at);
+        const int win = w ? lowest_index_lane(w, at, bj) : lowest_index_lane(__ballot(has), has, bj);
+        qidx = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(bi, win));
         break;
     }
     *nflip_out = nflip;
@@ -5168,16 +5167,21 @@ DEV void bfrt_wave(const Dev& d, int N, int bland, double ptol, double slope, do
 // kernel's sparse list (Dev::afl).  More: the flips one after the other, a
 // barrier each, after clearing all of a_F (r04's path).
 constexpr int AF_PAR = 256;
-DEV void bfrt_flip_column(const Dev& d, int nflip, int k) {
+// (myj / mydx: thread t's flip t, t < nflip <= BF_NT -- its column and dx)
+DEV void bfrt_flip_column(const Dev& d, int nflip, int k, int myj, double mydx) {
     __shared__ int s_off[BF_NT], s_row[AF_PAR], s_lpos[SPL], s_lkey[SPL], s_lsb[72], s_scan[BF_NT / 64];
     __shared__ double s_v[AF_PAR], s_dx[AF_PAR], s_lval[SPL];
+    __shared__ int64_t s_c0[BF_NT];
+    __shared__ double s_fdx[BF_NT];
     const int tid = threadIdx.x, m = d.m;
-    __syncthreads();  // (the flip ids / dx written above)
     int len = 0;
     if (tid < nflip) {
-        const int j = d.dflip[tid];
-        len = (int)(d.cptr[j + 1] - d.cptr[j]);
+        const int64_t c0 = d.cptr[myj];
+        len = (int)(d.cptr[myj + 1] - c0);
+        s_c0[tid] = c0;
+        s_fdx[tid] = mydx;
     }
+    __syncthreads();  // (also: the flip ids / dx written above, for the sequential path)
     int excl = 0, E = AF_PAR + 1;
     if (nflip <= BF_NT) E = block_scan_excl<BF_NT>(len, &excl, s_scan);
     const bool par = E <= AF_PAR;
@@ -5214,12 +5218,11 @@ DEV void bfrt_flip_column(const Dev& d, int nflip, int k) {
             if (s_off[mid] <= tid) lo = mid;
             else hi = mid - 1;
         }
-        const int j = d.dflip[lo];
-        const int64_t t = d.cptr[j] + (tid - s_off[lo]);
+        const int64_t t = s_c0[lo] + (tid - s_off[lo]);
         row = d.rind[t];
         s_row[tid] = row;
         s_v[tid] = d.cval[t];
-        s_dx[tid] = d.dflipdx[lo];
+        s_dx[tid] = s_fdx[lo];
     }
     __syncthreads();
     bool lead = false;
@@ -5263,6 +5266,7 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     __shared__ double red[BF_NT / 64];
     __shared__ int s_int[4];
     __shared__ double s_dbl[2];
+    __shared__ int s_flip[64 * BF_RR];  // (the one-wave path's flip list: compact indices)
     DevCtl* c = d.ctl;
     if (blockIdx.x > 0) {
         if (minv_pending(c)) {
@@ -5296,7 +5300,7 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     int nflip = 0, qidx = -1;
     const bool wave = reg_ok >= 2 && N <= 64 * BF_RR;  // (bfrt_wave: the usual case)
     if (wave) {
-        if (tid < 64) bfrt_wave(d, N, bland, ptol, fabs(c->dr_x - c->dr_beta), s_bun, &nflip, &qidx);
+        if (tid < 64) bfrt_wave(d, N, bland, ptol, fabs(c->dr_x - c->dr_beta), s_bun, &nflip, &qidx, s_flip);
         if (tid == 0) {
             s_int[2] = nflip;
             s_int[3] = qidx;
@@ -5487,24 +5491,30 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     __syncthreads();
     RSTAMP(22);
     // the flips: compact indices -> ids and dx = +-(u - l) (the record's range)
+    // (the new status and value from the record's bounds: the column's own)
+    int myj = -1;
+    double mydx = 0.0;
     for (int t = tid; t < nflip; t += BF_NT) {
-        const DualCand o = d.dcomp[d.dflip[t]];
+        const DualCand o = d.dcomp[wave ? s_flip[t] : d.dflip[t]];
         const bool at_lower = o.side > 0;  // (boxed columns act at their current bound)
-        d.dflipdx[t] = at_lower ? o.ub - o.lb : o.lb - o.ub;
+        const double dx = at_lower ? o.ub - o.lb : o.lb - o.ub;
+        d.dflipdx[t] = dx;
         d.dflip[t] = o.j;
-    }
-    __syncthreads();
-    for (int t = tid; t < nflip; t += BF_NT) {
-        const int jl = loc_of(d, d.dflip[t]);
+        if (t == tid) {
+            myj = o.j;
+            mydx = dx;
+        }
+        const int jl = loc_of(d, o.j);
         if (jl < 0) continue;  // (column-sharded: another shard's column)
-        const bool up = d.dflipdx[t] > 0.0;
+        const bool up = dx > 0.0;
         d.vstat[jl] = up ? VS_UPPER : VS_LOWER;
-        d.xval[jl] = up ? d.ub[jl] : d.lb[jl];
+        d.xval[jl] = up ? o.ub : o.lb;
     }
     // CSC (one GPU): a_F = sum of the flipped columns times their dx here, in
     // place of a one-workgroup k_dual_flip_col launch -- each row's entries in
     // flip order, the same fma chain
-    if (d.csc && !gathered && qidx >= 0 && nflip > 0) bfrt_flip_column(d, nflip, c->k);
+    if (d.csc && !gathered && qidx >= 0 && nflip > 0) bfrt_flip_column(d, nflip, c->k, myj, mydx);
+    else __syncthreads();  // (the flip list is read by the other threads below / in later launches)
     if (tid != 0) return;
     RSTAMP(23);
     const int64_t it = c->iter;
