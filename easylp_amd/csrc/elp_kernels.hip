@@ -2906,8 +2906,10 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
     // pass-2 candidates, then this wave's MinvT row (the B^-1 row, last)
     // entries of Rl past the real k are stale: range-checked before use
     const int rcol = ld_clamp(d.Rl, main_wg ? col : 0, k_ub);
+    // (DUAL: no primal ratio test -- the leaving entry is k_dual_row's, so
+    //  neither the pass-1 minima nor the pass-2 candidates are read)
 #pragma unroll
-    for (int t = 0; t < PFB; ++t) bm[t] = ld_clamp(d.blockmin, tid + 256 * t, nblk);
+    for (int t = 0; t < PFB; ++t) bm[t] = DUAL ? HUGE_VAL : ld_clamp(d.blockmin, tid + 256 * t, nblk);
     // the pass-2 candidates k_ftran_zr emitted, one region per emitting wave:
     // thread t takes regions t and t + 256 (PFR), count and first PFQ entries
     // prefetched (clamped, masked by the count at use)
@@ -2917,9 +2919,15 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
 #pragma unroll
     for (int s = 0; s < PFR; ++s) {
         const int reg = min(tid + 256 * s, nreg - 1);
-        rcn[s] = d.rcnt[reg];
+        rcn[s] = DUAL ? 0 : d.rcnt[reg];
 #pragma unroll
-        for (int t = 0; t < PFQ; ++t) rq[s][t] = d.rcand[(size_t)reg * RREG + t];
+        for (int t = 0; t < PFQ; ++t) {
+            if constexpr (DUAL) {
+                rq[s][t] = RCand{};
+            } else {
+                rq[s][t] = d.rcand[(size_t)reg * RREG + t];
+            }
+        }
     }
     // DUAL: the leaving entry's B^-1 row is k_dual_row's rho_r (same row, same
     // k): its value on this wave's position replaces the MinvT row
@@ -3000,7 +3008,7 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
     // ---- pass 1 result: min over the workgroup minima
     const double INF = HUGE_VAL;
     double tmax = INF;
-    if (pfb) {
+    if (pfb || DUAL) {
 #pragma unroll
         for (int t = 0; t < PFB; ++t) tmax = fmin(tmax, tid + 256 * t < nblk ? bm[t] : INF);
     } else {
@@ -3034,7 +3042,7 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
             if (t < rcn[s]) consider(rq[s][t]);
         for (int t = PFQ; t < rcn[s]; ++t) consider(d.rcand[(size_t)reg * RREG + t]);  // long regions
     }
-    for (int reg = tid + 256 * PFR; reg < nreg; reg += 256) {  // (huge m)
+    for (int reg = tid + 256 * PFR; reg < (DUAL ? 0 : nreg); reg += 256) {  // (huge m)
         const int cnt = d.rcnt[reg];
         for (int t = 0; t < cnt; ++t) consider(d.rcand[(size_t)reg * RREG + t]);
     }

@@ -1,0 +1,5 @@
+set -u
+timeout -k 10 900 python -u -m pytest tests/test_gpu_spf.py tests/test_gpu_spz.py tests/test_gpu_dual.py tests/test_gpu_csc.py -m gpu -x -q --timeout 800 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_r05g.log 2>&1 || { tail -30 gpurun_out/pytest_r05g.log; exit 1; }
+tail -3 gpurun_out/pytest_r05g.log
+bash tools/ab_sparse.sh r05g "lpr1 base" 2 || exit 3
+LP=kkt_feasible_20000x100000 bash tools/ab_sparse.sh r05g_feas "lpr1 base" 2 || exit 4
