@@ -682,10 +682,10 @@ static int alloc_all_body(elp_handle* h) {
     A(dalloc(&d.xs, mm));
     A(dalloc(&d.y, mm));
     A(dalloc(&d.yy, mm));
-    A(dalloc(&d.blockmin, (size_t)(mm / 16 + mm / 64 + 8)));  // k_ftran_zr(_sq) row + bump tiles
+    A(dalloc(&d.blockmin, (size_t)(mm / 32 + mm / 64 + 8)));  // k_ftran_zr row + bump tiles
     // pass-2 candidate regions: one per row tile (32 rows) and one per bump-tile
     // wave (64 positions): <= m/32 + k/64 + 8 (k <= m)
-    d.rregs = (int32_t)(mm / 16 + mm / 64 + 10);  // (k_ftran_zr_sq: 16-row tiles)
+    d.rregs = (int32_t)(mm / 32 + mm / 64 + 10);
     A(dalloc(&d.rcand, (size_t)d.rregs * RREG));
     A(dalloc(&d.rcnt, (size_t)d.rregs));
     A(dalloc(&d.pkt, (size_t)(mm + 4)));

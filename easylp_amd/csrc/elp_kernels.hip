@@ -2406,27 +2406,66 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt, int flip, in
 }
 
 // The same with four lanes per row (ELP_ZR_LPR = 4, the default since r05):
-// a wave takes 16 rows; each lane loads an interleaved quarter of its row's
-// entries (<= ZQB per batch: one batch of column / value loads, then one of
-// spos loads, for rows of <= 32 nonzeros -- r05e stamps: the one-lane walk's
-// two batches of 16 scattered loads each took ~19 us of the kernel), the
-// quad's basic entries meet in LDS, and the quad's lane 0 forms alpha_U
-// (and the Harris pass-1 entry) while lane 1 forms the flips' x_B update --
-// each from the sorted list, the zchunk chains of zrow_chain: the same bits.
-constexpr int ZLPR = 4, ZRPW = 64 / ZLPR, ZQB = 8;
-__global__ void __launch_bounds__(64) k_ftran_zr_sq(Dev d, int nrt, int flip, int dslot) {
-    __shared__ int s_p[ZRPW][SPZ_MAX];
-    __shared__ double s_v[ZRPW][SPZ_MAX];
+// a workgroup of 4 waves takes 64 rows, 16 per wave; each lane loads an
+// interleaved quarter of its row's entries (<= ZQB per batch: one batch of
+// column / value loads, then one of spos loads, for rows of <= 32 nonzeros --
+// r05e stamps: the one-lane walk's two batches of 16 scattered loads each took
+// ~19 us of the kernel), the quad's basic entries meet in LDS (up to ZSQ per
+// row, sorted there by the quad's lane 0), and lane 0 forms alpha_U (and the
+// Harris pass-1 entry) while lane 1 forms the flips' x_B update -- each the
+// zchunk chains of zrow_chain over the sorted list: the same bits.  One
+// pass-2 region and one pass-1 minimum per workgroup (k_ratio's prefetch
+// covers 512 regions; a row tile emits <= 64 candidates: one per row); bump
+// tiles of 64 positions (the first wave of the workgroup).
+constexpr int ZLPR = 4, ZRPW = 64 / ZLPR, ZQB = 8, ZSQ = 32, ZROWS = 4 * ZRPW;
+#ifndef ELP_ZR_LPR
+#define ELP_ZR_LPR 4
+#endif
+// ordered emission of a workgroup's pass-2 candidates into its region (every
+// wave's kept entries compacted by ballot, the waves' counts through LDS)
+DEV void emit_block(const Dev& d, int region, int var, int e, double g, double x, double l, double u, double bmin,
+                    double pivtol, int* wcnt) {
+    const double r = var >= 0 ? harris2(g, x, l, u, pivtol) : HUGE_VAL;
+    const bool keep = var >= 0 && r <= bmin && r != HUGE_VAL;
+    const unsigned long long mask = __ballot(keep);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) wcnt[w] = __popcll(mask);
+    __syncthreads();
+    int off = 0, tot = 0;
+    for (int t = 0; t < (int)blockDim.x / 64; ++t) {
+        off += t < w ? wcnt[t] : 0;
+        tot += wcnt[t];
+    }
+    if (keep) {
+        const int slot = off + __popcll(mask & ((1ull << lane) - 1ull));
+        if (slot < RREG) {
+            RCand cd;
+            cd.g = g;
+            cd.r = r;
+            cd.l = l;
+            cd.u = u;
+            cd.var = var;
+            cd.e = e;
+            d.rcand[(size_t)region * RREG + slot] = cd;
+        }
+    }
+    if (threadIdx.x == 0) d.rcnt[region] = tot < RREG ? tot : RREG;
+}
+__global__ void __launch_bounds__(256) k_ftran_zr_sq(Dev d, int nrt, int flip, int dslot) {
+    __shared__ int s_p[ZROWS][ZSQ];
+    __shared__ double s_v[ZROWS][ZSQ];
+    __shared__ double s_min[4];
+    __shared__ int s_wc[4];
     RSTAMP(16);
     const DevCtl* c = d.ctl;
     const int32_t st0 = c->status;
     int k = c->k, q = c->q;
-    const int bland = c->bland, m = d.m, lane = threadIdx.x;
+    const int bland = c->bland, m = d.m, tid = threadIdx.x;
     const double sig = c->sig, ptol = c->tol_primal, pivtol = c->tol_pivot;
     const int nfl = c->nflip;
-    const int r = lane / ZLPR, sub = lane % ZLPR;
+    const int r = tid / ZLPR, sub = tid % ZLPR;  // (r: the workgroup's row, 0..63)
     const bool roww = (int)blockIdx.x < nrt;
-    const int i = roww ? (int)blockIdx.x * ZRPW + r : 0;
+    const int i = roww ? (int)blockIdx.x * ZROWS + r : 0;
     const int ic = i < m ? i : (m > 0 ? m - 1 : 0);
     int64_t r0 = 0, r1 = 0;
     int u = -1;
@@ -2459,7 +2498,7 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sq(Dev d, int nrt, int flip, in
     }
     const bool fl = flip && nfl > 0;
     double tmin = HUGE_VAL, ge = 0.0, xe = 0.0, le = 0.0, he = 0.0;
-    int ve = -1, e = 0, region = blockIdx.x;
+    int ve = -1, e = 0;
     if (roww) {
         const bool act = i < m && u >= 0;
         int cnt = 0;
@@ -2478,8 +2517,8 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sq(Dev d, int nrt, int flip, in
             int mine = 0;
 #pragma unroll
             for (int b = 0; b < ZQB; ++b) mine += (t0 + sub + ZLPR * b < r1 && ps[b] >= 0 && ps[b] < k) ? 1 : 0;
-            // the quad's offsets: lanes 4r .. 4r + 3 (readlane-free: shuffles within the quad)
-            const int qb = lane & ~(ZLPR - 1);
+            // the quad's offsets (lanes 4r' .. 4r' + 3 of this wave: shuffles within the quad)
+            const int qb = (tid & 63) & ~(ZLPR - 1);
             int off = 0, tot = 0;
 #pragma unroll
             for (int s2 = 0; s2 < ZLPR; ++s2) {
@@ -2491,7 +2530,7 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sq(Dev d, int nrt, int flip, in
 #pragma unroll
             for (int b = 0; b < ZQB; ++b)
                 if (t0 + sub + ZLPR * b < r1 && ps[b] >= 0 && ps[b] < k) {
-                    if (o < SPZ_MAX) {
+                    if (o < ZSQ) {
                         s_p[r][o] = ps[b];
                         s_v[r][o] = vr[b];
                     }
@@ -2499,32 +2538,63 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sq(Dev d, int nrt, int flip, in
                 }
             cnt += tot;
         }
-        __syncthreads();  // (one wave: the quad's entries in LDS)
-        const bool over = cnt > SPZ_MAX;
-        if (act && (sub == 0 || (sub == 1 && fl))) {
-            int pp[SPZ_MAX];
-            double vv[SPZ_MAX];
-            const int nc = over ? 0 : cnt;
-#pragma unroll
-            for (int t = 0; t < SPZ_MAX; ++t) {
-                pp[t] = t < nc ? s_p[r][t] : 0;
-                vv[t] = t < nc ? s_v[r][t] : 0.0;
-            }
-            for (int a = 1; a < nc; ++a) {  // insertion sort by position (a handful of entries)
-                const int p = pp[a];
-                const double v = vv[a];
+        __syncthreads();  // (the quads' entries in LDS)
+        const bool over = cnt > ZSQ;
+        if (act && sub == 0 && !over) {  // insertion sort by position, in LDS (a handful of entries)
+            for (int a = 1; a < cnt; ++a) {
+                const int p = s_p[r][a];
+                const double v = s_v[r][a];
                 int b = a - 1;
-                while (b >= 0 && pp[b] > p) {
-                    pp[b + 1] = pp[b];
-                    vv[b + 1] = vv[b];
+                while (b >= 0 && s_p[r][b] > p) {
+                    s_p[r][b + 1] = s_p[r][b];
+                    s_v[r][b + 1] = s_v[r][b];
                     --b;
                 }
-                pp[b + 1] = p;
-                vv[b + 1] = v;
+                s_p[r][b + 1] = p;
+                s_v[r][b + 1] = v;
+            }
+        }
+        __syncthreads();
+        if (act && (sub == 0 || (sub == 1 && fl))) {
+            const double* xs = sub == 0 ? d.alS : d.fS;
+            double z = 0.0;
+            if (over) {  // the dense walk over AS, 32 positions' loads in flight per chunk
+                const size_t mm = (size_t)m;
+                for (int c0 = 0; c0 < k; c0 += ZCHUNK) {
+                    double a[ZCHUNK], xv[ZCHUNK];
+#pragma unroll
+                    for (int t = 0; t < ZCHUNK; ++t) {
+                        const int p = min(c0 + t, k - 1);
+                        a[t] = d.AS[(size_t)p * mm + i];
+                        xv[t] = xs[p];
+                    }
+                    double acc = 0.0;
+#pragma unroll
+                    for (int t = 0; t < ZCHUNK; ++t)
+                        if (c0 + t < k) acc = fma(a[t], xv[t], acc);
+                    z = z + acc;
+                }
+            } else {
+                double xv[ZSQ];
+#pragma unroll
+                for (int t = 0; t < ZSQ; ++t) xv[t] = xs[t < cnt ? s_p[r][t] : 0];
+                double acc = 0.0;
+                int ch = -1;
+#pragma unroll
+                for (int t = 0; t < ZSQ; ++t) {
+                    if (t >= cnt) break;
+                    const int pc = s_p[r][t] / ZCHUNK;
+                    if (pc != ch) {
+                        if (ch >= 0) z = z + acc;
+                        acc = 0.0;
+                        ch = pc;
+                    }
+                    acc = fma(s_v[r][t], xv[t], acc);
+                }
+                if (ch >= 0) z = z + acc;
             }
             const double sg = unit_sign(d, u, i);
             if (sub == 0) {
-                const double z = zrow_chain(d, i, k, pp, vv, nc, over, d.alS);
                 const double aiq = q >= d.N ? (i == q - d.N ? 1.0 : 0.0) : qi;
                 const double alU = sg * (aiq - z);
                 d.alU[i] = alU;
@@ -2538,15 +2608,14 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sq(Dev d, int nrt, int flip, in
                     tmin = harris1(ge, xe, le, he, ptol, pivtol, bland);
                 }
             } else {
-                const double tot = zrow_chain(d, i, k, pp, vv, nc, over, d.fS);
-                d.xr[i] = d.xr[i] - sg * (afi - tot);
+                d.xr[i] = d.xr[i] - sg * (afi - z);
             }
         }
         e = i;
-    } else {
-        const int p = (blockIdx.x - nrt) * 64 + lane;
+    } else {  // (64 positions per workgroup: a region holds at most RREG = 64 candidates)
+        const int p = (blockIdx.x - nrt) * 64 + tid;
         e = m + p;
-        if (p < k) {
+        if (tid < 64 && p < k) {
             if (flip) {
                 if (fl) d.xs[p] = d.xs[p] - d.fS[p];
             } else {
@@ -2559,9 +2628,9 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sq(Dev d, int nrt, int flip, in
             }
         }
     }
-    const double bmin = wave_min_f64(tmin);
-    if (lane == 0) d.blockmin[blockIdx.x] = bmin;
-    emit_wave(d, region, ve, e, ge, xe, le, he, bmin, pivtol);
+    const double bmin = block_min<256>(tmin, s_min);
+    if (tid == 0) d.blockmin[blockIdx.x] = bmin;
+    emit_block(d, blockIdx.x, ve, e, ge, xe, le, he, bmin, pivtol, s_wc);
     RSTAMP(19);
 }
 
@@ -5940,11 +6009,8 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     // CSC with a large bump: FTRAN-z from the rows of A (k_ftran_zr_sp: 64-row
     // tiles, 64-position bump tiles); else k_ftran_zr's 32-row tiles over AS
     const bool spz = use_spz(d, k_ub);
-#ifndef ELP_ZR_LPR
-#define ELP_ZR_LPR 4
-#endif
-    // (k_ftran_zr_sq: 16 rows per wave; ELP_ZR_LPR=1: k_ftran_zr_sp's 64)
-    const int nrt = spz ? (int)cdiv(m > 0 ? m : 1, ELP_ZR_LPR == 4 ? ZRPW : 64) : (int)cdiv(m > 0 ? m : 1, ZR_ROWS);
+    // (k_ftran_zr_sq: 64 rows per 4-wave workgroup; ELP_ZR_LPR=1: k_ftran_zr_sp's one wave)
+    const int nrt = spz ? (int)cdiv(m > 0 ? m : 1, 64) : (int)cdiv(m > 0 ? m : 1, ZR_ROWS);
     // z partials: 256 B per chunk of ZCHUNK bump positions in LDS (<= 64 KiB,
     // k <= 8192); larger bumps use a private slice of zpart per row tile
     const size_t lds = (size_t)cdiv(k_ub, ZCHUNK) * ZR_ROWS * sizeof(double);
@@ -5953,7 +6019,7 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     int zw = (ldsz && nrt > 256 && cdiv(k_ub, ZCHUNK) <= 8) ? 4 : 8;  // waves per row tile
     if (ldsz && (zw_env == 4 || zw_env == 8)) zw = zw_env;
     if (spz) zw = 1;
-    const int nbt = (int)cdiv(k_ub, 64 * zw);
+    const int nbt = (int)cdiv(k_ub, 64 * zw);  // bump tiles (k_ftran_zr_sq: 64 positions per workgroup)
     // alpha_S in LDS beside the z partials when the half-waves run more than one
     // chunk each (k_ub > 2 zw ZCHUNK) and it fits the prefetch (ZR_PA per thread):
     // 10 000 x 500 000 at k 529: 18.8 -> 16.3 us; with one chunk per half-wave the
@@ -5965,7 +6031,7 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     if (spz) {
         // (the dual phase: + nrt waves for the flips' x_B update, before the snapshot one)
         if (ELP_ZR_LPR == 4)
-            k_ftran_zr_sq<<<nrt + nbt + 1, 64, 0, st>>>(d, nrt, phase == 3 ? 1 : 0, dslot);
+            k_ftran_zr_sq<<<nrt + nbt + 1, 256, 0, st>>>(d, nrt, phase == 3 ? 1 : 0, dslot);
         else
             k_ftran_zr_sp<<<nrt + nbt + (phase == 3 && !ELP_ZR_MERGE ? nrt : 0) + 1, 64, 0, st>>>(
                 d, nrt, phase == 3 ? 1 : 0, dslot);
