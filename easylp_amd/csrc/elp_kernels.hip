@@ -2574,22 +2574,31 @@ __global__ void __launch_bounds__(256) k_ftran_zr_sq(Dev d, int nrt, int flip, i
                         if (c0 + t < k) acc = fma(a[t], xv[t], acc);
                     z = z + acc;
                 }
-            } else {
-                double xv[ZSQ];
-#pragma unroll
-                for (int t = 0; t < ZSQ; ++t) xv[t] = xs[t < cnt ? s_p[r][t] : 0];
+            } else {  // (batches of 8 gathers; static indices only -- no scratch)
                 double acc = 0.0;
                 int ch = -1;
 #pragma unroll
-                for (int t = 0; t < ZSQ; ++t) {
-                    if (t >= cnt) break;
-                    const int pc = s_p[r][t] / ZCHUNK;
-                    if (pc != ch) {
-                        if (ch >= 0) z = z + acc;
-                        acc = 0.0;
-                        ch = pc;
+                for (int t0 = 0; t0 < ZSQ; t0 += 8) {
+                    if (t0 < cnt) {
+                        int pv[8];
+                        double xv[8];
+#pragma unroll
+                        for (int b = 0; b < 8; ++b) {
+                            pv[b] = s_p[r][min(t0 + b, cnt - 1)];
+                            xv[b] = xs[pv[b]];
+                        }
+#pragma unroll
+                        for (int b = 0; b < 8; ++b)
+                            if (t0 + b < cnt) {
+                                const int pc = pv[b] / ZCHUNK;
+                                if (pc != ch) {
+                                    if (ch >= 0) z = z + acc;
+                                    acc = 0.0;
+                                    ch = pc;
+                                }
+                                acc = fma(s_v[r][t0 + b], xv[b], acc);
+                            }
                     }
-                    acc = fma(s_v[r][t], xv[t], acc);
                 }
                 if (ch >= 0) z = z + acc;
             }

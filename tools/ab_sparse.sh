@@ -31,6 +31,6 @@ for v in $NAMES; do
   unset "$(envof "$v" | cut -d= -f1)"
   cp "$(find "/tmp/ab_$v" -name '*kernel_stats.csv' | head -1)" "$OUT/ab_${TAG}_$v.csv"
   echo "== $v" | tee -a "$OUT/ab_$TAG.txt"
-  python3 "$ROOT/tools/kstats.py" "$OUT/ab_${TAG}_$v.csv" | head -12 | tee -a "$OUT/ab_$TAG.txt"
+  python3 "$ROOT/tools/kstats.py" "$OUT/ab_${TAG}_$v.csv" > "$OUT/ab_${TAG}_$v.txt"; head -12 "$OUT/ab_${TAG}_$v.txt" | tee -a "$OUT/ab_$TAG.txt"
 done
 echo done
