@@ -636,6 +636,13 @@ static int alloc_all_body(elp_handle* h) {
         }();
         d.noT = h->csc && !keep ? 1 : 0;
     }
+    {  // CSC: the sparse rank-one inverse update (ELP_SRU=0: the dense one, A/B)
+        static const bool off = [] {
+            const char* s = std::getenv("ELP_SRU");
+            return s && std::atoi(s) == 0;
+        }();
+        d.sru_on = h->csc && !off ? 1 : 0;
+    }
     // the mailbox carries the min-loc record only: with A not replicated the
     // entering column must travel, so that load uses the collective
     d.p2p = h->comm.p2p && h->replicated ? 1 : 0;
@@ -1987,6 +1994,8 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
                     if (r[i] && r[16]) h->stamp_sum[i] += 10.0 * (double)(long long)(r[i] - r[16]);
                 for (int i = 21; i < 24; ++i)  // the dual BFRT, relative to its start
                     if (r[i] && r[20]) h->stamp_sum[i] += 10.0 * (double)(long long)(r[i] - r[20]);
+                if (r[27] && r[20]) h->stamp_sum[27] += 10.0 * (double)(long long)(r[27] - r[20]);
+                for (int i : {24, 25, 26, 28}) h->stamp_sum[i] += (double)r[i];  // (counts)
                 h->stamp_n++;
             }
         }
@@ -2823,6 +2832,10 @@ extern "C" void elp_destroy(elp_handle* h) {
         std::fprintf(stderr, "k_dual_bfrt stamps (us after its start): compacted=%.2f decided=%.2f end=%.2f\n",
                      h->stamp_sum[21] / h->stamp_n / 1e3, h->stamp_sum[22] / h->stamp_n / 1e3,
                      h->stamp_sum[23] / h->stamp_n / 1e3);
+        std::fprintf(stderr, "k_dual_bfrt counts (per iteration): candidates=%.1f flips=%.2f one_wave=%.3f rounds=%.2f "
+                     "(wave: loaded=%.2f us)\n",
+                     h->stamp_sum[24] / h->stamp_n, h->stamp_sum[25] / h->stamp_n, h->stamp_sum[26] / h->stamp_n,
+                     h->stamp_sum[28] / h->stamp_n, h->stamp_sum[27] / h->stamp_n / 1e3);
     }
     if (!h) return;
     destroy_group(h);

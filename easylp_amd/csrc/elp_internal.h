@@ -46,7 +46,9 @@ enum : int32_t { ACT_NONE = 0, ACT_FLIP = 1, ACT_PIVOT = 2 };
 // slot chunks per pricing tile (one per wave); the oracle's PRICE_SPLIT must match
 constexpr int PRICE_SPLIT = ELP_PRICE_SPLIT;
 constexpr int ZCHUNK = 32;      // bump positions per FTRAN-z partial
-constexpr int DSTAMP_STRIDE = 24;  // ELP_STAMPS slots per chunk iteration (k_ratio 0-11, select 12-15, FTRAN-z 16-19, dual BFRT 20-23)
+constexpr int DSTAMP_STRIDE = 32;  // ELP_STAMPS slots per chunk iteration (k_ratio 0-11, select 12-15, FTRAN-z 16-19, dual BFRT 20-23;
+                                    // 24-26, 28: the dual BFRT's counts -- candidates, flips, one-wave path,
+                                    // bunch rounds; 27: bfrt_wave's candidates loaded)
 constexpr int RREG = 64;  // pass-2 candidate slots per k_ftran_zr wave region
 constexpr int TILE_COLS = 128;  // columns per pricing workgroup (2 per lane)
 
@@ -115,7 +117,8 @@ struct DevCtl {
     int32_t plan_seq, applied_seq;
     // the dual phase's deferred update (one GPU): the plan whose x_B / dual
     // Devex / AS part k_dual_chuzr applied (its inverse part: applied_seq)
-    int32_t copy_seq, pad9;
+    int32_t copy_seq;
+    int32_t pad9;
     int64_t mb_epoch;  // xGMI mailbox: loads so far (seq = epoch << 40 | iteration + 1)
     // Devex pricing (elp_control.pricing): the last pivot as the next pricing
     // pass needs it -- entering reduced cost and weight, leaving variable;
@@ -326,6 +329,11 @@ struct Dev {
     // (sparse lists) or a gather -- and the per-pivot inverse update moves half
     // the bytes; MinvT is then null
     int32_t noT;
+    // CSC: the per-pivot inverse update touches only the pairs of nonzero
+    // multipliers (apply_minv_sru: the bump inverse of a sparse LP is sparse),
+    // in trailing workgroups of the pricing launch, one per SRU_ROWS rows
+    // (ELP_SRU=0: the dense update over all k^2 entries)
+    int32_t sru_on;
 };
 constexpr int AFL_SB = 1;    // afl: bucket starts [1, 66)
 constexpr int AFL_POS = 66;  // afl: positions [66, 66 + SPL)

@@ -931,6 +931,8 @@ struct Plan;
 DEV void apply_plan(const Dev& d, const Plan& P, int blk, int nb, int nb_minv, bool do_ar, bool batch = true);
 DEV void apply_minv(const Dev& d, const Plan& P, int64_t e0, int64_t estride, bool batch = true);
 DEV void apply_copy(const Dev& d, const Plan& P, int64_t t0, int64_t tstride, bool do_ar);
+template <int NT>
+DEV void apply_minv_sru(const Dev& d, const Plan& P, int wg, int nwg);
 DEV bool plan_pending(const DevCtl* c) { return c->plan_seq != c->applied_seq && c->plan.action != ACT_NONE; }
 // the pricing launch's trailing `napply` workgroups apply the pending plan
 // batch: the inverse update's loads grouped ahead of its stores (apply_minv);
@@ -1396,7 +1398,75 @@ __global__ void __launch_bounds__(TILE_COLS) k_price_csc(Dev d, int napply, int 
 DEV void price_csc_body(const Dev& d, int napply, int nb_minv, int nsw) {
     __shared__ double sv[CSC_STAGE], sy[CSC_STAGE];
     __shared__ Cand red[TILE_COLS / 64];
-    if (apply_role(d, napply, nb_minv)) return;
+    if ((int)blockIdx.x >= (int)gridDim.x - napply) {  // (apply_role; the sparse update under Dev::sru_on)
+        PDBG(1, 1ull);
+        const DevCtl* cc = d.ctl;
+        if (plan_pending(cc) && cc->status != ST_NUMFAIL) {
+            const Plan P = cc->plan;
+            const int blk = (int)blockIdx.x - ((int)gridDim.x - napply);
+            if (d.sru_on && blk < nb_minv) apply_minv_sru<TILE_COLS>(d, P, blk, nb_minv);
+            else apply_plan(d, P, blk, napply, nb_minv, false, true);
+        }
+        return;
+    }
+#ifndef ELP_PCSC_PF
+#define ELP_PCSC_PF 1
+#endif
+#if ELP_PCSC_PF
+    const DevCtl* c = d.ctl;
+    const int64_t ntiles = gridDim.x - napply - nsw;
+    const bool tilewg = (int64_t)blockIdx.x < ntiles;
+    // the tile's extent and this column's (start, end, status, cost) issued
+    // with the control block's loads (straight-line: one round trip, not three)
+    const int64_t j0 = tilewg ? (int64_t)blockIdx.x * TILE_COLS : 0;
+    const int64_t j = j0 + threadIdx.x;
+    const int64_t jend = j0 + TILE_COLS < d.n ? j0 + TILE_COLS : d.n;
+    const int64_t jc = j < d.n ? j : (d.n > 0 ? d.n - 1 : 0);
+    const int64_t s0 = d.cptr[j0], s1 = d.cptr[jend];
+    const int64_t a = d.cptr[jc], b = d.cptr[jc + 1];
+    const int8_t vsj = d.vstat[jc];
+    const double cj = d.cost[jc];
+    const double dwj = d.dw ? d.dw[jc] : 1.0, dpj = d.dprev ? d.dprev[jc] : 0.0;
+    __builtin_amdgcn_sched_barrier(0);
+    if (c->status != ST_RUN) {
+        KEEP(s0);
+        KEEP(a);
+        KEEP(cj);
+        KEEP(dwj);
+        return;
+    }
+    if (!tilewg) {  // a slack workgroup
+        PDBG(1, 2ull);
+        price_slacks<TILE_COLS>(d, ntiles, (int)(blockIdx.x - ntiles), nsw, red);
+        return;
+    }
+    PDBG(1, __builtin_amdgcn_s_memrealtime());
+    const int bland = c->bland;
+    const bool staged = s1 - s0 <= CSC_STAGE;
+    if (staged) {  // (<= CSC_STAGE / TILE_COLS entries per thread: every gather in flight at once)
+        constexpr int SPT = CSC_STAGE / TILE_COLS;
+        int ii[SPT];
+        double vv[SPT], yv[SPT];
+#pragma unroll
+        for (int u = 0; u < SPT; ++u) {
+            const int64_t t = s0 + threadIdx.x + (int64_t)u * TILE_COLS;
+            const int64_t tc = t < s1 ? t : (s1 > s0 ? s1 - 1 : s0);
+            ii[u] = d.rind[tc];
+            vv[u] = d.cval[tc];
+        }
+#pragma unroll
+        for (int u = 0; u < SPT; ++u) yv[u] = d.y[ii[u]];
+#pragma unroll
+        for (int u = 0; u < SPT; ++u) {
+            const int64_t t = s0 + threadIdx.x + (int64_t)u * TILE_COLS;
+            if (t < s1) {
+                sv[t - s0] = vv[u];
+                sy[t - s0] = yv[u];
+            }
+        }
+        __syncthreads();
+    }
+#else
     const DevCtl* c = d.ctl;
     if (c->status != ST_RUN) return;
     const int64_t ntiles = gridDim.x - napply - nsw;
@@ -1417,9 +1487,15 @@ DEV void price_csc_body(const Dev& d, int napply, int nb_minv, int nsw) {
         }
         __syncthreads();
     }
+    const int64_t jc = j < d.n ? j : (d.n > 0 ? d.n - 1 : 0);
+    const int64_t a = d.cptr[jc], b = d.cptr[jc + 1];
+    const int8_t vsj = d.vstat[jc];
+    const double cj = d.cost[jc];
+    const double dwj = d.dw[jc], dpj = d.dprev[jc];
+#endif
+    PDBG(2, __builtin_amdgcn_s_memrealtime());
     double acc = 0.0;
     if (j < d.n) {
-        const int64_t a = d.cptr[j], b = d.cptr[j + 1];
         if (staged) {
             for (int64_t t = a - s0; t < b - s0; ++t) acc = fma(sv[t], sy[t], acc);
         } else {
@@ -1432,15 +1508,17 @@ DEV void price_csc_body(const Dev& d, int napply, int nb_minv, int nsw) {
     best.d = 0.0;
     best.w = 1.0;
     if (j < d.n) {
-        const int8_t vs = d.vstat[j];
+        const int8_t vs = vsj;
         if (vs != VS_BASIC && vs != VS_FIXED) {
-            const double dj = d.cost[j] - acc;
+            const double dj = cj - acc;
             const int devex = c->devex;
-            const double wj = devex ? devex_weight(d, devex_in(c), j, d.col0 + j, dj, d.dw[j], d.dprev[j]) : 1.0;
+            const double wj = devex ? devex_weight(d, devex_in(c), j, d.col0 + j, dj, dwj, dpj) : 1.0;
             best = price_cand(vs, dj, wj, devex, c->tol_dual, d.col0 + j);
         }
     }
+    PDBG(3, __builtin_amdgcn_s_memrealtime());
     best = block_best<TILE_COLS>(best, bland, red);
+    PDBG(4, __builtin_amdgcn_s_memrealtime());
     if (threadIdx.x == 0) d.cand[blockIdx.x] = best;
 }
 
@@ -3668,25 +3746,35 @@ struct OldM {
 // The plan k_ratio made: Minv and MinvT update (blocks [0, nb_minv)) + primal
 // update x_B -= step*alpha and AS copies (blocks [nb_minv, nb)); with do_ar also
 // the AR row copies (phase 1, where nothing is deferred).  Flips only update x_B.
+// The rank-one term of every update form: ov - x1 x2, and ov itself when a
+// multiplier is zero (the oracle's fma(-x1, x2, ov) returns ov then too, up to
+// the sign of a zero ov: -0 + +0 = +0).  The zero rule lets the sparse update
+// (apply_minv_sru) leave the untouched entries alone and still give every
+// path -- dense, sparse, on the fly -- the same bits; a zero's sign reaches no
+// later value or decision (products with it are zeros, sums with a nonzero
+// term ignore it, comparisons see +-0 alike, no entry of the inverse is a
+// divisor without passing the pivot tolerance), so the traces and solutions
+// stay the oracle's.
+DEV double r1(double ov, double x1, double x2) { return (x1 == 0.0 || x2 == 0.0) ? ov : fma(-x1, x2, ov); }
 // new value of bump-inverse element (i, j) (the sequential path below)
 DEV double minv_new(const Dev& d, const Plan& P, int i, int j, const OldM& old) {
     const int k = P.k_old;
     switch (P.pcase) {
         case PC_A:
-            return (i == P.p) ? d.vrow[j] : fma(-d.alS[i], d.vrow[j], old(i, j));
+            return (i == P.p) ? d.vrow[j] : r1(old(i, j), d.alS[i], d.vrow[j]);
         case PC_B:
-            if (i < k && j < k) return fma(d.alS[i], d.vvec[j], old(i, j));
+            if (i < k && j < k) return r1(old(i, j), -d.alS[i], d.vvec[j]);
             if (i < k) return -(d.alS[i] / P.piv);
             if (j < k) return -d.vvec[j];
             return 1.0 / P.piv;
         case PC_C: {
             const int sr = (i == P.b) ? P.last : i;
             const int sc = (j == P.a) ? P.last : j;
-            return fma(-d.colA[sr], d.vrow[sc], old(sr, sc));
+            return r1(old(sr, sc), d.colA[sr], d.vrow[sc]);
         }
         default: {  // PC_D
             const double ca = d.colA[i] / d.vvec[P.a];
-            return (j == P.a) ? ca : fma(-ca, d.vvec[j], old(i, j));
+            return (j == P.a) ? ca : r1(old(i, j), ca, d.vvec[j]);
         }
     }
 }
@@ -3790,17 +3878,17 @@ DEV void apply_minv_half(const Dev& d, const Plan& P, int64_t e, int64_t end, in
             const int i = ii[u], j = jj[u];
             double v;
             if (pc == PC_A) {
-                v = (i == P.p) ? x2[u] : fma(-x1[u], x2[u], ov[u]);
+                v = (i == P.p) ? x2[u] : r1(ov[u], x1[u], x2[u]);
             } else if (pc == PC_B) {
-                if (i < k && j < k) v = fma(x1[u], x2[u], ov[u]);
+                if (i < k && j < k) v = r1(ov[u], -x1[u], x2[u]);
                 else if (i < k) v = -(x1[u] / P.piv);
                 else if (j < k) v = -x2[u];
                 else v = 1.0 / P.piv;
             } else if (pc == PC_C) {
-                v = fma(-x1[u], x2[u], ov[u]);
+                v = r1(ov[u], x1[u], x2[u]);
             } else {  // PC_D
                 const double ca = x1[u] / va;
-                v = (j == P.a) ? ca : fma(-ca, x2[u], ov[u]);
+                v = (j == P.a) ? ca : r1(ov[u], ca, x2[u]);
             }
             if (TR) M[(size_t)j * ldm + (size_t)i] = v;
             else M[(size_t)i * ldm + (size_t)j] = v;
@@ -3821,6 +3909,135 @@ DEV void apply_minv(const Dev& d, const Plan& P, int64_t e0, int64_t estride, bo
         e0 += (nel - e0 + estride - 1) / estride * estride;
     }
     if (e0 < 2 * nel && !d.noT) apply_minv_half<true, MINV_U>(d, P, e0, 2 * nel, estride, nel, kk);
+}
+
+// The sparse rank-one update (Dev::sru_on, CSC): workgroup wg of nwg.  The
+// bump inverse of a sparse LP is sparse (the 20 000 x 100 000 KKT LP's final
+// bump is triangular after permutation: ~1.6 nonzeros per row of its
+// inverse), and so are the update's multipliers x1 (alpha_S / column a of the
+// inverse) and x2 (the pivot row / v): r05 counts 87 / 100 nonzeros of 2000 per
+// dual pivot there, ~900 / ~1000 per primal pivot of the feasible-start LP.  By
+// the zero rule of r1 only the pairs of nonzeros change, plus the border the
+// case rewrites (A: row p; B: row and column k; C: row b and column a, moved
+// from the last ones; D: column a).  Workgroup wg owns rows [wg R, wg R + R)
+// (R <= SRU_ROWS: the host launches cdiv(k + 1, SRU_ROWS) of them): one load
+// per row tells which of them have a nonzero multiplier -- the others exit
+// there -- then the workgroup lists x2's nonzeros in LDS (past SRU_CAP: every
+// column, tested) and updates its rows' pairs, SRU_U loads in flight per
+// thread; the border is strided over the whole launch.  Every entry it writes
+// is written by the dense update too, with the same bits.
+constexpr int SRU_CAP = 1024, SRU_ROWS = 8, SRU_U = 8;
+constexpr unsigned sru_wgs(int k_ub) { return (unsigned)((k_ub + 1 + SRU_ROWS - 1) / SRU_ROWS); }
+template <int NT>
+DEV void apply_minv_sru(const Dev& d, const Plan& P, int wg, int nwg) {
+    __shared__ int s_l2[SRU_CAP], s_rows[64], s_scan[NT / 64];
+    __shared__ double s_a1[64];
+    if (P.action != ACT_PIVOT || P.pcase == PC_E || nwg <= 0) return;
+    const int k = P.k_old, pc = P.pcase, tid = threadIdx.x, lane = tid & 63;
+    const int kk = pc == PC_B ? k + 1 : pc == PC_C ? k - 1 : k;
+    if (kk <= 0) return;
+    const int nl = pc == PC_B ? k : kk;  // the rank-one part's index range
+    const double* x1 = (pc == PC_C || pc == PC_D) ? d.colA : d.alS;
+    const double* x2 = (pc == PC_B || pc == PC_D) ? d.vvec : d.vrow;
+    const int ex1 = pc == PC_A ? P.p : pc == PC_C ? P.b : -1;  // (the row / column the border rewrites)
+    const int ex2 = (pc == PC_C || pc == PC_D) ? P.a : -1;
+    const double va = pc == PC_D ? d.vvec[P.a] : 1.0;
+    const size_t ldm = (size_t)d.ldm;
+    double* M = d.Minv;
+    double* MT = d.noT ? nullptr : d.MinvT;
+    const int R = (nl + nwg - 1) / nwg;
+    const int r0 = min(nl, wg * R), r1e = min(nl, r0 + R);
+    bool listed = false;
+    int n2 = 0;
+    for (int g0 = r0; g0 < r1e; g0 += 64) {  // (one pass: R <= 64)
+        // the multipliers of rows g0 + lane (every wave alike: a uniform mask)
+        const int i = g0 + lane;
+        double a1 = 0.0;
+        if (i < r1e && i != ex1) {
+            a1 = x1[i];
+            if (pc == PC_B) a1 = -a1;
+            else if (pc == PC_D) a1 = a1 / va;
+        }
+        const unsigned long long rm = __ballot(a1 != 0.0);
+        if (rm == 0ull) continue;
+        const int nr = __popcll(rm);
+        if (tid < 64 && a1 != 0.0) {
+            const int o = __popcll(rm & ((1ull << lane) - 1ull));
+            s_rows[o] = i;
+            s_a1[o] = a1;
+        }
+        if (!listed) {  // x2's nonzeros, ascending (an ordered scan: one segment per thread)
+            listed = true;
+            const int seg = (nl + NT - 1) / NT, s0 = min(nl, tid * seg), s1 = min(nl, s0 + seg);
+            int c2 = 0;
+            for (int t = s0; t < s1; ++t) c2 += (t != ex2 && x2[t] != 0.0) ? 1 : 0;
+            int o2;
+            n2 = block_scan_excl<NT>(c2, &o2, s_scan);
+            if (n2 <= SRU_CAP)
+                for (int t = s0; t < s1; ++t)
+                    if (t != ex2 && x2[t] != 0.0) s_l2[o2++] = t;
+        }
+        __syncthreads();  // (s_rows / s_a1 / the list)
+        const bool lst = n2 <= SRU_CAP;
+        const int nc = lst ? n2 : nl;  // (no list: every column, tested)
+        const int64_t ne = (int64_t)nr * nc;
+        for (int64_t e0 = tid; e0 < ne; e0 += (int64_t)NT * SRU_U) {
+            int ii[SRU_U], jj[SRU_U];
+            double aa[SRU_U], bb[SRU_U], ov[SRU_U];
+#pragma unroll
+            for (int u = 0; u < SRU_U; ++u) {
+                const int64_t e = e0 + (int64_t)u * NT;
+                const int64_t ec = e < ne ? e : ne - 1;
+                const int rr = (int)(ec / nc), t = (int)(ec % nc);
+                ii[u] = s_rows[rr];
+                aa[u] = s_a1[rr];
+                jj[u] = lst ? s_l2[t] : t;
+                bb[u] = x2[jj[u]];
+                ov[u] = M[(size_t)ii[u] * ldm + jj[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < SRU_U; ++u) {
+                if (e0 + (int64_t)u * NT >= ne || jj[u] == ex2 || bb[u] == 0.0) continue;
+                const double v = fma(-aa[u], bb[u], ov[u]);
+                M[(size_t)ii[u] * ldm + jj[u]] = v;
+                if (MT) MT[(size_t)jj[u] * ldm + ii[u]] = v;
+            }
+        }
+        __syncthreads();  // (s_rows is rewritten by a next group)
+    }
+    // ---- the border, strided over the launch
+    auto put = [&](int i, int j, double v) {
+        M[(size_t)i * ldm + j] = v;
+        if (MT) MT[(size_t)j * ldm + i] = v;
+    };
+    const int64_t g = (int64_t)wg * NT + tid, G = (int64_t)nwg * NT;
+    switch (pc) {
+        case PC_A:
+            for (int64_t j = g; j < k; j += G) put(P.p, (int)j, d.vrow[j]);
+            break;
+        case PC_B:
+            for (int64_t t = g; t < 2 * (int64_t)k + 1; t += G) {
+                if (t < k) put((int)t, k, -(d.alS[t] / P.piv));
+                else if (t < 2 * k) put(k, (int)(t - k), -d.vvec[t - k]);
+                else put(k, k, 1.0 / P.piv);
+            }
+            break;
+        case PC_C: {
+            const int last = P.last, b = P.b, a = P.a;
+            if (b != last)
+                for (int64_t j = g; j < kk; j += G) {
+                    const int sc = (int)j == a ? last : (int)j;
+                    put(b, (int)j, r1(M[(size_t)last * ldm + sc], d.colA[last], d.vrow[sc]));
+                }
+            if (a != last)
+                for (int64_t i = g; i < kk; i += G)
+                    if ((int)i != b) put((int)i, a, r1(M[(size_t)i * ldm + last], d.colA[i], d.vrow[last]));
+            break;
+        }
+        default:  // PC_D
+            for (int64_t i = g; i < k; i += G) put((int)i, P.a, d.colA[i] / va);
+            break;
+    }
 }
 
 // the primal update and the AS (/ AR) copies of a plan: thread t0 of tstride
@@ -3924,6 +4141,7 @@ DEV void apply_minv_part(const Dev& d, const Plan& P, int part, int64_t t0, int6
     const int k = P.k_old;
     const int kk = P.pcase == PC_B ? k + 1 : P.pcase == PC_C ? k - 1 : k;
     const int64_t nel = (int64_t)kk * kk;
+    if (d.sru_on) return;  // (the sparse update: all of it by the pricing launch's apply_minv_sru)
     if (nel == 0 || t0 >= nel) return;
     if (d.noT) {  // no MinvT: the two launches split Minv (rows [h, kk) here in part 0, [0, h) in part 1)
         const int64_t h = (int64_t)(kk / 2) * kk;
@@ -4935,8 +5153,8 @@ __global__ void __launch_bounds__(PRICE_THREADS) k_dual_price(Dev d, int nsw, in
     if (napply > 0 && (int)blockIdx.x >= (int)gridDim.x - napply) {
         if (minv_pending(c)) {
             const Plan P = c->plan;
-            apply_minv_part(d, P, 1, (int64_t)(blockIdx.x - (gridDim.x - napply)) * blockDim.x + threadIdx.x,
-                            (int64_t)napply * blockDim.x);
+            const int wg = (int)blockIdx.x - ((int)gridDim.x - napply);
+            apply_minv_part(d, P, 1, (int64_t)wg * blockDim.x + threadIdx.x, (int64_t)napply * blockDim.x);
         }
         return;
     }
@@ -5027,8 +5245,9 @@ __global__ void __launch_bounds__(TILE_COLS) k_dual_price_csc(Dev d, int nsw, in
     if (napply > 0 && (int)blockIdx.x >= (int)gridDim.x - napply) {
         if (minv_pending(c)) {
             const Plan P = c->plan;
-            apply_minv_part(d, P, 1, (int64_t)(blockIdx.x - (gridDim.x - napply)) * blockDim.x + threadIdx.x,
-                            (int64_t)napply * blockDim.x);
+            const int wg = (int)blockIdx.x - ((int)gridDim.x - napply);
+            if (d.sru_on) apply_minv_sru<TILE_COLS>(d, P, wg, napply);
+            else apply_minv_part(d, P, 1, (int64_t)wg * blockDim.x + threadIdx.x, (int64_t)napply * blockDim.x);
         }
         return;
     }
@@ -5054,14 +5273,38 @@ __global__ void __launch_bounds__(TILE_COLS) k_dual_price_csc(Dev d, int nsw, in
     if (j < d.n) {
         const int8_t vs = d.vstat[j];
         if (vs != VS_BASIC && vs != VS_FIXED) {
+            // batches of DPB entries: each level of the row index -> rpos / y ->
+            // rho_R gathers in flight together (one round trip per level, not
+            // three per nonzero), the chains in ascending rows as before
+#ifndef ELP_DPB
+#define ELP_DPB 1
+#endif
+            constexpr int DPB = ELP_DPB;
             double ad = 0.0, aa = 0.0;
-            for (int64_t t = d.cptr[j]; t < d.cptr[j + 1]; ++t) {
-                const int i = d.rind[t];
-                const double v = d.cval[t];
-                const int rp = d.rpos[i];
-                const double rho = rp >= 0 ? d.rhoR[rp] : (i == xrow ? xsig : 0.0);
-                ad = fma(v, d.y[i], ad);
-                aa = fma(v, rho, aa);
+            const int64_t t1 = d.cptr[j + 1];
+            for (int64_t t0 = d.cptr[j]; t0 < t1; t0 += DPB) {
+                int ii[DPB], rp[DPB];
+                double vv[DPB], yv[DPB], rh[DPB];
+#pragma unroll
+                for (int b = 0; b < DPB; ++b) {
+                    const int64_t tt = t0 + b < t1 ? t0 + b : t1 - 1;
+                    ii[b] = d.rind[tt];
+                    vv[b] = d.cval[tt];
+                }
+#pragma unroll
+                for (int b = 0; b < DPB; ++b) {
+                    rp[b] = d.rpos[ii[b]];
+                    yv[b] = d.y[ii[b]];
+                }
+#pragma unroll
+                for (int b = 0; b < DPB; ++b) rh[b] = d.rhoR[rp[b] >= 0 ? rp[b] : 0];
+#pragma unroll
+                for (int b = 0; b < DPB; ++b)
+                    if (t0 + b < t1) {
+                        const double rho = rp[b] >= 0 ? rh[b] : (ii[b] == xrow ? xsig : 0.0);
+                        ad = fma(vv[b], yv[b], ad);
+                        aa = fma(vv[b], rho, aa);
+                    }
             }
             f = dual_candidate(vs, aa, d.cost[j] - ad, d.lb[j], d.ub[j], rs, bland, dtol, pivtol, (int)j, d.xval[j],
                                d.cost[j], o);
@@ -5141,7 +5384,7 @@ __global__ void __launch_bounds__(BF_NT) k_dual_pack(Dev d, int nreg) {
 // shuffles (no workgroup barrier per step), the flip sum is lane 0's in-order
 // fma chain over the bunch staged in LDS.  Same decisions as the block path.
 DEV void bfrt_wave(const Dev& d, int N, int bland, double ptol, double slope, double* s_bun, int* nflip_out,
-                   int* qidx_out, int* s_flip) {
+                   int* qidx_out, int* s_flip, int dslot) {
     const int lane = threadIdx.x & 63;
     const int run = (N + 63) / 64;
     const int lo = min(N, lane * run), hi = min(N, lo + run);
@@ -5164,8 +5407,10 @@ DEV void bfrt_wave(const Dev& d, int N, int bland, double ptol, double slope, do
             ral |= 1u << q;
         }
     }
-    int nflip = 0, qidx = -1;
+    int nflip = 0, qidx = -1, rounds = 0;
+    RSTAMP(27);
     for (;;) {
+        ++rounds;
         if (!__any(ral != 0)) break;  // nothing left: the dual ray (q = -1)
         double bmin = INF;
 #pragma unroll
@@ -5240,6 +5485,7 @@ DEV void bfrt_wave(const Dev& d, int N, int bland, double ptol, double slope, do
         qidx = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(bi, win));
         break;
     }
+    if (ELP_DIAG && d.dstamp && threadIdx.x == 0) d.dstamp[dslot * DSTAMP_STRIDE + 28] = (unsigned long long)rounds;
     *nflip_out = nflip;
     *qidx_out = qidx;
 }
@@ -5386,7 +5632,7 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     int nflip = 0, qidx = -1;
     const bool wave = reg_ok >= 2 && N <= 64 * BF_RR;  // (bfrt_wave: the usual case)
     if (wave) {
-        if (tid < 64) bfrt_wave(d, N, bland, ptol, fabs(c->dr_x - c->dr_beta), s_bun, &nflip, &qidx, s_flip);
+        if (tid < 64) bfrt_wave(d, N, bland, ptol, fabs(c->dr_x - c->dr_beta), s_bun, &nflip, &qidx, s_flip, dslot);
         if (tid == 0) {
             s_int[2] = nflip;
             s_int[3] = qidx;
@@ -5576,6 +5822,11 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     }
     __syncthreads();
     RSTAMP(22);
+    if (ELP_DIAG && d.dstamp && tid == 0) {
+        d.dstamp[dslot * DSTAMP_STRIDE + 24] = (unsigned long long)N;
+        d.dstamp[dslot * DSTAMP_STRIDE + 25] = (unsigned long long)nflip;
+        d.dstamp[dslot * DSTAMP_STRIDE + 26] = wave ? 1ull : 0ull;
+    }
     // the flips: compact indices -> ids and dx = +-(u - l) (the record's range)
     // (the new status and value from the record's bounds: the column's own)
     int myj = -1;
@@ -5958,7 +6209,13 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phas
     #ifndef ELP_APPLY_PT
 #define ELP_APPLY_PT 4
 #endif
-    if (phase == 2 && d.csc) update_grid(d, k_ub, false, &nb_minv, &napply, TILE_COLS, ELP_APPLY_PT, ELP_MINV_WG_MAX);
+    if (phase == 2 && d.csc) {
+        update_grid(d, k_ub, false, &nb_minv, &napply, TILE_COLS, ELP_APPLY_PT, ELP_MINV_WG_MAX);
+        if (d.sru_on) {  // (the sparse update: sru_wgs workgroups instead of the dense share)
+            napply = napply - nb_minv + sru_wgs(k_ub);
+            nb_minv = sru_wgs(k_ub);
+        }
+    }
     // the dense deferred plan in trailing workgroups of the launch (r02's
     // layout, the default again since r04: 3 x 3 interleaved A/B at 5000 x 50000,
     // 25.4k against 24.7k iterations/s with the tiles' waves 1-3 applying it);
@@ -6167,7 +6424,7 @@ static int dual_head(const Dev& d, int k_ub, int ny_ub, hipStream_t st, int defe
     k_dual_row<<<nrw, 256, lds_row && !sp ? lds : 0, st>>>(d, (int)nchz, lds_row && !sp, sp, defer);
     const int nsw = d.dslack ? slack_wgs(d, ny_ub) : 0;
     if (d.csc) {
-        const int na = defer ? (int)defer_wgs(k_ub, TILE_COLS, 8192) : 0;
+        const int na = defer ? (d.sru_on ? (int)sru_wgs(k_ub) : (int)defer_wgs(k_ub, TILE_COLS, 8192)) : 0;
         k_dual_price_csc<<<d.ntiles + nsw + na, TILE_COLS, 0, st>>>(d, nsw, 0, na);
     } else {
         const int na = defer ? (int)defer_wgs(k_ub, PRICE_THREADS, 4096) : 0;
@@ -6208,7 +6465,9 @@ hipError_t launch_dual_iteration(const Dev& d, int k_ub, int ny_ub, hipStream_t 
     const int defer = d.dual_defer ? 1 : 0;
     const int nreg = dual_head(d, k_ub, ny_ub, st, defer);
     // (dual_defer: + the Minv half of the last plan's update beside the ratio test)
-    k_dual_bfrt<<<1 + (defer ? defer_wgs(k_ub, BF_NT, 1024) : 0), BF_NT, 0, st>>>(d, nreg, 0, bfrt_reg(), dslot);
+    // (the sparse update: none -- the pricing launch's workgroups took all of it)
+    const unsigned nbf = defer && !(d.csc && d.sru_on) ? defer_wgs(k_ub, BF_NT, 1024) : 0;
+    k_dual_bfrt<<<1 + nbf, BF_NT, 0, st>>>(d, nreg, 0, bfrt_reg(), dslot);
     return dual_tail(d, k_ub, st, true, defer, dslot);
 }
 

@@ -2,7 +2,9 @@
 20 000 x 100 000 sparse_kkt LPs of tests/golden/sparse_lu.json -- the
 feasible-start one and the phase-1 one (dual simplex phase 1) -- solved to
 optimality with the default basis (the bump inverse), timed, against the HiGHS
-objective.  ELP_LIB_PATH picks a library variant (A/B)."""
+objective.  ELP_LIB_PATH picks a library variant (A/B); ELP_PROBE_VERBOSE sets
+elp_control.verbose (diagnostic builds: 2 = the pricing stamps, for
+ELP_PDBG_FILE / ELP_PDBG_ITER timelines)."""
 import json
 import os
 import sys
@@ -22,7 +24,7 @@ def main():
         k = fx[name]
         cp, ri, v, b, c, u, obj = sparse_kkt(k["seed"], k["m"], k["n"], k["k"], feasible_start=k["feasible_start"])
         m, n = k["m"], k["n"]
-        with Problem(m, n) as p:
+        with Problem(m, n, verbose=int(os.environ.get("ELP_PROBE_VERBOSE", "0"))) as p:
             t0 = time.perf_counter()
             p.load_csc(cp, ri, v, np.ones(m, np.int32), b, c, np.zeros(n), u, maximize=True)
             st = p.solve()
