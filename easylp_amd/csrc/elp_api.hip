@@ -725,11 +725,12 @@ static int alloc_all_body(elp_handle* h) {
     // tile candidates + the slack workgroups' (|Y| <= m, >= 128 slots each)
     A(dalloc(&d.cand, (size_t)d.ntiles + (size_t)((mm + TILE_COLS - 1) / TILE_COLS) + 64));
     // one stamp pair per pricing workgroup: tiles, slack workgroups (<= m / 128 + 1)
-    // and the apply workgroups (<= 2048 + 1024, launch_btran_price)
+    // and the apply workgroups (<= ELP_MINV_WG_MAX 8192 + 1024 copy workgroups,
+    // launch_btran_price; the sparse update's <= 4096)
 #ifdef ELP_PDBG
-    A(dalloc(&d.pstamp, 6 * ((size_t)d.ntiles + (size_t)(mm / 128 + 1) + 3072 + 64)));
+    A(dalloc(&d.pstamp, 6 * ((size_t)d.ntiles + (size_t)(mm / 128 + 1) + 8192 + 1024 + 64)));
 #else
-    A(dalloc(&d.pstamp, 2 * ((size_t)d.ntiles + (size_t)(mm / 128 + 1) + 3072 + 64)));
+    A(dalloc(&d.pstamp, 2 * ((size_t)d.ntiles + (size_t)(mm / 128 + 1) + 8192 + 1024 + 64)));
 #endif
     if (h->csc) A(dalloc(&d.qcol, mm));
     if (h->csc) A(dalloc(&d.spos, (size_t)(n > 0 ? n : 1)));  // (the sparse FTRAN-z's column -> position)

@@ -1427,6 +1427,9 @@ DEV void price_csc_body(const Dev& d, int napply, int nb_minv, int nsw) {
     const int8_t vsj = d.vstat[jc];
     const double cj = d.cost[jc];
     const double dwj = d.dw ? d.dw[jc] : 1.0, dpj = d.dprev ? d.dprev[jc] : 0.0;
+    const int cdevex = c->devex;  // (the control fields the epilogue needs, with the status)
+    const DevexIn cdx = devex_in(c);
+    const double ctold = c->tol_dual;
     __builtin_amdgcn_sched_barrier(0);
     if (c->status != ST_RUN) {
         KEEP(s0);
@@ -1492,6 +1495,9 @@ DEV void price_csc_body(const Dev& d, int napply, int nb_minv, int nsw) {
     const int8_t vsj = d.vstat[jc];
     const double cj = d.cost[jc];
     const double dwj = d.dw[jc], dpj = d.dprev[jc];
+    const int cdevex = c->devex;
+    const DevexIn cdx = devex_in(c);
+    const double ctold = c->tol_dual;
 #endif
     PDBG(2, __builtin_amdgcn_s_memrealtime());
     double acc = 0.0;
@@ -1511,9 +1517,8 @@ DEV void price_csc_body(const Dev& d, int napply, int nb_minv, int nsw) {
         const int8_t vs = vsj;
         if (vs != VS_BASIC && vs != VS_FIXED) {
             const double dj = cj - acc;
-            const int devex = c->devex;
-            const double wj = devex ? devex_weight(d, devex_in(c), j, d.col0 + j, dj, dwj, dpj) : 1.0;
-            best = price_cand(vs, dj, wj, devex, c->tol_dual, d.col0 + j);
+            const double wj = cdevex ? devex_weight(d, cdx, j, d.col0 + j, dj, dwj, dpj) : 1.0;
+            best = price_cand(vs, dj, wj, cdevex, ctold, d.col0 + j);
         }
     }
     PDBG(3, __builtin_amdgcn_s_memrealtime());
@@ -3916,24 +3921,24 @@ DEV void apply_minv(const Dev& d, const Plan& P, int64_t e0, int64_t estride, bo
 // bump is triangular after permutation: ~1.6 nonzeros per row of its
 // inverse), and so are the update's multipliers x1 (alpha_S / column a of the
 // inverse) and x2 (the pivot row / v): r05 counts 87 / 100 nonzeros of 2000 per
-// dual pivot there, ~900 / ~1000 per primal pivot of the feasible-start LP.  By
-// the zero rule of r1 only the pairs of nonzeros change, plus the border the
-// case rewrites (A: row p; B: row and column k; C: row b and column a, moved
-// from the last ones; D: column a).  Workgroup wg owns rows [wg R, wg R + R)
-// (R <= SRU_ROWS: the host launches cdiv(k + 1, SRU_ROWS) of them): one load
-// per row tells which of them have a nonzero multiplier -- the others exit
-// there -- then the workgroup lists x2's nonzeros in LDS (past SRU_CAP: every
-// column, tested) and updates its rows' pairs, SRU_U loads in flight per
-// thread; the border is strided over the whole launch.  Every entry it writes
-// is written by the dense update too, with the same bits.
-constexpr int SRU_CAP = 1024, SRU_ROWS = 8, SRU_U = 8;
-constexpr unsigned sru_wgs(int k_ub) { return (unsigned)((k_ub + 1 + SRU_ROWS - 1) / SRU_ROWS); }
+// dual pivot there; the feasible-start LP's primal pivots reach ~50 % at bumps
+// of ~3000.  By the zero rule of r1 only the rows with a nonzero multiplier
+// change (and in them the entries with a nonzero x2), plus the border the case
+// rewrites (A: row p; B: row and column k; C: row b and column a, moved from
+// the last ones; D: column a).  One workgroup per row (the host launches one
+// per bump position up to SRU_WG_MAX; more rows: strided): one load tells
+// whether its multiplier is zero -- then it is done -- else the row and x2 go
+// out SRU_U per thread together (the row is read whole, so one round trip per
+// batch) and only the changed entries are stored.  The border is strided over
+// the whole launch.  Every entry written is written by the dense update too,
+// with the same bits.
+constexpr int SRU_U = 8;
+constexpr unsigned SRU_WG_MAX = 4096;
+constexpr unsigned sru_wgs(int k_ub) { return (unsigned)(k_ub + 1) < SRU_WG_MAX ? (unsigned)(k_ub + 1) : SRU_WG_MAX; }
 template <int NT>
 DEV void apply_minv_sru(const Dev& d, const Plan& P, int wg, int nwg) {
-    __shared__ int s_l2[SRU_CAP], s_rows[64], s_scan[NT / 64];
-    __shared__ double s_a1[64];
     if (P.action != ACT_PIVOT || P.pcase == PC_E || nwg <= 0) return;
-    const int k = P.k_old, pc = P.pcase, tid = threadIdx.x, lane = tid & 63;
+    const int k = P.k_old, pc = P.pcase, tid = threadIdx.x;
     const int kk = pc == PC_B ? k + 1 : pc == PC_C ? k - 1 : k;
     if (kk <= 0) return;
     const int nl = pc == PC_B ? k : kk;  // the rank-one part's index range
@@ -3941,69 +3946,34 @@ DEV void apply_minv_sru(const Dev& d, const Plan& P, int wg, int nwg) {
     const double* x2 = (pc == PC_B || pc == PC_D) ? d.vvec : d.vrow;
     const int ex1 = pc == PC_A ? P.p : pc == PC_C ? P.b : -1;  // (the row / column the border rewrites)
     const int ex2 = (pc == PC_C || pc == PC_D) ? P.a : -1;
-    const double va = pc == PC_D ? d.vvec[P.a] : 1.0;
     const size_t ldm = (size_t)d.ldm;
     double* M = d.Minv;
     double* MT = d.noT ? nullptr : d.MinvT;
-    const int R = (nl + nwg - 1) / nwg;
-    const int r0 = min(nl, wg * R), r1e = min(nl, r0 + R);
-    bool listed = false;
-    int n2 = 0;
-    for (int g0 = r0; g0 < r1e; g0 += 64) {  // (one pass: R <= 64)
-        // the multipliers of rows g0 + lane (every wave alike: a uniform mask)
-        const int i = g0 + lane;
-        double a1 = 0.0;
-        if (i < r1e && i != ex1) {
-            a1 = x1[i];
-            if (pc == PC_B) a1 = -a1;
-            else if (pc == PC_D) a1 = a1 / va;
-        }
-        const unsigned long long rm = __ballot(a1 != 0.0);
-        if (rm == 0ull) continue;
-        const int nr = __popcll(rm);
-        if (tid < 64 && a1 != 0.0) {
-            const int o = __popcll(rm & ((1ull << lane) - 1ull));
-            s_rows[o] = i;
-            s_a1[o] = a1;
-        }
-        if (!listed) {  // x2's nonzeros, ascending (an ordered scan: one segment per thread)
-            listed = true;
-            const int seg = (nl + NT - 1) / NT, s0 = min(nl, tid * seg), s1 = min(nl, s0 + seg);
-            int c2 = 0;
-            for (int t = s0; t < s1; ++t) c2 += (t != ex2 && x2[t] != 0.0) ? 1 : 0;
-            int o2;
-            n2 = block_scan_excl<NT>(c2, &o2, s_scan);
-            if (n2 <= SRU_CAP)
-                for (int t = s0; t < s1; ++t)
-                    if (t != ex2 && x2[t] != 0.0) s_l2[o2++] = t;
-        }
-        __syncthreads();  // (s_rows / s_a1 / the list)
-        const bool lst = n2 <= SRU_CAP;
-        const int nc = lst ? n2 : nl;  // (no list: every column, tested)
-        const int64_t ne = (int64_t)nr * nc;
-        for (int64_t e0 = tid; e0 < ne; e0 += (int64_t)NT * SRU_U) {
-            int ii[SRU_U], jj[SRU_U];
-            double aa[SRU_U], bb[SRU_U], ov[SRU_U];
+    const double va = pc == PC_D ? d.vvec[P.a] : 1.0;
+    for (int i = wg; i < nl; i += nwg) {
+        if (i == ex1) continue;
+        double a1 = x1[i];
+        if (pc == PC_B) a1 = -a1;
+        else if (pc == PC_D) a1 = a1 / va;
+        if (a1 == 0.0) continue;
+        double* row = M + (size_t)i * ldm;
+        for (int j0 = tid; j0 < nl; j0 += NT * SRU_U) {
+            double bb[SRU_U], ov[SRU_U];
 #pragma unroll
             for (int u = 0; u < SRU_U; ++u) {
-                const int64_t e = e0 + (int64_t)u * NT;
-                const int64_t ec = e < ne ? e : ne - 1;
-                const int rr = (int)(ec / nc), t = (int)(ec % nc);
-                ii[u] = s_rows[rr];
-                aa[u] = s_a1[rr];
-                jj[u] = lst ? s_l2[t] : t;
-                bb[u] = x2[jj[u]];
-                ov[u] = M[(size_t)ii[u] * ldm + jj[u]];
+                const int j = min(j0 + u * NT, nl - 1);
+                bb[u] = x2[j];
+                ov[u] = row[j];
             }
 #pragma unroll
             for (int u = 0; u < SRU_U; ++u) {
-                if (e0 + (int64_t)u * NT >= ne || jj[u] == ex2 || bb[u] == 0.0) continue;
-                const double v = fma(-aa[u], bb[u], ov[u]);
-                M[(size_t)ii[u] * ldm + jj[u]] = v;
-                if (MT) MT[(size_t)jj[u] * ldm + ii[u]] = v;
+                const int j = j0 + u * NT;
+                if (j >= nl || j == ex2 || bb[u] == 0.0) continue;
+                const double v = fma(-a1, bb[u], ov[u]);
+                row[j] = v;
+                if (MT) MT[(size_t)j * ldm + i] = v;
             }
         }
-        __syncthreads();  // (s_rows is rewritten by a next group)
     }
     // ---- the border, strided over the launch
     auto put = [&](int i, int j, double v) {
@@ -5251,15 +5221,27 @@ __global__ void __launch_bounds__(TILE_COLS) k_dual_price_csc(Dev d, int nsw, in
         }
         return;
     }
-    if (c->status != ST_RUN) return;
+    const int64_t tile = (int64_t)blockIdx.x - nsw;
+    const int64_t j = tile * TILE_COLS + threadIdx.x;
+    // the column's record and the control fields, issued with the status
+    // (straight-line: one round trip, not two)
+    const int64_t jc = j < 0 ? 0 : j < d.n ? j : (d.n > 0 ? d.n - 1 : 0);
+    const int8_t vsj = d.vstat[jc];
+    const int64_t ta = d.cptr[jc], tb = d.cptr[jc + 1];
+    const double cj = d.cost[jc], lbj = d.lb[jc], ubj = d.ub[jc], xj = d.xval[jc];
+    const int xrow = warm ? -1 : c->dr_xrow, rs = c->dr_s, bland = c->bland;
+    const double xsig = c->dr_xsig, dtol = c->tol_dual, pivtol = c->tol_pivot;
+    __builtin_amdgcn_sched_barrier(0);
+    if (c->status != ST_RUN) {
+        KEEP(ta);
+        KEEP(cj);
+        KEEP(xj);
+        return;
+    }
     if ((int)blockIdx.x < nsw) {
         dual_slacks<TILE_COLS>(d, d.ntiles + blockIdx.x, blockIdx.x, nsw, wcnt, warm);
         return;
     }
-    const int64_t tile = (int64_t)blockIdx.x - nsw;
-    const int64_t j = tile * TILE_COLS + threadIdx.x;
-    const int xrow = warm ? -1 : c->dr_xrow, rs = c->dr_s, bland = c->bland;
-    const double xsig = c->dr_xsig, dtol = c->tol_dual, pivtol = c->tol_pivot;
     DualCand o;
     bool f = false;
     if (warm) {
@@ -5271,7 +5253,7 @@ __global__ void __launch_bounds__(TILE_COLS) k_dual_price_csc(Dev d, int nsw, in
         return;
     }
     if (j < d.n) {
-        const int8_t vs = d.vstat[j];
+        const int8_t vs = vsj;
         if (vs != VS_BASIC && vs != VS_FIXED) {
             // batches of DPB entries: each level of the row index -> rpos / y ->
             // rho_R gathers in flight together (one round trip per level, not
@@ -5281,8 +5263,8 @@ __global__ void __launch_bounds__(TILE_COLS) k_dual_price_csc(Dev d, int nsw, in
 #endif
             constexpr int DPB = ELP_DPB;
             double ad = 0.0, aa = 0.0;
-            const int64_t t1 = d.cptr[j + 1];
-            for (int64_t t0 = d.cptr[j]; t0 < t1; t0 += DPB) {
+            const int64_t t1 = tb;
+            for (int64_t t0 = ta; t0 < t1; t0 += DPB) {
                 int ii[DPB], rp[DPB];
                 double vv[DPB], yv[DPB], rh[DPB];
 #pragma unroll
@@ -5306,8 +5288,7 @@ __global__ void __launch_bounds__(TILE_COLS) k_dual_price_csc(Dev d, int nsw, in
                         aa = fma(vv[b], rho, aa);
                     }
             }
-            f = dual_candidate(vs, aa, d.cost[j] - ad, d.lb[j], d.ub[j], rs, bland, dtol, pivtol, (int)j, d.xval[j],
-                               d.cost[j], o);
+            f = dual_candidate(vs, aa, cj - ad, lbj, ubj, rs, bland, dtol, pivtol, (int)j, xj, cj, o);
         }
     }
     emit_region<TILE_COLS>(d, (int)tile, f, o, false, o, wcnt);
@@ -5375,6 +5356,65 @@ __global__ void __launch_bounds__(BF_NT) k_dual_pack(Dev d, int nreg) {
     if (d.ctl->status != ST_RUN) return;
     const int total = compact_regions(d, nreg, d.dsend + 1, scan_lds);
     if (threadIdx.x == 0) d.dsend[0].j = total;
+}
+
+// Up to 64 candidates (the common case: ~42 per dual pivot on the 20 000 x
+// 100 000 KKT LP): one per lane, so a bunch round is a DPP minimum, one ballot
+// and the flip sum as lane 0's fma chain over the members' (|alpha|, u - l)
+// read lane by lane in lane order -- no LDS, no register slots to scan (r05:
+// ~0.8 us per round in bfrt_wave, mostly dependent latency of its four-slot
+// bookkeeping).  The same decisions in the same order.
+DEV void bfrt_wave1(const Dev& d, int N, int bland, double ptol, double slope, int* nflip_out, int* qidx_out,
+                    int* s_flip, int dslot) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const double INF = HUGE_VAL;
+    double rt = 0.0, rb = 0.0, ra = 0.0, rw = 0.0;
+    int rj = 0;
+    bool live = lane < N;
+    if (live) {
+        const DualCand& o = d.dcomp[lane];
+        rt = o.t;
+        rb = o.b;
+        ra = fabs(o.a);
+        rw = o.r;
+        rj = o.j;
+    }
+    int nflip = 0, qidx = -1, rounds = 0;
+    RSTAMP(27);
+    for (;;) {
+        ++rounds;
+        if (!__any(live)) break;  // nothing left: the dual ray (q = -1)
+        const double thmax = wave_min_f64(live ? rb : INF);
+        const bool mem = live && rt <= thmax;
+        const unsigned long long mm = __ballot(mem);
+        if (mm == 0ull) break;  // (NaN ratios only: no candidate qualifies -- the ray)
+        const bool boxed = __all(!mem || rw != INF);
+        double sum = 0.0;
+        if (boxed)  // |alpha| (u - l) in lane order (= the compacted order)
+            for (unsigned long long mk = mm; mk; mk &= mk - 1ull) {
+                const int l = __ffsll((long long)mk) - 1;
+                sum = fma(readlane_f64(ra, l), readlane_f64(rw, l), sum);
+            }
+        if (boxed && sum < slope - ptol) {  // flip the bunch
+            slope = slope - sum;
+            if (mem) s_flip[nflip + __popcll(mm & below)] = lane;
+            nflip += __popcll(mm);
+            live = live && !mem;
+            continue;
+        }
+        // the bunch's best enters: the largest |alpha| (Bland: the smallest
+        // ratio), then the lowest id
+        const double key = mem ? (bland ? -rt : ra) : -INF;
+        const double kmax = wave_max_f64(key);
+        const bool at = mem && key == kmax;
+        const unsigned long long w = __ballot(at);
+        qidx = w ? lowest_index_lane(w, at, rj) : lowest_index_lane(mm, mem, rj);
+        break;
+    }
+    if (ELP_DIAG && d.dstamp && threadIdx.x == 0) d.dstamp[dslot * DSTAMP_STRIDE + 28] = (unsigned long long)rounds;
+    *nflip_out = nflip;
+    *qidx_out = qidx;
 }
 
 // Small candidate sets (N <= 64 * BF_RR, the usual case: ~36 candidates per
@@ -5632,7 +5672,10 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     int nflip = 0, qidx = -1;
     const bool wave = reg_ok >= 2 && N <= 64 * BF_RR;  // (bfrt_wave: the usual case)
     if (wave) {
-        if (tid < 64) bfrt_wave(d, N, bland, ptol, fabs(c->dr_x - c->dr_beta), s_bun, &nflip, &qidx, s_flip, dslot);
+        if (tid < 64) {
+            if (N <= 64) bfrt_wave1(d, N, bland, ptol, fabs(c->dr_x - c->dr_beta), &nflip, &qidx, s_flip, dslot);
+            else bfrt_wave(d, N, bland, ptol, fabs(c->dr_x - c->dr_beta), s_bun, &nflip, &qidx, s_flip, dslot);
+        }
         if (tid == 0) {
             s_int[2] = nflip;
             s_int[3] = qidx;

@@ -501,7 +501,12 @@ static void btran(orc_t* s, int phase) {
  * (covered row lrow or bump position lpos); cases A-E of the header, the
  * bump inverse update, and -- phase 2 -- the dual update y += theta_d rho_r
  * with theta_d = dq / alpha_rq (run_phase and run_dual share it).  Returns
- * -1 on a numerical failure (case E off its row, AR growth). */
+ * -1 on a numerical failure (case E off its row, AR growth).
+ * The zero rule (r05): a rank-one term whose multiplier (the row's factor or
+ * the pivot-row entry) is zero leaves the entry as it is -- fma(-w, v, m)
+ * would return m then too, except m = -0 with a +0 product (+0) -- so the
+ * HIP update can skip the rows and entries it does not change
+ * (apply_minv_sru) and still match these bits. */
 static int basis_change(orc_t* s, int phase, int64_t q, int64_t lv, int64_t lrow, int64_t lpos, double dq,
                         double xq) {
     const int64_t m = s->m, n = s->n, k = s->k;
@@ -518,7 +523,9 @@ static int basis_change(orc_t* s, int phase, int64_t q, int64_t lv, int64_t lrow
             for (int64_t i = 0; i < k; ++i) {
                 if (i == p) continue;
                 const double wi = s->alS[i];
-                for (int64_t j = 0; j < k; ++j) *MI(s, i, j) = fma(-wi, s->v[j], *MI(s, i, j));
+                if (wi == 0.0) continue; /* (the zero rule) */
+                for (int64_t j = 0; j < k; ++j)
+                    if (s->v[j] != 0.0) *MI(s, i, j) = fma(-wi, s->v[j], *MI(s, i, j));
             }
             for (int64_t j = 0; j < k; ++j) *MI(s, p, j) = s->v[j];
             s->spos[lv] = -1;
@@ -537,7 +544,9 @@ static int basis_change(orc_t* s, int phase, int64_t q, int64_t lv, int64_t lrow
             }
             for (int64_t a = 0; a < k; ++a) {
                 const double wa = s->alS[a];
-                for (int64_t c = 0; c < k; ++c) *MI(s, a, c) = fma(wa, s->v[c], *MI(s, a, c));
+                if (wa == 0.0) continue;
+                for (int64_t c = 0; c < k; ++c)
+                    if (s->v[c] != 0.0) *MI(s, a, c) = fma(wa, s->v[c], *MI(s, a, c));
             }
             for (int64_t a = 0; a < k; ++a) *MI(s, a, k) = -(s->alS[a] / delta);
             for (int64_t c = 0; c < k; ++c) *MI(s, k, c) = -s->v[c];
@@ -572,8 +581,9 @@ static int basis_change(orc_t* s, int phase, int64_t q, int64_t lv, int64_t lrow
             for (int64_t r = 0; r < k; ++r) {
                 if (r == b) continue;
                 const double f = *MI(s, r, a);
+                if (f == 0.0) continue;
                 for (int64_t c = 0; c < k; ++c)
-                    if (c != a) *MI(s, r, c) = fma(-f, s->v[c], *MI(s, r, c));
+                    if (c != a && s->v[c] != 0.0) *MI(s, r, c) = fma(-f, s->v[c], *MI(s, r, c));
             }
             if (b != last) {
                 for (int64_t c = 0; c < k; ++c) *MI(s, b, c) = *MI(s, last, c);
@@ -606,8 +616,9 @@ static int basis_change(orc_t* s, int phase, int64_t q, int64_t lv, int64_t lrow
             for (int64_t r = 0; r < k; ++r) s->t[r] = *MI(s, r, a) / piv;
             for (int64_t r = 0; r < k; ++r) {
                 const double f = s->t[r];
-                for (int64_t c = 0; c < k; ++c)
-                    if (c != a) *MI(s, r, c) = fma(-f, s->v[c], *MI(s, r, c));
+                if (f != 0.0)
+                    for (int64_t c = 0; c < k; ++c)
+                        if (c != a && s->v[c] != 0.0) *MI(s, r, c) = fma(-f, s->v[c], *MI(s, r, c));
                 *MI(s, r, a) = f;
             }
             s->Rl[a] = i1;
