@@ -1446,14 +1446,14 @@ DEV void price_csc_body(const Dev& d, int napply, int nb_minv, int nsw) {
     PDBG(1, __builtin_amdgcn_s_memrealtime());
     const int bland = c->bland;
     const bool staged = s1 - s0 <= CSC_STAGE;
-    if (staged) {  // (<= CSC_STAGE / TILE_COLS entries per thread: every gather in flight at once)
+    if (staged && s1 > s0) {  // (<= CSC_STAGE / TILE_COLS entries per thread: every gather in flight at once)
         constexpr int SPT = CSC_STAGE / TILE_COLS;
         int ii[SPT];
         double vv[SPT], yv[SPT];
 #pragma unroll
         for (int u = 0; u < SPT; ++u) {
             const int64_t t = s0 + threadIdx.x + (int64_t)u * TILE_COLS;
-            const int64_t tc = t < s1 ? t : (s1 > s0 ? s1 - 1 : s0);
+            const int64_t tc = t < s1 ? t : s1 - 1;  // (s1 > s0: an entry of the tile)
             ii[u] = d.rind[tc];
             vv[u] = d.cval[tc];
         }
