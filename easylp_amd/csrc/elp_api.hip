@@ -1995,7 +1995,11 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
                     if (r[i] && r[16]) h->stamp_sum[i] += 10.0 * (double)(long long)(r[i] - r[16]);
                 for (int i = 21; i < 24; ++i)  // the dual BFRT, relative to its start
                     if (r[i] && r[20]) h->stamp_sum[i] += 10.0 * (double)(long long)(r[i] - r[20]);
-                if (r[27] && r[20]) h->stamp_sum[27] += 10.0 * (double)(long long)(r[27] - r[20]);
+                for (int i : {27, 29, 30, 31, 32, 33})  // (conditional: counted where present, in stamp_sum[34 + ...])
+                    if (r[i] && r[20] && r[i] >= r[20] && r[i] - r[20] < 100000ull) {
+                        h->stamp_sum[i] += 10.0 * (double)(long long)(r[i] - r[20]);
+                        h->stamp_sum[i == 27 ? 34 : i == 29 ? 35 : 36] += i < 30 || i == 30 ? 1.0 : 0.0;
+                    }
                 for (int i : {24, 25, 26, 28}) h->stamp_sum[i] += (double)r[i];  // (counts)
                 h->stamp_n++;
             }
@@ -2836,7 +2840,14 @@ extern "C" void elp_destroy(elp_handle* h) {
         std::fprintf(stderr, "k_dual_bfrt counts (per iteration): candidates=%.1f flips=%.2f one_wave=%.3f rounds=%.2f "
                      "(wave: loaded=%.2f us)\n",
                      h->stamp_sum[24] / h->stamp_n, h->stamp_sum[25] / h->stamp_n, h->stamp_sum[26] / h->stamp_n,
-                     h->stamp_sum[28] / h->stamp_n, h->stamp_sum[27] / h->stamp_n / 1e3);
+                     h->stamp_sum[28] / h->stamp_n, h->stamp_sum[27] / std::max(1.0, h->stamp_sum[34]) / 1e3);
+        const double nt = std::max(1.0, h->stamp_sum[36]);
+        std::fprintf(stderr, "k_dual_bfrt fast tail (us after its start; rounds over %.0f launches, the a_F phases over "
+                     "the %.0f with flips): rounds done %.2f, a_F offsets %.2f, chains %.2f, support scan %.2f, "
+                     "a_F[R] list %.2f\n",
+                     h->stamp_sum[35], h->stamp_sum[36], h->stamp_sum[29] / std::max(1.0, h->stamp_sum[35]) / 1e3,
+                     h->stamp_sum[30] / nt / 1e3, h->stamp_sum[31] / nt / 1e3, h->stamp_sum[32] / nt / 1e3,
+                     h->stamp_sum[33] / nt / 1e3);
     }
     if (!h) return;
     destroy_group(h);

@@ -46,9 +46,9 @@ enum : int32_t { ACT_NONE = 0, ACT_FLIP = 1, ACT_PIVOT = 2 };
 // slot chunks per pricing tile (one per wave); the oracle's PRICE_SPLIT must match
 constexpr int PRICE_SPLIT = ELP_PRICE_SPLIT;
 constexpr int ZCHUNK = 32;      // bump positions per FTRAN-z partial
-constexpr int DSTAMP_STRIDE = 32;  // ELP_STAMPS slots per chunk iteration (k_ratio 0-11, select 12-15, FTRAN-z 16-19, dual BFRT 20-23;
+constexpr int DSTAMP_STRIDE = 40;  // ELP_STAMPS slots per chunk iteration (k_ratio 0-11, select 12-15, FTRAN-z 16-19, dual BFRT 20-23;
                                     // 24-26, 28: the dual BFRT's counts -- candidates, flips, one-wave path,
-                                    // bunch rounds; 27: bfrt_wave's candidates loaded)
+                                    // bunch rounds; 27: its records loaded, 29: rounds done, 30-33: the LDS a_F phases)
 constexpr int RREG = 64;  // pass-2 candidate slots per k_ftran_zr wave region
 constexpr int TILE_COLS = 128;  // columns per pricing workgroup (2 per lane)
 

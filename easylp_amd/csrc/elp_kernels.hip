@@ -1595,6 +1595,9 @@ DEV void price_timer_sum(const Dev& d, unsigned long long* red) {
 // debug stamps (Dev::dstamp, ELP_STAMPS): s_memrealtime at the phases of workgroup 0
 #define RSTAMP(i) do { if (ELP_DIAG && d.dstamp && blockIdx.x == 0 && threadIdx.x == 0) \
     d.dstamp[dslot * DSTAMP_STRIDE + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+// k_dual_bfrt's stamps go to LDS (s_st) and out at the end of the launch: a
+// global store mid-launch would make the next barrier wait for its ack
+#define BSTAMP(i) do { if (ELP_DIAG && s_st && threadIdx.x == 0) s_st[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
 constexpr int MAX_P2P = 64;  // ranks a mailbox exchange supports
 
 // xGMI mailbox min-loc (Dev::p2p, column-sharded with A replicated): workgroup
@@ -5321,7 +5324,10 @@ static int bfrt_reg() {
 // scanned offsets in LDS), so the copies are independent loads in flight
 // instead of one thread walking a region's records one after another (a
 // region holds up to DREG)
-DEV int compact_regions(const Dev& d, int nreg, DualCand* dst, int* scan_lds) {
+// s_rec (k_dual_bfrt's fast tail; one chunk of regions): when the regions hold
+// <= 64 candidates they go to s_rec in LDS instead of dst -- no global stores
+// for the barrier after the compaction to wait on, no reload
+DEV int compact_regions(const Dev& d, int nreg, DualCand* dst, int* scan_lds, DualCand* s_rec = nullptr) {
     __shared__ int s_off[BF_NT];
     const int tid = threadIdx.x;
     int total = 0;
@@ -5341,7 +5347,9 @@ DEV int compact_regions(const Dev& d, int nreg, DualCand* dst, int* scan_lds) {
                 if (s_off[mid] <= o) lo = mid;
                 else hi = mid - 1;
             }
-            dst[total + o] = d.dcand[(size_t)(r0 + lo) * DREG + (o - s_off[lo])];
+            const DualCand* src = d.dcand + (size_t)(r0 + lo) * DREG + (o - s_off[lo]);
+            if (s_rec && tot <= 64) s_rec[o] = *src;  // (uniform: one chunk, nreg <= BF_NT)
+            else dst[total + o] = *src;
         }
         total += tot;
         __syncthreads();  // (s_off is rewritten by the next chunk)
@@ -5364,24 +5372,27 @@ __global__ void __launch_bounds__(BF_NT) k_dual_pack(Dev d, int nreg) {
 // read lane by lane in lane order -- no LDS, no register slots to scan (r05:
 // ~0.8 us per round in bfrt_wave, mostly dependent latency of its four-slot
 // bookkeeping).  The same decisions in the same order.
+// out (k_dual_bfrt's fast tail, one GPU CSC): the records are in s_rec (LDS);
+// the flips' ids / dx go to ofj / ofdx from the lanes that hold them
 DEV void bfrt_wave1(const Dev& d, int N, int bland, double ptol, double slope, int* nflip_out, int* qidx_out,
-                    int* s_flip, int dslot) {
+                    int* s_flip, unsigned long long* s_st, bool out = false, DualCand* s_rec = nullptr,
+                    int* ofj = nullptr, double* ofdx = nullptr) {
     const int lane = threadIdx.x & 63;
     const unsigned long long below = (1ull << lane) - 1ull;
     const double INF = HUGE_VAL;
     double rt = 0.0, rb = 0.0, ra = 0.0, rw = 0.0;
     int rj = 0;
     bool live = lane < N;
-    if (live) {
-        const DualCand& o = d.dcomp[lane];
-        rt = o.t;
-        rb = o.b;
-        ra = fabs(o.a);
-        rw = o.r;
-        rj = o.j;
+    if (live) {  // (out: the compaction left the records in s_rec)
+        const DualCand* o = out ? s_rec + lane : d.dcomp + lane;
+        rt = o->t;
+        rb = o->b;
+        ra = fabs(o->a);
+        rw = o->r;
+        rj = o->j;
     }
     int nflip = 0, qidx = -1, rounds = 0;
-    RSTAMP(27);
+    BSTAMP(7);
     for (;;) {
         ++rounds;
         if (!__any(live)) break;  // nothing left: the dual ray (q = -1)
@@ -5398,7 +5409,15 @@ DEV void bfrt_wave1(const Dev& d, int N, int bland, double ptol, double slope, i
             }
         if (boxed && sum < slope - ptol) {  // flip the bunch
             slope = slope - sum;
-            if (mem) s_flip[nflip + __popcll(mm & below)] = lane;
+            if (mem) {
+                const int pos = nflip + __popcll(mm & below);
+                s_flip[pos] = lane;
+                if (out) {  // dx = +-(u - l) (LDS only: k_dual_bfrt stores the flips after its last barrier)
+                    const DualCand& o = s_rec[lane];
+                    ofj[pos] = o.j;
+                    ofdx[pos] = o.side > 0 ? o.ub - o.lb : o.lb - o.ub;
+                }
+            }
             nflip += __popcll(mm);
             live = live && !mem;
             continue;
@@ -5412,7 +5431,8 @@ DEV void bfrt_wave1(const Dev& d, int N, int bland, double ptol, double slope, i
         qidx = w ? lowest_index_lane(w, at, rj) : lowest_index_lane(mm, mem, rj);
         break;
     }
-    if (ELP_DIAG && d.dstamp && threadIdx.x == 0) d.dstamp[dslot * DSTAMP_STRIDE + 28] = (unsigned long long)rounds;
+    BSTAMP(9);
+    if (ELP_DIAG && threadIdx.x == 0) s_st[15] = (unsigned long long)rounds;
     *nflip_out = nflip;
     *qidx_out = qidx;
 }
@@ -5629,6 +5649,84 @@ DEV void bfrt_flip_column(const Dev& d, int nflip, int k, int myj, double mydx) 
     }
 }
 
+// The fast tail's a_F (one GPU, CSC, <= 64 candidates): the candidates'
+// columns -- up to BF_ENT entries each, with the rows' bump positions -- were
+// loaded into LDS by waves 1-8 while wave 0 ran the bunch rounds, and a_F's
+// old support was cleared then too (k_dual_bfrt), so after the decision the
+// chains, the support list and the a_F[R] list come from LDS: bfrt_flip_column's
+// arithmetic without its four dependent global round trips.  Returns false
+// (uniform) when a flipped column is longer than BF_ENT or the flips hold more
+// than AF_PAR entries: the caller then runs bfrt_flip_column.
+constexpr int BF_ENT = 8;
+DEV bool bfrt_flip_lds(const Dev& d, int nflip, int k, const int* s_flip, const int* s_clen, const int* s_erow,
+                       const double* s_eval, const int* s_erp, const double* s_fdx, unsigned long long* s_st) {
+    __shared__ int s_off[64], s_row[AF_PAR], s_lpos[SPL], s_lkey[SPL], s_lsb[72], s_scan[BF_NT / 64];
+    __shared__ double s_v[AF_PAR], s_dx[AF_PAR], s_lval[SPL];
+    __shared__ int s_bad;
+    const int tid = threadIdx.x;
+    int len = 0;
+    if (tid == 0) s_bad = 0;
+    if (tid < nflip) len = s_clen[s_flip[tid]];
+    int excl;
+    const int E = block_scan_excl<BF_NT>(len > 0 ? len : 0, &excl, s_scan);
+    if (len < 0) s_bad = 1;  // (a slack or an overlong column)
+    if (tid < nflip) s_off[tid] = excl;
+    __syncthreads();
+    BSTAMP(10);
+    if (s_bad || E > AF_PAR) return false;
+    int row = -1, rp = -1;
+    if (tid < E) {
+        int lo = 0, hi = nflip - 1;  // the last flip whose offset is <= tid
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_off[mid] <= tid) lo = mid;
+            else hi = mid - 1;
+        }
+        const int sl = s_flip[lo] * BF_ENT + (tid - s_off[lo]);
+        row = s_erow[sl];
+        rp = s_erp[sl];
+        s_row[tid] = row;
+        s_v[tid] = s_eval[sl];
+        s_dx[tid] = s_fdx[lo];
+    }
+    __syncthreads();
+    bool lead = false;
+    double acc = 0.0;
+    if (tid < E) {
+        lead = true;
+        for (int e = 0; e < tid; ++e)
+            if (s_row[e] == row) {
+                lead = false;
+                break;
+            }
+        if (lead)
+            for (int e = tid; e < E; ++e)
+                if (s_row[e] == row) acc = fma(s_v[e], s_dx[e], acc);
+    }
+    // (every global store after the last barrier: a barrier waits for the
+    //  workgroup's outstanding stores)
+    BSTAMP(11);
+    int lex;
+    const int nl = block_scan_excl<BF_NT>(lead ? 1 : 0, &lex, s_scan);
+    BSTAMP(12);
+    const int n = spl_build<BF_NT>(lead && rp >= 0 && rp < k, rp, acc, s_lpos, s_lval, s_lsb, s_lkey, s_scan);
+    BSTAMP(13);
+    if (lead) {
+        d.aF[row] = acc;
+        d.afs[1 + lex] = row;
+    }
+    for (int t = tid; t < n; t += BF_NT) {
+        d.afl[AFL_POS + t] = s_lpos[t];
+        d.aflv[t] = s_lval[t];
+    }
+    if (tid <= 64) d.afl[AFL_SB + tid] = s_lsb[tid];
+    if (tid == 0) {
+        d.afs[0] = nl;
+        d.afl[0] = n;
+    }
+    return true;
+}
+
 // gathered: P = world ranks' packed records in drecv (rank order) instead of
 // this launch's regions
 // (workgroups 1 .. gridDim.x - 1: the deferred plan's Minv update, dual_defer)
@@ -5639,6 +5737,14 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     __shared__ int s_int[4];
     __shared__ double s_dbl[2];
     __shared__ int s_flip[64 * BF_RR];  // (the one-wave path's flip list: compact indices)
+    // the fast tail (one GPU, CSC, <= 64 candidates): the candidates' ids and
+    // columns (BF_ENT entries each, with the rows' bump positions), the flips'
+    // ids / dx and the entering record, all in LDS
+    __shared__ int s_clen[64], s_erow[64 * BF_ENT], s_erp[64 * BF_ENT], s_fj[64];
+    __shared__ double s_eval[64 * BF_ENT], s_fdx[64];
+    __shared__ DualCand s_rec[64];
+    __shared__ unsigned long long s_stb[16];
+    unsigned long long* s_st = (ELP_DIAG && d.dstamp) ? s_stb : nullptr;
     DevCtl* c = d.ctl;
     if (blockIdx.x > 0) {
         if (minv_pending(c)) {
@@ -5648,15 +5754,20 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
         }
         return;
     }
-    RSTAMP(20);
+    BSTAMP(0);
+    // (the counters the tail updates, read now: nothing else writes them during the launch)
+    const int64_t pf_flips = c->flips, pf_pp = c->price_passes;
+    const double pf_pb = c->price_bytes, pf_ib = c->iter_bytes;
+    const int pf_k = c->k, pf_ny = c->ny;
     if (c->status != ST_RUN) return;
     const int tid = threadIdx.x;
     const int bland = c->bland;
     // ---- compaction (one GPU: the regions; sharded: the ranks' records, in
     //      rank order = ascending structural id, the last rank's slacks last)
     int total = 0;
+    const bool lds_rec = !gathered && d.csc && nreg <= BF_NT && reg_ok >= 2;
     if (!gathered) {
-        total = compact_regions(d, nreg, d.dcomp, scan_lds);
+        total = compact_regions(d, nreg, d.dcomp, scan_lds, lds_rec ? s_rec : nullptr);
     } else {
         for (int r = 0; r < d.world; ++r) {
             const DualCand* src = d.drecv + (size_t)r * ((size_t)d.dcap + 1);
@@ -5666,15 +5777,47 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
         }
     }
     __syncthreads();  // (the compacted array is read by other threads below)
-    RSTAMP(21);
+    BSTAMP(1);
     const int N = total;
     const double ptol = c->tol_primal;
     int nflip = 0, qidx = -1;
     const bool wave = reg_ok >= 2 && N <= 64 * BF_RR;  // (bfrt_wave: the usual case)
+    // fast: wave 0 runs the rounds and leaves the flips / the entering record
+    // in LDS while waves 1-8 load the candidates' columns and waves 9-15
+    // clear the last a_F's support (every thread here is otherwise idle)
+    const bool fast = lds_rec && N <= 64;  // (then the records are in s_rec only)
     if (wave) {
         if (tid < 64) {
-            if (N <= 64) bfrt_wave1(d, N, bland, ptol, fabs(c->dr_x - c->dr_beta), &nflip, &qidx, s_flip, dslot);
+            if (N <= 64)
+                bfrt_wave1(d, N, bland, ptol, fabs(c->dr_x - c->dr_beta), &nflip, &qidx, s_flip, s_st, fast, s_rec,
+                           s_fj, s_fdx);
             else bfrt_wave(d, N, bland, ptol, fabs(c->dr_x - c->dr_beta), s_bun, &nflip, &qidx, s_flip, dslot);
+        } else if (fast && tid < 64 + 64 * BF_ENT) {
+            const int sl = tid - 64, cc = sl / BF_ENT, e = sl % BF_ENT;
+            if (cc < N) {
+                const int j = s_rec[cc].j;
+                const int jl = j < d.N ? loc_of(d, j) : -1;
+                int len = -1;  // (a slack: no column to scatter; it never flips -- no finite range)
+                if (jl >= 0) {
+                    const int64_t c0 = d.cptr[jl];
+                    len = (int)(d.cptr[jl + 1] - c0);
+                    if (e < len && len <= BF_ENT) {
+                        const int row = d.rind[c0 + e];
+                        s_eval[sl] = d.cval[c0 + e];
+                        s_erow[sl] = row;
+                        s_erp[sl] = d.rpos[row];
+                    }
+                }
+                if (e == 0) s_clen[cc] = len <= BF_ENT ? len : -1;
+            }
+        } else if (fast) {  // the last a_F's support back to zero (or all of a_F)
+            const int t0 = tid - (64 + 64 * BF_ENT), T = BF_NT - (64 + 64 * BF_ENT);
+            const int pn = d.afs[0];
+            if (pn < 0) {
+                for (int i = t0; i < d.m; i += T) d.aF[i] = 0.0;
+            } else {
+                for (int t = t0; t < pn; t += T) d.aF[d.afs[1 + t]] = 0.0;
+            }
         }
         if (tid == 0) {
             s_int[2] = nflip;
@@ -5864,17 +6007,16 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
         break;
     }
     __syncthreads();
-    RSTAMP(22);
-    if (ELP_DIAG && d.dstamp && tid == 0) {
-        d.dstamp[dslot * DSTAMP_STRIDE + 24] = (unsigned long long)N;
-        d.dstamp[dslot * DSTAMP_STRIDE + 25] = (unsigned long long)nflip;
-        d.dstamp[dslot * DSTAMP_STRIDE + 26] = wave ? 1ull : 0ull;
-    }
+    BSTAMP(2);
     // the flips: compact indices -> ids and dx = +-(u - l) (the record's range)
     // (the new status and value from the record's bounds: the column's own)
     int myj = -1;
     double mydx = 0.0;
-    for (int t = tid; t < nflip; t += BF_NT) {
+    if (fast && tid < nflip) {  // (wave 0 stored them already)
+        myj = s_fj[tid];
+        mydx = s_fdx[tid];
+    }
+    for (int t = fast ? BF_NT : tid; t < nflip; t += BF_NT) {
         const DualCand o = d.dcomp[wave ? s_flip[t] : d.dflip[t]];
         const bool at_lower = o.side > 0;  // (boxed columns act at their current bound)
         const double dx = at_lower ? o.ub - o.lb : o.lb - o.ub;
@@ -5893,10 +6035,46 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     // CSC (one GPU): a_F = sum of the flipped columns times their dx here, in
     // place of a one-workgroup k_dual_flip_col launch -- each row's entries in
     // flip order, the same fma chain
-    if (d.csc && !gathered && qidx >= 0 && nflip > 0) bfrt_flip_column(d, nflip, c->k, myj, mydx);
-    else __syncthreads();  // (the flip list is read by the other threads below / in later launches)
+    if (d.csc && !gathered && qidx >= 0 && nflip > 0) {
+        const int kq = pf_k;
+        if (!(fast && bfrt_flip_lds(d, nflip, kq, s_flip, s_clen, s_erow, s_eval, s_erp, s_fdx, s_st))) {
+            if (fast && tid < nflip) {  // (the sequential path reads the flip list from memory; its first barrier orders these)
+                d.dflip[tid] = s_fj[tid];
+                d.dflipdx[tid] = s_fdx[tid];
+            }
+            bfrt_flip_column(d, nflip, kq, myj, mydx);
+        }
+    } else {
+        __syncthreads();  // (the flip list is read by the other threads below / in later launches)
+    }
+    if (fast && tid < nflip) {  // the flips' list, status and value (after the last barrier)
+        const DualCand& o = s_rec[s_flip[tid]];
+        const double dx = s_fdx[tid];
+        d.dflip[tid] = o.j;
+        d.dflipdx[tid] = dx;
+        const int jl = loc_of(d, o.j);
+        if (jl >= 0) {
+            d.vstat[jl] = dx > 0.0 ? VS_UPPER : VS_LOWER;
+            d.xval[jl] = dx > 0.0 ? o.ub : o.lb;
+        }
+    }
     if (tid != 0) return;
-    RSTAMP(23);
+    BSTAMP(3);
+    if (ELP_DIAG && d.dstamp) {  // the LDS stamps out: 20-23 start / compacted / decided / tail end,
+                                 // 27 records loaded, 29 rounds done, 30-33 the LDS a_F phases; counts 24-26, 28
+        unsigned long long* o = d.dstamp + (size_t)dslot * DSTAMP_STRIDE;
+        o[20] = s_st[0];
+        o[21] = s_st[1];
+        o[22] = s_st[2];
+        o[23] = s_st[3];
+        o[27] = s_st[7];
+        o[29] = s_st[9];
+        for (int t = 0; t < 4; ++t) o[30 + t] = fast && nflip > 0 && qidx >= 0 ? s_st[10 + t] : 0ull;
+        o[24] = (unsigned long long)N;
+        o[25] = (unsigned long long)nflip;
+        o[26] = wave ? 1ull : 0ull;
+        o[28] = N <= 64 ? s_st[15] : 0ull;
+    }
     const int64_t it = c->iter;
     if (qidx < 0) {  // dual unbounded: the LP is infeasible (oracle: trace -2, the leaving variable)
         c->iter = it + 1;
@@ -5910,7 +6088,8 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
         c->status = ST_DUALINF;
         return;
     }
-    const DualCand q = d.dcomp[qidx];
+    const DualCand* qp = fast ? s_rec + qidx : d.dcomp + qidx;
+    const DualCand q = *qp;
     if (d.sharded) {  // the entering column's scalars, wherever it lives (k_ftran_zr's snapshot)
         d.pkt[d.m] = q.lb;
         d.pkt[d.m + 1] = q.ub;
@@ -5923,7 +6102,7 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     c->sig = q.side > 0 ? 1.0 : -1.0;
     c->dq_t = q.t;
     c->nflip = nflip;
-    c->flips += nflip;
+    c->flips = pf_flips + nflip;
     Cand e;
     e.score = 1.0;
     e.d = q.d;
@@ -5931,11 +6110,11 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     e.j = q.j;
     d.cand[0] = e;
     // (statistics: the pricing pass and the whole iteration's bytes)
-    const double kk = (double)c->k, mm = (double)d.m;
-    const double pb = price_pass_bytes(d, c->ny, 0) + 8.0 * (double)c->ny;  // (+ rho on the slots)
-    c->price_bytes += pb;
-    c->price_passes++;
-    c->iter_bytes += pb + 48.0 * kk * kk + 8.0 * mm * kk * (nflip > 0 ? 2.0 : 1.0) + 16.0 * (double)d.n + 16.0 * mm;
+    const double kk = (double)pf_k, mm = (double)d.m;
+    const double pb = price_pass_bytes(d, pf_ny, 0) + 8.0 * (double)pf_ny;  // (+ rho on the slots)
+    c->price_bytes = pf_pb + pb;
+    c->price_passes = pf_pp + 1;
+    c->iter_bytes = pf_ib + pb + 48.0 * kk * kk + 8.0 * mm * kk * (nflip > 0 ? 2.0 : 1.0) + 16.0 * (double)d.n + 16.0 * mm;
 }
 
 // a_F = sum over the flips (in list order) of a_j dx_j, dense A: one row per
