@@ -5727,6 +5727,75 @@ DEV bool bfrt_flip_lds(const Dev& d, int nflip, int k, const int* s_flip, const 
     return true;
 }
 
+// The fast tail's a_F when the flips hold <= 64 entries (the usual case: ~23):
+// wave 0 alone, no barrier -- entry t in lane t (its flip by the offsets'
+// scan in registers), the first lane of each row runs that row's chain over
+// the later lanes in flip order (readlane: the same terms in the same order as
+// bfrt_flip_column), the support list by ballot, and the a_F[R] list ranked by
+// (position mod 64, position) and bucketed as spl_build's, straight to memory.
+// r05t stamps: the block-level version spent ~6 us in its O(E) LDS loops.
+DEV void bfrt_flip_wave(const Dev& d, int nflip, int E, int k, const int* s_flip, const int* s_clen,
+                        const int* s_erow, const double* s_eval, const int* s_erp, const double* s_fdx) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const int len = lane < nflip ? s_clen[s_flip[lane]] : 0;
+    int incl = len;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int u = __shfl_up(incl, off);
+        if (lane >= off) incl += u;
+    }
+    const int excl = incl - len;
+    int f = 0;  // this entry's flip: the last one whose offset is <= lane
+    for (int g = 1; g < nflip; ++g)
+        if (__builtin_amdgcn_readlane(excl, g) <= lane) f = g;
+    const bool has = lane < E;
+    int row = -1, rp = -1;
+    double v = 0.0, dx = 0.0;
+    if (has) {
+        const int sl = s_flip[f] * BF_ENT + (lane - __shfl(excl, f));
+        row = s_erow[sl];
+        rp = s_erp[sl];
+        v = s_eval[sl];
+        dx = s_fdx[f];
+    }
+    bool lead = has;
+    double acc = 0.0;
+    for (int e = 0; e < E; ++e) {
+        const int re = __builtin_amdgcn_readlane(row, e);
+        const double ve = readlane_f64(v, e), de = readlane_f64(dx, e);
+        if (re == row) {
+            if (e < lane) lead = false;
+            else acc = fma(ve, de, acc);
+        }
+    }
+    const unsigned long long lm = __ballot(lead);
+    const bool val = lead && rp >= 0 && rp < k;
+    const unsigned long long vm = __ballot(val);
+    const int key = ((rp & 63) << 25) | (rp & 0x1ffffff);
+    int r = 0, b = 0;  // rank among the listed entries; bucket start of bucket `lane`
+    for (unsigned long long mk = vm; mk; mk &= mk - 1ull) {
+        const int kl = __builtin_amdgcn_readlane(key, __ffsll((long long)mk) - 1);
+        r += kl < key ? 1 : 0;
+        b += (kl >> 25) < lane ? 1 : 0;
+    }
+    const int n = __popcll(vm);
+    if (lead) {
+        d.aF[row] = acc;
+        d.afs[1 + __popcll(lm & below)] = row;
+    }
+    if (val) {
+        d.afl[AFL_POS + r] = rp;
+        d.aflv[r] = acc;
+    }
+    d.afl[AFL_SB + lane] = b;
+    if (lane == 0) {
+        d.afl[AFL_SB + 64] = n;
+        d.afs[0] = __popcll(lm);
+        d.afl[0] = n;
+    }
+}
+
 // gathered: P = world ranks' packed records in drecv (rank order) instead of
 // this launch's regions
 // (workgroups 1 .. gridDim.x - 1: the deferred plan's Minv update, dual_defer)
@@ -6037,7 +6106,19 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     // flip order, the same fma chain
     if (d.csc && !gathered && qidx >= 0 && nflip > 0) {
         const int kq = pf_k;
-        if (!(fast && bfrt_flip_lds(d, nflip, kq, s_flip, s_clen, s_erow, s_eval, s_erp, s_fdx, s_st))) {
+        int E = 0;  // (the flips' entries, every thread alike: the wave path or a block path, uniformly)
+        bool bad = false;
+        if (fast)
+            for (int f = 0; f < nflip; ++f) {
+                const int l = s_clen[s_flip[f]];
+                bad = bad || l < 0;
+                E += l > 0 ? l : 0;
+            }
+        if (fast && !bad && E <= 64) {  // wave 0 alone; the other waves are done
+            if (tid >= 64) return;
+            bfrt_flip_wave(d, nflip, E, kq, s_flip, s_clen, s_erow, s_eval, s_erp, s_fdx);
+            BSTAMP(13);
+        } else if (!(fast && bfrt_flip_lds(d, nflip, kq, s_flip, s_clen, s_erow, s_eval, s_erp, s_fdx, s_st))) {
             if (fast && tid < nflip) {  // (the sequential path reads the flip list from memory; its first barrier orders these)
                 d.dflip[tid] = s_fj[tid];
                 d.dflipdx[tid] = s_fdx[tid];
