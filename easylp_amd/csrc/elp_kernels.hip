@@ -4235,21 +4235,63 @@ __global__ void k_gj_init(Dev d, int k) {
     if (e < k) d.pivstep[e] = 0x7fffffff;
 }
 
-// one Gauss-Jordan column step, two launches: k_gj_pivot (one workgroup) picks
-// the pivot row of column `col` -- largest |W[r][col]| among the rows not used
-// yet, the lowest row on ties (a total order) -- into perm[col]; k_gj_elim then
-// eliminates with it, GJ_PT consecutive elements per thread.  (r03 and before:
-// every elimination workgroup searched the pivot column again itself -- k
-// strided loads per workgroup, ~360 us per step at k = 2000.)
+// one Gauss-Jordan column step, two launches, in place on W (r05; r04: W -> W2
+// every step).  The oracle's step with its zero rule (gauss_jordan): pivot p =
+// the unused row with the largest |W[r][c]| (lowest row on ties); row p becomes
+// q_j = W[p][j] / piv (1 / piv at c); column c becomes -(f_r / piv) with f_r =
+// W[r][c]; every other entry W[r][j] -= f_r q_j -- left alone when f_r or q_j
+// is zero.  k_gj_pivot (one workgroup) finds p, writes row p and column c in
+// place and leaves f (all rows) and q (row p) in side buffers, with lists of
+// the rows with f != 0 and the columns with q != 0; k_gj_elim updates those
+// pairs only (a sparse bump's GJ touches a handful of rows per step), or sweeps
+// every entry, tested, when the pairs are more than an eighth of k^2.
+// Side buffers in W1: q [0, k), f [k, 2k), the rows' f [2k, 3k), rows (int)
+// [3k, 4k), columns (int) [4k, 5k), the two counts at 5k.
 constexpr int GJ_PT = 4;
-__global__ void __launch_bounds__(1024) k_gj_pivot(Dev d, int k, int col, const double* __restrict__ W) {
+struct GjSide {
+    double *q, *f, *fv;
+    int *rows, *cols, *cnt;
+};
+DEV GjSide gj_side(double* W1, int k) {
+    GjSide g;
+    g.q = W1;
+    g.f = W1 + k;
+    g.fv = W1 + 2 * (size_t)k;
+    g.rows = reinterpret_cast<int*>(W1 + 3 * (size_t)k);
+    g.cols = reinterpret_cast<int*>(W1 + 4 * (size_t)k);
+    g.cnt = reinterpret_cast<int*>(W1 + 5 * (size_t)k);
+    return g;
+}
+__global__ void __launch_bounds__(1024) k_gj_pivot(Dev d, int k, int col, double* __restrict__ W) {
     __shared__ double sv[16];
-    __shared__ int sr[16];
+    __shared__ int sr[16], s_nr, s_nc;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const GjSide g = gj_side(d.W1, k);
     double bv = -1.0;
     int br = 0x7fffffff;
-    for (int r = tid; r < k; r += 1024) {
-        if (d.pivstep[r] < col) continue;  // used in an earlier step
+    // column c's entries of this thread's rows (up to GJ_RPT kept in registers
+    // for the factors below; the loads and the used-row flags go out together)
+    constexpr int GJ_RPT = 4;
+    double cv[GJ_RPT];
+    int ps[GJ_RPT];
+#pragma unroll
+    for (int u = 0; u < GJ_RPT; ++u) {
+        const int r = min(tid + 1024 * u, k - 1);
+        cv[u] = W[(size_t)r * k + col];
+        ps[u] = d.pivstep[r];
+    }
+#pragma unroll
+    for (int u = 0; u < GJ_RPT; ++u) {
+        const int r = tid + 1024 * u;
+        if (r >= k || ps[u] < col) continue;  // (used in an earlier step)
+        const double v = fabs(cv[u]);
+        if (v > bv || (v == bv && r < br)) {
+            bv = v;
+            br = r;
+        }
+    }
+    for (int r = tid + 1024 * GJ_RPT; r < k; r += 1024) {
+        if (d.pivstep[r] < col) continue;
         const double v = fabs(W[(size_t)r * k + col]);
         if (v > bv || (v == bv && r < br)) {
             bv = v;
@@ -4269,44 +4311,75 @@ __global__ void __launch_bounds__(1024) k_gj_pivot(Dev d, int k, int col, const 
         sv[w] = bv;
         sr[w] = br;
     }
-    __syncthreads();
     if (tid == 0) {
-        double v = sv[0];
-        int r = sr[0];
-        for (int i = 1; i < 16; ++i)
-            if (sv[i] > v || (sv[i] == v && sr[i] < r)) {
-                v = sv[i];
-                r = sr[i];
-            }
-        d.perm[col] = r;
-        d.pivstep[r] = col;
-        if (!(fabs(W[(size_t)r * k + col]) > d.tol_singular)) d.ctl->status = ST_NUMFAIL;
+        s_nr = 0;
+        s_nc = 0;
+    }
+    __syncthreads();
+    double v0 = sv[0];
+    int p = sr[0];
+    for (int i = 1; i < 16; ++i)
+        if (sv[i] > v0 || (sv[i] == v0 && sr[i] < p)) {
+            v0 = sv[i];
+            p = sr[i];
+        }
+    if (p >= k) p = 0;  // (no unused row: k steps never ask for more)
+    const double piv = W[(size_t)p * k + col];
+    if (tid == 0) {
+        d.perm[col] = p;
+        d.pivstep[p] = col;
+        if (!(fabs(piv) > d.tol_singular)) d.ctl->status = ST_NUMFAIL;
+    }
+    // row p's quotients and column c's factors, read before either is rewritten
+    for (int j = tid; j < k; j += 1024) {
+        const double q = j == col ? 0.0 : W[(size_t)p * k + j] / piv;
+        g.q[j] = q;
+        if (q != 0.0) g.cols[atomicAdd(&s_nc, 1)] = j;  // (any order: the pairs are independent)
+    }
+    for (int r = tid, u = 0; r < k; r += 1024, ++u) {
+        const double f = u < GJ_RPT ? cv[u < GJ_RPT ? u : 0] : W[(size_t)r * k + col];
+        g.f[r] = r == p ? 0.0 : f;
+        if (r != p && f != 0.0) {
+            const int o = atomicAdd(&s_nr, 1);
+            g.rows[o] = r;
+            g.fv[o] = f;
+        }
+    }
+    __syncthreads();  // (every read of row p and column c is done)
+    for (int j = tid; j < k; j += 1024)
+        if (j != col) W[(size_t)p * k + j] = g.q[j];
+    for (int r = tid; r < k; r += 1024) W[(size_t)r * k + col] = r == p ? 1.0 / piv : -(g.f[r] / piv);
+    if (tid == 0) {
+        g.cnt[0] = s_nr;
+        g.cnt[1] = s_nc;
     }
 }
 
-__global__ void __launch_bounds__(256) k_gj_elim(Dev d, int k, int col, const double* __restrict__ W,
-                                                 double* __restrict__ W2) {
+__global__ void __launch_bounds__(256) k_gj_elim(Dev d, int k, int col, double* __restrict__ W) {
+    const GjSide g = gj_side(d.W1, k);
+    const int nr = g.cnt[0], nc = g.cnt[1];
+    const int64_t np = (int64_t)nr * nc, kk = (int64_t)k * k;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, T = (int64_t)gridDim.x * blockDim.x;
+    if (np * 8 <= kk) {  // the pairs of nonzero factors
+        for (int64_t e = t0; e < np; e += T) {
+            const int a = (int)(e / nc), b = (int)(e % nc);
+            const int r = g.rows[a], j = g.cols[b];
+            double* x = W + (size_t)r * k + j;
+            *x = fma(-g.fv[a], g.q[j], *x);
+        }
+        return;
+    }
     const int p = d.perm[col];
-    const double piv = W[(size_t)p * k + col];
-    const int64_t kk = (int64_t)k * k;
-    const int64_t e0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * GJ_PT;
-    int r = (int)(e0 / k), j = (int)(e0 % k);
+    for (int64_t e0 = t0 * GJ_PT; e0 < kk; e0 += T * GJ_PT) {  // every entry, tested
 #pragma unroll
-    for (int t = 0; t < GJ_PT; ++t, ++j) {
-        const int64_t e = e0 + t;
-        if (e >= kk) return;
-        if (j == k) {
-            j = 0;
-            ++r;
+        for (int u = 0; u < GJ_PT; ++u) {
+            const int64_t e = e0 + u;
+            if (e >= kk) break;
+            const int r = (int)(e / k), j = (int)(e % k);
+            if (r == p || j == col) continue;
+            const double f = g.f[r], q = g.q[j];
+            if (f != 0.0 && q != 0.0) W[e] = fma(-f, q, W[e]);
         }
-        double v;
-        if (r == p) {
-            v = (j == col) ? 1.0 / piv : W[(size_t)p * k + j] / piv;
-        } else {
-            const double f = W[(size_t)r * k + col];
-            v = (j == col) ? -(f / piv) : fma(-f, W[(size_t)p * k + j] / piv, W[(size_t)r * k + j]);
-        }
-        W2[e] = v;
     }
 }
 
@@ -6874,13 +6947,12 @@ hipError_t launch_refactor_gj(const Dev& d, int k, hipStream_t st) {
     if (k <= 0) return hipSuccess;
     const int64_t kk = (int64_t)k * k;
     k_gj_init<<<cdiv(kk > k ? kk : k, 256), 256, 0, st>>>(d, k);
-    double *W = d.W0, *W2 = d.W1;
+    double* W = d.W0;  // (in place; d.W1 holds the step's side buffers)
+    unsigned ge = cdiv(kk, 256 * GJ_PT);
+    if (ge > 2048) ge = 2048;
     for (int c = 0; c < k; ++c) {
         k_gj_pivot<<<1, 1024, 0, st>>>(d, k, c, W);
-        k_gj_elim<<<cdiv(kk, 256 * GJ_PT), 256, 0, st>>>(d, k, c, W, W2);
-        double* sw = W;
-        W = W2;
-        W2 = sw;
+        k_gj_elim<<<ge, 256, 0, st>>>(d, k, c, W);
     }
     k_gj_final<<<cdiv(kk, 256), 256, 0, st>>>(d, k, W);
     return hipGetLastError();

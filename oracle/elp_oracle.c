@@ -370,10 +370,16 @@ static int gauss_jordan(orc_t* s) {
             if (r == p) {
                 for (int64_t j = 0; j < k; ++j)
                     W2[r * k + j] = (j == c) ? 1.0 / piv : W[p * k + j] / piv;
-            } else {
+            } else { /* (the zero rule, as basis_change's: a zero factor or quotient leaves the entry) */
                 const double f = W[r * k + c];
-                for (int64_t j = 0; j < k; ++j)
-                    W2[r * k + j] = (j == c) ? -(f / piv) : fma(-f, W[p * k + j] / piv, W[r * k + j]);
+                for (int64_t j = 0; j < k; ++j) {
+                    if (j == c) {
+                        W2[r * k + j] = -(f / piv);
+                        continue;
+                    }
+                    const double q = W[p * k + j] / piv;
+                    W2[r * k + j] = (f == 0.0 || q == 0.0) ? W[r * k + j] : fma(-f, q, W[r * k + j]);
+                }
             }
         }
         s->used[p] = 1;
