@@ -4427,22 +4427,36 @@ __global__ void __launch_bounds__(256) k_ns_gemm(Dev d, int k) {
             const int i = i0 + ty + 16 * u, j = j0 + tx + 16 * v;
             acc[u][v] = (MODE == 1 && i < k && j < k) ? d.Minv[(size_t)i * ldm + j] : 0.0;
         }
-    for (int l0 = 0; l0 < k; l0 += NS_L) {
+    // the next chunk's operands are loaded into registers while this chunk's
+    // fmas run (r05: one exposed global round trip per 16 values of l before)
+    constexpr int NS_PT = NS_T * NS_L / 256;
+    double na[NS_PT], nb[NS_PT];
+    auto load_chunk = [&](int l0) {
 #pragma unroll
-        for (int t = 0; t < NS_T * NS_L / 256; ++t) {
+        for (int t = 0; t < NS_PT; ++t) {
             const int e = tid + 256 * t;
             const int r = e / NS_L, c = e % NS_L;  // A: row r, l c
             const int i = i0 + r, l = l0 + c;
             double a = 0.0;
             if (i < k && l < k) a = MODE == 0 ? d.AS[(size_t)l * m + d.Rl[i]] : d.Minv[(size_t)i * ldm + l];
-            At[c][r] = a;
+            na[t] = a;
             const int rb = e / NS_T, cb = e % NS_T;  // B: l rb, column cb
             const int lb = l0 + rb, j = j0 + cb;
             double b = 0.0;
             if (lb < k && j < k) b = MODE == 0 ? d.Minv[(size_t)lb * ldm + j] : d.W0[(size_t)lb * k + j];
-            Bt[rb][cb] = b;
+            nb[t] = b;
+        }
+    };
+    load_chunk(0);
+    for (int l0 = 0; l0 < k; l0 += NS_L) {
+#pragma unroll
+        for (int t = 0; t < NS_PT; ++t) {
+            const int e = tid + 256 * t;
+            At[e % NS_L][e / NS_L] = na[t];
+            Bt[e / NS_T][e % NS_T] = nb[t];
         }
         __syncthreads();
+        if (l0 + NS_L < k) load_chunk(l0 + NS_L);
         const int lend = min(NS_L, k - l0);
         for (int ll = 0; ll < lend; ++ll) {
             double a[4], b[4];
