@@ -4410,20 +4410,25 @@ __global__ void k_refactor_rhs(Dev d) {
 // ONE fma chain over l in order (oracle newton_schulz: the same bits); per l the
 // thread reads 4 + 4 values for 16 fmas instead of 2 per fma (r03's 32 x 32
 // tiles, one output per thread: ~3 TFLOP/s, 5 ms at k = 2000).
-constexpr int NS_T = 64, NS_L = 16;
-template <int MODE>  // 0: E = I - M Minv (M[i][l] = AS[l][Rl[i]]) into W0; 1: W1 = Minv + Minv E
+// NS_R outputs per thread and dimension: 4 (64 x 64 tiles) below NS_R8_MIN
+// positions, 8 (128 x 128 tiles, 251 VGPRs) from there -- r05: 1.57 -> 1.36 ms
+// per call on the feasible-start KKT LP's bumps of ~3 000; small bumps keep the
+// smaller tiles' workgroup count
+constexpr int NS_L = 16, NS_R8_MIN = 1536;
+template <int MODE, int NS_R = 4>  // 0: E = I - M Minv (M[i][l] = AS[l][Rl[i]]) into W0; 1: W1 = Minv + Minv E
 __global__ void __launch_bounds__(256) k_ns_gemm(Dev d, int k) {
+    constexpr int NS_T = 16 * NS_R;
     __shared__ double At[NS_L][NS_T + 1];  // At[l][r]: operand A(i0 + r, l0 + l)
     __shared__ double Bt[NS_L][NS_T + 1];  // Bt[l][c]: operand B(l0 + l, j0 + c)
     __shared__ double red[4];
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
     const int i0 = blockIdx.y * NS_T, j0 = blockIdx.x * NS_T;
     const size_t ldm = (size_t)d.ldm, m = (size_t)d.m;
-    double acc[4][4];
+    double acc[NS_R][NS_R];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < NS_R; ++u)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
+        for (int v = 0; v < NS_R; ++v) {
             const int i = i0 + ty + 16 * u, j = j0 + tx + 16 * v;
             acc[u][v] = (MODE == 1 && i < k && j < k) ? d.Minv[(size_t)i * ldm + j] : 0.0;
         }
@@ -4459,23 +4464,23 @@ __global__ void __launch_bounds__(256) k_ns_gemm(Dev d, int k) {
         if (l0 + NS_L < k) load_chunk(l0 + NS_L);
         const int lend = min(NS_L, k - l0);
         for (int ll = 0; ll < lend; ++ll) {
-            double a[4], b[4];
+            double a[NS_R], b[NS_R];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) a[u] = At[ll][ty + 16 * u];
+            for (int u = 0; u < NS_R; ++u) a[u] = At[ll][ty + 16 * u];
 #pragma unroll
-            for (int v = 0; v < 4; ++v) b[v] = Bt[ll][tx + 16 * v];
+            for (int v = 0; v < NS_R; ++v) b[v] = Bt[ll][tx + 16 * v];
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < NS_R; ++u)
 #pragma unroll
-                for (int v = 0; v < 4; ++v) acc[u][v] = fma(a[u], b[v], acc[u][v]);
+                for (int v = 0; v < NS_R; ++v) acc[u][v] = fma(a[u], b[v], acc[u][v]);
         }
         __syncthreads();
     }
     double emax = 0.0;
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < NS_R; ++u)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
+        for (int v = 0; v < NS_R; ++v) {
             const int i = i0 + ty + 16 * u, j = j0 + tx + 16 * v;
             if (i >= k || j >= k) continue;
             if (MODE == 0) {
@@ -5413,7 +5418,9 @@ static int bfrt_reg() {
 // region holds up to DREG)
 // s_rec (k_dual_bfrt's fast tail; one chunk of regions): when the regions hold
 // <= 64 candidates they go to s_rec in LDS instead of dst -- no global stores
-// for the barrier after the compaction to wait on, no reload
+// for the barrier after the compaction to wait on, no reload (r05: loading
+// every region's first record with its count, to save the second round trip,
+// measured 1 us slower: ~900 scattered 80-byte records)
 DEV int compact_regions(const Dev& d, int nreg, DualCand* dst, int* scan_lds, DualCand* s_rec = nullptr) {
     __shared__ int s_off[BF_NT];
     const int tid = threadIdx.x;
@@ -6944,14 +6951,15 @@ hipError_t launch_refactor_ns_resid(const Dev& d, int k, hipStream_t st) {
         k_ns_resid_sp<<<k, 256, 0, st>>>(d, k);
         return hipGetLastError();
     }
-    dim3 g(cdiv(k, NS_T), cdiv(k, NS_T));
-    k_ns_gemm<0><<<g, 256, 0, st>>>(d, k);
+    if (k >= NS_R8_MIN) k_ns_gemm<0, 8><<<dim3(cdiv(k, 128), cdiv(k, 128)), 256, 0, st>>>(d, k);
+    else k_ns_gemm<0, 4><<<dim3(cdiv(k, 64), cdiv(k, 64)), 256, 0, st>>>(d, k);
     return hipGetLastError();
 }
 
 hipError_t launch_refactor_ns_update(const Dev& d, int k, hipStream_t st) {
     if (k <= 0) return hipSuccess;
-    k_ns_gemm<1><<<dim3(cdiv(k, NS_T), cdiv(k, NS_T)), 256, 0, st>>>(d, k);
+    if (k >= NS_R8_MIN) k_ns_gemm<1, 8><<<dim3(cdiv(k, 128), cdiv(k, 128)), 256, 0, st>>>(d, k);
+    else k_ns_gemm<1, 4><<<dim3(cdiv(k, 64), cdiv(k, 64)), 256, 0, st>>>(d, k);
     dim3 g(cdiv(k, 32), cdiv(k, 32));
     k_ns_store<<<g, dim3(32, 32), 0, st>>>(d, k);
     return hipGetLastError();
