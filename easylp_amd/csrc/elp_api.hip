@@ -2001,6 +2001,10 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
                         h->stamp_sum[i == 27 ? 34 : i == 29 ? 35 : 36] += i < 30 || i == 30 ? 1.0 : 0.0;
                     }
                 for (int i : {24, 25, 26, 28}) h->stamp_sum[i] += (double)r[i];  // (counts)
+                if (r[34] && r[23] > r[20]) {  // the BFRT launch's shader clock: s_memtime ticks per 10 ns
+                    h->stamp_sum[37] += (double)r[34];
+                    h->stamp_sum[38] += 10.0 * (double)(r[23] - r[20]);
+                }
                 h->stamp_n++;
             }
         }
@@ -2841,6 +2845,9 @@ extern "C" void elp_destroy(elp_handle* h) {
                      "(wave: loaded=%.2f us)\n",
                      h->stamp_sum[24] / h->stamp_n, h->stamp_sum[25] / h->stamp_n, h->stamp_sum[26] / h->stamp_n,
                      h->stamp_sum[28] / h->stamp_n, h->stamp_sum[27] / std::max(1.0, h->stamp_sum[34]) / 1e3);
+        if (h->stamp_sum[38] > 0)
+            std::fprintf(stderr, "k_dual_bfrt shader clock (s_memtime over s_memrealtime): %.0f MHz\n",
+                         1e3 * h->stamp_sum[37] / h->stamp_sum[38]);
         const double nt = std::max(1.0, h->stamp_sum[36]);
         std::fprintf(stderr, "k_dual_bfrt fast tail (us after its start; rounds over %.0f launches, the a_F phases over "
                      "the %.0f with flips): rounds done %.2f, a_F offsets %.2f, chains %.2f, support scan %.2f, "

@@ -5829,7 +5829,8 @@ DEV bool bfrt_flip_lds(const Dev& d, int nflip, int k, const int* s_flip, const 
 // (position mod 64, position) and bucketed as spl_build's, straight to memory.
 // r05t stamps: the block-level version spent ~6 us in its O(E) LDS loops.
 DEV void bfrt_flip_wave(const Dev& d, int nflip, int E, int k, const int* s_flip, const int* s_clen,
-                        const int* s_erow, const double* s_eval, const int* s_erp, const double* s_fdx) {
+                        const int* s_erow, const double* s_eval, const int* s_erp, const double* s_fdx,
+                        unsigned long long* s_st) {
     const int lane = threadIdx.x & 63;
     const unsigned long long below = (1ull << lane) - 1ull;
     const int len = lane < nflip ? s_clen[s_flip[lane]] : 0;
@@ -5853,6 +5854,7 @@ DEV void bfrt_flip_wave(const Dev& d, int nflip, int E, int k, const int* s_flip
         v = s_eval[sl];
         dx = s_fdx[f];
     }
+    BSTAMP(11);
     bool lead = has;
     double acc = 0.0;
     for (int e = 0; e < E; ++e) {
@@ -5863,6 +5865,7 @@ DEV void bfrt_flip_wave(const Dev& d, int nflip, int E, int k, const int* s_flip
             else acc = fma(ve, de, acc);
         }
     }
+    BSTAMP(12);
     const unsigned long long lm = __ballot(lead);
     const bool val = lead && rp >= 0 && rp < k;
     const unsigned long long vm = __ballot(val);
@@ -5918,6 +5921,7 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
         return;
     }
     BSTAMP(0);
+    if (ELP_DIAG && s_st && threadIdx.x == 0) s_st[4] = __builtin_amdgcn_s_memtime();  // (shader clock)
     // (the counters the tail updates, read now: nothing else writes them during the launch)
     const int64_t pf_flips = c->flips, pf_pp = c->price_passes;
     const double pf_pb = c->price_bytes, pf_ib = c->iter_bytes;
@@ -6210,7 +6214,8 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
             }
         if (fast && !bad && E <= 64) {  // wave 0 alone; the other waves are done
             if (tid >= 64) return;
-            bfrt_flip_wave(d, nflip, E, kq, s_flip, s_clen, s_erow, s_eval, s_erp, s_fdx);
+            BSTAMP(10);
+            bfrt_flip_wave(d, nflip, E, kq, s_flip, s_clen, s_erow, s_eval, s_erp, s_fdx, s_st);
             BSTAMP(13);
         } else if (!(fast && bfrt_flip_lds(d, nflip, kq, s_flip, s_clen, s_erow, s_eval, s_erp, s_fdx, s_st))) {
             if (fast && tid < nflip) {  // (the sequential path reads the flip list from memory; its first barrier orders these)
@@ -6235,6 +6240,7 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     }
     if (tid != 0) return;
     BSTAMP(3);
+    if (ELP_DIAG && s_st) s_st[5] = __builtin_amdgcn_s_memtime();
     if (ELP_DIAG && d.dstamp) {  // the LDS stamps out: 20-23 start / compacted / decided / tail end,
                                  // 27 records loaded, 29 rounds done, 30-33 the LDS a_F phases; counts 24-26, 28
         unsigned long long* o = d.dstamp + (size_t)dslot * DSTAMP_STRIDE;
@@ -6249,6 +6255,7 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
         o[25] = (unsigned long long)nflip;
         o[26] = wave ? 1ull : 0ull;
         o[28] = N <= 64 ? s_st[15] : 0ull;
+        o[34] = s_st[5] - s_st[4];  // shader clocks over the launch (s_memtime)
     }
     const int64_t it = c->iter;
     if (qidx < 0) {  // dual unbounded: the LP is infeasible (oracle: trace -2, the leaving variable)
