@@ -4898,18 +4898,40 @@ DEV void chz_none(ChzRec& r) {
     r.var = r.e = -1;
     r.s = r.pad = 0;
 }
-// block-wide best of NT records (tree in LDS; a total order, so any tree agrees)
+// block-wide best of NT records in chz_better's total order (the records' ids
+// are distinct): each wave's best by DPP reductions -- the largest score, then
+// the lowest id among the lanes holding it (Bland: the lowest id) -- then the
+// NT / 64 wave bests through LDS, one barrier (r05; r04: an 8-level LDS tree,
+// a barrier per level)
 template <int NT>
 DEV ChzRec block_best_chz(ChzRec r, int bland, ChzRec* lds) {
-    const int t = threadIdx.x;
-    lds[t] = r;
-    __syncthreads();
-    for (int h = NT / 2; h >= 1; h >>= 1) {
-        if (t < h && chz_better(lds[t + h], lds[t], bland)) lds[t] = lds[t + h];
-        __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const bool valid = r.var >= 0;
+    bool in = valid;
+    if (!bland) {
+        const double smax = wave_max_f64(valid ? r.score : -HUGE_VAL);
+        in = valid && r.score == smax;
     }
-    const ChzRec out = lds[0];
+    const int vmin = wave_min_i32(in ? r.var : 0x7fffffff);
+    ChzRec b;
+    chz_none(b);
+    if (vmin != 0x7fffffff) {
+        const int win = __ffsll((long long)__ballot(in && r.var == vmin)) - 1;
+        b.score = readlane_f64(r.score, win);
+        b.x = readlane_f64(r.x, win);
+        b.beta = readlane_f64(r.beta, win);
+        b.var = __builtin_amdgcn_readlane(r.var, win);
+        b.e = __builtin_amdgcn_readlane(r.e, win);
+        b.s = __builtin_amdgcn_readlane(r.s, win);
+    }
+    if (lane == 0) lds[w] = b;
     __syncthreads();
+    ChzRec out = lds[0];
+    for (int i = 1; i < NT / 64; ++i) {
+        const ChzRec o = lds[i];
+        chz_take(out, o, chz_better(o, out, bland));
+    }
+    __syncthreads();  // (lds may be rewritten by the caller)
     return out;
 }
 
