@@ -3937,7 +3937,13 @@ DEV void apply_minv(const Dev& d, const Plan& P, int64_t e0, int64_t estride, bo
 // with the same bits.
 constexpr int SRU_U = 8;
 constexpr unsigned SRU_WG_MAX = 4096;
-constexpr unsigned sru_wgs(int k_ub) { return (unsigned)(k_ub + 1) < SRU_WG_MAX ? (unsigned)(k_ub + 1) : SRU_WG_MAX; }
+#ifndef ELP_SRU_RPW
+#define ELP_SRU_RPW 1  // rows per workgroup (r05ze: 4 -- their multipliers in one round trip -- measured slower)
+#endif
+constexpr int SRU_RPW = ELP_SRU_RPW;
+constexpr unsigned sru_wgs(int k_ub) {
+    return (unsigned)((k_ub + SRU_RPW) / SRU_RPW) < SRU_WG_MAX ? (unsigned)((k_ub + SRU_RPW) / SRU_RPW) : SRU_WG_MAX;
+}
 template <int NT>
 DEV void apply_minv_sru(const Dev& d, const Plan& P, int wg, int nwg) {
     if (P.action != ACT_PIVOT || P.pcase == PC_E || nwg <= 0) return;
@@ -3953,9 +3959,19 @@ DEV void apply_minv_sru(const Dev& d, const Plan& P, int wg, int nwg) {
     double* M = d.Minv;
     double* MT = d.noT ? nullptr : d.MinvT;
     const double va = pc == PC_D ? d.vvec[P.a] : 1.0;
-    for (int i = wg; i < nl; i += nwg) {
-        if (i == ex1) continue;
-        double a1 = x1[i];
+    // rows wg, wg + nwg, ...: SRU_RPW multipliers loaded together per group
+    for (int i0 = wg; i0 < nl; i0 += nwg * SRU_RPW) {
+      double a1s[SRU_RPW];
+#pragma unroll
+      for (int u = 0; u < SRU_RPW; ++u) {
+          const int i = i0 + u * nwg;
+          a1s[u] = x1[i < nl ? i : 0];
+      }
+#pragma unroll
+      for (int u = 0; u < SRU_RPW; ++u) {
+        const int i = i0 + u * nwg;
+        if (i >= nl || i == ex1) continue;
+        double a1 = a1s[u];
         if (pc == PC_B) a1 = -a1;
         else if (pc == PC_D) a1 = a1 / va;
         if (a1 == 0.0) continue;
@@ -3977,6 +3993,7 @@ DEV void apply_minv_sru(const Dev& d, const Plan& P, int wg, int nwg) {
                 if (MT) MT[(size_t)j * ldm + i] = v;
             }
         }
+      }
     }
     // ---- the border, strided over the launch
     auto put = [&](int i, int j, double v) {
