@@ -19,12 +19,15 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-@pytest.mark.parametrize("spz,defer,minvt", [("0", "1", "0"), ("16", "1", "0"), ("0", "0", "0"), ("0", "1", "1")],
-                         ids=["rowwise", "default-zr", "rowwise-no-defer", "rowwise-minvt"])
-def test_csc_parity_with_sparse_ftran(spz, defer, minvt):
+@pytest.mark.parametrize("spz,defer,minvt,sru", [("0", "1", "0", "1"), ("16", "1", "0", "1"), ("0", "0", "0", "1"),
+                                                ("0", "1", "1", "1"), ("0", "1", "0", "0")],
+                         ids=["rowwise", "default-zr", "rowwise-no-defer", "rowwise-minvt", "rowwise-dense-update"])
+def test_csc_parity_with_sparse_ftran(spz, defer, minvt, sru):
     """(defer 0: the dual phase's update in its own k_update launch, ELP_DUAL_DEFER=0;
-    minvt 1: the CSC load keeps the transposed inverse, ELP_CSC_MINVT=1)"""
-    env = dict(os.environ, ELP_SPF_MIN="1", ELP_SPZ_MIN_MB=spz, ELP_DUAL_DEFER=defer, ELP_CSC_MINVT=minvt)
+    minvt 1: the CSC load keeps the transposed inverse, ELP_CSC_MINVT=1; sru 0: the
+    dense inverse update instead of the sparse one, ELP_SRU=0 -- the default CSC runs
+    of every suite take the sparse one, and both keep the oracle's zero rule)"""
+    env = dict(os.environ, ELP_SPF_MIN="1", ELP_SPZ_MIN_MB=spz, ELP_DUAL_DEFER=defer, ELP_CSC_MINVT=minvt, ELP_SRU=sru)
     cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", "-m", "gpu",
            os.path.join(HERE, "test_gpu_csc.py"),
            os.path.join(HERE, "test_gpu_dual.py") + "::test_dual_known_and_robust",
