@@ -1,62 +1,35 @@
-"""Per-kernel HBM traffic of one full solve from two rocprofv3 PMC passes
-(FETCH_SIZE and WRITE_SIZE need separate passes: MI355X_MICROARCH.md, TCC
-counter budget) of `bench.py --steps 1 --warmup 0 ...` -- the latency kernels
-next to the pricing sweep.
-
-FETCH_SIZE on gfx950 reports half the bytes of a wide (16 B per lane)
-coalesced read; narrower or scattered reads (most of the latency kernels) are
-uncalibrated, so both the raw 1024 x FETCH_SIZE and the doubled figure are
-given.  Algorithmic bytes are evaluated at the solve's
-final bump size k and |Y| (both grow nearly monotonically), i.e. an upper
-bound per iteration.
-Usage: python tools/pmc_kernels.py <fetch counter_collection.csv> <write counter_collection.csv> <bench.json>
-"""
+"""Per-kernel averages of a rocprofv3 --pmc pass (counter_collection.csv):
+counter value per dispatch, averaged over the dispatches of each kernel, plus
+the wave-cycle split (SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY over
+SQ_WAVE_CYCLES) when those counters are present.  usage: pmc_kernels.py CSV"""
+import collections
 import csv
-import json
 import sys
-from collections import defaultdict
 
 
-def per_kernel(path, counter):
-    acc = defaultdict(lambda: [0, 0.0])
+def main(path):
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    disp = collections.defaultdict(set)
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter:
-            continue
-        name = r["Kernel_Name"].split("(")[0]
-        acc[name][0] += 1
-        acc[name][1] += float(r["Counter_Value"]) * 1024.0
-    return acc
-
-
-def main(fetch_csv, write_csv, bench_json):
-    b = json.loads(open(bench_json).read().strip().splitlines()[-1])
-    m, n = b["config"]["m"], b["config"]["n"]
-    k, ny = b["final"]["bump_dim"], b["final"]["y_rows"]
-    model = {  # per launch, at the final k and |Y|
-        "k_price": 8.0 * ny * n + 9.0 * n + 12.0 * ny + 24.0 * n,
-        "k_select_ftran": 8.0 * k * k + 32.0 * (n / 128 + 2),
-        "k_ftran_zr": 8.0 * m * k,
-        "k_ratio": 8.0 * k * k + 16.0 * n,
-    }
-    f = per_kernel(fetch_csv, "FETCH_SIZE")
-    w = per_kernel(write_csv, "WRITE_SIZE")
-    rows = []
-    for name, (cnt, tot) in sorted(f.items(), key=lambda kv: -kv[1][1]):
-        if cnt < 100:
-            continue  # refactor / load kernels: a handful of dispatches
-        base = name.replace("void ", "").replace("elp::", "").split("<")[0]
-        wc, wt = w.get(name, (0, 0.0))
-        rows.append({
-            "kernel": name,
-            "dispatches": cnt,
-            "fetch_raw_bytes_per_launch": tot / cnt,
-            "fetch_x2_bytes_per_launch": 2.0 * tot / cnt,
-            "write_bytes_per_launch": wt / wc if wc else None,
-            "algorithmic_bytes_at_final_k": model.get(base),
-        })
-    print(json.dumps({"m": m, "n": n, "final_k": k, "final_y_rows": ny,
-                      "iterations": b["final"]["iterations_to_optimal"], "kernels": rows}, indent=1))
+        name = r.get("Kernel_Name", "?").split("(")[0]
+        ctr = r.get("Counter_Name")
+        val = float(r.get("Counter_Value", 0) or 0)
+        did = r.get("Dispatch_Id") or r.get("Correlation_Id")
+        per[name][ctr] += val
+        disp[name].add(did)
+    for name in sorted(per, key=lambda n: -per[n].get("SQ_WAVE_CYCLES", 0)):
+        n = max(1, len(disp[name]))
+        c = per[name]
+        line = f"{name[-30:]:30s} n {n:6d}"
+        for k in sorted(c):
+            line += f"  {k} {c[k] / n:.0f}"
+        wc = c.get("SQ_WAVE_CYCLES", 0)
+        if wc:
+            line += "  | wait %.0f%% issue-stall %.0f%% active %.0f%%" % (
+                100 * c.get("SQ_WAIT_ANY", 0) / wc, 100 * c.get("SQ_WAIT_INST_ANY", 0) / wc,
+                100 * c.get("SQ_ACTIVE_INST_ANY", 0) / wc)
+        print(line)
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(sys.argv[1])
