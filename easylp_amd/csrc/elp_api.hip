@@ -1982,7 +1982,7 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
         if (h->d.dstamp && c->status == ST_RUN && (h->phase == 2 || h->phase == 3)) {
             std::vector<unsigned long long> v(DSTAMP_STRIDE * 64);
             HIPCHK(hipMemcpy(v.data(), h->d.dstamp, v.size() * 8, hipMemcpyDeviceToHost));
-            if (h->stamp_sum.empty()) h->stamp_sum.assign(DSTAMP_STRIDE, 0.0);
+            if (h->stamp_sum.empty()) h->stamp_sum.assign(DSTAMP_STRIDE + 24, 0.0);
             for (int t = 0; t < chunk; ++t) {
                 const unsigned long long* r = &v[(size_t)t * DSTAMP_STRIDE];
                 // time base: the first workgroup's start (ELP_STAMPS=2), else workgroup 0's
@@ -2001,6 +2001,21 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
                         h->stamp_sum[i == 27 ? 34 : i == 29 ? 35 : 36] += i < 30 || i == 30 ? 1.0 : 0.0;
                     }
                 for (int i : {24, 25, 26, 28}) h->stamp_sum[i] += (double)r[i];  // (counts)
+                if (r[30] && r[20] && r[29] >= r[20] && r[23] >= r[20] && r[30] - r[20] < 100000ull) {
+                    // the launches whose fast tail ran (flips): every phase over the same launches
+                    int s = 40;
+                    for (int i : {21, 27, 29, 22, 30, 23}) h->stamp_sum[s++] += 10.0 * (double)(long long)(r[i] - r[20]);
+                    h->stamp_sum[46] += (double)r[24];
+                    h->stamp_sum[47] += (double)r[28];
+                    h->stamp_sum[48] += 1.0;
+                }
+                if (r[36] >= 1 && r[36] <= 3 && r[23] >= r[20] && r[23] - r[20] < 100000ull) {
+                    // per a_F path (1 one wave, 2 LDS block, 3 column walk): launches, end, entries
+                    const int b = 49 + 3 * (int)(r[36] - 1);
+                    h->stamp_sum[b] += 1.0;
+                    h->stamp_sum[b + 1] += 10.0 * (double)(r[23] - r[20]);
+                    h->stamp_sum[b + 2] += (double)(long long)r[35];
+                }
                 if (r[34] && r[23] > r[20]) {  // the BFRT launch's shader clock: s_memtime ticks per 10 ns
                     h->stamp_sum[37] += (double)r[34];
                     h->stamp_sum[38] += 10.0 * (double)(r[23] - r[20]);
@@ -2855,6 +2870,19 @@ extern "C" void elp_destroy(elp_handle* h) {
                      h->stamp_sum[35], h->stamp_sum[36], h->stamp_sum[29] / std::max(1.0, h->stamp_sum[35]) / 1e3,
                      h->stamp_sum[30] / nt / 1e3, h->stamp_sum[31] / nt / 1e3, h->stamp_sum[32] / nt / 1e3,
                      h->stamp_sum[33] / nt / 1e3);
+        const double nf = std::max(1.0, h->stamp_sum[48]);
+        std::fprintf(stderr, "k_dual_bfrt with a fast tail (%.0f launches; us after its start): compacted %.2f, "
+                     "records loaded %.2f, rounds done %.2f, decided %.2f, tail start %.2f, end %.2f "
+                     "(candidates %.1f, rounds %.2f)\n",
+                     h->stamp_sum[48], h->stamp_sum[40] / nf / 1e3, h->stamp_sum[41] / nf / 1e3,
+                     h->stamp_sum[42] / nf / 1e3, h->stamp_sum[43] / nf / 1e3, h->stamp_sum[44] / nf / 1e3,
+                     h->stamp_sum[45] / nf / 1e3, h->stamp_sum[46] / nf, h->stamp_sum[47] / nf);
+        for (int q = 0; q < 3; ++q) {
+            const double* b = &h->stamp_sum[49 + 3 * q];
+            std::fprintf(stderr, "k_dual_bfrt a_F by %s: %.0f launches, end %.2f us, flip entries %.1f\n",
+                         q == 0 ? "one wave" : q == 1 ? "LDS block" : "column walk", b[0],
+                         b[1] / std::max(1.0, b[0]) / 1e3, b[2] / std::max(1.0, b[0]));
+        }
     }
     if (!h) return;
     destroy_group(h);

@@ -148,6 +148,11 @@ struct DualCand {
     // the column's bounds, value and cost (scaled): what the other shards need
     // when it enters (column-sharded ranks exchange the candidates)
     double lb, ub, x, c;
+    // CSC: the column's first entry and length (cptr, as the pricing pass read
+    // it), so k_dual_bfrt's fast tail loads a flipped column without cptr's
+    // round trip; len -1: no column (a slack, or not a CSC record)
+    int64_t c0;
+    int32_t len, pad;
 };
 // a dual CHUZR partial (k_dual_chuzr, one per workgroup)
 struct ChzRec {

@@ -5190,6 +5190,9 @@ DEV bool dual_candidate(int8_t vs, double a, double dj, double lb, double ub, in
     o.ub = ub;
     o.x = xj;
     o.c = cj;
+    o.c0 = 0;
+    o.len = -1;
+    o.pad = 0;
     return true;
 }
 
@@ -5423,6 +5426,8 @@ __global__ void __launch_bounds__(TILE_COLS) k_dual_price_csc(Dev d, int nsw, in
                     }
             }
             f = dual_candidate(vs, aa, cj - ad, lbj, ubj, rs, bland, dtol, pivtol, (int)j, xj, cj, o);
+            o.c0 = ta;
+            o.len = (int)(t1 - ta < (1 << 30) ? t1 - ta : (1 << 30));
         }
     }
     emit_region<TILE_COLS>(d, (int)tile, f, o, false, o, wcnt);
@@ -5692,13 +5697,71 @@ DEV void bfrt_wave(const Dev& d, int N, int bland, double ptol, double slope, do
 // kernel's sparse list (Dev::afl).  More: the flips one after the other, a
 // barrier each, after clearing all of a_F (r04's path).
 constexpr int AF_PAR = 256;
+// The flips' entries grouped by row (bfrt_flip_column, bfrt_flip_lds): an
+// open-addressed LDS table of the rows (E <= AF_PAR < AF_HT entries: probing
+// ends) holding each row's entries as a bit set over the entry index, so the
+// row's first entry runs the chain over the row's own entries in ascending
+// index -- flip order, the same terms in the same order -- instead of every
+// thread scanning all E entries twice (r05zk: 29 us per launch at ~83
+// entries, against 12 us for the one-wave path).  Clear before a barrier,
+// insert before the next, chain after it.
+constexpr int AF_HT = 2 * AF_PAR, AF_W = AF_PAR / 64;
+DEV int* af_hkey() {
+    __shared__ int k[AF_HT];
+    return k;
+}
+DEV unsigned long long* af_hbit() {
+    __shared__ unsigned long long b[AF_HT * AF_W];
+    return b;
+}
+DEV void af_tab_clear() {
+    int* hk = af_hkey();
+    unsigned long long* hb = af_hbit();
+    for (int t = threadIdx.x; t < AF_HT; t += blockDim.x) {
+        hk[t] = -1;
+#pragma unroll
+        for (int w = 0; w < AF_W; ++w) hb[t * AF_W + w] = 0ull;
+    }
+}
+// entry e (< AF_PAR) of row `row` (>= 0) into the table; returns its slot
+DEV int af_tab_insert(int row, int e) {
+    int* hk = af_hkey();
+    int slot = (int)(((unsigned)row * 2654435761u) >> 23) & (AF_HT - 1);
+    for (;;) {
+        const int pr = atomicCAS(&hk[slot], -1, row);
+        if (pr == -1 || pr == row) break;
+        slot = (slot + 1) & (AF_HT - 1);
+    }
+    atomicOr(&af_hbit()[slot * AF_W + (e >> 6)], 1ull << (e & 63));
+    return slot;
+}
+// entry e leads its row when it is the row's first; the lead's chain in acc
+DEV bool af_tab_chain(int slot, int e, const double* s_v, const double* s_dx, double& acc) {
+    const unsigned long long* hb = af_hbit() + slot * AF_W;
+    unsigned long long bw[AF_W];
+#pragma unroll
+    for (int w = 0; w < AF_W; ++w) bw[w] = hb[w];
+    int first = -1;
+#pragma unroll
+    for (int w = AF_W - 1; w >= 0; --w)
+        if (bw[w]) first = 64 * w + __ffsll((long long)bw[w]) - 1;
+    if (first != e) return false;
+#pragma unroll
+    for (int w = 0; w < AF_W; ++w)
+        for (unsigned long long mk = bw[w]; mk; mk &= mk - 1ull) {
+            const int x = 64 * w + __ffsll((long long)mk) - 1;
+            acc = fma(s_v[x], s_dx[x], acc);
+        }
+    return true;
+}
 // (myj / mydx: thread t's flip t, t < nflip <= BF_NT -- its column and dx)
 DEV void bfrt_flip_column(const Dev& d, int nflip, int k, int myj, double mydx) {
-    __shared__ int s_off[BF_NT], s_row[AF_PAR], s_lpos[SPL], s_lkey[SPL], s_lsb[72], s_scan[BF_NT / 64];
+    __shared__ int s_off[BF_NT], s_lpos[SPL], s_lkey[SPL], s_lsb[72], s_scan[BF_NT / 64];
     __shared__ double s_v[AF_PAR], s_dx[AF_PAR], s_lval[SPL];
     __shared__ int64_t s_c0[BF_NT];
     __shared__ double s_fdx[BF_NT];
     const int tid = threadIdx.x, m = d.m;
+    af_tab_clear();
     int len = 0;
     if (tid < nflip) {
         const int64_t c0 = d.cptr[myj];
@@ -5735,7 +5798,7 @@ DEV void bfrt_flip_column(const Dev& d, int nflip, int k, int myj, double mydx) 
     }
     if (tid < nflip) s_off[tid] = excl;
     __syncthreads();  // (also orders the clear before the chains' stores)
-    int row = -1;
+    int row = -1, slot = 0;
     if (tid < E) {
         int lo = 0, hi = nflip - 1;  // the last flip whose offset is <= tid
         while (lo < hi) {
@@ -5745,24 +5808,17 @@ DEV void bfrt_flip_column(const Dev& d, int nflip, int k, int myj, double mydx) 
         }
         const int64_t t = s_c0[lo] + (tid - s_off[lo]);
         row = d.rind[t];
-        s_row[tid] = row;
         s_v[tid] = d.cval[t];
         s_dx[tid] = s_fdx[lo];
+        slot = af_tab_insert(row, tid);
     }
     __syncthreads();
     bool lead = false;
     double acc = 0.0;
     int p = -1;
     if (tid < E) {
-        lead = true;
-        for (int e = 0; e < tid; ++e)
-            if (s_row[e] == row) {
-                lead = false;
-                break;
-            }
+        lead = af_tab_chain(slot, tid, s_v, s_dx, acc);
         if (lead) {
-            for (int e = tid; e < E; ++e)
-                if (s_row[e] == row) acc = fma(s_v[e], s_dx[e], acc);
             d.aF[row] = acc;
             p = d.rpos[row];
         }
@@ -5793,10 +5849,11 @@ DEV void bfrt_flip_column(const Dev& d, int nflip, int k, int myj, double mydx) 
 constexpr int BF_ENT = 8;
 DEV bool bfrt_flip_lds(const Dev& d, int nflip, int k, const int* s_flip, const int* s_clen, const int* s_erow,
                        const double* s_eval, const int* s_erp, const double* s_fdx, unsigned long long* s_st) {
-    __shared__ int s_off[64], s_row[AF_PAR], s_lpos[SPL], s_lkey[SPL], s_lsb[72], s_scan[BF_NT / 64];
+    __shared__ int s_off[64], s_lpos[SPL], s_lkey[SPL], s_lsb[72], s_scan[BF_NT / 64];
     __shared__ double s_v[AF_PAR], s_dx[AF_PAR], s_lval[SPL];
     __shared__ int s_bad;
     const int tid = threadIdx.x;
+    af_tab_clear();  // (the entries grouped by row)
     int len = 0;
     if (tid == 0) s_bad = 0;
     if (tid < nflip) len = s_clen[s_flip[tid]];
@@ -5807,7 +5864,7 @@ DEV bool bfrt_flip_lds(const Dev& d, int nflip, int k, const int* s_flip, const 
     __syncthreads();
     BSTAMP(10);
     if (s_bad || E > AF_PAR) return false;
-    int row = -1, rp = -1;
+    int row = -1, rp = -1, slot = 0;
     if (tid < E) {
         int lo = 0, hi = nflip - 1;  // the last flip whose offset is <= tid
         while (lo < hi) {
@@ -5818,24 +5875,14 @@ DEV bool bfrt_flip_lds(const Dev& d, int nflip, int k, const int* s_flip, const 
         const int sl = s_flip[lo] * BF_ENT + (tid - s_off[lo]);
         row = s_erow[sl];
         rp = s_erp[sl];
-        s_row[tid] = row;
         s_v[tid] = s_eval[sl];
         s_dx[tid] = s_fdx[lo];
+        slot = af_tab_insert(row, tid);
     }
     __syncthreads();
     bool lead = false;
     double acc = 0.0;
-    if (tid < E) {
-        lead = true;
-        for (int e = 0; e < tid; ++e)
-            if (s_row[e] == row) {
-                lead = false;
-                break;
-            }
-        if (lead)
-            for (int e = tid; e < E; ++e)
-                if (s_row[e] == row) acc = fma(s_v[e], s_dx[e], acc);
-    }
+    if (tid < E) lead = af_tab_chain(slot, tid, s_v, s_dx, acc);
     // (every global store after the last barrier: a barrier waits for the
     //  workgroup's outstanding stores)
     BSTAMP(11);
@@ -5965,8 +6012,17 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     const int64_t pf_flips = c->flips, pf_pp = c->price_passes;
     const double pf_pb = c->price_bytes, pf_ib = c->iter_bytes;
     const int pf_k = c->k, pf_ny = c->ny;
-    if (c->status != ST_RUN) return;
     const int tid = threadIdx.x;
+    // (CSC: the last a_F's support count and this thread's first entry of it,
+    //  for the clearing waves of the fast tail -- read now, beside the
+    //  compaction's loads, not two dependent round trips after it; afs holds
+    //  1 + 1024 entries, the speculative index stays below 1 + 448)
+    int pf_afn = 0, pf_afr = 0;
+    if (d.csc && tid >= 64 + 64 * BF_ENT) {
+        pf_afn = d.afs[0];
+        pf_afr = d.afs[1 + tid - (64 + 64 * BF_ENT)];
+    }
+    if (c->status != ST_RUN) return;
     const int bland = c->bland;
     // ---- compaction (one GPU: the regions; sharded: the ranks' records, in
     //      rank order = ascending structural id, the last rank's slacks last)
@@ -6004,9 +6060,9 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
                 const int j = s_rec[cc].j;
                 const int jl = j < d.N ? loc_of(d, j) : -1;
                 int len = -1;  // (a slack: no column to scatter; it never flips -- no finite range)
-                if (jl >= 0) {
-                    const int64_t c0 = d.cptr[jl];
-                    len = (int)(d.cptr[jl + 1] - c0);
+                if (jl >= 0) {  // (the column's extent from its record: the pricing pass's cptr)
+                    const int64_t c0 = s_rec[cc].c0;
+                    len = s_rec[cc].len;
                     if (e < len && len <= BF_ENT) {
                         const int row = d.rind[c0 + e];
                         s_eval[sl] = d.cval[c0 + e];
@@ -6018,11 +6074,11 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
             }
         } else if (fast) {  // the last a_F's support back to zero (or all of a_F)
             const int t0 = tid - (64 + 64 * BF_ENT), T = BF_NT - (64 + 64 * BF_ENT);
-            const int pn = d.afs[0];
+            const int pn = pf_afn;
             if (pn < 0) {
                 for (int i = t0; i < d.m; i += T) d.aF[i] = 0.0;
             } else {
-                for (int t = t0; t < pn; t += T) d.aF[d.afs[1 + t]] = 0.0;
+                for (int t = t0; t < pn; t += T) d.aF[t == t0 ? pf_afr : d.afs[1 + t]] = 0.0;
             }
         }
         if (tid == 0) {
@@ -6241,6 +6297,7 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
     // CSC (one GPU): a_F = sum of the flipped columns times their dx here, in
     // place of a one-workgroup k_dual_flip_col launch -- each row's entries in
     // flip order, the same fma chain
+    int dbg_E = 0, dbg_path = 0;  // (diagnostic builds: the flips' entries and the a_F path taken)
     if (d.csc && !gathered && qidx >= 0 && nflip > 0) {
         const int kq = pf_k;
         int E = 0;  // (the flips' entries, every thread alike: the wave path or a block path, uniformly)
@@ -6251,12 +6308,15 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
                 bad = bad || l < 0;
                 E += l > 0 ? l : 0;
             }
+        dbg_E = bad ? -1 : E;
+        dbg_path = fast && !bad && E <= 64 ? 1 : fast ? 2 : 3;
         if (fast && !bad && E <= 64) {  // wave 0 alone; the other waves are done
             if (tid >= 64) return;
             BSTAMP(10);
             bfrt_flip_wave(d, nflip, E, kq, s_flip, s_clen, s_erow, s_eval, s_erp, s_fdx, s_st);
             BSTAMP(13);
         } else if (!(fast && bfrt_flip_lds(d, nflip, kq, s_flip, s_clen, s_erow, s_eval, s_erp, s_fdx, s_st))) {
+            if (ELP_DIAG) dbg_path = 3;
             if (fast && tid < nflip) {  // (the sequential path reads the flip list from memory; its first barrier orders these)
                 d.dflip[tid] = s_fj[tid];
                 d.dflipdx[tid] = s_fdx[tid];
@@ -6295,6 +6355,8 @@ __global__ void __launch_bounds__(BF_NT) k_dual_bfrt(Dev d, int nreg, int gather
         o[26] = wave ? 1ull : 0ull;
         o[28] = N <= 64 ? s_st[15] : 0ull;
         o[34] = s_st[5] - s_st[4];  // shader clocks over the launch (s_memtime)
+        o[35] = (unsigned long long)(long long)dbg_E;
+        o[36] = (unsigned long long)dbg_path;
     }
     const int64_t it = c->iter;
     if (qidx < 0) {  // dual unbounded: the LP is infeasible (oracle: trace -2, the leaving variable)

@@ -3,8 +3,9 @@
 // fp64 adds twice (the block is the body of a two-trip loop the compiler may
 // not unroll), stamping s_memrealtime (100 MHz) before, between and after: the
 // first trip runs cold code, the second the same code from the instruction
-// cache.  A second kernel of the same shape but a different body is launched
-// in between to evict the first one's lines.  Build:
+// cache.  Before each probe launch a read of 64 MiB (the code out of L2, still
+// in the MALL) or 1 GiB (out of the MALL too) evicts it further (r05zi: the
+// cold trip costs ~0.1-0.3 us per 8 KB in every case).  Build:
 //   hipcc --offload-arch=gfx950 -O3 tools/icache_probe.hip -o /tmp/icache_probe
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -33,20 +34,41 @@ __global__ void probe(unsigned long long* out, double* sink, int trips) {
     sink[threadIdx.x] = a0 + a1 + a2 + a3;
 }
 
+// reads n doubles (grid-stride): with 64 MB the probe's code is out of every
+// XCD's L2 (4 MB each) but still in the 256 MB MALL; with 1 GB out of both
+__global__ void evict(const double* buf, size_t n, double* sink) {
+    double a = 0.0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        a += buf[i];
+    if (a == 12345.678) sink[0] = a;
+}
+
 int main() {
     unsigned long long* out;
     double* sink;
+    double* buf;
     hipMalloc(&out, 64);
     hipMalloc(&sink, 64 * sizeof(double));
+    const size_t big = (size_t)1 << 27;  // 1 GiB of doubles
+    hipMalloc(&buf, big * sizeof(double));
+    hipMemset(buf, 0, big * sizeof(double));
     unsigned long long h[2];
-    for (int it = 0; it < 5; ++it) {
-        probe<1><<<1, 64>>>(out, sink, 2);
-        hipMemcpy(h, out, 16, hipMemcpyDeviceToHost);
-        printf("salt 1: first trip %.2f us, second trip %.2f us (4096 fp64 adds, ~8 KB of code)\n", h[0] / 100.0,
-               h[1] / 100.0);
-        probe<2><<<1, 64>>>(out, sink, 2);
-        hipMemcpy(h, out, 16, hipMemcpyDeviceToHost);
-        printf("salt 2: first trip %.2f us, second trip %.2f us\n", h[0] / 100.0, h[1] / 100.0);
+    const size_t modes[3] = {0, (size_t)8 << 20, big};  // none, 64 MiB, 1 GiB
+    const char* names[3] = {"hot (no eviction)", "after 64 MiB read (L2 evicted)", "after 1 GiB read (MALL evicted)"};
+    for (int md = 0; md < 3; ++md) {
+        double f = 0.0, s2 = 0.0;
+        const int R = 8;
+        for (int it = 0; it < R + 1; ++it) {
+            if (modes[md]) evict<<<2048, 256>>>(buf, modes[md], sink);
+            probe<1><<<1, 64>>>(out, sink, 2);
+            hipMemcpy(h, out, 16, hipMemcpyDeviceToHost);
+            if (it > 0) {  // (the first: the code object's first load)
+                f += h[0] / 100.0;
+                s2 += h[1] / 100.0;
+            }
+        }
+        printf("%-34s first trip %.2f us, second trip %.2f us (~8 KB of straight-line code)\n", names[md], f / R,
+               s2 / R);
     }
     return 0;
 }
