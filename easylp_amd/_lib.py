@@ -19,7 +19,7 @@ ELP_PROFILE_EVENTS = 4  # HIP events on every pricing dispatch
 ELP_PROFILE_SAMPLE = 8  # ... on those of every 8th chunk between host polls
 ELP_SCALE_GEOMETRIC, ELP_SCALE_EQUILIBRATE = 4, 64
 ELP_BASIS_AUTO, ELP_BASIS_INVERSE, ELP_BASIS_LU = 0, 1, 2
-ABI_VERSION = 6
+ABI_VERSION = 7
 ELP_SIMPLEX_PRIMAL_PRIMAL, ELP_SIMPLEX_DUAL_PRIMAL = 5, 6
 
 # every entry point the header declares (checked by tests/test_abi.py)
@@ -64,6 +64,8 @@ class ElpControl(ctypes.Structure):
         ("mailbox_timeout", ctypes.c_double),
         ("basis", ctypes.c_int32),
         ("simplex", ctypes.c_int32),
+        ("resident", ctypes.c_int32),
+        ("pad_resident", ctypes.c_int32),
     ]
 
 
@@ -95,11 +97,11 @@ class ElpStats(ctypes.Structure):
         ("max_inv_resid", ctypes.c_double),
         ("iter_bytes", ctypes.c_double),
         ("exchange", ctypes.c_int32),
-        ("reserved1", ctypes.c_int32),
+        ("resident", ctypes.c_int32),
         ("seconds_h2d", ctypes.c_double),
         ("h2d_bytes", ctypes.c_double),
-        ("lu_nnz", ctypes.c_int64),
-        ("eta_nnz", ctypes.c_int64),
+        ("resident_launches", ctypes.c_int64),
+        ("resident_ticks", ctypes.c_int64),
         ("basis", ctypes.c_int32),
         ("simplex", ctypes.c_int32),
         ("exchange_rtt_us", ctypes.c_double),

@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libeasylp_hip.so")
-SOURCES = ["elp_api.hip", "elp_kernels.hip", "elp_comm.hip"]
+SOURCES = ["elp_api.hip", "elp_kernels.hip", "elp_comm.hip", "elp_resident.hip"]
 HEADERS = ["elp_internal.h", "elp_comm.h", os.path.join("..", "..", "include", "easylp_hip.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",

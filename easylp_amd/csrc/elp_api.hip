@@ -141,6 +141,8 @@ struct elp_handle {
     int64_t kcap = 0;  // bump capacity: AS m x kcap, Minv / MinvT kcap x kcap (grown at polls)
 
     bool dual_used = false;  // the last load's phase 1 is the dual simplex (phase 3)
+    elp::ResOut* d_resout = nullptr;  // the resident solver's exit record
+    size_t res_lds_max = 0;           // LDS one workgroup may allocate (0: not queried yet)
     std::vector<double> mip_x;   // branch and bound: the incumbent (elp_get_solution)
 };
 
@@ -1812,6 +1814,80 @@ static void pdbg_dump(elp_handle* h, const DevCtl* c) {
 }
 #endif
 
+// The resident small-LP solver (elp_resident.hip): one GPU, no
+// column shards, and the LP's whole state within the LDS one workgroup may
+// allocate.  Returns the dynamic LDS bytes, 0 when not eligible.
+static size_t resident_fit(elp_handle* h) {
+    static const int env = [] {
+        const char* e = std::getenv("ELP_RESIDENT");  // test hook: 0 never, 1 when it fits
+        return e ? std::atoi(e) : -1;
+    }();
+    const int mode = env >= 0 ? (env == 0 ? 2 : 1) : h->ctl.resident;
+    if (mode == 2 || h->comm.kind != 0 || h->d.sharded || h->m < 1 || h->nloc < 1 || h->nloc != h->n) return 0;
+    if (h->res_lds_max == 0) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeSharedMemPerBlockOptin, h->dev) != hipSuccess || v <= 0) {
+            (void)hipGetLastError();
+            v = 65536;
+        }
+        h->res_lds_max = std::min<size_t>((size_t)v, (size_t)160 * 1024);
+    }
+    const size_t b = resident_lds_bytes((int)h->m, (int)h->n);
+    return b <= h->res_lds_max ? b : 0;
+}
+
+// One launch runs the loop to its end: optimal, infeasible, unbounded, a
+// limit, or the elp_iterate budget (phase changes and refactors inside).
+// Returns 1 when the pipeline must run instead (a plan still pending).
+static int run_resident(elp_handle* h, size_t lds, int32_t* lp_status, double t_loop0) {
+    DevCtl* c = h->hctl;
+    if (c->plan_seq != c->applied_seq || c->copy_seq != c->plan_seq) return 1;
+    int rc = ensure_ar(h, h->m);
+    if (rc) return rc;
+    rc = ensure_k(h, std::min(h->m, h->n));
+    if (rc) return rc;
+    if (!h->d_resout) HIPCHK(hipMalloc((void**)&h->d_resout, sizeof(ResOut)));
+    ResArgs a{};
+    a.phase = h->phase;
+    a.price_rule = h->ctl.pricing;
+    a.refactor_mode = h->ctl.refactor_mode;
+    a.tick_budget = 0;
+    if (h->ctl.time_limit > 0) {
+        const double left = h->ctl.time_limit - (now_s() - h->t_solve_start);
+        a.tick_budget = std::max<int64_t>(1, (int64_t)(left * 1e8));
+    }
+    a.out = h->d_resout;
+    HIPCHK(launch_resident(h->d, a, lds, h->st));
+    ResOut o{};
+    HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipMemcpyAsync(&o, h->d_resout, sizeof(ResOut), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    h->stats.host_polls++;
+    h->stats.refactors += o.refactors;
+    h->stats.gj_refactors += o.gj_refactors;
+    if (h->ctl.refactor_mode == 0 && o.emax_max > h->stats.max_inv_resid) h->stats.max_inv_resid = o.emax_max;
+    h->stats.resident = 1;
+    h->stats.resident_launches++;
+    h->stats.resident_ticks += o.ticks;
+    h->phase = o.phase;
+    const int32_t s = c->status;
+    h->stats.seconds_loop += now_s() - t_loop0;
+    if (s == ST_STOP) {
+        c->status = ST_RUN;
+        *lp_status = ELP_SUBOPTIMAL;
+        return push_ctl_fields(h);
+    }
+    h->done = true;
+    if (s == ST_PHASE_OPT) h->final_status = h->phase == 1 ? ELP_INFEASIBLE : ELP_OPTIMAL;
+    else if (s == ST_UNBOUNDED) h->final_status = ELP_UNBOUNDED;
+    else if (s == ST_DUALINF) h->final_status = ELP_INFEASIBLE;
+    else if (s == ST_ITERCAP) h->final_status = ELP_SUBOPTIMAL;
+    else if (s == ST_TIMEOUT) h->final_status = ELP_TIMEOUT;
+    else h->final_status = ELP_NUMFAILURE;
+    *lp_status = h->final_status;
+    return 0;
+}
+
 // the polling loop; budget = iterations allowed in this call
 static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
     if (h->done) {
@@ -1832,6 +1908,11 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
     c->phase = h->phase;
     int rc = push_ctl_fields(h);
     if (rc) return rc;
+    if (const size_t lds = resident_fit(h)) {
+        rc = run_resident(h, lds, lp_status, t_loop0);
+        if (rc != 1) return rc;
+    }
+    h->stats.resident = 0;
     const int period = h->ctl.refactor_period;
     // ELP_PROFILE_EVENTS: events on the pricing dispatches of every chunk;
     // ELP_PROFILE_SAMPLE: of every 8th chunk only (a uniform sample of the solve
@@ -2893,6 +2974,7 @@ extern "C" void elp_destroy(elp_handle* h) {
                 h->dbg_wait, (long long)h->stats.host_polls);
     free_dev(h);
     release_kept(h);
+    if (h->d_resout) (void)hipFree(h->d_resout);
     if (h->d_dev) (void)hipFree(h->d_dev);
     if (h->h_dev) (void)hipHostFree(h->h_dev);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);

@@ -34,6 +34,7 @@ enum : int32_t {
     ST_STOP = 7,       // elp_iterate budget reached at loop top
     ST_COMMFAIL = 8,   // xGMI mailbox: a peer's record did not arrive in time
     ST_DUALINF = 9,    // dual simplex: no entering candidate for the leaving row (primal infeasible)
+    ST_TIMEOUT = 10,   // resident solver: elp_control.time_limit reached at a loop top
 };
 
 // pivot cases (oracle/elp_oracle.c "case A".."case E")
@@ -435,5 +436,23 @@ hipError_t launch_dual_iteration_finish(const Dev& d, int k_ub, hipStream_t st);
 // scaled), real costs, y, and every nonbasic column re-placed for the node
 // (k, ny: the kept basis's bump dimension and |Y|); the host then refactors
 hipError_t launch_warm_start(const Dev& d, const double* lo, const double* up, int k, int ny, hipStream_t st);
+
+// resident small-LP solver (elp_resident.hip): the whole simplex loop of an LP
+// whose state fits in LDS, one wave, one launch.  phase: the host's h->phase
+// (1 primal phase 1, 2 primal phase 2, 3 dual phase 1); price_rule: 1 Devex,
+// 0 Dantzig (for the phase-2 start); tick_budget: s_memrealtime ticks (100 MHz)
+// the launch may run before it stops with ST_TIMEOUT (0: no limit)
+struct ResOut {
+    int64_t refactors, gj_refactors, devex_resets, ticks;
+    double emax_max;
+    int32_t phase, pad;
+};
+struct ResArgs {
+    int32_t phase, price_rule, refactor_mode, pad;
+    int64_t tick_budget;
+    ResOut* out;
+};
+size_t resident_lds_bytes(int m, int n);
+hipError_t launch_resident(const Dev& d, const ResArgs& a, size_t lds, hipStream_t st);
 
 }  // namespace elp

@@ -25,9 +25,10 @@
 extern "C" {
 #endif
 
-#define ELP_ABI_VERSION 6  /* 6: elp_stats.price_seconds_stamps / price_stamped_launches; 3: elp_stats.iter_bytes appended; 4: elp_control.exchange /
+#define ELP_ABI_VERSION 7  /* 7: elp_control.resident, elp_stats.resident / resident_launches /
+                             resident_ticks (were reserved / lu_nnz / eta_nnz); 6: elp_stats.price_seconds_stamps / price_stamped_launches; 3: elp_stats.iter_bytes appended; 4: elp_control.exchange /
                              basis, elp_load_dense_device_multi, elp_stats.exchange /
-                             h2d_bytes / lu_nnz / eta_nnz / basis; 5: elp_control.simplex,
+                             h2d_bytes / basis; 5: elp_control.simplex,
                              elp_stats.exchange_rtt_us / dual_iterations / simplex */
 
 /* row directions, mirroring R/class.R:272 ("==" -> "=") and the "<"/">"
@@ -129,6 +130,15 @@ typedef struct elp_control {
                                 GPU, or column-sharded ranks holding all of A,
                                 with the bump inverse), else PRIMAL_PRIMAL;
                                 elp_stats.simplex reports what ran */
+    int32_t resident;        /* the resident small-LP solver: the
+                                whole simplex loop of an LP whose state fits in
+                                one CU's LDS in ONE launch of one wave instead
+                                of 4-7 launches per pivot.  0 (default): when it
+                                fits (one GPU, no column shards); 1: the same
+                                (force: the tests); 2: never (the multi-workgroup
+                                pipeline).  Same pivots, same bits either way;
+                                elp_stats.resident reports what ran */
+    int32_t pad_resident;
 } elp_control;
 
 #define ELP_SIMPLEX_PRIMAL_PRIMAL 5  /* elp_control.simplex (lp_solve's SIMPLEX_*) */
@@ -180,12 +190,12 @@ typedef struct elp_stats {
                                   (select, FTRAN-z, ratio test, update)         */
     int32_t exchange;          /* min-loc transport of the last load: 0 none
                                   (one rank), 1 peer mailbox, 2 collective      */
-    int32_t reserved1;
+    int32_t resident;          /* 1: the last solve ran in the resident solver */
     double seconds_h2d;        /* elp_load_dense: host -> device copy of A     */
     double h2d_bytes;          /* bytes of A read from host memory (once, also
                                   when several devices receive them)            */
-    int64_t lu_nnz;            /* reserved (0; the removed sparse-LU engine)   */
-    int64_t eta_nnz;           /* reserved (0)                                 */
+    int64_t resident_launches; /* resident-solver launches of the last solve     */
+    int64_t resident_ticks;    /* their device time (s_memrealtime, 100 MHz)   */
     int32_t basis;             /* the representation the last load used
                                   (ELP_BASIS_INVERSE)                           */
     int32_t simplex;           /* the phase-1 method the last solve ran

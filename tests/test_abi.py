@@ -43,11 +43,12 @@ def test_abi_version_and_defaults():
     from easylp_amd._lib import ABI_VERSION, ElpControl, load
     _torch_first()
     lib = load()
-    assert lib.elp_abi_version() == ABI_VERSION == 6
+    assert lib.elp_abi_version() == ABI_VERSION == 7
     c = ElpControl()
     lib.elp_default_control(ctypes.byref(c))
     assert c.infinity == 1e30 and c.refactor_period == 250 and c.sync_every == 32
     assert c.tol_singular == 1e-13 and c.mailbox_timeout == 2.0 and c.ngpu == 1
+    assert c.resident == 0  # (auto: the resident solver when the LP fits in LDS)
 
 
 def _c_layout(struct, fields, tmp_path):

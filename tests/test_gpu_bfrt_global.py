@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 @pytest.mark.parametrize("mode", ["1", "0"])
 def test_dual_parity_with_global_bfrt(mode):
-    env = dict(os.environ, ELP_BFRT_REG=mode)
+    env = dict(os.environ, ELP_RESIDENT="0", ELP_BFRT_REG=mode)
     cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", "-m", "gpu",
            os.path.join(HERE, "test_gpu_dual.py"),
            os.path.join(HERE, "test_gpu_ngpu.py") + "::test_ngpu_dual_matches_oracle",

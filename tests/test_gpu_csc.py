@@ -134,3 +134,42 @@ def test_mps_file_through_csc(gpu, tmp_path):
     assert g.objval == o.objval
     np.testing.assert_array_equal(g.basis, o.basis)
     assert read_mps(str(f)).objective_constant == 3.5
+
+
+def _empty_tail_lp(seed, rows_ge):
+    """An LP whose last pricing tile (columns 256..299 of 300, TILE_COLS = 128)
+    holds only empty columns: that tile's extent is [nnz, nnz), so the staged
+    CSC pricing must not read rind / cval at nnz (the r05q fault: an
+    out-of-bounds read at s0 == nnz, elp_kernels.hip price_csc_body)."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(seed)
+    m, n, nfull = 40, 300, 256
+    rows, cols, vals = [], [], []
+    for j in range(nfull):
+        for i in rng.choice(m, 3, replace=False):
+            rows.append(int(i))
+            cols.append(j)
+            vals.append(float(rng.uniform(0.5, 2.0)))
+    A = sp.csc_matrix((vals, (rows, cols)), shape=(m, n))
+    assert A.indptr[nfull] == A.indptr[n] == A.nnz
+    dirs = np.ones(m, np.int32)
+    rhs = rng.uniform(5.0, 10.0, m)
+    if rows_ge:  # rows the slack basis violates: the dual phase (k_dual_price_csc)
+        dirs[:rows_ge] = 2
+        rhs[:rows_ge] = rng.uniform(1.0, 2.0, rows_ge)
+    obj = rng.uniform(0.1, 1.0, n)
+    lo = np.zeros(n)
+    up = np.full(n, 4.0)  # boxed: the empty columns go to their upper bound
+    return A, dirs, rhs, obj, lo, up
+
+
+@pytest.mark.parametrize("rows_ge", [0, 6], ids=["primal", "dual"])
+def test_empty_last_tile(gpu, rows_ge):
+    from oracle import solve_dense as orc
+    A, dirs, rhs, obj, lo, up = _empty_tail_lp(5, rows_ge)
+    g = gpu.solve_sparse(A, dirs, rhs, obj, lo, up, True, trace=100000, basis=1, resident=2)
+    o = orc(A.toarray(), dirs, rhs, obj, lo, up, True, trace_cap=100000, price_mode=1)
+    assert g.status == o.status == 0
+    _same(g, o)
+    assert feasible(A.toarray(), dirs, rhs, g.x, lo, up)
+    assert np.all(g.x[256:] == 4.0)

@@ -27,7 +27,7 @@ def test_csc_parity_with_sparse_ftran(spz, defer, minvt, sru):
     minvt 1: the CSC load keeps the transposed inverse, ELP_CSC_MINVT=1; sru 0: the
     dense inverse update instead of the sparse one, ELP_SRU=0 -- the default CSC runs
     of every suite take the sparse one, and both keep the oracle's zero rule)"""
-    env = dict(os.environ, ELP_SPF_MIN="1", ELP_SPZ_MIN_MB=spz, ELP_DUAL_DEFER=defer, ELP_CSC_MINVT=minvt, ELP_SRU=sru)
+    env = dict(os.environ, ELP_RESIDENT="0", ELP_SPF_MIN="1", ELP_SPZ_MIN_MB=spz, ELP_DUAL_DEFER=defer, ELP_CSC_MINVT=minvt, ELP_SRU=sru)
     cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", "-m", "gpu",
            os.path.join(HERE, "test_gpu_csc.py"),
            os.path.join(HERE, "test_gpu_dual.py") + "::test_dual_known_and_robust",

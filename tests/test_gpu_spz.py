@@ -19,7 +19,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def test_csc_parity_with_rowwise_ftran():
-    env = dict(os.environ, ELP_SPZ_MIN_MB="0")
+    env = dict(os.environ, ELP_RESIDENT="0", ELP_SPZ_MIN_MB="0")
     cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", "-m", "gpu",
            os.path.join(HERE, "test_gpu_csc.py"),
            os.path.join(HERE, "test_gpu_dual.py") + "::test_dual_known_and_robust",
