@@ -78,6 +78,8 @@ def parse():
                     help="N=1: run the sharded pipeline on a 1-rank RCCL communicator (overhead probe)")
     ap.add_argument("--sparse", type=int, default=1,
                     help="also time the CSC path on a sparse LP (BASELINE config 5)")
+    ap.add_argument("--small", type=int, default=1,
+                    help="the reference-sized LPs / MIPs: resident solver, pipeline and CPU oracle times")
     ap.add_argument("--c2", type=int, default=1,
                     help="N=1: also BASELINE configs[1] (500 x 2000) to optimality from host memory")
     ap.add_argument("--sparse-m", type=int, default=1000)
@@ -530,6 +532,78 @@ def c2_config(args, local, reps=5):
             "runs": [r["time_to_optimal_s"] for r in runs]}
 
 
+def small_lps(args, local, with_cpu, reps=5):
+    """The models EasyLP's R front-end builds: the reference's
+    DOP LP (tests/testthat/test-DOP.R:27-54), Klee-Minty n = 12 and 14
+    (BASELINE configs[4]'s degenerate case, unscaled, Dantzig: 2^n - 1 pivots)
+    and the MIP tests (test-students.R, test-investments.R), through the C ABI
+    from host memory (load + solve, what one easylp$solve() call pays), best of
+    `reps`: the resident solver (one launch, elp_resident.hip) and the
+    multi-workgroup pipeline (resident = 2) beside the oracle on one host core
+    (the same arithmetic; lp_solve itself is absent)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from conftest import load_known_answers, load_mip_known_answers
+    from make_sparse import klee_minty
+    from easylp_amd import Problem
+
+    def gpu_time(m, n, load, is_int=None, **ctl):
+        best, st, stats = None, None, None
+        for r in range(reps + 1):
+            with Problem(m, n, device=local, **ctl) as p:
+                t0 = time.perf_counter()
+                load(p)
+                if is_int is not None:
+                    p.set_int(is_int)
+                st = p.solve()
+                el = time.perf_counter() - t0
+                stats = p.stats()
+                obj = p.solution(st).objval
+            if r and (best is None or el < best):
+                best = el
+        return {"seconds": best, "status": st, "objective": obj, "iterations": stats["iterations"],
+                "resident": stats["resident"], "load_s": stats["seconds_load"],
+                "kernel_us": stats["resident_ticks"] / 100.0 if stats["resident"] else None,
+                "mip_nodes": stats["mip_nodes"] if is_int is not None else None}
+
+    cases = []
+    dop = next(r for r in load_known_answers() if r["name"] == "dop")
+    cases.append(("dop", "test-DOP.R:27-54 LP (%d x %d), default controls" % dop["A"].shape, dop, {}, {}, None))
+    for nk in (12, 14):
+        A, dirs, rhs, obj, lo, up, mx = klee_minty(nk)
+        rec = {"A": A.toarray(), "dir": dirs, "rhs": rhs, "obj": obj, "lo": lo, "up": up, "maximize": mx}
+        cases.append(("klee_minty_%d" % nk, "Klee-Minty cube n = %d, unscaled, Dantzig (%d pivots)" % (nk, 2 ** nk - 1),
+                      rec, {"pricing": 0, "scaling": 0}, {"price_rule": 0, "scaling": 0}, None))
+    for r in load_mip_known_answers():
+        if r["name"] in ("students", "investments"):
+            cases.append(("mip_" + r["name"], "test-%s.R MIP (%d x %d, %d integer columns)" % (
+                r["name"], r["m"], r["n"], int(r["is_int"].sum())), r, {}, {}, r["is_int"]))
+    out = {}
+    for name, what, rec, gctl, octl, is_int in cases:
+        m, n = rec["A"].shape
+        args_lp = (rec["A"], rec["dir"], rec["rhs"], rec["obj"], rec["lo"], rec["up"], rec["maximize"])
+        load = (lambda p, a=args_lp: p.load_dense(*a))
+        blk = {"workload": what,
+               "resident": gpu_time(m, n, load, is_int, resident=0, **gctl),
+               "pipeline": gpu_time(m, n, load, is_int, resident=2, **gctl)}
+        if with_cpu:
+            from oracle import solve_dense as orc, solve_mip
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                if is_int is None:
+                    o = orc(*args_lp, **octl)
+                else:
+                    o = solve_mip(*args_lp, is_int, **octl)
+                ts.append(time.perf_counter() - t0)
+            blk["cpu_oracle"] = {"seconds": min(ts), "status": o.status, "objective": o.objval, "cores": 1}
+            g = blk["resident"]["seconds"]
+            blk["gpu_over_cpu_time"] = g / min(ts) if g else None
+        out[name] = blk
+    return out
+
+
 def sparse_rate(args, local, with_cpu):
     """BASELINE config 5 on the CSC path (basis AUTO = the explicit bump
     inverse with k-sized buffers):
@@ -792,6 +866,7 @@ def main():
         sparse = sparse_rate(args, local, rank == 0 and not args.no_cpu)
 
     c2 = c2_config(args, local) if args.c2 and max(world, ctx.ngpu) == 1 else None
+    small = small_lps(args, local, rank == 0 and not args.no_cpu) if args.small and max(world, ctx.ngpu) == 1 else None
 
     highs_res = highs.result(timeout=400) if highs is not None else None
     # GPU / CPU on the same LPs (> 1: the GPU is faster)
@@ -862,6 +937,7 @@ def main():
             "scaling_config": c4,
             "c2": c2,
             "sparse_config": sparse,
+            "small_lps": small,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

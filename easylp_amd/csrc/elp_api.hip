@@ -66,8 +66,6 @@ struct elp_handle {
     // tens of GB right after a hipFree of the same size measured 0.4-3.7 s)
     double* keep_A = nullptr;
     size_t keep_A_bytes = 0, A_owned_bytes = 0;
-    double* keep_AT = nullptr;
-    size_t keep_AT_bytes = 0, AT_bytes = 0;
     size_t w_cap = 0;
     bool loaded = false, done = false;
     int maximize = 0;
@@ -126,18 +124,9 @@ struct elp_handle {
     // back instead of ~80 hipFree + hipMalloc pairs (1.8 ms at 5000 x 50000)
     std::unordered_map<void*, size_t> asize;
     std::multimap<size_t, void*> pool;
-    // device copy of Dev for the per-iteration kernels (Dev::self) and its
-    // pinned staging copy, which also remembers what was last uploaded
-    Dev* d_dev = nullptr;
-    Dev* h_dev = nullptr;
-    bool dev_uploaded = false;
     // scaling (elp_control.scaling): the solver works on A~ = 2^srow A 2^scol
     // (exponents per row and per GLOBAL column; empty: unscaled)
     std::vector<int32_t> srow_h, scol_h;
-    // sparse-LU engine (elp_control.basis, CSC input): host copy of the scaled
-    // CSC (the refactor builds B from it), artificial signs, the last factors,
-    // the device descriptor and its buffers (grown as needed within a load, freed by
-    // every load: free_dev)
     int64_t kcap = 0;  // bump capacity: AS m x kcap, Minv / MinvT kcap x kcap (grown at polls)
 
     bool dual_used = false;  // the last load's phase 1 is the dual simplex (phase 3)
@@ -175,9 +164,8 @@ extern "C" int32_t elp_abi_version(void) { return ELP_ABI_VERSION; }
 
 static void release_kept(elp_handle* h) {
     if (h->keep_A) (void)hipFree(h->keep_A);
-    if (h->keep_AT) (void)hipFree(h->keep_AT);
-    h->keep_A = h->keep_AT = nullptr;
-    h->keep_A_bytes = h->keep_AT_bytes = 0;
+    h->keep_A = nullptr;
+    h->keep_A_bytes = 0;
 }
 
 static void drain_pool(elp_handle* h) {
@@ -185,18 +173,15 @@ static void drain_pool(elp_handle* h) {
     h->pool.clear();
 }
 
-// keep_big: a reload -- A's copy and A^T stay allocated for the next load, the
-// other buffers go to the handle's pool (dalloc inside alloc_all takes them back)
+// keep_big: a reload -- A's copy stays allocated for the next load, the other
+// buffers go to the handle's pool (dalloc inside alloc_all takes them back)
 static void free_dev(elp_handle* h, bool keep_big = false) {
     Dev& d = h->d;
     if (keep_big) {
         release_kept(h);
         h->keep_A = h->A_owned;
         h->keep_A_bytes = h->A_owned ? h->A_owned_bytes : 0;
-        h->keep_AT = d.AT;
-        h->keep_AT_bytes = d.AT ? h->AT_bytes : 0;
         h->A_owned = nullptr;
-        d.AT = nullptr;
     }
     auto release = [&](void* p) {
         const auto it = h->asize.find(p);
@@ -209,7 +194,7 @@ static void free_dev(elp_handle* h, bool keep_big = false) {
                     d.t,        d.acol, d.aR,   d.alS,   d.alU,  d.zz,    d.zpart, d.vrow,
                     d.vvec,     d.colA, d.rhs,  d.vstat, d.cover, d.rpos, d.Rl,    d.Sl,
                     d.Yl,  d.ypos,  d.perm,  d.pivstep, d.nzlist, d.nzcount, d.nzchunk,
-                    d.cand,     d.pstamp, d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand, d.rcnt, d.AT,
+                    d.cand,     d.pstamp, d.ctl, d.trace, d.MinvT, d.yy, d.blockmin, d.rcand, d.rcnt,
                     d.pkt, d.objg, d.ract, d.cand_xchg, h->d_flag, d.cS, d.slo, d.shi, d.rlo, d.rhi,
                     (void*)d.cptr, (void*)d.rind, (void*)d.cval, (void*)d.rptr, (void*)d.cind,
                     (void*)d.rval, d.qcol, d.qz, d.spos, d.dstamp, d.rowvs, d.yvs, d.dw, d.dprev, (void*)d.srow,
@@ -232,30 +217,6 @@ static void free_dev(elp_handle* h, bool keep_big = false) {
         (void)hipHostFree(h->hctl);
         h->hctl = nullptr;
     }
-}
-
-// Dev::self: upload h->d when it changed since the last upload (loads and
-// growths change it; a chunk usually finds it as it was)
-static int upload_dev(elp_handle* h) {
-    if (!h->d_dev) {
-        if (hipMalloc((void**)&h->d_dev, sizeof(Dev)) != hipSuccess) {
-            h->d_dev = nullptr;
-            return fail(ELP_E_NOMEM, "device Dev allocation failed");
-        }
-        if (hipHostMalloc((void**)&h->h_dev, sizeof(Dev), hipHostMallocDefault) != hipSuccess) {
-            h->h_dev = nullptr;
-            return fail(ELP_E_NOMEM, "pinned Dev allocation failed");
-        }
-        h->dev_uploaded = false;
-    }
-    h->d.self = h->d_dev;
-    if (h->dev_uploaded && std::memcmp(h->h_dev, &h->d, sizeof(Dev)) == 0) return 0;
-    // the staging copy may still feed the previous upload: let it land first
-    HIPCHK(hipStreamSynchronize(h->st));
-    std::memcpy((void*)h->h_dev, (const void*)&h->d, sizeof(Dev));
-    HIPCHK(hipMemcpyAsync(h->d_dev, h->h_dev, sizeof(Dev), hipMemcpyHostToDevice, h->st));
-    h->dev_uploaded = true;
-    return 0;
 }
 
 // a buffer a growth replaced (see elp_handle::retired)
@@ -406,8 +367,6 @@ static void destroy_group(elp_handle* g) {
 static void enable_group_p2p(elp_handle* g) {
     const int P = (int)g->ranks.size();
     if (P > 64 || g->ctl.exchange == 1) return;
-    if (const char* e = std::getenv("ELP_NGPU_MAILBOX"))
-        if (std::atoi(e) == 0) return;
     const size_t rec = sizeof(MboxRec), bytes = 2 * (size_t)P * rec;
     std::vector<void*> mb(P, nullptr);
     std::vector<void**> dp(P, nullptr);
@@ -591,24 +550,12 @@ static int alloc_all_body(elp_handle* h) {
     if (const char* e = std::getenv("ELP_KCAP_INIT"))  // test hook: force growth
         h->kcap = std::max<int64_t>(1, std::min<int64_t>(mm, std::atoll(e)));
     d.ldm = h->kcap;
-    // pricing tiles (price_body): TILE_COLS columns.  ELP_TILE_BAL=1 (A/B
-    // switch): once there are 256+ tiles, as many as the next multiple of
-    // 2 x 256 (two resident per CU), narrower, so every CU sweeps the same
-    // share -- measured slower at 5000 x 50000 (21.6 vs 19.9 us per launch,
-    // r03: idle lanes and more row loads cost more than the imbalance)
-    {
-        const int64_t t0 = (n + TILE_COLS - 1) / TILE_COLS;
-        int64_t tw = TILE_COLS;
-        const char* bal = std::getenv("ELP_TILE_BAL");
-        if (!h->csc && t0 >= 256 && bal && std::atoi(bal) == 1) {
-            const int64_t t1 = (t0 + 511) / 512 * 512;
-            tw = 2 * ((n + 2 * t1 - 1) / (2 * t1));
-        }
-        if (const char* e = std::getenv("ELP_TILE_W"))  // A/B switch
-            if (!h->csc) tw = std::max<int64_t>(2, std::min<int64_t>(TILE_COLS, std::atoll(e) & ~1ll));
-        d.tile_w = (int32_t)tw;
-        d.ntiles = (int32_t)std::max<int64_t>(1, (n + tw - 1) / tw);
-    }
+    // pricing tiles (price_body): TILE_COLS columns each.  (r03 tried balanced
+    // narrower tiles once there are 256+ -- every CU sweeping the same share:
+    // slower at 5000 x 50000, 21.6 vs 19.9 us per launch, idle lanes and more
+    // row loads cost more than the imbalance; removed in r06)
+    d.tile_w = TILE_COLS;
+    d.ntiles = (int32_t)std::max<int64_t>(1, (n + TILE_COLS - 1) / TILE_COLS);
     d.ldr = (int64_t)d.ntiles * d.tile_w;  // AR: [tile][row][tile_w], rows packed
     d.infinity = h->ctl.infinity;
     d.tol_singular = h->ctl.tol_singular;
@@ -665,7 +612,7 @@ static int alloc_all_body(elp_handle* h) {
     if (h->csc) h->ar_rows = 1;  // CSC prices from the columns: no AR
     d.arcap = h->ar_rows;
     A(dalloc(&d.AR, (size_t)h->ar_rows * (size_t)d.ldr));
-    // the explicit bump inverse's m x m buffers (none with the sparse LU)
+    // the explicit bump inverse's buffers (kcap positions, grown by ensure_k)
     const size_t msq = (size_t)h->kcap * (size_t)h->kcap;
     A(dalloc(&d.AS, (size_t)mm * (size_t)h->kcap));
     A(dalloc(&d.Minv, msq));
@@ -736,7 +683,7 @@ static int alloc_all_body(elp_handle* h) {
 #endif
     if (h->csc) A(dalloc(&d.qcol, mm));
     if (h->csc) A(dalloc(&d.spos, (size_t)(n > 0 ? n : 1)));  // (the sparse FTRAN-z's column -> position)
-    if (!h->csc && !std::getenv("ELP_NO_QZ")) A(dalloc(&d.qz, mm));  // (dense only; ELP_NO_QZ: A/B switch)
+    if (!h->csc) A(dalloc(&d.qz, mm));  // (dense only)
     if (ELP_DIAG && std::getenv("ELP_STAMPS")) {  // (diagnostic builds)
         A(dalloc(&d.dstamp, DSTAMP_STRIDE * 64));
         d.stamp_wide = std::atoi(std::getenv("ELP_STAMPS")) >= 2;
@@ -1077,9 +1024,8 @@ static void scale_csc(elp_handle* h, const int64_t* cp, const int32_t* ri, doubl
 }
 
 // the phase-1 method (elp_control.simplex; lp_solve's set_simplextype): the
-// dual simplex with the bump inverse, on one GPU or column-sharded; the
-// sparse-LU engine keeps the primal phase 1 on artificials (elp_stats.simplex
-// reports what ran)
+// dual simplex with the bump inverse, on one GPU or column-sharded
+// (elp_stats.simplex reports what ran)
 static int simplex_type(const elp_handle* h) {
     return h->ctl.simplex == 0 ? ELP_SIMPLEX_DEFAULT : h->ctl.simplex;
 }
@@ -1175,37 +1121,10 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
         if (rc) return rc;
     }
     load_mark(h, "cols / rows / Y");
-    // dense A: a row-major copy for the AR row copies (contiguous reads); without
-    // the memory for it they read A's rows in place
-    // (only while the AR rows could still grow to a full copy of A beside it)
-    size_t mem_free = 0, mem_total = 0;
-    const size_t at_bytes = (size_t)m * (size_t)nl * sizeof(double);
-    if (!d.csc && d.A && !d.AT && at_bytes > 0 && h->keep_AT && h->keep_AT_bytes == at_bytes) {
-        d.AT = h->keep_AT;  // a reload of the same shape
-        h->keep_AT = nullptr;
-        h->keep_AT_bytes = 0;
-    }
-    if (h->keep_AT) {
-        (void)hipFree(h->keep_AT);
-        h->keep_AT = nullptr;
-        h->keep_AT_bytes = 0;
-    }
-    // the row-major copy for AR row appends: off unless ELP_USE_AT=1 -- r02 measured no
-    // difference with and without it (C3 and C4), and it doubles A's footprint (40 GB at
-    // C4, whose allocation alone took 0.4-3.7 s on some loads)
-    static const bool no_at = std::getenv("ELP_USE_AT") == nullptr;
-    if (!no_at && !d.csc && d.A && !d.AT && at_bytes > 0 && hipMemGetInfo(&mem_free, &mem_total) == hipSuccess &&
-        mem_free > 2 * at_bytes + ((size_t)1 << 30)) {
-        if (hipMalloc((void**)&d.AT, at_bytes) != hipSuccess) {
-            d.AT = nullptr;
-            (void)hipGetLastError();
-        }
-    }
-    h->AT_bytes = d.AT ? at_bytes : 0;
+    // (r01-r05 kept an opt-in row-major copy of A for the AR row copies; with
+    // and without it C3 and C4 measured the same and it doubled A's footprint:
+    // removed in r06 -- the copies read A's rows in place)
     release_kept(h);  // whatever this load did not take
-    load_mark(h, "A^T alloc");
-    if (d.AT) HIPCHK(launch_transpose_A(d, h->st));
-    load_mark(h, d.AT ? "A^T copy" : "A^T (none)");
     HIPCHK(launch_fill_AR(h->d, h->st));
     (void)hipFree(dlo);
     (void)hipFree(dup);
@@ -1973,7 +1892,6 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
             HIPCHK(hipMemcpyAsync(h->d.dstamp, init.data(), init.size() * 8, hipMemcpyHostToDevice, h->st));
             HIPCHK(hipStreamSynchronize(h->st));
         }
-        if (ELP_DEV_PTR && (rc = upload_dev(h))) return rc;  // (Dev::self for this chunk's launches)
         const double t_enq0 = now_s();
         const bool prof_chunk = prof && (prof_all || h->prof_chunks++ % 8 == 0);
         // (the device-clock timer of the same launches: ticks before the chunk)
@@ -2975,8 +2893,6 @@ extern "C" void elp_destroy(elp_handle* h) {
     free_dev(h);
     release_kept(h);
     if (h->d_resout) (void)hipFree(h->d_resout);
-    if (h->d_dev) (void)hipFree(h->d_dev);
-    if (h->h_dev) (void)hipHostFree(h->h_dev);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     h->comm.destroy();
     if (h->st) (void)hipStreamDestroy(h->st);

@@ -11,10 +11,6 @@
 #ifndef ELP_DIAG
 #define ELP_DIAG 0
 #endif
-// Dev by pointer for the per-iteration kernels (A/B switch, see elp_kernels.hip)
-#ifndef ELP_DEV_PTR
-#define ELP_DEV_PTR 0
-#endif
 
 namespace elp {
 
@@ -204,7 +200,6 @@ struct Dev {
     int32_t tile_w, ntiles;  // pricing tiles: tile_w (even, <= TILE_COLS) columns each
     int64_t arcap; // AR rows per column tile (capacity)
     const double* A;  // column-major m x n (this shard's columns)
-    double* AT;       // its row-major copy (m x n, ld n): AR row copies read it contiguously
     const double* Afull;  // sharded + replicated: all N columns (A = Afull + col0*m);
                           // null: the entering column comes in the exchanged pkt
     double* AR;       // Y rows, tile-major: [ntiles][arcap rows][tile_w cols]
@@ -257,11 +252,6 @@ struct Dev {
     // the peer mailbox, and P - 1 ranks' spinning grids must leave the device
     // room for the last rank's pricing launch (else it never starts)
     int32_t sel_cap, sel_pad;
-    // device copy of this struct (elp_api upload_dev, refreshed at every chunk
-    // when it changed): the four per-iteration kernels take it by pointer
-    // (ELP_DEV_PTR) so their prologues read it through the scalar cache / L2
-    // instead of ~800 B of fresh kernel arguments per launch
-    const Dev* self;
     int64_t nnz;
     const int64_t* cptr;
     const int32_t* rind;
@@ -386,7 +376,6 @@ hipError_t launch_refactor_gj(const Dev& d, int k, hipStream_t st);
 hipError_t launch_btran_exact(const Dev& d, int k, hipStream_t st);  // phase-2 duals
 hipError_t launch_refactor_primal(const Dev& d, int k, hipStream_t st);  // needs ract
 hipError_t launch_nzlist(const Dev& d, hipStream_t st);
-hipError_t launch_transpose_A(const Dev& d, hipStream_t st);
 // scaling (elp_control.scaling): exponents rho (m rows), gamma (ncols columns);
 // rmn / rmx: per-row work (m each: max of -e, max of e; rmx must follow rmn in
 // one 2m buffer so shards combine them with one all-reduce max); changed: set

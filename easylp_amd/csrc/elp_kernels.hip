@@ -22,21 +22,12 @@
 
 #include <type_traits>
 
-// The per-iteration kernels read Dev by value from the kernel arguments or,
-// with ELP_DEV_PTR 1, through a pointer to its device copy (Dev::self).  The
-// pointer form measured slower (r03: 38.3-38.9 against 36.8-37.3 us per C3
-// iteration): pointers loaded from memory lose their global address space,
-// so the control-block reads became flat loads that wait for every load in
-// flight; kernel-argument pointers stay global.
-#if ELP_DEV_PTR
-#define DEV_PARAM const Dev* __restrict__ dp_
-#define DEV_BIND const Dev& d = *dp_;
-#define DEV_ARG(x) ((x).self)
-#else
-#define DEV_PARAM Dev d
-#define DEV_BIND
-#define DEV_ARG(x) (x)
-#endif
+// The per-iteration kernels take Dev by value from the kernel arguments.  A
+// pointer to a device copy (r03) measured slower -- 38.3-38.9 against
+// 36.8-37.3 us per C3 iteration: pointers loaded from memory lose their global
+// address space, so the control-block reads became flat loads that wait for
+// every load in flight; kernel-argument pointers stay global -- and r06
+// removed it.
 
 namespace elp {
 
@@ -659,27 +650,10 @@ __global__ void __launch_bounds__(1024) k_init_Y(Dev d) {
     }
 }
 
-// a_ij of this shard, read along a row (AR row copies): the row-major copy when
-// there is one (contiguous over j), else the column-major A (one line per element)
+// a_ij of this shard, read along a row (AR row copies): the column-major A,
+// one line per element (r01-r05's opt-in row-major copy measured no faster)
 DEV double a_row(const Dev& d, int64_t i, int64_t j) {
-    return d.AT ? d.AT[(size_t)i * (size_t)d.n + (size_t)j]  // (scaled by k_transpose_A)
-                : sca(d, d.A[(size_t)j * (size_t)d.m + (size_t)i], i, d.col0 + j);
-}
-
-// AT = A^T through 64 x 64 LDS tiles (reads down columns, writes along rows)
-__global__ void __launch_bounds__(256) k_transpose_A(Dev d) {
-    __shared__ double t[64][65];
-    const int64_t j0 = (int64_t)blockIdx.x * 64, i0 = (int64_t)blockIdx.y * 64;
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    for (int r = ty; r < 64; r += 4) {
-        const int64_t j = j0 + r, i = i0 + tx;
-        if (j < d.n && i < d.m) t[r][tx] = sca(d, d.A[(size_t)j * (size_t)d.m + (size_t)i], i, d.col0 + j);
-    }
-    __syncthreads();
-    for (int r = ty; r < 64; r += 4) {
-        const int64_t i = i0 + r, j = j0 + tx;
-        if (i < d.m && j < d.n) d.AT[(size_t)i * (size_t)d.n + (size_t)j] = t[tx][r];
-    }
+    return sca(d, d.A[(size_t)j * (size_t)d.m + (size_t)i], i, d.col0 + j);
 }
 
 // ============================================================== scaling
@@ -1059,9 +1033,6 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
 #ifndef ELP_PRICE_UNR
 #define ELP_PRICE_UNR 16
 #endif
-#ifndef ELP_PRICE_YLANE
-#define ELP_PRICE_YLANE 1  // (0: one uniform y load per row, 16 more vector-memory instructions per block)
-#endif
 // lane l's double, read by every lane (v_readlane pair)
 DEV double lane_bcast(double v, int l) {
     const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
@@ -1074,41 +1045,21 @@ DEV double lane_bcast(double v, int l) {
 // on |Y|, so they go out right behind the control-block loads, before the
 // control block arrives (rows past |Y| are masked when it does), and the sweep
 // overlaps the control-block round trip instead of following it.
-// waves 1..3 of tile `tile` apply their share of the pending deferred plan
-// (whatever the loop status: the next select kernel marks the plan applied)
-DEV void tile_apply(const Dev& d, int64_t tile, int64_t ntiles) {
-    const DevCtl* cc = d.ctl;
-    if (!plan_pending(cc) || cc->status == ST_NUMFAIL) return;
-    const Plan P = cc->plan;
-    const int64_t vt = tile * (PRICE_THREADS - 64) + ((int)threadIdx.x - 64);
-    const int64_t VT = ntiles * (PRICE_THREADS - 64);
-    apply_minv(d, P, vt, VT);
-    apply_copy(d, P, vt, VT, false);
-}
-
-// Grid (r03): [nsw slack workgroups][d.ntiles column tiles of d.tile_w columns]
-// (tile_w = 128, or narrower balanced tiles under ELP_TILE_BAL=1, alloc_all);
-// the slack workgroups go first (their candidates are needed as soon as the
-// tiles'), and the deferred update of the last pivot is applied by waves 1..3
-// of every tile once their sweep is done (phase 2; nothing the sweep reads)
-// instead of by trailing workgroups that started only as tiles retired.
-// napply > 0 (A/B switch ELP_TRAIL_APPLY=1, r02's layout): the plan is applied
-// by napply trailing workgroups instead (apply = 0 then)
-// TW: the tile width at compile time (TILE_COLS, the default layout: every AR
-// row offset a shift) or 0 (ELP_TILE_BAL's balanced tiles: d.tile_w at run time).
-// ELP_SLACK_LAST (build switch, default 1 since r04): the slack workgroups after
-// the tiles (r02's order; 0: first, r03).  r04 A/B, one session each: k_price
-// 17.94 us under rocprof against 18.83 with the slacks first.
-#ifndef ELP_SLACK_LAST
-#define ELP_SLACK_LAST 1
-#endif
+// Grid: [d.ntiles column tiles of TILE_COLS columns][nsw slack workgroups]
+// [napply trailing workgroups that apply the last pivot's deferred plan (phase
+// 2; nothing the sweep reads)].  r03 applied the plan in waves 1..3 of every
+// tile and put the slack workgroups first; r04's A/B measured both slower
+// (k_price 17.94 us under rocprof against 18.83 with the slacks first; 25.4k
+// against 24.7k iterations/s with the tiles applying the plan), and r06
+// removed those variants.  TW: the tile width (TILE_COLS: every AR row offset
+// a shift).
 template <int NTL, int TW>
-DEV void price_body(const Dev& d, int nsw, int apply, int napply, int nb_minv) {
+DEV void price_body(const Dev& d, int nsw, int napply, int nb_minv) {
     __shared__ double part[PRICE_SPLIT][TILE_COLS];
     __shared__ Cand red[PRICE_SPLIT];
     const int64_t ntiles = d.ntiles;
     if (napply > 0 && apply_role(d, napply, nb_minv, false)) return;
-    const int sw = ELP_SLACK_LAST ? (int)blockIdx.x - (int)ntiles : (int)blockIdx.x;  // slack workgroup index
+    const int sw = (int)blockIdx.x - (int)ntiles;  // slack workgroup index
     if (sw >= 0 && sw < nsw) {
         PDBG(1, 2ull);
         PDBG(2, 0ull);
@@ -1118,8 +1069,8 @@ DEV void price_body(const Dev& d, int nsw, int apply, int napply, int nb_minv) {
         price_slacks<PRICE_THREADS>(d, ntiles, sw, nsw, red);  // a slack workgroup
         return;
     }
-    const int64_t tile = ELP_SLACK_LAST ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - nsw;
-    const int tw = TW ? TW : d.tile_w;
+    const int64_t tile = (int64_t)blockIdx.x;
+    constexpr int tw = TW;
     // Software-pipelined sweep: the control block is loaded FIRST (vmcnt
     // retires in issue order, so the status test and the loop bound wait for
     // it alone, not for the rows issued behind it), then the first UNR rows
@@ -1149,20 +1100,13 @@ DEV void price_body(const Dev& d, int nsw, int apply, int napply, int nb_minv) {
     const double* __restrict__ yy = d.yy;
     const int cap = (int)d.arcap;
     dbl2 va[UNR], vb[UNR];
-#if ELP_PRICE_YLANE
     // y of a block: lane l loads slot p + S (l mod UNR), the fma takes it by readlane
     double ya, yb;
     ya = yy[min(w + S * (lane % UNR), cap - 1)];
-#else
-    double ya[UNR], yb[UNR];
-#endif
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {  // slot w + S u, clamped into AR (masked by |Y| at use)
         const int pp = min(w + S * u, cap - 1);
         va[u] = AR_LOAD(col + (size_t)pp * (size_t)tw);
-#if !ELP_PRICE_YLANE
-        ya[u] = yy[pp];
-#endif
     }
     // the epilogue's per-column operands (status, cost, Devex weight, previous
     // d) of columns 2 lane, 2 lane + 1 -- wave 0's: the other waves load element
@@ -1182,15 +1126,9 @@ DEV void price_body(const Dev& d, int nsw, int apply, int napply, int nb_minv) {
     if (st0 != ST_RUN) {
 #pragma unroll
         for (int u = 0; u < UNR; ++u) KEEP(va[u].x);
-#if ELP_PRICE_YLANE
         KEEP(ya);
-#else
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) KEEP(ya[u]);
-#endif
         KEEP(pf_c0);
         KEEP(pf_c1);
-        if (apply && w != 0) tile_apply(d, tile, ntiles);
         return;
     }
     PDBG(1, __builtin_amdgcn_s_memrealtime());
@@ -1198,7 +1136,6 @@ DEV void price_body(const Dev& d, int nsw, int apply, int napply, int nb_minv) {
     double acc0 = 0.0, acc1 = 0.0;
     // rows of a block at or past |Y| re-read the block's first row (p < |Y|;
     // an L1/L2 hit) and are masked when consumed
-#if ELP_PRICE_YLANE
 #define PIPE_ISSUE(V, Y, P)                                                          \
     do {                                                                             \
         _Pragma("unroll") for (int u = 0; u < UNR; ++u) {                            \
@@ -1209,17 +1146,6 @@ DEV void price_body(const Dev& d, int nsw, int apply, int napply, int nb_minv) {
         Y = yy[ry_ < nys ? ry_ : (P)];                                               \
     } while (0)
 #define PIPE_Y(Y, u) lane_bcast(Y, u)
-#else
-#define PIPE_ISSUE(V, Y, P)                                                          \
-    do {                                                                             \
-        _Pragma("unroll") for (int u = 0; u < UNR; ++u) {                            \
-            const int r_ = (P) + S * u < nys ? (P) + S * u : (P);                    \
-            V[u] = AR_LOAD(col + (size_t)r_ * (size_t)tw);                           \
-            Y[u] = yy[r_];                                                           \
-        }                                                                            \
-    } while (0)
-#define PIPE_Y(Y, u) Y[u]
-#endif
 #define PIPE_CONSUME(V, Y, P)                                                        \
     do {                                                                             \
         _Pragma("unroll") for (int u = 0; u < UNR; ++u) {                            \
@@ -1261,11 +1187,8 @@ DEV void price_body(const Dev& d, int nsw, int apply, int napply, int nb_minv) {
     PDBG(3, __builtin_amdgcn_s_memrealtime());
     // the epilogue is wave 0's: lane l finishes columns 2l, 2l+1 (the classes
     // added in order), takes the better of the two, and the wave reduces
-    // without LDS or a barrier; waves 1..3 apply the pending plan meanwhile
-    if (w != 0) {
-        if (apply) tile_apply(d, tile, ntiles);  // (phase 2 only: phase 1 applies in k_update)
-        return;
-    }
+    // without LDS or a barrier
+    if (w != 0) return;
     Cand cb[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1326,12 +1249,11 @@ DEV void tstamp_end(const Dev& d, int tslot) {
 }
 
 template <int NTL, int TW, bool TIMED = false>
-__global__ void __launch_bounds__(PRICE_THREADS) k_price(DEV_PARAM, int nsw, int apply, int napply, int nb_minv,
+__global__ void __launch_bounds__(PRICE_THREADS) k_price(Dev d, int nsw, int napply, int nb_minv,
                                                          int tslot) {
-    DEV_BIND
     if (TIMED) tstamp_begin(d, tslot);
     pstamp_begin<PRICE_THREADS>(d);
-    price_body<NTL, TW>(d, nsw, apply, napply, nb_minv);
+    price_body<NTL, TW>(d, nsw, napply, nb_minv);
     pstamp_end(d);
     if (TIMED) tstamp_end(d, tslot);
 }
@@ -1409,10 +1331,6 @@ DEV void price_csc_body(const Dev& d, int napply, int nb_minv, int nsw) {
         }
         return;
     }
-#ifndef ELP_PCSC_PF
-#define ELP_PCSC_PF 1
-#endif
-#if ELP_PCSC_PF
     const DevCtl* c = d.ctl;
     const int64_t ntiles = gridDim.x - napply - nsw;
     const bool tilewg = (int64_t)blockIdx.x < ntiles;
@@ -1469,36 +1387,6 @@ DEV void price_csc_body(const Dev& d, int napply, int nb_minv, int nsw) {
         }
         __syncthreads();
     }
-#else
-    const DevCtl* c = d.ctl;
-    if (c->status != ST_RUN) return;
-    const int64_t ntiles = gridDim.x - napply - nsw;
-    if ((int64_t)blockIdx.x >= ntiles) {  // a slack workgroup
-        price_slacks<TILE_COLS>(d, ntiles, (int)(blockIdx.x - ntiles), nsw, red);
-        return;
-    }
-    const int bland = c->bland;
-    const int64_t j0 = (int64_t)blockIdx.x * TILE_COLS;
-    const int64_t j = j0 + threadIdx.x;
-    const int64_t jend = j0 + TILE_COLS < d.n ? j0 + TILE_COLS : d.n;
-    const int64_t s0 = d.cptr[j0], s1 = d.cptr[jend];
-    const bool staged = s1 - s0 <= CSC_STAGE;
-    if (staged) {
-        for (int64_t t = s0 + threadIdx.x; t < s1; t += TILE_COLS) {
-            sv[t - s0] = d.cval[t];
-            sy[t - s0] = d.y[d.rind[t]];
-        }
-        __syncthreads();
-    }
-    const int64_t jc = j < d.n ? j : (d.n > 0 ? d.n - 1 : 0);
-    const int64_t a = d.cptr[jc], b = d.cptr[jc + 1];
-    const int8_t vsj = d.vstat[jc];
-    const double cj = d.cost[jc];
-    const double dwj = d.dw[jc], dpj = d.dprev[jc];
-    const int cdevex = c->devex;
-    const DevexIn cdx = devex_in(c);
-    const double ctold = c->tol_dual;
-#endif
     PDBG(2, __builtin_amdgcn_s_memrealtime());
     double acc = 0.0;
     if (j < d.n) {
@@ -1851,9 +1739,8 @@ DEV void select_ftran_sparse(const Dev& d, int q, int k, int pr, int nrw, int du
 constexpr int QZ_PT = 8;
 // SP: the CSC sparse FTRAN (select_ftran_sparse) after the min-loc
 template <int PFM, bool SP = false>  // Minv values per lane held in registers (k <= 64 PFM): 8 or 16 by the host's bound
-__global__ void __launch_bounds__(256) k_select_ftran(DEV_PARAM, int ntiles, int nsw, int k_ub, int dslot, int nrw,
+__global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw, int k_ub, int dslot, int nrw,
                                                       int nqz, int dual) {
-    DEV_BIND
     extern __shared__ __attribute__((aligned(16))) double aRs[];  // [k]
     __shared__ Cand red[4];
     RSTAMP(12);
@@ -2289,14 +2176,11 @@ constexpr int SPZ_MAX = 16;  // basic entries of a row the CSC row walk keeps (m
 #define ELP_ZB 16
 #endif
 constexpr int ZB = ELP_ZB;
-// ELP_ZR_MERGE 1 (default): the flips' row walk in the same lane as alpha_U's,
-// from the same row entries (one set of row waves); 0: waves of their own
-// (r04's layout).  r05c A/B on the 20 000 x 100 000 phase-1 LP
-// (profiles/r05c_ab_zr_variants.txt): 24.4 us merged against 25.5 split, and
-// 28-31 us with 32 entries' loads per batch (ELP_ZB=32: 256 VGPRs)
-#ifndef ELP_ZR_MERGE
-#define ELP_ZR_MERGE 1
-#endif
+// (r05c A/B on the 20 000 x 100 000 phase-1 LP, profiles/r05c_ab_zr_variants.txt:
+// the flips' row walk in the same lane as alpha_U's 24.4 us against 25.5 in
+// waves of their own, and 28-31 us with 32 entries' loads per batch (ZB = 32:
+// 256 VGPRs); r06 removed the one-lane-per-row kernel k_ftran_zr_sp, which
+// k_ftran_zr_sq replaced in r05)
 DEV int csr_basic(const Dev& d, int64_t r0, int64_t r1, int* pp, double* vv, bool* over) {
     int cnt = 0;
     *over = false;
@@ -2373,125 +2257,7 @@ DEV double zrow_chain(const Dev& d, int i, int k, const int* pp, const double* v
     return z;
 }
 
-// FTRAN-z + Harris pass 1 for CSC input: row tiles of 64 rows (one per lane:
-// csr_basic + zrow_chain), then bump tiles of 64 positions, then the snapshot
-// workgroup -- k_ftran_zr's regions and minima with one wave per tile (zw = 1).
-// Everything that depends on neither the control block nor this iteration's
-// decision (the row extent, cover, the entering column's and a_F's entry) is
-// loaded before the status test.
-// flip (the dual phase): the bound flips' x_B update rides along -- a covered
-// row's lane also forms A[i, S] fS from the same entries and updates
-// x -= sigma (a_F,i - A[i, S] fS); bump positions x -= fS (k_dual_flip_apply's
-// arithmetic); the dual leaves on k_dual_row's row, so no primal pass 1 runs.
-// (r04: the flips' row walk in waves of its own; until then a launch of its own)
-__global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt, int flip, int dslot) {
-    RSTAMP(16);
-    const DevCtl* c = d.ctl;
-    const int32_t st0 = c->status;
-    int k = c->k, q = c->q;
-    const int bland = c->bland, m = d.m, lane = threadIdx.x;
-    const double sig = c->sig, ptol = c->tol_primal, pivtol = c->tol_pivot;
-    const int nfl = c->nflip;
-    const bool roww = (int)blockIdx.x < nrt;
-    const int i = roww ? (int)blockIdx.x * 64 + lane : 0;
-    const int ic = i < m ? i : (m > 0 ? m - 1 : 0);
-    int64_t r0 = 0, r1 = 0;
-    int u = -1;
-    double qi = 0.0, afi = 0.0;
-    if (m > 0) {  // (straight-line, masked at use)
-        r0 = d.rptr[ic];
-        r1 = d.rptr[ic + 1];
-        u = d.cover[ic];
-        qi = d.qcol[ic];
-        afi = d.aF ? d.aF[ic] : 0.0;
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("" : "+v"(k), "+v"(q));
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) d.ctl->snap_status = st0;  // for k_ratio
-    if (st0 != ST_RUN) {
-        KEEP(r0);
-        KEEP(u);
-        KEEP(qi);
-        KEEP(afi);
-        return;
-    }
-    RSTAMP(17);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        d.ctl->snap_k = k;
-        d.ctl->snap_bland = bland;
-    }
-    if (blockIdx.x == gridDim.x - 1) {
-        if (threadIdx.x == 0) zr_snapshot(d, k, q);
-        return;
-    }
-    const bool fl = flip && nfl > 0;
-    if (!ELP_ZR_MERGE && flip && (int)blockIdx.x >= (int)gridDim.x - 1 - nrt) {  // the flips' row waves
-        const int fi = (blockIdx.x - (gridDim.x - 1 - nrt)) * 64 + lane;
-        if (!fl || fi >= m) return;
-        const int fu = d.cover[fi];
-        if (fu >= 0) {
-            int pp[SPZ_MAX];
-            double vv[SPZ_MAX];
-            bool over;
-            const int cnt = csr_basic(d, d.rptr[fi], d.rptr[fi + 1], pp, vv, &over);
-            const double tot = zrow_chain(d, fi, k, pp, vv, cnt, over, d.fS);
-            d.xr[fi] = d.xr[fi] - unit_sign(d, fu, fi) * (d.aF[fi] - tot);
-        }
-        return;
-    }
-    double tmin = HUGE_VAL, ge = 0.0, xe = 0.0, le = 0.0, he = 0.0;
-    int ve = -1, e = 0, region;
-    if (roww) {
-        e = i;
-        region = blockIdx.x;
-        if (i < m && u >= 0) {
-            int pp[SPZ_MAX];
-            double vv[SPZ_MAX];
-            bool over;
-            const int cnt = csr_basic(d, r0, r1, pp, vv, &over);
-            const double z = zrow_chain(d, i, k, pp, vv, cnt, over, d.alS);
-            const double aiq = q >= d.N ? (i == q - d.N ? 1.0 : 0.0) : qi;
-            const double sg = unit_sign(d, u, i);
-            const double alU = sg * (aiq - z);
-            d.alU[i] = alU;
-            RSTAMP(18);
-            if (ELP_ZR_MERGE && fl) {
-                const double tot = zrow_chain(d, i, k, pp, vv, cnt, over, d.fS);
-                d.xr[i] = d.xr[i] - sg * (afi - tot);
-            }
-            if (!flip) {
-                ge = sig * alU;
-                xe = d.xr[i];
-                le = d.rlo[i];
-                he = d.rhi[i];
-                ve = u;
-                tmin = harris1(ge, xe, le, he, ptol, pivtol, bland);
-            }
-        }
-    } else {
-        const int p = (blockIdx.x - nrt) * 64 + lane;
-        e = m + p;
-        region = blockIdx.x;  // (= nrt + bump tile: one wave per tile)
-        if (p < k) {
-            if (flip) {
-                if (fl) d.xs[p] = d.xs[p] - d.fS[p];
-            } else {
-                ge = sig * d.alS[p];
-                xe = d.xs[p];
-                le = d.slo[p];
-                he = d.shi[p];
-                ve = d.Sl[p];
-                tmin = harris1(ge, xe, le, he, ptol, pivtol, bland);
-            }
-        }
-    }
-    const double bmin = wave_min_f64(tmin);
-    if (lane == 0) d.blockmin[blockIdx.x] = bmin;
-    emit_wave(d, region, ve, e, ge, xe, le, he, bmin, pivtol);
-    RSTAMP(19);
-}
-
-// The same with four lanes per row (ELP_ZR_LPR = 4, the default since r05):
+// FTRAN-z + Harris pass 1 for CSC input (the row walk): four lanes per row --
 // a workgroup of 4 waves takes 64 rows, 16 per wave; each lane loads an
 // interleaved quarter of its row's entries (<= ZQB per batch: one batch of
 // column / value loads, then one of spos loads, for rows of <= 32 nonzeros --
@@ -2504,9 +2270,6 @@ __global__ void __launch_bounds__(64) k_ftran_zr_sp(Dev d, int nrt, int flip, in
 // covers 512 regions; a row tile emits <= 64 candidates: one per row); bump
 // tiles of 64 positions (the first wave of the workgroup).
 constexpr int ZLPR = 4, ZRPW = 64 / ZLPR, ZQB = 8, ZSQ = 32, ZROWS = 4 * ZRPW;
-#ifndef ELP_ZR_LPR
-#define ELP_ZR_LPR 4
-#endif
 // ordered emission of a workgroup's pass-2 candidates into its region (every
 // wave's kept entries compacted by ballot, the waves' counts through LDS)
 DEV void emit_block(const Dev& d, int region, int var, int e, double g, double x, double l, double u, double bmin,
@@ -2748,8 +2511,7 @@ constexpr int ZR_PA = 4;
 // dependent round trip to AS.  Same chain, same order: same bits.
 constexpr int ZR_XPF = 2;
 template <bool LDSZ, int ZR_WAVES, bool ALS>
-__global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(DEV_PARAM, int nrt, int k_ub, int dslot, int qz) {
-    DEV_BIND
+__global__ void __launch_bounds__(64 * ZR_WAVES) k_ftran_zr(Dev d, int nrt, int k_ub, int dslot, int qz) {
     extern __shared__ __attribute__((aligned(16))) double zlds[];  // [nch_ub][ZR_ROWS], then (ALS) [k_ub] alpha_S
     __shared__ double red[ZR_WAVES];
     RSTAMP(16);
@@ -3014,9 +2776,8 @@ enum { SI_VSQ, SI_RPOS0, SI_YPOS0, SI_YLAST, SI_SLLAST, SI_RLLAST, SI_RPOSYL, SI
 #define ELP_BOOK_WG 1
 #endif
 template <int PFT, bool DUAL = false>
-__global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, int lds_row, int defer,
+__global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int lds_row, int defer,
                                                int nmain, int k_ub, int dslot, int nreg) {
-    DEV_BIND
     extern __shared__ __attribute__((aligned(16))) double asrow_lds[];  // [k]: A[lrow, S]
     __shared__ double dred[4];
     __shared__ Leave lred[4];
@@ -3056,9 +2817,6 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
     //      out next (bounded by the host's k_ub, masked by the real k below):
     //      the pass-1 minima, this wave's row of MinvT (B^-1 row, cases B / D)
     //      and its bump row R_col (dual update)
-#ifndef ELP_RATIO_PFQ
-#define ELP_RATIO_PFQ 1  // (4: +0.5 us of k_ratio, rocprof A/B r02)
-#endif
     constexpr int PFB = 4;
     const bool main_wg = (int)blockIdx.x < nmain;
     const bool pfb = nblk <= 256 * PFB, pft = k_ub <= 64 * PFT;
@@ -3077,7 +2835,7 @@ __global__ void __launch_bounds__(256) k_ratio(DEV_PARAM, int phase, int nblk, i
     // the pass-2 candidates k_ftran_zr emitted, one region per emitting wave:
     // thread t takes regions t and t + 256 (PFR), count and first PFQ entries
     // prefetched (clamped, masked by the count at use)
-    constexpr int PFQ = ELP_RATIO_PFQ, PFR = 2;
+    constexpr int PFQ = 1, PFR = 2;  // (PFQ 4: +0.5 us of k_ratio, rocprof A/B r02)
     int rcn[PFR];
     RCand rq[PFR][PFQ];
 #pragma unroll
@@ -3937,10 +3695,7 @@ DEV void apply_minv(const Dev& d, const Plan& P, int64_t e0, int64_t estride, bo
 // with the same bits.
 constexpr int SRU_U = 8;
 constexpr unsigned SRU_WG_MAX = 4096;
-#ifndef ELP_SRU_RPW
-#define ELP_SRU_RPW 1  // rows per workgroup (r05ze: 4 -- their multipliers in one round trip -- measured slower)
-#endif
-constexpr int SRU_RPW = ELP_SRU_RPW;
+constexpr int SRU_RPW = 1;  // rows per workgroup (r05ze: 4 -- their multipliers in one round trip -- measured slower)
 constexpr unsigned sru_wgs(int k_ub) {
     return (unsigned)((k_ub + SRU_RPW) / SRU_RPW) < SRU_WG_MAX ? (unsigned)((k_ub + SRU_RPW) / SRU_RPW) : SRU_WG_MAX;
 }
@@ -5395,10 +5150,7 @@ __global__ void __launch_bounds__(TILE_COLS) k_dual_price_csc(Dev d, int nsw, in
             // batches of DPB entries: each level of the row index -> rpos / y ->
             // rho_R gathers in flight together (one round trip per level, not
             // three per nonzero), the chains in ascending rows as before
-#ifndef ELP_DPB
-#define ELP_DPB 1
-#endif
-            constexpr int DPB = ELP_DPB;
+            constexpr int DPB = 1;  // (r05: batches of 4 measured slower, 13.1 -> 15.3 us)
             double ad = 0.0, aa = 0.0;
             const int64_t t1 = tb;
             for (int64_t t0 = ta; t0 < t1; t0 += DPB) {
@@ -6609,11 +6361,6 @@ hipError_t launch_scale_apply(int m, int64_t ncols, double* A, const int32_t* rh
     return hipGetLastError();
 }
 
-hipError_t launch_transpose_A(const Dev& d, hipStream_t st) {
-    if (d.m > 0 && d.n > 0)
-        k_transpose_A<<<dim3((unsigned)cdiv(d.n, 64), (unsigned)cdiv(d.m, 64)), 256, 0, st>>>(d);
-    return hipGetLastError();
-}
 
 hipError_t launch_nzlist(const Dev& d, hipStream_t st) {
     const unsigned nb = (unsigned)cdiv(d.n > 0 ? d.n : 1, NZ_CHUNK);
@@ -6629,16 +6376,11 @@ hipError_t launch_row_chain(const Dev& d, hipStream_t st) {
 }
 
 
-// the dense pricing kernel for a launch: non-temporal sweep loads or not, the
-// default tile width as a compile-time constant or ELP_TILE_BAL's at run time
-typedef void (*PriceFn)(DEV_PARAM, int, int, int, int, int);
-static PriceFn price_kernel(bool nt, int tw, bool timed) {
-    if (timed) {
-        if (tw == TILE_COLS) return nt ? k_price<1, TILE_COLS, true> : k_price<0, TILE_COLS, true>;
-        return nt ? k_price<1, 0, true> : k_price<0, 0, true>;
-    }
-    if (tw == TILE_COLS) return nt ? k_price<1, TILE_COLS> : k_price<0, TILE_COLS>;
-    return nt ? k_price<1, 0> : k_price<0, 0>;
+// the dense pricing kernel for a launch: non-temporal sweep loads or not, timed or not
+typedef void (*PriceFn)(Dev d, int, int, int, int);
+static PriceFn price_kernel(bool nt, bool timed) {
+    if (timed) return nt ? k_price<1, TILE_COLS, true> : k_price<0, TILE_COLS, true>;
+    return nt ? k_price<1, TILE_COLS> : k_price<0, TILE_COLS>;
 }
 
 hipError_t launch_ptimer_reduce(const Dev& d, int nslots, hipStream_t st) {
@@ -6748,15 +6490,9 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phas
     }
     // the dense deferred plan in trailing workgroups of the launch (r02's
     // layout, the default again since r04: 3 x 3 interleaved A/B at 5000 x 50000,
-    // 25.4k against 24.7k iterations/s with the tiles' waves 1-3 applying it);
-    // ELP_TRAIL_APPLY=0 restores the waves (r03)
-    static const bool trail = [] {
-        const char* e = std::getenv("ELP_TRAIL_APPLY");
-        return !(e && std::atoi(e) == 0);
-    }();
+    // 25.4k against 24.7k iterations/s with the tiles' waves 1-3 applying it)
     unsigned dnapply = 0, dnb_minv = 0;
-    if (phase == 2 && !d.csc && trail) update_grid(d, k_ub, false, &dnb_minv, &dnapply, PRICE_THREADS, ELP_APPLY_PT, ELP_MINV_WG_MAX);
-    const int dapply = phase == 2 && !trail ? 1 : 0;
+    if (phase == 2 && !d.csc) update_grid(d, k_ub, false, &dnb_minv, &dnapply, PRICE_THREADS, ELP_APPLY_PT, ELP_MINV_WG_MAX);
     // + nsw: the slack workgroups (candidates [ntiles, ntiles + nsw)); the dense
     // sweep applies the deferred plan inside its tiles (price_body)
     const int nsw = slack_wgs(d, ny_ub);
@@ -6773,16 +6509,16 @@ static hipError_t launch_btran_price(const Dev& d, int k_ub, int ny_ub, int phas
             hipExtLaunchKernelGGL(timed ? k_price_csc<true> : k_price_csc<false>, dim3(grid), dim3(TILE_COLS), 0, st,
                                   ev0, ev1, 0, d, (int)napply, (int)nb_minv, nsw, tslot);
         else
-            hipExtLaunchKernelGGL(price_kernel(nt, d.tile_w, timed), dim3(grid), dim3(PRICE_THREADS), 0, st, ev0,
-                                  ev1, 0, DEV_ARG(d), nsw, dapply, (int)dnapply, (int)dnb_minv, tslot);
+            hipExtLaunchKernelGGL(price_kernel(nt, timed), dim3(grid), dim3(PRICE_THREADS), 0, st, ev0,
+                                  ev1, 0, d, nsw, (int)dnapply, (int)dnb_minv, tslot);
         return hipGetLastError();
     }
     if (d.csc) {
         if (timed) k_price_csc<true><<<grid, TILE_COLS, 0, st>>>(d, (int)napply, (int)nb_minv, nsw, tslot);
         else k_price_csc<false><<<grid, TILE_COLS, 0, st>>>(d, (int)napply, (int)nb_minv, nsw, tslot);
     } else {
-        hipLaunchKernelGGL(price_kernel(nt, d.tile_w, timed), dim3(grid), dim3(PRICE_THREADS), 0, st, DEV_ARG(d),
-                           nsw, dapply, (int)dnapply, (int)dnb_minv, tslot);
+        hipLaunchKernelGGL(price_kernel(nt, timed), dim3(grid), dim3(PRICE_THREADS), 0, st, d,
+                           nsw, (int)dnapply, (int)dnb_minv, tslot);
     }
     return hipGetLastError();
 }
@@ -6802,46 +6538,39 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
     const bool dskip = phase == 4;
     if (phase >= 3) phase = 3;
     if (bump_ftran && k_ub > 0) k_ftran_bump<<<cdiv(k_ub, 4), 256, 0, st>>>(d, d.aR, d.alS, 1);
-    // CSC with a large bump: FTRAN-z from the rows of A (k_ftran_zr_sp: 64-row
-    // tiles, 64-position bump tiles); else k_ftran_zr's 32-row tiles over AS
+    // CSC with a large bump: FTRAN-z from the rows of A (k_ftran_zr_sq: 64 rows
+    // per 4-wave workgroup, 64-position bump tiles); else k_ftran_zr's 32-row
+    // tiles over AS
     const bool spz = use_spz(d, k_ub);
-    // (k_ftran_zr_sq: 64 rows per 4-wave workgroup; ELP_ZR_LPR=1: k_ftran_zr_sp's one wave)
     const int nrt = spz ? (int)cdiv(m > 0 ? m : 1, 64) : (int)cdiv(m > 0 ? m : 1, ZR_ROWS);
     // z partials: 256 B per chunk of ZCHUNK bump positions in LDS (<= 64 KiB,
     // k <= 8192); larger bumps use a private slice of zpart per row tile
     const size_t lds = (size_t)cdiv(k_ub, ZCHUNK) * ZR_ROWS * sizeof(double);
     const bool ldsz = lds <= 64 * 1024 && !d.force_select;
-    static const int zw_env = getenv("ELP_ZW") ? atoi(getenv("ELP_ZW")) : 0;  // A/B override
     int zw = (ldsz && nrt > 256 && cdiv(k_ub, ZCHUNK) <= 8) ? 4 : 8;  // waves per row tile
-    if (ldsz && (zw_env == 4 || zw_env == 8)) zw = zw_env;
     if (spz) zw = 1;
     const int nbt = (int)cdiv(k_ub, 64 * zw);  // bump tiles (k_ftran_zr_sq: 64 positions per workgroup)
     // alpha_S in LDS beside the z partials when the half-waves run more than one
     // chunk each (k_ub > 2 zw ZCHUNK) and it fits the prefetch (ZR_PA per thread):
     // 10 000 x 500 000 at k 529: 18.8 -> 16.3 us; with one chunk per half-wave the
     // registers win (the LDS round trip cost 0.8 us at 5000 x 50000, r02)
-    static const bool no_als = getenv("ELP_NO_ALS") != nullptr;  // A/B
     const int nxp = (int)std::min<int64_t>(std::max<int64_t>((int64_t)cdiv(k_ub, ZCHUNK) - 2 * zw, 0), ZR_XPF);
     const size_t lds_als = lds + (size_t)k_ub * sizeof(double) + (size_t)nxp * ZCHUNK * ZR_ROWS * sizeof(double);
-    const bool als = !no_als && ldsz && k_ub > 2 * zw * ZCHUNK && k_ub <= ZR_PA * 64 * zw && lds_als <= 64 * 1024;
+    const bool als = ldsz && k_ub > 2 * zw * ZCHUNK && k_ub <= ZR_PA * 64 * zw && lds_als <= 64 * 1024;
     if (spz) {
         // (the dual phase: + nrt waves for the flips' x_B update, before the snapshot one)
-        if (ELP_ZR_LPR == 4)
-            k_ftran_zr_sq<<<nrt + nbt + 1, 256, 0, st>>>(d, nrt, phase == 3 ? 1 : 0, dslot);
-        else
-            k_ftran_zr_sp<<<nrt + nbt + (phase == 3 && !ELP_ZR_MERGE ? nrt : 0) + 1, 64, 0, st>>>(
-                d, nrt, phase == 3 ? 1 : 0, dslot);
+        k_ftran_zr_sq<<<nrt + nbt + 1, 256, 0, st>>>(d, nrt, phase == 3 ? 1 : 0, dslot);
     } else {
         // + 1: the snapshot workgroup
         if (als) {
-            if (zw == 4) k_ftran_zr<true, 4, true><<<nrt + nbt + 1, 256, lds_als, st>>>(DEV_ARG(d), nrt, k_ub, dslot, qz);
-            else k_ftran_zr<true, 8, true><<<nrt + nbt + 1, 512, lds_als, st>>>(DEV_ARG(d), nrt, k_ub, dslot, qz);
+            if (zw == 4) k_ftran_zr<true, 4, true><<<nrt + nbt + 1, 256, lds_als, st>>>(d, nrt, k_ub, dslot, qz);
+            else k_ftran_zr<true, 8, true><<<nrt + nbt + 1, 512, lds_als, st>>>(d, nrt, k_ub, dslot, qz);
         } else if (zw == 4) {
-            k_ftran_zr<true, 4, false><<<nrt + nbt + 1, 256, lds, st>>>(DEV_ARG(d), nrt, k_ub, dslot, qz);
+            k_ftran_zr<true, 4, false><<<nrt + nbt + 1, 256, lds, st>>>(d, nrt, k_ub, dslot, qz);
         } else if (ldsz) {
-            k_ftran_zr<true, 8, false><<<nrt + nbt + 1, 512, lds, st>>>(DEV_ARG(d), nrt, k_ub, dslot, qz);
+            k_ftran_zr<true, 8, false><<<nrt + nbt + 1, 512, lds, st>>>(d, nrt, k_ub, dslot, qz);
         } else {
-            k_ftran_zr<false, 8, false><<<nrt + nbt + 1, 512, 0, st>>>(DEV_ARG(d), nrt, k_ub, dslot, qz);
+            k_ftran_zr<false, 8, false><<<nrt + nbt + 1, 512, 0, st>>>(d, nrt, k_ub, dslot, qz);
         }
     }
     // ratio test + (cases B/D) B^-1 row: one workgroup per 4 bump columns;
@@ -6873,10 +6602,10 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
         //  529, r03 A/B over the last 2000 iterations))
         const unsigned nbk = ELP_BOOK_WG;  // (the bookkeeping workgroup after the main ones)
         if (phase == 3)
-            k_ratio<8, true><<<nmain + nbk, 256, lds_row ? lds : 0, st>>>(DEV_ARG(d), 2, nrt + nbt, lds_row, 0,
+            k_ratio<8, true><<<nmain + nbk, 256, lds_row ? lds : 0, st>>>(d, 2, nrt + nbt, lds_row, 0,
                                                                          (int)nmain, k_ub, dslot, nrt + nbt * zw);
         else
-            k_ratio<8><<<nmain + nbk + nar, 256, lds_row ? lds : 0, st>>>(DEV_ARG(d), phase, nrt + nbt, lds_row,
+            k_ratio<8><<<nmain + nbk + nar, 256, lds_row ? lds : 0, st>>>(d, phase, nrt + nbt, lds_row,
                                                                          defer, (int)nmain, k_ub, dslot,
                                                                          nrt + nbt * zw);
     }
@@ -6908,11 +6637,11 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
         // last 4 000 iterations of 10 000 x 500 000, k 529; 16 measured no faster
         // there, r01 -- fewer waves per SIMD), else the row is read after a_R
         if (sp)
-            k_select_ftran<8, true><<<g, 256, ldsz, st>>>(DEV_ARG(d), ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz, 0);
+            k_select_ftran<8, true><<<g, 256, ldsz, st>>>(d, ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz, 0);
         else if (k_ub > 512 && k_ub <= 640)
-            k_select_ftran<10><<<g, 256, ldsz, st>>>(DEV_ARG(d), ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz, 0);
+            k_select_ftran<10><<<g, 256, ldsz, st>>>(d, ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz, 0);
         else
-            k_select_ftran<8><<<g, 256, ldsz, st>>>(DEV_ARG(d), ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz, 0);
+            k_select_ftran<8><<<g, 256, ldsz, st>>>(d, ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz, 0);
         return launch_iteration_tail(d, k_ub, phase, st, false, dslot, nqz > 0 ? 1 : 0);
     }
     k_select<<<1, 1024, 0, st>>>(d, ntiles, nsw, 0);
@@ -7016,7 +6745,7 @@ static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_co
     const bool fold_fs = spz && (sp || 2 * lds <= 64 * 1024) && !d.force_select;
     if (k_ub > 0 && !fold_fs) k_dual_flip_bump<<<nrw, 256, lds_row ? lds : 0, st>>>(d, lds_row);
     if (spz) {
-        // (the row-wise x_B update runs inside k_ftran_zr_sp, below)
+        // (the row-wise x_B update runs inside k_ftran_zr_sq, below)
     } else {
         const unsigned nrt = cdiv(m > 0 ? m : 1, ZR_ROWS), nbt = cdiv(k_ub > 0 ? k_ub : 1, 512);
         const size_t zl = (size_t)cdiv(k_ub > 0 ? k_ub : 1, ZCHUNK) * ZR_ROWS * sizeof(double);
@@ -7030,11 +6759,11 @@ static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_co
         const unsigned nqz = d.qz && !d.csc ? cdiv(m, 256 * QZ_PT) : 0;
         const unsigned g = nrw + nqz + (d.csc ? 1 : 0);
         if (sp)
-            k_select_ftran<8, true><<<g, 256, ldsz, st>>>(DEV_ARG(d), 1, 0, k_ub, 0, (int)nrw, (int)nqz, dual);
+            k_select_ftran<8, true><<<g, 256, ldsz, st>>>(d, 1, 0, k_ub, 0, (int)nrw, (int)nqz, dual);
         else if (k_ub > 512 && k_ub <= 640)
-            k_select_ftran<10><<<g, 256, ldsz, st>>>(DEV_ARG(d), 1, 0, k_ub, 0, (int)nrw, (int)nqz, dual);
+            k_select_ftran<10><<<g, 256, ldsz, st>>>(d, 1, 0, k_ub, 0, (int)nrw, (int)nqz, dual);
         else
-            k_select_ftran<8><<<g, 256, ldsz, st>>>(DEV_ARG(d), 1, 0, k_ub, dslot, (int)nrw, (int)nqz, dual);
+            k_select_ftran<8><<<g, 256, ldsz, st>>>(d, 1, 0, k_ub, dslot, (int)nrw, (int)nqz, dual);
         return launch_iteration_tail(d, k_ub, defer ? 4 : 3, st, false, dslot, nqz > 0 ? 1 : 0);
     }
     k_select<<<1, 1024, 0, st>>>(d, 1, 0, 1);

@@ -1,33 +1,42 @@
 // elp_resident.hip -- the resident small-LP solver: the whole simplex loop of
-// an LP that fits in one CU's LDS, run by ONE wave in ONE launch.
+// an LP with at most 64 rows whose state fits in one CU's LDS, run by ONE
+// wave in ONE launch.
 //
 // Why: the multi-workgroup pipeline (elp_kernels.hip) pays 4-7 dependent
-// launches per pivot, a ~25 us floor per pivot that no amount of bandwidth
+// launches per pivot, a ~20 us floor per pivot that no amount of bandwidth
 // hides.  The models EasyLP's R front-end actually builds (README, test-DOP.R,
 // the vignettes, the MIP tests' nodes; BASELINE configs[4]'s Klee-Minty cube)
-// are a few dozen rows and columns: their whole state -- A, the bump inverse,
-// every per-variable and per-row vector -- fits in the 160 KiB of LDS, and one
-// wave of 64 lanes does a pivot's pricing, FTRAN, ratio test and update in a
-// few hundred dependent LDS / DPP steps, no kernel boundary and no global
-// round trip between them.
+// are a few dozen rows and columns: their whole state fits beside one wave,
+// which does a pivot's pricing, FTRAN, ratio test and update with no kernel
+// boundary and no global round trip.
+//
+// Layout: lane r holds row r's values (x_B of a covered row, its cover, rpos,
+// Y slot, y_r, a_q's entry, alpha_U, ...), lane p bump position p's (S_p,
+// R_p, x_S, alpha_S) and Y slot p's row, all in registers; a value of another
+// lane is a v_readlane (uniform index) or a ds_bpermute (per-lane index, in
+// uniform control flow).  LDS holds what is indexed by column or variable: A
+// (column-major), the bump inverse, bounds / costs / values / statuses, Devex
+// weights, the dual ratio test's candidates.  One wave's LDS operations
+// complete in issue order, so a store and another lane's later load need only
+// the compiler's ordering (R_FENCE).
 //
 // Arithmetic: identical to oracle/elp_oracle.c (run_phase, run_dual,
-// basis_change, refactor, btran) and therefore to the multi-workgroup kernels
-// -- the same reduction shapes evaluated lane-serially: a wave_dot (64
-// lane-strided fma chains + the pairwise tree, offsets 1, 2, ..., 32) becomes
-// one lane's chains and the same tree (carry stack over the chains in lane
-// order); zchunk, the price slot classes and the column chains are already
-// per-output fma chains.  The orchestration is elp_api.hip run_loop's: loop-top
-// checks (phase-1 sum, iteration cap, budget stop, refactor period), the
-// recheck refactor after updated values reach optimality, the phase changes
-// (primal phase 1 or dual phase -> real costs, refactor, primal phase 2).
+// basis_change, refactor, btran) and therefore to the pipeline -- the same
+// reduction shapes, evaluated per output lane: a wave_dot (64 lane-strided
+// fma chains + the pairwise tree, offsets 1, 2, ..., 32) becomes one lane's
+// terms in order folded by the same tree (a carry stack), zchunk, the price
+// slot classes and the column chains are per-output fma chains already.  The
+// orchestration is elp_api.hip run_loop's: loop-top checks (phase-1 sum,
+// iteration cap, budget stop, time limit, refactor period), the recheck
+// refactor after updated values reach optimality, and the phase changes
+// (primal phase 1 or the dual phase -> real costs, refactor, primal phase 2).
 //
-// State: read from the device buffers the load left (elp_api.hip
-// load_common / reload_bounds_warm), kept in LDS during the solve, written
-// back at exit in the multi-workgroup path's own layout -- lists, bump inverse
-// (and MinvT), AS, AR, the per-position / per-row / per-slot caches -- so
-// elp_get_solution, elp_sensitivity and a MIP node's warm start read it as if
-// the pipeline had run.
+// State is read from the device buffers the load left (elp_api.hip
+// load_common / reload_bounds_warm) and written back at exit in the
+// pipeline's own layout -- lists, bump inverse (and MinvT), AS, AR, the
+// per-position / per-row / per-slot caches -- so elp_get_solution,
+// elp_sensitivity, elp_iterate and a MIP node's warm start read it as if the
+// pipeline had run.
 #include "elp_internal.h"
 
 #include <math.h>
@@ -40,6 +49,7 @@ constexpr int RW = 64;
 constexpr double R_WMAX = 1e20;   // DEVEX_WMAX (oracle, elp_kernels.hip)
 constexpr double R_RESET = 1e6;   // DEVEX_RESET
 constexpr double R_INF = HUGE_VAL;
+#define R_FENCE() asm volatile("" ::: "memory")
 
 // ------------------------------------------------------------ wave helpers
 template <int CTRL>
@@ -55,19 +65,27 @@ RDEV double r_swz16(double v) {
     const int hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), 0x401F);
     return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
-RDEV double r_rl(double v, int l) {
+// lane l's value (l uniform)
+RDEV double rl(double v, int l) {
     const long long b = __double_as_longlong(v);
     const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
     return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
-RDEV int r_rli(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+RDEV int rli(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+// lane src's value, src per lane (0..63); every lane active
+RDEV double shf(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)b);
+    const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
 RDEV double r_wmax(double v) {
     v = fmax(v, r_dpp<0xB1>(v));
     v = fmax(v, r_dpp<0x4E>(v));
     v = fmax(v, r_dpp<0x141>(v));
     v = fmax(v, r_dpp<0x140>(v));
     v = fmax(v, r_swz16(v));
-    return fmax(r_rl(v, 0), r_rl(v, 32));
+    return fmax(rl(v, 0), rl(v, 32));
 }
 RDEV double r_wmin(double v) {
     v = fmin(v, r_dpp<0xB1>(v));
@@ -75,7 +93,7 @@ RDEV double r_wmin(double v) {
     v = fmin(v, r_dpp<0x141>(v));
     v = fmin(v, r_dpp<0x140>(v));
     v = fmin(v, r_swz16(v));
-    return fmin(r_rl(v, 0), r_rl(v, 32));
+    return fmin(rl(v, 0), rl(v, 32));
 }
 RDEV int r_wmini(int v) {
     v = min(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));
@@ -85,8 +103,8 @@ RDEV int r_wmini(int v) {
     v = min(v, __builtin_amdgcn_ds_swizzle(v, 0x401F));
     return min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 32));
 }
-// the lane holding the best record: largest key (or smallest with MIN), then
-// the smallest id; -1 when no lane is valid (uniform)
+// the lane holding the best record: largest key (smallest with MIN), then the
+// smallest id; -1 when no lane is valid (uniform)
 template <bool MIN>
 RDEV int r_argbest(bool valid, double key, int id) {
     const unsigned long long vm = __ballot(valid);
@@ -94,48 +112,62 @@ RDEV int r_argbest(bool valid, double key, int id) {
     const double b = MIN ? r_wmin(valid ? key : R_INF) : r_wmax(valid ? key : -R_INF);
     bool in = valid && key == b;
     if (__ballot(in) == 0ull) in = valid;  // (NaN keys only)
-    const int im = r_wmini(in ? id : 0x7fffffff);
-    return __builtin_amdgcn_readfirstlane(__ffsll((long long)__ballot(in && id == im)) - 1);
+    const unsigned long long im = __ballot(in);
+    if (__popcll(im) == 1) return __builtin_amdgcn_readfirstlane(__ffsll((long long)im) - 1);
+    const int mn = r_wmini(in ? id : 0x7fffffff);
+    return __builtin_amdgcn_readfirstlane(__ffsll((long long)__ballot(in && id == mn)) - 1);
 }
 RDEV int r_argminid(bool valid, int id) {
     if (__ballot(valid) == 0ull) return -1;
-    const int im = r_wmini(valid ? id : 0x7fffffff);
-    return __builtin_amdgcn_readfirstlane(__ffsll((long long)__ballot(valid && id == im)) - 1);
+    const int mn = r_wmini(valid ? id : 0x7fffffff);
+    return __builtin_amdgcn_readfirstlane(__ffsll((long long)__ballot(valid && id == mn)) - 1);
 }
-#define RSYNC() __syncthreads()
+// the GPU wave_tree of one value per lane (uniform result)
+RDEV double r_wtree(double acc) {
+    acc = acc + r_dpp<0xB1>(acc);
+    acc = acc + r_dpp<0x4E>(acc);
+    acc = acc + r_dpp<0x141>(acc);
+    acc = acc + r_dpp<0x140>(acc);
+    acc = acc + r_swz16(acc);
+    return rl(acc, 0) + rl(acc, 32);
+}
 
-// wave_dot's bits, one lane: chain l = fma over i = l, l + 64, ... < len of
-// x(i) * y(i), then the pairwise tree over the chains in lane order, folded
-// as a carry stack (a pair (l, l + off) exists only when l + off < min(len,
-// 64); the chains past it are the +0.0 of an idle lane)
-template <class F>
-RDEV double lane_wave_dot(F xy, int len) {
-    const int nl = len < RW ? len : RW;
-    double st[7];
-    int cnt = 0;
-    for (int l = 0; l < nl; ++l) {
-        double v = 0.0;
-        for (int i = l; i < len; i += RW) v = xy(i, v);
+// wave_dot's bits in one lane, for len <= 64: lane l's chain is one fma
+// from 0.0, the idle lanes (l >= len) hold +0.0, and the tree pairs lanes
+// (l, l + off) for off = 1, 2, ..., 32 -- so the sum is the fixed 64-leaf
+// tree: eight blocks ((t0+t1)+(t2+t3))+((t4+t5)+(t6+t7)), then the blocks'
+// tree.  Blocks past len are +0.0 (their adds change nothing but a zero's
+// sign, which the top level reproduces by adding the +0.0 as the oracle
+// does).  X(l): x_l (a per-lane load), Y(l): y_l (a readlane at a constant
+// lane); a block's 8 loads go out together.
+template <class FX, class FY>
+RDEV double wdot(FX X, FY Y, int len) {
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, tot = 0.0;  // the blocks' tree: pending block, pair, quad
+#pragma unroll 1
+    for (int b = 0; b < 8; ++b) {
+        double B = 0.0;
+        if (8 * b < len) {
+            double x[8], t[8];
 #pragma unroll
-        for (int L = 0; L < 7; ++L) {
-            if (cnt & (1 << L)) {
-                v = st[L] + v;
+            for (int u = 0; u < 8; ++u) x[u] = X(8 * b + u < len ? 8 * b + u : len - 1);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) t[u] = 8 * b + u < len ? fma(x[u], Y(8 * b + u), 0.0) : 0.0;
+            B = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
+        }
+        if ((b & 1) == 0) {
+            s0 = B;
+        } else {
+            const double pr = s0 + B;
+            if ((b & 2) == 0) {
+                s1 = pr;
             } else {
-                st[L] = v;
-                break;
+                const double qd = s1 + pr;
+                if ((b & 4) == 0) s2 = qd;
+                else tot = s2 + qd;
             }
         }
-        ++cnt;
     }
-    double t = 0.0;
-    bool have = false;
-#pragma unroll
-    for (int L = 0; L < 7; ++L)
-        if (cnt & (1 << L)) {
-            t = have ? st[L] + t : st[L];
-            have = true;
-        }
-    return t;
+    return tot;
 }
 
 // ------------------------------------------------------------ LDS state
@@ -146,16 +178,11 @@ struct RS {
     double* W;      // refactor work: 2 * kc * kc
     double *lb, *ub, *cost, *xval;  // nv
     double *dw, *dprev;             // n + m
-    double *b, *xr, *asgn, *y, *rho, *acol, *z, *alU, *aF, *yy, *rhoY;  // m
-    double *xs, *alS, *aR, *v, *tv, *fS;  // kc
     double *dvec, *avec, *ct, *cb, *ca, *cr;  // n + m
-    int *cover, *rpos, *Rl, *Yl, *ypos;  // m
-    int *Sl, *perm;                      // kc
-    int* spos;                           // n
-    int *cj, *flips;                     // n + m
-    int8_t *vst, *calive;                // nv, n + m
+    int* spos;                      // n
+    int *cj, *flips;                // n + m
+    int8_t *vst, *calive;           // nv, n + m
 };
-// carve dynamic LDS (base may be null: only the size is wanted)
 __host__ __device__ inline size_t r_carve(RS& s, char* base, int m, int n) {
     s.m = m;
     s.n = n;
@@ -179,7 +206,7 @@ __host__ __device__ inline size_t r_carve(RS& s, char* base, int m, int n) {
         off += cnt;
         off = (off + 7) & ~(size_t)7;
     };
-    const size_t mm = m > 0 ? m : 1, nm = (size_t)n + m, kc = s.kc;
+    const size_t nm = (size_t)n + m, kc = s.kc;
     dd(s.A, (size_t)s.lda * n);
     dd(s.Mi, (size_t)s.ldm * kc);
     dd(s.W, 2 * kc * kc);
@@ -189,36 +216,12 @@ __host__ __device__ inline size_t r_carve(RS& s, char* base, int m, int n) {
     dd(s.xval, s.nv);
     dd(s.dw, nm);
     dd(s.dprev, nm);
-    dd(s.b, mm);
-    dd(s.xr, mm);
-    dd(s.asgn, mm);
-    dd(s.y, mm);
-    dd(s.rho, mm);
-    dd(s.acol, mm);
-    dd(s.z, mm);
-    dd(s.alU, mm);
-    dd(s.aF, mm);
-    dd(s.yy, mm);
-    dd(s.rhoY, mm);
-    dd(s.xs, kc);
-    dd(s.alS, kc);
-    dd(s.aR, kc);
-    dd(s.v, kc);
-    dd(s.tv, kc);
-    dd(s.fS, kc);
     dd(s.dvec, nm);
     dd(s.avec, nm);
     dd(s.ct, nm);
     dd(s.cb, nm);
     dd(s.ca, nm);
     dd(s.cr, nm);
-    ii(s.cover, mm);
-    ii(s.rpos, mm);
-    ii(s.Rl, mm);
-    ii(s.Yl, mm);
-    ii(s.ypos, mm);
-    ii(s.Sl, kc);
-    ii(s.perm, kc);
     ii(s.spos, n);
     ii(s.cj, nm);
     ii(s.flips, nm);
@@ -227,7 +230,16 @@ __host__ __device__ inline size_t r_carve(RS& s, char* base, int m, int n) {
     return off;
 }
 
-// the uniform scalars of the loop (every lane holds the same values)
+// the lane-resident vectors (lane r: row r; lane p: bump position / Y slot p)
+struct RV {
+    double b, xr, asgn, y;      // row
+    int cover, rpos, ypos;      // row
+    int Sl, Rl, Yl;             // position / slot
+    double xs;                  // position
+    double acol, z, alU;        // FTRAN of the entering column (row)
+    double alS;                 // (position)
+};
+// the uniform scalars of the loop
 struct RC {
     int phase;  // 1 primal phase 1, 2 primal phase 2, 3 dual phase 1 (h->phase)
     int k, ny;
@@ -245,242 +257,231 @@ struct RC {
     int64_t trace_cap;
 };
 
-RDEV double r_usign(const RS& s, int var, int row) { return var >= s.n + s.m ? s.asgn[row] : 1.0; }
+RDEV double r_usign(const RS& s, const RV& v, int var) { return var >= s.n + s.m ? v.asgn : 1.0; }  // (row lane)
 RDEV double r_colA(const RS& s, int i, int j) {
     return j < s.n ? s.A[i + (size_t)j * s.lda] : (i == j - s.n ? 1.0 : 0.0);
 }
-// zchunk_row: z_i = sum_p A[i, S_p] w_p, chunks of 32 positions
-RDEV double r_zchunk(const RS& s, int i, const double* w, int k) {
+// lane r: z_r = sum_p A[r, S_p] w_p in zchunk order (w: per-position register)
+RDEV double r_zchunk(const RS& s, const RV& v, int r, double w, int k) {
     double tot = 0.0;
     for (int c0 = 0; c0 < k; c0 += ZCHUNK) {
-        double acc = 0.0;
         const int c1 = c0 + ZCHUNK < k ? c0 + ZCHUNK : k;
-        for (int p = c0; p < c1; ++p) acc = fma(s.A[i + (size_t)s.Sl[p] * s.lda], w[p], acc);
+        double acc = 0.0;
+        for (int p0 = c0; p0 < c1; p0 += 8) {
+            double a[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int p = p0 + u < c1 ? p0 + u : c1 - 1;
+                a[u] = s.A[r + (size_t)rli(v.Sl, p) * s.lda];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (p0 + u < c1) acc = fma(a[u], rl(w, p0 + u), acc);
+        }
         tot = tot + acc;
     }
     return tot;
 }
-// row p of Minv . w (wave order over the k positions)
-RDEV double r_minv_row_dot(const RS& s, int p, const double* w, int k) {
-    const double* row = s.Mi + (size_t)p * s.ldm;
-    return lane_wave_dot([&](int i, double acc) { return fma(row[i], w[i], acc); }, k);
+// lane p: row p of Minv . w (wave order over the k positions; w per position)
+RDEV double r_minv_row(const RS& s, int p, double w, int k) {
+    const double* row = s.Mi + (size_t)(p < k ? p : 0) * s.ldm;
+    return wdot([&](int l) { return row[l]; }, [&](int l) { return rl(w, l); }, k);
 }
-// column c of Minv . w (row_times_minv / BTRAN: one wave per c over rows of Minv^T)
-RDEV double r_minv_col_dot(const RS& s, int c, const double* w, int k) {
-    const double* col = s.Mi + c;
+// lane c: column c of Minv . w (BTRAN / row_times_minv: wave order over rows)
+RDEV double r_minv_col(const RS& s, int c, double w, int k) {
+    const double* col = s.Mi + (c < k ? c : 0);
     const int ld = s.ldm;
-    return lane_wave_dot([&](int i, double acc) { return fma(col[(size_t)i * ld], w[i], acc); }, k);
+    return wdot([&](int l) { return col[(size_t)l * ld]; }, [&](int l) { return rl(w, l); }, k);
 }
 
 // ------------------------------------------------------------ refactor
-RDEV bool r_gauss_jordan(RS& s, RC& c) {
+// M = A[R, S] into W (k x k) -- lane c: column c
+RDEV void r_load_M(const RS& s, const RV& v, int k, double* W) {
+    const int lane = threadIdx.x;
+    const double* col = s.A + (size_t)(lane < k ? v.Sl : 0) * s.lda;
+    for (int a = 0; a < k; ++a) {
+        const int ra = rli(v.Rl, a);
+        if (lane < k) W[(size_t)a * k + lane] = col[ra];
+    }
+    R_FENCE();
+}
+RDEV bool r_gauss_jordan(RS& s, const RV& v, RC& c) {
     const int k = c.k, lane = threadIdx.x;
-    double* W = s.W;               // k x k, row-major (ld k)
-    double* q = s.W + (size_t)k * k;  // row p's quotients (k), then the factors (k)
-    double* f = q + k;
-    for (int e = lane; e < k * k; e += RW) {
-        const int a = e / k, cc = e - a * k;
-        W[e] = s.A[s.Rl[a] + (size_t)s.Sl[cc] * s.lda];
-    }
-    for (int r = lane; r < k; r += RW) s.calive[r] = 0;  // (used rows)
-    RSYNC();
+    double* W = s.W;  // k x k, row-major (ld k), in place
+    r_load_M(s, v, k, W);
+    bool used = false;  // (lane r: row r used)
+    int perm = 0;       // (lane c: the pivot row of column c)
     for (int col = 0; col < k; ++col) {
-        double bv = -1.0;
-        int br = 0x7fffffff;
-        for (int r = lane; r < k; r += RW) {
-            if (s.calive[r]) continue;
-            const double a = fabs(W[(size_t)r * k + col]);
-            if (a > bv) {  // (ascending r per lane: the lowest row on ties)
-                bv = a;
-                br = r;
-            }
-        }
-        const int wl = r_argbest<false>(br != 0x7fffffff, bv, br);
-        const int p = wl >= 0 ? r_rli(br, wl) : 0;
-        const double piv = W[(size_t)p * k + col];
+        const double wv = lane < k ? W[(size_t)lane * k + col] : 0.0;
+        const bool cand = lane < k && !used;
+        const int pl = r_argbest<false>(cand, fabs(wv), lane);  // largest |W[r][c]|, lowest row
+        const int p = pl >= 0 ? pl : 0;
+        const double piv = rl(wv, p);
         if (!(fabs(piv) > c.tol_singular)) return false;
-        for (int j = lane; j < k; j += RW) q[j] = W[(size_t)p * k + j] / piv;
-        for (int r = lane; r < k; r += RW) f[r] = W[(size_t)r * k + col];
-        if (lane == 0) {
-            s.perm[col] = p;
-            s.calive[p] = 1;
+        if (lane == col) perm = p;
+        if (lane == p) used = true;
+        const double q = lane < k ? W[(size_t)p * k + lane] / piv : 0.0;  // row p's quotient of column lane
+        const double f = wv;                                                // row lane's factor
+        R_FENCE();
+        for (int r = 0; r < k; ++r) {  // row r: every column j = lane
+            const double fr = rl(f, r);
+            if (lane >= k) continue;
+            double& x = W[(size_t)r * k + lane];
+            if (r == p) x = lane == col ? 1.0 / piv : q;
+            else if (lane == col) x = -(fr / piv);
+            else if (fr != 0.0 && q != 0.0) x = fma(-fr, q, x);
         }
-        RSYNC();
-        for (int e = lane; e < k * k; e += RW) {
-            const int r = e / k, j = e - r * k;
-            double& x = W[e];
-            if (r == p) {
-                x = j == col ? 1.0 / piv : q[j];
-            } else if (j == col) {
-                x = -(f[r] / piv);
-            } else {
-                const double fr = f[r], qj = q[j];
-                if (fr != 0.0 && qj != 0.0) x = fma(-fr, qj, x);
-            }
-        }
-        RSYNC();
+        R_FENCE();
     }
-    for (int e = lane; e < k * k; e += RW) {
-        const int a = e / k, cc = e - a * k;
-        s.Mi[(size_t)a * s.ldm + s.perm[cc]] = W[(size_t)s.perm[a] * k + cc];
+    // Minv[a][perm[c]] = W[perm[a]][c]: lane c writes column perm[c]
+    for (int a = 0; a < k; ++a) {
+        const int pa = rli(perm, a);
+        if (lane < k) s.Mi[(size_t)a * s.ldm + perm] = W[(size_t)pa * k + lane];
     }
-    RSYNC();
+    R_FENCE();
     return true;
 }
 // one Newton-Schulz correction; false: the residual is too large
-RDEV bool r_newton_schulz(RS& s, RC& c) {
+RDEV bool r_newton_schulz(RS& s, const RV& v, RC& c) {
     const int k = c.k, lane = threadIdx.x;
-    double* E = s.W;
-    double* N = s.W + (size_t)k * k;
+    double* M = s.W;
+    double* E = s.W + (size_t)k * k;
+    r_load_M(s, v, k, M);
     double emax = 0.0;
-    for (int e = lane; e < k * k; e += RW) {
-        const int i = e / k, j = e - i * k;
-        const int ri = s.Rl[i];
-        double acc = 0.0;  // (M Minv)_ij, seq over l
-        for (int l = 0; l < k; ++l) acc = fma(s.A[ri + (size_t)s.Sl[l] * s.lda], s.Mi[(size_t)l * s.ldm + j], acc);
-        const double ev = (i == j ? 1.0 : 0.0) - acc;
-        E[e] = ev;
-        emax = fmax(emax, fabs(ev));
+    for (int i = 0; i < k; ++i) {  // E[i][j], lane j: (M Minv)_ij seq over l
+        double acc = 0.0;
+        if (lane < k)
+            for (int l = 0; l < k; ++l) acc = fma(M[(size_t)i * k + l], s.Mi[(size_t)l * s.ldm + lane], acc);
+        const double ev = (i == lane ? 1.0 : 0.0) - acc;
+        if (lane < k) {
+            E[(size_t)i * k + lane] = ev;
+            emax = fmax(emax, fabs(ev));
+        }
     }
     emax = r_wmax(emax);
     if (emax > c.emax_max) c.emax_max = emax;
     if (!(emax <= NS_TOL)) return false;
-    RSYNC();
-    for (int e = lane; e < k * k; e += RW) {
-        const int i = e / k, j = e - i * k;
-        double acc = s.Mi[(size_t)i * s.ldm + j];
-        for (int l = 0; l < k; ++l) acc = fma(s.Mi[(size_t)i * s.ldm + l], E[(size_t)l * k + j], acc);
-        N[e] = acc;
+    R_FENCE();
+    for (int i = 0; i < k; ++i) {  // Minv_new[i][j] = Minv[i][j] + sum_l Minv[i][l] E[l][j], row by row in place
+        double acc = 0.0;
+        if (lane < k) {
+            acc = s.Mi[(size_t)i * s.ldm + lane];
+            for (int l = 0; l < k; ++l) acc = fma(s.Mi[(size_t)i * s.ldm + l], E[(size_t)l * k + lane], acc);
+        }
+        R_FENCE();
+        if (lane < k) s.Mi[(size_t)i * s.ldm + lane] = acc;
+        R_FENCE();
     }
-    RSYNC();
-    for (int e = lane; e < k * k; e += RW) {
-        const int i = e / k, j = e - i * k;
-        s.Mi[(size_t)i * s.ldm + j] = N[e];
-    }
-    RSYNC();
     return true;
 }
 // oracle refactor(): the inverse corrected or rebuilt, then x_B from b
-RDEV bool r_refactor(RS& s, RC& c, int refactor_mode) {
+RDEV bool r_refactor(RS& s, RV& v, RC& c, int refactor_mode) {
     const int k = c.k, m = s.m, n = s.n, lane = threadIdx.x;
     if (k > 0) {
-        if (refactor_mode != 0 || !r_newton_schulz(s, c)) {
+        if (refactor_mode != 0 || !r_newton_schulz(s, v, c)) {
             c.gj++;
-            if (!r_gauss_jordan(s, c)) return false;
+            if (!r_gauss_jordan(s, v, c)) return false;
         }
     }
-    for (int i = lane; i < m; i += RW) {
-        double acc = 0.0;  // nonzero nonbasic structurals, ascending j
-        for (int j = 0; j < n; ++j) {
-            const double xj = s.xval[j];
-            if (s.vst[j] != VS_BASIC && xj != 0.0) acc = fma(s.A[i + (size_t)j * s.lda], xj, acc);
+    double acc = 0.0;  // lane r: nonzero nonbasic structurals, ascending j
+    for (int j0 = 0; j0 < n; j0 += 8) {
+        double a[8], x[8];
+        bool on[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int j = j0 + u < n ? j0 + u : n - 1;
+            a[u] = lane < m ? s.A[lane + (size_t)j * s.lda] : 0.0;
+            x[u] = s.xval[j];
+            on[u] = j0 + u < n && s.vst[j] != VS_BASIC;
         }
-        double r = s.b[i] - acc;
-        if (s.vst[n + i] != VS_BASIC) r = r - s.xval[n + i];
-        s.acol[i] = r;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (on[u] && x[u] != 0.0) acc = fma(a[u], x[u], acc);
     }
-    RSYNC();
-    for (int p = lane; p < k; p += RW) s.aR[p] = s.acol[s.Rl[p]];
-    RSYNC();
-    for (int p = lane; p < k; p += RW) s.xs[p] = r_minv_row_dot(s, p, s.aR, k);
-    RSYNC();
-    for (int i = lane; i < m; i += RW) {
-        const int u = s.cover[i];
-        if (u >= 0) s.xr[i] = r_usign(s, u, i) * (s.acol[i] - r_zchunk(s, i, s.xs, k));
-    }
+    double r = v.b - acc;
+    if (lane < m && s.vst[n + lane] != VS_BASIC) r = r - s.xval[n + lane];
+    v.acol = r;
+    const double aR = shf(v.acol, v.Rl & 63);  // (position lane)
+    v.xs = lane < k ? r_minv_row(s, lane, aR, k) : v.xs;
+    if (lane < m && v.cover >= 0) v.xr = r_usign(s, v, v.cover) * (v.acol - r_zchunk(s, v, lane, v.xs, k));
     c.refactors++;
-    RSYNC();
+    R_FENCE();
     return true;
 }
 
 // y = B^-T c_B (oracle btran): covered rows sigma_u c_u, R rows Minv^T t
-RDEV void r_btran(RS& s, RC& c, int phase) {
+RDEV void r_btran(RS& s, RV& v, RC& c, int phase) {
     const int k = c.k, m = s.m, lane = threadIdx.x;
-    for (int i = lane; i < m; i += RW) {
-        const int u = s.cover[i];
-        s.y[i] = u >= 0 ? r_usign(s, u, i) * s.cost[u] : 0.0;
-    }
-    RSYNC();
-    for (int p = lane; p < k; p += RW) {
-        const int sp = s.Sl[p];
+    v.y = (lane < m && v.cover >= 0) ? r_usign(s, v, v.cover) * s.cost[v.cover] : 0.0;
+    double t = 0.0;  // lane p
+    if (lane < k) {
+        t = s.cost[v.Sl];
         if (phase == 1) {
-            const double* col = s.A + (size_t)sp * s.lda;
-            const double* y = s.y;
-            s.tv[p] = s.cost[sp] - lane_wave_dot([&](int i, double acc) { return fma(col[i], y[i], acc); }, m);
-        } else {
-            s.tv[p] = s.cost[sp];
+            const double* col = s.A + (size_t)v.Sl * s.lda;
+            const double yv = v.y;
+            t = t - wdot([&](int i) { return col[i]; }, [&](int i) { return rl(yv, i); }, m);
         }
     }
-    RSYNC();
-    for (int p = lane; p < k; p += RW) s.fS[p] = r_minv_col_dot(s, p, s.tv, k);  // (fS: scratch)
-    RSYNC();
-    for (int p = lane; p < k; p += RW) s.y[s.Rl[p]] = s.fS[p];
-    RSYNC();
+    const double yR = r_minv_col(s, lane, t, k);  // lane p
+    const double g = shf(yR, v.rpos & 63);
+    if (lane < m && v.rpos >= 0) v.y = g;
 }
 
-// phase-1 infeasibility sum (oracle art_sum: wave order)
-RDEV double r_art_sum(const RS& s) {
+// phase-1 infeasibility sum (oracle art_sum: wave order, one row per lane)
+RDEV double r_art_sum(const RS& s, const RV& v) {
     const int lane = threadIdx.x;
     double acc = 0.0;
-    for (int i = lane; i < s.m; i += RW)
-        if (s.cover[i] >= s.n + s.m) acc = acc + s.xr[i];
-    acc = acc + r_dpp<0xB1>(acc);  // (the GPU wave tree: pairs, then pairs of pairs, ...)
-    acc = acc + r_dpp<0x4E>(acc);
-    acc = acc + r_dpp<0x141>(acc);
-    acc = acc + r_dpp<0x140>(acc);
-    acc = acc + r_swz16(acc);
-    return r_rl(acc, 0) + r_rl(acc, 32);
+    if (lane < s.m && v.cover >= s.n + s.m) acc = acc + v.xr;
+    return r_wtree(acc);
 }
 
-// FTRAN of column q: alpha_S (bump), alpha_U on covered rows (oracle run_phase)
-RDEV void r_ftran(RS& s, const RC& c, int q, const double* aq /* null: column q of A or the unit */) {
-    const int k = c.k, m = s.m, n = s.n, lane = threadIdx.x;
-    for (int i = lane; i < m; i += RW) s.acol[i] = aq ? aq[i] : r_colA(s, i, q);
-    (void)n;
-    RSYNC();
-    for (int p = lane; p < k; p += RW) s.aR[p] = s.acol[s.Rl[p]];
-    RSYNC();
-    for (int p = lane; p < k; p += RW) s.alS[p] = r_minv_row_dot(s, p, s.aR, k);
-    RSYNC();
-    for (int i = lane; i < m; i += RW) {
-        const int u = s.cover[i];
-        if (u < 0) continue;
-        const double z = r_zchunk(s, i, s.alS, k);
-        s.z[i] = z;
-        s.alU[i] = r_usign(s, u, i) * (s.acol[i] - z);
+// FTRAN of column q: alpha_S (positions), alpha_U on covered rows
+RDEV void r_ftran(const RS& s, RV& v, const RC& c, int q) {
+    const int k = c.k, m = s.m, lane = threadIdx.x;
+    v.acol = lane < m ? r_colA(s, lane, q) : 0.0;
+    const double aR = shf(v.acol, v.Rl & 63);
+    v.alS = lane < k ? r_minv_row(s, lane, aR, k) : 0.0;
+    v.z = 0.0;
+    v.alU = 0.0;
+    if (lane < m && v.cover >= 0) {
+        v.z = r_zchunk(s, v, lane, v.alS, k);
+        v.alU = r_usign(s, v, v.cover) * (v.acol - v.z);
     }
-    RSYNC();
 }
-// v = A[i, S] Minv (oracle row_times_minv)
-RDEV void r_row_times_minv(RS& s, const RC& c, int i) {
-    const int k = c.k, lane = threadIdx.x;
-    for (int p = lane; p < k; p += RW) s.aR[p] = s.A[i + (size_t)s.Sl[p] * s.lda];
-    RSYNC();
-    for (int cc = lane; cc < k; cc += RW) s.v[cc] = r_minv_col_dot(s, cc, s.aR, k);
-    RSYNC();
+// lane c: A[i, S] Minv (oracle row_times_minv)
+RDEV double r_row_times_minv(const RS& s, const RV& v, int k, int i) {
+    const int lane = threadIdx.x;
+    const double aR = lane < k ? s.A[i + (size_t)v.Sl * s.lda] : 0.0;
+    return r_minv_col(s, lane, aR, k);
 }
 
-RDEV void r_y_append(RS& s, RC& c, int i) {
-    if (threadIdx.x == 0) {
-        s.Yl[c.ny] = i;
-        s.ypos[i] = c.ny;
-    }
+RDEV void r_y_append(RV& v, RC& c, int i) {
+    const int lane = threadIdx.x;
+    if (lane == c.ny) v.Yl = i;
+    if (lane == i) v.ypos = c.ny;
     c.ny++;
 }
-RDEV void r_y_remove(RS& s, RC& c, int i) {
-    if (threadIdx.x == 0) {
-        const int p = s.ypos[i], last = c.ny - 1;
-        if (p != last) {
-            s.Yl[p] = s.Yl[last];
-            s.ypos[s.Yl[p]] = p;
-        }
-        s.ypos[i] = -1;
+RDEV void r_y_remove(RV& v, RC& c, int i) {
+    const int lane = threadIdx.x;
+    const int p = rli(v.ypos, i), last = c.ny - 1;
+    if (p != last) {
+        const int moved = rli(v.Yl, last);
+        if (lane == p) v.Yl = moved;
+        if (lane == moved) v.ypos = p;
     }
+    if (lane == i) v.ypos = -1;
     c.ny--;
+}
+// y_r = fma(f, u(rpos_r), y_r) on the rows of R (u: per position), position skip excepted
+RDEV void r_dual_upd(const RS& s, RV& v, double f, double u, int skip) {
+    const int lane = threadIdx.x;
+    const double g = shf(u, v.rpos & 63);
+    if (lane < s.m && v.rpos >= 0 && v.rpos != skip) v.y = fma(f, g, v.y);
 }
 
 // oracle basis_change (cases A-E, the zero rule, phase 2: the dual update)
-RDEV bool r_basis_change(RS& s, RC& c, int phase, int q, int lv, int lrow, int lpos, double dq, double xq) {
+RDEV bool r_basis_change(RS& s, RV& v, RC& c, int phase, int q, int lv, int lrow, int lpos, double dq,
+                         double xq) {
     const int m = s.m, n = s.n, k = c.k, lane = threadIdx.x;
     const size_t ld = s.ldm;
     const bool leave_art = lv >= n + m;
@@ -488,164 +489,138 @@ RDEV bool r_basis_change(RS& s, RC& c, int phase, int q, int lv, int lrow, int l
     if (q < n) {
         if (lpos >= 0) {  // case A: structural replaces structural at position p
             const int p = lpos;
-            const double piv = s.alS[p];
-            for (int j = lane; j < k; j += RW) s.v[j] = Mi[(size_t)p * ld + j] / piv;
-            RSYNC();
-            if (phase == 2)
-                for (int j = lane; j < k; j += RW) s.y[s.Rl[j]] = fma(dq, s.v[j], s.y[s.Rl[j]]);
-            for (int e = lane; e < k * k; e += RW) {
-                const int i = e / k, j = e - i * k;
-                if (i == p) continue;
-                const double wi = s.alS[i], vj = s.v[j];
-                if (wi != 0.0 && vj != 0.0) Mi[(size_t)i * ld + j] = fma(-wi, vj, Mi[(size_t)i * ld + j]);
+            const double piv = rl(v.alS, p);
+            const double vv = lane < k ? Mi[(size_t)p * ld + lane] / piv : 0.0;
+            if (phase == 2) r_dual_upd(s, v, dq, vv, -1);
+            R_FENCE();
+            for (int i = 0; i < k; ++i) {
+                const double wi = rl(v.alS, i);
+                if (i == p || wi == 0.0) continue;
+                if (lane < k && vv != 0.0) Mi[(size_t)i * ld + lane] = fma(-wi, vv, Mi[(size_t)i * ld + lane]);
             }
-            RSYNC();
-            for (int j = lane; j < k; j += RW) Mi[(size_t)p * ld + j] = s.v[j];
+            if (lane < k) Mi[(size_t)p * ld + lane] = vv;
+            if (lane == p) {
+                v.Sl = q;
+                v.xs = xq;
+            }
             if (lane == 0) {
                 s.spos[lv] = -1;
-                s.Sl[p] = q;
                 s.spos[q] = p;
-                s.xs[p] = xq;
             }
         } else {  // case B: structural enters, the unit variable of row i leaves
             const int i = lrow;
-            const double delta = s.acol[i] - s.z[i];
-            r_row_times_minv(s, c, i);
-            for (int cc = lane; cc < k; cc += RW) s.v[cc] = s.v[cc] / delta;
-            RSYNC();
+            const double delta = rl(v.acol, i) - rl(v.z, i);
+            const double vv = r_row_times_minv(s, v, k, i) / delta;
             if (phase == 2) {
-                for (int cc = lane; cc < k; cc += RW) s.y[s.Rl[cc]] = fma(-dq, s.v[cc], s.y[s.Rl[cc]]);
-                if (lane == 0) s.y[i] = dq / delta;
+                r_dual_upd(s, v, -dq, vv, -1);
+                if (lane == i) v.y = dq / delta;
             }
-            for (int e = lane; e < k * k; e += RW) {
-                const int a = e / k, cc = e - a * k;
-                const double wa = s.alS[a], vc = s.v[cc];
-                if (wa != 0.0 && vc != 0.0) Mi[(size_t)a * ld + cc] = fma(wa, vc, Mi[(size_t)a * ld + cc]);
+            R_FENCE();
+            for (int a = 0; a < k; ++a) {
+                const double wa = rl(v.alS, a);
+                if (wa == 0.0) continue;
+                if (lane < k && vv != 0.0) Mi[(size_t)a * ld + lane] = fma(wa, vv, Mi[(size_t)a * ld + lane]);
             }
-            RSYNC();
-            for (int a = lane; a < k; a += RW) Mi[(size_t)a * ld + k] = -(s.alS[a] / delta);
-            for (int cc = lane; cc < k; cc += RW) Mi[(size_t)k * ld + cc] = -s.v[cc];
+            if (lane < k) {
+                Mi[(size_t)lane * ld + k] = -(v.alS / delta);
+                Mi[(size_t)k * ld + lane] = -vv;
+            }
             if (lane == 0) {
                 Mi[(size_t)k * ld + k] = 1.0 / delta;
-                s.Rl[k] = i;
-                s.rpos[i] = k;
-                s.Sl[k] = q;
                 s.spos[q] = k;
-                s.xs[k] = xq;
-                s.cover[i] = -1;
+            }
+            if (lane == k) {
+                v.Rl = i;
+                v.Sl = q;
+                v.xs = xq;
+            }
+            if (lane == i) {
+                v.rpos = k;
+                v.cover = -1;
             }
             c.k = k + 1;
-            if (!leave_art) r_y_append(s, c, i);
+            if (!leave_art) r_y_append(v, c, i);
         }
     } else {
         const int i0 = q - n;
-        const int a = s.rpos[i0];
+        const int a = rli(v.rpos, i0);
         if (a < 0) {  // case E: the slack replaces the artificial of its own row
             if (lrow != i0) return false;
-            if (lane == 0) {
-                s.cover[i0] = q;
-                s.xr[i0] = xq;
+            if (lane == i0) {
+                v.cover = q;
+                v.xr = xq;
             }
         } else if (lpos >= 0) {  // case C: slack of row i0 (in R) enters, structural at b leaves
             const int b = lpos, last = k - 1;
             const double piv = Mi[(size_t)b * ld + a];
-            for (int cc = lane; cc < k; cc += RW) s.v[cc] = Mi[(size_t)b * ld + cc] / piv;
-            RSYNC();
-            if (phase == 2)
-                for (int cc = lane; cc < k; cc += RW)
-                    if (cc != a) s.y[s.Rl[cc]] = fma(dq, s.v[cc], s.y[s.Rl[cc]]);
-            for (int e = lane; e < k * k; e += RW) {
-                const int r = e / k, cc = e - r * k;
-                if (r == b || cc == a) continue;
-                const double f = Mi[(size_t)r * ld + a], vc = s.v[cc];
-                if (f != 0.0 && vc != 0.0) Mi[(size_t)r * ld + cc] = fma(-f, vc, Mi[(size_t)r * ld + cc]);
+            const double vv = lane < k ? Mi[(size_t)b * ld + lane] / piv : 0.0;
+            if (phase == 2) r_dual_upd(s, v, dq, vv, a);
+            R_FENCE();
+            for (int r = 0; r < k; ++r) {
+                if (r == b) continue;
+                const double f = Mi[(size_t)r * ld + a];
+                if (f == 0.0) continue;
+                if (lane < k && lane != a && vv != 0.0) Mi[(size_t)r * ld + lane] = fma(-f, vv, Mi[(size_t)r * ld + lane]);
             }
-            RSYNC();
-            if (phase == 2 && lane == 0) s.y[i0] = 0.0;
+            R_FENCE();
+            if (phase == 2 && lane == i0) v.y = 0.0;
+            const int sl_last = rli(v.Sl, last), rl_last = rli(v.Rl, last);
+            const double xs_last = rl(v.xs, last);
             if (b != last) {
-                for (int cc = lane; cc < k; cc += RW) Mi[(size_t)b * ld + cc] = Mi[(size_t)last * ld + cc];
-                if (lane == 0) {
-                    s.Sl[b] = s.Sl[last];
-                    s.spos[s.Sl[b]] = b;
-                    s.xs[b] = s.xs[last];
+                if (lane < k) Mi[(size_t)b * ld + lane] = Mi[(size_t)last * ld + lane];
+                if (lane == b) {
+                    v.Sl = sl_last;
+                    v.xs = xs_last;
                 }
+                if (lane == 0) s.spos[sl_last] = b;
             }
-            RSYNC();
+            R_FENCE();
             if (a != last) {
-                for (int r = lane; r < k; r += RW) Mi[(size_t)r * ld + a] = Mi[(size_t)r * ld + last];
-                if (lane == 0) {
-                    s.Rl[a] = s.Rl[last];
-                    s.rpos[s.Rl[a]] = a;
-                }
+                if (lane < k) Mi[(size_t)lane * ld + a] = Mi[(size_t)lane * ld + last];
+                if (lane == a) v.Rl = rl_last;
+                if (lane == rl_last) v.rpos = a;
             }
-            if (lane == 0) {
-                s.spos[lv] = -1;
-                s.rpos[i0] = -1;
-                s.cover[i0] = q;
-                s.xr[i0] = xq;
+            if (lane == 0) s.spos[lv] = -1;
+            if (lane == i0) {
+                v.rpos = -1;
+                v.cover = q;
+                v.xr = xq;
             }
             c.k = k - 1;
         } else {  // case D: slack of row i0 (in R) enters, unit variable of row i1 leaves
             const int i1 = lrow;
-            r_row_times_minv(s, c, i1);
-            const double piv = s.v[a];
+            const double vv = r_row_times_minv(s, v, k, i1);
+            const double piv = rl(vv, a);
             if (phase == 2) {
                 const double w = dq / piv;
-                for (int cc = lane; cc < k; cc += RW)
-                    if (cc != a) s.y[s.Rl[cc]] = fma(w, s.v[cc], s.y[s.Rl[cc]]);
-                if (lane == 0) {
-                    s.y[i0] = 0.0;
-                    s.y[i1] = -w;
-                }
+                r_dual_upd(s, v, w, vv, a);
+                if (lane == i0) v.y = 0.0;
+                if (lane == i1) v.y = -w;
             }
-            for (int r = lane; r < k; r += RW) s.tv[r] = Mi[(size_t)r * ld + a] / piv;
-            RSYNC();
-            for (int e = lane; e < k * k; e += RW) {
-                const int r = e / k, cc = e - r * k;
-                if (cc == a) continue;
-                const double f = s.tv[r], vc = s.v[cc];
-                if (f != 0.0 && vc != 0.0) Mi[(size_t)r * ld + cc] = fma(-f, vc, Mi[(size_t)r * ld + cc]);
+            const double tr = lane < k ? Mi[(size_t)lane * ld + a] / piv : 0.0;  // (lane r)
+            R_FENCE();
+            for (int r = 0; r < k; ++r) {
+                const double f = rl(tr, r);
+                if (f == 0.0) continue;
+                if (lane < k && lane != a && vv != 0.0) Mi[(size_t)r * ld + lane] = fma(-f, vv, Mi[(size_t)r * ld + lane]);
             }
-            RSYNC();
-            for (int r = lane; r < k; r += RW) Mi[(size_t)r * ld + a] = s.tv[r];
-            if (lane == 0) {
-                s.Rl[a] = i1;
-                s.rpos[i1] = a;
-                s.rpos[i0] = -1;
-                s.cover[i1] = -1;
-                s.cover[i0] = q;
-                s.xr[i0] = xq;
+            if (lane < k) Mi[(size_t)lane * ld + a] = tr;
+            if (lane == a) v.Rl = i1;
+            if (lane == i1) {
+                v.rpos = a;
+                v.cover = -1;
+            }
+            if (lane == i0) {
+                v.rpos = -1;
+                v.cover = q;
+                v.xr = xq;
             }
         }
-        RSYNC();
-        r_y_remove(s, c, i0);
-        RSYNC();
-        if (a >= 0 && lpos < 0 && !leave_art) r_y_append(s, c, lrow);
+        r_y_remove(v, c, i0);
+        if (a >= 0 && lpos < 0 && !leave_art) r_y_append(v, c, lrow);
     }
-    RSYNC();
+    R_FENCE();
     return true;
-}
-
-// pricing of structural j: d_j = c_j - y'a_j (price slot classes over the Y
-// rows, or CSC's column chain over the nonzero rows)
-RDEV double r_price_col(const RS& s, const RC& c, int j, bool mode1) {
-    const double* col = s.A + (size_t)j * s.lda;
-    if (mode1) {
-        double acc = 0.0;
-        for (int i = 0; i < s.m; ++i) {
-            const double a = col[i];
-            if (a != 0.0) acc = fma(a, s.y[i], acc);
-        }
-        return s.cost[j] - acc;
-    }
-    double tot = 0.0;
-#pragma unroll
-    for (int w = 0; w < PRICE_SPLIT; ++w) {
-        double pw = 0.0;
-        for (int p = w; p < c.ny; p += PRICE_SPLIT) pw = fma(col[s.Yl[p]], s.yy[p], pw);
-        tot = tot + pw;
-    }
-    return s.cost[j] - tot;
 }
 
 RDEV void r_trace(const Dev& d, const RC& c, int a, int b) {
@@ -656,30 +631,71 @@ RDEV void r_trace(const Dev& d, const RC& c, int a, int b) {
 }
 RDEV void r_dw_reset(RS& s) {
     for (int j = threadIdx.x; j < s.n + s.m; j += RW) s.dw[j] = 1.0;
+    R_FENCE();
 }
 
-enum { R_CONT = 0, R_EXIT = 1, R_RECHECK = 2, R_TO_P2 = 3 };
+// pricing sums of structural j: the price slot classes over the Y rows (yY:
+// y on the slot of this lane) or CSC's column chain over the nonzero rows
+RDEV double r_price_sum(const RS& s, const RV& v, const RC& c, int j, bool mode1, double yY) {
+    const double* col = s.A + (size_t)j * s.lda;
+    if (mode1) {
+        double acc = 0.0;
+        for (int i0 = 0; i0 < s.m; i0 += 8) {
+            double a[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a[u] = col[i0 + u < s.m ? i0 + u : s.m - 1];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (i0 + u < s.m && a[u] != 0.0) acc = fma(a[u], rl(v.y, i0 + u), acc);
+        }
+        return acc;
+    }
+    double pw[PRICE_SPLIT] = {0.0, 0.0, 0.0, 0.0};
+    const int ny = c.ny;
+    for (int p0 = 0; p0 < ny; p0 += 2 * PRICE_SPLIT) {
+        double a[2 * PRICE_SPLIT];
+#pragma unroll
+        for (int w = 0; w < 2 * PRICE_SPLIT; ++w) a[w] = col[rli(v.Yl, p0 + w < ny ? p0 + w : ny - 1)];
+#pragma unroll
+        for (int w = 0; w < 2 * PRICE_SPLIT; ++w)
+            if (p0 + w < ny) pw[w % PRICE_SPLIT] = fma(a[w], rl(yY, p0 + w), pw[w % PRICE_SPLIT]);
+    }
+    double tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < PRICE_SPLIT; ++w) tot = tot + pw[w];
+    return tot;
+}
 
-// one primal iteration (oracle run_phase body after the loop top)
-RDEV int r_primal(const Dev& d, RS& s, RC& c, bool mode1, int refactor_mode) {
+enum { R_CONT = 0, R_EXIT = 1, R_RECHECK = 2, R_TO_P2 = 3, R_PIVOT = 4 };
+
+// the pivot an iteration chose: entering q (reduced cost dq, its Devex
+// weight qw, direction sig), the leaving variable and entry, the new value of
+// q; the dual's leaving row (CHUZR) rides along
+struct Piv {
+    int q, lv, lrow, lpos;
+    double dq, qw, sig, xq;
+    int rv, re, rs;
+    double rx, rbeta, qt, qa;
+};
+
+// primal pricing (oracle run_phase, after the loop top and BTRAN): the
+// entering column, or the phase's end
+RDEV int r_primal_select(const Dev& d, RS& s, RV& v, RC& c, bool mode1, Piv& P) {
     const int m = s.m, n = s.n, lane = threadIdx.x;
     const int ph = c.phase;
-    if (ph == 1 || !c.y_valid) {
-        c.y_valid = 1;
-        r_btran(s, c, ph);
-    }
-    if (!mode1) {
-        for (int p = lane; p < c.ny; p += RW) s.yy[p] = s.y[s.Yl[p]];
-        RSYNC();
-    }
+    const double yY = mode1 ? 0.0 : shf(v.y, v.Yl & 63);  // (slot lane: y on its Y row)
     const double dtol = c.tol_dual;
     const bool devex = c.devex != 0;
     int bq = 0x7fffffff;
     double bscore = 0.0, bd = 0.0, bw = 1.0;
-    for (int j = lane; j < n + m; j += RW) {
+    for (int j0 = 0; j0 < n + m; j0 += RW) {
+        const int j = j0 + lane;
+        const double sum = j0 < n ? r_price_sum(s, v, c, j < n ? j : n - 1, mode1, yY) : 0.0;
+        const double yslack = shf(v.y, (j - n) & 63);
+        if (j >= n + m) continue;
         const int8_t vs = s.vst[j];
         if (vs == VS_BASIC || s.lb[j] == s.ub[j]) continue;
-        const double dj = j < n ? r_price_col(s, c, j, mode1) : s.cost[j] - s.y[j - n];
+        const double dj = j < n ? s.cost[j] - sum : s.cost[j] - yslack;
         double wj = 1.0;
         if (devex) {
             wj = s.dw[j];
@@ -706,20 +722,12 @@ RDEV int r_primal(const Dev& d, RS& s, RC& c, bool mode1, int refactor_mode) {
             bw = wj;
         }
     }
+    R_FENCE();
     c.price_bytes += mode1 ? 12.0 * (double)d.nnz + 17.0 * n : 8.0 * ((double)c.ny * n + n + c.ny);
     const bool have = bq != 0x7fffffff;
     const int wl = c.bland ? r_argminid(have, bq) : r_argbest<false>(have, bscore, bq);
-    RSYNC();  // (dw / dprev written; yy read)
     if (wl < 0) {
-        if (ph == 2 && c.since > 0) {  // optimal under updated duals: confirm
-            if (!r_refactor(s, c, refactor_mode)) {
-                c.status = ST_NUMFAIL;
-                return R_EXIT;
-            }
-            c.since = 0;
-            c.y_valid = 0;
-            return R_RECHECK;
-        }
+        if (ph == 2 && c.since > 0) return R_RECHECK;  // optimal under updated duals: confirm
         if (ph == 1) {
             if (c.art_sum > c.tol_inf) {
                 c.status = ST_PHASE_OPT;  // (the host: infeasible)
@@ -730,63 +738,67 @@ RDEV int r_primal(const Dev& d, RS& s, RC& c, bool mode1, int refactor_mode) {
         c.status = ST_PHASE_OPT;
         return R_EXIT;
     }
-    const int q = r_rli(bq, wl);
-    const double dq = r_rl(bd, wl), qw = r_rl(bw, wl);
-    const double sig = dq < 0.0 ? 1.0 : -1.0;
-    const int k = c.k;
-    r_ftran(s, c, q, nullptr);
-    // Harris two-pass ratio test (textbook under Bland)
+    P.q = rli(bq, wl);
+    P.dq = rl(bd, wl);
+    P.qw = rl(bw, wl);
+    P.sig = P.dq < 0.0 ? 1.0 : -1.0;
+    return R_PIVOT;
+}
+
+// primal ratio test and update (after the FTRAN of P.q)
+RDEV int r_primal_finish(const Dev& d, RS& s, RV& v, RC& c, Piv& P) {
+    const int m = s.m, n = s.n, lane = threadIdx.x;
+    const int ph = c.phase, k = c.k, q = P.q;
+    const double dq = P.dq, qw = P.qw, sig = P.sig;
+    const bool devex = c.devex != 0;
+    // Harris two-pass ratio test (textbook under Bland) over each lane's two
+    // basic entries: its covered row (e = lane), its bump position (e = m + lane)
     const double ptol = c.tol_primal, pivtol = c.tol_pivot;
+    int evar[2], ee[2];
+    double eg[2], rr[2];
+    bool ok[2];
+    evar[0] = lane < m ? v.cover : -1;
+    ee[0] = lane;
+    eg[0] = sig * v.alU;
+    evar[1] = lane < k ? v.Sl : -1;
+    ee[1] = m + lane;
+    eg[1] = sig * v.alS;
+    const double ex[2] = {v.xr, v.xs};
     double tmax = R_INF;
-    for (int e = lane; e < m + k; e += RW) {
-        int var;
-        double g, x;
-        if (e < m) {
-            var = s.cover[e];
-            if (var < 0) continue;
-            g = sig * s.alU[e];
-            x = s.xr[e];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        ok[h] = false;
+        rr[h] = 0.0;
+        if (evar[h] < 0) continue;
+        const double l = s.lb[evar[h]], u = s.ub[evar[h]], g = eg[h], x = ex[h];
+        double r1;
+        if (g > pivtol && l > -R_INF) {
+            r1 = c.bland ? (x - l) / g : (x - l + ptol) / g;
+            rr[h] = (x - l) / g;
+        } else if (g < -pivtol && u < R_INF) {
+            r1 = c.bland ? (u - x) / (-g) : (u - x + ptol) / (-g);
+            rr[h] = (u - x) / (-g);
         } else {
-            var = s.Sl[e - m];
-            g = sig * s.alS[e - m];
-            x = s.xs[e - m];
+            continue;
         }
-        const double l = s.lb[var], u = s.ub[var];
-        double r;
-        if (g > pivtol && l > -R_INF) r = c.bland ? (x - l) / g : (x - l + ptol) / g;
-        else if (g < -pivtol && u < R_INF) r = c.bland ? (u - x) / (-g) : (u - x + ptol) / (-g);
-        else continue;
-        if (r < tmax) tmax = r;
+        ok[h] = true;
+        if (r1 < tmax) tmax = r1;
     }
     tmax = r_wmin(tmax);
     int lv = -1, le = 0;
     double lg = 0.0, lr = 0.0;
-    for (int e = lane; e < m + k; e += RW) {
-        int var;
-        double g, x;
-        if (e < m) {
-            var = s.cover[e];
-            if (var < 0) continue;
-            g = sig * s.alU[e];
-            x = s.xr[e];
-        } else {
-            var = s.Sl[e - m];
-            g = sig * s.alS[e - m];
-            x = s.xs[e - m];
-        }
-        const double l = s.lb[var], u = s.ub[var];
-        double r;
-        if (g > pivtol && l > -R_INF) r = (x - l) / g;
-        else if (g < -pivtol && u < R_INF) r = (u - x) / (-g);
-        else continue;
-        if (!(r <= tmax)) continue;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (!ok[h] || !(rr[h] <= tmax)) continue;
+        const int var = evar[h];
+        const double g = eg[h], r = rr[h];
         bool take;
         if (lv < 0) take = true;
         else if (c.bland) take = (r < lr) || (r == lr && var < lv);
         else take = (fabs(g) > fabs(lg)) || (fabs(g) == fabs(lg) && var < lv);
         if (take) {
             lv = var;
-            le = e;
+            le = ee[h];
             lg = g;
             lr = r;
         }
@@ -794,10 +806,10 @@ RDEV int r_primal(const Dev& d, RS& s, RC& c, bool mode1, int refactor_mode) {
     const bool lhave = lv >= 0;
     const int ll = c.bland ? r_argbest<true>(lhave, lr, lv) : r_argbest<false>(lhave, fabs(lg), lv);
     if (ll >= 0) {
-        lv = r_rli(lv, ll);
-        le = r_rli(le, ll);
-        lg = r_rl(lg, ll);
-        lr = r_rl(lr, ll);
+        lv = rli(lv, ll);
+        le = rli(le, ll);
+        lg = rl(lg, ll);
+        lr = rl(lr, ll);
     } else {
         lv = -1;
     }
@@ -807,9 +819,8 @@ RDEV int r_primal(const Dev& d, RS& s, RC& c, bool mode1, int refactor_mode) {
     if (ph == 1) c.phase1_iters++;
     c.iter_bytes += 8.0 * (6.0 * k * k + (double)m * k + 2.0 * n + 2.0 * m);
     if (flip < R_INF && flip <= theta) {  // bound flip
-        for (int i = lane; i < m; i += RW)
-            if (s.cover[i] >= 0) s.xr[i] = fma(-flip, sig * s.alU[i], s.xr[i]);
-        for (int p = lane; p < k; p += RW) s.xs[p] = fma(-flip, sig * s.alS[p], s.xs[p]);
+        if (lane < m && v.cover >= 0) v.xr = fma(-flip, sig * v.alU, v.xr);
+        if (lane < k) v.xs = fma(-flip, sig * v.alS, v.xs);
         if (lane == 0) {
             if (s.vst[q] == VS_LOWER) {
                 s.vst[q] = VS_UPPER;
@@ -824,7 +835,7 @@ RDEV int r_primal(const Dev& d, RS& s, RC& c, bool mode1, int refactor_mode) {
         c.dv_valid = 0;
         c.ndegen = 0;
         c.bland = 0;
-        RSYNC();
+        R_FENCE();
         return R_CONT;
     }
     if (theta == R_INF) {
@@ -856,12 +867,11 @@ RDEV int r_primal(const Dev& d, RS& s, RC& c, bool mode1, int refactor_mode) {
         c.ndegen = 0;
         c.bland = 0;
     }
-    for (int i = lane; i < m; i += RW)
-        if (s.cover[i] >= 0) s.xr[i] = fma(-theta, sig * s.alU[i], s.xr[i]);
-    for (int p = lane; p < k; p += RW) s.xs[p] = fma(-theta, sig * s.alS[p], s.xs[p]);
+    if (lane < m && v.cover >= 0) v.xr = fma(-theta, sig * v.alU, v.xr);
+    if (lane < k) v.xs = fma(-theta, sig * v.alS, v.xs);
     const double xq = s.xval[q] + sig * theta;
     const bool at_lower = lg > 0.0;
-    RSYNC();
+    R_FENCE();
     if (lane == 0) {
         if (lv >= n + m) {
             s.lb[lv] = 0.0;
@@ -875,36 +885,29 @@ RDEV int r_primal(const Dev& d, RS& s, RC& c, bool mode1, int refactor_mode) {
         }
         s.vst[q] = VS_BASIC;
     }
-    RSYNC();
-    const int lrow = le < m ? le : -1, lpos = le < m ? -1 : le - m;
-    if (!r_basis_change(s, c, ph, q, lv, lrow, lpos, dq, xq)) {
-        c.status = ST_NUMFAIL;
-        return R_EXIT;
-    }
-    c.since++;
-    return R_CONT;
+    R_FENCE();
+    P.lv = lv;
+    P.lrow = le < m ? le : -1;
+    P.lpos = le < m ? -1 : le - m;
+    P.xq = xq;
+    return R_PIVOT;
 }
 
-// one dual iteration (oracle run_dual body after the loop top)
-RDEV int r_dual(const Dev& d, RS& s, RC& c, bool mode1, int refactor_mode) {
+// dual CHUZR, pivot row, bound-flipping ratio test and the flips (oracle
+// run_dual, after the loop top): the entering column, or the phase's end
+RDEV int r_dual_select(const Dev& d, RS& s, RV& v, RC& c, bool mode1, Piv& P) {
     const int m = s.m, n = s.n, lane = threadIdx.x;
     const double ptol = c.tol_primal, dtol = c.tol_dual, pivtol = c.tol_pivot;
     const bool devex = c.ddevex != 0;
-    int k = c.k;
-    // ---- CHUZR
+    const int k = c.k;
+    // ---- CHUZR over this lane's covered row and bump position
     int rv = -1, re = 0, rs = 0;
     double rscore = 0.0, rx = 0.0, rbeta = 0.0;
-    for (int e = lane; e < m + k; e += RW) {
-        int var;
-        double x;
-        if (e < m) {
-            var = s.cover[e];
-            if (var < 0) continue;
-            x = s.xr[e];
-        } else {
-            var = s.Sl[e - m];
-            x = s.xs[e - m];
-        }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int var = h == 0 ? (lane < m ? v.cover : -1) : (lane < k ? v.Sl : -1);
+        if (var < 0) continue;
+        const double x = h == 0 ? v.xr : v.xs;
         const double l = s.lb[var], u = s.ub[var];
         double delta, beta;
         int sd;
@@ -926,7 +929,7 @@ RDEV int r_dual(const Dev& d, RS& s, RC& c, bool mode1, int refactor_mode) {
         else take = score > rscore || (score == rscore && var < rv);
         if (take) {
             rv = var;
-            re = e;
+            re = h == 0 ? lane : m + lane;
             rscore = score;
             rx = x;
             rbeta = beta;
@@ -935,82 +938,77 @@ RDEV int r_dual(const Dev& d, RS& s, RC& c, bool mode1, int refactor_mode) {
     }
     const bool rh = rv >= 0;
     const int wl = c.bland ? r_argminid(rh, rv) : r_argbest<false>(rh, rscore, rv);
-    if (wl < 0) {
-        if (c.since > 0) {  // updated values: confirm on a fresh x_B
-            if (!r_refactor(s, c, refactor_mode)) {
-                c.status = ST_NUMFAIL;
-                return R_EXIT;
-            }
-            c.since = 0;
-            r_btran(s, c, 2);
-            return R_RECHECK;
-        }
-        return R_TO_P2;
-    }
-    rv = r_rli(rv, wl);
-    re = r_rli(re, wl);
-    rs = r_rli(rs, wl);
-    rx = r_rl(rx, wl);
-    rbeta = r_rl(rbeta, wl);
-    // ---- rho_r
+    if (wl < 0) return c.since > 0 ? R_RECHECK : R_TO_P2;  // (recheck: confirm on a fresh x_B)
+    rv = rli(rv, wl);
+    re = rli(re, wl);
+    rs = rli(rs, wl);
+    rx = rl(rx, wl);
+    rbeta = rl(rbeta, wl);
+    // ---- rho_r (per position), then on the rows
     int xrow = -1;
-    double xsig = 0.0;
+    double xsig = 0.0, vv;
     if (re >= m) {
-        for (int cc = lane; cc < k; cc += RW) s.v[cc] = s.Mi[(size_t)(re - m) * s.ldm + cc];
+        vv = lane < k ? s.Mi[(size_t)(re - m) * s.ldm + lane] : 0.0;
     } else {
         xrow = re;
-        xsig = r_usign(s, s.cover[re], re);
-        r_row_times_minv(s, c, re);
-        for (int cc = lane; cc < k; cc += RW) s.v[cc] = -(xsig * s.v[cc]);
+        xsig = rli(v.cover, re) >= n + m ? rl(v.asgn, re) : 1.0;
+        vv = -(xsig * r_row_times_minv(s, v, k, re));
     }
-    for (int i = lane; i < m; i += RW) s.rho[i] = 0.0;
-    RSYNC();
-    for (int cc = lane; cc < k; cc += RW) s.rho[s.Rl[cc]] = s.v[cc];
-    if (xrow >= 0 && lane == 0) s.rho[xrow] = xsig;
-    RSYNC();
+    double rho = shf(vv, v.rpos & 63);
+    if (!(lane < m && v.rpos >= 0)) rho = 0.0;
+    if (lane == xrow) rho = xsig;
     // ---- one sweep: d_j (y) and alpha_j (rho)
-    if (!mode1) {
-        for (int p = lane; p < c.ny; p += RW) {
-            s.yy[p] = s.y[s.Yl[p]];
-            s.rhoY[p] = s.rho[s.Yl[p]];
-        }
-        RSYNC();
-    }
-    for (int j = lane; j < n; j += RW) {
+    const double yY = mode1 ? 0.0 : shf(v.y, v.Yl & 63), rY = mode1 ? 0.0 : shf(rho, v.Yl & 63);
+    for (int j0 = 0; j0 < n; j0 += RW) {
+        const int j = j0 + lane < n ? j0 + lane : n - 1;
         const double* col = s.A + (size_t)j * s.lda;
+        double td = 0.0, ta = 0.0;
         if (mode1) {
-            double ad = 0.0, aa = 0.0;
-            for (int i = 0; i < m; ++i) {
-                const double a = col[i];
-                if (a == 0.0) continue;
-                ad = fma(a, s.y[i], ad);
-                aa = fma(a, s.rho[i], aa);
+            for (int i0 = 0; i0 < m; i0 += 8) {
+                double a[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) a[u] = col[i0 + u < m ? i0 + u : m - 1];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (i0 + u < m && a[u] != 0.0) {
+                        td = fma(a[u], rl(v.y, i0 + u), td);
+                        ta = fma(a[u], rl(rho, i0 + u), ta);
+                    }
             }
-            s.dvec[j] = s.cost[j] - ad;
-            s.avec[j] = aa;
         } else {
-            double td = 0.0, ta = 0.0;
+            double pd[PRICE_SPLIT] = {0.0, 0.0, 0.0, 0.0}, pa[PRICE_SPLIT] = {0.0, 0.0, 0.0, 0.0};
+            const int ny = c.ny;
+            for (int p0 = 0; p0 < ny; p0 += 2 * PRICE_SPLIT) {
+                double a[2 * PRICE_SPLIT];
+#pragma unroll
+                for (int w = 0; w < 2 * PRICE_SPLIT; ++w) a[w] = col[rli(v.Yl, p0 + w < ny ? p0 + w : ny - 1)];
+#pragma unroll
+                for (int w = 0; w < 2 * PRICE_SPLIT; ++w)
+                    if (p0 + w < ny) {
+                        pd[w % PRICE_SPLIT] = fma(a[w], rl(yY, p0 + w), pd[w % PRICE_SPLIT]);
+                        pa[w % PRICE_SPLIT] = fma(a[w], rl(rY, p0 + w), pa[w % PRICE_SPLIT]);
+                    }
+            }
+            double sd2 = 0.0, sa = 0.0;
 #pragma unroll
             for (int w = 0; w < PRICE_SPLIT; ++w) {
-                double pd = 0.0, pa = 0.0;
-                for (int p = w; p < c.ny; p += PRICE_SPLIT) {
-                    const double a = col[s.Yl[p]];
-                    pd = fma(a, s.yy[p], pd);
-                    pa = fma(a, s.rhoY[p], pa);
-                }
-                td = td + pd;
-                ta = ta + pa;
+                sd2 = sd2 + pd[w];
+                sa = sa + pa[w];
             }
+            td = sd2;
+            ta = xrow >= 0 ? fma(xsig, col[xrow], sa) : sa;
+        }
+        if (j0 + lane < n) {
             s.dvec[j] = s.cost[j] - td;
-            s.avec[j] = xrow >= 0 ? fma(xsig, col[xrow], ta) : ta;
+            s.avec[j] = ta;
         }
     }
-    for (int i = lane; i < m; i += RW) {
-        s.dvec[n + i] = s.cost[n + i] - s.y[i];
-        s.avec[n + i] = s.rho[i];
+    if (lane < m) {
+        s.dvec[n + lane] = s.cost[n + lane] - v.y;
+        s.avec[n + lane] = rho;
     }
     c.price_bytes += mode1 ? 12.0 * (double)d.nnz + 17.0 * n : 8.0 * ((double)c.ny * n + n + c.ny);
-    RSYNC();
+    R_FENCE();
     // ---- candidates, ascending id (ballot compaction)
     int nc = 0;
     for (int j0 = 0; j0 < n + m; j0 += RW) {
@@ -1045,7 +1043,7 @@ RDEV int r_dual(const Dev& d, RS& s, RC& c, bool mode1, int refactor_mode) {
         }
         nc += __popcll(bm);
     }
-    RSYNC();
+    R_FENCE();
     // ---- bound-flipping Harris ratio test
     double slope = fabs(rx - rbeta);
     int q = -1, nflip = 0;
@@ -1060,21 +1058,22 @@ RDEV int r_dual(const Dev& d, RS& s, RC& c, bool mode1, int refactor_mode) {
             }
         if (__ballot(any) == 0ull) break;
         thmax = r_wmin(thmax);
-        // the bunch: alive and exact ratio <= thmax; its boxed members' sum in ascending order
         int nq = 0;
         bool allbox = true;
         double sum = 0.0;
         for (int c0 = 0; c0 < nc; c0 += RW) {
             const int cc = c0 + lane;
-            const bool in = cc < nc && s.calive[cc] && s.ct[cc] <= thmax;
+            const int ccc = cc < nc ? cc : 0;
+            const bool in = cc < nc && s.calive[ccc] && s.ct[ccc] <= thmax;
+            const double cav = s.ca[ccc], crv = s.cr[ccc];
             unsigned long long bm = __ballot(in);
             nq += __popcll(bm);
-            if (__ballot(in && s.cr[cc < nc ? cc : 0] == R_INF)) allbox = false;
-            while (bm) {  // (uniform: every lane walks the bunch in ascending order)
+            if (__ballot(in && crv == R_INF)) allbox = false;
+            while (bm) {  // (uniform: the bunch in ascending order)
                 const int t = __ffsll((long long)bm) - 1;
                 bm &= bm - 1ull;
-                const int ct = c0 + t;
-                if (s.cr[ct] != R_INF) sum = fma(s.ca[ct], s.cr[ct], sum);
+                const double crt = rl(crv, t);
+                if (crt != R_INF) sum = fma(rl(cav, t), crt, sum);
             }
         }
         if (nq == 0) break;  // (NaN ratios only)
@@ -1090,7 +1089,7 @@ RDEV int r_dual(const Dev& d, RS& s, RC& c, bool mode1, int refactor_mode) {
                 }
                 nflip += __popcll(bm);
             }
-            RSYNC();
+            R_FENCE();
             continue;
         }
         bool h = false;
@@ -1113,7 +1112,7 @@ RDEV int r_dual(const Dev& d, RS& s, RC& c, bool mode1, int refactor_mode) {
             }
         }
         const int w2 = c.bland ? r_argbest<true>(h, bt, bj) : r_argbest<false>(h, ba, bj);
-        bc = r_rli(bc, w2);
+        bc = rli(bc, w2);
         q = s.cj[bc];
         qt = s.ct[bc];
         qa = s.avec[q];
@@ -1135,59 +1134,62 @@ RDEV int r_dual(const Dev& d, RS& s, RC& c, bool mode1, int refactor_mode) {
             const int j = s.flips[f];
             dx[f] = s.vst[j] == VS_LOWER ? s.ub[j] - s.lb[j] : s.lb[j] - s.ub[j];
         }
-        RSYNC();
-        for (int i = lane; i < m; i += RW) {
-            double acc = 0.0;
-            for (int f = 0; f < nflip; ++f) acc = fma(r_colA(s, i, s.flips[f]), dx[f], acc);
-            s.aF[i] = acc;
+        R_FENCE();
+        double aF = 0.0;  // (row lane)
+        for (int f = 0; f < nflip; ++f) {
+            const int j = s.flips[f];
+            aF = fma(lane < m ? r_colA(s, lane, j) : 0.0, dx[f], aF);
         }
-        RSYNC();
+        R_FENCE();
         for (int f = lane; f < nflip; f += RW) {
             const int j = s.flips[f];
-            const int8_t nv = s.vst[j] == VS_LOWER ? VS_UPPER : VS_LOWER;
-            s.vst[j] = nv;
-            s.xval[j] = nv == VS_LOWER ? s.lb[j] : s.ub[j];
+            const int8_t nvs = s.vst[j] == VS_LOWER ? VS_UPPER : VS_LOWER;
+            s.vst[j] = nvs;
+            s.xval[j] = nvs == VS_LOWER ? s.lb[j] : s.ub[j];
         }
-        for (int p = lane; p < k; p += RW) s.aR[p] = s.aF[s.Rl[p]];
-        RSYNC();
-        for (int p = lane; p < k; p += RW) s.fS[p] = r_minv_row_dot(s, p, s.aR, k);
-        RSYNC();
-        for (int i = lane; i < m; i += RW) {
-            const int u = s.cover[i];
-            if (u >= 0) s.xr[i] = s.xr[i] - r_usign(s, u, i) * (s.aF[i] - r_zchunk(s, i, s.fS, k));
-        }
-        for (int p = lane; p < k; p += RW) s.xs[p] = s.xs[p] - s.fS[p];
+        const double aR = shf(aF, v.Rl & 63);
+        const double fS = lane < k ? r_minv_row(s, lane, aR, k) : 0.0;
+        if (lane < m && v.cover >= 0) v.xr = v.xr - r_usign(s, v, v.cover) * (aF - r_zchunk(s, v, lane, fS, k));
+        if (lane < k) v.xs = v.xs - fS;
         c.flips += nflip;
-        RSYNC();
-        rx = re < m ? s.xr[re] : s.xs[re - m];
+        R_FENCE();
+        rx = re < m ? rl(v.xr, re) : rl(v.xs, re - m);
     }
-    const double dq = s.dvec[q];
     const int8_t vq = s.vst[q];
-    const double sig = (vq == VS_LOWER || (vq == VS_FREE && rs * qa < 0.0)) ? 1.0 : -1.0;
-    r_ftran(s, c, q, nullptr);
-    const double arq = re < m ? s.alU[re] : s.alS[re - m];
+    P.q = q;
+    P.dq = s.dvec[q];
+    P.sig = (vq == VS_LOWER || (vq == VS_FREE && rs * qa < 0.0)) ? 1.0 : -1.0;
+    P.rv = rv;
+    P.re = re;
+    P.rs = rs;
+    P.rx = rx;
+    P.rbeta = rbeta;
+    P.qt = qt;
+    return R_PIVOT;
+}
+
+// the dual update (after the FTRAN of P.q)
+RDEV int r_dual_finish(const Dev& d, RS& s, RV& v, RC& c, Piv& P) {
+    const int m = s.m, n = s.n, lane = threadIdx.x, k = c.k, q = P.q, rv = P.rv, re = P.re, rs = P.rs;
+    const bool devex = c.ddevex != 0;
+    const double sig = P.sig, rx = P.rx, rbeta = P.rbeta, qt = P.qt;
+    const double arq = re < m ? rl(v.alU, re) : rl(v.alS, re - m);
     const double step = fabs((rx - rbeta) / arq);
     r_trace(d, c, q, rv);
     if (devex) {  // dual Devex weights of the basic entries (old basis)
         const double wr = rv < n + m ? s.dw[rv] : 1.0;
-        for (int e = lane; e < m + k; e += RW) {
-            if (e == re) continue;
-            int var;
-            double ae;
-            if (e < m) {
-                var = s.cover[e];
-                if (var < 0) continue;
-                ae = s.alU[e];
-            } else {
-                var = s.Sl[e - m];
-                ae = s.alS[e - m];
-            }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int e = h == 0 ? lane : m + lane;
+            const int var = h == 0 ? (lane < m ? v.cover : -1) : (lane < k ? v.Sl : -1);
+            if (var < 0 || e == re) continue;
+            const double ae = h == 0 ? v.alU : v.alS;
             const double r = ae / arq;
             double wn = (r * r) * wr;
             if (wn > R_WMAX) wn = R_WMAX;
             if (var < n + m && wn > s.dw[var]) s.dw[var] = wn;
         }
-        RSYNC();
+        R_FENCE();
         double wq = wr / (arq * arq);
         if (wq < 1.0) wq = 1.0;
         if (wq > R_WMAX) wq = R_WMAX;
@@ -1205,48 +1207,59 @@ RDEV int r_dual(const Dev& d, RS& s, RC& c, bool mode1, int refactor_mode) {
         c.ndegen = 0;
         c.bland = 0;
     }
-    for (int i = lane; i < m; i += RW)
-        if (s.cover[i] >= 0) s.xr[i] = fma(-step, sig * s.alU[i], s.xr[i]);
-    for (int p = lane; p < k; p += RW) s.xs[p] = fma(-step, sig * s.alS[p], s.xs[p]);
+    if (lane < m && v.cover >= 0) v.xr = fma(-step, sig * v.alU, v.xr);
+    if (lane < k) v.xs = fma(-step, sig * v.alS, v.xs);
     const double xq = s.xval[q] + sig * step;
-    RSYNC();
+    R_FENCE();
     if (lane == 0) {
         const double l = s.lb[rv], u = s.ub[rv];
         s.vst[rv] = l == u ? VS_FIXED : rs > 0 ? VS_LOWER : VS_UPPER;
         s.xval[rv] = rbeta;
         s.vst[q] = VS_BASIC;
     }
-    RSYNC();
-    if (!r_basis_change(s, c, 2, q, rv, re < m ? re : -1, re < m ? -1 : re - m, dq, xq)) {
-        c.status = ST_NUMFAIL;
-        return R_EXIT;
-    }
-    c.since++;
-    return R_CONT;
+    R_FENCE();
+    P.lv = rv;
+    P.lrow = re < m ? re : -1;
+    P.lpos = re < m ? -1 : re - m;
+    P.xq = xq;
+    return R_PIVOT;
 }
 
-// the real costs and the primal phase 2 (launch_phase2 + do_refactor + BTRAN)
-RDEV bool r_to_phase2(const Dev& d, RS& s, RC& c, int price_rule, int refactor_mode) {
+// the real costs and the primal phase 2 (launch_phase2; the refactor and BTRAN follow)
+RDEV void r_to_phase2(const Dev& d, RS& s, RC& c, int price_rule) {
     const int m = s.m, n = s.n, lane = threadIdx.x;
     for (int j = lane; j < n; j += RW) s.cost[j] = d.maximize ? -d.obj[j] : d.obj[j];
-    for (int i = lane; i < m; i += RW) {
-        const int av = n + m + i;
-        s.cost[n + i] = 0.0;
+    if (lane < m) {
+        const int av = n + m + lane;
+        s.cost[n + lane] = 0.0;
         s.cost[av] = 0.0;
         s.lb[av] = 0.0;
         s.ub[av] = 0.0;
     }
     r_dw_reset(s);
-    RSYNC();
     c.dv_valid = 0;
-    if (!r_refactor(s, c, refactor_mode)) return false;
     c.phase = 2;
     c.since = 0;
     c.ndegen = 0;
     c.bland = 0;
     c.devex = price_rule == 1;
     c.y_valid = 0;
-    return true;
+}
+
+// dst[e] = src(e) for e < cnt, 8 global loads in flight per lane
+template <class T, class F>
+RDEV void r_gather(T* dst, int64_t cnt, F src) {
+    for (int64_t e0 = threadIdx.x; e0 < cnt; e0 += RW * 8) {
+        T x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t e = e0 + (int64_t)u * RW;
+            x[u] = src(e < cnt ? e : cnt - 1);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (e0 + (int64_t)u * RW < cnt) dst[e0 + (int64_t)u * RW] = x[u];
+    }
 }
 
 __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
@@ -1294,68 +1307,112 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
     c.trace_cap = d.trace ? g->trace_cap : 0;
     c.y_valid = 1;  // (the load's BTRAN, or the updated duals of the last exit)
     const int k0 = c.k, ny0 = c.ny;
-    // ---- state into LDS
+    // ---- state into LDS and registers (global loads 8 in flight per lane)
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     if (mode1) {
         for (int e = lane; e < s.lda * n; e += RW) s.A[e] = 0.0;
-        RSYNC();
-        for (int j = 0; j < n; ++j)
-            for (int64_t t = d.cptr[j] + lane; t < d.cptr[j + 1]; t += RW) s.A[d.rind[t] + (size_t)j * s.lda] = d.cval[t];
-    } else {
-        for (int j = 0; j < n; ++j)
-            for (int i = lane; i < m; i += RW) {
-                const double v = d.A[(size_t)j * m + i];
-                s.A[i + (size_t)j * s.lda] = d.srow ? ldexp(v, d.srow[i] + d.scol[j]) : v;
+        R_FENCE();
+        // lane j: column j's entries, 4 in flight
+        for (int j0 = 0; j0 < n; j0 += RW) {
+            const int j = j0 + lane < n ? j0 + lane : n - 1;
+            const int64_t c0 = d.cptr[j], c1 = j0 + lane < n ? d.cptr[j + 1] : c0;
+            for (int64_t t = c0; __ballot(t < c1); t += 4) {
+                int ri[4];
+                double vv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int64_t tt = t + u < c1 ? t + u : (c1 > c0 ? c1 - 1 : c0);
+                    ri[u] = c1 > c0 ? d.rind[tt] : 0;
+                    vv[u] = c1 > c0 ? d.cval[tt] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (t + u < c1) s.A[ri[u] + (size_t)j * s.lda] = vv[u];
             }
+        }
+    } else {
+        r_gather(s.A, (int64_t)s.lda * n, [&](int64_t e) {
+            const int64_t j = e / s.lda, i = e - j * s.lda;
+            if (i >= m) return 0.0;
+            const double x = d.A[(size_t)j * m + i];
+            return d.srow ? ldexp(x, d.srow[i] + d.scol[j]) : x;
+        });
     }
-    for (int j = lane; j < nv; j += RW) {
-        s.lb[j] = d.lb[j];
-        s.ub[j] = d.ub[j];
-        s.cost[j] = d.cost[j];
-        s.xval[j] = d.xval[j];
-        s.vst[j] = d.vstat[j];
-    }
-    for (int j = lane; j < n + m; j += RW) {
-        s.dw[j] = d.dw[j];
-        s.dprev[j] = d.dprev[j];
-    }
+    r_gather(s.lb, nv, [&](int64_t j) { return d.lb[j]; });
+    r_gather(s.ub, nv, [&](int64_t j) { return d.ub[j]; });
+    r_gather(s.cost, nv, [&](int64_t j) { return d.cost[j]; });
+    r_gather(s.xval, nv, [&](int64_t j) { return d.xval[j]; });
+    r_gather(s.vst, nv, [&](int64_t j) { return d.vstat[j]; });
+    r_gather(s.dw, (int64_t)n + m, [&](int64_t j) { return d.dw[j]; });
+    r_gather(s.dprev, (int64_t)n + m, [&](int64_t j) { return d.dprev[j]; });
     for (int j = lane; j < n; j += RW) s.spos[j] = -1;
-    for (int i = lane; i < m; i += RW) {
-        s.b[i] = d.b[i];
-        s.xr[i] = d.xr[i];
-        s.asgn[i] = d.asgn[i];
-        s.y[i] = d.y[i];
-        s.cover[i] = d.cover[i];
-        s.rpos[i] = d.rpos[i];
-        s.ypos[i] = d.ypos[i];
+    RV v;
+    const bool rowl = lane < m;
+    const int rr = rowl ? lane : 0;
+    v.b = d.b[rr];
+    v.xr = d.xr[rr];
+    v.asgn = d.asgn[rr];
+    v.y = d.y[rr];
+    v.cover = d.cover[rr];
+    v.rpos = d.rpos[rr];
+    v.ypos = d.ypos[rr];
+    v.Yl = d.Yl[lane < ny0 ? lane : 0];
+    v.Rl = d.Rl[lane < k0 ? lane : 0];
+    v.Sl = d.Sl[lane < k0 ? lane : 0];
+    v.xs = d.xs[lane < k0 ? lane : 0];
+    if (!rowl) {
+        v.b = v.xr = v.y = 0.0;
+        v.asgn = 1.0;
+        v.cover = v.rpos = v.ypos = -1;
     }
-    for (int p = lane; p < ny0; p += RW) s.Yl[p] = d.Yl[p];
-    for (int p = lane; p < k0; p += RW) {
-        s.Rl[p] = d.Rl[p];
-        s.Sl[p] = d.Sl[p];
-        s.xs[p] = d.xs[p];
+    if (lane >= ny0) v.Yl = 0;
+    if (lane >= k0) {
+        v.Rl = v.Sl = 0;
+        v.xs = 0.0;
     }
-    for (int e = lane; e < k0 * k0; e += RW) {
-        const int i = e / k0, j = e - i * k0;
-        s.Mi[(size_t)i * s.ldm + j] = d.Minv[(size_t)i * d.ldm + j];
+    v.acol = v.z = v.alU = v.alS = 0.0;
+    for (int i0 = 0; i0 < k0; i0 += 8) {
+        double x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            x[u] = lane < k0 ? d.Minv[(size_t)(i0 + u < k0 ? i0 + u : k0 - 1) * d.ldm + lane] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (i0 + u < k0 && lane < k0) s.Mi[(size_t)(i0 + u) * s.ldm + lane] = x[u];
     }
-    RSYNC();
-    for (int p = lane; p < k0; p += RW) s.spos[s.Sl[p]] = p;
+    R_FENCE();
+    if (lane < k0) s.spos[v.Sl] = lane;
     if (c.dv_valid == 2) {  // (the pipeline's deferred framework restart)
         r_dw_reset(s);
         c.dv_valid = 0;
     }
-    RSYNC();
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    int recheck = 0;
+    R_FENCE();
+    // The loop (elp_api.hip run_loop / oracle solve_core): one call site each
+    // for the refactor, BTRAN, FTRAN and basis change keeps the code small
+    // enough to stay in the instruction cache.
+    enum { RF_NONE = 0, RF_TOP, RF_RECHECK, RF_TO_P2 };
+    int recheck = 0, refac = RF_NONE;
+    Piv P;
     for (;;) {
+        if (refac != RF_NONE) {
+            if (!r_refactor(s, v, c, a.refactor_mode)) {
+                c.status = ST_NUMFAIL;
+                break;
+            }
+            c.since = 0;
+            c.y_valid = 0;
+            // after the loop top's refactor the iteration runs; a recheck skips
+            // the loop top; a new phase 2 starts at its loop top
+            recheck = refac != RF_TO_P2;
+            refac = RF_NONE;
+            continue;
+        }
         if (!recheck) {
             if (c.phase == 1) {
-                c.art_sum = r_art_sum(s);
+                c.art_sum = r_art_sum(s, v);
                 if (c.art_sum <= c.tol_inf) {
-                    if (!r_to_phase2(d, s, c, a.price_rule, a.refactor_mode)) {
-                        c.status = ST_NUMFAIL;
-                        break;
-                    }
+                    r_to_phase2(d, s, c, a.price_rule);
+                    refac = RF_TO_P2;
                     continue;
                 }
             }
@@ -1372,30 +1429,37 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
                 break;
             }
             if (c.since >= c.period) {
-                if (!r_refactor(s, c, a.refactor_mode)) {
-                    c.status = ST_NUMFAIL;
-                    break;
-                }
-                c.since = 0;
-                c.y_valid = 0;
-                if (c.phase == 3) r_btran(s, c, 2);
+                refac = RF_TOP;
+                continue;
             }
         }
         recheck = 0;
-        const int r = c.phase == 3 ? r_dual(d, s, c, mode1, a.refactor_mode) : r_primal(d, s, c, mode1, a.refactor_mode);
+        if (c.phase == 1 || !c.y_valid) {  // (phase 1: every iteration; else after a refactor)
+            c.y_valid = 1;
+            r_btran(s, v, c, c.phase == 1 ? 1 : 2);
+        }
+        int r = c.phase == 3 ? r_dual_select(d, s, v, c, mode1, P) : r_primal_select(d, s, v, c, mode1, P);
         if (r == R_EXIT) break;
         if (r == R_RECHECK) {
-            recheck = 1;
+            refac = RF_RECHECK;
             continue;
         }
         if (r == R_TO_P2) {
-            if (!r_to_phase2(d, s, c, a.price_rule, a.refactor_mode)) {
-                c.status = ST_NUMFAIL;
-                break;
-            }
+            r_to_phase2(d, s, c, a.price_rule);
+            refac = RF_TO_P2;
+            continue;
         }
+        r_ftran(s, v, c, P.q);
+        r = c.phase == 3 ? r_dual_finish(d, s, v, c, P) : r_primal_finish(d, s, v, c, P);
+        if (r == R_EXIT) break;
+        if (r == R_CONT) continue;
+        if (!r_basis_change(s, v, c, c.phase == 1 ? 1 : 2, P.q, P.lv, P.lrow, P.lpos, P.dq, P.xq)) {
+            c.status = ST_NUMFAIL;
+            break;
+        }
+        c.since++;
     }
-    RSYNC();
+    R_FENCE();
     // ---- write back in the pipeline's layout
     const int k = c.k, ny = c.ny;
     for (int j = lane; j < nv; j += RW) {
@@ -1411,52 +1475,51 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
     }
     if (d.spos)
         for (int j = lane; j < n; j += RW) d.spos[j] = s.spos[j];
-    for (int i = lane; i < m; i += RW) {
-        d.xr[i] = s.xr[i];
-        d.y[i] = s.y[i];
-        const int u = s.cover[i];
-        d.cover[i] = u;
-        d.rpos[i] = s.rpos[i];
-        d.ypos[i] = s.ypos[i];
-        if (u >= 0) {
-            d.rlo[i] = s.lb[u];
-            d.rhi[i] = s.ub[u];
+    if (rowl) {
+        d.xr[lane] = v.xr;
+        d.y[lane] = v.y;
+        d.cover[lane] = v.cover;
+        d.rpos[lane] = v.rpos;
+        d.ypos[lane] = v.ypos;
+        if (v.cover >= 0) {
+            d.rlo[lane] = s.lb[v.cover];
+            d.rhi[lane] = s.ub[v.cover];
         }
     }
-    for (int p = lane; p < ny; p += RW) {
-        const int i = s.Yl[p];
-        d.Yl[p] = i;
-        d.yvs[p] = d.rowvs[i];
-        d.yy[p] = s.y[i];
+    const double yYl = shf(v.y, v.Yl & 63);
+    if (lane < ny) {
+        d.Yl[lane] = v.Yl;
+        d.yvs[lane] = d.rowvs[v.Yl];
+        d.yy[lane] = yYl;
     }
-    for (int p = lane; p < k; p += RW) {
-        const int j = s.Sl[p];
-        d.Rl[p] = s.Rl[p];
-        d.Sl[p] = j;
-        d.xs[p] = s.xs[p];
-        d.cS[p] = s.cost[j];
-        d.slo[p] = s.lb[j];
-        d.shi[p] = s.ub[j];
+    if (lane < k) {
+        d.Rl[lane] = v.Rl;
+        d.Sl[lane] = v.Sl;
+        d.xs[lane] = v.xs;
+        d.cS[lane] = s.cost[v.Sl];
+        d.slo[lane] = s.lb[v.Sl];
+        d.shi[lane] = s.ub[v.Sl];
     }
-    for (int e = lane; e < k * k; e += RW) {
-        const int i = e / k, j = e - i * k;
-        const double v = s.Mi[(size_t)i * s.ldm + j];
-        d.Minv[(size_t)i * d.ldm + j] = v;
-        if (!d.noT) d.MinvT[(size_t)j * d.ldm + i] = v;
-    }
+    for (int i = 0; i < k; ++i)
+        if (lane < k) {
+            const double x = s.Mi[(size_t)i * s.ldm + lane];
+            d.Minv[(size_t)i * d.ldm + lane] = x;
+            if (!d.noT) d.MinvT[(size_t)lane * d.ldm + i] = x;
+        }
     for (int p = 0; p < k; ++p) {
-        const double* col = s.A + (size_t)s.Sl[p] * s.lda;
-        for (int i = lane; i < m; i += RW) d.AS[(size_t)p * m + i] = col[i];
+        const double* col = s.A + (size_t)rli(v.Sl, p) * s.lda;
+        if (rowl) d.AS[(size_t)p * m + lane] = col[lane];
     }
     if (!mode1 && d.AR) {
         const int64_t tw = d.tile_w;
         for (int p = 0; p < ny; ++p) {
-            const int i = s.Yl[p];
+            const int i = rli(v.Yl, p);
             for (int j = lane; j < n; j += RW)
                 d.AR[((size_t)(j / tw) * (size_t)d.arcap + (size_t)p) * (size_t)tw + (size_t)(j % tw)] =
                     s.A[i + (size_t)j * s.lda];
         }
     }
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {
         g->status = c.status;
         g->phase = c.phase;
@@ -1486,13 +1549,14 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
         a.out->gj_refactors = c.gj;
         a.out->devex_resets = c.resets;
         a.out->emax_max = c.emax_max;
-        a.out->ticks = (int64_t)(__builtin_amdgcn_s_memrealtime() - t0);
+        a.out->ticks = (int64_t)(t1 - t0);
     }
 }
 
 }  // namespace
 
 size_t resident_lds_bytes(int m, int n) {
+    if (m > RW) return (size_t)-1;  // (one row per lane)
     RS s;
     return r_carve(s, nullptr, m, n);
 }

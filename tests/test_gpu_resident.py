@@ -64,8 +64,8 @@ def _pair(gpu, rec, sparse=False, gctl=None, octl=None, expect_resident=True):
         ran = g.stats["resident"] == 1
         if res == 2:
             assert not ran
-        elif expect_resident and rec["A"].shape[0] >= 1:
-            assert ran, "the resident solver did not run"
+        elif expect_resident and rec["A"].shape[0] >= 1 and not np.any(np.asarray(rec["lo"]) > np.asarray(rec["up"])):
+            assert ran, "the resident solver did not run"  # (lower > upper: decided at the load)
         _same(g, o)
         out.append(g)
     return out
@@ -87,7 +87,8 @@ def test_known_answers_resident(gpu, rec, rule, simplex):
 @pytest.mark.parametrize("rec", ROBUST, ids=[r["name"] for r in ROBUST])
 def test_robust_resident(gpu, rec):
     g, _ = _pair(gpu, rec)
-    assert g.status == rec["expected"]["status"]
+    assert g.status == 0
+    assert abs(g.objval - rec["objective"]) <= 1e-9 * max(1.0, abs(rec["objective"]))
     _pair(gpu, rec, gctl={"scaling": 0, "refactor_mode": 1, "refactor_period": 7},
           octl={"scaling": 0, "refactor_mode": 1, "refactor_period": 7})
 
@@ -100,18 +101,20 @@ def test_sparse_fixtures_resident(gpu, rec):
 
 
 def test_fuzz_resident(gpu):
-    seen = set()
+    seen, ran = set(), 0
     for rec in FUZZ:
         rid = f"f{rec['seed']}_{rec['m']}x{rec['n']}"
         try:
             for sparse in (False, True):
-                g, _ = _pair(gpu, rec, sparse=sparse,
+                g, _ = _pair(gpu, rec, sparse=sparse, expect_resident=False,
                              gctl={"pricing": rec["seed"] % 2, "refactor_period": 5 + rec["seed"] % 40},
                              octl={"price_rule": rec["seed"] % 2, "refactor_period": 5 + rec["seed"] % 40})
                 seen.add(g.status)
+                ran += g.stats["resident"]
         except Exception as e:  # name the LP
             raise AssertionError(f"{rid}: {type(e).__name__}: {e}") from None
     assert {0, 2, 3} <= seen
+    assert ran >= len(FUZZ)  # (most fuzz LPs fit; the larger ones take the pipeline)
 
 
 @pytest.mark.parametrize("rule", [0, 1], ids=["dantzig", "devex"])
