@@ -1788,6 +1788,15 @@ static int run_resident(elp_handle* h, size_t lds, int32_t* lp_status, double t_
     h->stats.resident = 1;
     h->stats.resident_launches++;
     h->stats.resident_ticks += o.ticks;
+    if (o.stage[1] && std::getenv("ELP_DEBUG_RESIDENT"))  // (a -DELP_RES_PROF=1 build)
+        std::fprintf(stderr, "elp resident: %lld iterations, shader cycles top+btran %lld select %lld ftran %lld "
+                     "finish %lld basis %lld refactor %lld loop %lld; kernel %.1f us\n", (long long)c->iter,
+                     (long long)o.stage[0], (long long)o.stage[1], (long long)o.stage[2], (long long)o.stage[3],
+                     (long long)o.stage[4], (long long)o.stage[5], (long long)o.stage[7], o.ticks / 100.0);
+    if (o.stage[1] && std::getenv("ELP_DEBUG_RESIDENT"))
+        std::fprintf(stderr, "elp resident inner: ftran colA+shf %lld wdot %lld zchunk %lld; price loop %lld argbest %lld; "
+                     "ratio pass1 %lld pass2 %lld\n", (long long)o.stage2[0], (long long)o.stage2[1], (long long)o.stage2[2],
+                     (long long)o.stage2[3], (long long)o.stage2[4], (long long)o.stage2[5], (long long)o.stage2[6]);
     h->phase = o.phase;
     const int32_t s = c->status;
     h->stats.seconds_loop += now_s() - t_loop0;

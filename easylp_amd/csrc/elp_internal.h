@@ -435,6 +435,7 @@ struct ResOut {
     int64_t refactors, gj_refactors, devex_resets, ticks;
     double emax_max;
     int32_t phase, pad;
+    int64_t stage[8], stage2[8];  // diagnostic builds (-DELP_RES_PROF=1): shader cycles per loop stage
 };
 struct ResArgs {
     int32_t phase, price_rule, refactor_mode, pad;

@@ -50,6 +50,20 @@ constexpr double R_WMAX = 1e20;   // DEVEX_WMAX (oracle, elp_kernels.hip)
 constexpr double R_RESET = 1e6;   // DEVEX_RESET
 constexpr double R_INF = HUGE_VAL;
 #define R_FENCE() asm volatile("" ::: "memory")
+// diagnostic build (tools/build_variant.sh resprof "-DELP_RES_PROF=1"): shader
+// cycles (s_memtime) per loop stage, summed in ResOut::stage
+#ifndef ELP_RES_PROF
+#define ELP_RES_PROF 0
+#endif
+__shared__ unsigned long long r_prof[17];  // [16]: the last stamp
+#define R_STAMP(i)                                                        \
+    do {                                                                  \
+        if (ELP_RES_PROF && threadIdx.x == 0) {                           \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();   \
+            r_prof[i] += t_ - r_prof[16];                                 \
+            r_prof[16] = t_;                                              \
+        }                                                                 \
+    } while (0)
 
 // ------------------------------------------------------------ wave helpers
 template <int CTRL>
@@ -239,20 +253,24 @@ struct RV {
     double acol, z, alU;        // FTRAN of the entering column (row)
     double alS;                 // (position)
 };
+// run statistics, in LDS (lane 0 updates them: no registers held across the loop)
+struct RStat {
+    int64_t phase1_iters, flips, degenerate, dual_iters, refactors, gj, resets;
+    double price_bytes, iter_bytes, emax_max, unb_sig;
+    int32_t unb_var, pad;
+};
 // the uniform scalars of the loop
 struct RC {
     int phase;  // 1 primal phase 1, 2 primal phase 2, 3 dual phase 1 (h->phase)
     int k, ny;
-    int64_t iter, iter_limit, iter_stop, phase1_iters, flips, degenerate, dual_iters;
+    int64_t iter, iter_limit, iter_stop;
     int since, period, ndegen, bland, degen_switch;
     int devex, ddevex, dv_valid, dv_lv;
     double dv_dq, dv_wq;
     double tol_primal, tol_dual, tol_pivot, tol_inf, tol_singular;
-    double art_sum, unb_sig;
-    int unb_var, status;
-    double price_bytes, iter_bytes;
-    int64_t refactors, gj, resets;
-    double emax_max;
+    double art_sum;
+    int status;
+    RStat* st;
     int y_valid;
     int64_t trace_cap;
 };
@@ -359,7 +377,7 @@ RDEV bool r_newton_schulz(RS& s, const RV& v, RC& c) {
         }
     }
     emax = r_wmax(emax);
-    if (emax > c.emax_max) c.emax_max = emax;
+    if (threadIdx.x == 0 && emax > c.st->emax_max) c.st->emax_max = emax;
     if (!(emax <= NS_TOL)) return false;
     R_FENCE();
     for (int i = 0; i < k; ++i) {  // Minv_new[i][j] = Minv[i][j] + sum_l Minv[i][l] E[l][j], row by row in place
@@ -379,7 +397,7 @@ RDEV bool r_refactor(RS& s, RV& v, RC& c, int refactor_mode) {
     const int k = c.k, m = s.m, n = s.n, lane = threadIdx.x;
     if (k > 0) {
         if (refactor_mode != 0 || !r_newton_schulz(s, v, c)) {
-            c.gj++;
+            if (threadIdx.x == 0) c.st->gj++;
             if (!r_gauss_jordan(s, v, c)) return false;
         }
     }
@@ -404,7 +422,7 @@ RDEV bool r_refactor(RS& s, RV& v, RC& c, int refactor_mode) {
     const double aR = shf(v.acol, v.Rl & 63);  // (position lane)
     v.xs = lane < k ? r_minv_row(s, lane, aR, k) : v.xs;
     if (lane < m && v.cover >= 0) v.xr = r_usign(s, v, v.cover) * (v.acol - r_zchunk(s, v, lane, v.xs, k));
-    c.refactors++;
+    if (threadIdx.x == 0) c.st->refactors++;
     R_FENCE();
     return true;
 }
@@ -440,13 +458,16 @@ RDEV void r_ftran(const RS& s, RV& v, const RC& c, int q) {
     const int k = c.k, m = s.m, lane = threadIdx.x;
     v.acol = lane < m ? r_colA(s, lane, q) : 0.0;
     const double aR = shf(v.acol, v.Rl & 63);
+    R_STAMP(8);
     v.alS = lane < k ? r_minv_row(s, lane, aR, k) : 0.0;
+    R_STAMP(9);
     v.z = 0.0;
     v.alU = 0.0;
     if (lane < m && v.cover >= 0) {
         v.z = r_zchunk(s, v, lane, v.alS, k);
         v.alU = r_usign(s, v, v.cover) * (v.acol - v.z);
     }
+    R_STAMP(10);
 }
 // lane c: A[i, S] Minv (oracle row_times_minv)
 RDEV double r_row_times_minv(const RS& s, const RV& v, int k, int i) {
@@ -723,9 +744,11 @@ RDEV int r_primal_select(const Dev& d, RS& s, RV& v, RC& c, bool mode1, Piv& P) 
         }
     }
     R_FENCE();
-    c.price_bytes += mode1 ? 12.0 * (double)d.nnz + 17.0 * n : 8.0 * ((double)c.ny * n + n + c.ny);
+    R_STAMP(11);
+    if (lane == 0) c.st->price_bytes += mode1 ? 12.0 * (double)d.nnz + 17.0 * n : 8.0 * ((double)c.ny * n + n + c.ny);
     const bool have = bq != 0x7fffffff;
     const int wl = c.bland ? r_argminid(have, bq) : r_argbest<false>(have, bscore, bq);
+    R_STAMP(12);
     if (wl < 0) {
         if (ph == 2 && c.since > 0) return R_RECHECK;  // optimal under updated duals: confirm
         if (ph == 1) {
@@ -785,6 +808,7 @@ RDEV int r_primal_finish(const Dev& d, RS& s, RV& v, RC& c, Piv& P) {
         if (r1 < tmax) tmax = r1;
     }
     tmax = r_wmin(tmax);
+    R_STAMP(13);
     int lv = -1, le = 0;
     double lg = 0.0, lr = 0.0;
 #pragma unroll
@@ -813,11 +837,14 @@ RDEV int r_primal_finish(const Dev& d, RS& s, RV& v, RC& c, Piv& P) {
     } else {
         lv = -1;
     }
+    R_STAMP(14);
     const double theta = lv >= 0 ? (lr > 0.0 ? lr : 0.0) : R_INF;
     const double flip = (s.lb[q] > -R_INF && s.ub[q] < R_INF) ? s.ub[q] - s.lb[q] : R_INF;
     c.iter++;
-    if (ph == 1) c.phase1_iters++;
-    c.iter_bytes += 8.0 * (6.0 * k * k + (double)m * k + 2.0 * n + 2.0 * m);
+    if (lane == 0) {
+        if (ph == 1) c.st->phase1_iters++;
+        c.st->iter_bytes += 8.0 * (6.0 * k * k + (double)m * k + 2.0 * n + 2.0 * m);
+    }
     if (flip < R_INF && flip <= theta) {  // bound flip
         if (lane < m && v.cover >= 0) v.xr = fma(-flip, sig * v.alU, v.xr);
         if (lane < k) v.xs = fma(-flip, sig * v.alS, v.xs);
@@ -830,7 +857,7 @@ RDEV int r_primal_finish(const Dev& d, RS& s, RV& v, RC& c, Piv& P) {
                 s.xval[q] = s.lb[q];
             }
         }
-        c.flips++;
+        if (lane == 0) c.st->flips++;
         r_trace(d, c, q, -1);
         c.dv_valid = 0;
         c.ndegen = 0;
@@ -840,8 +867,10 @@ RDEV int r_primal_finish(const Dev& d, RS& s, RV& v, RC& c, Piv& P) {
     }
     if (theta == R_INF) {
         r_trace(d, c, q, -2);
-        c.unb_var = q;
-        c.unb_sig = sig;
+        if (lane == 0) {
+            c.st->unb_var = q;
+            c.st->unb_sig = sig;
+        }
         c.status = ST_UNBOUNDED;
         return R_EXIT;
     }
@@ -849,7 +878,7 @@ RDEV int r_primal_finish(const Dev& d, RS& s, RV& v, RC& c, Piv& P) {
     if (devex && qw > R_RESET) {
         r_dw_reset(s);
         c.dv_valid = 0;
-        c.resets++;
+        if (lane == 0) c.st->resets++;
     } else if (devex) {
         double wl2 = qw / (lg * lg);
         if (wl2 < 1.0) wl2 = 1.0;
@@ -861,7 +890,7 @@ RDEV int r_primal_finish(const Dev& d, RS& s, RV& v, RC& c, Piv& P) {
         c.dv_wq = qw;
     }
     if (theta == 0.0) {
-        c.degenerate++;
+        if (lane == 0) c.st->degenerate++;
         if (++c.ndegen >= c.degen_switch) c.bland = 1;
     } else {
         c.ndegen = 0;
@@ -1007,7 +1036,7 @@ RDEV int r_dual_select(const Dev& d, RS& s, RV& v, RC& c, bool mode1, Piv& P) {
         s.dvec[n + lane] = s.cost[n + lane] - v.y;
         s.avec[n + lane] = rho;
     }
-    c.price_bytes += mode1 ? 12.0 * (double)d.nnz + 17.0 * n : 8.0 * ((double)c.ny * n + n + c.ny);
+    if (lane == 0) c.st->price_bytes += mode1 ? 12.0 * (double)d.nnz + 17.0 * n : 8.0 * ((double)c.ny * n + n + c.ny);
     R_FENCE();
     // ---- candidates, ascending id (ballot compaction)
     int nc = 0;
@@ -1119,9 +1148,11 @@ RDEV int r_dual_select(const Dev& d, RS& s, RV& v, RC& c, bool mode1, Piv& P) {
         break;
     }
     c.iter++;
-    c.phase1_iters++;
-    c.dual_iters++;
-    c.iter_bytes += 8.0 * (6.0 * k * k + (double)m * k + 2.0 * n + 2.0 * m);
+    if (lane == 0) {
+        c.st->phase1_iters++;
+        c.st->dual_iters++;
+        c.st->iter_bytes += 8.0 * (6.0 * k * k + (double)m * k + 2.0 * n + 2.0 * m);
+    }
     if (q < 0) {  // the dual ray: primal infeasible
         r_trace(d, c, -2, rv);
         c.status = ST_DUALINF;
@@ -1151,7 +1182,7 @@ RDEV int r_dual_select(const Dev& d, RS& s, RV& v, RC& c, bool mode1, Piv& P) {
         const double fS = lane < k ? r_minv_row(s, lane, aR, k) : 0.0;
         if (lane < m && v.cover >= 0) v.xr = v.xr - r_usign(s, v, v.cover) * (aF - r_zchunk(s, v, lane, fS, k));
         if (lane < k) v.xs = v.xs - fS;
-        c.flips += nflip;
+        if (lane == 0) c.st->flips += nflip;
         R_FENCE();
         rx = re < m ? rl(v.xr, re) : rl(v.xs, re - m);
     }
@@ -1195,13 +1226,13 @@ RDEV int r_dual_finish(const Dev& d, RS& s, RV& v, RC& c, Piv& P) {
         if (wq > R_WMAX) wq = R_WMAX;
         if (wq > R_RESET) {
             r_dw_reset(s);
-            c.resets++;
+            if (lane == 0) c.st->resets++;
         } else if (lane == 0) {
             s.dw[q] = wq;
         }
     }
     if (!(qt > 0.0)) {
-        c.degenerate++;
+        if (lane == 0) c.st->degenerate++;
         if (++c.ndegen >= c.degen_switch) c.bland = 1;
     } else {
         c.ndegen = 0;
@@ -1276,10 +1307,20 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
     c.iter = g->iter;
     c.iter_limit = g->iter_limit;
     c.iter_stop = g->iter_stop;
-    c.phase1_iters = g->phase1_iters;
-    c.flips = g->flips;
-    c.degenerate = g->degenerate;
-    c.dual_iters = g->dual_iters;
+    __shared__ RStat r_stat;
+    c.st = &r_stat;
+    if (lane == 0) {
+        r_stat.phase1_iters = g->phase1_iters;
+        r_stat.flips = g->flips;
+        r_stat.degenerate = g->degenerate;
+        r_stat.dual_iters = g->dual_iters;
+        r_stat.unb_sig = g->unb_sig;
+        r_stat.unb_var = g->unb_var;
+        r_stat.price_bytes = g->price_bytes;
+        r_stat.iter_bytes = g->iter_bytes;
+        r_stat.refactors = r_stat.gj = r_stat.resets = 0;
+        r_stat.emax_max = 0.0;
+    }
     c.since = g->since_refactor;
     c.period = g->refactor_period;
     c.ndegen = g->ndegen;
@@ -1297,13 +1338,7 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
     c.tol_inf = g->tol_inf;
     c.tol_singular = d.tol_singular;
     c.art_sum = g->art_sum;
-    c.unb_sig = g->unb_sig;
-    c.unb_var = g->unb_var;
     c.status = ST_RUN;
-    c.price_bytes = g->price_bytes;
-    c.iter_bytes = g->iter_bytes;
-    c.refactors = c.gj = c.resets = 0;
-    c.emax_max = 0.0;
     c.trace_cap = d.trace ? g->trace_cap : 0;
     c.y_valid = 1;  // (the load's BTRAN, or the updated duals of the last exit)
     const int k0 = c.k, ny0 = c.ny;
@@ -1393,9 +1428,16 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
     enum { RF_NONE = 0, RF_TOP, RF_RECHECK, RF_TO_P2 };
     int recheck = 0, refac = RF_NONE;
     Piv P;
+    if (ELP_RES_PROF && lane == 0) {
+        for (int i = 0; i < 16; ++i) r_prof[i] = 0;
+        r_prof[16] = __builtin_amdgcn_s_memtime();
+    }
     for (;;) {
+        R_STAMP(7);
         if (refac != RF_NONE) {
-            if (!r_refactor(s, v, c, a.refactor_mode)) {
+            const bool ok = r_refactor(s, v, c, a.refactor_mode);
+            R_STAMP(5);
+            if (!ok) {
                 c.status = ST_NUMFAIL;
                 break;
             }
@@ -1438,7 +1480,9 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
             c.y_valid = 1;
             r_btran(s, v, c, c.phase == 1 ? 1 : 2);
         }
+        R_STAMP(0);
         int r = c.phase == 3 ? r_dual_select(d, s, v, c, mode1, P) : r_primal_select(d, s, v, c, mode1, P);
+        R_STAMP(1);
         if (r == R_EXIT) break;
         if (r == R_RECHECK) {
             refac = RF_RECHECK;
@@ -1450,10 +1494,14 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
             continue;
         }
         r_ftran(s, v, c, P.q);
+        R_STAMP(2);
         r = c.phase == 3 ? r_dual_finish(d, s, v, c, P) : r_primal_finish(d, s, v, c, P);
+        R_STAMP(3);
         if (r == R_EXIT) break;
         if (r == R_CONT) continue;
-        if (!r_basis_change(s, v, c, c.phase == 1 ? 1 : 2, P.q, P.lv, P.lrow, P.lpos, P.dq, P.xq)) {
+        const bool ok = r_basis_change(s, v, c, c.phase == 1 ? 1 : 2, P.q, P.lv, P.lrow, P.lpos, P.dq, P.xq);
+        R_STAMP(4);
+        if (!ok) {
             c.status = ST_NUMFAIL;
             break;
         }
@@ -1526,10 +1574,10 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
         g->k = k;
         g->ny = ny;
         g->iter = c.iter;
-        g->phase1_iters = c.phase1_iters;
-        g->flips = c.flips;
-        g->degenerate = c.degenerate;
-        g->dual_iters = c.dual_iters;
+        g->phase1_iters = r_stat.phase1_iters;
+        g->flips = r_stat.flips;
+        g->degenerate = r_stat.degenerate;
+        g->dual_iters = r_stat.dual_iters;
         g->since_refactor = c.since;
         g->ndegen = c.ndegen;
         g->bland = c.bland;
@@ -1540,16 +1588,18 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
         g->dv_dq = c.dv_dq;
         g->dv_wq = c.dv_wq;
         g->art_sum = c.art_sum;
-        g->unb_var = c.unb_var;
-        g->unb_sig = c.unb_sig;
-        g->price_bytes = c.price_bytes;
-        g->iter_bytes = c.iter_bytes;
+        g->unb_var = r_stat.unb_var;
+        g->unb_sig = r_stat.unb_sig;
+        g->price_bytes = r_stat.price_bytes;
+        g->iter_bytes = r_stat.iter_bytes;
         a.out->phase = c.phase;
-        a.out->refactors = c.refactors;
-        a.out->gj_refactors = c.gj;
-        a.out->devex_resets = c.resets;
-        a.out->emax_max = c.emax_max;
+        a.out->refactors = r_stat.refactors;
+        a.out->gj_refactors = r_stat.gj;
+        a.out->devex_resets = r_stat.resets;
+        a.out->emax_max = r_stat.emax_max;
         a.out->ticks = (int64_t)(t1 - t0);
+        for (int i = 0; i < 8; ++i) a.out->stage[i] = ELP_RES_PROF ? (int64_t)(r_prof[i] + (i == 0 ? 0 : 0)) : 0;
+        for (int i = 8; i < 16; ++i) a.out->stage2[i - 8] = ELP_RES_PROF ? (int64_t)r_prof[i] : 0;
     }
 }
 
