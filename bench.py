@@ -928,6 +928,18 @@ def main():
                 **roof,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                #  C3's live AR rows (~100 MB per sweep) stay in the
+                # 256 MiB Infinity Cache (MALL) between sweeps, and FETCH_SIZE counts
+                # its hits: the fraction above is against the 8 TB/s HBM peak, but
+                # the bytes come from the MALL.  The HBM figure is C4's 2 GB
+                # non-temporal sweep, which no cache holds (scaling_config.price_sweep)
+                "residency": "MALL-resident (C3 sweep ~100 MB < 256 MiB Infinity Cache)",
+                "hbm_sweep": ({"workload": "C4 m=10000 n=500000 pricing sweep, non-temporal loads (beyond "
+                                           "the Infinity Cache)",
+                               "achieved": c4["price_sweep"]["achieved"], "frac": c4["price_sweep"]["frac"],
+                               "avg_launch_us": c4["price_sweep"]["avg_launch_us"],
+                               "bytes_per_launch": c4["price_sweep"]["bytes_per_launch"]}
+                              if c4 and c4.get("price_sweep") else None),
             },
             "iteration_roofline": iteration_roofline(stats),
             "host_input": hosted,

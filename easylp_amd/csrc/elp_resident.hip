@@ -213,16 +213,16 @@ __host__ __device__ inline size_t r_carve(RS& s, char* base, int m, int n) {
     auto ii = [&](int*& p, size_t cnt) {
         p = (int*)(base + off);
         off += cnt * sizeof(int);
-        off = (off + 7) & ~(size_t)7;
+        off = (off + 7) & ~7;
     };
     auto bb = [&](int8_t*& p, size_t cnt) {
         p = (int8_t*)(base + off);
         off += cnt;
-        off = (off + 7) & ~(size_t)7;
+        off = (off + 7) & ~7;
     };
-    const size_t nm = (size_t)n + m, kc = s.kc;
-    dd(s.A, (size_t)s.lda * n);
-    dd(s.Mi, (size_t)s.ldm * kc);
+    const size_t nm = n + m, kc = s.kc;
+    dd(s.A, s.lda * n);
+    dd(s.Mi, s.ldm * kc);
     dd(s.W, 2 * kc * kc);
     dd(s.lb, s.nv);
     dd(s.ub, s.nv);
@@ -277,7 +277,7 @@ struct RC {
 
 RDEV double r_usign(const RS& s, const RV& v, int var) { return var >= s.n + s.m ? v.asgn : 1.0; }  // (row lane)
 RDEV double r_colA(const RS& s, int i, int j) {
-    return j < s.n ? s.A[i + (size_t)j * s.lda] : (i == j - s.n ? 1.0 : 0.0);
+    return j < s.n ? s.A[i + j * s.lda] : (i == j - s.n ? 1.0 : 0.0);
 }
 // lane r: z_r = sum_p A[r, S_p] w_p in zchunk order (w: per-position register)
 RDEV double r_zchunk(const RS& s, const RV& v, int r, double w, int k) {
@@ -290,7 +290,7 @@ RDEV double r_zchunk(const RS& s, const RV& v, int r, double w, int k) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int p = p0 + u < c1 ? p0 + u : c1 - 1;
-                a[u] = s.A[r + (size_t)rli(v.Sl, p) * s.lda];
+                a[u] = s.A[r + rli(v.Sl, p) * s.lda];
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u)
@@ -302,24 +302,24 @@ RDEV double r_zchunk(const RS& s, const RV& v, int r, double w, int k) {
 }
 // lane p: row p of Minv . w (wave order over the k positions; w per position)
 RDEV double r_minv_row(const RS& s, int p, double w, int k) {
-    const double* row = s.Mi + (size_t)(p < k ? p : 0) * s.ldm;
+    const double* row = s.Mi + (p < k ? p : 0) * s.ldm;
     return wdot([&](int l) { return row[l]; }, [&](int l) { return rl(w, l); }, k);
 }
 // lane c: column c of Minv . w (BTRAN / row_times_minv: wave order over rows)
 RDEV double r_minv_col(const RS& s, int c, double w, int k) {
     const double* col = s.Mi + (c < k ? c : 0);
     const int ld = s.ldm;
-    return wdot([&](int l) { return col[(size_t)l * ld]; }, [&](int l) { return rl(w, l); }, k);
+    return wdot([&](int l) { return col[l * ld]; }, [&](int l) { return rl(w, l); }, k);
 }
 
 // ------------------------------------------------------------ refactor
 // M = A[R, S] into W (k x k) -- lane c: column c
 RDEV void r_load_M(const RS& s, const RV& v, int k, double* W) {
     const int lane = threadIdx.x;
-    const double* col = s.A + (size_t)(lane < k ? v.Sl : 0) * s.lda;
+    const double* col = s.A + (lane < k ? v.Sl : 0) * s.lda;
     for (int a = 0; a < k; ++a) {
         const int ra = rli(v.Rl, a);
-        if (lane < k) W[(size_t)a * k + lane] = col[ra];
+        if (lane < k) W[a * k + lane] = col[ra];
     }
     R_FENCE();
 }
@@ -330,7 +330,7 @@ RDEV bool r_gauss_jordan(RS& s, const RV& v, RC& c) {
     bool used = false;  // (lane r: row r used)
     int perm = 0;       // (lane c: the pivot row of column c)
     for (int col = 0; col < k; ++col) {
-        const double wv = lane < k ? W[(size_t)lane * k + col] : 0.0;
+        const double wv = lane < k ? W[lane * k + col] : 0.0;
         const bool cand = lane < k && !used;
         const int pl = r_argbest<false>(cand, fabs(wv), lane);  // largest |W[r][c]|, lowest row
         const int p = pl >= 0 ? pl : 0;
@@ -338,13 +338,13 @@ RDEV bool r_gauss_jordan(RS& s, const RV& v, RC& c) {
         if (!(fabs(piv) > c.tol_singular)) return false;
         if (lane == col) perm = p;
         if (lane == p) used = true;
-        const double q = lane < k ? W[(size_t)p * k + lane] / piv : 0.0;  // row p's quotient of column lane
+        const double q = lane < k ? W[p * k + lane] / piv : 0.0;  // row p's quotient of column lane
         const double f = wv;                                                // row lane's factor
         R_FENCE();
         for (int r = 0; r < k; ++r) {  // row r: every column j = lane
             const double fr = rl(f, r);
             if (lane >= k) continue;
-            double& x = W[(size_t)r * k + lane];
+            double& x = W[r * k + lane];
             if (r == p) x = lane == col ? 1.0 / piv : q;
             else if (lane == col) x = -(fr / piv);
             else if (fr != 0.0 && q != 0.0) x = fma(-fr, q, x);
@@ -354,7 +354,7 @@ RDEV bool r_gauss_jordan(RS& s, const RV& v, RC& c) {
     // Minv[a][perm[c]] = W[perm[a]][c]: lane c writes column perm[c]
     for (int a = 0; a < k; ++a) {
         const int pa = rli(perm, a);
-        if (lane < k) s.Mi[(size_t)a * s.ldm + perm] = W[(size_t)pa * k + lane];
+        if (lane < k) s.Mi[a * s.ldm + perm] = W[pa * k + lane];
     }
     R_FENCE();
     return true;
@@ -363,16 +363,16 @@ RDEV bool r_gauss_jordan(RS& s, const RV& v, RC& c) {
 RDEV bool r_newton_schulz(RS& s, const RV& v, RC& c) {
     const int k = c.k, lane = threadIdx.x;
     double* M = s.W;
-    double* E = s.W + (size_t)k * k;
+    double* E = s.W + k * k;
     r_load_M(s, v, k, M);
     double emax = 0.0;
     for (int i = 0; i < k; ++i) {  // E[i][j], lane j: (M Minv)_ij seq over l
         double acc = 0.0;
         if (lane < k)
-            for (int l = 0; l < k; ++l) acc = fma(M[(size_t)i * k + l], s.Mi[(size_t)l * s.ldm + lane], acc);
+            for (int l = 0; l < k; ++l) acc = fma(M[i * k + l], s.Mi[l * s.ldm + lane], acc);
         const double ev = (i == lane ? 1.0 : 0.0) - acc;
         if (lane < k) {
-            E[(size_t)i * k + lane] = ev;
+            E[i * k + lane] = ev;
             emax = fmax(emax, fabs(ev));
         }
     }
@@ -383,11 +383,11 @@ RDEV bool r_newton_schulz(RS& s, const RV& v, RC& c) {
     for (int i = 0; i < k; ++i) {  // Minv_new[i][j] = Minv[i][j] + sum_l Minv[i][l] E[l][j], row by row in place
         double acc = 0.0;
         if (lane < k) {
-            acc = s.Mi[(size_t)i * s.ldm + lane];
-            for (int l = 0; l < k; ++l) acc = fma(s.Mi[(size_t)i * s.ldm + l], E[(size_t)l * k + lane], acc);
+            acc = s.Mi[i * s.ldm + lane];
+            for (int l = 0; l < k; ++l) acc = fma(s.Mi[i * s.ldm + l], E[l * k + lane], acc);
         }
         R_FENCE();
-        if (lane < k) s.Mi[(size_t)i * s.ldm + lane] = acc;
+        if (lane < k) s.Mi[i * s.ldm + lane] = acc;
         R_FENCE();
     }
     return true;
@@ -408,7 +408,7 @@ RDEV bool r_refactor(RS& s, RV& v, RC& c, int refactor_mode) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const int j = j0 + u < n ? j0 + u : n - 1;
-            a[u] = lane < m ? s.A[lane + (size_t)j * s.lda] : 0.0;
+            a[u] = lane < m ? s.A[lane + j * s.lda] : 0.0;
             x[u] = s.xval[j];
             on[u] = j0 + u < n && s.vst[j] != VS_BASIC;
         }
@@ -435,7 +435,7 @@ RDEV void r_btran(RS& s, RV& v, RC& c, int phase) {
     if (lane < k) {
         t = s.cost[v.Sl];
         if (phase == 1) {
-            const double* col = s.A + (size_t)v.Sl * s.lda;
+            const double* col = s.A + v.Sl * s.lda;
             const double yv = v.y;
             t = t - wdot([&](int i) { return col[i]; }, [&](int i) { return rl(yv, i); }, m);
         }
@@ -472,7 +472,7 @@ RDEV void r_ftran(const RS& s, RV& v, const RC& c, int q) {
 // lane c: A[i, S] Minv (oracle row_times_minv)
 RDEV double r_row_times_minv(const RS& s, const RV& v, int k, int i) {
     const int lane = threadIdx.x;
-    const double aR = lane < k ? s.A[i + (size_t)v.Sl * s.lda] : 0.0;
+    const double aR = lane < k ? s.A[i + v.Sl * s.lda] : 0.0;
     return r_minv_col(s, lane, aR, k);
 }
 
@@ -504,22 +504,22 @@ RDEV void r_dual_upd(const RS& s, RV& v, double f, double u, int skip) {
 RDEV bool r_basis_change(RS& s, RV& v, RC& c, int phase, int q, int lv, int lrow, int lpos, double dq,
                          double xq) {
     const int m = s.m, n = s.n, k = c.k, lane = threadIdx.x;
-    const size_t ld = s.ldm;
+    const int ld = s.ldm;
     const bool leave_art = lv >= n + m;
     double* Mi = s.Mi;
     if (q < n) {
         if (lpos >= 0) {  // case A: structural replaces structural at position p
             const int p = lpos;
             const double piv = rl(v.alS, p);
-            const double vv = lane < k ? Mi[(size_t)p * ld + lane] / piv : 0.0;
+            const double vv = lane < k ? Mi[p * ld + lane] / piv : 0.0;
             if (phase == 2) r_dual_upd(s, v, dq, vv, -1);
             R_FENCE();
             for (int i = 0; i < k; ++i) {
                 const double wi = rl(v.alS, i);
                 if (i == p || wi == 0.0) continue;
-                if (lane < k && vv != 0.0) Mi[(size_t)i * ld + lane] = fma(-wi, vv, Mi[(size_t)i * ld + lane]);
+                if (lane < k && vv != 0.0) Mi[i * ld + lane] = fma(-wi, vv, Mi[i * ld + lane]);
             }
-            if (lane < k) Mi[(size_t)p * ld + lane] = vv;
+            if (lane < k) Mi[p * ld + lane] = vv;
             if (lane == p) {
                 v.Sl = q;
                 v.xs = xq;
@@ -540,14 +540,14 @@ RDEV bool r_basis_change(RS& s, RV& v, RC& c, int phase, int q, int lv, int lrow
             for (int a = 0; a < k; ++a) {
                 const double wa = rl(v.alS, a);
                 if (wa == 0.0) continue;
-                if (lane < k && vv != 0.0) Mi[(size_t)a * ld + lane] = fma(wa, vv, Mi[(size_t)a * ld + lane]);
+                if (lane < k && vv != 0.0) Mi[a * ld + lane] = fma(wa, vv, Mi[a * ld + lane]);
             }
             if (lane < k) {
-                Mi[(size_t)lane * ld + k] = -(v.alS / delta);
-                Mi[(size_t)k * ld + lane] = -vv;
+                Mi[lane * ld + k] = -(v.alS / delta);
+                Mi[k * ld + lane] = -vv;
             }
             if (lane == 0) {
-                Mi[(size_t)k * ld + k] = 1.0 / delta;
+                Mi[k * ld + k] = 1.0 / delta;
                 s.spos[q] = k;
             }
             if (lane == k) {
@@ -573,22 +573,22 @@ RDEV bool r_basis_change(RS& s, RV& v, RC& c, int phase, int q, int lv, int lrow
             }
         } else if (lpos >= 0) {  // case C: slack of row i0 (in R) enters, structural at b leaves
             const int b = lpos, last = k - 1;
-            const double piv = Mi[(size_t)b * ld + a];
-            const double vv = lane < k ? Mi[(size_t)b * ld + lane] / piv : 0.0;
+            const double piv = Mi[b * ld + a];
+            const double vv = lane < k ? Mi[b * ld + lane] / piv : 0.0;
             if (phase == 2) r_dual_upd(s, v, dq, vv, a);
             R_FENCE();
             for (int r = 0; r < k; ++r) {
                 if (r == b) continue;
-                const double f = Mi[(size_t)r * ld + a];
+                const double f = Mi[r * ld + a];
                 if (f == 0.0) continue;
-                if (lane < k && lane != a && vv != 0.0) Mi[(size_t)r * ld + lane] = fma(-f, vv, Mi[(size_t)r * ld + lane]);
+                if (lane < k && lane != a && vv != 0.0) Mi[r * ld + lane] = fma(-f, vv, Mi[r * ld + lane]);
             }
             R_FENCE();
             if (phase == 2 && lane == i0) v.y = 0.0;
             const int sl_last = rli(v.Sl, last), rl_last = rli(v.Rl, last);
             const double xs_last = rl(v.xs, last);
             if (b != last) {
-                if (lane < k) Mi[(size_t)b * ld + lane] = Mi[(size_t)last * ld + lane];
+                if (lane < k) Mi[b * ld + lane] = Mi[last * ld + lane];
                 if (lane == b) {
                     v.Sl = sl_last;
                     v.xs = xs_last;
@@ -597,7 +597,7 @@ RDEV bool r_basis_change(RS& s, RV& v, RC& c, int phase, int q, int lv, int lrow
             }
             R_FENCE();
             if (a != last) {
-                if (lane < k) Mi[(size_t)lane * ld + a] = Mi[(size_t)lane * ld + last];
+                if (lane < k) Mi[lane * ld + a] = Mi[lane * ld + last];
                 if (lane == a) v.Rl = rl_last;
                 if (lane == rl_last) v.rpos = a;
             }
@@ -618,14 +618,14 @@ RDEV bool r_basis_change(RS& s, RV& v, RC& c, int phase, int q, int lv, int lrow
                 if (lane == i0) v.y = 0.0;
                 if (lane == i1) v.y = -w;
             }
-            const double tr = lane < k ? Mi[(size_t)lane * ld + a] / piv : 0.0;  // (lane r)
+            const double tr = lane < k ? Mi[lane * ld + a] / piv : 0.0;  // (lane r)
             R_FENCE();
             for (int r = 0; r < k; ++r) {
                 const double f = rl(tr, r);
                 if (f == 0.0) continue;
-                if (lane < k && lane != a && vv != 0.0) Mi[(size_t)r * ld + lane] = fma(-f, vv, Mi[(size_t)r * ld + lane]);
+                if (lane < k && lane != a && vv != 0.0) Mi[r * ld + lane] = fma(-f, vv, Mi[r * ld + lane]);
             }
-            if (lane < k) Mi[(size_t)lane * ld + a] = tr;
+            if (lane < k) Mi[lane * ld + a] = tr;
             if (lane == a) v.Rl = i1;
             if (lane == i1) {
                 v.rpos = a;
@@ -658,7 +658,7 @@ RDEV void r_dw_reset(RS& s) {
 // pricing sums of structural j: the price slot classes over the Y rows (yY:
 // y on the slot of this lane) or CSC's column chain over the nonzero rows
 RDEV double r_price_sum(const RS& s, const RV& v, const RC& c, int j, bool mode1, double yY) {
-    const double* col = s.A + (size_t)j * s.lda;
+    const double* col = s.A + j * s.lda;
     if (mode1) {
         double acc = 0.0;
         for (int i0 = 0; i0 < s.m; i0 += 8) {
@@ -977,7 +977,7 @@ RDEV int r_dual_select(const Dev& d, RS& s, RV& v, RC& c, bool mode1, Piv& P) {
     int xrow = -1;
     double xsig = 0.0, vv;
     if (re >= m) {
-        vv = lane < k ? s.Mi[(size_t)(re - m) * s.ldm + lane] : 0.0;
+        vv = lane < k ? s.Mi[(re - m) * s.ldm + lane] : 0.0;
     } else {
         xrow = re;
         xsig = rli(v.cover, re) >= n + m ? rl(v.asgn, re) : 1.0;
@@ -990,7 +990,7 @@ RDEV int r_dual_select(const Dev& d, RS& s, RV& v, RC& c, bool mode1, Piv& P) {
     const double yY = mode1 ? 0.0 : shf(v.y, v.Yl & 63), rY = mode1 ? 0.0 : shf(rho, v.Yl & 63);
     for (int j0 = 0; j0 < n; j0 += RW) {
         const int j = j0 + lane < n ? j0 + lane : n - 1;
-        const double* col = s.A + (size_t)j * s.lda;
+        const double* col = s.A + j * s.lda;
         double td = 0.0, ta = 0.0;
         if (mode1) {
             for (int i0 = 0; i0 < m; i0 += 8) {
@@ -1362,7 +1362,7 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
-                    if (t + u < c1) s.A[ri[u] + (size_t)j * s.lda] = vv[u];
+                    if (t + u < c1) s.A[ri[u] + j * s.lda] = vv[u];
             }
         }
     } else {
@@ -1413,7 +1413,7 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
             x[u] = lane < k0 ? d.Minv[(size_t)(i0 + u < k0 ? i0 + u : k0 - 1) * d.ldm + lane] : 0.0;
 #pragma unroll
         for (int u = 0; u < 8; ++u)
-            if (i0 + u < k0 && lane < k0) s.Mi[(size_t)(i0 + u) * s.ldm + lane] = x[u];
+            if (i0 + u < k0 && lane < k0) s.Mi[(i0 + u) * s.ldm + lane] = x[u];
     }
     R_FENCE();
     if (lane < k0) s.spos[v.Sl] = lane;
@@ -1550,12 +1550,12 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
     }
     for (int i = 0; i < k; ++i)
         if (lane < k) {
-            const double x = s.Mi[(size_t)i * s.ldm + lane];
+            const double x = s.Mi[i * s.ldm + lane];
             d.Minv[(size_t)i * d.ldm + lane] = x;
             if (!d.noT) d.MinvT[(size_t)lane * d.ldm + i] = x;
         }
     for (int p = 0; p < k; ++p) {
-        const double* col = s.A + (size_t)rli(v.Sl, p) * s.lda;
+        const double* col = s.A + rli(v.Sl, p) * s.lda;
         if (rowl) d.AS[(size_t)p * m + lane] = col[lane];
     }
     if (!mode1 && d.AR) {
@@ -1564,7 +1564,7 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
             const int i = rli(v.Yl, p);
             for (int j = lane; j < n; j += RW)
                 d.AR[((size_t)(j / tw) * (size_t)d.arcap + (size_t)p) * (size_t)tw + (size_t)(j % tw)] =
-                    s.A[i + (size_t)j * s.lda];
+                    s.A[i + j * s.lda];
         }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
@@ -1606,7 +1606,7 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
 }  // namespace
 
 size_t resident_lds_bytes(int m, int n) {
-    if (m > RW) return (size_t)-1;  // (one row per lane)
+    if (m > RW) return -1;  // (one row per lane)
     RS s;
     return r_carve(s, nullptr, m, n);
 }

@@ -55,5 +55,11 @@ python3 "$ROOT/tools/timeline.py" "$(find "$TMP/tl" -name '*kernel_trace.csv' | 
 timeout -k 10 300 python3 "$ROOT/tools/sparse_probe.py" > "$OUT/sparse_probe_$TAG.txt" 2>&1 && cat "$OUT/sparse_probe_$TAG.txt" || { echo "sparse probe failed"; exit 8; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$TMP/sp" -o run -- python3 "$ROOT/tools/sparse_probe.py" kkt_20000x100000 > "$OUT/sparse_prof_$TAG.txt" 2>&1 || { echo "sparse rocprof failed"; exit 9; }
 cp "$(find "$TMP/sp" -name '*kernel_stats.csv' | head -1)" "$OUT/sparse_kernel_stats_$TAG.csv"
+# ... and of the feasible-start (primal) solve
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$TMP/spf" -o run -- python3 "$ROOT/tools/sparse_probe.py" kkt_feasible_20000x100000 > "$OUT/feasible_prof_$TAG.txt" 2>&1 || { echo "feasible rocprof failed"; exit 10; }
+cp "$(find "$TMP/spf" -name '*kernel_stats.csv' | head -1)" "$OUT/feasible_kernel_stats_$TAG.csv"
+# the resident small-LP solver: Klee-Minty and the per-stage counters
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$TMP/km" -o run -- python3 "$ROOT/tools/resident_km.py" > "$OUT/resident_prof_$TAG.txt" 2>&1 || { echo "resident rocprof failed"; exit 11; }
+cp "$(find "$TMP/km" -name '*kernel_stats.csv' | head -1)" "$OUT/resident_kernel_stats_$TAG.csv"
 rm -rf "$TMP"
 echo done
