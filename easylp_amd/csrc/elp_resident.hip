@@ -24,7 +24,8 @@
 // basis_change, refactor, btran) and therefore to the pipeline -- the same
 // reduction shapes, evaluated per output lane: a wave_dot (64 lane-strided
 // fma chains + the pairwise tree, offsets 1, 2, ..., 32) becomes one lane's
-// terms in order folded by the same tree (a carry stack), zchunk, the price
+// terms in order folded by the same tree (wdot: the fixed 64-leaf tree in
+// blocks of eight), zchunk, the price
 // slot classes and the column chains are per-output fma chains already.  The
 // orchestration is elp_api.hip run_loop's: loop-top checks (phase-1 sum,
 // iteration cap, budget stop, time limit, refactor period), the recheck
