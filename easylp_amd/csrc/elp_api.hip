@@ -132,6 +132,15 @@ struct elp_handle {
     bool dual_used = false;  // the last load's phase 1 is the dual simplex (phase 3)
     elp::ResOut* d_resout = nullptr;  // the resident solver's exit record
     size_t res_lds_max = 0;           // LDS one workgroup may allocate (0: not queried yet)
+    // the resident solver's exit: the structurals' values (scaled) brought back
+    // with the control block; res_fresh: hctl and res_x equal the device's
+    // (nothing ran since), so the next node, elp_get_stats and
+    // elp_get_solution skip their round trips; res_warm: the next resident
+    // launch runs the node warm start first
+    double* d_resx = nullptr;
+    std::vector<double> res_x;
+    bool res_fresh = false;
+    int32_t res_warm = 0;
     std::vector<double> mip_x;   // branch and bound: the incumbent (elp_get_solution)
 };
 
@@ -1023,6 +1032,72 @@ static void scale_csc(elp_handle* h, const int64_t* cp, const int32_t* ri, doubl
     h->scol_h = std::move(gam);
 }
 
+// The same factors for a small dense A on the host (m n <= SCALE_HOST_MAX:
+// below that the device passes' launches and one synchronisation per pass cost
+// more than the arithmetic -- 0.2 ms of a 0.4 ms load at the DOP LP's 11 x 14):
+// the exponents of the nonzero finite entries once, then the passes of
+// scale_dense's kernels on them; returns the scaled copy of A.
+constexpr double SCALE_HOST_MAX = 16384.0;
+static std::vector<double> scale_dense_host(elp_handle* h, const double* A) {
+    const int64_t m = h->m, n = h->n;
+    constexpr int EMN = 0x3fffffff, EMX = -0x3fffffff, NONE = INT32_MIN;
+    std::vector<int32_t> ex((size_t)(m * n));
+    for (int64_t t = 0; t < m * n; ++t)
+        ex[(size_t)t] = (A[t] != 0.0 && std::isfinite(A[t])) ? ilogb_i(A[t]) : NONE;
+    std::vector<int32_t> rho((size_t)m, 0), gam((size_t)n, 0);
+    auto col_pass = [&](bool equil) {
+        bool changed = false;
+        for (int64_t j = 0; j < n; ++j) {
+            int mn = EMN, mx = EMX;
+            for (int64_t i = 0; i < m; ++i) {
+                const int e0 = ex[(size_t)(j * m + i)];
+                if (e0 == NONE) continue;
+                const int e = e0 + rho[(size_t)i];
+                mn = std::min(mn, e);
+                mx = std::max(mx, e);
+            }
+            const int g = mx == EMX ? 0 : equil ? -(mx + 1) : -floor_half_h(mn + mx);
+            if (g != gam[(size_t)j]) {
+                gam[(size_t)j] = g;
+                changed = true;
+            }
+        }
+        return changed;
+    };
+    auto row_pass = [&]() {
+        bool changed = false;
+        for (int64_t i = 0; i < m; ++i) {
+            int mn = EMN, mx = EMX;
+            for (int64_t j = 0; j < n; ++j) {
+                const int e0 = ex[(size_t)(j * m + i)];
+                if (e0 == NONE) continue;
+                const int e = e0 + gam[(size_t)j];
+                mn = std::min(mn, e);
+                mx = std::max(mx, e);
+            }
+            const int r = mx == EMX ? 0 : -floor_half_h(mn + mx);
+            if (r != rho[(size_t)i]) {
+                rho[(size_t)i] = r;
+                changed = true;
+            }
+        }
+        return changed;
+    };
+    if (h->ctl.scaling & ELP_SCALE_GEOMETRIC)
+        for (int pass = 0; pass < SCALE_PASSES; ++pass) {
+            const bool ch = row_pass();
+            if (!(col_pass(false) | ch)) break;
+        }
+    if (h->ctl.scaling & ELP_SCALE_EQUILIBRATE) col_pass(true);
+    std::vector<double> As((size_t)(m * n));
+    for (int64_t j = 0; j < n; ++j)
+        for (int64_t i = 0; i < m; ++i)
+            As[(size_t)(j * m + i)] = std::ldexp(A[j * m + i], rho[(size_t)i] + gam[(size_t)j]);
+    h->srow_h = std::move(rho);
+    h->scol_h = std::move(gam);
+    return As;
+}
+
 // the phase-1 method (elp_control.simplex; lp_solve's set_simplextype): the
 // dual simplex with the bump inverse, on one GPU or column-sharded
 // (elp_stats.simplex reports what ran)
@@ -1039,6 +1114,8 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
                        const double* lo, const double* up, int32_t maximize) {
     const int64_t m = h->m, n = h->n, n0 = h->col0, nl = h->nloc;
     Dev& d = h->d;
+    h->res_fresh = false;
+    h->res_warm = 0;
     load_mark(h, "A + scaling");
     for (int64_t i = 0; i < m; ++i)
         if (dir[i] < ELP_LE || dir[i] > ELP_EQ) return fail(ELP_E_ARG, "dir must be 1 (<=), 2 (>=) or 3 (==)");
@@ -1359,6 +1436,8 @@ static int64_t shard_ncols(const elp_handle* h) {
 static int prep_load(elp_handle* h, bool csc = false) {
     if (!h) return fail(ELP_E_ARG, "NULL handle");
     HIPCHK(hipSetDevice(h->dev));
+    h->res_fresh = false;
+    h->res_warm = 0;
     load_mark(h, nullptr);
     if (h->loaded) free_dev(h, true);
     load_mark(h, "free previous");
@@ -1405,11 +1484,13 @@ static H2DTarget dense_host_target(elp_handle* h) {
 }
 // part 2 (A uploaded): scaling in place, then the common tail
 static int dense_host_finish(elp_handle* h, const int32_t* dir, const double* rhs, const double* obj,
-                             const double* lo, const double* up, int32_t maximize) {
+                             const double* lo, const double* up, int32_t maximize, bool host_scaled = false) {
     HIPCHK(hipSetDevice(h->dev));
     const int64_t c0 = h->replicated ? 0 : h->col0, nc = h->replicated ? h->n : h->nloc;
-    int rc = scale_dense(h, h->A_owned, c0, nc);
-    if (rc) return rc;
+    if (!host_scaled) {
+        const int rc = scale_dense(h, h->A_owned, c0, nc);
+        if (rc) return rc;
+    }
     h->d.A = h->A_owned + (size_t)(h->col0 - c0) * (size_t)h->m;
     h->d.Afull = h->replicated ? h->A_owned : nullptr;
     return load_common(h, dir, rhs, obj, lo, up, maximize);
@@ -1439,14 +1520,19 @@ extern "C" int elp_load_dense(elp_handle* h, const double* A, const int32_t* dir
         hi_e = std::max(hi_e, tg.back().e1);
     }
     if (hi_e > lo_e) hbytes = (double)(hi_e - lo_e) * sizeof(double);
+    // a small A on one GPU is scaled on the host and crosses scaled
+    const bool host_scale = !is_group(h) && h->comm.kind == 0 && scaling_on(h) && h->m > 0 &&
+                            (double)h->m * (double)h->n <= SCALE_HOST_MAX;
+    std::vector<double> As;
+    if (host_scale) As = scale_dense_host(h, A);
     const double t1 = now_s();
-    int rc = h2d_staged(A, tg);
+    int rc = h2d_staged(host_scale ? As.data() : A, tg);
     const double th2d = now_s() - t1;
     if (rc) return rc;
     if (is_group(h))
         rc = fan_out(h, [&](elp_handle* r, int) { return dense_host_finish(r, dir, rhs, obj, lo, up, maximize); });
     else
-        rc = dense_host_finish(h, dir, rhs, obj, lo, up, maximize);
+        rc = dense_host_finish(h, dir, rhs, obj, lo, up, maximize, host_scale);
     for (elp_handle* r : rk) {
         r->stats.seconds_load = now_s() - t0;
         r->stats.seconds_h2d = th2d;
@@ -1766,10 +1852,13 @@ static int run_resident(elp_handle* h, size_t lds, int32_t* lp_status, double t_
     rc = ensure_k(h, std::min(h->m, h->n));
     if (rc) return rc;
     if (!h->d_resout) HIPCHK(hipMalloc((void**)&h->d_resout, sizeof(ResOut)));
+    if (!h->d_resx) HIPCHK(hipMalloc((void**)&h->d_resx, (size_t)h->n * sizeof(double)));
     ResArgs a{};
     a.phase = h->phase;
     a.price_rule = h->ctl.pricing;
     a.refactor_mode = h->ctl.refactor_mode;
+    a.warm = h->res_warm;
+    a.xout = h->d_resx;
     a.tick_budget = 0;
     if (h->ctl.time_limit > 0) {
         const double left = h->ctl.time_limit - (now_s() - h->t_solve_start);
@@ -1780,9 +1869,14 @@ static int run_resident(elp_handle* h, size_t lds, int32_t* lp_status, double t_
     ResOut o{};
     HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
     HIPCHK(hipMemcpyAsync(&o, h->d_resout, sizeof(ResOut), hipMemcpyDeviceToHost, h->st));
+    h->res_x.resize((size_t)h->n);
+    HIPCHK(hipMemcpyAsync(h->res_x.data(), h->d_resx, (size_t)h->n * sizeof(double), hipMemcpyDeviceToHost, h->st));
     HIPCHK(hipStreamSynchronize(h->st));
+    h->res_fresh = true;
     h->stats.host_polls++;
-    h->stats.refactors += o.refactors;
+    // (a warm start's refactor is not counted: reload_bounds_warm resets the count after it)
+    h->stats.refactors += o.refactors - (a.warm ? 1 : 0);
+    h->res_warm = 0;
     h->stats.gj_refactors += o.gj_refactors;
     if (h->ctl.refactor_mode == 0 && o.emax_max > h->stats.max_inv_resid) h->stats.max_inv_resid = o.emax_max;
     h->stats.resident = 1;
@@ -1828,9 +1922,12 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
         h->timing_started = true;
     }
     DevCtl* c = h->hctl;
-    // resume: refresh the mirror, set the stop budget
-    HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
-    HIPCHK(hipStreamSynchronize(h->st));
+    // resume: refresh the mirror (unless it is the device's already), set the stop budget
+    if (!h->res_fresh) {
+        HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+        HIPCHK(hipStreamSynchronize(h->st));
+    }
+    h->res_fresh = false;
     c->iter_stop = budget >= INT64_MAX - c->iter ? INT64_MAX : c->iter + budget;
     if (c->status == ST_STOP) c->status = ST_RUN;
     c->phase = h->phase;
@@ -1840,6 +1937,8 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
         rc = run_resident(h, lds, lp_status, t_loop0);
         if (rc != 1) return rc;
     }
+    if (h->res_warm)  // (reload_bounds_warm took the resident path: its device part is the kernel's)
+        return fail(ELP_E_STATE, "internal: a resident warm start fell back to the pipeline");
     h->stats.resident = 0;
     const int period = h->ctl.refactor_period;
     // ELP_PROFILE_EVENTS: events on the pricing dispatches of every chunk;
@@ -2212,14 +2311,25 @@ static int reload_bounds_warm(elp_handle* h, const std::vector<double>& lo, cons
         lo_s[(size_t)j] = unscale_col(h, fin(lo[(size_t)j]), j, -1);
         up_s[(size_t)j] = unscale_col(h, fin(up[(size_t)j]), j, -1);
     }
-    if (!h->warm_lo) HIPCHK(hipMalloc((void**)&h->warm_lo, (size_t)std::max<int64_t>(n, 1) * sizeof(double)));
-    if (!h->warm_up) HIPCHK(hipMalloc((void**)&h->warm_up, (size_t)std::max<int64_t>(n, 1) * sizeof(double)));
-    double *dlo = h->warm_lo, *dup = h->warm_up;
+    // the last node ran on the resident solver and nothing ran since: the
+    // mirror is the device's control block, and the next resident launch does
+    // the device part (launch_warm_start, do_refactor, the weights' reset)
+    const bool res = h->res_fresh && resident_fit(h) != 0;
+    h->res_fresh = false;
+    double *dlo = d.lb, *dup = d.ub;  // (res: the structurals' bounds in place)
+    if (!res) {
+        if (!h->warm_lo) HIPCHK(hipMalloc((void**)&h->warm_lo, (size_t)std::max<int64_t>(n, 1) * sizeof(double)));
+        if (!h->warm_up) HIPCHK(hipMalloc((void**)&h->warm_up, (size_t)std::max<int64_t>(n, 1) * sizeof(double)));
+        dlo = h->warm_lo;
+        dup = h->warm_up;
+    }
     HIPCHK(hipMemcpyAsync(dlo, lo_s.data(), (size_t)n * sizeof(double), hipMemcpyHostToDevice, h->st));
     HIPCHK(hipMemcpyAsync(dup, up_s.data(), (size_t)n * sizeof(double), hipMemcpyHostToDevice, h->st));
     // the control block of a fresh solve, the basis kept
-    HIPCHK(hipMemcpyAsync(h->hctl, d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
-    HIPCHK(hipStreamSynchronize(h->st));
+    if (!res) {
+        HIPCHK(hipMemcpyAsync(h->hctl, d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+        HIPCHK(hipStreamSynchronize(h->st));
+    }
     DevCtl& c = *h->hctl;
     const int k = c.k, ny = c.ny;
     c.status = ST_RUN;
@@ -2245,6 +2355,28 @@ static int reload_bounds_warm(elp_handle* h, const std::vector<double>& lo, cons
     c.ddevex = h->ctl.pricing == ELP_PRICE_DEVEX;
     c.dv_valid = 0;
     c.dual_iters = c.dflat = 0;
+    if (res) {
+        bool bad = false;  // (k_warm_bounds' test, on the host's copy)
+        for (int64_t j = 0; j < n; ++j) bad |= lo_s[(size_t)j] > up_s[(size_t)j];
+        h->stats = elp_stats{};
+        h->stats.world_size = h->comm.world;
+        h->stats.ncols = h->nloc;
+        h->stats.basis = ELP_BASIS_INVERSE;
+        h->timing_started = false;
+        h->done = false;
+        h->dual_used = true;
+        if (bad) {  // (the oracle's warm_core: nothing of the node runs)
+            h->done = true;
+            h->final_status = ELP_INFEASIBLE;
+        } else {
+            h->phase = 3;
+            h->res_warm = 1;
+        }
+        const int rc = push_ctl_fields(h);
+        if (rc) return rc;
+        h->res_fresh = true;  // (the mirror was just written to the device)
+        return 0;
+    }
     HIPCHK(hipMemcpyAsync(d.ctl, h->hctl, sizeof(DevCtl), hipMemcpyHostToDevice, h->st));
     HIPCHK(launch_warm_start(d, dlo, dup, k, ny, h->st));
     HIPCHK(hipMemcpyAsync(h->hctl, d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
@@ -2454,21 +2586,25 @@ extern "C" int elp_get_solution(elp_handle* h, double* objval, double* x, double
     if (!h || !h->loaded) return fail(ELP_E_STATE, "elp_get_solution: no problem loaded");
     HIPCHK(hipSetDevice(h->dev));
     const int64_t m = h->m, n = h->n, nl = h->nloc;
-    HIPCHK(hipMemcpyAsync(h->hctl, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
-    // structural values: each shard writes its columns into a zeroed full-length
-    // vector, the all-reduce (sum with zeros: exact) gives every rank all of x
     std::vector<double> xs((size_t)n, 0.0);
-    double* dx = nullptr;
-    HIPCHK(dalloc(&dx, n));
-    HIPCHK(hipMemsetAsync(dx, 0, (size_t)n * sizeof(double), h->st));
-    HIPCHK(launch_extract(h->d, dx + h->col0, h->st));
-    {
-        const int rc = h->comm.allreduce_sum_f64(dx, (size_t)n, h->st);
-        if (rc) return fail(rc, "solution all-reduce failed");
+    if (h->res_fresh && h->res_x.size() == (size_t)n) {
+        xs = h->res_x;  // (the resident solver's exit brought them back with the control block)
+    } else {
+        HIPCHK(hipMemcpyAsync(h->hctl, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+        // structural values: each shard writes its columns into a zeroed full-length
+        // vector, the all-reduce (sum with zeros: exact) gives every rank all of x
+        double* dx = nullptr;
+        HIPCHK(dalloc(&dx, n));
+        HIPCHK(hipMemsetAsync(dx, 0, (size_t)n * sizeof(double), h->st));
+        HIPCHK(launch_extract(h->d, dx + h->col0, h->st));
+        {
+            const int rc = h->comm.allreduce_sum_f64(dx, (size_t)n, h->st);
+            if (rc) return fail(rc, "solution all-reduce failed");
+        }
+        HIPCHK(hipMemcpyAsync(xs.data(), dx, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, h->st));
+        HIPCHK(hipStreamSynchronize(h->st));
+        (void)hipFree(dx);
     }
-    HIPCHK(hipMemcpyAsync(xs.data(), dx, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, h->st));
-    HIPCHK(hipStreamSynchronize(h->st));
-    (void)hipFree(dx);
     (void)nl;
     const DevCtl& c = *h->hctl;
     const double BIG = h->ctl.infinity;
@@ -2542,6 +2678,7 @@ struct SensPart {
 };
 
 static int sens_part(elp_handle* h, SensPart& sp) {
+    h->res_fresh = false;
     HIPCHK(hipSetDevice(h->dev));
     HIPCHK(hipMemcpyAsync(h->hctl, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
     HIPCHK(hipStreamSynchronize(h->st));
@@ -2797,8 +2934,10 @@ extern "C" int elp_get_stats(elp_handle* h, elp_stats* st) {
     if (!h || !st) return fail(ELP_E_ARG, "elp_get_stats: NULL argument");
     if (h->loaded) {
         HIPCHK(hipSetDevice(h->dev));
-        HIPCHK(hipMemcpyAsync(h->hctl, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
-        HIPCHK(hipStreamSynchronize(h->st));
+        if (!h->res_fresh) {
+            HIPCHK(hipMemcpyAsync(h->hctl, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
+            HIPCHK(hipStreamSynchronize(h->st));
+        }
         const DevCtl& c = *h->hctl;
         h->stats.iterations = c.iter;
         h->stats.phase1_iterations = c.phase1_iters;
@@ -2902,6 +3041,7 @@ extern "C" void elp_destroy(elp_handle* h) {
     free_dev(h);
     release_kept(h);
     if (h->d_resout) (void)hipFree(h->d_resout);
+    if (h->d_resx) (void)hipFree(h->d_resx);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     h->comm.destroy();
     if (h->st) (void)hipStreamDestroy(h->st);

@@ -437,10 +437,14 @@ struct ResOut {
     int32_t phase, pad;
     int64_t stage[8], stage2[8];  // diagnostic builds (-DELP_RES_PROF=1): shader cycles per loop stage
 };
+// warm: a branch-and-bound node's warm start runs first (reload_bounds_warm's
+// device part: real costs, BTRAN, every nonbasic column re-placed, the dual
+// weights reset, a refactor); xout: the structurals' values (scaled, n) at exit
 struct ResArgs {
-    int32_t phase, price_rule, refactor_mode, pad;
+    int32_t phase, price_rule, refactor_mode, warm;
     int64_t tick_budget;
     ResOut* out;
+    double* xout;
 };
 size_t resident_lds_bytes(int m, int n);
 hipError_t launch_resident(const Dev& d, const ResArgs& a, size_t lds, hipStream_t st);

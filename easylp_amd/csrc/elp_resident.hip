@@ -688,6 +688,38 @@ RDEV double r_price_sum(const RS& s, const RV& v, const RC& c, int j, bool mode1
     return tot;
 }
 
+// a warm-started node's nonbasic column j re-placed for the node's bounds and
+// its reduced cost dj (elp_kernels.hip warm_fix, oracle warm_core); 1 when its
+// cost was flattened to make it dual feasible
+RDEV int r_warm_fix(RS& s, int j, bool structural, double dj, double dtol) {
+    int8_t vs = s.vst[j];
+    if (vs == VS_BASIC) return 0;
+    const double l = s.lb[j], u = s.ub[j];
+    if (l == u) {
+        if (structural) {
+            s.vst[j] = VS_FIXED;
+            s.xval[j] = l;
+        }
+        return 0;
+    }
+    if (structural) {
+        const bool lo_ok = l > -R_INF, up_ok = u < R_INF;
+        if (vs == VS_FIXED) vs = VS_LOWER;
+        if (vs == VS_LOWER && !lo_ok) vs = up_ok ? VS_UPPER : VS_FREE;
+        else if (vs == VS_UPPER && !up_ok) vs = lo_ok ? VS_LOWER : VS_FREE;
+        else if (vs == VS_FREE && (lo_ok || up_ok)) vs = lo_ok ? VS_LOWER : VS_UPPER;
+        if (vs == VS_LOWER && dj < -dtol && up_ok) vs = VS_UPPER;
+        else if (vs == VS_UPPER && dj > dtol && lo_ok) vs = VS_LOWER;
+        s.vst[j] = vs;
+        s.xval[j] = vs == VS_LOWER ? l : vs == VS_UPPER ? u : 0.0;
+    }
+    if ((vs == VS_LOWER && dj < -dtol) || (vs == VS_UPPER && dj > dtol) || (vs == VS_FREE && fabs(dj) > dtol)) {
+        s.cost[j] = s.cost[j] - dj;
+        return 1;
+    }
+    return 0;
+}
+
 enum { R_CONT = 0, R_EXIT = 1, R_RECHECK = 2, R_TO_P2 = 3, R_PIVOT = 4 };
 
 // the pivot an iteration chose: entering q (reduced cost dq, its Devex
@@ -1429,6 +1461,31 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
     enum { RF_NONE = 0, RF_TOP, RF_RECHECK, RF_TO_P2 };
     int recheck = 0, refac = RF_NONE;
     Piv P;
+    int64_t flat = 0;
+    if (a.warm) {
+        // a branch-and-bound node from the last node's basis (reload_bounds_warm:
+        // launch_warm_start, do_refactor, launch_devex_reset): the real costs, y
+        // of them on the last inverse, each nonbasic column re-placed for the
+        // node's bounds (the host wrote them) and its reduced cost, then the
+        // refactor; the dual phase starts at its loop top
+        for (int j = lane; j < n; j += RW) s.cost[j] = d.maximize ? -d.obj[j] : d.obj[j];
+        if (lane < m) s.cost[n + lane] = 0.0;
+        R_FENCE();
+        r_btran(s, v, c, 2);
+        const double yY = mode1 ? 0.0 : shf(v.y, v.Yl & 63);
+        int nf = 0;
+        for (int j0 = 0; j0 < n; j0 += RW) {
+            const int j = j0 + lane < n ? j0 + lane : n - 1;
+            const double td = r_price_sum(s, v, c, j, mode1, yY);
+            if (j0 + lane < n) nf += r_warm_fix(s, j, true, s.cost[j] - td, c.tol_dual);
+        }
+        if (lane < m) nf += r_warm_fix(s, n + lane, false, s.cost[n + lane] - v.y, c.tol_dual);
+        flat = (int64_t)r_wtree((double)nf);  // (exact: small integers)
+        R_FENCE();
+        r_dw_reset(s);
+        c.dv_valid = 0;
+        refac = RF_TO_P2;
+    }
     if (ELP_RES_PROF && lane == 0) {
         for (int i = 0; i < 16; ++i) r_prof[i] = 0;
         r_prof[16] = __builtin_amdgcn_s_memtime();
@@ -1559,6 +1616,13 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
         const double* col = s.A + rli(v.Sl, p) * s.lda;
         if (rowl) d.AS[(size_t)p * m + lane] = col[lane];
     }
+    if (a.xout)  // the structurals' values (k_extract + k_extract_basic)
+        for (int j0 = 0; j0 < n; j0 += RW) {
+            const int j = j0 + lane < n ? j0 + lane : n - 1;
+            const int p = s.spos[j];
+            const double xb = shf(v.xs, p & 63);
+            if (j0 + lane < n) a.xout[j] = p >= 0 ? xb : s.xval[j];
+        }
     if (!mode1 && d.AR) {
         const int64_t tw = d.tile_w;
         for (int p = 0; p < ny; ++p) {
@@ -1579,6 +1643,7 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
         g->flips = r_stat.flips;
         g->degenerate = r_stat.degenerate;
         g->dual_iters = r_stat.dual_iters;
+        if (a.warm) g->dflat += flat;
         g->since_refactor = c.since;
         g->ndegen = c.ndegen;
         g->bland = c.bland;
