@@ -40,14 +40,14 @@ fi
 timeout -k 10 600 python bench.py --gpus 1 --steps "$STEPS" --warmup "$WARM" > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err" || { echo "bench failed rc=$?"; tail -20 "$OUT/bench_$TAG.err"; exit 4; }
 cat "$OUT/bench_$TAG.json"
 
-REG="--steps $STEPS --warmup $WARM --c4 0 --sparse 0 --no-cpu --compare-rules 0 --window 0 --host-input 0 --host-c4 0 --c2 0"
+REG="--steps $STEPS --warmup $WARM --c4 0 --sparse 0 --no-cpu --compare-rules 0 --window 0 --host-input 0 --host-c4 0 --c2 0 --small 0"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$TMP/kt" -o run -- python3 "$ROOT/bench.py" $REG > "$OUT/prof_bench_$TAG.json" 2> "$OUT/prof_bench_$TAG.err" || { echo "rocprof failed rc=$?"; tail -20 "$OUT/prof_bench_$TAG.err"; exit 5; }
 cp "$(find "$TMP/kt" -name '*kernel_stats.csv' | head -1)" "$OUT/kernel_stats_$TAG.csv"
 python3 "$ROOT/tools/window_stats.py" "$(find "$TMP/kt" -name '*kernel_trace.csv' | head -1)" "$OUT/prof_bench_$TAG.json" > "$OUT/window_stats_$TAG.json" && cat "$OUT/window_stats_$TAG.json"
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_price --output-format csv -d "$TMP/pmc" -o run -- python3 "$ROOT/bench.py" $REG > "$OUT/pmc_bench_$TAG.json" 2> "$OUT/pmc_bench_$TAG.err" || { echo "rocprof pmc failed rc=$?"; tail -20 "$OUT/pmc_bench_$TAG.err"; exit 6; }
 python3 "$ROOT/tools/pmc_traffic.py" "$(find "$TMP/pmc" -name '*counter_collection.csv' | head -1)" "$OUT/pmc_bench_$TAG.json" > "$OUT/pmc_traffic_$TAG.json" && cat "$OUT/pmc_traffic_$TAG.json"
-WIN="--steps 0 --warmup 0 --window 1 --c4 0 --sparse 0 --no-cpu --compare-rules 0 --host-input 0 --host-c4 0 --c2 0"
+WIN="--steps 0 --warmup 0 --window 1 --c4 0 --sparse 0 --no-cpu --compare-rules 0 --host-input 0 --host-c4 0 --c2 0 --small 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$TMP/tl" -o run -- python3 "$ROOT/bench.py" $WIN > "$OUT/tl_bench_$TAG.json" 2>&1 || { echo "rocprof timeline failed"; exit 7; }
 python3 "$ROOT/tools/timeline.py" "$(find "$TMP/tl" -name '*kernel_trace.csv' | head -1)" 100 1000 > "$OUT/timeline_$TAG.txt" && cat "$OUT/timeline_$TAG.txt"
 # the sparse 20000 x 100000 LPs: probe times, then the per-kernel
