@@ -139,6 +139,9 @@ struct elp_handle {
     // launch runs the node warm start first
     double* d_resx = nullptr;
     std::vector<double> res_x;
+    // pinned host block of the resident exchanges: [ResOut][x: n][node lo: n][node up: n]
+    // (pageable copies of these few bytes block the host for the whole transfer)
+    char* res_pin = nullptr;
     bool res_fresh = false;
     int32_t res_warm = 0;
     std::vector<double> mip_x;   // branch and bound: the incumbent (elp_get_solution)
@@ -1841,6 +1844,14 @@ static size_t resident_fit(elp_handle* h) {
     return b <= h->res_lds_max ? b : 0;
 }
 
+// the pinned block's parts (elp_handle::res_pin), allocated at the first use
+static constexpr size_t RES_PIN_X = (sizeof(ResOut) + 63) & ~(size_t)63;
+static int ensure_res_pin(elp_handle* h) {
+    if (!h->res_pin) HIPCHK(hipHostMalloc((void**)&h->res_pin, RES_PIN_X + 3 * (size_t)std::max<int64_t>(h->n, 1) * sizeof(double)));
+    return 0;
+}
+static double* res_pin_x(elp_handle* h) { return reinterpret_cast<double*>(h->res_pin + RES_PIN_X); }
+
 // One launch runs the loop to its end: optimal, infeasible, unbounded, a
 // limit, or the elp_iterate budget (phase changes and refactors inside).
 // Returns 1 when the pipeline must run instead (a plan still pending).
@@ -1853,6 +1864,7 @@ static int run_resident(elp_handle* h, size_t lds, int32_t* lp_status, double t_
     if (rc) return rc;
     if (!h->d_resout) HIPCHK(hipMalloc((void**)&h->d_resout, sizeof(ResOut)));
     if (!h->d_resx) HIPCHK(hipMalloc((void**)&h->d_resx, (size_t)h->n * sizeof(double)));
+    if (const int rp = ensure_res_pin(h)) return rp;
     ResArgs a{};
     a.phase = h->phase;
     a.price_rule = h->ctl.pricing;
@@ -1868,10 +1880,11 @@ static int run_resident(elp_handle* h, size_t lds, int32_t* lp_status, double t_
     HIPCHK(launch_resident(h->d, a, lds, h->st));
     ResOut o{};
     HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
-    HIPCHK(hipMemcpyAsync(&o, h->d_resout, sizeof(ResOut), hipMemcpyDeviceToHost, h->st));
-    h->res_x.resize((size_t)h->n);
-    HIPCHK(hipMemcpyAsync(h->res_x.data(), h->d_resx, (size_t)h->n * sizeof(double), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipMemcpyAsync(h->res_pin, h->d_resout, sizeof(ResOut), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipMemcpyAsync(res_pin_x(h), h->d_resx, (size_t)h->n * sizeof(double), hipMemcpyDeviceToHost, h->st));
     HIPCHK(hipStreamSynchronize(h->st));
+    std::memcpy(&o, h->res_pin, sizeof(ResOut));
+    h->res_x.assign(res_pin_x(h), res_pin_x(h) + h->n);
     h->res_fresh = true;
     h->stats.host_polls++;
     // (a warm start's refactor is not counted: reload_bounds_warm resets the count after it)
@@ -2317,14 +2330,22 @@ static int reload_bounds_warm(elp_handle* h, const std::vector<double>& lo, cons
     const bool res = h->res_fresh && resident_fit(h) != 0;
     h->res_fresh = false;
     double *dlo = d.lb, *dup = d.ub;  // (res: the structurals' bounds in place)
-    if (!res) {
+    const double *src_lo = lo_s.data(), *src_up = up_s.data();
+    if (res) {  // (from the pinned block: an asynchronous copy)
+        if (const int rp = ensure_res_pin(h)) return rp;
+        double* pl = res_pin_x(h) + n;
+        std::memcpy(pl, lo_s.data(), (size_t)n * sizeof(double));
+        std::memcpy(pl + n, up_s.data(), (size_t)n * sizeof(double));
+        src_lo = pl;
+        src_up = pl + n;
+    } else {
         if (!h->warm_lo) HIPCHK(hipMalloc((void**)&h->warm_lo, (size_t)std::max<int64_t>(n, 1) * sizeof(double)));
         if (!h->warm_up) HIPCHK(hipMalloc((void**)&h->warm_up, (size_t)std::max<int64_t>(n, 1) * sizeof(double)));
         dlo = h->warm_lo;
         dup = h->warm_up;
     }
-    HIPCHK(hipMemcpyAsync(dlo, lo_s.data(), (size_t)n * sizeof(double), hipMemcpyHostToDevice, h->st));
-    HIPCHK(hipMemcpyAsync(dup, up_s.data(), (size_t)n * sizeof(double), hipMemcpyHostToDevice, h->st));
+    HIPCHK(hipMemcpyAsync(dlo, src_lo, (size_t)n * sizeof(double), hipMemcpyHostToDevice, h->st));
+    HIPCHK(hipMemcpyAsync(dup, src_up, (size_t)n * sizeof(double), hipMemcpyHostToDevice, h->st));
     // the control block of a fresh solve, the basis kept
     if (!res) {
         HIPCHK(hipMemcpyAsync(h->hctl, d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
@@ -3042,6 +3063,7 @@ extern "C" void elp_destroy(elp_handle* h) {
     release_kept(h);
     if (h->d_resout) (void)hipFree(h->d_resout);
     if (h->d_resx) (void)hipFree(h->d_resx);
+    if (h->res_pin) (void)hipHostFree(h->res_pin);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     h->comm.destroy();
     if (h->st) (void)hipStreamDestroy(h->st);
