@@ -273,6 +273,49 @@ static hipError_t take_or_alloc(double** p, size_t bytes, double** keep, size_t*
     return hipMalloc((void**)p, bytes ? bytes : sizeof(double));  // (m = 0: kernels read element 0)
 }
 
+// ---------------------------------------------------------------- spares
+// A destroyed one-GPU handle leaves its stream, its device buffers (by size),
+// its pinned blocks and its copy of A for the next elp_create on the same
+// device (R's flow: one handle per easylp$solve(), make.lp ... finalize): a
+// stream creation costs 0.4-8 ms and a small LP's ~45 buffers ~0.13 ms, more
+// than the solve.  Bounded: SPARE_MAX handles' worth, SPARE_BYTES of device
+// memory in all; ELP_NO_SPARE=1 turns it off.  The next load takes buffers
+// of the sizes it needs (alloc_all's pool) and frees the rest.
+struct Spare {
+    int dev = 0;
+    hipStream_t st = nullptr;
+    std::multimap<size_t, void*> pool;
+    size_t bytes = 0;
+    double* keep_A = nullptr;
+    size_t keep_A_bytes = 0;
+    DevCtl* hctl = nullptr;
+    ResOut* resout = nullptr;
+    double* resx = nullptr;
+    int64_t resx_n = 0;
+    char* respin = nullptr;
+};
+static std::mutex g_spare_mu;
+static std::vector<Spare> g_spares;
+constexpr int SPARE_MAX = 4;
+constexpr size_t SPARE_BYTES = (size_t)1 << 30;
+static bool spares_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("ELP_NO_SPARE");
+        return !(e && std::atoi(e) != 0);
+    }();
+    return on;
+}
+static void spare_free(Spare& sp) {
+    (void)hipSetDevice(sp.dev);
+    for (auto& kv : sp.pool) (void)hipFree(kv.second);
+    if (sp.keep_A) (void)hipFree(sp.keep_A);
+    if (sp.hctl) (void)hipHostFree(sp.hctl);
+    if (sp.resout) (void)hipFree(sp.resout);
+    if (sp.resx) (void)hipFree(sp.resx);
+    if (sp.respin) (void)hipHostFree(sp.respin);
+    if (sp.st) (void)hipStreamDestroy(sp.st);
+}
+
 // ---------------------------------------------------------------- ngpu
 // Single-process multi-device (elp_control.ngpu = P > 1; SURVEY.md 8b
 // "Threading": the R caller stays one synchronous process): the handle the
@@ -508,7 +551,31 @@ extern "C" int elp_create(elp_handle** out, int64_t m, int64_t n, const elp_cont
         delete h;
         return fail(ELP_E_HIP, "elp_create: hipSetDevice failed");
     }
-    if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess) {
+    if (h->ctl.ngpu <= 1 && spares_on()) {
+        std::lock_guard<std::mutex> lk(g_spare_mu);
+        for (size_t i = g_spares.size(); i-- > 0;)
+            if (g_spares[i].dev == h->dev) {
+                Spare sp = std::move(g_spares[i]);
+                g_spares.erase(g_spares.begin() + (long)i);
+                h->st = sp.st;
+                h->pool = std::move(sp.pool);
+                h->keep_A = sp.keep_A;
+                h->keep_A_bytes = sp.keep_A_bytes;
+                h->hctl = sp.hctl;
+                h->d_resout = sp.resout;
+                if (sp.resx_n == n) {  // (sized by n)
+                    h->d_resx = sp.resx;
+                    h->res_pin = sp.respin;
+                } else {
+                    if (sp.resx) (void)hipFree(sp.resx);
+                    if (sp.respin) (void)hipHostFree(sp.respin);
+                }
+                break;
+            }
+    }
+    if (!h->st && hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess) {
+        drain_pool(h);
+        release_kept(h);
         delete h;
         return fail(ELP_E_HIP, "elp_create: stream creation failed");
     }
@@ -3059,6 +3126,48 @@ extern "C" void elp_destroy(elp_handle* h) {
     if (getenv("ELP_DEBUG_ENQUEUE"))
         fprintf(stderr, "elp: host enqueue %.4f s, poll wait %.4f s, polls %lld\n", h->dbg_enqueue,
                 h->dbg_wait, (long long)h->stats.host_polls);
+    // a plain one-GPU handle leaves its resources for the next elp_create (Spare)
+    if (h->st && spares_on() && h->ranks.empty() && h->comm.kind == 0 && h->ctl.ngpu <= 1 && h->ev.empty()) {
+        free_dev(h, true);  // (every buffer into the pool, A's copy kept)
+        Spare sp;
+        sp.dev = h->dev;
+        sp.st = h->st;
+        sp.pool = std::move(h->pool);
+        for (auto& kv : sp.pool) sp.bytes += kv.first;
+        sp.keep_A = h->keep_A;
+        sp.keep_A_bytes = h->keep_A_bytes;
+        sp.bytes += sp.keep_A_bytes;
+        sp.hctl = h->hctl;
+        sp.resout = h->d_resout;
+        sp.resx = h->d_resx;
+        sp.resx_n = h->n;
+        sp.respin = h->res_pin;
+        h->pool.clear();
+        h->keep_A = nullptr;
+        h->hctl = nullptr;
+        h->d_resout = nullptr;
+        h->d_resx = nullptr;
+        h->res_pin = nullptr;
+        h->st = nullptr;
+        std::vector<Spare> drop;
+        {
+            std::lock_guard<std::mutex> lk(g_spare_mu);
+            size_t tot = sp.bytes;
+            for (const Spare& o : g_spares) tot += o.bytes;
+            if (sp.bytes <= SPARE_BYTES) {
+                g_spares.push_back(std::move(sp));
+                while (!g_spares.empty() && ((int)g_spares.size() > SPARE_MAX || tot > SPARE_BYTES)) {
+                    tot -= g_spares.front().bytes;  // (the oldest goes)
+                    drop.push_back(std::move(g_spares.front()));
+                    g_spares.erase(g_spares.begin());
+                }
+            } else {
+                drop.push_back(std::move(sp));
+            }
+        }
+        for (Spare& o : drop) spare_free(o);
+        (void)hipSetDevice(h->dev);
+    }
     free_dev(h);
     release_kept(h);
     if (h->d_resout) (void)hipFree(h->d_resout);
