@@ -1772,10 +1772,11 @@ __global__ void __launch_bounds__(256) k_select_ftran(Dev d, int ntiles, int nsw
     //  is drained at the block's end; masks are applied where values are used)
 #pragma unroll
     for (int t = 0; t < PFC; ++t) cc[t] = ld_clamp(d.cand, tid + 256 * t, ncand);
-    {
+    {  // (read by the dense register path only: past it every lane loads element 0)
+        const int mlim = !SP && pfm ? k_ub : 1;
         const double* row = d.Minv + (size_t)(pr < k_ub ? pr : 0) * d.ldm;
 #pragma unroll
-        for (int t = 0; t < PFM; ++t) mrow[t] = ld_clamp(row, lane + 64 * t, k_ub);
+        for (int t = 0; t < PFM; ++t) mrow[t] = ld_clamp(row, lane + 64 * t, mlim);
     }
 #pragma unroll
     for (int t = 0; t < PFR; ++t) rl[t] = ld_clamp(d.Rl, tid + 256 * t, k_ub);
@@ -2858,10 +2859,15 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         rho_col = ld_clamp(d.rhoR, main_wg ? col : 0, k_ub);
 #pragma unroll
         for (int t = 0; t < PFT; ++t) trow[t] = 0.0;
-    } else {  // (AR-copy workgroups fetch row 0: harmless; no MinvT: Minv, unused)
+    } else {  // (AR-copy workgroups fetch row 0: harmless)
+        // only the register path (k_ub <= 64 PFT, MinvT kept) reads these: past
+        // it -- and without MinvT -- every lane loads element 0 (one line), not a
+        // row nobody reads (8 KB per wave with arow below: 24 MB per pivot at the
+        // CSC feasible-start LP's k ~ 3 000)
+        const int tlim = pft && !d.noT ? k_ub : 1;
         const double* row = (d.noT ? d.Minv : d.MinvT) + (size_t)(main_wg && col < k_ub ? col : 0) * d.ldm;
 #pragma unroll
-        for (int t = 0; t < PFT; ++t) trow[t] = ld_clamp(row, lane + 64 * t, k_ub);
+        for (int t = 0; t < PFT; ++t) trow[t] = ld_clamp(row, lane + 64 * t, tlim);
     }
     __builtin_amdgcn_sched_barrier(0);  // all of the above issued before any use
     // the control-block integers stay vector values up to here: their scalar
@@ -2922,10 +2928,11 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
         dxsig = c->dr_xsig;
 #pragma unroll
         for (int t = 0; t < PFT; ++t) arow[t] = 0.0;
-    } else {
+    } else {  // (as trow: read by the register path only)
         const double* row = (d.noT ? d.Minv : d.MinvT) + (size_t)(apos_c >= 0 ? apos_c : 0) * d.ldm;
+        const int alim = pft && !d.noT ? k : 1;
 #pragma unroll
-        for (int t = 0; t < PFT; ++t) arow[t] = ld_clamp(row, lane + 64 * t, k);
+        for (int t = 0; t < PFT; ++t) arow[t] = ld_clamp(row, lane + 64 * t, alim);
     }
     // ---- pass 1 result: min over the workgroup minima
     const double INF = HUGE_VAL;
