@@ -3283,16 +3283,30 @@ __global__ void __launch_bounds__(256) k_ratio(Dev d, int phase, int nblk, int l
                 if (pc == PC_A || pc == PC_C) d.vrow[j] = vr[t] / piv;
                 if (pc == PC_C || pc == PC_D) d.colA[j] = ca[t];
             }
-        } else if (pc == PC_A) {
-            for (int j = tid; j < k; j += 256) d.vrow[j] = d.Minv[(size_t)lposx * d.ldm + j] / piv;
-        } else if (pc == PC_C) {
-            for (int j = tid; j < k; j += 256) {
-                d.vrow[j] = d.Minv[(size_t)lposx * d.ldm + j] / piv;
-                d.colA[j] = d.noT ? d.Minv[(size_t)j * d.ldm + apos] : d.MinvT[(size_t)apos * d.ldm + j];
+        } else if (pc != PC_B && pc != PC_E) {
+            // k > 256 PFV (the CSC bumps): eight entries per thread in flight, the
+            // loads ahead of the stores (one at a time, each store waited for the
+            // next load: vrow / colA may alias Minv as far as the compiler knows
+            // -- ~1 us per entry, the CSC feasible-start LP's k_ratio tail)
+            const bool wr = pc == PC_A || pc == PC_C, wc = pc == PC_C || pc == PC_D;
+            const size_t rv = (size_t)(lposx >= 0 ? lposx : 0) * d.ldm;
+            const int ap = apos >= 0 ? apos : 0;
+            for (int j0 = tid; j0 < k; j0 += 256 * 8) {
+                double a[8], b[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int j = j0 + 256 * u < k ? j0 + 256 * u : k - 1;
+                    a[u] = wr ? d.Minv[rv + j] : 0.0;
+                    b[u] = wc ? (d.noT ? d.Minv[(size_t)j * d.ldm + ap] : d.MinvT[(size_t)ap * d.ldm + j]) : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int j = j0 + 256 * u;
+                    if (j >= k) break;
+                    if (wr) d.vrow[j] = a[u] / piv;
+                    if (wc) d.colA[j] = b[u];
+                }
             }
-        } else if (pc == PC_D) {
-            for (int j = tid; j < k; j += 256)
-                d.colA[j] = d.noT ? d.Minv[(size_t)j * d.ldm + apos] : d.MinvT[(size_t)apos * d.ldm + j];
         }
     }
     // ---- pivot: bookkeeping, its stores split by destination over the four waves
@@ -6608,9 +6622,16 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
         //  500 000 (16.5 vs 14.7 us, r01), 10 as well (12.01 vs 11.75 us at k
         //  529, r03 A/B over the last 2000 iterations))
         const unsigned nbk = ELP_BOOK_WG;  // (the bookkeeping workgroup after the main ones)
+        // (past the register path -- k > 512 -- the row registers only cost
+        //  occupancy: the <1> instance, 135 -> ~107 VGPRs, four waves per SIMD
+        //  instead of three, so the ~k/4 workgroups of a CSC bump all fit at once)
         if (phase == 3)
             k_ratio<8, true><<<nmain + nbk, 256, lds_row ? lds : 0, st>>>(d, 2, nrt + nbt, lds_row, 0,
                                                                          (int)nmain, k_ub, dslot, nrt + nbt * zw);
+        else if (k_ub > 64 * 8)
+            k_ratio<1><<<nmain + nbk + nar, 256, lds_row ? lds : 0, st>>>(d, phase, nrt + nbt, lds_row,
+                                                                         defer, (int)nmain, k_ub, dslot,
+                                                                         nrt + nbt * zw);
         else
             k_ratio<8><<<nmain + nbk + nar, 256, lds_row ? lds : 0, st>>>(d, phase, nrt + nbt, lds_row,
                                                                          defer, (int)nmain, k_ub, dslot,
@@ -6644,7 +6665,7 @@ hipError_t launch_iteration(const Dev& d, int k_ub, int ny_ub, int phase, hipStr
         // last 4 000 iterations of 10 000 x 500 000, k 529; 16 measured no faster
         // there, r01 -- fewer waves per SIMD), else the row is read after a_R
         if (sp)
-            k_select_ftran<8, true><<<g, 256, ldsz, st>>>(d, ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz, 0);
+            k_select_ftran<1, true><<<g, 256, ldsz, st>>>(d, ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz, 0);
         else if (k_ub > 512 && k_ub <= 640)
             k_select_ftran<10><<<g, 256, ldsz, st>>>(d, ntiles, nsw, k_ub, dslot, (int)nrw, (int)nqz, 0);
         else
@@ -6766,7 +6787,7 @@ static hipError_t dual_tail(const Dev& d, int k_ub, hipStream_t st, bool flip_co
         const unsigned nqz = d.qz && !d.csc ? cdiv(m, 256 * QZ_PT) : 0;
         const unsigned g = nrw + nqz + (d.csc ? 1 : 0);
         if (sp)
-            k_select_ftran<8, true><<<g, 256, ldsz, st>>>(d, 1, 0, k_ub, 0, (int)nrw, (int)nqz, dual);
+            k_select_ftran<1, true><<<g, 256, ldsz, st>>>(d, 1, 0, k_ub, 0, (int)nrw, (int)nqz, dual);
         else if (k_ub > 512 && k_ub <= 640)
             k_select_ftran<10><<<g, 256, ldsz, st>>>(d, 1, 0, k_ub, 0, (int)nrw, (int)nqz, dual);
         else
