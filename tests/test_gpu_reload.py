@@ -74,3 +74,48 @@ def test_reload_pool_alternating_inputs(gpu, monkeypatch):
             assert g.stats["bump_dim"] > 3
             np.testing.assert_array_equal(g.trace, o.trace)
             assert g.objval == o.objval
+
+
+def test_handle_spares_across_shapes(gpu):
+    """Destroyed one-GPU handles leave their stream, buffers and pinned blocks
+    for the next elp_create (elp_api.hip Spare; R creates one handle per
+    solve): handles of alternating shapes -- resident-sized, pipeline-sized,
+    dense and CSC, LP and MIP -- created and destroyed in turn, each trace and
+    objective the oracle's, whatever the previous handle left behind."""
+    import scipy.sparse as sp
+    from oracle import solve_dense as orc, solve_mip
+    rng = np.random.default_rng(11)
+    shapes = [(12, 30, "dense"), (150, 600, "dense"), (12, 30, "csc"), (40, 90, "mip"), (150, 600, "dense"),
+              (12, 31, "dense"), (40, 90, "mip"), (12, 30, "dense")]
+    for m, n, kind in shapes:
+        A = rng.uniform(-1, 1, (m, n)) * (rng.uniform(0, 1, (m, n)) < 0.4)
+        A[:, 0] = 1.0
+        dirs = rng.integers(1, 4, m).astype(np.int32)
+        rhs = rng.uniform(1, 5, m) * np.where(dirs == 2, -1, 1)
+        c = rng.uniform(-1, 1, n)
+        up = np.full(n, 4.0)
+        with gpu.Problem(m, n) as p:
+            p.set_trace(100000)
+            if kind == "csc":
+                S = sp.csc_matrix(A)
+                p.load_csc(S.indptr.astype(np.int64), S.indices.astype(np.int32), S.data, dirs, rhs, c,
+                           np.zeros(n), up, maximize=True)
+            else:
+                p.load_dense(A, dirs, rhs, c, up=up, maximize=True)
+            if kind == "mip":
+                isint = np.zeros(n, np.int32)
+                isint[::3] = 1
+                p.set_int(isint)
+            st = p.solve()
+            sol = p.solution(st)
+            tr = p.trace() if kind != "mip" else None
+        if kind == "mip":
+            o = solve_mip(A, dirs, rhs, c, np.zeros(n), up, True, isint)
+            assert st == o.status and (st != 0 or sol.objval == o.objval), (m, n, kind)
+        else:
+            o = orc(A, dirs, rhs, c, up=up, maximize=True, trace_cap=100000,
+                    **({"price_mode": 1} if kind == "csc" else {}))
+            assert st == o.status, (m, n, kind)
+            assert np.array_equal(tr, o.trace), (m, n, kind)
+            if st == 0:
+                assert sol.objval == o.objval, (m, n, kind)
