@@ -1955,7 +1955,7 @@ static int run_resident(elp_handle* h, size_t lds, int32_t* lp_status, double t_
     h->res_fresh = true;
     h->stats.host_polls++;
     // (a warm start's refactor is not counted: reload_bounds_warm resets the count after it)
-    h->stats.refactors += o.refactors - (a.warm ? 1 : 0);
+    h->stats.refactors += std::max<int64_t>(0, o.refactors - (a.warm ? 1 : 0));
     h->res_warm = 0;
     h->stats.gj_refactors += o.gj_refactors;
     if (h->ctl.refactor_mode == 0 && o.emax_max > h->stats.max_inv_resid) h->stats.max_inv_resid = o.emax_max;
