@@ -158,8 +158,10 @@ RDEV double r_wtree(double acc) {
 template <class FX, class FY>
 RDEV double wdot(FX X, FY Y, int len) {
     double s0 = 0.0, s1 = 0.0, s2 = 0.0, tot = 0.0;  // the blocks' tree: pending block, pair, quad
+    // len <= 16: blocks 2..7 are +0.0 and fold to ((B0 + B1) + 0) + 0 = (B0 + B1) + 0
+    const int nb = len <= 16 ? 2 : 8;
 #pragma unroll 1
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < nb; ++b) {
         double B = 0.0;
         if (8 * b < len) {
             double x[8], t[8];
@@ -182,7 +184,7 @@ RDEV double wdot(FX X, FY Y, int len) {
             }
         }
     }
-    return tot;
+    return nb == 2 ? s1 + 0.0 : tot;
 }
 
 // ------------------------------------------------------------ LDS state
