@@ -119,6 +119,9 @@ struct elp_handle {
     // wait for peers spinning on this rank's record when ranks share a device)
     double* warm_lo = nullptr;
     double* warm_up = nullptr;
+    // the load's staging of the scaled bounds and rhs (load_common: lo, up | rhs),
+    // allocated with the other buffers -- a hipFree per load waited for the device
+    double* ld_stage = nullptr;
     // buffers of the last load kept for the next one (free_dev on a reload):
     // alloc_all's allocations by size; a reload of the same shape takes them
     // back instead of ~80 hipFree + hipMalloc pairs (1.8 ms at 5000 x 50000)
@@ -144,6 +147,9 @@ struct elp_handle {
     char* res_pin = nullptr;
     bool res_fresh = false;
     int32_t res_warm = 0;
+    // ctl_fresh: hctl equals the device's control block (the load's last
+    // transfer wrote it), so run_loop skips its refresh
+    bool ctl_fresh = false;
     std::vector<double> mip_x;   // branch and bound: the incumbent (elp_get_solution)
 };
 
@@ -212,7 +218,7 @@ static void free_dev(elp_handle* h, bool keep_big = false) {
                     (void*)d.rval, d.qcol, d.qz, d.spos, d.dstamp, d.rowvs, d.yvs, d.dw, d.dprev, (void*)d.srow,
                     (void*)d.scol, d.rhoR, d.rr, d.dchz, d.dcand, d.dcnt, d.dcomp, d.dalive, d.dflip,
                     d.dflipdx, d.aF, d.fS, d.ddw != d.dw ? (void*)d.ddw : nullptr, d.dsend, d.drecv,
-                    d.afs, d.afl, d.aflv, d.ptst, d.ptgrid};
+                    d.afs, d.afl, d.aflv, d.ptst, d.ptgrid, h->ld_stage};
     for (void* p : ptrs)
         if (p) release(p);
     if (!keep_big) drain_pool(h);
@@ -223,6 +229,7 @@ static void free_dev(elp_handle* h, bool keep_big = false) {
     h->warm_lo = h->warm_up = nullptr;
     h->A_owned = nullptr;
     h->d_flag = nullptr;
+    h->ld_stage = nullptr;
     h->w_cap = 0;  // (W0 / W1 went with the rest)
     d = Dev{};
     if (h->hctl && !keep_big) {  // (a reload keeps the pinned control-block copy)
@@ -799,8 +806,11 @@ static int alloc_all_body(elp_handle* h) {
             A(dalloc(&d.afs, (size_t)(1 + 1024)));
             A(dalloc(&d.afl, (size_t)(AFL_POS + 256)));
             A(dalloc(&d.aflv, (size_t)256));
-            A(hipMemsetAsync(d.afs, 0xff, sizeof(int32_t), h->st));  // -1: clear all of a_F first
-            A(hipMemsetAsync(d.afl, 0xff, sizeof(int32_t), h->st));  // -1: no list
+            Fill32List fc{};  // -1: clear all of a_F first; -1: no list
+            fc.f[0] = Fill32{d.afs, 1, 0xffffffffu, 0};
+            fc.f[1] = Fill32{d.afl, 1, 0xffffffffu, 0};
+            fc.count = 2;
+            A(launch_fill32(fc, h->st));
         }
         d.dslack = !d.sharded || h->comm.rank == h->comm.world - 1;
         if (d.sharded) {
@@ -812,6 +822,7 @@ static int alloc_all_body(elp_handle* h) {
         }
     }
     if (!d.ddw) d.ddw = d.dw;  // (one GPU: local ids are the global ids)
+    A(dalloc(&h->ld_stage, (size_t)(2 * n + mm)));
     if (e != hipSuccess) {
         free_dev(h);
         return fail(ELP_E_NOMEM, std::string("device allocation failed: ") + hipGetErrorString(e));
@@ -819,14 +830,19 @@ static int alloc_all_body(elp_handle* h) {
     if (!h->hctl) A(hipHostMalloc((void**)&h->hctl, sizeof(DevCtl)));
     // (AR padding columns [n, ldr) are read by the 128-column tiles but their
     //  results are discarded, so AR needs no clearing); Minv / work start clean
-    A(hipMemsetAsync(d.rcnt, 0, (size_t)d.rregs * sizeof(int32_t), h->st));
-    A(hipMemsetAsync(d.Minv, 0, msq * sizeof(double), h->st));
-    if (d.MinvT) A(hipMemsetAsync(d.MinvT, 0, msq * sizeof(double), h->st));
-    if (d.qcol) A(hipMemsetAsync(d.qcol, 0, (size_t)mm * sizeof(double), h->st));
+    // (one launch for all of them: a small LP's load is its launches)
+    Fill32List fl{};
+    auto fill = [&](void* p, int64_t words, uint32_t v) {
+        if (p && fl.count < FILL32_MAX) fl.f[fl.count++] = Fill32{p, words, v, 0};
+    };
+    fill(d.rcnt, d.rregs, 0u);
+    fill(d.Minv, 2 * (int64_t)msq, 0u);
+    fill(d.MinvT, 2 * (int64_t)msq, 0u);
+    fill(d.qcol, 2 * mm, 0u);
     // index lists: entries past k / |Y| are read speculatively (and discarded):
     // start them at -1 rather than whatever the allocator hands out
-    for (int32_t* lst : {d.Rl, d.Sl, d.Yl, d.rpos, d.ypos})
-        A(hipMemsetAsync(lst, 0xff, (size_t)mm * sizeof(int32_t), h->st));
+    for (int32_t* lst : {d.Rl, d.Sl, d.Yl, d.rpos, d.ypos}) fill(lst, mm, 0xffffffffu);
+    A(launch_fill32(fl, h->st));
 
     if (e != hipSuccess) {
         free_dev(h);
@@ -1186,6 +1202,7 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
     Dev& d = h->d;
     h->res_fresh = false;
     h->res_warm = 0;
+    h->ctl_fresh = false;
     load_mark(h, "A + scaling");
     for (int64_t i = 0; i < m; ++i)
         if (dir[i] < ELP_LE || dir[i] > ELP_EQ) return fail(ELP_E_ARG, "dir must be 1 (<=), 2 (>=) or 3 (==)");
@@ -1220,10 +1237,7 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
         slb[i] = dir[i] == ELP_GE ? -HUGE_VAL : 0.0;
         sub[i] = dir[i] == ELP_LE ? HUGE_VAL : 0.0;
     }
-    double *dlo = nullptr, *dup = nullptr, *drhs = nullptr;
-    HIPCHK(dalloc(&dlo, nl));
-    HIPCHK(dalloc(&dup, nl));
-    HIPCHK(dalloc(&drhs, m));
+    double *dlo = h->ld_stage, *dup = h->ld_stage + nl, *drhs = h->ld_stage + 2 * nl;
     HIPCHK(hipMemcpyAsync(dlo, lo_h.data(), nl * sizeof(double), hipMemcpyHostToDevice, h->st));
     HIPCHK(hipMemcpyAsync(dup, up_h.data(), nl * sizeof(double), hipMemcpyHostToDevice, h->st));
     if (m) {
@@ -1273,9 +1287,6 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
     // removed in r06 -- the copies read A's rows in place)
     release_kept(h);  // whatever this load did not take
     HIPCHK(launch_fill_AR(h->d, h->st));
-    (void)hipFree(dlo);
-    (void)hipFree(dup);
-    (void)hipFree(drhs);
     int infeasible = 0;
     {
         const int rc = any_rank(h, h->hctl->infeasible_bounds, &infeasible);
@@ -1319,10 +1330,10 @@ static int load_common(elp_handle* h, const int32_t* dir, const double* rhs, con
         h->hctl->devex = 0;  // (the primal Devex weights: dw holds the dual ones)
         h->hctl->ddevex = h->ctl.pricing == ELP_PRICE_DEVEX;
         HIPCHK(hipMemcpyAsync(d.ctl, h->hctl, sizeof(DevCtl), hipMemcpyHostToDevice, h->st));
-        HIPCHK(hipStreamSynchronize(h->st));
         h->phase = 3;
         h->any_art = false;
         h->dual_used = true;
+        h->ctl_fresh = true;  // (no wait: the stream orders what reads it)
     } else if (h->any_art) {
         h->phase = 1;
     } else {
@@ -1431,12 +1442,14 @@ static int h2d_staged(const double* src, std::vector<H2DTarget>& tg) {
         }
     if (hi <= lo) return 0;
     if ((hi - lo) * sizeof(double) < STAGE_MIN) {
+        // (a pageable source is consumed before the call returns; one device's
+        //  stream orders the rest of the load behind the copy: no wait)
         for (const H2DTarget& t : tg)
             if (t.e1 > t.e0) {
                 HIPCHK(hipSetDevice(t.dev));
                 HIPCHK(hipMemcpyAsync(t.dst, src + t.e0, (t.e1 - t.e0) * sizeof(double), hipMemcpyHostToDevice,
                                       t.st));
-                HIPCHK(hipStreamSynchronize(t.st));
+                if (tg.size() > 1) HIPCHK(hipStreamSynchronize(t.st));
             }
         return 0;
     }
@@ -1508,6 +1521,7 @@ static int prep_load(elp_handle* h, bool csc = false) {
     HIPCHK(hipSetDevice(h->dev));
     h->res_fresh = false;
     h->res_warm = 0;
+    h->ctl_fresh = false;
     load_mark(h, nullptr);
     if (h->loaded) free_dev(h, true);
     load_mark(h, "free previous");
@@ -2003,11 +2017,12 @@ static int run_loop(elp_handle* h, int64_t budget, int32_t* lp_status) {
     }
     DevCtl* c = h->hctl;
     // resume: refresh the mirror (unless it is the device's already), set the stop budget
-    if (!h->res_fresh) {
+    if (!h->res_fresh && !h->ctl_fresh) {
         HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
         HIPCHK(hipStreamSynchronize(h->st));
     }
     h->res_fresh = false;
+    h->ctl_fresh = false;
     c->iter_stop = budget >= INT64_MAX - c->iter ? INT64_MAX : c->iter + budget;
     if (c->status == ST_STOP) c->status = ST_RUN;
     c->phase = h->phase;
@@ -2767,6 +2782,7 @@ struct SensPart {
 
 static int sens_part(elp_handle* h, SensPart& sp) {
     h->res_fresh = false;
+    h->ctl_fresh = false;
     HIPCHK(hipSetDevice(h->dev));
     HIPCHK(hipMemcpyAsync(h->hctl, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
     HIPCHK(hipStreamSynchronize(h->st));

@@ -339,6 +339,20 @@ constexpr int AFL_POS = 66;  // afl: positions [66, 66 + SPL)
 hipError_t launch_generate(const Dev& d, uint64_t seed, int64_t col0, int64_t n_global,
                            double* A, double* b, double* c, hipStream_t st);
 // init in two parts: columns (+ nonzero list), then rows once ract is complete
+// several buffers filled with a 32-bit pattern in one launch (the load's
+// zeroed / -1 buffers: one launch instead of one hipMemsetAsync each)
+struct Fill32 {
+    void* p;
+    int64_t words;  // 32-bit words
+    uint32_t val;
+    int32_t pad;
+};
+constexpr int FILL32_MAX = 12;
+struct Fill32List {
+    Fill32 f[FILL32_MAX];
+    int32_t count, pad;
+};
+hipError_t launch_fill32(const Fill32List& l, hipStream_t st);
 hipError_t launch_init_cols(const Dev& d, const double* lo, const double* up, hipStream_t st);
 hipError_t launch_init_rows(const Dev& d, const double* rhs, hipStream_t st);
 hipError_t launch_fill_AR(const Dev& d, hipStream_t st);  // AR rows for the initial Y

@@ -6892,6 +6892,24 @@ hipError_t launch_refactor_primal(const Dev& d, int k, hipStream_t st) {
     return hipGetLastError();
 }
 
+__global__ void __launch_bounds__(256) k_fill32(Fill32List l) {
+    const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x, T = (int64_t)gridDim.x * 256;
+    for (int b = 0; b < l.count; ++b) {
+        uint32_t* p = static_cast<uint32_t*>(l.f[b].p);
+        const int64_t nw = l.f[b].words;
+        const uint32_t v = l.f[b].val;
+        for (int64_t i = t0; i < nw; i += T) p[i] = v;
+    }
+}
+hipError_t launch_fill32(const Fill32List& l, hipStream_t st) {
+    if (l.count <= 0) return hipSuccess;
+    int64_t mx = 1;
+    for (int b = 0; b < l.count; ++b) mx = std::max<int64_t>(mx, l.f[b].words);
+    const int64_t g = std::min<int64_t>(cdiv(mx, 256), 2048);
+    k_fill32<<<(unsigned)g, 256, 0, st>>>(l);
+    return hipGetLastError();
+}
+
 hipError_t launch_devex_reset(const Dev& d, hipStream_t st) {
     k_devex_reset<<<cdiv((int64_t)(d.N > d.n ? d.N : d.n) + d.m, 256), 256, 0, st>>>(d);
     return hipGetLastError();
