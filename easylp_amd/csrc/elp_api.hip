@@ -1985,6 +1985,10 @@ static int run_resident(elp_handle* h, size_t lds, int32_t* lp_status, double t_
         std::fprintf(stderr, "elp resident inner: ftran colA+shf %lld wdot %lld zchunk %lld; price loop %lld argbest %lld; "
                      "ratio pass1 %lld pass2 %lld\n", (long long)o.stage2[0], (long long)o.stage2[1], (long long)o.stage2[2],
                      (long long)o.stage2[3], (long long)o.stage2[4], (long long)o.stage2[5], (long long)o.stage2[6]);
+    if (o.stage[1] && std::getenv("ELP_DEBUG_RESIDENT"))
+        std::fprintf(stderr, "elp resident dual select: chuzr %lld rho %lld sweep %lld compaction %lld bfrt %lld flips %lld\n",
+                     (long long)o.stage3[0], (long long)o.stage3[1], (long long)o.stage3[2], (long long)o.stage3[3],
+                     (long long)o.stage3[4], (long long)o.stage3[5]);
     h->phase = o.phase;
     const int32_t s = c->status;
     h->stats.seconds_loop += now_s() - t_loop0;

@@ -449,7 +449,7 @@ struct ResOut {
     int64_t refactors, gj_refactors, devex_resets, ticks;
     double emax_max;
     int32_t phase, pad;
-    int64_t stage[8], stage2[8];  // diagnostic builds (-DELP_RES_PROF=1): shader cycles per loop stage
+    int64_t stage[8], stage2[8], stage3[8];  // diagnostic builds (-DELP_RES_PROF=1): shader cycles per loop stage
 };
 // warm: a branch-and-bound node's warm start runs first (reload_bounds_warm's
 // device part: real costs, BTRAN, every nonbasic column re-placed, the dual

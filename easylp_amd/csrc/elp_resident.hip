@@ -56,13 +56,13 @@ constexpr double R_INF = HUGE_VAL;
 #ifndef ELP_RES_PROF
 #define ELP_RES_PROF 0
 #endif
-__shared__ unsigned long long r_prof[17];  // [16]: the last stamp
+__shared__ unsigned long long r_prof[25];  // [24]: the last stamp
 #define R_STAMP(i)                                                        \
     do {                                                                  \
         if (ELP_RES_PROF && threadIdx.x == 0) {                           \
             const unsigned long long t_ = __builtin_amdgcn_s_memtime();   \
-            r_prof[i] += t_ - r_prof[16];                                 \
-            r_prof[16] = t_;                                              \
+            r_prof[i] += t_ - r_prof[24];                                 \
+            r_prof[24] = t_;                                              \
         }                                                                 \
     } while (0)
 
@@ -344,13 +344,20 @@ RDEV bool r_gauss_jordan(RS& s, const RV& v, RC& c) {
         const double q = lane < k ? W[p * k + lane] / piv : 0.0;  // row p's quotient of column lane
         const double f = wv;                                                // row lane's factor
         R_FENCE();
-        for (int r = 0; r < k; ++r) {  // row r: every column j = lane
-            const double fr = rl(f, r);
-            if (lane >= k) continue;
-            double& x = W[r * k + lane];
-            if (r == p) x = lane == col ? 1.0 / piv : q;
-            else if (lane == col) x = -(fr / piv);
-            else if (fr != 0.0 && q != 0.0) x = fma(-fr, q, x);
+        for (int r0 = 0; r0 < k; r0 += 8) {  // rows r0.., every column j = lane: 8 loads, then 8 stores
+            double x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = lane < k ? W[(r0 + u < k ? r0 + u : k - 1) * k + lane] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int r = r0 + u;
+                if (r >= k) break;
+                const double fr = rl(f, r);
+                if (r == p) x[u] = lane == col ? 1.0 / piv : q;
+                else if (lane == col) x[u] = -(fr / piv);
+                else if (fr != 0.0 && q != 0.0) x[u] = fma(-fr, q, x[u]);
+                if (lane < k) W[r * k + lane] = x[u];
+            }
         }
         R_FENCE();
     }
@@ -369,10 +376,21 @@ RDEV bool r_newton_schulz(RS& s, const RV& v, RC& c) {
     double* E = s.W + k * k;
     r_load_M(s, v, k, M);
     double emax = 0.0;
-    for (int i = 0; i < k; ++i) {  // E[i][j], lane j: (M Minv)_ij seq over l
+    for (int i = 0; i < k; ++i) {  // E[i][j], lane j: (M Minv)_ij seq over l (8 terms' loads at a time)
         double acc = 0.0;
         if (lane < k)
-            for (int l = 0; l < k; ++l) acc = fma(M[i * k + l], s.Mi[l * s.ldm + lane], acc);
+            for (int l0 = 0; l0 < k; l0 += 8) {
+                double mv[8], iv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int l = l0 + u < k ? l0 + u : k - 1;
+                    mv[u] = M[i * k + l];
+                    iv[u] = s.Mi[l * s.ldm + lane];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (l0 + u < k) acc = fma(mv[u], iv[u], acc);
+            }
         const double ev = (i == lane ? 1.0 : 0.0) - acc;
         if (lane < k) {
             E[i * k + lane] = ev;
@@ -387,7 +405,18 @@ RDEV bool r_newton_schulz(RS& s, const RV& v, RC& c) {
         double acc = 0.0;
         if (lane < k) {
             acc = s.Mi[i * s.ldm + lane];
-            for (int l = 0; l < k; ++l) acc = fma(s.Mi[i * s.ldm + l], E[l * k + lane], acc);
+            for (int l0 = 0; l0 < k; l0 += 8) {
+                double mv[8], ev[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int l = l0 + u < k ? l0 + u : k - 1;
+                    mv[u] = s.Mi[i * s.ldm + l];
+                    ev[u] = E[l * k + lane];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (l0 + u < k) acc = fma(mv[u], ev[u], acc);
+            }
         }
         R_FENCE();
         if (lane < k) s.Mi[i * s.ldm + lane] = acc;
@@ -1003,6 +1032,7 @@ RDEV int r_dual_select(const Dev& d, RS& s, RV& v, RC& c, bool mode1, Piv& P) {
     const bool rh = rv >= 0;
     const int wl = c.bland ? r_argminid(rh, rv) : r_argbest<false>(rh, rscore, rv);
     if (wl < 0) return c.since > 0 ? R_RECHECK : R_TO_P2;  // (recheck: confirm on a fresh x_B)
+    R_STAMP(16);
     rv = rli(rv, wl);
     re = rli(re, wl);
     rs = rli(rs, wl);
@@ -1021,6 +1051,7 @@ RDEV int r_dual_select(const Dev& d, RS& s, RV& v, RC& c, bool mode1, Piv& P) {
     double rho = shf(vv, v.rpos & 63);
     if (!(lane < m && v.rpos >= 0)) rho = 0.0;
     if (lane == xrow) rho = xsig;
+    R_STAMP(17);
     // ---- one sweep: d_j (y) and alpha_j (rho)
     const double yY = mode1 ? 0.0 : shf(v.y, v.Yl & 63), rY = mode1 ? 0.0 : shf(rho, v.Yl & 63);
     for (int j0 = 0; j0 < n; j0 += RW) {
@@ -1073,6 +1104,7 @@ RDEV int r_dual_select(const Dev& d, RS& s, RV& v, RC& c, bool mode1, Piv& P) {
     }
     if (lane == 0) c.st->price_bytes += mode1 ? 12.0 * (double)d.nnz + 17.0 * n : 8.0 * ((double)c.ny * n + n + c.ny);
     R_FENCE();
+    R_STAMP(18);
     // ---- candidates, ascending id (ballot compaction)
     int nc = 0;
     for (int j0 = 0; j0 < n + m; j0 += RW) {
@@ -1108,6 +1140,7 @@ RDEV int r_dual_select(const Dev& d, RS& s, RV& v, RC& c, bool mode1, Piv& P) {
         nc += __popcll(bm);
     }
     R_FENCE();
+    R_STAMP(19);
     // ---- bound-flipping Harris ratio test
     double slope = fabs(rx - rbeta);
     int q = -1, nflip = 0;
@@ -1182,6 +1215,7 @@ RDEV int r_dual_select(const Dev& d, RS& s, RV& v, RC& c, bool mode1, Piv& P) {
         qa = s.avec[q];
         break;
     }
+    R_STAMP(20);
     c.iter++;
     if (lane == 0) {
         c.st->phase1_iters++;
@@ -1221,6 +1255,7 @@ RDEV int r_dual_select(const Dev& d, RS& s, RV& v, RC& c, bool mode1, Piv& P) {
         R_FENCE();
         rx = re < m ? rl(v.xr, re) : rl(v.xs, re - m);
     }
+    R_STAMP(21);
     const int8_t vq = s.vst[q];
     P.q = q;
     P.dq = s.dvec[q];
@@ -1515,8 +1550,8 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
         refac = RF_TO_P2;
     }
     if (ELP_RES_PROF && lane == 0) {
-        for (int i = 0; i < 16; ++i) r_prof[i] = 0;
-        r_prof[16] = __builtin_amdgcn_s_memtime();
+        for (int i = 0; i < 24; ++i) r_prof[i] = 0;
+        r_prof[24] = __builtin_amdgcn_s_memtime();
     }
     for (;;) {
         R_STAMP(7);
@@ -1694,6 +1729,7 @@ __global__ void __launch_bounds__(RW) k_resident(Dev d, ResArgs a) {
         a.out->ticks = (int64_t)(t1 - t0);
         for (int i = 0; i < 8; ++i) a.out->stage[i] = ELP_RES_PROF ? (int64_t)(r_prof[i] + (i == 0 ? 0 : 0)) : 0;
         for (int i = 8; i < 16; ++i) a.out->stage2[i - 8] = ELP_RES_PROF ? (int64_t)r_prof[i] : 0;
+        for (int i = 16; i < 24; ++i) a.out->stage3[i - 16] = ELP_RES_PROF ? (int64_t)r_prof[i] : 0;
     }
 }
 
