@@ -1844,19 +1844,34 @@ static int do_refactor(elp_handle* h, int k) {
     if (k > 0) {
         int rc = ensure_w(h, k);
         if (rc) return rc;
-        HIPCHK(hipMemsetAsync(&h->d.ctl->ns_emax_bits, 0, sizeof(unsigned long long), h->st));
-        HIPCHK(launch_refactor_ns_resid(h->d, k, h->st));
-        unsigned long long bits = 0;
-        HIPCHK(hipMemcpyAsync(&h->hctl->ns_emax_bits, &h->d.ctl->ns_emax_bits, sizeof(bits),
-                              hipMemcpyDeviceToHost, h->st));
-        HIPCHK(hipStreamSynchronize(h->st));
-        bits = h->hctl->ns_emax_bits;
-        double emax;
-        std::memcpy(&emax, &bits, sizeof(emax));
-        if (h->ctl.refactor_mode == 0 && emax > h->stats.max_inv_resid) h->stats.max_inv_resid = emax;
-        if (emax <= NS_TOL && h->ctl.refactor_mode == 0) {
+        // E = I - M Minv (its max |e| back to the host)
+        auto resid = [&](double* emax) -> int {
+            HIPCHK(hipMemsetAsync(&h->d.ctl->ns_emax_bits, 0, sizeof(unsigned long long), h->st));
+            HIPCHK(launch_refactor_ns_resid(h->d, k, h->st));
+            HIPCHK(hipMemcpyAsync(&h->hctl->ns_emax_bits, &h->d.ctl->ns_emax_bits, sizeof(unsigned long long),
+                                  hipMemcpyDeviceToHost, h->st));
+            HIPCHK(hipStreamSynchronize(h->st));
+            const unsigned long long bits = h->hctl->ns_emax_bits;
+            std::memcpy(emax, &bits, sizeof(*emax));
+            if (h->ctl.refactor_mode == 0 && *emax > h->stats.max_inv_resid) h->stats.max_inv_resid = *emax;
+            return 0;
+        };
+        double emax = 0.0;
+        if (const int rc = resid(&emax)) return rc;
+        bool ok = false;
+        if (h->ctl.refactor_mode == 0 && emax <= NS_TOL) {
             HIPCHK(launch_refactor_ns_update(h->d, k, h->st));
-        } else {
+            ok = true;
+        } else if (h->ctl.refactor_mode == 0 && emax <= NS_TOL2) {  // (oracle refactor(): two corrections)
+            HIPCHK(launch_refactor_ns_update(h->d, k, h->st));
+            double e2 = 0.0;
+            if (const int rc = resid(&e2)) return rc;
+            if (e2 <= NS_TOL) {
+                HIPCHK(launch_refactor_ns_update(h->d, k, h->st));
+                ok = true;
+            }
+        }
+        if (!ok) {
             HIPCHK(launch_refactor_gj(h->d, k, h->st));
             h->stats.gj_refactors++;
         }

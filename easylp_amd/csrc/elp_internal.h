@@ -384,6 +384,9 @@ hipError_t launch_iteration_tail(const Dev& d, int k_ub, int phase, hipStream_t 
 hipError_t launch_row_chain(const Dev& d, hipStream_t st);
 // refactor = ns_resid; (host reads ns_emax) ns_update | gauss_jordan; primal
 constexpr double NS_TOL = 1e-6;
+// (NS_TOL, NS_TOL2]: a correction and, if the residual is then within NS_TOL,
+// a second one instead of a Gauss-Jordan rebuild (oracle refactor())
+constexpr double NS_TOL2 = 1e-2;
 hipError_t launch_refactor_ns_resid(const Dev& d, int k, hipStream_t st);
 hipError_t launch_refactor_ns_update(const Dev& d, int k, hipStream_t st);
 hipError_t launch_refactor_gj(const Dev& d, int k, hipStream_t st);

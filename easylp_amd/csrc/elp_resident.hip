@@ -369,8 +369,8 @@ RDEV bool r_gauss_jordan(RS& s, const RV& v, RC& c) {
     R_FENCE();
     return true;
 }
-// one Newton-Schulz correction; false: the residual is too large
-RDEV bool r_newton_schulz(RS& s, const RV& v, RC& c) {
+// one Newton-Schulz correction; false: the residual is above tol (nothing changed)
+RDEV bool r_newton_schulz(RS& s, const RV& v, RC& c, double tol) {
     const int k = c.k, lane = threadIdx.x;
     double* M = s.W;
     double* E = s.W + k * k;
@@ -399,7 +399,7 @@ RDEV bool r_newton_schulz(RS& s, const RV& v, RC& c) {
     }
     emax = r_wmax(emax);
     if (threadIdx.x == 0 && emax > c.st->emax_max) c.st->emax_max = emax;
-    if (!(emax <= NS_TOL)) return false;
+    if (!(emax <= tol)) return false;
     R_FENCE();
     for (int i = 0; i < k; ++i) {  // Minv_new[i][j] = Minv[i][j] + sum_l Minv[i][l] E[l][j], row by row in place
         double acc = 0.0;
@@ -428,7 +428,20 @@ RDEV bool r_newton_schulz(RS& s, const RV& v, RC& c) {
 RDEV bool r_refactor(RS& s, RV& v, RC& c, int refactor_mode) {
     const int k = c.k, m = s.m, n = s.n, lane = threadIdx.x;
     if (k > 0) {
-        if (refactor_mode != 0 || !r_newton_schulz(s, v, c)) {
+        // oracle refactor(): a correction within NS_TOL; else one within NS_TOL2
+        // and, if the new residual is within NS_TOL, a second; else Gauss-Jordan
+        // (one call site: the loop keeps the code in the instruction cache)
+        bool ok = false;
+        for (int t = 0; refactor_mode == 0 && t < 3; ++t) {
+            const bool applied = r_newton_schulz(s, v, c, t == 1 ? NS_TOL2 : NS_TOL);
+            if (t == 0 && applied) {
+                ok = true;
+                break;
+            }
+            if (t == 1 && !applied) break;
+            if (t == 2) ok = applied;
+        }
+        if (!ok) {
             if (threadIdx.x == 0) c.st->gj++;
             if (!r_gauss_jordan(s, v, c)) return false;
         }

@@ -344,10 +344,16 @@ static void y_remove(orc_t* s, int64_t i) {
 
 /* ------------------------------------------------------------------ */
 /* refactor: one Newton-Schulz correction of the maintained inverse    */
-/* (E = I - M Minv; Minv += Minv E) when max|E| <= NS_TOL, otherwise a  */
-/* fresh Gauss-Jordan inversion with partial pivoting; then x_B from b. */
+/* (E = I - M Minv; Minv += Minv E) when max|E| <= NS_TOL; from         */
+/* NS_TOL up to NS_TOL2 a correction and, if the new residual is within */
+/* NS_TOL, a second one (the residual squares: 1e-3 -> ~1e-6 -> ~1e-12, */
+/* two k^3 products instead of a k-step Gauss-Jordan -- r06: 64 ms of   */
+/* the CSC feasible-start LP's 0.53 s went into one at k = 3 452);      */
+/* otherwise a fresh Gauss-Jordan inversion with partial pivoting; then */
+/* x_B from b.                                                          */
 /* ------------------------------------------------------------------ */
 #define NS_TOL 1e-6
+#define NS_TOL2 1e-2
 
 static int gauss_jordan(orc_t* s) {
     const int64_t k = s->k;
@@ -392,8 +398,9 @@ static int gauss_jordan(orc_t* s) {
     return 0;
 }
 
-/* one Newton-Schulz step; returns 1 if applied, 0 if the residual is too large */
-static int newton_schulz(orc_t* s) {
+/* one Newton-Schulz step; returns 1 if applied, 0 if the residual is   */
+/* above tol (nothing changed)                                          */
+static int newton_schulz(orc_t* s, double tol) {
     const int64_t k = s->k;
     double *E = s->tmp, *Mk = s->tmp + (size_t)k * (size_t)k;
     for (int64_t a = 0; a < k; ++a)
@@ -408,7 +415,7 @@ static int newton_schulz(orc_t* s) {
             if (fabs(e) > emax) emax = fabs(e);
         }
     if (emax > s->emax_max) s->emax_max = emax;
-    if (!(emax <= NS_TOL)) return 0;
+    if (!(emax <= tol)) return 0;
     /* Minv_new[i][j] = Minv[i][j] + sum_l Minv[i][l] E[l][j]  (seq, from Minv[i][j]) */
     double* Nw = Mk;
     for (int64_t i = 0; i < k; ++i)
@@ -424,7 +431,12 @@ static int newton_schulz(orc_t* s) {
 
 static int refactor(orc_t* s) {
     const int64_t k = s->k, m = s->m, n = s->n;
-    if (k > 0 && (s->refactor_mode != 0 || !newton_schulz(s))) {
+    int ok = 0;
+    if (k > 0 && s->refactor_mode == 0) {
+        ok = newton_schulz(s, NS_TOL);
+        if (!ok && newton_schulz(s, NS_TOL2)) ok = newton_schulz(s, NS_TOL);
+    }
+    if (k > 0 && !ok) {
         s->gj_count++;
         if (gauss_jordan(s)) return -1;
     }
