@@ -1854,6 +1854,8 @@ static int do_refactor(elp_handle* h, int k) {
             const unsigned long long bits = h->hctl->ns_emax_bits;
             std::memcpy(emax, &bits, sizeof(*emax));
             if (h->ctl.refactor_mode == 0 && *emax > h->stats.max_inv_resid) h->stats.max_inv_resid = *emax;
+            static const bool dbg = std::getenv("ELP_DEBUG_REFACTOR") != nullptr;
+            if (dbg) std::fprintf(stderr, "elp refactor: k %d max|I - M Minv| %.3e\n", k, *emax);
             return 0;
         };
         double emax = 0.0;
