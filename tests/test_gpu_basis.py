@@ -27,6 +27,10 @@ def test_kkt_feasible_20000x100000_optimum(gpu):
         st = p.solve()
         g = p.solution(st)
     assert st == 0 and g.stats["basis"] == 1
+    # the refactor policy (oracle refactor()): the one refactor
+    # whose residual reaches 1.3e-3 takes two Newton-Schulz corrections, not a
+    # k = 3 452 Gauss-Jordan rebuild
+    assert g.stats["gj_refactors"] == 0 and 1e-6 < g.stats["max_inv_resid"] <= 1e-2
     assert abs(g.objval - fx["highs_objective"]) <= 1e-8 * abs(fx["highs_objective"])
     assert abs(g.objval - obj) <= 1e-8 * abs(obj)
     print("kkt feasible 20000x100000 (inverse): %d iterations, %.2f s, k %d" % (
