@@ -133,14 +133,14 @@ struct elp_handle {
     int64_t kcap = 0;  // bump capacity: AS m x kcap, Minv / MinvT kcap x kcap (grown at polls)
 
     bool dual_used = false;  // the last load's phase 1 is the dual simplex (phase 3)
-    elp::ResOut* d_resout = nullptr;  // the resident solver's exit record
+    elp::ResOut* d_resout = nullptr;  // the resident solver's exit record, then x (RES_PIN_X: one copy back)
     size_t res_lds_max = 0;           // LDS one workgroup may allocate (0: not queried yet)
     // the resident solver's exit: the structurals' values (scaled) brought back
     // with the control block; res_fresh: hctl and res_x equal the device's
     // (nothing ran since), so the next node, elp_get_stats and
     // elp_get_solution skip their round trips; res_warm: the next resident
     // launch runs the node warm start first
-    double* d_resx = nullptr;
+    double* d_resx = nullptr;  // (inside d_resout's allocation)
     std::vector<double> res_x;
     // pinned host block of the resident exchanges: [ResOut][x: n][node lo: n][node up: n]
     // (pageable copies of these few bytes block the host for the whole transfer)
@@ -297,8 +297,7 @@ struct Spare {
     size_t keep_A_bytes = 0;
     DevCtl* hctl = nullptr;
     ResOut* resout = nullptr;
-    double* resx = nullptr;
-    int64_t resx_n = 0;
+    int64_t resx_n = 0;  // (resout holds the record and x: sized by n)
     char* respin = nullptr;
 };
 static std::mutex g_spare_mu;
@@ -318,7 +317,6 @@ static void spare_free(Spare& sp) {
     if (sp.keep_A) (void)hipFree(sp.keep_A);
     if (sp.hctl) (void)hipHostFree(sp.hctl);
     if (sp.resout) (void)hipFree(sp.resout);
-    if (sp.resx) (void)hipFree(sp.resx);
     if (sp.respin) (void)hipHostFree(sp.respin);
     if (sp.st) (void)hipStreamDestroy(sp.st);
 }
@@ -569,12 +567,11 @@ extern "C" int elp_create(elp_handle** out, int64_t m, int64_t n, const elp_cont
                 h->keep_A = sp.keep_A;
                 h->keep_A_bytes = sp.keep_A_bytes;
                 h->hctl = sp.hctl;
-                h->d_resout = sp.resout;
                 if (sp.resx_n == n) {  // (sized by n)
-                    h->d_resx = sp.resx;
+                    h->d_resout = sp.resout;
                     h->res_pin = sp.respin;
                 } else {
-                    if (sp.resx) (void)hipFree(sp.resx);
+                    if (sp.resout) (void)hipFree(sp.resout);
                     if (sp.respin) (void)hipHostFree(sp.respin);
                 }
                 break;
@@ -1960,8 +1957,8 @@ static int run_resident(elp_handle* h, size_t lds, int32_t* lp_status, double t_
     if (rc) return rc;
     rc = ensure_k(h, std::min(h->m, h->n));
     if (rc) return rc;
-    if (!h->d_resout) HIPCHK(hipMalloc((void**)&h->d_resout, sizeof(ResOut)));
-    if (!h->d_resx) HIPCHK(hipMalloc((void**)&h->d_resx, (size_t)h->n * sizeof(double)));
+    if (!h->d_resout) HIPCHK(hipMalloc((void**)&h->d_resout, RES_PIN_X + (size_t)h->n * sizeof(double)));
+    h->d_resx = reinterpret_cast<double*>(reinterpret_cast<char*>(h->d_resout) + RES_PIN_X);
     if (const int rp = ensure_res_pin(h)) return rp;
     ResArgs a{};
     a.phase = h->phase;
@@ -1978,8 +1975,8 @@ static int run_resident(elp_handle* h, size_t lds, int32_t* lp_status, double t_
     HIPCHK(launch_resident(h->d, a, lds, h->st));
     ResOut o{};
     HIPCHK(hipMemcpyAsync(c, h->d.ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, h->st));
-    HIPCHK(hipMemcpyAsync(h->res_pin, h->d_resout, sizeof(ResOut), hipMemcpyDeviceToHost, h->st));
-    HIPCHK(hipMemcpyAsync(res_pin_x(h), h->d_resx, (size_t)h->n * sizeof(double), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipMemcpyAsync(h->res_pin, h->d_resout, RES_PIN_X + (size_t)h->n * sizeof(double), hipMemcpyDeviceToHost,
+                          h->st));  // (the record and x together: the pinned block's layout)
     HIPCHK(hipStreamSynchronize(h->st));
     std::memcpy(&o, h->res_pin, sizeof(ResOut));
     h->res_x.assign(res_pin_x(h), res_pin_x(h) + h->n);
@@ -3176,7 +3173,6 @@ extern "C" void elp_destroy(elp_handle* h) {
         sp.bytes += sp.keep_A_bytes;
         sp.hctl = h->hctl;
         sp.resout = h->d_resout;
-        sp.resx = h->d_resx;
         sp.resx_n = h->n;
         sp.respin = h->res_pin;
         h->pool.clear();
@@ -3208,7 +3204,6 @@ extern "C" void elp_destroy(elp_handle* h) {
     free_dev(h);
     release_kept(h);
     if (h->d_resout) (void)hipFree(h->d_resout);
-    if (h->d_resx) (void)hipFree(h->d_resx);
     if (h->res_pin) (void)hipHostFree(h->res_pin);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     h->comm.destroy();

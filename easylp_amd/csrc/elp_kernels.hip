@@ -4211,8 +4211,11 @@ constexpr int NS_L = 16, NS_R8_MIN = 1536;
 template <int MODE, int NS_R = 4>  // 0: E = I - M Minv (M[i][l] = AS[l][Rl[i]]) into W0; 1: W1 = Minv + Minv E
 __global__ void __launch_bounds__(256) k_ns_gemm(Dev d, int k) {
     constexpr int NS_T = 16 * NS_R;
-    __shared__ double At[NS_L][NS_T + 1];  // At[l][r]: operand A(i0 + r, l0 + l)
-    __shared__ double Bt[NS_L][NS_T + 1];  // Bt[l][c]: operand B(l0 + l, j0 + c)
+    // thread (tx, ty) owns rows i0 + NS_R ty + u and columns j0 + NS_R tx + v:
+    // its operands are NS_R consecutive doubles of an LDS row (16-byte loads;
+    // the row pitch NS_T + 2 keeps them aligned)
+    __shared__ __attribute__((aligned(16))) double At[NS_L][NS_T + 2];  // At[l][r]: operand A(i0 + r, l0 + l)
+    __shared__ __attribute__((aligned(16))) double Bt[NS_L][NS_T + 2];  // Bt[l][c]: operand B(l0 + l, j0 + c)
     __shared__ double red[4];
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
     const int i0 = blockIdx.y * NS_T, j0 = blockIdx.x * NS_T;
@@ -4222,7 +4225,7 @@ __global__ void __launch_bounds__(256) k_ns_gemm(Dev d, int k) {
     for (int u = 0; u < NS_R; ++u)
 #pragma unroll
         for (int v = 0; v < NS_R; ++v) {
-            const int i = i0 + ty + 16 * u, j = j0 + tx + 16 * v;
+            const int i = i0 + NS_R * ty + u, j = j0 + NS_R * tx + v;
             acc[u][v] = (MODE == 1 && i < k && j < k) ? d.Minv[(size_t)i * ldm + j] : 0.0;
         }
     // the next chunk's operands are loaded into registers while this chunk's
@@ -4258,10 +4261,16 @@ __global__ void __launch_bounds__(256) k_ns_gemm(Dev d, int k) {
         const int lend = min(NS_L, k - l0);
         for (int ll = 0; ll < lend; ++ll) {
             double a[NS_R], b[NS_R];
+            const double2* ap = reinterpret_cast<const double2*>(&At[ll][NS_R * ty]);
+            const double2* bp = reinterpret_cast<const double2*>(&Bt[ll][NS_R * tx]);
 #pragma unroll
-            for (int u = 0; u < NS_R; ++u) a[u] = At[ll][ty + 16 * u];
-#pragma unroll
-            for (int v = 0; v < NS_R; ++v) b[v] = Bt[ll][tx + 16 * v];
+            for (int u = 0; u < NS_R / 2; ++u) {
+                const double2 x = ap[u], y = bp[u];
+                a[2 * u] = x.x;
+                a[2 * u + 1] = x.y;
+                b[2 * u] = y.x;
+                b[2 * u + 1] = y.y;
+            }
 #pragma unroll
             for (int u = 0; u < NS_R; ++u)
 #pragma unroll
@@ -4274,7 +4283,7 @@ __global__ void __launch_bounds__(256) k_ns_gemm(Dev d, int k) {
     for (int u = 0; u < NS_R; ++u)
 #pragma unroll
         for (int v = 0; v < NS_R; ++v) {
-            const int i = i0 + ty + 16 * u, j = j0 + tx + 16 * v;
+            const int i = i0 + NS_R * ty + u, j = j0 + NS_R * tx + v;
             if (i >= k || j >= k) continue;
             if (MODE == 0) {
                 const double e = (i == j ? 1.0 : 0.0) - acc[u][v];
