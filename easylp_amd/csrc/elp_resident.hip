@@ -546,6 +546,31 @@ RDEV void r_dual_upd(const RS& s, RV& v, double f, double u, int skip) {
 }
 
 // oracle basis_change (cases A-E, the zero rule, phase 2: the dual update)
+// the rank-one update of the bump inverse (oracle basis_change, zero rule):
+// Mi[r][lane] = fma(-f_r, vv, Mi[r][lane]) for rows r != skip with f_r != 0,
+// on lanes < k other than `keep` whose vv != 0; eight rows' entries (and
+// factors) loaded before any is stored -- each entry's arithmetic unchanged
+template <class F>
+RDEV void r_rank1(double* Mi, int ld, int k, int skip, int keep, double vv, F fac) {
+    const int lane = threadIdx.x;
+    const bool lw = lane < k && lane != keep && vv != 0.0;
+    for (int r0 = 0; r0 < k; r0 += 8) {
+        double x[8], f[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int r = r0 + u < k ? r0 + u : k - 1;
+            f[u] = fac(r);
+            x[u] = lw ? Mi[r * ld + lane] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int r = r0 + u;
+            if (r >= k) break;
+            if (r != skip && f[u] != 0.0 && lw) Mi[r * ld + lane] = fma(-f[u], vv, x[u]);
+        }
+    }
+}
+
 RDEV bool r_basis_change(RS& s, RV& v, RC& c, int phase, int q, int lv, int lrow, int lpos, double dq,
                          double xq) {
     const int m = s.m, n = s.n, k = c.k, lane = threadIdx.x;
@@ -559,11 +584,7 @@ RDEV bool r_basis_change(RS& s, RV& v, RC& c, int phase, int q, int lv, int lrow
             const double vv = lane < k ? Mi[p * ld + lane] / piv : 0.0;
             if (phase == 2) r_dual_upd(s, v, dq, vv, -1);
             R_FENCE();
-            for (int i = 0; i < k; ++i) {
-                const double wi = rl(v.alS, i);
-                if (i == p || wi == 0.0) continue;
-                if (lane < k && vv != 0.0) Mi[i * ld + lane] = fma(-wi, vv, Mi[i * ld + lane]);
-            }
+            r_rank1(Mi, ld, k, p, -1, vv, [&](int i) { return rl(v.alS, i); });
             if (lane < k) Mi[p * ld + lane] = vv;
             if (lane == p) {
                 v.Sl = q;
@@ -582,11 +603,7 @@ RDEV bool r_basis_change(RS& s, RV& v, RC& c, int phase, int q, int lv, int lrow
                 if (lane == i) v.y = dq / delta;
             }
             R_FENCE();
-            for (int a = 0; a < k; ++a) {
-                const double wa = rl(v.alS, a);
-                if (wa == 0.0) continue;
-                if (lane < k && vv != 0.0) Mi[a * ld + lane] = fma(wa, vv, Mi[a * ld + lane]);
-            }
+            r_rank1(Mi, ld, k, -1, -1, vv, [&](int a) { return -rl(v.alS, a); });  // (fma(-(-w), vv, .) = fma(w, vv, .))
             if (lane < k) {
                 Mi[lane * ld + k] = -(v.alS / delta);
                 Mi[k * ld + lane] = -vv;
@@ -622,12 +639,7 @@ RDEV bool r_basis_change(RS& s, RV& v, RC& c, int phase, int q, int lv, int lrow
             const double vv = lane < k ? Mi[b * ld + lane] / piv : 0.0;
             if (phase == 2) r_dual_upd(s, v, dq, vv, a);
             R_FENCE();
-            for (int r = 0; r < k; ++r) {
-                if (r == b) continue;
-                const double f = Mi[r * ld + a];
-                if (f == 0.0) continue;
-                if (lane < k && lane != a && vv != 0.0) Mi[r * ld + lane] = fma(-f, vv, Mi[r * ld + lane]);
-            }
+            r_rank1(Mi, ld, k, b, a, vv, [&](int r) { return Mi[r * ld + a]; });  // (column a is not written)
             R_FENCE();
             if (phase == 2 && lane == i0) v.y = 0.0;
             const int sl_last = rli(v.Sl, last), rl_last = rli(v.Rl, last);
@@ -665,11 +677,7 @@ RDEV bool r_basis_change(RS& s, RV& v, RC& c, int phase, int q, int lv, int lrow
             }
             const double tr = lane < k ? Mi[lane * ld + a] / piv : 0.0;  // (lane r)
             R_FENCE();
-            for (int r = 0; r < k; ++r) {
-                const double f = rl(tr, r);
-                if (f == 0.0) continue;
-                if (lane < k && lane != a && vv != 0.0) Mi[r * ld + lane] = fma(-f, vv, Mi[r * ld + lane]);
-            }
+            r_rank1(Mi, ld, k, -1, a, vv, [&](int r) { return rl(tr, r); });
             if (lane < k) Mi[lane * ld + a] = tr;
             if (lane == a) v.Rl = i1;
             if (lane == i1) {
