@@ -137,7 +137,8 @@ typedef struct elp_control {
                                 fits (one GPU, no column shards); 1: the same
                                 (force: the tests); 2: never (the multi-workgroup
                                 pipeline).  Same pivots, same bits either way;
-                                elp_stats.resident reports what ran */
+                                branch-and-bound nodes warm-start inside the
+                                same launch; elp_stats.resident reports what ran */
     int32_t pad_resident;
 } elp_control;
 
@@ -344,7 +345,10 @@ int elp_comm_init_host(elp_handle* h, int32_t world_size, int32_t rank, elp_host
                        elp_host_allreduce_fn ar, elp_host_bcast_fn bc, void* user);
 
 /* R finalizer for self$pointer (R/class.R:300; EasyLP's finalize at
- * R/class.R:497-501 is empty, this one frees device memory). */
+ * R/class.R:497-501 is empty, this one frees device memory).  A one-GPU
+ * handle leaves its stream, device buffers and pinned blocks to the next
+ * elp_create on the same device (a bounded cache, ELP_NO_SPARE=1: off), so
+ * R's one-handle-per-solve pattern pays no stream creation after the first. */
 void elp_destroy(elp_handle* h);
 
 /* Thread-local description of the last negative return. */
